@@ -1,0 +1,148 @@
+"""North-star benchmark: ResNet-50 PyTorchTrial training throughput (samples/sec, whole node).
+
+    python bench.py --gpus N --steps K --warmup W            # N=1
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+The step that is timed is the real framework path, not a bare loop: a ``PyTorchTrialController``
+is built exactly as a cluster trial process builds it and fed ``RUN_STEP`` workloads:
+  warmup RUN_STEP(W batches) -> barrier + synchronize -> t0 -> RUN_STEP(K batches)
+  -> synchronize + barrier -> t1.
+Each batch is: synthetic uint8 ImageNet-shape images DMA'd from pinned memory -> HIP normalize
+kernel -> ResNet-50 fwd/bwd (bf16 autocast, channels_last) -> [RCCL bucketed all-reduce overlapped
+with backward] -> fused arena SGD-momentum HIP kernel.  Weak scaling: fixed per-GPU batch.
+
+Rank 0 prints ONE JSON line; ``value`` = K * global_batch / max-over-ranks(t1 - t0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE_VALUE = None  # BASELINE.json "published": {} -- the reference publishes no ResNet-50 number
+
+
+def parse() -> argparse.Namespace:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DET_BENCH_BS", "256")))
+    ap.add_argument("--amp", default=os.environ.get("DET_BENCH_AMP", "O1"), choices=["O0", "O1", "O2"])
+    ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--bucket-mb", type=int, default=int(os.environ.get("DET_BENCH_BUCKET_MB", "64")))
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "0")))
+    return ap.parse_args()
+
+
+def main() -> None:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
+            sys.exit(2)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
+
+    from determined_1_amd import workload
+    from determined_1_amd.experimental import make_controller
+    from determined_1_amd.models.imagenet_trial import ResNetImageNetTrial
+    from determined_1_amd.parallel import dist as pdist
+
+    gbs = args.batch_per_gpu * world
+    config = {
+        "entrypoint": "determined_1_amd.models.imagenet_trial:ResNetImageNetTrial",
+        "hyperparameters": {
+            "global_batch_size": gbs,
+            "lr": 0.1 * gbs / 256,
+            "momentum": 0.9,
+            "weight_decay": 5e-5,
+            "arch": args.arch,
+            "amp": args.amp,
+            "channels_last": not args.no_channels_last,
+        },
+        "resources": {"slots_per_trial": world},
+        "optimizations": {"tensor_fusion_threshold": args.bucket_mb},
+        "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": args.steps}},
+        "scheduling_unit": args.steps,
+    }
+    timing = {}
+
+    def sync_barrier() -> None:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        pdist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def stream():
+        resp = {}
+
+        def keep(r):
+            resp["last"] = r
+
+        if args.warmup > 0:
+            yield workload.train_workload(1, num_batches=args.warmup, total_batches_processed=0), [], keep
+        sync_barrier()
+        timing["t0"] = time.perf_counter()
+        yield workload.train_workload(2, num_batches=args.steps, total_batches_processed=args.warmup), [], keep
+        sync_barrier()
+        timing["t1"] = time.perf_counter()
+        timing["resp"] = resp.get("last")
+        yield workload.terminate_workload(3), [], workload.ignore_response
+
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+    ctrl = make_controller(ResNetImageNetTrial, config, stream(), trial_seed=1234)
+    ctrl.run()
+    elapsed = timing["t1"] - timing["t0"]
+    all_elapsed = pdist.allgather_object(elapsed)
+    t = max(all_elapsed)
+    value = args.steps * gbs / t
+    loss = None
+    r = timing.get("resp")
+    if isinstance(r, dict):
+        loss = r.get("metrics", {}).get("avg_metrics", {}).get("loss")
+    if rank == 0:
+        out = {
+            "metric": "samples/sec (whole node) ResNet-50 PyTorchTrial",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * t / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16" if args.amp != "O0" else "fp32",
+            "data": "synthetic (random uint8 224x224x3 images, random labels; random-init weights)",
+            "config": {
+                "model": args.arch,
+                "global_batch": gbs,
+                "per_gpu_batch": args.batch_per_gpu,
+                "seq_len": None,
+                "image_size": 224,
+                "parallelism": f"dp{world}",
+                "amp": args.amp,
+                "optimizer": "SGD-momentum (fused arena HIP kernel)",
+                "bucket_mb": args.bucket_mb,
+                "final_avg_loss": loss,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+"""Synthetic datasets of the benchmark shapes (no network: no ImageNet / CIFAR / SQuAD here).
+
+``SyntheticImages`` mimics a decoded-image pipeline: a fixed pool of random uint8 HWC images in
+*pinned* host memory.  ``__getitems__`` (torch>=2 batched fetch) returns contiguous batches as
+zero-copy views of the pinned pool, so the only per-batch host work is the DMA the
+``DevicePrefetcher`` issues; normalisation to bf16 NCHW-channels_last happens on the GPU in one
+``det_u8_normalize`` kernel pass.
+"""
+from typing import Any, List, Sequence, Tuple
+
+import torch
+import torch.utils.data as tud
+
+IMAGENET_MEAN = (0.485 * 255, 0.456 * 255, 0.406 * 255)
+IMAGENET_STD = (0.229 * 255, 0.224 * 255, 0.225 * 255)
+
+
+class SyntheticImages(tud.Dataset):
+    def __init__(self, length: int, image_size: int = 224, channels: int = 3, num_classes: int = 1000,
+                 pool: int = 512, seed: int = 0, pin: bool = True) -> None:
+        g = torch.Generator().manual_seed(seed)
+        self.length = int(length)
+        self.pool = min(pool, self.length)
+        imgs = torch.randint(0, 256, (self.pool, image_size, image_size, channels), dtype=torch.uint8, generator=g)
+        labels = torch.randint(0, num_classes, (self.pool,), dtype=torch.int64, generator=g)
+        if pin and torch.cuda.is_available():
+            imgs = imgs.pin_memory()
+            labels = labels.pin_memory()
+        self.images = imgs
+        self.labels = labels
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        j = i % self.pool
+        return self.images[j], self.labels[j]
+
+    def __getitems__(self, idx: Sequence[int]) -> Tuple[torch.Tensor, torch.Tensor]:
+        n = len(idx)
+        j0 = idx[0] % self.pool
+        contiguous = all(idx[k] == idx[0] + k for k in range(n)) and j0 + n <= self.pool
+        if contiguous:
+            return self.images[j0:j0 + n], self.labels[j0:j0 + n]
+        sel = torch.tensor([i % self.pool for i in idx], dtype=torch.int64)
+        return self.images.index_select(0, sel), self.labels.index_select(0, sel)
+
+
+def passthrough_collate(batch: Any) -> Any:
+    """Collate for datasets whose ``__getitems__`` already returns a stacked batch."""
+    return batch
+
+
+class SyntheticTokens(tud.Dataset):
+    """BERT/SQuAD-shaped synthetic batches: input_ids, attention_mask, token_type_ids,
+    start/end positions."""
+
+    def __init__(self, length: int, seq_len: int = 384, vocab: int = 30522, seed: int = 0, pool: int = 256) -> None:
+        g = torch.Generator().manual_seed(seed)
+        self.length = int(length)
+        self.pool = min(pool, self.length)
+        self.input_ids = torch.randint(0, vocab, (self.pool, seq_len), generator=g)
+        self.attention_mask = torch.ones(self.pool, seq_len, dtype=torch.int64)
+        self.token_type_ids = torch.zeros(self.pool, seq_len, dtype=torch.int64)
+        self.token_type_ids[:, seq_len // 2:] = 1
+        self.start = torch.randint(0, seq_len, (self.pool,), generator=g)
+        self.end = torch.clamp(self.start + torch.randint(0, 16, (self.pool,), generator=g), max=seq_len - 1)
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int) -> List[torch.Tensor]:
+        j = i % self.pool
+        return [self.input_ids[j], self.attention_mask[j], self.token_type_ids[j], self.start[j], self.end[j]]

@@ -1,0 +1,129 @@
+"""Loader for the hand-written gfx950 kernel library (``libdetkernels.so``).
+
+The library is a plain C ABI built by ``hipcc --offload-arch=gfx950 -shared`` (see
+``determined_1_amd/ops/build.py``) and loaded with ctypes.  Kernels are launched on the caller's
+current HIP stream (``torch.cuda.current_stream().cuda_stream``) so they order correctly with
+PyTorch work and are capturable into hipGraphs.
+
+Policy: on a GPU tensor the HIP library MUST be used.  If it is missing we raise instead of
+silently falling back to eager PyTorch (the harness's "native code loaded" check depends on
+that).  CPU tensors (unit tests on the build host) use the pure-PyTorch reference
+implementations in ``functional.py``.
+"""
+import ctypes
+import os
+import pathlib
+import threading
+from typing import Optional
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_NAME = "libdetkernels.so"
+LIB_PATH = _HERE / LIB_NAME
+ABI_VERSION = 3
+
+_lock = threading.Lock()
+_lib = None  # type: Optional[ctypes.CDLL]
+
+F32, BF16, F16 = 0, 1, 2
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_float = ctypes.c_float
+
+_SIGNATURES = {
+    "det_abi_version": ([], c_int),
+    # stream, g_dtype, out_dtype, p, g, buf, out_model, n, lr, momentum, dampening, wd,
+    # nesterov, first_step, g_scale, g_scale_dev, found_inf
+    "det_sgd_step": (
+        [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_i64]
+        + [c_float] * 4
+        + [c_int, c_int, c_float, c_void_p, c_void_p],
+        c_int,
+    ),
+    # stream, g_dtype, out_dtype, p, g, m, v, vmax, out_model, n, lr, b1, b2, eps, wd, adamw,
+    # amsgrad, bias_c1, bias_c2_sqrt, g_scale, g_scale_dev, found_inf
+    "det_adam_step": (
+        [c_void_p, c_int, c_int] + [c_void_p] * 6 + [c_i64] + [c_float] * 5
+        + [c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p],
+        c_int,
+    ),
+    # stream, g_dtype, out_dtype, p, g, square_avg, momentum_buf, grad_avg, out_model, n, lr,
+    # alpha, eps, wd, momentum, centered, g_scale, g_scale_dev, found_inf
+    "det_rmsprop_step": (
+        [c_void_p, c_int, c_int] + [c_void_p] * 6 + [c_i64] + [c_float] * 5
+        + [c_int, c_float, c_void_p, c_void_p],
+        c_int,
+    ),
+    # stream, g_dtype, out_dtype, p, g, sum, out_model, n, clr, eps, wd, g_scale, g_scale_dev,
+    # found_inf
+    "det_adagrad_step": (
+        [c_void_p, c_int, c_int] + [c_void_p] * 4 + [c_i64] + [c_float] * 3
+        + [c_float, c_void_p, c_void_p],
+        c_int,
+    ),
+    # stream, g_dtype, out_dtype, p, g, square_avg, acc_delta, out_model, n, lr, rho, eps, wd,
+    # g_scale, g_scale_dev, found_inf
+    "det_adadelta_step": (
+        [c_void_p, c_int, c_int] + [c_void_p] * 5 + [c_i64] + [c_float] * 4
+        + [c_float, c_void_p, c_void_p],
+        c_int,
+    ),
+    "det_scale_cast": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_i64, c_float, c_void_p], c_int),
+    "det_sumsq_num_partials": ([c_i64], c_int),
+    "det_sumsq_partials": ([c_void_p, c_void_p, c_int, c_i64, c_void_p], c_int),
+    "det_norm_finalize": (
+        [c_void_p, c_void_p, c_int, c_float, c_float, c_void_p, c_void_p, c_void_p],
+        c_int,
+    ),
+    "det_unscale_check": ([c_void_p, c_void_p, c_int, c_i64, c_float, c_void_p], c_int),
+    "det_mt_copy": ([c_void_p, c_void_p, c_int, c_int, c_int, c_i64, c_float], c_int),
+    "det_u8_normalize": (
+        [c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_void_p, c_void_p],
+        c_int,
+    ),
+}
+
+
+class KernelLibraryMissing(RuntimeError):
+    pass
+
+
+def lib_available() -> bool:
+    try:
+        get_lib()
+        return True
+    except (KernelLibraryMissing, OSError):
+        return False
+
+
+def get_lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = os.environ.get("DET_KERNELS_LIB", str(LIB_PATH))
+        if not os.path.exists(path):
+            raise KernelLibraryMissing(
+                f"{path} not found: build it with `python -m determined_1_amd.ops.build` "
+                "(hipcc --offload-arch=gfx950).  GPU tensors never fall back to eager PyTorch."
+            )
+        lib = ctypes.CDLL(path)
+        for name, (argtypes, restype) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = restype
+        ver = lib.det_abi_version()
+        if ver != ABI_VERSION:
+            raise KernelLibraryMissing(
+                f"{path} has ABI {ver}, expected {ABI_VERSION}; rebuild the kernels"
+            )
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"HIP kernel {what} failed with hipError {rc}")

@@ -1,0 +1,428 @@
+"""PyTorchTrialContext: model/optimizer/scheduler wrapping, backward and optimizer stepping.
+
+Reference API: ``harness/determined/pytorch/_pytorch_context.py:21-571`` (wrap_model,
+wrap_optimizer, wrap_lr_scheduler, configure_apex_amp, backward, step_optimizer, to_device,
+is_epoch_start/end).  Semantics kept:
+  * gradients are communicated and the optimizer stepped only every ``aggregation_frequency``
+    batches (``_should_communicate_and_update``, reference :384-389);
+  * grads are averaged over ``aggregation_frequency`` when ``average_aggregated_gradients``
+    (:470-477) and over ranks (Horovod's allreduce-average) *before* ``clip_grads`` runs;
+  * ``auto_zero_grads`` must stay true when aggregating.
+
+Implementation (MI355X-first): wrapping is declarative; ``_finalize()`` (called by the controller
+once the user's ``__init__`` returns) moves every wrapped optimizer's parameters into flat
+arenas, attaches the fused HIP optimizer, and (multi-GPU) a backward-overlapped RCCL bucketer.
+All gradient scale factors are folded into the optimizer's one pass over the gradients, unless a
+user ``clip_grads`` function needs real gradients first (then one in-place scale kernel runs).
+"""
+import logging
+from typing import Any, Callable, Dict, Iterator, List, Optional, Set, Tuple, Type, Union
+
+import torch
+import torch.nn as nn
+
+from determined_1_amd import check, errors, trial
+from determined_1_amd.ops import functional as F
+from determined_1_amd.ops.optim import FusedOptimizer, fused_kind
+from determined_1_amd.parallel import dist as pdist
+from determined_1_amd.parallel.ddp import GradientBucketer, broadcast_arenas, broadcast_tensors_coalesced
+from determined_1_amd.pytorch import _amp
+from determined_1_amd.pytorch._data import TorchData, to_device
+from determined_1_amd.pytorch._lr_scheduler import LRScheduler
+
+
+class ClipGradsNorm:
+    """Device-side global-norm clipping that the context folds into the fused optimizer step
+    (no host sync, no extra pass over the gradients besides the norm reduction).
+
+    ``context.step_optimizer(opt, clip_grads=det.pytorch.ClipGradsNorm(1.0))`` is numerically
+    ``torch.nn.utils.clip_grad_norm_(params, 1.0)`` (coef = max_norm / (norm + 1e-6), <= 1).
+    Called with a parameter iterator (non-fused optimizers) it falls back to the torch function.
+    """
+
+    def __init__(self, max_norm: float) -> None:
+        self.max_norm = float(max_norm)
+
+    def __call__(self, parameters: Iterator) -> None:
+        torch.nn.utils.clip_grad_norm_(list(parameters), self.max_norm)
+
+
+class _OptState:
+    """Per wrapped optimizer: fused engine, bucketer, workspace, bookkeeping."""
+
+    def __init__(self, opt: torch.optim.Optimizer, backward_passes_per_step: int) -> None:
+        self.opt = opt
+        self.bpps = backward_passes_per_step
+        self.fused = None  # type: Optional[FusedOptimizer]
+        self.bucketer = None  # type: Optional[GradientBucketer]
+        self.norm_ws = None  # type: Optional[F.NormWorkspace]
+        self.last_batch = None  # type: Optional[int]
+        self.calls = 0
+
+
+class PyTorchTrialContext(trial.TrialContext):
+    def __init__(self, *args: Any, **kwargs: Any) -> None:
+        super().__init__(*args, **kwargs)
+        self._init_device()
+        self._to_device_warned_types = set()  # type: Set[Type]
+        self.models = []  # type: List[nn.Module]
+        self.optimizers = []  # type: List[torch.optim.Optimizer]
+        self.lr_schedulers = []  # type: List[LRScheduler]
+        self._opt_states = []  # type: List[_OptState]
+        self._epoch_len = None  # type: Optional[int]
+        self._main_model = nn.Module()
+        self._use_amp = False
+        self._amp = None  # type: Optional[_amp.AmpConfig]
+        self._loss_ids = {}  # type: Dict[Any, int]
+        self._last_backward_batch_idx = None  # type: Optional[int]
+        self._current_batch_idx = None  # type: Optional[int]
+        self._finalized = False
+        self._fuse = True
+        self._input_cast_hooks = []  # type: List[Any]
+
+    # ------------------------------------------------------------------------------------------
+    # device
+    # ------------------------------------------------------------------------------------------
+    def _init_device(self) -> None:
+        self.n_gpus = len(self.env.container_gpus)
+        if self.dist_config.use and torch.cuda.is_available():
+            self.device = torch.device("cuda", self.distributed.get_local_rank())
+            torch.cuda.set_device(self.device)
+        elif self.n_gpus > 0 and torch.cuda.is_available():
+            self.device = torch.device("cuda", 0)
+        else:
+            self.device = torch.device("cpu")
+
+    def to_device(self, data: Any) -> TorchData:
+        return to_device(data, self.device, self._to_device_warned_types)
+
+    # ------------------------------------------------------------------------------------------
+    # wrapping
+    # ------------------------------------------------------------------------------------------
+    def wrap_model(self, model: nn.Module) -> nn.Module:
+        if self.env.managed_training:
+            check.false(self._use_amp, "Must call wrap_model() before configure_apex_amp.")
+            check.false(self._finalized, "wrap_model() must be called from the trial's __init__().")
+            model = model.to(self.device)
+            if not self.dist_config.use and self.n_gpus > 1 and torch.cuda.device_count() > 1:
+                check.eq(self.dist_config.aggregation_frequency, 1,
+                         "Please enable `optimized_parallel` to use aggregation frequency greater than 1 for "
+                         "single machine multi-GPU training.")
+                logging.warning("native_parallel uses single-process nn.DataParallel; multi-process DP over RCCL "
+                                "(native_parallel: false) is the fast path on MI355X.")
+                model = nn.DataParallel(model)
+        model_id = len(self.models)
+        self._main_model.__setattr__(f"model_{model_id}", model)
+        self.models.append(model)
+        return model
+
+    def wrap_optimizer(self, optimizer: torch.optim.Optimizer, backward_passes_per_step: int = 1) -> torch.optim.Optimizer:
+        if self.env.managed_training:
+            check.false(self._use_amp, "Must call wrap_optimizer() before configure_apex_amp.")
+            check.gt_eq(backward_passes_per_step, 1,
+                        "backward_passes_per_step for local gradient aggregation must be >= 1")
+        self.optimizers.append(optimizer)
+        self._opt_states.append(_OptState(optimizer, backward_passes_per_step))
+        return optimizer
+
+    def wrap_lr_scheduler(self, lr_scheduler: Any, step_mode: LRScheduler.StepMode) -> Any:
+        opt = getattr(lr_scheduler, "optimizer", None)
+        if opt is not None:
+            check.is_in(opt, self.optimizers, "Must use an optimizer that is returned by wrap_optimizer()")
+        self.lr_schedulers.append(LRScheduler(lr_scheduler, step_mode))
+        return lr_scheduler
+
+    def configure_apex_amp(
+        self,
+        models: Union[nn.Module, List[nn.Module]],
+        optimizers: Union[torch.optim.Optimizer, List[torch.optim.Optimizer]],
+        enabled: Optional[bool] = True,
+        opt_level: Optional[str] = "O1",
+        cast_model_type: Optional[torch.dtype] = None,
+        patch_torch_functions: Optional[bool] = None,
+        keep_batchnorm_fp32: Optional[Union[bool, str]] = None,
+        master_weights: Optional[bool] = None,
+        loss_scale: Optional[Union[float, str]] = None,
+        cast_model_outputs: Optional[torch.dtype] = None,
+        num_losses: Optional[int] = 1,
+        verbosity: Optional[int] = 1,
+        min_loss_scale: Optional[float] = None,
+        max_loss_scale: Optional[float] = 2.0 ** 24,
+    ) -> Tuple:
+        if not self.env.managed_training:
+            return models, optimizers
+        check.false(self._use_amp, "Please only call configure_apex_amp once.")
+        if self.dist_config.use:
+            check.eq(num_losses, 1, "When using parallel/distributed training, Determined only supports "
+                                    "configure_apex_amp with num_losses = 1")
+            check.eq(self.dist_config.aggregation_frequency, 1,
+                     "Mixed precision training (AMP) is not supported with aggregation frequency > 1.")
+        if not enabled or opt_level == "O0":
+            return models, optimizers
+        self._use_amp = True
+        self._amp = _amp.make_amp_config(self.device, opt_level or "O1", cast_model_type, keep_batchnorm_fp32,
+                                         loss_scale, min_loss_scale, max_loss_scale)
+        logging.info(f"Enabling mixed precision training with opt_level: {opt_level} ({self._amp.dtype}).")
+        model_list = models if isinstance(models, list) else [models]
+        if self._amp.casts_model:
+            for m in model_list:
+                _amp.cast_model(m, self._amp.dtype, self._amp.keep_batchnorm_fp32)
+                self._input_cast_hooks.append(_amp.install_input_cast(m, self._amp.dtype))
+        return models, optimizers
+
+    # ------------------------------------------------------------------------------------------
+    def _finalize(self) -> None:
+        """Realise the declared wrapping: arenas + fused optimizers + RCCL bucketers.
+        Idempotent.  (The controller loads a checkpoint after this and then calls
+        ``_broadcast_state``.)"""
+        if self._finalized:
+            return
+        self._finalized = True
+        for st in self._opt_states:
+            if self._fuse and fused_kind(st.opt) is not None:
+                try:
+                    st.fused = FusedOptimizer(st.opt, self.device)
+                except ValueError as e:
+                    logging.warning(f"optimizer not fused ({e}); using stock torch step")
+            elif fused_kind(st.opt) is None:
+                logging.info(f"{type(st.opt).__name__} has no fused gfx950 kernel; using its own step()")
+            if st.fused is not None:
+                st.norm_ws = F.NormWorkspace([a.flat_grad for a in st.fused.arenas]) if st.fused.arenas else None
+            if self.dist_config.use and pdist.is_initialized():
+                if st.fused is not None and st.fused.arenas:
+                    comp = None
+                    if self.dist_config.grad_compression:
+                        comp = torch.float16 if self.dist_config.compression_dtype == "float16" else torch.bfloat16
+                    st.bucketer = GradientBucketer(
+                        st.fused.arenas,
+                        world_size=self.distributed.get_size(),
+                        cap_mb=self.dist_config.fusion_threshold_mb,
+                        compression=comp,
+                    )
+
+    def _broadcast_state(self) -> None:
+        """Rank 0's parameters, buffers and optimizer state to all ranks (SURVEY C-2/C-3)."""
+        arena_param_ids = set()
+        for st in self._opt_states:
+            if st.fused is not None:
+                broadcast_arenas(st.fused.arenas)
+                for a in st.fused.arenas:
+                    arena_param_ids.update(id(p) for p in a.params)
+        real = []
+        for m in self._main_model.modules():
+            for p in m.parameters(recurse=False):
+                if id(p) not in arena_param_ids:
+                    real.append(p.data)
+            for b in m.buffers(recurse=False):
+                real.append(b)
+        if real:
+            broadcast_tensors_coalesced(real)
+        for st in self._opt_states:
+            state_tensors = [t for s in st.opt.state.values() for t in s.values()
+                             if isinstance(t, torch.Tensor) and t.device.type == self.device.type]
+            if state_tensors:
+                broadcast_tensors_coalesced(state_tensors)
+
+    # ------------------------------------------------------------------------------------------
+    # training step API
+    # ------------------------------------------------------------------------------------------
+    def _should_communicate_and_update(self) -> bool:
+        if not self.env.managed_training:
+            return True
+        if self._current_batch_idx is None:
+            raise errors.InternalException("Training hasn't started.")
+        return (self._current_batch_idx + 1) % self.dist_config.aggregation_frequency == 0
+
+    def backward(self, loss: torch.Tensor, gradient: Optional[torch.Tensor] = None, retain_graph: bool = False,
+                 create_graph: bool = False) -> None:
+        if not self._finalized:
+            self._finalize()
+        comm = self._should_communicate_and_update() if self.env.managed_training else True
+        for st in self._opt_states:
+            if st.fused is not None:
+                st.fused.ensure_grads()
+            if st.last_batch != self._current_batch_idx:
+                st.last_batch = self._current_batch_idx
+                st.calls = 0
+            st.calls += 1
+            if st.bucketer is not None:
+                # communicate on the backward pass that completes backward_passes_per_step passes
+                # of a batch that ends an aggregation window (Horovod's
+                # backward_passes_per_step * aggregation_frequency, reference :192-198)
+                st.bucketer.prepare_backward(comm and st.calls == st.bpps)
+        if self._use_amp and self._amp is not None and self._amp.scaler is not None:
+            if (self._last_backward_batch_idx is not None and self._current_batch_idx is not None
+                    and self._last_backward_batch_idx >= self._current_batch_idx and self.dist_config.use):
+                raise errors.InvalidExperimentException(
+                    "Calling context.backward(loss) multiple times is not supported while using AMP loss "
+                    "scaling and parallel/distributed training")
+            self._last_backward_batch_idx = self._current_batch_idx
+            loss = self._amp.scaler.scale_loss(loss)
+        loss.backward(gradient=gradient, retain_graph=retain_graph, create_graph=create_graph)  # type: ignore
+
+    def _grad_scale(self) -> float:
+        s = 1.0
+        if self.dist_config.use and pdist.is_initialized():
+            s /= self.distributed.get_size()
+        if self.dist_config.average_aggregated_gradients and self.dist_config.aggregation_frequency > 1:
+            s /= self.dist_config.aggregation_frequency
+        return s
+
+    def step_optimizer(self, optimizer: torch.optim.Optimizer, clip_grads: Optional[Callable[[Iterator], None]] = None,
+                       auto_zero_grads: bool = True) -> None:
+        check.true(auto_zero_grads or self.dist_config.aggregation_frequency == 1,
+                   "if optimizations.aggregation_frequency is larger than 1, you can only set auto_zero_grads "
+                   "to be true.")
+        if not self._should_communicate_and_update():
+            return
+        st = next((s for s in self._opt_states if s.opt is optimizer), None)
+        check.is_not_none(st, "step_optimizer() needs an optimizer returned by wrap_optimizer()")
+        assert st is not None
+        if not self._finalized:
+            self._finalize()
+        if st.bucketer is not None:
+            st.bucketer.synchronize()
+        scaler = self._amp.scaler if (self._amp is not None) else None
+        host_scale = self._grad_scale()
+        params = [p for g in optimizer.param_groups for p in g.get("params", [])]
+        if st.fused is None:
+            self._step_unfused(st, optimizer, params, clip_grads, host_scale, scaler)
+        else:
+            self._step_fused(st, params, clip_grads, host_scale, scaler)
+        if scaler is not None:
+            scaler.update()
+            scaler.reset_found_inf()
+        if auto_zero_grads:
+            optimizer.zero_grad()
+
+    def _step_fused(self, st: _OptState, params: List[torch.Tensor], clip_grads: Optional[Callable],
+                    host_scale: float, scaler: Optional[_amp.DynamicLossScaler]) -> None:
+        fused = st.fused
+        assert fused is not None
+        fused.grad_scale = host_scale
+        fused.grad_scale_dev = None
+        fused.found_inf = None
+        if isinstance(clip_grads, ClipGradsNorm) and st.norm_ws is not None:
+            # norm of the *true* gradients: fold host scale (and the AMP inverse scale) in
+            st.norm_ws.found_inf.zero_()
+            F.global_norm_(st.norm_ws, pre_scale=host_scale, max_norm=clip_grads.max_norm)
+            if scaler is not None:
+                # the reduction saw loss-scaled grads: recompute the coefficient on the true norm
+                # (device scalars only) and fold the inverse loss scale into it
+                st.norm_ws.norm.mul_(scaler.inv_scale)
+                coef = torch.clamp(clip_grads.max_norm / (st.norm_ws.norm + 1e-6), max=1.0)
+                st.norm_ws.clip_coef.copy_(coef * scaler.inv_scale)
+                st.norm_ws.found_inf.copy_(torch.maximum(st.norm_ws.found_inf, scaler.found_inf))
+                fused.found_inf = st.norm_ws.found_inf
+                scaler.found_inf.copy_(st.norm_ws.found_inf)
+            fused.grad_scale_dev = st.norm_ws.clip_coef
+        elif clip_grads is not None:
+            # user function needs the real (averaged, unscaled) gradients materialised
+            inv = host_scale
+            for a in fused.arenas:
+                if scaler is not None:
+                    F.unscale_check_(a.flat_grad, inv, scaler.found_inf)
+                    a.flat_grad.mul_(scaler.inv_scale.to(a.flat_grad.dtype))
+                elif inv != 1.0:
+                    F.unscale_check_(a.flat_grad, inv, _dummy_flag(a.flat_grad.device))
+            fused.grad_scale = 1.0
+            clip_grads(iter(params))
+            if scaler is not None:
+                fused.found_inf = scaler.found_inf
+        elif scaler is not None:
+            # overflow detection without writing the gradients: norm reduction only
+            assert st.norm_ws is not None
+            st.norm_ws.found_inf.zero_()
+            F.global_norm_(st.norm_ws, pre_scale=1.0, max_norm=0.0)
+            fused.found_inf = st.norm_ws.found_inf
+            scaler.found_inf.copy_(st.norm_ws.found_inf)
+            fused.grad_scale_dev = scaler.inv_scale
+        st.opt.step()
+
+    def _step_unfused(self, st: _OptState, optimizer: torch.optim.Optimizer, params: List[torch.Tensor],
+                      clip_grads: Optional[Callable], host_scale: float,
+                      scaler: Optional[_amp.DynamicLossScaler]) -> None:
+        grads = [p.grad for p in params if p.grad is not None]
+        if self.dist_config.use and pdist.is_initialized() and st.bucketer is None and grads:
+            # non-arena parameters: one coalesced all-reduce per dtype (SUM; scaled below)
+            import torch.distributed as dist
+
+            by_dt = {}  # type: Dict[torch.dtype, List[torch.Tensor]]
+            for g in grads:
+                by_dt.setdefault(g.dtype, []).append(g)
+            for gs in by_dt.values():
+                flat = torch.cat([g.reshape(-1) for g in gs])
+                dist.all_reduce(flat)
+                off = 0
+                for g in gs:
+                    g.copy_(flat[off:off + g.numel()].view_as(g))
+                    off += g.numel()
+        scale = host_scale
+        if grads and (scale != 1.0 or scaler is not None):
+            with torch.no_grad():
+                if scaler is not None:
+                    torch._amp_foreach_non_finite_check_and_unscale_(grads, scaler.found_inf.float(), scaler.inv_scale)
+                if scale != 1.0:
+                    torch._foreach_mul_(grads, scale)
+        if clip_grads is not None:
+            clip_grads(iter(params))
+        if scaler is not None and bool(scaler.found_inf.item()):
+            return
+        optimizer.step()
+
+    # ------------------------------------------------------------------------------------------
+    def _autocast(self) -> Any:
+        if self._amp is not None and self._amp.autocast and self.device.type == "cuda":
+            return torch.autocast(device_type="cuda", dtype=self._amp.dtype)
+        import contextlib
+
+        return contextlib.nullcontext()
+
+    def _amp_state_dict(self) -> Optional[Dict[str, Any]]:
+        return self._amp.state_dict() if self._amp is not None else None
+
+    def _sync_master_weights(self) -> None:
+        for st in self._opt_states:
+            if st.fused is not None:
+                st.fused.sync_master_from_params()
+
+    def is_epoch_start(self) -> bool:
+        if self._current_batch_idx is None:
+            raise errors.InternalException("Training hasn't started.")
+        if self._epoch_len is None:
+            raise errors.InternalException("Training DataLoader uninitialized.")
+        return self._current_batch_idx % self._epoch_len == 0
+
+    def is_epoch_end(self) -> bool:
+        if self._current_batch_idx is None:
+            raise errors.InternalException("Training hasn't started.")
+        if self._epoch_len is None:
+            raise errors.InternalException("Training DataLoader uninitialized.")
+        return self._current_batch_idx % self._epoch_len == self._epoch_len - 1
+
+    # deprecated accessors (reference :63-126)
+    def get_model(self) -> nn.Module:
+        logging.warning("PyTorchTrialContext.get_model is deprecated.")
+        check.len_eq(self.models, 1)
+        return self.models[0]
+
+    def get_optimizer(self) -> torch.optim.Optimizer:
+        logging.warning("PyTorchTrialContext.get_optimizer is deprecated.")
+        check.len_eq(self.optimizers, 1)
+        return self.optimizers[0]
+
+    def get_lr_scheduler(self) -> Optional[LRScheduler]:
+        logging.warning("PyTorchTrialContext.get_lr_scheduler is deprecated.")
+        check.lt_eq(len(self.lr_schedulers), 1)
+        return self.lr_schedulers[0] if self.lr_schedulers else None
+
+
+_DUMMY = {}  # type: Dict[Any, torch.Tensor]
+
+
+def _dummy_flag(device: torch.device) -> torch.Tensor:
+    t = _DUMMY.get(device)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=device)
+        _DUMMY[device] = t
+    return t

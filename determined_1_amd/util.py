@@ -1,0 +1,137 @@
+"""Metric packaging, JSON encoding and checkpoint-code helpers
+(reference ``harness/determined/util.py:29-166``)."""
+import datetime
+import enum
+import json
+import math
+import os
+import pathlib
+import shutil
+import uuid
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from determined_1_amd import check, workload
+
+
+def is_overridden(full_method: Any, parent_class: Any) -> bool:
+    """True if ``full_method`` (bound) is not the implementation defined on ``parent_class``."""
+    name = getattr(full_method, "__name__", None)
+    if name is None:
+        return True
+    base = getattr(parent_class, name, None)
+    impl = getattr(full_method, "__func__", full_method)
+    return impl is not base
+
+
+def _list_to_dict(list_of_dicts: List[Dict[str, Any]]) -> Dict[str, List[Any]]:
+    out = {}  # type: Dict[str, List[Any]]
+    for d in list_of_dicts:
+        for k, v in d.items():
+            out.setdefault(k, []).append(v)
+    return out
+
+
+def _dict_to_list(dict_of_lists: Dict[str, List[Any]]) -> List[Dict[str, Any]]:
+    keys = list(dict_of_lists.keys())
+    if not keys:
+        return []
+    n = len(dict_of_lists[keys[0]])
+    for k in keys:
+        check.eq(len(dict_of_lists[k]), n, "metric lists have different lengths")
+    return [{k: dict_of_lists[k][i] for k in keys} for i in range(n)]
+
+
+def validate_batch_metrics(batch_metrics: List[Dict[str, Any]]) -> None:
+    if not batch_metrics:
+        return
+    keys = set(batch_metrics[0].keys())
+    for idx, m in enumerate(batch_metrics):
+        check.eq(set(m.keys()), keys, f"inconsistent training metrics: index: {idx}")
+
+
+def make_metrics(num_inputs: Optional[int], batch_metrics: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """``{"batch_metrics": [...], "avg_metrics": {...}, "num_inputs": N}`` (C-done RUN_STEP)."""
+    validate_batch_metrics(batch_metrics)
+    avg = {}  # type: Dict[str, Optional[float]]
+    for name, values in _list_to_dict(batch_metrics).items():
+        m = None
+        try:
+            arr = np.array(values, dtype=object)
+            kept = np.array([v for v in arr if v is not None], dtype=np.float64)
+            m = float(np.mean(kept)) if kept.size else None
+        except (TypeError, ValueError):
+            pass
+        avg[name] = m
+    out = {"batch_metrics": batch_metrics, "avg_metrics": avg}  # type: Dict[str, Any]
+    if num_inputs is not None:
+        out["num_inputs"] = num_inputs
+    return out
+
+
+def wrap_metrics(metrics: workload.Response, stop_requested: bool) -> workload.Response:
+    if isinstance(metrics, workload.Skipped):
+        return metrics
+    return {"metrics": metrics, "stop_requested": stop_requested}
+
+
+def _json_default(obj: Any) -> Any:
+    if isinstance(obj, datetime.datetime):
+        return obj.isoformat()
+    if isinstance(obj, enum.Enum):
+        return obj.name
+    if isinstance(obj, (np.floating,)):
+        return float(obj)
+    if isinstance(obj, (np.integer,)):
+        return int(obj)
+    if isinstance(obj, np.bool_):
+        return bool(obj)
+    if isinstance(obj, uuid.UUID):
+        return str(obj)
+    if isinstance(obj, np.ndarray):
+        return obj.tolist()
+    if isinstance(obj, pathlib.Path):
+        return str(obj)
+    if hasattr(obj, "__json__"):
+        return obj.__json__()
+    try:
+        import torch
+
+        if isinstance(obj, torch.Tensor):
+            return obj.detach().cpu().tolist()
+    except ImportError:  # pragma: no cover
+        pass
+    raise TypeError(f"Unserializable object {obj!r} of type {type(obj)}")
+
+
+def _nan_to_none(o: Any) -> Any:
+    if isinstance(o, float) and (math.isnan(o) or math.isinf(o)):
+        return None
+    if isinstance(o, dict):
+        return {k: _nan_to_none(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_nan_to_none(v) for v in o]
+    return o
+
+
+def json_encode(obj: Any, indent: Optional[int] = None, sort_keys: bool = False) -> str:
+    """JSON with NaN/Infinity serialized as null (not valid JSON otherwise)."""
+    # round-trip through the default hook first so numpy scalars become floats we can check
+    s = json.dumps(obj, default=_json_default, allow_nan=True)
+    return json.dumps(_nan_to_none(json.loads(s)), indent=indent, sort_keys=sort_keys)
+
+
+def write_user_code(path: pathlib.Path, src: Optional[str] = None) -> None:
+    """Copy the model definition directory (cwd by default) to ``<ckpt>/code`` (C-ckpt)."""
+    code_path = path.joinpath("code")
+    if code_path.exists():
+        shutil.rmtree(str(code_path))
+    src = src or os.getcwd()
+
+    def _ignore(d: str, names: List[str]) -> List[str]:
+        ignored = {"__pycache__", ".git", "gpurun_out", ".pytest_cache", "checkpoints"}
+        return [n for n in names if n in ignored or n.endswith(".so") or n.endswith(".pth")]
+
+    shutil.copytree(src, code_path, ignore=_ignore)
+    os.chmod(code_path, 0o755)
