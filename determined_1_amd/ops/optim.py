@@ -116,7 +116,12 @@ class FusedOptimizer:
         self._orig_step = optimizer.step
         self._orig_zero_grad = optimizer.zero_grad
         self._orig_load_state_dict = optimizer.load_state_dict
-        optimizer.step = self.step  # type: ignore
+        def _step(closure: Optional[Callable[[], Any]] = None) -> Any:
+            optimizer._opt_called = True  # type: ignore  # LR schedulers check this
+            return self.step(closure)
+
+        _step._wrapped_by_lr_sched = True  # type: ignore
+        optimizer.step = _step  # type: ignore
         optimizer.zero_grad = self.zero_grad  # type: ignore
         optimizer.load_state_dict = self.load_state_dict  # type: ignore
         optimizer._det_fused = self  # type: ignore
