@@ -59,6 +59,9 @@ def test_bf16_params_fp32_master(gpu):
     torch.manual_seed(0)
     ref = torch.nn.Linear(64, 33)
     dut = copy.deepcopy(ref).to(gpu).to(torch.bfloat16)
+    with torch.no_grad():  # the fp32 master starts from the bf16 model weights
+        for p in ref.parameters():
+            p.copy_(p.bfloat16().float())
     o_ref = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
     o_dut = torch.optim.SGD(dut.parameters(), lr=0.05, momentum=0.9)
     fused = FusedOptimizer(o_dut, gpu)
