@@ -1,0 +1,171 @@
+// C ABI of libdetcore for Python (ctypes): JSON in, JSON out.  Every entry point catches C++
+// exceptions and reports them as {"error": "..."} so a bad config never crashes the caller.
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "detcore/json.h"
+#include "detcore/searcher.h"
+
+using detcore::Json;
+
+namespace {
+
+char* dup(const std::string& s) {
+  char* p = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(p, s.data(), s.size() + 1);
+  return p;
+}
+
+char* err(const std::exception& e) {
+  Json j = Json::object();
+  j["error"] = std::string(e.what());
+  return dup(j.dump());
+}
+
+Json ops_json(const detcore::Ops& ops) {
+  Json a = Json::array();
+  for (const auto& op : ops) a.push_back(op.ToJson());
+  return a;
+}
+
+struct SearcherHandle {
+  std::unique_ptr<detcore::Searcher> s;
+};
+
+detcore::ValidationFn make_valfn(const Json& spec, uint64_t seed) {
+  std::string kind = spec.get_string("kind", "constant");
+  if (kind == "constant") {
+    double v = spec.get_double("value", 1.0);
+    return [v](int, int) { return v; };
+  }
+  if (kind == "random") {
+    auto rng = std::make_shared<detcore::NpRand>(static_cast<uint32_t>(seed ^ 0x5bd1e995u));
+    return [rng](int, int) { return rng->UnitInterval(); };
+  }
+  if (kind == "trial_id") {  // metric = trial_id (or -trial_id): deterministic ranking
+    double sign = spec.get_double("sign", 1.0);
+    return [sign](int tid, int) { return sign * static_cast<double>(tid); };
+  }
+  throw std::invalid_argument("unknown validation function kind " + kind);
+}
+
+}  // namespace
+
+extern "C" {
+
+void detcore_free(char* p) { std::free(p); }
+
+int detcore_abi_version() { return 1; }
+
+void* detcore_searcher_new(const char* searcher_cfg, const char* hparams, uint32_t seed, char** error) {
+  try {
+    Json cfg = Json::parse(searcher_cfg);
+    Json hp = Json::parse(hparams && *hparams ? hparams : "{}");
+    auto* h = new SearcherHandle;
+    h->s = std::make_unique<detcore::Searcher>(seed, detcore::NewSearchMethod(cfg), hp);
+    if (error) *error = nullptr;
+    return h;
+  } catch (const std::exception& e) {
+    if (error) *error = dup(e.what());
+    return nullptr;
+  }
+}
+
+void detcore_searcher_free(void* h) { delete static_cast<SearcherHandle*>(h); }
+
+char* detcore_searcher_call(void* handle, const char* method, const char* args) {
+  try {
+    auto& s = *static_cast<SearcherHandle*>(handle)->s;
+    Json a = Json::parse(args && *args ? args : "{}");
+    std::string m = method;
+    Json out = Json::object();
+    if (m == "initial_operations") {
+      out["ops"] = ops_json(s.InitialOperations());
+    } else if (m == "trial_created") {
+      out["ops"] = ops_json(s.TrialCreated(detcore::Op::FromJson(a.at("create")), static_cast<int>(a.at("trial_id").as_int())));
+    } else if (m == "operation_completed") {
+      out["ops"] = ops_json(s.OperationCompleted(static_cast<int>(a.at("trial_id").as_int()),
+                                                 detcore::Op::FromJson(a.at("op")), a["metrics"]));
+    } else if (m == "trial_closed") {
+      out["ops"] = ops_json(s.TrialClosed(detcore::ParseRequestID(a.at("request_id").as_string())));
+    } else if (m == "trial_exited_early") {
+      out["ops"] = ops_json(s.TrialExitedEarly(static_cast<int>(a.at("trial_id").as_int()),
+                                               detcore::ParseExitedReason(a.get_string("reason", "ERRORED"))));
+    } else if (m == "workload_completed") {
+      s.WorkloadCompleted(a["msg"], a.get_double("units", 0));
+    } else if (m == "progress") {
+      out["progress"] = s.Progress();
+    } else if (m == "uncommitted_events") {
+      Json ev = Json::array();
+      for (auto& e : s.UncommittedEvents()) ev.push_back(e);
+      out["events"] = ev;
+    } else if (m == "state") {
+      out["trials_requested"] = s.trials_requested();
+      out["trials_closed"] = s.trials_closed();
+      out["shutdown"] = s.shutdown();
+      out["total_units_completed"] = s.total_units_completed();
+    } else {
+      throw std::invalid_argument("unknown searcher method " + m);
+    }
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+char* detcore_simulate(const char* searcher_cfg, const char* hparams, uint32_t seed, const char* valfn,
+                       int random_order, uint64_t sim_seed) {
+  try {
+    Json cfg = Json::parse(searcher_cfg);
+    Json hp = Json::parse(hparams && *hparams ? hparams : "{}");
+    detcore::Searcher s(seed, detcore::NewSearchMethod(cfg), hp);
+    auto fn = make_valfn(Json::parse(valfn && *valfn ? valfn : "{}"), sim_seed);
+    auto res = detcore::Simulate(s, fn, random_order != 0, sim_seed, cfg.get_string("metric", "metric"));
+    Json out = Json::object();
+    out["results"] = res.Summary();
+    out["seed"] = static_cast<int64_t>(sim_seed);
+    Json trials = Json::array();
+    for (const auto& rid : res.order) {
+      Json t = Json::object();
+      t["request_id"] = detcore::RequestIDString(rid);
+      Json ops = Json::array();
+      for (const auto& op : res.results.at(rid)) ops.push_back(op.ToJson());
+      t["ops"] = ops;
+      trials.push_back(t);
+    }
+    out["trials"] = trials;
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+char* detcore_nprand(uint32_t seed, const char* op, int64_t arg, int64_t n) {
+  try {
+    detcore::NpRand r(seed);
+    std::string o = op;
+    Json out = Json::array();
+    for (int64_t i = 0; i < n; ++i) {
+      if (o == "bits32") out.push_back(static_cast<int64_t>(r.Bits32()));
+      else if (o == "unit_interval") out.push_back(r.UnitInterval());
+      else if (o == "intn") out.push_back(r.Intn(arg));
+      else if (o == "request_id") out.push_back(detcore::RequestIDString(detcore::NewRequestID(r)));
+      else throw std::invalid_argument("unknown nprand op " + o);
+    }
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+char* detcore_json_roundtrip(const char* text) {
+  try {
+    return dup(Json::parse(text).dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+}  // extern "C"
