@@ -1,0 +1,136 @@
+"""Python binding of the native C++ hyperparameter searchers (``native/src/search*.cc``).
+
+The master (C++) links the searchers directly; this binding serves ``det preview-search``,
+local tooling and the test-suite.  Calls cross the boundary as JSON (``detcore_searcher_call``).
+Reference behaviour: ``master/pkg/searcher`` (Searcher event log, 9 search methods, Simulate).
+"""
+import ctypes
+import json
+from typing import Any, Dict, List, Optional
+
+from determined_1_amd._native import load_detcore
+
+
+def _lib() -> ctypes.CDLL:
+    lib = load_detcore()
+    if not getattr(lib, "_det_searcher_sigs", False):
+        lib.detcore_free.argtypes = [ctypes.c_void_p]
+        lib.detcore_searcher_new.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_void_p)]
+        lib.detcore_searcher_new.restype = ctypes.c_void_p
+        lib.detcore_searcher_free.argtypes = [ctypes.c_void_p]
+        lib.detcore_searcher_call.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+        lib.detcore_searcher_call.restype = ctypes.c_void_p
+        lib.detcore_simulate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                         ctypes.c_int, ctypes.c_uint64]
+        lib.detcore_simulate.restype = ctypes.c_void_p
+        lib.detcore_nprand.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int64, ctypes.c_int64]
+        lib.detcore_nprand.restype = ctypes.c_void_p
+        lib.detcore_json_roundtrip.argtypes = [ctypes.c_char_p]
+        lib.detcore_json_roundtrip.restype = ctypes.c_void_p
+        lib._det_searcher_sigs = True
+    return lib
+
+
+def _take(ptr: int) -> Any:
+    lib = _lib()
+    try:
+        s = ctypes.cast(ptr, ctypes.c_char_p).value.decode()
+    finally:
+        lib.detcore_free(ptr)
+    out = json.loads(s)
+    if isinstance(out, dict) and "error" in out and len(out) == 1:
+        raise SearcherError(out["error"])
+    return out
+
+
+class SearcherError(RuntimeError):
+    pass
+
+
+class Searcher:
+    """A seeded searcher: ``initial_operations()``, ``trial_created()``,
+    ``operation_completed()``, ``trial_closed()``, ``trial_exited_early()``, ``progress()``."""
+
+    def __init__(self, searcher_config: Dict[str, Any], hyperparameters: Optional[Dict[str, Any]] = None,
+                 seed: int = 0) -> None:
+        lib = _lib()
+        err = ctypes.c_void_p()
+        h = lib.detcore_searcher_new(json.dumps(searcher_config).encode(), json.dumps(hyperparameters or {}).encode(),
+                                     seed & 0xFFFFFFFF, ctypes.byref(err))
+        if not h:
+            msg = ctypes.cast(err, ctypes.c_char_p).value.decode() if err.value else "unknown error"
+            if err.value:
+                lib.detcore_free(err)
+            raise SearcherError(msg)
+        self._h = h
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if h:
+            _lib().detcore_searcher_free(h)
+            self._h = None
+
+    def _call(self, method: str, args: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+        return _take(_lib().detcore_searcher_call(self._h, method.encode(), json.dumps(args or {}).encode()))
+
+    def initial_operations(self) -> List[Dict[str, Any]]:
+        return self._call("initial_operations")["ops"]
+
+    def trial_created(self, create: Dict[str, Any], trial_id: int) -> List[Dict[str, Any]]:
+        return self._call("trial_created", {"create": create, "trial_id": trial_id})["ops"]
+
+    def operation_completed(self, trial_id: int, op: Dict[str, Any], metrics: Any = None) -> List[Dict[str, Any]]:
+        return self._call("operation_completed", {"trial_id": trial_id, "op": op, "metrics": metrics or {}})["ops"]
+
+    def trial_closed(self, request_id: str) -> List[Dict[str, Any]]:
+        return self._call("trial_closed", {"request_id": request_id})["ops"]
+
+    def trial_exited_early(self, trial_id: int, reason: str = "ERRORED") -> List[Dict[str, Any]]:
+        return self._call("trial_exited_early", {"trial_id": trial_id, "reason": reason})["ops"]
+
+    def workload_completed(self, msg: Dict[str, Any], units: float) -> None:
+        self._call("workload_completed", {"msg": msg, "units": units})
+
+    def progress(self) -> float:
+        return float(self._call("progress")["progress"])
+
+    def uncommitted_events(self) -> List[Dict[str, Any]]:
+        return self._call("uncommitted_events")["events"]
+
+    def state(self) -> Dict[str, Any]:
+        return self._call("state")
+
+
+def simulate(searcher_config: Dict[str, Any], hyperparameters: Optional[Dict[str, Any]] = None, seed: int = 0,
+             validation: Optional[Dict[str, Any]] = None, random_order: bool = True, sim_seed: int = 0) -> Dict[str, Any]:
+    """Offline simulation (``det preview-search``): ``{"results": {"<ops short form>": count}, ...}``."""
+    return _take(_lib().detcore_simulate(
+        json.dumps(searcher_config).encode(), json.dumps(hyperparameters or {}).encode(), seed & 0xFFFFFFFF,
+        json.dumps(validation or {"kind": "constant", "value": 1.0}).encode(), int(random_order), sim_seed))
+
+
+def nprand(seed: int, op: str, n: int, arg: int = 0) -> List[Any]:
+    return _take(_lib().detcore_nprand(seed & 0xFFFFFFFF, op.encode(), arg, n))
+
+
+def json_roundtrip(text: str) -> Any:
+    return _take(_lib().detcore_json_roundtrip(text.encode()))
+
+
+def short_form(ops: List[Dict[str, Any]]) -> str:
+    """Runnable ops of one trial as the reference tests' short form ("1000B V 2000B V")."""
+    parts = []
+    for op in ops:
+        t = op["type"]
+        if t == "Train":
+            (unit, n), = op["length"].items()
+            parts.append(f"{n}{unit[0].upper()}")
+        elif t == "Validate":
+            parts.append("V")
+        elif t == "Checkpoint":
+            parts.append("C")
+    return " ".join(parts)
+
+
+__all__ = ["Searcher", "SearcherError", "json_roundtrip", "nprand", "short_form", "simulate"]

@@ -16,13 +16,6 @@ namespace {
 
 constexpr double kExitedMetric = DBL_MAX;
 
-Unit unit_of(const Json& cfg) {
-  for (const char* k : {"max_length", "length_per_round", "budget"}) {
-    if (cfg.has(k)) return Length::FromJson(cfg[k]).unit;
-  }
-  return Unit::Batches;
-}
-
 int64_t imax(int64_t a, int64_t b) { return a > b ? a : b; }
 int64_t imin(int64_t a, int64_t b) { return a < b ? a : b; }
 
