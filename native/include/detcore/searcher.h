@@ -59,6 +59,16 @@ struct Length {
   std::string ShortString() const;  // "64000R" / "5B" / "2E"
 };
 
+// Unit conversions (master/pkg/model/length.go).
+struct UnitContext {
+  Unit default_unit = Unit::Batches;
+  int64_t global_batch_size = 1;
+  int64_t records_per_epoch = 0;
+};
+int64_t ToNearestBatch(const Length& l, const UnitContext& c);
+bool EqualWithinBatch(const Length& l, int64_t batches, const UnitContext& c);
+double UnitsFromBatches(int64_t batches, const UnitContext& c);
+
 using RequestID = std::array<uint8_t, 16>;
 std::string RequestIDString(const RequestID& r);
 RequestID ParseRequestID(const std::string& s);

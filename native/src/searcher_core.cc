@@ -142,6 +142,35 @@ std::string Length::ShortString() const {
   return std::to_string(units) + suffix;
 }
 
+int64_t ToNearestBatch(const Length& l, const UnitContext& c) {
+  switch (l.unit) {
+    case Unit::Records: return l.units / c.global_batch_size;
+    case Unit::Batches: return l.units;
+    case Unit::Epochs: return (l.units * c.records_per_epoch) / c.global_batch_size;
+  }
+  return l.units;
+}
+
+bool EqualWithinBatch(const Length& l, int64_t batches, const UnitContext& c) {
+  switch (l.unit) {
+    case Unit::Records: return std::llabs(l.units - batches * c.global_batch_size) < c.global_batch_size;
+    case Unit::Batches: return l.units == batches;
+    case Unit::Epochs:
+      return std::llabs(l.units * c.records_per_epoch - batches * c.global_batch_size) < c.global_batch_size;
+  }
+  return false;
+}
+
+double UnitsFromBatches(int64_t batches, const UnitContext& c) {
+  switch (c.default_unit) {
+    case Unit::Records: return static_cast<double>(batches * c.global_batch_size);
+    case Unit::Batches: return static_cast<double>(batches);
+    case Unit::Epochs:
+      return static_cast<double>(batches * c.global_batch_size) / static_cast<double>(c.records_per_epoch);
+  }
+  return static_cast<double>(batches);
+}
+
 std::string RequestIDString(const RequestID& r) {
   char buf[37];
   std::snprintf(buf, sizeof(buf), "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", r[0], r[1],

@@ -1,0 +1,155 @@
+// Sequencer scenarios (cf. reference master/internal/trial_workload_sequencer_test.go).
+#include "detcore/sequencer.h"
+#include "test_util.h"
+
+using namespace detcore;
+
+namespace {
+
+SequencerConfig cfg(int64_t min_val, int64_t min_ckpt, const char* policy = "none", int64_t unit = 100) {
+  SequencerConfig c;
+  c.experiment_id = 1;
+  c.checkpoint_policy = policy;
+  c.min_validation_period = Length(Unit::Batches, min_val);
+  c.min_checkpoint_period = Length(Unit::Batches, min_ckpt);
+  c.global_batch_size = 64;
+  c.scheduling_unit = unit;
+  return c;
+}
+
+CompletedMessage done(const Workload& w, Json metrics = Json::object()) {
+  CompletedMessage m;
+  m.workload = w;
+  m.metrics = std::move(metrics);
+  return m;
+}
+
+Json ckpt_metrics(const char* uuid) {
+  Json j = Json::object();
+  j["uuid"] = uuid;
+  return j;
+}
+
+}  // namespace
+
+TEST(sequencer_min_periods_and_scheduling_unit) {
+  NpRand rand(0);
+  Op create = Op::Create(rand, Json::object());
+  TrialWorkloadSequencer s(cfg(200, 400));
+  s.SetTrialID(1);
+  s.OperationRequested(Op::Train(create.request_id, Length(Unit::Batches, 500)));
+  s.OperationRequested(Op::Validate(create.request_id));
+  s.OperationRequested(Op::Checkpoint(create.request_id));
+  // two 100-batch steps, then the min-validation validation
+  Workload w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::RunStep && w.num_batches == 100 && w.step_id == 1 && w.total_batches_processed == 0);
+  EXPECT(!s.WorkloadCompleted(done(w), false).op);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::RunStep && w.step_id == 2 && w.total_batches_processed == 100);
+  s.WorkloadCompleted(done(w), false);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::ComputeValidationMetrics && w.step_id == 2);
+  s.WorkloadCompleted(done(w), false);
+  // steps 3,4 -> min checkpoint at 400
+  for (int i = 3; i <= 4; ++i) {
+    w = s.NextWorkload();
+    EXPECT(w.kind == Workload::Kind::RunStep && w.step_id == i);
+    s.WorkloadCompleted(done(w), false);
+  }
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::ComputeValidationMetrics);  // 200 since last val
+  s.WorkloadCompleted(done(w), false);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::CheckpointModel && w.step_id == 4);
+  s.WorkloadCompleted(done(w, ckpt_metrics("c4")), false);
+  // last train step completes the Train op
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::RunStep && w.step_id == 5 && w.num_batches == 100);
+  auto c = s.WorkloadCompleted(done(w), false);
+  EXPECT(c.op && c.op->kind == Op::Kind::Train);
+  // Validate op: un-checkpointed batches -> checkpoint first
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::CheckpointModel && w.step_id == 5);
+  s.WorkloadCompleted(done(w, ckpt_metrics("c5")), false);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::ComputeValidationMetrics);
+  c = s.WorkloadCompleted(done(w), false);
+  EXPECT(c.op && c.op->kind == Op::Kind::Validate);
+  // Checkpoint op: the cached step-5 checkpoint completes it without a new workload
+  EXPECT(!s.UpToDate());
+  c = s.CompleteCachedCheckpoints();
+  EXPECT(c.op && c.op->kind == Op::Kind::Checkpoint);
+  EXPECT(s.UpToDate());
+  EXPECT_EQ(s.LatestCheckpoint()["uuid"].as_string(), std::string("c5"));
+}
+
+TEST(sequencer_rollback_to_last_checkpoint) {
+  NpRand rand(0);
+  Op create = Op::Create(rand, Json::object());
+  TrialWorkloadSequencer s(cfg(0, 0, "none", 10));
+  s.SetTrialID(7);
+  s.OperationRequested(Op::Train(create.request_id, Length(Unit::Batches, 30)));
+  s.OperationRequested(Op::Checkpoint(create.request_id));
+  Workload w = s.NextWorkload();
+  s.WorkloadCompleted(done(w), false);
+  auto pc = s.PrecloseCheckpointWorkload();
+  EXPECT(pc.has_value() && pc->step_id == 1 && pc->total_batches_processed == 10);
+  s.WorkloadCompleted(done(*pc, ckpt_metrics("a")), false);
+  w = s.NextWorkload();
+  s.WorkloadCompleted(done(w), false);
+  EXPECT_EQ(s.TotalBatchesProcessed(), 20);
+  int64_t step = s.RollBack();
+  EXPECT_EQ(step, 1);
+  EXPECT_EQ(s.TotalBatchesProcessed(), 10);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::RunStep && w.step_id == 2 && w.total_batches_processed == 10 && w.num_batches == 10);
+}
+
+TEST(sequencer_best_policy_post_validation_checkpoint) {
+  NpRand rand(0);
+  Op create = Op::Create(rand, Json::object());
+  TrialWorkloadSequencer s(cfg(5, 0, "best", 5));
+  s.SetTrialID(1);
+  s.OperationRequested(Op::Train(create.request_id, Length(Unit::Batches, 10)));
+  Workload w = s.NextWorkload();
+  s.WorkloadCompleted(done(w), false);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::ComputeValidationMetrics);
+  s.WorkloadCompleted(done(w), /*is_best=*/true);
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::CheckpointModel);
+}
+
+TEST(sequencer_graceful_stop_checkpoints_then_up_to_date) {
+  NpRand rand(0);
+  Op create = Op::Create(rand, Json::object());
+  TrialWorkloadSequencer s(cfg(0, 0, "none", 5));
+  s.SetTrialID(1);
+  s.OperationRequested(Op::Train(create.request_id, Length(Unit::Batches, 100)));
+  Workload w = s.NextWorkload();
+  CompletedMessage m = done(w);
+  m.exited_reason = ExitedReason::UserCanceled;
+  s.WorkloadCompleted(m, false);
+  EXPECT(!s.UpToDate());
+  w = s.NextWorkload();
+  EXPECT(w.kind == Workload::Kind::CheckpointModel);
+  s.WorkloadCompleted(done(w, ckpt_metrics("g")), false);
+  EXPECT(s.UpToDate());
+}
+
+TEST(json_roundtrip_and_ordering) {
+  Json j = Json::parse(R"({"b": [1, 2.5, "x"], "a": {"z": null, "y": true}, "c": -0.000001})");
+  EXPECT_EQ(j.dump(), std::string(R"({"a":{"y":true,"z":null},"b":[1,2.5,"x"],"c":-0.000001})"));
+  Json k = j;
+  k["a"]["y"] = false;  // copy-on-write: j unchanged
+  EXPECT(j["a"]["y"].as_bool());
+  EXPECT_EQ(Json::parse("1e21").dump(), std::string("1e+21"));
+}
+
+TEST(length_conversions) {
+  UnitContext c{Unit::Records, 64, 6400};
+  EXPECT_EQ(ToNearestBatch(Length(Unit::Records, 640), c), 10);
+  EXPECT_EQ(ToNearestBatch(Length(Unit::Epochs, 2), c), 200);
+  EXPECT(EqualWithinBatch(Length(Unit::Records, 650), 10, c));
+  EXPECT(!EqualWithinBatch(Length(Unit::Records, 704), 10, c));
+}
