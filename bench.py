@@ -38,6 +38,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--arch", default="resnet50")
     ap.add_argument("--bucket-mb", type=int, default=int(os.environ.get("DET_BENCH_BUCKET_MB", "64")))
     ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--no-fused-bn", action="store_true", help="stock MIOpen BN + separate add/ReLU (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "0")))
     return ap.parse_args()
 
@@ -70,6 +71,7 @@ def main() -> None:
             "arch": args.arch,
             "amp": args.amp,
             "channels_last": not args.no_channels_last,
+            "fused_bn": not args.no_fused_bn,
         },
         "resources": {"slots_per_trial": world},
         "optimizations": {"tensor_fusion_threshold": args.bucket_mb},
@@ -137,6 +139,7 @@ def main() -> None:
                 "amp": args.amp,
                 "optimizer": "SGD-momentum (fused arena HIP kernel)",
                 "bucket_mb": args.bucket_mb,
+                "fused_bn": not args.no_fused_bn,
                 "final_avg_loss": loss,
             },
         }

@@ -7,7 +7,8 @@ HIP kernel -> bf16 channels_last tensor -> ResNet-50 forward/backward (MIOpen NH
 backward when ``slots_per_trial > 1``.
 
 Hyperparameters: ``global_batch_size``, ``lr``, ``momentum``, ``weight_decay``, ``arch``,
-``amp`` (O0/O1/O2), ``channels_last``, ``num_classes``, ``image_size``.
+``amp`` (O0/O1/O2), ``channels_last``, ``num_classes``, ``image_size``, ``fused_bn`` (fused
+BN(+add)(+ReLU) HIP kernels, default true).
 """
 from typing import Any, Dict
 
@@ -28,6 +29,7 @@ class ResNetImageNetTrial(det_torch.PyTorchTrial):
         self.num_classes = int(hp.get("num_classes", 1000))
         self.image_size = int(hp.get("image_size", 224))
         self.channels_last = bool(hp.get("channels_last", True))
+        resnet.FUSED_BN = bool(hp.get("fused_bn", True))
         model = getattr(resnet, arch)(num_classes=self.num_classes)
         if self.channels_last:
             model = model.to(memory_format=torch.channels_last)

@@ -11,6 +11,16 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from determined_1_amd.ops.norm import BatchNormAct2d
+
+# Fused BN(+add)(+ReLU) HIP kernels (ops/csrc/det_norm.hip) on by default; set
+# ``resnet.FUSED_BN = False`` (or hparam ``fused_bn: false``) for the stock MIOpen path.
+FUSED_BN = True
+
+
+def bn(c: int, relu: bool) -> BatchNormAct2d:
+    return BatchNormAct2d(c, relu=relu, fused=FUSED_BN)
+
 
 def conv3x3(cin: int, cout: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
@@ -26,17 +36,16 @@ class BasicBlock(nn.Module):
     def __init__(self, cin: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None) -> None:
         super().__init__()
         self.conv1 = conv3x3(cin, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = bn(planes, relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = bn(planes, relu=True)  # relu(bn2(conv2) + identity), fused
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), idt)
 
 
 class Bottleneck(nn.Module):
@@ -45,20 +54,19 @@ class Bottleneck(nn.Module):
     def __init__(self, cin: int, planes: int, stride: int = 1, downsample: Optional[nn.Module] = None) -> None:
         super().__init__()
         self.conv1 = conv1x1(cin, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = bn(planes, relu=True)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = bn(planes, relu=True)
         self.conv3 = conv1x1(planes, planes * self.expansion)
-        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.bn3 = bn(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity), fused
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), idt)
 
 
 class ResNet(nn.Module):
@@ -67,7 +75,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = bn(64, relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -94,7 +102,7 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                       nn.BatchNorm2d(planes * block.expansion))
+                                       bn(planes * block.expansion, relu=False))
         layers = [block(self.inplanes, planes, stride, downsample)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
@@ -102,7 +110,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

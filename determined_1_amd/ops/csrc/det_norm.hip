@@ -1,0 +1,627 @@
+// det_norm.hip — fused training BatchNorm (+ residual add) (+ ReLU) for channels_last activations.
+//
+// Why this exists: in the ResNet-50 north-star step (profiles/r1_resnet50_bs256_o1_kernel_stats.csv)
+// MIOpen's NHWC batch-norm kernels plus the separate residual-add / ReLU / ReLU-backward
+// elementwise launches are ~20 ms of a 44 ms step (>45%).  Every one of them is HBM-bound, so the
+// only way to speed them up is to touch fewer bytes: fold the add and the activation into the
+// normalisation pass and recompute the ReLU mask from the saved input instead of materialising it.
+//
+// Layout: x is a [M, C] row-major matrix (M = N*H*W, channels contiguous = torch channels_last),
+// C % 8 == 0, 16-byte aligned.  A lane owns 8 consecutive channels (one 16 B bf16 vector) and
+// walks rows; a 256-thread block covers `tpr` channel groups x `R` rows per iteration.
+//
+// Forward (training), 3 launches, x read twice (the 2nd read often hits the 256 MiB MALL):
+//   1. stats_partial : per (row-block, channel) mean / M2 from shifted sums (no cancellation)
+//   2. stats_finalize: Chan merge of the partials -> mean, rstd, scale=g*rstd, shift=b-mean*scale,
+//                      running-stat update and num_batches_tracked += 1 (no extra torch launch)
+//   3. apply_fwd     : y = act(x*scale + shift [+ res])
+// Backward, 3 launches:
+//   1. bwd_partial   : sum(dz), sum(dz*(x-mean)) with dz = dy * relu'(.)
+//                      relu' comes from x itself (z = x*scale+shift > 0, bit-identical to fwd) when
+//                      there is no residual, else from the saved output y > 0
+//   2. bwd_finalize  : dgamma, dbeta and the affine dx coefficients  dx = A*dz + B*x + C
+//   3. apply_bwd     : dx (and d_residual = dz when the block had a residual input)
+//
+// Reductions are two-level (LDS, then a finalize launch) with no float atomics: results are
+// bitwise reproducible run to run.  No host syncs: capturable in a hipGraph.
+//
+// Reference parity: the reference delegates BN to torch/cuDNN inside user models
+// (examples/computer_vision/*); SURVEY §2.4 K7.  Semantics follow torch.nn.BatchNorm2d
+// (biased variance for normalisation, unbiased for running_var, momentum=None -> cumulative).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kFinThreads = 1024;  // finalize: 64 channels x 16 waves
+constexpr int kFinCh = 64;
+constexpr int kFinLanes = kFinThreads / kFinCh;
+
+typedef unsigned short us8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<unsigned short>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<unsigned short>(u >> 16);
+}
+
+// 8-element vector IO: bf16 = one 16 B load, fp32 = two 16 B loads.
+template <typename T> struct IO8;
+template <> struct IO8<unsigned short> {
+  static __device__ __forceinline__ void load(const unsigned short* p, float (&v)[8]) {
+    us8 r = *reinterpret_cast<const us8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(r[j]);
+  }
+  static __device__ __forceinline__ void store(unsigned short* p, const float (&v)[8]) {
+    us8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
+    *reinterpret_cast<us8*>(p) = r;
+  }
+};
+template <> struct IO8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    float4 a = reinterpret_cast<const float4*>(p)[0];
+    float4 b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) { IO8<float>::load(p, v); }
+
+struct Geom {
+  int64_t M;   // rows
+  int C;       // channels
+  int tpr;     // threads per row (channel groups per block)
+  int R;       // rows per block iteration
+  int64_t rpb; // rows per row-block
+  int nrb;     // number of row-blocks
+};
+
+// ---------------------------------------------------------------------------------------------
+// Forward stats: per-thread shifted sums -> (mean, M2) -> block merge in LDS -> partials.
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+bn_stats_partial(const T* __restrict__ x, Geom g, float* __restrict__ pmean, float* __restrict__ pm2) {
+  __shared__ float lmean[kThreads * 8];
+  __shared__ float lm2[kThreads * 8];
+  __shared__ int lcnt[kThreads];
+  const int tx = threadIdx.x % g.tpr, ty = threadIdx.x / g.tpr;
+  const int cgrp = blockIdx.y * g.tpr + tx;
+  const bool active = ty < g.R && cgrp * 8 < g.C;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * g.rpb;
+  const int64_t r1 = min(g.M, r0 + g.rpb);
+  float k[8], s[8], ss[8];
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { k[j] = 0.f; s[j] = 0.f; ss[j] = 0.f; }
+  if (active && r0 + ty < r1) {
+    const int64_t C = g.C;
+    const T* base = x + cgrp * 8;
+    IO8<T>::load(base + (r0 + ty) * C, k);  // shift = first sample of this lane
+    int64_t r = r0 + ty;
+    const int64_t R = g.R;
+    for (; r + 3 * R < r1; r += 4 * R) {
+      float a[8], b[8], c[8], d[8];
+      IO8<T>::load(base + r * C, a);
+      IO8<T>::load(base + (r + R) * C, b);
+      IO8<T>::load(base + (r + 2 * R) * C, c);
+      IO8<T>::load(base + (r + 3 * R) * C, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float da = a[j] - k[j], db = b[j] - k[j], dc = c[j] - k[j], dd = d[j] - k[j];
+        s[j] += (da + db) + (dc + dd);
+        ss[j] += (da * da + db * db) + (dc * dc + dd * dd);
+      }
+      n += 4;
+    }
+    for (; r < r1; r += R) {
+      float a[8];
+      IO8<T>::load(base + r * C, a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float da = a[j] - k[j];
+        s[j] += da;
+        ss[j] += da * da;
+      }
+      n += 1;
+    }
+  }
+  const float inv_n = n > 0 ? 1.f / static_cast<float>(n) : 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float m = s[j] * inv_n;
+    lmean[threadIdx.x * 8 + j] = n > 0 ? k[j] + m : 0.f;
+    lm2[threadIdx.x * 8 + j] = n > 0 ? fmaxf(ss[j] - s[j] * m, 0.f) : 0.f;
+  }
+  lcnt[threadIdx.x] = n;
+  __syncthreads();
+  if (ty == 0 && cgrp * 8 < g.C) {
+    // closed-form merge of the R row-lanes of this channel group
+    float tot = 0.f, mu[8], m2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = 0.f; m2[j] = 0.f; }
+    for (int q = 0; q < g.R; ++q) {
+      const int t = q * g.tpr + tx;
+      const float nq = static_cast<float>(lcnt[t]);
+      tot += nq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mu[j] += nq * lmean[t * 8 + j];
+    }
+    const float inv_tot = tot > 0.f ? 1.f / tot : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mu[j] *= inv_tot;
+    for (int q = 0; q < g.R; ++q) {
+      const int t = q * g.tpr + tx;
+      const float nq = static_cast<float>(lcnt[t]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = lmean[t * 8 + j] - mu[j];
+        m2[j] += lm2[t * 8 + j] + nq * d * d;
+      }
+    }
+    const int64_t o = static_cast<int64_t>(blockIdx.x) * g.C + cgrp * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pmean[o + j] = mu[j];
+      pm2[o + j] = m2[j];
+    }
+  }
+}
+
+struct FinArgs {
+  const float* gamma;  // may be null (affine=False)
+  const float* beta;
+  float* running_mean;  // may be null (track_running_stats=False)
+  float* running_var;
+  int64_t* num_batches_tracked;  // may be null
+  float momentum;                // < 0: cumulative moving average (torch momentum=None)
+  float eps;
+  float* save_mean;
+  float* save_rstd;
+  float* scale;
+  float* shift;
+};
+
+// One block = 64 channels x 16 row-lanes (one wave per row-lane: 256 B coalesced partial rows).
+__global__ void __launch_bounds__(kFinThreads)
+bn_stats_finalize(const float* __restrict__ pmean, const float* __restrict__ pm2, Geom g, FinArgs a) {
+  __shared__ float red[kFinLanes][kFinCh];
+  __shared__ float gmean[kFinCh];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  // pass 1: global mean = sum(n_b * mean_b) / M
+  float acc = 0.f;
+  if (ok) {
+    for (int b = lane; b < g.nrb; b += kFinLanes) {
+      const int64_t nb = min(g.rpb, g.M - static_cast<int64_t>(b) * g.rpb);
+      acc += static_cast<float>(nb) * pmean[static_cast<int64_t>(b) * g.C + c];
+    }
+  }
+  red[lane][cl] = acc;
+  __syncthreads();
+  if (lane == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) t += red[q][cl];
+    gmean[cl] = t / static_cast<float>(g.M);
+  }
+  __syncthreads();
+  const float mean = gmean[cl];
+  // pass 2: M2 = sum(M2_b + n_b * (mean_b - mean)^2)
+  acc = 0.f;
+  if (ok) {
+    for (int b = lane; b < g.nrb; b += kFinLanes) {
+      const int64_t nb = min(g.rpb, g.M - static_cast<int64_t>(b) * g.rpb);
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      const float d = pmean[o] - mean;
+      acc += pm2[o] + static_cast<float>(nb) * d * d;
+    }
+  }
+  __syncthreads();
+  red[lane][cl] = acc;
+  __syncthreads();
+  if (lane == 0 && ok) {
+    float m2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) m2 += red[q][cl];
+    const float var = m2 / static_cast<float>(g.M);
+    const float rstd = rsqrtf(var + a.eps);
+    const float gm = a.gamma ? a.gamma[c] : 1.f;
+    const float bt = a.beta ? a.beta[c] : 0.f;
+    const float sc = gm * rstd;
+    a.save_mean[c] = mean;
+    a.save_rstd[c] = rstd;
+    a.scale[c] = sc;
+    a.shift[c] = bt - mean * sc;
+    if (a.running_mean) {
+      float f = a.momentum;
+      if (f < 0.f) f = a.num_batches_tracked ? 1.f / static_cast<float>(*a.num_batches_tracked + 1) : 0.f;
+      const float unbiased = g.M > 1 ? m2 / static_cast<float>(g.M - 1) : var;
+      a.running_mean[c] = (1.f - f) * a.running_mean[c] + f * mean;
+      a.running_var[c] = (1.f - f) * a.running_var[c] + f * unbiased;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Elementwise apply: y = act(x*scale + shift [+ res]); grid-stride over 8-element vectors, 4 in
+// flight per thread.
+// ---------------------------------------------------------------------------------------------
+template <typename T, bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads)
+bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
+             const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int C,
+             int64_t* __restrict__ bump) {
+  // num_batches_tracked += 1 rides on this launch (stream-ordered after the finalize that read it)
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
+  const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v0 < nvec; v0 += 4 * S) {
+    float xv[4][8], rv[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t v = v0 + u * S;
+      if (v < nvec) {
+        IO8<T>::load(x + v * 8, xv[u]);
+        if (RES) IO8<T>::load(res + v * 8, rv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t v = v0 + u * S;
+      if (v < nvec) {
+        const int c0 = static_cast<int>((v * 8) % C);
+        float sc[8], sh[8], o[8];
+        load8f(scale + c0, sc);
+        load8f(shift + c0, sh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float z = __fmaf_rn(xv[u][j], sc[j], sh[j]);
+          if (RES) z += rv[u][j];
+          o[j] = RELU ? fmaxf(z, 0.f) : z;
+        }
+        IO8<T>::store(y + v * 8, o);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward partial sums.  MASK: 0 = identity, 1 = relu mask recomputed from x, 2 = from y > 0.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int MASK>
+__global__ void __launch_bounds__(kThreads)
+bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y, Geom g,
+               const float* __restrict__ mean, const float* __restrict__ scale,
+               const float* __restrict__ shift, float* __restrict__ psum, float* __restrict__ psumx) {
+  __shared__ float l1[kThreads * 8];
+  __shared__ float l2[kThreads * 8];
+  const int tx = threadIdx.x % g.tpr, ty = threadIdx.x / g.tpr;
+  const int cgrp = blockIdx.y * g.tpr + tx;
+  const bool chan_ok = cgrp * 8 < g.C;
+  const bool active = ty < g.R && chan_ok;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * g.rpb;
+  const int64_t r1 = min(g.M, r0 + g.rpb);
+  float s[8], sx[8], mu[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; sx[j] = 0.f; mu[j] = 0.f; sc[j] = 0.f; sh[j] = 0.f; }
+  if (active) {
+    const int c0 = cgrp * 8;
+    load8f(mean + c0, mu);
+    if (MASK == 1) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
+    const int64_t C = g.C, R = g.R;
+    const int64_t off = c0;
+    int64_t r = r0 + ty;
+    for (; r + R < r1; r += 2 * R) {
+      float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
+      IO8<T>::load(dy + r * C + off, d0);
+      IO8<T>::load(x + r * C + off, x0);
+      IO8<T>::load(dy + (r + R) * C + off, d1);
+      IO8<T>::load(x + (r + R) * C + off, x1);
+      if (MASK == 2) { IO8<T>::load(y + r * C + off, y0); IO8<T>::load(y + (r + R) * C + off, y1); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = d0[j], b = d1[j];
+        if (MASK == 1) {
+          a = __fmaf_rn(x0[j], sc[j], sh[j]) > 0.f ? a : 0.f;
+          b = __fmaf_rn(x1[j], sc[j], sh[j]) > 0.f ? b : 0.f;
+        } else if (MASK == 2) {
+          a = y0[j] > 0.f ? a : 0.f;
+          b = y1[j] > 0.f ? b : 0.f;
+        }
+        s[j] += a + b;
+        sx[j] += a * (x0[j] - mu[j]) + b * (x1[j] - mu[j]);
+      }
+    }
+    for (; r < r1; r += R) {
+      float d0[8], x0[8], y0[8];
+      IO8<T>::load(dy + r * C + off, d0);
+      IO8<T>::load(x + r * C + off, x0);
+      if (MASK == 2) IO8<T>::load(y + r * C + off, y0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = d0[j];
+        if (MASK == 1) a = __fmaf_rn(x0[j], sc[j], sh[j]) > 0.f ? a : 0.f;
+        else if (MASK == 2) a = y0[j] > 0.f ? a : 0.f;
+        s[j] += a;
+        sx[j] += a * (x0[j] - mu[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    l1[threadIdx.x * 8 + j] = s[j];
+    l2[threadIdx.x * 8 + j] = sx[j];
+  }
+  __syncthreads();
+  if (ty == 0 && chan_ok) {
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a[j] = 0.f; b[j] = 0.f; }
+    for (int q = 0; q < g.R; ++q) {
+      const int t = q * g.tpr + tx;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] += l1[t * 8 + j]; b[j] += l2[t * 8 + j]; }
+    }
+    const int64_t o = static_cast<int64_t>(blockIdx.x) * g.C + cgrp * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { psum[o + j] = a[j]; psumx[o + j] = b[j]; }
+  }
+}
+
+struct BwdFin {
+  const float* gamma;  // may be null
+  const float* rstd;
+  const float* mean;
+  float* dgamma;  // may be null
+  float* dbeta;   // may be null
+  float* coef;    // [3][C]: A, B, C
+};
+
+__global__ void __launch_bounds__(kFinThreads)
+bn_bwd_finalize(const float* __restrict__ psum, const float* __restrict__ psumx, Geom g, BwdFin a) {
+  __shared__ float r1[kFinLanes][kFinCh];
+  __shared__ float r2[kFinLanes][kFinCh];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  float s = 0.f, sx = 0.f;
+  if (ok) {
+    for (int b = lane; b < g.nrb; b += kFinLanes) {
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      s += psum[o];
+      sx += psumx[o];
+    }
+  }
+  r1[lane][cl] = s;
+  r2[lane][cl] = sx;
+  __syncthreads();
+  if (lane == 0 && ok) {
+    float ts = 0.f, tsx = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) { ts += r1[q][cl]; tsx += r2[q][cl]; }
+    const float rstd = a.rstd[c], mu = a.mean[c];
+    const float gm = a.gamma ? a.gamma[c] : 1.f;
+    const float dbeta = ts;
+    const float dgamma = tsx * rstd;
+    if (a.dgamma) a.dgamma[c] = dgamma;
+    if (a.dbeta) a.dbeta[c] = dbeta;
+    const float invM = 1.f / static_cast<float>(g.M);
+    const float A = gm * rstd;
+    const float B = -gm * rstd * rstd * dgamma * invM;
+    const float C0 = -A * dbeta * invM - B * mu;
+    a.coef[c] = A;
+    a.coef[g.C + c] = B;
+    a.coef[2 * g.C + c] = C0;
+  }
+}
+
+template <typename T, int MASK, bool DRES>
+__global__ void __launch_bounds__(kThreads)
+bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
+             const float* __restrict__ coef, const float* __restrict__ scale,
+             const float* __restrict__ shift, T* __restrict__ dx, T* __restrict__ dres,
+             int64_t nvec, int C) {
+  const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v0 < nvec; v0 += 2 * S) {
+    float dv[2][8], xv[2][8], yv[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t v = v0 + u * S;
+      if (v < nvec) {
+        IO8<T>::load(dy + v * 8, dv[u]);
+        IO8<T>::load(x + v * 8, xv[u]);
+        if (MASK == 2) IO8<T>::load(y + v * 8, yv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t v = v0 + u * S;
+      if (v < nvec) {
+        const int c0 = static_cast<int>((v * 8) % C);
+        float A[8], B[8], Cc[8], o[8], dz[8];
+        load8f(coef + c0, A);
+        load8f(coef + C + c0, B);
+        load8f(coef + 2 * C + c0, Cc);
+        float sc[8], sh[8];
+        if (MASK == 1) { load8f(scale + c0, sc); load8f(shift + c0, sh); }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float d = dv[u][j];
+          if (MASK == 1) d = __fmaf_rn(xv[u][j], sc[j], sh[j]) > 0.f ? d : 0.f;
+          else if (MASK == 2) d = yv[u][j] > 0.f ? d : 0.f;
+          dz[j] = d;
+          o[j] = __fmaf_rn(A[j], d, __fmaf_rn(B[j], xv[u][j], Cc[j]));
+        }
+        IO8<T>::store(dx + v * 8, o);
+        if (DRES) IO8<T>::store(dres + v * 8, dz);
+      }
+    }
+  }
+}
+
+Geom make_geom(int64_t M, int C) {
+  Geom g;
+  g.M = M;
+  g.C = C;
+  const int cg = C / 8;
+  g.tpr = cg < kThreads ? cg : kThreads;
+  g.R = kThreads / g.tpr;
+  const int cblocks = (cg + g.tpr - 1) / g.tpr;
+  const int64_t target = cblocks >= 1024 ? 1 : 1024 / cblocks;
+  const int64_t min_rows_per_thread = 32;
+  int64_t by_work = (M + g.R * min_rows_per_thread - 1) / (g.R * min_rows_per_thread);
+  int64_t nrb = target < by_work ? target : by_work;
+  if (nrb < 1) nrb = 1;
+  int64_t rpb = (M + nrb - 1) / nrb;
+  rpb = (rpb + g.R - 1) / g.R * g.R;
+  g.rpb = rpb;
+  g.nrb = static_cast<int>((M + rpb - 1) / rpb);
+  return g;
+}
+
+int apply_grid(int64_t nvec, int per_thread) {
+  int64_t blocks = (nvec + static_cast<int64_t>(kThreads) * per_thread - 1) / (static_cast<int64_t>(kThreads) * per_thread);
+  if (blocks < 1) blocks = 1;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  return static_cast<int>(blocks);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Number of fp32 workspace elements the fwd/bwd entry points need for an [M, C] activation.
+int64_t det_bn_ws_elems(int64_t M, int C) {
+  Geom g = make_geom(M, C);
+  return 2 * static_cast<int64_t>(g.nrb) * C + 3 * static_cast<int64_t>(C);
+}
+
+// dtype: 0 = fp32, 1 = bf16.  res may be null.  Outputs save_mean/save_rstd/scale/shift [C].
+int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                     const float* gamma, const float* beta, float* running_mean, float* running_var,
+                     int64_t* num_batches_tracked, float momentum, float eps, int relu,
+                     float* save_mean, float* save_rstd, float* scale, float* shift, float* ws) {
+  if (C % 8 != 0 || M <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Geom g = make_geom(M, C);
+  float* pmean = ws;
+  float* pm2 = ws + static_cast<int64_t>(g.nrb) * C;
+  dim3 grid(g.nrb, (C / 8 + g.tpr - 1) / g.tpr);
+  if (dtype == 1)
+    hipLaunchKernelGGL(bn_stats_partial<unsigned short>, grid, dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), g, pmean, pm2);
+  else
+    hipLaunchKernelGGL(bn_stats_partial<float>, grid, dim3(kThreads), 0, st, static_cast<const float*>(x), g,
+                       pmean, pm2);
+  FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+             save_mean, save_rstd, scale, shift};
+  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, pmean, pm2, g,
+                     fa);
+  int64_t* bump = num_batches_tracked;
+  const int64_t nvec = M * C / 8;
+  const int grid2 = apply_grid(nvec, 4);
+#define DET_BN_FWD(T, RL, RS)                                                                          \
+  hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                    \
+                     static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, shift, \
+                     nvec, C, bump)
+  if (dtype == 1) {
+    if (relu && res) DET_BN_FWD(unsigned short, true, true);
+    else if (relu) DET_BN_FWD(unsigned short, true, false);
+    else if (res) DET_BN_FWD(unsigned short, false, true);
+    else DET_BN_FWD(unsigned short, false, false);
+  } else {
+    if (relu && res) DET_BN_FWD(float, true, true);
+    else if (relu) DET_BN_FWD(float, true, false);
+    else if (res) DET_BN_FWD(float, false, true);
+    else DET_BN_FWD(float, false, false);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+// Inference / frozen-stats path: y = act(x*scale + shift [+ res]) with host-prepared scale/shift.
+int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                 const float* scale, const float* shift, int relu) {
+  if (C % 8 != 0 || M <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t nvec = M * C / 8;
+  const int grid2 = apply_grid(nvec, 4);
+  int64_t* bump = nullptr;
+  if (dtype == 1) {
+    if (relu && res) DET_BN_FWD(unsigned short, true, true);
+    else if (relu) DET_BN_FWD(unsigned short, true, false);
+    else if (res) DET_BN_FWD(unsigned short, false, true);
+    else DET_BN_FWD(unsigned short, false, false);
+  } else {
+    if (relu && res) DET_BN_FWD(float, true, true);
+    else if (relu) DET_BN_FWD(float, true, false);
+    else if (res) DET_BN_FWD(float, false, true);
+    else DET_BN_FWD(float, false, false);
+  }
+#undef DET_BN_FWD
+  return static_cast<int>(hipGetLastError());
+}
+
+// mask_mode: 0 none, 1 relu (mask from x), 2 relu (mask from y).  dres may be null.
+// dgamma/dbeta may be null.  ws >= det_bn_ws_elems(M, C).
+int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const void* y, int64_t M, int C,
+               int mask_mode, const float* gamma, const float* save_mean, const float* save_rstd,
+               const float* scale, const float* shift, void* dx, void* dres, float* dgamma, float* dbeta,
+               float* ws) {
+  if (C % 8 != 0 || M <= 0) return -1;
+  if (mask_mode == 2 && !y) return -2;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Geom g = make_geom(M, C);
+  float* psum = ws;
+  float* psumx = ws + static_cast<int64_t>(g.nrb) * C;
+  float* coef = psumx + static_cast<int64_t>(g.nrb) * C;
+  dim3 grid(g.nrb, (C / 8 + g.tpr - 1) / g.tpr);
+#define DET_BN_P(T, MK)                                                                                \
+  hipLaunchKernelGGL((bn_bwd_partial<T, MK>), grid, dim3(kThreads), 0, st, static_cast<const T*>(dy),   \
+                     static_cast<const T*>(x), static_cast<const T*>(y), g, save_mean, scale, shift, psum, psumx)
+  if (dtype == 1) {
+    if (mask_mode == 0) DET_BN_P(unsigned short, 0);
+    else if (mask_mode == 1) DET_BN_P(unsigned short, 1);
+    else DET_BN_P(unsigned short, 2);
+  } else {
+    if (mask_mode == 0) DET_BN_P(float, 0);
+    else if (mask_mode == 1) DET_BN_P(float, 1);
+    else DET_BN_P(float, 2);
+  }
+#undef DET_BN_P
+  BwdFin bf{gamma, save_rstd, save_mean, dgamma, dbeta, coef};
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, psum, psumx, g,
+                     bf);
+  const int64_t nvec = M * C / 8;
+  const int grid2 = apply_grid(nvec, 2);
+#define DET_BN_B(T, MK, DR)                                                                            \
+  hipLaunchKernelGGL((bn_apply_bwd<T, MK, DR>), dim3(grid2), dim3(kThreads), 0, st,                     \
+                     static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), coef,  \
+                     scale, shift, static_cast<T*>(dx), static_cast<T*>(dres), nvec, C)
+#define DET_BN_B_MASK(T, DR)                 \
+  if (mask_mode == 0) DET_BN_B(T, 0, DR);    \
+  else if (mask_mode == 1) DET_BN_B(T, 1, DR); \
+  else DET_BN_B(T, 2, DR);
+  if (dtype == 1) {
+    if (dres) { DET_BN_B_MASK(unsigned short, true) } else { DET_BN_B_MASK(unsigned short, false) }
+  } else {
+    if (dres) { DET_BN_B_MASK(float, true) } else { DET_BN_B_MASK(float, false) }
+  }
+#undef DET_BN_B_MASK
+#undef DET_BN_B
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

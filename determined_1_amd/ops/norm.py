@@ -1,0 +1,180 @@
+"""Fused training BatchNorm (+ residual add) (+ ReLU) for channels_last activations.
+
+GPU path: ``det_norm.hip`` (3 launches forward, 3 backward; see the header of that file for the
+byte accounting).  CPU path: the plain PyTorch composite ``relu(batch_norm(x) + residual)``, which
+is also the numerics reference the GPU tests compare against.
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` subclass: same parameters, buffers and
+state-dict keys (so checkpoints stay interchangeable with stock torchvision-style models), with
+``forward(x, residual=None)`` applying ``act(bn(x) + residual)`` in one fused pass.
+
+Layouts the kernels do not cover (C % 8 != 0, non-channels_last GPU tensors, fp16) take the
+composite path and are counted in ``FALLBACKS`` so a benchmark can assert it stayed native.
+"""
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from determined_1_amd.ops import _lib
+
+FALLBACKS = {"count": 0}
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _nhwc_ok(x: torch.Tensor) -> bool:
+    if x.dtype not in _DT or x.device.type != "cuda":
+        return False
+    if x.dim() == 4:
+        c = x.shape[1]
+        return c % 8 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+    if x.dim() == 2:
+        return x.shape[1] % 8 == 0 and x.is_contiguous()
+    return False
+
+
+def _rows(x: torch.Tensor) -> Tuple[int, int]:
+    c = x.shape[1]
+    return x.numel() // c, c
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def reference_bn_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu):
+    """The composite the fused kernels implement (fp32 math on CPU)."""
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum if momentum is not None else 0.0, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class _BNActTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
+        M, C = _rows(x)
+        lib = _lib.get_lib()
+        fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
+        y = torch.empty_like(x, memory_format=fmt)
+        stats = torch.empty((4, C), dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
+        if residual is not None:
+            residual = residual.to(x.dtype).contiguous(memory_format=fmt)
+        _lib.check(
+            lib.det_bn_fwd_train(
+                _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C,
+                _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
+                float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)),
+                stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                ws.data_ptr(),
+            ),
+            "bn_fwd_train",
+        )
+        mask_mode = 0 if not relu else (2 if residual is not None else 1)
+        ctx.mask_mode = mask_mode
+        ctx.has_res = residual is not None
+        ctx.fmt = fmt
+        ctx.save_for_backward(x, y if mask_mode == 2 else None, weight, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, stats = ctx.saved_tensors
+        M, C = _rows(x)
+        lib = _lib.get_lib()
+        dy = dy.to(x.dtype).contiguous(memory_format=ctx.fmt)
+        dx = torch.empty_like(x, memory_format=ctx.fmt)
+        dres = torch.empty_like(x, memory_format=ctx.fmt) if ctx.has_res and ctx.needs_input_grad[1] else None
+        dgb = None
+        if weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
+            dgb = torch.empty((2, C), dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
+        _lib.check(
+            lib.det_bn_bwd(
+                _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), _ptr(y), M, C, ctx.mask_mode,
+                _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                dx.data_ptr(), _ptr(dres),
+                None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(),
+                ws.data_ptr(),
+            ),
+            "bn_bwd",
+        )
+        if ctx.has_res and dres is None and ctx.needs_input_grad[1]:
+            raise RuntimeError("residual grad requested but not produced")
+        dw = dgb[0] if dgb is not None and ctx.needs_input_grad[2] else None
+        db = dgb[1] if dgb is not None and ctx.needs_input_grad[3] else None
+        return dx, dres, dw, db, None, None, None, None, None, None
+
+
+def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optional[torch.Tensor] = None,
+           relu: bool = True) -> torch.Tensor:
+    """``act(bn(x) + residual)`` with the module's parameters/buffers and train/eval semantics."""
+    use_batch_stats = bn.training or not bn.track_running_stats
+    rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
+    rv = bn.running_var if (bn.track_running_stats and bn.training) else None
+    res_ok = residual is None or (residual.shape == x.shape and residual.device == x.device)
+    if _nhwc_ok(x) and res_ok:
+        if use_batch_stats:
+            nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
+            return _BNActTrain.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, bn.momentum, bn.eps, relu)
+        needs_grad = torch.is_grad_enabled() and (
+            x.requires_grad or (residual is not None and residual.requires_grad)
+            or (bn.weight is not None and bn.weight.requires_grad))
+        if not needs_grad:
+            return _apply_frozen(x, bn, residual, relu)
+    if x.device.type == "cuda":
+        FALLBACKS["count"] += 1
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    momentum = bn.momentum
+    if momentum is None and bn.training and bn.track_running_stats:
+        momentum = 1.0 / float(bn.num_batches_tracked.item())
+    return reference_bn_act(x, residual, bn.weight, bn.bias,
+                            bn.running_mean if not use_batch_stats or bn.training else None,
+                            bn.running_var if not use_batch_stats or bn.training else None,
+                            use_batch_stats, momentum if momentum is not None else 0.1, bn.eps, relu)
+
+
+def _apply_frozen(x, bn, residual, relu):
+    M, C = _rows(x)
+    rstd = torch.rsqrt(bn.running_var.float() + bn.eps)
+    w = bn.weight.float() if bn.weight is not None else torch.ones_like(rstd)
+    b = bn.bias.float() if bn.bias is not None else torch.zeros_like(rstd)
+    scale = (w * rstd).contiguous()
+    shift = (b - bn.running_mean.float() * scale).contiguous()
+    fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
+    y = torch.empty_like(x, memory_format=fmt)
+    if residual is not None:
+        residual = residual.to(x.dtype).contiguous(memory_format=fmt)
+    _lib.check(
+        _lib.get_lib().det_bn_apply(_stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C,
+                                    scale.data_ptr(), shift.data_ptr(), int(bool(relu))),
+        "bn_apply",
+    )
+    return y
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` + optional residual add + optional ReLU in one fused HIP pass."""
+
+    def __init__(self, num_features: int, relu: bool = True, fused: bool = True, **kw) -> None:
+        super().__init__(num_features, **kw)
+        self.relu = relu
+        self.fused = fused  # False: stock torch/MIOpen BN + separate add/ReLU (A/B comparisons)
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:  # type: ignore[override]
+        if self.fused:
+            return bn_act(x, self, residual, self.relu)
+        y = super().forward(x)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if self.relu else y
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + f", relu={self.relu}"
