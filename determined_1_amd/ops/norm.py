@@ -20,6 +20,13 @@ import torch.nn.functional as F
 from determined_1_amd.ops import _lib
 
 FALLBACKS = {"count": 0}
+_SYNC_DEBUG = bool(__import__("os").environ.get("DET_SYNC_DEBUG"))
+
+
+def _dbg(what: str, x: torch.Tensor) -> None:
+    if _SYNC_DEBUG:
+        torch.cuda.synchronize()
+        print(f"[det_norm] {what} ok shape={tuple(x.shape)} dtype={x.dtype}", flush=True)
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
@@ -76,6 +83,7 @@ class _BNActTrain(torch.autograd.Function):
             ),
             "bn_fwd_train",
         )
+        _dbg("fwd_train", x)
         mask_mode = 0 if not relu else (2 if residual is not None else 1)
         ctx.mask_mode = mask_mode
         ctx.has_res = residual is not None
@@ -105,6 +113,7 @@ class _BNActTrain(torch.autograd.Function):
             ),
             "bn_bwd",
         )
+        _dbg("bwd", x)
         if ctx.has_res and dres is None and ctx.needs_input_grad[1]:
             raise RuntimeError("residual grad requested but not produced")
         dw = dgb[0] if dgb is not None and ctx.needs_input_grad[2] else None

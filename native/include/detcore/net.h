@@ -1,0 +1,140 @@
+// Minimal HTTP/1.1 + WebSocket (RFC 6455) server and client over POSIX sockets for the control
+// plane (master REST API, master<->harness and master<->agent WebSockets).
+// No TLS; JSON bodies.  One thread per connection: the control plane carries tens of
+// connections, not thousands.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace detcore {
+namespace net {
+
+std::string Base64Encode(const std::string& in);
+std::string Base64Decode(const std::string& in);
+std::string Sha1(const std::string& in);  // 20 raw bytes
+std::string UrlDecode(const std::string& s);
+
+struct Request {
+  std::string method;
+  std::string path;                            // without query string
+  std::map<std::string, std::string> query;    // decoded
+  std::map<std::string, std::string> headers;  // lower-case keys
+  std::map<std::string, std::string> params;   // route ":name" captures
+  std::string body;
+  std::string remote_addr;
+  std::string Query(const std::string& k, const std::string& dflt = "") const {
+    auto it = query.find(k);
+    return it == query.end() ? dflt : it->second;
+  }
+  std::string Param(const std::string& k) const {
+    auto it = params.find(k);
+    return it == params.end() ? "" : it->second;
+  }
+};
+
+struct Response {
+  int status = 200;
+  std::string content_type = "application/json";
+  std::map<std::string, std::string> headers;
+  std::string body;
+  static Response Json(int status, const std::string& body) {
+    Response r;
+    r.status = status;
+    r.body = body;
+    return r;
+  }
+  static Response Text(int status, const std::string& body) {
+    Response r;
+    r.status = status;
+    r.content_type = "text/plain";
+    r.body = body;
+    return r;
+  }
+};
+
+// A WebSocket connection (either side).  Send is thread-safe.
+class WsConn : public std::enable_shared_from_this<WsConn> {
+ public:
+  WsConn(int fd, bool client_side, std::string peer, std::string initial = "");
+  ~WsConn();
+  bool Send(const std::string& text);
+  void Close();
+  bool closed() const { return closed_.load(); }
+  const std::string& peer() const { return peer_; }
+  // Blocking read loop: calls on_message for each text/binary message; returns on close/error.
+  void ReadLoop(const std::function<void(const std::string&)>& on_message);
+  // Blocking read of one message; false on close.
+  bool Recv(std::string* out);
+
+ private:
+  bool SendFrame(int opcode, const std::string& payload);
+  int fd_;
+  bool client_;
+  std::string peer_;
+  std::mutex send_mu_;
+  std::atomic<bool> closed_{false};
+  std::string rbuf_;
+};
+using WsPtr = std::shared_ptr<WsConn>;
+
+using Handler = std::function<Response(const Request&)>;
+// Called on the connection's thread after the upgrade; should run ws->ReadLoop(...).
+using WsHandler = std::function<void(const Request&, WsPtr ws)>;
+
+class HttpServer {
+ public:
+  HttpServer() = default;
+  ~HttpServer();
+  // Pattern segments starting with ':' capture; a trailing "*" matches the rest.
+  void Route(const std::string& method, const std::string& pattern, Handler h);
+  void RouteWs(const std::string& pattern, WsHandler h);
+  // Binds host:port (port 0 = ephemeral); returns the bound port.
+  int Listen(const std::string& host, int port);
+  void Start();  // accept loop on a background thread
+  void Stop();
+  int port() const { return port_; }
+
+ private:
+  struct RouteEntry {
+    std::string method;
+    std::vector<std::string> segs;
+    Handler h;
+    WsHandler ws;
+  };
+  bool Match(const RouteEntry& r, const std::vector<std::string>& segs, std::map<std::string, std::string>* params) const;
+  void Serve(int fd, std::string peer);
+  std::vector<RouteEntry> routes_;
+  int listen_fd_ = -1;
+  int port_ = 0;
+  std::atomic<bool> running_{false};
+  std::thread accept_thread_;
+  std::mutex conns_mu_;
+  std::condition_variable conns_cv_;
+  std::vector<int> conn_fds_;
+  int active_conns_ = 0;
+};
+
+// Client helpers.
+struct ClientResponse {
+  int status = 0;
+  std::string body;
+  std::string error;  // non-empty on transport failure
+};
+ClientResponse HttpCall(const std::string& host, int port, const std::string& method, const std::string& path,
+                        const std::string& body = "", int timeout_ms = 30000);
+WsPtr WsConnect(const std::string& host, int port, const std::string& path, std::string* error = nullptr);
+
+int ConnectTcp(const std::string& host, int port, int timeout_ms, std::string* error);
+std::string LocalIPForPeer(const std::string& host, int port);
+
+}  // namespace net
+}  // namespace detcore

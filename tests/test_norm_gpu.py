@@ -39,6 +39,7 @@ def test_bn_act_train_matches_reference(gpu, case):
         ref.bias.uniform_(-0.5, 0.5)
         ref.running_mean.uniform_(-0.1, 0.1)
     dut = copy.deepcopy(ref).to(gpu)
+    dut.fused = True
     x = (torch.randn(n, c, h, w) * 2 + 0.7).to(memory_format=torch.channels_last)
     res = torch.randn(n, c, h, w).to(memory_format=torch.channels_last) if use_res else None
     dy = torch.randn(n, c, h, w).to(memory_format=torch.channels_last)
@@ -69,6 +70,7 @@ def test_bn_act_eval_and_momentum_none(gpu):
     torch.manual_seed(1)
     ref = norm.BatchNormAct2d(64, relu=True, fused=False, momentum=None)
     dut = copy.deepcopy(ref).to(gpu)
+    dut.fused = True
     for _ in range(3):
         x = torch.randn(4, 64, 6, 6).to(memory_format=torch.channels_last)
         ref(x)
