@@ -195,49 +195,62 @@ struct FinArgs {
 };
 
 // One block = 64 channels x 16 row-lanes (one wave per row-lane: 256 B coalesced partial rows).
+// Single pass in fp64: S1 = sum n_b*mean_b, S2 = sum(M2_b + n_b*mean_b^2); var = S2/M - mean^2.
+// fp64 keeps the cancellation harmless, and the 4-way unroll keeps 4 independent partial loads
+// in flight per lane (the loop is L2-latency bound, not bandwidth bound).
 __global__ void __launch_bounds__(kFinThreads)
 bn_stats_finalize(const float* __restrict__ pmean, const float* __restrict__ pm2, Geom g, FinArgs a) {
-  __shared__ float red[kFinLanes][kFinCh];
-  __shared__ float gmean[kFinCh];
+  __shared__ double red1[kFinLanes][kFinCh];
+  __shared__ double red2[kFinLanes][kFinCh];
   const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
   const int c = blockIdx.x * kFinCh + cl;
   const bool ok = c < g.C;
-  // pass 1: global mean = sum(n_b * mean_b) / M
-  float acc = 0.f;
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
   if (ok) {
-    for (int b = lane; b < g.nrb; b += kFinLanes) {
-      const int64_t nb = min(g.rpb, g.M - static_cast<int64_t>(b) * g.rpb);
-      acc += static_cast<float>(nb) * pmean[static_cast<int64_t>(b) * g.C + c];
-    }
-  }
-  red[lane][cl] = acc;
-  __syncthreads();
-  if (lane == 0) {
-    float t = 0.f;
+    const int last = g.nrb - 1;
+    const double n_full = static_cast<double>(g.rpb);
+    const double n_last = static_cast<double>(g.M - static_cast<int64_t>(last) * g.rpb);
+    int b = lane;
+    for (; b + 3 * kFinLanes < g.nrb; b += 4 * kFinLanes) {
+      float mv[4], qv[4];
 #pragma unroll
-    for (int q = 0; q < kFinLanes; ++q) t += red[q][cl];
-    gmean[cl] = t / static_cast<float>(g.M);
-  }
-  __syncthreads();
-  const float mean = gmean[cl];
-  // pass 2: M2 = sum(M2_b + n_b * (mean_b - mean)^2)
-  acc = 0.f;
-  if (ok) {
-    for (int b = lane; b < g.nrb; b += kFinLanes) {
-      const int64_t nb = min(g.rpb, g.M - static_cast<int64_t>(b) * g.rpb);
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = static_cast<int64_t>(b + u * kFinLanes) * g.C + c;
+        mv[u] = pmean[o];
+        qv[u] = pm2[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double nb = (b + u * kFinLanes) == last ? n_last : n_full;
+        const double m = mv[u];
+        s1[u] += nb * m;
+        s2[u] += static_cast<double>(qv[u]) + nb * m * m;
+      }
+    }
+    for (; b < g.nrb; b += kFinLanes) {
       const int64_t o = static_cast<int64_t>(b) * g.C + c;
-      const float d = pmean[o] - mean;
-      acc += pm2[o] + static_cast<float>(nb) * d * d;
+      const double nb = b == last ? n_last : n_full;
+      const double m = pmean[o];
+      s1[0] += nb * m;
+      s2[0] += static_cast<double>(pm2[o]) + nb * m * m;
     }
   }
-  __syncthreads();
-  red[lane][cl] = acc;
+  red1[lane][cl] = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+  red2[lane][cl] = (s2[0] + s2[1]) + (s2[2] + s2[3]);
   __syncthreads();
   if (lane == 0 && ok) {
-    float m2 = 0.f;
+    double t1 = 0, t2 = 0;
 #pragma unroll
-    for (int q = 0; q < kFinLanes; ++q) m2 += red[q][cl];
-    const float var = m2 / static_cast<float>(g.M);
+    for (int q = 0; q < kFinLanes; ++q) {
+      t1 += red1[q][cl];
+      t2 += red2[q][cl];
+    }
+    const double M = static_cast<double>(g.M);
+    const double meand = t1 / M;
+    double m2 = t2 - M * meand * meand;
+    if (m2 < 0) m2 = 0;
+    const float mean = static_cast<float>(meand);
+    const float var = static_cast<float>(m2 / M);
     const float rstd = rsqrtf(var + a.eps);
     const float gm = a.gamma ? a.gamma[c] : 1.f;
     const float bt = a.beta ? a.beta[c] : 0.f;
@@ -249,7 +262,7 @@ bn_stats_finalize(const float* __restrict__ pmean, const float* __restrict__ pm2
     if (a.running_mean) {
       float f = a.momentum;
       if (f < 0.f) f = a.num_batches_tracked ? 1.f / static_cast<float>(*a.num_batches_tracked + 1) : 0.f;
-      const float unbiased = g.M > 1 ? m2 / static_cast<float>(g.M - 1) : var;
+      const float unbiased = g.M > 1 ? static_cast<float>(m2 / (M - 1.0)) : var;
       a.running_mean[c] = (1.f - f) * a.running_mean[c] + f * mean;
       a.running_var[c] = (1.f - f) * a.running_var[c] + f * unbiased;
     }
@@ -399,11 +412,23 @@ bn_bwd_finalize(const float* __restrict__ psum, const float* __restrict__ psumx,
   const bool ok = c < g.C;
   float s = 0.f, sx = 0.f;
   if (ok) {
-    for (int b = lane; b < g.nrb; b += kFinLanes) {
-      const int64_t o = static_cast<int64_t>(b) * g.C + c;
-      s += psum[o];
-      sx += psumx[o];
+    float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = lane;
+    for (; b + 3 * kFinLanes < g.nrb; b += 4 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = static_cast<int64_t>(b + u * kFinLanes) * g.C + c;
+        sa[u] += psum[o];
+        sb[u] += psumx[o];
+      }
     }
+    for (; b < g.nrb; b += kFinLanes) {
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      sa[0] += psum[o];
+      sb[0] += psumx[o];
+    }
+    s = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+    sx = (sb[0] + sb[1]) + (sb[2] + sb[3]);
   }
   r1[lane][cl] = s;
   r2[lane][cl] = sx;
@@ -481,7 +506,7 @@ Geom make_geom(int64_t M, int C) {
   g.R = kThreads / g.tpr;
   const int cblocks = (cg + g.tpr - 1) / g.tpr;
   const int64_t target = cblocks >= 1024 ? 1 : 1024 / cblocks;
-  const int64_t min_rows_per_thread = 32;
+  const int64_t min_rows_per_thread = 48;
   int64_t by_work = (M + g.R * min_rows_per_thread - 1) / (g.R * min_rows_per_thread);
   int64_t nrb = target < by_work ? target : by_work;
   if (nrb < 1) nrb = 1;

@@ -1,0 +1,43 @@
+// Experiment-config defaults / merge / validation on the master side (SURVEY M26, C-config;
+// reference master/pkg/model/{defaults,experiment_config,searcher_config,
+// hyperparameters_config}.go) and the master's own config.
+//
+// Merge order: defaults -> master checkpoint_storage -> template -> user config
+// (core_experiment.go:355-416).  Tagged unions (searcher.name, checkpoint_storage.type) replace
+// the selected arm wholesale when the tag changes.  The Python side
+// (determined_1_amd/config/experiment_config.py) implements the same schema for the CLI and local
+// mode; tests pin the two to the same defaults.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "detcore/json.h"
+
+namespace detcore {
+
+Json DefaultExperimentConfig(uint32_t experiment_seed);
+Json DeepMerge(const Json& base, const Json& over);
+Json MergeExperimentConfig(const Json& user, const Json& master_checkpoint_storage, const Json& tmpl,
+                           uint32_t default_seed);
+std::vector<std::string> ValidateExperimentConfig(const Json& cfg);
+
+// Master config (reference master/internal/config.go:24-86): port, store dir, scheduler,
+// fitting policy, resource pools, checkpoint storage, task defaults.
+struct MasterConfig {
+  std::string listen_host = "0.0.0.0";
+  int port = 8080;
+  std::string store_dir;  // empty: in-memory
+  std::string scheduler = "fair_share";
+  std::string fitting_policy = "best";
+  bool priority_preemption = true;
+  std::vector<std::string> resource_pools{"default"};
+  Json checkpoint_storage;  // default for experiments that do not set one
+  std::string cluster_name = "determined-mi355x";
+  double scheduler_tick_ms = 500;
+  std::string python = "python3";
+  static MasterConfig FromJson(const Json& j);
+  Json ToJson() const;
+};
+
+}  // namespace detcore

@@ -1,0 +1,98 @@
+// det-master: the control plane (reference master/internal/*.go).
+//
+//   REST + WebSocket API (HttpServer)
+//     └─ actor system
+//          ├─ /pools/<name>            resource pool: agents, gang scheduling tick (fair_share /
+//          │                           priority / round_robin + fitting), preemption requests
+//          └─ /experiments/<id>        experiment: Searcher, checkpoint policy, state machine
+//                └─ /<request-id>      trial: sequencer, allocation, containers, rendezvous,
+//                                      workload relay, restarts / rollback, preemption
+//   Agents connect over /agents (WebSocket) and run trial processes; trial processes connect
+//   over /ws/trial/<e>/<t>/<c>.  All durable state lives in the embedded Store (WAL+snapshot),
+//   including the experiment event log replayed on master restart.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "detcore/actor.h"
+#include "detcore/config.h"
+#include "detcore/json.h"
+#include "detcore/net.h"
+#include "detcore/store.h"
+
+namespace detcore {
+namespace master {
+
+class Master;
+
+struct AgentConn {
+  std::string id;
+  std::string pool;
+  std::string label;
+  std::string host;  // address the agent connected from (trial processes run there)
+  net::WsPtr ws;
+  Json devices;
+  std::set<std::string> containers;
+};
+
+class Master {
+ public:
+  explicit Master(MasterConfig cfg);
+  ~Master();
+  int Start();  // bind + serve; returns the port
+  void Stop();
+  void Wait();  // until Stop() (signal handler)
+
+  // ---- used by actors / handlers
+  Store& store() { return *store_; }
+  actor::System& system() { return *sys_; }
+  const MasterConfig& config() const { return cfg_; }
+  actor::Ref Pool(const std::string& name);
+  bool SendToAgent(const std::string& agent_id, const Json& msg);
+  std::string AgentHost(const std::string& agent_id);
+  void BindContainer(const std::string& cid, const std::string& agent_id, actor::Ref trial);
+  void UnbindContainer(const std::string& cid);
+  actor::Ref TrialForContainer(const std::string& cid);
+  actor::Ref ExperimentRef(int64_t id);
+  std::string master_host() const { return advertised_host_; }
+  int port() const { return port_; }
+  void AppendTrialLog(int64_t trial_id, const std::string& line, const std::string& stdtype,
+                      const std::string& container_id, int rank);
+  void RunCheckpointGC(int64_t experiment_id, const Json& exp_config, const Json& to_delete);
+  std::string cluster_id() const { return cluster_id_; }
+
+ private:
+  void InstallRoutes();
+  void HandleAgentSocket(const net::Request& req, net::WsPtr ws);
+  void HandleTrialSocket(const net::Request& req, net::WsPtr ws);
+  void RestoreExperiments();
+  int64_t CreateExperiment(const Json& body, bool* activate);
+
+  MasterConfig cfg_;
+  std::unique_ptr<Store> store_;
+  std::unique_ptr<actor::System> sys_;
+  net::HttpServer http_;
+  std::map<std::string, actor::Ref> pools_;
+  std::mutex mu_;
+  std::map<std::string, std::shared_ptr<AgentConn>> agents_;
+  std::map<std::string, std::pair<std::string, actor::Ref>> containers_;  // cid -> (agent, trial)
+  std::string advertised_host_ = "127.0.0.1";
+  std::string cluster_id_;
+  int port_ = 0;
+  std::mutex stop_mu_;
+  std::condition_variable stop_cv_;
+  bool stopped_ = false;
+};
+
+// Helpers shared by the master translation units.
+std::string NowRFC3339();
+std::string NewUUID();
+Json CheckpointsToGC(Store& store, int64_t experiment_id, const Json& exp_config);
+
+}  // namespace master
+}  // namespace detcore

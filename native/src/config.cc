@@ -1,0 +1,234 @@
+// Experiment/master config (see include/detcore/config.h).
+#include "detcore/config.h"
+
+#include <set>
+
+#include "detcore/searcher.h"
+
+namespace detcore {
+
+Json DefaultExperimentConfig(uint32_t seed) {
+  Json c = Json::parse(R"({
+    "description": "Experiment",
+    "checkpoint_storage": {"type": "shared_fs", "host_path": "/tmp", "save_experiment_best": 0,
+                           "save_trial_best": 1, "save_trial_latest": 1},
+    "checkpoint_policy": "best",
+    "data_layer": {"type": "shared_fs"},
+    "hyperparameters": {},
+    "searcher": {"smaller_is_better": true},
+    "resources": {"slots_per_trial": 1, "weight": 1, "native_parallel": false, "agent_label": "",
+                  "resource_pool": ""},
+    "optimizations": {"aggregation_frequency": 1, "average_aggregated_gradients": true,
+                      "average_training_metrics": false, "gradient_compression": false,
+                      "mixed_precision": "O0", "tensor_fusion_threshold": 64,
+                      "tensor_fusion_cycle_time": 5, "auto_tune_tensor_fusion": false},
+    "perform_initial_validation": false,
+    "min_checkpoint_period": {"batches": 0},
+    "min_validation_period": {"batches": 0},
+    "records_per_epoch": 0,
+    "scheduling_unit": 100,
+    "environment": {"image": {"cpu": "determined-mi355x:cpu", "gpu": "determined-mi355x:rocm"}},
+    "reproducibility": {},
+    "max_restarts": 5,
+    "debug": false,
+    "internal": null,
+    "entrypoint": ""
+  })");
+  c["reproducibility"]["experiment_seed"] = static_cast<int64_t>(seed);
+  return c;
+}
+
+static Json SearcherArmDefaults(const std::string& name) {
+  if (name == "sync_halving") return Json::parse(R"({"divisor": 4, "train_stragglers": true})");
+  if (name == "adaptive") return Json::parse(R"({"divisor": 4, "train_stragglers": true, "mode": "standard", "max_rungs": 5})");
+  if (name == "adaptive_simple") return Json::parse(R"({"divisor": 4, "mode": "standard", "max_rungs": 5})");
+  if (name == "async_halving") return Json::parse(R"({"divisor": 4, "max_concurrent_trials": 0})");
+  if (name == "adaptive_asha")
+    return Json::parse(R"({"divisor": 4, "mode": "standard", "max_rungs": 5, "max_concurrent_trials": 0})");
+  return Json::object();
+}
+
+Json DeepMerge(const Json& base, const Json& over) {
+  if (!base.is_object() || !over.is_object()) return over.clone();
+  Json out = base.clone();
+  for (auto& kv : over.as_object()) {
+    const std::string& k = kv.first;
+    const Json& v = kv.second;
+    if (v.is_object() && out[k].is_object() && k != "hyperparameters" && k != "data") {
+      const char* tag = nullptr;
+      if (v.has("type") || out[k].has("type")) tag = "type";
+      else if (v.has("name")) tag = "name";
+      if (tag && v.has(tag) && out[k].has(tag) && !out[k][tag].is_null() && out[k][tag] != v[tag]) {
+        Json arm = Json::object();
+        for (auto& bk : out[k].as_object())
+          if (bk.first.rfind("save_", 0) == 0 || bk.first == "smaller_is_better") arm[bk.first] = bk.second;
+        for (auto& ok : v.as_object()) arm[ok.first] = ok.second.clone();
+        out[k] = arm;
+      } else {
+        out[k] = DeepMerge(out[k], v);
+      }
+    } else {
+      out[k] = v.clone();
+    }
+  }
+  return out;
+}
+
+Json MergeExperimentConfig(const Json& user, const Json& master_ckpt, const Json& tmpl, uint32_t seed) {
+  Json cfg = DefaultExperimentConfig(seed);
+  if (master_ckpt.is_object() && !master_ckpt.as_object().empty()) {
+    Json o = Json::object();
+    o["checkpoint_storage"] = master_ckpt;
+    cfg = DeepMerge(cfg, o);
+  }
+  if (tmpl.is_object()) cfg = DeepMerge(cfg, tmpl);
+  cfg = DeepMerge(cfg, user);
+  Json& s = cfg["searcher"];
+  if (s.has("name")) {
+    Json arm = SearcherArmDefaults(s["name"].as_string());
+    for (auto& kv : arm.as_object())
+      if (!s.has(kv.first)) s[kv.first] = kv.second;
+  }
+  if (!s.has("smaller_is_better")) s["smaller_is_better"] = true;
+  return cfg;
+}
+
+static bool ParseLen(const Json& v, Length* out) {
+  try {
+    *out = Length::FromJson(v);
+    return true;
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+std::vector<std::string> ValidateExperimentConfig(const Json& cfg) {
+  static const std::set<std::string> kTop = {
+      "description", "labels", "data", "checkpoint_storage", "tensorboard_storage", "perform_initial_validation",
+      "min_checkpoint_period", "min_validation_period", "checkpoint_policy", "hyperparameters", "searcher",
+      "resources", "optimizations", "records_per_epoch", "scheduling_unit", "bind_mounts", "environment",
+      "reproducibility", "max_restarts", "security", "debug", "internal", "entrypoint", "data_layer",
+      "batches_per_step"};
+  static const std::set<std::string> kSearchers = {"single", "random", "grid", "sync_halving", "adaptive",
+                                                   "adaptive_simple", "async_halving", "adaptive_asha", "pbt"};
+  std::vector<std::string> errs;
+  for (auto& kv : cfg.as_object())
+    if (!kTop.count(kv.first)) errs.push_back("unknown config key: " + kv.first);
+  bool native = cfg["internal"].is_object() && !cfg["internal"]["native"].is_null();
+  if (!native && cfg.get_string("entrypoint", "").empty())
+    errs.push_back("Must specify an entrypoint that references the trial class.");
+  const Json& s = cfg["searcher"];
+  std::string name = s.get_string("name", "");
+  if (!kSearchers.count(name)) errs.push_back("searcher.name: unknown searcher '" + name + "'");
+  if (s.get_string("metric", "").empty()) errs.push_back("searcher.metric must be set");
+  bool epochs = false;
+  for (const char* f : {"max_length", "budget", "length_per_round"}) {
+    if (!s.has(f)) continue;
+    Length l;
+    if (!ParseLen(s[f], &l)) errs.push_back(std::string("searcher.") + f + ": invalid length");
+    else {
+      if (l.units <= 0) errs.push_back(std::string(f) + " must be > 0");
+      epochs |= l.unit == Unit::Epochs;
+    }
+  }
+  if ((name == "random" || name == "async_halving" || name == "adaptive_simple" || name == "adaptive_asha") &&
+      s.get_int("max_trials", 0) <= 0)
+    errs.push_back("max_trials must be > 0");
+  if ((name == "sync_halving" || name == "async_halving" || name == "adaptive" || name == "adaptive_simple" ||
+       name == "adaptive_asha") &&
+      !(s.get_double("divisor", 0) > 1.0))
+    errs.push_back("divisor must be > 1.0");
+  if ((name == "sync_halving" || name == "async_halving") && s.get_int("num_rungs", 0) <= 0)
+    errs.push_back("num_rungs must be > 0");
+  if (name == "adaptive" || name == "adaptive_simple" || name == "adaptive_asha") {
+    std::string mode = s.get_string("mode", "");
+    if (mode != "aggressive" && mode != "standard" && mode != "conservative")
+      errs.push_back("mode must be one of aggressive, standard, conservative");
+    if (s.get_int("max_rungs", 0) <= 0) errs.push_back("max_rungs must be > 0");
+  }
+  if (name == "pbt") {
+    if (s.get_int("population_size", 0) <= 0) errs.push_back("population_size must be > 0");
+    if (s.get_int("num_rounds", 0) <= 0) errs.push_back("num_rounds must be > 0");
+  }
+  for (const char* f : {"min_validation_period", "min_checkpoint_period"}) {
+    if (!cfg.has(f)) continue;
+    Length l;
+    if (!ParseLen(cfg[f], &l)) errs.push_back(std::string(f) + ": invalid length");
+    else epochs |= l.unit == Unit::Epochs && l.units > 0;
+  }
+  if (epochs && cfg.get_int("records_per_epoch", 0) <= 0)
+    errs.push_back("Must specify records_per_epoch when any configuration is in terms of epochs");
+  if (cfg["hyperparameters"].is_object()) {
+    for (auto& kv : cfg["hyperparameters"].as_object()) {
+      const Json& hp = kv.second;
+      if (!hp.is_object() || !hp.has("type")) continue;
+      std::string t = hp["type"].as_string();
+      if (t == "const") {
+        if (!hp.has("val")) errs.push_back("hyperparameters." + kv.first + ": const needs val");
+      } else if (t == "int" || t == "double" || t == "log") {
+        if (!(hp.get_double("maxval", 0) > hp.get_double("minval", 0)))
+          errs.push_back("hyperparameters." + kv.first + ": minval is greater than maxval");
+        if (name == "grid" && !hp.has("count"))
+          errs.push_back("hyperparameters." + kv.first + ": grid search needs a count");
+      } else if (t == "categorical") {
+        if (!hp["vals"].is_array() || hp["vals"].size() == 0)
+          errs.push_back("hyperparameters." + kv.first + ": must have at least one category");
+      } else {
+        errs.push_back("hyperparameters." + kv.first + ": unknown type '" + t + "'");
+      }
+    }
+  }
+  if (cfg.get_int("max_restarts", 0) < 0) errs.push_back("max_restarts must be >= 0");
+  std::string ct = cfg["checkpoint_storage"].get_string("type", "shared_fs");
+  if (ct != "shared_fs" && ct != "s3" && ct != "gcs" && ct != "hdfs")
+    errs.push_back("checkpoint_storage.type: unknown '" + ct + "'");
+  std::string cp = cfg.get_string("checkpoint_policy", "best");
+  if (cp != "best" && cp != "all" && cp != "none") errs.push_back("checkpoint_policy must be one of best, all, none");
+  if (cfg["resources"].get_int("slots_per_trial", 1) < 0) errs.push_back("slots_per_trial must be >= 0");
+  if (cfg["optimizations"].get_int("aggregation_frequency", 1) < 1) errs.push_back("aggregation_frequency must be >= 1");
+  if (cfg.get_int("scheduling_unit", 100) <= 0) errs.push_back("scheduling_unit must be > 0");
+  return errs;
+}
+
+MasterConfig MasterConfig::FromJson(const Json& j) {
+  MasterConfig c;
+  c.listen_host = j.get_string("listen_host", c.listen_host);
+  c.port = static_cast<int>(j.get_int("port", c.port));
+  c.store_dir = j.get_string("store_dir", c.store_dir);
+  if (j["scheduler"].is_object()) {
+    c.scheduler = j["scheduler"].get_string("type", c.scheduler);
+    c.fitting_policy = j["scheduler"].get_string("fitting_policy", c.fitting_policy);
+    c.priority_preemption = j["scheduler"].get_bool("preemption", c.priority_preemption);
+  }
+  if (j["resource_pools"].is_array()) {
+    c.resource_pools.clear();
+    for (auto& p : j["resource_pools"].as_array()) c.resource_pools.push_back(p.is_string() ? p.as_string() : p.get_string("pool_name", "default"));
+  }
+  c.checkpoint_storage = j["checkpoint_storage"];
+  c.cluster_name = j.get_string("cluster_name", c.cluster_name);
+  c.scheduler_tick_ms = j.get_double("scheduler_tick_ms", c.scheduler_tick_ms);
+  c.python = j.get_string("python", c.python);
+  return c;
+}
+
+Json MasterConfig::ToJson() const {
+  Json j = Json::object();
+  j["listen_host"] = listen_host;
+  j["port"] = port;
+  j["store_dir"] = store_dir;
+  Json s = Json::object();
+  s["type"] = scheduler;
+  s["fitting_policy"] = fitting_policy;
+  s["preemption"] = priority_preemption;
+  j["scheduler"] = s;
+  Json pools = Json::array();
+  for (auto& p : resource_pools) pools.push_back(p);
+  j["resource_pools"] = pools;
+  j["checkpoint_storage"] = checkpoint_storage;
+  j["cluster_name"] = cluster_name;
+  j["scheduler_tick_ms"] = scheduler_tick_ms;
+  j["python"] = python;
+  return j;
+}
+
+}  // namespace detcore
