@@ -1,0 +1,6 @@
+"""REST client for det-master (reference ``common/determined_common/api/``) and model-definition
+packaging (``common/determined_common/context.py``)."""
+from determined_1_amd.api.context import read_context, read_detignore
+from determined_1_amd.api.request import MasterClient, make_url, parse_master_address
+
+__all__ = ["MasterClient", "make_url", "parse_master_address", "read_context", "read_detignore"]

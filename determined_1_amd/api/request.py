@@ -1,0 +1,103 @@
+"""Thin HTTP client for the det-master REST API (reference ``api/request.py:93``,
+``api/experiment.py:196-325``)."""
+import json
+import os
+import time
+from typing import Any, Dict, Iterator, List, Optional, Tuple
+
+import requests
+
+
+def parse_master_address(addr: Optional[str]) -> Tuple[str, int]:
+    addr = addr or os.environ.get("DET_MASTER", "127.0.0.1:8080")
+    addr = addr.replace("http://", "").rstrip("/")
+    if ":" in addr:
+        h, p = addr.rsplit(":", 1)
+        return h, int(p)
+    return addr, 8080
+
+
+def make_url(master: str, path: str) -> str:
+    h, p = parse_master_address(master)
+    return f"http://{h}:{p}{path}"
+
+
+class APIError(RuntimeError):
+    def __init__(self, status: int, msg: str) -> None:
+        super().__init__(f"master returned {status}: {msg}")
+        self.status = status
+
+
+class MasterClient:
+    def __init__(self, master: Optional[str] = None, timeout: float = 60.0) -> None:
+        self.master = master or os.environ.get("DET_MASTER", "127.0.0.1:8080")
+        self.timeout = timeout
+        self.session = requests.Session()
+
+    def _call(self, method: str, path: str, body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+        r = self.session.request(method, make_url(self.master, path), params=params,
+                                 data=None if body is None else json.dumps(body), timeout=self.timeout,
+                                 headers={"Content-Type": "application/json"})
+        if r.status_code >= 300:
+            try:
+                msg = r.json().get("error", r.text)
+            except ValueError:
+                msg = r.text
+            raise APIError(r.status_code, msg)
+        return r.json() if r.text else None
+
+    def get(self, path: str, **params: Any) -> Any:
+        return self._call("GET", path, params=params or None)
+
+    def post(self, path: str, body: Any = None) -> Any:
+        return self._call("POST", path, body)
+
+    def patch(self, path: str, body: Any) -> Any:
+        return self._call("PATCH", path, body)
+
+    def put(self, path: str, body: Any) -> Any:
+        return self._call("PUT", path, body)
+
+    def delete(self, path: str) -> Any:
+        return self._call("DELETE", path)
+
+    # ------------------------------------------------------------------------ experiments
+    def create_experiment(self, config: Dict[str, Any], model_definition: List[Dict[str, Any]],
+                          activate: bool = True, template: Optional[str] = None,
+                          validate_only: bool = False, parent_id: Optional[int] = None) -> Dict[str, Any]:
+        body = {"config": config, "model_definition": model_definition, "activate": activate,
+                "validate_only": validate_only}
+        if template:
+            body["template"] = template
+        if parent_id is not None:
+            body["parent_id"] = parent_id
+        return self.post("/experiments", body)
+
+    def experiment(self, exp_id: int) -> Dict[str, Any]:
+        return self.get(f"/experiments/{exp_id}")
+
+    def set_state(self, exp_id: int, state: str) -> Dict[str, Any]:
+        return self.patch(f"/experiments/{exp_id}", {"state": state})
+
+    def wait_for_experiment(self, exp_id: int, timeout: float = 3600.0, poll: float = 0.5) -> str:
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            st = self.experiment(exp_id)["state"]
+            if st in ("COMPLETED", "CANCELED", "ERROR"):
+                return st
+            time.sleep(poll)
+        raise TimeoutError(f"experiment {exp_id} did not finish in {timeout}s")
+
+    def trial_logs(self, trial_id: int, follow: bool = False, poll: float = 0.5) -> Iterator[Dict[str, Any]]:
+        offset = 0
+        while True:
+            logs = self.get(f"/trials/{trial_id}/logs", offset=offset)
+            for l in logs:
+                offset = max(offset, l["id"])
+                yield l
+            if not follow:
+                return
+            t = self.get(f"/trials/{trial_id}")
+            if t["state"] != "ACTIVE" and not logs:
+                return
+            time.sleep(poll)

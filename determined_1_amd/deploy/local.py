@@ -1,0 +1,135 @@
+"""``det deploy local``: run det-master and N det-agents as local processes (the reference's
+``det-deploy local cluster-up --agents N`` runs them as containers; ``--artificial-slots`` fakes
+devices so multi-agent gang scheduling can be exercised on a CPU-only machine)."""
+import os
+import pathlib
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+from typing import List, Optional
+
+import requests
+
+NATIVE_DIR = pathlib.Path(__file__).resolve().parent.parent / "_native"
+
+
+def native_binary(name: str) -> str:
+    p = NATIVE_DIR / name
+    if not p.exists():
+        from determined_1_amd.native_build import build_native
+
+        build_native()
+    if not p.exists():
+        raise FileNotFoundError(f"{p} missing: run `make -C native`")
+    return str(p)
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class LocalCluster:
+    def __init__(self, agents: int = 1, slots_per_agent: int = 0, port: Optional[int] = None,
+                 store_dir: Optional[str] = None, checkpoint_dir: Optional[str] = None,
+                 scheduler: str = "fair_share", work_dir: Optional[str] = None, gpu: bool = False,
+                 log_dir: Optional[str] = None, tick_ms: int = 100) -> None:
+        self.port = port or free_port()
+        self.tmp = tempfile.mkdtemp(prefix="det-local-")
+        self.store_dir = store_dir or os.path.join(self.tmp, "store")
+        self.checkpoint_dir = checkpoint_dir or os.path.join(self.tmp, "checkpoints")
+        self.work_dir = work_dir or os.path.join(self.tmp, "agents")
+        self.log_dir = log_dir or self.tmp
+        self.agents = agents
+        self.slots_per_agent = slots_per_agent
+        self.scheduler = scheduler
+        self.gpu = gpu
+        self.tick_ms = tick_ms
+        self.master_proc = None  # type: Optional[subprocess.Popen]
+        self.agent_procs = []  # type: List[subprocess.Popen]
+
+    @property
+    def address(self) -> str:
+        return f"127.0.0.1:{self.port}"
+
+    def start_master(self) -> None:
+        os.makedirs(self.checkpoint_dir, exist_ok=True)
+        log = open(os.path.join(self.log_dir, "master.log"), "ab")
+        self.master_proc = subprocess.Popen(
+            [native_binary("det-master"), "--host", "127.0.0.1", "--port", str(self.port), "--store-dir",
+             self.store_dir, "--scheduler", self.scheduler, "--checkpoint-host-path", self.checkpoint_dir,
+             "--python", sys.executable, "--scheduler-tick-ms", str(self.tick_ms)],
+            stdout=log, stderr=subprocess.STDOUT)
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            try:
+                requests.get(f"http://{self.address}/info", timeout=1)
+                return
+            except requests.RequestException:
+                if self.master_proc.poll() is not None:
+                    raise RuntimeError(f"det-master exited with {self.master_proc.returncode}; see {log.name}")
+                time.sleep(0.1)
+        raise RuntimeError("det-master did not come up")
+
+    def start_agent(self, i: int) -> subprocess.Popen:
+        log = open(os.path.join(self.log_dir, f"agent-{i}.log"), "ab")
+        args = [native_binary("det-agent"), "--master-host", "127.0.0.1", "--master-port", str(self.port),
+                "--agent-id", f"agent-{i}", "--work-dir", os.path.join(self.work_dir, f"agent-{i}"),
+                "--python", sys.executable]
+        if self.slots_per_agent > 0 and not self.gpu:
+            args += ["--artificial-slots", str(self.slots_per_agent)]
+        elif self.gpu:
+            args += ["--slot-type", "gpu"]
+        p = subprocess.Popen(args, stdout=log, stderr=subprocess.STDOUT)
+        self.agent_procs.append(p)
+        return p
+
+    def wait_for_slots(self, n: int, timeout: float = 30.0) -> None:
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            agents = requests.get(f"http://{self.address}/agents", timeout=5).json()
+            if sum(len(a["slots"]) for a in agents) >= n:
+                return
+            time.sleep(0.1)
+        raise RuntimeError(f"cluster did not reach {n} slots")
+
+    def up(self) -> "LocalCluster":
+        self.start_master()
+        for i in range(self.agents):
+            self.start_agent(i)
+        if self.slots_per_agent:
+            self.wait_for_slots(self.agents * self.slots_per_agent)
+        return self
+
+    def restart_master(self) -> None:
+        self.stop_master()
+        self.start_master()
+
+    def stop_master(self) -> None:
+        if self.master_proc is not None:
+            self.master_proc.terminate()
+            try:
+                self.master_proc.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                self.master_proc.kill()
+            self.master_proc = None
+
+    def down(self) -> None:
+        for p in self.agent_procs:
+            p.terminate()
+        for p in self.agent_procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        self.agent_procs = []
+        self.stop_master()
+
+    def __enter__(self) -> "LocalCluster":
+        return self.up()
+
+    def __exit__(self, *a: object) -> None:
+        self.down()

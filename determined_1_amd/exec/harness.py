@@ -1,0 +1,94 @@
+"""Trial-process entrypoint started by the agent (reference ``exec/harness.py:150-227``).
+
+    python -m determined_1_amd.exec.harness          (env: the C-env contract)
+
+1. parse/validate the ``DET_*`` environment into an ``EnvContext``;
+2. build + validate checkpoint storage (write/read/delete probe);
+3. connect the master socket and wait for rendezvous;
+4. restore the latest checkpoint (if any);
+5. run the pipeline: SocketManager -> WorkloadManager -> (SubprocessLauncher | controller).
+``InvalidHP`` raised by user code becomes ``exited_reason: INVALID_HP``; other exceptions exit
+non-zero so the master restarts the trial from its last checkpoint.
+"""
+import contextlib
+import faulthandler
+import json
+import logging
+import os
+import pathlib
+import sys
+import traceback
+from typing import Iterator, Optional
+
+from determined_1_amd import errors, storage
+from determined_1_amd.env import EnvContext
+from determined_1_amd.harness.load import prepare_controller
+from determined_1_amd.harness.socket_manager import SocketManager
+from determined_1_amd.harness.workload_manager import build_workload_manager
+from determined_1_amd.parallel.dist import DistributedConfig, RankInfo
+
+
+@contextlib.contextmanager
+def maybe_load_checkpoint(storage_mgr: storage.StorageManager, latest: Optional[dict]) -> Iterator[Optional[pathlib.Path]]:
+    if not latest or not latest.get("uuid"):
+        yield None
+        return
+    md = storage.StorageMetadata.from_json(latest)
+    with storage_mgr.restore_path(md) as path:
+        yield pathlib.Path(path)
+
+
+def local_slot_count(env: EnvContext) -> int:
+    if env.use_gpu:
+        return max(1, len(env.container_gpus) or len(env.slot_ids))
+    # CPU slots (artificial agents): one gloo process per slot
+    return max(1, len(env.slot_ids))
+
+
+def main() -> int:
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s [harness] %(levelname)s %(message)s")
+    env = EnvContext.from_environ()
+    if env.debug:
+        faulthandler.dump_traceback_later(30, repeat=True)
+    cfg = env.experiment_config
+    storage_mgr = storage.build(cfg.get("checkpoint_storage", {}))
+    storage.validate_manager(storage_mgr)
+    socket_mgr = SocketManager(env)
+    rendezvous = socket_mgr.rendezvous_info
+    metric_writer = None
+    tb_mgr = None
+    try:
+        from determined_1_amd import tensorboard
+
+        tb_mgr = tensorboard.build(env, cfg.get("checkpoint_storage", {}))
+        metric_writer = tensorboard.MetricWriter(tb_mgr.base_dir) if rendezvous.get_rank() == 0 else None
+    except ImportError:
+        pass
+    wm = build_workload_manager(env, iter(socket_mgr), rendezvous, storage_mgr, tb_mgr, metric_writer)
+    local_size = local_slot_count(env)
+    world = local_size * max(1, rendezvous.get_size())
+    native_parallel = bool(cfg.get("resources", {}).get("native_parallel", False))
+    try:
+        with maybe_load_checkpoint(storage_mgr, env.latest_checkpoint) as load_path:
+            if world > 1 and not native_parallel:
+                from determined_1_amd.harness.launcher import SubprocessLauncher
+
+                SubprocessLauncher(env, iter(wm), rendezvous, local_size, load_path).run()
+            else:
+                dist_cfg = DistributedConfig.from_configs(cfg, world_size=1, num_agents=1)
+                dist_cfg.use = False
+                ctrl = prepare_controller(env, iter(wm), load_path, rendezvous, dist_cfg, RankInfo())
+                ctrl.run()
+    except errors.InvalidHP as e:
+        logging.warning("trial reported invalid hyperparameters: %s", e)
+        socket_mgr.respond_current({"metrics": None, "exited_reason": "INVALID_HP"})
+    except Exception:
+        traceback.print_exc()
+        socket_mgr.close()
+        return 1
+    socket_mgr.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,47 @@
+"""Load the user's Trial class and build its controller (reference ``load/_load_implementation.py``
+and ``load/_load_trial_controller.py:10-143``)."""
+import importlib
+import logging
+import pathlib
+import sys
+from typing import Any, Optional, Type
+
+from determined_1_amd import trial, workload
+from determined_1_amd.env import EnvContext, RendezvousInfo
+from determined_1_amd.parallel.dist import DistributedConfig, RankInfo
+
+
+def load_trial_class(entrypoint: str, model_dir: Optional[str] = None) -> Type[trial.Trial]:
+    """``"module.sub:Class[.Inner]"`` -> the class.  The module is re-imported fresh (the reference
+    pops it from ``sys.modules`` so a changed model definition is picked up)."""
+    if ":" not in entrypoint:
+        raise ValueError(f"entrypoint must look like 'module:TrialClass', got {entrypoint!r}")
+    mod_name, qual = entrypoint.split(":", 1)
+    if model_dir:
+        d = str(pathlib.Path(model_dir).resolve())
+        if d not in sys.path:
+            sys.path.insert(0, d)
+    sys.modules.pop(mod_name, None)
+    mod = importlib.import_module(mod_name)
+    obj: Any = mod
+    for part in qual.split("."):
+        obj = getattr(obj, part)
+    if not (isinstance(obj, type) and issubclass(obj, trial.Trial)):
+        raise TypeError(f"{entrypoint} is not a Trial subclass")
+    return obj
+
+
+def prepare_controller(env: EnvContext, workloads: workload.Stream, load_path: Optional[pathlib.Path],
+                       rendezvous: RendezvousInfo, dist_config: DistributedConfig,
+                       rank_info: Optional[RankInfo] = None) -> trial.TrialController:
+    """pre_execute_hook -> context -> Trial(context) -> controller.from_trial (reference
+    ``load_controller_from_trial``)."""
+    trial_class = load_trial_class(env.experiment_config["entrypoint"])
+    controller_cls = trial_class.trial_controller_class
+    assert controller_cls is not None, f"{trial_class.__name__} has no trial_controller_class"
+    controller_cls.pre_execute_hook(env, dist_config)
+    rank = rank_info or RankInfo.from_env()
+    context = trial_class.trial_context_class(env, dist_config, rank)
+    logging.info("constructing %s (rank %d/%d)", trial_class.__name__, rank.rank, rank.size)
+    trial_inst = trial_class(context)
+    return controller_cls.from_trial(trial_inst, context, env, workloads, load_path, rendezvous, dist_config)

@@ -1,0 +1,45 @@
+"""Checkpoint storage managers (reference ``common/determined_common/storage/``).
+
+``build(checkpoint_storage_config)`` returns a manager with:
+  * ``store_path()``   context manager yielding ``(uuid, local_dir)``; on exit remote stores upload
+                        the directory (``post_store_path``) and remove the local copy;
+  * ``restore_path(metadata)`` context manager yielding a local directory with the checkpoint;
+  * ``delete(metadata)``;
+  * ``StorageMetadata(uuid, resources={relpath: size}, framework, format)`` with ``__json__``.
+Layout on shared_fs: ``<host_path>[/<storage_path>]/<uuid>/`` (``storage/shared.py:9-29``).
+"""
+from determined_1_amd.storage.base import StorageManager, StorageMetadata, list_directory, validate_manager
+from determined_1_amd.storage.shared import SharedFSStorageManager
+from determined_1_amd.storage.cloud import GCSStorageManager, HDFSStorageManager, S3StorageManager
+
+_TYPES = {
+    "shared_fs": SharedFSStorageManager,
+    "s3": S3StorageManager,
+    "gcs": GCSStorageManager,
+    "hdfs": HDFSStorageManager,
+}
+
+
+def build(config: dict, container_path: str = None) -> StorageManager:
+    cfg = dict(config or {"type": "shared_fs", "host_path": "/tmp"})
+    t = cfg.pop("type", "shared_fs")
+    for k in ("save_experiment_best", "save_trial_best", "save_trial_latest"):
+        cfg.pop(k, None)
+    if t not in _TYPES:
+        raise ValueError(f"unknown checkpoint storage type {t!r}")
+    if t == "shared_fs":
+        return SharedFSStorageManager.from_config(cfg, container_path)
+    return _TYPES[t].from_config(cfg)
+
+
+__all__ = [
+    "GCSStorageManager",
+    "HDFSStorageManager",
+    "S3StorageManager",
+    "SharedFSStorageManager",
+    "StorageManager",
+    "StorageMetadata",
+    "build",
+    "list_directory",
+    "validate_manager",
+]

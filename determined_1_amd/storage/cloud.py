@@ -1,0 +1,124 @@
+"""Object-store checkpoint managers: S3, GCS, HDFS (reference ``storage/{s3,gcs,hdfs}.py``).
+
+Checkpoints are staged in a local temp dir and uploaded in ``post_store_path``; restore downloads
+into a temp dir.  The SDK clients (boto3, google-cloud-storage, hdfs) are not installed in this
+image: the managers take an injectable ``client`` object exposing ``upload_file(local, key)``,
+``download_dir(prefix, local_dir)`` and ``delete_prefix(prefix)``, which is what the tests use
+(mirroring the reference's monkeypatched-boto tests, ``harness/tests/storage/test_s3.py``).
+"""
+import contextlib
+import os
+import pathlib
+import shutil
+import tempfile
+from typing import Any, Dict, Iterator, Optional, Tuple
+
+from determined_1_amd.storage.base import StorageManager, StorageMetadata
+
+
+class ObjectClient:
+    def upload_file(self, local: str, key: str) -> None:
+        raise NotImplementedError
+
+    def download_dir(self, prefix: str, local_dir: str) -> None:
+        raise NotImplementedError
+
+    def delete_prefix(self, prefix: str) -> None:
+        raise NotImplementedError
+
+
+class _Boto3Client(ObjectClient):
+    def __init__(self, bucket: str, **kw: Any) -> None:
+        import boto3  # noqa: F401  (raises ImportError with a clear message when absent)
+
+        self.bucket = boto3.resource("s3", **{k: v for k, v in kw.items() if v is not None}).Bucket(bucket)
+
+    def upload_file(self, local: str, key: str) -> None:
+        self.bucket.upload_file(local, key)
+
+    def download_dir(self, prefix: str, local_dir: str) -> None:
+        for obj in self.bucket.objects.filter(Prefix=prefix):
+            dst = os.path.join(local_dir, os.path.relpath(obj.key, prefix))
+            if obj.key.endswith("/"):
+                os.makedirs(dst, exist_ok=True)
+                continue
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            self.bucket.download_file(obj.key, dst)
+
+    def delete_prefix(self, prefix: str) -> None:
+        self.bucket.objects.filter(Prefix=prefix).delete()
+
+
+class _ObjectStoreManager(StorageManager):
+    def __init__(self, client: ObjectClient, prefix: str = "") -> None:
+        super().__init__(tempfile.mkdtemp(prefix="det-ckpt-stage-"))
+        self.client = client
+        self.prefix = prefix.strip("/")
+
+    def _key(self, storage_id: str, rel: str) -> str:
+        return "/".join(p for p in (self.prefix, storage_id, rel) if p)
+
+    def post_store_path(self, storage_id: str, storage_dir: pathlib.Path, metadata: StorageMetadata) -> None:
+        for rel in metadata.resources:
+            if rel.endswith("/"):
+                continue
+            self.client.upload_file(str(storage_dir.joinpath(rel)), self._key(storage_id, rel))
+        shutil.rmtree(storage_dir, ignore_errors=True)
+
+    @contextlib.contextmanager
+    def restore_path(self, metadata: StorageMetadata) -> Iterator[pathlib.Path]:
+        d = tempfile.mkdtemp(prefix="det-ckpt-restore-")
+        try:
+            self.client.download_dir(self._key(metadata.storage_id, ""), d)
+            yield pathlib.Path(d)
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+
+    def delete(self, metadata: StorageMetadata) -> None:
+        self.client.delete_prefix(self._key(metadata.storage_id, ""))
+
+
+class S3StorageManager(_ObjectStoreManager):
+    @classmethod
+    def from_config(cls, cfg: Dict[str, Any], client: Optional[ObjectClient] = None) -> "S3StorageManager":
+        if client is None:
+            client = _Boto3Client(cfg["bucket"], aws_access_key_id=cfg.get("access_key"),
+                                  aws_secret_access_key=cfg.get("secret_key"), endpoint_url=cfg.get("endpoint_url"))
+        return cls(client, cfg.get("prefix", ""))
+
+
+class GCSStorageManager(_ObjectStoreManager):
+    @classmethod
+    def from_config(cls, cfg: Dict[str, Any], client: Optional[ObjectClient] = None) -> "GCSStorageManager":
+        if client is None:
+            raise ImportError("google-cloud-storage is not installed; inject an ObjectClient")
+        return cls(client, cfg.get("prefix", ""))
+
+
+class HDFSStorageManager(_ObjectStoreManager):
+    @classmethod
+    def from_config(cls, cfg: Dict[str, Any], client: Optional[ObjectClient] = None) -> "HDFSStorageManager":
+        if client is None:
+            raise ImportError("hdfs is not installed; inject an ObjectClient")
+        return cls(client, cfg.get("hdfs_path", ""))
+
+
+class DirectoryObjectClient(ObjectClient):
+    """An object store backed by a local directory (tests, air-gapped single-node setups)."""
+
+    def __init__(self, root: str) -> None:
+        self.root = root
+        os.makedirs(root, exist_ok=True)
+
+    def upload_file(self, local: str, key: str) -> None:
+        dst = os.path.join(self.root, key)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copyfile(local, dst)
+
+    def download_dir(self, prefix: str, local_dir: str) -> None:
+        src = os.path.join(self.root, prefix)
+        if os.path.isdir(src):
+            shutil.copytree(src, local_dir, dirs_exist_ok=True)
+
+    def delete_prefix(self, prefix: str) -> None:
+        shutil.rmtree(os.path.join(self.root, prefix), ignore_errors=True)

@@ -12,6 +12,8 @@
 //   including the experiment event log replayed on master restart.
 #pragma once
 
+#include <atomic>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -65,6 +67,7 @@ class Master {
                       const std::string& container_id, int rank);
   void RunCheckpointGC(int64_t experiment_id, const Json& exp_config, const Json& to_delete);
   std::string cluster_id() const { return cluster_id_; }
+  bool shutting_down() const { return shutting_down_.load(); }
 
  private:
   void InstallRoutes();
@@ -87,6 +90,7 @@ class Master {
   std::mutex stop_mu_;
   std::condition_variable stop_cv_;
   bool stopped_ = false;
+  std::atomic<bool> shutting_down_{false};
 };
 
 // Helpers shared by the master translation units.

@@ -1,0 +1,856 @@
+// det-master process: HTTP/WebSocket API, agent + trial sockets, experiment lifecycle,
+// checkpoint GC, restore-on-restart (see include/detcore/master.h).
+//
+// REST surface (reference master/internal/core.go:518-573 + api_*.go, JSON only):
+//   GET    /info                                   cluster id, version
+//   POST   /experiments                            {config, model_definition, activate, template}
+//   GET    /experiments                            summaries
+//   GET    /experiments/:id                        config + trials + state
+//   PATCH  /experiments/:id                        {state | archived | description}
+//   POST   /experiments/:id/kill                   cancel + kill containers
+//   DELETE /experiments/:id                        delete rows + checkpoint GC of everything
+//   GET    /experiments/:id/model_def              model definition files
+//   GET    /experiments/:id/checkpoints            checkpoints (sorted by the searcher metric)
+//   GET    /experiments/:id/metrics                per-trial training/validation metric series
+//   GET    /trials/:id                             trial + steps/validations/checkpoints
+//   GET    /trials/:id/logs?offset=&limit=         trial logs
+//   POST   /trials/:id/kill
+//   GET    /checkpoints/:uuid
+//   GET    /agents                                 agents + slots (all pools)
+//   POST   /agents/:id/slots/:slot/(enable|disable) and /agents/:id/(enable|disable)
+//   GET    /resource_pools
+//   POST   /searcher/preview                       offline simulation of a searcher config
+//   GET|PUT|DELETE /templates[/:name]
+//   GET|POST /models[/:name[/versions]]            model registry
+//   POST   /trial_logs                             log shipping (agents / harness)
+//   WS     /agents?id=&resource_pool=&label=      agent channel
+//   WS     /ws/trial/:e/:t/:c                      harness channel (C-ws / C-done)
+#include "detcore/master.h"
+
+#include <signal.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <ctime>
+#include <fstream>
+#include <random>
+#include <sstream>
+
+#include "detcore/config.h"
+#include "detcore/master_actors.h"
+#include "detcore/searcher.h"
+
+extern char** environ;
+
+namespace detcore {
+namespace master {
+
+using actor::Ref;
+
+static const char* kVersion = "0.13.10.dev0+mi355x";
+
+static void Log(const std::string& s) { std::fprintf(stderr, "[det-master] %s\n", s.c_str()); }
+
+std::string NowRFC3339() {
+  auto now = std::chrono::system_clock::now();
+  std::time_t t = std::chrono::system_clock::to_time_t(now);
+  auto us = std::chrono::duration_cast<std::chrono::microseconds>(now.time_since_epoch()).count() % 1000000;
+  std::tm tm{};
+  gmtime_r(&t, &tm);
+  char buf[64];
+  std::strftime(buf, sizeof(buf), "%Y-%m-%dT%H:%M:%S", &tm);
+  char out[80];
+  std::snprintf(out, sizeof(out), "%s.%06lldZ", buf, static_cast<long long>(us));
+  return out;
+}
+
+std::string NewUUID() {
+  static thread_local std::mt19937_64 rng{std::random_device{}() ^ static_cast<uint64_t>(
+                                                std::chrono::steady_clock::now().time_since_epoch().count())};
+  uint64_t a = rng(), b = rng();
+  a = (a & 0xFFFFFFFFFFFF0FFFull) | 0x0000000000004000ull;
+  b = (b & 0x3FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;
+  char buf[40];
+  std::snprintf(buf, sizeof(buf), "%08x-%04x-%04x-%04x-%012llx", static_cast<unsigned>(a >> 32),
+                static_cast<unsigned>((a >> 16) & 0xFFFF), static_cast<unsigned>(a & 0xFFFF),
+                static_cast<unsigned>(b >> 48), static_cast<unsigned long long>(b & 0xFFFFFFFFFFFFull));
+  return buf;
+}
+
+// Checkpoints the retention policy does not keep (reference db/postgres.go:1046-1157): keep the
+// experiment's top `save_experiment_best`, each trial's top `save_trial_best` (by the searcher
+// metric of the validation at the same step) and each trial's latest `save_trial_latest`.
+Json CheckpointsToGC(Store& store, int64_t experiment_id, const Json& cfg) {
+  const Json& cs = cfg["checkpoint_storage"];
+  int64_t keep_exp = cs.get_int("save_experiment_best", 0), keep_best = cs.get_int("save_trial_best", 1),
+          keep_latest = cs.get_int("save_trial_latest", 1);
+  const std::string metric = cfg["searcher"].get_string("metric", "");
+  const bool smaller = cfg["searcher"].get_bool("smaller_is_better", true);
+  struct C {
+    Json row;
+    bool has_metric = false;
+    double metric = 0;
+  };
+  std::map<int64_t, std::vector<C>> by_trial;
+  for (auto& r : store.Scan("checkpoints", [&](const Json& r) {
+         return r.get_int("experiment_id", -1) == experiment_id && r.get_string("state", "") == "COMPLETED";
+       })) {
+    C c{r};
+    int64_t tid = r["trial_id"].as_int(), step = r["step_id"].as_int();
+    for (auto& v : store.Scan("validations", [&](const Json& v) {
+           return v.get_int("trial_id", -1) == tid && v.get_int("step_id", -1) == step && v.get_string("state", "") == "COMPLETED";
+         })) {
+      try {
+        c.metric = ValidationMetric(v["metrics"]["validation_metrics"], metric);
+        c.has_metric = true;
+      } catch (const std::exception&) {
+      }
+    }
+    by_trial[tid].push_back(c);
+  }
+  auto better = [&](const C& a, const C& b) {
+    if (a.has_metric != b.has_metric) return a.has_metric;
+    return smaller ? a.metric < b.metric : a.metric > b.metric;
+  };
+  std::set<std::string> keep;
+  std::vector<C> all;
+  for (auto& kv : by_trial) {
+    auto v = kv.second;
+    std::sort(v.begin(), v.end(), [](const C& a, const C& b) { return a.row.get_int("step_id", 0) > b.row.get_int("step_id", 0); });
+    for (int64_t i = 0; i < keep_latest && i < static_cast<int64_t>(v.size()); ++i) keep.insert(v[i].row["uuid"].as_string());
+    std::stable_sort(v.begin(), v.end(), better);
+    for (int64_t i = 0; i < keep_best && i < static_cast<int64_t>(v.size()); ++i)
+      if (v[i].has_metric) keep.insert(v[i].row["uuid"].as_string());
+    for (auto& c : v) all.push_back(c);
+  }
+  std::stable_sort(all.begin(), all.end(), better);
+  for (int64_t i = 0; i < keep_exp && i < static_cast<int64_t>(all.size()); ++i)
+    if (all[i].has_metric) keep.insert(all[i].row["uuid"].as_string());
+  // model-registry versions pin their checkpoints
+  for (auto& mv : store.Scan("model_versions")) keep.insert(mv.get_string("checkpoint_uuid", ""));
+  Json out = Json::array();
+  for (auto& c : all)
+    if (!keep.count(c.row["uuid"].as_string())) out.push_back(c.row);
+  return out;
+}
+
+// ---------------------------------------------------------------------------------- Master
+Master::Master(MasterConfig cfg) : cfg_(std::move(cfg)) {
+  store_ = std::make_unique<Store>(cfg_.store_dir);
+  sys_ = std::make_unique<actor::System>(8);
+  Json cid;
+  if (store_->Get("cluster_id", 1, &cid)) {
+    cluster_id_ = cid["cluster_id"].as_string();
+  } else {
+    cluster_id_ = NewUUID();
+    Json row = Json::object();
+    row["cluster_id"] = cluster_id_;
+    store_->Put("cluster_id", 1, row);
+  }
+  if (cfg_.resource_pools.empty()) cfg_.resource_pools.push_back("default");
+}
+
+Master::~Master() { Stop(); }
+
+Ref Master::Pool(const std::string& name) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = pools_.find(name);
+  if (it != pools_.end()) return it->second;
+  return pools_.begin()->second;
+}
+
+bool Master::SendToAgent(const std::string& agent_id, const Json& msg) {
+  std::shared_ptr<AgentConn> a;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = agents_.find(agent_id);
+    if (it == agents_.end()) return false;
+    a = it->second;
+  }
+  return a->ws->Send(msg.dump());
+}
+
+std::string Master::AgentHost(const std::string& agent_id) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = agents_.find(agent_id);
+  return it == agents_.end() ? "127.0.0.1" : it->second->host;
+}
+
+void Master::BindContainer(const std::string& cid, const std::string& agent_id, Ref trial) {
+  std::lock_guard<std::mutex> g(mu_);
+  containers_[cid] = {agent_id, std::move(trial)};
+  auto it = agents_.find(agent_id);
+  if (it != agents_.end()) it->second->containers.insert(cid);
+}
+
+void Master::UnbindContainer(const std::string& cid) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = containers_.find(cid);
+  if (it == containers_.end()) return;
+  auto a = agents_.find(it->second.first);
+  if (a != agents_.end()) a->second->containers.erase(cid);
+  containers_.erase(it);
+}
+
+Ref Master::TrialForContainer(const std::string& cid) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = containers_.find(cid);
+  return it == containers_.end() ? nullptr : it->second.second;
+}
+
+Ref Master::ExperimentRef(int64_t id) { return sys_->Get("/experiments/" + std::to_string(id)); }
+
+void Master::AppendTrialLog(int64_t trial_id, const std::string& line, const std::string& stdtype,
+                            const std::string& container_id, int rank) {
+  Json row = Json::object();
+  row["trial_id"] = trial_id;
+  row["message"] = line;
+  row["stdtype"] = stdtype;
+  row["container_id"] = container_id;
+  row["rank_id"] = rank;
+  row["timestamp"] = NowRFC3339();
+  store_->Insert("trial_logs", row);
+}
+
+void Master::RunCheckpointGC(int64_t experiment_id, const Json& exp_config, const Json& to_delete) {
+  // The reference starts a GC container (checkpoint_gc.go); here the GC job is the harness's
+  // `determined_1_amd.exec.gc_checkpoints` entrypoint run as a child process of the master,
+  // which has the same view of shared_fs / object storage as the trial processes.
+  std::string dir = (cfg_.store_dir.empty() ? std::string("/tmp") : cfg_.store_dir) + "/gc";
+  ::mkdir(dir.c_str(), 0755);
+  std::string path = dir + "/gc-" + std::to_string(experiment_id) + "-" + NewUUID() + ".json";
+  Json spec = Json::object();
+  spec["experiment_config"] = exp_config;
+  spec["checkpoints"] = to_delete;
+  {
+    std::ofstream f(path);
+    f << spec.dump();
+  }
+  for (auto& c : to_delete.as_array()) {
+    Json patch = Json::object();
+    patch["state"] = "DELETED";
+    store_->Update("checkpoints", c["id"].as_int(), patch);
+  }
+  std::string py = cfg_.python;
+  std::vector<std::string> args = {py, "-m", "determined_1_amd.exec.gc_checkpoints", path};
+  std::vector<char*> argv;
+  for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
+  argv.push_back(nullptr);
+  pid_t pid;
+  if (posix_spawnp(&pid, py.c_str(), nullptr, nullptr, argv.data(), environ) == 0) {
+    std::thread([pid] {
+      int st;
+      waitpid(pid, &st, 0);
+    }).detach();
+    Log("checkpoint GC for experiment " + std::to_string(experiment_id) + ": " + std::to_string(to_delete.size()) +
+        " checkpoints");
+  } else {
+    Log("failed to start checkpoint GC");
+  }
+}
+
+int64_t Master::CreateExperiment(const Json& body, bool* activate) {
+  Json user = body["config"];
+  if (user.is_string()) user = Json::parse(user.as_string());
+  if (!user.is_object()) throw std::invalid_argument("config must be a JSON object");
+  Json tmpl;
+  if (body.has("template") && body["template"].is_string()) {
+    for (auto& t : store_->Where("templates", "name", body["template"]))
+      tmpl = t["config"];
+    if (tmpl.is_null()) throw std::invalid_argument("template not found: " + body["template"].as_string());
+  }
+  uint32_t seed = static_cast<uint32_t>(std::chrono::system_clock::now().time_since_epoch().count() & 0xFFFFFFFF);
+  Json cfg = MergeExperimentConfig(user, cfg_.checkpoint_storage, tmpl, seed);
+  auto errs = ValidateExperimentConfig(cfg);
+  if (!errs.empty()) {
+    std::string m = "invalid experiment config:";
+    for (auto& e : errs) m += "\n  " + e;
+    throw std::invalid_argument(m);
+  }
+  // validates the searcher config by building it
+  NewSearchMethod(cfg["searcher"]);
+  if (body.get_bool("validate_only", false)) return 0;
+  *activate = body.get_bool("activate", true);
+  Json row = Json::object();
+  row["config"] = cfg;
+  row["state"] = *activate ? "ACTIVE" : "PAUSED";
+  row["start_time"] = NowRFC3339();
+  row["archived"] = false;
+  row["progress"] = 0.0;
+  row["owner"] = body.get_string("owner", "determined");
+  row["parent_id"] = body["parent_id"];
+  row["description"] = cfg.get_string("description", "");
+  int64_t id = store_->Insert("experiments", row);
+  Json md = Json::object();
+  md["experiment_id"] = id;
+  md["files"] = body["model_definition"].is_array() ? body["model_definition"] : Json::array();
+  store_->Put("model_definitions", id, md);
+  return id;
+}
+
+static net::Response J(int status, const Json& j) { return net::Response::Json(status, j.dump()); }
+static net::Response Err(int status, const std::string& m) {
+  Json j = Json::object();
+  j["error"] = m;
+  return J(status, j);
+}
+static int64_t IntParam(const net::Request& r, const std::string& k) { return std::stoll(r.Param(k)); }
+
+void Master::InstallRoutes() {
+  http_.Route("GET", "/info", [this](const net::Request&) {
+    Json j = Json::object();
+    j["cluster_id"] = cluster_id_;
+    j["cluster_name"] = cfg_.cluster_name;
+    j["version"] = kVersion;
+    j["master_id"] = cluster_id_;
+    return J(200, j);
+  });
+  http_.Route("GET", "/master/config", [this](const net::Request&) { return J(200, cfg_.ToJson()); });
+
+  // ---------------------------------------------------------------------- experiments
+  http_.Route("POST", "/experiments", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    bool activate = true;
+    int64_t id = CreateExperiment(body, &activate);
+    Json out = Json::object();
+    if (id == 0) {
+      out["valid"] = true;
+      return J(200, out);
+    }
+    Json row;
+    store_->Get("experiments", id, &row);
+    sys_->ActorOf("experiments/" + std::to_string(id),
+                  std::make_unique<ExperimentActor>(this, id, row["config"], false));
+    Log("experiment " + std::to_string(id) + " created (" + row["config"]["searcher"].get_string("name", "") + ")");
+    out["id"] = id;
+    out["config"] = row["config"];
+    net::Response resp = J(201, out);
+    resp.headers["Location"] = "/experiments/" + std::to_string(id);
+    return resp;
+  });
+  http_.Route("GET", "/experiments", [this](const net::Request& r) {
+    bool all = r.Query("all", "false") == "true";
+    Json out = Json::array();
+    for (auto& e : store_->Scan("experiments")) {
+      if (!all && e.get_bool("archived", false)) continue;
+      Json s = Json::object();
+      for (const char* k : {"id", "state", "start_time", "end_time", "archived", "progress", "owner", "description"})
+        s[k] = e[k];
+      s["searcher"] = e["config"]["searcher"].get_string("name", "");
+      s["num_trials"] = static_cast<int64_t>(store_->Where("trials", "experiment_id", e["id"]).size());
+      s["labels"] = e["config"]["labels"];
+      out.push_back(s);
+    }
+    return J(200, out);
+  });
+  http_.Route("GET", "/experiments/:id", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json e;
+    if (!store_->Get("experiments", id, &e)) return Err(404, "experiment not found");
+    Json trials = Json::array();
+    for (auto& t : store_->Where("trials", "experiment_id", Json(id))) {
+      Json tj = t;
+      int64_t tid = t["id"].as_int();
+      int64_t batches = 0;
+      for (auto& s : store_->Where("steps", "trial_id", Json(tid)))
+        if (s.get_string("state", "") == "COMPLETED") batches = std::max(batches, s.get_int("prior_batches_processed", 0) + s.get_int("num_batches", 0));
+      tj["total_batches_processed"] = batches;
+      Json best;
+      const std::string metric = e["config"]["searcher"].get_string("metric", "");
+      const bool smaller = e["config"]["searcher"].get_bool("smaller_is_better", true);
+      for (auto& v : store_->Where("validations", "trial_id", Json(tid))) {
+        if (v.get_string("state", "") != "COMPLETED") continue;
+        try {
+          double m = ValidationMetric(v["metrics"]["validation_metrics"], metric);
+          if (best.is_null() || (smaller ? m < best.as_double() : m > best.as_double())) best = m;
+        } catch (const std::exception&) {
+        }
+      }
+      tj["best_validation_metric"] = best;
+      trials.push_back(tj);
+    }
+    e["trials"] = trials;
+    return J(200, e);
+  });
+  http_.Route("PATCH", "/experiments/:id", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json e;
+    if (!store_->Get("experiments", id, &e)) return Err(404, "experiment not found");
+    Json body = Json::parse(r.body);
+    Json patch = Json::object();
+    if (body.has("archived")) patch["archived"] = body["archived"];
+    if (body.has("description")) patch["description"] = body["description"];
+    if (body.has("labels")) patch["labels"] = body["labels"];
+    if (patch.size() > 0) store_->Update("experiments", id, patch);
+    if (body.has("state")) {
+      Ref ex = ExperimentRef(id);
+      if (!ex) return Err(409, "experiment is not running (state " + e.get_string("state", "") + ")");
+      actor::Message m = ex->AskSync(SetExperimentState{body["state"].as_string(), false});
+      std::string err = m.has_value() ? std::any_cast<std::string>(m) : "no response";
+      if (!err.empty()) return Err(409, err);
+    }
+    store_->Get("experiments", id, &e);
+    return J(200, e);
+  });
+  http_.Route("POST", "/experiments/:id/kill", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Ref ex = ExperimentRef(id);
+    if (!ex) return Err(409, "experiment is not running");
+    ex->AskSync(SetExperimentState{"STOPPING_CANCELED", true});
+    return J(200, Json::object());
+  });
+  http_.Route("DELETE", "/experiments/:id", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json e;
+    if (!store_->Get("experiments", id, &e)) return Err(404, "experiment not found");
+    if (ExperimentRef(id)) return Err(409, "experiment is still running; kill it first");
+    Json all = Json::array();
+    for (auto& c : store_->Scan("checkpoints", [&](const Json& c) {
+           return c.get_int("experiment_id", -1) == id && c.get_string("state", "") == "COMPLETED";
+         }))
+      all.push_back(c);
+    if (all.size() > 0) RunCheckpointGC(id, e["config"], all);
+    std::vector<int64_t> trial_ids;
+    for (auto& t : store_->Where("trials", "experiment_id", Json(id))) trial_ids.push_back(t["id"].as_int());
+    for (int64_t tid : trial_ids) {
+      auto of = [&](const Json& x) { return x.get_int("trial_id", -1) == tid; };
+      store_->DeleteWhere("steps", of);
+      store_->DeleteWhere("validations", of);
+      store_->DeleteWhere("trial_logs", of);
+      store_->DeleteWhere("checkpoints", of);
+      store_->Delete("trials", tid);
+    }
+    store_->Delete("model_definitions", id);
+    store_->Delete("experiments", id);
+    return J(200, Json::object());
+  });
+  http_.Route("GET", "/experiments/:id/model_def", [this](const net::Request& r) {
+    Json md;
+    if (!store_->Get("model_definitions", IntParam(r, "id"), &md)) return Err(404, "not found");
+    return J(200, md);
+  });
+  http_.Route("GET", "/experiments/:id/checkpoints", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json e;
+    if (!store_->Get("experiments", id, &e)) return Err(404, "experiment not found");
+    const std::string metric = e["config"]["searcher"].get_string("metric", "");
+    const bool smaller = e["config"]["searcher"].get_bool("smaller_is_better", true);
+    std::vector<Json> out;
+    for (auto& c : store_->Scan("checkpoints", [&](const Json& c) {
+           return c.get_int("experiment_id", -1) == id && c.get_string("state", "") == "COMPLETED";
+         })) {
+      Json cj = c;
+      for (auto& v : store_->Scan("validations", [&](const Json& v) {
+             return v.get_int("trial_id", -1) == c["trial_id"].as_int() && v.get_int("step_id", -1) == c["step_id"].as_int();
+           })) {
+        cj["validation_metrics"] = v["metrics"]["validation_metrics"];
+        try {
+          cj["searcher_metric"] = ValidationMetric(v["metrics"]["validation_metrics"], metric);
+        } catch (const std::exception&) {
+        }
+      }
+      out.push_back(cj);
+    }
+    std::stable_sort(out.begin(), out.end(), [&](const Json& a, const Json& b) {
+      bool ha = a.has("searcher_metric"), hb = b.has("searcher_metric");
+      if (ha != hb) return ha;
+      if (!ha) return false;
+      return smaller ? a["searcher_metric"].as_double() < b["searcher_metric"].as_double()
+                     : a["searcher_metric"].as_double() > b["searcher_metric"].as_double();
+    });
+    Json arr = Json::array();
+    for (auto& c : out) arr.push_back(c);
+    return J(200, arr);
+  });
+  http_.Route("GET", "/experiments/:id/metrics", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json out = Json::array();
+    for (auto& t : store_->Where("trials", "experiment_id", Json(id))) {
+      Json tj = Json::object();
+      int64_t tid = t["id"].as_int();
+      tj["trial_id"] = tid;
+      Json tr = Json::array(), va = Json::array();
+      for (auto& s : store_->Where("steps", "trial_id", Json(tid))) {
+        if (s.get_string("state", "") != "COMPLETED") continue;
+        Json p = Json::object();
+        p["step_id"] = s["step_id"];
+        p["total_batches"] = s.get_int("prior_batches_processed", 0) + s.get_int("num_batches", 0);
+        p["metrics"] = s["metrics"]["avg_metrics"];
+        tr.push_back(p);
+      }
+      for (auto& v : store_->Where("validations", "trial_id", Json(tid))) {
+        if (v.get_string("state", "") != "COMPLETED") continue;
+        Json p = Json::object();
+        p["step_id"] = v["step_id"];
+        p["total_batches"] = v.get_int("prior_batches_processed", 0);
+        p["metrics"] = v["metrics"]["validation_metrics"];
+        va.push_back(p);
+      }
+      tj["training"] = tr;
+      tj["validation"] = va;
+      out.push_back(tj);
+    }
+    return J(200, out);
+  });
+
+  // --------------------------------------------------------------------------- trials
+  http_.Route("GET", "/trials/:id", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json t;
+    if (!store_->Get("trials", id, &t)) return Err(404, "trial not found");
+    Json steps = Json::array(), vals = Json::array(), ckpts = Json::array();
+    for (auto& s : store_->Where("steps", "trial_id", Json(id))) steps.push_back(s);
+    for (auto& s : store_->Where("validations", "trial_id", Json(id))) vals.push_back(s);
+    for (auto& s : store_->Where("checkpoints", "trial_id", Json(id))) ckpts.push_back(s);
+    t["steps"] = steps;
+    t["validations"] = vals;
+    t["checkpoints"] = ckpts;
+    return J(200, t);
+  });
+  http_.Route("GET", "/trials/:id/logs", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    int64_t offset = std::stoll(r.Query("offset", "0"));
+    int64_t limit = std::stoll(r.Query("limit", "100000"));
+    Json out = Json::array();
+    int64_t i = 0;
+    for (auto& l : store_->Where("trial_logs", "trial_id", Json(id))) {
+      if (l["id"].as_int() <= offset) continue;
+      if (i++ >= limit) break;
+      out.push_back(l);
+    }
+    return J(200, out);
+  });
+  http_.Route("POST", "/trials/:id/kill", [this](const net::Request& r) {
+    int64_t id = IntParam(r, "id");
+    Json t;
+    if (!store_->Get("trials", id, &t)) return Err(404, "trial not found");
+    Ref tr = sys_->Get("/experiments/" + std::to_string(t["experiment_id"].as_int()) + "/" + t["request_id"].as_string());
+    if (!tr) return Err(409, "trial is not running");
+    tr->Tell(TrialKill{});
+    return J(200, Json::object());
+  });
+  http_.Route("POST", "/trial_logs", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    Json items = body.is_array() ? body : Json(Json::Array{body});
+    for (auto& l : items.as_array())
+      AppendTrialLog(l.get_int("trial_id", 0), l.get_string("message", l.get_string("log", "")),
+                     l.get_string("stdtype", "stdout"), l.get_string("container_id", ""), static_cast<int>(l.get_int("rank_id", 0)));
+    return J(200, Json::object());
+  });
+  http_.Route("GET", "/checkpoints/:uuid", [this](const net::Request& r) {
+    for (auto& c : store_->Where("checkpoints", "uuid", Json(r.Param("uuid")))) {
+      Json t;
+      if (store_->Get("trials", c["trial_id"].as_int(), &t)) {
+        c["hparams"] = t["hparams"];
+        Json e;
+        if (store_->Get("experiments", t["experiment_id"].as_int(), &e)) c["experiment_config"] = e["config"];
+      }
+      for (auto& v : store_->Scan("validations", [&](const Json& v) {
+             return v.get_int("trial_id", -1) == c["trial_id"].as_int() && v.get_int("step_id", -1) == c["step_id"].as_int();
+           }))
+        c["validation_metrics"] = v["metrics"]["validation_metrics"];
+      return J(200, c);
+    }
+    return Err(404, "checkpoint not found");
+  });
+
+  // --------------------------------------------------------------------- agents/pools
+  auto agents_json = [this]() {
+    Json out = Json::array();
+    std::vector<std::string> pools;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& p : pools_) pools.push_back(p.first);
+    }
+    for (auto& p : pools) {
+      actor::Message m = Pool(p)->AskSync(PoolSummary{});
+      if (!m.has_value()) continue;
+      Json s = std::any_cast<Json>(m);
+      for (auto& a : s["agents"].as_array()) {
+        Json aj = a;
+        aj["resource_pool"] = p;
+        out.push_back(aj);
+      }
+    }
+    return out;
+  };
+  http_.Route("GET", "/agents", [agents_json](const net::Request&) { return J(200, agents_json()); });
+  auto slot_toggle = [this](const net::Request& r, int device, bool enable) {
+    std::string agent = r.Param("id");
+    std::string pool;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = agents_.find(agent);
+      if (it == agents_.end()) return Err(404, "agent not found");
+      pool = it->second->pool;
+    }
+    actor::Message m = Pool(pool)->AskSync(SetSlotEnabled{agent, device, enable});
+    bool ok = m.has_value() && std::any_cast<bool>(m);
+    return ok ? J(200, Json::object()) : Err(404, "slot not found");
+  };
+  http_.Route("POST", "/agents/:id/slots/:slot/enable",
+              [slot_toggle](const net::Request& r) { return slot_toggle(r, std::stoi(r.Param("slot")), true); });
+  http_.Route("POST", "/agents/:id/slots/:slot/disable",
+              [slot_toggle](const net::Request& r) { return slot_toggle(r, std::stoi(r.Param("slot")), false); });
+  http_.Route("POST", "/agents/:id/enable", [slot_toggle](const net::Request& r) { return slot_toggle(r, -1, true); });
+  http_.Route("POST", "/agents/:id/disable", [slot_toggle](const net::Request& r) { return slot_toggle(r, -1, false); });
+  http_.Route("GET", "/resource_pools", [this](const net::Request&) {
+    Json out = Json::array();
+    std::vector<std::string> pools;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& p : pools_) pools.push_back(p.first);
+    }
+    for (auto& p : pools) {
+      actor::Message m = Pool(p)->AskSync(PoolSummary{});
+      if (m.has_value()) {
+        Json s = std::any_cast<Json>(m);
+        s.as_object().erase("agents");
+        out.push_back(s);
+      }
+    }
+    return J(200, out);
+  });
+
+  // --------------------------------------------------------------- searcher preview
+  http_.Route("POST", "/searcher/preview", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    Json user = body["config"].is_string() ? Json::parse(body["config"].as_string()) : body["config"];
+    Json cfg = MergeExperimentConfig(user, cfg_.checkpoint_storage, Json(), 0);
+    uint32_t seed = static_cast<uint32_t>(cfg["reproducibility"].get_int("experiment_seed", 0));
+    Searcher s(seed, NewSearchMethod(cfg["searcher"]), cfg["hyperparameters"]);
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    auto res = Simulate(s, [&](int, int) { return U(rng); }, true, seed, cfg["searcher"].get_string("metric", "metric"));
+    Json out = Json::object();
+    out["results"] = res.Summary();
+    out["num_trials"] = static_cast<int64_t>(res.order.size());
+    return J(200, out);
+  });
+
+  // ------------------------------------------------------------------------ templates
+  http_.Route("GET", "/templates", [this](const net::Request&) {
+    Json out = Json::array();
+    for (auto& t : store_->Scan("templates")) out.push_back(t);
+    return J(200, out);
+  });
+  http_.Route("GET", "/templates/:name", [this](const net::Request& r) {
+    for (auto& t : store_->Where("templates", "name", Json(r.Param("name")))) return J(200, t);
+    return Err(404, "template not found");
+  });
+  http_.Route("PUT", "/templates/:name", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    Json cfg = body.has("config") ? body["config"] : body;
+    if (cfg.is_string()) cfg = Json::parse(cfg.as_string());
+    store_->DeleteWhere("templates", [&](const Json& t) { return t.get_string("name", "") == r.Param("name"); });
+    Json row = Json::object();
+    row["name"] = r.Param("name");
+    row["config"] = cfg;
+    store_->Insert("templates", row);
+    return J(200, row);
+  });
+  http_.Route("DELETE", "/templates/:name", [this](const net::Request& r) {
+    store_->DeleteWhere("templates", [&](const Json& t) { return t.get_string("name", "") == r.Param("name"); });
+    return J(200, Json::object());
+  });
+
+  // ------------------------------------------------------------------- model registry
+  http_.Route("GET", "/models", [this](const net::Request&) {
+    Json out = Json::array();
+    for (auto& m : store_->Scan("models")) out.push_back(m);
+    return J(200, out);
+  });
+  http_.Route("POST", "/models/:name", [this](const net::Request& r) {
+    if (!store_->Where("models", "name", Json(r.Param("name"))).empty()) return Err(409, "model exists");
+    Json body = r.body.empty() ? Json::object() : Json::parse(r.body);
+    Json row = Json::object();
+    row["name"] = r.Param("name");
+    row["description"] = body.get_string("description", "");
+    row["metadata"] = body["metadata"];
+    row["creation_time"] = NowRFC3339();
+    store_->Insert("models", row);
+    return J(201, row);
+  });
+  http_.Route("GET", "/models/:name", [this](const net::Request& r) {
+    for (auto& m : store_->Where("models", "name", Json(r.Param("name")))) {
+      Json vs = Json::array();
+      for (auto& v : store_->Where("model_versions", "model_name", Json(r.Param("name")))) vs.push_back(v);
+      m["versions"] = vs;
+      return J(200, m);
+    }
+    return Err(404, "model not found");
+  });
+  http_.Route("GET", "/models/:name/versions", [this](const net::Request& r) {
+    Json vs = Json::array();
+    for (auto& v : store_->Where("model_versions", "model_name", Json(r.Param("name")))) vs.push_back(v);
+    return J(200, vs);
+  });
+  http_.Route("POST", "/models/:name/versions", [this](const net::Request& r) {
+    if (store_->Where("models", "name", Json(r.Param("name"))).empty()) return Err(404, "model not found");
+    Json body = Json::parse(r.body);
+    std::string uuid = body.get_string("checkpoint_uuid", "");
+    if (store_->Where("checkpoints", "uuid", Json(uuid)).empty()) return Err(404, "checkpoint not found");
+    int64_t ver = static_cast<int64_t>(store_->Where("model_versions", "model_name", Json(r.Param("name"))).size()) + 1;
+    Json row = Json::object();
+    row["model_name"] = r.Param("name");
+    row["version"] = ver;
+    row["checkpoint_uuid"] = uuid;
+    row["creation_time"] = NowRFC3339();
+    store_->Insert("model_versions", row);
+    return J(201, row);
+  });
+
+  // ----------------------------------------------------------------------- websockets
+  http_.RouteWs("/agents", [this](const net::Request& r, net::WsPtr ws) { HandleAgentSocket(r, ws); });
+  http_.RouteWs("/ws/trial/:e/:t/:c", [this](const net::Request& r, net::WsPtr ws) { HandleTrialSocket(r, ws); });
+}
+
+void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
+  auto conn = std::make_shared<AgentConn>();
+  conn->id = r.Query("id", "agent-" + NewUUID().substr(0, 8));
+  conn->pool = r.Query("resource_pool", "");
+  conn->label = r.Query("label", "");
+  conn->host = r.Query("host", r.remote_addr);
+  conn->ws = ws;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (conn->pool.empty() || !pools_.count(conn->pool)) conn->pool = pools_.begin()->first;
+    if (agents_.count(conn->id)) {
+      Json m = Json::object();
+      m["type"] = "Error";
+      m["error"] = "agent id already connected: " + conn->id;
+      ws->Send(m.dump());
+      return;
+    }
+    agents_[conn->id] = conn;
+  }
+  Json opts = Json::object();
+  opts["type"] = "MasterSetAgentOptions";
+  opts["master_host"] = advertised_host_;
+  opts["master_port"] = port_;
+  opts["cluster_id"] = cluster_id_;
+  ws->Send(opts.dump());
+  ws->ReadLoop([&](const std::string& text) {
+    Json m;
+    try {
+      m = Json::parse(text);
+    } catch (const std::exception&) {
+      return;
+    }
+    const std::string t = m.get_string("type", "");
+    if (t == "AgentStarted") {
+      sched::Agent a;
+      a.id = conn->id;
+      a.label = m.get_string("label", conn->label);
+      conn->devices = m["devices"];
+      for (auto& d : m["devices"].as_array()) {
+        sched::Slot s;
+        s.device_id = static_cast<int>(d.get_int("id", 0));
+        s.uuid = d.get_string("uuid", "");
+        s.type = d.get_string("type", "gpu");
+        a.slots.push_back(s);
+      }
+      Pool(conn->pool)->Tell(AddAgent{a});
+    } else if (t == "ContainerStateChanged") {
+      std::string cid = m.get_string("container_id", "");
+      Ref tr = TrialForContainer(cid);
+      if (tr)
+        tr->Tell(ContainerStateMsg{cid, m.get_string("state", ""), static_cast<int>(m.get_int("exit_code", 0)),
+                                   m.get_string("failure", ""), m.get_string("address", "")});
+    } else if (t == "ContainerLog") {
+      AppendTrialLog(m.get_int("trial_id", 0), m.get_string("log", ""), m.get_string("stdtype", "stdout"),
+                     m.get_string("container_id", ""), static_cast<int>(m.get_int("rank", 0)));
+    }
+  });
+  // disconnect: every container on the agent is gone (reference agent.go:114-126)
+  std::vector<std::string> cids;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    cids.assign(conn->containers.begin(), conn->containers.end());
+    agents_.erase(conn->id);
+  }
+  Pool(conn->pool)->Tell(RemoveAgent{conn->id});
+  for (auto& cid : cids) {
+    Ref tr = TrialForContainer(cid);
+    if (tr) tr->Tell(ContainerStateMsg{cid, "Terminated", -1, "agent failed while container was running", ""});
+  }
+  Log("agent " + conn->id + " disconnected");
+}
+
+void Master::HandleTrialSocket(const net::Request& r, net::WsPtr ws) {
+  std::string cid = r.Param("c");
+  Ref tr = TrialForContainer(cid);
+  if (!tr) return;
+  tr->Tell(SocketConnected{cid, ws});
+  ws->ReadLoop([&](const std::string& text) {
+    try {
+      tr->Tell(SocketMessage{cid, Json::parse(text)});
+    } catch (const std::exception&) {
+    }
+  });
+  tr->Tell(SocketClosed{cid});
+}
+
+void Master::RestoreExperiments() {
+  // Non-terminal experiments are rebuilt from the event log (experiment.go:238-294).
+  for (auto& e : store_->Scan("experiments")) {
+    std::string st = e.get_string("state", "");
+    if (st == "COMPLETED" || st == "CANCELED" || st == "ERROR") continue;
+    int64_t id = e["id"].as_int();
+    std::vector<Json> events = store_->Where("searcher_events", "experiment_id", Json(id));
+    std::sort(events.begin(), events.end(), [](const Json& a, const Json& b) { return a["id"].as_int() < b["id"].as_int(); });
+    if (st.rfind("STOPPING_", 0) == 0) {
+      // nothing left running: finish the stop
+      Json patch = Json::object();
+      patch["state"] = st == "STOPPING_CANCELED" ? "CANCELED" : st == "STOPPING_ERROR" ? "ERROR" : "COMPLETED";
+      patch["end_time"] = NowRFC3339();
+      store_->Update("experiments", id, patch);
+      continue;
+    }
+    Ref ex = sys_->ActorOf("experiments/" + std::to_string(id), std::make_unique<ExperimentActor>(this, id, e["config"], true));
+    ex->Tell(ReplayEvents{events});
+    Log("restoring experiment " + std::to_string(id) + " from " + std::to_string(events.size()) + " events");
+  }
+}
+
+int Master::Start() {
+  for (auto& p : cfg_.resource_pools) pools_[p] = sys_->ActorOf("pools/" + p, std::make_unique<ResourcePoolActor>(this, p));
+  InstallRoutes();
+  port_ = http_.Listen(cfg_.listen_host, cfg_.port);
+  if (port_ < 0) throw std::runtime_error("cannot bind port " + std::to_string(cfg_.port));
+  if (cfg_.listen_host != "0.0.0.0" && !cfg_.listen_host.empty()) advertised_host_ = cfg_.listen_host;
+  http_.Start();
+  RestoreExperiments();
+  Log(std::string("listening on ") + cfg_.listen_host + ":" + std::to_string(port_) + " scheduler=" + cfg_.scheduler);
+  return port_;
+}
+
+void Master::Stop() {
+  {
+    std::lock_guard<std::mutex> g(stop_mu_);
+    if (stopped_) return;
+    stopped_ = true;
+  }
+  shutting_down_ = true;
+  http_.Stop();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& a : agents_) a.second->ws->Close();
+  }
+  sys_->Shutdown();
+  store_->Flush();
+  stop_cv_.notify_all();
+}
+
+void Master::Wait() {
+  std::unique_lock<std::mutex> l(stop_mu_);
+  stop_cv_.wait(l, [&] { return stopped_; });
+}
+
+}  // namespace master
+}  // namespace detcore

@@ -138,13 +138,14 @@ ExperimentActor::ExperimentActor(Master* m, int64_t id, Json config, bool replay
 }
 
 void ExperimentActor::Event(const std::string& type, Json body) {
-  if (replaying_) return;
+  if (replaying_ || m_->shutting_down()) return;
   body["type"] = type;
   body["experiment_id"] = id_;
   m_->store().Insert("searcher_events", body);
 }
 
 void ExperimentActor::SaveState() {
+  if (m_->shutting_down()) return;
   Json patch = Json::object();
   patch["state"] = state_;
   patch["progress"] = searcher_->Progress();
@@ -321,6 +322,7 @@ void ExperimentActor::Receive(Context& ctx) {
 }
 
 void ExperimentActor::ChildGone(Context& ctx, const Ref& child) {
+  if (m_->shutting_down()) return;  // master restart: trials are restored, not closed
   RequestID rid;
   try {
     rid = ParseRequestID(child->id());
@@ -492,7 +494,7 @@ void TrialActor::Receive(Context& ctx) {
   } else if (ctx.Is<actor::PostStop>()) {
     if (!task_id_.empty()) m_->Pool(pool_)->Tell(ResourcesReleased{task_id_});
     for (auto& c : containers_) m_->UnbindContainer(c.first);
-    if (trial_id_) {
+    if (trial_id_ && !m_->shutting_down()) {
       Json patch = Json::object();
       patch["state"] = errored_ ? "ERROR" : (canceled_ ? "CANCELED" : "COMPLETED");
       patch["end_time"] = NowRFC3339();

@@ -1,0 +1,93 @@
+// det-master entrypoint (reference master/cmd/determined-master/root.go): flags + optional JSON
+// config file (YAML configs are converted by the Python launcher `det-master` wrapper).
+#include <signal.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+
+#include "detcore/master.h"
+
+static detcore::master::Master* g_master = nullptr;
+
+static void OnSignal(int) {
+  // Stop() is not async-signal-safe; hand it to a thread.
+  static bool once = false;
+  if (once) return;
+  once = true;
+  std::thread([] {
+    if (g_master) g_master->Stop();
+  }).detach();
+}
+
+static void Usage() {
+  std::fprintf(stderr,
+               "usage: det-master [--config-file FILE.json] [--host H] [--port P] [--store-dir DIR]\n"
+               "                  [--scheduler fair_share|priority|round_robin] [--fitting-policy best|worst]\n"
+               "                  [--resource-pools a,b] [--checkpoint-host-path DIR] [--python PY]\n");
+}
+
+int main(int argc, char** argv) {
+  detcore::Json cfgj = detcore::Json::object();
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        Usage();
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--config-file") {
+      std::ifstream f(next());
+      std::stringstream ss;
+      ss << f.rdbuf();
+      detcore::Json file = detcore::Json::parse(ss.str());
+      for (auto& kv : file.as_object()) cfgj[kv.first] = kv.second;
+    } else if (a == "--host") {
+      cfgj["listen_host"] = next();
+    } else if (a == "--port") {
+      cfgj["port"] = std::stoi(next());
+    } else if (a == "--store-dir") {
+      cfgj["store_dir"] = next();
+    } else if (a == "--scheduler") {
+      cfgj["scheduler"]["type"] = next();
+    } else if (a == "--fitting-policy") {
+      cfgj["scheduler"]["fitting_policy"] = next();
+    } else if (a == "--resource-pools") {
+      detcore::Json pools = detcore::Json::array();
+      std::stringstream ss(next());
+      std::string p;
+      while (std::getline(ss, p, ',')) pools.push_back(p);
+      cfgj["resource_pools"] = pools;
+    } else if (a == "--checkpoint-host-path") {
+      detcore::Json cs = detcore::Json::object();
+      cs["type"] = "shared_fs";
+      cs["host_path"] = next();
+      cfgj["checkpoint_storage"] = cs;
+    } else if (a == "--python") {
+      cfgj["python"] = next();
+    } else if (a == "--scheduler-tick-ms") {
+      cfgj["scheduler_tick_ms"] = std::stod(next());
+    } else if (a == "-h" || a == "--help") {
+      Usage();
+      return 0;
+    } else {
+      std::fprintf(stderr, "unknown flag %s\n", a.c_str());
+      Usage();
+      return 2;
+    }
+  }
+  signal(SIGPIPE, SIG_IGN);
+  detcore::master::Master m(detcore::MasterConfig::FromJson(cfgj));
+  g_master = &m;
+  signal(SIGINT, OnSignal);
+  signal(SIGTERM, OnSignal);
+  int port = m.Start();
+  std::printf("det-master listening on port %d\n", port);
+  std::fflush(stdout);
+  m.Wait();
+  return 0;
+}

@@ -11,7 +11,7 @@ step() {  # name timeout cmd...
   echo "[session] $name rc=$rc" | tee -a gpurun_out/session.log
   if [ $rc -ne 0 ]; then tail -40 "gpurun_out/$name.log"; exit $rc; fi
 }
-step build 300 python -c "import __graft_entry__ as g; g.build()"
+step build 300 python -m determined_1_amd.ops.build --force
 step pytest_norm 400 python -m pytest tests/test_norm_gpu.py -x -q
 step bench_fused 400 python bench.py
 step bench_stock 400 python bench.py --no-fused-bn
