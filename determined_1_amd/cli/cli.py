@@ -1,0 +1,460 @@
+"""``det`` CLI: experiment / trial / checkpoint / model / agent / slot / template / preview-search /
+deploy / version (reference ``cli/determined_cli/cli.py:73-171``, ``experiment.py``, ``trial.py``).
+
+    python -m determined_1_amd.cli -m 127.0.0.1:8080 experiment create const.yaml model_dir
+"""
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+from typing import Any, Dict, List
+
+import yaml
+
+from determined_1_amd import __version__
+from determined_1_amd.api import MasterClient, read_context
+from determined_1_amd.config import merge_with_defaults, validate_experiment_config
+
+
+def _load_config(path: str) -> Dict[str, Any]:
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
+
+
+def _table(rows: List[Dict[str, Any]], cols: List[str]) -> str:
+    if not rows:
+        return "(none)"
+    w = {c: max(len(c), *(len(str(r.get(c, ""))) for r in rows)) for c in cols}
+    line = " | ".join(c.ljust(w[c]) for c in cols)
+    out = [line, "-+-".join("-" * w[c] for c in cols)]
+    for r in rows:
+        out.append(" | ".join(str(r.get(c, "")).ljust(w[c]) for c in cols))
+    return "\n".join(out)
+
+
+def make_test_config(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    """Test mode (reference ``api/experiment.py:258-299``): 1-batch single search, validation every
+    batch, no restarts, sampled hyperparameters."""
+    import random
+
+    c = json.loads(json.dumps(cfg))
+    hps = {}
+    for name, hp in (c.get("hyperparameters") or {}).items():
+        if not isinstance(hp, dict) or "type" not in hp:
+            hps[name] = hp
+        elif hp["type"] == "const":
+            hps[name] = hp["val"]
+        elif hp["type"] == "int":
+            hps[name] = random.randint(hp["minval"], hp["maxval"])
+        elif hp["type"] == "double":
+            hps[name] = random.uniform(hp["minval"], hp["maxval"])
+        elif hp["type"] == "log":
+            hps[name] = hp.get("base", 10.0) ** random.uniform(hp["minval"], hp["maxval"])
+        elif hp["type"] == "categorical":
+            hps[name] = random.choice(hp["vals"])
+    c["hyperparameters"] = {k: {"type": "const", "val": v} for k, v in hps.items()}
+    metric = c.get("searcher", {}).get("metric", "validation_loss")
+    c["searcher"] = {"name": "single", "metric": metric, "max_length": {"batches": 1},
+                     "smaller_is_better": c.get("searcher", {}).get("smaller_is_better", True)}
+    c["scheduling_unit"] = 1
+    c["min_validation_period"] = {"batches": 1}
+    c["max_restarts"] = 0
+    cs = c.setdefault("checkpoint_storage", {})
+    cs.update({"save_experiment_best": 0, "save_trial_best": 0, "save_trial_latest": 0})
+    c.pop("min_checkpoint_period", None)
+    return c
+
+
+# --------------------------------------------------------------------------- experiment
+def cmd_experiment_create(args: argparse.Namespace) -> None:
+    cfg = _load_config(args.config_file)
+    for kv in args.config or []:
+        k, v = kv.split("=", 1)
+        node = cfg
+        parts = k.split(".")
+        for p in parts[:-1]:
+            node = node.setdefault(p, {})
+        node[parts[-1]] = yaml.safe_load(v)
+    if args.test_mode:
+        cfg = make_test_config(cfg)
+    errs = validate_experiment_config(merge_with_defaults(cfg))
+    if errs:
+        sys.exit("invalid experiment config:\n  " + "\n  ".join(errs))
+    if args.local:
+        from determined_1_amd.experimental import run_local_test
+
+        run_local_test(cfg, args.model_def)
+        print("local test mode passed")
+        return
+    client = MasterClient(args.master)
+    ctx = read_context(pathlib.Path(args.model_def))
+    r = client.create_experiment(cfg, ctx, activate=not args.paused, template=args.template)
+    eid = r["id"]
+    print(f"Created experiment {eid}")
+    if args.test_mode or args.follow:
+        st = _follow(client, eid)
+        if args.test_mode:
+            if st != "COMPLETED":
+                sys.exit(f"test experiment {eid} ended in state {st}")
+            client.patch(f"/experiments/{eid}", {"archived": True})
+            print("Model definition test succeeded!")
+
+
+def _follow(client: MasterClient, eid: int) -> str:
+    seen = {}  # type: Dict[int, int]
+    while True:
+        e = client.experiment(eid)
+        for t in e.get("trials", []):
+            off = seen.get(t["id"], 0)
+            for l in client.get(f"/trials/{t['id']}/logs", offset=off):
+                print(f"[trial {t['id']}] {l['message']}")
+                seen[t["id"]] = l["id"]
+        if e["state"] in ("COMPLETED", "CANCELED", "ERROR"):
+            print(f"Experiment {eid} {e['state']}")
+            return e["state"]
+        time.sleep(1.0)
+
+
+def cmd_experiment_list(args: argparse.Namespace) -> None:
+    rows = MasterClient(args.master).get("/experiments", all="true" if args.all else "false")
+    print(_table(rows, ["id", "state", "searcher", "num_trials", "progress", "start_time", "description"]))
+
+
+def cmd_experiment_describe(args: argparse.Namespace) -> None:
+    e = MasterClient(args.master).experiment(args.experiment_id)
+    if args.json:
+        print(json.dumps(e, indent=2))
+        return
+    print(f"Experiment {e['id']}: {e['state']}  progress={e.get('progress')}  searcher={e['config']['searcher'].get('name')}")
+    print(_table(e["trials"], ["id", "state", "total_batches_processed", "best_validation_metric", "restarts"]))
+
+
+def _set_state(state: str):
+    def f(args: argparse.Namespace) -> None:
+        MasterClient(args.master).set_state(args.experiment_id, state)
+        print(f"experiment {args.experiment_id}: {state}")
+
+    return f
+
+
+def cmd_experiment_kill(args: argparse.Namespace) -> None:
+    MasterClient(args.master).post(f"/experiments/{args.experiment_id}/kill")
+    print(f"killed experiment {args.experiment_id}")
+
+
+def cmd_experiment_archive(args: argparse.Namespace, archived: bool = True) -> None:
+    MasterClient(args.master).patch(f"/experiments/{args.experiment_id}", {"archived": archived})
+
+
+def cmd_experiment_delete(args: argparse.Namespace) -> None:
+    MasterClient(args.master).delete(f"/experiments/{args.experiment_id}")
+    print(f"deleted experiment {args.experiment_id}")
+
+
+def cmd_experiment_wait(args: argparse.Namespace) -> None:
+    st = MasterClient(args.master).wait_for_experiment(args.experiment_id, timeout=args.timeout)
+    print(st)
+    if st != "COMPLETED":
+        sys.exit(1)
+
+
+def cmd_experiment_download_model_def(args: argparse.Namespace) -> None:
+    import base64
+
+    md = MasterClient(args.master).get(f"/experiments/{args.experiment_id}/model_def")
+    out = pathlib.Path(args.output_dir)
+    for f in md["files"]:
+        p = out.joinpath(f["path"])
+        if f.get("type") == "dir":
+            p.mkdir(parents=True, exist_ok=True)
+            continue
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(base64.b64decode(f["content"]))
+    print(f"wrote {len(md['files'])} entries to {out}")
+
+
+def cmd_experiment_checkpoints(args: argparse.Namespace) -> None:
+    rows = MasterClient(args.master).get(f"/experiments/{args.experiment_id}/checkpoints")
+    if args.best is not None:
+        rows = rows[: args.best]
+    print(_table(rows, ["uuid", "trial_id", "step_id", "total_batches_processed", "searcher_metric", "state"]))
+
+
+# ------------------------------------------------------------------------------- trial
+def cmd_trial_describe(args: argparse.Namespace) -> None:
+    t = MasterClient(args.master).get(f"/trials/{args.trial_id}")
+    if args.json:
+        print(json.dumps(t, indent=2))
+        return
+    print(f"Trial {t['id']} (experiment {t['experiment_id']}): {t['state']}  hparams={json.dumps(t['hparams'])}")
+    rows = [{"step": s["step_id"], "state": s["state"], "batches": s.get("num_batches"),
+             "metrics": json.dumps((s.get("metrics") or {}).get("avg_metrics"))} for s in t["steps"]]
+    print(_table(rows, ["step", "state", "batches", "metrics"]))
+
+
+def cmd_trial_logs(args: argparse.Namespace) -> None:
+    for l in MasterClient(args.master).trial_logs(args.trial_id, follow=args.follow):
+        print(l["message"])
+
+
+def cmd_trial_kill(args: argparse.Namespace) -> None:
+    MasterClient(args.master).post(f"/trials/{args.trial_id}/kill")
+
+
+# -------------------------------------------------------------------------- checkpoint
+def cmd_checkpoint_describe(args: argparse.Namespace) -> None:
+    print(json.dumps(MasterClient(args.master).get(f"/checkpoints/{args.uuid}"), indent=2))
+
+
+def cmd_checkpoint_download(args: argparse.Namespace) -> None:
+    from determined_1_amd.experimental import Determined
+
+    path = Determined(args.master).get_checkpoint(args.uuid).download(args.output_dir)
+    print(path)
+
+
+# ----------------------------------------------------------------------- agents / slots
+def cmd_agent_list(args: argparse.Namespace) -> None:
+    rows = [{"id": a["id"], "resource_pool": a.get("resource_pool"), "slots": len(a["slots"]),
+             "used": sum(1 for s in a["slots"] if s["task"]), "enabled": a["enabled"], "label": a["label"]}
+            for a in MasterClient(args.master).get("/agents")]
+    print(_table(rows, ["id", "resource_pool", "slots", "used", "enabled", "label"]))
+
+
+def cmd_slot_list(args: argparse.Namespace) -> None:
+    rows = []
+    for a in MasterClient(args.master).get("/agents"):
+        for s in a["slots"]:
+            rows.append({"agent": a["id"], "slot": s["id"], "type": s["type"], "uuid": s["uuid"],
+                         "enabled": s["enabled"], "task": s["task"]})
+    print(_table(rows, ["agent", "slot", "type", "uuid", "enabled", "task"]))
+
+
+def _slot_toggle(enable: bool):
+    def f(args: argparse.Namespace) -> None:
+        path = f"/agents/{args.agent_id}/slots/{args.slot_id}/" if args.slot_id is not None else f"/agents/{args.agent_id}/"
+        MasterClient(args.master).post(path + ("enable" if enable else "disable"))
+
+    return f
+
+
+def cmd_resource_pools(args: argparse.Namespace) -> None:
+    print(_table(MasterClient(args.master).get("/resource_pools"),
+                 ["name", "scheduler", "num_slots", "slots_used", "num_tasks", "tasks_pending"]))
+
+
+# ---------------------------------------------------------------------------- templates
+def cmd_template_list(args: argparse.Namespace) -> None:
+    print(_table(MasterClient(args.master).get("/templates"), ["name"]))
+
+
+def cmd_template_set(args: argparse.Namespace) -> None:
+    MasterClient(args.master).put(f"/templates/{args.name}", {"config": _load_config(args.template_file)})
+
+
+def cmd_template_describe(args: argparse.Namespace) -> None:
+    print(yaml.safe_dump(MasterClient(args.master).get(f"/templates/{args.name}")["config"]))
+
+
+def cmd_template_remove(args: argparse.Namespace) -> None:
+    MasterClient(args.master).delete(f"/templates/{args.name}")
+
+
+# ------------------------------------------------------------------------------- models
+def cmd_model_create(args: argparse.Namespace) -> None:
+    print(json.dumps(MasterClient(args.master).post(f"/models/{args.name}", {"description": args.description or ""})))
+
+
+def cmd_model_list(args: argparse.Namespace) -> None:
+    print(_table(MasterClient(args.master).get("/models"), ["name", "description", "creation_time"]))
+
+
+def cmd_model_describe(args: argparse.Namespace) -> None:
+    print(json.dumps(MasterClient(args.master).get(f"/models/{args.name}"), indent=2))
+
+
+def cmd_model_register(args: argparse.Namespace) -> None:
+    print(json.dumps(MasterClient(args.master).post(f"/models/{args.name}/versions", {"checkpoint_uuid": args.uuid})))
+
+
+# ---------------------------------------------------------------------------- misc
+def cmd_preview_search(args: argparse.Namespace) -> None:
+    cfg = _load_config(args.config_file)
+    if args.master_side:
+        r = MasterClient(args.master).post("/searcher/preview", {"config": cfg})
+        results = r["results"]
+    else:
+        from determined_1_amd.searcher import simulate_config
+
+        results = simulate_config(cfg)["results"]
+    total = sum(results.values())
+    print(f"Using search configuration:\n{yaml.safe_dump(cfg.get('searcher', {}))}")
+    print(f"This search will create a total of {total} trial(s).")
+    for ops, n in sorted(results.items(), key=lambda kv: -kv[1]):
+        print(f"  {n:5d} trial(s): {ops}")
+
+
+def cmd_version(args: argparse.Namespace) -> None:
+    print(f"client: {__version__}")
+    try:
+        print("master:", json.dumps(MasterClient(args.master, timeout=3).get("/info")))
+    except Exception as e:  # noqa: BLE001
+        print(f"master: unreachable ({e})")
+
+
+def cmd_master_config(args: argparse.Namespace) -> None:
+    print(json.dumps(MasterClient(args.master).get("/master/config"), indent=2))
+
+
+def cmd_deploy_local(args: argparse.Namespace) -> None:
+    from determined_1_amd.deploy import LocalCluster
+
+    c = LocalCluster(agents=args.agents, slots_per_agent=args.artificial_slots, port=args.port,
+                     store_dir=args.store_dir, checkpoint_dir=args.checkpoint_dir, gpu=args.gpu,
+                     scheduler=args.scheduler)
+    c.up()
+    print(f"cluster up: DET_MASTER={c.address}  (Ctrl-C to stop)")
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        c.down()
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="det", description="Determined (MI355X-native) command line")
+    p.add_argument("-m", "--master", default=os.environ.get("DET_MASTER", "127.0.0.1:8080"))
+    sub = p.add_subparsers(dest="cmd")
+
+    e = sub.add_parser("experiment", aliases=["e"]).add_subparsers(dest="sub")
+    c = e.add_parser("create")
+    c.add_argument("config_file")
+    c.add_argument("model_def")
+    c.add_argument("--test-mode", "--test", action="store_true")
+    c.add_argument("--local", action="store_true")
+    c.add_argument("--paused", action="store_true")
+    c.add_argument("--follow", "-f", action="store_true")
+    c.add_argument("--template")
+    c.add_argument("--config", action="append", help="override: key.sub=value")
+    c.set_defaults(func=cmd_experiment_create)
+    ls = e.add_parser("list")
+    ls.add_argument("--all", "-a", action="store_true")
+    ls.set_defaults(func=cmd_experiment_list)
+    for name, fn in (("describe", cmd_experiment_describe),):
+        d = e.add_parser(name)
+        d.add_argument("experiment_id", type=int)
+        d.add_argument("--json", action="store_true")
+        d.set_defaults(func=fn)
+    for name, fn in (("activate", _set_state("ACTIVE")), ("pause", _set_state("PAUSED")),
+                     ("cancel", _set_state("STOPPING_CANCELED")), ("kill", cmd_experiment_kill),
+                     ("archive", cmd_experiment_archive), ("unarchive", lambda a: cmd_experiment_archive(a, False)),
+                     ("delete", cmd_experiment_delete)):
+        d = e.add_parser(name)
+        d.add_argument("experiment_id", type=int)
+        d.set_defaults(func=fn)
+    w = e.add_parser("wait")
+    w.add_argument("experiment_id", type=int)
+    w.add_argument("--timeout", type=float, default=86400)
+    w.set_defaults(func=cmd_experiment_wait)
+    dm = e.add_parser("download-model-def")
+    dm.add_argument("experiment_id", type=int)
+    dm.add_argument("--output-dir", default=".")
+    dm.set_defaults(func=cmd_experiment_download_model_def)
+    lc = e.add_parser("list-checkpoints")
+    lc.add_argument("experiment_id", type=int)
+    lc.add_argument("--best", type=int)
+    lc.set_defaults(func=cmd_experiment_checkpoints)
+
+    t = sub.add_parser("trial", aliases=["t"]).add_subparsers(dest="sub")
+    d = t.add_parser("describe")
+    d.add_argument("trial_id", type=int)
+    d.add_argument("--json", action="store_true")
+    d.set_defaults(func=cmd_trial_describe)
+    lg = t.add_parser("logs")
+    lg.add_argument("trial_id", type=int)
+    lg.add_argument("--follow", "-f", action="store_true")
+    lg.set_defaults(func=cmd_trial_logs)
+    k = t.add_parser("kill")
+    k.add_argument("trial_id", type=int)
+    k.set_defaults(func=cmd_trial_kill)
+
+    ck = sub.add_parser("checkpoint", aliases=["c"]).add_subparsers(dest="sub")
+    d = ck.add_parser("describe")
+    d.add_argument("uuid")
+    d.set_defaults(func=cmd_checkpoint_describe)
+    dl = ck.add_parser("download")
+    dl.add_argument("uuid")
+    dl.add_argument("--output-dir", "-o", default=None)
+    dl.set_defaults(func=cmd_checkpoint_download)
+
+    ag = sub.add_parser("agent", aliases=["a"]).add_subparsers(dest="sub")
+    ag.add_parser("list").set_defaults(func=cmd_agent_list)
+    for name, en in (("enable", True), ("disable", False)):
+        x = ag.add_parser(name)
+        x.add_argument("agent_id")
+        x.set_defaults(func=_slot_toggle(en), slot_id=None)
+    sl = sub.add_parser("slot", aliases=["s"]).add_subparsers(dest="sub")
+    sl.add_parser("list").set_defaults(func=cmd_slot_list)
+    for name, en in (("enable", True), ("disable", False)):
+        x = sl.add_parser(name)
+        x.add_argument("agent_id")
+        x.add_argument("slot_id", type=int)
+        x.set_defaults(func=_slot_toggle(en))
+    rp = sub.add_parser("resource-pool", aliases=["rp"]).add_subparsers(dest="sub")
+    rp.add_parser("list").set_defaults(func=cmd_resource_pools)
+
+    tp = sub.add_parser("template", aliases=["tpl"]).add_subparsers(dest="sub")
+    tp.add_parser("list").set_defaults(func=cmd_template_list)
+    x = tp.add_parser("set")
+    x.add_argument("name")
+    x.add_argument("template_file")
+    x.set_defaults(func=cmd_template_set)
+    for name, fn in (("describe", cmd_template_describe), ("remove", cmd_template_remove)):
+        x = tp.add_parser(name)
+        x.add_argument("name")
+        x.set_defaults(func=fn)
+
+    md = sub.add_parser("model", aliases=["m"]).add_subparsers(dest="sub")
+    x = md.add_parser("create")
+    x.add_argument("name")
+    x.add_argument("--description")
+    x.set_defaults(func=cmd_model_create)
+    md.add_parser("list").set_defaults(func=cmd_model_list)
+    x = md.add_parser("describe")
+    x.add_argument("name")
+    x.set_defaults(func=cmd_model_describe)
+    x = md.add_parser("register-version")
+    x.add_argument("name")
+    x.add_argument("uuid")
+    x.set_defaults(func=cmd_model_register)
+
+    ps = sub.add_parser("preview-search")
+    ps.add_argument("config_file")
+    ps.add_argument("--master-side", action="store_true")
+    ps.set_defaults(func=cmd_preview_search)
+    sub.add_parser("version").set_defaults(func=cmd_version)
+    mc = sub.add_parser("master").add_subparsers(dest="sub")
+    mc.add_parser("config").set_defaults(func=cmd_master_config)
+
+    dp = sub.add_parser("deploy").add_subparsers(dest="sub")
+    lo = dp.add_parser("local")
+    lo.add_argument("--agents", type=int, default=1)
+    lo.add_argument("--artificial-slots", type=int, default=0)
+    lo.add_argument("--gpu", action="store_true")
+    lo.add_argument("--port", type=int, default=8080)
+    lo.add_argument("--store-dir")
+    lo.add_argument("--checkpoint-dir")
+    lo.add_argument("--scheduler", default="fair_share")
+    lo.set_defaults(func=cmd_deploy_local)
+    return p
+
+
+def main(argv: List[str] = None) -> None:
+    p = build_parser()
+    args = p.parse_args(argv)
+    if not getattr(args, "func", None):
+        p.print_help()
+        sys.exit(2)
+    args.func(args)

@@ -1,10 +1,30 @@
-"""Native API and local/test execution (``determined.experimental`` equivalent)."""
+"""Native API, local/test execution and the Python SDK (``determined.experimental`` equivalent)."""
 from determined_1_amd.experimental._local import (
     make_controller,
     make_local_env,
     make_test_workloads,
+    run_local_test,
     sample_hparams,
     test_one_batch,
 )
+from determined_1_amd.experimental.client import (
+    Checkpoint,
+    Determined,
+    ExperimentReference,
+    TrialReference,
+    load_checkpoint,
+)
 
-__all__ = ["make_controller", "make_local_env", "make_test_workloads", "sample_hparams", "test_one_batch"]
+__all__ = [
+    "Checkpoint",
+    "Determined",
+    "ExperimentReference",
+    "TrialReference",
+    "load_checkpoint",
+    "make_controller",
+    "make_local_env",
+    "make_test_workloads",
+    "run_local_test",
+    "sample_hparams",
+    "test_one_batch",
+]

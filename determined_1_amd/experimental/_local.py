@@ -153,6 +153,15 @@ def test_one_batch(trial_class: Type[trial.Trial], config: Optional[Dict[str, An
     return ctrl
 
 
+def run_local_test(config: Dict[str, Any], model_dir: str) -> trial.TrialController:
+    """``det experiment create --local --test``: load the trial from ``model_dir`` and run the
+    test-mode workload sequence in this process."""
+    from determined_1_amd.harness.load import load_trial_class
+
+    cls = load_trial_class(config["entrypoint"], model_dir)
+    return test_one_batch(cls, config)
+
+
 def dump_env(env: EnvContext) -> Dict[str, str]:
     """Inverse of ``EnvContext.from_environ`` (used by the agent/launcher to spawn ranks)."""
     return {

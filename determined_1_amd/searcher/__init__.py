@@ -110,6 +110,16 @@ def simulate(searcher_config: Dict[str, Any], hyperparameters: Optional[Dict[str
         json.dumps(validation or {"kind": "constant", "value": 1.0}).encode(), int(random_order), sim_seed))
 
 
+def simulate_config(experiment_config: Dict[str, Any], seed: int = 0) -> Dict[str, Any]:
+    """``det preview-search``: simulate the experiment's searcher with random validation metrics."""
+    from determined_1_amd.config import merge_with_defaults
+
+    cfg = merge_with_defaults(experiment_config)
+    return simulate(cfg["searcher"], cfg.get("hyperparameters", {}),
+                    seed or int(cfg.get("reproducibility", {}).get("experiment_seed", 0)),
+                    {"kind": "random"}, True, seed)
+
+
 def nprand(seed: int, op: str, n: int, arg: int = 0) -> List[Any]:
     return _take(_lib().detcore_nprand(seed & 0xFFFFFFFF, op.encode(), arg, n))
 
@@ -133,4 +143,4 @@ def short_form(ops: List[Dict[str, Any]]) -> str:
     return " ".join(parts)
 
 
-__all__ = ["Searcher", "SearcherError", "json_roundtrip", "nprand", "short_form", "simulate"]
+__all__ = ["Searcher", "SearcherError", "json_roundtrip", "nprand", "short_form", "simulate", "simulate_config"]

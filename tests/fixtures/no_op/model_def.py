@@ -60,8 +60,10 @@ class NoOpTrialController(trial.CallbackTrialController):
 
     def compute_validation_metrics(self, step_id: int) -> Dict[str, Any]:
         hp = self.context.get_hparams()
-        if hp.get("fail_on_first_validation") and not os.environ.get("DET_NOOP_FAILED_ONCE"):
-            os.environ["DET_NOOP_FAILED_ONCE"] = "1"
+        marker = pathlib.Path("/tmp", f"det-noop-failed-{self.env.det_cluster_id}-{self.env.det_experiment_id}-"
+                                      f"{self.env.det_trial_id}")
+        if hp.get("fail_on_first_validation") and not marker.exists():
+            marker.write_text("1")  # survives the process restart
             raise RuntimeError("failing on first validation")
         self._chaos("validate")
         return {"validation_metrics": {"validation_error": self.metric}, "num_inputs": int(hp.get("validation_set_size", 32))}

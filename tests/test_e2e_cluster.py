@@ -1,0 +1,189 @@
+"""End-to-end control-plane tests on CPU: det-master + det-agents (artificial slots) as real
+processes, experiments submitted over REST, trial processes launched by the agents (the
+reference's e2e_cpu strategy: ``e2e_tests/tests/test_system.py`` + the no-op fixture)."""
+import pathlib
+import subprocess
+import sys
+import time
+
+import pytest
+
+from determined_1_amd.api import MasterClient, read_context
+from determined_1_amd.deploy import LocalCluster
+
+FIXTURES = pathlib.Path(__file__).resolve().parent / "fixtures"
+NOOP = FIXTURES / "no_op"
+
+
+def noop_config(searcher, **extra):
+    cfg = {
+        "description": "noop",
+        "entrypoint": "model_def:NoOpTrial",
+        "hyperparameters": {"global_batch_size": 4, "metrics_base": 0.9},
+        "searcher": dict(searcher),
+        "scheduling_unit": 5,
+        "max_restarts": 2,
+    }
+    cfg["searcher"].setdefault("metric", "validation_error")
+    cfg.update(extra)
+    return cfg
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    d = tmp_path_factory.mktemp("cluster")
+    c = LocalCluster(agents=2, slots_per_agent=2, store_dir=str(d / "store"), checkpoint_dir=str(d / "ckpt"),
+                     log_dir=str(d), tick_ms=50)
+    c.up()
+    yield c
+    c.down()
+
+
+def submit(c, cfg, model_dir=NOOP, **kw):
+    cl = MasterClient(c.address)
+    return cl, cl.create_experiment(cfg, read_context(model_dir), **kw)["id"]
+
+
+def test_single_trial_completes_and_gc(cluster):
+    cl, eid = submit(cluster, noop_config({"name": "single", "max_length": {"batches": 20}},
+                                          min_validation_period={"batches": 5}))
+    assert cl.wait_for_experiment(eid, timeout=120) == "COMPLETED"
+    e = cl.experiment(eid)
+    assert len(e["trials"]) == 1
+    t = cl.get(f"/trials/{e['trials'][0]['id']}")
+    assert t["state"] == "COMPLETED"
+    assert [s["step_id"] for s in t["steps"]] == [1, 2, 3, 4]
+    assert all(s["state"] == "COMPLETED" for s in t["steps"])
+    assert len(t["validations"]) == 4
+    # checkpoint_policy=best with a decreasing metric checkpoints after every validation; GC keeps
+    # save_trial_best=1 / save_trial_latest=1 (both the last one here)
+    completed = [c for c in t["checkpoints"] if c["state"] == "COMPLETED"]
+    assert len(completed) == 1
+    assert pathlib.Path(cluster.checkpoint_dir, completed[0]["uuid"], "no_op_checkpoint").exists()
+    deleted = [c for c in t["checkpoints"] if c["state"] == "DELETED"]
+    time.sleep(1.0)
+    for c in deleted:
+        assert not pathlib.Path(cluster.checkpoint_dir, c["uuid"]).exists()
+    assert e["progress"] == pytest.approx(1.0)
+
+
+def test_adaptive_asha_runs_all_trials(cluster):
+    cfg = noop_config({"name": "adaptive_asha", "max_length": {"batches": 40}, "max_trials": 8, "divisor": 4,
+                       "max_rungs": 3, "mode": "aggressive"},
+                      hyperparameters={"global_batch_size": 4,
+                                       "metrics_base": {"type": "double", "minval": 0.5, "maxval": 0.9}})
+    cl, eid = submit(cluster, cfg)
+    assert cl.wait_for_experiment(eid, timeout=240) == "COMPLETED"
+    e = cl.experiment(eid)
+    assert len(e["trials"]) == 8
+    assert all(t["state"] == "COMPLETED" for t in e["trials"])
+    # promotions: some trials trained further than the first rung
+    batches = sorted(t["total_batches_processed"] for t in e["trials"])
+    assert batches[-1] > batches[0]
+
+
+def test_pause_activate_and_cancel(cluster):
+    cl, eid = submit(cluster, noop_config({"name": "single", "max_length": {"batches": 400}},
+                                          hyperparameters={"global_batch_size": 4, "sleep": 0.05}))
+    time.sleep(2.0)
+    cl.set_state(eid, "PAUSED")
+    time.sleep(2.0)
+    agents = cl.get("/agents")
+    assert all(not s["task"] for a in agents for s in a["slots"]), "paused experiment still holds slots"
+    cl.set_state(eid, "ACTIVE")
+    time.sleep(1.5)
+    cl.set_state(eid, "STOPPING_CANCELED")
+    assert cl.wait_for_experiment(eid, timeout=120) == "CANCELED"
+
+
+def test_restart_after_failure(cluster):
+    cfg = noop_config({"name": "single", "max_length": {"batches": 10}},
+                      hyperparameters={"global_batch_size": 4, "fail_on_first_validation": True},
+                      min_validation_period={"batches": 5})
+    cl, eid = submit(cluster, cfg)
+    assert cl.wait_for_experiment(eid, timeout=120) == "COMPLETED"
+    t = cl.experiment(eid)["trials"][0]
+    assert t["restarts"] >= 1
+
+
+def test_max_restarts_exceeded_errors(cluster):
+    cfg = noop_config({"name": "single", "max_length": {"batches": 10}},
+                      hyperparameters={"global_batch_size": 4, "chaos_probability_train": 1.0}, max_restarts=1)
+    cl, eid = submit(cluster, cfg)
+    assert cl.wait_for_experiment(eid, timeout=120) == "ERROR"
+    t = cl.experiment(eid)["trials"][0]
+    assert t["state"] == "ERROR" and t["restarts"] == 2
+
+
+def test_invalid_hp_closes_trial(cluster):
+    cfg = noop_config({"name": "random", "max_length": {"batches": 10}, "max_trials": 2},
+                      hyperparameters={"global_batch_size": 4, "invalid_hp": True})
+    cl, eid = submit(cluster, cfg)
+    st = cl.wait_for_experiment(eid, timeout=120)
+    assert st in ("COMPLETED", "ERROR")
+    assert all(t["state"] != "ACTIVE" for t in cl.experiment(eid)["trials"])
+
+
+def test_distributed_gloo_trial_through_launcher(cluster):
+    cfg = {
+        "entrypoint": "model_def:OneVarTrial",
+        "hyperparameters": {"global_batch_size": 4, "lr": 0.01},
+        "searcher": {"name": "single", "metric": "val_loss", "max_length": {"batches": 6}},
+        "scheduling_unit": 3,
+        "resources": {"slots_per_trial": 2},
+        "max_restarts": 0,
+    }
+    cl, eid = submit(cluster, cfg, model_dir=FIXTURES / "onevar_dist")
+    st = cl.wait_for_experiment(eid, timeout=240)
+    t = cl.experiment(eid)["trials"][0]
+    logs = "\n".join(l["message"] for l in cl.trial_logs(t["id"]))
+    assert st == "COMPLETED", logs[-3000:]
+    tr = cl.get(f"/trials/{t['id']}")
+    w = tr["steps"][-1]["metrics"]["batch_metrics"][-1]["weight"]
+    # 6 SGD steps of w' = w + 2 lr (1 - w) from w=0 (identical on both ranks; averaged grads)
+    w_exp = 0.0
+    for _ in range(6):
+        w_exp = w_exp + 2 * 0.01 * (1 - w_exp)
+    assert w == pytest.approx(w_exp, rel=1e-5)
+
+
+def test_cli_test_mode_and_listing(cluster):
+    cfg_path = pathlib.Path(cluster.tmp, "noop.yaml")
+    import yaml
+
+    cfg_path.write_text(yaml.safe_dump(noop_config({"name": "single", "max_length": {"batches": 10}})))
+    env = {"DET_MASTER": cluster.address, "PYTHONPATH": str(pathlib.Path(__file__).resolve().parent.parent)}
+    import os
+
+    env = {**os.environ, **env}
+    r = subprocess.run([sys.executable, "-m", "determined_1_amd.cli", "experiment", "create", "--test", str(cfg_path),
+                        str(NOOP)], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Model definition test succeeded" in r.stdout
+    r = subprocess.run([sys.executable, "-m", "determined_1_amd.cli", "agent", "list"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert "agent-0" in r.stdout and "agent-1" in r.stdout
+
+
+def test_master_restart_resumes_experiment(tmp_path):
+    c = LocalCluster(agents=1, slots_per_agent=1, store_dir=str(tmp_path / "store"),
+                     checkpoint_dir=str(tmp_path / "ckpt"), log_dir=str(tmp_path), tick_ms=50)
+    c.up()
+    try:
+        cl, eid = submit(c, noop_config({"name": "single", "max_length": {"batches": 60}},
+                                        hyperparameters={"global_batch_size": 4, "sleep": 0.1},
+                                        min_validation_period={"batches": 10}))
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            e = cl.experiment(eid)
+            if e["trials"] and any(ck["state"] == "COMPLETED" for ck in cl.get(f"/trials/{e['trials'][0]['id']}")["checkpoints"]):
+                break
+            time.sleep(0.2)
+        c.restart_master()
+        cl = MasterClient(c.address)
+        assert cl.wait_for_experiment(eid, timeout=180) == "COMPLETED"
+        t = cl.get(f"/trials/{cl.experiment(eid)['trials'][0]['id']}")
+        done = [s for s in t["steps"] if s["state"] == "COMPLETED"]
+        assert sum(s["num_batches"] for s in done) == 60
+    finally:
+        c.down()
