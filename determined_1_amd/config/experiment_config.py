@@ -38,6 +38,8 @@ _SEARCHER_DEFAULTS = {
 }
 
 _LENGTH_FIELDS = ("max_length", "budget", "length_per_round")
+# replaced wholesale on merge: free-form dicts and Length unions ({"batches": n} vs {"epochs": n})
+_ATOMIC_KEYS = ("hyperparameters", "data", "min_validation_period", "min_checkpoint_period") + _LENGTH_FIELDS
 
 
 def default_experiment_config(experiment_seed: Optional[int] = None) -> Dict[str, Any]:
@@ -85,7 +87,7 @@ def default_experiment_config(experiment_seed: Optional[int] = None) -> Dict[str
 def _deep_merge(base: Dict[str, Any], over: Dict[str, Any]) -> Dict[str, Any]:
     out = copy.deepcopy(base)
     for k, v in over.items():
-        if isinstance(v, dict) and isinstance(out.get(k), dict) and k not in ("hyperparameters", "data"):
+        if isinstance(v, dict) and isinstance(out.get(k), dict) and k not in _ATOMIC_KEYS:
             # tagged unions: a different "type"/"name" replaces the arm wholesale
             tag = "type" if "type" in v or "type" in out[k] else ("name" if "name" in v else None)
             if tag and tag in v and out[k].get(tag) not in (None, v[tag]):

@@ -72,3 +72,55 @@ class SyntheticTokens(tud.Dataset):
     def __getitem__(self, i: int) -> List[torch.Tensor]:
         j = i % self.pool
         return [self.input_ids[j], self.attention_mask[j], self.token_type_ids[j], self.start[j], self.end[j]]
+
+
+class SyntheticClassification(tud.Dataset):
+    """Learnable synthetic classification data: each class has a fixed random template and a
+    sample is ``template[label] + noise``, so accuracy rises with training (stands in for MNIST /
+    CIFAR-10, which cannot be downloaded here)."""
+
+    def __init__(self, length: int, shape: Sequence[int], num_classes: int = 10, noise: float = 1.0,
+                 seed: int = 0, template_seed: int = 1234) -> None:
+        self.length = int(length)
+        self.shape = tuple(shape)
+        self.num_classes = num_classes
+        self.noise = noise
+        self.seed = seed
+        gt = torch.Generator().manual_seed(template_seed)
+        self.templates = torch.randn((num_classes,) + self.shape, generator=gt)
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        y = int(torch.randint(0, self.num_classes, (1,), generator=g))
+        x = self.templates[y] + self.noise * torch.randn(self.shape, generator=g)
+        return x, torch.tensor(y, dtype=torch.int64)
+
+
+class SyntheticSQuAD(tud.Dataset):
+    """SQuAD-shaped extractive-QA features (input_ids, token_type_ids, attention_mask,
+    start/end positions) for BERT throughput runs; random tokens, answer span inside the context."""
+
+    def __init__(self, length: int, seq_len: int = 384, vocab_size: int = 30522, seed: int = 0) -> None:
+        self.length = int(length)
+        self.seq_len = seq_len
+        self.vocab = vocab_size
+        self.seed = seed
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int) -> Tuple[torch.Tensor, ...]:
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        L = self.seq_len
+        q = 64
+        ids = torch.randint(1000, self.vocab, (L,), generator=g)
+        ids[0], ids[q - 1], ids[L - 1] = 101, 102, 102
+        tt = torch.zeros(L, dtype=torch.int64)
+        tt[q:] = 1
+        am = torch.ones(L, dtype=torch.int64)
+        s = int(torch.randint(q, L - 31, (1,), generator=g))
+        e = s + int(torch.randint(0, 30, (1,), generator=g))
+        return ids, tt, am, torch.tensor(s), torch.tensor(e)

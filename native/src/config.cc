@@ -54,7 +54,10 @@ Json DeepMerge(const Json& base, const Json& over) {
   for (auto& kv : over.as_object()) {
     const std::string& k = kv.first;
     const Json& v = kv.second;
-    if (v.is_object() && out[k].is_object() && k != "hyperparameters" && k != "data") {
+    static const std::set<std::string> kAtomic = {"hyperparameters", "data", "min_validation_period",
+                                                  "min_checkpoint_period", "max_length", "budget",
+                                                  "length_per_round"};
+    if (v.is_object() && out[k].is_object() && !kAtomic.count(k)) {
       const char* tag = nullptr;
       if (v.has("type") || out[k].has("type")) tag = "type";
       else if (v.has("name")) tag = "name";

@@ -1,0 +1,40 @@
+"""Every official example's configs validate and its trial passes local test mode on CPU
+(reference ``examples/tests/test_official.py``).  Heavy models are shrunk through hparam
+overrides so the test stays CPU-sized."""
+import pathlib
+
+import pytest
+import yaml
+
+from determined_1_amd.config import merge_with_defaults, validate_experiment_config
+from determined_1_amd.experimental import run_local_test
+
+EX = pathlib.Path(__file__).resolve().parent.parent / "examples"
+CONFIGS = sorted(EX.rglob("*.yaml"))
+SHRINK = {
+    "resnet50_pytorch": {"arch": "resnet18", "image_size": 32, "num_classes": 10, "global_batch_size": 2,
+                         "train_records": 16, "validation_records": 4, "amp": "O0", "channels_last": False},
+    "bert_squad_pytorch": {"num_hidden_layers": 1, "hidden_size": 64, "num_attention_heads": 2,
+                           "intermediate_size": 128, "max_seq_length": 128, "global_batch_size": 2,
+                           "train_records": 8, "validation_records": 4, "amp": "O0"},
+    "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
+    "mnist_pytorch": {"global_batch_size": 4},
+    "gan_mnist_pytorch": {"global_batch_size": 4},
+}
+
+
+@pytest.mark.parametrize("cfg_path", CONFIGS, ids=lambda p: f"{p.parent.name}/{p.name}")
+def test_example_config_validates(cfg_path):
+    cfg = yaml.safe_load(cfg_path.read_text())
+    assert validate_experiment_config(merge_with_defaults(cfg)) == []
+
+
+@pytest.mark.parametrize("example", sorted({p.parent for p in CONFIGS}), ids=lambda p: p.name)
+def test_example_local_test_mode(example):
+    cfg = yaml.safe_load(example.joinpath("const.yaml").read_text())
+    hp = {}
+    for k, v in cfg["hyperparameters"].items():
+        hp[k] = v["val"] if isinstance(v, dict) and v.get("type") == "const" else v
+    hp.update(SHRINK.get(example.name, {}))
+    cfg["hyperparameters"] = hp
+    run_local_test(cfg, str(example))
