@@ -7,6 +7,7 @@ from determined_1_amd.experimental._local import (
     sample_hparams,
     test_one_batch,
 )
+from determined_1_amd.experimental.native import create
 from determined_1_amd.experimental.client import (
     Checkpoint,
     Determined,
@@ -18,6 +19,7 @@ from determined_1_amd.experimental.client import (
 __all__ = [
     "Checkpoint",
     "Determined",
+    "create",
     "ExperimentReference",
     "TrialReference",
     "load_checkpoint",

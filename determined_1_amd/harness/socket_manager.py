@@ -37,6 +37,9 @@ class SocketManager(workload.Source):
         if self.ws is None:
             raise RuntimeError(f"cannot connect to master at {env.master_addr}:{env.master_port}: {last}")
         self.current = None  # type: Optional[workload.Workload]
+        from determined_1_amd.harness.profiler import HarnessProfiler
+
+        self.profiler = HarnessProfiler() if HarnessProfiler.enabled() else None
         self.rendezvous_info = self._wait_for_rendezvous()
 
     def _wait_for_rendezvous(self) -> RendezvousInfo:
@@ -54,6 +57,8 @@ class SocketManager(workload.Source):
         """``respond({"metrics": ..., "exited_reason"?: ...})`` -> WORKLOAD_COMPLETED."""
 
         def respond(resp: workload.Response) -> None:
+            if self.profiler is not None:
+                self.profiler.stop()
             if isinstance(resp, workload.Skipped) or w.kind == workload.Workload.Kind.TERMINATE:
                 return
             msg: Dict[str, Any] = {
@@ -74,8 +79,14 @@ class SocketManager(workload.Source):
         if self.current is not None:
             self._responder(self.current, _now())(resp)
 
+    def _profiled(self, w: workload.Workload):
+        """Run the harness profiler around one workload (reference _socket_manager.py:179-207)."""
+        if self.profiler is not None:
+            self.profiler.start(f"step-{w.step_id}-{w.kind.name}")
+        return w
+
     def __iter__(self) -> workload.Stream:
-        w = self.env.initial_workload
+        w = self._profiled(self.env.initial_workload)
         self.current = w
         yield w, [], self._responder(w, _now())
         while True:
@@ -87,7 +98,7 @@ class SocketManager(workload.Source):
             if m.get("type") != "RUN_WORKLOAD":
                 logging.warning("unexpected message from master: %s", m.get("type"))
                 continue
-            w = workload.Workload.from_json(m["workload"])
+            w = self._profiled(workload.Workload.from_json(m["workload"]))
             self.current = w
             yield w, [], self._responder(w, _now())
             if w.kind == workload.Workload.Kind.TERMINATE:

@@ -596,6 +596,19 @@ void TrialActor::OnAllocated(Context& ctx, const ResourcesAllocated& ra) {
     env["DET_NUM_CONTAINERS"] = std::to_string(order_.size());
     env["DET_CONTAINER_RANK"] = std::to_string(c.rank);
     env["DET_TOTAL_SLOTS"] = std::to_string(total);
+    // user environment (environment.environment_variables: ["K=V"] or {cpu: [...], gpu: [...]})
+    const Json& ev = config_["environment"]["environment_variables"];
+    auto add_env = [&](const Json& list) {
+      if (!list.is_array()) return;
+      for (auto& kv : list.as_array()) {
+        if (!kv.is_string()) continue;
+        const std::string& s = kv.as_string();
+        auto eq = s.find('=');
+        if (eq != std::string::npos) env[s.substr(0, eq)] = s.substr(eq + 1);
+      }
+    };
+    if (ev.is_array()) add_env(ev);
+    else if (ev.is_object()) add_env(ev[c.devices.empty() ? "cpu" : "gpu"]);
     Json files = Json::array();
     const Json& latest = seq_->LatestCheckpoint();
     if (!latest.is_null() && latest.is_object() && latest.has("uuid")) {

@@ -160,3 +160,20 @@ def test_invalid_checkpoint(tmp_path: pathlib.Path):
 
     with pytest.raises(errors.CheckpointNotFoundException):
         run(xor.XORTrial, {"global_batch_size": 4}, Recorder(), load_path=tmp_path / "missing", total_batches=1)
+
+
+def test_native_api_local_training(tmp_path):
+    """det.experimental.create(local=True): full single-trial schedule in-process, analytic weight."""
+    from determined_1_amd.experimental import create
+    from tests.fixtures.onevar import OneVarTrial
+
+    cfg = {"hyperparameters": {"global_batch_size": 4, "lr": 0.01},
+           "searcher": {"name": "single", "metric": "val_loss", "max_length": {"batches": 5}},
+           "scheduling_unit": 2, "min_validation_period": {"batches": 4}}
+    ctrl = create(OneVarTrial, cfg, local=True, checkpoint_dir=str(tmp_path))
+    w = ctrl.context.models[0].weight.item()
+    exp = 0.0
+    for _ in range(5):
+        exp = exp + 2 * 0.01 * (1 - exp)
+    assert abs(w - exp) < 1e-6
+    assert len(list(tmp_path.iterdir())) == 1
