@@ -279,6 +279,54 @@ def cmd_model_register(args: argparse.Namespace) -> None:
     print(json.dumps(MasterClient(args.master).post(f"/models/{args.name}/versions", {"checkpoint_uuid": args.uuid})))
 
 
+# ----------------------------------------------------------------------------- commands
+def cmd_command_run(args: argparse.Namespace) -> None:
+    cfg = {"entrypoint": args.entrypoint, "resources": {"slots": args.slots},
+           "description": args.description or " ".join(args.entrypoint)}
+    if args.config_file:
+        cfg.update(_load_config(args.config_file))
+    ctx = read_context(pathlib.Path(args.context)) if args.context else []
+    client = MasterClient(args.master)
+    cid = client.post("/commands", {"config": cfg, "context": ctx})["id"]
+    print(f"Launched command {cid}")
+    if args.detach:
+        return
+    off = 0
+    while True:
+        for l in client.get(f"/commands/{cid}/logs", offset=off):
+            print(l["message"])
+            off = l["id"]
+        c = client.get(f"/commands/{cid}")
+        if c["state"] == "TERMINATED":
+            for l in client.get(f"/commands/{cid}/logs", offset=off):
+                print(l["message"])
+            if c.get("exit_code", 0) != 0:
+                sys.exit(c.get("exit_code", 1))
+            return
+        time.sleep(0.5)
+
+
+def cmd_command_list(args: argparse.Namespace) -> None:
+    print(_table(MasterClient(args.master).get("/commands"), ["id", "state", "description", "agent", "exit_code"]))
+
+
+def cmd_command_logs(args: argparse.Namespace) -> None:
+    for l in MasterClient(args.master).get(f"/commands/{args.command_id}/logs"):
+        print(l["message"])
+
+
+def cmd_command_kill(args: argparse.Namespace) -> None:
+    MasterClient(args.master).post(f"/commands/{args.command_id}/kill")
+
+
+def cmd_unavailable(what: str):
+    def f(args: argparse.Namespace) -> None:
+        sys.exit(f"{what} needs packages that are not installed on this image (jupyter / sshd / tensorboard); "
+                 "use `det cmd run` for arbitrary processes")
+
+    return f
+
+
 # ---------------------------------------------------------------------------- misc
 def cmd_preview_search(args: argparse.Namespace) -> None:
     cfg = _load_config(args.config_file)
@@ -429,6 +477,23 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("name")
     x.add_argument("uuid")
     x.set_defaults(func=cmd_model_register)
+
+    cm = sub.add_parser("command", aliases=["cmd"]).add_subparsers(dest="sub")
+    x = cm.add_parser("run")
+    x.add_argument("entrypoint", nargs="+")
+    x.add_argument("--slots", type=int, default=0)
+    x.add_argument("--config-file")
+    x.add_argument("--context")
+    x.add_argument("--description")
+    x.add_argument("--detach", "-d", action="store_true")
+    x.set_defaults(func=cmd_command_run)
+    cm.add_parser("list").set_defaults(func=cmd_command_list)
+    for name, fn in (("logs", cmd_command_logs), ("kill", cmd_command_kill)):
+        x = cm.add_parser(name)
+        x.add_argument("command_id", type=int)
+        x.set_defaults(func=fn)
+    for name in ("notebook", "shell", "tensorboard"):
+        sub.add_parser(name).set_defaults(func=cmd_unavailable(name))
 
     ps = sub.add_parser("preview-search")
     ps.add_argument("config_file")

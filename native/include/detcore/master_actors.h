@@ -172,6 +172,26 @@ class ExperimentActor : public actor::Actor {
   std::map<std::string, Json> latest_ckpt_;  // request id -> latest checkpoint metadata (PBT)
 };
 
+// Generic command task (reference master/internal/command/command.go): run an argv
+// on an agent with N slots (0 = CPU-only, non-preemptible), stream its logs, report exit status.
+struct CommandKill {};
+class CommandActor : public actor::Actor {
+ public:
+  CommandActor(Master* m, int64_t id, Json config);
+  void Receive(actor::Context& ctx) override;
+
+ private:
+  void Save(const std::string& state, int exit_code = 0);
+  Master* m_;
+  int64_t id_;
+  Json config_;
+  std::string pool_;
+  std::string task_id_;
+  std::string container_;
+  std::string agent_;
+  bool killed_ = false;
+};
+
 struct TrialSpec {
   Op create;
   Json warm_start;

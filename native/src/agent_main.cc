@@ -242,9 +242,10 @@ class Agent {
     State(cid, "Starting");
     std::string dir = o_.work_dir + "/" + cid;
     MkdirP(dir);
-    // model definition from the master
+    // model definition (trials) or command context from the master
     int64_t exp_id = spec.get_int("experiment_id", 0);
-    auto r = net::HttpCall(o_.master_host, o_.master_port, "GET", "/experiments/" + std::to_string(exp_id) + "/model_def");
+    std::string ctx_url = spec.get_string("context_url", "/experiments/" + std::to_string(exp_id) + "/model_def");
+    auto r = net::HttpCall(o_.master_host, o_.master_port, "GET", ctx_url);
     if (r.status != 200) {
       State(cid, "Terminated", 1, "cannot fetch model definition: " + r.error + " " + r.body.substr(0, 200));
       return;
@@ -316,6 +317,10 @@ class Agent {
     for (auto& s : envs) envp.push_back(const_cast<char*>(s.c_str()));
     envp.push_back(nullptr);
     std::vector<std::string> args = {o_.python, "-m", "determined_1_amd.exec.harness"};
+    if (spec["cmd"].is_array() && spec["cmd"].size() > 0) {
+      args.clear();
+      for (auto& a : spec["cmd"].as_array()) args.push_back(a.as_string());
+    }
     std::vector<char*> argv;
     for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
     argv.push_back(nullptr);
@@ -360,8 +365,9 @@ class Agent {
     Send(running);
     int64_t trial_id = spec.get_int("trial_id", 0);
     int rank = static_cast<int>(spec.get_int("rank", 0));
-    std::thread t_out([=] { Pump(out_pipe[0], cid, trial_id, rank, "stdout", dir + "/stdout.log"); });
-    std::thread t_err([=] { Pump(err_pipe[0], cid, trial_id, rank, "stderr", dir + "/stderr.log"); });
+    std::string task_id = spec.get_string("task_id", "");
+    std::thread t_out([=] { Pump(out_pipe[0], cid, trial_id, rank, "stdout", dir + "/stdout.log", task_id); });
+    std::thread t_err([=] { Pump(err_pipe[0], cid, trial_id, rank, "stderr", dir + "/stderr.log", task_id); });
     int status = 0;
     waitpid(pid, &status, 0);
     t_out.join();
@@ -375,7 +381,7 @@ class Agent {
   }
 
   void Pump(int fd, const std::string& cid, int64_t trial_id, int rank, const std::string& stdtype,
-            const std::string& logfile) {
+            const std::string& logfile, const std::string& task_id) {
     FILE* in = fdopen(fd, "r");
     std::ofstream lf(logfile, std::ios::app);
     char* line = nullptr;
@@ -390,6 +396,7 @@ class Agent {
       m["type"] = "ContainerLog";
       m["container_id"] = cid;
       m["trial_id"] = trial_id;
+      if (!task_id.empty()) m["task_id"] = task_id;
       m["rank"] = rank;
       m["stdtype"] = stdtype;
       m["log"] = s;

@@ -617,6 +617,56 @@ void Master::InstallRoutes() {
     return J(200, out);
   });
 
+  // ------------------------------------------------------------------------- commands
+  http_.Route("POST", "/commands", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    Json cfg = body["config"];
+    if (!cfg["entrypoint"].is_array() || cfg["entrypoint"].size() == 0)
+      throw std::invalid_argument("command config needs entrypoint: [argv...]");
+    Json row = Json::object();
+    row["config"] = cfg;
+    row["state"] = "PENDING";
+    row["start_time"] = NowRFC3339();
+    row["description"] = cfg.get_string("description", "");
+    int64_t id = store_->Insert("commands", row);
+    Json ctxrow = Json::object();
+    ctxrow["files"] = body["context"].is_array() ? body["context"] : Json::array();
+    store_->Put("command_contexts", id, ctxrow);
+    sys_->ActorOf("commands/" + std::to_string(id), std::make_unique<CommandActor>(this, id, cfg));
+    Json out = Json::object();
+    out["id"] = id;
+    return J(201, out);
+  });
+  http_.Route("GET", "/commands", [this](const net::Request&) {
+    Json out = Json::array();
+    for (auto& c : store_->Scan("commands")) out.push_back(c);
+    return J(200, out);
+  });
+  http_.Route("GET", "/commands/:id", [this](const net::Request& r) {
+    Json c;
+    if (!store_->Get("commands", IntParam(r, "id"), &c)) return Err(404, "command not found");
+    return J(200, c);
+  });
+  http_.Route("GET", "/commands/:id/context", [this](const net::Request& r) {
+    Json c;
+    if (!store_->Get("command_contexts", IntParam(r, "id"), &c)) return Err(404, "not found");
+    return J(200, c);
+  });
+  http_.Route("GET", "/commands/:id/logs", [this](const net::Request& r) {
+    std::string task = "cmd-" + r.Param("id");
+    int64_t offset = std::stoll(r.Query("offset", "0"));
+    Json out = Json::array();
+    for (auto& l : store_->Where("task_logs", "task_id", Json(task)))
+      if (l["id"].as_int() > offset) out.push_back(l);
+    return J(200, out);
+  });
+  http_.Route("POST", "/commands/:id/kill", [this](const net::Request& r) {
+    Ref c = sys_->Get("/commands/" + r.Param("id"));
+    if (!c) return Err(409, "command is not running");
+    c->Tell(CommandKill{});
+    return J(200, Json::object());
+  });
+
   // --------------------------------------------------------------- searcher preview
   http_.Route("POST", "/searcher/preview", [this](const net::Request& r) {
     Json body = Json::parse(r.body);
@@ -762,6 +812,13 @@ void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
       if (tr)
         tr->Tell(ContainerStateMsg{cid, m.get_string("state", ""), static_cast<int>(m.get_int("exit_code", 0)),
                                    m.get_string("failure", ""), m.get_string("address", "")});
+    } else if (t == "ContainerLog" && !m.get_string("task_id", "").empty()) {
+      Json row = Json::object();
+      row["task_id"] = m["task_id"];
+      row["message"] = m["log"];
+      row["stdtype"] = m["stdtype"];
+      row["timestamp"] = NowRFC3339();
+      store_->Insert("task_logs", row);
     } else if (t == "ContainerLog") {
       AppendTrialLog(m.get_int("trial_id", 0), m.get_string("log", ""), m.get_string("stdtype", "stdout"),
                      m.get_string("container_id", ""), static_cast<int>(m.get_int("rank", 0)));

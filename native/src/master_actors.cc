@@ -972,5 +972,95 @@ void TrialActor::SaveWorkloadEnd(const CompletedMessage& cm) {
   }
 }
 
+// =================================================================================== command
+CommandActor::CommandActor(Master* m, int64_t id, Json config) : m_(m), id_(id), config_(std::move(config)) {
+  pool_ = config_["resources"].get_string("resource_pool", "");
+  if (pool_.empty()) pool_ = m_->config().resource_pools.empty() ? "default" : m_->config().resource_pools[0];
+}
+
+void CommandActor::Save(const std::string& state, int exit_code) {
+  Json patch = Json::object();
+  patch["state"] = state;
+  if (state == "TERMINATED") {
+    patch["exit_code"] = exit_code;
+    patch["end_time"] = NowRFC3339();
+  }
+  if (!agent_.empty()) patch["agent"] = agent_;
+  m_->store().Update("commands", id_, patch);
+}
+
+void CommandActor::Receive(Context& ctx) {
+  if (ctx.Is<actor::PreStart>()) {
+    task_id_ = "cmd-" + std::to_string(id_);
+    AllocateRequest req;
+    req.task_id = task_id_;
+    req.group = task_id_;
+    req.slots = static_cast<int>(config_["resources"].get_int("slots", 0));
+    req.label = config_["resources"].get_string("agent_label", "");
+    req.non_preemptible = true;  // commands are not checkpointable
+    req.handler = ctx.Self();
+    req.name = "Command " + std::to_string(id_);
+    m_->Pool(pool_)->Tell(req);
+    Save("PENDING");
+  } else if (auto ra = ctx.As<ResourcesAllocated>()) {
+    if (ra->task_id != task_id_ || !container_.empty() || killed_) return;
+    const sched::Fit& f = ra->fits.front();
+    container_ = NewUUID();
+    agent_ = f.agent;
+    m_->BindContainer(container_, f.agent, ctx.Self());
+    Json env = Json::object();
+    env["DET_TASK_ID"] = task_id_;
+    env["DET_MASTER"] = m_->master_host() + ":" + std::to_string(m_->port());
+    const Json& ev = config_["environment"]["environment_variables"];
+    if (ev.is_array())
+      for (auto& kv : ev.as_array()) {
+        const std::string& str = kv.as_string();
+        auto eq = str.find('=');
+        if (eq != std::string::npos) env[str.substr(0, eq)] = str.substr(eq + 1);
+      }
+    Json spec = Json::object();
+    spec["env"] = env;
+    spec["files"] = Json::array();
+    spec["cmd"] = config_["entrypoint"];
+    spec["task_id"] = task_id_;
+    spec["context_url"] = "/commands/" + std::to_string(id_) + "/context";
+    Json dev = Json::array();
+    for (int d : f.devices) dev.push_back(d);
+    Json msg = Json::object();
+    msg["type"] = "StartContainer";
+    msg["container_id"] = container_;
+    msg["devices"] = dev;
+    msg["spec"] = spec;
+    if (!m_->SendToAgent(f.agent, msg)) {
+      Save("TERMINATED", -1);
+      ctx.Self()->Stop();
+      return;
+    }
+    Save("ASSIGNED");
+  } else if (auto cs = ctx.As<ContainerStateMsg>()) {
+    if (cs->container_id != container_) return;
+    if (cs->state == "Running") Save("RUNNING");
+    if (cs->state == "Terminated") {
+      Save("TERMINATED", cs->exit_code);
+      ctx.Self()->Stop();
+    }
+  } else if (ctx.Is<ReleaseResources>() || ctx.Is<CommandKill>()) {
+    killed_ = true;
+    if (container_.empty()) {
+      Save("TERMINATED", -1);
+      ctx.Self()->Stop();
+    } else {
+      Json msg = Json::object();
+      msg["type"] = "SignalContainer";
+      msg["container_id"] = container_;
+      msg["signal"] = "SIGKILL";
+      m_->SendToAgent(agent_, msg);
+    }
+  } else if (ctx.Is<actor::PostStop>()) {
+    m_->Pool(pool_)->Tell(ResourcesReleased{task_id_});
+    if (!container_.empty()) m_->UnbindContainer(container_);
+  }
+}
+
 }  // namespace master
 }  // namespace detcore

@@ -61,7 +61,10 @@ def test_single_trial_completes_and_gc(cluster):
     assert len(completed) == 1
     assert pathlib.Path(cluster.checkpoint_dir, completed[0]["uuid"], "no_op_checkpoint").exists()
     deleted = [c for c in t["checkpoints"] if c["state"] == "DELETED"]
-    time.sleep(1.0)
+    assert len(deleted) == 3
+    deadline = time.time() + 30  # the GC job is an asynchronous child process of the master
+    while time.time() < deadline and any(pathlib.Path(cluster.checkpoint_dir, c["uuid"]).exists() for c in deleted):
+        time.sleep(0.2)
     for c in deleted:
         assert not pathlib.Path(cluster.checkpoint_dir, c["uuid"]).exists()
     assert e["progress"] == pytest.approx(1.0)
@@ -163,6 +166,19 @@ def test_cli_test_mode_and_listing(cluster):
     r = subprocess.run([sys.executable, "-m", "determined_1_amd.cli", "agent", "list"], env=env,
                        capture_output=True, text=True, timeout=60)
     assert "agent-0" in r.stdout and "agent-1" in r.stdout
+
+
+def test_command_runs_on_agent(cluster):
+    cl = MasterClient(cluster.address)
+    cid = cl.post("/commands", {"config": {"entrypoint": [sys.executable, "-c", "print('hello from command')"],
+                                           "resources": {"slots": 1}}})["id"]
+    deadline = time.time() + 60
+    while time.time() < deadline and cl.get(f"/commands/{cid}")["state"] != "TERMINATED":
+        time.sleep(0.2)
+    c = cl.get(f"/commands/{cid}")
+    assert c["state"] == "TERMINATED" and c["exit_code"] == 0
+    time.sleep(0.3)
+    assert any("hello from command" in l["message"] for l in cl.get(f"/commands/{cid}/logs"))
 
 
 def test_master_restart_resumes_experiment(tmp_path):
