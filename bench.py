@@ -39,7 +39,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--bucket-mb", type=int, default=int(os.environ.get("DET_BENCH_BUCKET_MB", "64")))
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true", help="stock MIOpen BN + separate add/ReLU (A/B)")
-    ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "0")))
+    ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
+                    help="MIOpen find mode for the conv algorithms (tuned during the untimed warmup)")
     return ap.parse_args()
 
 

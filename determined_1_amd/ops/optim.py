@@ -113,6 +113,7 @@ class FusedOptimizer:
         self.grad_scale = 1.0
         self.grad_scale_dev = None  # type: Optional[torch.Tensor]
         self.found_inf = None  # type: Optional[torch.Tensor]
+        self.sink = None  # type: Optional[Any]  # ops.arena.GradSink, attached by the trial context
         self._orig_step = optimizer.step
         self._orig_zero_grad = optimizer.zero_grad
         self._orig_load_state_dict = optimizer.load_state_dict
@@ -135,11 +136,16 @@ class FusedOptimizer:
     def arenas(self) -> List[Arena]:
         return [a for g in self.groups for a in g.arenas]
 
-    def zero_grad(self, set_to_none: bool = True) -> None:  # noqa: ARG002 (arena grads are never None)
+    def zero_grad(self, set_to_none: bool = True) -> None:  # noqa: ARG002
+        if self.sink is not None:
+            self.sink.start_window()  # grads -> None; the next backward lands them in one copy
+            return
         for a in self.arenas:
             a.zero_grad()
 
     def ensure_grads(self) -> None:
+        if self.sink is not None and self.sink.fresh:
+            return
         for a in self.arenas:
             a.ensure_grads()
 

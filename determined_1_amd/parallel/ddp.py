@@ -98,11 +98,24 @@ class GradientBucketer:
         self._comm = False
         self._launched_any = False
         self._handles = []
+        self._sink = None  # type: Any
         for a in self.arenas:
             for p in a.params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
         logging.debug("gradient bucketer: %d buckets (%s MB cap), compression=%s", len(self.buckets), cap_mb,
                       compression)
+
+    def attach_sink(self, sink: Any) -> None:
+        """Gradients land through ``ops.arena.GradSink`` (one batched copy per bucket): on fresh
+        passes the sink announces complete buckets instead of the per-parameter hooks."""
+        self._sink = sink
+        sink.listeners.append(self._group_ready)
+
+    def _group_ready(self, bi: int) -> None:
+        if not self._comm:
+            return
+        self._ready[bi] = True
+        self._launch_in_order()
 
     def remove(self) -> None:
         for h in self._handles:
@@ -121,7 +134,7 @@ class GradientBucketer:
             self._next = 0
 
     def _hook(self, p: torch.Tensor) -> None:
-        if not self._comm:
+        if not self._comm or (self._sink is not None and self._sink.fresh):
             return
         bi = self._bucket_of.get(id(p))
         if bi is None:
