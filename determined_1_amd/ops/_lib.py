@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -85,15 +85,15 @@ _SIGNATURES = {
     # det_norm.hip: fused BatchNorm(+add)(+ReLU), channels_last
     "det_bn_ws_elems": ([c_i64, c_int], c_i64),
     # stream, dtype, x, res, y, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
-    # relu, save_mean, save_rstd, scale, shift, ws
+    # relu, save_mean, save_rstd, scale, shift, ws, mask_bits
     "det_bn_fwd_train": (
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int] + [c_void_p] * 5
-        + [c_float, c_float, c_int] + [c_void_p] * 5,
+        + [c_float, c_float, c_int] + [c_void_p] * 6,
         c_int,
     ),
     # stream, dtype, x, res, y, M, C, scale, shift, relu
     "det_bn_apply": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
-    # stream, dtype, dy, x, y, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
+    # stream, dtype, dy, x, mask_bits, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws
     "det_bn_bwd": (
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int] + [c_void_p] * 10,

@@ -277,7 +277,7 @@ template <typename T, bool RELU, bool RES>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
              const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int C,
-             int64_t* __restrict__ bump) {
+             int64_t* __restrict__ bump, uint8_t* __restrict__ mbits) {
   // num_batches_tracked += 1 rides on this launch (stream-ordered after the finalize that read it)
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
   const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
@@ -299,13 +299,18 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
         float sc[8], sh[8], o[8];
         load8f(scale + c0, sc);
         load8f(shift + c0, sh);
+        unsigned bits = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float z = __fmaf_rn(xv[u][j], sc[j], sh[j]);
           if (RES) z += rv[u][j];
           o[j] = RELU ? fmaxf(z, 0.f) : z;
+          bits |= (z > 0.f ? 1u : 0u) << j;
         }
         IO8<T>::store(y + v * 8, o);
+        // ReLU mask, 1 bit per element (1/16 of a bf16 stream): the residual-block backward
+        // reads it instead of re-reading the 16-bit output twice
+        if (RELU && RES && mbits) mbits[v] = static_cast<uint8_t>(bits);
       }
     }
   }
@@ -316,7 +321,7 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
 // ---------------------------------------------------------------------------------------------
 template <typename T, int MASK>
 __global__ void __launch_bounds__(kThreads)
-bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y, Geom g,
+bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t* __restrict__ mbits, Geom g,
                const float* __restrict__ mean, const float* __restrict__ scale,
                const float* __restrict__ shift, float* __restrict__ psum, float* __restrict__ psumx) {
   __shared__ float l1[kThreads * 8];
@@ -338,12 +343,13 @@ bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const T* __res
     const int64_t off = c0;
     int64_t r = r0 + ty;
     for (; r + R < r1; r += 2 * R) {
-      float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
+      float d0[8], x0[8], d1[8], x1[8];
+      unsigned b0 = 0xFFu, b1 = 0xFFu;
       IO8<T>::load(dy + r * C + off, d0);
       IO8<T>::load(x + r * C + off, x0);
       IO8<T>::load(dy + (r + R) * C + off, d1);
       IO8<T>::load(x + (r + R) * C + off, x1);
-      if (MASK == 2) { IO8<T>::load(y + r * C + off, y0); IO8<T>::load(y + (r + R) * C + off, y1); }
+      if (MASK == 2) { b0 = mbits[(r * C + off) >> 3]; b1 = mbits[((r + R) * C + off) >> 3]; }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = d0[j], b = d1[j];
@@ -351,23 +357,24 @@ bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const T* __res
           a = __fmaf_rn(x0[j], sc[j], sh[j]) > 0.f ? a : 0.f;
           b = __fmaf_rn(x1[j], sc[j], sh[j]) > 0.f ? b : 0.f;
         } else if (MASK == 2) {
-          a = y0[j] > 0.f ? a : 0.f;
-          b = y1[j] > 0.f ? b : 0.f;
+          a = (b0 >> j) & 1u ? a : 0.f;
+          b = (b1 >> j) & 1u ? b : 0.f;
         }
         s[j] += a + b;
         sx[j] += a * (x0[j] - mu[j]) + b * (x1[j] - mu[j]);
       }
     }
     for (; r < r1; r += R) {
-      float d0[8], x0[8], y0[8];
+      float d0[8], x0[8];
+      unsigned b0 = 0xFFu;
       IO8<T>::load(dy + r * C + off, d0);
       IO8<T>::load(x + r * C + off, x0);
-      if (MASK == 2) IO8<T>::load(y + r * C + off, y0);
+      if (MASK == 2) b0 = mbits[(r * C + off) >> 3];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = d0[j];
         if (MASK == 1) a = __fmaf_rn(x0[j], sc[j], sh[j]) > 0.f ? a : 0.f;
-        else if (MASK == 2) a = y0[j] > 0.f ? a : 0.f;
+        else if (MASK == 2) a = (b0 >> j) & 1u ? a : 0.f;
         s[j] += a;
         sx[j] += a * (x0[j] - mu[j]);
       }
@@ -455,20 +462,21 @@ bn_bwd_finalize(const float* __restrict__ psum, const float* __restrict__ psumx,
 
 template <typename T, int MASK, bool DRES>
 __global__ void __launch_bounds__(kThreads)
-bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
+bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t* __restrict__ mbits,
              const float* __restrict__ coef, const float* __restrict__ scale,
              const float* __restrict__ shift, T* __restrict__ dx, T* __restrict__ dres,
              int64_t nvec, int C) {
   const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v0 < nvec; v0 += 2 * S) {
-    float dv[2][8], xv[2][8], yv[2][8];
+    float dv[2][8], xv[2][8];
+    unsigned mb[2] = {0xFFu, 0xFFu};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t v = v0 + u * S;
       if (v < nvec) {
         IO8<T>::load(dy + v * 8, dv[u]);
         IO8<T>::load(x + v * 8, xv[u]);
-        if (MASK == 2) IO8<T>::load(y + v * 8, yv[u]);
+        if (MASK == 2) mb[u] = mbits[v];
       }
     }
 #pragma unroll
@@ -486,7 +494,7 @@ bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const T* __restr
         for (int j = 0; j < 8; ++j) {
           float d = dv[u][j];
           if (MASK == 1) d = __fmaf_rn(xv[u][j], sc[j], sh[j]) > 0.f ? d : 0.f;
-          else if (MASK == 2) d = yv[u][j] > 0.f ? d : 0.f;
+          else if (MASK == 2) d = (mb[u] >> j) & 1u ? d : 0.f;
           dz[j] = d;
           o[j] = __fmaf_rn(A[j], d, __fmaf_rn(B[j], xv[u][j], Cc[j]));
         }
@@ -538,7 +546,8 @@ int64_t det_bn_ws_elems(int64_t M, int C) {
 int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                      const float* gamma, const float* beta, float* running_mean, float* running_var,
                      int64_t* num_batches_tracked, float momentum, float eps, int relu,
-                     float* save_mean, float* save_rstd, float* scale, float* shift, float* ws) {
+                     float* save_mean, float* save_rstd, float* scale, float* shift, float* ws,
+                     uint8_t* mbits) {
   if (C % 8 != 0 || M <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   Geom g = make_geom(M, C);
@@ -561,7 +570,7 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
 #define DET_BN_FWD(T, RL, RS)                                                                          \
   hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                    \
                      static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, shift, \
-                     nvec, C, bump)
+                     nvec, C, bump, mbits)
   if (dtype == 1) {
     if (relu && res) DET_BN_FWD(unsigned short, true, true);
     else if (relu) DET_BN_FWD(unsigned short, true, false);
@@ -584,6 +593,7 @@ int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* 
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
   int64_t* bump = nullptr;
+  uint8_t* mbits = nullptr;
   if (dtype == 1) {
     if (relu && res) DET_BN_FWD(unsigned short, true, true);
     else if (relu) DET_BN_FWD(unsigned short, true, false);
@@ -599,14 +609,15 @@ int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* 
   return static_cast<int>(hipGetLastError());
 }
 
-// mask_mode: 0 none, 1 relu (mask from x), 2 relu (mask from y).  dres may be null.
+// mask_mode: 0 none, 1 relu (mask recomputed from x), 2 relu (bitmask written by the forward).
+// dres may be null.
 // dgamma/dbeta may be null.  ws >= det_bn_ws_elems(M, C).
-int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const void* y, int64_t M, int C,
+int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const void* mbits, int64_t M, int C,
                int mask_mode, const float* gamma, const float* save_mean, const float* save_rstd,
                const float* scale, const float* shift, void* dx, void* dres, float* dgamma, float* dbeta,
                float* ws) {
   if (C % 8 != 0 || M <= 0) return -1;
-  if (mask_mode == 2 && !y) return -2;
+  if (mask_mode == 2 && !mbits) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   Geom g = make_geom(M, C);
   float* psum = ws;
@@ -615,7 +626,7 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const voi
   dim3 grid(g.nrb, (C / 8 + g.tpr - 1) / g.tpr);
 #define DET_BN_P(T, MK)                                                                                \
   hipLaunchKernelGGL((bn_bwd_partial<T, MK>), grid, dim3(kThreads), 0, st, static_cast<const T*>(dy),   \
-                     static_cast<const T*>(x), static_cast<const T*>(y), g, save_mean, scale, shift, psum, psumx)
+                     static_cast<const T*>(x), static_cast<const uint8_t*>(mbits), g, save_mean, scale, shift, psum, psumx)
   if (dtype == 1) {
     if (mask_mode == 0) DET_BN_P(unsigned short, 0);
     else if (mask_mode == 1) DET_BN_P(unsigned short, 1);
@@ -633,7 +644,7 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const voi
   const int grid2 = apply_grid(nvec, 2);
 #define DET_BN_B(T, MK, DR)                                                                            \
   hipLaunchKernelGGL((bn_apply_bwd<T, MK, DR>), dim3(grid2), dim3(kThreads), 0, st,                     \
-                     static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(y), coef,  \
+                     static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const uint8_t*>(mbits), coef, \
                      scale, shift, static_cast<T*>(dx), static_cast<T*>(dres), nvec, C)
 #define DET_BN_B_MASK(T, DR)                 \
   if (mask_mode == 0) DET_BN_B(T, 0, DR);    \

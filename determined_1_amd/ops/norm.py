@@ -73,13 +73,15 @@ class _BNActTrain(torch.autograd.Function):
         ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
         if residual is not None:
             residual = residual.to(x.dtype).contiguous(memory_format=fmt)
+        mbits = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) \
+            if (relu and residual is not None) else None
         _lib.check(
             lib.det_bn_fwd_train(
                 _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C,
                 _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
                 float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)),
                 stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
-                ws.data_ptr(),
+                ws.data_ptr(), _ptr(mbits),
             ),
             "bn_fwd_train",
         )
@@ -88,12 +90,12 @@ class _BNActTrain(torch.autograd.Function):
         ctx.mask_mode = mask_mode
         ctx.has_res = residual is not None
         ctx.fmt = fmt
-        ctx.save_for_backward(x, y if mask_mode == 2 else None, weight, stats)
+        ctx.save_for_backward(x, mbits, weight, stats)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, stats = ctx.saved_tensors
+        x, mbits, weight, stats = ctx.saved_tensors
         M, C = _rows(x)
         lib = _lib.get_lib()
         dy = dy.to(x.dtype).contiguous(memory_format=ctx.fmt)
@@ -105,7 +107,7 @@ class _BNActTrain(torch.autograd.Function):
         ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
         _lib.check(
             lib.det_bn_bwd(
-                _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), _ptr(y), M, C, ctx.mask_mode,
+                _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), _ptr(mbits), M, C, ctx.mask_mode,
                 _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
                 dx.data_ptr(), _ptr(dres),
                 None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(),
