@@ -28,11 +28,49 @@ class APIError(RuntimeError):
         self.status = status
 
 
+TOKEN_FILE = os.path.join(os.path.expanduser("~"), ".det-mi355x", "token.json")
+
+
+def _load_token(master: str) -> Optional[str]:
+    if os.environ.get("DET_USER_TOKEN"):
+        return os.environ["DET_USER_TOKEN"]
+    try:
+        with open(TOKEN_FILE) as f:
+            return json.load(f).get(master)
+    except (OSError, ValueError):
+        return None
+
+
+def save_token(master: str, token: Optional[str]) -> None:
+    os.makedirs(os.path.dirname(TOKEN_FILE), exist_ok=True)
+    try:
+        with open(TOKEN_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = {}
+    if token is None:
+        d.pop(master, None)
+    else:
+        d[master] = token
+    with open(TOKEN_FILE, "w") as f:
+        json.dump(d, f)
+    os.chmod(TOKEN_FILE, 0o600)
+
+
 class MasterClient:
     def __init__(self, master: Optional[str] = None, timeout: float = 60.0) -> None:
         self.master = master or os.environ.get("DET_MASTER", "127.0.0.1:8080")
         self.timeout = timeout
         self.session = requests.Session()
+        tok = _load_token(self.master)
+        if tok:
+            self.session.headers["Authorization"] = f"Bearer {tok}"
+
+    def login(self, username: str, password: str = "") -> str:
+        tok = self.post("/login", {"username": username, "password": password})["token"]
+        self.session.headers["Authorization"] = f"Bearer {tok}"
+        save_token(self.master, tok)
+        return tok
 
     def _call(self, method: str, path: str, body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
         r = self.session.request(method, make_url(self.master, path), params=params,

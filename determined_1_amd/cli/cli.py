@@ -279,6 +279,40 @@ def cmd_model_register(args: argparse.Namespace) -> None:
     print(json.dumps(MasterClient(args.master).post(f"/models/{args.name}/versions", {"checkpoint_uuid": args.uuid})))
 
 
+# -------------------------------------------------------------------------------- users
+def cmd_user_login(args: argparse.Namespace) -> None:
+    import getpass
+
+    pw = args.password if args.password is not None else getpass.getpass(f"Password for user '{args.username}': ")
+    MasterClient(args.master).login(args.username, pw)
+    print(f"logged in as {args.username}")
+
+
+def cmd_user_logout(args: argparse.Namespace) -> None:
+    from determined_1_amd.api.request import save_token
+
+    c = MasterClient(args.master)
+    c.post("/logout")
+    save_token(c.master, None)
+
+
+def cmd_user_whoami(args: argparse.Namespace) -> None:
+    print(MasterClient(args.master).get("/me")["username"])
+
+
+def cmd_user_list(args: argparse.Namespace) -> None:
+    print(_table(MasterClient(args.master).get("/users"), ["username", "admin", "active"]))
+
+
+def cmd_user_create(args: argparse.Namespace) -> None:
+    MasterClient(args.master).post("/users", {"username": args.username, "password": args.password or "",
+                                              "admin": args.admin})
+
+
+def cmd_user_change_password(args: argparse.Namespace) -> None:
+    MasterClient(args.master).patch(f"/users/{args.username}", {"password": args.password})
+
+
 # ----------------------------------------------------------------------------- commands
 def cmd_command_run(args: argparse.Namespace) -> None:
     cfg = {"entrypoint": args.entrypoint, "resources": {"slots": args.slots},
@@ -477,6 +511,24 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("name")
     x.add_argument("uuid")
     x.set_defaults(func=cmd_model_register)
+
+    us = sub.add_parser("user", aliases=["u"]).add_subparsers(dest="sub")
+    x = us.add_parser("login")
+    x.add_argument("username", nargs="?", default="determined")
+    x.add_argument("--password")
+    x.set_defaults(func=cmd_user_login)
+    us.add_parser("logout").set_defaults(func=cmd_user_logout)
+    us.add_parser("whoami").set_defaults(func=cmd_user_whoami)
+    us.add_parser("list").set_defaults(func=cmd_user_list)
+    x = us.add_parser("create")
+    x.add_argument("username")
+    x.add_argument("--password")
+    x.add_argument("--admin", action="store_true")
+    x.set_defaults(func=cmd_user_create)
+    x = us.add_parser("change-password")
+    x.add_argument("username")
+    x.add_argument("password")
+    x.set_defaults(func=cmd_user_change_password)
 
     cm = sub.add_parser("command", aliases=["cmd"]).add_subparsers(dest="sub")
     x = cm.add_parser("run")

@@ -74,6 +74,8 @@ class Master {
   void HandleAgentSocket(const net::Request& req, net::WsPtr ws);
   void HandleTrialSocket(const net::Request& req, net::WsPtr ws);
   void RestoreExperiments();
+  void EnsureDefaultUsers();
+  std::string UserForRequest(const net::Request& r);
   int64_t CreateExperiment(const Json& body, bool* activate);
 
   MasterConfig cfg_;

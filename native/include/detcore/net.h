@@ -97,6 +97,8 @@ class HttpServer {
   // Pattern segments starting with ':' capture; a trailing "*" matches the rest.
   void Route(const std::string& method, const std::string& pattern, Handler h);
   void RouteWs(const std::string& pattern, WsHandler h);
+  // Optional authorisation hook for plain HTTP routes: return false -> 401.
+  void SetAuth(std::function<bool(const Request&)> auth) { auth_ = std::move(auth); }
   // Binds host:port (port 0 = ephemeral); returns the bound port.
   int Listen(const std::string& host, int port);
   void Start();  // accept loop on a background thread
@@ -113,6 +115,7 @@ class HttpServer {
   bool Match(const RouteEntry& r, const std::vector<std::string>& segs, std::map<std::string, std::string>* params) const;
   void Serve(int fd, std::string peer);
   std::vector<RouteEntry> routes_;
+  std::function<bool(const Request&)> auth_;
   int listen_fd_ = -1;
   int port_ = 0;
   std::atomic<bool> running_{false};

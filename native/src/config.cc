@@ -211,6 +211,7 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
   c.cluster_name = j.get_string("cluster_name", c.cluster_name);
   c.scheduler_tick_ms = j.get_double("scheduler_tick_ms", c.scheduler_tick_ms);
   c.python = j.get_string("python", c.python);
+  if (j["security"].is_object()) c.require_auth = j["security"].get_bool("authentication", c.require_auth);
   return c;
 }
 
@@ -231,6 +232,9 @@ Json MasterConfig::ToJson() const {
   j["cluster_name"] = cluster_name;
   j["scheduler_tick_ms"] = scheduler_tick_ms;
   j["python"] = python;
+  Json sec = Json::object();
+  sec["authentication"] = require_auth;
+  j["security"] = sec;
   return j;
 }
 

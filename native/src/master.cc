@@ -42,6 +42,7 @@
 #include <sstream>
 
 #include "detcore/config.h"
+#include "detcore/lttb.h"
 #include "detcore/master_actors.h"
 #include "detcore/searcher.h"
 
@@ -301,7 +302,125 @@ static net::Response Err(int status, const std::string& m) {
 }
 static int64_t IntParam(const net::Request& r, const std::string& k) { return std::stoll(r.Param(k)); }
 
+// ------------------------------------------------------------------------- users & sessions
+// (reference master/internal/user/service.go): salted SHA-1 password hashes,
+// bearer-token sessions, the built-in "admin" and "determined" users with empty passwords.
+static std::string Hex(const std::string& raw) {
+  static const char* d = "0123456789abcdef";
+  std::string o;
+  for (unsigned char c : raw) {
+    o.push_back(d[c >> 4]);
+    o.push_back(d[c & 15]);
+  }
+  return o;
+}
+
+static std::string HashPassword(const std::string& salt, const std::string& pw) { return Hex(net::Sha1(salt + ":" + pw)); }
+
+void Master::EnsureDefaultUsers() {
+  for (const char* name : {"admin", "determined"}) {
+    if (!store_->Where("users", "username", Json(name)).empty()) continue;
+    Json u = Json::object();
+    u["username"] = name;
+    u["salt"] = NewUUID();
+    u["password_hash"] = HashPassword(u["salt"].as_string(), "");
+    u["admin"] = std::string(name) == "admin";
+    u["active"] = true;
+    store_->Insert("users", u);
+  }
+}
+
+std::string Master::UserForRequest(const net::Request& r) {
+  auto it = r.headers.find("authorization");
+  if (it == r.headers.end()) return "";
+  std::string v = it->second;
+  if (v.rfind("Bearer ", 0) == 0) v = v.substr(7);
+  for (auto& s : store_->Where("sessions", "token", Json(v))) return s.get_string("username", "");
+  return "";
+}
+
 void Master::InstallRoutes() {
+  EnsureDefaultUsers();
+  if (cfg_.require_auth) {
+    http_.SetAuth([this](const net::Request& r) {
+      if (r.path == "/login" || r.path == "/info" || r.path == "/trial_logs") return true;
+      if (r.path.rfind("/experiments/", 0) == 0 && r.path.size() > 10 &&
+          r.path.find("/model_def") != std::string::npos)
+        return true;  // agents fetch model definitions
+      if (r.path.rfind("/commands/", 0) == 0 && r.path.find("/context") != std::string::npos) return true;
+      return !UserForRequest(r).empty();
+    });
+  }
+  http_.Route("POST", "/login", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    std::string name = body.get_string("username", "");
+    for (auto& u : store_->Where("users", "username", Json(name))) {
+      if (!u.get_bool("active", true) ||
+          HashPassword(u.get_string("salt", ""), body.get_string("password", "")) != u.get_string("password_hash", ""))
+        break;
+      Json sess = Json::object();
+      sess["username"] = name;
+      sess["token"] = Hex(net::Sha1(NewUUID() + NewUUID()));
+      sess["created"] = NowRFC3339();
+      store_->Insert("sessions", sess);
+      Json out = Json::object();
+      out["token"] = sess["token"];
+      out["username"] = name;
+      return J(200, out);
+    }
+    return Err(401, "invalid credentials");
+  });
+  http_.Route("POST", "/logout", [this](const net::Request& r) {
+    auto it = r.headers.find("authorization");
+    if (it != r.headers.end()) {
+      std::string tok = it->second.rfind("Bearer ", 0) == 0 ? it->second.substr(7) : it->second;
+      store_->DeleteWhere("sessions", [&](const Json& s) { return s.get_string("token", "") == tok; });
+    }
+    return J(200, Json::object());
+  });
+  http_.Route("GET", "/me", [this](const net::Request& r) {
+    std::string u = UserForRequest(r);
+    if (u.empty()) return Err(401, "not logged in");
+    Json out = Json::object();
+    out["username"] = u;
+    return J(200, out);
+  });
+  http_.Route("GET", "/users", [this](const net::Request&) {
+    Json out = Json::array();
+    for (auto& u : store_->Scan("users")) {
+      Json v = Json::object();
+      for (const char* k : {"id", "username", "admin", "active"}) v[k] = u[k];
+      out.push_back(v);
+    }
+    return J(200, out);
+  });
+  http_.Route("POST", "/users", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    std::string name = body.get_string("username", "");
+    if (name.empty()) return Err(400, "username required");
+    if (!store_->Where("users", "username", Json(name)).empty()) return Err(409, "user exists");
+    Json u = Json::object();
+    u["username"] = name;
+    u["salt"] = NewUUID();
+    u["password_hash"] = HashPassword(u["salt"].as_string(), body.get_string("password", ""));
+    u["admin"] = body.get_bool("admin", false);
+    u["active"] = true;
+    store_->Insert("users", u);
+    return J(201, Json::object());
+  });
+  http_.Route("PATCH", "/users/:name", [this](const net::Request& r) {
+    Json body = Json::parse(r.body);
+    for (auto& u : store_->Where("users", "username", Json(r.Param("name")))) {
+      Json patch = Json::object();
+      if (body.has("password")) patch["password_hash"] = HashPassword(u.get_string("salt", ""), body["password"].as_string());
+      if (body.has("active")) patch["active"] = body["active"];
+      if (body.has("admin")) patch["admin"] = body["admin"];
+      store_->Update("users", u["id"].as_int(), patch);
+      return J(200, Json::object());
+    }
+    return Err(404, "user not found");
+  });
+
   http_.Route("GET", "/info", [this](const net::Request&) {
     Json j = Json::object();
     j["cluster_id"] = cluster_id_;
@@ -316,6 +435,8 @@ void Master::InstallRoutes() {
   http_.Route("POST", "/experiments", [this](const net::Request& r) {
     Json body = Json::parse(r.body);
     bool activate = true;
+    std::string user = UserForRequest(r);
+    if (!user.empty()) body["owner"] = user;
     int64_t id = CreateExperiment(body, &activate);
     Json out = Json::object();
     if (id == 0) {
@@ -491,8 +612,31 @@ void Master::InstallRoutes() {
         p["metrics"] = v["metrics"]["validation_metrics"];
         va.push_back(p);
       }
-      tj["training"] = tr;
-      tj["validation"] = va;
+      // ?downsample=N: LTTB over (total_batches, metric) per metric name (reference TrialsSample)
+      size_t ds = static_cast<size_t>(std::stoll(r.Query("downsample", "0")));
+      const std::string mname = r.Query("metric", "");
+      if (ds >= 3 && !mname.empty()) {
+        auto sample = [&](const Json& series) {
+          std::vector<Point> pts;
+          for (auto& p : series.as_array())
+            if (p["metrics"].is_object() && p["metrics"][mname].is_number())
+              pts.push_back({static_cast<double>(p.get_int("total_batches", 0)), p["metrics"][mname].as_double()});
+          std::sort(pts.begin(), pts.end(), [](const Point& a, const Point& b) { return a.x < b.x; });
+          Json arr = Json::array();
+          for (auto& p : Downsample(pts, ds)) {
+            Json j = Json::object();
+            j["total_batches"] = static_cast<int64_t>(p.x);
+            j["value"] = p.y;
+            arr.push_back(j);
+          }
+          return arr;
+        };
+        tj["training"] = sample(tr);
+        tj["validation"] = sample(va);
+      } else {
+        tj["training"] = tr;
+        tj["validation"] = va;
+      }
       out.push_back(tj);
     }
     return J(200, out);

@@ -69,6 +69,8 @@ int main(int argc, char** argv) {
       cfgj["checkpoint_storage"] = cs;
     } else if (a == "--python") {
       cfgj["python"] = next();
+    } else if (a == "--require-auth") {
+      cfgj["security"]["authentication"] = true;
     } else if (a == "--scheduler-tick-ms") {
       cfgj["scheduler_tick_ms"] = std::stod(next());
     } else if (a == "-h" || a == "--help") {

@@ -528,6 +528,8 @@ void HttpServer::Serve(int fd, std::string peer) {
     Response res;
     if (!hit) {
       res = Response::Json(path_hit ? 405 : 404, R"({"error":"not found"})");
+    } else if (auth_ && !auth_(req)) {
+      res = Response::Json(401, R"({"error":"unauthenticated: log in with POST /login"})");
     } else {
       try {
         res = hit->h(req);

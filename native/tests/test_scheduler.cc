@@ -148,3 +148,18 @@ TEST(round_robin_interleaves_groups) {
   for (auto& a : d.allocate) x += a.first[0] == 'x';
   EXPECT(x == 1 || x == 2);
 }
+
+#include "detcore/lttb.h"
+
+TEST(lttb_keeps_endpoints_and_peaks) {
+  std::vector<detcore::Point> pts;
+  for (int i = 0; i < 1000; ++i) pts.push_back({static_cast<double>(i), i == 500 ? 100.0 : 0.0});
+  auto out = detcore::Downsample(pts, 20);
+  EXPECT_EQ(out.size(), size_t(20));
+  EXPECT_EQ(out.front().x, 0.0);
+  EXPECT_EQ(out.back().x, 999.0);
+  bool peak = false;
+  for (auto& p : out) peak |= p.y == 100.0;
+  EXPECT(peak);
+  EXPECT_EQ(detcore::Downsample(pts, 2000).size(), size_t(1000));
+}

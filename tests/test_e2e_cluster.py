@@ -203,3 +203,33 @@ def test_master_restart_resumes_experiment(tmp_path):
         assert sum(s["num_batches"] for s in done) == 60
     finally:
         c.down()
+
+
+def test_auth_required_master(tmp_path, monkeypatch):
+    import requests
+
+    monkeypatch.setenv("HOME", str(tmp_path))
+    from determined_1_amd.deploy.local import free_port, native_binary
+
+    port = free_port()
+    p = subprocess.Popen([native_binary("det-master"), "--host", "127.0.0.1", "--port", str(port), "--require-auth"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            try:
+                requests.get(f"http://127.0.0.1:{port}/info", timeout=1)
+                break
+            except requests.RequestException:
+                time.sleep(0.1)
+        assert requests.get(f"http://127.0.0.1:{port}/experiments").status_code == 401
+        cl = MasterClient(f"127.0.0.1:{port}")
+        cl.login("admin", "")
+        assert cl.get("/me")["username"] == "admin"
+        cl.post("/users", {"username": "alice", "password": "pw"})
+        with pytest.raises(Exception):
+            MasterClient(f"127.0.0.1:{port}").login("alice", "wrong")
+        assert cl.get("/experiments") == []
+    finally:
+        p.terminate()
+        p.wait(timeout=10)
