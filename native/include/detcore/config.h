@@ -36,7 +36,8 @@ struct MasterConfig {
   std::string cluster_name = "determined-mi355x";
   double scheduler_tick_ms = 500;
   std::string python = "python3";
-  bool require_auth = false;  // security.authentication: tokens required on the REST API
+  bool require_auth = false;
+  Json provisioner;  // {max_instances, min_instances, slots_per_instance, ...}; empty = disabled  // security.authentication: tokens required on the REST API
   static MasterConfig FromJson(const Json& j);
   Json ToJson() const;
 };

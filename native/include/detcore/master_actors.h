@@ -10,6 +10,7 @@
 
 #include "detcore/actor.h"
 #include "detcore/master.h"
+#include "detcore/provisioner.h"
 #include "detcore/scheduler.h"
 #include "detcore/searcher.h"
 #include "detcore/sequencer.h"
@@ -170,6 +171,21 @@ class ExperimentActor : public actor::Actor {
   double best_metric_ = 0;
   Json best_validation_;
   std::map<std::string, Json> latest_ckpt_;  // request id -> latest checkpoint metadata (PBT)
+};
+
+// Elastic agent provisioning for one pool: a 1 s tick feeds the pool's demand to
+// the ScaleDecider and applies its launch/terminate decisions through the provider.
+class ProvisionerActor : public actor::Actor {
+ public:
+  ProvisionerActor(Master* m, std::string pool, prov::ProvisionerConfig cfg);
+  void Receive(actor::Context& ctx) override;
+
+ private:
+  Master* m_;
+  std::string pool_;
+  prov::ProvisionerConfig cfg_;
+  prov::ScaleDecider decider_;
+  std::unique_ptr<prov::Provider> provider_;
 };
 
 // Generic command task (reference master/internal/command/command.go): run an argv

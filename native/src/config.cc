@@ -211,6 +211,7 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
   c.cluster_name = j.get_string("cluster_name", c.cluster_name);
   c.scheduler_tick_ms = j.get_double("scheduler_tick_ms", c.scheduler_tick_ms);
   c.python = j.get_string("python", c.python);
+  c.provisioner = j["provisioner"];
   if (j["security"].is_object()) c.require_auth = j["security"].get_bool("authentication", c.require_auth);
   return c;
 }
@@ -235,6 +236,7 @@ Json MasterConfig::ToJson() const {
   Json sec = Json::object();
   sec["authentication"] = require_auth;
   j["security"] = sec;
+  j["provisioner"] = provisioner;
   return j;
 }
 

@@ -1026,6 +1026,21 @@ int Master::Start() {
   if (port_ < 0) throw std::runtime_error("cannot bind port " + std::to_string(cfg_.port));
   if (cfg_.listen_host != "0.0.0.0" && !cfg_.listen_host.empty()) advertised_host_ = cfg_.listen_host;
   http_.Start();
+  if (cfg_.provisioner.is_object() && cfg_.provisioner.get_int("max_instances", 0) > 0) {
+    prov::ProvisionerConfig pc = prov::ProvisionerConfig::FromJson(cfg_.provisioner);
+    pc.master_host = advertised_host_;
+    pc.master_port = port_;
+    pc.python = cfg_.python;
+    if (pc.agent_binary.empty()) {
+      char buf[4096];
+      ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+      std::string self = n > 0 ? std::string(buf, static_cast<size_t>(n)) : "det-master";
+      pc.agent_binary = self.substr(0, self.rfind('/')) + "/det-agent";
+    }
+    for (auto& p : cfg_.resource_pools)
+      sys_->ActorOf("provisioners/" + p, std::make_unique<ProvisionerActor>(this, p, pc));
+    Log("provisioner enabled: max " + std::to_string(pc.max_instances) + " agents per pool");
+  }
   RestoreExperiments();
   Log(std::string("listening on ") + cfg_.listen_host + ":" + std::to_string(port_) + " scheduler=" + cfg_.scheduler);
   return port_;

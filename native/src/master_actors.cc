@@ -112,15 +112,21 @@ void ResourcePoolActor::Receive(Context& ctx) {
         used += !s.task.empty();
       }
       a["slots"] = sl;
+      a["idle"] = kv.second.Idle();
       agents.push_back(a);
     }
     out["agents"] = agents;
     out["num_slots"] = slots;
     out["slots_used"] = used;
     out["num_tasks"] = static_cast<int64_t>(st_.tasks.size());
-    int pending = 0;
-    for (auto& kv : st_.tasks) pending += !kv.second.allocated();
+    int pending = 0, pending_slots = 0;
+    for (auto& kv : st_.tasks)
+      if (!kv.second.allocated()) {
+        ++pending;
+        pending_slots += kv.second.slots_needed;
+      }
     out["tasks_pending"] = pending;
+    out["pending_slots"] = pending_slots;
     out["scheduler"] = m_->config().scheduler;
     ctx.Respond(out);
   }
@@ -969,6 +975,32 @@ void TrialActor::SaveWorkloadEnd(const CompletedMessage& cm) {
       patch["metrics"] = cm.metrics;
     }
     m_->store().Update(table, r["id"].as_int(), patch);
+  }
+}
+
+// =============================================================================== provisioner
+ProvisionerActor::ProvisionerActor(Master* m, std::string pool, prov::ProvisionerConfig cfg)
+    : m_(m), pool_(std::move(pool)), cfg_(cfg), decider_(cfg) {
+  provider_ = std::make_unique<prov::LocalProvider>(cfg, pool_);
+}
+
+void ProvisionerActor::Receive(Context& ctx) {
+  if (ctx.Is<actor::PreStart>() || ctx.Is<SchedulerTick>()) {
+    if (ctx.Is<SchedulerTick>()) {
+      actor::Message msum = m_->Pool(pool_)->AskSync(PoolSummary{}, std::chrono::milliseconds(5000));
+      if (msum.has_value()) {
+        Json s = std::any_cast<Json>(msum);
+        std::vector<prov::AgentInfo> agents;
+        for (auto& a : s["agents"].as_array()) agents.push_back({a.get_string("id", ""), a.get_bool("idle", true)});
+        auto d = decider_.Decide(static_cast<int>(s.get_int("pending_slots", 0)), agents, provider_->List(),
+                                 prov::Clock::now());
+        if (!d.terminate.empty()) provider_->Terminate(d.terminate);
+        if (d.launch > 0) provider_->Launch(d.launch);
+      }
+    }
+    ctx.system().NotifyAfter(ctx.Self(), std::chrono::milliseconds(1000), SchedulerTick{});
+  } else if (ctx.Is<actor::PostStop>()) {
+    provider_.reset();
   }
 }
 

@@ -69,6 +69,12 @@ int main(int argc, char** argv) {
       cfgj["checkpoint_storage"] = cs;
     } else if (a == "--python") {
       cfgj["python"] = next();
+    } else if (a == "--provision-max") {
+      cfgj["provisioner"]["max_instances"] = std::stoi(next());
+    } else if (a == "--provision-slots") {
+      cfgj["provisioner"]["slots_per_instance"] = std::stoi(next());
+    } else if (a == "--provision-idle-ms") {
+      cfgj["provisioner"]["max_idle_agent_period_ms"] = std::stoi(next());
     } else if (a == "--require-auth") {
       cfgj["security"]["authentication"] = true;
     } else if (a == "--scheduler-tick-ms") {

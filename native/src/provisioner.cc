@@ -1,0 +1,136 @@
+// Elastic provisioning (see include/detcore/provisioner.h).
+#include "detcore/provisioner.h"
+
+#include <signal.h>
+#include <spawn.h>
+#include <sys/wait.h>
+
+#include <algorithm>
+#include <cstdio>
+
+extern char** environ;
+
+namespace detcore {
+namespace prov {
+
+ProvisionerConfig ProvisionerConfig::FromJson(const Json& j) {
+  ProvisionerConfig c;
+  c.min_instances = static_cast<int>(j.get_int("min_instances", 0));
+  c.max_instances = static_cast<int>(j.get_int("max_instances", 0));
+  c.slots_per_instance = static_cast<int>(j.get_int("slots_per_instance", 1));
+  c.max_idle_period = std::chrono::milliseconds(j.get_int("max_idle_agent_period_ms", 300000));
+  c.max_starting_period = std::chrono::milliseconds(j.get_int("max_agent_starting_period_ms", 300000));
+  c.provider = j.get_string("provider", "local");
+  c.agent_binary = j.get_string("agent_binary", "");
+  c.artificial = j.get_bool("artificial_slots", true);
+  c.work_dir = j.get_string("work_dir", c.work_dir);
+  return c;
+}
+
+Decision ScaleDecider::Decide(int pending_slots, const std::vector<AgentInfo>& agents,
+                              const std::vector<Instance>& instances, Clock::time_point now) {
+  Decision d;
+  std::map<std::string, bool> connected_idle;
+  for (auto& a : agents) connected_idle[a.id] = a.idle;
+  int live = 0;
+  std::vector<const Instance*> idle_candidates;
+  for (auto& inst : instances) {
+    if (inst.state == "Stopped") continue;
+    ++live;
+    auto it = connected_idle.find(inst.id);
+    if (it == connected_idle.end()) {
+      // no agent yet: starting, or stuck / disconnected
+      idle_since_.erase(inst.id);
+      if (now - inst.launched > cfg_.max_starting_period) d.terminate.push_back(inst.id);
+      continue;
+    }
+    if (!it->second) {
+      idle_since_.erase(inst.id);
+      continue;
+    }
+    auto ins = idle_since_.emplace(inst.id, now).first;
+    if (now - ins->second > cfg_.max_idle_period) idle_candidates.push_back(&inst);
+  }
+  // keep min_instances alive; terminate the longest-idle first
+  std::sort(idle_candidates.begin(), idle_candidates.end(),
+            [&](const Instance* a, const Instance* b) { return idle_since_[a->id] < idle_since_[b->id]; });
+  int removable = live - static_cast<int>(d.terminate.size()) - cfg_.min_instances;
+  if (pending_slots > 0) removable = 0;  // demand exists: don't shrink
+  for (const Instance* inst : idle_candidates) {
+    if (removable <= 0) break;
+    d.terminate.push_back(inst->id);
+    idle_since_.erase(inst->id);
+    --removable;
+  }
+  // launch for unmet demand: instances still starting count as capacity on the way
+  int starting = 0;
+  for (auto& inst : instances)
+    if (inst.state != "Stopped" && !connected_idle.count(inst.id)) ++starting;
+  int spi = std::max(1, cfg_.slots_per_instance);
+  int want = (pending_slots + spi - 1) / spi - starting;
+  int room = cfg_.max_instances - (live - static_cast<int>(d.terminate.size()));
+  d.launch = std::max(0, std::min(want, room));
+  if (live - static_cast<int>(d.terminate.size()) + d.launch < cfg_.min_instances)
+    d.launch = cfg_.min_instances - (live - static_cast<int>(d.terminate.size()));
+  return d;
+}
+
+LocalProvider::LocalProvider(ProvisionerConfig cfg, std::string pool) : cfg_(std::move(cfg)), pool_(std::move(pool)) {}
+
+LocalProvider::~LocalProvider() {
+  std::vector<std::string> ids;
+  for (auto& kv : procs_) ids.push_back(kv.first);
+  Terminate(ids);
+}
+
+std::vector<Instance> LocalProvider::List() {
+  std::vector<Instance> out;
+  for (auto it = procs_.begin(); it != procs_.end();) {
+    int st;
+    if (waitpid(it->second.first, &st, WNOHANG) == it->second.first) {
+      it = procs_.erase(it);
+      continue;
+    }
+    out.push_back(it->second.second);
+    ++it;
+  }
+  return out;
+}
+
+void LocalProvider::Launch(int n) {
+  for (int i = 0; i < n; ++i) {
+    std::string id = pool_ + "-prov-" + std::to_string(next_++);
+    std::vector<std::string> args = {cfg_.agent_binary, "--master-host", cfg_.master_host, "--master-port",
+                                     std::to_string(cfg_.master_port), "--agent-id", id, "--resource-pool", pool_,
+                                     "--python", cfg_.python, "--work-dir", cfg_.work_dir + "/" + id};
+    if (cfg_.artificial) {
+      args.push_back("--artificial-slots");
+      args.push_back(std::to_string(cfg_.slots_per_instance));
+    }
+    std::vector<char*> argv;
+    for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
+    argv.push_back(nullptr);
+    pid_t pid;
+    if (posix_spawn(&pid, cfg_.agent_binary.c_str(), nullptr, nullptr, argv.data(), environ) != 0) {
+      std::fprintf(stderr, "[det-master] provisioner: failed to launch %s\n", cfg_.agent_binary.c_str());
+      continue;
+    }
+    procs_[id] = {pid, Instance{id, "Starting", Clock::now()}};
+    std::fprintf(stderr, "[det-master] provisioner: launched agent %s (pid %d)\n", id.c_str(), pid);
+  }
+}
+
+void LocalProvider::Terminate(const std::vector<std::string>& ids) {
+  for (auto& id : ids) {
+    auto it = procs_.find(id);
+    if (it == procs_.end()) continue;
+    ::kill(it->second.first, SIGTERM);
+    int st;
+    waitpid(it->second.first, &st, 0);
+    procs_.erase(it);
+    std::fprintf(stderr, "[det-master] provisioner: terminated agent %s\n", id.c_str());
+  }
+}
+
+}  // namespace prov
+}  // namespace detcore

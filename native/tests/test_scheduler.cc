@@ -163,3 +163,28 @@ TEST(lttb_keeps_endpoints_and_peaks) {
   EXPECT(peak);
   EXPECT_EQ(detcore::Downsample(pts, 2000).size(), size_t(1000));
 }
+
+#include "detcore/provisioner.h"
+
+TEST(scale_decider_launch_and_idle_terminate) {
+  using namespace detcore::prov;
+  ProvisionerConfig cfg;
+  cfg.max_instances = 3;
+  cfg.slots_per_instance = 2;
+  cfg.max_idle_period = std::chrono::milliseconds(1000);
+  cfg.max_starting_period = std::chrono::milliseconds(5000);
+  ScaleDecider sd(cfg);
+  auto t0 = Clock::now();
+  auto d = sd.Decide(5, {}, {}, t0);
+  EXPECT_EQ(d.launch, 3);  // ceil(5/2) = 3, capped by max 3
+  std::vector<Instance> inst = {{"a", "Starting", t0}, {"b", "Starting", t0}, {"c", "Starting", t0}};
+  d = sd.Decide(5, {}, inst, t0 + std::chrono::milliseconds(10));
+  EXPECT_EQ(d.launch, 0);  // still starting
+  std::vector<AgentInfo> agents = {{"a", true}, {"b", true}, {"c", false}};
+  d = sd.Decide(0, agents, inst, t0 + std::chrono::milliseconds(100));
+  EXPECT(d.terminate.empty());  // idle, but not for long yet
+  d = sd.Decide(0, agents, inst, t0 + std::chrono::milliseconds(1500));
+  EXPECT_EQ(d.terminate.size(), size_t(2));  // a and b idle > 1s, c busy
+  d = sd.Decide(0, {}, {{"z", "Starting", t0}}, t0 + std::chrono::milliseconds(6000));
+  EXPECT_EQ(d.terminate.size(), size_t(1));  // never connected within the starting period
+}
