@@ -1,0 +1,74 @@
+"""ASHA trials/hr on a real cluster (BASELINE north-star #2): det-master + det-agent (GPU slots from
+KFD) on this host, the 16-trial adaptive_asha CIFAR-10 experiment (examples/computer_vision/
+cifar10_pytorch/adaptive.yaml) with max_length scaled down so the search fits a short run.
+Reports trials completed / hour, wall time and the GPU-busy fraction sampled from amdgpu sysfs.
+
+    python scripts/bench_asha.py [--max-length-batches 400] [--max-trials 16] [--timeout 900]
+"""
+import argparse
+import json
+import os
+import pathlib
+import sys
+import threading
+import time
+
+import yaml
+
+REPO = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--max-length-batches", type=int, default=400)
+    ap.add_argument("--max-trials", type=int, default=16)
+    ap.add_argument("--timeout", type=float, default=900)
+    ap.add_argument("--artificial-slots", type=int, default=0, help="CPU dry run without GPUs")
+    args = ap.parse_args()
+    from determined_1_amd import gpu
+    from determined_1_amd.api import MasterClient, read_context
+    from determined_1_amd.deploy import LocalCluster
+
+    ex = REPO / "examples" / "computer_vision" / "cifar10_pytorch"
+    cfg = yaml.safe_load((ex / "adaptive.yaml").read_text())
+    cfg["searcher"]["max_length"] = {"batches": args.max_length_batches}
+    cfg["searcher"]["max_trials"] = args.max_trials
+    cfg["min_validation_period"] = {"batches": max(1, args.max_length_batches // 4)}
+    cfg["scheduling_unit"] = 50
+    cfg.pop("records_per_epoch", None)
+    busy = []
+    stop = threading.Event()
+
+    def sample() -> None:
+        while not stop.wait(0.5):
+            u = gpu.utilization()
+            if u:
+                busy.append(sum(x.get("gpu_busy_percent", 0) for x in u) / len(u))
+
+    with LocalCluster(agents=1, slots_per_agent=args.artificial_slots, gpu=args.artificial_slots == 0,
+                      log_dir=os.environ.get("DET_BENCH_LOGDIR", "/tmp")) as c:
+        if args.artificial_slots == 0:
+            c.wait_for_slots(1)
+        cl = MasterClient(c.address)
+        th = threading.Thread(target=sample, daemon=True)
+        th.start()
+        t0 = time.time()
+        eid = cl.create_experiment(cfg, read_context(ex))["id"]
+        state = cl.wait_for_experiment(eid, timeout=args.timeout)
+        wall = time.time() - t0
+        stop.set()
+        e = cl.experiment(eid)
+        done = sum(1 for t in e["trials"] if t["state"] == "COMPLETED")
+        slots = sum(len(a["slots"]) for a in cl.get("/agents"))
+        print(json.dumps({"metric": "ASHA trials/hr (16-trial adaptive_asha CIFAR-10)",
+                          "value": round(done * 3600.0 / wall, 2), "unit": "trials/hr", "state": state,
+                          "trials_completed": done, "wall_s": round(wall, 1), "slots": slots,
+                          "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
+                          "config": {"max_length_batches": args.max_length_batches, "max_trials": args.max_trials,
+                                     "searcher": "adaptive_asha", "amp": cfg["hyperparameters"].get("amp")}}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+"""BERT-base SQuAD-shape throughput through the real PyTorchTrial path (BASELINE config 5 shape:
+seq 384, per-GPU batch 12 (global 96 on 8 GPUs), AdamW fused HIP kernel, bf16 AMP O2, clipping).
+
+    python scripts/bench_bert.py [--steps K] [--warmup W] [--batch-per-gpu B] [--amp O2]
+One JSON line: examples/s (whole node) + ms/step.  Multi-GPU: launch with torch.distributed.run.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch-per-gpu", type=int, default=12)
+    ap.add_argument("--amp", default="O2")
+    ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    from determined_1_amd import workload
+    from determined_1_amd.experimental import make_controller
+    from determined_1_amd.models.bert import BertSQuADTrial
+    from determined_1_amd.parallel import dist as pdist
+
+    gbs = args.batch_per_gpu * world
+    cfg = {
+        "hyperparameters": {"global_batch_size": gbs, "learning_rate": 3e-5, "max_seq_length": 384, "amp": args.amp,
+                            "max_grad_norm": 1.0, "train_records": 100000},
+        "resources": {"slots_per_trial": world},
+        "optimizations": {"aggregation_frequency": args.agg},
+        "searcher": {"name": "single", "metric": "f1", "max_length": {"batches": args.steps}, "smaller_is_better": False},
+    }
+    t = {}
+
+    def sync() -> None:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        pdist.barrier()
+
+    def stream():
+        yield workload.train_workload(1, num_batches=args.warmup), [], workload.ignore_response
+        sync()
+        t["t0"] = time.perf_counter()
+        yield workload.train_workload(2, num_batches=args.steps, total_batches_processed=args.warmup), [], workload.ignore_response
+        sync()
+        t["t1"] = time.perf_counter()
+        yield workload.terminate_workload(3), [], workload.ignore_response
+
+    ctrl = make_controller(BertSQuADTrial, cfg, stream(), trial_seed=7)
+    ctrl.run()
+    el = max(pdist.allgather_object(t["t1"] - t["t0"]))
+    if rank == 0:
+        print(json.dumps({"metric": "examples/sec (whole node) BERT-base SQuAD-shape PyTorchTrial",
+                          "value": round(args.steps * gbs / el, 2), "unit": "examples/s", "n_gpus": world,
+                          "ms_per_step": round(1000 * el / args.steps, 2), "dtype": "bf16" if args.amp != "O0" else "fp32",
+                          "config": {"model": "bert-base (random init)", "seq_len": 384, "global_batch": gbs,
+                                     "amp": args.amp, "aggregation_frequency": args.agg,
+                                     "optimizer": "AdamW (fused arena HIP kernel)"}}), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()
