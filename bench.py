@@ -33,7 +33,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DET_BENCH_BS", "256")))
+    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DET_BENCH_BS", "512")),
+                    help="per-GPU batch (weak scaling); 512 uses the 288 GB HBM of an MI355X")
     ap.add_argument("--amp", default=os.environ.get("DET_BENCH_AMP", "O2"), choices=["O0", "O1", "O2"])
     ap.add_argument("--arch", default="resnet50")
     ap.add_argument("--bucket-mb", type=int, default=int(os.environ.get("DET_BENCH_BUCKET_MB", "64")))
