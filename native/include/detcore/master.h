@@ -96,6 +96,8 @@ class Master {
 };
 
 // Helpers shared by the master translation units.
+void MasterLog(const std::string& line);  // stderr + the in-memory ring buffer behind GET /logs
+Json MasterLogTail(int64_t offset, int64_t limit);
 std::string NowRFC3339();
 std::string NewUUID();
 Json CheckpointsToGC(Store& store, int64_t experiment_id, const Json& exp_config);

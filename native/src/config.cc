@@ -111,7 +111,7 @@ std::vector<std::string> ValidateExperimentConfig(const Json& cfg) {
       "min_checkpoint_period", "min_validation_period", "checkpoint_policy", "hyperparameters", "searcher",
       "resources", "optimizations", "records_per_epoch", "scheduling_unit", "bind_mounts", "environment",
       "reproducibility", "max_restarts", "security", "debug", "internal", "entrypoint", "data_layer",
-      "batches_per_step"};
+      "batches_per_step", "internal_warm_start"};
   static const std::set<std::string> kSearchers = {"single", "random", "grid", "sync_halving", "adaptive",
                                                    "adaptive_simple", "async_halving", "adaptive_asha", "pbt"};
   std::vector<std::string> errs;

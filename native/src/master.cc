@@ -38,6 +38,8 @@
 #include <cstdio>
 #include <ctime>
 #include <fstream>
+#include <deque>
+#include <mutex>
 #include <random>
 #include <sstream>
 
@@ -55,7 +57,37 @@ using actor::Ref;
 
 static const char* kVersion = "0.13.10.dev0+mi355x";
 
-static void Log(const std::string& s) { std::fprintf(stderr, "[det-master] %s\n", s.c_str()); }
+// Master log ring buffer (reference pkg/logger/log_buffer.go: last 25k entries, GET /logs).
+namespace {
+std::mutex g_log_mu;
+std::deque<Json> g_log;
+int64_t g_log_seq = 0;
+constexpr size_t kLogCap = 25000;
+}  // namespace
+
+void MasterLog(const std::string& line) {
+  std::fprintf(stderr, "[det-master] %s\n", line.c_str());
+  std::lock_guard<std::mutex> g(g_log_mu);
+  Json e = Json::object();
+  e["id"] = ++g_log_seq;
+  e["time"] = NowRFC3339();
+  e["message"] = line;
+  g_log.push_back(e);
+  if (g_log.size() > kLogCap) g_log.pop_front();
+}
+
+Json MasterLogTail(int64_t offset, int64_t limit) {
+  std::lock_guard<std::mutex> g(g_log_mu);
+  Json out = Json::array();
+  for (auto& e : g_log) {
+    if (e["id"].as_int() <= offset) continue;
+    if (static_cast<int64_t>(out.size()) >= limit) break;
+    out.push_back(e);
+  }
+  return out;
+}
+
+static void Log(const std::string& s) { MasterLog(s); }
 
 std::string NowRFC3339() {
   auto now = std::chrono::system_clock::now();
@@ -275,6 +307,24 @@ int64_t Master::CreateExperiment(const Json& body, bool* activate) {
   }
   // validates the searcher config by building it
   NewSearchMethod(cfg["searcher"]);
+  // warm start (reference experiment.go:112, experiment_utils.go:16-45): every trial of the new
+  // experiment starts from the given checkpoint (or the source trial's latest checkpoint)
+  const Json& sc = cfg["searcher"];
+  if (sc.has("source_checkpoint_uuid") || sc.has("source_trial_id")) {
+    Json ck;
+    if (sc.has("source_checkpoint_uuid")) {
+      for (auto& c : store_->Where("checkpoints", "uuid", sc["source_checkpoint_uuid"])) ck = c;
+    } else {
+      int64_t best_step = -1;
+      for (auto& c : store_->Where("checkpoints", "trial_id", sc["source_trial_id"]))
+        if (c.get_string("state", "") == "COMPLETED" && c.get_int("step_id", 0) > best_step) {
+          best_step = c.get_int("step_id", 0);
+          ck = c;
+        }
+    }
+    if (ck.is_null() || !ck["checkpoint"].is_object()) throw std::invalid_argument("warm-start checkpoint not found");
+    cfg["internal_warm_start"] = ck["checkpoint"];
+  }
   if (body.get_bool("validate_only", false)) return 0;
   *activate = body.get_bool("activate", true);
   Json row = Json::object();
@@ -430,6 +480,9 @@ void Master::InstallRoutes() {
     return J(200, j);
   });
   http_.Route("GET", "/master/config", [this](const net::Request&) { return J(200, cfg_.ToJson()); });
+  http_.Route("GET", "/logs", [](const net::Request& r) {
+    return J(200, MasterLogTail(std::stoll(r.Query("offset", "0")), std::stoll(r.Query("limit", "25000"))));
+  });
 
   // ---------------------------------------------------------------------- experiments
   http_.Route("POST", "/experiments", [this](const net::Request& r) {

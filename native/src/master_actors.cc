@@ -23,7 +23,7 @@ namespace master {
 using actor::Context;
 using actor::Ref;
 
-static void Log(const std::string& s) { std::fprintf(stderr, "[det-master] %s\n", s.c_str()); }
+static void Log(const std::string& s) { MasterLog(s); }
 
 // =========================================================================== resource pool
 ResourcePoolActor::ResourcePoolActor(Master* m, std::string name)
@@ -174,7 +174,7 @@ void ExperimentActor::ProcessOps(Context& ctx, const Ops& ops) {
       case Op::Kind::Create: {
         std::string rid = RequestIDString(op.request_id);
         if (ctx.Child(rid)) break;
-        Json warm;
+        Json warm = config_["internal_warm_start"];
         if (op.has_checkpoint) {
           // PBT: warm start from the checkpoint of the parent trial's latest checkpoint
           auto it = latest_ckpt_.find(RequestIDString(op.checkpoint_request_id));

@@ -181,6 +181,20 @@ def test_command_runs_on_agent(cluster):
     assert any("hello from command" in l["message"] for l in cl.get(f"/commands/{cid}/logs"))
 
 
+def test_warm_start_from_source_trial(cluster):
+    cl, eid = submit(cluster, noop_config({"name": "single", "max_length": {"batches": 10}},
+                                          min_validation_period={"batches": 5}))
+    assert cl.wait_for_experiment(eid, timeout=120) == "COMPLETED"
+    src = cl.experiment(eid)["trials"][0]["id"]
+    cfg = noop_config({"name": "single", "max_length": {"batches": 5}, "source_trial_id": src})
+    cl, eid2 = submit(cluster, cfg)
+    assert cl.wait_for_experiment(eid2, timeout=120) == "COMPLETED"
+    t = cl.get(f"/trials/{cl.experiment(eid2)['trials'][0]['id']}")
+    # the source ended at 0.9 * 0.9^2 after two steps; one more step continues from there
+    loss = t["steps"][0]["metrics"]["avg_metrics"]["loss"]
+    assert loss == pytest.approx(0.9 * 0.9 ** 3, rel=1e-6)
+
+
 def test_master_restart_resumes_experiment(tmp_path):
     c = LocalCluster(agents=1, slots_per_agent=1, store_dir=str(tmp_path / "store"),
                      checkpoint_dir=str(tmp_path / "ckpt"), log_dir=str(tmp_path), tick_ms=50)
