@@ -37,6 +37,7 @@ def parse() -> argparse.Namespace:
                     help="per-GPU batch (weak scaling); 512 uses the 288 GB HBM of an MI355X")
     ap.add_argument("--amp", default=os.environ.get("DET_BENCH_AMP", "O2"), choices=["O0", "O1", "O2"])
     ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--image-size", type=int, default=224, help="(smoke tests only; the metric is 224)")
     ap.add_argument("--bucket-mb", type=int, default=int(os.environ.get("DET_BENCH_BUCKET_MB", "64")))
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true", help="stock MIOpen BN + separate add/ReLU (A/B)")
@@ -74,6 +75,7 @@ def main() -> None:
             "amp": args.amp,
             "channels_last": not args.no_channels_last,
             "fused_bn": not args.no_fused_bn,
+            "image_size": args.image_size,
         },
         "resources": {"slots_per_trial": world},
         "optimizations": {"tensor_fusion_threshold": args.bucket_mb},
@@ -130,13 +132,13 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16" if args.amp != "O0" else "fp32",
-            "data": "synthetic (random uint8 224x224x3 images, random labels; random-init weights)",
+            "data": f"synthetic (random uint8 {args.image_size}x{args.image_size}x3 images, random labels; random-init weights)",
             "config": {
                 "model": args.arch,
                 "global_batch": gbs,
                 "per_gpu_batch": args.batch_per_gpu,
                 "seq_len": None,
-                "image_size": 224,
+                "image_size": args.image_size,
                 "parallelism": f"dp{world}",
                 "amp": args.amp,
                 "optimizer": "SGD-momentum (fused arena HIP kernel)",

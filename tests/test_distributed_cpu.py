@@ -1,4 +1,5 @@
 """Multi-process data parallelism on CPU (gloo): N ranks x per-slot batch == 1 rank x global batch."""
+import json
 import os
 import socket
 import subprocess
@@ -60,3 +61,22 @@ def test_dp2_bf16_compression_close(tmp_path):
     ref = torch.load(str(tmp_path / "single.0.pt"))
     r0 = torch.load(str(tmp_path / "dpc.0.pt"))
     torch.testing.assert_close(r0, ref, rtol=5e-2, atol=5e-3)
+
+
+def test_bench_two_ranks_gloo_smoke(tmp_path):
+    """bench.py under torch.distributed.run with 2 CPU ranks: the exact multi-GPU code path of the
+    driver's scaling run (bucketer + grad sink + fused optimizer + metric gather), on gloo."""
+    import subprocess
+    import sys
+
+    from determined_1_amd.deploy.local import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(repo, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--arch", "resnet18", "--batch-per-gpu", "2",
+                        "--image-size", "32", "--amp", "O0"], capture_output=True, text=True, timeout=600, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
