@@ -455,7 +455,8 @@ def _metrics_to_host(batch_metrics: List[Dict[str, Any]]) -> List[Dict[str, Any]
     for i, m in enumerate(batch_metrics):
         for k, v in m.items():
             if isinstance(v, torch.Tensor):
-                flat.append(v)
+                # numpy has no bfloat16: widen low-precision metrics (O2 models) on device
+                flat.append(v.detach().float() if v.dtype in (torch.bfloat16, torch.float16) else v.detach())
                 where.append((i, k))
     if not flat:
         return batch_metrics
@@ -479,7 +480,8 @@ def _metrics_to_host(batch_metrics: List[Dict[str, Any]]) -> List[Dict[str, Any]
 def _convert_metrics_to_numpy(metrics: Dict[str, Any]) -> Dict[str, Any]:
     for k, v in metrics.items():
         if isinstance(v, torch.Tensor):
-            metrics[k] = v.cpu().numpy()
+            v = v.detach()
+            metrics[k] = (v.float() if v.dtype in (torch.bfloat16, torch.float16) else v).cpu().numpy()
     return metrics
 
 

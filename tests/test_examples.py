@@ -16,7 +16,7 @@ SHRINK = {
                          "train_records": 16, "validation_records": 4, "amp": "O0", "channels_last": False},
     "bert_squad_pytorch": {"num_hidden_layers": 1, "hidden_size": 64, "num_attention_heads": 2,
                            "intermediate_size": 128, "max_seq_length": 128, "global_batch_size": 2,
-                           "train_records": 8, "validation_records": 4, "amp": "O0"},
+                           "train_records": 8, "validation_records": 4, "amp": "O2"},
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
     "mnist_pytorch": {"global_batch_size": 4},
     "gan_mnist_pytorch": {"global_batch_size": 4},
