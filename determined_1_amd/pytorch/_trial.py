@@ -16,6 +16,7 @@ MI355X-specific changes to the loop:
 import logging
 import pathlib
 import random
+import time
 from abc import abstractmethod
 from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple, Union, cast
 
@@ -222,8 +223,11 @@ class PyTorchTrialController(trial.LoopTrialController):
         start, end = total_batches_processed, total_batches_processed + num_batches
         per_batch = []  # type: List[Dict[str, Any]]
         num_inputs = 0
+        timers = self.context._timers
         for batch_idx in range(start, end):
+            t_data = time.perf_counter()
             n, batch = next(self.training_iterator)
+            timers.batch_start(time.perf_counter() - t_data)
             num_inputs += n
             self.context._current_batch_idx = batch_idx
             self.context._loss_ids = {}
@@ -238,6 +242,7 @@ class PyTorchTrialController(trial.LoopTrialController):
                 self._auto_step_lr_scheduler_per_batch(batch_idx, lr_scheduler)
             per_batch.append({k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in tr_metrics.items()})
         per_batch = _metrics_to_host(per_batch)
+        self.last_step_timers = timers.report(step_id)
         if self.dist_config.use and self.dist_config.average_training_metrics:
             per_batch = self._average_training_metrics(per_batch)
         if self.dist_config.use:
