@@ -126,7 +126,9 @@ def make_amp_config(device: torch.device, opt_level: str, cast_model_type: Optio
     return AmpConfig(opt_level, dtype, keep_bn, scaler)
 
 
-_BN_TYPES = (torch.nn.modules.batchnorm._BatchNorm, torch.nn.GroupNorm, torch.nn.LayerNorm)
+# apex O2 keeps only BatchNorm in fp32 (F.batch_norm accepts a bf16 input with fp32 affine
+# params); LayerNorm/GroupNorm require matching dtypes, so they are cast with the rest.
+_BN_TYPES = (torch.nn.modules.batchnorm._BatchNorm,)
 
 
 def cast_model(model: torch.nn.Module, dtype: torch.dtype, keep_batchnorm_fp32: bool) -> torch.nn.Module:
