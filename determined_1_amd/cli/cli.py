@@ -195,7 +195,19 @@ def cmd_trial_describe(args: argparse.Namespace) -> None:
 
 
 def cmd_trial_logs(args: argparse.Namespace) -> None:
-    for l in MasterClient(args.master).trial_logs(args.trial_id, follow=args.follow):
+    c = MasterClient(args.master)
+    if args.tail is not None or args.rank is not None or args.stdtype or args.contains:
+        params = {"limit": args.tail if args.tail is not None else 100000, "tail": "true" if args.tail else "false"}
+        if args.rank is not None:
+            params["rank_id"] = args.rank
+        if args.stdtype:
+            params["stdtype"] = args.stdtype
+        if args.contains:
+            params["contains"] = args.contains
+        for l in c.get(f"/trials/{args.trial_id}/logs", **params):
+            print(l["message"])
+        return
+    for l in c.trial_logs(args.trial_id, follow=args.follow):
         print(l["message"])
 
 
@@ -457,6 +469,10 @@ def build_parser() -> argparse.ArgumentParser:
     lg = t.add_parser("logs")
     lg.add_argument("trial_id", type=int)
     lg.add_argument("--follow", "-f", action="store_true")
+    lg.add_argument("--tail", type=int)
+    lg.add_argument("--rank", type=int)
+    lg.add_argument("--stdtype", choices=["stdout", "stderr"])
+    lg.add_argument("--contains")
     lg.set_defaults(func=cmd_trial_logs)
     k = t.add_parser("kill")
     k.add_argument("trial_id", type=int)

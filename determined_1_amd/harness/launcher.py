@@ -13,6 +13,7 @@ import os
 import secrets
 import subprocess
 import sys
+import threading
 import time
 from multiprocessing.connection import Client, Connection, Listener, wait
 from typing import Any, Dict, List, Optional
@@ -23,6 +24,12 @@ from determined_1_amd.env import EnvContext, RendezvousInfo
 
 class WorkerFailed(RuntimeError):
     pass
+
+
+def _prefix_lines(stream: Any, prefix: str) -> None:
+    for raw in iter(stream.readline, b""):
+        sys.stdout.write(prefix + raw.decode(errors="replace"))
+        sys.stdout.flush()
 
 
 class SubprocessLauncher:
@@ -42,6 +49,7 @@ class SubprocessLauncher:
         chief_host = rendezvous.get_ip_addresses()[0] if rendezvous.get_size() else "127.0.0.1"
         store_port = constants.DIST_STORE_PORT + int(env.det_trial_unique_port_offset)
         self.procs = []  # type: List[subprocess.Popen]
+        self._log_threads = []  # type: List[threading.Thread]
         for local_rank in range(local_size):
             e = dict(os.environ)
             e.update(extra_env or {})
@@ -61,7 +69,14 @@ class SubprocessLauncher:
                 "DET_RENDEZVOUS_RANK": str(cross_rank),
                 "DET_LOAD_PATH": str(load_path) if load_path else "",
             })
-            self.procs.append(subprocess.Popen([python, "-m", "determined_1_amd.exec.worker_process"], env=e))
+            proc = subprocess.Popen([python, "-m", "determined_1_amd.exec.worker_process"], env=e,
+                                    stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+            self.procs.append(proc)
+            # rank-prefixed log lines (reference exec/worker_process_wrapper.py:15-18)
+            rank = cross_rank * local_size + local_rank
+            t = threading.Thread(target=_prefix_lines, args=(proc.stdout, f"[rank={rank}] "), daemon=True)
+            t.start()
+            self._log_threads.append(t)
         self.conns = [None] * local_size  # type: List[Optional[Connection]]
         deadline = time.time() + constants.DIST_STARTUP_TIMEOUT_SECONDS
         self.listener._listener._socket.settimeout(1.0)  # type: ignore[attr-defined]
@@ -129,6 +144,8 @@ class SubprocessLauncher:
                 p.wait(timeout=max(0.1, deadline - time.time()))
             except subprocess.TimeoutExpired:
                 p.kill()
+        for t in self._log_threads:
+            t.join(timeout=5)
         self.listener.close()
 
 

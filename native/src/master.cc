@@ -710,16 +710,27 @@ void Master::InstallRoutes() {
     return J(200, t);
   });
   http_.Route("GET", "/trials/:id/logs", [this](const net::Request& r) {
+    // filters as the reference TrialLogsRequest: rank_id, stdtype, container_id, agent (via
+    // container), substring match, head/tail limits
     int64_t id = IntParam(r, "id");
     int64_t offset = std::stoll(r.Query("offset", "0"));
     int64_t limit = std::stoll(r.Query("limit", "100000"));
-    Json out = Json::array();
-    int64_t i = 0;
+    const std::string rank = r.Query("rank_id", ""), stdtype = r.Query("stdtype", ""),
+                      cid = r.Query("container_id", ""), grep = r.Query("contains", "");
+    const bool tail = r.Query("tail", "false") == "true";
+    std::vector<Json> hits;
     for (auto& l : store_->Where("trial_logs", "trial_id", Json(id))) {
       if (l["id"].as_int() <= offset) continue;
-      if (i++ >= limit) break;
-      out.push_back(l);
+      if (!rank.empty() && std::to_string(l.get_int("rank_id", 0)) != rank) continue;
+      if (!stdtype.empty() && l.get_string("stdtype", "") != stdtype) continue;
+      if (!cid.empty() && l.get_string("container_id", "") != cid) continue;
+      if (!grep.empty() && l.get_string("message", "").find(grep) == std::string::npos) continue;
+      hits.push_back(l);
     }
+    size_t n = std::min<size_t>(hits.size(), static_cast<size_t>(std::max<int64_t>(0, limit)));
+    size_t start = tail ? hits.size() - n : 0;
+    Json out = Json::array();
+    for (size_t i = start; i < start + n; ++i) out.push_back(hits[i]);
     return J(200, out);
   });
   http_.Route("POST", "/trials/:id/kill", [this](const net::Request& r) {

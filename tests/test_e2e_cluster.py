@@ -142,6 +142,8 @@ def test_distributed_gloo_trial_through_launcher(cluster):
     logs = "\n".join(l["message"] for l in cl.trial_logs(t["id"]))
     assert st == "COMPLETED", logs[-3000:]
     tr = cl.get(f"/trials/{t['id']}")
+    # every rank's output reaches the trial logs with its rank prefix (reference test_system.py:544)
+    assert "[rank=0]" in logs and "[rank=1]" in logs
     w = tr["steps"][-1]["metrics"]["batch_metrics"][-1]["weight"]
     # 6 SGD steps of w' = w + 2 lr (1 - w) from w=0 (identical on both ranks; averaged grads)
     w_exp = 0.0
