@@ -162,6 +162,28 @@ def _validate_hparams(hps: Dict[str, Any], errs: List[str], grid: bool) -> int:
     return n
 
 
+def _is_number(v: Any) -> bool:
+    return isinstance(v, (int, float)) and not isinstance(v, bool)
+
+
+def _validate_global_batch_size(hps: Dict[str, Any], errs: List[str]) -> None:
+    """reference master/pkg/model/hyperparameters_config.go:20-44."""
+    if "global_batch_size" not in hps:
+        errs.append("global_batch_size hyperparameter must be specified")
+        return
+    b = hps["global_batch_size"]
+    if isinstance(b, dict) and b.get("type") == "categorical":
+        vals = b.get("vals", [])
+    elif isinstance(b, dict) and b.get("type") == "const":
+        vals = [b.get("val")]
+    elif isinstance(b, dict):
+        vals = []  # ranged types are numeric by construction
+    else:
+        vals = [b]
+    if not all(_is_number(v) for v in vals):
+        errs.append("global_batch_size hyperparameter must be a numeric value")
+
+
 def validate_experiment_config(cfg: Dict[str, Any], require_entrypoint: bool = True) -> List[str]:
     errs = []  # type: List[str]
     unknown = set(cfg) - TOP_LEVEL_KEYS
@@ -232,6 +254,7 @@ def validate_experiment_config(cfg: Dict[str, Any], require_entrypoint: bool = T
     if EPOCHS in units and not cfg.get("records_per_epoch", 0) > 0:
         errs.append("Must specify records_per_epoch when any configuration is in terms of epochs")
     hps = cfg.get("hyperparameters", {}) or {}
+    _validate_global_batch_size(hps, errs)
     n_grid = _validate_hparams(hps, errs, grid=(name == "grid"))
     if name == "grid" and n_grid > MAX_ALLOWED_TRIALS:
         errs.append(f"number of trials for grid search must be <= {MAX_ALLOWED_TRIALS}")
@@ -241,6 +264,14 @@ def validate_experiment_config(cfg: Dict[str, Any], require_entrypoint: bool = T
     for k in ("save_experiment_best", "save_trial_best", "save_trial_latest"):
         if cs.get(k, 0) < 0:
             errs.append(f"{k} must be >= 0")
+    if cfg.get("checkpoint_policy", "best") not in ("best", "all", "none"):
+        errs.append("checkpoint_policy must be one of best, all, none")
+    if (cfg.get("resources", {}) or {}).get("slots_per_trial", 1) < 0:
+        errs.append("slots_per_trial must be >= 0")
+    if (cfg.get("optimizations", {}) or {}).get("aggregation_frequency", 1) < 1:
+        errs.append("aggregation_frequency must be >= 1")
+    if cfg.get("scheduling_unit", 100) <= 0:
+        errs.append("scheduling_unit must be > 0")
     if cs.get("type") not in (None, "shared_fs", "s3", "gcs", "hdfs"):
         errs.append(f"checkpoint_storage.type: unknown {cs.get('type')!r}")
     if cfg.get("checkpoint_policy", "best") not in ("best", "all", "none"):

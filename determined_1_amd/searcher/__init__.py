@@ -28,6 +28,8 @@ def _lib() -> ctypes.CDLL:
         lib.detcore_nprand.restype = ctypes.c_void_p
         lib.detcore_json_roundtrip.argtypes = [ctypes.c_char_p]
         lib.detcore_json_roundtrip.restype = ctypes.c_void_p
+        lib.detcore_merge_config.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
+        lib.detcore_merge_config.restype = ctypes.c_void_p
         lib._det_searcher_sigs = True
     return lib
 
@@ -126,6 +128,14 @@ def nprand(seed: int, op: str, n: int, arg: int = 0) -> List[Any]:
 
 def json_roundtrip(text: str) -> Any:
     return _take(_lib().detcore_json_roundtrip(text.encode()))
+
+
+def master_merge_config(user: Dict[str, Any], master_checkpoint_storage: Optional[Dict[str, Any]] = None,
+                        template: Optional[Dict[str, Any]] = None, seed: int = 0) -> Dict[str, Any]:
+    """The experiment config exactly as det-master would store it: ``{"config", "errors"}``."""
+    enc = lambda d: json.dumps(d).encode() if d is not None else b""  # noqa: E731
+    return _take(_lib().detcore_merge_config(enc(user), enc(master_checkpoint_storage), enc(template),
+                                             seed & 0xFFFFFFFF))
 
 
 def short_form(ops: List[Dict[str, Any]]) -> str:

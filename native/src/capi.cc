@@ -5,6 +5,7 @@
 #include <memory>
 #include <string>
 
+#include "detcore/config.h"
 #include "detcore/json.h"
 #include "detcore/searcher.h"
 
@@ -154,6 +155,25 @@ char* detcore_nprand(uint32_t seed, const char* op, int64_t arg, int64_t n) {
       else if (o == "request_id") out.push_back(detcore::RequestIDString(detcore::NewRequestID(r)));
       else throw std::invalid_argument("unknown nprand op " + o);
     }
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+// Master-side experiment-config merge + validation, exposed so tests can pin the Python schema
+// (determined_1_amd/config) to the one the master applies.
+char* detcore_merge_config(const char* user, const char* master_storage, const char* tmpl, uint32_t seed) {
+  try {
+    Json u = Json::parse(user && *user ? user : "{}");
+    Json ms = master_storage && *master_storage ? Json::parse(master_storage) : Json();
+    Json t = tmpl && *tmpl ? Json::parse(tmpl) : Json();
+    Json out = Json::object();
+    Json merged = detcore::MergeExperimentConfig(u, ms, t, seed);
+    Json errs = Json::array();
+    for (auto& e : detcore::ValidateExperimentConfig(merged)) errs.push_back(e);
+    out["config"] = merged;
+    out["errors"] = errs;
     return dup(out.dump());
   } catch (const std::exception& e) {
     return err(e);

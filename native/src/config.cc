@@ -1,6 +1,7 @@
 // Experiment/master config (see include/detcore/config.h).
 #include "detcore/config.h"
 
+#include <algorithm>
 #include <set>
 
 #include "detcore/searcher.h"
@@ -96,6 +97,8 @@ Json MergeExperimentConfig(const Json& user, const Json& master_ckpt, const Json
   return cfg;
 }
 
+static constexpr int kMaxAllowedTrials = 2000;
+
 static bool ParseLen(const Json& v, Length* out) {
   try {
     *out = Length::FromJson(v);
@@ -149,39 +152,102 @@ std::vector<std::string> ValidateExperimentConfig(const Json& cfg) {
       errs.push_back("mode must be one of aggressive, standard, conservative");
     if (s.get_int("max_rungs", 0) <= 0) errs.push_back("max_rungs must be > 0");
   }
+  if ((name == "async_halving" || name == "adaptive_asha") && s.get_int("max_concurrent_trials", 0) < 0)
+    errs.push_back("max_concurrent_trials must be >= 0");
+  if ((name == "adaptive" || name == "sync_halving") && s.has("budget") && s.has("max_length")) {
+    Length b, m;
+    if (ParseLen(s["budget"], &b) && ParseLen(s["max_length"], &m)) {
+      if (b.unit != m.unit)
+        errs.push_back("max_length and budget must be specified in terms of the same unit");
+      else if (name == "adaptive" && !(b.units > m.units))
+        errs.push_back("budget must be greater than max_length");
+    }
+  }
+  if (name == "adaptive_simple" && s.get_int("max_trials", 0) > kMaxAllowedTrials)
+    errs.push_back("max_trials must be <= " + std::to_string(kMaxAllowedTrials));
   if (name == "pbt") {
     if (s.get_int("population_size", 0) <= 0) errs.push_back("population_size must be > 0");
     if (s.get_int("num_rounds", 0) <= 0) errs.push_back("num_rounds must be > 0");
+    double tf = s["replace_function"].get_double("truncate_fraction", 0.0);
+    if (!(tf >= 0.0 && tf <= 0.5)) errs.push_back("truncate_fraction must be in [0, 0.5]");
+    double rp = s["explore_function"].get_double("resample_probability", 0.0);
+    if (!(rp >= 0.0 && rp <= 1.0)) errs.push_back("resample_probability must be in [0, 1]");
+    double pf = s["explore_function"].get_double("perturb_factor", 0.0);
+    if (!(pf >= 0.0 && pf <= 1.0)) errs.push_back("perturb_factor must be in [0, 1]");
   }
   for (const char* f : {"min_validation_period", "min_checkpoint_period"}) {
     if (!cfg.has(f)) continue;
     Length l;
     if (!ParseLen(cfg[f], &l)) errs.push_back(std::string(f) + ": invalid length");
-    else epochs |= l.unit == Unit::Epochs && l.units > 0;
+    else epochs |= l.unit == Unit::Epochs;
   }
   if (epochs && cfg.get_int("records_per_epoch", 0) <= 0)
     errs.push_back("Must specify records_per_epoch when any configuration is in terms of epochs");
-  if (cfg["hyperparameters"].is_object()) {
-    for (auto& kv : cfg["hyperparameters"].as_object()) {
+  const Json& hps = cfg["hyperparameters"];
+  // global_batch_size (reference hyperparameters_config.go:20-44)
+  if (!hps.is_object() || !hps.has("global_batch_size")) {
+    errs.push_back("global_batch_size hyperparameter must be specified");
+  } else {
+    const Json& b = hps["global_batch_size"];
+    std::vector<const Json*> vals;
+    if (b.is_object() && b.get_string("type", "") == "categorical" && b["vals"].is_array()) {
+      for (size_t i = 0; i < b["vals"].size(); ++i) vals.push_back(&b["vals"][i]);
+    } else if (b.is_object() && b.get_string("type", "") == "const") {
+      vals.push_back(&b["val"]);
+    } else if (!b.is_object()) {
+      vals.push_back(&b);
+    }
+    for (auto* v : vals)
+      if (!v->is_number()) {
+        errs.push_back("global_batch_size hyperparameter must be a numeric value");
+        break;
+      }
+  }
+  double n_grid = 1;
+  std::vector<std::string> missing;
+  if (hps.is_object()) {
+    for (auto& kv : hps.as_object()) {
       const Json& hp = kv.second;
       if (!hp.is_object() || !hp.has("type")) continue;
       std::string t = hp["type"].as_string();
       if (t == "const") {
         if (!hp.has("val")) errs.push_back("hyperparameters." + kv.first + ": const needs val");
       } else if (t == "int" || t == "double" || t == "log") {
-        if (!(hp.get_double("maxval", 0) > hp.get_double("minval", 0)))
-          errs.push_back("hyperparameters." + kv.first + ": minval is greater than maxval");
-        if (name == "grid" && !hp.has("count"))
-          errs.push_back("hyperparameters." + kv.first + ": grid search needs a count");
+        double lo = hp.get_double("minval", 0), hi = hp.get_double("maxval", 0);
+        if (!(hi > lo)) errs.push_back("hyperparameters." + kv.first + ": minval is greater than maxval");
+        if (t == "log" && !(hp.get_double("base", 0) > 0))
+          errs.push_back("hyperparameters." + kv.first + ": base must be >= 0");
+        bool has_count = hp.has("count") && !hp["count"].is_null();
+        if (has_count && hp.get_int("count", 0) <= 0)
+          errs.push_back("hyperparameters." + kv.first + ": count must be >= 0");
+        if (name == "grid") {
+          if (!has_count) {
+            missing.push_back(kv.first);
+          } else {
+            double c = static_cast<double>(hp.get_int("count", 0));
+            // int counts clamp to the size of the range (reference grid.go)
+            n_grid *= (t == "int" && c > hi - lo) ? hi - lo : c;
+          }
+        }
       } else if (t == "categorical") {
         if (!hp["vals"].is_array() || hp["vals"].size() == 0)
           errs.push_back("hyperparameters." + kv.first + ": must have at least one category");
+        n_grid *= std::max<size_t>(1, hp["vals"].is_array() ? hp["vals"].size() : 0);
       } else {
         errs.push_back("hyperparameters." + kv.first + ": unknown type '" + t + "'");
       }
     }
   }
+  if (name == "grid" && !missing.empty()) {
+    std::string m = "these hyperparameters must specify counts for grid search: ";
+    for (size_t i = 0; i < missing.size(); ++i) m += (i ? ", " : "") + missing[i];
+    errs.push_back(m);
+  }
+  if (name == "grid" && n_grid > kMaxAllowedTrials)
+    errs.push_back("number of trials for grid search must be <= " + std::to_string(kMaxAllowedTrials));
   if (cfg.get_int("max_restarts", 0) < 0) errs.push_back("max_restarts must be >= 0");
+  for (const char* k : {"save_experiment_best", "save_trial_best", "save_trial_latest"})
+    if (cfg["checkpoint_storage"].get_int(k, 0) < 0) errs.push_back(std::string(k) + " must be >= 0");
   std::string ct = cfg["checkpoint_storage"].get_string("type", "shared_fs");
   if (ct != "shared_fs" && ct != "s3" && ct != "gcs" && ct != "hdfs")
     errs.push_back("checkpoint_storage.type: unknown '" + ct + "'");
