@@ -23,6 +23,7 @@ from typing import Iterator, Optional
 from determined_1_amd import errors, storage
 from determined_1_amd.env import EnvContext
 from determined_1_amd.harness.load import prepare_controller
+from determined_1_amd.harness import timeline
 from determined_1_amd.harness.socket_manager import SocketManager
 from determined_1_amd.harness.workload_manager import build_workload_manager
 from determined_1_amd.parallel.dist import DistributedConfig, RankInfo
@@ -47,14 +48,17 @@ def local_slot_count(env: EnvContext) -> int:
 
 def main() -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [harness] %(levelname)s %(message)s")
+    timeline.mark("imports done")
     env = EnvContext.from_environ()
     if env.debug:
         faulthandler.dump_traceback_later(30, repeat=True)
     cfg = env.experiment_config
     storage_mgr = storage.build(cfg.get("checkpoint_storage", {}))
     storage.validate_manager(storage_mgr)
+    timeline.mark("storage validated")
     socket_mgr = SocketManager(env)
     rendezvous = socket_mgr.rendezvous_info
+    timeline.mark("rendezvous")
     metric_writer = None
     tb_mgr = None
     try:
@@ -87,6 +91,7 @@ def main() -> int:
         socket_mgr.close()
         return 1
     socket_mgr.close()
+    timeline.mark("exit")
     return 0
 
 

@@ -60,12 +60,19 @@ def prepare_controller(env: EnvContext, workloads: workload.Stream, load_path: O
                        rank_info: Optional[RankInfo] = None) -> trial.TrialController:
     """pre_execute_hook -> context -> Trial(context) -> controller.from_trial (reference
     ``load_controller_from_trial``)."""
+    from determined_1_amd.harness import timeline
+
     trial_class = load_trial_class(env.experiment_config["entrypoint"])
+    timeline.mark("user code imported")
     controller_cls = trial_class.trial_controller_class
     assert controller_cls is not None, f"{trial_class.__name__} has no trial_controller_class"
     controller_cls.pre_execute_hook(env, dist_config)
+    timeline.mark("pre_execute_hook (device init)")
     rank = rank_info or RankInfo.from_env()
     context = trial_class.trial_context_class(env, dist_config, rank)
     logging.info("constructing %s (rank %d/%d)", trial_class.__name__, rank.rank, rank.size)
     trial_inst = trial_class(context)
-    return controller_cls.from_trial(trial_inst, context, env, workloads, load_path, rendezvous, dist_config)
+    timeline.mark("trial constructed")
+    ctrl = controller_cls.from_trial(trial_inst, context, env, workloads, load_path, rendezvous, dist_config)
+    timeline.mark("controller ready")
+    return ctrl

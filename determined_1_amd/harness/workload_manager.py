@@ -21,6 +21,7 @@ from typing import Any, Callable, Dict, Optional
 import numpy as np
 
 from determined_1_amd import errors, util, workload
+from determined_1_amd.harness import timeline
 from determined_1_amd.env import EnvContext, RendezvousInfo
 from determined_1_amd.storage import StorageManager, StorageMetadata, list_directory
 
@@ -50,6 +51,7 @@ class WorkloadManager(workload.Source):
         for w, args, respond in self.stream:
             self.check_sane_workload(w)
             k = w.kind
+            timeline.mark(f"start {k.name} step={w.step_id}")
             if k == workload.Workload.Kind.RUN_STEP:
                 yield from self.yield_train_for_step(w, args, respond)
             elif k == workload.Workload.Kind.COMPUTE_VALIDATION_METRICS:
@@ -61,6 +63,7 @@ class WorkloadManager(workload.Source):
                 return
             else:
                 raise AssertionError(f"unexpected workload {w}")
+            timeline.mark(f"done {k.name} step={w.step_id}")
 
     @staticmethod
     def _exited(message: Dict[str, Any]) -> Optional[str]:

@@ -77,7 +77,13 @@ class SyntheticTokens(tud.Dataset):
 class SyntheticClassification(tud.Dataset):
     """Learnable synthetic classification data: each class has a fixed random template and a
     sample is ``template[label] + noise``, so accuracy rises with training (stands in for MNIST /
-    CIFAR-10, which cannot be downloaded here)."""
+    CIFAR-10, which cannot be downloaded here).
+
+    Labels are drawn once per index and noise comes from a fixed pool indexed by a hash of the
+    sample index, so ``__getitems__`` builds a whole batch with two gathers instead of one
+    generator + ``randn`` per sample (which dominated short ASHA trials' validation passes)."""
+
+    NOISE_POOL = 1024
 
     def __init__(self, length: int, shape: Sequence[int], num_classes: int = 10, noise: float = 1.0,
                  seed: int = 0, template_seed: int = 1234) -> None:
@@ -88,15 +94,28 @@ class SyntheticClassification(tud.Dataset):
         self.seed = seed
         gt = torch.Generator().manual_seed(template_seed)
         self.templates = torch.randn((num_classes,) + self.shape, generator=gt)
+        g = torch.Generator().manual_seed(seed * 1000003 + 17)
+        self.labels = torch.randint(0, num_classes, (self.length,), generator=g)
+        pool = min(self.NOISE_POOL, self.length)
+        self.noise_pool = noise * torch.randn((pool,) + self.shape, generator=g)
+        self._mul = 2654435761 % pool or 1  # Knuth multiplicative hash over the pool
 
     def __len__(self) -> int:
         return self.length
 
+    def _noise_index(self, idx: torch.Tensor) -> torch.Tensor:
+        return (idx * self._mul + self.seed) % self.noise_pool.shape[0]
+
     def __getitem__(self, i: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
-        y = int(torch.randint(0, self.num_classes, (1,), generator=g))
-        x = self.templates[y] + self.noise * torch.randn(self.shape, generator=g)
-        return x, torch.tensor(y, dtype=torch.int64)
+        y = self.labels[i]
+        j = int(self._noise_index(torch.tensor(i)))
+        return self.templates[y] + self.noise_pool[j], y.clone()
+
+    def __getitems__(self, idx: Sequence[int]) -> List[Tuple[torch.Tensor, torch.Tensor]]:
+        ii = torch.as_tensor(list(idx), dtype=torch.int64)
+        y = self.labels.index_select(0, ii)
+        x = self.templates.index_select(0, y) + self.noise_pool.index_select(0, self._noise_index(ii))
+        return list(zip(x.unbind(0), y.unbind(0)))
 
 
 class SyntheticSQuAD(tud.Dataset):

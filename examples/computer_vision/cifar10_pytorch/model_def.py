@@ -25,12 +25,13 @@ class CIFARTrial(pytorch.PyTorchTrial):
         self.loss = nn.CrossEntropyLoss()
 
     def build_training_data_loader(self) -> pytorch.DataLoader:
+        # in-memory synthetic data: batched __getitems__ is cheaper than worker-process IPC
         ds = SyntheticClassification(50000, (3, 32, 32), noise=3.0)
-        return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size(), shuffle=True, num_workers=2)
+        return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size(), shuffle=True)
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:
         ds = SyntheticClassification(10000, (3, 32, 32), noise=3.0, seed=1)
-        return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size(), num_workers=2)
+        return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size())
 
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:
         x, y = batch

@@ -19,6 +19,43 @@ REPO = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 
 
+def summarize_timelines(cl, trials, t0):
+    """Mean seconds per trial container spent in each harness phase (from DET_TIMELINE logs);
+    full per-trial timelines go to $DET_BENCH_LOGDIR/asha_timeline.txt."""
+    import re
+    from collections import defaultdict
+
+    pat = re.compile(r"\[timeline\] \+([0-9.]+)s (.*)$")
+    phases = defaultdict(list)
+    lines = []
+    for t in trials:
+        by_container = defaultdict(list)
+        for rec in cl.get(f"/trials/{t['id']}/logs"):
+            m = pat.search(rec.get("message", ""))
+            if m:
+                by_container[rec.get("container_id")].append((float(m.group(1)), m.group(2)))
+        for cid, marks in by_container.items():
+            lines.append(f"trial {t['id']} container {cid}")
+            prev = 0.0
+            workload = 0.0
+            for ts, label in marks:
+                lines.append(f"  +{ts:8.3f}s (+{ts - prev:6.3f}) {label}")
+                if label.startswith("done "):
+                    workload += ts - prev
+                elif not label.startswith("start "):
+                    phases[label].append(ts - prev)
+                else:
+                    phases["between workloads"].append(ts - prev)
+                prev = ts
+            phases["workloads"].append(workload)
+            phases["total"].append(prev)
+    out_dir = os.environ.get("DET_BENCH_LOGDIR", "/tmp")
+    with open(os.path.join(out_dir, "asha_timeline.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    n = max(1, len(phases["total"]))
+    return {k: round(sum(v) / n, 3) for k, v in phases.items()}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-length-batches", type=int, default=400)
@@ -34,9 +71,13 @@ def main() -> None:
     cfg = yaml.safe_load((ex / "adaptive.yaml").read_text())
     cfg["searcher"]["max_length"] = {"batches": args.max_length_batches}
     cfg["searcher"]["max_trials"] = args.max_trials
-    cfg["min_validation_period"] = {"batches": max(1, args.max_length_batches // 4)}
+    # validate only where the searcher asks (end of each rung); the real config validates every
+    # epoch = 1/32 of max_length, which a scaled-down max_length would turn into a validation storm
+    cfg.pop("min_validation_period", None)
     cfg["scheduling_unit"] = 50
     cfg.pop("records_per_epoch", None)
+    env_vars = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
+    env_vars.append("DET_TIMELINE=1")
     busy = []
     stop = threading.Event()
 
@@ -60,11 +101,13 @@ def main() -> None:
         stop.set()
         e = cl.experiment(eid)
         done = sum(1 for t in e["trials"] if t["state"] == "COMPLETED")
+        timeline = summarize_timelines(cl, e["trials"], t0)
         slots = sum(len(a["slots"]) for a in cl.get("/agents"))
         print(json.dumps({"metric": "ASHA trials/hr (16-trial adaptive_asha CIFAR-10)",
                           "value": round(done * 3600.0 / wall, 2), "unit": "trials/hr", "state": state,
                           "trials_completed": done, "wall_s": round(wall, 1), "slots": slots,
                           "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
+                          "per_container_s": timeline,
                           "config": {"max_length_batches": args.max_length_batches, "max_trials": args.max_trials,
                                      "searcher": "adaptive_asha", "amp": cfg["hyperparameters"].get("amp")}}),
               flush=True)
