@@ -21,6 +21,7 @@ namespace master {
 
 // ------------------------------------------------------------------ resource-pool messages
 struct SchedulerTick {};
+struct SchedulerKick {};  // event-driven pass between ticks (task added / released, agent joined)
 struct AddAgent {
   sched::Agent agent;
 };
@@ -139,6 +140,9 @@ class ResourcePoolActor : public actor::Actor {
   sched::FitMethod fit_;
   std::map<std::string, actor::Ref> handlers_;
   std::set<std::string> released_;
+  bool kick_pending_ = false;
+  void Kick(actor::Context& ctx);
+  void SchedulePass(actor::Context& ctx);
 };
 
 class ExperimentActor : public actor::Actor {

@@ -33,12 +33,37 @@ ResourcePoolActor::ResourcePoolActor(Master* m, std::string name)
   st_.preemption = m->config().priority_preemption;
 }
 
+// The reference only schedules on its periodic tick (resource_pool.go); with short HP-search
+// trials the tick latency is paid twice per trial (release, then allocate), so state changes also
+// queue one coalesced pass.  The tick remains for time-based policies and as a safety net.
+void ResourcePoolActor::Kick(Context& ctx) {
+  if (kick_pending_) return;
+  kick_pending_ = true;
+  ctx.Self()->Tell(SchedulerKick{}, ctx.Self());
+}
+
+void ResourcePoolActor::SchedulePass(Context& ctx) {
+  sched::Decision d = sched::Schedule(st_, policy_, fit_);
+  for (auto& a : d.allocate) {
+    st_.Allocate(a.first, a.second);
+    auto h = handlers_.find(a.first);
+    if (h != handlers_.end()) h->second->Tell(ResourcesAllocated{a.first, a.second}, ctx.Self());
+  }
+  for (auto& id : d.release) {
+    if (released_.count(id)) continue;
+    released_.insert(id);
+    auto h = handlers_.find(id);
+    if (h != handlers_.end()) h->second->Tell(ReleaseResources{id}, ctx.Self());
+  }
+}
+
 void ResourcePoolActor::Receive(Context& ctx) {
   if (ctx.Is<actor::PreStart>()) {
     ctx.system().NotifyAfter(ctx.Self(), std::chrono::milliseconds(static_cast<int>(m_->config().scheduler_tick_ms)),
                              SchedulerTick{});
   } else if (auto a = ctx.As<AddAgent>()) {
     st_.agents[a->agent.id] = a->agent;
+    Kick(ctx);
     Log("pool " + name_ + ": agent " + a->agent.id + " joined with " + std::to_string(a->agent.NumSlots()) + " slots");
   } else if (auto r = ctx.As<RemoveAgent>()) {
     st_.agents.erase(r->id);
@@ -52,16 +77,19 @@ void ResourcePoolActor::Receive(Context& ctx) {
     st_.AddTask(t);
     handlers_[req->task_id] = req->handler;
     released_.erase(req->task_id);
+    Kick(ctx);
   } else if (auto rel = ctx.As<ResourcesReleased>()) {
     st_.RemoveTask(rel->task_id);
     handlers_.erase(rel->task_id);
     released_.erase(rel->task_id);
+    Kick(ctx);
   } else if (auto g = ctx.As<SetGroup>()) {
     sched::Group& grp = st_.groups[g->group];
     grp.id = g->group;
     grp.weight = g->weight;
     grp.priority = g->priority;
     grp.max_slots = g->max_slots;
+    Kick(ctx);
   } else if (auto se = ctx.As<SetSlotEnabled>()) {
     auto it = st_.agents.find(se->agent);
     bool ok = false;
@@ -75,20 +103,12 @@ void ResourcePoolActor::Receive(Context& ctx) {
     }
     ctx.Respond(ok);
   } else if (ctx.Is<SchedulerTick>()) {
-    sched::Decision d = sched::Schedule(st_, policy_, fit_);
-    for (auto& a : d.allocate) {
-      st_.Allocate(a.first, a.second);
-      auto h = handlers_.find(a.first);
-      if (h != handlers_.end()) h->second->Tell(ResourcesAllocated{a.first, a.second}, ctx.Self());
-    }
-    for (auto& id : d.release) {
-      if (released_.count(id)) continue;
-      released_.insert(id);
-      auto h = handlers_.find(id);
-      if (h != handlers_.end()) h->second->Tell(ReleaseResources{id}, ctx.Self());
-    }
+    SchedulePass(ctx);
     ctx.system().NotifyAfter(ctx.Self(), std::chrono::milliseconds(static_cast<int>(m_->config().scheduler_tick_ms)),
                              SchedulerTick{});
+  } else if (ctx.Is<SchedulerKick>()) {
+    kick_pending_ = false;
+    SchedulePass(ctx);
   } else if (ctx.Is<PoolSummary>()) {
     Json out = Json::object();
     out["name"] = name_;
