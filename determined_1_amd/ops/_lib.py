@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -99,6 +99,28 @@ _SIGNATURES = {
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int] + [c_void_p] * 10,
         c_int,
     ),
+    # det_transformer.hip: fused LayerNorm / dropout / residual / GELU / bias-grad epilogues
+    "det_tf_ln_max_hidden": ([], c_int),
+    "det_tf_ln_ws_elems": ([c_i64, c_int], c_i64),
+    # stream, dtype, h, r, y, rows, H, gamma, beta, eps, p, seed, offset, mean, rstd
+    "det_tf_ln_fwd": (
+        [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_float, c_float,
+         ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p],
+        c_int,
+    ),
+    # stream, dtype, dy, h, r, mean, rstd, gamma, rows, H, p, seed, offset, dr, dh, dgamma, dbeta, dbias, ws
+    "det_tf_ln_bwd": (
+        [c_void_p, c_int] + [c_void_p] * 6 + [c_i64, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64]
+        + [c_void_p] * 6,
+        c_int,
+    ),
+    "det_tf_col_ws_elems": ([c_i64, c_int], c_i64),
+    "det_tf_gelu_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_i64], c_int),
+    # stream, dtype, da, z, dz, rows, C, dbias, ws
+    "det_tf_gelu_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
+    # stream, dtype, x, rows, C, out, ws
+    "det_tf_colsum": ([c_void_p, c_int, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
+    "det_tf_dropout_mask": ([c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p], c_int),
 }
 
 

@@ -455,7 +455,7 @@ u8_normalize_kernel(const uint8_t* __restrict__ in, TO* __restrict__ out, int64_
 // ============================================================================================
 extern "C" {
 
-int det_abi_version() { return 5; }
+int det_abi_version() { return 6; }
 
 int det_sgd_step(void* stream, int g_dtype, int out_dtype, float* p, const void* g, float* buf,
                  void* out_model, int64_t n, float lr, float momentum, float dampening, float wd,

@@ -1,0 +1,674 @@
+// det_transformer.hip — fused transformer-encoder epilogues for CDNA4 (gfx950, wave64).
+//
+// Why this exists: in the BERT-base SQuAD-shape step (profiles/r1_bert_base_bs12_o2_steady.csv,
+// 12.7 ms of GPU time per step) ~3.9 ms go to HBM-bound glue around the GEMMs: torch's
+// LayerNorm fwd/bwd (4 launches per LN), dropout + masked-scale, residual adds, GELU fwd/bwd and
+// 73 bias-gradient column reductions at ~17 us each.  These kernels fold that glue into the
+// minimum number of passes:
+//
+//   ln_fwd        y = LayerNorm(dropout(h) + r)         one pass: reads h, r; writes y, mean, rstd
+//   ln_bwd        dz = LN'(dy); dr = dz; dh = dropout'(dz) and per-block partial sums of
+//                 dgamma = sum(dy * xhat), dbeta = sum(dy), dbias = sum(dh)   (one pass)
+//   ln_finalize   reduces the partials -> dgamma, dbeta and the preceding Linear's bias grad
+//   gelu_fwd      a = gelu(z) (erf form, as BERT)
+//   gelu_bwd      dz = da * gelu'(z) with the bias-grad partials of the producing Linear fused
+//   colsum        bias grad of a plain Linear (QKV) without torch's generic reduction
+//
+// Dropout masks are never stored: a counter-based Philox4x32-10 stream keyed by (seed, offset)
+// and indexed by element/4 regenerates the identical mask in the backward pass, so a lane draws
+// exactly one Philox block for its 4 consecutive elements.
+//
+// Row kernels (LN): one wavefront per row, lane owns 4 consecutive elements at 4*(lane + 64*i),
+// i < K (K = ceil(H/256), templated, H <= 2048); the two-pass mean/variance is exact in
+// registers.  Column reductions use two levels (LDS per block, then a finalize launch) and no
+// float atomics, so every gradient is bitwise reproducible.  No host syncs anywhere.
+//
+// Reference parity: the reference runs BERT through HuggingFace modules on torch/cuDNN
+// (examples/nlp/bert_squad_pytorch/model_def.py:39-75); these kernels implement the same math
+// (LayerNorm eps, dropout-before-residual, erf GELU) for determined_1_amd/models/bert.py.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kFinThreads = 1024;
+constexpr int kFinCols = 64;
+constexpr int kFinLanes = kFinThreads / kFinCols;
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<unsigned short>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<unsigned short>(u >> 16);
+}
+
+typedef unsigned short us4 __attribute__((ext_vector_type(4)));
+typedef unsigned short us8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct V4;
+template <> struct V4<unsigned short> {
+  static __device__ __forceinline__ void load(const unsigned short* p, float (&v)[4]) {
+    us4 r = *reinterpret_cast<const us4*>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = bf2f(r[j]);
+  }
+  static __device__ __forceinline__ void store(unsigned short* p, const float (&v)[4]) {
+    us4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = f2bf(v[j]);
+    *reinterpret_cast<us4*>(p) = r;
+  }
+};
+template <> struct V4<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+
+template <typename T> struct V8;
+template <> struct V8<unsigned short> {
+  static __device__ __forceinline__ void load(const unsigned short* p, float (&v)[8]) {
+    us8 r = *reinterpret_cast<const us8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(r[j]);
+  }
+  static __device__ __forceinline__ void store(unsigned short* p, const float (&v)[8]) {
+    us8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
+    *reinterpret_cast<us8*>(p) = r;
+  }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    float4 a = reinterpret_cast<const float4*>(p)[0];
+    float4 b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+template <typename T> __device__ __forceinline__ T from_float(float f);
+template <> __device__ __forceinline__ float from_float<float>(float f) { return f; }
+template <> __device__ __forceinline__ unsigned short from_float<unsigned short>(float f) { return f2bf(f); }
+
+// ---- Philox4x32-10 (counter-based; Salmon et al. 2011) --------------------------------------
+struct Rng {
+  uint32_t k0, k1, o0, o1;  // key = seed, counter words 2/3 = offset
+  uint32_t thresh;          // drop if u < thresh  (thresh = p * 2^32)
+  float scale;              // 1 / (1 - p)
+};
+
+__device__ __forceinline__ void philox(uint64_t idx, const Rng& g, uint32_t (&u)[4]) {
+  uint32_t c0 = static_cast<uint32_t>(idx), c1 = static_cast<uint32_t>(idx >> 32), c2 = g.o0, c3 = g.o1;
+  uint32_t k0 = g.k0, k1 = g.k1;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  u[0] = c0; u[1] = c1; u[2] = c2; u[3] = c3;
+}
+
+// mask * scale for the 4 elements of element-group `grp`
+__device__ __forceinline__ void drop_factors(uint64_t grp, const Rng& g, float (&m)[4]) {
+  uint32_t u[4];
+  philox(grp, g, u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m[j] = u[j] >= g.thresh ? g.scale : 0.f;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+struct LnArgs {
+  const void* h;      // [rows, H] input of the dropout (output of the preceding Linear)
+  const void* r;      // [rows, H] residual (nullable)
+  void* y;            // [rows, H]
+  const void* gamma;  // [H]
+  const void* beta;   // [H]
+  float* mean;        // [rows]
+  float* rstd;        // [rows]
+  int64_t rows;
+  int H;
+  float eps;
+  int dropout;        // 0: identity
+  Rng rng;
+};
+
+// ---------------------------------------------------------------------------------------------
+// y = LN(dropout(h) + r): one wave per row, grid-stride over rows.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int K>
+__global__ void __launch_bounds__(kThreads) ln_fwd_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int H4 = a.H >> 2;
+  const T* h = static_cast<const T*>(a.h);
+  const T* r = static_cast<const T*>(a.r);
+  T* y = static_cast<T*>(a.y);
+  float g[K][4], b[K][4];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < H4) {
+      V4<T>::load(static_cast<const T*>(a.gamma) + 4 * c4, g[i]);
+      V4<T>::load(static_cast<const T*>(a.beta) + 4 * c4, b[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[i][j] = b[i][j] = 0.f;
+    }
+  }
+  const float inv_h = 1.f / static_cast<float>(a.H);
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6); row < a.rows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row * a.H;
+    float v[K][4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < H4) {
+        V4<T>::load(h + base + 4 * c4, v[i]);
+        if (a.dropout) {
+          float m[4];
+          drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[i][j] *= m[j];
+        }
+        if (r) {
+          float t[4];
+          V4<T>::load(r + base + 4 * c4, t);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[i][j] += t[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += v[i][j];
+    }
+    const float mean = wave_sum(s) * inv_h;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      if (lane + 64 * i < H4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = v[i][j] - mean;
+          s2 += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(s2) * inv_h + a.eps);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < H4) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[i][j] + b[i][j];
+        V4<T>::store(y + base + 4 * c4, o);
+      }
+    }
+    if (lane == 0) {
+      a.mean[row] = mean;
+      a.rstd[row] = rstd;
+    }
+  }
+}
+
+struct LnBwdArgs {
+  const void* dy;
+  const void* h;
+  const void* r;      // nullable (then z = dropout(h))
+  const float* mean;
+  const float* rstd;
+  const void* gamma;
+  void* dr;           // grad of the residual (= dz), nullable
+  void* dh;           // grad of h (= dropout'(dz)), nullable
+  float* ws;          // [gridDim.x][3][H] partials: dgamma, dbeta, dbias
+  int64_t rows;
+  int H;
+  int dropout;
+  Rng rng;
+};
+
+template <typename T, int K>
+__global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
+  extern __shared__ float red[];  // [kWaves][H]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H4 = a.H >> 2;
+  const T* dy = static_cast<const T*>(a.dy);
+  const T* h = static_cast<const T*>(a.h);
+  const T* r = static_cast<const T*>(a.r);
+  T* dr = static_cast<T*>(a.dr);
+  T* dh = static_cast<T*>(a.dh);
+  float g[K][4], adg[K][4], adb[K][4], adh[K][4];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < H4) V4<T>::load(static_cast<const T*>(a.gamma) + 4 * c4, g[i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (c4 >= H4) g[i][j] = 0.f;
+      adg[i][j] = adb[i][j] = adh[i][j] = 0.f;
+    }
+  }
+  const float inv_h = 1.f / static_cast<float>(a.H);
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wave; row < a.rows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row * a.H;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float d[K][4], xh[K][4], m[K][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < H4) {
+        float z[4];
+        V4<T>::load(dy + base + 4 * c4, d[i]);
+        V4<T>::load(h + base + 4 * c4, z);
+        if (a.dropout) {
+          drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m[i]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) z[j] *= m[i][j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m[i][j] = 1.f;
+        }
+        if (r) {
+          float t[4];
+          V4<T>::load(r + base + 4 * c4, t);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) z[j] += t[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[i][j] = (z[j] - mean) * rstd;
+          const float dx = d[i][j] * g[i][j];
+          s1 += dx;
+          s2 += dx * xh[i][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = xh[i][j] = m[i][j] = 0.f;
+      }
+    }
+    s1 = wave_sum(s1) * inv_h;
+    s2 = wave_sum(s2) * inv_h;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < H4) {
+        float dz[4], dhv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dz[j] = rstd * (d[i][j] * g[i][j] - s1 - xh[i][j] * s2);
+          dhv[j] = dz[j] * m[i][j];
+          adg[i][j] += d[i][j] * xh[i][j];
+          adb[i][j] += d[i][j];
+          adh[i][j] += dhv[j];
+        }
+        if (dr) V4<T>::store(dr + base + 4 * c4, dz);
+        if (dh) V4<T>::store(dh + base + 4 * c4, dhv);
+      }
+    }
+  }
+  // block merge of the per-lane column partials (one quantity at a time: LDS = kWaves * H floats),
+  // then one partial row per block
+  const int H = a.H;
+  float* out = a.ws + static_cast<int64_t>(blockIdx.x) * 3 * H;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < H4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[wave * H + 4 * c4 + j] = q == 0 ? adg[i][j] : q == 1 ? adb[i][j] : adh[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += kThreads) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) s += red[w * H + c];
+      out[q * H + c] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// Sum `parts` partial rows of width W (fp32) -> up to 3 outputs of width W/3 each (or one of W).
+template <typename T>
+__global__ void __launch_bounds__(kFinThreads)
+colsum_finalize(const float* __restrict__ ws, int parts, int W, int seg, T* __restrict__ o0, T* __restrict__ o1,
+                T* __restrict__ o2) {
+  __shared__ float red[kFinLanes][kFinCols];
+  const int cl = threadIdx.x % kFinCols, ln = threadIdx.x / kFinCols;
+  const int col = blockIdx.x * kFinCols + cl;
+  float s = 0.f;
+  if (col < W) {
+    int p = ln;
+    for (; p + 3 * kFinLanes < parts; p += 4 * kFinLanes) {
+      const float a = ws[static_cast<int64_t>(p) * W + col];
+      const float b = ws[static_cast<int64_t>(p + kFinLanes) * W + col];
+      const float c = ws[static_cast<int64_t>(p + 2 * kFinLanes) * W + col];
+      const float d = ws[static_cast<int64_t>(p + 3 * kFinLanes) * W + col];
+      s += (a + b) + (c + d);
+    }
+    for (; p < parts; p += kFinLanes) s += ws[static_cast<int64_t>(p) * W + col];
+  }
+  red[ln][cl] = s;
+  __syncthreads();
+  if (ln == 0 && col < W) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < kFinLanes; ++l) t += red[l][cl];
+    const int which = col / seg, c = col - which * seg;
+    T* o = which == 0 ? o0 : which == 1 ? o1 : o2;
+    if (o) o[c] = from_float<T>(t);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Column-tiled elementwise + bias-grad partials over a [rows, C] matrix (C % 8 == 0):
+// a lane owns 8 consecutive columns, a block covers tpr column groups x R rows per iteration and
+// one row-block; partial column sums land in ws[row_block][C].
+// ---------------------------------------------------------------------------------------------
+struct ColGeom {
+  int64_t rows;
+  int C;
+  int tpr;
+  int R;
+  int64_t rpb;
+  int nrb;
+};
+
+ColGeom make_col_geom(int64_t rows, int C) {
+  ColGeom g;
+  g.rows = rows;
+  g.C = C;
+  const int groups = C / 8;
+  int tpr = 1;
+  while (tpr * 2 <= kThreads && groups % (tpr * 2) == 0) tpr *= 2;
+  g.tpr = tpr;
+  g.R = kThreads / tpr;
+  const int gy = groups / tpr;
+  // ~1024 blocks in total, >= 4 row iterations per thread so the partial traffic stays small
+  int64_t nrb = (1024 + gy - 1) / gy;
+  const int64_t max_rb = (rows + 4 * g.R - 1) / (4 * g.R);
+  if (nrb > max_rb) nrb = max_rb;
+  if (nrb < 1) nrb = 1;
+  int64_t rpb = (rows + nrb - 1) / nrb;
+  rpb = (rpb + g.R - 1) / g.R * g.R;
+  g.rpb = rpb;
+  g.nrb = static_cast<int>((rows + rpb - 1) / rpb);
+  return g;
+}
+
+__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float z) {
+  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
+  return cdf + z * pdf;
+}
+
+// MODE 0: colsum(x) only;  MODE 1: dz = da * gelu'(z) (stored) and colsum(dz)
+template <typename T, int MODE>
+__global__ void __launch_bounds__(kThreads)
+col_kernel(const T* __restrict__ a, const T* __restrict__ z, T* __restrict__ dz, ColGeom g, float* __restrict__ ws) {
+  __shared__ float red[kThreads * 8];
+  const int tx = threadIdx.x % g.tpr, ty = threadIdx.x / g.tpr;
+  const int cg = blockIdx.y * g.tpr + tx;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * g.rpb;
+  const int64_t r1 = min(g.rows, r0 + g.rpb);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int64_t C = g.C;
+  for (int64_t r = r0 + ty; r < r1; r += g.R) {
+    const int64_t off = r * C + cg * 8;
+    float v[8];
+    V8<T>::load(a + off, v);
+    if (MODE == 1) {
+      float zz[8];
+      V8<T>::load(z + off, zz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(zz[j]);
+      V8<T>::store(dz + off, v);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  if (!ws) return;  // gelu backward without a bias (uniform across the block)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = acc[j];
+  __syncthreads();
+  if (ty == 0) {
+    for (int k = 1; k < g.R; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += red[(k * g.tpr + tx) * 8 + j];
+    float* out = ws + static_cast<int64_t>(blockIdx.x) * C + cg * 8;
+    reinterpret_cast<float4*>(out)[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    reinterpret_cast<float4*>(out)[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) gelu_fwd_kernel(const T* __restrict__ z, T* __restrict__ a, int64_t nvec) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    float v[8];
+    V8<T>::load(z + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+    V8<T>::store(a + i * 8, v);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) dropout_mask_kernel(int64_t ngroups, Rng g, uint8_t* __restrict__ out) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < ngroups;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    float m[4];
+    drop_factors(static_cast<uint64_t>(i), g, m);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[i * 4 + j] = m[j] != 0.f;
+  }
+}
+
+Rng make_rng(float p, uint64_t seed, uint64_t offset) {
+  Rng g;
+  g.k0 = static_cast<uint32_t>(seed);
+  g.k1 = static_cast<uint32_t>(seed >> 32);
+  g.o0 = static_cast<uint32_t>(offset);
+  g.o1 = static_cast<uint32_t>(offset >> 32);
+  double t = static_cast<double>(p) * 4294967296.0;
+  g.thresh = t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
+  g.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  return g;
+}
+
+int ln_k(int H) { return (H / 4 + 63) / 64; }
+
+int64_t ln_bwd_blocks(int64_t rows) {
+  int64_t b = (rows + kWaves - 1) / kWaves;
+  return b < 512 ? b : 512;
+}
+
+int grid_for(int64_t work, int per_block) {
+  int64_t b = (work + per_block - 1) / per_block;
+  if (b > 8192) b = 8192;
+  return static_cast<int>(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" {
+
+// Max hidden size of the LayerNorm kernels (K <= 8 register groups of 256 columns).
+int det_tf_ln_max_hidden() { return 2048; }
+
+int64_t det_tf_ln_ws_elems(int64_t rows, int H) { return ln_bwd_blocks(rows) * 3 * static_cast<int64_t>(H); }
+
+// dtype: 0 = fp32, 1 = bf16 (x, r, y, gamma, beta all of that dtype).  p = dropout probability
+// applied to h (0 disables).  Writes y, mean[rows], rstd[rows].
+int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y, int64_t rows, int H,
+                  const void* gamma, const void* beta, float eps, float p, uint64_t seed, uint64_t offset,
+                  float* mean, float* rstd) {
+  if (H % 4 != 0 || H > 2048 || rows <= 0) return -1;
+  LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset)};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int grid = grid_for(rows, kWaves);
+  const int K = ln_k(H);
+#define DET_LNF(T, KK) hipLaunchKernelGGL((ln_fwd_kernel<T, KK>), dim3(grid), dim3(kThreads), 0, st, a)
+#define DET_LNF_K(T)                                                              \
+  switch (K) {                                                                    \
+    case 1: DET_LNF(T, 1); break;                                                 \
+    case 2: DET_LNF(T, 2); break;                                                 \
+    case 3: DET_LNF(T, 3); break;                                                 \
+    case 4: DET_LNF(T, 4); break;                                                 \
+    case 5: case 6: DET_LNF(T, 6); break;                                         \
+    default: DET_LNF(T, 8); break;                                                \
+  }
+  if (dtype == 1) {
+    DET_LNF_K(unsigned short)
+  } else {
+    DET_LNF_K(float)
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+// Backward of det_tf_ln_fwd.  Outputs (each nullable): dr = dL/dz (the residual's grad),
+// dh = dropout'(dz), dgamma, dbeta, dbias = column sums of dh (bias grad of the Linear that
+// produced h).  ws: det_tf_ln_ws_elems(rows, H) fp32.
+int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const void* r, const float* mean,
+                  const float* rstd, const void* gamma, int64_t rows, int H, float p, uint64_t seed,
+                  uint64_t offset, void* dr, void* dh, void* dgamma, void* dbeta, void* dbias, float* ws) {
+  if (H % 4 != 0 || H > 2048 || rows <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int blocks = static_cast<int>(ln_bwd_blocks(rows));
+  LnBwdArgs a{dy, h, r, mean, rstd, gamma, dr, dh, ws, rows, H, p > 0.f, make_rng(p, seed, offset)};
+  const size_t lds = static_cast<size_t>(kWaves) * H * sizeof(float);
+  const int K = ln_k(H);
+#define DET_LNB(T, KK) hipLaunchKernelGGL((ln_bwd_kernel<T, KK>), dim3(blocks), dim3(kThreads), lds, st, a)
+#define DET_LNB_K(T)                                                              \
+  switch (K) {                                                                    \
+    case 1: DET_LNB(T, 1); break;                                                 \
+    case 2: DET_LNB(T, 2); break;                                                 \
+    case 3: DET_LNB(T, 3); break;                                                 \
+    case 4: DET_LNB(T, 4); break;                                                 \
+    case 5: case 6: DET_LNB(T, 6); break;                                         \
+    default: DET_LNB(T, 8); break;                                                \
+  }
+  if (dtype == 1) {
+    DET_LNB_K(unsigned short)
+    hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads),
+                       0, st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
+                       static_cast<unsigned short*>(dbeta), static_cast<unsigned short*>(dbias));
+  } else {
+    DET_LNB_K(float)
+    hipLaunchKernelGGL(colsum_finalize<float>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st,
+                       ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
+                       static_cast<float*>(dbias));
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+int64_t det_tf_col_ws_elems(int64_t rows, int C) {
+  ColGeom g = make_col_geom(rows, C);
+  return static_cast<int64_t>(g.nrb) * C;
+}
+
+// a = gelu(z), elementwise over n elements (n % 8 == 0).
+int det_tf_gelu_fwd(void* stream, int dtype, const void* z, void* a, int64_t n) {
+  if (n % 8 != 0 || n <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t nvec = n / 8;
+  const int grid = grid_for(nvec, kThreads * 4);
+  if (dtype == 1)
+    hipLaunchKernelGGL(gelu_fwd_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(z), static_cast<unsigned short*>(a), nvec);
+  else
+    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(grid), dim3(kThreads), 0, st, static_cast<const float*>(z),
+                       static_cast<float*>(a), nvec);
+  return static_cast<int>(hipGetLastError());
+}
+
+// dz = da * gelu'(z) over [rows, C]; dbias (nullable) = column sums of dz.
+int det_tf_gelu_bwd(void* stream, int dtype, const void* da, const void* z, void* dz, int64_t rows, int C,
+                    void* dbias, float* ws) {
+  if (C % 8 != 0 || rows <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  ColGeom g = make_col_geom(rows, C);
+  dim3 grid(g.nrb, C / 8 / g.tpr);
+  float* w = dbias ? ws : nullptr;
+  if (dtype == 1) {
+    hipLaunchKernelGGL((col_kernel<unsigned short, 1>), grid, dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(da), static_cast<const unsigned short*>(z),
+                       static_cast<unsigned short*>(dz), g, w);
+    if (dbias)
+      hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0,
+                         st, ws, g.nrb, C, C, static_cast<unsigned short*>(dbias), nullptr, nullptr);
+  } else {
+    hipLaunchKernelGGL((col_kernel<float, 1>), grid, dim3(kThreads), 0, st, static_cast<const float*>(da),
+                       static_cast<const float*>(z), static_cast<float*>(dz), g, w);
+    if (dbias)
+      hipLaunchKernelGGL(colsum_finalize<float>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
+                         g.nrb, C, C, static_cast<float*>(dbias), nullptr, nullptr);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+// out[C] = column sums of x[rows, C] (the bias grad of a Linear), deterministic two-level.
+int det_tf_colsum(void* stream, int dtype, const void* x, int64_t rows, int C, void* out, float* ws) {
+  if (C % 8 != 0 || rows <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  ColGeom g = make_col_geom(rows, C);
+  dim3 grid(g.nrb, C / 8 / g.tpr);
+  if (dtype == 1) {
+    hipLaunchKernelGGL((col_kernel<unsigned short, 0>), grid, dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), nullptr, nullptr, g, ws);
+    hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0,
+                       st, ws, g.nrb, C, C, static_cast<unsigned short*>(out), nullptr, nullptr);
+  } else {
+    hipLaunchKernelGGL((col_kernel<float, 0>), grid, dim3(kThreads), 0, st, static_cast<const float*>(x), nullptr,
+                       nullptr, g, ws);
+    hipLaunchKernelGGL(colsum_finalize<float>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
+                       g.nrb, C, C, static_cast<float*>(out), nullptr, nullptr);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+// Materialise the keep-mask (1 = kept) the LN kernels use for [n] elements (n % 4 == 0); tests only.
+int det_tf_dropout_mask(void* stream, int64_t n, float p, uint64_t seed, uint64_t offset, uint8_t* out) {
+  if (n % 4 != 0 || n <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n / 4, kThreads)), dim3(kThreads), 0, st, n / 4,
+                     make_rng(p, seed, offset), out);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

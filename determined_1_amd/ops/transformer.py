@@ -1,0 +1,262 @@
+"""Fused transformer-encoder ops on the ``det_transformer.hip`` kernels.
+
+    linear(x, W, b)                                   y = x W^T + b, bias grad by det_tf_colsum
+    linear_gelu(x, W, b)                              a = gelu(x W^T + b), bias grad fused in gelu bwd
+    linear_dropout_add_layernorm(x, W, b, r, g, be)   y = LN(dropout(x W^T + b) + r)
+    layer_norm(x, g, be)                              y = LN(x)
+
+GEMMs stay on hipBLASLt (``torch.addmm`` / ``torch.mm``); everything between them is one HIP
+pass per direction, and every Linear's bias gradient is produced inside the kernel that already
+reads the gradient (LayerNorm bwd, GELU bwd) instead of a separate reduction.  Dropout masks are
+regenerated from a Philox (seed, offset) pair in the backward pass rather than stored.
+
+CPU tensors, and GPU layouts the kernels do not cover (fp16, hidden > 2048, hidden % 8 != 0),
+run the plain PyTorch composite, which is also the numerics reference of the GPU tests; GPU
+fallbacks are counted in ``FALLBACKS`` so benchmarks can assert the native path ran.
+"""
+import itertools
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from determined_1_amd.ops import _lib
+
+FALLBACKS = {"count": 0}
+_DT = {torch.float32: 0, torch.bfloat16: 1}
+_MAX_H = 2048
+_offsets = itertools.count(1)
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def next_rng() -> Tuple[int, int]:
+    """(seed, offset) of the next dropout call: the seed follows the trial's torch seed, the offset
+    is unique per call within the process, so masks are reproducible run to run."""
+    return torch.initial_seed() & 0xFFFFFFFFFFFFFFFF, next(_offsets)
+
+
+def _native(*ts: Optional[torch.Tensor], width: int, max_width: Optional[int] = None) -> bool:
+    dev = [t for t in ts if t is not None]
+    if not dev or dev[0].device.type != "cuda":
+        return False
+    dt = dev[0].dtype
+    ok = dt in _DT and all(t.dtype == dt and t.device == dev[0].device for t in dev) and width % 8 == 0
+    if max_width is not None:
+        ok = ok and width <= max_width
+    if not ok:
+        FALLBACKS["count"] += 1
+    return ok
+
+
+def _autocast(*ts: Optional[torch.Tensor]):
+    """Under autocast run in the autocast dtype (what F.linear would do) with autocast off."""
+    if torch.is_autocast_enabled("cuda") and any(t is not None and t.is_cuda for t in ts):
+        dt = torch.get_autocast_dtype("cuda")
+        return [t.to(dt) if t is not None and t.is_floating_point() else t for t in ts], True
+    return list(ts), False
+
+
+def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool):
+    dx = dz @ weight if need_x else None
+    dw = dz.t() @ x2 if need_w else None
+    return dx, dw
+
+
+def _addmm(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    return torch.addmm(bias, x2, weight.t()) if bias is not None else x2 @ weight.t()
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = _addmm(x2, weight, bias)
+        ctx.save_for_backward(x2, weight)
+        ctx.has_bias = bias is not None
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, weight.shape[0]).contiguous()
+        dx, dw = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            lib = _lib.get_lib()
+            rows, C = dy2.shape
+            db = torch.empty(C, dtype=dy2.dtype, device=dy2.device)
+            ws = torch.empty(int(lib.det_tf_col_ws_elems(rows, C)), dtype=torch.float32, device=dy2.device)
+            _lib.check(lib.det_tf_colsum(_stream(dy2), _DT[dy2.dtype], dy2.data_ptr(), rows, C, db.data_ptr(),
+                                         ws.data_ptr()), "det_tf_colsum")
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db
+
+
+class _LinearGELU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x2 = x.reshape(-1, x.shape[-1])
+        z = _addmm(x2, weight, bias)
+        a = torch.empty_like(z)
+        lib = _lib.get_lib()
+        _lib.check(lib.det_tf_gelu_fwd(_stream(z), _DT[z.dtype], z.data_ptr(), a.data_ptr(), z.numel()),
+                   "det_tf_gelu_fwd")
+        ctx.save_for_backward(x2, weight, z)
+        ctx.has_bias = bias is not None
+        ctx.xshape = x.shape
+        return a.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, da):
+        x2, weight, z = ctx.saved_tensors
+        rows, C = z.shape
+        da2 = da.reshape(rows, C).contiguous()
+        lib = _lib.get_lib()
+        dz = torch.empty_like(z)
+        db = torch.empty(C, dtype=z.dtype, device=z.device) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        ws = torch.empty(int(lib.det_tf_col_ws_elems(rows, C)) if db is not None else 1, dtype=torch.float32,
+                         device=z.device)
+        _lib.check(lib.det_tf_gelu_bwd(_stream(z), _DT[z.dtype], da2.data_ptr(), z.data_ptr(), dz.data_ptr(), rows, C,
+                                       _ptr(db), ws.data_ptr()), "det_tf_gelu_bwd")
+        dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db
+
+
+def _ln_forward(h: torch.Tensor, r: Optional[torch.Tensor], gamma, beta, p: float, eps: float):
+    rows, H = h.shape
+    lib = _lib.get_lib()
+    y = torch.empty_like(h)
+    mean = torch.empty(rows, dtype=torch.float32, device=h.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=h.device)
+    seed, off = next_rng() if p > 0 else (0, 0)
+    _lib.check(lib.det_tf_ln_fwd(_stream(h), _DT[h.dtype], h.data_ptr(), _ptr(r), y.data_ptr(), rows, H,
+                                 gamma.data_ptr(), beta.data_ptr(), eps, p, seed, off, mean.data_ptr(),
+                                 rstd.data_ptr()), "det_tf_ln_fwd")
+    return y, mean, rstd, seed, off
+
+
+def _ln_backward(ctx, dy, h, r, gamma, mean, rstd, need_dh: bool, need_dr: bool, need_bias: bool):
+    rows, H = h.shape
+    lib = _lib.get_lib()
+    dy2 = dy.reshape(rows, H).contiguous()
+    dh = torch.empty_like(h) if need_dh else None
+    dr = torch.empty_like(h) if need_dr else None
+    dgamma = torch.empty_like(gamma) if ctx.need_gamma else None
+    dbeta = torch.empty_like(gamma) if ctx.need_beta else None
+    dbias = torch.empty(H, dtype=h.dtype, device=h.device) if need_bias else None
+    ws = torch.empty(int(lib.det_tf_ln_ws_elems(rows, H)), dtype=torch.float32, device=h.device)
+    _lib.check(lib.det_tf_ln_bwd(_stream(h), _DT[h.dtype], dy2.data_ptr(), h.data_ptr(), _ptr(r), mean.data_ptr(),
+                                 rstd.data_ptr(), gamma.data_ptr(), rows, H, ctx.p, ctx.seed, ctx.off, _ptr(dr),
+                                 _ptr(dh), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), ws.data_ptr()), "det_tf_ln_bwd")
+    return dh, dr, dgamma, dbeta, dbias
+
+
+class _LinearDropAddLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, gamma, beta, p, eps):
+        x2 = x.reshape(-1, x.shape[-1])
+        h = _addmm(x2, weight, bias)
+        r2 = residual.reshape(h.shape).contiguous()
+        y, mean, rstd, ctx.seed, ctx.off = _ln_forward(h, r2, gamma, beta, p, eps)
+        ctx.p = p
+        ctx.has_bias = bias is not None
+        ctx.xshape, ctx.rshape = x.shape, residual.shape
+        ctx.need_gamma, ctx.need_beta = ctx.needs_input_grad[4], ctx.needs_input_grad[5]
+        ctx.save_for_backward(x2, weight, h, r2, gamma, mean, rstd)
+        return y.view(residual.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, h, r2, gamma, mean, rstd = ctx.saved_tensors
+        need_h = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        dh, dr, dgamma, dbeta, dbias = _ln_backward(
+            ctx, dy, h, r2, gamma, mean, rstd, need_dh=True, need_dr=ctx.needs_input_grad[3],
+            need_bias=ctx.has_bias and ctx.needs_input_grad[2])
+        dx, dw = (_mm_backward(dh, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+                  if need_h else (None, None))
+        return ((dx.view(ctx.xshape) if dx is not None else None), dw, dbias,
+                (dr.view(ctx.rshape) if dr is not None else None), dgamma, dbeta, None, None)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        h = x.reshape(-1, x.shape[-1]).contiguous()
+        y, mean, rstd, ctx.seed, ctx.off = _ln_forward(h, None, gamma, beta, 0.0, eps)
+        ctx.p = 0.0
+        ctx.xshape = x.shape
+        ctx.need_gamma, ctx.need_beta = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        ctx.save_for_backward(h, gamma, mean, rstd)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, gamma, mean, rstd = ctx.saved_tensors
+        dh, _, dgamma, dbeta, _ = _ln_backward(ctx, dy, h, None, gamma, mean, rstd, need_dh=ctx.needs_input_grad[0],
+                                               need_dr=False, need_bias=False)
+        return (dh.view(ctx.xshape) if dh is not None else None), dgamma, dbeta, None
+
+
+# ------------------------------------------------------------------------------------------------
+# public functional API (composite reference on CPU / uncovered layouts)
+# ------------------------------------------------------------------------------------------------
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    (x, weight, bias), ac = _autocast(x, weight, bias)
+    if not _native(x, weight, bias, width=weight.shape[0]):
+        return F.linear(x, weight, bias)
+    with torch.autocast("cuda", enabled=False) if ac else _null():
+        return _Linear.apply(x, weight, bias)
+
+
+def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    (x, weight, bias), ac = _autocast(x, weight, bias)
+    if not _native(x, weight, bias, width=weight.shape[0]):
+        return F.gelu(F.linear(x, weight, bias))
+    with torch.autocast("cuda", enabled=False) if ac else _null():
+        return _LinearGELU.apply(x, weight, bias)
+
+
+def linear_dropout_add_layernorm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                                 residual: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, p: float = 0.0,
+                                 eps: float = 1e-12, training: bool = True) -> torch.Tensor:
+    """``LayerNorm(dropout(x W^T + b) + residual)`` — BERT's SelfOutput / Output block."""
+    p = float(p) if training else 0.0
+    (x, weight, bias, residual, gamma, beta), ac = _autocast(x, weight, bias, residual, gamma, beta)
+    if not _native(x, weight, bias, residual, gamma, beta, width=weight.shape[0], max_width=_MAX_H):
+        h = F.dropout(F.linear(x, weight, bias), p, training)
+        return F.layer_norm(h + residual, (weight.shape[0],), gamma, beta, eps)
+    with torch.autocast("cuda", enabled=False) if ac else _null():
+        return _LinearDropAddLN.apply(x, weight, bias, residual, gamma, beta, p, float(eps))
+
+
+def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    (x, gamma, beta), ac = _autocast(x, gamma, beta)
+    if not _native(x, gamma, beta, width=x.shape[-1], max_width=_MAX_H):
+        return F.layer_norm(x, (x.shape[-1],), gamma, beta, eps)
+    with torch.autocast("cuda", enabled=False) if ac else _null():
+        return _LayerNorm.apply(x, gamma, beta, float(eps))
+
+
+def dropout_mask(n: int, p: float, seed: int, offset: int, device: torch.device) -> torch.Tensor:
+    """The keep-mask the kernels derive from (seed, offset) for n elements (tests)."""
+    lib = _lib.get_lib()
+    out = torch.empty(n, dtype=torch.uint8, device=device)
+    with torch.cuda.device(device):
+        _lib.check(lib.det_tf_dropout_mask(torch.cuda.current_stream(device).cuda_stream, n, p, seed, offset,
+                                           out.data_ptr()), "det_tf_dropout_mask")
+    return out.bool()
+
+
+class _null:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False

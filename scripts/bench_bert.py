@@ -23,6 +23,7 @@ def main() -> None:
     ap.add_argument("--batch-per-gpu", type=int, default=12)
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
+    ap.add_argument("--impl", default="native", choices=["native", "hf"], help="fused MI355X encoder or HF BERT")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -36,7 +37,7 @@ def main() -> None:
     gbs = args.batch_per_gpu * world
     cfg = {
         "hyperparameters": {"global_batch_size": gbs, "learning_rate": 3e-5, "max_seq_length": 384, "amp": args.amp,
-                            "max_grad_norm": 1.0, "train_records": 100000},
+                            "max_grad_norm": 1.0, "train_records": 100000, "impl": args.impl},
         "resources": {"slots_per_trial": world},
         "optimizations": {"aggregation_frequency": args.agg},
         "searcher": {"name": "single", "metric": "f1", "max_length": {"batches": args.steps}, "smaller_is_better": False},
@@ -60,13 +61,16 @@ def main() -> None:
     ctrl = make_controller(BertSQuADTrial, cfg, stream(), trial_seed=7)
     ctrl.run()
     el = max(pdist.allgather_object(t["t1"] - t["t0"]))
+    from determined_1_amd.ops import transformer as tfops
+
     if rank == 0:
         print(json.dumps({"metric": "examples/sec (whole node) BERT-base SQuAD-shape PyTorchTrial",
                           "value": round(args.steps * gbs / el, 2), "unit": "examples/s", "n_gpus": world,
                           "ms_per_step": round(1000 * el / args.steps, 2), "dtype": "bf16" if args.amp != "O0" else "fp32",
                           "config": {"model": "bert-base (random init)", "seq_len": 384, "global_batch": gbs,
                                      "amp": args.amp, "aggregation_frequency": args.agg,
-                                     "optimizer": "AdamW (fused arena HIP kernel)"}}), flush=True)
+                                     "optimizer": "AdamW (fused arena HIP kernel)", "impl": args.impl,
+                                     "tf_fallbacks": tfops.FALLBACKS["count"]}}), flush=True)
     pdist.shutdown()
 
 

@@ -1,0 +1,135 @@
+"""Fused transformer kernels (ops/csrc/det_transformer.hip) vs the fp32 PyTorch composite."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from determined_1_amd.ops import transformer as tfops
+
+pytestmark = pytest.mark.gpu
+
+
+def _tol(dt):
+    return dict(atol=2e-4, rtol=2e-4) if dt == torch.float32 else dict(atol=4e-2, rtol=4e-2)
+
+
+def _leaf(t, dev=None, dt=None):
+    t = t.detach()
+    if dev is not None:
+        t = t.to(dev, dt)
+    return t.clone().requires_grad_(True)
+
+
+@pytest.mark.parametrize("rows,K,H,dt,p", [
+    (512, 768, 768, torch.float32, 0.0),
+    (4608, 768, 768, torch.bfloat16, 0.0),
+    (1000, 3072, 768, torch.bfloat16, 0.1),
+    (300, 256, 1024, torch.float32, 0.1),
+    (77, 64, 200, torch.float32, 0.25),  # H not a multiple of 256 (inactive lanes)
+])
+def test_linear_dropout_add_layernorm(gpu, monkeypatch, rows, K, H, dt, p):
+    torch.manual_seed(0)
+    x = torch.randn(rows, K).to(dt).float()
+    w = (torch.randn(H, K) / K ** 0.5).to(dt).float()
+    b = (torch.randn(H) * 0.1).to(dt).float()
+    r = torch.randn(rows, H).to(dt).float()
+    g = (1 + 0.1 * torch.randn(H)).to(dt).float()
+    be = (0.1 * torch.randn(H)).to(dt).float()
+    dy = torch.randn(rows, H).to(dt).float()
+    seed, off = 1234, 77
+    monkeypatch.setattr(tfops, "next_rng", lambda: (seed, off))
+    keep = tfops.dropout_mask(rows * H, p, seed, off, torch.device(gpu)).view(rows, H).cpu() if p > 0 else None
+    if keep is not None:
+        frac = keep.float().mean().item()
+        assert abs(frac - (1 - p)) < 0.01, frac
+    # reference: fp32 composite with the kernel's mask
+    ref = [_leaf(t) for t in (x, w, b, r, g, be)]
+    h = F.linear(ref[0], ref[1], ref[2])
+    if keep is not None:
+        h = h * keep.float() / (1 - p)
+    yr = F.layer_norm(h + ref[3], (H,), ref[4], ref[5], 1e-12)
+    yr.backward(dy)
+    dut = [_leaf(t, gpu, dt) for t in (x, w, b, r, g, be)]
+    before = tfops.FALLBACKS["count"]
+    yd = tfops.linear_dropout_add_layernorm(*dut, p=p, eps=1e-12, training=True)
+    yd.backward(dy.to(gpu, dt))
+    assert tfops.FALLBACKS["count"] == before, "fused path fell back"
+    tol = _tol(dt)
+    torch.testing.assert_close(yd.float().cpu(), yr.detach(), **tol)
+    for a, e, name in zip(dut, ref, ("dx", "dW", "db", "dres", "dgamma", "dbeta")):
+        scale = max(1.0, e.grad.abs().max().item())
+        torch.testing.assert_close(a.grad.float().cpu() / scale, e.grad / scale, **tol, msg=name)
+
+
+@pytest.mark.parametrize("rows,K,N,dt", [(512, 768, 3072, torch.float32), (4608, 768, 3072, torch.bfloat16),
+                                         (100, 64, 264, torch.float32)])
+def test_linear_gelu(gpu, rows, K, N, dt):
+    torch.manual_seed(1)
+    x, w, b = torch.randn(rows, K).to(dt).float(), (torch.randn(N, K) / K ** 0.5).to(dt).float(), torch.randn(N).to(dt).float()
+    da = torch.randn(rows, N).to(dt).float()
+    ref = [_leaf(t) for t in (x, w, b)]
+    F.gelu(F.linear(*ref)).backward(da)
+    dut = [_leaf(t, gpu, dt) for t in (x, w, b)]
+    out = tfops.linear_gelu(*dut)
+    out.backward(da.to(gpu, dt))
+    tol = _tol(dt)
+    torch.testing.assert_close(out.float().cpu(), F.gelu(F.linear(x, w, b)), **tol)
+    for a, e in zip(dut, ref):
+        scale = max(1.0, e.grad.abs().max().item())
+        torch.testing.assert_close(a.grad.float().cpu() / scale, e.grad / scale, **tol)
+
+
+@pytest.mark.parametrize("rows,K,N,dt", [(4608, 768, 2304, torch.bfloat16), (333, 128, 72, torch.float32)])
+def test_linear_bias_grad(gpu, rows, K, N, dt):
+    torch.manual_seed(2)
+    x, w, b = torch.randn(rows, K).to(dt).float(), torch.randn(N, K).to(dt).float(), torch.randn(N).to(dt).float()
+    dy = torch.randn(rows, N).to(dt).float()
+    ref = [_leaf(t) for t in (x, w, b)]
+    F.linear(*ref).backward(dy)
+    dut = [_leaf(t, gpu, dt) for t in (x, w, b)]
+    tfops.linear(*dut).backward(dy.to(gpu, dt))
+    tol = _tol(dt)
+    scale = max(1.0, ref[2].grad.abs().max().item())
+    torch.testing.assert_close(dut[2].grad.float().cpu() / scale, ref[2].grad / scale, **tol)
+
+
+def test_layer_norm(gpu):
+    torch.manual_seed(3)
+    x = torch.randn(1536, 768) * 3 + 1
+    g, b = 1 + 0.1 * torch.randn(768), 0.1 * torch.randn(768)
+    dy = torch.randn(1536, 768)
+    ref = [_leaf(t) for t in (x, g, b)]
+    F.layer_norm(ref[0], (768,), ref[1], ref[2], 1e-12).backward(dy)
+    dut = [_leaf(t, gpu, torch.float32) for t in (x, g, b)]
+    tfops.layer_norm(*dut, eps=1e-12).backward(dy.to(gpu))
+    for a, e in zip(dut, ref):
+        torch.testing.assert_close(a.grad.cpu(), e.grad, atol=3e-4, rtol=3e-4)
+
+
+def test_bert_layer_fused_matches_composite(gpu, monkeypatch):
+    """Whole fp32 BERT model on the GPU: fused kernels vs the composite path, dropout off."""
+    from determined_1_amd.models.bert import BertEncoderConfig, BertForQA
+
+    cfg = BertEncoderConfig(vocab_size=512, hidden_size=256, num_hidden_layers=2, num_attention_heads=4,
+                            intermediate_size=1024, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    torch.manual_seed(4)
+    m = BertForQA(cfg).to(gpu)
+    ids = torch.randint(1, 512, (4, 128), device=gpu)
+    am = torch.ones_like(ids)
+    am[1, -10:] = 0
+    s = torch.randint(0, 128, (4,), device=gpu)
+    e = (s + 2).clamp(max=127)
+
+    def run():
+        m.zero_grad(set_to_none=True)
+        out = m(ids, None, am, s, e)
+        out.loss.backward()
+        return out.loss.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+    before = tfops.FALLBACKS["count"]
+    loss_f, g_f = run()
+    assert tfops.FALLBACKS["count"] == before
+    monkeypatch.setattr(tfops, "_native", lambda *a, **k: False)
+    loss_c, g_c = run()
+    torch.testing.assert_close(loss_f, loss_c, atol=1e-5, rtol=1e-5)
+    for k in g_c:
+        torch.testing.assert_close(g_f[k], g_c[k], atol=1e-4, rtol=1e-3, msg=k)
