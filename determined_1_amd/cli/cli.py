@@ -15,6 +15,7 @@ import yaml
 
 from determined_1_amd import __version__
 from determined_1_amd.api import MasterClient, read_context
+from determined_1_amd.api.request import make_url
 from determined_1_amd.config import merge_with_defaults, validate_experiment_config
 
 
@@ -361,6 +362,33 @@ def cmd_command_logs(args: argparse.Namespace) -> None:
         print(l["message"])
 
 
+def cmd_tensorboard_start(args: argparse.Namespace) -> None:
+    """``det tensorboard start <exp ids>``: a zero-slot command task running the scalar dashboard
+    (determined_1_amd/tensorboard/serve.py), reachable through the master's /proxy/cmd-<id>/."""
+    client = MasterClient(args.master)
+    eids = ",".join(str(e) for e in args.experiment_ids)
+    argv = ["python3", "-m", "determined_1_amd.tensorboard.serve", "--experiment-ids", eids]
+    if args.trial_ids:
+        argv += ["--trial-ids", ",".join(str(t) for t in args.trial_ids)]
+    cfg = {"entrypoint": argv, "type": "tensorboard", "resources": {"slots": 0},
+           "description": f"TensorBoard (Experiment {eids})"}
+    cid = client.post("/commands", {"config": cfg, "context": []})["id"]
+    url = make_url(client.master, f"/proxy/cmd-{cid}/")
+    if not args.detach:
+        deadline = time.time() + args.timeout
+        while time.time() < deadline:
+            c = client.get(f"/commands/{cid}")
+            if c.get("ready") or c.get("state") == "TERMINATED":
+                break
+            time.sleep(0.5)
+    print(f"TensorBoard {cid}: {url}")
+
+
+def cmd_tensorboard_list(args: argparse.Namespace) -> None:
+    rows = MasterClient(args.master).get("/commands", type="tensorboard")
+    print(_table(rows, ["id", "state", "description", "ready", "service_address"]))
+
+
 def cmd_command_kill(args: argparse.Namespace) -> None:
     MasterClient(args.master).post(f"/commands/{args.command_id}/kill")
 
@@ -560,7 +588,18 @@ def build_parser() -> argparse.ArgumentParser:
         x = cm.add_parser(name)
         x.add_argument("command_id", type=int)
         x.set_defaults(func=fn)
-    for name in ("notebook", "shell", "tensorboard"):
+    tb = sub.add_parser("tensorboard").add_subparsers(dest="sub")
+    x = tb.add_parser("start")
+    x.add_argument("experiment_ids", type=int, nargs="+")
+    x.add_argument("--trial-ids", type=int, nargs="*")
+    x.add_argument("--detach", "-d", action="store_true")
+    x.add_argument("--timeout", type=float, default=60)
+    x.set_defaults(func=cmd_tensorboard_start)
+    tb.add_parser("list").set_defaults(func=cmd_tensorboard_list)
+    x = tb.add_parser("kill")
+    x.add_argument("command_id", type=int)
+    x.set_defaults(func=cmd_command_kill)
+    for name in ("notebook", "shell"):
         sub.add_parser(name).set_defaults(func=cmd_unavailable(name))
 
     ps = sub.add_parser("preview-search")

@@ -98,6 +98,12 @@ def _read_varint(b: bytes, i: int) -> Tuple[int, int]:
 
 def read_events(path: str) -> Iterator[Tuple[int, str, float]]:
     """(step, tag, value) of every scalar in an event file; verifies both CRCs."""
+    for _, step, tag, value in read_scalars(path):
+        yield step, tag, value
+
+
+def read_scalars(path: str) -> Iterator[Tuple[float, int, str, float]]:
+    """(wall_time, step, tag, value) of every scalar in an event file; verifies both CRCs."""
     data = open(path, "rb").read()
     i = 0
     while i < len(data):
@@ -111,11 +117,14 @@ def read_events(path: str) -> Iterator[Tuple[int, str, float]]:
             raise ValueError("bad data crc")
         i += 16 + n
         step, j = 0, 0
+        wall = 0.0
         summary = None
         while j < len(rec):
             key, j = _read_varint(rec, j)
             f, wt = key >> 3, key & 7
             if wt == 1:
+                if f == 1:
+                    (wall,) = struct.unpack_from("<d", rec, j)
                 j += 8
             elif wt == 0:
                 v, j = _read_varint(rec, j)
@@ -148,4 +157,4 @@ def read_events(path: str) -> Iterator[Tuple[int, str, float]]:
                     m += 4
                 else:
                     break
-            yield step, tag, value
+            yield wall, step, tag, value

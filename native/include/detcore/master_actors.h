@@ -195,6 +195,9 @@ class ProvisionerActor : public actor::Actor {
 // Generic command task (reference master/internal/command/command.go): run an argv
 // on an agent with N slots (0 = CPU-only, non-preemptible), stream its logs, report exit status.
 struct CommandKill {};
+struct ServiceReady {  // a command's HTTP service is listening (POST /commands/:id/ready)
+  int port = 0;
+};
 class CommandActor : public actor::Actor {
  public:
   CommandActor(Master* m, int64_t id, Json config);
@@ -209,6 +212,7 @@ class CommandActor : public actor::Actor {
   std::string task_id_;
   std::string container_;
   std::string agent_;
+  std::string address_;  // agent address the container runs at (for the service proxy)
   bool killed_ = false;
 };
 

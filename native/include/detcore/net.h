@@ -22,6 +22,7 @@ std::string Base64Encode(const std::string& in);
 std::string Base64Decode(const std::string& in);
 std::string Sha1(const std::string& in);  // 20 raw bytes
 std::string UrlDecode(const std::string& s);
+std::string UrlEncode(const std::string& s);
 
 struct Request {
   std::string method;
@@ -130,10 +131,12 @@ class HttpServer {
 struct ClientResponse {
   int status = 0;
   std::string body;
+  std::string content_type;
   std::string error;  // non-empty on transport failure
 };
 ClientResponse HttpCall(const std::string& host, int port, const std::string& method, const std::string& path,
-                        const std::string& body = "", int timeout_ms = 30000);
+                        const std::string& body = "", int timeout_ms = 30000,
+                        const std::string& content_type = "application/json");
 WsPtr WsConnect(const std::string& host, int port, const std::string& path, std::string* error = nullptr);
 
 int ConnectTcp(const std::string& host, int port, int timeout_ms, std::string* error);

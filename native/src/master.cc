@@ -836,6 +836,7 @@ void Master::InstallRoutes() {
     row["state"] = "PENDING";
     row["start_time"] = NowRFC3339();
     row["description"] = cfg.get_string("description", "");
+    row["type"] = cfg.get_string("type", "command");
     int64_t id = store_->Insert("commands", row);
     Json ctxrow = Json::object();
     ctxrow["files"] = body["context"].is_array() ? body["context"] : Json::array();
@@ -845,11 +846,57 @@ void Master::InstallRoutes() {
     out["id"] = id;
     return J(201, out);
   });
-  http_.Route("GET", "/commands", [this](const net::Request&) {
+  http_.Route("GET", "/commands", [this](const net::Request& r) {
     Json out = Json::array();
-    for (auto& c : store_->Scan("commands")) out.push_back(c);
+    std::string type = r.Query("type", "");
+    for (auto& c : store_->Scan("commands"))
+      if (type.empty() || c.get_string("type", "command") == type) out.push_back(c);
     return J(200, out);
   });
+  http_.Route("POST", "/commands/:id/ready", [this](const net::Request& r) {
+    Json body = Json::parse(r.body.empty() ? "{}" : r.body);
+    Ref ref = sys_->Get("/commands/" + r.Param("id"));
+    if (!ref) return Err(404, "command not running");
+    ServiceReady sr;
+    sr.port = static_cast<int>(body.get_int("port", 0));
+    if (sr.port <= 0) return Err(400, "ready needs a port");
+    auto f = ref->Ask(sr);
+    if (f.wait_for(std::chrono::seconds(10)) != std::future_status::ready) return Err(504, "command did not answer");
+    return J(200, Json::object());
+  });
+  // Service proxy (reference /proxy/:service/*, master/internal/proxy): forwards to a ready
+  // command's HTTP service, e.g. `det tensorboard start` -> /proxy/cmd-<id>/
+  auto proxy = [this](const net::Request& r) {
+    std::string task = r.Param("task");
+    int64_t id = 0;
+    try {
+      id = std::stoll(task.rfind("cmd-", 0) == 0 ? task.substr(4) : task);
+    } catch (const std::exception&) {
+      return Err(404, "unknown service " + task);
+    }
+    Json c;
+    if (!store_->Get("commands", id, &c) || c.get_string("service_address", "").empty())
+      return Err(404, "service " + task + " is not ready");
+    if (c.get_string("state", "") == "TERMINATED") return Err(404, "service " + task + " has exited");
+    std::string addr = c.get_string("service_address", "");
+    auto colon = addr.rfind(':');
+    std::string path = "/" + r.Param("*");
+    std::string qs;
+    for (auto& kv : r.query) qs += (qs.empty() ? "?" : "&") + net::UrlEncode(kv.first) + "=" + net::UrlEncode(kv.second);
+    auto it = r.headers.find("content-type");
+    auto resp = net::HttpCall(addr.substr(0, colon), std::stoi(addr.substr(colon + 1)), r.method, path + qs, r.body,
+                              30000, it == r.headers.end() ? "application/json" : it->second);
+    if (!resp.error.empty()) return Err(502, "proxy: " + resp.error);
+    net::Response out;
+    out.status = resp.status;
+    out.body = resp.body;
+    out.content_type = resp.content_type.empty() ? "application/octet-stream" : resp.content_type;
+    return out;
+  };
+  for (const char* m : {"GET", "POST", "PUT", "DELETE"}) {
+    http_.Route(m, "/proxy/:task/*", proxy);
+    http_.Route(m, "/proxy/:task", proxy);
+  }
   http_.Route("GET", "/commands/:id", [this](const net::Request& r) {
     Json c;
     if (!store_->Get("commands", IntParam(r, "id"), &c)) return Err(404, "command not found");

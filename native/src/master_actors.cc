@@ -1091,11 +1091,22 @@ void CommandActor::Receive(Context& ctx) {
     Save("ASSIGNED");
   } else if (auto cs = ctx.As<ContainerStateMsg>()) {
     if (cs->container_id != container_) return;
-    if (cs->state == "Running") Save("RUNNING");
+    if (cs->state == "Running") {
+      address_ = cs->address.empty() ? "127.0.0.1" : cs->address;
+      Save("RUNNING");
+    }
     if (cs->state == "Terminated") {
       Save("TERMINATED", cs->exit_code);
       ctx.Self()->Stop();
     }
+  } else if (auto sr = ctx.As<ServiceReady>()) {
+    // reference readiness: log-pattern checks (master/internal/command); here the service reports
+    // its bound port, and /proxy/<task>/ forwards to it
+    Json patch = Json::object();
+    patch["service_address"] = (address_.empty() ? std::string("127.0.0.1") : address_) + ":" + std::to_string(sr->port);
+    patch["ready"] = true;
+    m_->store().Update("commands", id_, patch);
+    ctx.Respond(true);
   } else if (ctx.Is<ReleaseResources>() || ctx.Is<CommandKill>()) {
     killed_ = true;
     if (container_.empty()) {

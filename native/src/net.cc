@@ -559,8 +559,23 @@ void HttpServer::Serve(int fd, std::string peer) {
 }
 
 // ------------------------------------------------------------------------------------- clients
+std::string UrlEncode(const std::string& s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string out;
+  for (unsigned char c : s) {
+    if (std::isalnum(c) || c == '-' || c == '_' || c == '.' || c == '~') {
+      out += static_cast<char>(c);
+    } else {
+      out += '%';
+      out += hex[c >> 4];
+      out += hex[c & 15];
+    }
+  }
+  return out;
+}
+
 ClientResponse HttpCall(const std::string& host, int port, const std::string& method, const std::string& path,
-                        const std::string& body, int timeout_ms) {
+                        const std::string& body, int timeout_ms, const std::string& content_type) {
   ClientResponse out;
   int fd = ConnectTcp(host, port, timeout_ms, &out.error);
   if (fd < 0) return out;
@@ -568,7 +583,7 @@ ClientResponse HttpCall(const std::string& host, int port, const std::string& me
   setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
   std::ostringstream os;
   os << method << " " << path << " HTTP/1.1\r\nHost: " << host << ":" << port
-     << "\r\nConnection: close\r\nContent-Type: application/json\r\nContent-Length: " << body.size() << "\r\n\r\n"
+     << "\r\nConnection: close\r\nContent-Type: " << content_type << "\r\nContent-Length: " << body.size() << "\r\n\r\n"
      << body;
   std::string req = os.str();
   if (!WriteAll(fd, req.data(), req.size())) {
@@ -592,7 +607,10 @@ ClientResponse HttpCall(const std::string& host, int port, const std::string& me
   std::string line;
   while (std::getline(hs, line)) {
     auto c = line.find(':');
-    if (c != std::string::npos && Lower(Trim(line.substr(0, c))) == "content-length") cl = std::stoul(Trim(line.substr(c + 1)));
+    if (c == std::string::npos) continue;
+    const std::string key = Lower(Trim(line.substr(0, c)));
+    if (key == "content-length") cl = std::stoul(Trim(line.substr(c + 1)));
+    else if (key == "content-type") out.content_type = Trim(line.substr(c + 1));
   }
   if (cl != std::string::npos) ReadN(fd, buf, cl);
   else {

@@ -15,6 +15,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     m = re.search(r"(bn_\w+)(<[^(]*>)?", name)
     if m:
         return m.group(0)

@@ -286,3 +286,33 @@ def test_provisioner_scales_agents_up_and_down(tmp_path):
     finally:
         p.terminate()
         p.wait(timeout=20)
+
+
+def test_tensorboard_service_through_proxy(cluster):
+    """`det tensorboard start`: a zero-slot command serving the trials' event files, reached
+    through the master's /proxy/cmd-<id>/ route (reference M21 + proxy)."""
+    import requests
+
+    cl, eid = submit(cluster, noop_config({"name": "single", "max_length": {"batches": 10}},
+                                          min_validation_period={"batches": 5}))
+    assert cl.wait_for_experiment(eid, timeout=120) == "COMPLETED"
+    from determined_1_amd.cli.cli import main as det_main
+
+    det_main(["-m", cluster.address, "tensorboard", "start", str(eid), "--timeout", "60"])
+    tbs = cl.get("/commands", type="tensorboard")
+    assert tbs and tbs[-1].get("ready"), tbs
+    cid = tbs[-1]["id"]
+    base = f"http://{cluster.address}/proxy/cmd-{cid}"
+    try:
+        runs = requests.get(f"{base}/data/runs", timeout=10).json()
+        tid = cl.experiment(eid)["trials"][0]["id"]
+        assert runs == [f"exp{eid}/trial{tid}"]
+        tags = requests.get(f"{base}/data/plugin/scalars/tags", timeout=10).json()[runs[0]]
+        assert "Determined/loss" in tags and "validation_error" in tags
+        pts = requests.get(f"{base}/data/plugin/scalars/scalars", params={"run": runs[0], "tag": "Determined/loss"},
+                           timeout=10).json()
+        assert len(pts) >= 10 and all(len(p) == 3 for p in pts)
+        page = requests.get(f"{base}/", timeout=10)
+        assert page.status_code == 200 and "<svg" in page.text and page.headers["Content-Type"].startswith("text/html")
+    finally:
+        cl.post(f"/commands/{cid}/kill")
