@@ -29,6 +29,7 @@ class StepTimers:
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         self._cur[name] = e
+        self._cur["cpu_" + name] = time.perf_counter()  # host issue time: CPU-bound phases show here
 
     def batch_start(self, data_seconds: float) -> None:
         if not self.enabled:
@@ -54,15 +55,19 @@ class StepTimers:
         if not self.enabled or not self._marks:
             return {}
         torch.cuda.synchronize(self.device)
-        acc = {"forward": 0.0, "backward": 0.0, "optimizer": 0.0}
+        acc = {"forward": 0.0, "backward": 0.0, "optimizer": 0.0, "cpu_forward": 0.0, "cpu_backward": 0.0,
+               "cpu_optimizer": 0.0}
         n = 0
         for m in self._marks:
             if not all(k in m for k in ("start", "bwd0", "bwd1")):
                 continue
             acc["forward"] += m["start"].elapsed_time(m["bwd0"])
             acc["backward"] += m["bwd0"].elapsed_time(m["bwd1"])
+            acc["cpu_forward"] += 1000.0 * (m["cpu_bwd0"] - m["cpu_start"])
+            acc["cpu_backward"] += 1000.0 * (m["cpu_bwd1"] - m["cpu_bwd0"])
             if "opt1" in m:
                 acc["optimizer"] += m["bwd1"].elapsed_time(m["opt1"])
+                acc["cpu_optimizer"] += 1000.0 * (m["cpu_opt1"] - m["cpu_bwd1"])
             n += 1
         out = {f"timer/{k}_ms": v / max(1, n) for k, v in acc.items()}
         out["timer/data_ms"] = 1000.0 * self._data_s / max(1, len(self._marks))

@@ -25,6 +25,10 @@ def main() -> None:
     ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
     ap.add_argument("--impl", default="native", choices=["native", "hf"], help="fused MI355X encoder or HF BERT")
     args = ap.parse_args()
+    if os.environ.get("DET_STEP_TIMERS"):
+        import logging
+
+        logging.basicConfig(level=logging.INFO, format="%(message)s")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if torch.cuda.is_available():
