@@ -109,7 +109,7 @@ class BertLayer(nn.Module):
         B, S, H = x.shape
         qkv = tfops.linear(x, self.qkv.weight, self.qkv.bias)  # [B, S, 3H]
         q, k, v = qkv.view(B, S, 3, self.nh, self.hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd] views
-        if mask_bias is not None:
+        if mask_bias is not None and mask_bias.dtype != q.dtype:
             mask_bias = mask_bias.to(q.dtype)
         ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask_bias,
                                              dropout_p=self.p_attn if self.training else 0.0)

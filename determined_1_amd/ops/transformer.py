@@ -26,10 +26,11 @@ FALLBACKS = {"count": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 _MAX_H = 2048
 _offsets = itertools.count(1)
+_seed = []  # lazily cached: the trial seeds torch before the first dropout call
 
 
 def _stream(t: torch.Tensor) -> int:
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return torch._C._cuda_getCurrentRawStream(t.device.index)
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -39,7 +40,9 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 def next_rng() -> Tuple[int, int]:
     """(seed, offset) of the next dropout call: the seed follows the trial's torch seed, the offset
     is unique per call within the process, so masks are reproducible run to run."""
-    return torch.initial_seed() & 0xFFFFFFFFFFFFFFFF, next(_offsets)
+    if not _seed:
+        _seed.append(torch.initial_seed() & 0xFFFFFFFFFFFFFFFF)
+    return _seed[0], next(_offsets)
 
 
 def _native(*ts: Optional[torch.Tensor], width: int, max_width: Optional[int] = None) -> bool:

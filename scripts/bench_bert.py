@@ -24,6 +24,9 @@ def main() -> None:
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
     ap.add_argument("--impl", default="native", choices=["native", "hf"], help="fused MI355X encoder or HF BERT")
+    ap.add_argument("--cprof", default="", help="write a cProfile of the timed steps to this path")
+    ap.add_argument("--autograd-threads", type=int, default=0,
+                    help="1: stock multithreaded autograd engine (the controller disables it by default)")
     args = ap.parse_args()
     if os.environ.get("DET_STEP_TIMERS"):
         import logging
@@ -53,13 +56,26 @@ def main() -> None:
             torch.cuda.synchronize()
         pdist.barrier()
 
+    prof = None
+    if args.cprof:
+        import cProfile
+
+        prof = cProfile.Profile()
+    if args.autograd_threads:
+        os.environ["DET_AUTOGRAD_THREADS"] = "1"
+
     def stream():
         yield workload.train_workload(1, num_batches=args.warmup), [], workload.ignore_response
         sync()
+        if prof is not None:
+            prof.enable()
         t["t0"] = time.perf_counter()
         yield workload.train_workload(2, num_batches=args.steps, total_batches_processed=args.warmup), [], workload.ignore_response
         sync()
         t["t1"] = time.perf_counter()
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(args.cprof)
         yield workload.terminate_workload(3), [], workload.ignore_response
 
     ctrl = make_controller(BertSQuADTrial, cfg, stream(), trial_seed=7)
