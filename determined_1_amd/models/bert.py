@@ -108,12 +108,7 @@ class BertLayer(nn.Module):
     def forward(self, x: torch.Tensor, mask_bias: Optional[torch.Tensor]) -> torch.Tensor:
         B, S, H = x.shape
         qkv = tfops.linear(x, self.qkv.weight, self.qkv.bias)  # [B, S, 3H]
-        q, k, v = qkv.view(B, S, 3, self.nh, self.hd).permute(2, 0, 3, 1, 4).unbind(0)  # [B, nh, S, hd] views
-        if mask_bias is not None and mask_bias.dtype != q.dtype:
-            mask_bias = mask_bias.to(q.dtype)
-        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask_bias,
-                                             dropout_p=self.p_attn if self.training else 0.0)
-        ctx = ctx.transpose(1, 2).reshape(B, S, H)
+        ctx = tfops.qkv_self_attention(qkv, self.nh, mask_bias, self.p_attn, self.training)
         a = tfops.linear_dropout_add_layernorm(ctx, self.attn_out.weight, self.attn_out.bias, x, self.attn_ln.weight,
                                                self.attn_ln.bias, self.p, self.attn_ln.eps, self.training)
         i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias)

@@ -120,6 +120,9 @@ _SIGNATURES = {
     "det_tf_gelu_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
     # stream, dtype, x, rows, C, out, ws
     "det_tf_colsum": ([c_void_p, c_int, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
+    # stream, dtype, gq, gk, gv, strides9 (host int64[9]), out, B, S, nh, hd
+    "det_tf_pack_qkv": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int],
+                        c_int),
     "det_tf_dropout_mask": ([c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p], c_int),
 }
 

@@ -133,3 +133,27 @@ def test_bert_layer_fused_matches_composite(gpu, monkeypatch):
     torch.testing.assert_close(loss_f, loss_c, atol=1e-5, rtol=1e-5)
     for k in g_c:
         torch.testing.assert_close(g_f[k], g_c[k], atol=1e-4, rtol=1e-3, msg=k)
+
+
+@pytest.mark.parametrize("B,S,nh,hd,masked", [(4, 384, 12, 64, True), (2, 128, 4, 64, False)])
+def test_qkv_self_attention(gpu, B, S, nh, hd, masked):
+    """Fused-QKV attention (AOTriton fwd/bwd + det_tf_pack_qkv) vs fp32 SDPA on CPU, dropout off."""
+    torch.manual_seed(5)
+    H = nh * hd
+    qkv = torch.randn(B, S, 3 * H).to(torch.bfloat16).float()
+    am = torch.ones(B, S)
+    if masked:
+        am[0, -37:] = 0
+    bias = ((1.0 - am[:, None, None, :]) * -1e9) if masked else None
+    dy = torch.randn(B, S, H).to(torch.bfloat16).float()
+    ref_in = qkv.clone().requires_grad_(True)
+    q, k, v = ref_in.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias).transpose(1, 2).reshape(B, S, H)
+    ref.backward(dy)
+    dut_in = qkv.to(gpu, torch.bfloat16).requires_grad_(True)
+    before = tfops.FALLBACKS["count"]
+    out = tfops.qkv_self_attention(dut_in, nh, None if bias is None else bias.to(gpu, torch.bfloat16), 0.0)
+    out.backward(dy.to(gpu, torch.bfloat16))
+    assert tfops.FALLBACKS["count"] == before
+    torch.testing.assert_close(out.float().cpu(), ref.detach(), atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, atol=5e-2, rtol=5e-2)
