@@ -215,6 +215,46 @@ def _split_qkv(qkv: torch.Tensor, nh: int):
     return qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # 3 x [B, nh, S, hd] views
 
 
+class _MFMAAttention(torch.autograd.Function):
+    """``det_attention.hip``: hand-written MFMA forward/backward (head_dim 64, S in 128..512).
+    Reads Q/K/V straight from the fused [B, S, 3H] GEMM output and writes dQ/dK/dV straight into
+    its gradient; dropout masks are regenerated from (seed, offset) in the backward."""
+
+    @staticmethod
+    def forward(ctx, qkv, bias, p, nh):
+        B, S, H3 = qkv.shape
+        lib = _lib.get_lib()
+        out = torch.empty(B, S, H3 // 3, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
+        seed, off = next_rng() if p > 0 else (0, 0)
+        _lib.check(lib.det_attn_fwd(_stream(qkv), qkv.data_ptr(), _ptr(bias), out.data_ptr(), lse.data_ptr(), B, S, nh,
+                                    p, seed, off), "det_attn_fwd")
+        ctx.save_for_backward(qkv, bias, out, lse)
+        ctx.p, ctx.nh, ctx.seed, ctx.off = p, nh, seed, off
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, bias, out, lse = ctx.saved_tensors
+        B, S, H3 = qkv.shape
+        lib = _lib.get_lib()
+        dout = dout.contiguous()
+        delta = torch.empty_like(lse)
+        dqkv = torch.empty_like(qkv)
+        _lib.check(lib.det_attn_bwd(_stream(qkv), qkv.data_ptr(), _ptr(bias), out.data_ptr(), dout.data_ptr(),
+                                    lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, S, ctx.nh, ctx.p, ctx.seed,
+                                    ctx.off), "det_attn_bwd")
+        return dqkv, None, None, None
+
+
+def mfma_attention_supported(S: int, head_dim: int) -> bool:
+    import os
+
+    if os.environ.get("DET_ATTN", "mfma") != "mfma":
+        return False
+    return bool(_lib.get_lib().det_attn_supported(S, head_dim))
+
+
 class _QKVAttention(torch.autograd.Function):
     """Self-attention reading Q/K/V as strided views of the fused QKV GEMM output.  Forward and
     backward call the AOTriton memory-efficient attention ops directly; the backward packs dQ/dK/dV
@@ -307,7 +347,22 @@ def qkv_self_attention(qkv: torch.Tensor, num_heads: int, mask_bias: Optional[to
         ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask_bias, dropout_p=p)
         return ctx.transpose(1, 2).reshape(B, S, H3 // 3)
     with torch.autocast("cuda", enabled=False) if ac else _null():
+        if qkv.is_contiguous() and mfma_attention_supported(S, hd) and \
+                (mask_bias is None or mask_bias.numel() == B * S):
+            bias = None if mask_bias is None else mask_bias.reshape(B, S).float().contiguous()
+            return _MFMAAttention.apply(qkv, bias, p, num_heads)
         return _QKVAttention.apply(qkv, mask_bias, p, num_heads)
+
+
+def attention_dropout_mask(B: int, nh: int, S: int, p: float, seed: int, offset: int,
+                           device: torch.device) -> torch.Tensor:
+    """Keep mask [B, nh, S, S] the MFMA attention kernels use for (p, seed, offset) (tests)."""
+    lib = _lib.get_lib()
+    out = torch.empty(B, nh, S, S, dtype=torch.uint8, device=device)
+    with torch.cuda.device(device):
+        _lib.check(lib.det_attn_dropout_mask(torch.cuda.current_stream(device).cuda_stream, B, nh, S, p, seed, offset,
+                                             out.data_ptr()), "det_attn_dropout_mask")
+    return out.bool()
 
 
 def dropout_mask(n: int, p: float, seed: int, offset: int, device: torch.device) -> torch.Tensor:

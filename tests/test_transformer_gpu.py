@@ -157,3 +157,37 @@ def test_qkv_self_attention(gpu, B, S, nh, hd, masked):
     assert tfops.FALLBACKS["count"] == before
     torch.testing.assert_close(out.float().cpu(), ref.detach(), atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, atol=5e-2, rtol=5e-2)
+
+
+@pytest.mark.parametrize("B,S,nh,p", [(2, 384, 4, 0.0), (3, 256, 2, 0.1), (1, 512, 2, 0.2), (2, 128, 3, 0.1)])
+def test_mfma_attention_with_dropout(gpu, monkeypatch, B, S, nh, p):
+    """det_attention.hip fwd+bwd vs an fp32 composite using the kernels' own dropout mask."""
+    hd = 64
+    H = nh * hd
+    assert tfops.mfma_attention_supported(S, hd)
+    torch.manual_seed(6)
+    qkv = (torch.randn(B, S, 3 * H) * 1.5).to(torch.bfloat16).float()
+    am = torch.ones(B, S)
+    am[-1, S - 19:] = 0
+    bias = (1.0 - am) * -10000.0
+    dy = torch.randn(B, S, H).to(torch.bfloat16).float()
+    seed, off = 4242, 9
+    monkeypatch.setattr(tfops, "next_rng", lambda: (seed, off))
+    ref_in = qkv.clone().requires_grad_(True)
+    q, k, v = ref_in.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)
+    probs = torch.softmax(q @ k.transpose(-1, -2) / 8.0 + bias[:, None, None, :], dim=-1)
+    if p > 0:
+        keep = tfops.attention_dropout_mask(B, nh, S, p, seed, off, torch.device(gpu)).cpu()
+        thr = min(65535, int(p * 65536 + 0.5))
+        assert abs(keep.float().mean().item() - (1 - thr / 65536)) < 5e-3
+        probs = probs * keep.float() * (65536.0 / (65536 - thr))
+    ref = (probs @ v).transpose(1, 2).reshape(B, S, H)
+    ref.backward(dy)
+    dut_in = qkv.to(gpu, torch.bfloat16).requires_grad_(True)
+    mb = bias.to(gpu, torch.bfloat16)[:, None, None, :]
+    out = tfops.qkv_self_attention(dut_in, nh, mb, p, training=True)
+    out.backward(dy.to(gpu, torch.bfloat16))
+    torch.testing.assert_close(out.float().cpu(), ref.detach(), atol=3e-2, rtol=3e-2)
+    g, gr = dut_in.grad.float().cpu(), ref_in.grad
+    scale = gr.abs().max().item()
+    torch.testing.assert_close(g / scale, gr / scale, atol=2e-2, rtol=2e-2)
