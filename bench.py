@@ -18,6 +18,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -109,6 +110,15 @@ def main() -> None:
 
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank)
+    t_start = time.perf_counter()
+
+    def heartbeat() -> None:  # MIOpen find mode can run minutes in warmup with no other output
+        while True:
+            time.sleep(30)
+            phase = "timed" if "t0" in timing else "warmup"
+            print(f"[bench rank{rank}] {phase} {time.perf_counter() - t_start:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     ctrl = make_controller(ResNetImageNetTrial, config, stream(), trial_seed=1234)
     ctrl.run()
     elapsed = timing["t1"] - timing["t0"]
