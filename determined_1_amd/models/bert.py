@@ -31,7 +31,7 @@ class BertEncoderConfig:
                  num_attention_heads: int = 12, intermediate_size: int = 3072, hidden_dropout_prob: float = 0.1,
                  attention_probs_dropout_prob: float = 0.1, max_position_embeddings: int = 512,
                  type_vocab_size: int = 2, layer_norm_eps: float = 1e-12, initializer_range: float = 0.02,
-                 pad_token_id: int = 0) -> None:
+                 pad_token_id: int = 0, hidden_act: str = "gelu") -> None:
         self.vocab_size = vocab_size
         self.hidden_size = hidden_size
         self.num_hidden_layers = num_hidden_layers
@@ -44,6 +44,9 @@ class BertEncoderConfig:
         self.layer_norm_eps = layer_norm_eps
         self.initializer_range = initializer_range
         self.pad_token_id = pad_token_id
+        if hidden_act not in ("gelu", "gelu_new"):
+            raise ValueError(f"hidden_act {hidden_act!r}: the fused encoder implements gelu and gelu_new")
+        self.hidden_act = hidden_act
 
     @classmethod
     def from_hparams(cls, hp: Dict[str, Any]) -> "BertEncoderConfig":
@@ -104,6 +107,7 @@ class BertLayer(nn.Module):
         self.ffn_ln = _LN(H, c.layer_norm_eps)
         self.p = c.hidden_dropout_prob
         self.p_attn = c.attention_probs_dropout_prob
+        self.gelu_approx = "tanh" if c.hidden_act == "gelu_new" else "none"
 
     def forward(self, x: torch.Tensor, mask_bias: Optional[torch.Tensor]) -> torch.Tensor:
         B, S, H = x.shape
@@ -111,7 +115,7 @@ class BertLayer(nn.Module):
         ctx = tfops.qkv_self_attention(qkv, self.nh, mask_bias, self.p_attn, self.training)
         a = tfops.linear_dropout_add_layernorm(ctx, self.attn_out.weight, self.attn_out.bias, x, self.attn_ln.weight,
                                                self.attn_ln.bias, self.p, self.attn_ln.eps, self.training)
-        i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias)
+        i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias, self.gelu_approx)
         return tfops.linear_dropout_add_layernorm(i, self.ffn_out.weight, self.ffn_out.bias, a, self.ffn_ln.weight,
                                                   self.ffn_ln.bias, self.p, self.ffn_ln.eps, self.training)
 

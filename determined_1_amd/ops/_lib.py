@@ -115,9 +115,9 @@ _SIGNATURES = {
         c_int,
     ),
     "det_tf_col_ws_elems": ([c_i64, c_int], c_i64),
-    "det_tf_gelu_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_i64], c_int),
+    "det_tf_gelu_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_i64, c_int], c_int),
     # stream, dtype, da, z, dz, rows, C, dbias, ws
-    "det_tf_gelu_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
+    "det_tf_gelu_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, x, rows, C, out, ws
     "det_tf_colsum": ([c_void_p, c_int, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
     # stream, dtype, gq, gk, gv, strides9 (host int64[9]), out, B, S, nh, hd

@@ -10,7 +10,7 @@
 //   ln_bwd        dz = LN'(dy); dr = dz; dh = dropout'(dz) and per-block partial sums of
 //                 dgamma = sum(dy * xhat), dbeta = sum(dy), dbias = sum(dh)   (one pass)
 //   ln_finalize   reduces the partials -> dgamma, dbeta and the preceding Linear's bias grad
-//   gelu_fwd      a = gelu(z) (erf form, as BERT)
+//   gelu_fwd      a = gelu(z) (erf form, as BERT; tanh form for ALBERT's gelu_new)
 //   gelu_bwd      dz = da * gelu'(z) with the bias-grad partials of the producing Linear fused
 //   colsum        bias grad of a plain Linear (QKV) without torch's generic reduction
 //
@@ -19,7 +19,7 @@
 // exactly one Philox block for its 4 consecutive elements.
 //
 // Row kernels (LN): one wavefront per row, lane owns 4 consecutive elements at 4*(lane + 64*i),
-// i < K (K = ceil(H/256), templated, H <= 2048); the two-pass mean/variance is exact in
+// i < K (K = ceil(H/256), templated, H <= 4096); the two-pass mean/variance is exact in
 // registers.  Column reductions use two levels (LDS per block, then a finalize launch) and no
 // float atomics, so every gradient is bitwise reproducible.  No host syncs anywhere.
 //
@@ -35,6 +35,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kFinThreads = 1024;
+constexpr int kMaxH = 4096;  // LayerNorm width limit (ALBERT-xxlarge)
 constexpr int kFinCols = 64;
 constexpr int kFinLanes = kFinThreads / kFinCols;
 
@@ -257,6 +258,11 @@ struct LnBwdArgs {
 
 template <typename T, int K>
 __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
+  // K <= 8 keeps dy, xhat and the dropout factors of the row in registers between the two
+  // passes; wider rows (ALBERT-xxlarge, H = 4096) re-read them from L1/L2 in the second pass
+  // (the row is 8 KB per tensor and was touched a few hundred cycles earlier) instead of spilling.
+  constexpr bool kKeep = K <= 8;
+  constexpr int KR = kKeep ? K : 1;
   extern __shared__ float red[];  // [kWaves][H]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int H4 = a.H >> 2;
@@ -277,43 +283,48 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
     }
   }
   const float inv_h = 1.f / static_cast<float>(a.H);
+  // z = dropout(h) + r for column group c4 of `row`; m = dropout factors
+  auto load_z = [&](int64_t row, int64_t base, int c4, float (&z)[4], float (&m)[4]) {
+    V4<T>::load(h + base + 4 * c4, z);
+    if (a.dropout) {
+      drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z[j] *= m[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = 1.f;
+    }
+    if (r) {
+      float t[4];
+      V4<T>::load(r + base + 4 * c4, t);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z[j] += t[j];
+    }
+  };
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wave; row < a.rows;
        row += static_cast<int64_t>(gridDim.x) * kWaves) {
     const int64_t base = row * a.H;
     const float mean = a.mean[row], rstd = a.rstd[row];
-    float d[K][4], xh[K][4], m[K][4];
+    float d[KR][4], xh[KR][4], m[KR][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const int c4 = lane + 64 * i;
+      const int ir = kKeep ? i : 0;
       if (c4 < H4) {
         float z[4];
-        V4<T>::load(dy + base + 4 * c4, d[i]);
-        V4<T>::load(h + base + 4 * c4, z);
-        if (a.dropout) {
-          drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m[i]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) z[j] *= m[i][j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) m[i][j] = 1.f;
-        }
-        if (r) {
-          float t[4];
-          V4<T>::load(r + base + 4 * c4, t);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) z[j] += t[j];
-        }
+        V4<T>::load(dy + base + 4 * c4, d[ir]);
+        load_z(row, base, c4, z, m[ir]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          xh[i][j] = (z[j] - mean) * rstd;
-          const float dx = d[i][j] * g[i][j];
+          xh[ir][j] = (z[j] - mean) * rstd;
+          const float dx = d[ir][j] * g[i][j];
           s1 += dx;
-          s2 += dx * xh[i][j];
+          s2 += dx * xh[ir][j];
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d[i][j] = xh[i][j] = m[i][j] = 0.f;
+        for (int j = 0; j < 4; ++j) d[ir][j] = xh[ir][j] = m[ir][j] = 0.f;
       }
     }
     s1 = wave_sum(s1) * inv_h;
@@ -321,14 +332,22 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const int c4 = lane + 64 * i;
+      const int ir = kKeep ? i : 0;
       if (c4 < H4) {
+        if (!kKeep) {
+          float z[4];
+          V4<T>::load(dy + base + 4 * c4, d[ir]);
+          load_z(row, base, c4, z, m[ir]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xh[ir][j] = (z[j] - mean) * rstd;
+        }
         float dz[4], dhv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          dz[j] = rstd * (d[i][j] * g[i][j] - s1 - xh[i][j] * s2);
-          dhv[j] = dz[j] * m[i][j];
-          adg[i][j] += d[i][j] * xh[i][j];
-          adb[i][j] += d[i][j];
+          dz[j] = rstd * (d[ir][j] * g[i][j] - s1 - xh[ir][j] * s2);
+          dhv[j] = dz[j] * m[ir][j];
+          adg[i][j] += d[ir][j] * xh[ir][j];
+          adb[i][j] += d[ir][j];
           adh[i][j] += dhv[j];
         }
         if (dr) V4<T>::store(dr + base + 4 * c4, dz);
@@ -429,14 +448,24 @@ ColGeom make_col_geom(int64_t rows, int C) {
   return g;
 }
 
-__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float z) {
-  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
-  return cdf + z * pdf;
+// ACT 0: erf GELU (BERT);  ACT 1: tanh GELU ("gelu_new": ALBERT, GPT-2)
+template <int ACT> __device__ __forceinline__ float gelu_f(float z) {
+  if (ACT == 0) return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+  const float u = 0.7978845608028654f * (z + 0.044715f * z * z * z);
+  return 0.5f * z * (1.f + tanhf(u));
+}
+template <int ACT> __device__ __forceinline__ float gelu_grad(float z) {
+  if (ACT == 0) {
+    const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
+    return cdf + z * pdf;
+  }
+  const float z2 = z * z;
+  const float t = tanhf(0.7978845608028654f * z * (1.f + 0.044715f * z2));
+  return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * z2);
 }
 
-// MODE 0: colsum(x) only;  MODE 1: dz = da * gelu'(z) (stored) and colsum(dz)
+// MODE 0: colsum(x) only;  MODE 1: dz = da * gelu'(z) (stored) and colsum(dz);  MODE 2: as 1, tanh GELU
 template <typename T, int MODE>
 __global__ void __launch_bounds__(kThreads)
 col_kernel(const T* __restrict__ a, const T* __restrict__ z, T* __restrict__ dz, ColGeom g, float* __restrict__ ws) {
@@ -453,11 +482,11 @@ col_kernel(const T* __restrict__ a, const T* __restrict__ z, T* __restrict__ dz,
     const int64_t off = r * C + cg * 8;
     float v[8];
     V8<T>::load(a + off, v);
-    if (MODE == 1) {
+    if (MODE >= 1) {
       float zz[8];
       V8<T>::load(z + off, zz);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(zz[j]);
+      for (int j = 0; j < 8; ++j) v[j] *= gelu_grad<MODE - 1>(zz[j]);
       V8<T>::store(dz + off, v);
     }
 #pragma unroll
@@ -477,14 +506,14 @@ col_kernel(const T* __restrict__ a, const T* __restrict__ z, T* __restrict__ dz,
   }
 }
 
-template <typename T>
+template <typename T, int ACT>
 __global__ void __launch_bounds__(kThreads) gelu_fwd_kernel(const T* __restrict__ z, T* __restrict__ a, int64_t nvec) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
        i += static_cast<int64_t>(gridDim.x) * kThreads) {
     float v[8];
     V8<T>::load(z + i * 8, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f<ACT>(v[j]);
     V8<T>::store(a + i * 8, v);
   }
 }
@@ -559,8 +588,8 @@ int grid_for(int64_t work, int per_block) {
 
 extern "C" {
 
-// Max hidden size of the LayerNorm kernels (K <= 8 register groups of 256 columns).
-int det_tf_ln_max_hidden() { return 2048; }
+// Max hidden size of the LayerNorm kernels (K <= 16 register groups of 256 columns).
+int det_tf_ln_max_hidden() { return kMaxH; }
 
 int64_t det_tf_ln_ws_elems(int64_t rows, int H) { return ln_bwd_blocks(rows) * 3 * static_cast<int64_t>(H); }
 
@@ -569,7 +598,7 @@ int64_t det_tf_ln_ws_elems(int64_t rows, int H) { return ln_bwd_blocks(rows) * 3
 int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y, int64_t rows, int H,
                   const void* gamma, const void* beta, float eps, float p, uint64_t seed, uint64_t offset,
                   float* mean, float* rstd) {
-  if (H % 4 != 0 || H > 2048 || rows <= 0) return -1;
+  if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset)};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int grid = grid_for(rows, kWaves);
@@ -582,7 +611,9 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
     case 3: DET_LNF(T, 3); break;                                                 \
     case 4: DET_LNF(T, 4); break;                                                 \
     case 5: case 6: DET_LNF(T, 6); break;                                         \
-    default: DET_LNF(T, 8); break;                                                \
+    case 7: case 8: DET_LNF(T, 8); break;                                         \
+    case 9: case 10: case 11: case 12: DET_LNF(T, 12); break;                     \
+    default: DET_LNF(T, 16); break;                                               \
   }
   if (dtype == 1) {
     DET_LNF_K(unsigned short)
@@ -598,7 +629,7 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
 int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const void* r, const float* mean,
                   const float* rstd, const void* gamma, int64_t rows, int H, float p, uint64_t seed,
                   uint64_t offset, void* dr, void* dh, void* dgamma, void* dbeta, void* dbias, float* ws) {
-  if (H % 4 != 0 || H > 2048 || rows <= 0) return -1;
+  if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int blocks = static_cast<int>(ln_bwd_blocks(rows));
   LnBwdArgs a{dy, h, r, mean, rstd, gamma, dr, dh, ws, rows, H, p > 0.f, make_rng(p, seed, offset)};
@@ -612,7 +643,9 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
     case 3: DET_LNB(T, 3); break;                                                 \
     case 4: DET_LNB(T, 4); break;                                                 \
     case 5: case 6: DET_LNB(T, 6); break;                                         \
-    default: DET_LNB(T, 8); break;                                                \
+    case 7: case 8: DET_LNB(T, 8); break;                                         \
+    case 9: case 10: case 11: case 12: DET_LNB(T, 12); break;                     \
+    default: DET_LNB(T, 16); break;                                               \
   }
   if (dtype == 1) {
     DET_LNB_K(unsigned short)
@@ -633,39 +666,51 @@ int64_t det_tf_col_ws_elems(int64_t rows, int C) {
   return static_cast<int64_t>(g.nrb) * C;
 }
 
-// a = gelu(z), elementwise over n elements (n % 8 == 0).
-int det_tf_gelu_fwd(void* stream, int dtype, const void* z, void* a, int64_t n) {
+// a = gelu(z), elementwise over n elements (n % 8 == 0); approx = 1 selects the tanh form.
+int det_tf_gelu_fwd(void* stream, int dtype, const void* z, void* a, int64_t n, int approx) {
   if (n % 8 != 0 || n <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nvec = n / 8;
   const int grid = grid_for(nvec, kThreads * 4);
-  if (dtype == 1)
-    hipLaunchKernelGGL(gelu_fwd_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st,
-                       static_cast<const unsigned short*>(z), static_cast<unsigned short*>(a), nvec);
-  else
-    hipLaunchKernelGGL(gelu_fwd_kernel<float>, dim3(grid), dim3(kThreads), 0, st, static_cast<const float*>(z),
-                       static_cast<float*>(a), nvec);
+#define DET_GELUF(T, ACT)                                                                          \
+  hipLaunchKernelGGL((gelu_fwd_kernel<T, ACT>), dim3(grid), dim3(kThreads), 0, st, static_cast<const T*>(z), \
+                     static_cast<T*>(a), nvec)
+  if (dtype == 1) {
+    if (approx) DET_GELUF(unsigned short, 1); else DET_GELUF(unsigned short, 0);
+  } else {
+    if (approx) DET_GELUF(float, 1); else DET_GELUF(float, 0);
+  }
+#undef DET_GELUF
   return static_cast<int>(hipGetLastError());
 }
 
-// dz = da * gelu'(z) over [rows, C]; dbias (nullable) = column sums of dz.
+// dz = da * gelu'(z) over [rows, C]; dbias (nullable) = column sums of dz.  approx = 1: tanh form.
 int det_tf_gelu_bwd(void* stream, int dtype, const void* da, const void* z, void* dz, int64_t rows, int C,
-                    void* dbias, float* ws) {
+                    void* dbias, float* ws, int approx) {
   if (C % 8 != 0 || rows <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   ColGeom g = make_col_geom(rows, C);
   dim3 grid(g.nrb, C / 8 / g.tpr);
   float* w = dbias ? ws : nullptr;
   if (dtype == 1) {
-    hipLaunchKernelGGL((col_kernel<unsigned short, 1>), grid, dim3(kThreads), 0, st,
-                       static_cast<const unsigned short*>(da), static_cast<const unsigned short*>(z),
-                       static_cast<unsigned short*>(dz), g, w);
+    if (approx)
+      hipLaunchKernelGGL((col_kernel<unsigned short, 2>), grid, dim3(kThreads), 0, st,
+                         static_cast<const unsigned short*>(da), static_cast<const unsigned short*>(z),
+                         static_cast<unsigned short*>(dz), g, w);
+    else
+      hipLaunchKernelGGL((col_kernel<unsigned short, 1>), grid, dim3(kThreads), 0, st,
+                         static_cast<const unsigned short*>(da), static_cast<const unsigned short*>(z),
+                         static_cast<unsigned short*>(dz), g, w);
     if (dbias)
       hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0,
                          st, ws, g.nrb, C, C, static_cast<unsigned short*>(dbias), nullptr, nullptr);
   } else {
-    hipLaunchKernelGGL((col_kernel<float, 1>), grid, dim3(kThreads), 0, st, static_cast<const float*>(da),
-                       static_cast<const float*>(z), static_cast<float*>(dz), g, w);
+    if (approx)
+      hipLaunchKernelGGL((col_kernel<float, 2>), grid, dim3(kThreads), 0, st, static_cast<const float*>(da),
+                         static_cast<const float*>(z), static_cast<float*>(dz), g, w);
+    else
+      hipLaunchKernelGGL((col_kernel<float, 1>), grid, dim3(kThreads), 0, st, static_cast<const float*>(da),
+                         static_cast<const float*>(z), static_cast<float*>(dz), g, w);
     if (dbias)
       hipLaunchKernelGGL(colsum_finalize<float>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
                          g.nrb, C, C, static_cast<float*>(dbias), nullptr, nullptr);

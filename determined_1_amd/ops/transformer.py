@@ -1,7 +1,7 @@
 """Fused transformer-encoder ops on the ``det_transformer.hip`` kernels.
 
     linear(x, W, b)                                   y = x W^T + b, bias grad by det_tf_colsum
-    linear_gelu(x, W, b)                              a = gelu(x W^T + b), bias grad fused in gelu bwd
+    linear_gelu(x, W, b[, approximate])               a = gelu(x W^T + b), bias grad fused in gelu bwd
     linear_dropout_add_layernorm(x, W, b, r, g, be)   y = LN(dropout(x W^T + b) + r)
     layer_norm(x, g, be)                              y = LN(x)
 
@@ -10,7 +10,7 @@ pass per direction, and every Linear's bias gradient is produced inside the kern
 reads the gradient (LayerNorm bwd, GELU bwd) instead of a separate reduction.  Dropout masks are
 regenerated from a Philox (seed, offset) pair in the backward pass rather than stored.
 
-CPU tensors, and GPU layouts the kernels do not cover (fp16, hidden > 2048, hidden % 8 != 0),
+CPU tensors, and GPU layouts the kernels do not cover (fp16, hidden > 4096, hidden % 8 != 0),
 run the plain PyTorch composite, which is also the numerics reference of the GPU tests; GPU
 fallbacks are counted in ``FALLBACKS`` so benchmarks can assert the native path ran.
 """
@@ -25,7 +25,7 @@ from determined_1_amd.ops import _lib
 
 FALLBACKS = {"count": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
-_MAX_H = 2048
+_MAX_H = 4096  # det_tf_ln_max_hidden(): ALBERT-xxlarge width
 ctypes_i64 = ctypes.c_int64
 _offsets = itertools.count(1)
 _seed = []  # lazily cached: the trial seeds torch before the first dropout call
@@ -106,13 +106,14 @@ class _Linear(torch.autograd.Function):
 
 class _LinearGELU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, approx):
         x2 = x.reshape(-1, x.shape[-1])
         z = _addmm(x2, weight, bias)
         a = torch.empty_like(z)
         lib = _lib.get_lib()
-        _lib.check(lib.det_tf_gelu_fwd(_stream(z), _DT[z.dtype], z.data_ptr(), a.data_ptr(), z.numel()),
+        _lib.check(lib.det_tf_gelu_fwd(_stream(z), _DT[z.dtype], z.data_ptr(), a.data_ptr(), z.numel(), int(approx)),
                    "det_tf_gelu_fwd")
+        ctx.approx = int(approx)
         ctx.save_for_backward(x2, weight, z)
         ctx.has_bias = bias is not None
         ctx.xshape = x.shape
@@ -129,9 +130,9 @@ class _LinearGELU(torch.autograd.Function):
         ws = torch.empty(int(lib.det_tf_col_ws_elems(rows, C)) if db is not None else 1, dtype=torch.float32,
                          device=z.device)
         _lib.check(lib.det_tf_gelu_bwd(_stream(z), _DT[z.dtype], da2.data_ptr(), z.data_ptr(), dz.data_ptr(), rows, C,
-                                       _ptr(db), ws.data_ptr()), "det_tf_gelu_bwd")
+                                       _ptr(db), ws.data_ptr(), ctx.approx), "det_tf_gelu_bwd")
         dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, db
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None
 
 
 def _ln_forward(h: torch.Tensor, r: Optional[torch.Tensor], gamma, beta, p: float, eps: float):
@@ -302,12 +303,14 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         return _Linear.apply(x, weight, bias)
 
 
-def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                approximate: str = "none") -> torch.Tensor:
+    """``gelu(x W^T + b)``; ``approximate="tanh"`` is HF's ``gelu_new`` (ALBERT, GPT-2)."""
     (x, weight, bias), ac = _autocast(x, weight, bias)
     if not _native(x, weight, bias, width=weight.shape[0]):
-        return F.gelu(F.linear(x, weight, bias))
+        return F.gelu(F.linear(x, weight, bias), approximate=approximate)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _LinearGELU.apply(x, weight, bias)
+        return _LinearGELU.apply(x, weight, bias, approximate == "tanh")
 
 
 def linear_dropout_add_layernorm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],

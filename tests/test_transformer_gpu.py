@@ -25,6 +25,8 @@ def _leaf(t, dev=None, dt=None):
     (1000, 3072, 768, torch.bfloat16, 0.1),
     (300, 256, 1024, torch.float32, 0.1),
     (77, 64, 200, torch.float32, 0.25),  # H not a multiple of 256 (inactive lanes)
+    (768, 512, 4096, torch.bfloat16, 0.0),  # ALBERT-xxlarge width (K = 16 register groups, re-read bwd)
+    (200, 256, 3072, torch.float32, 0.1),   # K = 12
 ])
 def test_linear_dropout_add_layernorm(gpu, monkeypatch, rows, K, H, dt, p):
     torch.manual_seed(0)
@@ -60,19 +62,24 @@ def test_linear_dropout_add_layernorm(gpu, monkeypatch, rows, K, H, dt, p):
         torch.testing.assert_close(a.grad.float().cpu() / scale, e.grad / scale, **tol, msg=name)
 
 
-@pytest.mark.parametrize("rows,K,N,dt", [(512, 768, 3072, torch.float32), (4608, 768, 3072, torch.bfloat16),
-                                         (100, 64, 264, torch.float32)])
-def test_linear_gelu(gpu, rows, K, N, dt):
+@pytest.mark.parametrize("rows,K,N,dt,approx", [(512, 768, 3072, torch.float32, "none"),
+                                                (4608, 768, 3072, torch.bfloat16, "none"),
+                                                (100, 64, 264, torch.float32, "none"),
+                                                (512, 256, 1024, torch.float32, "tanh"),
+                                                (1536, 512, 2048, torch.bfloat16, "tanh")])
+def test_linear_gelu(gpu, rows, K, N, dt, approx):
     torch.manual_seed(1)
     x, w, b = torch.randn(rows, K).to(dt).float(), (torch.randn(N, K) / K ** 0.5).to(dt).float(), torch.randn(N).to(dt).float()
     da = torch.randn(rows, N).to(dt).float()
     ref = [_leaf(t) for t in (x, w, b)]
-    F.gelu(F.linear(*ref)).backward(da)
+    F.gelu(F.linear(*ref), approximate=approx).backward(da)
     dut = [_leaf(t, gpu, dt) for t in (x, w, b)]
-    out = tfops.linear_gelu(*dut)
+    before = tfops.FALLBACKS["count"]
+    out = tfops.linear_gelu(*dut, approximate=approx)
     out.backward(da.to(gpu, dt))
+    assert tfops.FALLBACKS["count"] == before, "fused path fell back"
     tol = _tol(dt)
-    torch.testing.assert_close(out.float().cpu(), F.gelu(F.linear(x, w, b)), **tol)
+    torch.testing.assert_close(out.float().cpu(), F.gelu(F.linear(x, w, b), approximate=approx), **tol)
     for a, e in zip(dut, ref):
         scale = max(1.0, e.grad.abs().max().item())
         torch.testing.assert_close(a.grad.float().cpu() / scale, e.grad / scale, **tol)
@@ -117,6 +124,37 @@ def test_bert_layer_fused_matches_composite(gpu, monkeypatch):
     am = torch.ones_like(ids)
     am[1, -10:] = 0
     s = torch.randint(0, 128, (4,), device=gpu)
+    e = (s + 2).clamp(max=127)
+
+    def run():
+        m.zero_grad(set_to_none=True)
+        out = m(ids, None, am, s, e)
+        out.loss.backward()
+        return out.loss.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+    before = tfops.FALLBACKS["count"]
+    loss_f, g_f = run()
+    assert tfops.FALLBACKS["count"] == before
+    monkeypatch.setattr(tfops, "_native", lambda *a, **k: False)
+    loss_c, g_c = run()
+    torch.testing.assert_close(loss_f, loss_c, atol=1e-5, rtol=1e-5)
+    for k in g_c:
+        torch.testing.assert_close(g_f[k], g_c[k], atol=1e-4, rtol=1e-3, msg=k)
+
+
+def test_albert_fused_matches_composite(gpu, monkeypatch):
+    """Shared-layer ALBERT (tanh GELU, factorised embeddings) in fp32 on the GPU: fused kernels vs
+    the composite path."""
+    from determined_1_amd.models.albert import AlbertConfig, AlbertForQA
+
+    cfg = AlbertConfig(vocab_size=512, embedding_size=64, hidden_size=256, num_hidden_layers=3, num_attention_heads=4,
+                       intermediate_size=1024, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    torch.manual_seed(5)
+    m = AlbertForQA(cfg).to(gpu)
+    ids = torch.randint(1, 512, (2, 128), device=gpu)
+    am = torch.ones_like(ids)
+    am[0, -7:] = 0
+    s = torch.randint(0, 128, (2,), device=gpu)
     e = (s + 2).clamp(max=127)
 
     def run():
