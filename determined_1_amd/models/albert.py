@@ -12,8 +12,9 @@ HF checkpoints onto this layout and the CPU tests pin both to the same outputs):
     ``embedding_hidden_mapping_in`` Linear E -> H;
   * ONE transformer layer (fused QKV GEMM, MFMA attention, Linear+dropout+residual+LayerNorm and
     Linear+tanh-GELU on ``det_transformer.hip``) applied ``num_hidden_layers`` times with shared
-    weights — autograd sums the 12 per-use weight gradients in its input buffer, so the shared
-    parameters produce one gradient per backward and land in the arena / all-reduce bucket once;
+    weights — the 12 per-use weight gradients accumulate in one buffer through the dW GEMMs
+    themselves (``tfops.SharedWeightGrads``: beta = 1, no elementwise sums), so each shared
+    parameter produces one gradient per backward and lands in the arena / all-reduce bucket once;
   * QA head Linear(H, 2).
 Weights are random-init (no network for pretrained checkpoints); data is ``SyntheticSQuAD``.
 """
@@ -103,8 +104,9 @@ class AlbertForQA(nn.Module):
         mask_bias = None
         if attention_mask is not None:
             mask_bias = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * torch.finfo(x.dtype).min
+        acc = tfops.SharedWeightGrads()  # one dW buffer per shared weight, accumulated by GEMM beta=1
         for _ in range(self.config.num_hidden_layers):
-            x = self.layer(x, mask_bias)
+            x = self.layer(x, mask_bias, acc)
         logits = self.qa_outputs(x)
         start_logits, end_logits = (t.squeeze(-1).contiguous() for t in logits.split(1, dim=-1))
         loss = None

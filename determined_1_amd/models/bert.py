@@ -109,15 +109,17 @@ class BertLayer(nn.Module):
         self.p_attn = c.attention_probs_dropout_prob
         self.gelu_approx = "tanh" if c.hidden_act == "gelu_new" else "none"
 
-    def forward(self, x: torch.Tensor, mask_bias: Optional[torch.Tensor]) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, mask_bias: Optional[torch.Tensor],
+                acc: Optional[tfops.SharedWeightGrads] = None) -> torch.Tensor:
+        """``acc``: weight-gradient accumulator when this layer is applied repeatedly (ALBERT)."""
         B, S, H = x.shape
-        qkv = tfops.linear(x, self.qkv.weight, self.qkv.bias)  # [B, S, 3H]
+        qkv = tfops.linear(x, self.qkv.weight, self.qkv.bias, acc=acc)  # [B, S, 3H]
         ctx = tfops.qkv_self_attention(qkv, self.nh, mask_bias, self.p_attn, self.training)
         a = tfops.linear_dropout_add_layernorm(ctx, self.attn_out.weight, self.attn_out.bias, x, self.attn_ln.weight,
-                                               self.attn_ln.bias, self.p, self.attn_ln.eps, self.training)
-        i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias, self.gelu_approx)
+                                               self.attn_ln.bias, self.p, self.attn_ln.eps, self.training, acc=acc)
+        i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias, self.gelu_approx, acc=acc)
         return tfops.linear_dropout_add_layernorm(i, self.ffn_out.weight, self.ffn_out.bias, a, self.ffn_ln.weight,
-                                                  self.ffn_ln.bias, self.p, self.ffn_ln.eps, self.training)
+                                                  self.ffn_ln.bias, self.p, self.ffn_ln.eps, self.training, acc=acc)
 
 
 class BertForQA(nn.Module):

@@ -68,10 +68,50 @@ def _autocast(*ts: Optional[torch.Tensor]):
     return list(ts), False
 
 
-def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool):
+class SharedWeightGrads:
+    """Weight gradients of layers applied several times in one forward (ALBERT's shared layer).
+
+    Autograd would compute one dW per use and sum them in its input buffer: an elementwise add of
+    the whole weight per extra use (11 x 201M elements per ALBERT-xxlarge step, 6 % of the step
+    in profiles/r1_albert_xxlarge_bs8_o2_per_step.txt).  Instead the first backward use writes dW
+    with a GEMM, later uses accumulate into it with ``addmm_`` (hipBLASLt beta = 1, no extra pass)
+    and only the last use hands the buffer to autograd; the other uses return None.
+    Create one per forward pass (``track`` counts the uses of each weight)."""
+
+    def __init__(self) -> None:
+        self._state = {}  # id(weight) -> [remaining uses, buffer]
+
+    def track(self, weight: torch.Tensor) -> "SharedWeightGrads":
+        st = self._state.setdefault(id(weight), [0, None])
+        st[0] += 1
+        return self
+
+    def accumulate(self, weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> Optional[torch.Tensor]:
+        st = self._state[id(weight)]
+        if st[1] is None:
+            st[1] = dz.t() @ x2
+        else:
+            st[1].addmm_(dz.t(), x2)
+        st[0] -= 1
+        if st[0] > 0:
+            return None
+        out, st[1] = st[1], None
+        return out
+
+
+def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool,
+                 acc: Optional[SharedWeightGrads] = None):
     dx = dz @ weight if need_x else None
-    dw = dz.t() @ x2 if need_w else None
+    dw = None
+    if need_w:
+        dw = acc.accumulate(weight, dz, x2) if acc is not None else dz.t() @ x2
     return dx, dw
+
+
+def _track(acc: Optional[SharedWeightGrads], weight: torch.Tensor) -> Optional[SharedWeightGrads]:
+    if acc is None or not (torch.is_grad_enabled() and weight.requires_grad):
+        return None
+    return acc.track(weight)
 
 
 def _addmm(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
@@ -80,9 +120,10 @@ def _addmm(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor])
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, acc):
         x2 = x.reshape(-1, x.shape[-1])
         y = _addmm(x2, weight, bias)
+        ctx.acc = acc
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         ctx.xshape = x.shape
@@ -92,7 +133,7 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x2, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, weight.shape[0]).contiguous()
-        dx, dw = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dx, dw = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             lib = _lib.get_lib()
@@ -101,12 +142,12 @@ class _Linear(torch.autograd.Function):
             ws = torch.empty(int(lib.det_tf_col_ws_elems(rows, C)), dtype=torch.float32, device=dy2.device)
             _lib.check(lib.det_tf_colsum(_stream(dy2), _DT[dy2.dtype], dy2.data_ptr(), rows, C, db.data_ptr(),
                                          ws.data_ptr()), "det_tf_colsum")
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, db
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None
 
 
 class _LinearGELU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, approx):
+    def forward(ctx, x, weight, bias, approx, acc):
         x2 = x.reshape(-1, x.shape[-1])
         z = _addmm(x2, weight, bias)
         a = torch.empty_like(z)
@@ -114,6 +155,7 @@ class _LinearGELU(torch.autograd.Function):
         _lib.check(lib.det_tf_gelu_fwd(_stream(z), _DT[z.dtype], z.data_ptr(), a.data_ptr(), z.numel(), int(approx)),
                    "det_tf_gelu_fwd")
         ctx.approx = int(approx)
+        ctx.acc = acc
         ctx.save_for_backward(x2, weight, z)
         ctx.has_bias = bias is not None
         ctx.xshape = x.shape
@@ -131,8 +173,8 @@ class _LinearGELU(torch.autograd.Function):
                          device=z.device)
         _lib.check(lib.det_tf_gelu_bwd(_stream(z), _DT[z.dtype], da2.data_ptr(), z.data_ptr(), dz.data_ptr(), rows, C,
                                        _ptr(db), ws.data_ptr(), ctx.approx), "det_tf_gelu_bwd")
-        dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None
+        dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None
 
 
 def _ln_forward(h: torch.Tensor, r: Optional[torch.Tensor], gamma, beta, p: float, eps: float):
@@ -166,8 +208,9 @@ def _ln_backward(ctx, dy, h, r, gamma, mean, rstd, need_dh: bool, need_dr: bool,
 
 class _LinearDropAddLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, gamma, beta, p, eps):
+    def forward(ctx, x, weight, bias, residual, gamma, beta, p, eps, acc):
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.acc = acc
         h = _addmm(x2, weight, bias)
         r2 = residual.reshape(h.shape).contiguous()
         y, mean, rstd, ctx.seed, ctx.off = _ln_forward(h, r2, gamma, beta, p, eps)
@@ -185,10 +228,10 @@ class _LinearDropAddLN(torch.autograd.Function):
         dh, dr, dgamma, dbeta, dbias = _ln_backward(
             ctx, dy, h, r2, gamma, mean, rstd, need_dh=True, need_dr=ctx.needs_input_grad[3],
             need_bias=ctx.has_bias and ctx.needs_input_grad[2])
-        dx, dw = (_mm_backward(dh, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dx, dw = (_mm_backward(dh, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
                   if need_h else (None, None))
         return ((dx.view(ctx.xshape) if dx is not None else None), dw, dbias,
-                (dr.view(ctx.rshape) if dr is not None else None), dgamma, dbeta, None, None)
+                (dr.view(ctx.rshape) if dr is not None else None), dgamma, dbeta, None, None, None)
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -295,27 +338,29 @@ class _QKVAttention(torch.autograd.Function):
 # ------------------------------------------------------------------------------------------------
 # public functional API (composite reference on CPU / uncovered layouts)
 # ------------------------------------------------------------------------------------------------
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+           acc: Optional[SharedWeightGrads] = None) -> torch.Tensor:
     (x, weight, bias), ac = _autocast(x, weight, bias)
     if not _native(x, weight, bias, width=weight.shape[0]):
         return F.linear(x, weight, bias)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _Linear.apply(x, weight, bias)
+        return _Linear.apply(x, weight, bias, _track(acc, weight))
 
 
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
-                approximate: str = "none") -> torch.Tensor:
+                approximate: str = "none", *, acc: Optional[SharedWeightGrads] = None) -> torch.Tensor:
     """``gelu(x W^T + b)``; ``approximate="tanh"`` is HF's ``gelu_new`` (ALBERT, GPT-2)."""
     (x, weight, bias), ac = _autocast(x, weight, bias)
     if not _native(x, weight, bias, width=weight.shape[0]):
         return F.gelu(F.linear(x, weight, bias), approximate=approximate)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _LinearGELU.apply(x, weight, bias, approximate == "tanh")
+        return _LinearGELU.apply(x, weight, bias, approximate == "tanh", _track(acc, weight))
 
 
 def linear_dropout_add_layernorm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
                                  residual: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, p: float = 0.0,
-                                 eps: float = 1e-12, training: bool = True) -> torch.Tensor:
+                                 eps: float = 1e-12, training: bool = True, *,
+                                 acc: Optional[SharedWeightGrads] = None) -> torch.Tensor:
     """``LayerNorm(dropout(x W^T + b) + residual)`` — BERT's SelfOutput / Output block."""
     p = float(p) if training else 0.0
     (x, weight, bias, residual, gamma, beta), ac = _autocast(x, weight, bias, residual, gamma, beta)
@@ -323,7 +368,7 @@ def linear_dropout_add_layernorm(x: torch.Tensor, weight: torch.Tensor, bias: Op
         h = F.dropout(F.linear(x, weight, bias), p, training)
         return F.layer_norm(h + residual, (weight.shape[0],), gamma, beta, eps)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _LinearDropAddLN.apply(x, weight, bias, residual, gamma, beta, p, float(eps))
+        return _LinearDropAddLN.apply(x, weight, bias, residual, gamma, beta, p, float(eps), _track(acc, weight))
 
 
 def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:

@@ -72,3 +72,28 @@ def test_xxlarge_v2_param_count():
     with torch.device("meta"):
         hf = transformers.AlbertForQuestionAnswering(hf_cfg)
     assert sum(p.numel() for p in m.parameters()) == sum(p.numel() for p in hf.parameters())
+
+
+def test_shared_weight_grads_accumulate_through_gemm():
+    """SharedWeightGrads: 3 uses of one weight -> the last backward use returns the summed dW
+    (GEMM beta=1 accumulation), the others None; equals autograd's own summation."""
+    from determined_1_amd.ops import transformer as tfops
+
+    torch.manual_seed(0)
+    w = torch.randn(16, 16, requires_grad=True)
+    x = torch.randn(5, 16, requires_grad=True)
+    acc = tfops.SharedWeightGrads()
+    y = x
+    for _ in range(3):
+        y = torch.tanh(tfops._Linear.apply(y, w, None, tfops._track(acc, w)))
+    y.sum().backward()
+    g_acc, gx_acc = w.grad.clone(), x.grad.clone()
+    w.grad = None
+    x.grad = None
+    y = x
+    for _ in range(3):
+        y = torch.tanh(torch.nn.functional.linear(y, w))
+    y.sum().backward()
+    torch.testing.assert_close(g_acc, w.grad)
+    torch.testing.assert_close(gx_acc, x.grad)
+    assert not any(st[1] is not None for st in acc._state.values())
