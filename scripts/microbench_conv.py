@@ -8,7 +8,7 @@ import torch.nn.functional as F
 
 torch.backends.cudnn.benchmark = bool(int(sys.argv[1])) if len(sys.argv) > 1 else False
 dev = torch.device("cuda")
-N = 256
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 # (Cin, Cout, k, stride, H_in) for every distinct conv of ResNet-50 v1.5, with multiplicity
 shapes = {}
 def add(ci, co, k, s, h):

@@ -197,7 +197,8 @@ def test_qkv_self_attention(gpu, B, S, nh, hd, masked):
     torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, atol=5e-2, rtol=5e-2)
 
 
-@pytest.mark.parametrize("B,S,nh,p", [(2, 384, 4, 0.0), (3, 256, 2, 0.1), (1, 512, 2, 0.2), (2, 128, 3, 0.1)])
+@pytest.mark.parametrize("B,S,nh,p", [(2, 384, 4, 0.0), (3, 256, 2, 0.1), (1, 512, 2, 0.2), (2, 128, 3, 0.1),
+                                      (2, 192, 2, 0.1), (1, 1024, 2, 0.0), (2, 64, 2, 0.0)])
 def test_mfma_attention_with_dropout(gpu, monkeypatch, B, S, nh, p):
     """det_attention.hip fwd+bwd vs an fp32 composite using the kernels' own dropout mask."""
     hd = 64
