@@ -109,7 +109,7 @@ def main() -> None:
         yield workload.terminate_workload(3), [], workload.ignore_response
 
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(pdist.local_cuda_device(local_rank))
     t_start = time.perf_counter()
 
     def heartbeat() -> None:  # MIOpen find mode can run minutes in warmup with no other output

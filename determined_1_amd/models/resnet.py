@@ -12,6 +12,7 @@ import torch
 import torch.nn as nn
 
 from determined_1_amd.ops.norm import BatchNormAct2d
+from determined_1_amd.ops.pool import MaxPool3x3s2
 
 # Fused BN(+add)(+ReLU) HIP kernels (ops/csrc/det_norm.hip) on by default; set
 # ``resnet.FUSED_BN = False`` (or hparam ``fused_bn: false``) for the stock MIOpen path.
@@ -45,7 +46,7 @@ class BasicBlock(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else self.downsample(x)
         out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), idt)
+        return self.bn2(self.conv2(out), idt, shortcut_link=self.downsample is None)
 
 
 class Bottleneck(nn.Module):
@@ -66,7 +67,8 @@ class Bottleneck(nn.Module):
         idt = x if self.downsample is None else self.downsample(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), idt)
+        # identity shortcut: its gradient goes straight to the previous block's fused BN backward
+        return self.bn3(self.conv3(out), idt, shortcut_link=self.downsample is None)
 
 
 class ResNet(nn.Module):
@@ -77,7 +79,7 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = bn(64, relu=True)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool3x3s2() if FUSED_BN else nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

@@ -42,11 +42,10 @@ constexpr int kFinLanes = kFinThreads / kFinCh;
 typedef unsigned short us8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+// RNE; adjacent conversions pair into gfx950's v_cvt_pk_bf16_f32 (1 op per 2 elements instead of
+// ~6 per element: the apply kernels are close enough to the HBM roof that VALU work shows)
 __device__ __forceinline__ unsigned short f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<unsigned short>((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<unsigned short>(u >> 16);
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
 }
 
 // 8-element vector IO: bf16 = one 16 B load, fp32 = two 16 B loads.
@@ -295,7 +294,8 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
     for (int u = 0; u < 4; ++u) {
       const int64_t v = v0 + u * S;
       if (v < nvec) {
-        const int c0 = static_cast<int>((v * 8) % C);
+        // vector index -> first channel; 32-bit modulo (nvec < 2^32 checked on the host)
+        const int c0 = static_cast<int>(static_cast<uint32_t>(v) % static_cast<uint32_t>(C >> 3)) << 3;
         float sc[8], sh[8], o[8];
         load8f(scale + c0, sc);
         load8f(shift + c0, sh);
@@ -321,7 +321,8 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
 // ---------------------------------------------------------------------------------------------
 template <typename T, int MASK>
 __global__ void __launch_bounds__(kThreads)
-bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t* __restrict__ mbits, Geom g,
+bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ dy2, const T* __restrict__ x,
+               const uint8_t* __restrict__ mbits, Geom g,
                const float* __restrict__ mean, const float* __restrict__ scale,
                const float* __restrict__ shift, float* __restrict__ psum, float* __restrict__ psumx) {
   __shared__ float l1[kThreads * 8];
@@ -349,6 +350,13 @@ bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t*
       IO8<T>::load(x + r * C + off, x0);
       IO8<T>::load(dy + (r + R) * C + off, d1);
       IO8<T>::load(x + (r + R) * C + off, x1);
+      if (dy2) {
+        float e0[8], e1[8];
+        IO8<T>::load(dy2 + r * C + off, e0);
+        IO8<T>::load(dy2 + (r + R) * C + off, e1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { d0[j] += e0[j]; d1[j] += e1[j]; }
+      }
       if (MASK == 2) { b0 = mbits[(r * C + off) >> 3]; b1 = mbits[((r + R) * C + off) >> 3]; }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -369,6 +377,12 @@ bn_bwd_partial(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t*
       unsigned b0 = 0xFFu;
       IO8<T>::load(dy + r * C + off, d0);
       IO8<T>::load(x + r * C + off, x0);
+      if (dy2) {
+        float e0[8];
+        IO8<T>::load(dy2 + r * C + off, e0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d0[j] += e0[j];
+      }
       if (MASK == 2) b0 = mbits[(r * C + off) >> 3];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -462,7 +476,8 @@ bn_bwd_finalize(const float* __restrict__ psum, const float* __restrict__ psumx,
 
 template <typename T, int MASK, bool DRES>
 __global__ void __launch_bounds__(kThreads)
-bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t* __restrict__ mbits,
+bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ dy2, const T* __restrict__ x,
+             const uint8_t* __restrict__ mbits,
              const float* __restrict__ coef, const float* __restrict__ scale,
              const float* __restrict__ shift, T* __restrict__ dx, T* __restrict__ dres,
              int64_t nvec, int C) {
@@ -476,6 +491,12 @@ bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t* _
       if (v < nvec) {
         IO8<T>::load(dy + v * 8, dv[u]);
         IO8<T>::load(x + v * 8, xv[u]);
+        if (dy2) {
+          float e[8];
+          IO8<T>::load(dy2 + v * 8, e);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dv[u][j] += e[j];
+        }
         if (MASK == 2) mb[u] = mbits[v];
       }
     }
@@ -483,7 +504,8 @@ bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ x, const uint8_t* _
     for (int u = 0; u < 2; ++u) {
       const int64_t v = v0 + u * S;
       if (v < nvec) {
-        const int c0 = static_cast<int>((v * 8) % C);
+        // vector index -> first channel; 32-bit modulo (nvec < 2^32 checked on the host)
+        const int c0 = static_cast<int>(static_cast<uint32_t>(v) % static_cast<uint32_t>(C >> 3)) << 3;
         float A[8], B[8], Cc[8], o[8], dz[8];
         load8f(coef + c0, A);
         load8f(coef + C + c0, B);
@@ -549,6 +571,7 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
                      float* save_mean, float* save_rstd, float* scale, float* shift, float* ws,
                      uint8_t* mbits) {
   if (C % 8 != 0 || M <= 0) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;  // 32-bit vector indexing in apply
   hipStream_t st = static_cast<hipStream_t>(stream);
   Geom g = make_geom(M, C);
   float* pmean = ws;
@@ -589,6 +612,7 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
 int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                  const float* scale, const float* shift, int relu) {
   if (C % 8 != 0 || M <= 0) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;  // 32-bit vector indexing in apply
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
@@ -610,13 +634,17 @@ int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* 
 }
 
 // mask_mode: 0 none, 1 relu (mask recomputed from x), 2 relu (bitmask written by the forward).
+// dy2 (nullable): a second upstream gradient of the output, summed with dy inside both passes —
+// the identity-shortcut gradient of a residual block, which would otherwise cost an elementwise
+// add over the whole activation (read 2, write 1) before this backward.
 // dres may be null.
 // dgamma/dbeta may be null.  ws >= det_bn_ws_elems(M, C).
-int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const void* mbits, int64_t M, int C,
+int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const void* x, const void* mbits, int64_t M, int C,
                int mask_mode, const float* gamma, const float* save_mean, const float* save_rstd,
                const float* scale, const float* shift, void* dx, void* dres, float* dgamma, float* dbeta,
                float* ws) {
   if (C % 8 != 0 || M <= 0) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;  // 32-bit vector indexing in apply
   if (mask_mode == 2 && !mbits) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   Geom g = make_geom(M, C);
@@ -626,7 +654,7 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const voi
   dim3 grid(g.nrb, (C / 8 + g.tpr - 1) / g.tpr);
 #define DET_BN_P(T, MK)                                                                                \
   hipLaunchKernelGGL((bn_bwd_partial<T, MK>), grid, dim3(kThreads), 0, st, static_cast<const T*>(dy),   \
-                     static_cast<const T*>(x), static_cast<const uint8_t*>(mbits), g, save_mean, scale, shift, psum, psumx)
+                     static_cast<const T*>(dy2), static_cast<const T*>(x), static_cast<const uint8_t*>(mbits), g, save_mean, scale, shift, psum, psumx)
   if (dtype == 1) {
     if (mask_mode == 0) DET_BN_P(unsigned short, 0);
     else if (mask_mode == 1) DET_BN_P(unsigned short, 1);
@@ -644,7 +672,8 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* x, const voi
   const int grid2 = apply_grid(nvec, 2);
 #define DET_BN_B(T, MK, DR)                                                                            \
   hipLaunchKernelGGL((bn_apply_bwd<T, MK, DR>), dim3(grid2), dim3(kThreads), 0, st,                     \
-                     static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const uint8_t*>(mbits), coef, \
+                     static_cast<const T*>(dy), static_cast<const T*>(dy2), static_cast<const T*>(x),              \
+                     static_cast<const uint8_t*>(mbits), coef,                                                \
                      scale, shift, static_cast<T*>(dx), static_cast<T*>(dres), nvec, C)
 #define DET_BN_B_MASK(T, DR)                 \
   if (mask_mode == 0) DET_BN_B(T, 0, DR);    \

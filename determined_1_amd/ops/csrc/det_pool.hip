@@ -1,0 +1,198 @@
+// det_pool.hip — 3x3 / stride-2 / pad-1 max pooling (the ResNet stem) for channels_last bf16/fp32.
+//
+// Why this exists: torch's NHWC max_pool2d stores an int64 argmax per output element (8 B next to
+// a 2-B bf16 value) and its backward zero-fills the input gradient and scatters into it: 1.7 ms per
+// ResNet-50 step at batch 512 (profiles/r1_resnet50_bs512_o2_steady.csv, 'max_pool_*_nhwc'), at
+// 1.2-2.9 TB/s.  Here:
+//   forward  one thread = 8 channels of one output pixel: 9 x 16-B loads, per-channel max and the
+//            winning window slot (0..8) as ONE byte;
+//   backward one thread = 8 channels of one INPUT pixel: it gathers the (at most 2 x 2) windows
+//            that contain it and adds dy where the window's argmax byte names it — no zero fill,
+//            no atomics, every input-gradient element written exactly once.
+// Tie-breaking matches torch (first maximum in row-major window order wins; NaN propagates).
+//
+// Reference parity: torchvision ResNet stem nn.MaxPool2d(3, 2, 1) used by the reference's
+// examples/computer_vision (SURVEY §6 north-star model).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
+}
+
+typedef unsigned char uc8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct Vec8;
+template <> struct Vec8<unsigned short> {  // 16 B as four 32-bit words (two bf16 each)
+  static __device__ __forceinline__ void load(const unsigned short* p, float (&v)[8]) {
+    const uint4 r = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(w[k] << 16);
+      v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(unsigned short* p, const float (&v)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = static_cast<uint32_t>(f2bf(v[2 * k])) | (static_cast<uint32_t>(f2bf(v[2 * k + 1])) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+struct PoolGeom {
+  int N, H, W, C, Ho, Wo;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x, T* __restrict__ y,
+                                                        uint8_t* __restrict__ idx, PoolGeom g, int64_t nvec) {
+  const int cv = g.C / 8;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    int64_t t = i;
+    const int c8 = static_cast<int>(t % cv); t /= cv;
+    const int ow = static_cast<int>(t % g.Wo); t /= g.Wo;
+    const int oh = static_cast<int>(t % g.Ho);
+    const int n = static_cast<int>(t / g.Ho);
+    // torch semantics: start from -inf with the window's first valid slot, take v if v > max
+    // or v is NaN (the first NaN then sticks)
+    const uint8_t slot0 = static_cast<uint8_t>(3 * (oh == 0 ? 1 : 0) + (ow == 0 ? 1 : 0));
+    float m[8];
+    uint8_t a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      a[j] = slot0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = 2 * oh - 1 + kh;
+      if (h < 0 || h >= g.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = 2 * ow - 1 + kw;
+        if (w < 0 || w >= g.W) continue;
+        float v[8];
+        Vec8<T>::load(x + ((static_cast<int64_t>(n) * g.H + h) * g.W + w) * g.C + 8 * c8, v);
+        const uint8_t slot = static_cast<uint8_t>(3 * kh + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (v[j] > m[j] || (__builtin_isnan(v[j]) && !__builtin_isnan(m[j]))) {
+            m[j] = v[j];
+            a[j] = slot;
+          }
+        }
+      }
+    }
+    Vec8<T>::store(y + i * 8, m);
+    uc8 av;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) av[j] = a[j];
+    *reinterpret_cast<uc8*>(idx + i * 8) = av;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
+                                                        T* __restrict__ dx, PoolGeom g, int64_t nvec) {
+  const int cv = g.C / 8;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    int64_t t = i;
+    const int c8 = static_cast<int>(t % cv); t /= cv;
+    const int w = static_cast<int>(t % g.W); t /= g.W;
+    const int h = static_cast<int>(t % g.H);
+    const int n = static_cast<int>(t / g.H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // windows oh with 2*oh-1 <= h <= 2*oh+1  ->  oh in {(h+1)/2 - 1 + d : d = 0,1} (>= 0, < Ho)
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const int oh = (h + 1) / 2 - dh;
+      const int kh = h - (2 * oh - 1);
+      if (oh < 0 || oh >= g.Ho || kh < 0 || kh > 2) continue;
+#pragma unroll
+      for (int dw = 0; dw < 2; ++dw) {
+        const int ow = (w + 1) / 2 - dw;
+        const int kw = w - (2 * ow - 1);
+        if (ow < 0 || ow >= g.Wo || kw < 0 || kw > 2) continue;
+        const int64_t o = ((static_cast<int64_t>(n) * g.Ho + oh) * g.Wo + ow) * g.C + 8 * c8;
+        const uc8 av = *reinterpret_cast<const uc8*>(idx + o);
+        const uint8_t me = static_cast<uint8_t>(3 * kh + kw);
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) any |= av[j] == me;
+        if (!any) continue;
+        float d[8];
+        Vec8<T>::load(dy + o, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += av[j] == me ? d[j] : 0.f;
+      }
+    }
+    Vec8<T>::store(dx + i * 8, acc);
+  }
+}
+
+int grid_for(int64_t work) {
+  int64_t b = (work + kThreads - 1) / kThreads;
+  if (b > 16384) b = 16384;
+  return static_cast<int>(b < 1 ? 1 : b);
+}
+
+}  // namespace
+
+extern "C" {
+
+// x [N, H, W, C] (channels_last) -> y [N, Ho, Wo, C], idx [N, Ho, Wo, C] uint8 (window slot 0..8).
+// dtype 0 = fp32, 1 = bf16; C % 8 == 0.  Ho = (H - 1) / 2 + 1 (kernel 3, stride 2, pad 1).
+int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t* idx, int N, int H, int W, int C) {
+  if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0) return -1;
+  PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
+  const int64_t nvec = static_cast<int64_t>(N) * g.Ho * g.Wo * (C / 8);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == 1)
+    hipLaunchKernelGGL(maxpool_fwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g, nvec);
+  else
+    hipLaunchKernelGGL(maxpool_fwd<float>, dim3(grid_for(nvec)), dim3(kThreads), 0, st, static_cast<const float*>(x),
+                       static_cast<float*>(y), idx, g, nvec);
+  return static_cast<int>(hipGetLastError());
+}
+
+// dy [N, Ho, Wo, C], idx from the forward -> dx [N, H, W, C] (fully overwritten).
+int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W,
+                       int C) {
+  if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0) return -1;
+  PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
+  const int64_t nvec = static_cast<int64_t>(N) * H * W * (C / 8);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == 1)
+    hipLaunchKernelGGL(maxpool_bwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(dy), idx, static_cast<unsigned short*>(dx), g, nvec);
+  else
+    hipLaunchKernelGGL(maxpool_bwd<float>, dim3(grid_for(nvec)), dim3(kThreads), 0, st, static_cast<const float*>(dy),
+                       idx, static_cast<float*>(dx), g, nvec);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

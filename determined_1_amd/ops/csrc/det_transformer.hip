@@ -19,7 +19,7 @@
 // exactly one Philox block for its 4 consecutive elements.
 //
 // Row kernels (LN): one wavefront per row, lane owns 4 consecutive elements at 4*(lane + 64*i),
-// i < K (K = ceil(H/256), templated, H <= 4096); the two-pass mean/variance is exact in
+// i < K (K = ceil(H/256), templated, H <= 2048; wider rows use a workgroup per row); the two-pass mean/variance is exact in
 // registers.  Column reductions use two levels (LDS per block, then a finalize launch) and no
 // float atomics, so every gradient is bitwise reproducible.  No host syncs anywhere.
 //
@@ -35,7 +35,8 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kFinThreads = 1024;
-constexpr int kMaxH = 4096;  // LayerNorm width limit (ALBERT-xxlarge)
+constexpr int kMaxH = 8192;        // LayerNorm width limit (workgroup-per-row kernels above 2048)
+constexpr int kMaxNarrowH = 2048;  // wave-per-row kernels up to here
 constexpr int kFinCols = 64;
 constexpr int kFinLanes = kFinThreads / kFinCols;
 
@@ -380,6 +381,216 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide rows (H > 2048: ALBERT-xxlarge's 4096): one 512-thread workgroup per row, a thread owns
+// 8 consecutive columns per 4096 (16-B vectors), block reductions through LDS.  The wave-per-row
+// kernels above would keep 64+ columns per lane at one wave per SIMD (measured 1.4 TB/s fwd,
+// profiles/r1_albert_xxlarge_bs8_o2_per_step.txt); here every lane has one 16-B load per tensor
+// in flight per row and the register footprint is small.  The backward keeps its dgamma / dbeta /
+// dbias partials in registers across a grid-stride row loop and writes one partial row per
+// workgroup for colsum_finalize.
+// ---------------------------------------------------------------------------------------------
+constexpr int kWideThreads = 512;
+constexpr int kWideWaves = kWideThreads / 64;
+
+__device__ __forceinline__ float block_sum_wide(float v, float* red) {  // red: kWideWaves floats
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < kWideWaves; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ void block_sum2_wide(float& a, float& b, float* red) {  // red: 2 x kWideWaves
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = a;
+    red[kWideWaves + (threadIdx.x >> 6)] = b;
+  }
+  __syncthreads();
+  float ta = 0.f, tb = 0.f;
+#pragma unroll
+  for (int w = 0; w < kWideWaves; ++w) {
+    ta += red[w];
+    tb += red[kWideWaves + w];
+  }
+  __syncthreads();
+  a = ta;
+  b = tb;
+}
+
+// dropout factors of the 8 columns starting at 8*c8 of `row` (two Philox groups of 4, the same
+// group indexing as the wave-per-row kernels)
+__device__ __forceinline__ void wide_drop(int64_t row, int H, int c8, const Rng& g, float (&m)[8]) {
+  float m0[4], m1[4];
+  const uint64_t grp = static_cast<uint64_t>(row) * (H >> 2) + 2 * c8;
+  drop_factors(grp, g, m0);
+  drop_factors(grp + 1, g, m1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    m[j] = m0[j];
+    m[4 + j] = m1[j];
+  }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(kWideThreads) ln_fwd_wide(LnArgs a) {
+  __shared__ float red[2 * kWideWaves];
+  const int H8 = a.H >> 3;
+  const T* h = static_cast<const T*>(a.h);
+  const T* r = static_cast<const T*>(a.r);
+  T* y = static_cast<T*>(a.y);
+  const float inv_h = 1.f / static_cast<float>(a.H);
+  for (int64_t row = blockIdx.x; row < a.rows; row += gridDim.x) {
+    const int64_t base = row * a.H;
+    float v[V][8];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const int c8 = threadIdx.x + kWideThreads * q;
+      if (c8 < H8) {
+        V8<T>::load(h + base + 8 * c8, v[q]);
+        if (a.dropout) {
+          float m[8];
+          wide_drop(row, a.H, c8, a.rng, m);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][j] *= m[j];
+        }
+        if (r) {
+          float t[8];
+          V8<T>::load(r + base + 8 * c8, t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][j] += t[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[q][j];
+      }
+    }
+    const float mean = block_sum_wide(s, red) * inv_h;
+    float s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      if (threadIdx.x + kWideThreads * q < H8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[q][j] - mean;
+          s2 += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(block_sum_wide(s2, red + kWideWaves) * inv_h + a.eps);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const int c8 = threadIdx.x + kWideThreads * q;
+      if (c8 < H8) {
+        float g[8], b[8], o[8];
+        V8<T>::load(static_cast<const T*>(a.gamma) + 8 * c8, g);
+        V8<T>::load(static_cast<const T*>(a.beta) + 8 * c8, b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[q][j] - mean) * rstd * g[j] + b[j];
+        V8<T>::store(y + base + 8 * c8, o);
+      }
+    }
+    if (threadIdx.x == 0) {
+      a.mean[row] = mean;
+      a.rstd[row] = rstd;
+    }
+  }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(kWideThreads) ln_bwd_wide(LnBwdArgs a) {
+  __shared__ float red[2 * kWideWaves];
+  const int H = a.H, H8 = H >> 3;
+  const T* dy = static_cast<const T*>(a.dy);
+  const T* h = static_cast<const T*>(a.h);
+  const T* r = static_cast<const T*>(a.r);
+  T* dr = static_cast<T*>(a.dr);
+  T* dh = static_cast<T*>(a.dh);
+  float g[V][8], adg[V][8], adb[V][8], adh[V][8];
+#pragma unroll
+  for (int q = 0; q < V; ++q) {
+    const int c8 = threadIdx.x + kWideThreads * q;
+    if (c8 < H8) V8<T>::load(static_cast<const T*>(a.gamma) + 8 * c8, g[q]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c8 >= H8) g[q][j] = 0.f;
+      adg[q][j] = adb[q][j] = adh[q][j] = 0.f;
+    }
+  }
+  const float inv_h = 1.f / static_cast<float>(H);
+  for (int64_t row = blockIdx.x; row < a.rows; row += gridDim.x) {
+    const int64_t base = row * H;
+    const float mean = a.mean[row], rstd = a.rstd[row];
+    float d[V][8], xh[V][8], m[V][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const int c8 = threadIdx.x + kWideThreads * q;
+      if (c8 < H8) {
+        float z[8];
+        V8<T>::load(dy + base + 8 * c8, d[q]);
+        V8<T>::load(h + base + 8 * c8, z);
+        if (a.dropout) {
+          wide_drop(row, H, c8, a.rng, m[q]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) z[j] *= m[q][j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) m[q][j] = 1.f;
+        }
+        if (r) {
+          float t[8];
+          V8<T>::load(r + base + 8 * c8, t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) z[j] += t[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[q][j] = (z[j] - mean) * rstd;
+          const float dx = d[q][j] * g[q][j];
+          s1 += dx;
+          s2 += dx * xh[q][j];
+        }
+      }
+    }
+    block_sum2_wide(s1, s2, red);
+    s1 *= inv_h;
+    s2 *= inv_h;
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const int c8 = threadIdx.x + kWideThreads * q;
+      if (c8 < H8) {
+        float dz[8], dhv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dz[j] = rstd * (d[q][j] * g[q][j] - s1 - xh[q][j] * s2);
+          dhv[j] = dz[j] * m[q][j];
+          adg[q][j] += d[q][j] * xh[q][j];
+          adb[q][j] += d[q][j];
+          adh[q][j] += dhv[j];
+        }
+        if (dr) V8<T>::store(dr + base + 8 * c8, dz);
+        if (dh) V8<T>::store(dh + base + 8 * c8, dhv);
+      }
+    }
+  }
+  float* out = a.ws + static_cast<int64_t>(blockIdx.x) * 3 * H;
+#pragma unroll
+  for (int q = 0; q < V; ++q) {
+    const int c8 = threadIdx.x + kWideThreads * q;
+    if (c8 < H8) {
+      V8<float>::store(out + 8 * c8, adg[q]);
+      V8<float>::store(out + H + 8 * c8, adb[q]);
+      V8<float>::store(out + 2 * H + 8 * c8, adh[q]);
+    }
+  }
+}
+
 // Sum `parts` partial rows of width W (fp32) -> up to 3 outputs of width W/3 each (or one of W).
 template <typename T>
 __global__ void __launch_bounds__(kFinThreads)
@@ -601,6 +812,19 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
   if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset)};
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (H > kMaxNarrowH) {
+    if (H % 8 != 0) return -1;
+    const dim3 wg(static_cast<unsigned>(rows < 65536 ? rows : 65536));
+    const bool v1 = H <= 8 * kWideThreads;
+    if (dtype == 1) {
+      if (v1) hipLaunchKernelGGL((ln_fwd_wide<unsigned short, 1>), wg, dim3(kWideThreads), 0, st, a);
+      else hipLaunchKernelGGL((ln_fwd_wide<unsigned short, 2>), wg, dim3(kWideThreads), 0, st, a);
+    } else {
+      if (v1) hipLaunchKernelGGL((ln_fwd_wide<float, 1>), wg, dim3(kWideThreads), 0, st, a);
+      else hipLaunchKernelGGL((ln_fwd_wide<float, 2>), wg, dim3(kWideThreads), 0, st, a);
+    }
+    return static_cast<int>(hipGetLastError());
+  }
   const int grid = grid_for(rows, kWaves);
   const int K = ln_k(H);
 #define DET_LNF(T, KK) hipLaunchKernelGGL((ln_fwd_kernel<T, KK>), dim3(grid), dim3(kThreads), 0, st, a)
@@ -611,9 +835,7 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
     case 3: DET_LNF(T, 3); break;                                                 \
     case 4: DET_LNF(T, 4); break;                                                 \
     case 5: case 6: DET_LNF(T, 6); break;                                         \
-    case 7: case 8: DET_LNF(T, 8); break;                                         \
-    case 9: case 10: case 11: case 12: DET_LNF(T, 12); break;                     \
-    default: DET_LNF(T, 16); break;                                               \
+    default: DET_LNF(T, 8); break;                                                \
   }
   if (dtype == 1) {
     DET_LNF_K(unsigned short)
@@ -631,8 +853,27 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
                   uint64_t offset, void* dr, void* dh, void* dgamma, void* dbeta, void* dbias, float* ws) {
   if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int blocks = static_cast<int>(ln_bwd_blocks(rows));
+  int blocks = static_cast<int>(ln_bwd_blocks(rows));
   LnBwdArgs a{dy, h, r, mean, rstd, gamma, dr, dh, ws, rows, H, p > 0.f, make_rng(p, seed, offset)};
+  if (H > kMaxNarrowH) {
+    if (H % 8 != 0) return -1;
+    if (blocks > 256) blocks = 256;  // <= ln_bwd_blocks(rows): fits det_tf_ln_ws_elems
+    const bool v1 = H <= 8 * kWideThreads;
+    if (dtype == 1) {
+      if (v1) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      else hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 2>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads),
+                         0, st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
+                         static_cast<unsigned short*>(dbeta), static_cast<unsigned short*>(dbias));
+    } else {
+      if (v1) hipLaunchKernelGGL((ln_bwd_wide<float, 1>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      else hipLaunchKernelGGL((ln_bwd_wide<float, 2>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      hipLaunchKernelGGL(colsum_finalize<float>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st,
+                         ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
+                         static_cast<float*>(dbias));
+    }
+    return static_cast<int>(hipGetLastError());
+  }
   const size_t lds = static_cast<size_t>(kWaves) * H * sizeof(float);
   const int K = ln_k(H);
 #define DET_LNB(T, KK) hipLaunchKernelGGL((ln_bwd_kernel<T, KK>), dim3(blocks), dim3(kThreads), lds, st, a)
@@ -643,9 +884,7 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
     case 3: DET_LNB(T, 3); break;                                                 \
     case 4: DET_LNB(T, 4); break;                                                 \
     case 5: case 6: DET_LNB(T, 6); break;                                         \
-    case 7: case 8: DET_LNB(T, 8); break;                                         \
-    case 9: case 10: case 11: case 12: DET_LNB(T, 12); break;                     \
-    default: DET_LNB(T, 16); break;                                               \
+    default: DET_LNB(T, 8); break;                                                \
   }
   if (dtype == 1) {
     DET_LNB_K(unsigned short)

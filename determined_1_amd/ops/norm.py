@@ -20,6 +20,7 @@ import torch.nn.functional as F
 from determined_1_amd.ops import _lib
 
 FALLBACKS = {"count": 0}
+SHORTCUT_LINK = True  # identity-shortcut gradients through the producer's BN backward (A/B switch)
 _SYNC_DEBUG = bool(__import__("os").environ.get("DET_SYNC_DEBUG"))
 
 
@@ -63,8 +64,14 @@ def reference_bn_act(x, residual, weight, bias, running_mean, running_var, train
 
 
 class _BNActTrain(torch.autograd.Function):
+    """``act(bn(x) + residual)``.  ``link`` (identity shortcuts): the residual is the output of
+    another ``_BNActTrain`` (the previous block's) that also feeds this block's first conv; its
+    gradient is then handed to that producer's backward as a second upstream gradient (``dy2``,
+    summed inside the BN-backward kernels) instead of returned to autograd, which would add it to
+    the conv's input gradient with a separate elementwise pass over the whole activation."""
+
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, link=None):
         M, C = _rows(x)
         lib = _lib.get_lib()
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
@@ -89,6 +96,8 @@ class _BNActTrain(torch.autograd.Function):
         mask_mode = 0 if not relu else (2 if residual is not None else 1)
         ctx.mask_mode = mask_mode
         ctx.has_res = residual is not None
+        ctx.link = link  # producer ctx of the residual (identity shortcut) or None
+        ctx.extra_dy = None  # set by the consumer of this output as identity shortcut
         ctx.fmt = fmt
         ctx.save_for_backward(x, mbits, weight, stats)
         return y
@@ -99,15 +108,17 @@ class _BNActTrain(torch.autograd.Function):
         M, C = _rows(x)
         lib = _lib.get_lib()
         dy = dy.to(x.dtype).contiguous(memory_format=ctx.fmt)
+        dy2, ctx.extra_dy = ctx.extra_dy, None
         dx = torch.empty_like(x, memory_format=ctx.fmt)
-        dres = torch.empty_like(x, memory_format=ctx.fmt) if ctx.has_res and ctx.needs_input_grad[1] else None
+        want_res = ctx.has_res and (ctx.needs_input_grad[1] or ctx.link is not None)
+        dres = torch.empty_like(x, memory_format=ctx.fmt) if want_res else None
         dgb = None
         if weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
             dgb = torch.empty((2, C), dtype=torch.float32, device=x.device)
         ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
         _lib.check(
             lib.det_bn_bwd(
-                _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), _ptr(mbits), M, C, ctx.mask_mode,
+                _stream(x), _DT[x.dtype], dy.data_ptr(), _ptr(dy2), x.data_ptr(), _ptr(mbits), M, C, ctx.mask_mode,
                 _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
                 dx.data_ptr(), _ptr(dres),
                 None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(),
@@ -118,14 +129,26 @@ class _BNActTrain(torch.autograd.Function):
         _dbg("bwd", x)
         if ctx.has_res and dres is None and ctx.needs_input_grad[1]:
             raise RuntimeError("residual grad requested but not produced")
+        if ctx.link is not None:
+            # the producer runs later (its output also feeds our block's first conv, whose input
+            # gradient it waits for); it sums dres in its own backward kernels
+            if ctx.link.extra_dy is not None:
+                raise RuntimeError("identity-shortcut gradient linked twice to one producer")
+            ctx.link.extra_dy = dres
+            ctx.link = None
+            dres = None
         dw = dgb[0] if dgb is not None and ctx.needs_input_grad[2] else None
         db = dgb[1] if dgb is not None and ctx.needs_input_grad[3] else None
-        return dx, dres, dw, db, None, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optional[torch.Tensor] = None,
-           relu: bool = True) -> torch.Tensor:
-    """``act(bn(x) + residual)`` with the module's parameters/buffers and train/eval semantics."""
+           relu: bool = True, shortcut_link: bool = False) -> torch.Tensor:
+    """``act(bn(x) + residual)`` with the module's parameters/buffers and train/eval semantics.
+
+    ``shortcut_link``: the caller guarantees ``residual`` is an identity shortcut, i.e. also the
+    input of a differentiable op upstream of ``x`` (the block's first conv).  When ``residual`` was
+    produced by this fused op, its gradient then travels to the producer's backward directly."""
     use_batch_stats = bn.training or not bn.track_running_stats
     rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
     rv = bn.running_var if (bn.track_running_stats and bn.training) else None
@@ -133,7 +156,14 @@ def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optio
     if _nhwc_ok(x) and res_ok:
         if use_batch_stats:
             nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
-            return _BNActTrain.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, bn.momentum, bn.eps, relu)
+            link = None
+            if (shortcut_link and SHORTCUT_LINK and residual is not None and torch.is_grad_enabled() and residual.requires_grad
+                    and isinstance(residual.grad_fn, _BNActTrain._backward_cls) and residual.dtype == x.dtype
+                    and residual.is_contiguous(memory_format=torch.channels_last if x.dim() == 4
+                                               else torch.contiguous_format)):
+                link = residual.grad_fn
+                residual = residual.detach()
+            return _BNActTrain.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, bn.momentum, bn.eps, relu, link)
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or (residual is not None and residual.requires_grad)
             or (bn.weight is not None and bn.weight.requires_grad))
@@ -179,9 +209,10 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.relu = relu
         self.fused = fused  # False: stock torch/MIOpen BN + separate add/ReLU (A/B comparisons)
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:  # type: ignore[override]
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,  # type: ignore[override]
+                shortcut_link: bool = False) -> torch.Tensor:
         if self.fused:
-            return bn_act(x, self, residual, self.relu)
+            return bn_act(x, self, residual, self.relu, shortcut_link)
         y = super().forward(x)
         if residual is not None:
             y = y + residual

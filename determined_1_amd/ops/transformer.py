@@ -10,7 +10,7 @@ pass per direction, and every Linear's bias gradient is produced inside the kern
 reads the gradient (LayerNorm bwd, GELU bwd) instead of a separate reduction.  Dropout masks are
 regenerated from a Philox (seed, offset) pair in the backward pass rather than stored.
 
-CPU tensors, and GPU layouts the kernels do not cover (fp16, hidden > 4096, hidden % 8 != 0),
+CPU tensors, and GPU layouts the kernels do not cover (fp16, hidden > 8192, hidden % 8 != 0),
 run the plain PyTorch composite, which is also the numerics reference of the GPU tests; GPU
 fallbacks are counted in ``FALLBACKS`` so benchmarks can assert the native path ran.
 """
@@ -25,7 +25,7 @@ from determined_1_amd.ops import _lib
 
 FALLBACKS = {"count": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
-_MAX_H = 4096  # det_tf_ln_max_hidden(): ALBERT-xxlarge width
+_MAX_H = 8192  # det_tf_ln_max_hidden() (workgroup-per-row kernels above 2048, e.g. ALBERT-xxlarge)
 ctypes_i64 = ctypes.c_int64
 _offsets = itertools.count(1)
 _seed = []  # lazily cached: the trial seeds torch before the first dropout call

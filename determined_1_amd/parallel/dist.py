@@ -115,6 +115,16 @@ class RankInfo:
 _control_group = None  # gloo group for CPU-side control collectives
 
 
+def local_cuda_device(local_rank: int) -> torch.device:
+    """GPU of this rank: ``cuda:<local_rank>`` (one process per GPU).  Rehearsal mode
+    ``DET_DIST_SHARE_GPU=1`` folds ranks onto the visible GPUs (``local_rank % count``) so a
+    multi-rank data-parallel run (with ``DET_DIST_BACKEND=gloo``) can exercise the GPU-side
+    gradient path on a one-GPU box; RCCL itself refuses two ranks on one device."""
+    if os.environ.get("DET_DIST_SHARE_GPU", "0") == "1":
+        return torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    return torch.device("cuda", local_rank)
+
+
 def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
@@ -128,6 +138,7 @@ def init_process_groups(device: torch.device, timeout_s: int = constants.DIST_ST
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     backend = "nccl" if device.type == "cuda" else "gloo"
+    backend = os.environ.get("DET_DIST_BACKEND", backend)  # gloo: GPU-sharing rehearsals (see above)
     kwargs = {}
     if backend == "nccl":
         kwargs["device_id"] = device  # eager RCCL communicator init, bound to this GPU

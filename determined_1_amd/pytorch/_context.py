@@ -93,7 +93,9 @@ class PyTorchTrialContext(trial.TrialContext):
     def _init_device(self) -> None:
         self.n_gpus = len(self.env.container_gpus)
         if self.dist_config.use and torch.cuda.is_available():
-            self.device = torch.device("cuda", self.distributed.get_local_rank())
+            from determined_1_amd.parallel import dist as pdist
+
+            self.device = pdist.local_cuda_device(self.distributed.get_local_rank())
             torch.cuda.set_device(self.device)
         elif self.n_gpus > 0 and torch.cuda.is_available():
             self.device = torch.device("cuda", 0)
@@ -162,13 +164,19 @@ class PyTorchTrialContext(trial.TrialContext):
         if self.dist_config.use:
             check.eq(num_losses, 1, "When using parallel/distributed training, Determined only supports "
                                     "configure_apex_amp with num_losses = 1")
-            check.eq(self.dist_config.aggregation_frequency, 1,
-                     "Mixed precision training (AMP) is not supported with aggregation frequency > 1.")
         if not enabled or opt_level == "O0":
             return models, optimizers
         self._use_amp = True
         self._amp = _amp.make_amp_config(self.device, opt_level or "O1", cast_model_type, keep_batchnorm_fp32,
                                          loss_scale, min_loss_scale, max_loss_scale)
+        if self.dist_config.use and self._amp.scaler is not None:
+            # The reference forbids AMP with aggregation > 1 under Horovod because apex's dynamic
+            # loss scale can change between the aggregated backward passes
+            # (harness/determined/pytorch/_pytorch_context.py:347-351).  bf16 (the MI355X default)
+            # needs no loss scaler, so the restriction applies only to fp16 / explicit loss scales.
+            check.eq(self.dist_config.aggregation_frequency, 1,
+                     "Mixed precision training (AMP) with a loss scaler is not supported with aggregation "
+                     "frequency > 1.")
         logging.info(f"Enabling mixed precision training with opt_level: {opt_level} ({self._amp.dtype}).")
         model_list = models if isinstance(models, list) else [models]
         if self._amp.casts_model:

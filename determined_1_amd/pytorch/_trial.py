@@ -70,8 +70,8 @@ class PyTorchTrialController(trial.LoopTrialController):
     @staticmethod
     def pre_execute_hook(env: Any, dist_config: Any) -> None:
         if dist_config.use:
-            device = torch.device("cuda", int(pdist.RankInfo.from_env().local_rank)) if torch.cuda.is_available() \
-                else torch.device("cpu")
+            device = pdist.local_cuda_device(int(pdist.RankInfo.from_env().local_rank)) \
+                if torch.cuda.is_available() else torch.device("cpu")
             if device.type == "cuda":
                 torch.cuda.set_device(device)
             pdist.init_process_groups(device)

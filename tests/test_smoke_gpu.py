@@ -7,3 +7,28 @@ def test_graft_smoke(gpu):
     import __graft_entry__ as g
 
     g.smoke()
+
+
+def test_bench_two_ranks_sharing_the_gpu(gpu, tmp_path):
+    """bench.py under torch.distributed.run with 2 ranks folded onto this GPU (DET_DIST_SHARE_GPU=1)
+    over gloo: the data-parallel GPU path of the driver's scaling run (GradSink landing, bucketed
+    async all-reduce launched from backward hooks on CUDA tensors, fused SGD, metric gather).  RCCL
+    itself refuses two ranks on one device, so the collective backend is the only difference."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from determined_1_amd.deploy.local import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DET_DIST_SHARE_GPU="1", DET_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(repo, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch-per-gpu", "16", "--image-size", "64",
+                        "--bucket-mb", "8", "--cudnn-benchmark", "0"],
+                       capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
+    assert out["config"]["final_avg_loss"] is not None

@@ -25,8 +25,10 @@ def _leaf(t, dev=None, dt=None):
     (1000, 3072, 768, torch.bfloat16, 0.1),
     (300, 256, 1024, torch.float32, 0.1),
     (77, 64, 200, torch.float32, 0.25),  # H not a multiple of 256 (inactive lanes)
-    (768, 512, 4096, torch.bfloat16, 0.0),  # ALBERT-xxlarge width (K = 16 register groups, re-read bwd)
-    (200, 256, 3072, torch.float32, 0.1),   # K = 12
+    (768, 512, 4096, torch.bfloat16, 0.0),  # ALBERT-xxlarge width: workgroup-per-row kernels
+    (700, 256, 4096, torch.bfloat16, 0.1),  # ... with dropout, rows not a multiple of the bwd grid
+    (200, 256, 3072, torch.float32, 0.1),   # wide, inactive threads
+    (64, 128, 6144, torch.float32, 0.0),    # two 16-B vectors per thread
 ])
 def test_linear_dropout_add_layernorm(gpu, monkeypatch, rows, K, H, dt, p):
     torch.manual_seed(0)
