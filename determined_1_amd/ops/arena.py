@@ -24,6 +24,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 
 ALIGN_ELEMS = 64  # 256 B for fp32: every param view starts on a full HBM burst
+DIRECT_LANDING = True  # landing_buffer(): producers may write gradients straight into the arena
 
 
 def _round_up(x: int, a: int) -> int:
@@ -126,6 +127,22 @@ class Arena:
         return slice(lo, hi)
 
 
+def landing_buffer(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """Where a backward kernel may write ``p``'s gradient directly: a fresh tensor aliasing the
+    parameter's arena slot while its GradSink window is fresh and the gradient has not landed yet
+    (else None).  The producer writes the GEMM output there (``torch.mm(..., out=buf)``) and returns
+    it; AccumulateGrad adopts it and the sink hook sees the alias and skips the landing copy
+    (``det_mt_copy`` of that parameter).  If autograd clones instead, the normal copy path runs."""
+    slot = getattr(p, "_det_grad_slot", None)
+    if slot is None or not DIRECT_LANDING:
+        return None
+    sink, gi, a, i = slot
+    if not sink.fresh or i in sink._seen[gi] or p.grad is not None or (gi, i) in sink._landing_taken:
+        return None  # a second producer of the same window gets its own buffer; autograd sums them
+    sink._landing_taken.add((gi, i))
+    return a.view(a.flat_grad, i)
+
+
 def build_arenas(params: Sequence[torch.nn.Parameter], device: torch.device) -> List[Arena]:
     """Group ``params`` (one optimizer param group) by dtype and build one arena per dtype.
 
@@ -181,11 +198,13 @@ class GradSink:
         self._seen = [set() for _ in self.groups]  # type: List[set]
         self._stolen = [[] for _ in self.groups]  # type: List[List[Tuple[int, torch.Tensor]]]
         self._keep = []  # type: List[torch.Tensor]
+        self._landing_taken = set()  # type: set  # (group, index) slots handed out by landing_buffer
         self._tables = {}  # type: Dict[int, Any]
         self._handles = []
-        for a, idx in self.groups:
+        for gi, (a, idx) in enumerate(self.groups):
             for i in idx:
                 self._handles.append(a.params[i].register_post_accumulate_grad_hook(self._hook))
+                a.params[i]._det_grad_slot = (self, gi, a, i)  # see landing_buffer()
 
     @staticmethod
     def for_arenas(arenas: Sequence["Arena"]) -> "GradSink":
@@ -206,6 +225,7 @@ class GradSink:
             for i in idx:
                 a.params[i].grad = None
         self._keep = []
+        self._landing_taken = set()
 
     def _hook(self, p: torch.Tensor) -> None:
         if not self.fresh:
@@ -220,7 +240,10 @@ class GradSink:
         self._seen[gi].add(i)
         g = p.grad
         view = a.grad_views[i]
-        if g is not None and g is not view:
+        if g is not None and g is not view and g.data_ptr() == view.data_ptr() and g.shape == view.shape \
+                and g.stride() == view.stride() and g.dtype == view.dtype:
+            p.grad = view  # produced in place by its backward (landing_buffer): nothing to move
+        elif g is not None and g is not view:
             # same shape + the arena view's (dense) strides => g is dense with the same element order
             if g.dtype == view.dtype and g.shape == view.shape and g.stride() == view.stride() \
                     and g.device == view.device:

@@ -227,10 +227,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnArgs a) {
         ls += p;
       }
     l = fmaf(l, alpha, ls);
+    if (__any(alpha != 1.f)) {  // no lane's running max moved: the rescale is an exact no-op
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[u][i] *= alpha;
+        for (int i = 0; i < 16; ++i) o[u][i] *= alpha;
+    }
     if (a.drop_thr) {  // keys 4g..4g+3 of each 32-key tile = 2 hashes (same draws as the backward)
 #pragma unroll
       for (int t = 0; t < 2; ++t)

@@ -18,9 +18,10 @@
 // and indexed by element/4 regenerates the identical mask in the backward pass, so a lane draws
 // exactly one Philox block for its 4 consecutive elements.
 //
-// Row kernels (LN): one wavefront per row, lane owns 4 consecutive elements at 4*(lane + 64*i),
-// i < K (K = ceil(H/256), templated, H <= 2048; wider rows use a workgroup per row); the two-pass mean/variance is exact in
-// registers.  Column reductions use two levels (LDS per block, then a finalize launch) and no
+// Row kernels (LN): forward = one workgroup per row (128/256/512 threads x 8 columns, block
+// reductions); backward = one wavefront per row up to H = 2048 (lane owns 4 consecutive elements at
+// 4*(lane + 64*i), i < K = ceil(H/256)), a workgroup per row above.  The two-pass mean/variance
+// is exact in registers.  Column reductions use two levels (LDS per block, then a finalize launch) and no
 // float atomics, so every gradient is bitwise reproducible.  No host syncs anywhere.
 //
 // Reference parity: the reference runs BERT through HuggingFace modules on torch/cuDNN
@@ -41,11 +42,9 @@ constexpr int kFinCols = 64;
 constexpr int kFinLanes = kFinThreads / kFinCols;
 
 __device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+// RNE; adjacent conversions pair into gfx950's v_cvt_pk_bf16_f32
 __device__ __forceinline__ unsigned short f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<unsigned short>((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<unsigned short>(u >> 16);
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
 }
 
 typedef unsigned short us4 __attribute__((ext_vector_type(4)));
@@ -390,33 +389,35 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
 // dbias partials in registers across a grid-stride row loop and writes one partial row per
 // workgroup for colsum_finalize.
 // ---------------------------------------------------------------------------------------------
-constexpr int kWideThreads = 512;
-constexpr int kWideWaves = kWideThreads / 64;
+constexpr int kWideThreads = 512;     // workgroup of the widest rows (H > 2048)
+constexpr int kWideMaxWaves = kWideThreads / 64;
 
-__device__ __forceinline__ float block_sum_wide(float v, float* red) {  // red: kWideWaves floats
+template <int NT>
+__device__ __forceinline__ float block_sum_wide(float v, float* red) {  // red: NT/64 floats
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   float t = 0.f;
 #pragma unroll
-  for (int w = 0; w < kWideWaves; ++w) t += red[w];
+  for (int w = 0; w < NT / 64; ++w) t += red[w];
   __syncthreads();
   return t;
 }
 
-__device__ __forceinline__ void block_sum2_wide(float& a, float& b, float* red) {  // red: 2 x kWideWaves
+template <int NT>
+__device__ __forceinline__ void block_sum2_wide(float& a, float& b, float* red) {  // red: 2 x NT/64
   a = wave_sum(a);
   b = wave_sum(b);
   if ((threadIdx.x & 63) == 0) {
     red[threadIdx.x >> 6] = a;
-    red[kWideWaves + (threadIdx.x >> 6)] = b;
+    red[NT / 64 + (threadIdx.x >> 6)] = b;
   }
   __syncthreads();
   float ta = 0.f, tb = 0.f;
 #pragma unroll
-  for (int w = 0; w < kWideWaves; ++w) {
+  for (int w = 0; w < NT / 64; ++w) {
     ta += red[w];
-    tb += red[kWideWaves + w];
+    tb += red[NT / 64 + w];
   }
   __syncthreads();
   a = ta;
@@ -437,9 +438,9 @@ __device__ __forceinline__ void wide_drop(int64_t row, int H, int c8, const Rng&
   }
 }
 
-template <typename T, int V>
-__global__ void __launch_bounds__(kWideThreads) ln_fwd_wide(LnArgs a) {
-  __shared__ float red[2 * kWideWaves];
+template <typename T, int V, int NT>
+__global__ void __launch_bounds__(NT) ln_fwd_wide(LnArgs a) {
+  __shared__ float red[2 * kWideMaxWaves];
   const int H8 = a.H >> 3;
   const T* h = static_cast<const T*>(a.h);
   const T* r = static_cast<const T*>(a.r);
@@ -451,7 +452,7 @@ __global__ void __launch_bounds__(kWideThreads) ln_fwd_wide(LnArgs a) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-      const int c8 = threadIdx.x + kWideThreads * q;
+      const int c8 = threadIdx.x + NT * q;
       if (c8 < H8) {
         V8<T>::load(h + base + 8 * c8, v[q]);
         if (a.dropout) {
@@ -470,11 +471,11 @@ __global__ void __launch_bounds__(kWideThreads) ln_fwd_wide(LnArgs a) {
         for (int j = 0; j < 8; ++j) s += v[q][j];
       }
     }
-    const float mean = block_sum_wide(s, red) * inv_h;
+    const float mean = block_sum_wide<NT>(s, red) * inv_h;
     float s2 = 0.f;
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-      if (threadIdx.x + kWideThreads * q < H8) {
+      if (threadIdx.x + NT * q < H8) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float d = v[q][j] - mean;
@@ -482,10 +483,10 @@ __global__ void __launch_bounds__(kWideThreads) ln_fwd_wide(LnArgs a) {
         }
       }
     }
-    const float rstd = rsqrtf(block_sum_wide(s2, red + kWideWaves) * inv_h + a.eps);
+    const float rstd = rsqrtf(block_sum_wide<NT>(s2, red + NT / 64) * inv_h + a.eps);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-      const int c8 = threadIdx.x + kWideThreads * q;
+      const int c8 = threadIdx.x + NT * q;
       if (c8 < H8) {
         float g[8], b[8], o[8];
         V8<T>::load(static_cast<const T*>(a.gamma) + 8 * c8, g);
@@ -502,9 +503,9 @@ __global__ void __launch_bounds__(kWideThreads) ln_fwd_wide(LnArgs a) {
   }
 }
 
-template <typename T, int V>
-__global__ void __launch_bounds__(kWideThreads) ln_bwd_wide(LnBwdArgs a) {
-  __shared__ float red[2 * kWideWaves];
+template <typename T, int V, int NT>
+__global__ void __launch_bounds__(NT) ln_bwd_wide(LnBwdArgs a) {
+  __shared__ float red[2 * kWideMaxWaves];
   const int H = a.H, H8 = H >> 3;
   const T* dy = static_cast<const T*>(a.dy);
   const T* h = static_cast<const T*>(a.h);
@@ -514,7 +515,7 @@ __global__ void __launch_bounds__(kWideThreads) ln_bwd_wide(LnBwdArgs a) {
   float g[V][8], adg[V][8], adb[V][8], adh[V][8];
 #pragma unroll
   for (int q = 0; q < V; ++q) {
-    const int c8 = threadIdx.x + kWideThreads * q;
+    const int c8 = threadIdx.x + NT * q;
     if (c8 < H8) V8<T>::load(static_cast<const T*>(a.gamma) + 8 * c8, g[q]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -530,7 +531,7 @@ __global__ void __launch_bounds__(kWideThreads) ln_bwd_wide(LnBwdArgs a) {
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-      const int c8 = threadIdx.x + kWideThreads * q;
+      const int c8 = threadIdx.x + NT * q;
       if (c8 < H8) {
         float z[8];
         V8<T>::load(dy + base + 8 * c8, d[q]);
@@ -558,12 +559,12 @@ __global__ void __launch_bounds__(kWideThreads) ln_bwd_wide(LnBwdArgs a) {
         }
       }
     }
-    block_sum2_wide(s1, s2, red);
+    block_sum2_wide<NT>(s1, s2, red);
     s1 *= inv_h;
     s2 *= inv_h;
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-      const int c8 = threadIdx.x + kWideThreads * q;
+      const int c8 = threadIdx.x + NT * q;
       if (c8 < H8) {
         float dz[8], dhv[8];
 #pragma unroll
@@ -582,7 +583,7 @@ __global__ void __launch_bounds__(kWideThreads) ln_bwd_wide(LnBwdArgs a) {
   float* out = a.ws + static_cast<int64_t>(blockIdx.x) * 3 * H;
 #pragma unroll
   for (int q = 0; q < V; ++q) {
-    const int c8 = threadIdx.x + kWideThreads * q;
+    const int c8 = threadIdx.x + NT * q;
     if (c8 < H8) {
       V8<float>::store(out + 8 * c8, adg[q]);
       V8<float>::store(out + H + 8 * c8, adb[q]);
@@ -812,19 +813,24 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
   if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset)};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (H > kMaxNarrowH) {
-    if (H % 8 != 0) return -1;
+  if (H % 8 == 0) {  // workgroup per row (128 / 256 / 512 threads of 8 columns each)
     const dim3 wg(static_cast<unsigned>(rows < 65536 ? rows : 65536));
-    const bool v1 = H <= 8 * kWideThreads;
+#define DET_LNFW(T, VV, NT) hipLaunchKernelGGL((ln_fwd_wide<T, VV, NT>), wg, dim3(NT), 0, st, a)
+#define DET_LNFW_T(T)                                   \
+    if (H <= 8 * 128) DET_LNFW(T, 1, 128);              \
+    else if (H <= 8 * 256) DET_LNFW(T, 1, 256);         \
+    else if (H <= 8 * kWideThreads) DET_LNFW(T, 1, 512); \
+    else DET_LNFW(T, 2, 512);
     if (dtype == 1) {
-      if (v1) hipLaunchKernelGGL((ln_fwd_wide<unsigned short, 1>), wg, dim3(kWideThreads), 0, st, a);
-      else hipLaunchKernelGGL((ln_fwd_wide<unsigned short, 2>), wg, dim3(kWideThreads), 0, st, a);
+      DET_LNFW_T(unsigned short)
     } else {
-      if (v1) hipLaunchKernelGGL((ln_fwd_wide<float, 1>), wg, dim3(kWideThreads), 0, st, a);
-      else hipLaunchKernelGGL((ln_fwd_wide<float, 2>), wg, dim3(kWideThreads), 0, st, a);
+      DET_LNFW_T(float)
     }
+#undef DET_LNFW_T
+#undef DET_LNFW
     return static_cast<int>(hipGetLastError());
   }
+  if (H > kMaxNarrowH) return -1;
   const int grid = grid_for(rows, kWaves);
   const int K = ln_k(H);
 #define DET_LNF(T, KK) hipLaunchKernelGGL((ln_fwd_kernel<T, KK>), dim3(grid), dim3(kThreads), 0, st, a)
@@ -860,14 +866,14 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
     if (blocks > 256) blocks = 256;  // <= ln_bwd_blocks(rows): fits det_tf_ln_ws_elems
     const bool v1 = H <= 8 * kWideThreads;
     if (dtype == 1) {
-      if (v1) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1>), dim3(blocks), dim3(kWideThreads), 0, st, a);
-      else hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 2>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      if (v1) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      else hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 2, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads),
                          0, st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
                          static_cast<unsigned short*>(dbeta), static_cast<unsigned short*>(dbias));
     } else {
-      if (v1) hipLaunchKernelGGL((ln_bwd_wide<float, 1>), dim3(blocks), dim3(kWideThreads), 0, st, a);
-      else hipLaunchKernelGGL((ln_bwd_wide<float, 2>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      if (v1) hipLaunchKernelGGL((ln_bwd_wide<float, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      else hipLaunchKernelGGL((ln_bwd_wide<float, 2, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       hipLaunchKernelGGL(colsum_finalize<float>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st,
                          ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
                          static_cast<float*>(dbias));

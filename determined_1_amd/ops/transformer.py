@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from determined_1_amd.ops import _lib
+from determined_1_amd.ops.arena import landing_buffer
 
 FALLBACKS = {"count": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
@@ -89,7 +90,7 @@ class SharedWeightGrads:
     def accumulate(self, weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> Optional[torch.Tensor]:
         st = self._state[id(weight)]
         if st[1] is None:
-            st[1] = dz.t() @ x2
+            st[1] = _weight_grad(weight, dz, x2)
         else:
             st[1].addmm_(dz.t(), x2)
         st[0] -= 1
@@ -99,12 +100,21 @@ class SharedWeightGrads:
         return out
 
 
+def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """dW = dz^T x, written straight into the parameter's gradient-arena slot when that is where
+    it will land (ops.arena.landing_buffer): no separate landing copy for the largest gradients."""
+    buf = landing_buffer(weight) if weight.is_cuda else None
+    if buf is not None and buf.dtype == dz.dtype and buf.is_contiguous():
+        return torch.mm(dz.t(), x2, out=buf)
+    return dz.t() @ x2
+
+
 def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool,
                  acc: Optional[SharedWeightGrads] = None):
     dx = dz @ weight if need_x else None
     dw = None
     if need_w:
-        dw = acc.accumulate(weight, dz, x2) if acc is not None else dz.t() @ x2
+        dw = acc.accumulate(weight, dz, x2) if acc is not None else _weight_grad(weight, dz, x2)
     return dx, dw
 
 

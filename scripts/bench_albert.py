@@ -39,8 +39,10 @@ def main() -> None:
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    from determined_1_amd.parallel import dist as pdist
+
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(pdist.local_cuda_device(int(os.environ.get("LOCAL_RANK", "0"))))
     from determined_1_amd import workload
     from determined_1_amd.experimental import make_controller
     from determined_1_amd.models.albert import AlbertSQuADTrial

@@ -34,8 +34,10 @@ def main() -> None:
         logging.basicConfig(level=logging.INFO, format="%(message)s")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    from determined_1_amd.parallel import dist as pdist
+
     if torch.cuda.is_available():
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(pdist.local_cuda_device(int(os.environ.get("LOCAL_RANK", "0"))))
     from determined_1_amd import workload
     from determined_1_amd.experimental import make_controller
     from determined_1_amd.models.bert import BertSQuADTrial

@@ -32,3 +32,24 @@ def test_bench_two_ranks_sharing_the_gpu(gpu, tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
     assert out["config"]["final_avg_loss"] is not None
+
+
+def test_bert_two_ranks_sharing_the_gpu_with_aggregation(gpu):
+    """scripts/bench_bert.py with 2 ranks on this GPU over gloo and aggregation_frequency 2 under
+    bf16 O2: DP bucketing + gradient landing straight into the arena + skipped-sync windows."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from determined_1_amd.deploy.local import free_port
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DET_DIST_SHARE_GPU="1", DET_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(repo, "scripts", "bench_bert.py"), "--steps", "4", "--warmup", "2", "--agg", "2"],
+                       capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["config"]["tf_fallbacks"] == 0

@@ -232,3 +232,41 @@ def test_mfma_attention_with_dropout(gpu, monkeypatch, B, S, nh, p):
     g, gr = dut_in.grad.float().cpu(), ref_in.grad
     scale = gr.abs().max().item()
     torch.testing.assert_close(g / scale, gr / scale, atol=2e-2, rtol=2e-2)
+
+
+def test_bert_trial_direct_gradient_landing(gpu, monkeypatch):
+    """BERT trial on the GPU through the real controller (arenas, GradSink, fused AdamW): dW GEMMs
+    writing straight into the gradient arena (ops.arena.landing_buffer) give the same parameters
+    after 3 steps as the copy-landing path, and the landing copy really is skipped for them."""
+    import copy as _copy
+
+    from determined_1_amd.models.bert import BertSQuADTrial
+    from determined_1_amd.ops import arena
+    from tests.utils import Recorder, run
+
+    hp = {"global_batch_size": 4, "num_hidden_layers": 2, "hidden_size": 128, "num_attention_heads": 2,
+          "intermediate_size": 512, "max_seq_length": 128, "amp": "O2", "train_records": 64, "validation_records": 8,
+          "learning_rate": 1e-3}
+    out = {}
+    import itertools
+
+    for direct in (False, True):
+        monkeypatch.setattr(arena, "DIRECT_LANDING", direct)
+        monkeypatch.setattr(tfops, "_offsets", itertools.count(1))  # same dropout masks in both runs
+        tfops._seed.clear()
+        landed = []
+        orig = arena.landing_buffer
+
+        def spy(p, _orig=orig, _landed=landed):
+            b = _orig(p)
+            if b is not None:
+                _landed.append(b.data_ptr())
+            return b
+
+        monkeypatch.setattr(arena, "landing_buffer", spy)
+        monkeypatch.setattr(tfops, "landing_buffer", spy)
+        ctrl, _ = run(BertSQuADTrial, _copy.deepcopy(hp), Recorder().train(1, 3, 0), trial_seed=3, use_gpu=True)
+        out[direct] = (torch.cat([p.detach().float().reshape(-1) for p in ctrl.context.models[0].parameters()]).cpu(),
+                       len(landed))
+    assert out[False][1] == 0 and out[True][1] > 0
+    torch.testing.assert_close(out[True][0], out[False][0], atol=1e-6, rtol=1e-5)
