@@ -258,11 +258,8 @@ struct LnBwdArgs {
 
 template <typename T, int K>
 __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
-  // K <= 8 keeps dy, xhat and the dropout factors of the row in registers between the two
-  // passes; wider rows (ALBERT-xxlarge, H = 4096) re-read them from L1/L2 in the second pass
-  // (the row is 8 KB per tensor and was touched a few hundred cycles earlier) instead of spilling.
-  constexpr bool kKeep = K <= 8;
-  constexpr int KR = kKeep ? K : 1;
+  // H <= 2048 (K <= 8): dy, xhat and the dropout factors of the row stay in registers between the
+  // two passes; wider rows use ln_bwd_wide.
   extern __shared__ float red[];  // [kWaves][H]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int H4 = a.H >> 2;
@@ -283,48 +280,43 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
     }
   }
   const float inv_h = 1.f / static_cast<float>(a.H);
-  // z = dropout(h) + r for column group c4 of `row`; m = dropout factors
-  auto load_z = [&](int64_t row, int64_t base, int c4, float (&z)[4], float (&m)[4]) {
-    V4<T>::load(h + base + 4 * c4, z);
-    if (a.dropout) {
-      drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) z[j] *= m[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) m[j] = 1.f;
-    }
-    if (r) {
-      float t[4];
-      V4<T>::load(r + base + 4 * c4, t);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) z[j] += t[j];
-    }
-  };
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wave; row < a.rows;
        row += static_cast<int64_t>(gridDim.x) * kWaves) {
     const int64_t base = row * a.H;
     const float mean = a.mean[row], rstd = a.rstd[row];
-    float d[KR][4], xh[KR][4], m[KR][4];
+    float d[K][4], xh[K][4], m[K][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const int c4 = lane + 64 * i;
-      const int ir = kKeep ? i : 0;
       if (c4 < H4) {
-        float z[4];
-        V4<T>::load(dy + base + 4 * c4, d[ir]);
-        load_z(row, base, c4, z, m[ir]);
+        float z[4];  // z = dropout(h) + r
+        V4<T>::load(dy + base + 4 * c4, d[i]);
+        V4<T>::load(h + base + 4 * c4, z);
+        if (a.dropout) {
+          drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m[i]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) z[j] *= m[i][j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) m[i][j] = 1.f;
+        }
+        if (r) {
+          float t[4];
+          V4<T>::load(r + base + 4 * c4, t);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) z[j] += t[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          xh[ir][j] = (z[j] - mean) * rstd;
-          const float dx = d[ir][j] * g[i][j];
+          xh[i][j] = (z[j] - mean) * rstd;
+          const float dx = d[i][j] * g[i][j];
           s1 += dx;
-          s2 += dx * xh[ir][j];
+          s2 += dx * xh[i][j];
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d[ir][j] = xh[ir][j] = m[ir][j] = 0.f;
+        for (int j = 0; j < 4; ++j) d[i][j] = xh[i][j] = m[i][j] = 0.f;
       }
     }
     s1 = wave_sum(s1) * inv_h;
@@ -332,22 +324,14 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
 #pragma unroll
     for (int i = 0; i < K; ++i) {
       const int c4 = lane + 64 * i;
-      const int ir = kKeep ? i : 0;
       if (c4 < H4) {
-        if (!kKeep) {
-          float z[4];
-          V4<T>::load(dy + base + 4 * c4, d[ir]);
-          load_z(row, base, c4, z, m[ir]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) xh[ir][j] = (z[j] - mean) * rstd;
-        }
         float dz[4], dhv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          dz[j] = rstd * (d[ir][j] * g[i][j] - s1 - xh[ir][j] * s2);
-          dhv[j] = dz[j] * m[ir][j];
-          adg[i][j] += d[ir][j] * xh[ir][j];
-          adb[i][j] += d[ir][j];
+          dz[j] = rstd * (d[i][j] * g[i][j] - s1 - xh[i][j] * s2);
+          dhv[j] = dz[j] * m[i][j];
+          adg[i][j] += d[i][j] * xh[i][j];
+          adb[i][j] += d[i][j];
           adh[i][j] += dhv[j];
         }
         if (dr) V4<T>::store(dr + base + 4 * c4, dz);
