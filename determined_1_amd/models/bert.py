@@ -52,7 +52,8 @@ class BertEncoderConfig:
     def from_hparams(cls, hp: Dict[str, Any]) -> "BertEncoderConfig":
         return cls(hidden_size=int(hp.get("hidden_size", 768)), num_hidden_layers=int(hp.get("num_hidden_layers", 12)),
                    num_attention_heads=int(hp.get("num_attention_heads", 12)),
-                   intermediate_size=int(hp.get("intermediate_size", 3072)))
+                   intermediate_size=int(hp.get("intermediate_size", 3072)),
+                   vocab_size=int(hp.get("vocab_size", 30522)))
 
 
 class _LN(nn.Module):
@@ -166,18 +167,15 @@ class BertForQA(nn.Module):
         return SimpleNamespace(loss=loss, start_logits=start_logits, end_logits=end_logits)
 
 
-def load_hf_state_dict(model: BertForQA, sd: Dict[str, torch.Tensor]) -> None:
-    """Load a ``transformers`` BertForQuestionAnswering state dict into the fused layout."""
+def hf_encoder_state(sd: Dict[str, torch.Tensor], num_layers: int) -> Dict[str, torch.Tensor]:
+    """Embeddings + encoder layers of a ``transformers`` BERT state dict in the fused layout."""
     out = {}
     for k, v in sd.items():
         if k.startswith("bert.embeddings."):
             if "position_ids" in k or "token_type_ids" in k:
                 continue
             out[k[len("bert."):]] = v
-        elif k.startswith("qa_outputs."):
-            out[k] = v
-    n = model.config.num_hidden_layers
-    for i in range(n):
+    for i in range(num_layers):
         pre = f"bert.encoder.layer.{i}."
         for t in ("weight", "bias"):
             out[f"layers.{i}.qkv.{t}"] = torch.cat([sd[pre + f"attention.self.{m}.{t}"] for m in ("query", "key", "value")])
@@ -186,6 +184,13 @@ def load_hf_state_dict(model: BertForQA, sd: Dict[str, torch.Tensor]) -> None:
             out[f"layers.{i}.ffn_in.{t}"] = sd[pre + f"intermediate.dense.{t}"]
             out[f"layers.{i}.ffn_out.{t}"] = sd[pre + f"output.dense.{t}"]
             out[f"layers.{i}.ffn_ln.{t}"] = sd[pre + f"output.LayerNorm.{t}"]
+    return out
+
+
+def load_hf_state_dict(model: BertForQA, sd: Dict[str, torch.Tensor]) -> None:
+    """Load a ``transformers`` BertForQuestionAnswering state dict into the fused layout."""
+    out = hf_encoder_state(sd, model.config.num_hidden_layers)
+    out.update({k: v for k, v in sd.items() if k.startswith("qa_outputs.")})
     model.load_state_dict(out)
 
 

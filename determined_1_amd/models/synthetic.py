@@ -143,3 +143,39 @@ class SyntheticSQuAD(tud.Dataset):
         s = int(torch.randint(q, L - 31, (1,), generator=g))
         e = s + int(torch.randint(0, 30, (1,), generator=g))
         return ids, tt, am, torch.tensor(s), torch.tensor(e)
+
+
+class SyntheticGLUEPairs(tud.Dataset):
+    """MRPC-shaped sentence-pair classification features (input_ids, attention_mask,
+    token_type_ids, label) with a learnable rule: label 1 pairs repeat a span of sentence A inside
+    sentence B (a paraphrase stand-in), label 0 pairs do not.  Variable sentence lengths exercise
+    the padding mask."""
+
+    def __init__(self, length: int, seq_len: int = 128, vocab_size: int = 30522, seed: int = 0) -> None:
+        self.length = int(length)
+        self.seq_len = seq_len
+        self.vocab = vocab_size
+        self.seed = seed
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int) -> Tuple[torch.Tensor, ...]:
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        L = self.seq_len
+        la = int(torch.randint(L // 8, L // 2 - 2, (1,), generator=g))
+        lb = int(torch.randint(L // 8, L - la - 3, (1,), generator=g))
+        a = torch.randint(1000, self.vocab, (la,), generator=g)
+        b = torch.randint(1000, self.vocab, (lb,), generator=g)
+        label = int(torch.randint(0, 2, (1,), generator=g))
+        if label == 1:
+            n = min(la, lb, 8)
+            b[:n] = a[:n]
+        ids = torch.zeros(L, dtype=torch.int64)
+        tt = torch.zeros(L, dtype=torch.int64)
+        am = torch.zeros(L, dtype=torch.int64)
+        seq = torch.cat([torch.tensor([101]), a, torch.tensor([102]), b, torch.tensor([102])])
+        ids[:seq.numel()] = seq
+        am[:seq.numel()] = 1
+        tt[la + 2:seq.numel()] = 1
+        return ids, am, tt, torch.tensor(label)

@@ -21,6 +21,9 @@ SHRINK = {
                              "intermediate_size": 128, "embedding_size": 16, "vocab_size": 2000,
                              "max_seq_length": 128, "global_batch_size": 2, "train_records": 8,
                              "validation_records": 4, "amp": "O2"},
+    "bert_glue_pytorch": {"num_hidden_layers": 1, "hidden_size": 64, "num_attention_heads": 2,
+                          "intermediate_size": 128, "vocab_size": 2000, "max_seq_length": 64, "global_batch_size": 2,
+                          "train_records": 8, "validation_records": 4, "amp": "O2"},
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
     "mnist_pytorch": {"global_batch_size": 4},
     "gan_mnist_pytorch": {"global_batch_size": 4},
