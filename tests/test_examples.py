@@ -24,6 +24,8 @@ SHRINK = {
     "bert_glue_pytorch": {"num_hidden_layers": 1, "hidden_size": 64, "num_attention_heads": 2,
                           "intermediate_size": 128, "vocab_size": 2000, "max_seq_length": 64, "global_batch_size": 2,
                           "train_records": 8, "validation_records": 4, "amp": "O2"},
+    "protonet_omniglot_pytorch": {"num_classes_train": 5, "num_classes_val": 5, "hidden_dim": 16, "embedding_dim": 16,
+                                  "tasks_per_epoch_train": 4, "tasks_per_epoch_val": 2, "num_glyph_classes": 40},
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
     "mnist_pytorch": {"global_batch_size": 4},
     "gan_mnist_pytorch": {"global_batch_size": 4},
