@@ -26,6 +26,8 @@ SHRINK = {
                           "train_records": 8, "validation_records": 4, "amp": "O2"},
     "protonet_omniglot_pytorch": {"num_classes_train": 5, "num_classes_val": 5, "hidden_dim": 16, "embedding_dim": 16,
                                   "tasks_per_epoch_train": 4, "tasks_per_epoch_val": 2, "num_glyph_classes": 40},
+    "darts_cifar10_pytorch": {"init_channels": 8, "layers": 5, "global_batch_size": 2, "train_records": 8,
+                              "validation_records": 4},
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
     "mnist_pytorch": {"global_batch_size": 4},
     "gan_mnist_pytorch": {"global_batch_size": 4},
