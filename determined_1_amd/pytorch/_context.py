@@ -307,7 +307,9 @@ class PyTorchTrialContext(trial.TrialContext):
         if not self._finalized:
             self._finalize()
         if st.bucketer is not None:
+            self._timers.comm_start()
             st.bucketer.synchronize()
+            self._timers.comm_end()
         scaler = self._amp.scaler if (self._amp is not None) else None
         host_scale = self._grad_scale()
         params = [p for g in optimizer.param_groups for p in g.get("params", [])]

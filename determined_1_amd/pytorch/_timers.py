@@ -1,5 +1,5 @@
-"""Per-batch phase timers (SURVEY §5.1 "new build": data / forward / backward / communication +
-optimizer), enabled with ``DET_STEP_TIMERS=1``.
+"""Per-batch phase timers (SURVEY §5.1 "new build": data / forward / backward / exposed
+communication / optimizer), enabled with ``DET_STEP_TIMERS=1``.
 
 Device phases are bracketed with HIP events on the compute stream, so timing adds no host
 synchronisation inside the step; the events are resolved once at the end of each RUN_STEP
@@ -47,6 +47,17 @@ class StepTimers:
         if self.enabled:
             self._ev("bwd1")
 
+    def comm_start(self) -> None:
+        if self.enabled:
+            self._ev("comm0")
+
+    def comm_end(self) -> None:
+        """After the compute stream was made to wait for the gradient all-reduces: the device
+        time between comm0 and comm1 is the EXPOSED communication (RCCL work still running after
+        backward finished); the overlapped part is already inside ``backward``."""
+        if self.enabled:
+            self._ev("comm1")
+
     def step_end(self) -> None:
         if self.enabled:
             self._ev("opt1")
@@ -55,8 +66,8 @@ class StepTimers:
         if not self.enabled or not self._marks:
             return {}
         torch.cuda.synchronize(self.device)
-        acc = {"forward": 0.0, "backward": 0.0, "optimizer": 0.0, "cpu_forward": 0.0, "cpu_backward": 0.0,
-               "cpu_optimizer": 0.0}
+        acc = {"forward": 0.0, "backward": 0.0, "comm_exposed": 0.0, "optimizer": 0.0, "cpu_forward": 0.0,
+               "cpu_backward": 0.0, "cpu_optimizer": 0.0}
         n = 0
         for m in self._marks:
             if not all(k in m for k in ("start", "bwd0", "bwd1")):
@@ -66,7 +77,10 @@ class StepTimers:
             acc["cpu_forward"] += 1000.0 * (m["cpu_bwd0"] - m["cpu_start"])
             acc["cpu_backward"] += 1000.0 * (m["cpu_bwd1"] - m["cpu_bwd0"])
             if "opt1" in m:
-                acc["optimizer"] += m["bwd1"].elapsed_time(m["opt1"])
+                opt0 = "comm1" if "comm1" in m else "bwd1"
+                if "comm1" in m:
+                    acc["comm_exposed"] += m["comm0"].elapsed_time(m["comm1"])
+                acc["optimizer"] += m[opt0].elapsed_time(m["opt1"])
                 acc["cpu_optimizer"] += 1000.0 * (m["cpu_opt1"] - m["cpu_bwd1"])
             n += 1
         out = {f"timer/{k}_ms": v / max(1, n) for k, v in acc.items()}
