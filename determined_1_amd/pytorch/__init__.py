@@ -15,7 +15,7 @@ from determined_1_amd.pytorch._data import (
 from determined_1_amd.pytorch._lr_scheduler import LRScheduler
 from determined_1_amd.pytorch._reducer import Reducer, _reduce_metrics
 from determined_1_amd.pytorch._context import ClipGradsNorm, PyTorchTrialContext
-from determined_1_amd.pytorch._trial import PyTorchTrial, PyTorchTrialController
+from determined_1_amd.pytorch._trial import PyTorchTrial, PyTorchTrialController, reset_parameters
 
 __all__ = [
     "ClipGradsL2Norm",
@@ -35,5 +35,6 @@ __all__ = [
     "TorchData",
     "adapt_batch_sampler",
     "data_length",
+    "reset_parameters",
     "to_device",
 ]

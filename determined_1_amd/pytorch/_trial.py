@@ -540,3 +540,13 @@ class PyTorchTrial(trial.Trial):
 
     def evaluate_full_dataset(self, data_loader: torch.utils.data.DataLoader) -> Dict[str, Any]:
         pass  # type: ignore
+
+
+def reset_parameters(model: torch.nn.Module) -> None:
+    """Deprecated reference helper (``harness/determined/pytorch/_pytorch_trial.py:1023``): call
+    ``reset_parameters()`` on every submodule that defines it."""
+    logging.warning("det.pytorch.reset_parameters() is deprecated; modules should reset themselves in __init__().")
+    for m in model.modules():
+        fn = getattr(m, "reset_parameters", None)
+        if callable(fn):
+            fn()

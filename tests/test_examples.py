@@ -28,6 +28,9 @@ SHRINK = {
                                   "tasks_per_epoch_train": 4, "tasks_per_epoch_val": 2, "num_glyph_classes": 40},
     "darts_cifar10_pytorch": {"init_channels": 8, "layers": 5, "global_batch_size": 2, "train_records": 8,
                               "validation_records": 4},
+    "darts_penntreebank_pytorch": {"emsize": 32, "nhid": 32, "nhidlast": 32, "vocab_size": 200, "train_tokens": 4000,
+                                   "valid_tokens": 800, "global_batch_size": 4, "eval_batch_size": 4, "bptt": 10,
+                                   "max_seq_length_delta": 4},
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
     "mnist_pytorch": {"global_batch_size": 4},
     "gan_mnist_pytorch": {"global_batch_size": 4},
