@@ -27,24 +27,29 @@ PRIMITIVES = ("none", "max_pool_3x3", "avg_pool_3x3", "skip_connect", "sep_conv_
 
 
 class ReLUConvBN(nn.Sequential):
-    def __init__(self, cin: int, cout: int, k: int, stride: int, pad: int) -> None:
-        super().__init__(nn.ReLU(inplace=False), nn.Conv2d(cin, cout, k, stride, pad, bias=False), nn.BatchNorm2d(cout))
+    """act -> conv -> BN (``act`` is ReLU in DARTS, swish in the GAEA ImageNet network)."""
+
+    def __init__(self, cin: int, cout: int, k: int, stride: int, pad: int, affine: bool = True,
+                 act: Callable[[], nn.Module] = nn.ReLU) -> None:
+        super().__init__(act(), nn.Conv2d(cin, cout, k, stride, pad, bias=False), nn.BatchNorm2d(cout, affine=affine))
 
 
 class DilConv(nn.Sequential):
     """ReLU -> depthwise k x k (dilation d) -> pointwise 1x1 -> BN."""
 
-    def __init__(self, cin: int, cout: int, k: int, stride: int, pad: int, dilation: int) -> None:
-        super().__init__(nn.ReLU(inplace=False),
+    def __init__(self, cin: int, cout: int, k: int, stride: int, pad: int, dilation: int, affine: bool = True,
+                 act: Callable[[], nn.Module] = nn.ReLU) -> None:
+        super().__init__(act(),
                          nn.Conv2d(cin, cin, k, stride, pad, dilation=dilation, groups=cin, bias=False),
-                         nn.Conv2d(cin, cout, 1, bias=False), nn.BatchNorm2d(cout))
+                         nn.Conv2d(cin, cout, 1, bias=False), nn.BatchNorm2d(cout, affine=affine))
 
 
 class SepConv(nn.Sequential):
     """Two stacked dilation-1 DilConv blocks, the first carrying the stride."""
 
-    def __init__(self, cin: int, cout: int, k: int, stride: int, pad: int) -> None:
-        super().__init__(DilConv(cin, cin, k, stride, pad, 1), DilConv(cin, cout, k, 1, pad, 1))
+    def __init__(self, cin: int, cout: int, k: int, stride: int, pad: int, affine: bool = True,
+                 act: Callable[[], nn.Module] = nn.ReLU) -> None:
+        super().__init__(DilConv(cin, cin, k, stride, pad, 1, affine, act), DilConv(cin, cout, k, 1, pad, 1, affine, act))
 
 
 class Zero(nn.Module):
@@ -59,27 +64,28 @@ class Zero(nn.Module):
 class FactorizedReduce(nn.Module):
     """Stride-2 1x1 convolutions on two offset pixel grids, concatenated (shape-preserving skip)."""
 
-    def __init__(self, cin: int, cout: int) -> None:
+    def __init__(self, cin: int, cout: int, affine: bool = True, act: Callable[[], nn.Module] = nn.ReLU) -> None:
         super().__init__()
+        self.act = act()
         self.conv1 = nn.Conv2d(cin, cout // 2, 1, 2, bias=False)
         self.conv2 = nn.Conv2d(cin, cout - cout // 2, 1, 2, bias=False)
-        self.bn = nn.BatchNorm2d(cout)
+        self.bn = nn.BatchNorm2d(cout, affine=affine)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = F.relu(x)
+        x = self.act(x)
         return self.bn(torch.cat([self.conv1(x), self.conv2(x[:, :, 1:, 1:])], dim=1))
 
 
 OPS = {
-    "none": lambda c, s: Zero(s),
-    "max_pool_3x3": lambda c, s: nn.MaxPool2d(3, s, 1),
-    "avg_pool_3x3": lambda c, s: nn.AvgPool2d(3, s, 1, count_include_pad=False),
-    "skip_connect": lambda c, s: nn.Identity() if s == 1 else FactorizedReduce(c, c),
-    "sep_conv_3x3": lambda c, s: SepConv(c, c, 3, s, 1),
-    "sep_conv_5x5": lambda c, s: SepConv(c, c, 5, s, 2),
-    "dil_conv_3x3": lambda c, s: DilConv(c, c, 3, s, 2, 2),
-    "dil_conv_5x5": lambda c, s: DilConv(c, c, 5, s, 4, 2),
-}  # type: Dict[str, Callable[[int, int], nn.Module]]
+    "none": lambda c, s, affine=True, act=nn.ReLU: Zero(s),
+    "max_pool_3x3": lambda c, s, affine=True, act=nn.ReLU: nn.MaxPool2d(3, s, 1),
+    "avg_pool_3x3": lambda c, s, affine=True, act=nn.ReLU: nn.AvgPool2d(3, s, 1, count_include_pad=False),
+    "skip_connect": lambda c, s, affine=True, act=nn.ReLU: nn.Identity() if s == 1 else FactorizedReduce(c, c, affine, act),
+    "sep_conv_3x3": lambda c, s, affine=True, act=nn.ReLU: SepConv(c, c, 3, s, 1, affine, act),
+    "sep_conv_5x5": lambda c, s, affine=True, act=nn.ReLU: SepConv(c, c, 5, s, 2, affine, act),
+    "dil_conv_3x3": lambda c, s, affine=True, act=nn.ReLU: DilConv(c, c, 3, s, 2, 2, affine, act),
+    "dil_conv_5x5": lambda c, s, affine=True, act=nn.ReLU: DilConv(c, c, 5, s, 4, 2, affine, act),
+}  # type: Dict[str, Callable[..., nn.Module]]
 
 
 def drop_path(x: torch.Tensor, p: float) -> torch.Tensor:

@@ -31,6 +31,10 @@ SHRINK = {
     "darts_penntreebank_pytorch": {"emsize": 32, "nhid": 32, "nhidlast": 32, "vocab_size": 200, "train_tokens": 4000,
                                    "valid_tokens": 800, "global_batch_size": 4, "eval_batch_size": 4, "bptt": 10,
                                    "max_seq_length_delta": 4},
+    "search": {"init_channels": 8, "layers": 3, "nodes": 2, "global_batch_size": 2, "train_records": 8,
+               "validation_records": 4},  # nas/gaea_pytorch/search
+    "eval": {"num_classes": 10, "image_size": 32, "init_channels": 8, "layers": 3, "global_batch_size": 2,
+             "train_records": 8, "validation_records": 4},  # nas/gaea_pytorch/eval
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4},
     "mnist_pytorch": {"global_batch_size": 4},
     "gan_mnist_pytorch": {"global_batch_size": 4},
