@@ -157,6 +157,9 @@ def main() -> None:
                 "final_avg_loss": loss,
             },
         }
+        phases = getattr(ctrl, "last_step_timers", None)
+        if phases:  # DET_STEP_TIMERS=1: per-batch device phases of the timed window (forward/backward/comm/opt)
+            out["config"]["phase_ms"] = {k.split("/", 1)[1]: round(v, 3) for k, v in phases.items()}
         print(json.dumps(out), flush=True)
     pdist.shutdown()
 

@@ -22,7 +22,7 @@ def test_bench_two_ranks_sharing_the_gpu(gpu, tmp_path):
     from determined_1_amd.deploy.local import free_port
 
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, DET_DIST_SHARE_GPU="1", DET_DIST_BACKEND="gloo")
+    env = dict(os.environ, DET_DIST_SHARE_GPU="1", DET_DIST_BACKEND="gloo", DET_STEP_TIMERS="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(repo, "bench.py"),
                         "--gpus", "2", "--steps", "3", "--warmup", "2", "--batch-per-gpu", "16", "--image-size", "64",
@@ -32,6 +32,8 @@ def test_bench_two_ranks_sharing_the_gpu(gpu, tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
     assert out["config"]["final_avg_loss"] is not None
+    ph = out["config"]["phase_ms"]  # step timers, incl. the exposed all-reduce wait after backward
+    assert ph["forward_ms"] > 0 and ph["backward_ms"] > 0 and ph["optimizer_ms"] > 0 and ph["comm_exposed_ms"] >= 0
 
 
 def test_bert_two_ranks_sharing_the_gpu_with_aggregation(gpu):
