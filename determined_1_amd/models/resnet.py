@@ -11,7 +11,7 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
-from determined_1_amd.ops.norm import BatchNormAct2d
+from determined_1_amd.ops.norm import BatchNormAct2d, linked_conv2d
 from determined_1_amd.ops.pool import MaxPool3x3s2
 
 # Fused BN(+add)(+ReLU) HIP kernels (ops/csrc/det_norm.hip) on by default; set
@@ -31,6 +31,15 @@ def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
+def _shortcut(downsample: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """Projection shortcut; its conv's input gradient is summed inside the producer's fused BN
+    backward (``linked_conv2d``) rather than added to conv1's input gradient by autograd."""
+    if (FUSED_BN and isinstance(downsample, nn.Sequential) and len(downsample) == 2
+            and isinstance(downsample[0], nn.Conv2d) and isinstance(downsample[1], BatchNormAct2d)):
+        return downsample[1](linked_conv2d(x, downsample[0]))
+    return downsample(x)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -44,7 +53,7 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.downsample is None else self.downsample(x)
+        idt = x if self.downsample is None else _shortcut(self.downsample, x)
         out = self.bn1(self.conv1(x))
         return self.bn2(self.conv2(out), idt, shortcut_link=self.downsample is None)
 
@@ -64,7 +73,7 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.downsample is None else self.downsample(x)
+        idt = x if self.downsample is None else _shortcut(self.downsample, x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward

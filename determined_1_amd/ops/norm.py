@@ -142,6 +142,58 @@ class _BNActTrain(torch.autograd.Function):
         return dx, dres, dw, db, None, None, None, None, None, None, None
 
 
+class _LinkedConv(torch.autograd.Function):
+    """``conv2d(x, w)`` where ``x`` is the output of a ``_BNActTrain`` that also feeds another conv
+    (a ResNet downsample block: ``x`` -> block conv1 and -> shortcut conv).  The input gradient of
+    this conv is handed to the producer's backward as its second upstream gradient (summed in the
+    BN-backward kernels) instead of returned to autograd, which would add it to the other conv's
+    input gradient in a separate elementwise pass over the whole activation.  ``x`` keeps its
+    autograd edge (a None gradient is returned), so the producer's backward is ordered after
+    this one by the graph itself."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, dilation, groups, link):
+        ctx.save_for_backward(x, weight)
+        ctx.conv = (stride, padding, dilation, groups)
+        ctx.link = link
+        return F.conv2d(x, weight, None, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.conv
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            dy, x, weight, None, list(stride), list(padding), list(dilation), False, [0] * len(stride), groups,
+            [True, bool(ctx.needs_input_grad[1]), False])
+        link, ctx.link = ctx.link, None
+        if link is None:  # a repeated backward (retain_graph): plain autograd accumulation
+            return dx, dw, None, None, None, None, None
+        if link.extra_dy is not None:
+            raise RuntimeError("second upstream gradient linked twice to one producer")
+        link.extra_dy = dx.contiguous(memory_format=torch.channels_last)
+        return None, dw, None, None, None, None, None
+
+
+def _autocast_keeps(x: torch.Tensor) -> bool:
+    """True when autocast (if on) would leave ``x``'s dtype unchanged for a conv."""
+    dev = x.device.type
+    if not torch.is_autocast_enabled(dev):
+        return True
+    return torch.get_autocast_dtype(dev) == x.dtype
+
+
+def linked_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)``; when ``x`` came from the fused BN-act op and feeds another consumer too, the
+    conv's input gradient is summed inside the producer's BN-backward kernels (``_LinkedConv``)."""
+    if (SHORTCUT_LINK and conv.bias is None and torch.is_grad_enabled() and x.requires_grad
+            and isinstance(x.grad_fn, _BNActTrain._backward_cls) and x.dim() == 4
+            and x.dtype == conv.weight.dtype and _autocast_keeps(x)
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.padding_mode == "zeros"
+            and getattr(x.grad_fn, "extra_dy", None) is None):
+        return _LinkedConv.apply(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, x.grad_fn)
+    return conv(x)
+
+
 def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optional[torch.Tensor] = None,
            relu: bool = True, shortcut_link: bool = False) -> torch.Tensor:
     """``act(bn(x) + residual)`` with the module's parameters/buffers and train/eval semantics.

@@ -111,6 +111,33 @@ def test_resnet50_fused_matches_stock(gpu):
         torch.testing.assert_close(pb.grad, pa.grad, atol=2e-3, rtol=2e-2, msg=lambda s: f"{na}: {s}")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linked_projection_conv_matches_autograd_sum(gpu, dtype, monkeypatch):
+    """x = fused BN-act output feeding two convs; the projection conv's input gradient handed to
+    the producer's BN backward (dy2) == autograd summing both conv input gradients."""
+    torch.manual_seed(3)
+    bn = norm.BatchNormAct2d(64, relu=True).to(gpu)
+    conv_a = torch.nn.Conv2d(64, 32, 1, bias=False).to(gpu, dtype).to(memory_format=torch.channels_last)
+    conv_b = torch.nn.Conv2d(64, 128, 1, stride=2, bias=False).to(gpu, dtype).to(memory_format=torch.channels_last)
+    x0 = torch.randn(4, 64, 14, 14, device=gpu, dtype=dtype).to(memory_format=torch.channels_last)
+    ga = torch.randn(4, 32, 14, 14, device=gpu, dtype=dtype).to(memory_format=torch.channels_last)
+    gb = torch.randn(4, 128, 7, 7, device=gpu, dtype=dtype).to(memory_format=torch.channels_last)
+    outs = []
+    for link in (False, True):
+        monkeypatch.setattr(norm, "SHORTCUT_LINK", link)
+        for m in (bn, conv_a, conv_b):
+            m.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        h = bn(x)
+        b = norm.linked_conv2d(h, conv_b)
+        assert (type(b.grad_fn).__name__ == "_LinkedConvBackward") == link
+        torch.autograd.backward([conv_a(h), b], [ga, gb])
+        outs.append([x.grad, bn.weight.grad, bn.bias.grad, conv_a.weight.grad, conv_b.weight.grad])
+    tol = dict(atol=1e-4, rtol=1e-4) if dtype == torch.float32 else dict(atol=3e-2, rtol=3e-2)
+    for r, d in zip(*outs):
+        torch.testing.assert_close(d.float(), r.float(), **tol)
+
+
 def test_resnet50_fused_shortcut_link_and_pool_match_stock(gpu, monkeypatch):
     """Fused BN with identity-shortcut gradient links (dy2 summed in the BN backward) and the HIP
     stem max-pool vs stock modules; non-zero residual gammas so every branch carries gradient.
