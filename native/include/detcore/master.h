@@ -25,6 +25,7 @@
 #include "detcore/config.h"
 #include "detcore/json.h"
 #include "detcore/net.h"
+#include "detcore/rw_coordinator.h"
 #include "detcore/store.h"
 
 namespace detcore {
@@ -73,6 +74,7 @@ class Master {
   void InstallRoutes();
   void HandleAgentSocket(const net::Request& req, net::WsPtr ws);
   void HandleTrialSocket(const net::Request& req, net::WsPtr ws);
+  void HandleRWLockSocket(const net::Request& req, net::WsPtr ws);
   void RestoreExperiments();
   void EnsureDefaultUsers();
   std::string UserForRequest(const net::Request& r);
@@ -81,6 +83,7 @@ class Master {
   MasterConfig cfg_;
   std::unique_ptr<Store> store_;
   std::unique_ptr<actor::System> sys_;
+  RWCoordinator rw_coordinator_;  // before http_: socket threads use it until the server stops
   net::HttpServer http_;
   std::map<std::string, actor::Ref> pools_;
   std::mutex mu_;

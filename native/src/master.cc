@@ -25,6 +25,7 @@
 //   POST   /trial_logs                             log shipping (agents / harness)
 //   WS     /agents?id=&resource_pool=&label=      agent channel
 //   WS     /ws/trial/:e/:t/:c                      harness channel (C-ws / C-done)
+//   WS     /ws/data-layer/*?read_lock=true|false   readers-writer lock per resource path (M24)
 #include "detcore/master.h"
 
 #include <signal.h>
@@ -34,6 +35,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <ctime>
@@ -1013,6 +1015,26 @@ void Master::InstallRoutes() {
   // ----------------------------------------------------------------------- websockets
   http_.RouteWs("/agents", [this](const net::Request& r, net::WsPtr ws) { HandleAgentSocket(r, ws); });
   http_.RouteWs("/ws/trial/:e/:t/:c", [this](const net::Request& r, net::WsPtr ws) { HandleTrialSocket(r, ws); });
+  http_.RouteWs("/ws/data-layer/*", [this](const net::Request& r, net::WsPtr ws) { HandleRWLockSocket(r, ws); });
+}
+
+// One socket = one lock request; the lock is held until the socket closes (reference
+// core.go:253-289).  The resource is the full request path, as in the reference.
+void Master::HandleRWLockSocket(const net::Request& r, net::WsPtr ws) {
+  std::string mode = r.Query("read_lock", "");
+  for (auto& ch : mode) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  if (mode != "true" && mode != "false") {
+    ws->Send("error: read_lock must be true or false");
+    ws->Close();
+    return;
+  }
+  const bool read = mode == "true";
+  std::weak_ptr<net::WsConn> weak = ws;
+  int64_t ticket = rw_coordinator_.Acquire(r.path, read, [weak](int64_t, bool granted_read) {
+    if (auto s = weak.lock()) s->Send(granted_read ? "read_lock_granted" : "write_lock_granted");
+  });
+  ws->ReadLoop([](const std::string&) {});
+  rw_coordinator_.Release(ticket);
 }
 
 void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {

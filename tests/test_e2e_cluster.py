@@ -316,3 +316,58 @@ def test_tensorboard_service_through_proxy(cluster):
         assert page.status_code == 200 and "<svg" in page.text and page.headers["Content-Type"].startswith("text/html")
     finally:
         cl.post(f"/commands/{cid}/kill")
+
+
+def test_rw_coordinator_lock_semantics(tmp_path, monkeypatch):
+    """WS /ws/data-layer/*: readers share, a writer excludes, a waiting writer blocks later readers,
+    and closing a socket releases its lock (reference master/internal/rw_coordinator.go)."""
+    import threading
+
+    import requests
+
+    from determined_1_amd.api import LockError, RWLock
+    from determined_1_amd.deploy.local import free_port, native_binary
+
+    monkeypatch.setenv("HOME", str(tmp_path))
+    port = free_port()
+    p = subprocess.Popen([native_binary("det-master"), "--host", "127.0.0.1", "--port", str(port)],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    addr = f"127.0.0.1:{port}"
+    try:
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            try:
+                requests.get(f"http://{addr}/info", timeout=1)
+                break
+            except requests.RequestException:
+                time.sleep(0.1)
+        r1, r2 = RWLock(addr, "cache/ds", read=True), RWLock(addr, "cache/ds", read=True)
+        r1.acquire()
+        r2.acquire()  # shared
+        with pytest.raises(LockError):
+            RWLock(addr, "cache/ds", read=False, timeout=0.5).acquire()
+        events = []
+        writer = RWLock(addr, "cache/ds", read=False)
+        t = threading.Thread(target=lambda: (writer.acquire(), events.append("w")))
+        t.start()
+        time.sleep(0.3)
+        late_reader = RWLock(addr, "cache/ds", read=True)
+        rt = threading.Thread(target=lambda: (late_reader.acquire(), events.append("r")))
+        rt.start()
+        time.sleep(0.3)
+        assert events == []
+        with RWLock(addr, "cache/other", read=False):  # independent resource
+            pass
+        r1.release()
+        time.sleep(0.2)
+        assert events == []
+        r2.release()
+        t.join(timeout=5)
+        assert events == ["w"]
+        writer.release()
+        rt.join(timeout=5)
+        assert events == ["w", "r"]
+        late_reader.release()
+    finally:
+        p.terminate()
+        p.wait(timeout=10)
