@@ -32,6 +32,17 @@ class _TrainContext(metaclass=abc.ABCMeta):
         env, dist_cfg, rank = _local.make_local_env(config, managed_training=False)
         return cls(env, dist_cfg, rank)
 
+    @property
+    def experimental(self) -> Any:
+        """Dataset cache decorators (``cache_train_dataset`` / ``cache_validation_dataset``), see
+        ``determined_1_amd/_data_layer.py``; reference ``_data_layer/_context.py``."""
+        if getattr(self, "_data_layer", None) is None:
+            from determined_1_amd._data_layer import DataLayerContext
+
+            self._data_layer = DataLayerContext(self.env, self.distributed.get_rank(), self.distributed.get_size(),
+                                                managed=bool(self.env.managed_training and self.env.master_addr))
+        return self._data_layer
+
     def get_experiment_config(self) -> Dict[str, Any]:
         return self.env.experiment_config
 
