@@ -36,7 +36,7 @@ class LocalCluster:
     def __init__(self, agents: int = 1, slots_per_agent: int = 0, port: Optional[int] = None,
                  store_dir: Optional[str] = None, checkpoint_dir: Optional[str] = None,
                  scheduler: str = "fair_share", work_dir: Optional[str] = None, gpu: bool = False,
-                 log_dir: Optional[str] = None, tick_ms: int = 100) -> None:
+                 log_dir: Optional[str] = None, tick_ms: int = 100, master_args: Optional[List[str]] = None) -> None:
         self.port = port or free_port()
         self.tmp = tempfile.mkdtemp(prefix="det-local-")
         self.store_dir = store_dir or os.path.join(self.tmp, "store")
@@ -48,6 +48,7 @@ class LocalCluster:
         self.scheduler = scheduler
         self.gpu = gpu
         self.tick_ms = tick_ms
+        self.master_args = list(master_args or [])
         self.master_proc = None  # type: Optional[subprocess.Popen]
         self.agent_procs = []  # type: List[subprocess.Popen]
 
@@ -61,7 +62,7 @@ class LocalCluster:
         self.master_proc = subprocess.Popen(
             [native_binary("det-master"), "--host", "127.0.0.1", "--port", str(self.port), "--store-dir",
              self.store_dir, "--scheduler", self.scheduler, "--checkpoint-host-path", self.checkpoint_dir,
-             "--python", sys.executable, "--scheduler-tick-ms", str(self.tick_ms)],
+             "--python", sys.executable, "--scheduler-tick-ms", str(self.tick_ms)] + self.master_args,
             stdout=log, stderr=subprocess.STDOUT)
         deadline = time.time() + 30
         while time.time() < deadline:

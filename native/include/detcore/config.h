@@ -37,6 +37,9 @@ struct MasterConfig {
   double scheduler_tick_ms = 500;
   std::string python = "python3";
   bool require_auth = false;
+  // telemetry.{enabled, file}: reference Segment events (master/internal/telemetry) written as JSON
+  // lines to a local file -- there is no egress; disabled unless a file is configured.
+  std::string telemetry_file;
   Json provisioner;  // {max_instances, min_instances, slots_per_instance, ...}; empty = disabled  // security.authentication: tokens required on the REST API
   static MasterConfig FromJson(const Json& j);
   Json ToJson() const;

@@ -69,6 +69,8 @@ class Master {
   void RunCheckpointGC(int64_t experiment_id, const Json& exp_config, const Json& to_delete);
   std::string cluster_id() const { return cluster_id_; }
   bool shutting_down() const { return shutting_down_.load(); }
+  // Append one telemetry event (reference telemetry/reports.go) when telemetry is configured.
+  void ReportTelemetry(const std::string& event, Json properties);
 
  private:
   void InstallRoutes();
@@ -96,6 +98,7 @@ class Master {
   std::condition_variable stop_cv_;
   bool stopped_ = false;
   std::atomic<bool> shutting_down_{false};
+  std::mutex telemetry_mu_;
 };
 
 // Helpers shared by the master translation units.

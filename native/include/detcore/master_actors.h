@@ -170,6 +170,7 @@ class ExperimentActor : public actor::Actor {
   std::string metric_;
   std::string pool_;
   std::string state_ = "ACTIVE";
+  std::string reported_state_;  // last state sent to telemetry
   bool shutdown_ = false, shutdown_failure_ = false, stopping_ = false;
   bool has_best_ = false;
   double best_metric_ = 0;

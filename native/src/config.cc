@@ -279,6 +279,8 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
   c.python = j.get_string("python", c.python);
   c.provisioner = j["provisioner"];
   if (j["security"].is_object()) c.require_auth = j["security"].get_bool("authentication", c.require_auth);
+  if (j["telemetry"].is_object() && j["telemetry"].get_bool("enabled", true))
+    c.telemetry_file = j["telemetry"].get_string("file", "");
   return c;
 }
 
@@ -303,6 +305,10 @@ Json MasterConfig::ToJson() const {
   sec["authentication"] = require_auth;
   j["security"] = sec;
   j["provisioner"] = provisioner;
+  Json tel = Json::object();
+  tel["enabled"] = !telemetry_file.empty();
+  tel["file"] = telemetry_file;
+  j["telemetry"] = tel;
   return j;
 }
 

@@ -343,6 +343,13 @@ int64_t Master::CreateExperiment(const Json& body, bool* activate) {
   md["experiment_id"] = id;
   md["files"] = body["model_definition"].is_array() ? body["model_definition"] : Json::array();
   store_->Put("model_definitions", id, md);
+  Json props = Json::object();
+  props["id"] = id;
+  props["searcher"] = cfg["searcher"];
+  props["resources"] = cfg["resources"];
+  props["num_hparams"] = static_cast<int64_t>(cfg["hyperparameters"].is_object() ? cfg["hyperparameters"].as_object().size() : 0);
+  props["batches_per_step"] = cfg["scheduling_unit"];
+  ReportTelemetry("experiment_created", props);
   return id;
 }
 
@@ -1037,6 +1044,18 @@ void Master::HandleRWLockSocket(const net::Request& r, net::WsPtr ws) {
   rw_coordinator_.Release(ticket);
 }
 
+void Master::ReportTelemetry(const std::string& event, Json properties) {
+  if (cfg_.telemetry_file.empty()) return;
+  Json line = Json::object();
+  line["event"] = event;
+  line["timestamp"] = NowRFC3339();
+  line["cluster_id"] = cluster_id_;
+  line["properties"] = std::move(properties);
+  std::lock_guard<std::mutex> g(telemetry_mu_);
+  std::ofstream f(cfg_.telemetry_file, std::ios::app);
+  f << line.dump() << "\n";
+}
+
 void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
   auto conn = std::make_shared<AgentConn>();
   conn->id = r.Query("id", "agent-" + NewUUID().substr(0, 8));
@@ -1075,6 +1094,12 @@ void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
       a.id = conn->id;
       a.label = m.get_string("label", conn->label);
       conn->devices = m["devices"];
+      {
+        Json props = Json::object();
+        props["uuid"] = conn->id;
+        props["devices"] = conn->devices;
+        ReportTelemetry("agent_connected", props);
+      }
       for (auto& d : m["devices"].as_array()) {
         sched::Slot s;
         s.device_id = static_cast<int>(d.get_int("id", 0));
@@ -1107,6 +1132,9 @@ void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
     std::lock_guard<std::mutex> g(mu_);
     cids.assign(conn->containers.begin(), conn->containers.end());
     agents_.erase(conn->id);
+    Json props = Json::object();
+    props["uuid"] = conn->id;
+    ReportTelemetry("agent_disconnected", props);
   }
   Pool(conn->pool)->Tell(RemoveAgent{conn->id});
   for (auto& cid : cids) {

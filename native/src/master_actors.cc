@@ -178,6 +178,14 @@ void ExperimentActor::SaveState() {
   if (IsTerminal(state_)) patch["end_time"] = NowRFC3339();
   if (!best_validation_.is_null()) patch["best_validation"] = best_validation_;
   m_->store().Update("experiments", id_, patch);
+  if (state_ != reported_state_) {
+    reported_state_ = state_;
+    Json props = Json::object();
+    props["id"] = id_;
+    props["state"] = state_;
+    if (IsTerminal(state_)) props["num_trials"] = static_cast<int64_t>(m_->store().Where("trials", "experiment_id", Json(id_)).size());
+    m_->ReportTelemetry("experiment_state_changed", props);
+  }
 }
 
 bool ExperimentActor::IsTerminal(const std::string& s) {

@@ -75,6 +75,8 @@ int main(int argc, char** argv) {
       cfgj["provisioner"]["slots_per_instance"] = std::stoi(next());
     } else if (a == "--provision-idle-ms") {
       cfgj["provisioner"]["max_idle_agent_period_ms"] = std::stoi(next());
+    } else if (a == "--telemetry-file") {
+      cfgj["telemetry"]["file"] = next();
     } else if (a == "--require-auth") {
       cfgj["security"]["authentication"] = true;
     } else if (a == "--scheduler-tick-ms") {

@@ -33,7 +33,7 @@ def noop_config(searcher, **extra):
 def cluster(tmp_path_factory):
     d = tmp_path_factory.mktemp("cluster")
     c = LocalCluster(agents=2, slots_per_agent=2, store_dir=str(d / "store"), checkpoint_dir=str(d / "ckpt"),
-                     log_dir=str(d), tick_ms=50)
+                     log_dir=str(d), tick_ms=50, master_args=["--telemetry-file", str(d / "telemetry.jsonl")])
     c.up()
     yield c
     c.down()
@@ -371,3 +371,23 @@ def test_rw_coordinator_lock_semantics(tmp_path, monkeypatch):
     finally:
         p.terminate()
         p.wait(timeout=10)
+
+
+def test_telemetry_events_written(cluster):
+    """Reference master/internal/telemetry/reports.go events, written locally (no egress)."""
+    import json
+
+    path = pathlib.Path(cluster.log_dir) / "telemetry.jsonl"
+    _, exp_id = submit(cluster, noop_config({"name": "single", "metric": "validation_error",
+                                             "max_length": {"batches": 1}}))
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        events = [json.loads(l) for l in path.read_text().splitlines()] if path.exists() else []
+        names = {e["event"] for e in events}
+        if {"agent_connected", "experiment_created", "experiment_state_changed"} <= names:
+            break
+        time.sleep(0.2)
+    assert {"agent_connected", "experiment_created", "experiment_state_changed"} <= names
+    created = [e for e in events if e["event"] == "experiment_created" and e["properties"]["id"] == exp_id]
+    assert created and created[0]["properties"]["searcher"]["name"] == "single"
+    assert all(e["cluster_id"] for e in events)
