@@ -1,8 +1,16 @@
 """North-star benchmark: ResNet-50 PyTorchTrial training throughput (samples/sec, whole node).
 
-    python bench.py --gpus N --steps K --warmup W            # N=1
+    python bench.py --gpus N --steps K --warmup W     # self-launches N ranks (one per GPU)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+Launch (reference: ``harness/determined/horovod.py:124-163`` builds a ``horovodrun -np N``
+command, ``layers/_worker_process.py:165-184`` runs it): when ``--gpus N > 1`` and no launcher
+env is present, this process becomes a pure launcher -- it makes NO GPU call (torch is not even
+imported), spawns N children with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, relays rank 0's JSON
+line and exits with the first failing child's code.  Each child binds ``cuda:<local_rank>`` and
+joins ProcessGroupNCCL (= RCCL over xGMI).  MIOpen's find database is seeded from the tuned copy
+shipped in-tree (``determined_1_amd/ops/miopen_db.py``) so N ranks do not re-tune concurrently.
 
 The step that is timed is the real framework path, not a bare loop: a ``PyTorchTrialController``
 is built exactly as a cluster trial process builds it and fed ``RUN_STEP`` workloads:
@@ -17,11 +25,11 @@ Rank 0 prints ONE JSON line; ``value`` = K * global_batch / max-over-ranks(t1 - 
 import argparse
 import json
 import os
+import signal
+import subprocess
 import sys
 import threading
 import time
-
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -44,19 +52,110 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--no-fused-bn", action="store_true", help="stock MIOpen BN + separate add/ReLU (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
                     help="MIOpen find mode for the conv algorithms (tuned during the untimed warmup)")
+    ap.add_argument("--launch-timeout", type=float, default=float(os.environ.get("DET_BENCH_LAUNCH_TIMEOUT", "0")),
+                    help="self-launch mode: kill all ranks after this many seconds (0 = no limit)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _miopen_db():
+    """``determined_1_amd/ops/miopen_db.py`` loaded by path: importing the package would import
+    torch, and the launcher must stay GPU-free."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "_det_miopen_db", os.path.join(REPO, "determined_1_amd", "ops", "miopen_db.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # type: ignore
+    return mod
+
+
+def self_launch(args: argparse.Namespace) -> int:
+    """Spawn ``args.gpus`` ranks of this script (one process per GPU) and relay rank 0's output.
+
+    The parent never initialises the GPU: it only forks children (no exec of itself), so a
+    child's HIP context is the only one on its device.  Children run in their own process group
+    so a failure (or the launch timeout) tears the whole job down."""
+    miopen_db = _miopen_db()
+    n = args.gpus
+    port = _free_port()
+    base = dict(os.environ)
+    miopen_db.configure(base)
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DET_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+
+    out_lines = []
+
+    def pump() -> None:
+        assert procs[0].stdout is not None
+        for raw in procs[0].stdout:
+            line = raw.decode(errors="replace")
+            out_lines.append(line)
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    deadline = time.time() + args.launch_timeout if args.launch_timeout > 0 else None
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.remove(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in procs:
+                    if q.poll() is None:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+        if deadline is not None and time.time() > deadline and live:
+            print(f"bench.py: launch timeout {args.launch_timeout}s; killing ranks {live}", file=sys.stderr, flush=True)
+            for r in live:
+                try:
+                    os.killpg(procs[r].pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+            rc = rc or 124
+            deadline = None
+        time.sleep(0.2)
+    t.join(timeout=10)
+    return rc
 
 
 def main() -> None:
     args = parse()
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        sys.exit(self_launch(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes", file=sys.stderr)
-            sys.exit(2)
+        print(f"bench.py: launcher started {world} ranks but --gpus is {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if os.environ.get("DET_BENCH_CHILD") != "1":
+        _miopen_db().configure(os.environ)
+    import torch
+
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
     from determined_1_amd import workload
@@ -122,8 +221,12 @@ def main() -> None:
     ctrl = make_controller(ResNetImageNetTrial, config, stream(), trial_seed=1234)
     ctrl.run()
     elapsed = timing["t1"] - timing["t0"]
-    all_elapsed = pdist.allgather_object(elapsed)
-    t = max(all_elapsed)
+    warmup_s = timing["t0"] - t_start
+    import torch.distributed as tdist
+
+    seen = (tdist.get_world_size(), tdist.get_backend()) if tdist.is_initialized() else (1, None)
+    per_rank = pdist.allgather_object((elapsed, warmup_s, seen[0], seen[1]))
+    t = max(e[0] for e in per_rank)
     value = args.steps * gbs / t
     loss = None
     r = timing.get("resp")
@@ -155,6 +258,10 @@ def main() -> None:
                 "bucket_mb": args.bucket_mb,
                 "fused_bn": not args.no_fused_bn,
                 "final_avg_loss": loss,
+                "world_size_seen": [e[2] for e in per_rank],
+                "backend": per_rank[0][3],
+                "warmup_s": round(max(e[1] for e in per_rank), 1),
+                "miopen_find_db": os.environ.get("MIOPEN_USER_DB_PATH"),
             },
         }
         phases = getattr(ctrl, "last_step_timers", None)

@@ -67,6 +67,8 @@ def default_experiment_config(experiment_seed: Optional[int] = None) -> Dict[str
             "tensor_fusion_threshold": 64,
             "tensor_fusion_cycle_time": 5,
             "auto_tune_tensor_fusion": False,
+            "grad_reduction": "fp32_accum",
+            "rccl": {},
         },
         "perform_initial_validation": False,
         "min_checkpoint_period": {"batches": 0},
@@ -282,6 +284,10 @@ def validate_experiment_config(cfg: Dict[str, Any], require_entrypoint: bool = T
     opt = cfg.get("optimizations", {})
     if opt.get("aggregation_frequency", 1) < 1:
         errs.append("aggregation_frequency must be >= 1")
+    if opt.get("grad_reduction", "fp32_accum") not in ("fp32_accum", "allreduce"):
+        errs.append("optimizations.grad_reduction must be fp32_accum or allreduce")
+    if not isinstance(opt.get("rccl", {}) or {}, dict):
+        errs.append("optimizations.rccl must be a mapping")
     if opt.get("mixed_precision", "O0") not in ("O0", "O1", "O2", "O3"):
         errs.append("mixed_precision must be one of O0, O1, O2, O3")
     if cfg.get("scheduling_unit", 100) <= 0:

@@ -101,7 +101,7 @@ def make_local_env(
         test_mode=test_mode,
     )
     dist_cfg = DistributedConfig.from_configs(cfg, world_size=rank.size, num_agents=rank.cross_size)
-    if rank.size <= 1:
+    if rank.size <= 1 and os.environ.get("DET_FORCE_DISTRIBUTED", "0") != "1":
         dist_cfg.use = False
     return env, dist_cfg, rank
 

@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -70,6 +70,8 @@ _SIGNATURES = {
         c_int,
     ),
     "det_scale_cast": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_i64, c_float, c_void_p], c_int),
+    # stream, in, in_dtype, out, out_dtype, rows, n, scale
+    "det_sum_rows": ([c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_i64, c_float], c_int),
     "det_sumsq_num_partials": ([c_i64], c_int),
     "det_sumsq_partials": ([c_void_p, c_void_p, c_int, c_i64, c_void_p], c_int),
     "det_norm_finalize": (

@@ -448,6 +448,35 @@ u8_normalize_kernel(const uint8_t* __restrict__ in, TO* __restrict__ out, int64_
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Shard reduction for the fp32-accumulating gradient reduce-scatter (parallel/ddp.py): after an
+// all-to-all over xGMI each rank holds `rows` low-precision copies of its own 1/rows shard of a
+// gradient bucket, one per peer.  out[i] = scale * sum_r in[r * n + i], accumulated in fp32 and
+// rounded ONCE (a ring all-reduce in bf16 rounds after every hop).  4 elements per lane per
+// row; rows (= world size) is small, so the row loop is fully in registers.
+// ------------------------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(kBlock)
+sum_rows_kernel(const TI* __restrict__ in, TO* __restrict__ out, int rows, int64_t n, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rows; ++r) {
+      float4 v = Vec4<TI>::load(in + r * n, i);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+    Vec4<TO>::store(out, i, acc);
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float acc = 0.f;
+    for (int r = 0; r < rows; ++r) acc += to_f(in[r * n + i]);
+    out[i] = from_f<TO>(acc * scale);
+  }
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -455,7 +484,7 @@ u8_normalize_kernel(const uint8_t* __restrict__ in, TO* __restrict__ out, int64_
 // ============================================================================================
 extern "C" {
 
-int det_abi_version() { return 6; }
+int det_abi_version() { return 7; }
 
 int det_sgd_step(void* stream, int g_dtype, int out_dtype, float* p, const void* g, float* buf,
                  void* out_model, int64_t n, float lr, float momentum, float dampening, float wd,
@@ -528,6 +557,28 @@ int det_scale_cast(void* stream, const void* in, int in_dtype, void* out, int ou
   else { DET_SC_OUT(__half) }
 #undef DET_SC_OUT
 #undef DET_SC
+  return static_cast<int>(hipGetLastError());
+}
+
+// out[0:n] = scale * sum_{r<rows} in[r*n : (r+1)*n]  (fp32 accumulation).  n % 4 == 0 is the
+// fast path; `in` rows must be 8-byte aligned for 16-bit types (callers pass arena slices).
+int det_sum_rows(void* stream, const void* in, int in_dtype, void* out, int out_dtype, int rows,
+                 int64_t n, float scale) {
+  if (n <= 0 || rows <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  int grid = grid_for((n + 3) / 4);
+#define DET_SR(TI, TO)                                                                       \
+  hipLaunchKernelGGL((sum_rows_kernel<TI, TO>), dim3(grid), dim3(kBlock), 0, st,              \
+                     static_cast<const TI*>(in), static_cast<TO*>(out), rows, n, scale)
+#define DET_SR_OUT(TI)                          \
+  if (out_dtype == kF32) DET_SR(TI, float);     \
+  else if (out_dtype == kBF16) DET_SR(TI, __hip_bfloat16); \
+  else DET_SR(TI, __half);
+  if (in_dtype == kF32) { DET_SR_OUT(float) }
+  else if (in_dtype == kBF16) { DET_SR_OUT(__hip_bfloat16) }
+  else { DET_SR_OUT(__half) }
+#undef DET_SR_OUT
+#undef DET_SR
   return static_cast<int>(hipGetLastError());
 }
 

@@ -36,6 +36,26 @@ def is_gpu(t: torch.Tensor) -> bool:
 # ----------------------------------------------------------------------------------------------
 # scale / cast
 # ----------------------------------------------------------------------------------------------
+def sum_rows_(src: torch.Tensor, rows: int, dst: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+    """dst[:] = scale * src.view(rows, -1).sum(0) with fp32 accumulation and one final rounding
+    (the shard reduction of the fp32-accumulating gradient reduce-scatter, ``parallel/ddp.py``)."""
+    n = dst.numel()
+    assert src.numel() == rows * n, (src.shape, rows, dst.shape)
+    assert src.is_contiguous() and dst.is_contiguous()
+    if is_gpu(src):
+        _lib.check(
+            _lib.get_lib().det_sum_rows(_stream_ptr(src), src.data_ptr(), dtype_code(src.dtype), dst.data_ptr(),
+                                        dtype_code(dst.dtype), int(rows), n, float(scale)),
+            "sum_rows",
+        )
+    else:
+        s = src.view(rows, n).float().sum(0)
+        if scale != 1.0:
+            s = s * scale
+        dst.copy_(s.view_as(dst))
+    return dst
+
+
 def scale_cast_(
     src: torch.Tensor,
     dst: torch.Tensor,

@@ -1,0 +1,96 @@
+"""Persistent MIOpen find/perf database and kernel cache for the conv layers MIOpen still runs.
+
+Problem: with ``torch.backends.cudnn.benchmark`` on, MIOpen "find" times every applicable solver
+for every conv problem on first use and JIT-compiles the HIP/CK kernels it tries.  On a fresh
+MI355X box there is no gfx950 system find-db in ``/opt/rocm/share/miopen/db``, so a ResNet-50 run
+spent ~360 s of warmup tuning (BENCH_r01.json), and N ranks of one job would each tune the same
+problems concurrently against one user db.
+
+Fix (MI355X-first, no reference counterpart -- the reference runs cuDNN/Horovod images):
+  * the user find-db / perf-db that a tuning run wrote is shipped IN-TREE under
+    ``determined_1_amd/ops/miopen_db/`` (text files keyed by problem + ``gfx950_256``);
+  * ``configure(env)`` points ``MIOPEN_USER_DB_PATH`` / ``MIOPEN_CUSTOM_CACHE_DIR`` at a writable
+    per-user copy under ``$TMPDIR`` seeded from the shipped files, before any process touches the
+    GPU, so every rank (and every trial container) gets find results from the db instead of
+    re-tuning; only the kernels MIOpen actually picked are compiled (or loaded from the seeded
+    kernel cache);
+  * ``harvest(dst)`` copies a run's db back so a tuning run can refresh the shipped copy.
+
+This module deliberately imports nothing from torch or the package: launchers call it before
+deciding which process owns which GPU.
+"""
+import os
+import shutil
+from typing import MutableMapping, Optional
+
+SHIPPED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
+
+
+def _copy_tree_missing(src: str, dst: str) -> int:
+    """Copy files from ``src`` into ``dst`` that are missing or smaller there; returns count."""
+    n = 0
+    if not os.path.isdir(src):
+        return 0
+    for root, _, files in os.walk(src):
+        rel = os.path.relpath(root, src)
+        out = os.path.join(dst, rel) if rel != "." else dst
+        os.makedirs(out, exist_ok=True)
+        for f in files:
+            if f.startswith(".") or f.endswith(".md"):
+                continue
+            s = os.path.join(root, f)
+            d = os.path.join(out, f)
+            try:
+                if not os.path.exists(d) or os.path.getsize(d) < os.path.getsize(s):
+                    tmp = d + ".tmp%d" % os.getpid()
+                    shutil.copyfile(s, tmp)
+                    os.replace(tmp, d)
+                    n += 1
+            except OSError:
+                continue
+    return n
+
+
+def run_root(env: Optional[MutableMapping[str, str]] = None) -> str:
+    e = os.environ if env is None else env
+    base = e.get("DET_MIOPEN_DIR") or os.path.join(e.get("TMPDIR", "/tmp"), "det-miopen-%d" % os.getuid())
+    return base
+
+
+def configure(env: Optional[MutableMapping[str, str]] = None) -> Optional[str]:
+    """Seed and select the MIOpen user db + kernel cache for processes started with ``env``.
+
+    Respects an explicit ``MIOPEN_USER_DB_PATH`` (a user-chosen db is left alone) and
+    ``DET_MIOPEN_DB=0`` (disable).  Returns the user-db directory in use."""
+    e = os.environ if env is None else env
+    if e.get("DET_MIOPEN_DB", "1") == "0":
+        return e.get("MIOPEN_USER_DB_PATH")
+    if e.get("MIOPEN_USER_DB_PATH"):
+        return e["MIOPEN_USER_DB_PATH"]
+    root = run_root(e)
+    db = os.path.join(root, "db")
+    cache = os.path.join(root, "cache")
+    try:
+        os.makedirs(db, exist_ok=True)
+        os.makedirs(cache, exist_ok=True)
+        _copy_tree_missing(os.path.join(SHIPPED, "db"), db)
+        _copy_tree_missing(os.path.join(SHIPPED, "cache"), cache)
+    except OSError:
+        return None
+    e["MIOPEN_USER_DB_PATH"] = db
+    e.setdefault("MIOPEN_CUSTOM_CACHE_DIR", cache)
+    return db
+
+
+def harvest(dst: str, env: Optional[MutableMapping[str, str]] = None, with_cache: bool = False) -> int:
+    """Copy the active user db (and optionally the kernel cache) to ``dst`` (e.g. to refresh
+    ``SHIPPED`` after a tuning run)."""
+    e = os.environ if env is None else env
+    n = 0
+    db = e.get("MIOPEN_USER_DB_PATH")
+    if db:
+        n += _copy_tree_missing(db, os.path.join(dst, "db"))
+    cache = e.get("MIOPEN_CUSTOM_CACHE_DIR")
+    if with_cache and cache:
+        n += _copy_tree_missing(cache, os.path.join(dst, "cache"))
+    return n

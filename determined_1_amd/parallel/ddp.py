@@ -1,40 +1,64 @@
-"""Bucketed, backward-overlapped gradient all-reduce over RCCL/xGMI on flat arenas.
+"""Bucketed, backward-overlapped gradient reduction over RCCL/xGMI on flat arenas.
 
 Replaces ``hvd.DistributedOptimizer`` (reference ``_pytorch_context.py:152-204``; SURVEY C-1).
 
 Design (MI355X-first, not a translation of Horovod's per-tensor async + 5 ms fusion cycle):
   * gradients already live in contiguous arenas (``ops/arena.py``) laid out in reverse
     registration order, so a bucket is a *slice* of ``flat_grad`` -- no pack/unpack copies;
-  * a ``post_accumulate_grad`` hook per parameter counts down its bucket; when a bucket is
-    complete it is all-reduced immediately (``async_op=True``), in strict bucket order so every
-    rank issues identical collective sequences (buckets that complete out of order wait for their
-    predecessors);
-  * RCCL runs on its own HIP stream (ProcessGroupNCCL's internal stream, event-synchronised with
-    the compute stream), so the all-reduce of bucket k overlaps the backward of layers < k;
-  * SUM (not AVG) is used: the 1/world_size (and 1/aggregation_frequency, AMP 1/loss_scale)
-    factors are folded into the fused optimizer's single gradient read (``ops/optim.py``);
-  * optional compression casts each bucket to bf16 (MI355X-native; fp16 also accepted) with the
-    ``det_scale_cast`` kernel before the collective and back after it;
-  * bucket size comes from ``optimizations.tensor_fusion_threshold`` (MB, default 64, as the
-    reference).  On an 8x MI355X node each GPU has 7 xGMI links (~153 GB/s each); a 64 MB ring
-    all-reduce moves ~2*(7/8)*64 MB per GPU which keeps every link busy for ~0.1 ms+, well above
-    the per-collective launch/latency floor, while the smaller first bucket starts communication
-    early in backward.
+  * a bucket-complete notification (GradSink flush or per-parameter hook) launches the bucket's
+    collective immediately, in strict bucket order so every rank issues identical collective
+    sequences (buckets that complete out of order wait for their predecessors);
+  * RCCL runs on ProcessGroupNCCL's own HIP stream (event-synchronised with the compute stream),
+    so the reduction of bucket k overlaps the backward of layers < k;
+  * SUM is used: the 1/world_size (and 1/aggregation_frequency, AMP 1/loss_scale) factors are
+    folded into the fused optimizer's single gradient read (``ops/optim.py``).
+
+Bucket plan (``plan_buckets``): the cap is ``min(tensor_fusion_threshold, grad_bytes / 8)``
+clamped to [2 MB, threshold] -- about eight buckets per model.  On an 8x MI355X node each GPU
+has 7 point-to-point xGMI links; a few-MB bucket already keeps them busy far above the ~20-40 us
+per-collective floor, while small buckets let communication start early in backward.  Planning
+runs from the arena TAIL (the first layers, whose gradients arrive last) with a quarter-size
+tail bucket, so the one collective that cannot overlap anything is short.
+
+Reduction of 16-bit buckets (bf16 O2 arenas, or any arena with gradient compression) defaults to
+``fp32_accum``: a ring all-reduce in bf16 rounds after every hop, so an 8-rank sum carries up to
+7 roundings.  Instead each bucket is reduce-scattered as an **all-to-all** over the xGMI mesh
+(every rank sends shard j straight to rank j -- on a fully connected node that drives all 7
+links at once, no hop-by-hop arithmetic), each rank sums its N received copies in fp32 with the
+``det_sum_rows`` HIP kernel (ONE rounding), and an in-place all-gather returns the reduced
+bucket.  Bytes on the wire equal a ring all-reduce: 2 (N-1)/N x bucket.  ``grad_reduction:
+allreduce`` selects the plain RCCL all-reduce instead.  fp32 buckets always use the RCCL
+all-reduce.
+
+RCCL knobs (the analogue of Horovod's fusion/cycle knobs, reference ``horovod.py:92-110``) come
+from ``optimizations.rccl`` and are applied as NCCL_* environment before the communicator is
+created (``apply_rccl_env``).
 """
 import logging
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+import os
+from typing import Any, Dict, List, MutableMapping, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
 from determined_1_amd.ops.arena import Arena
-from determined_1_amd.ops.functional import scale_cast_
+from determined_1_amd.ops.functional import scale_cast_, sum_rows_
 
-FIRST_BUCKET_BYTES = 4 * 1024 * 1024
+MB = 1024 * 1024
+MIN_BUCKET_BYTES = 2 * MB
+TARGET_BUCKETS = 8
+REDUCTIONS = ("fp32_accum", "allreduce")
+
+
+def auto_bucket_cap(total_bytes: int, threshold_bytes: int) -> int:
+    """Per-bucket byte cap: ~TARGET_BUCKETS buckets, never below 2 MB, never above the
+    configured ``tensor_fusion_threshold``."""
+    cap = max(MIN_BUCKET_BYTES, total_bytes // TARGET_BUCKETS)
+    return int(min(threshold_bytes, cap))
 
 
 class _Bucket:
-    __slots__ = ("arena", "lo", "hi", "params", "comp", "work")
+    __slots__ = ("arena", "lo", "hi", "params", "comp", "recv", "work", "mode")
 
     def __init__(self, arena: Arena, lo: int, hi: int, params: List[int]) -> None:
         self.arena = arena
@@ -42,34 +66,69 @@ class _Bucket:
         self.hi = hi
         self.params = params
         self.comp = None  # type: Optional[torch.Tensor]
+        self.recv = None  # type: Optional[torch.Tensor]
         self.work = None  # type: Any
+        self.mode = "allreduce"
 
     @property
     def grad(self) -> torch.Tensor:
         return self.arena.flat_grad[self.lo:self.hi]
 
+    @property
+    def nbytes(self) -> int:
+        return (self.hi - self.lo) * self.arena.flat_grad.element_size()
 
-def plan_buckets(arenas: Sequence[Arena], cap_bytes: int, first_bytes: int = FIRST_BUCKET_BYTES) -> List[_Bucket]:
-    """Split each arena into contiguous buckets at parameter boundaries."""
-    buckets = []  # type: List[_Bucket]
+
+def plan_buckets(arenas: Sequence[Arena], cap_bytes: int, tail_bytes: Optional[int] = None) -> List[_Bucket]:
+    """Split each arena into contiguous buckets at parameter boundaries.
+
+    Buckets are cut from the END of each arena (the earliest layers, whose gradients are produced
+    last): the first cut uses ``tail_bytes`` (default cap/4), the rest ``cap_bytes``.  The list
+    is returned in arena order, i.e. the order in which backward completes them."""
+    if tail_bytes is None:
+        tail_bytes = max(cap_bytes // 4, 1)
+    out = []  # type: List[_Bucket]
     for a in arenas:
         es = a.flat_grad.element_size()
-        start = 0
-        cur = []  # type: List[int]
-        limit = min(first_bytes, cap_bytes) if not buckets else cap_bytes
-        for i in range(len(a.params)):
-            cur.append(i)
-            lo = a.offsets[start]
-            hi = a.offsets[i + 1] if i + 1 < len(a.params) else a.numel
-            if (hi - lo) * es >= limit:
-                buckets.append(_Bucket(a, lo, hi, cur))
-                cur = []
-                start = i + 1
+        n = len(a.params)
+        cuts = []  # type: List[Tuple[int, int]]  # [first_param, last_param] inclusive, reversed
+        end = n - 1
+        limit = tail_bytes
+        i = n - 1
+        while i >= 0:
+            lo = a.offsets[i]
+            hi = a.offsets[end + 1] if end + 1 < n else a.numel
+            if (hi - lo) * es >= limit or i == 0:
+                cuts.append((i, end))
+                end = i - 1
                 limit = cap_bytes
-        if cur:
-            lo = a.offsets[start]
-            buckets.append(_Bucket(a, lo, a.numel, cur))
-    return buckets
+            i -= 1
+        for first, last in reversed(cuts):
+            lo = a.offsets[first]
+            hi = a.offsets[last + 1] if last + 1 < n else a.numel
+            out.append(_Bucket(a, lo, hi, list(range(first, last + 1))))
+    return out
+
+
+def apply_rccl_env(opt: Dict[str, Any], env: Optional[MutableMapping[str, str]] = None) -> Dict[str, str]:
+    """Translate ``optimizations.rccl`` into NCCL_* variables (RCCL reads them at communicator
+    creation, so call before ``init_process_group``).  Explicit environment wins.
+
+    Keys: ``algo`` (Ring/Tree), ``protocol`` (Simple/LL/LL128), ``min_channels``,
+    ``max_channels``, ``buffsize`` (bytes)."""
+    e = os.environ if env is None else env
+    r = (opt or {}).get("rccl") or {}
+    mapping = {"algo": "NCCL_ALGO", "protocol": "NCCL_PROTO", "min_channels": "NCCL_MIN_NCHANNELS",
+               "max_channels": "NCCL_MAX_NCHANNELS", "buffsize": "NCCL_BUFFSIZE"}
+    applied = {}
+    for k, var in mapping.items():
+        v = r.get(k)
+        if v in (None, "", 0):
+            continue
+        if var not in e:
+            e[var] = str(v)
+            applied[var] = str(v)
+    return applied
 
 
 class GradientBucketer:
@@ -80,18 +139,28 @@ class GradientBucketer:
         cap_mb: float = 64.0,
         compression: Optional[torch.dtype] = None,
         group: Any = None,
+        reduction: str = "fp32_accum",
+        rank: Optional[int] = None,
     ) -> None:
+        if reduction not in REDUCTIONS:
+            raise ValueError(f"grad_reduction must be one of {REDUCTIONS}, got {reduction!r}")
         self.arenas = list(arenas)
         self.world_size = world_size
+        self.rank = dist.get_rank(group) if rank is None and dist.is_initialized() else (rank or 0)
         self.group = group
         self.compression = compression
-        self.buckets = plan_buckets(self.arenas, int(cap_mb * 1024 * 1024))
-        self._bucket_of = {}  # type: Dict[int, int]
-        for bi, b in enumerate(self.buckets):
-            for pi in b.params:
-                self._bucket_of[id(b.arena.params[pi])] = bi
+        total = sum(a.numel * a.flat_grad.element_size() for a in self.arenas)
+        self.cap_bytes = auto_bucket_cap(total, int(cap_mb * MB))
+        self.buckets = plan_buckets(self.arenas, self.cap_bytes)
+        self._side = None  # type: Any
+        for b in self.buckets:
             if compression is not None:
                 b.comp = torch.empty(b.hi - b.lo, dtype=compression, device=b.arena.device)
+            wire_dtype = compression if compression is not None else b.arena.flat_grad.dtype
+            n = b.hi - b.lo
+            if reduction == "fp32_accum" and wire_dtype in (torch.bfloat16, torch.float16) and n % world_size == 0:
+                b.mode = "fp32_accum"
+                b.recv = torch.empty(n, dtype=wire_dtype, device=b.arena.device)
         self._pending = [0] * len(self.buckets)
         self._ready = [False] * len(self.buckets)
         self._next = 0
@@ -99,11 +168,19 @@ class GradientBucketer:
         self._launched_any = False
         self._handles = []
         self._sink = None  # type: Any
+        self._bucket_of = {}  # type: Dict[int, int]
+        for bi, b in enumerate(self.buckets):
+            for pi in b.params:
+                self._bucket_of[id(b.arena.params[pi])] = bi
         for a in self.arenas:
             for p in a.params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
-        logging.debug("gradient bucketer: %d buckets (%s MB cap), compression=%s", len(self.buckets), cap_mb,
-                      compression)
+        logging.info("gradient bucketer: %d buckets (cap %.1f MB of %.1f MB), reduction=%s, compression=%s",
+                     len(self.buckets), self.cap_bytes / MB, total / MB,
+                     sorted({b.mode for b in self.buckets}), compression)
+
+    def describe(self) -> List[Dict[str, Any]]:
+        return [{"params": len(b.params), "mb": round(b.nbytes / MB, 3), "mode": b.mode} for b in self.buckets]
 
     def attach_sink(self, sink: Any) -> None:
         """Gradients land through ``ops.arena.GradSink`` (one batched copy per bucket): on fresh
@@ -125,7 +202,7 @@ class GradientBucketer:
     # ------------------------------------------------------------------------------------------
     def prepare_backward(self, communicate: bool) -> None:
         """Called before every backward pass; ``communicate`` says whether this pass ends an
-        aggregation window (then buckets all-reduce as they complete)."""
+        aggregation window (then buckets are reduced as they complete)."""
         self._comm = communicate
         if self._comm:
             for bi, b in enumerate(self.buckets):
@@ -149,17 +226,40 @@ class GradientBucketer:
             self._launch(self.buckets[self._next])
             self._next += 1
 
+    def _side_stream(self, device: torch.device) -> Any:
+        if self._side is None and device.type == "cuda":
+            self._side = torch.cuda.Stream(device=device, priority=-1)
+        return self._side
+
     def _launch(self, b: _Bucket) -> None:
-        buf = b.grad
+        wire = b.grad
         if b.comp is not None:
-            scale_cast_(buf, b.comp)
-            buf = b.comp
-        b.work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            scale_cast_(wire, b.comp)
+            wire = b.comp
+        if b.mode == "allreduce":
+            b.work = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            assert b.recv is not None
+            n = wire.numel() // self.world_size
+            shard = wire[self.rank * n:(self.rank + 1) * n]
+            w1 = dist.all_to_all_single(b.recv, wire, group=self.group, async_op=True)
+            side = self._side_stream(wire.device)
+            if side is None:  # CPU / gloo: blocking semantics
+                w1.wait()
+                sum_rows_(b.recv, self.world_size, shard)
+                b.work = dist.all_gather_into_tensor(wire, shard, group=self.group, async_op=True)
+            else:
+                # Reduce on a side stream that waits only for the all-to-all, so the compute
+                # stream (backward of earlier layers) never stalls on communication.
+                with torch.cuda.stream(side):
+                    w1.wait()
+                    sum_rows_(b.recv, self.world_size, shard)
+                    b.work = dist.all_gather_into_tensor(wire, shard, group=self.group, async_op=True)
         self._launched_any = True
 
     def synchronize(self) -> bool:
         """Launch any bucket not yet launched (unused parameters), then make the current stream
-        wait for every all-reduce.  Returns True if a communication round happened."""
+        wait for every reduction.  Returns True if a communication round happened."""
         if not self._comm:
             return False
         for bi in range(len(self.buckets)):
@@ -171,6 +271,8 @@ class GradientBucketer:
                 b.work = None
                 if b.comp is not None:
                     scale_cast_(b.comp, b.grad)
+        if self._side is not None:
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         self._comm = False
         return True
 

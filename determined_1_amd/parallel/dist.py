@@ -40,6 +40,8 @@ class DistributedConfig:
         cycle_time_ms: int = 5,
         auto_tune: bool = False,
         compression_dtype: str = "bfloat16",
+        grad_reduction: str = "fp32_accum",
+        rccl: Optional[Dict[str, Any]] = None,
     ) -> None:
         self.use = use
         self.aggregation_frequency = max(1, int(aggregation_frequency))
@@ -50,6 +52,8 @@ class DistributedConfig:
         self.cycle_time_ms = cycle_time_ms
         self.auto_tune = auto_tune
         self.compression_dtype = compression_dtype
+        self.grad_reduction = grad_reduction
+        self.rccl = dict(rccl or {})
 
     # reference attribute name used by user code
     @property
@@ -65,6 +69,10 @@ class DistributedConfig:
         multi_machine = num_agents > 1
         multi_slot = slots > 1 or world_size > 1
         use = multi_machine or (multi_slot and not native_parallel)
+        # DET_FORCE_DISTRIBUTED=1: run the multi-process path (process groups, bucketer,
+        # broadcasts) even with one rank -- exercises RCCL on a one-GPU box.
+        if os.environ.get("DET_FORCE_DISTRIBUTED", "0") == "1":
+            use = True
         return DistributedConfig(
             use=use,
             aggregation_frequency=int(opt.get("aggregation_frequency", 1)),
@@ -74,6 +82,9 @@ class DistributedConfig:
             fusion_threshold_mb=int(opt.get("tensor_fusion_threshold", 64)),
             cycle_time_ms=int(opt.get("tensor_fusion_cycle_time", 5)),
             auto_tune=bool(opt.get("auto_tune_tensor_fusion", False)),
+            compression_dtype=str(opt.get("gradient_compression_dtype", "bfloat16")),
+            grad_reduction=str(opt.get("grad_reduction", "fp32_accum")),
+            rccl=opt.get("rccl") or {},
         )
 
     @staticmethod

@@ -213,6 +213,7 @@ class PyTorchTrialContext(trial.TrialContext):
                         world_size=self.distributed.get_size(),
                         cap_mb=self.dist_config.fusion_threshold_mb,
                         compression=comp,
+                        reduction=getattr(self.dist_config, "grad_reduction", "fp32_accum"),
                     )
             if st.fused is not None and st.fused.arenas and self._grad_sink:
                 if st.bucketer is not None:

@@ -74,6 +74,9 @@ class PyTorchTrialController(trial.LoopTrialController):
                 if torch.cuda.is_available() else torch.device("cpu")
             if device.type == "cuda":
                 torch.cuda.set_device(device)
+                from determined_1_amd.parallel.ddp import apply_rccl_env
+
+                apply_rccl_env({"rccl": getattr(dist_config, "rccl", {})})
             pdist.init_process_groups(device)
         PyTorchTrialController._set_random_seeds(env.trial_seed)
         # One process drives one GPU here, so autograd's per-device worker thread only adds a

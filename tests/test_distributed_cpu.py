@@ -80,3 +80,28 @@ def test_bench_two_ranks_gloo_smoke(tmp_path):
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
+
+
+def test_bench_self_launch_plain_invocation():
+    """``python bench.py --gpus 2`` with no launcher env: bench.py spawns its own 2 ranks (the
+    driver's SCALE invocation), joins them over gloo on CPU and prints one JSON line."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--arch", "resnet18", "--batch-per-gpu", "2", "--image-size", "32", "--amp", "O0"],
+                       capture_output=True, text=True, timeout=600, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["world_size_seen"] == [2, 2] and out["config"]["backend"] == "gloo"
+    assert out["config"]["warmup_s"] >= 0 and out["value"] > 0
+
+
+def test_bench_rejects_mismatched_world():
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert r.returncode == 2 and "--gpus is 2" in r.stderr

@@ -142,3 +142,15 @@ def test_u8_normalize(gpu, out_dt):
     assert got.is_contiguous(memory_format=torch.channels_last)
     tol = dict(rtol=1e-2, atol=1e-2) if out_dt == torch.bfloat16 else dict(rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(got.float().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("rows,n", [(1, 4096), (8, 1_000_003), (3, 6), (8, 2 ** 20)])
+@pytest.mark.parametrize("src_dt,dst_dt", [(torch.bfloat16, torch.bfloat16), (torch.float16, torch.float16),
+                                           (torch.bfloat16, torch.float32), (torch.float32, torch.float32)])
+def test_sum_rows_fp32_accumulation(gpu, rows, n, src_dt, dst_dt):
+    """det_sum_rows vs the fp32 reference: one rounding of the fp32 sum of the rows."""
+    x = (torch.randn(rows * n, device=gpu) * 3).to(src_dt)
+    y = torch.empty(n, device=gpu, dtype=dst_dt)
+    F.sum_rows_(x, rows, y, scale=0.5)
+    ref = (x.float().cpu().view(rows, n).sum(0) * 0.5).to(dst_dt)
+    torch.testing.assert_close(y.cpu(), ref, rtol=1e-6 if dst_dt == torch.float32 else 0, atol=1e-5 if dst_dt == torch.float32 else 0)
