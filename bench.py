@@ -197,8 +197,14 @@ def main() -> None:
         def keep(r):
             resp["last"] = r
 
-        if args.warmup > 0:
-            yield workload.train_workload(1, num_batches=args.warmup, total_batches_processed=0), [], keep
+        # warmup one batch per workload so the time to each completed batch is visible (MIOpen
+        # find/compile cost lands in the first batches; the rest is steady state)
+        for i in range(args.warmup):
+            yield workload.train_workload(1, num_batches=1, total_batches_processed=i), [], keep
+            timing.setdefault("warm", []).append(round(time.perf_counter() - t_start, 2))
+            if rank == 0:
+                print(f"[bench rank0] warmup batch {i + 1}/{args.warmup} done at {timing['warm'][-1]:.1f}s",
+                      file=sys.stderr, flush=True)
         sync_barrier()
         timing["t0"] = time.perf_counter()
         yield workload.train_workload(2, num_batches=args.steps, total_batches_processed=args.warmup), [], keep
@@ -219,6 +225,7 @@ def main() -> None:
 
     threading.Thread(target=heartbeat, daemon=True).start()
     ctrl = make_controller(ResNetImageNetTrial, config, stream(), trial_seed=1234)
+    timing["ctrl_built"] = time.perf_counter()
     ctrl.run()
     elapsed = timing["t1"] - timing["t0"]
     warmup_s = timing["t0"] - t_start
@@ -261,6 +268,8 @@ def main() -> None:
                 "world_size_seen": [e[2] for e in per_rank],
                 "backend": per_rank[0][3],
                 "warmup_s": round(max(e[1] for e in per_rank), 1),
+                "warmup_batch_done_s": timing.get("warm"),
+                "startup_s": round(timing.get("ctrl_built", 0.0) - t_start, 1),
                 "miopen_find_db": os.environ.get("MIOPEN_USER_DB_PATH"),
             },
         }

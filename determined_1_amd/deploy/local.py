@@ -16,6 +16,12 @@ NATIVE_DIR = pathlib.Path(__file__).resolve().parent.parent / "_native"
 
 
 def native_binary(name: str) -> str:
+    override = os.environ.get("DET_NATIVE_BIN_DIR")  # e.g. native/build-address/bin (sanitizer builds)
+    if override:
+        p = pathlib.Path(override) / name
+        if not p.exists():
+            raise FileNotFoundError(f"{p} missing (DET_NATIVE_BIN_DIR={override})")
+        return str(p)
     p = NATIVE_DIR / name
     if not p.exists():
         from determined_1_amd.native_build import build_native
@@ -79,7 +85,7 @@ class LocalCluster:
         log = open(os.path.join(self.log_dir, f"agent-{i}.log"), "ab")
         args = [native_binary("det-agent"), "--master-host", "127.0.0.1", "--master-port", str(self.port),
                 "--agent-id", f"agent-{i}", "--work-dir", os.path.join(self.work_dir, f"agent-{i}"),
-                "--python", sys.executable]
+                "--python", sys.executable, "--framework-root", str(NATIVE_DIR.parent.parent)]
         if self.slots_per_agent > 0 and not self.gpu:
             args += ["--artificial-slots", str(self.slots_per_agent)]
         elif self.gpu:

@@ -14,6 +14,7 @@
 
 #include <any>
 #include <chrono>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -163,7 +164,7 @@ class System {
   std::map<std::string, std::weak_ptr<Cell>> registry_;
   std::map<std::string, Ref> roots_;
   std::vector<std::thread> workers_;
-  bool shutdown_ = false;
+  std::atomic<bool> shutdown_{false};  // written under mu_, read under tmu_ by TimerLoop
 
   struct Timer {
     std::chrono::steady_clock::time_point at;

@@ -29,6 +29,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <utility>
 #include <thread>
 #include <vector>
 
@@ -290,7 +291,7 @@ class Agent {
     for (auto& d : m["devices"].as_array()) {
       int id = static_cast<int>(d.as_int());
       slot_ids.push_back(id);
-      for (auto& dev : devices_.as_array())
+      for (const auto& dev : std::as_const(devices_).as_array())  // const: no COW detach (Start runs per container thread)
         if (dev.get_int("id", -1) == id && dev.get_string("type", "") == "gpu") {
           gpu = true;
           hip += (hip.empty() ? "" : ",") + std::to_string(id);
