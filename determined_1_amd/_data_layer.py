@@ -13,11 +13,21 @@ the columns instead of re-running the (usually expensive) decode/pre-processing.
 
 The writer holds an exclusive lock and readers a shared one: through the master's RW coordinator
 (WS ``/ws/data-layer/*``, ``native/src/rw_coordinator.cc``) when the trial runs under a master, and
-an ``fcntl`` file lock in local mode.  The decorated function returns a :class:`CachedStream`, an
-``IterableDataset`` that shards (``rank::size``), shuffles with the trial seed (reshuffled per
-epoch unless ``skip_shuffle_at_epoch_end``) and starts at ``total_batches_processed * per_slot``
-samples into the stream, so a resumed trial continues where its checkpoint left off.  Training
-streams repeat forever; validation streams are one pass without dropping the shard remainder.
+an ``fcntl`` file lock in local mode.
+
+Exactly ONE layer owns sharding, shuffling and resume, depending on who consumes the data:
+  * PyTorchTrial (``map_style=True``, what ``PyTorchTrialContext.experimental`` uses): the decorated
+    function returns the map-style :class:`CachedDataset`.  The user wraps it in
+    ``det.pytorch.DataLoader`` as with any dataset, and the controller's sampler stack
+    (Repeat -> DistributedBatchSampler -> SkipBatchSampler, ``pytorch/_data.py``) shards it and
+    skips the batches a restored trial already trained on.  ``shuffle=True`` applies one fixed
+    permutation seeded by the trial seed (``skip_shuffle_at_epoch_end`` semantics); per-epoch
+    reshuffling is ``DataLoader(shuffle=True)``'s job, as for any map-style dataset.
+  * other consumers (native loops, ``map_style=False``): a :class:`CachedStream`, an
+    ``IterableDataset`` that shards (``rank::size``), shuffles with the trial seed (reshuffled per
+    epoch unless ``skip_shuffle_at_epoch_end``) and starts ``total_batches_processed * per_slot``
+    samples in, so a resumed trial continues where its checkpoint left off.  Training streams repeat
+    forever; validation streams are one pass without dropping the shard remainder.
 """
 import contextlib
 import fcntl
@@ -37,9 +47,9 @@ SUPPORTED_TYPES = ("shared_fs",)
 
 
 def init_container_storage_path(configured: Optional[str]) -> pathlib.Path:
-    """Reference ``_data_layer.py:17-24``: default ``/determined_local_fs/data_layer_storage``,
-    falling back to a per-user temp dir where that is not writable."""
-    path = pathlib.Path(configured) if configured else pathlib.Path("/determined_local_fs/data_layer_storage")
+    """Reference ``_data_layer.py:17-24``: the configured path, default ``~/data/determined``; falls
+    back to a per-user temp dir where that is not writable."""
+    path = pathlib.Path(configured) if configured else pathlib.Path.home().joinpath("data/determined")
     try:
         path.mkdir(parents=True, exist_ok=True)
         if not os.access(path, os.W_OK):
@@ -63,6 +73,19 @@ def _flatten(sample: Any):
     if isinstance(sample, (tuple, list)):
         return "tuple", None, [_to_numpy(v) for v in sample]
     return "single", None, [_to_numpy(sample)]
+
+
+def remove_stale_temp_dirs(path: pathlib.Path) -> int:
+    """Delete ``.tmp_*`` siblings a killed writer left next to ``path`` (call under the write lock)."""
+    n = 0
+    parent = path.parent
+    if not parent.is_dir():
+        return 0
+    for p in parent.iterdir():
+        if p.name.startswith(".tmp_") and p.is_dir():
+            shutil.rmtree(str(p), ignore_errors=True)
+            n += 1
+    return n
 
 
 def write_cache(dataset: Any, path: pathlib.Path) -> None:
@@ -92,12 +115,14 @@ def write_cache(dataset: Any, path: pathlib.Path) -> None:
 
 
 class CachedDataset(torch.utils.data.Dataset):
-    """Random access over a written cache (memory-mapped columns)."""
+    """Random access over a written cache (memory-mapped columns).  ``order`` (optional) is a fixed
+    index permutation applied to ``__getitem__`` (the decorator's ``shuffle=True`` in map style)."""
 
-    def __init__(self, path: pathlib.Path) -> None:
+    def __init__(self, path: pathlib.Path, order: Optional[np.ndarray] = None) -> None:
         self.path = path
         self.meta = json.loads((path / "meta.json").read_text())
         self._cols: Optional[List[np.ndarray]] = None
+        self.order = order
 
     def _columns(self) -> List[np.ndarray]:
         if self._cols is None:  # opened lazily so DataLoader workers map the file themselves
@@ -106,12 +131,14 @@ class CachedDataset(torch.utils.data.Dataset):
         return self._cols
 
     def __getstate__(self) -> Dict[str, Any]:
-        return {"path": self.path, "meta": self.meta, "_cols": None}
+        return {"path": self.path, "meta": self.meta, "_cols": None, "order": self.order}
 
     def __len__(self) -> int:
         return int(self.meta["length"])
 
     def __getitem__(self, i: int) -> Any:
+        if self.order is not None:
+            i = int(self.order[i])
         vals = [torch.from_numpy(np.array(c[i])) for c in self._columns()]
         if self.meta["kind"] == "dict":
             return dict(zip(self.meta["keys"], vals))
@@ -168,8 +195,9 @@ class CachedStream(torch.utils.data.IterableDataset):
 
 
 class _CacheableDecorator:
-    def __init__(self, env: Any, rank: int, size: int, training: bool, managed: bool) -> None:
+    def __init__(self, env: Any, rank: int, size: int, training: bool, managed: bool, map_style: bool = False) -> None:
         self._env = env
+        self._map_style = map_style
         self._rank, self._size = (rank, size)
         self._training = training
         self._managed = managed
@@ -224,14 +252,24 @@ class _CacheableDecorator:
 
         def _wrap(make_dataset_fn: Callable) -> Callable:
             @functools.wraps(make_dataset_fn)
-            def _decorated(*args: Any, **kwargs: Any) -> CachedStream:
+            def _decorated(*args: Any, **kwargs: Any) -> Any:
                 with self._lock(path, read=True):
                     hit = (path / "meta.json").exists()
                 if not hit:
                     with self._lock(path, read=False):
                         if not (path / "meta.json").exists():
+                            stale = remove_stale_temp_dirs(path)
+                            if stale:
+                                logging.info(f"removed {stale} partial cache dir(s) of a killed writer")
                             logging.info(f"Caching dataset {dataset_id}:{version} to {path}.")
                             write_cache(make_dataset_fn(*args, **kwargs), path)
+                if self._map_style:
+                    data = CachedDataset(path)
+                    if shuffle:
+                        seed = int(getattr(self._env, "trial_seed", 0)) % (2 ** 32)
+                        data.order = np.random.RandomState(seed).permutation(len(data))
+                    self._length = len(data)
+                    return data
                 stream = CachedStream(
                     CachedDataset(path), start_offset=self._offset, shuffle=shuffle,
                     skip_shuffle_at_epoch_end=skip_shuffle_at_epoch_end, shuffle_seed=self._env.trial_seed,
@@ -248,9 +286,9 @@ class _CacheableDecorator:
 class DataLayerContext:
     """``context.experimental`` (reference ``_data_layer/_context.py``)."""
 
-    def __init__(self, env: Any, rank: int = 0, size: int = 1, managed: bool = False) -> None:
-        self._train = _CacheableDecorator(env, rank, size, training=True, managed=managed)
-        self._val = _CacheableDecorator(env, rank, size, training=False, managed=managed)
+    def __init__(self, env: Any, rank: int = 0, size: int = 1, managed: bool = False, map_style: bool = False) -> None:
+        self._train = _CacheableDecorator(env, rank, size, training=True, managed=managed, map_style=map_style)
+        self._val = _CacheableDecorator(env, rank, size, training=False, managed=managed, map_style=map_style)
 
     def cache_train_dataset(self, dataset_id: str, dataset_version: str, shuffle: bool = False,
                             skip_shuffle_at_epoch_end: bool = False) -> Callable:

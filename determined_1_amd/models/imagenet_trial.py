@@ -30,6 +30,7 @@ class ResNetImageNetTrial(det_torch.PyTorchTrial):
         self.image_size = int(hp.get("image_size", 224))
         self.channels_last = bool(hp.get("channels_last", True))
         resnet.FUSED_BN = bool(hp.get("fused_bn", True))
+        resnet.NATIVE_CONV1X1 = bool(hp.get("native_conv1x1", True))
         model = getattr(resnet, arch)(num_classes=self.num_classes)
         if self.channels_last:
             model = model.to(memory_format=torch.channels_last)

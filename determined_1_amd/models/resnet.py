@@ -11,12 +11,22 @@ from typing import List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from determined_1_amd.ops import conv as native_conv
 from determined_1_amd.ops.norm import BatchNormAct2d, linked_conv2d
 from determined_1_amd.ops.pool import MaxPool3x3s2
 
 # Fused BN(+add)(+ReLU) HIP kernels (ops/csrc/det_norm.hip) on by default; set
 # ``resnet.FUSED_BN = False`` (or hparam ``fused_bn: false``) for the stock MIOpen path.
 FUSED_BN = True
+# Stride-1 1x1 convs as hand-written MFMA GEMMs with the BN statistics in the forward epilogue
+# (ops/csrc/det_conv.hip); hparam ``native_conv1x1: false`` keeps them on MIOpen (A/B).
+NATIVE_CONV1X1 = True
+
+
+def c1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    if NATIVE_CONV1X1 and FUSED_BN:
+        return native_conv.conv1x1(x, conv)
+    return conv(x)
 
 
 def bn(c: int, relu: bool) -> BatchNormAct2d:
@@ -74,10 +84,10 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
-        out = self.bn1(self.conv1(x))
+        out = self.bn1(c1x1(x, self.conv1))
         out = self.bn2(self.conv2(out))
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
-        return self.bn3(self.conv3(out), idt, shortcut_link=self.downsample is None)
+        return self.bn3(c1x1(out, self.conv3), idt, shortcut_link=self.downsample is None)
 
 
 class ResNet(nn.Module):

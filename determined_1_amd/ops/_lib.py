@@ -107,6 +107,20 @@ _SIGNATURES = {
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int] + [c_void_p] * 10,
         c_int,
     ),
+    # stream, dtype, x, res, y, M, C, rpb, nrb, pmean, pm2, gamma, beta, rmean, rvar, nbt, momentum, eps, relu,
+    # apply, save_mean, save_rstd, scale, shift, mbits
+    "det_bn_fwd_from_partials": (
+        [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int] + [c_void_p] * 7
+        + [c_float, c_float, c_int, c_int] + [c_void_p] * 5,
+        c_int,
+    ),
+    # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
+    "det_conv_nt_rows_per_block": ([c_int], c_int),
+    # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
+    "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4, c_int),
+    "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),
+    # stream, dY, X, out, out_dtype, M, N, K, scale_x, shift_x, ws, out_scale, Ho, Wo, Hi, Wi
+    "det_conv_tn": ([c_void_p] * 4 + [c_int, c_i64, c_int, c_int] + [c_void_p] * 3 + [c_float] + [c_int] * 4, c_int),
     # det_transformer.hip: fused LayerNorm / dropout / residual / GELU / bias-grad epilogues
     "det_tf_ln_max_hidden": ([], c_int),
     "det_tf_ln_ws_elems": ([c_i64, c_int], c_i64),

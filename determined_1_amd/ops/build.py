@@ -17,7 +17,7 @@ from typing import List
 HERE = pathlib.Path(__file__).resolve().parent
 SRC_DIR = HERE / "csrc"
 SOURCES = [SRC_DIR / "det_kernels.hip", SRC_DIR / "det_norm.hip", SRC_DIR / "det_transformer.hip", SRC_DIR / "det_attention.hip",
-           SRC_DIR / "det_pool.hip"]
+           SRC_DIR / "det_pool.hip", SRC_DIR / "det_conv.hip"]
 OUT = HERE / "libdetkernels.so"
 ARCH = os.environ.get("DET_OFFLOAD_ARCH", "gfx950")
 
@@ -37,20 +37,30 @@ def needs_build(out: pathlib.Path, sources: List[pathlib.Path]) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
+    """Compile each source to an object in parallel (one hipcc per .hip), then link the .so."""
     sources = [s for s in SOURCES if s.exists()]
     if not force and not needs_build(OUT, sources):
         return OUT
+    from concurrent.futures import ThreadPoolExecutor
+
+    objdir = HERE / "build"
+    objdir.mkdir(exist_ok=True)
+    flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC"]
+
+    def compile_one(src: pathlib.Path) -> pathlib.Path:
+        obj = objdir / (src.stem + ".o")
+        if force or not obj.exists() or obj.stat().st_mtime < src.stat().st_mtime:
+            cmd = [hipcc()] + flags + ["-c", str(src), "-o", str(obj)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = max(1, min(len(sources), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, sources))
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [
-        hipcc(),
-        "-O3",
-        f"--offload-arch={ARCH}",
-        "-std=c++17",
-        "-shared",
-        "-fPIC",
-        "-o",
-        str(tmp),
-    ] + [str(s) for s in sources]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,206 @@
+"""Python entry points for the 1x1-convolution GEMMs of ``csrc/det_conv.hip``.
+
+All tensors are row-major 2-D views of channels_last activations: ``x2d`` is ``[N*H*W, C]``.
+The kernels need bf16, 16-byte aligned, contiguous operands with channel counts that are
+multiples of 64 (every 1x1 conv of ResNet-50 qualifies); ``supported()`` says whether a call
+can take the HIP path.  On CPU tensors the functions compute the same result with torch ops
+(fp32 accumulate), which is what the unit tests compare against.
+"""
+from typing import Optional, Tuple
+
+import torch
+
+from determined_1_amd.ops import _lib
+from determined_1_amd.ops.functional import is_gpu
+
+Gather = Tuple[int, int, int, int]  # (Ho, Wo, Hi, Wi) of a 1x1 stride-2 conv
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def supported(x2d: torch.Tensor, w2d: torch.Tensor) -> bool:
+    return (x2d.dtype == torch.bfloat16 and w2d.dtype == torch.bfloat16 and x2d.dim() == 2 and w2d.dim() == 2
+            and x2d.shape[1] % 64 == 0 and w2d.shape[0] % 64 == 0 and w2d.shape[1] == x2d.shape[1]
+            and x2d.is_contiguous() and w2d.is_contiguous()
+            and x2d.data_ptr() % 16 == 0 and w2d.data_ptr() % 16 == 0)
+
+
+def rows_per_block(n: int) -> int:
+    return int(_lib.get_lib().det_conv_nt_rows_per_block(int(n)))
+
+
+def _gather_rows(x2d: torch.Tensor, gather: Optional[Gather], m: int) -> torch.Tensor:
+    if gather is None:
+        return x2d
+    ho, wo, hi, wi = gather
+    n = m // (ho * wo)
+    x4 = x2d.view(n, hi, wi, -1)
+    return x4[:, ::2, ::2, :].reshape(m, -1)
+
+
+def _affine_relu_ref(x: torch.Tensor, scale: Optional[torch.Tensor], shift: Optional[torch.Tensor]) -> torch.Tensor:
+    if scale is None:
+        return x
+    return torch.relu(x.float() * scale + shift).to(x.dtype)
+
+
+def conv1x1_nt(a2d: torch.Tensor, b2d: torch.Tensor, m: Optional[int] = None, scale: Optional[torch.Tensor] = None,
+               shift: Optional[torch.Tensor] = None, stats: bool = False, gather: Optional[Gather] = None,
+               out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
+    """``C = op(A) . B^T`` with ``op(A) = relu(A*scale+shift)`` when scale/shift are given.
+
+    Returns ``(C [M, N] bf16, partials)`` where partials is ``(pmean, pm2, rows_per_block)`` of the
+    bf16-rounded C when ``stats`` (the BatchNorm statistics of the conv output), else None."""
+    n, k = b2d.shape
+    if m is None:
+        m = a2d.shape[0] if gather is None else None
+    assert m is not None
+    if not is_gpu(a2d):
+        a = _affine_relu_ref(_gather_rows(a2d, gather, m), scale, shift)
+        c = (a.float() @ b2d.float().t()).to(a2d.dtype)
+        parts = None
+        if stats:
+            rpb = 128
+            nrb = (m + rpb - 1) // rpb
+            cf = c.float()
+            pad = nrb * rpb - m
+            blocks = torch.cat([cf, cf.new_zeros(pad, n)]).view(nrb, rpb, n)
+            cnt = torch.full((nrb, 1), float(rpb))
+            cnt[-1, 0] = float(m - (nrb - 1) * rpb)
+            mean = blocks.sum(1) / cnt
+            valid = (torch.arange(rpb).view(1, rpb, 1) < cnt.view(nrb, 1, 1))
+            m2 = (((blocks - mean.unsqueeze(1)) ** 2) * valid).sum(1)
+            parts = (mean.contiguous(), m2.contiguous(), rpb)
+        if out is not None:
+            out.copy_(c)
+            c = out
+        return c, parts
+    c = out if out is not None else torch.empty(m, n, dtype=a2d.dtype, device=a2d.device)
+    parts = None
+    pm = pq = None
+    if stats:
+        rpb = rows_per_block(n)
+        nrb = (m + rpb - 1) // rpb
+        pm = torch.empty(nrb, n, dtype=torch.float32, device=a2d.device)
+        pq = torch.empty(nrb, n, dtype=torch.float32, device=a2d.device)
+        parts = (pm, pq, rpb)
+    g = gather or (0, 0, 0, 0)
+    _lib.check(_lib.get_lib().det_conv_nt(_stream(a2d), a2d.data_ptr(), b2d.data_ptr(), c.data_ptr(), int(m), int(n),
+                                          int(k), _ptr(scale), _ptr(shift), _ptr(pm), _ptr(pq), *[int(v) for v in g]),
+               "conv_nt")
+    return c, parts
+
+
+def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, out: torch.Tensor, scale: Optional[torch.Tensor] = None,
+                  shift: Optional[torch.Tensor] = None, gather: Optional[Gather] = None,
+                  out_scale: float = 1.0) -> torch.Tensor:
+    """``out[N, K] = out_scale * dY[M, N]^T . op(X)[M, K]`` (fp32 accumulation, split over M)."""
+    m, n = dy2d.shape
+    k = x2d.shape[1]
+    if not is_gpu(dy2d):
+        xg = _affine_relu_ref(_gather_rows(x2d, gather, m), scale, shift)
+        res = (dy2d.float().t() @ xg.float()) * out_scale
+        out.copy_(res.view_as(out))
+        return out
+    ws = torch.empty(int(_lib.get_lib().det_conv_tn_ws_elems(m, n, k)), dtype=torch.float32, device=dy2d.device)
+    g = gather or (0, 0, 0, 0)
+    code = 1 if out.dtype == torch.bfloat16 else 0
+    assert out.dtype in (torch.bfloat16, torch.float32) and out.is_contiguous() and out.numel() == n * k
+    _lib.check(_lib.get_lib().det_conv_tn(_stream(dy2d), dy2d.data_ptr(), x2d.data_ptr(), out.data_ptr(), code, int(m),
+                                          int(n), int(k), _ptr(scale), _ptr(shift), ws.data_ptr(), float(out_scale),
+                                          *[int(v) for v in g]),
+               "conv_tn")
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# autograd: stride-1 1x1 convolution on channels_last bf16 activations
+# ------------------------------------------------------------------------------------------------
+COUNTS = {"native": 0, "fallback": 0}
+ENABLED = True  # A/B switch (models.resnet.NATIVE_CONV1X1 toggles it)
+
+
+def _attach_partials(y: torch.Tensor, parts: Optional[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:
+    """Hand the BN statistics partials of ``y`` to the BatchNorm that consumes it (ops/norm.py)."""
+    if parts is not None:
+        y._det_bn_parts = (y.data_ptr(), parts)  # type: ignore[attr-defined]
+
+
+def take_partials(x: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor, int]]:
+    p = getattr(x, "_det_bn_parts", None)
+    if p is None or p[0] != x.data_ptr():
+        return None
+    return p[1]
+
+
+class _Conv1x1(torch.autograd.Function):
+    """``conv2d(x, w)`` for a 1x1 stride-1 kernel as det_conv GEMMs: forward with the output's
+    BatchNorm statistics in the epilogue, dgrad through the transposed weight, split-M wgrad that
+    writes the weight gradient straight into its arena slot when the parameter has one."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stats):
+        n, c, h, w_ = x.shape
+        cout = weight.shape[0]
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # channels_last: a free view
+        w2 = weight.reshape(cout, c)
+        wb = w2 if w2.dtype == torch.bfloat16 else w2.to(torch.bfloat16)
+        y2, parts = conv1x1_nt(x2, wb.contiguous(), stats=stats)
+        y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
+        _attach_partials(y, parts)
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        n, c, h, w_ = x.shape
+        cout = weight.shape[0]
+        dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, c)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            wt = weight.reshape(cout, c).to(torch.bfloat16).t().contiguous()
+            dx2, _ = conv1x1_nt(dy2, wt)
+            dx = dx2.view(n, h, w_, c).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            from determined_1_amd.ops.arena import landing_buffer
+
+            buf = landing_buffer(weight)
+            if buf is not None and buf.is_contiguous() and buf.dtype in (torch.bfloat16, torch.float32):
+                dw = buf
+            else:
+                dw = torch.empty(weight.shape, dtype=weight.dtype if weight.dtype in (torch.bfloat16, torch.float32)
+                                 else torch.float32, device=weight.device)
+            conv1x1_wgrad(dy2, x2, dw.view(cout, c))
+            if dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
+        return dx, dw, None
+
+
+def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> torch.Tensor:
+    """``conv_mod(x)``; takes the native GEMM path for bias-free 1x1 stride-1 convs on channels_last
+    bf16 CUDA activations (channels % 64 == 0), else the module itself."""
+    w = conv_mod.weight
+    ok = (ENABLED and x.device.type == "cuda" and x.dim() == 4 and conv_mod.bias is None
+          and conv_mod.kernel_size == (1, 1) and conv_mod.stride == (1, 1) and conv_mod.groups == 1
+          and conv_mod.padding in ((0, 0), 0, "valid") and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+          and x.is_contiguous(memory_format=torch.channels_last))
+    if ok:
+        autocast = torch.is_autocast_enabled("cuda")
+        if x.dtype != torch.bfloat16 and not (autocast and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            ok = False
+    if not ok:
+        COUNTS["fallback"] += 1
+        return conv_mod(x)
+    COUNTS["native"] += 1
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    with torch.autocast("cuda", enabled=False):
+        return _Conv1x1.apply(x, w, stats)

@@ -1,0 +1,547 @@
+// det_conv.hip — hand-written bf16 MFMA GEMMs for ResNet's 1x1 convolutions in NHWC, with the
+// BatchNorm work that surrounds them folded into the GEMM passes.
+//
+// A 1x1 convolution over a channels_last activation is a plain GEMM on [rows = N*H*W, channels]:
+//   forward  Y[M, Cout]   = X[M, Cin] . W[Cout, Cin]^T            (gemm_nt, "NT": both K-contiguous)
+//   dgrad    dX[M, Cin]   = dY[M, Cout] . W^T[Cin, Cout]^T         (gemm_nt with the transposed weight)
+//   wgrad    dW[Cout,Cin] = dY[M, Cout]^T . X[M, Cin]             (gemm_tn: reduction over the M rows)
+// At ResNet-50 / bs512 shapes these are HBM-bound (layer1: K = 64 input channels, arithmetic
+// intensity ~50 FLOP/B), so what matters is touching each activation byte once:
+//   * forward epilogue computes the BatchNorm batch statistics of Y from the accumulators
+//     (per-(row-block, channel) mean and M2 = sum of squared deviations, Chan-mergeable), which
+//     removes the separate stats pass over Y (det_norm.hip bn_stats_partial);
+//   * optional prologue: the A operand is relu(X * scale[k] + shift[k]) applied while staging, i.e.
+//     the preceding BatchNorm-apply + ReLU is fused into the GEMM load and that activation is never
+//     written to HBM (forward of conv3 over bn2's input; wgrad recomputes it the same way);
+//   * 1x1 stride-2 (projection shortcut) convolutions gather their input rows in the A load.
+//
+// CDNA4 mapping (cdna_hip_programming.md §3, §5):
+//   * v_mfma_f32_16x16x32_bf16; 4 waves (256 threads) per workgroup, wave tile 64x64 (4x4 MFMA tiles,
+//     64 fp32 accumulators per lane) for the 128x128 block tile;
+//   * K tile 64 (128-B LDS rows), double-buffered LDS, register staging with the next tile's global
+//     loads in flight during the MFMAs and ONE barrier per K tile; XOR-swizzled 16-B chunks
+//     (chunk ^ (row & 7)) so the 16 rows of an A/B fragment read spread over the banks;
+//   * wgrad stages [m][n] / [m][k] row tiles as they come from HBM and reads both MFMA operands
+//     with ds_read_b64_tr_b16 (hardware transpose) from an XOR-swizzled image;
+//   * workgroup -> tile mapping is XCD-aware and bijective (8 XCDs, private L2 each): the blocks that
+//     share an A row-panel run on one XCD;
+//   * no float atomics: split-K wgrad writes fp32 slabs reduced by a second launch (deterministic).
+//
+// Reference parity: the reference leaves convolutions to cuDNN inside user models
+// (examples/computer_vision/*); semantics are torch.nn.functional.conv2d's.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBK = 64;  // K tile (elements): one 128-B LDS row per operand row
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// byte offset of 16-B chunk `ch` (0..7) of row `row` in a [rows][64 bf16] tile
+__device__ __forceinline__ int swz(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
+
+// Bijective XCD-aware remap: hardware dispatches workgroup ids round-robin over the 8 XCDs; give
+// each XCD a contiguous range of logical tiles (cdna_hip_programming.md §5 "XCD swizzle").
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+// Input-row gather of a 1x1 stride-2 convolution: output row m = ((n*Ho)+ho)*Wo+wo reads input
+// row (n*Hi + 2ho)*Wi + 2wo.
+struct Gather {
+  int Ho, Wo, Hi, Wi;
+  __device__ __forceinline__ int64_t row(int64_t m) const {
+    const int64_t hw = static_cast<int64_t>(Ho) * Wo;
+    const int64_t n = m / hw;
+    const int rem = static_cast<int>(m - n * hw);
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    return (n * Hi + 2 * ho) * Wi + 2 * wo;
+  }
+};
+
+// relu(x * scale + shift) of 8 consecutive channels, re-rounded to bf16
+__device__ __forceinline__ us8 affine_relu8(us8 v, const float* __restrict__ scale, const float* __restrict__ shift,
+                                            int c0) {
+  const float4 s0 = *reinterpret_cast<const float4*>(scale + c0);
+  const float4 s1 = *reinterpret_cast<const float4*>(scale + c0 + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(shift + c0);
+  const float4 h1 = *reinterpret_cast<const float4*>(shift + c0 + 4);
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  us8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(fmaxf(__fmaf_rn(bf2f(v[j]), sc[j], sh[j]), 0.f));
+  return o;
+}
+
+struct NtArgs {
+  const unsigned short* A;  // [rows, K]
+  const unsigned short* B;  // [N, K]
+  unsigned short* C;        // [M, N]
+  int64_t M;
+  int N, K;
+  const float* scale;  // PRO: A <- relu(A*scale[k] + shift[k])
+  const float* shift;
+  float* pmean;  // STATS: [ceil(M/BM), N] block mean / M2 of the bf16-rounded C
+  float* pm2;
+  Gather g;  // STRIDE2
+};
+
+// ------------------------------------------------------------------------------------------------
+// C[M,N] = op(A)[M,K] . B[N,K]^T, bf16 in/out, fp32 accumulate.  N % BN == 0, K % 64 == 0.
+// ------------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, bool STRIDE2>
+__global__ void __launch_bounds__(kThreads, 2) gemm_nt_kernel(NtArgs a) {
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
+  constexpr int A_BYTES = BM * 128, BUF = (BM + BN) * 128;
+  constexpr int LDC = BN + 16;  // epilogue tile row stride (bf16): +32 B keeps the 4 row groups on distinct banks
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(FM >= 1 && FN >= 1 && ACH >= 1 && BCH >= 1, "tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ float red[WM][BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = a.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int64_t m0 = static_cast<int64_t>(mt) * BM;
+  const int n0 = nt * BN;
+  const int kc = tid & 7, r0 = tid >> 3;
+  const int64_t K = a.K;
+
+  const unsigned short* aptr[ACH];
+  bool aval[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int64_t m = m0 + r0 + 32 * i;
+    aval[i] = m < a.M;
+    int64_t row = aval[i] ? m : 0;
+    if (STRIDE2) row = a.g.row(row);
+    aptr[i] = a.A + row * K + kc * 8;
+  }
+  const unsigned short* bptr = a.B + static_cast<int64_t>(n0 + r0) * K + kc * 8;
+
+  us8 ra[ACH], rb[BCH];
+  auto gload = [&](int kt) {
+    const int64_t k = static_cast<int64_t>(kt) * kBK;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      if (aval[i]) ra[i] = *reinterpret_cast<const us8*>(aptr[i] + k);
+      else ra[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) rb[j] = *reinterpret_cast<const us8*>(bptr + 32 * j * K + k);
+  };
+  auto lstore = [&](int buf, int kt) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      us8 v = ra[i];
+      if (PRO) {
+        v = affine_relu8(v, a.scale, a.shift, kt * kBK + kc * 8);
+        if (!aval[i]) v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      *reinterpret_cast<us8*>(base + swz(r0 + 32 * i, kc)) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < BCH; ++j) *reinterpret_cast<us8*>(base + A_BYTES + swz(r0 + 32 * j, kc)) = rb[j];
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / kBK;
+  gload(0);
+  lstore(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const unsigned char* base = smem + cur * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(base + swz(wm * TM + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(cur ^ 1, kt + 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bf16 tile through LDS (coalesced 16-B row stores) + BN statistics ----
+  unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
+  const int64_t rows_left = a.M - m0;
+  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * TN + j * 16 + (lane & 15);
+        ct[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  if (STATS) {
+    float cs[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (row < nvalid) s += round_bf(acc[i][j][r]);
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      cs[j] = s;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm][wn * TN + j * 16 + lane] = cs[j];
+    }
+    __syncthreads();
+    const float inv_n = 1.f / static_cast<float>(nvalid);
+    float mu[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * TN + j * 16 + (lane & 15);
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w][col];
+      mu[j] = s * inv_n;
+    }
+    __syncthreads();  // every lane has read red[] before it is reused for M2
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          const float d = round_bf(acc[i][j][r]) - mu[j];
+          if (row < nvalid) q += d * d;
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) red[wm][wn * TN + j * 16 + lane] = q;
+      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
+    }
+  }
+  __syncthreads();
+  if (STATS && tid < BN) {
+    float q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) q += red[w][tid];
+    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
+  }
+  constexpr int CPR = BN / 8;  // 16-B chunks per output row
+#pragma unroll
+  for (int q = 0; q < BM * CPR / kThreads; ++q) {
+    const int idx = tid + q * kThreads;
+    const int row = idx / CPR, cc = idx - row * CPR;
+    if (row < nvalid)
+      *reinterpret_cast<us8*>(a.C + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// wgrad: P[s][N][K] (fp32 slab per M split s) = sum_{m in split s} dY[m][n] * op(X)[g(m)][k]
+// ------------------------------------------------------------------------------------------------
+struct TnArgs {
+  const unsigned short* dY;  // [M, N]
+  const unsigned short* X;   // [rows, K]
+  float* P;                  // [S, N, K]
+  int64_t M;
+  int N, K;
+  int64_t rows_per_split;  // multiple of 64
+  const float* scale;      // PRO: X <- relu(X*scale[k] + shift[k])
+  const float* shift;
+  Gather g;
+};
+
+// byte offset of 16-B chunk ch of row `row` in a [64][W] bf16 tile (W = 64 or 128): XOR pattern
+// that makes the ds_read_b64_tr_b16 fragment reads (4 rows x 2 chunks per 16-lane group, two such
+// groups 8 rows apart per 32-lane half) hit distinct banks
+template <int W>
+__device__ __forceinline__ int tswz(int row, int ch) {
+  if (W == 128) return row * 256 + ((ch ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3))) << 4);
+  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
+}
+
+// MFMA operand (16 columns x 32 k-rows) via two transposed 4x16 reads: lane (g = lane>>4, i = lane&15)
+// gets rows k0 + 8g + 0..7 of column c0 + i.
+template <int W>
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned char* tile, int k0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = c0 + 4 * p;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int o0 = tswz<W>(k0 + 8 * g + q, col >> 3) + ((col & 4) << 1);
+  const int o1 = tswz<W>(k0 + 8 * g + 4 + q, col >> 3) + ((col & 4) << 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + o1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BN, int BK, bool PRO, bool STRIDE2>
+__global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
+  constexpr int TN = BN / 2, TK = BK / 2, FN = TN / 16, FK = TK / 16;
+  constexpr int YB = 64 * BN * 2, XB = 64 * BK * 2, BUF = YB + XB;
+  constexpr int YCH = 64 * BN / 8 / kThreads, XCH = 64 * BK / 8 / kThreads;  // 16-B chunks per thread
+  constexpr int YCPR = BN / 8, XCPR = BK / 8;                                // chunks per row
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid >> 1, wk = wid & 1;
+  const int ntn = a.N / BN, ntk = a.K / BK, ntiles = ntn * ntk;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int nt = tile / ntk, kt_ = tile - nt * ntk;
+  const int n0 = nt * BN, k0 = kt_ * BK;
+  const int64_t mbeg = static_cast<int64_t>(split) * a.rows_per_split;
+  int64_t mend = mbeg + a.rows_per_split;
+  if (mend > a.M) mend = a.M;
+
+  us8 ry[YCH], rx[XCH];
+  bool xval[XCH];
+  auto gload = [&](int64_t mb) {
+#pragma unroll
+    for (int i = 0; i < YCH; ++i) {
+      const int idx = tid + i * kThreads, r = idx / YCPR, c = idx - r * YCPR;
+      const int64_t m = mb + r;
+      if (m < mend) ry[i] = *reinterpret_cast<const us8*>(a.dY + m * a.N + n0 + c * 8);
+      else ry[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int idx = tid + i * kThreads, r = idx / XCPR, c = idx - r * XCPR;
+      const int64_t m = mb + r;
+      xval[i] = m < mend;
+      const int64_t row = STRIDE2 ? a.g.row(xval[i] ? m : 0) : (xval[i] ? m : 0);
+      if (xval[i]) rx[i] = *reinterpret_cast<const us8*>(a.X + row * a.K + k0 + c * 8);
+      else rx[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < YCH; ++i) {
+      const int idx = tid + i * kThreads, r = idx / YCPR, c = idx - r * YCPR;
+      *reinterpret_cast<us8*>(base + tswz<BN>(r, c)) = ry[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int idx = tid + i * kThreads, r = idx / XCPR, c = idx - r * XCPR;
+      us8 v = rx[i];
+      if (PRO) {
+        v = affine_relu8(v, a.scale, a.shift, k0 + c * 8);
+        if (!xval[i]) v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      *reinterpret_cast<us8*>(base + YB + tswz<BK>(r, c)) = v;
+    }
+  };
+
+  f32x4 acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = mend > mbeg ? static_cast<int>((mend - mbeg + 63) / 64) : 0;
+  if (nsteps > 0) {
+    gload(mbeg);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) gload(mbeg + static_cast<int64_t>(s + 1) * 64);
+    const unsigned char* base = smem + cur * BUF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 yf[FN], xf[FK];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) yf[i] = tr_frag<BN>(base, ks * 32, wn * TN + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FK; ++j) xf[j] = tr_frag<BK>(base + YB, ks * 32, wk * TK + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = a.P + static_cast<int64_t>(split) * a.N * a.K;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * TN + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wk * TK + j * 16 + (lane & 15);
+        out[static_cast<int64_t>(n) * a.K + k] = acc[i][j][r];
+      }
+}
+
+// out[i] = scale * sum_s P[s][i]  (fp32 slabs -> bf16 or fp32)
+template <typename TO>
+__global__ void __launch_bounds__(kThreads) slab_reduce_kernel(const float* __restrict__ P, int S, int64_t n, float scale,
+                                                                TO* __restrict__ out) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n4;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    float4 acc = reinterpret_cast<const float4*>(P)[i];
+    for (int s = 1; s < S; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(P + s * n)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    if constexpr (sizeof(TO) == 4) {
+      reinterpret_cast<float4*>(out)[i] = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
+    } else {
+      ushort4 o;
+      o.x = f2bf(acc.x * scale); o.y = f2bf(acc.y * scale); o.z = f2bf(acc.z * scale); o.w = f2bf(acc.w * scale);
+      reinterpret_cast<ushort4*>(out)[i] = o;
+    }
+  }
+}
+
+template <int BM, int BN>
+constexpr int nt_smem() {
+  return (2 * (BM + BN) * 128) > (BM * (BN + 16) * 2) ? 2 * (BM + BN) * 128 : BM * (BN + 16) * 2;
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2) {
+  const int64_t mtiles = (a.M + BM - 1) / BM;
+  const int64_t nwg = mtiles * (a.N / BN);
+  if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
+  constexpr int smem = nt_smem<BM, BN>();
+#define DET_NT(P, S, G)                                                                          \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G>), dim3(static_cast<unsigned>(nwg)), \
+                     dim3(kThreads), smem, st, a)
+  if (stride2) {
+    if (pro) { if (stats) DET_NT(true, true, true); else DET_NT(true, false, true); }
+    else { if (stats) DET_NT(false, true, true); else DET_NT(false, false, true); }
+  } else {
+    if (pro) { if (stats) DET_NT(true, true, false); else DET_NT(true, false, false); }
+    else { if (stats) DET_NT(false, true, false); else DET_NT(false, false, false); }
+  }
+#undef DET_NT
+  return static_cast<int>(hipGetLastError());
+}
+
+template <int BN, int BK>
+int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride2) {
+  const int nwg = (a.N / BN) * (a.K / BK) * splits;
+  constexpr int smem = 2 * 64 * (BN + BK) * 2;
+#define DET_TN(P, G) \
+  hipLaunchKernelGGL((gemm_tn_kernel<BN, BK, P, G>), dim3(nwg), dim3(kThreads), smem, st, a)
+  if (stride2) { if (pro) DET_TN(true, true); else DET_TN(false, true); }
+  else { if (pro) DET_TN(true, false); else DET_TN(false, false); }
+#undef DET_TN
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+// Rows per statistics block of det_conv_nt for an N-column output (the BN finalize needs it).
+int det_conv_nt_rows_per_block(int N) { return 128; }
+
+// C[M,N] = op(A)[M,K] . B[N,K]^T.  bf16.  N % 64 == 0, K % 64 == 0, pointers 16-B aligned.
+// scale/shift (nullable): prologue relu(A*scale+shift) per K channel.  pmean/pm2 (nullable):
+// BN statistics partials [ceil(M/rpb), N].  Ho..Wi > 0 selects the 1x1 stride-2 row gather.
+int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K,
+                const float* scale, const float* shift, float* pmean, float* pm2, int Ho, int Wo, int Hi, int Wi) {
+  if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
+  if ((scale == nullptr) != (shift == nullptr) || (pmean == nullptr) != (pm2 == nullptr)) return -2;
+  const bool stride2 = Ho > 0;
+  if (stride2 && M != static_cast<int64_t>(M / (static_cast<int64_t>(Ho) * Wo)) * Ho * Wo) return -3;
+  NtArgs a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C),
+           M, N, K, scale, shift, pmean, pm2, Gather{Ho, Wo, Hi, Wi}};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool pro = scale != nullptr, stats = pmean != nullptr;
+  if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(st, a, pro, stats, stride2);
+  return launch_nt<128, 64, 2, 2>(st, a, pro, stats, stride2);
+}
+
+// fp32 workspace elements det_conv_tn needs (slabs) for an [N, K] output from M rows.
+int64_t det_conv_tn_ws_elems(int64_t M, int N, int K) {
+  const int bn = N % 128 == 0 ? 128 : 64, bk = K % 128 == 0 ? 128 : 64;
+  const int64_t tiles = static_cast<int64_t>(N / bn) * (K / bk);
+  int64_t splits = (512 + tiles - 1) / tiles;    // ~2 workgroups per CU
+  const int64_t max_rows = (M + 1023) / 1024;    // >= 1024 rows per split
+  // fp32 slab traffic (write + reduce read) at most ~1/4 of the operand bytes the GEMM streams
+  const int64_t max_bytes = (M * (N + K) * 2) / (4 * 4 * static_cast<int64_t>(N) * K * 2);
+  if (splits > max_rows) splits = max_rows;
+  if (splits > max_bytes) splits = max_bytes;
+  if (splits < 1) splits = 1;
+  return splits * N * K;
+}
+
+// dW[N,K] (out_dtype 0 fp32 / 1 bf16) = scale * dY[M,N]^T . op(X)[M,K], via fp32 split-M slabs
+// in ws (>= det_conv_tn_ws_elems) reduced by a second launch.
+int det_conv_tn(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int N, int K,
+                const float* scale_x, const float* shift_x, float* ws, float out_scale, int Ho, int Wo, int Hi,
+                int Wi) {
+  if (M <= 0 || N % 64 != 0 || K % 64 != 0) return -1;
+  if ((scale_x == nullptr) != (shift_x == nullptr)) return -2;
+  const int bn = N % 128 == 0 ? 128 : 64, bk = K % 128 == 0 ? 128 : 64;
+  const int64_t slab = static_cast<int64_t>(N) * K;
+  const int splits = static_cast<int>(det_conv_tn_ws_elems(M, N, K) / slab);
+  int64_t rps = (M + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  TnArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, N, K, rps,
+           scale_x, shift_x, Gather{Ho, Wo, Hi, Wi}};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool pro = scale_x != nullptr, stride2 = Ho > 0;
+  int rc;
+  if (bn == 128 && bk == 128) rc = launch_tn<128, 128>(st, a, splits, pro, stride2);
+  else if (bn == 128) rc = launch_tn<128, 64>(st, a, splits, pro, stride2);
+  else if (bk == 128) rc = launch_tn<64, 128>(st, a, splits, pro, stride2);
+  else rc = launch_tn<64, 64>(st, a, splits, pro, stride2);
+  if (rc != 0) return rc;
+  int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
+  if (grid > 2048) grid = 2048;
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
+                       static_cast<unsigned short*>(out));
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
+                       static_cast<float*>(out));
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

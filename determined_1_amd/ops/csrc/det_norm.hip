@@ -179,6 +179,8 @@ bn_stats_partial(const T* __restrict__ x, Geom g, float* __restrict__ pmean, flo
   }
 }
 
+__global__ void bump_counter(int64_t* c) { *c += 1; }
+
 struct FinArgs {
   const float* gamma;  // may be null (affine=False)
   const float* beta;
@@ -588,6 +590,50 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
   hipLaunchKernelGGL(bn_stats_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, pmean, pm2, g,
                      fa);
   int64_t* bump = num_batches_tracked;
+  const int64_t nvec = M * C / 8;
+  const int grid2 = apply_grid(nvec, 4);
+#define DET_BN_FWD(T, RL, RS)                                                                          \
+  hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                    \
+                     static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, shift, \
+                     nvec, C, bump, mbits)
+  if (dtype == 1) {
+    if (relu && res) DET_BN_FWD(unsigned short, true, true);
+    else if (relu) DET_BN_FWD(unsigned short, true, false);
+    else if (res) DET_BN_FWD(unsigned short, false, true);
+    else DET_BN_FWD(unsigned short, false, false);
+  } else {
+    if (relu && res) DET_BN_FWD(float, true, true);
+    else if (relu) DET_BN_FWD(float, true, false);
+    else if (res) DET_BN_FWD(float, false, true);
+    else DET_BN_FWD(float, false, false);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+// Training forward when the producer already computed the statistics partials (det_conv.hip GEMM
+// epilogue): Chan-merge the [nrb, C] (mean, M2) partials over row-blocks of `rpb` rows, then apply.
+// Skips the stats pass over x entirely.  apply = 0 stops after the finalize (the consumer applies
+// scale/shift itself, e.g. in its GEMM prologue); num_batches_tracked is then bumped here.
+int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
+                             int rpb, int nrb, const float* pmean, const float* pm2, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var,
+                             int64_t* num_batches_tracked, float momentum, float eps, int relu, int apply,
+                             float* save_mean, float* save_rstd, float* scale, float* shift, uint8_t* mbits) {
+  if (C % 8 != 0 || M <= 0 || rpb <= 0 || nrb != static_cast<int>((M + rpb - 1) / rpb)) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Geom g = make_geom(M, C);
+  g.rpb = rpb;
+  g.nrb = nrb;
+  FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+             save_mean, save_rstd, scale, shift};
+  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, pmean, pm2, g,
+                     fa);
+  int64_t* bump = num_batches_tracked;
+  if (!apply) {
+    if (bump) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, bump);
+    return static_cast<int>(hipGetLastError());
+  }
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
 #define DET_BN_FWD(T, RL, RS)                                                                          \

@@ -63,6 +63,13 @@ def configure(env: Optional[MutableMapping[str, str]] = None) -> Optional[str]:
     Respects an explicit ``MIOPEN_USER_DB_PATH`` (a user-chosen db is left alone) and
     ``DET_MIOPEN_DB=0`` (disable).  Returns the user-db directory in use."""
     e = os.environ if env is None else env
+    if e.get("DET_MIOPEN_NAIVE", "0") != "1":
+        # MIOpen's find times every applicable solver, including the GPU reference ("naive")
+        # convolutions, which take 0.05-0.5 s per call at batch 512: rocprofv3 showed 114 s of
+        # naive_conv_ab_nonpacked_{fwd,bwd,wrw} in the first ResNet-50 batch
+        # (profiles/r2_resnet50_first_batch_find.txt).  They are never the fastest solver here.
+        for d in ("FWD", "BWD", "WRW"):
+            e.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_" + d, "0")
     if e.get("DET_MIOPEN_DB", "1") == "0":
         return e.get("MIOPEN_USER_DB_PATH")
     if e.get("MIOPEN_USER_DB_PATH"):

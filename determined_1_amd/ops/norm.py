@@ -82,16 +82,32 @@ class _BNActTrain(torch.autograd.Function):
             residual = residual.to(x.dtype).contiguous(memory_format=fmt)
         mbits = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) \
             if (relu and residual is not None) else None
-        _lib.check(
-            lib.det_bn_fwd_train(
-                _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C,
-                _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
-                float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)),
-                stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
-                ws.data_ptr(), _ptr(mbits),
-            ),
-            "bn_fwd_train",
-        )
+        from determined_1_amd.ops.conv import take_partials
+
+        parts = take_partials(x)  # statistics already computed by the producing GEMM's epilogue
+        if parts is not None:
+            pm, pq, rpb = parts
+            _lib.check(
+                lib.det_bn_fwd_from_partials(
+                    _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C, int(rpb),
+                    int(pm.shape[0]), pm.data_ptr(), pq.data_ptr(),
+                    _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
+                    float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)), 1,
+                    stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits),
+                ),
+                "bn_fwd_from_partials",
+            )
+        else:
+            _lib.check(
+                lib.det_bn_fwd_train(
+                    _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C,
+                    _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
+                    float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)),
+                    stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                    ws.data_ptr(), _ptr(mbits),
+                ),
+                "bn_fwd_train",
+            )
         _dbg("fwd_train", x)
         mask_mode = 0 if not relu else (2 if residual is not None else 1)
         ctx.mask_mode = mask_mode

@@ -63,6 +63,8 @@ class _OptState:
 
 
 class PyTorchTrialContext(trial.TrialContext):
+    _data_layer_map_style = True  # cached datasets come back map-style; the controller's samplers own them
+
     def __init__(self, *args: Any, **kwargs: Any) -> None:
         super().__init__(*args, **kwargs)
         self._init_device()

@@ -32,6 +32,9 @@ class _TrainContext(metaclass=abc.ABCMeta):
         env, dist_cfg, rank = _local.make_local_env(config, managed_training=False)
         return cls(env, dist_cfg, rank)
 
+    # PyTorchTrial's controller shards/skips map-style datasets itself (see _data_layer.py)
+    _data_layer_map_style = False
+
     @property
     def experimental(self) -> Any:
         """Dataset cache decorators (``cache_train_dataset`` / ``cache_validation_dataset``), see
@@ -40,7 +43,8 @@ class _TrainContext(metaclass=abc.ABCMeta):
             from determined_1_amd._data_layer import DataLayerContext
 
             self._data_layer = DataLayerContext(self.env, self.distributed.get_rank(), self.distributed.get_size(),
-                                                managed=bool(self.env.managed_training and self.env.master_addr))
+                                                managed=bool(self.env.managed_training and self.env.master_addr),
+                                                map_style=self._data_layer_map_style)
         return self._data_layer
 
     def get_experiment_config(self) -> Dict[str, Any]:

@@ -73,3 +73,83 @@ def test_trial_context_exposes_experimental(tmp_path):
     ctx = PyTorchTrialContext.from_config(cfg)
     s = ctx.experimental.cache_train_dataset("sq", "v2")(Squares)()
     assert len(s) == 10 and ctx.experimental.get_train_cacheable().get_dataset_length() == 10
+
+
+def _make_id_trial(storage):
+    """PyTorchTrial over a cached dataset that records which sample ids it trains on."""
+    from determined_1_amd import pytorch
+
+    class Ids(torch.utils.data.Dataset):
+        def __len__(self):
+            return 24
+
+        def __getitem__(self, i):
+            return {"id": torch.tensor(i), "x": torch.full((2,), float(i))}
+
+    class CachedIdTrial(pytorch.PyTorchTrial):
+        seen = []
+
+        def __init__(self, context):
+            self.context = context
+            self.model = context.wrap_model(torch.nn.Linear(2, 1))
+            self.opt = context.wrap_optimizer(torch.optim.SGD(self.model.parameters(), lr=0.01))
+
+        def train_batch(self, batch, epoch_idx, batch_idx):
+            CachedIdTrial.seen.append([int(v) for v in batch["id"]])
+            loss = self.model(batch["x"]).pow(2).mean()
+            self.context.backward(loss)
+            self.context.step_optimizer(self.opt)
+            return {"loss": loss}
+
+        def evaluate_batch(self, batch):
+            return {"validation_loss": self.model(batch["x"]).pow(2).mean()}
+
+        def build_training_data_loader(self):
+            @self.context.experimental.cache_train_dataset("ids", "v1", shuffle=True)
+            def make():
+                return Ids()
+
+            return pytorch.DataLoader(make(), batch_size=self.context.get_per_slot_batch_size())
+
+        def build_validation_data_loader(self):
+            @self.context.experimental.cache_validation_dataset("ids", "v1")
+            def make():
+                return Ids()
+
+            return pytorch.DataLoader(make(), batch_size=self.context.get_per_slot_batch_size())
+
+    return CachedIdTrial
+
+
+def test_pytorch_trial_trains_on_cached_dataset_and_resumes(tmp_path):
+    """the data layer through a real PyTorchTrial -- cached map-style dataset, controller
+    samplers shard/skip it, checkpoint + resume continues exactly where the first run stopped."""
+    from tests.utils import Recorder, run
+
+    trial = _make_id_trial(tmp_path)
+    hp = {"global_batch_size": 4}
+    extra = {"data_layer": {"type": "shared_fs", "container_storage_path": str(tmp_path / "cache")}}
+    trial.seen = []
+    run(trial, hp, Recorder().train(1, 3, 0).train(2, 3, 3), trial_seed=5, **extra)
+    straight = list(trial.seen)
+    assert len(straight) == 6
+    first_epoch = sorted(i for b in straight for i in b)
+    assert first_epoch == list(range(24))  # one pass over the (fixed-permuted) cache, no repeats
+    assert [i for b in straight for i in b] != list(range(24))  # shuffle=True permuted it
+    trial.seen = []
+    ckpt = tmp_path / "ckpt"
+    run(trial, hp, Recorder().train(1, 3, 0).checkpoint(1, 3, ckpt), trial_seed=5, **extra)
+    trial.seen = []
+    run(trial, hp, Recorder().train(2, 3, 3), load_path=ckpt, total_batches=3, trial_seed=5, **extra)
+    assert trial.seen == straight[3:]
+    assert not list((tmp_path / "cache" / "ids").glob(".tmp_*"))
+
+
+def test_stale_writer_temp_dirs_removed(tmp_path):
+    env = make_env(tmp_path)
+    (tmp_path / "sq").mkdir()
+    (tmp_path / "sq" / ".tmp_dead").mkdir()
+    ctx = _data_layer.DataLayerContext(env, map_style=True)
+    ds = ctx.cache_train_dataset("sq", "v9")(Squares)()
+    assert isinstance(ds, _data_layer.CachedDataset) and len(ds) == 10
+    assert not (tmp_path / "sq" / ".tmp_dead").exists()
