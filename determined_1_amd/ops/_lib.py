@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -86,6 +86,7 @@ _SIGNATURES = {
     ),
     # det_norm.hip: fused BatchNorm(+add)(+ReLU), channels_last
     "det_bn_ws_elems": ([c_i64, c_int], c_i64),
+    "det_bn_fin_ws_elems": ([c_int], c_i64),
     # stream, dtype, x, res, y, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
     # relu, save_mean, save_rstd, scale, shift, ws, mask_bits
     "det_bn_fwd_train": (
@@ -108,10 +109,10 @@ _SIGNATURES = {
         c_int,
     ),
     # stream, dtype, x, res, y, M, C, rpb, nrb, pmean, pm2, gamma, beta, rmean, rvar, nbt, momentum, eps, relu,
-    # apply, save_mean, save_rstd, scale, shift, mbits
+    # apply, save_mean, save_rstd, scale, shift, mbits, ws
     "det_bn_fwd_from_partials": (
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int] + [c_void_p] * 7
-        + [c_float, c_float, c_int, c_int] + [c_void_p] * 5,
+        + [c_float, c_float, c_int, c_int] + [c_void_p] * 6,
         c_int,
     ),
     # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
@@ -119,6 +120,10 @@ _SIGNATURES = {
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
     "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4, c_int),
     "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),
+    # det_igemm.hip: pipelined implicit-GEMM conv (LDS-DMA ring)
+    "det_igemm_rows_per_block": ([], c_int),
+    # stream, X, W, Y, zero, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, pmean, pm2
+    "det_igemm_conv": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2, c_int),
     # stream, dY, X, out, out_dtype, M, N, K, scale_x, shift_x, ws, out_scale, Ho, Wo, Hi, Wi
     "det_conv_tn": ([c_void_p] * 4 + [c_int, c_i64, c_int, c_int] + [c_void_p] * 3 + [c_float] + [c_int] * 4, c_int),
     # det_transformer.hip: fused LayerNorm / dropout / residual / GELU / bias-grad epilogues

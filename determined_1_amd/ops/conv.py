@@ -120,6 +120,69 @@ def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, out: torch.Tensor, scal
 
 
 # ------------------------------------------------------------------------------------------------
+# pipelined implicit-GEMM convolution (csrc/det_igemm.hip)
+# ------------------------------------------------------------------------------------------------
+_ZERO = {}
+
+
+def _zero_page(dev: torch.device) -> torch.Tensor:
+    """256 zero bytes on ``dev``: the source the conv gather reads for padding taps and row tails."""
+    z = _ZERO.get(dev)
+    if z is None:
+        z = _ZERO[dev] = torch.zeros(128, dtype=torch.bfloat16, device=dev)
+    return z
+
+
+def krsc(w: torch.Tensor) -> torch.Tensor:
+    """Conv weight [Cout, Cin, R, S] as the [Cout, R*S*Cin] KRSC matrix det_igemm reads (a view for
+    channels_last weights)."""
+    co = w.shape[0]
+    return w.permute(0, 2, 3, 1).reshape(co, -1).contiguous()
+
+
+def igemm_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
+               w_krsc: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
+    """``conv2d(x, w, stride, pad)`` for channels_last bf16 ``x`` (Cin % 64 == 0) and Cout % 64 == 0.
+    Returns (y channels_last bf16, BN statistics partials of y when ``stats``).  ``w_krsc``: the
+    weight already in [Cout, R*S*Cin] form (e.g. the flipped/transposed dgrad weight)."""
+    nb, cin, hi, wi = x.shape
+    cout, _, r, s = w.shape
+    ho = (hi + 2 * pad - r) // stride + 1
+    wo = (wi + 2 * pad - s) // stride + 1
+    m = nb * ho * wo
+    if not is_gpu(x):
+        y = torch.nn.functional.conv2d(x.float(), w.float(), stride=stride, padding=pad).to(x.dtype)
+        y = y.contiguous(memory_format=torch.channels_last)
+        parts = None
+        if stats:
+            y2 = y.permute(0, 2, 3, 1).reshape(m, cout)
+            _, parts = conv1x1_nt(y2, torch.eye(cout, dtype=y.dtype), stats=True)  # exact copy + stats
+        return y, parts
+    wk = krsc(w) if w_krsc is None else w_krsc
+    assert wk.dtype == torch.bfloat16 and wk.is_contiguous() and wk.shape == (cout, r * s * cin)
+    y = torch.empty((nb, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    parts = None
+    pm = pq = None
+    if stats:
+        rpb = int(_lib.get_lib().det_igemm_rows_per_block())
+        nrb = (m + rpb - 1) // rpb
+        pm = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
+        pq = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
+        parts = (pm, pq, rpb)
+    _lib.check(_lib.get_lib().det_igemm_conv(_stream(x), x.data_ptr(), wk.data_ptr(), y.data_ptr(),
+                                             _zero_page(x.device).data_ptr(), int(m), int(cout), int(cin), int(hi),
+                                             int(wi), int(ho), int(wo), int(r), int(s), int(stride), int(pad),
+                                             _ptr(pm), _ptr(pq)),
+               "igemm_conv")
+    return y, parts
+
+
+# ------------------------------------------------------------------------------------------------
 # autograd: stride-1 1x1 convolution on channels_last bf16 activations
 # ------------------------------------------------------------------------------------------------
 COUNTS = {"native": 0, "fallback": 0}

@@ -37,6 +37,10 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kBK = 64;  // K tile (elements): one 128-B LDS row per operand row
+#ifndef DET_NT_SINGLE_OCC
+#define DET_NT_SINGLE_OCC 3
+#endif
+constexpr int kSingleOcc = DET_NT_SINGLE_OCC;  // workgroups per CU of the K == 64 variant
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -103,8 +107,11 @@ struct NtArgs {
 // ------------------------------------------------------------------------------------------------
 // C[M,N] = op(A)[M,K] . B[N,K]^T, bf16 in/out, fp32 accumulate.  N % BN == 0, K % 64 == 0.
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, bool STRIDE2>
-__global__ void __launch_bounds__(kThreads, 2) gemm_nt_kernel(NtArgs a) {
+// OCC: workgroups per CU the register budget is sized for.  K == 64 (one K tile: layer1's
+// 64-channel side, every dgrad into a 64-channel input) is a pure streaming pass with no K loop
+// to overlap loads with, so it runs single-buffered (half the LDS) at higher occupancy instead.
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, bool STRIDE2, int OCC>
+__global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
   constexpr int A_BYTES = BM * 128, BUF = (BM + BN) * 128;
@@ -436,19 +443,19 @@ __global__ void __launch_bounds__(kThreads) slab_reduce_kernel(const float* __re
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NBUF>
 constexpr int nt_smem() {
-  return (2 * (BM + BN) * 128) > (BM * (BN + 16) * 2) ? 2 * (BM + BN) * 128 : BM * (BN + 16) * 2;
+  return (NBUF * (BM + BN) * 128) > (BM * (BN + 16) * 2) ? NBUF * (BM + BN) * 128 : BM * (BN + 16) * 2;
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int OCC>
 int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2) {
   const int64_t mtiles = (a.M + BM - 1) / BM;
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
-  constexpr int smem = nt_smem<BM, BN>();
-#define DET_NT(P, S, G)                                                                          \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G>), dim3(static_cast<unsigned>(nwg)), \
+  constexpr int smem = nt_smem<BM, BN, OCC == 2 ? 2 : 1>();
+#define DET_NT(P, S, G)                                                                               \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G, OCC>), dim3(static_cast<unsigned>(nwg)), \
                      dim3(kThreads), smem, st, a)
   if (stride2) {
     if (pro) { if (stats) DET_NT(true, true, true); else DET_NT(true, false, true); }
@@ -493,8 +500,12 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
            M, N, K, scale, shift, pmean, pm2, Gather{Ho, Wo, Hi, Wi}};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool pro = scale != nullptr, stats = pmean != nullptr;
-  if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(st, a, pro, stats, stride2);
-  return launch_nt<128, 64, 2, 2>(st, a, pro, stats, stride2);
+  if (K == kBK) {
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
+    return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
+  }
+  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, pro, stats, stride2);
+  return launch_nt<128, 64, 2, 2, 2>(st, a, pro, stats, stride2);
 }
 
 // fp32 workspace elements det_conv_tn needs (slabs) for an [N, K] output from M rows.

@@ -1,0 +1,328 @@
+// det_igemm.hip — pipelined implicit-GEMM convolution for NHWC bf16 activations on CDNA4 MFMA.
+//
+//   Y[M, N] = sum_{tap (r,s), c} X[n, ho*st - pad + r, wo*st - pad + s, c] . W[N][r][s][c]
+//   (M = Nb*Ho*Wo output pixels, N = output channels, K = R*S*Cin, W in KRSC = torch channels_last
+//   weight order, so the B operand is the weight tensor as it sits in memory)
+//
+// One kernel covers every ResNet conv whose input channel count is a multiple of 64: 1x1 stride 1/2,
+// 3x3 stride 1/2 pad 1, and the stride-1 input gradients (dgrad of a 1x1 is this GEMM against W^T;
+// dgrad of a 3x3/pad-1 is a 3x3/pad-1 conv of dY against the spatially flipped, transposed weight).
+//
+// Why a new kernel: the register-staged det_conv GEMM and the library convs both run ResNet-50's
+// convolutions at ~19 % of the bf16 MFMA peak (profiles/r2_resnet50_bs512_fin2_steady.csv): with
+// one K tile of prefetch in registers, HBM/L2 latency (~1-2 us under load) is not covered by the
+// ~0.2 us of MFMA work per K step.  Here (cdna_hip_programming.md §5):
+//   * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4): no staging VGPRs, no
+//     ds_write pass; the per-lane SOURCE address does the im2col gather (a 16-B chunk per lane,
+//     zero-padding and the M tail read a zero page), so the LDS image stays lane-linear and the
+//     XOR swizzle (chunk ^ row&7, conflict-free ds_read_b128 fragments) is applied on the source;
+//   * a 3-stage LDS ring with a COUNTED vmcnt: two K tiles are in flight while the MFMAs consume
+//     the third, and the barrier is a raw s_barrier (a __syncthreads() would drain the DMA queue);
+//   * 256 x BN block tile, 8 waves (2 per SIMD), 64x64 (or 32x64) wave tiles of
+//     v_mfma_f32_16x16x32_bf16, one workgroup per CU (3 x 48 KiB ring);
+//   * epilogue: bf16 tile through LDS -> coalesced 16-B row stores, optional BatchNorm statistics
+//     of the bf16-rounded output per (256-row block, channel) for the consuming BN (det_norm.hip
+//     det_bn_fwd_from_partials);
+//   * XCD-aware bijective block remap (blocks sharing an A row-panel on one XCD's L2).
+//
+// Reference parity: convolutions belong to the user's model in the reference (cuDNN through torch,
+// examples/computer_vision/*); semantics are torch.nn.functional.conv2d's.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kBK = 64;       // K tile: one 128-B LDS row per operand row
+constexpr int kStages = 3;    // LDS ring depth
+constexpr int kThreads = 512; // 8 waves
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ int swz(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+struct IgArgs {
+  const unsigned short* X;     // NHWC [Nb, Hi, Wi, Cin] (DENSE: [M, K] rows)
+  const unsigned short* W;     // [N, K], K = R*S*Cin (KRSC)
+  unsigned short* Y;           // [M, N]
+  const unsigned short* zero;  // >= 128 zero bytes, 16-B aligned
+  float* pmean;                // STATS: [ceil(M/BM), N]
+  float* pm2;
+  int64_t M;
+  int N, K, Cin;
+  int Hi, Wi, Ho, Wo, stride, pad, S;
+};
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)(const_cast<void*>(g)), (lds_void*)(lds_wave_base), 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void block_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// DENSE: A rows are X rows (1x1 stride-1 conv / plain GEMM).  Otherwise the conv gather.
+template <int BM, int BN, int WM, int WN, bool DENSE, bool STATS>
+__global__ void __launch_bounds__(kThreads, 1) igemm_kernel(IgArgs a) {
+  constexpr int NW = kThreads / 64;
+  static_assert(WM * WN == NW, "8 waves");
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int AI = BM / 64, BI = BN / 64;  // glds instructions per lane per K tile
+  constexpr int NI = AI + BI;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int LDC = BN + 16;
+  constexpr int RED_OFF = kStages * STAGE;  // stats scratch after the ring (one LDS array: no 2nd __shared__)
+  static_assert(BM * LDC * 2 <= kStages * STAGE, "C tile fits in the ring");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* red = reinterpret_cast<float*>(smem + RED_OFF);  // [WM][BN]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = a.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int64_t m0 = static_cast<int64_t>(mt) * BM;
+  const int n0 = nt * BN;
+  const int64_t K = a.K;
+
+  // lane -> (row within an 8-row glds group, swizzled source chunk): LDS slot (row, lane&7) holds
+  // source chunk (lane&7) ^ (row&7) with row&7 == lane>>3
+  const int lrow = lane >> 3;
+  const int gch = (lane & 7) ^ lrow;
+
+  // per-lane A row descriptors for its AI rows
+  int64_t arow[AI];  // DENSE: element offset of the row start; else pixel base (n*Hi*Wi) or -1
+  int ahi[AI], awi[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (i * NW + wid) * 8 + lrow;
+    const int64_t m = m0 + row;
+    if (DENSE) {
+      arow[i] = m < a.M ? m * K : -1;
+      ahi[i] = awi[i] = 0;
+    } else if (m < a.M) {
+      const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
+      const int64_t n = m / hw;
+      const int rem = static_cast<int>(m - n * hw);
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      arow[i] = n * a.Hi;
+      ahi[i] = ho * a.stride - a.pad;
+      awi[i] = wo * a.stride - a.pad;
+    } else {
+      arow[i] = -1;
+      ahi[i] = awi[i] = 0;
+    }
+  }
+  const unsigned short* bbase = a.W + static_cast<int64_t>(n0) * K + gch * 8;
+  const unsigned short* zsrc = a.zero;
+
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % kStages) * STAGE;
+    const int k0 = kt * kBK;
+    if (DENSE) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const unsigned short* src = arow[i] >= 0 ? a.X + arow[i] + k0 + gch * 8 : zsrc;
+        glds16(src, st + ((i * NW + wid) * 8) * 128);
+      }
+    } else {
+      const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
+      const int r = tap / a.S, s = tap - r * a.S;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int hi = ahi[i] + r, wi = awi[i] + s;
+        const bool ok = arow[i] >= 0 && hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi;
+        const unsigned short* src =
+            ok ? a.X + ((arow[i] + hi) * a.Wi + wi) * static_cast<int64_t>(a.Cin) + c0 + gch * 8 : zsrc;
+        glds16(src, st + ((i * NW + wid) * 8) * 128);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int row = (j * NW + wid) * 8 + lrow;
+      glds16(bbase + static_cast<int64_t>(row) * K + k0, st + A_BYTES + ((j * NW + wid) * 8) * 128);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / kBK;
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vmcnt<NI>();  // tile kt landed (this wave's DMAs); kt+1 may stay in flight
+    else wait_vmcnt<0>();
+    block_barrier();  // every wave's tile-kt DMAs landed; every wave is done reading tile kt-1
+    if (kt + 2 < nk) issue(kt + 2);  // into tile kt-1's buffer
+    const unsigned char* base = smem + (kt % kStages) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(base + swz(wm * TM + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // all fragment reads done before the ring is reused for the C tile
+
+  // ---- epilogue: bf16 tile through LDS (coalesced 16-B row stores) + BN statistics ----
+  unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
+  const int64_t rows_left = a.M - m0;
+  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * TN + j * 16 + (lane & 15);
+        ct[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  if (STATS) {
+    // per-lane (mean, M2) over its rows of each column, Chan-merged across the 4 row groups of the
+    // wave by shuffles and across the WM waves through LDS
+    float cs[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (row < nvalid) s += round_bf(acc[i][j][r]);
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      cs[j] = s;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + j * 16 + lane] = cs[j];
+    }
+    __syncthreads();
+    const float inv_n = 1.f / static_cast<float>(nvalid);
+    float mu[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * TN + j * 16 + (lane & 15);
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + col];
+      mu[j] = s * inv_n;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          const float d = round_bf(acc[i][j][r]) - mu[j];
+          if (row < nvalid) q += d * d;
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) red[wm * BN + wn * TN + j * 16 + lane] = q;
+      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
+    }
+  }
+  __syncthreads();
+  if (STATS && tid < BN) {
+    float q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
+    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
+  }
+  constexpr int CPR = BN / 8;
+#pragma unroll
+  for (int q = 0; q < BM * CPR / kThreads; ++q) {
+    const int idx = tid + q * kThreads;
+    const int row = idx / CPR, cc = idx - row * CPR;
+    if (row < nvalid)
+      *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+  const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
+  constexpr int smem = kStages * (BM + BN) * 128 + 4 * WM * BN;
+#define DET_IG(D, S) \
+  hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, D, S>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a)
+  if (dense) { if (stats) DET_IG(true, true); else DET_IG(true, false); }
+  else { if (stats) DET_IG(false, true); else DET_IG(false, false); }
+#undef DET_IG
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+// Rows per statistics block of det_igemm (the BN finalize needs it).
+int det_igemm_rows_per_block() { return 256; }
+
+// Y[M, N] = conv(X, W) as described at the top.  bf16 NHWC.  Requirements (checked): Cin % 64 == 0,
+// N % 64 == 0, K == R*S*Cin, pointers 16-B aligned, zero -> >= 128 zero bytes.  R == S == 1,
+// stride 1, pad 0 with Hi*Wi == Ho*Wo takes the dense path.  pmean/pm2 (nullable, [ceil(M/256), N]):
+// BatchNorm statistics partials of the bf16-rounded Y.
+int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,
+                   int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* pmean, float* pm2) {
+  if (M <= 0 || N <= 0 || N % 64 != 0 || Cin <= 0 || Cin % 64 != 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
+    return -1;
+  if ((pmean == nullptr) != (pm2 == nullptr) || zero == nullptr) return -2;
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y) |
+        reinterpret_cast<uintptr_t>(zero)) & 15) != 0)
+    return -5;
+  const int64_t hw = static_cast<int64_t>(Ho) * Wo;
+  if (hw <= 0 || M % hw != 0) return -3;
+  const int K = R * S * Cin;
+  IgArgs a{static_cast<const unsigned short*>(X), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(Y),
+           static_cast<const unsigned short*>(zero), pmean, pm2, M, N, K, Cin, Hi, Wi, Ho, Wo, stride, pad, S};
+  const bool dense = R == 1 && S == 1 && stride == 1 && pad == 0 && Hi == Ho && Wi == Wo;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool stats = pmean != nullptr;
+  if (N % 128 == 0) return launch<256, 128, 4, 2>(st, a, dense, stats);
+  return launch<256, 64, 8, 1>(st, a, dense, stats);
+}
+
+}  // extern "C"

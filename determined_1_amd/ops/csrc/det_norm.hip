@@ -270,6 +270,124 @@ bn_stats_finalize(const float* __restrict__ pmean, const float* __restrict__ pm2
   }
 }
 
+// Two-stage finalize for long partial lists (the GEMM-epilogue partials of det_conv.hip come in
+// 128-row blocks: 12,544 rows of partials for a layer1 activation, which one 64-channel block
+// walked serially in ~30 us).  Stage 1 spreads the row-blocks over S slices x C/64 channel blocks
+// and writes fp64 (S1, S2) per (slice, channel); stage 2 merges the S slices in a fixed order
+// (deterministic, no atomics) and applies the same epilogue as bn_stats_finalize.
+constexpr int kMaxSlices = 64;
+
+__global__ void __launch_bounds__(kFinThreads)
+bn_stats_reduce(const float* __restrict__ pmean, const float* __restrict__ pm2, Geom g, int per_slice,
+                double* __restrict__ part) {
+  __shared__ double red1[kFinLanes][kFinCh];
+  __shared__ double red2[kFinLanes][kFinCh];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  const int b0 = blockIdx.y * per_slice;
+  const int b1 = min(g.nrb, b0 + per_slice);
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (ok) {
+    const int last = g.nrb - 1;
+    const double n_full = static_cast<double>(g.rpb);
+    const double n_last = static_cast<double>(g.M - static_cast<int64_t>(last) * g.rpb);
+    int b = b0 + lane;
+    for (; b + 3 * kFinLanes < b1; b += 4 * kFinLanes) {
+      float mv[4], qv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = static_cast<int64_t>(b + u * kFinLanes) * g.C + c;
+        mv[u] = pmean[o];
+        qv[u] = pm2[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double nb = (b + u * kFinLanes) == last ? n_last : n_full;
+        const double m = mv[u];
+        s1[u] += nb * m;
+        s2[u] += static_cast<double>(qv[u]) + nb * m * m;
+      }
+    }
+    for (; b < b1; b += kFinLanes) {
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      const double nb = b == last ? n_last : n_full;
+      const double m = pmean[o];
+      s1[0] += nb * m;
+      s2[0] += static_cast<double>(pm2[o]) + nb * m * m;
+    }
+  }
+  red1[lane][cl] = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+  red2[lane][cl] = (s2[0] + s2[1]) + (s2[2] + s2[3]);
+  __syncthreads();
+  if (lane == 0 && ok) {
+    double t1 = 0, t2 = 0;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) {
+      t1 += red1[q][cl];
+      t2 += red2[q][cl];
+    }
+    const int64_t o = (static_cast<int64_t>(blockIdx.y) * g.C + c) * 2;
+    part[o] = t1;
+    part[o + 1] = t2;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_stats_combine(const double* __restrict__ part, int S, Geom g, FinArgs a) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= g.C) return;
+  double t1 = 0, t2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const int64_t o = (static_cast<int64_t>(s) * g.C + c) * 2;
+    t1 += part[o];
+    t2 += part[o + 1];
+  }
+  const double M = static_cast<double>(g.M);
+  const double meand = t1 / M;
+  double m2 = t2 - M * meand * meand;
+  if (m2 < 0) m2 = 0;
+  const float mean = static_cast<float>(meand);
+  const float var = static_cast<float>(m2 / M);
+  const float rstd = rsqrtf(var + a.eps);
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  const float bt = a.beta ? a.beta[c] : 0.f;
+  const float sc = gm * rstd;
+  a.save_mean[c] = mean;
+  a.save_rstd[c] = rstd;
+  a.scale[c] = sc;
+  a.shift[c] = bt - mean * sc;
+  if (a.running_mean) {
+    float f = a.momentum;
+    if (f < 0.f) f = a.num_batches_tracked ? 1.f / static_cast<float>(*a.num_batches_tracked + 1) : 0.f;
+    const float unbiased = g.M > 1 ? static_cast<float>(m2 / (M - 1.0)) : var;
+    a.running_mean[c] = (1.f - f) * a.running_mean[c] + f * mean;
+    a.running_var[c] = (1.f - f) * a.running_var[c] + f * unbiased;
+  }
+}
+
+// fp32 elements of scratch the two-stage finalize needs for C channels (fp64 pairs per slice)
+inline int64_t fin_scratch_elems(int C) { return static_cast<int64_t>(kMaxSlices) * C * 4; }
+
+// Statistics finalize over g.nrb partial rows: one launch when the list is short, two otherwise.
+void launch_stats_finalize(hipStream_t st, const float* pmean, const float* pm2, const Geom& g, const FinArgs& fa,
+                           float* scratch) {
+  const int cb = (g.C + kFinCh - 1) / kFinCh;
+  int S = 1024 / cb;
+  if (S > kMaxSlices) S = kMaxSlices;
+  const int by_rows = g.nrb / (4 * kFinLanes);  // >= 4 partial rows per lane
+  if (S > by_rows) S = by_rows;
+  if (scratch == nullptr || S < 4) {
+    hipLaunchKernelGGL(bn_stats_finalize, dim3(cb), dim3(kFinThreads), 0, st, pmean, pm2, g, fa);
+    return;
+  }
+  const int per = (g.nrb + S - 1) / S;
+  S = (g.nrb + per - 1) / per;
+  double* part = reinterpret_cast<double*>(scratch);
+  hipLaunchKernelGGL(bn_stats_reduce, dim3(cb, S), dim3(kFinThreads), 0, st, pmean, pm2, g, per, part);
+  hipLaunchKernelGGL(bn_stats_combine, dim3((g.C + 255) / 256), dim3(256), 0, st, part, S, g, fa);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Elementwise apply: y = act(x*scale + shift [+ res]); grid-stride over 8-element vectors, 4 in
 // flight per thread.
@@ -563,8 +681,11 @@ extern "C" {
 // Number of fp32 workspace elements the fwd/bwd entry points need for an [M, C] activation.
 int64_t det_bn_ws_elems(int64_t M, int C) {
   Geom g = make_geom(M, C);
-  return 2 * static_cast<int64_t>(g.nrb) * C + 3 * static_cast<int64_t>(C);
+  return 2 * static_cast<int64_t>(g.nrb) * C + 3 * static_cast<int64_t>(C) + fin_scratch_elems(C);
 }
+
+// fp32 workspace elements det_bn_fwd_from_partials needs (two-stage finalize scratch).
+int64_t det_bn_fin_ws_elems(int C) { return fin_scratch_elems(C); }
 
 // dtype: 0 = fp32, 1 = bf16.  res may be null.  Outputs save_mean/save_rstd/scale/shift [C].
 int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
@@ -587,8 +708,7 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
                        pmean, pm2);
   FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
              save_mean, save_rstd, scale, shift};
-  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, pmean, pm2, g,
-                     fa);
+  launch_stats_finalize(st, pmean, pm2, g, fa, ws + 2 * static_cast<int64_t>(g.nrb) * C + 3 * static_cast<int64_t>(C));
   int64_t* bump = num_batches_tracked;
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
@@ -612,13 +732,15 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
 
 // Training forward when the producer already computed the statistics partials (det_conv.hip GEMM
 // epilogue): Chan-merge the [nrb, C] (mean, M2) partials over row-blocks of `rpb` rows, then apply.
+// ws (nullable, >= det_bn_fin_ws_elems(C) floats, 8-B aligned): scratch of the two-stage finalize.
 // Skips the stats pass over x entirely.  apply = 0 stops after the finalize (the consumer applies
 // scale/shift itself, e.g. in its GEMM prologue); num_batches_tracked is then bumped here.
 int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                              int rpb, int nrb, const float* pmean, const float* pm2, const float* gamma,
                              const float* beta, float* running_mean, float* running_var,
                              int64_t* num_batches_tracked, float momentum, float eps, int relu, int apply,
-                             float* save_mean, float* save_rstd, float* scale, float* shift, uint8_t* mbits) {
+                             float* save_mean, float* save_rstd, float* scale, float* shift, uint8_t* mbits,
+                             float* ws) {
   if (C % 8 != 0 || M <= 0 || rpb <= 0 || nrb != static_cast<int>((M + rpb - 1) / rpb)) return -1;
   if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -627,8 +749,7 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
   g.nrb = nrb;
   FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
              save_mean, save_rstd, scale, shift};
-  hipLaunchKernelGGL(bn_stats_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, pmean, pm2, g,
-                     fa);
+  launch_stats_finalize(st, pmean, pm2, g, fa, ws);
   int64_t* bump = num_batches_tracked;
   if (!apply) {
     if (bump) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, bump);

@@ -77,7 +77,6 @@ class _BNActTrain(torch.autograd.Function):
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         y = torch.empty_like(x, memory_format=fmt)
         stats = torch.empty((4, C), dtype=torch.float32, device=x.device)
-        ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
         if residual is not None:
             residual = residual.to(x.dtype).contiguous(memory_format=fmt)
         mbits = torch.empty(x.numel() // 8, dtype=torch.uint8, device=x.device) \
@@ -85,6 +84,8 @@ class _BNActTrain(torch.autograd.Function):
         from determined_1_amd.ops.conv import take_partials
 
         parts = take_partials(x)  # statistics already computed by the producing GEMM's epilogue
+        ws = torch.empty(int(lib.det_bn_fin_ws_elems(C) if parts is not None else lib.det_bn_ws_elems(M, C)),
+                         dtype=torch.float32, device=x.device)
         if parts is not None:
             pm, pq, rpb = parts
             _lib.check(
@@ -94,6 +95,7 @@ class _BNActTrain(torch.autograd.Function):
                     _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
                     float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)), 1,
                     stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits),
+                    ws.data_ptr(),
                 ),
                 "bn_fwd_from_partials",
             )

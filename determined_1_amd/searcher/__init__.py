@@ -28,6 +28,8 @@ def _lib() -> ctypes.CDLL:
         lib.detcore_nprand.restype = ctypes.c_void_p
         lib.detcore_json_roundtrip.argtypes = [ctypes.c_char_p]
         lib.detcore_json_roundtrip.restype = ctypes.c_void_p
+        lib.detcore_searcher_util.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        lib.detcore_searcher_util.restype = ctypes.c_void_p
         lib.detcore_merge_config.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
         lib.detcore_merge_config.restype = ctypes.c_void_p
         lib._det_searcher_sigs = True
@@ -102,6 +104,32 @@ class Searcher:
 
     def state(self) -> Dict[str, Any]:
         return self._call("state")
+
+
+def searcher_util(name: str, **args: Any) -> Any:
+    """Native searcher helpers the reference pins in its unit tests: ``adaptive_mode``,
+    ``hyperparameter_grid``, ``grid_values``, ``sample_all`` (see also the wrappers below)."""
+    return _take(_lib().detcore_searcher_util(name.encode(), json.dumps(args).encode()))
+
+
+def bracket_max_trials(max_trials: int, divisor: float, brackets: List[int]) -> List[int]:
+    """adaptive_asha per-bracket trial budgets (reference adaptive_asha.go getBracketMaxTrials)."""
+    return _take(_lib().detcore_searcher_util(b"bracket_max_trials", json.dumps(
+        {"max_trials": max_trials, "divisor": divisor, "brackets": brackets}).encode()))
+
+
+def bracket_max_concurrent_trials(max_concurrent_trials: int, divisor: float, bracket_max_trials: List[int]) -> List[int]:
+    """adaptive_asha per-bracket concurrency (reference getBracketMaxConcurrentTrials)."""
+    return _take(_lib().detcore_searcher_util(b"bracket_max_concurrent_trials", json.dumps(
+        {"max_concurrent_trials": max_concurrent_trials, "divisor": divisor,
+         "bracket_max_trials": bracket_max_trials}).encode()))
+
+
+def pbt_explore(pbt_config: Dict[str, Any], hyperparameters: Dict[str, Any], sample: Dict[str, Any],
+                seed: int = 0) -> Dict[str, Any]:
+    """One PBT exploreParams step of ``sample`` with an RNG seeded ``seed`` (reference pbt.go)."""
+    return _take(_lib().detcore_searcher_util(b"pbt_explore", json.dumps(
+        {"config": pbt_config, "hyperparameters": hyperparameters, "sample": sample, "seed": seed}).encode()))
 
 
 def simulate(searcher_config: Dict[str, Any], hyperparameters: Optional[Dict[str, Any]] = None, seed: int = 0,

@@ -131,8 +131,19 @@ class SearchMethod {
   virtual Unit unit() const = 0;
 };
 
-// Build a search method from a (defaulted) searcher config object.
+// Build a search method from a (defaulted) searcher config object.  Besides the nine searcher
+// names, {"name": "tournament", "subs": [cfg, ...]} runs sub-searchers side by side
+// (tournament.go newTournamentSearch, which adaptive/adaptive_simple/adaptive_asha build on).
 std::unique_ptr<SearchMethod> NewSearchMethod(const Json& searcher_config);
+
+// Bracket rung counts of an adaptive mode (adaptive.go conservativeMode/standardMode/aggressiveMode).
+std::vector<int64_t> AdaptiveModeBrackets(const std::string& mode, int64_t max_rungs);
+// adaptive_asha bracket sizing (adaptive_asha.go getBracketMaxTrials / getBracketMaxConcurrentTrials).
+std::vector<int64_t> BracketMaxTrials(int64_t max_trials, double divisor, const std::vector<int64_t>& brackets);
+std::vector<int64_t> BracketMaxConcurrentTrials(int64_t max_concurrent, double divisor,
+                                                const std::vector<int64_t>& bracket_max_trials);
+// PBT exploreParams of `sample` under a pbt searcher config (pbt.go).
+Json PbtExplore(const Json& pbt_searcher_config, Context& ctx, const Json& sample);
 
 // Extract a scalar validation metric (ValidationMetrics.Metric): throws if missing/non-float.
 double ValidationMetric(const Json& validation_metrics, const std::string& name);

@@ -49,6 +49,9 @@ detcore::ValidationFn make_valfn(const Json& spec, uint64_t seed) {
     double sign = spec.get_double("sign", 1.0);
     return [sign](int tid, int) { return sign * static_cast<double>(tid); };
   }
+  if (kind == "trial_id_parity") {  // odd trial ids +id, even -id (pbt_test.go "even_odd")
+    return [](int tid, int) { return tid % 2 == 0 ? -static_cast<double>(tid) : static_cast<double>(tid); };
+  }
   throw std::invalid_argument("unknown validation function kind " + kind);
 }
 
@@ -137,6 +140,50 @@ char* detcore_simulate(const char* searcher_cfg, const char* hparams, uint32_t s
       trials.push_back(t);
     }
     out["trials"] = trials;
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+// Searcher helpers pinned by the reference's unit tests: bracket sizing and PBT explore.
+char* detcore_searcher_util(const char* name, const char* args) {
+  try {
+    Json a = Json::parse(args && *args ? args : "{}");
+    std::string n = name;
+    auto ints = [](const Json& arr) {
+      std::vector<int64_t> v;
+      for (const auto& x : arr.as_array()) v.push_back(x.as_int());
+      return v;
+    };
+    Json out = Json::array();
+    if (n == "bracket_max_trials") {
+      for (auto v : detcore::BracketMaxTrials(a.at("max_trials").as_int(), a.at("divisor").as_double(), ints(a.at("brackets"))))
+        out.push_back(v);
+    } else if (n == "bracket_max_concurrent_trials") {
+      for (auto v : detcore::BracketMaxConcurrentTrials(a.at("max_concurrent_trials").as_int(), a.at("divisor").as_double(),
+                                                        ints(a.at("bracket_max_trials"))))
+        out.push_back(v);
+    } else if (n == "adaptive_mode") {
+      for (auto v : detcore::AdaptiveModeBrackets(a.at("mode").as_string(), a.at("max_rungs").as_int())) out.push_back(v);
+    } else if (n == "hyperparameter_grid") {
+      for (auto& v : detcore::HyperparameterGrid(a.at("hyperparameters"))) out.push_back(v);
+    } else if (n == "grid_values") {
+      for (auto& v : detcore::GridValues(a.at("hyperparameter"))) out.push_back(v);
+    } else if (n == "sample_all") {  // {"sample": ..., "next_bits64": RNG state probe after sampling}
+      detcore::NpRand r(static_cast<uint32_t>(a.get_int("seed", 0)));
+      Json o = Json::object();
+      o["sample"] = detcore::SampleAll(a.at("hyperparameters"), r);
+      o["next_bits64"] = std::to_string(r.Bits64());
+      return dup(o.dump());
+    } else if (n == "pbt_explore") {
+      detcore::NpRand r(static_cast<uint32_t>(a.get_int("seed", 0)));
+      Json hp = a["hyperparameters"];
+      detcore::Context ctx{r, hp};
+      return dup(detcore::PbtExplore(a.at("config"), ctx, a.at("sample")).dump());
+    } else {
+      throw std::invalid_argument("unknown searcher util " + n);
+    }
     return dup(out.dump());
   } catch (const std::exception& e) {
     return err(e);

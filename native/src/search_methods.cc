@@ -485,6 +485,42 @@ class PBTSearch : public SearchMethod {
   }
   Unit unit() const override { return cfg_.length_per_round.unit; }
 
+  // exploreParams (pbt.go): resample each hyperparameter with resample_probability, else perturb
+  // numeric ones by (1 +- perturb_factor) clamped to their range; sorted-name RNG order.
+  Json Explore(Context& ctx, const Json& old) {
+    Json out = Json::object();
+    if (!ctx.hparams.is_object()) return out;
+    for (const auto& kv : ctx.hparams.as_object()) {
+      const std::string& name = kv.first;
+      const Json& hp = kv.second;
+      if (ctx.rand.UnitInterval() < cfg_.resample_probability) {
+        out[name] = SampleOne(hp, ctx.rand);
+        continue;
+      }
+      Json val = old[name];
+      bool decrease = ctx.rand.UnitInterval() < .5;
+      double mult = decrease ? 1 - cfg_.perturb_factor : 1 + cfg_.perturb_factor;
+      std::string t = hp.is_object() ? hp.get_string("type", "") : "";
+      if (t == "int") {
+        double v = static_cast<double>(val.as_int()) * mult;
+        int64_t iv = static_cast<int64_t>(decrease ? std::floor(v) : std::ceil(v));
+        iv = std::min(std::max(iv, hp.at("minval").as_int()), hp.at("maxval").as_int());
+        val = Json(iv);
+      } else if (t == "double") {
+        double v = val.as_double() * mult;
+        v = std::min(std::max(v, hp.at("minval").as_double()), hp.at("maxval").as_double());
+        val = Json(v);
+      } else if (t == "log") {
+        double base = hp.at("base").as_double();
+        double lo = std::pow(base, hp.at("minval").as_double()), hi = std::pow(base, hp.at("maxval").as_double());
+        double v = std::min(std::max(val.as_double() * mult, lo), hi);
+        val = Json(v);
+      }
+      out[name] = val;
+    }
+    return out;
+  }
+
  private:
   Ops RunNewTrials(Context& ctx, const RequestID& rid) {
     Ops ops;
@@ -528,40 +564,6 @@ class PBTSearch : public SearchMethod {
       }
     }
     return ops;
-  }
-
-  Json Explore(Context& ctx, const Json& old) {
-    Json out = Json::object();
-    if (!ctx.hparams.is_object()) return out;
-    for (const auto& kv : ctx.hparams.as_object()) {
-      const std::string& name = kv.first;
-      const Json& hp = kv.second;
-      if (ctx.rand.UnitInterval() < cfg_.resample_probability) {
-        out[name] = SampleOne(hp, ctx.rand);
-        continue;
-      }
-      Json val = old[name];
-      bool decrease = ctx.rand.UnitInterval() < .5;
-      double mult = decrease ? 1 - cfg_.perturb_factor : 1 + cfg_.perturb_factor;
-      std::string t = hp.is_object() ? hp.get_string("type", "") : "";
-      if (t == "int") {
-        double v = static_cast<double>(val.as_int()) * mult;
-        int64_t iv = static_cast<int64_t>(decrease ? std::floor(v) : std::ceil(v));
-        iv = std::min(std::max(iv, hp.at("minval").as_int()), hp.at("maxval").as_int());
-        val = Json(iv);
-      } else if (t == "double") {
-        double v = val.as_double() * mult;
-        v = std::min(std::max(v, hp.at("minval").as_double()), hp.at("maxval").as_double());
-        val = Json(v);
-      } else if (t == "log") {
-        double base = hp.at("base").as_double();
-        double lo = std::pow(base, hp.at("minval").as_double()), hi = std::pow(base, hp.at("maxval").as_double());
-        double v = std::min(std::max(val.as_double() * mult, lo), hi);
-        val = Json(v);
-      }
-      out[name] = val;
-    }
-    return out;
   }
 
   PbtConfig cfg_;
@@ -643,10 +645,47 @@ std::vector<int64_t> bracket_max_concurrent(int64_t max_conc, double divisor, co
   return out;
 }
 
+PbtConfig pbt_config(const Json& c) {
+  PbtConfig p;
+  p.metric = c.get_string("metric", "");
+  p.smaller_is_better = c.get_bool("smaller_is_better", true);
+  p.population_size = c.at("population_size").as_int();
+  p.num_rounds = c.at("num_rounds").as_int();
+  p.length_per_round = Length::FromJson(c.at("length_per_round"));
+  p.truncate_fraction = c["replace_function"].get_double("truncate_fraction", 0);
+  p.resample_probability = c["explore_function"].get_double("resample_probability", 0);
+  p.perturb_factor = c["explore_function"].get_double("perturb_factor", 0);
+  return p;
+}
+
 }  // namespace
+
+std::vector<int64_t> AdaptiveModeBrackets(const std::string& mode, int64_t max_rungs) {
+  return adaptive_brackets(mode, max_rungs);
+}
+
+std::vector<int64_t> BracketMaxTrials(int64_t max_trials, double divisor, const std::vector<int64_t>& brackets) {
+  return bracket_max_trials(max_trials, divisor, brackets);
+}
+
+std::vector<int64_t> BracketMaxConcurrentTrials(int64_t max_concurrent, double divisor,
+                                                const std::vector<int64_t>& bracket_max_trials) {
+  return bracket_max_concurrent(max_concurrent, divisor, bracket_max_trials);
+}
+
+Json PbtExplore(const Json& pbt_searcher_config, Context& ctx, const Json& sample) {
+  PBTSearch p(pbt_config(pbt_searcher_config));
+  return p.Explore(ctx, sample);
+}
 
 std::unique_ptr<SearchMethod> NewSearchMethod(const Json& c) {
   const std::string name = c.get_string("name", "");
+  if (name == "tournament") {  // newTournamentSearch(subs...): arbitrary sub-searchers side by side
+    std::vector<std::unique_ptr<SearchMethod>> subs;
+    for (const auto& sc : c.at("subs").as_array()) subs.push_back(NewSearchMethod(sc));
+    if (subs.empty()) throw std::invalid_argument("tournament needs at least one sub-searcher");
+    return std::make_unique<TournamentSearch>(std::move(subs));
+  }
   if (name == "single") return std::make_unique<RandomSearch>(1, Length::FromJson(c.at("max_length")));
   if (name == "random")
     return std::make_unique<RandomSearch>(c.at("max_trials").as_int(), Length::FromJson(c.at("max_length")));
@@ -720,18 +759,7 @@ std::unique_ptr<SearchMethod> NewSearchMethod(const Json& c) {
     }
     return std::make_unique<TournamentSearch>(std::move(subs));
   }
-  if (name == "pbt") {
-    PbtConfig p;
-    p.metric = c.get_string("metric", "");
-    p.smaller_is_better = c.get_bool("smaller_is_better", true);
-    p.population_size = c.at("population_size").as_int();
-    p.num_rounds = c.at("num_rounds").as_int();
-    p.length_per_round = Length::FromJson(c.at("length_per_round"));
-    p.truncate_fraction = c["replace_function"].get_double("truncate_fraction", 0);
-    p.resample_probability = c["explore_function"].get_double("resample_probability", 0);
-    p.perturb_factor = c["explore_function"].get_double("perturb_factor", 0);
-    return std::make_unique<PBTSearch>(p);
-  }
+  if (name == "pbt") return std::make_unique<PBTSearch>(pbt_config(c));
   throw std::invalid_argument("no searcher type specified (searcher.name=" + name + ")");
 }
 

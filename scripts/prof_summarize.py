@@ -1,4 +1,4 @@
-"""Steady-state per-step kernel summary from a rocprofv3 kernel trace.
+"""Steady-state per-step kernel summary from a rocprofv3 kernel trace (CSV or rocpd ``.db``).
 
     python scripts/prof_summarize.py gpurun_out/prof/bench_kernel_trace.csv --step-kernel opt_kernel \
         [--skip-steps 3] [--out profiles/x.csv]
@@ -31,9 +31,15 @@ def main() -> None:
     ap.add_argument("--out")
     args = ap.parse_args()
     rows = []
-    with open(args.trace) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    if args.trace.endswith(".db"):  # rocprofv3 >= 7 default output (rocpd sqlite)
+        import sqlite3
+
+        con = sqlite3.connect(args.trace)
+        rows = [(int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels")]
+    else:
+        with open(args.trace) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     last_find = max((i for i, r in enumerate(rows) if "naive_conv" in r[2]), default=-1)
     # one step = the run of consecutive optimizer launches (one per arena) that ends it

@@ -140,3 +140,30 @@ def test_resnet50_native_conv1x1_matches_miopen(gpu):
     assert nc.COUNTS["native"] - before >= 3 * 32  # 32 stride-1 1x1 convs per ResNet-50 forward
     for a, b in zip(got, ref):
         assert abs(a - b) < 0.05 * max(1.0, abs(b)), (got, ref)
+
+
+@pytest.mark.parametrize("m,cout", [(65536 + 40, 256), (200704, 64)])
+def test_conv_stats_feed_bn_two_stage_finalize(gpu, m, cout):
+    """GEMM-epilogue statistics of a long activation (hundreds of 128-row partial blocks) through
+    the two-stage BN finalize: batch mean/var, running stats and the normalized output match
+    torch.batch_norm on the same bf16 conv output."""
+    from determined_1_amd.ops import norm
+
+    torch.manual_seed(3)
+    cin = 64
+    x = (torch.randn(m, cin, device=gpu) + 0.3).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, device=gpu) / cin ** 0.5).to(torch.bfloat16)
+    conv_mod = torch.nn.Conv2d(cin, cout, 1, bias=False).to(gpu).to(torch.bfloat16)
+    with torch.no_grad():
+        conv_mod.weight.copy_(w.view(cout, cin, 1, 1))
+    x4 = x.view(1, m, 1, cin).permute(0, 3, 1, 2)  # channels_last view [1, cin, m, 1]
+    bn = norm.BatchNormAct2d(cout, relu=False, fused=True).to(gpu)
+    ref_bn = norm.BatchNormAct2d(cout, relu=False, fused=False).to(gpu)
+    with torch.no_grad():
+        y = conv.conv1x1(x4, conv_mod)
+        out = bn(y)
+        yr = (x.float() @ w.float().t()).to(torch.bfloat16).float().view(1, m, 1, cout).permute(0, 3, 1, 2)
+        ref = torch.nn.functional.batch_norm(yr, ref_bn.running_mean, ref_bn.running_var, None, None, True, 0.1, bn.eps)
+    torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=3e-2)

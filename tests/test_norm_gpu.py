@@ -18,6 +18,7 @@ CASES = [
     (5, 512, 13, 11, True, True, torch.bfloat16),
     (2, 40, 5, 5, True, False, torch.float32),  # C not a power of two (C % 8 == 0)
     (1000, 128, 1, 1, False, True, torch.float32),  # tall-skinny, many row blocks
+    (8, 64, 224, 224, True, True, torch.bfloat16),  # 401k rows: two-stage statistics finalize
 ]
 
 
@@ -55,9 +56,16 @@ def test_bn_act_train_matches_reference(gpu, case):
     assert norm.FALLBACKS["count"] == before, "fused path fell back to the composite"
     tol = dict(atol=2e-4, rtol=2e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(yd.float().cpu(), yr, **tol)
-    torch.testing.assert_close(dxd.float().cpu(), dxr, **tol)
-    if use_res:
-        torch.testing.assert_close(drd.float().cpu(), drr, **tol)
+    if x.numel() > 10_000_000:
+        # at 25M elements a few pre-activations land within rounding of 0 and take the other ReLU
+        # branch than the fp32 reference: allow a handful of elements (< 1e-6) to flip
+        for got, want in ((dxd, dxr), (drd, drr)) if use_res else ((dxd, dxr),):
+            bad = ~torch.isclose(got.float().cpu(), want, **tol)
+            assert int(bad.sum()) <= max(4, x.numel() // 1_000_000), int(bad.sum())
+    else:
+        torch.testing.assert_close(dxd.float().cpu(), dxr, **tol)
+        if use_res:
+            torch.testing.assert_close(drd.float().cpu(), drr, **tol)
     gtol = dict(atol=1e-3 * (n * h * w) ** 0.5, rtol=1e-3) if dt == torch.float32 else dict(atol=2e-2 * (n * h * w) ** 0.5, rtol=2e-2)
     torch.testing.assert_close(dwd.cpu(), dwr, **gtol)
     torch.testing.assert_close(dbd.cpu(), dbr, **gtol)
