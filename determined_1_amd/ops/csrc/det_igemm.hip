@@ -25,17 +25,24 @@
 //     det_bn_fwd_from_partials);
 //   * XCD-aware bijective block remap (blocks sharing an A row-panel on one XCD's L2).
 //
+// Measured (profiles/r2_igemm_microbench.jsonl, ResNet-50 bs512 forward shapes on MI355X): ~590 TF/s
+// on every 3x3 (118 GFLOP each), 130-720 TF/s on the 1x1s.  That beats the register-staged det_conv
+// GEMM on the K >= 256 1x1 shapes by 5-20 % but not MIOpen's 3x3 forward (700-880 TF/s), so the
+// ResNet model does not route through it yet; the next step is the 2-phase-per-K-step interleave
+// (ds_read || glds || MFMA) that the one-barrier-per-K-step loop here lacks.
+//
 // Reference parity: convolutions belong to the user's model in the reference (cuDNN through torch,
 // examples/computer_vision/*); semantics are torch.nn.functional.conv2d's.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int kBK = 64;       // K tile: one 128-B LDS row per operand row
 constexpr int kStages = 3;    // LDS ring depth
-constexpr int kThreads = 512; // 8 waves
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -84,12 +91,13 @@ __device__ __forceinline__ void block_barrier() {
 }
 
 // DENSE: A rows are X rows (1x1 stride-1 conv / plain GEMM).  Otherwise the conv gather.
+// WM x WN waves of 64 lanes; each wave owns a (BM/WM) x (BN/WN) accumulator tile.
 template <int BM, int BN, int WM, int WN, bool DENSE, bool STATS>
-__global__ void __launch_bounds__(kThreads, 1) igemm_kernel(IgArgs a) {
-  constexpr int NW = kThreads / 64;
-  static_assert(WM * WN == NW, "8 waves");
+__global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
+  constexpr int NW = WM * WN, kThreads = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
-  constexpr int AI = BM / 64, BI = BN / 64;  // glds instructions per lane per K tile
+  constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // glds instructions per lane per K tile
+  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows split evenly over the waves");
   constexpr int NI = AI + BI;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int LDC = BN + 16;
@@ -181,21 +189,26 @@ __global__ void __launch_bounds__(kThreads, 1) igemm_kernel(IgArgs a) {
     block_barrier();  // every wave's tile-kt DMAs landed; every wave is done reading tile kt-1
     if (kt + 2 < nk) issue(kt + 2);  // into tile kt-1's buffer
     const unsigned char* base = smem + (kt % kStages) * STAGE;
+    // both 32-deep k halves' fragments are read up front (two register sets): the second half's
+    // ds_reads are in flight under the first half's MFMAs
+    bf16x8 af[2][FM], bfr[2][FN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(base + swz(wm * TM + i * 16 + (lane & 15), ch));
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(base + swz(wm * TM + i * 16 + (lane & 15), ch));
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+        bfr[ks][j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
   }
   __syncthreads();  // all fragment reads done before the ring is reused for the C tile
 
@@ -283,6 +296,7 @@ __global__ void __launch_bounds__(kThreads, 1) igemm_kernel(IgArgs a) {
 
 template <int BM, int BN, int WM, int WN>
 int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+  constexpr int kThreads = WM * WN * 64;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int smem = kStages * (BM + BN) * 128 + 4 * WM * BN;
@@ -321,6 +335,15 @@ int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const vo
   const bool dense = R == 1 && S == 1 && stride == 1 && pad == 0 && Hi == Ho && Wi == Wo;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool stats = pmean != nullptr;
+  static const int waves = [] {
+    const char* e = std::getenv("DET_IGEMM_WAVES");
+    return e ? std::atoi(e) : 8;
+  }();
+  if (waves == 4) {  // A/B: one wave per SIMD, 128 x 64 wave tiles (measured ~25 % slower: the
+                     // per-K-step barrier + fragment-read latency is exposed with no partner wave)
+    if (N % 128 == 0) return launch<256, 128, 2, 2>(st, a, dense, stats);
+    return launch<256, 64, 4, 1>(st, a, dense, stats);
+  }
   if (N % 128 == 0) return launch<256, 128, 4, 2>(st, a, dense, stats);
   return launch<256, 64, 8, 1>(st, a, dense, stats);
 }

@@ -27,8 +27,10 @@ struct Slot {
 struct Agent {
   std::string id;
   std::string label;
+  std::string address;  // tie-break identity (reference: the agent actor's address); empty = id
   std::vector<Slot> slots;
   int zero_slot_tasks = 0;
+  int max_zero_slot_tasks = 100;  // master max_zero_slot_containers_per_agent
   bool enabled = true;
   int NumSlots() const;
   int NumEmptySlots() const;
@@ -41,7 +43,11 @@ struct Group {
   double weight = 1.0;
   std::optional<int> priority;  // smaller = more important (priority scheduler)
   int max_slots = -1;           // -1: unlimited
+  int64_t registered_seq = 0;   // registration order (the group actor's registration time)
 };
+
+constexpr int kDefaultPriority = 42;          // model.DefaultSchedulingPriority
+constexpr int kMaxUserPriority = 99;          // model.MaxUserSchedulingPriority
 
 struct Fit {
   std::string agent;
@@ -75,8 +81,10 @@ class PoolState {
   std::map<std::string, Group> groups;
   std::map<std::string, Task> tasks;
   int64_t next_seq = 0;
+  int64_t next_group_seq = 0;
   bool preemption = true;  // priority scheduler preemption
 
+  Group& EnsureGroup(const std::string& id);  // creates it (weight 1, registered now) if new
   void AddTask(Task t);
   void RemoveTask(const std::string& id);  // frees its slots
   // Commit an allocation (marks devices busy).
@@ -85,8 +93,12 @@ class PoolState {
   int Capacity(const std::string& label) const;
 };
 
-// Gang placement for one task against the current agents (fitting.go:70 findFits).
+// Gang placement for one task against the current agents (fitting.go:70 findFits): one agent
+// holding the whole gang (best score, then md5 hash distance, then address), else fully unused
+// agents of one size dividing the gang.
 std::optional<std::vector<Fit>> FindFits(const Task& t, const std::map<std::string, Agent>& agents, FitMethod m);
+// Soft-constraint score of placing `t` on `a` (fitting_methods.go BestFit / WorstFit).
+double FitScore(const Task& t, const Agent& a, FitMethod m);
 
 Decision Schedule(PoolState& st, Policy p, FitMethod m);
 Policy ParsePolicy(const std::string& s);

@@ -7,6 +7,7 @@
 
 #include "detcore/config.h"
 #include "detcore/json.h"
+#include "detcore/scheduler.h"
 #include "detcore/searcher.h"
 
 using detcore::Json;
@@ -141,6 +142,204 @@ char* detcore_simulate(const char* searcher_cfg, const char* hparams, uint32_t s
     }
     out["trials"] = trials;
     return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Scheduler state from a JSON scenario in the shape of the reference's resource-manager test
+// fixtures (resourcemanagers/scheduler_test.go mockAgent / mockGroup / mockTask):
+//   agents: [{id, label, slots, slots_used, max_zero_slot_containers, zero_slot_containers}]
+//   groups: [{id, weight (default 0), max_slots (default none), priority (default none)}]
+//   tasks:  [{id, group (default: its own group), slots_needed, label, non_preemptible,
+//             allocated_agent, container_started}]
+// Groups register first (in order), then each task (and its own implicit group), as the fixtures
+// create their actors.  An allocated task whose container has not started holds no devices.
+namespace sched_api {
+using namespace detcore::sched;
+
+Agent MakeAgent(const Json& j) {
+  Agent a;
+  a.id = j.at("id").as_string();
+  a.label = j.get_string("label", "");
+  a.address = j.get_string("address", "/" + a.id);
+  a.max_zero_slot_tasks = static_cast<int>(j.get_int("max_zero_slot_containers", 0));
+  const int n = static_cast<int>(j.get_int("slots", 0)), used = static_cast<int>(j.get_int("slots_used", 0));
+  for (int i = 0; i < n; ++i) a.slots.push_back(Slot{i, a.id + "-" + std::to_string(i), "gpu", true, i < used ? "used" : ""});
+  a.zero_slot_tasks = static_cast<int>(j.get_int("zero_slot_containers", 0));
+  return a;
+}
+
+Task MakeTask(const Json& j) {
+  Task t;
+  t.id = j.at("id").as_string();
+  t.group = j.get_string("group", t.id);
+  t.label = j.get_string("label", "");
+  t.slots_needed = static_cast<int>(j.get_int("slots_needed", 0));
+  t.non_preemptible = j.get_bool("non_preemptible", false);
+  t.single_agent = j.get_bool("single_agent", false);
+  return t;
+}
+
+void AddTasks(PoolState& st, const Json& tasks) {
+  for (const auto& j : tasks.as_array()) {
+    Task t = MakeTask(j);
+    if (!st.groups.count(t.id)) st.EnsureGroup(t.id).weight = 0.0;  // every task actor is also a group
+    if (!st.groups.count(t.group)) st.EnsureGroup(t.group).weight = 0.0;
+    const std::string agent = j.get_string("allocated_agent", "");
+    st.AddTask(t);
+    if (agent.empty()) continue;
+    Task& tt = st.tasks.at(t.id);
+    Fit f{agent, {}};
+    if (j.get_bool("container_started", false)) {
+      Agent& ag = st.agents.at(agent);
+      if (t.slots_needed == 0) ++ag.zero_slot_tasks;
+      for (auto& sl : ag.slots)
+        if (sl.task.empty() && static_cast<int>(f.devices.size()) < t.slots_needed) {
+          sl.task = t.id;
+          f.devices.push_back(sl.device_id);
+        }
+      if (static_cast<int>(f.devices.size()) != t.slots_needed) throw std::invalid_argument("over allocated to agent " + agent);
+    }
+    tt.allocation = {f};
+  }
+}
+
+PoolState MakeState(const Json& a) {
+  PoolState st;
+  st.preemption = a.get_bool("preemption", false);
+  if (a["agents"].is_array())
+    for (const auto& j : a["agents"].as_array()) {
+      Agent ag = MakeAgent(j);
+      st.agents[ag.id] = ag;
+    }
+  if (a["groups"].is_array())
+    for (const auto& j : a["groups"].as_array()) {
+      Group& g = st.EnsureGroup(j.at("id").as_string());
+      g.weight = j.get_double("weight", 0.0);
+      g.max_slots = j["max_slots"].is_null() ? -1 : static_cast<int>(j["max_slots"].as_int());
+      if (!j["priority"].is_null()) g.priority = static_cast<int>(j["priority"].as_int());
+    }
+  if (a["tasks"].is_array()) AddTasks(st, a["tasks"]);
+  return st;
+}
+
+Json FitsJson(const std::vector<Fit>& fits) {
+  Json out = Json::array();
+  for (auto& f : fits) {
+    Json e = Json::array();
+    e.push_back(f.agent);
+    e.push_back(static_cast<int64_t>(f.devices.size()));
+    out.push_back(e);
+  }
+  return out;
+}
+}  // namespace sched_api
+
+// Stateful scenario (multi-step tests): "schedule" {policy, fit}; "allocate" {tasks} (fit with
+// BestFit on the live agents and commit, the fixtures' AllocateTasks); "add_tasks" {tasks};
+// "remove" {task, delete} (free devices; delete=false leaves it pending, RemoveTask); "state".
+void* detcore_sched_new(const char* args, char** error) {
+  try {
+    auto* st = new sched_api::PoolState(sched_api::MakeState(Json::parse(args && *args ? args : "{}")));
+    if (error) *error = nullptr;
+    return st;
+  } catch (const std::exception& e) {
+    if (error) *error = dup(e.what());
+    return nullptr;
+  }
+}
+
+void detcore_sched_free(void* h) { delete static_cast<sched_api::PoolState*>(h); }
+
+char* detcore_sched_do(void* h, const char* op, const char* args) {
+  try {
+    using namespace sched_api;
+    PoolState& st = *static_cast<PoolState*>(h);
+    Json a = Json::parse(args && *args ? args : "{}");
+    std::string o = op;
+    Json out = Json::object();
+    if (o == "schedule") {
+      if (a.has("preemption")) st.preemption = a.get_bool("preemption", false);
+      Decision d = Schedule(st, ParsePolicy(a.get_string("policy", "fair_share")), ParseFitMethod(a.get_string("fit", "best")));
+      Json alloc = Json::array(), rel = Json::array();
+      for (auto& x : d.allocate) alloc.push_back(x.first);
+      for (auto& r : d.release) rel.push_back(r);
+      out["allocate"] = alloc;
+      out["release"] = rel;
+    } else if (o == "allocate") {
+      for (const auto& id : a.at("tasks").as_array()) {
+        const Task& t = st.tasks.at(id.as_string());
+        auto fits = FindFits(t, st.agents, FitMethod::BestFit);
+        if (!fits) throw std::invalid_argument("no fit for " + t.id);
+        st.Allocate(t.id, *fits);
+      }
+    } else if (o == "add_tasks") {
+      AddTasks(st, a.at("tasks"));
+    } else if (o == "remove") {
+      const std::string id = a.at("task").as_string();
+      if (a.get_bool("delete", true)) {
+        st.RemoveTask(id);
+      } else {
+        Task& t = st.tasks.at(id);
+        for (auto& f : t.allocation) {
+          auto ag = st.agents.find(f.agent);
+          if (ag == st.agents.end()) continue;
+          if (t.slots_needed == 0 && !f.devices.empty()) continue;
+          if (t.slots_needed == 0) ag->second.zero_slot_tasks = std::max(0, ag->second.zero_slot_tasks - 1);
+          for (auto& sl : ag->second.slots)
+            if (sl.task == id) sl.task.clear();
+        }
+        t.allocation.clear();
+      }
+    } else if (o == "state") {
+      Json ag = Json::object();
+      for (auto& kv : st.agents) ag[kv.first] = kv.second.NumEmptySlots();
+      out["empty_slots"] = ag;
+      out["num_tasks"] = static_cast<int64_t>(st.tasks.size());
+    } else {
+      throw std::invalid_argument("unknown scheduler op " + o);
+    }
+    return dup(out.dump());
+  } catch (const std::exception& e) {
+    return err(e);
+  }
+}
+
+char* detcore_sched_call(const char* op, const char* args) {
+  try {
+    using namespace sched_api;
+    Json a = Json::parse(args && *args ? args : "{}");
+    std::string o = op;
+    const FitMethod fm = ParseFitMethod(a.get_string("fit", "best"));
+    if (o == "fit_score") {
+      Task t;
+      t.slots_needed = static_cast<int>(a.get_int("slots_needed", 0));
+      Json out = FitScore(t, MakeAgent(a.at("agent")), fm);
+      return dup(out.dump());
+    }
+    if (o == "find_fits") {
+      PoolState st = MakeState(a);
+      auto fits = FindFits(MakeTask(a.at("task")), st.agents, fm);
+      return dup((fits ? FitsJson(*fits) : Json::array()).dump());
+    }
+    if (o == "schedule") {
+      PoolState st = MakeState(a);
+      Decision d = Schedule(st, ParsePolicy(a.get_string("policy", "fair_share")), fm);
+      Json out = Json::object();
+      Json alloc = Json::array(), fits = Json::object(), rel = Json::array();
+      for (auto& x : d.allocate) {
+        alloc.push_back(x.first);
+        fits[x.first] = FitsJson(x.second);
+      }
+      for (auto& r : d.release) rel.push_back(r);
+      out["allocate"] = alloc;
+      out["release"] = rel;
+      out["fits"] = fits;
+      return dup(out.dump());
+    }
+    throw std::invalid_argument("unknown scheduler op " + o);
   } catch (const std::exception& e) {
     return err(e);
   }

@@ -84,8 +84,7 @@ void ResourcePoolActor::Receive(Context& ctx) {
     released_.erase(rel->task_id);
     Kick(ctx);
   } else if (auto g = ctx.As<SetGroup>()) {
-    sched::Group& grp = st_.groups[g->group];
-    grp.id = g->group;
+    sched::Group& grp = st_.EnsureGroup(g->group);
     grp.weight = g->weight;
     grp.priority = g->priority;
     grp.max_slots = g->max_slots;

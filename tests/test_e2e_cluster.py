@@ -90,8 +90,12 @@ def test_pause_activate_and_cancel(cluster):
                                           hyperparameters={"global_batch_size": 4, "sleep": 0.05}))
     time.sleep(2.0)
     cl.set_state(eid, "PAUSED")
-    time.sleep(2.0)
-    agents = cl.get("/agents")
+    deadline = time.time() + 20.0  # the trial checkpoints and exits first (slow under a loaded box)
+    while True:
+        agents = cl.get("/agents")
+        if all(not s["task"] for a in agents for s in a["slots"]) or time.time() > deadline:
+            break
+        time.sleep(0.2)
     assert all(not s["task"] for a in agents for s in a["slots"]), "paused experiment still holds slots"
     cl.set_state(eid, "ACTIVE")
     time.sleep(1.5)
