@@ -223,6 +223,17 @@ struct TrialSpec {
   int64_t trial_id = 0;  // non-zero when restored
 };
 
+// Rendezvous information every rank of a distributed trial receives (reference trial.go
+// pushRendezvous / rendezvousInfoMessage): the chief-first list of "host:port" addresses of each
+// container's rendezvous port (1734 + its lowest device id, the slot-offset port the harness
+// binds) and the second list 16 ports higher, identical for every rank but the rank itself.
+struct RendezvousMember {
+  int rank = 0;
+  std::string host;
+  std::vector<int> devices;
+};
+Json RendezvousInfo(std::vector<RendezvousMember> members, int rank);
+
 class TrialActor : public actor::Actor {
  public:
   TrialActor(Master* m, actor::Ref exp, int64_t exp_id, Json config, std::string pool, TrialSpec spec,

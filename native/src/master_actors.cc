@@ -697,28 +697,34 @@ void TrialActor::OnContainerState(Context& ctx, const ContainerStateMsg& cs) {
   }
 }
 
+Json RendezvousInfo(std::vector<RendezvousMember> members, int rank) {
+  std::stable_sort(members.begin(), members.end(),
+                   [](const RendezvousMember& a, const RendezvousMember& b) { return a.rank < b.rank; });
+  Json addrs = Json::array(), addrs2 = Json::array();
+  for (const auto& m : members) {
+    const int offset = m.devices.empty() ? 0 : *std::min_element(m.devices.begin(), m.devices.end());
+    addrs.push_back(m.host + ":" + std::to_string(1734 + offset));
+    addrs2.push_back(m.host + ":" + std::to_string(1734 + offset + 16));
+  }
+  Json msg = Json::object();
+  msg["type"] = "RENDEZVOUS_INFO";
+  msg["addrs"] = addrs;
+  msg["addrs2"] = addrs2;
+  msg["rank"] = rank;
+  return msg;
+}
+
 void TrialActor::MaybeRendezvous(Context& ctx) {
   if (rendezvous_done_ || containers_.empty()) return;
+  std::vector<RendezvousMember> members;
   for (auto& cid : order_) {
     const Container& c = containers_[cid];
     if (c.state != "Running" || !c.ws) return;
-  }
-  Json addrs = Json::array(), addrs2 = Json::array();
-  for (auto& cid : order_) {
-    const Container& c = containers_[cid];
-    std::string host = c.address.empty() ? m_->AgentHost(c.agent) : c.address;
-    int offset = c.devices.empty() ? 0 : *std::min_element(c.devices.begin(), c.devices.end());
-    addrs.push_back(host + ":" + std::to_string(1734 + offset));
-    addrs2.push_back(host + ":" + std::to_string(1734 + offset + 16));
+    members.push_back(RendezvousMember{c.rank, c.address.empty() ? m_->AgentHost(c.agent) : c.address, c.devices});
   }
   for (auto& cid : order_) {
     const Container& c = containers_[cid];
-    Json msg = Json::object();
-    msg["type"] = "RENDEZVOUS_INFO";
-    msg["addrs"] = addrs;
-    msg["addrs2"] = addrs2;
-    msg["rank"] = c.rank;
-    c.ws->Send(msg.dump());
+    c.ws->Send(RendezvousInfo(members, c.rank).dump());
   }
   rendezvous_done_ = true;
   // the initial workload travels in DET_INITIAL_WORKLOAD; the harness answers it first

@@ -153,3 +153,112 @@ TEST(length_conversions) {
   EXPECT(EqualWithinBatch(Length(Unit::Records, 650), 10, c));
   EXPECT(!EqualWithinBatch(Length(Unit::Records, 704), 10, c));
 }
+
+// ---- named counterparts of master/internal/trial_workload_sequencer_test.go ----------------
+namespace {
+Workload W(Workload::Kind k, int64_t step, int64_t nb, int64_t total) {
+  Workload w;
+  w.kind = k;
+  w.experiment_id = 1;
+  w.trial_id = 1;
+  w.step_id = step;
+  w.num_batches = nb;
+  w.total_batches_processed = total;
+  return w;
+}
+bool Same(const Workload& a, const Workload& b) {
+  return a.kind == b.kind && a.experiment_id == b.experiment_id && a.trial_id == b.trial_id && a.step_id == b.step_id &&
+         a.num_batches == b.num_batches && a.total_batches_processed == b.total_batches_processed;
+}
+}  // namespace
+
+TEST(TestTrialWorkloadSequencer) {
+  const int64_t su = 100;  // DefaultExperimentConfig().SchedulingUnit
+  using K = Workload::Kind;
+  Workload train1 = W(K::RunStep, 1, su, 0), train2 = W(K::RunStep, 2, su, su), train3 = W(K::RunStep, 3, su, 2 * su),
+           train4 = W(K::RunStep, 4, su, 3 * su), train5 = W(K::RunStep, 5, su, 4 * su);
+  Workload ckpt1 = W(K::CheckpointModel, 1, 0, su), ckpt2 = W(K::CheckpointModel, 2, 0, 2 * su),
+           ckpt4 = W(K::CheckpointModel, 4, 0, 4 * su), ckpt5 = W(K::CheckpointModel, 5, 0, 5 * su);
+  Workload val2 = W(K::ComputeValidationMetrics, 2, 0, 2 * su), val4 = W(K::ComputeValidationMetrics, 4, 0, 4 * su),
+           val5 = W(K::ComputeValidationMetrics, 5, 0, 5 * su);
+  NpRand rand(0);
+  Json hp = Json::object();
+  hp["global_batch_size"] = 64;
+  Op create = Op::Create(rand, hp);
+  Op train = Op::Train(create.request_id, Length(Unit::Batches, 500));
+  Op validate = Op::Validate(create.request_id), checkpoint = Op::Checkpoint(create.request_id);
+  TrialWorkloadSequencer s(cfg(200, 400, "none", su));
+  EXPECT(s.UpToDate());
+  s.OperationRequested(train);
+  EXPECT(!s.UpToDate());
+  s.OperationRequested(validate);
+  s.OperationRequested(checkpoint);
+  bool threw = false;
+  try { s.NextWorkload(); } catch (const std::logic_error&) { threw = true; }
+  EXPECT(threw);  // before SetTrialID
+  s.SetTrialID(1);
+  EXPECT(Same(s.NextWorkload(), train1));
+  EXPECT(!s.PrecloseCheckpointWorkload());  // nothing trained yet
+  EXPECT(!s.WorkloadCompleted(done(train1), false).op);
+  EXPECT(Same(s.NextWorkload(), train2));
+  EXPECT(Same(*s.PrecloseCheckpointWorkload(), ckpt1));
+  EXPECT(!s.WorkloadCompleted(done(train2), false).op);
+  EXPECT(Same(s.NextWorkload(), val2));
+  EXPECT(Same(*s.PrecloseCheckpointWorkload(), ckpt2));
+  EXPECT(!s.WorkloadCompleted(done(val2), false).op);
+  EXPECT(Same(s.NextWorkload(), train3));
+  EXPECT(!s.WorkloadCompleted(done(train3), false).op);
+  EXPECT(Same(s.NextWorkload(), train4));
+  EXPECT(!s.WorkloadCompleted(done(train4), false).op);
+  EXPECT(Same(s.NextWorkload(), val4));
+  EXPECT(!s.WorkloadCompleted(done(val4), false).op);
+  EXPECT(Same(s.NextWorkload(), ckpt4));
+  EXPECT(!s.WorkloadCompleted(done(ckpt4, ckpt_metrics("c4")), false).op);
+  EXPECT(!s.PrecloseCheckpointWorkload());
+  auto c = s.WorkloadCompleted(done(train5), false);
+  EXPECT(c.op && c.op->kind == Op::Kind::Train && c.op->request_id == train.request_id);
+  EXPECT(Same(s.NextWorkload(), ckpt5));
+  EXPECT_EQ(s.RollBack(), 4);  // back to the step-4 checkpoint
+  EXPECT(Same(s.NextWorkload(), train5));
+  c = s.WorkloadCompleted(done(train5), false);  // replay
+  EXPECT(c.op && c.op->kind == Op::Kind::Train);
+  EXPECT(Same(s.NextWorkload(), ckpt5));
+  EXPECT(!s.WorkloadCompleted(done(ckpt5, ckpt_metrics("c5")), false).op);
+  EXPECT(Same(s.NextWorkload(), val5));
+  c = s.WorkloadCompleted(done(val5), false);
+  EXPECT(c.op && c.op->kind == Op::Kind::Validate);
+  EXPECT(!s.PrecloseCheckpointWorkload());
+  c = s.CompleteCachedCheckpoints();
+  EXPECT(c.op && c.op->kind == Op::Kind::Checkpoint);
+  EXPECT(s.UpToDate());
+  threw = false;
+  try { s.NextWorkload(); } catch (const std::logic_error&) { threw = true; }
+  EXPECT(threw);  // up to date
+}
+
+TEST(TestTrialWorkloadSequencerFailedWorkloads) {
+  NpRand rand(0);
+  Op create = Op::Create(rand, Json::object());
+  TrialWorkloadSequencer s(cfg(0, 100, "best", 100));
+  s.SetTrialID(1);
+  s.OperationRequested(Op::Train(create.request_id, Length(Unit::Batches, 500)));
+  s.WorkloadCompleted(done(W(Workload::Kind::RunStep, 1, 100, 0)), false);
+  CompletedMessage m = done(W(Workload::Kind::CheckpointModel, 1, 0, 100), Json());
+  m.exited_reason = ExitedReason::Errored;  // "not ok": a failed checkpoint, no metrics
+  auto c = s.WorkloadCompleted(m, false);
+  EXPECT(!c.op);
+  EXPECT(s.DebugState()["exiting_early"].as_bool());
+}
+
+TEST(TestTrialWorkloadSequencerOperationLessThanBatchSize) {
+  NpRand rand(0);
+  Op create = Op::Create(rand, Json::object());
+  SequencerConfig c0 = cfg(0, 0, "best", 100);
+  c0.default_unit = Unit::Records;
+  TrialWorkloadSequencer s(c0);
+  s.SetTrialID(1);
+  Op train = Op::Train(create.request_id, Length(Unit::Records, 24));  // < one 64-record batch
+  s.OperationRequested(train);
+  auto c = s.WorkloadCompleted(done(W(Workload::Kind::RunStep, 1, 1, 0)), false);
+  EXPECT(c.op && c.op->kind == Op::Kind::Train && c.op->request_id == train.request_id);
+}
