@@ -53,6 +53,7 @@ class Master {
 
   // ---- used by actors / handlers
   Store& store() { return *store_; }
+  LogStore& logs() { return *logs_; }
   actor::System& system() { return *sys_; }
   const MasterConfig& config() const { return cfg_; }
   actor::Ref Pool(const std::string& name);
@@ -84,6 +85,7 @@ class Master {
 
   MasterConfig cfg_;
   std::unique_ptr<Store> store_;
+  std::unique_ptr<LogStore> logs_;  // trial-<id> / task-<id> log segments
   std::unique_ptr<actor::System> sys_;
   RWCoordinator rw_coordinator_;  // before http_: socket threads use it until the server stops
   net::HttpServer http_;

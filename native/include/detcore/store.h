@@ -6,6 +6,9 @@
 //   <dir>/wal.jsonl       {"t": table, "k": id, "v": row} | {"t": table, "k": id, "d": true}
 // Opening replays snapshot + WAL, so a restarted master sees every committed row (experiments,
 // trials, steps, validations, checkpoints, searcher_events, trial_logs, templates, models, ...).
+// Secondary indexes on the foreign-key / lookup columns (experiment_id, trial_id, uuid, name, ...)
+// make Where() a hash lookup instead of a table scan.  High-volume append-only streams (trial and
+// task logs) do not live here: see LogStore.
 // All methods are thread-safe.
 #pragma once
 
@@ -14,7 +17,9 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "detcore/json.h"
@@ -39,6 +44,8 @@ class Store {
   std::vector<Json> Where(const std::string& table, const std::string& field, const Json& value) const;
   size_t Count(const std::string& table) const;
   void DeleteWhere(const std::string& table, const std::function<bool(const Json&)>& pred);
+  // Delete every row whose indexed `field` equals `value` (index lookup, no scan).
+  void DeleteWhereEq(const std::string& table, const std::string& field, const Json& value);
   void Flush();     // fsync the WAL
   void Compact();   // snapshot + truncate WAL
   const std::string& dir() const { return dir_; }
@@ -47,6 +54,10 @@ class Store {
   void Load();
   void Log(const Json& entry);
   void CompactLocked();
+  void IndexRow(const std::string& table, int64_t id, const Json& row, bool add);
+  std::vector<Json> ScanLocked(const std::string& table, const std::function<bool(const Json&)>& pred) const;
+  // table -> field -> value key -> row ids
+  std::map<std::string, std::map<std::string, std::unordered_map<std::string, std::set<int64_t>>>> index_;
   std::string dir_;
   size_t compact_every_;
   size_t wal_entries_ = 0;
@@ -54,6 +65,35 @@ class Store {
   std::map<std::string, std::map<int64_t, Json>> tables_;
   std::map<std::string, int64_t> seq_;
   FILE* wal_ = nullptr;
+};
+
+// Append-only, per-stream log segments (trial / task logs): <dir>/logs/<stream>.jsonl, one JSON
+// line per entry, with only the byte offset of each line kept in memory (8 B/line), so a long
+// HP search with millions of log lines costs disk, not master RSS.  Entry ids are 1-based line
+// numbers per stream (the cursor clients follow).  Memory-only when dir is empty (tests).
+class LogStore {
+ public:
+  explicit LogStore(std::string dir = "");
+  ~LogStore();
+  // Appends rows to `stream`, setting row["id"]; returns the last id.
+  int64_t Append(const std::string& stream, std::vector<Json> rows);
+  // Entries with id > after_id passing `pred`, at most `limit` (the last `limit` when tail).
+  std::vector<Json> Read(const std::string& stream, int64_t after_id, int64_t limit,
+                         const std::function<bool(const Json&)>& pred = nullptr, bool tail = false);
+  int64_t Count(const std::string& stream) const;
+  void Delete(const std::string& stream);
+
+ private:
+  struct Stream {
+    std::vector<uint64_t> offsets;  // byte offset of every line
+    uint64_t size = 0;
+    std::vector<std::string> mem;   // memory-only mode
+  };
+  std::string Path(const std::string& stream) const;
+  Stream& Open(const std::string& stream);  // loads the offsets of an existing segment
+  std::string dir_;
+  mutable std::mutex mu_;
+  std::map<std::string, Stream> streams_;
 };
 
 }  // namespace detcore

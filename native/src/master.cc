@@ -132,19 +132,26 @@ Json CheckpointsToGC(Store& store, int64_t experiment_id, const Json& cfg) {
     double metric = 0;
   };
   std::map<int64_t, std::vector<C>> by_trial;
-  for (auto& r : store.Scan("checkpoints", [&](const Json& r) {
-         return r.get_int("experiment_id", -1) == experiment_id && r.get_string("state", "") == "COMPLETED";
-       })) {
-    C c{r};
-    int64_t tid = r["trial_id"].as_int(), step = r["step_id"].as_int();
-    for (auto& v : store.Scan("validations", [&](const Json& v) {
-           return v.get_int("trial_id", -1) == tid && v.get_int("step_id", -1) == step && v.get_string("state", "") == "COMPLETED";
-         })) {
-      try {
-        c.metric = ValidationMetric(v["metrics"]["validation_metrics"], metric);
-        c.has_metric = true;
-      } catch (const std::exception&) {
+  std::map<int64_t, std::map<int64_t, double>> metric_at;  // trial -> step -> searcher metric
+  for (auto& r : store.Where("checkpoints", "experiment_id", Json(experiment_id))) {
+    if (r.get_string("state", "") != "COMPLETED") continue;
+    const int64_t tid = r["trial_id"].as_int();
+    if (!metric_at.count(tid)) {  // one index lookup of the trial's validations
+      auto& m = metric_at[tid];
+      for (auto& v : store.Where("validations", "trial_id", Json(tid))) {
+        if (v.get_string("state", "") != "COMPLETED") continue;
+        try {
+          m[v.get_int("step_id", -1)] = ValidationMetric(v["metrics"]["validation_metrics"], metric);
+        } catch (const std::exception&) {
+        }
       }
+    }
+    C c{r};
+    auto& m = metric_at[tid];
+    auto it = m.find(r["step_id"].as_int());
+    if (it != m.end()) {
+      c.metric = it->second;
+      c.has_metric = true;
     }
     by_trial[tid].push_back(c);
   }
@@ -177,6 +184,7 @@ Json CheckpointsToGC(Store& store, int64_t experiment_id, const Json& cfg) {
 // ---------------------------------------------------------------------------------- Master
 Master::Master(MasterConfig cfg) : cfg_(std::move(cfg)) {
   store_ = std::make_unique<Store>(cfg_.store_dir);
+  logs_ = std::make_unique<LogStore>(cfg_.store_dir.empty() ? std::string() : cfg_.store_dir + "/logs");
   sys_ = std::make_unique<actor::System>(8);
   Json cid;
   if (store_->Get("cluster_id", 1, &cid)) {
@@ -249,7 +257,7 @@ void Master::AppendTrialLog(int64_t trial_id, const std::string& line, const std
   row["container_id"] = container_id;
   row["rank_id"] = rank;
   row["timestamp"] = NowRFC3339();
-  store_->Insert("trial_logs", row);
+  logs_->Append("trial-" + std::to_string(trial_id), {row});
 }
 
 void Master::RunCheckpointGC(int64_t experiment_id, const Json& exp_config, const Json& to_delete) {
@@ -601,11 +609,10 @@ void Master::InstallRoutes() {
     std::vector<int64_t> trial_ids;
     for (auto& t : store_->Where("trials", "experiment_id", Json(id))) trial_ids.push_back(t["id"].as_int());
     for (int64_t tid : trial_ids) {
-      auto of = [&](const Json& x) { return x.get_int("trial_id", -1) == tid; };
-      store_->DeleteWhere("steps", of);
-      store_->DeleteWhere("validations", of);
-      store_->DeleteWhere("trial_logs", of);
-      store_->DeleteWhere("checkpoints", of);
+      store_->DeleteWhereEq("steps", "trial_id", Json(tid));
+      store_->DeleteWhereEq("validations", "trial_id", Json(tid));
+      store_->DeleteWhereEq("checkpoints", "trial_id", Json(tid));
+      logs_->Delete("trial-" + std::to_string(tid));
       store_->Delete("trials", tid);
     }
     store_->Delete("model_definitions", id);
@@ -727,19 +734,16 @@ void Master::InstallRoutes() {
     const std::string rank = r.Query("rank_id", ""), stdtype = r.Query("stdtype", ""),
                       cid = r.Query("container_id", ""), grep = r.Query("contains", "");
     const bool tail = r.Query("tail", "false") == "true";
-    std::vector<Json> hits;
-    for (auto& l : store_->Where("trial_logs", "trial_id", Json(id))) {
-      if (l["id"].as_int() <= offset) continue;
-      if (!rank.empty() && std::to_string(l.get_int("rank_id", 0)) != rank) continue;
-      if (!stdtype.empty() && l.get_string("stdtype", "") != stdtype) continue;
-      if (!cid.empty() && l.get_string("container_id", "") != cid) continue;
-      if (!grep.empty() && l.get_string("message", "").find(grep) == std::string::npos) continue;
-      hits.push_back(l);
-    }
-    size_t n = std::min<size_t>(hits.size(), static_cast<size_t>(std::max<int64_t>(0, limit)));
-    size_t start = tail ? hits.size() - n : 0;
+    auto pred = [&](const Json& l) {
+      if (!rank.empty() && std::to_string(l.get_int("rank_id", 0)) != rank) return false;
+      if (!stdtype.empty() && l.get_string("stdtype", "") != stdtype) return false;
+      if (!cid.empty() && l.get_string("container_id", "") != cid) return false;
+      if (!grep.empty() && l.get_string("message", "").find(grep) == std::string::npos) return false;
+      return true;
+    };
     Json out = Json::array();
-    for (size_t i = start; i < start + n; ++i) out.push_back(hits[i]);
+    for (auto& l : logs_->Read("trial-" + std::to_string(id), offset, std::max<int64_t>(0, limit), pred, tail))
+      out.push_back(l);
     return J(200, out);
   });
   http_.Route("POST", "/trials/:id/kill", [this](const net::Request& r) {
@@ -754,9 +758,19 @@ void Master::InstallRoutes() {
   http_.Route("POST", "/trial_logs", [this](const net::Request& r) {
     Json body = Json::parse(r.body);
     Json items = body.is_array() ? body : Json(Json::Array{body});
-    for (auto& l : items.as_array())
-      AppendTrialLog(l.get_int("trial_id", 0), l.get_string("message", l.get_string("log", "")),
-                     l.get_string("stdtype", "stdout"), l.get_string("container_id", ""), static_cast<int>(l.get_int("rank_id", 0)));
+    std::map<int64_t, std::vector<Json>> by_trial;  // one segment append per trial per request
+    const std::string now = NowRFC3339();
+    for (auto& l : items.as_array()) {
+      Json row = Json::object();
+      row["trial_id"] = l.get_int("trial_id", 0);
+      row["message"] = l.get_string("message", l.get_string("log", ""));
+      row["stdtype"] = l.get_string("stdtype", "stdout");
+      row["container_id"] = l.get_string("container_id", "");
+      row["rank_id"] = l.get_int("rank_id", 0);
+      row["timestamp"] = now;
+      by_trial[row["trial_id"].as_int()].push_back(row);
+    }
+    for (auto& kv : by_trial) logs_->Append("trial-" + std::to_string(kv.first), std::move(kv.second));
     return J(200, Json::object());
   });
   http_.Route("GET", "/checkpoints/:uuid", [this](const net::Request& r) {
@@ -920,8 +934,7 @@ void Master::InstallRoutes() {
     std::string task = "cmd-" + r.Param("id");
     int64_t offset = std::stoll(r.Query("offset", "0"));
     Json out = Json::array();
-    for (auto& l : store_->Where("task_logs", "task_id", Json(task)))
-      if (l["id"].as_int() > offset) out.push_back(l);
+    for (auto& l : logs_->Read("task-" + task, offset, INT64_MAX)) out.push_back(l);
     return J(200, out);
   });
   http_.Route("POST", "/commands/:id/kill", [this](const net::Request& r) {
@@ -1120,7 +1133,7 @@ void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
       row["message"] = m["log"];
       row["stdtype"] = m["stdtype"];
       row["timestamp"] = NowRFC3339();
-      store_->Insert("task_logs", row);
+      logs_->Append("task-" + m.get_string("task_id", ""), {row});
     } else if (t == "ContainerLog") {
       AppendTrialLog(m.get_int("trial_id", 0), m.get_string("log", ""), m.get_string("stdtype", "stdout"),
                      m.get_string("container_id", ""), static_cast<int>(m.get_int("rank", 0)));

@@ -4,11 +4,30 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <dirent.h>
+
+#include <algorithm>
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
 
 namespace detcore {
+
+namespace {
+// Columns the master looks rows up by (Where()): indexed in every table that has them.
+const char* const kIndexed[] = {"experiment_id", "trial_id", "uuid", "name", "model_name", "username",
+                                "token", "task_id", "checkpoint_uuid"};
+}  // namespace
+
+void Store::IndexRow(const std::string& table, int64_t id, const Json& row, bool add) {
+  if (!row.is_object()) return;
+  for (const char* f : kIndexed) {
+    if (!row.has(f)) continue;
+    auto& bucket = index_[table][f][row[f].dump()];
+    if (add) bucket.insert(id);
+    else bucket.erase(id);
+  }
+}
 
 Store::Store(std::string dir, size_t compact_every) : dir_(std::move(dir)), compact_every_(compact_every) {
   if (!dir_.empty()) {
@@ -56,6 +75,8 @@ void Store::Load() {
     if (k > seq_[t]) seq_[t] = k;
     ++wal_entries_;
   }
+  for (auto& t : tables_)
+    for (auto& r : t.second) IndexRow(t.first, r.first, r.second, true);
 }
 
 void Store::Log(const Json& entry) {
@@ -77,6 +98,7 @@ int64_t Store::Insert(const std::string& table, Json row) {
   int64_t id = ++seq_[table];
   row["id"] = id;
   tables_[table][id] = row;
+  IndexRow(table, id, row, true);
   Json e = Json::object();
   e["t"] = table;
   e["k"] = id;
@@ -88,7 +110,11 @@ int64_t Store::Insert(const std::string& table, Json row) {
 void Store::Put(const std::string& table, int64_t id, Json row) {
   std::lock_guard<std::mutex> g(mu_);
   row["id"] = id;
-  tables_[table][id] = row;
+  auto& tab = tables_[table];
+  auto old = tab.find(id);
+  if (old != tab.end()) IndexRow(table, id, old->second, false);
+  tab[id] = row;
+  IndexRow(table, id, row, true);
   if (id > seq_[table]) seq_[table] = id;
   Json e = Json::object();
   e["t"] = table;
@@ -110,7 +136,11 @@ bool Store::Get(const std::string& table, int64_t id, Json* out) const {
 bool Store::Delete(const std::string& table, int64_t id) {
   std::lock_guard<std::mutex> g(mu_);
   auto t = tables_.find(table);
-  if (t == tables_.end() || !t->second.erase(id)) return false;
+  if (t == tables_.end()) return false;
+  auto r = t->second.find(id);
+  if (r == t->second.end()) return false;
+  IndexRow(table, id, r->second, false);
+  t->second.erase(r);
   Json e = Json::object();
   e["t"] = table;
   e["k"] = id;
@@ -127,7 +157,9 @@ bool Store::Update(const std::string& table, int64_t id, const Json& patch) {
   if (r == t->second.end()) return false;
   Json row = r->second;
   for (auto& kv : patch.as_object()) row[kv.first] = kv.second;
+  IndexRow(table, id, r->second, false);
   r->second = row;
+  IndexRow(table, id, row, true);
   Json e = Json::object();
   e["t"] = table;
   e["k"] = id;
@@ -138,6 +170,10 @@ bool Store::Update(const std::string& table, int64_t id, const Json& patch) {
 
 std::vector<Json> Store::Scan(const std::string& table, const std::function<bool(const Json&)>& pred) const {
   std::lock_guard<std::mutex> g(mu_);
+  return ScanLocked(table, pred);
+}
+
+std::vector<Json> Store::ScanLocked(const std::string& table, const std::function<bool(const Json&)>& pred) const {
   std::vector<Json> out;
   auto t = tables_.find(table);
   if (t == tables_.end()) return out;
@@ -147,7 +183,23 @@ std::vector<Json> Store::Scan(const std::string& table, const std::function<bool
 }
 
 std::vector<Json> Store::Where(const std::string& table, const std::string& field, const Json& value) const {
-  return Scan(table, [&](const Json& r) { return r[field] == value; });
+  std::lock_guard<std::mutex> g(mu_);
+  if (std::find_if(std::begin(kIndexed), std::end(kIndexed), [&](const char* f) { return field == f; }) ==
+      std::end(kIndexed))
+    return ScanLocked(table, [&](const Json& r) { return r[field] == value; });
+  std::vector<Json> out;
+  auto ti = index_.find(table);
+  auto t = tables_.find(table);
+  if (ti == index_.end() || t == tables_.end()) return out;
+  auto fi = ti->second.find(field);
+  if (fi == ti->second.end()) return out;
+  auto b = fi->second.find(value.dump());
+  if (b == fi->second.end()) return out;
+  for (int64_t id : b->second) {  // ascending id, as a scan would return them
+    auto r = t->second.find(id);
+    if (r != t->second.end() && r->second[field] == value) out.push_back(r->second);
+  }
+  return out;
 }
 
 size_t Store::Count(const std::string& table) const {
@@ -156,9 +208,15 @@ size_t Store::Count(const std::string& table) const {
   return t == tables_.end() ? 0 : t->second.size();
 }
 
-void Store::DeleteWhere(const std::string& table, const std::function<bool(const Json&)>& pred) {
+void Store::DeleteWhere(const std::string& table, const std::function<bool(const Json&)>& pred) {  // NOLINT
   std::vector<int64_t> ids;
   for (auto& r : Scan(table, pred)) ids.push_back(r["id"].as_int());
+  for (int64_t id : ids) Delete(table, id);
+}
+
+void Store::DeleteWhereEq(const std::string& table, const std::string& field, const Json& value) {
+  std::vector<int64_t> ids;
+  for (auto& r : Where(table, field, value)) ids.push_back(r["id"].as_int());
   for (int64_t id : ids) Delete(table, id);
 }
 
@@ -198,6 +256,99 @@ void Store::CompactLocked() {
   if (wal_) std::fclose(wal_);
   wal_ = std::fopen((dir_ + "/wal.jsonl").c_str(), "w");
   wal_entries_ = 0;
+}
+
+// ---------------------------------------------------------------------------------- LogStore
+LogStore::LogStore(std::string dir) : dir_(std::move(dir)) {
+  if (dir_.empty()) return;
+  ::mkdir(dir_.c_str(), 0755);
+}
+
+LogStore::~LogStore() = default;
+
+std::string LogStore::Path(const std::string& stream) const { return dir_ + "/" + stream + ".jsonl"; }
+
+LogStore::Stream& LogStore::Open(const std::string& stream) {
+  auto it = streams_.find(stream);
+  if (it != streams_.end()) return it->second;
+  Stream& s = streams_[stream];
+  if (dir_.empty()) return s;
+  std::ifstream f(Path(stream), std::ios::binary);
+  std::string line;
+  uint64_t off = 0;
+  while (std::getline(f, line)) {
+    if (f.eof() && line.empty()) break;
+    s.offsets.push_back(off);
+    off += line.size() + 1;
+  }
+  s.size = off;
+  return s;
+}
+
+int64_t LogStore::Append(const std::string& stream, std::vector<Json> rows) {
+  std::lock_guard<std::mutex> g(mu_);
+  Stream& s = Open(stream);
+  std::string buf;
+  for (auto& r : rows) {
+    r["id"] = static_cast<int64_t>(s.offsets.size() + 1);
+    std::string line = r.dump();
+    s.offsets.push_back(s.size + buf.size());
+    if (dir_.empty()) s.mem.push_back(line);
+    buf += line;
+    buf.push_back('\n');
+  }
+  if (!dir_.empty() && !buf.empty()) {
+    FILE* f = std::fopen(Path(stream).c_str(), "ab");
+    if (!f) throw std::runtime_error("cannot append to log segment " + Path(stream));
+    std::fwrite(buf.data(), 1, buf.size(), f);
+    std::fclose(f);
+  }
+  s.size += buf.size();
+  return static_cast<int64_t>(s.offsets.size());
+}
+
+std::vector<Json> LogStore::Read(const std::string& stream, int64_t after_id, int64_t limit,
+                                 const std::function<bool(const Json&)>& pred, bool tail) {
+  std::lock_guard<std::mutex> g(mu_);
+  Stream& s = Open(stream);
+  std::vector<Json> out;
+  const int64_t n = static_cast<int64_t>(s.offsets.size());
+  if (after_id < 0) after_id = 0;
+  if (after_id >= n || limit <= 0) return out;
+  std::ifstream f;
+  if (!dir_.empty()) {
+    f.open(Path(stream), std::ios::binary);
+    f.seekg(static_cast<std::streamoff>(s.offsets[static_cast<size_t>(after_id)]));
+  }
+  std::string line;
+  for (int64_t i = after_id; i < n; ++i) {
+    if (dir_.empty()) line = s.mem[static_cast<size_t>(i)];
+    else if (!std::getline(f, line)) break;
+    Json row;
+    try {
+      row = Json::parse(line);
+    } catch (const std::exception&) {
+      continue;
+    }
+    if (pred && !pred(row)) continue;
+    out.push_back(std::move(row));
+    if (!tail && static_cast<int64_t>(out.size()) >= limit) break;
+  }
+  if (tail && static_cast<int64_t>(out.size()) > limit) out.erase(out.begin(), out.end() - limit);
+  return out;
+}
+
+int64_t LogStore::Count(const std::string& stream) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = streams_.find(stream);
+  if (it != streams_.end()) return static_cast<int64_t>(it->second.offsets.size());
+  return const_cast<LogStore*>(this)->Open(stream).offsets.size();
+}
+
+void LogStore::Delete(const std::string& stream) {
+  std::lock_guard<std::mutex> g(mu_);
+  streams_.erase(stream);
+  if (!dir_.empty()) ::unlink(Path(stream).c_str());
 }
 
 }  // namespace detcore
