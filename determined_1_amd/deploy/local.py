@@ -42,7 +42,8 @@ class LocalCluster:
     def __init__(self, agents: int = 1, slots_per_agent: int = 0, port: Optional[int] = None,
                  store_dir: Optional[str] = None, checkpoint_dir: Optional[str] = None,
                  scheduler: str = "fair_share", work_dir: Optional[str] = None, gpu: bool = False,
-                 log_dir: Optional[str] = None, tick_ms: int = 100, master_args: Optional[List[str]] = None) -> None:
+                 log_dir: Optional[str] = None, tick_ms: int = 100, master_args: Optional[List[str]] = None,
+                 visible_gpus: Optional[str] = None, agent_args: Optional[List[str]] = None) -> None:
         self.port = port or free_port()
         self.tmp = tempfile.mkdtemp(prefix="det-local-")
         self.store_dir = store_dir or os.path.join(self.tmp, "store")
@@ -55,6 +56,8 @@ class LocalCluster:
         self.gpu = gpu
         self.tick_ms = tick_ms
         self.master_args = list(master_args or [])
+        self.visible_gpus = visible_gpus
+        self.agent_args = list(agent_args or [])
         self.master_proc = None  # type: Optional[subprocess.Popen]
         self.agent_procs = []  # type: List[subprocess.Popen]
 
@@ -90,6 +93,9 @@ class LocalCluster:
             args += ["--artificial-slots", str(self.slots_per_agent)]
         elif self.gpu:
             args += ["--slot-type", "gpu"]
+            if self.visible_gpus:
+                args += ["--visible-gpus", self.visible_gpus]
+        args += self.agent_args
         p = subprocess.Popen(args, stdout=log, stderr=subprocess.STDOUT)
         self.agent_procs.append(p)
         return p

@@ -46,10 +46,32 @@ def local_slot_count(env: EnvContext) -> int:
     return max(1, len(env.slot_ids))
 
 
+def _warm_gpu() -> None:
+    """HIP runtime + device init (~0.3-0.5 s on an MI355X) on a side thread, overlapped with the
+    storage probe, the master rendezvous and the user-code import; the model's first ``.cuda()``
+    then finds the runtime up.  torch serialises its lazy init, so a concurrent caller just waits."""
+    try:
+        import torch
+
+        torch.cuda.init()
+        torch.empty(1, device="cuda")  # primary context + caching allocator
+    except Exception as e:  # the trial's own device use reports real problems
+        logging.debug("early GPU init failed: %s", e)
+
+
 def main() -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [harness] %(levelname)s %(message)s")
+    if os.environ.get("DET_ZYGOTE_PID"):
+        logging.info("trial process forked from warm zygote %s", os.environ["DET_ZYGOTE_PID"])
     timeline.mark("imports done")
     env = EnvContext.from_environ()
+    slots_per_trial = int((env.experiment_config.get("resources") or {}).get("slots_per_trial", 1) or 1)
+    if env.use_gpu and slots_per_trial == 1 and os.environ.get("DET_EARLY_GPU_INIT", "1") == "1":
+        # single-process trial: this process is the one that uses the GPU (a multi-slot launcher
+        # parent never touches it)
+        import threading
+
+        threading.Thread(target=_warm_gpu, name="det-gpu-init", daemon=True).start()
     if env.debug:
         faulthandler.dump_traceback_later(30, repeat=True)
     cfg = env.experiment_config

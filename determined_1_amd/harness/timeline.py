@@ -6,7 +6,6 @@ import logging
 import os
 import time
 
-_ENABLED = os.environ.get("DET_TIMELINE", "0") == "1"
 _T0 = None
 
 
@@ -23,9 +22,10 @@ def _start() -> float:
 
 
 def enabled() -> bool:
-    return _ENABLED
+    # read per call: a zygote-forked trial process imported this module before its env was set
+    return os.environ.get("DET_TIMELINE", "0") == "1"
 
 
 def mark(label: str) -> None:
-    if _ENABLED:
+    if enabled():
         logging.info("[timeline] +%.3fs %s", time.time() - _start(), label)

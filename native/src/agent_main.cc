@@ -11,11 +11,17 @@
 //     ContainerLog lines (the reference's Fluent Bit path);
 //   * container state machine Assigned -> Starting -> Running -> Terminated(exit code);
 //   * SignalContainer -> kill(-pgid); master disconnect -> kill everything, reconnect w/ backoff.
+//   * harness containers are forked from a warm zygote (determined_1_amd/exec/zygote.py) that has
+//     torch + the harness imported but no GPU context, instead of a cold `python -m` exec; the
+//     zygote reports the child's pid and exit status over its unix socket.  Without a zygote
+//     (`--no-zygote`, or it is not up) containers are fork/exec'd as before.
 #include <dirent.h>
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <sys/un.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -56,6 +62,7 @@ struct Options {
   std::string work_dir = "/tmp/det-agent";
   std::string framework_root;
   std::string advertise_host;
+  bool zygote = true;  // serve harness containers from a warm pre-imported Python (exec/zygote.py)
 };
 
 void Log(const std::string& s) { std::fprintf(stderr, "[det-agent] %s\n", s.c_str()); }
@@ -166,6 +173,7 @@ class Agent {
 
   int Run() {
     devices_ = DetectDevices(o_);
+    if (o_.zygote) StartZygote();
     Log("detected " + std::to_string(devices_.size()) + " slots: " + devices_.dump());
     int backoff_ms = 500;
     while (!stop_.load()) {
@@ -194,6 +202,7 @@ class Agent {
       std::this_thread::sleep_for(std::chrono::milliseconds(backoff_ms));
     }
     KillAll();
+    StopZygote();
     return 0;
   }
 
@@ -202,7 +211,135 @@ class Agent {
     if (ws_) ws_->Close();
   }
 
+  void StopZygote() {
+    if (zygote_pid_ > 0) {
+      ::kill(zygote_pid_, SIGTERM);
+      int st = 0;
+      for (int i = 0; i < 50 && waitpid(zygote_pid_, &st, WNOHANG) == 0; ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      ::kill(zygote_pid_, SIGKILL);
+      waitpid(zygote_pid_, &st, WNOHANG);
+      zygote_pid_ = -1;
+    }
+  }
+
  private:
+  // The zygote is a child of the agent (it exits when the agent goes away); its stderr is the
+  // agent's.  Startup is asynchronous: until its socket accepts, containers are fork/exec'd.
+  void StartZygote() {
+    zygote_sock_ = o_.work_dir + "/zygote-" + std::to_string(getpid()) + ".sock";
+    std::string pp = o_.framework_root;
+    const char* old = getenv("PYTHONPATH");
+    if (old && *old) pp += std::string(":") + old;
+    pid_t pid = fork();
+    if (pid == 0) {
+      setenv("PYTHONPATH", pp.c_str(), 1);
+      setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 1);
+      execlp(o_.python.c_str(), o_.python.c_str(), "-m", "determined_1_amd.exec.zygote", "--socket",
+             zygote_sock_.c_str(), static_cast<char*>(nullptr));
+      _exit(127);
+    }
+    if (pid <= 0) return;
+    zygote_pid_ = pid;
+    // wait for the socket before registering slots with the master, so the first containers are
+    // served warm; give up (cold fork/exec for every container) if the zygote exits or stalls
+    for (int i = 0; i < 600; ++i) {
+      struct stat st;
+      if (::stat(zygote_sock_.c_str(), &st) == 0) return;
+      int status = 0;
+      if (waitpid(pid, &status, WNOHANG) == pid) {
+        Log("zygote exited during preload; containers will be fork/exec'd");
+        zygote_pid_ = -1;
+        return;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    Log("zygote not ready after 30 s; containers will be fork/exec'd until it is");
+  }
+
+  // Ask the zygote to fork a harness child with the container's stdout/stderr pipes, env and cwd.
+  // Returns the connected socket (the exit status arrives on it later) and sets *child; -1 when the
+  // zygote is unavailable or refused, in which case the caller fork/execs.
+  int ZygoteSpawn(const std::vector<std::string>& args, const std::map<std::string, std::string>& env,
+                  const std::string& cwd, int out_fd, int err_fd, pid_t* child) {
+    if (zygote_pid_ <= 0 || args.size() < 3 || args[1] != "-m") return -1;
+    int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (fd < 0) return -1;
+    sockaddr_un addr{};
+    addr.sun_family = AF_UNIX;
+    if (zygote_sock_.size() >= sizeof(addr.sun_path)) {
+      close(fd);
+      return -1;
+    }
+    std::strncpy(addr.sun_path, zygote_sock_.c_str(), sizeof(addr.sun_path) - 1);
+    if (connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+      close(fd);
+      return -1;
+    }
+    Json req = Json::object();
+    Json argv = Json::array();
+    for (size_t i = 1; i < args.size(); ++i) argv.push_back(args[i]);
+    req["argv"] = argv;
+    Json je = Json::object();
+    for (auto& kv : env) je[kv.first] = kv.second;
+    req["env"] = je;
+    req["cwd"] = cwd;
+    std::string body = req.dump();
+    std::string msg(4, '\0');
+    uint32_t n = static_cast<uint32_t>(body.size());
+    msg[0] = static_cast<char>((n >> 24) & 0xff);
+    msg[1] = static_cast<char>((n >> 16) & 0xff);
+    msg[2] = static_cast<char>((n >> 8) & 0xff);
+    msg[3] = static_cast<char>(n & 0xff);
+    msg += body;
+    int fds[2] = {out_fd, err_fd};
+    char cbuf[CMSG_SPACE(sizeof(fds))];
+    std::memset(cbuf, 0, sizeof(cbuf));
+    iovec iov{const_cast<char*>(msg.data()), msg.size()};
+    msghdr mh{};
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    mh.msg_control = cbuf;
+    mh.msg_controllen = sizeof(cbuf);
+    cmsghdr* cm = CMSG_FIRSTHDR(&mh);
+    cm->cmsg_level = SOL_SOCKET;
+    cm->cmsg_type = SCM_RIGHTS;
+    cm->cmsg_len = CMSG_LEN(sizeof(fds));
+    std::memcpy(CMSG_DATA(cm), fds, sizeof(fds));
+    ssize_t sent = sendmsg(fd, &mh, MSG_NOSIGNAL);
+    if (sent < 0) {
+      close(fd);
+      return -1;
+    }
+    size_t off = static_cast<size_t>(sent);
+    while (off < msg.size()) {
+      ssize_t w = send(fd, msg.data() + off, msg.size() - off, MSG_NOSIGNAL);
+      if (w <= 0) {
+        close(fd);
+        return -1;
+      }
+      off += static_cast<size_t>(w);
+    }
+    std::string line = ReadLine(fd);
+    if (line.rfind("pid ", 0) != 0) {
+      close(fd);
+      return -1;
+    }
+    *child = static_cast<pid_t>(std::atol(line.c_str() + 4));
+    return *child > 0 ? fd : (close(fd), -1);
+  }
+
+  static std::string ReadLine(int fd) {
+    std::string out;
+    char c;
+    while (true) {
+      ssize_t r = read(fd, &c, 1);
+      if (r <= 0 || c == '\n') break;
+      out.push_back(c);
+    }
+    return out;
+  }
+
   void Send(const Json& m) {
     auto ws = ws_;
     if (ws) ws->Send(m.dump());
@@ -331,7 +468,11 @@ class Agent {
       State(cid, "Terminated", 1, "pipe failed");
       return;
     }
-    pid_t pid = fork();
+    pid_t pid = -1;
+    int zfd = spec["cmd"].is_array() && spec["cmd"].size() > 0
+                  ? -1
+                  : ZygoteSpawn(args, env, dir, out_pipe[1], err_pipe[1], &pid);
+    if (zfd < 0) pid = fork();
     if (pid == 0) {
       setpgid(0, 0);
       dup2(out_pipe[1], 1);
@@ -348,7 +489,7 @@ class Agent {
       State(cid, "Terminated", 1, "fork failed");
       return;
     }
-    setpgid(pid, pid);
+    if (zfd < 0) setpgid(pid, pid);
     {
       std::lock_guard<std::mutex> g(mu_);
       Proc p;
@@ -369,11 +510,23 @@ class Agent {
     std::string task_id = spec.get_string("task_id", "");
     std::thread t_out([=] { Pump(out_pipe[0], cid, trial_id, rank, "stdout", dir + "/stdout.log", task_id); });
     std::thread t_err([=] { Pump(err_pipe[0], cid, trial_id, rank, "stderr", dir + "/stderr.log", task_id); });
-    int status = 0;
-    waitpid(pid, &status, 0);
+    int code = 1;
+    if (zfd >= 0) {
+      // the zygote owns (and reaps) the child; it sends "exit <code>" when it ends
+      std::string line = ReadLine(zfd);
+      close(zfd);
+      if (line.rfind("exit ", 0) == 0) {
+        code = std::atoi(line.c_str() + 5);
+      } else {  // zygote gone: wait for the orphaned child by polling
+        while (::kill(pid, 0) == 0) std::this_thread::sleep_for(std::chrono::milliseconds(200));
+      }
+    } else {
+      int status = 0;
+      waitpid(pid, &status, 0);
+      code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
+    }
     t_out.join();
     t_err.join();
-    int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
     {
       std::lock_guard<std::mutex> g(mu_);
       procs_.erase(cid);
@@ -426,6 +579,8 @@ class Agent {
   std::mutex mu_;
   std::map<std::string, Proc> procs_;
   std::atomic<bool> stop_{false};
+  pid_t zygote_pid_ = -1;
+  std::string zygote_sock_;
 };
 
 Agent* g_agent = nullptr;
@@ -467,6 +622,7 @@ int main(int argc, char** argv) {
     else if (a == "--work-dir") o.work_dir = next();
     else if (a == "--framework-root") o.framework_root = next();
     else if (a == "--advertise-host") o.advertise_host = next();
+    else if (a == "--no-zygote") o.zygote = false;
     else if (a == "--detect-only") {
       std::printf("%s\n", DetectDevices(o).dump().c_str());
       return 0;
@@ -474,7 +630,7 @@ int main(int argc, char** argv) {
       std::fprintf(stderr,
                    "usage: det-agent --master-host H --master-port P [--agent-id ID] [--resource-pool P]\n"
                    "                 [--label L] [--artificial-slots N] [--slot-type auto|gpu|cpu|none]\n"
-                   "                 [--visible-gpus 0,1] [--python PY] [--work-dir DIR] [--detect-only]\n");
+                   "                 [--visible-gpus 0,1] [--python PY] [--work-dir DIR] [--no-zygote] [--detect-only]\n");
       return a == "-h" || a == "--help" ? 0 : 2;
     }
   }

@@ -1,9 +1,14 @@
 """ASHA trials/hr on a real cluster (BASELINE north-star #2): det-master + det-agent (GPU slots from
-KFD) on this host, the 16-trial adaptive_asha CIFAR-10 experiment (examples/computer_vision/
-cifar10_pytorch/adaptive.yaml) with max_length scaled down so the search fits a short run.
-Reports trials completed / hour, wall time and the GPU-busy fraction sampled from amdgpu sysfs.
+KFD) on this host running the 16-trial adaptive_asha CIFAR-10 experiment of
+examples/computer_vision/cifar10_pytorch/adaptive.yaml (reference adaptive.yaml:26-31: max_length
+32 epochs of 50,000 records, validation every epoch) UNCHANGED by default.
 
-    python scripts/bench_asha.py [--max-length-batches 400] [--max-trials 16] [--timeout 900]
+Reports trials completed / hour, wall time, the GPU-busy fraction sampled from amdgpu sysfs, slot
+occupancy (container-seconds / (wall x slots)) and the scheduler idle fraction (1 - occupancy), plus
+per-container startup phases from the harness timeline.
+
+    python scripts/bench_asha.py [--slots 8] [--timeout 3600]            # the BASELINE shape
+    python scripts/bench_asha.py --max-length-batches 300                 # scaled-down smoke run
 """
 import argparse
 import json
@@ -53,14 +58,19 @@ def summarize_timelines(cl, trials, t0):
     with open(os.path.join(out_dir, "asha_timeline.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
     n = max(1, len(phases["total"]))
-    return {k: round(sum(v) / n, 3) for k, v in phases.items()}
+    out = {k: round(sum(v) / n, 3) for k, v in phases.items()}
+    out["_containers"] = len(phases["total"])
+    return out
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--max-length-batches", type=int, default=400)
+    ap.add_argument("--max-length-batches", type=int, default=0,
+                    help="scale the search down to this many batches (0 = the reference's 32 epochs)")
     ap.add_argument("--max-trials", type=int, default=16)
-    ap.add_argument("--timeout", type=float, default=900)
+    ap.add_argument("--slots", type=int, default=0, help="GPU slots to use (0 = every GPU the agent detects)")
+    ap.add_argument("--timeout", type=float, default=3600)
+    ap.add_argument("--no-zygote", action="store_true", help="cold python exec per container (A/B)")
     ap.add_argument("--artificial-slots", type=int, default=0, help="CPU dry run without GPUs")
     args = ap.parse_args()
     from determined_1_amd import gpu
@@ -69,13 +79,14 @@ def main() -> None:
 
     ex = REPO / "examples" / "computer_vision" / "cifar10_pytorch"
     cfg = yaml.safe_load((ex / "adaptive.yaml").read_text())
-    cfg["searcher"]["max_length"] = {"batches": args.max_length_batches}
     cfg["searcher"]["max_trials"] = args.max_trials
-    # validate only where the searcher asks (end of each rung); the real config validates every
-    # epoch = 1/32 of max_length, which a scaled-down max_length would turn into a validation storm
-    cfg.pop("min_validation_period", None)
-    cfg["scheduling_unit"] = 50
-    cfg.pop("records_per_epoch", None)
+    if args.max_length_batches:
+        cfg["searcher"]["max_length"] = {"batches": args.max_length_batches}
+        # validate only where the searcher asks (end of each rung); the real config validates every
+        # epoch = 1/32 of max_length, which a scaled-down max_length would turn into a validation storm
+        cfg.pop("min_validation_period", None)
+        cfg["scheduling_unit"] = 50
+        cfg.pop("records_per_epoch", None)
     env_vars = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
     env_vars.append("DET_TIMELINE=1")
     busy = []
@@ -87,28 +98,51 @@ def main() -> None:
             if u:
                 busy.append(sum(x.get("gpu_busy_percent", 0) for x in u) / len(u))
 
+    visible = ",".join(str(i) for i in range(args.slots)) if args.slots and not args.artificial_slots else None
     with LocalCluster(agents=1, slots_per_agent=args.artificial_slots, gpu=args.artificial_slots == 0,
-                      log_dir=os.environ.get("DET_BENCH_LOGDIR", "/tmp")) as c:
+                      log_dir=os.environ.get("DET_BENCH_LOGDIR", "/tmp"), visible_gpus=visible,
+                      agent_args=["--no-zygote"] if args.no_zygote else []) as c:
         if args.artificial_slots == 0:
-            c.wait_for_slots(1)
+            c.wait_for_slots(args.slots or 1, timeout=60)
         cl = MasterClient(c.address)
         th = threading.Thread(target=sample, daemon=True)
         th.start()
         t0 = time.time()
         eid = cl.create_experiment(cfg, read_context(ex))["id"]
-        state = cl.wait_for_experiment(eid, timeout=args.timeout)
+        state = None
+        last = 0.0
+        while time.time() - t0 < args.timeout:  # progress line every 20 s (long runs must not look hung)
+            ex = cl.experiment(eid)
+            state = ex["state"]
+            if state in ("COMPLETED", "CANCELED", "ERROR"):
+                break
+            if time.time() - last > 20:
+                last = time.time()
+                ts = ex["trials"]
+                print(f"[bench_asha] +{time.time() - t0:6.0f}s state={state} trials={len(ts)} "
+                      f"completed={sum(t['state'] == 'COMPLETED' for t in ts)} "
+                      f"batches={sum(t.get('total_batches_processed', 0) for t in ts)}", file=sys.stderr, flush=True)
+            time.sleep(2)
         wall = time.time() - t0
         stop.set()
         e = cl.experiment(eid)
         done = sum(1 for t in e["trials"] if t["state"] == "COMPLETED")
         timeline = summarize_timelines(cl, e["trials"], t0)
         slots = sum(len(a["slots"]) for a in cl.get("/agents"))
+        containers = timeline.pop("_containers", 0)
+        occupancy = timeline.get("total", 0.0) * containers / max(1e-9, wall * slots)
+        records = sum(t.get("total_batches_processed", 0) * t.get("hparams", {}).get("global_batch_size", 0)
+                      for t in e["trials"])
         print(json.dumps({"metric": "ASHA trials/hr (16-trial adaptive_asha CIFAR-10)",
                           "value": round(done * 3600.0 / wall, 2), "unit": "trials/hr", "state": state,
                           "trials_completed": done, "wall_s": round(wall, 1), "slots": slots,
+                          "containers": containers, "train_records": records,
                           "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
-                          "per_container_s": timeline,
-                          "config": {"max_length_batches": args.max_length_batches, "max_trials": args.max_trials,
+                          "slot_occupancy": round(occupancy, 3), "scheduler_idle_frac": round(1 - occupancy, 3),
+                          "zygote": not args.no_zygote, "per_container_s": timeline,
+                          "config": {"max_length": cfg["searcher"]["max_length"], "max_trials": args.max_trials,
+                                     "records_per_epoch": cfg.get("records_per_epoch"),
+                                     "min_validation_period": cfg.get("min_validation_period"),
                                      "searcher": "adaptive_asha", "amp": cfg["hyperparameters"].get("amp")}}),
               flush=True)
 

@@ -68,6 +68,9 @@ def test_single_trial_completes_and_gc(cluster):
     for c in deleted:
         assert not pathlib.Path(cluster.checkpoint_dir, c["uuid"]).exists()
     assert e["progress"] == pytest.approx(1.0)
+    # the agent served the trial from its warm zygote (exec/zygote.py), not a cold python exec
+    logs = [r["message"] for r in cl.get(f"/trials/{t['id']}/logs")]
+    assert any("forked from warm zygote" in m for m in logs), logs[:20]
 
 
 def test_adaptive_asha_runs_all_trials(cluster):
