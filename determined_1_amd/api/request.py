@@ -126,16 +126,50 @@ class MasterClient:
             time.sleep(poll)
         raise TimeoutError(f"experiment {exp_id} did not finish in {timeout}s")
 
-    def trial_logs(self, trial_id: int, follow: bool = False, poll: float = 0.5) -> Iterator[Dict[str, Any]]:
-        offset = 0
-        while True:
-            logs = self.get(f"/trials/{trial_id}/logs", offset=offset)
-            for l in logs:
-                offset = max(offset, l["id"])
-                yield l
-            if not follow:
-                return
-            t = self.get(f"/trials/{trial_id}")
-            if t["state"] != "ACTIVE" and not logs:
-                return
-            time.sleep(poll)
+    # ------------------------------------------------------------------ /api/v1 streams
+    def stream(self, path: str, **params: Any) -> Iterator[Dict[str, Any]]:
+        """A server-streaming /api/v1 RPC: one ``{"result": ...}`` JSON object per line over a
+        chunked response (grpc-gateway framing); yields each ``result``."""
+        q = {k: ("true" if v is True else "false" if v is False else v) for k, v in params.items() if v is not None}
+        r = self.session.get(make_url(self.master, path), params=q, stream=True, timeout=(self.timeout, None))
+        try:
+            if r.status_code >= 300:
+                try:
+                    msg = r.json().get("error", r.text)
+                except ValueError:
+                    msg = r.text
+                raise APIError(r.status_code, msg)
+            for line in r.iter_lines():
+                line = line.strip()
+                if not line:
+                    continue
+                msg = json.loads(line)
+                if "error" in msg:
+                    raise APIError(500, str(msg["error"]))
+                yield msg.get("result", msg)
+        finally:
+            r.close()
+
+    def trial_logs(self, trial_id: int, follow: bool = False, tail: Optional[int] = None,
+                   **filters: Any) -> Iterator[Dict[str, Any]]:
+        """TrialLogs (``GET /api/v1/trials/:id/logs``): ``follow`` streams until the trial ends;
+        ``tail=N`` starts N matching lines before the end; filters: rank_ids, container_ids,
+        stdtypes (lists or comma strings)."""
+        params: Dict[str, Any] = {"follow": follow}
+        if tail:
+            params["offset"] = -int(tail)
+        for k, v in filters.items():
+            if v is not None:
+                params[k] = ",".join(str(x) for x in v) if isinstance(v, (list, tuple)) else v
+        yield from self.stream(f"/api/v1/trials/{trial_id}/logs", **params)
+
+    def trials_sample(self, exp_id: int, metric: str, metric_type: str = "METRIC_TYPE_VALIDATION",
+                      period_seconds: float = 30, **params: Any) -> Iterator[Dict[str, Any]]:
+        """TrialsSample (``/api/v1/experiments/:id/metrics-stream/trials-sample``)."""
+        yield from self.stream(f"/api/v1/experiments/{exp_id}/metrics-stream/trials-sample", metric_name=metric,
+                               metric_type=metric_type, period_seconds=period_seconds, **params)
+
+    def metric_batches(self, exp_id: int, metric: str, metric_type: str = "METRIC_TYPE_VALIDATION",
+                       period_seconds: float = 30) -> Iterator[Dict[str, Any]]:
+        yield from self.stream(f"/api/v1/experiments/{exp_id}/metrics-stream/batches", metric_name=metric,
+                               metric_type=metric_type, period_seconds=period_seconds)

@@ -176,6 +176,20 @@ def cmd_experiment_download_model_def(args: argparse.Namespace) -> None:
     print(f"wrote {len(md['files'])} entries to {out}")
 
 
+def cmd_experiment_metrics(args: argparse.Namespace) -> None:
+    """Follows ``/api/v1/experiments/:id/metrics-stream/trials-sample`` (the WebUI's learning-curve
+    feed): one line per new (trial, batches, value) point until the experiment ends."""
+    c = MasterClient(args.master)
+    mtype = "METRIC_TYPE_TRAINING" if args.type == "training" else "METRIC_TYPE_VALIDATION"
+    for msg in c.trials_sample(args.experiment_id, args.metric, mtype, period_seconds=args.period,
+                               max_trials=args.max_trials):
+        for t in msg.get("trials", []):
+            for d in t.get("data", []):
+                print(f"trial {t['trialId']}\tbatches {d['batches']}\t{args.metric} {d['value']:.6g}", flush=True)
+        if not args.follow:
+            return
+
+
 def cmd_experiment_checkpoints(args: argparse.Namespace) -> None:
     rows = MasterClient(args.master).get(f"/experiments/{args.experiment_id}/checkpoints")
     if args.best is not None:
@@ -196,20 +210,17 @@ def cmd_trial_describe(args: argparse.Namespace) -> None:
 
 
 def cmd_trial_logs(args: argparse.Namespace) -> None:
+    """Streams ``GET /api/v1/trials/:id/logs`` (reference ``det trial logs``)."""
     c = MasterClient(args.master)
-    if args.tail is not None or args.rank is not None or args.stdtype or args.contains:
-        params = {"limit": args.tail if args.tail is not None else 100000, "tail": "true" if args.tail else "false"}
-        if args.rank is not None:
-            params["rank_id"] = args.rank
-        if args.stdtype:
-            params["stdtype"] = args.stdtype
-        if args.contains:
-            params["contains"] = args.contains
-        for l in c.get(f"/trials/{args.trial_id}/logs", **params):
-            print(l["message"])
-        return
-    for l in c.trial_logs(args.trial_id, follow=args.follow):
-        print(l["message"])
+    filters = {}
+    if args.rank is not None:
+        filters["rank_ids"] = [args.rank]
+    if args.stdtype:
+        filters["stdtypes"] = [args.stdtype]
+    for l in c.trial_logs(args.trial_id, follow=args.follow, tail=args.tail, **filters):
+        if args.contains and args.contains not in l["message"]:
+            continue
+        print(l["message"], flush=True)
 
 
 def cmd_trial_kill(args: argparse.Namespace) -> None:
@@ -488,6 +499,14 @@ def build_parser() -> argparse.ArgumentParser:
     lc.add_argument("experiment_id", type=int)
     lc.add_argument("--best", type=int)
     lc.set_defaults(func=cmd_experiment_checkpoints)
+    mt = e.add_parser("metrics", help="stream a metric's learning curves (TrialsSample)")
+    mt.add_argument("experiment_id", type=int)
+    mt.add_argument("--metric", required=True)
+    mt.add_argument("--type", choices=["training", "validation"], default="validation")
+    mt.add_argument("--follow", "-f", action="store_true")
+    mt.add_argument("--period", type=float, default=5.0)
+    mt.add_argument("--max-trials", type=int, default=25)
+    mt.set_defaults(func=cmd_experiment_metrics)
 
     t = sub.add_parser("trial", aliases=["t"]).add_subparsers(dest="sub")
     d = t.add_parser("describe")

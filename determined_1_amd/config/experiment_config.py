@@ -69,6 +69,7 @@ def default_experiment_config(experiment_seed: Optional[int] = None) -> Dict[str
             "auto_tune_tensor_fusion": False,
             "grad_reduction": "fp32_accum",
             "rccl": {},
+            "hip_graph": False,
         },
         "perform_initial_validation": False,
         "min_checkpoint_period": {"batches": 0},

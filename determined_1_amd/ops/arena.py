@@ -215,6 +215,20 @@ class GradSink:
             h.remove()
         self._handles = []
 
+    def detach(self) -> None:
+        """Stop landing gradients (hooks, direct-landing slots) and re-pin ``.grad`` to the arena
+        views, leaving plain in-place accumulation.  Used before hipGraph capture: the sink's
+        pointer tables are uploaded from host staging buffers that a replay must not re-read."""
+        self.remove()
+        for a, idx in self.groups:
+            for i in idx:
+                p = a.params[i]
+                if getattr(p, "_det_grad_slot", None) is not None and p._det_grad_slot[0] is self:
+                    del p._det_grad_slot
+        self.fresh = False
+        for a, _ in self.groups:
+            a.zero_grad()
+
     def start_window(self) -> None:
         """Called by zero_grad: grads become None and the next backward steals them."""
         self.fresh = True

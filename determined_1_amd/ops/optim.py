@@ -22,7 +22,7 @@ RMSprop (``cifar10_pytorch/model_def.py:69``), Adadelta (``mnist_pytorch/model_d
 AdamW (``bert_squad_pytorch/model_def.py:63``).
 """
 import math
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import torch
 
@@ -217,6 +217,47 @@ class FusedOptimizer:
             if not any(MASTER_KEY in sd for sd in state_dict.get("state", {}).values()):
                 for a in gs.arenas:
                     a.sync_master_from_params()
+
+    # ------------------------------------------------------------------------------------------
+    # HIP-graph support (pytorch/_graph.py): a captured step replays the kernel launches with the
+    # scalar hyper-parameters baked in, so the graph is keyed by the values the NEXT step would
+    # pass, and the host-side bookkeeping a replay skips is advanced explicitly.
+    def graph_capturable(self) -> bool:
+        """Kernel arguments do not change from step to step by themselves (Adam's bias corrections
+        and Adagrad's lr decay do)."""
+        if self.kind in ("adam", "adamw"):
+            return False
+        if self.kind == "adagrad":
+            return all(float(g.get("lr_decay", 0.0)) == 0.0 for g in self.opt.param_groups)
+        return True
+
+    def graph_signature(self) -> Tuple[Any, ...]:
+        sig = []
+        for gi, gs in enumerate(self.groups):
+            group = self.opt.param_groups[gi]
+            h = self._hyper(group, gs) if gs.initialized else {"uninitialized": 1}
+            if self.kind == "sgd" and gs.initialized:
+                h["first"] = int(not gs.momentum_ready)
+            sig.append(tuple(sorted(h.items())))
+        return tuple(sig)
+
+    def host_state(self) -> List[Tuple[Optional[float], bool]]:
+        return [(float(gs.step) if gs.step is not None else None, gs.momentum_ready) for gs in self.groups]
+
+    def set_host_state(self, state: List[Tuple[Optional[float], bool]]) -> None:
+        for gs, (step, ready) in zip(self.groups, state):
+            if gs.step is not None and step is not None:
+                gs.step.fill_(step)
+            gs.momentum_ready = ready
+
+    def graph_replayed(self) -> None:
+        """What step() does on the host besides launching kernels."""
+        self.opt._opt_called = True  # type: ignore
+        for gs in self.groups:
+            if gs.step is not None:
+                gs.step += 1
+            if self.kind == "sgd":
+                gs.momentum_ready = True
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()

@@ -1,0 +1,198 @@
+"""HIP-graph replay of ``train_batch`` (``optimizations.hip_graph: true``).
+
+Small models (the CIFAR-10 CNN of the ASHA benchmark) are launch-bound on an MI355X: a batch of
+forward + backward + fused optimizer step is ~60 kernels of a few microseconds each, while the
+Python/dispatcher cost of issuing them is ~1.5 ms (``scripts/bench_cifar_trial.py``), so the GPU
+idles ~90% of a trial (``profiles/r2_asha_baseline_shape.json``).  The reference has no
+counterpart (it runs eager PyTorch under Horovod); the MI355X-first answer is to capture the whole
+user ``train_batch`` -- autograd, the arena optimizer's fused HIP kernel, ``zero_grad`` -- into one
+hipGraph and replay it per batch: one launch, no per-kernel host work.
+
+Why it is safe here: the arena design already keeps every tensor a step touches at a fixed
+address (flat parameter/gradient/optimizer-state arenas), so a replay sees the same memory as the
+capture.  What is NOT in the graph and is handled on the host:
+
+  * inputs: each batch is copied into the static input tensors the graph was captured with;
+  * outputs: the returned metric tensors are static; they are cloned before the next replay;
+  * optimizer bookkeeping: ``FusedOptimizer.graph_replayed()`` advances step counters;
+  * anything that changes kernel arguments (input shapes, learning rate / other
+    hyper-parameters, SGD's first-step flag, the epoch index passed to ``train_batch``) is part
+    of the graph key: a new key runs eagerly for ``WARMUP`` batches (lazy state, MIOpen find),
+    then is captured.  A key that keeps changing (per-batch LR schedules) turns graphs off.
+
+Requirements on user code (documented in the README): ``train_batch`` must not branch on host
+values other than the epoch index and must not synchronise (``.item()``) -- the same contract as
+CUDA graphs.  Eligibility is checked once: one process (no data-parallel bucketer), aggregation
+frequency 1, no dynamic loss scaler, every optimizer fused with step-invariant kernel arguments.
+Anything else runs eagerly, logged once.
+"""
+import logging
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import torch
+from torch.utils import _pytree as pytree
+
+WARMUP = 2        # eager batches per key before capturing (lazy init, MIOpen find, allocator)
+MAX_GRAPHS = 2    # live graphs (the epoch's full batch + its tail batch)
+THRASH_LIMIT = 8  # captures that replayed fewer than THRASH_MIN times -> graphs off
+THRASH_MIN = 4
+
+
+def _leaf_sig(x: Any) -> Any:
+    if isinstance(x, torch.Tensor):
+        return ("T", tuple(x.shape), x.dtype, x.device.type)
+    return ("V", repr(x))
+
+
+class _Graph:
+    def __init__(self, graph: "torch.cuda.CUDAGraph", static_in: List[torch.Tensor], in_spec: Any,
+                 out: Any) -> None:
+        self.graph = graph
+        self.static_in = static_in
+        self.in_spec = in_spec
+        self.out = out
+        self.replays = 0
+
+
+class TrainStepGraph:
+    """Per-controller graph cache.  ``run(batch, epoch_idx, batch_idx)`` returns the train_batch
+    metrics, eagerly or from a replay."""
+
+    def __init__(self, context: Any, train_batch: Callable[..., Any]) -> None:
+        self.context = context
+        self.train_batch = train_batch
+        self.fused = [st.fused for st in context._opt_states if st.fused is not None]
+        for f in self.fused:
+            # in a graph the per-parameter accumulate launches cost nothing on the host, and the
+            # sink's host-staged pointer tables are not replay-safe: plain arena accumulation
+            if f.sink is not None:
+                f.sink.detach()
+                f.sink = None
+        self.graphs: Dict[Any, _Graph] = {}
+        self.seen: Dict[Any, int] = {}
+        self.captures = 0
+        self.failed_captures = 0
+        self.replays = 0
+        self.disabled_reason: Optional[str] = None
+        self.pool = None
+
+    # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def ineligible_reason(context: Any) -> Optional[str]:
+        if context.device.type != "cuda":
+            return "not on a GPU"
+        if context.dist_config.use:
+            return "data-parallel trial (gradient bucketer runs on its own stream)"
+        if context.dist_config.aggregation_frequency != 1:
+            return "aggregation_frequency > 1"
+        if context._amp is not None and context._amp.scaler is not None:
+            return "dynamic loss scaling syncs on overflow"
+        if context._timers.enabled:
+            return "DET_STEP_TIMERS synchronises the step"
+        if not context._opt_states:
+            return "no wrapped optimizer"
+        for st in context._opt_states:
+            if st.fused is None:
+                return f"optimizer {type(st.opt).__name__} is not fused"
+            if not st.fused.graph_capturable():
+                return f"fused {st.fused.kind} changes kernel arguments every step"
+        return None
+
+    def _key(self, leaves: List[Any], epoch_idx: int) -> Any:
+        return (tuple(_leaf_sig(x) for x in leaves), epoch_idx, tuple(f.graph_signature() for f in self.fused))
+
+    def _eager(self, batch: Any, epoch_idx: int, batch_idx: int) -> Any:
+        with self.context._autocast():
+            return self.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
+
+    # ------------------------------------------------------------------------------------------
+    def run(self, batch: Any, epoch_idx: int, batch_idx: int) -> Any:
+        if self.disabled_reason is not None:
+            return self._eager(batch, epoch_idx, batch_idx)
+        leaves, spec = pytree.tree_flatten(batch)
+        if any(isinstance(x, torch.Tensor) and x.device.type != "cuda" for x in leaves):
+            self._disable("train batch has host tensors")
+            return self._eager(batch, epoch_idx, batch_idx)
+        key = self._key(leaves, epoch_idx)
+        g = self.graphs.get(key)
+        if g is not None:
+            return self._replay(g, leaves)
+        n = self.seen.get(key, 0) + 1
+        self.seen[key] = n
+        if n <= WARMUP:
+            return self._eager(batch, epoch_idx, batch_idx)
+        g = self._capture(key, leaves, spec, epoch_idx, batch_idx)
+        if g is None:
+            return self._eager(batch, epoch_idx, batch_idx)
+        # the capture recorded but did not execute this batch's work: run it now (host state
+        # was advanced during the capture itself)
+        g.graph.replay()
+        self.replays += 1
+        g.replays += 1
+        return self._clone_out(g.out)
+
+    def _replay(self, g: _Graph, leaves: List[Any]) -> Any:
+        for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
+            dst.copy_(src, non_blocking=True)
+        g.graph.replay()
+        for f in self.fused:
+            f.graph_replayed()
+        self.replays += 1
+        g.replays += 1
+        return self._clone_out(g.out)
+
+    @staticmethod
+    def _clone_out(out: Any) -> Any:
+        return pytree.tree_map(lambda t: t.detach().clone() if isinstance(t, torch.Tensor) else t, out)
+
+    def _capture(self, key: Any, leaves: List[Any], spec: Any, epoch_idx: int, batch_idx: int) -> Optional[_Graph]:
+        stale = [k for k, v in self.graphs.items() if v.replays < THRASH_MIN]
+        if self.captures - len(self.graphs) >= THRASH_LIMIT and len(stale) == len(self.graphs):
+            self._disable("graph key changes every few batches (per-batch hyper-parameter schedule?)")
+            return None
+        while len(self.graphs) >= MAX_GRAPHS:
+            oldest = next(iter(self.graphs))
+            del self.graphs[oldest]
+        static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
+        it = iter(static_in)
+        static_leaves = [next(it) if isinstance(x, torch.Tensor) else x for x in leaves]
+        static_batch = pytree.tree_unflatten(static_leaves, spec)
+        host = [f.host_state() for f in self.fused]
+        graph = torch.cuda.CUDAGraph()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        try:
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph, pool=self.pool):
+                out = self._eager(static_batch, epoch_idx, batch_idx)
+        except Exception as e:  # capture-unsafe op in user code or a library: stay eager
+            for f, h in zip(self.fused, host):
+                f.set_host_state(h)
+            self.failed_captures += 1
+            self._disable(f"capture failed: {type(e).__name__}: {e}")
+            torch.cuda.synchronize()
+            return None
+        self.captures += 1
+        g = _Graph(graph, static_in, spec, out)
+        self.graphs[key] = g
+        return g
+
+    def _disable(self, reason: str) -> None:
+        if self.disabled_reason is None:
+            logging.warning("hip_graph: running train_batch eagerly: %s", reason)
+        self.disabled_reason = reason
+        self.graphs.clear()
+
+    def stats(self) -> Dict[str, Any]:
+        return {"captures": self.captures, "replays": self.replays, "failed_captures": self.failed_captures,
+                "disabled": self.disabled_reason}
+
+
+def build(context: Any, train_batch: Callable[..., Any], enabled: bool) -> Tuple[Optional[TrainStepGraph], Optional[str]]:
+    if not enabled:
+        return None, None
+    reason = TrainStepGraph.ineligible_reason(context)
+    if reason is not None:
+        logging.warning("optimizations.hip_graph is set but train_batch will run eagerly: %s", reason)
+        return None, reason
+    return TrainStepGraph(context, train_batch), None

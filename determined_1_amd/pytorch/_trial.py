@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from determined_1_amd import check, errors, trial, util, workload
 from determined_1_amd.parallel import dist as pdist
-from determined_1_amd.pytorch import _callback
+from determined_1_amd.pytorch import _callback, _graph
 from determined_1_amd.pytorch._context import PyTorchTrialContext
 from determined_1_amd.pytorch._data import DataLoader, DevicePrefetcher, TorchData, data_length
 from determined_1_amd.pytorch._lr_scheduler import LRScheduler
@@ -60,6 +60,8 @@ class PyTorchTrialController(trial.LoopTrialController):
         self.validation_loader = None  # type: Optional[torch.utils.data.DataLoader]
         self._set_data_loaders()
         self.training_iterator = self._make_train_iterator()
+        self._graph = None  # type: Optional[_graph.TrainStepGraph]
+        self._graph_checked = False
         # arenas / fused optimizers / bucketers, then restore, then rank-0 broadcast
         self.context._finalize()
         self._load()
@@ -214,6 +216,13 @@ class PyTorchTrialController(trial.LoopTrialController):
             else:
                 raise AssertionError(f"Unexpected workload: {w.kind}")
 
+    def _hip_graph_enabled(self) -> bool:
+        env = os.environ.get("DET_HIP_GRAPH")
+        if env is not None:
+            return env not in ("", "0")
+        opt = self.env.experiment_config.get("optimizations", {}) or {}
+        return bool(opt.get("hip_graph", False))
+
     def get_epoch_idx(self, batch_id: int) -> int:
         return batch_id // len(self.training_loader)
 
@@ -240,9 +249,15 @@ class PyTorchTrialController(trial.LoopTrialController):
             num_inputs += n
             self.context._current_batch_idx = batch_idx
             self.context._loss_ids = {}
-            with self.context._autocast():
-                tr_metrics = self.trial.train_batch(batch=batch, epoch_idx=self.get_epoch_idx(batch_idx),
-                                                    batch_idx=batch_idx)
+            if self._graph is not None:
+                tr_metrics = self._graph.run(batch, self.get_epoch_idx(batch_idx), batch_idx)
+            else:
+                with self.context._autocast():
+                    tr_metrics = self.trial.train_batch(batch=batch, epoch_idx=self.get_epoch_idx(batch_idx),
+                                                        batch_idx=batch_idx)
+                if not self._graph_checked and self.context._finalized:
+                    self._graph_checked = True
+                    self._graph, _ = _graph.build(self.context, self.trial.train_batch, self._hip_graph_enabled())
             if isinstance(tr_metrics, torch.Tensor):
                 tr_metrics = {"loss": tr_metrics}
             check.is_instance(tr_metrics, dict, "train_batch() must return a dictionary mapping string names to "
@@ -250,6 +265,9 @@ class PyTorchTrialController(trial.LoopTrialController):
             for lr_scheduler in self.context.lr_schedulers:
                 self._auto_step_lr_scheduler_per_batch(batch_idx, lr_scheduler)
             per_batch.append({k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in tr_metrics.items()})
+            # drop the last batch's autograd graph now: a live graph keeps its AccumulateGrad
+            # nodes bound to this stream, which breaks a hipGraph capture of the next batch
+            del tr_metrics
         per_batch = _metrics_to_host(per_batch)
         self.last_step_timers = timers.report(step_id)
         if self.dist_config.use and self.dist_config.average_training_metrics:

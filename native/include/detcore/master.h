@@ -75,6 +75,7 @@ class Master {
 
  private:
   void InstallRoutes();
+  void InstallApiV1();  // api_v1.cc: the reference's /api/v1 grpc-gateway surface
   void HandleAgentSocket(const net::Request& req, net::WsPtr ws);
   void HandleTrialSocket(const net::Request& req, net::WsPtr ws);
   void HandleRWLockSocket(const net::Request& req, net::WsPtr ws);

@@ -47,6 +47,11 @@ struct Response {
   std::string content_type = "application/json";
   std::map<std::string, std::string> headers;
   std::string body;
+  // Streaming body (grpc-gateway server streams): when set, the server sends the headers with
+  // chunked transfer encoding and calls stream(write); each write(chunk) sends one chunk and
+  // returns false once the client is gone or the server is stopping.
+  using Writer = std::function<bool(const std::string&)>;
+  std::function<void(const Writer&)> stream;
   static Response Json(int status, const std::string& body) {
     Response r;
     r.status = status;
@@ -104,6 +109,10 @@ class HttpServer {
   int Listen(const std::string& host, int port);
   void Start();  // accept loop on a background thread
   void Stop();
+  // Route a request in-process (no auth hook, plain HTTP routes only): lets one API surface be
+  // layered on another, e.g. /api/v1/* over the legacy REST handlers.
+  Response Dispatch(Request req) const;
+  bool running() const { return running_.load(); }
   int port() const { return port_; }
 
  private:
@@ -114,6 +123,7 @@ class HttpServer {
     WsHandler ws;
   };
   bool Match(const RouteEntry& r, const std::vector<std::string>& segs, std::map<std::string, std::string>* params) const;
+  const RouteEntry* Find(Request* req, bool want_ws, bool* path_hit) const;
   void Serve(int fd, std::string peer);
   std::vector<RouteEntry> routes_;
   std::function<bool(const Request&)> auth_;

@@ -23,7 +23,7 @@ Json DefaultExperimentConfig(uint32_t seed) {
                       "average_training_metrics": false, "gradient_compression": false,
                       "mixed_precision": "O0", "tensor_fusion_threshold": 64,
                       "tensor_fusion_cycle_time": 5, "auto_tune_tensor_fusion": false,
-                      "grad_reduction": "fp32_accum", "rccl": {}},
+                      "grad_reduction": "fp32_accum", "rccl": {}, "hip_graph": false},
     "perform_initial_validation": false,
     "min_checkpoint_period": {"batches": 0},
     "min_validation_period": {"batches": 0},

@@ -1036,6 +1036,7 @@ void Master::InstallRoutes() {
   http_.RouteWs("/agents", [this](const net::Request& r, net::WsPtr ws) { HandleAgentSocket(r, ws); });
   http_.RouteWs("/ws/trial/:e/:t/:c", [this](const net::Request& r, net::WsPtr ws) { HandleTrialSocket(r, ws); });
   http_.RouteWs("/ws/data-layer/*", [this](const net::Request& r, net::WsPtr ws) { HandleRWLockSocket(r, ws); });
+  InstallApiV1();
 }
 
 // One socket = one lock request; the lock is held until the socket closes (reference

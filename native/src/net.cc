@@ -456,6 +456,27 @@ void HttpServer::Stop() {
   conns_cv_.wait_for(l, std::chrono::seconds(5), [&] { return active_conns_ == 0; });
 }
 
+const HttpServer::RouteEntry* HttpServer::Find(Request* req, bool want_ws, bool* path_hit) const {
+  auto segs = SplitPath(req->path);
+  for (auto& r : routes_) {
+    std::map<std::string, std::string> params;
+    if (!Match(r, segs, &params)) continue;
+    if ((r.ws != nullptr) != want_ws) continue;
+    *path_hit = true;
+    if (r.method != req->method) continue;
+    req->params = std::move(params);
+    return &r;
+  }
+  return nullptr;
+}
+
+Response HttpServer::Dispatch(Request req) const {
+  bool path_hit = false;
+  const RouteEntry* hit = Find(&req, false, &path_hit);
+  if (!hit) return Response::Json(path_hit ? 405 : 404, R"({"error":"not found"})");
+  return hit->h(req);
+}
+
 void HttpServer::Serve(int fd, std::string peer) {
   std::string buf;
   for (;;) {
@@ -499,21 +520,9 @@ void HttpServer::Serve(int fd, std::string peer) {
       req.body = buf.substr(0, cl);
       buf.erase(0, cl);
     }
-    // route
-    auto segs = SplitPath(req.path);
-    const RouteEntry* hit = nullptr;
     bool path_hit = false;
     bool want_ws = Lower(req.headers["upgrade"]) == "websocket";
-    for (auto& r : routes_) {
-      std::map<std::string, std::string> params;
-      if (!Match(r, segs, &params)) continue;
-      if ((r.ws != nullptr) != want_ws) continue;
-      path_hit = true;
-      if (r.method != req.method) continue;
-      hit = &r;
-      req.params = std::move(params);
-      break;
-    }
+    const RouteEntry* hit = Find(&req, want_ws, &path_hit);
     if (hit && hit->ws) {
       std::string key = req.headers["sec-websocket-key"];
       std::string accept = Base64Encode(Sha1(key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11"));
@@ -544,12 +553,36 @@ void HttpServer::Serve(int fd, std::string peer) {
         res = Response::Json(400, "{\"error\":\"" + esc + "\"}");
       }
     }
+    bool close_after = Lower(req.headers["connection"]) == "close";
+    if (res.stream) {
+      std::ostringstream hs;
+      hs << "HTTP/1.1 " << res.status << " " << StatusText(res.status) << "\r\n"
+         << "Content-Type: " << res.content_type << "\r\n"
+         << "Transfer-Encoding: chunked\r\n";
+      for (auto& kv : res.headers) hs << kv.first << ": " << kv.second << "\r\n";
+      hs << (close_after ? "Connection: close\r\n" : "Connection: keep-alive\r\n") << "\r\n";
+      std::string h = hs.str();
+      bool ok = WriteAll(fd, h.data(), h.size());
+      if (ok) {
+        res.stream([&](const std::string& chunk) {
+          if (!ok || !running_.load()) return false;
+          if (chunk.empty()) return true;  // an empty chunk would end the body
+          char len[32];
+          std::snprintf(len, sizeof(len), "%zx\r\n", chunk.size());
+          std::string frame = std::string(len) + chunk + "\r\n";
+          ok = WriteAll(fd, frame.data(), frame.size());
+          return ok;
+        });
+        ok = ok && WriteAll(fd, "0\r\n\r\n", 5);
+      }
+      if (!ok || close_after) break;
+      continue;
+    }
     std::ostringstream os;
     os << "HTTP/1.1 " << res.status << " " << StatusText(res.status) << "\r\n"
        << "Content-Type: " << res.content_type << "\r\n"
        << "Content-Length: " << res.body.size() << "\r\n";
     for (auto& kv : res.headers) os << kv.first << ": " << kv.second << "\r\n";
-    bool close_after = Lower(req.headers["connection"]) == "close";
     os << (close_after ? "Connection: close\r\n" : "Connection: keep-alive\r\n") << "\r\n";
     std::string out = os.str() + res.body;
     if (!WriteAll(fd, out.data(), out.size()) || close_after) break;

@@ -22,6 +22,7 @@ def main() -> None:
     ap.add_argument("--batches", type=int, default=2000)
     ap.add_argument("--chunk", type=int, default=500)
     ap.add_argument("--amp", default="O2")
+    ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
     args = ap.parse_args()
     t0 = time.time()
     import torch
@@ -35,7 +36,8 @@ def main() -> None:
                                "layer1_dropout": 0.25, "layer2_dropout": 0.25, "layer3_dropout": 0.5,
                                "amp": args.amp},
            "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": args.batches}},
-           "records_per_epoch": 50000, "scheduling_unit": args.chunk}
+           "records_per_epoch": 50000, "scheduling_unit": args.chunk,
+           "optimizations": {"hip_graph": bool(args.hip_graph)}}
     marks = []
     res = {}
 
@@ -75,6 +77,7 @@ def main() -> None:
                       "records_per_s": round(args.batch * 1000.0 / ms_batch, 1),
                       "first_chunk_s": round(trains[0], 3), "validation_10k_s": round(per["val"], 3),
                       "import_s": round(t_import, 2), "controller_build_s": round(t_build, 2),
+                      "hip_graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
                       "loss": res[names[-2]]["metrics"]["avg_metrics"].get("loss") if len(names) > 1 else None}),
           flush=True)
 

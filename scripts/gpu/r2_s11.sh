@@ -6,5 +6,5 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/s11
 export TMPDIR=/tmp DET_BENCH_LOGDIR=$GRAFT_REPO_ROOT/gpurun_out/s11
-timeout -k 10 1000 python -u scripts/bench_asha.py --slots 1 --timeout 960 > gpurun_out/s11/asha.json 2> gpurun_out/s11/asha.err || { tail -30 gpurun_out/s11/asha.err; tail -30 gpurun_out/s11/agent-0.log; exit 1; }
+timeout -k 10 1080 python -u scripts/bench_asha.py --slots 1 --timeout 1040 > gpurun_out/s11/asha.json 2> gpurun_out/s11/asha.err || { tail -30 gpurun_out/s11/asha.err; tail -30 gpurun_out/s11/agent-0.log; exit 1; }
 cat gpurun_out/s11/asha.json
