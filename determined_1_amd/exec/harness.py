@@ -65,6 +65,11 @@ def main() -> int:
         logging.info("trial process forked from warm zygote %s", os.environ["DET_ZYGOTE_PID"])
     timeline.mark("imports done")
     env = EnvContext.from_environ()
+    # the shipped MIOpen find-db + kernel cache (ops/miopen_db): trial containers start with the
+    # conv kernels already compiled instead of JIT-compiling them per container
+    from determined_1_amd.ops import miopen_db
+
+    miopen_db.configure(os.environ)
     slots_per_trial = int((env.experiment_config.get("resources") or {}).get("slots_per_trial", 1) or 1)
     if env.use_gpu and slots_per_trial == 1 and os.environ.get("DET_EARLY_GPU_INIT", "1") == "1":
         # single-process trial: this process is the one that uses the GPU (a multi-slot launcher

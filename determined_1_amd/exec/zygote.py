@@ -42,6 +42,9 @@ def preload() -> None:
     import torch.nn  # noqa: F401
     import torch.optim  # noqa: F401
     import torch.utils.data  # noqa: F401
+    # torch.optim.Optimizer.__init__ imports torch._dynamo lazily: 1.5 s per trial process on a
+    # fresh box (bytecode-compiling dynamo + sympy), measured in scripts/dbg/profile_trial_build.py
+    import torch._dynamo  # noqa: F401
 
     import determined_1_amd  # noqa: F401
     import determined_1_amd.exec.harness  # noqa: F401

@@ -40,6 +40,7 @@ struct MasterConfig {
   // telemetry.{enabled, file}: reference Segment events (master/internal/telemetry) written as JSON
   // lines to a local file -- there is no egress; disabled unless a file is configured.
   std::string telemetry_file;
+  Json kubernetes;   // resource_manager {type: kubernetes, api_server, namespace, max_slots_per_pod, ...}; empty = agents
   Json provisioner;  // {max_instances, min_instances, slots_per_instance, ...}; empty = disabled  // security.authentication: tokens required on the REST API
   static MasterConfig FromJson(const Json& j);
   Json ToJson() const;

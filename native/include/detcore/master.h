@@ -14,6 +14,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -24,6 +25,7 @@
 #include "detcore/actor.h"
 #include "detcore/config.h"
 #include "detcore/json.h"
+#include "detcore/kubernetes.h"
 #include "detcore/net.h"
 #include "detcore/rw_coordinator.h"
 #include "detcore/store.h"
@@ -39,6 +41,7 @@ struct AgentConn {
   std::string label;
   std::string host;  // address the agent connected from (trial processes run there)
   net::WsPtr ws;
+  std::function<bool(const Json&)> send;  // virtual agents (Kubernetes RM): master -> agent messages
   Json devices;
   std::set<std::string> containers;
 };
@@ -77,6 +80,14 @@ class Master {
   void InstallRoutes();
   void InstallApiV1();  // api_v1.cc: the reference's /api/v1 grpc-gateway surface
   void HandleAgentSocket(const net::Request& req, net::WsPtr ws);
+ public:
+  // agent protocol, shared by WebSocket agents and virtual agents (kubernetes.cc)
+  bool RegisterAgent(const std::shared_ptr<AgentConn>& conn, std::string* err);
+  void OnAgentMessage(const std::shared_ptr<AgentConn>& conn, const Json& m);
+  void AgentGone(const std::shared_ptr<AgentConn>& conn);
+  std::string advertised_host() const { return advertised_host_; }
+
+ private:
   void HandleTrialSocket(const net::Request& req, net::WsPtr ws);
   void HandleRWLockSocket(const net::Request& req, net::WsPtr ws);
   void RestoreExperiments();
@@ -102,6 +113,7 @@ class Master {
   bool stopped_ = false;
   std::atomic<bool> shutting_down_{false};
   std::mutex telemetry_mu_;
+  std::unique_ptr<KubernetesRM> kube_;
 };
 
 // Helpers shared by the master translation units.

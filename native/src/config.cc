@@ -279,6 +279,8 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
   c.scheduler_tick_ms = j.get_double("scheduler_tick_ms", c.scheduler_tick_ms);
   c.python = j.get_string("python", c.python);
   c.provisioner = j["provisioner"];
+  if (j["resource_manager"].is_object() && j["resource_manager"].get_string("type", "agent") == "kubernetes")
+    c.kubernetes = j["resource_manager"];
   if (j["security"].is_object()) c.require_auth = j["security"].get_bool("authentication", c.require_auth);
   if (j["telemetry"].is_object() && j["telemetry"].get_bool("enabled", true))
     c.telemetry_file = j["telemetry"].get_string("file", "");
@@ -306,6 +308,7 @@ Json MasterConfig::ToJson() const {
   sec["authentication"] = require_auth;
   j["security"] = sec;
   j["provisioner"] = provisioner;
+  if (kubernetes.is_object()) j["resource_manager"] = kubernetes;
   Json tel = Json::object();
   tel["enabled"] = !telemetry_file.empty();
   tel["file"] = telemetry_file;

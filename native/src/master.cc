@@ -215,7 +215,8 @@ bool Master::SendToAgent(const std::string& agent_id, const Json& msg) {
     if (it == agents_.end()) return false;
     a = it->second;
   }
-  return a->ws->Send(msg.dump());
+  if (a->send) return a->send(msg);
+  return a->ws && a->ws->Send(msg.dump());
 }
 
 std::string Master::AgentHost(const std::string& agent_id) {
@@ -1070,6 +1071,17 @@ void Master::ReportTelemetry(const std::string& event, Json properties) {
   f << line.dump() << "\n";
 }
 
+bool Master::RegisterAgent(const std::shared_ptr<AgentConn>& conn, std::string* err) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (conn->pool.empty() || !pools_.count(conn->pool)) conn->pool = pools_.begin()->first;
+  if (agents_.count(conn->id)) {
+    *err = "agent id already connected: " + conn->id;
+    return false;
+  }
+  agents_[conn->id] = conn;
+  return true;
+}
+
 void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
   auto conn = std::make_shared<AgentConn>();
   conn->id = r.Query("id", "agent-" + NewUUID().substr(0, 8));
@@ -1077,17 +1089,13 @@ void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
   conn->label = r.Query("label", "");
   conn->host = r.Query("host", r.remote_addr);
   conn->ws = ws;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (conn->pool.empty() || !pools_.count(conn->pool)) conn->pool = pools_.begin()->first;
-    if (agents_.count(conn->id)) {
-      Json m = Json::object();
-      m["type"] = "Error";
-      m["error"] = "agent id already connected: " + conn->id;
-      ws->Send(m.dump());
-      return;
-    }
-    agents_[conn->id] = conn;
+  std::string err;
+  if (!RegisterAgent(conn, &err)) {
+    Json m = Json::object();
+    m["type"] = "Error";
+    m["error"] = err;
+    ws->Send(m.dump());
+    return;
   }
   Json opts = Json::object();
   opts["type"] = "MasterSetAgentOptions";
@@ -1102,45 +1110,55 @@ void Master::HandleAgentSocket(const net::Request& r, net::WsPtr ws) {
     } catch (const std::exception&) {
       return;
     }
-    const std::string t = m.get_string("type", "");
-    if (t == "AgentStarted") {
-      sched::Agent a;
-      a.id = conn->id;
-      a.label = m.get_string("label", conn->label);
-      conn->devices = m["devices"];
-      {
-        Json props = Json::object();
-        props["uuid"] = conn->id;
-        props["devices"] = conn->devices;
-        ReportTelemetry("agent_connected", props);
-      }
-      for (auto& d : m["devices"].as_array()) {
-        sched::Slot s;
-        s.device_id = static_cast<int>(d.get_int("id", 0));
-        s.uuid = d.get_string("uuid", "");
-        s.type = d.get_string("type", "gpu");
-        a.slots.push_back(s);
-      }
-      Pool(conn->pool)->Tell(AddAgent{a});
-    } else if (t == "ContainerStateChanged") {
-      std::string cid = m.get_string("container_id", "");
-      Ref tr = TrialForContainer(cid);
-      if (tr)
-        tr->Tell(ContainerStateMsg{cid, m.get_string("state", ""), static_cast<int>(m.get_int("exit_code", 0)),
-                                   m.get_string("failure", ""), m.get_string("address", "")});
-    } else if (t == "ContainerLog" && !m.get_string("task_id", "").empty()) {
-      Json row = Json::object();
-      row["task_id"] = m["task_id"];
-      row["message"] = m["log"];
-      row["stdtype"] = m["stdtype"];
-      row["timestamp"] = NowRFC3339();
-      logs_->Append("task-" + m.get_string("task_id", ""), {row});
-    } else if (t == "ContainerLog") {
-      AppendTrialLog(m.get_int("trial_id", 0), m.get_string("log", ""), m.get_string("stdtype", "stdout"),
-                     m.get_string("container_id", ""), static_cast<int>(m.get_int("rank", 0)));
-    }
+    OnAgentMessage(conn, m);
   });
-  // disconnect: every container on the agent is gone (reference agent.go:114-126)
+  AgentGone(conn);
+}
+
+// One agent -> master message (a real agent's WebSocket, or a virtual agent such as the
+// Kubernetes resource manager's).
+void Master::OnAgentMessage(const std::shared_ptr<AgentConn>& conn, const Json& m) {
+  const std::string t = m.get_string("type", "");
+  if (t == "AgentStarted") {
+    sched::Agent a;
+    a.id = conn->id;
+    a.label = m.get_string("label", conn->label);
+    conn->devices = m["devices"];
+    {
+      Json props = Json::object();
+      props["uuid"] = conn->id;
+      props["devices"] = conn->devices;
+      ReportTelemetry("agent_connected", props);
+    }
+    for (auto& d : m["devices"].as_array()) {
+      sched::Slot s;
+      s.device_id = static_cast<int>(d.get_int("id", 0));
+      s.uuid = d.get_string("uuid", "");
+      s.type = d.get_string("type", "gpu");
+      a.slots.push_back(s);
+    }
+    Pool(conn->pool)->Tell(AddAgent{a});
+  } else if (t == "ContainerStateChanged") {
+    std::string cid = m.get_string("container_id", "");
+    Ref tr = TrialForContainer(cid);
+    if (tr)
+      tr->Tell(ContainerStateMsg{cid, m.get_string("state", ""), static_cast<int>(m.get_int("exit_code", 0)),
+                                 m.get_string("failure", ""), m.get_string("address", "")});
+  } else if (t == "ContainerLog" && !m.get_string("task_id", "").empty()) {
+    Json row = Json::object();
+    row["task_id"] = m["task_id"];
+    row["message"] = m["log"];
+    row["stdtype"] = m["stdtype"];
+    row["timestamp"] = NowRFC3339();
+    logs_->Append("task-" + m.get_string("task_id", ""), {row});
+  } else if (t == "ContainerLog") {
+    AppendTrialLog(m.get_int("trial_id", 0), m.get_string("log", ""), m.get_string("stdtype", "stdout"),
+                   m.get_string("container_id", ""), static_cast<int>(m.get_int("rank", 0)));
+  }
+}
+
+void Master::AgentGone(const std::shared_ptr<AgentConn>& conn) {
+  // every container on the agent is gone (reference agent.go:114-126)
   std::vector<std::string> cids;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -1216,6 +1234,10 @@ int Master::Start() {
       sys_->ActorOf("provisioners/" + p, std::make_unique<ProvisionerActor>(this, p, pc));
     Log("provisioner enabled: max " + std::to_string(pc.max_instances) + " agents per pool");
   }
+  if (cfg_.kubernetes.is_object()) {
+    kube_ = std::make_unique<KubernetesRM>(this, KubeConfig::FromJson(cfg_.kubernetes));
+    kube_->Start();
+  }
   RestoreExperiments();
   Log(std::string("listening on ") + cfg_.listen_host + ":" + std::to_string(port_) + " scheduler=" + cfg_.scheduler);
   return port_;
@@ -1228,10 +1250,12 @@ void Master::Stop() {
     stopped_ = true;
   }
   shutting_down_ = true;
+  if (kube_) kube_->Stop();
   http_.Stop();
   {
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& a : agents_) a.second->ws->Close();
+    for (auto& a : agents_)
+      if (a.second->ws) a.second->ws->Close();
   }
   sys_->Shutdown();
   store_->Flush();

@@ -26,7 +26,10 @@ static void Usage() {
   std::fprintf(stderr,
                "usage: det-master [--config-file FILE.json] [--host H] [--port P] [--store-dir DIR]\n"
                "                  [--scheduler fair_share|priority|round_robin] [--fitting-policy best|worst]\n"
-               "                  [--resource-pools a,b] [--checkpoint-host-path DIR] [--python PY]\n");
+               "                  [--resource-pools a,b] [--checkpoint-host-path DIR] [--python PY]\n"
+               "                  [--kubernetes-api HOST:PORT [--kubernetes-namespace NS]\n"
+               "                   [--kubernetes-max-slots-per-pod N] [--kubernetes-slot-type gpu|cpu]\n"
+               "                   [--kubernetes-cpu-slots-per-node N] [--kubernetes-master-host H]]\n");
 }
 
 int main(int argc, char** argv) {
@@ -75,6 +78,21 @@ int main(int argc, char** argv) {
       cfgj["provisioner"]["slots_per_instance"] = std::stoi(next());
     } else if (a == "--provision-idle-ms") {
       cfgj["provisioner"]["max_idle_agent_period_ms"] = std::stoi(next());
+    } else if (a == "--kubernetes-api") {
+      cfgj["resource_manager"]["type"] = "kubernetes";
+      cfgj["resource_manager"]["api_server"] = next();
+    } else if (a == "--kubernetes-namespace") {
+      cfgj["resource_manager"]["namespace"] = next();
+    } else if (a == "--kubernetes-max-slots-per-pod") {
+      cfgj["resource_manager"]["max_slots_per_pod"] = std::stoi(next());
+    } else if (a == "--kubernetes-slot-type") {
+      cfgj["resource_manager"]["slot_type"] = next();
+    } else if (a == "--kubernetes-cpu-slots-per-node") {
+      cfgj["resource_manager"]["cpu_slots_per_node"] = std::stoi(next());
+    } else if (a == "--kubernetes-python") {
+      cfgj["resource_manager"]["python"] = next();
+    } else if (a == "--kubernetes-master-host") {
+      cfgj["resource_manager"]["master_service_host"] = next();
     } else if (a == "--telemetry-file") {
       cfgj["telemetry"]["file"] = next();
     } else if (a == "--require-auth") {

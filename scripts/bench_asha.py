@@ -71,6 +71,8 @@ def main() -> None:
     ap.add_argument("--slots", type=int, default=0, help="GPU slots to use (0 = every GPU the agent detects)")
     ap.add_argument("--timeout", type=float, default=3600)
     ap.add_argument("--no-zygote", action="store_true", help="cold python exec per container (A/B)")
+    ap.add_argument("--seed", type=int, default=1, help="reproducibility.experiment_seed (fixes the sampled hparams)")
+    ap.add_argument("--no-hip-graph", action="store_true", help="eager train_batch (A/B)")
     ap.add_argument("--artificial-slots", type=int, default=0, help="CPU dry run without GPUs")
     args = ap.parse_args()
     from determined_1_amd import gpu
@@ -80,6 +82,9 @@ def main() -> None:
     ex = REPO / "examples" / "computer_vision" / "cifar10_pytorch"
     cfg = yaml.safe_load((ex / "adaptive.yaml").read_text())
     cfg["searcher"]["max_trials"] = args.max_trials
+    cfg.setdefault("reproducibility", {})["experiment_seed"] = args.seed
+    if args.no_hip_graph:
+        cfg.setdefault("optimizations", {})["hip_graph"] = False
     if args.max_length_batches:
         cfg["searcher"]["max_length"] = {"batches": args.max_length_batches}
         # validate only where the searcher asks (end of each rung); the real config validates every
@@ -140,6 +145,8 @@ def main() -> None:
                           "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
                           "slot_occupancy": round(occupancy, 3), "scheduler_idle_frac": round(1 - occupancy, 3),
                           "zygote": not args.no_zygote, "per_container_s": timeline,
+                          "hip_graph": bool((cfg.get("optimizations") or {}).get("hip_graph", False)),
+                          "experiment_seed": args.seed,
                           "config": {"max_length": cfg["searcher"]["max_length"], "max_trials": args.max_trials,
                                      "records_per_epoch": cfg.get("records_per_epoch"),
                                      "min_validation_period": cfg.get("min_validation_period"),
