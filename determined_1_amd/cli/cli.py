@@ -404,10 +404,82 @@ def cmd_command_kill(args: argparse.Namespace) -> None:
     MasterClient(args.master).post(f"/commands/{args.command_id}/kill")
 
 
-def cmd_unavailable(what: str):
+def _start_task(client: MasterClient, kind: str, argv: List[str], env: List[str], slots: int,
+                description: str, wait: float) -> int:
+    cfg = {"entrypoint": argv, "type": kind, "resources": {"slots": slots}, "description": description,
+           "environment": {"environment_variables": env}}
+    cid = client.post("/commands", {"config": cfg, "context": []})["id"]
+    deadline = time.time() + wait
+    while time.time() < deadline:
+        c = client.get(f"/commands/{cid}")
+        if c.get("ready") or c.get("state") == "TERMINATED":
+            break
+        time.sleep(0.2)
+    return cid
+
+
+def cmd_shell_start(args: argparse.Namespace) -> None:
+    """``det shell start``: a shell task (exec/shell.py) with a fresh token; attaches unless -d."""
+    import secrets
+
+    client = MasterClient(args.master)
+    token = secrets.token_hex(16)
+    cid = _start_task(client, "shell", ["python3", "-m", "determined_1_amd.exec.shell"],
+                      [f"DET_SHELL_TOKEN={token}"], args.slots, "Shell", args.timeout)
+    _save_shell_token(client.master, cid, token)
+    c = client.get(f"/commands/{cid}")
+    if not c.get("ready"):
+        sys.exit(f"shell {cid} did not become ready (state {c.get('state')})")
+    print(f"Shell {cid} ready", file=sys.stderr)
+    if not args.detach:
+        from determined_1_amd.exec.shell import open_shell
+
+        sys.exit(open_shell(client, cid, token))
+
+
+def _shell_token_path(master: str) -> str:
+    return os.path.join(os.path.expanduser("~"), ".det-mi355x", "shells-" + master.replace(":", "_") + ".json")
+
+
+def _save_shell_token(master: str, cid: int, token: str) -> None:
+    p = _shell_token_path(master)
+    os.makedirs(os.path.dirname(p), exist_ok=True)
+    data = json.load(open(p)) if os.path.exists(p) else {}
+    data[str(cid)] = token
+    fd = os.open(p, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    with os.fdopen(fd, "w") as f:
+        json.dump(data, f)
+
+
+def cmd_shell_open(args: argparse.Namespace) -> None:
+    from determined_1_amd.exec.shell import open_shell
+
+    client = MasterClient(args.master)
+    p = _shell_token_path(client.master)
+    token = (json.load(open(p)) if os.path.exists(p) else {}).get(str(args.shell_id))
+    if not token:
+        sys.exit(f"no token for shell {args.shell_id}: only the CLI that started it can open it")
+    sys.exit(open_shell(client, args.shell_id, token))
+
+
+def cmd_notebook_start(args: argparse.Namespace) -> None:
+    import secrets
+
+    client = MasterClient(args.master)
+    token = secrets.token_hex(16)
+    cid = _start_task(client, "notebook", ["python3", "-m", "determined_1_amd.exec.notebook"],
+                      [f"DET_NOTEBOOK_TOKEN={token}"], args.slots, "Notebook", args.timeout)
+    c = client.get(f"/commands/{cid}")
+    if not c.get("ready"):
+        logs = "\n".join(l["message"] for l in client.get(f"/commands/{cid}/logs"))
+        sys.exit(f"notebook {cid} did not become ready (state {c.get('state')}):\n{logs}")
+    print(f"Notebook {cid}: {make_url(client.master, f'/proxy/cmd-{cid}/')}?token={token}")
+
+
+def cmd_task_list(kind: str):
     def f(args: argparse.Namespace) -> None:
-        sys.exit(f"{what} needs packages that are not installed on this image (jupyter / sshd / tensorboard); "
-                 "use `det cmd run` for arbitrary processes")
+        rows = MasterClient(args.master).get("/commands", type=kind)
+        print(_table(rows, ["id", "state", "description", "ready", "service_address"]))
 
     return f
 
@@ -618,8 +690,26 @@ def build_parser() -> argparse.ArgumentParser:
     x = tb.add_parser("kill")
     x.add_argument("command_id", type=int)
     x.set_defaults(func=cmd_command_kill)
-    for name in ("notebook", "shell"):
-        sub.add_parser(name).set_defaults(func=cmd_unavailable(name))
+    sh = sub.add_parser("shell").add_subparsers(dest="sub")
+    x = sh.add_parser("start")
+    x.add_argument("--slots", type=int, default=0)
+    x.add_argument("--detach", "-d", action="store_true")
+    x.add_argument("--timeout", type=float, default=60)
+    x.set_defaults(func=cmd_shell_start)
+    x = sh.add_parser("open")
+    x.add_argument("shell_id", type=int)
+    x.set_defaults(func=cmd_shell_open)
+    nb = sub.add_parser("notebook").add_subparsers(dest="sub")
+    x = nb.add_parser("start")
+    x.add_argument("--slots", type=int, default=1)
+    x.add_argument("--timeout", type=float, default=120)
+    x.set_defaults(func=cmd_notebook_start)
+    for grp, kind in ((sh, "shell"), (nb, "notebook")):
+        grp.add_parser("list").set_defaults(func=cmd_task_list(kind))
+        for name, fn in (("logs", cmd_command_logs), ("kill", cmd_command_kill)):
+            x = grp.add_parser(name)
+            x.add_argument("command_id", type=int)
+            x.set_defaults(func=fn)
 
     ps = sub.add_parser("preview-search")
     ps.add_argument("config_file")
