@@ -161,12 +161,14 @@ def main() -> None:
 
     from determined_1_amd import workload
     from determined_1_amd.experimental import make_controller
-    from determined_1_amd.models.imagenet_trial import ResNetImageNetTrial
+    from determined_1_amd.experimental import load_model_def
+
+    ResNetImageNetTrial = load_model_def(os.path.join(REPO, "examples", "computer_vision", "resnet50_pytorch")).ResNetImageNetTrial
     from determined_1_amd.parallel import dist as pdist
 
     gbs = args.batch_per_gpu * world
     config = {
-        "entrypoint": "determined_1_amd.models.imagenet_trial:ResNetImageNetTrial",
+        "entrypoint": "model_def:ResNetImageNetTrial",
         "hyperparameters": {
             "global_batch_size": gbs,
             "lr": 0.1 * gbs / 256,

@@ -1,5 +1,6 @@
 """Native API, local/test execution and the Python SDK (``determined.experimental`` equivalent)."""
 from determined_1_amd.experimental._local import (
+    load_model_def,
     make_controller,
     make_local_env,
     make_test_workloads,
@@ -23,6 +24,7 @@ __all__ = [
     "ExperimentReference",
     "TrialReference",
     "load_checkpoint",
+    "load_model_def",
     "make_controller",
     "make_local_env",
     "make_test_workloads",

@@ -187,3 +187,28 @@ def dump_env(env: EnvContext) -> Dict[str, str]:
 def list_of_workloads(items: List[Tuple[workload.Workload, List[Any]]]) -> Iterator:
     for w, args in items:
         yield w, args, workload.ignore_response
+
+
+def load_model_def(model_dir: str, name: str = "model_def") -> Any:
+    """Import ``<model_dir>/<name>.py`` as a uniquely named module (so several example directories,
+    each with its own ``model_def.py``, can be loaded in one process) with ``model_dir`` on
+    ``sys.path`` for its sibling imports.  Used by bench.py and the benchmark scripts to run the
+    examples' Trial classes -- the same user code an experiment's checkpoint ``code/`` holds."""
+    import hashlib
+    import importlib.util
+    import os
+    import sys
+
+    path = os.path.join(os.path.abspath(model_dir), name + ".py")
+    modname = "det_model_def_" + hashlib.sha1(path.encode()).hexdigest()[:12]
+    if modname in sys.modules:
+        return sys.modules[modname]
+    d = os.path.dirname(path)
+    if d not in sys.path:
+        sys.path.insert(0, d)
+    spec = importlib.util.spec_from_file_location(modname, path)
+    assert spec is not None and spec.loader is not None, path
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[modname] = mod
+    spec.loader.exec_module(mod)
+    return mod

@@ -213,81 +213,6 @@ class BilevelPairs(torch.utils.data.Dataset):
         return xt, yt, xv, yv
 
 
-class _GenotypeLogger(det_torch.PyTorchCallback):
-    def __init__(self, net: SearchNetwork) -> None:
-        self.net = net
-        self.last = None  # type: Optional[Dict[str, Any]]
-
-    def on_validation_end(self, metrics: Dict[str, Any]) -> None:
-        self.last = self.net.genotype()
-        logging.info(f"genotype: {self.last}")
-
-
-class GAEASearchTrial(det_torch.PyTorchTrial):
-    def __init__(self, context: det_torch.PyTorchTrialContext) -> None:
-        self.context = context
-        hp = context.get_hparams()
-        self.hp = hp
-        self.net = SearchNetwork(int(hp.get("init_channels", 16)), int(hp.get("n_classes", 10)),
-                                 int(hp.get("layers", 8)), int(hp.get("nodes", 4)), k=int(hp.get("shuffle_factor", 4)))
-        self.model = context.wrap_model(self.net)
-        self.ws_opt = context.wrap_optimizer(torch.optim.SGD(self.net.ws_parameters(), float(hp.get("learning_rate", 0.1)),
-                                                             momentum=float(hp.get("momentum", 0.9)),
-                                                             weight_decay=float(hp.get("weight_decay", 3e-4))))
-        self.arch_opt = context.wrap_optimizer(EG(self.net.arch_parameters(), float(hp.get("arch_learning_rate", 0.1))))
-        context.wrap_lr_scheduler(torch.optim.lr_scheduler.CosineAnnealingLR(
-            self.ws_opt, int(hp.get("scheduler_epochs", 50)), float(hp.get("min_learning_rate", 0.0))),
-            det_torch.LRScheduler.StepMode.STEP_EVERY_EPOCH)
-        self.genotype_cb = _GenotypeLogger(self.net)
-        self.train_data = None  # type: Optional[BilevelPairs]
-        self.last_epoch = 0
-
-    def build_callbacks(self) -> Dict[str, det_torch.PyTorchCallback]:
-        return {"genotype": self.genotype_cb}
-
-    def build_training_data_loader(self) -> det_torch.DataLoader:
-        n = int(self.hp.get("train_records", 50000))
-        self.train_data = BilevelPairs(SyntheticClassification(n, (3, 32, 32)))
-        return det_torch.DataLoader(self.train_data, batch_size=self.context.get_per_slot_batch_size(), shuffle=True,
-                                    drop_last=True)
-
-    def build_validation_data_loader(self) -> det_torch.DataLoader:
-        n = int(self.hp.get("validation_records", 10000))
-        return det_torch.DataLoader(SyntheticClassification(n, (3, 32, 32), seed=1),
-                                    batch_size=self.context.get_per_slot_batch_size())
-
-    def _trainable(self, arch: bool) -> None:
-        for p in self.net.arch_parameters():
-            p.requires_grad_(arch)
-        for p in self.net.ws_parameters():
-            p.requires_grad_(not arch)
-
-    def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
-        if epoch_idx != self.last_epoch and self.train_data is not None:
-            self.train_data.shuffle_val()
-        self.last_epoch = epoch_idx
-        x_train, y_train, x_val, y_val = batch
-        self._trainable(arch=False)
-        loss = F.cross_entropy(self.model(x_train), y_train)
-        self.context.backward(loss)
-        self.context.step_optimizer(self.ws_opt)
-        self._trainable(arch=True)
-        arch_loss = F.cross_entropy(self.model(x_val), y_val)
-        self.context.backward(arch_loss)
-        self.context.step_optimizer(self.arch_opt)
-        self._trainable(arch=False)
-        return {"loss": loss, "arch_loss": arch_loss}
-
-    def evaluate_batch(self, batch: Any) -> Dict[str, Any]:
-        x, y = batch
-        logits = self.model(x)
-        top1, top5 = topk_accuracy(logits, y)
-        return {"loss": F.cross_entropy(logits, y), "top1_accuracy": top1, "top5_accuracy": top5}
-
-
-# ------------------------------------------------------------------------------------------------
-# evaluation network (ImageNet)
-# ------------------------------------------------------------------------------------------------
 GAEA_IMAGENET_GENOTYPE = {
     "normal": [("skip_connect", 1), ("skip_connect", 0), ("sep_conv_3x3", 2), ("sep_conv_3x3", 1),
                ("sep_conv_5x5", 2), ("sep_conv_3x3", 0), ("sep_conv_5x5", 3), ("sep_conv_5x5", 2)],
@@ -451,67 +376,3 @@ def lr_multiplier(kind: str, epoch: int, warmup: int, max_epochs: int, gamma: fl
     if kind == "efficientnet":
         return gamma ** int((epoch + 1) / decay_every)
     raise ValueError(f"unknown lr_scheduler {kind!r}")
-
-
-class GAEAEvalTrial(det_torch.PyTorchTrial):
-    def __init__(self, context: det_torch.PyTorchTrialContext) -> None:
-        self.context = context
-        hp = context.get_hparams()
-        self.hp = hp
-        self.num_classes = int(hp.get("num_classes", 1000))
-        self.image_size = int(hp.get("image_size", 224))
-        genotype = hp.get("genotype") or GAEA_IMAGENET_GENOTYPE
-        net = NetworkImageNet(genotype, ACTIVATIONS[str(hp.get("activation", "swish"))], int(hp.get("init_channels", 48)),
-                              self.num_classes, int(hp.get("layers", 14)), bool(hp.get("auxiliary", False)),
-                              bool(hp.get("do_SE", True)), float(hp.get("drop_path_prob", 0.2)),
-                              float(hp.get("drop_prob", 0.2)))
-        self.ema = EMAModel(net, float(hp.get("ema_decay", 0.999)))
-        self.model = context.wrap_model(self.ema)
-        self.opt = context.wrap_optimizer(torch.optim.SGD(net.parameters(), lr=float(hp.get("learning_rate", 0.5)),
-                                                          momentum=float(hp.get("momentum", 0.9)),
-                                                          weight_decay=float(hp.get("weight_decay", 3e-5))))
-        kind = str(hp.get("lr_scheduler", "linear"))
-        warm, max_ep = int(hp.get("warmup_epochs", 5)), int(hp.get("lr_epochs", 300))
-        gamma, every = float(hp.get("lr_gamma", 0.97)), int(hp.get("lr_decay_every", 2))
-        self.sched = torch.optim.lr_scheduler.LambdaLR(
-            self.opt, lambda e: lr_multiplier(kind, e, warm, max_ep, gamma, every))
-        context.wrap_lr_scheduler(self.sched, det_torch.LRScheduler.StepMode.STEP_EVERY_EPOCH)
-        self.smooth = float(hp.get("label_smoothing_rate", 0.1))
-        self.clip = float(hp.get("clip_gradients_l2_norm", 5.0))
-
-    def _data(self, n: int, seed: int) -> SyntheticClassification:
-        return SyntheticClassification(n, (3, self.image_size, self.image_size), num_classes=self.num_classes, seed=seed)
-
-    def build_training_data_loader(self) -> det_torch.DataLoader:
-        return det_torch.DataLoader(self._data(int(self.hp.get("train_records", 1281167)), 0),
-                                    batch_size=self.context.get_per_slot_batch_size(), shuffle=True, drop_last=True)
-
-    def build_validation_data_loader(self) -> det_torch.DataLoader:
-        return det_torch.DataLoader(self._data(int(self.hp.get("validation_records", 50000)), 1),
-                                    batch_size=self.context.get_per_slot_batch_size())
-
-    def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
-        self.ema.update()
-        x, y = batch
-        logits, logits_aux = self.model(x)
-        loss = label_smoothing_ce(logits, y, self.smooth)
-        if logits_aux is not None:
-            loss = loss + float(self.hp.get("auxiliary_weight", 0.4)) * label_smoothing_ce(logits_aux, y, self.smooth)
-        self.context.backward(loss)
-        self.context.step_optimizer(self.opt, clip_grads=det_torch.ClipGradsNorm(self.clip) if self.clip > 0 else None)
-        top1, top5 = topk_accuracy(logits, y)
-        return {"loss": loss, "top1_accuracy": top1, "top5_accuracy": top5}
-
-    def evaluate_batch(self, batch: Any) -> Dict[str, Any]:
-        x, y = batch
-        logits, _ = self.model(x)
-        top1, top5 = topk_accuracy(logits, y)
-        out = {"loss": label_smoothing_ce(logits, y, self.smooth), "top1_accuracy": top1, "top5_accuracy": top5}
-        self.ema.swap()
-        try:
-            logits, _ = self.model(x)
-        finally:
-            self.ema.swap()
-        top1, top5 = topk_accuracy(logits, y)
-        out.update({"ema_loss": label_smoothing_ce(logits, y, self.smooth), "top1_ema": top1, "top5_ema": top5})
-        return out

@@ -200,10 +200,22 @@ def _autocast_keeps(x: torch.Tensor) -> bool:
     return torch.get_autocast_dtype(dev) == x.dtype
 
 
+def _observed(x: torch.Tensor) -> bool:
+    """``x``'s own gradient is observable (retain_grad / tensor hooks): the link would hand only
+    part of it to autograd, so it must not be used."""
+    return bool(x.retains_grad or getattr(x, "_backward_hooks", None))
+
+
 def linked_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)``; when ``x`` came from the fused BN-act op and feeds another consumer too, the
-    conv's input gradient is summed inside the producer's BN-backward kernels (``_LinkedConv``)."""
+    conv's input gradient is summed inside the producer's BN-backward kernels (``_LinkedConv``).
+
+    Limitation of the link: autograd sees no gradient for ``x`` from this conv (it is added inside
+    the producer's backward), so ``torch.autograd.grad(loss, x)`` taken *without* running the full
+    backward would miss this consumer's share.  ``x.retain_grad()`` and ``x.register_hook`` are
+    detected and fall back to plain ``conv(x)`` (``_observed``)."""
     if (SHORTCUT_LINK and conv.bias is None and torch.is_grad_enabled() and x.requires_grad
+            and not _observed(x)
             and isinstance(x.grad_fn, _BNActTrain._backward_cls) and x.dim() == 4
             and x.dtype == conv.weight.dtype and _autocast_keeps(x)
             and x.is_contiguous(memory_format=torch.channels_last) and conv.padding_mode == "zeros"

@@ -1164,7 +1164,9 @@ void Master::AgentGone(const std::shared_ptr<AgentConn>& conn) {
     std::lock_guard<std::mutex> g(mu_);
     cids.assign(conn->containers.begin(), conn->containers.end());
     agents_.erase(conn->id);
-    Json props = Json::object();
+  }
+  {
+    Json props = Json::object();  // telemetry file I/O outside mu_
     props["uuid"] = conn->id;
     ReportTelemetry("agent_disconnected", props);
   }

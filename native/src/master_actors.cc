@@ -160,6 +160,11 @@ ExperimentActor::ExperimentActor(Master* m, int64_t id, Json config, bool replay
   metric_ = config_["searcher"].get_string("metric", "");
   pool_ = config_["resources"].get_string("resource_pool", "");
   if (pool_.empty()) pool_ = m_->config().resource_pools.empty() ? "default" : m_->config().resource_pools[0];
+  if (replay) {
+    // a restored experiment already reported its current state before the master restarted
+    Json row;
+    if (m_->store().Get("experiments", id_, &row)) reported_state_ = row.get_string("state", "");
+  }
 }
 
 void ExperimentActor::Event(const std::string& type, Json body) {

@@ -45,7 +45,9 @@ def main() -> None:
         torch.cuda.set_device(pdist.local_cuda_device(int(os.environ.get("LOCAL_RANK", "0"))))
     from determined_1_amd import workload
     from determined_1_amd.experimental import make_controller
-    from determined_1_amd.models.albert import AlbertSQuADTrial
+    from determined_1_amd.experimental import load_model_def
+
+    AlbertSQuADTrial = load_model_def(os.path.join(REPO, "examples", "nlp", "albert_squad_pytorch")).AlbertSQuADTrial
     from determined_1_amd.ops import transformer as tfops
     from determined_1_amd.parallel import dist as pdist
 

@@ -40,7 +40,9 @@ def main() -> None:
         torch.cuda.set_device(pdist.local_cuda_device(int(os.environ.get("LOCAL_RANK", "0"))))
     from determined_1_amd import workload
     from determined_1_amd.experimental import make_controller
-    from determined_1_amd.models.bert import BertSQuADTrial
+    from determined_1_amd.experimental import load_model_def
+
+    BertSQuADTrial = load_model_def(os.path.join(REPO, "examples", "nlp", "bert_squad_pytorch")).BertSQuADTrial
     from determined_1_amd.parallel import dist as pdist
 
     gbs = args.batch_per_gpu * world

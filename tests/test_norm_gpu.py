@@ -146,6 +146,32 @@ def test_linked_projection_conv_matches_autograd_sum(gpu, dtype, monkeypatch):
         torch.testing.assert_close(d.float(), r.float(), **tol)
 
 
+def test_linked_conv_falls_back_when_input_grad_is_observed(gpu):
+    """retain_grad()/register_hook on the producer's output: the link would hide this conv's share
+    of h.grad, so linked_conv2d must run plain conv(h) and h.grad is the full autograd sum."""
+    torch.manual_seed(4)
+    bn = norm.BatchNormAct2d(64, relu=True).to(gpu)
+    conv_a = torch.nn.Conv2d(64, 32, 1, bias=False).to(gpu).to(memory_format=torch.channels_last)
+    conv_b = torch.nn.Conv2d(64, 128, 1, stride=2, bias=False).to(gpu).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 64, 14, 14, device=gpu).to(memory_format=torch.channels_last).requires_grad_(True)
+    for observe in ("retain", "hook"):
+        h = bn(x)
+        seen = []
+        if observe == "retain":
+            h.retain_grad()
+        else:
+            h.register_hook(lambda g: seen.append(g))
+        b = norm.linked_conv2d(h, conv_b)
+        assert type(b.grad_fn).__name__ != "_LinkedConvBackward"
+        a = conv_a(h)
+        ga, gb = torch.randn_like(a), torch.randn_like(b)
+        torch.autograd.backward([a, b], [ga, gb])
+        got = h.grad if observe == "retain" else seen[0]
+        hd = h.detach().requires_grad_(True)
+        want = torch.autograd.grad([conv_a(hd), conv_b(hd)], [hd], [ga, gb])[0]
+        torch.testing.assert_close(got, want, atol=1e-4, rtol=1e-4)
+
+
 def test_resnet50_fused_shortcut_link_and_pool_match_stock(gpu, monkeypatch):
     """Fused BN with identity-shortcut gradient links (dy2 summed in the BN backward) and the HIP
     stem max-pool vs stock modules; non-zero residual gammas so every branch carries gradient.

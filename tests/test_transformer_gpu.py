@@ -1,4 +1,5 @@
 """Fused transformer kernels (ops/csrc/det_transformer.hip) vs the fp32 PyTorch composite."""
+import os
 import pytest
 import torch
 import torch.nn.functional as F
@@ -240,7 +241,9 @@ def test_bert_trial_direct_gradient_landing(gpu, monkeypatch):
     after 3 steps as the copy-landing path, and the landing copy really is skipped for them."""
     import copy as _copy
 
-    from determined_1_amd.models.bert import BertSQuADTrial
+    from determined_1_amd.experimental import load_model_def
+
+    BertSQuADTrial = load_model_def(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "nlp", "bert_squad_pytorch")).BertSQuADTrial
     from determined_1_amd.ops import arena
     from tests.utils import Recorder, run
 
