@@ -83,7 +83,7 @@ class PyTorchTrialController(trial.LoopTrialController):
         PyTorchTrialController._set_random_seeds(env.trial_seed)
         # One process drives one GPU here, so autograd's per-device worker thread only adds a
         # cross-thread handoff per backward (measured +8-13% BERT-base throughput without it,
-        # scripts/gpu_s10.sh).  DET_AUTOGRAD_THREADS=1 restores the stock engine.
+        # round-1 A/B, profiles/r1_bench_bert_base_bs12.json).  DET_AUTOGRAD_THREADS=1 restores the stock engine.
         if os.environ.get("DET_AUTOGRAD_THREADS", "0") != "1":
             torch.autograd.set_multithreading_enabled(False)
 

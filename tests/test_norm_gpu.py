@@ -177,7 +177,7 @@ def test_resnet50_fused_shortcut_link_and_pool_match_stock(gpu, monkeypatch):
     stem max-pool vs stock modules; non-zero residual gammas so every branch carries gradient.
     Relative Frobenius error per parameter, judged against the run-to-run noise of the stock model
     itself (a second stock copy): MIOpen's fp32 conv algorithms are not bitwise deterministic and
-    50 layers of BN amplify that to ~1 % in the small-batch late layers (scripts/dbg_link.py)."""
+    50 layers of BN amplify that to ~1 % in the small-batch late layers (scripts/dbg/dbg_link.py)."""
     from determined_1_amd.models import resnet
     from determined_1_amd.ops.pool import MaxPool3x3s2
 
