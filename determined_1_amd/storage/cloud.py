@@ -1,10 +1,11 @@
 """Object-store checkpoint managers: S3, GCS, HDFS (reference ``storage/{s3,gcs,hdfs}.py``).
 
 Checkpoints are staged in a local temp dir and uploaded in ``post_store_path``; restore downloads
-into a temp dir.  The SDK clients (boto3, google-cloud-storage, hdfs) are not installed in this
-image: the managers take an injectable ``client`` object exposing ``upload_file(local, key)``,
-``download_dir(prefix, local_dir)`` and ``delete_prefix(prefix)``, which is what the tests use
-(mirroring the reference's monkeypatched-boto tests, ``harness/tests/storage/test_s3.py``).
+into a temp dir.  The vendor SDKs (boto3, google-cloud-storage, hdfs) are not installed in this
+image, so the default clients speak the stores' HTTP APIs directly
+(``storage/rest_clients.py``: S3 SigV4 + multipart, GCS JSON API, WebHDFS); any object exposing
+``upload_file(local, key)``, ``download_dir(prefix, local_dir)`` and ``delete_prefix(prefix)``
+can be injected instead.
 """
 import contextlib
 import os
@@ -25,28 +26,6 @@ class ObjectClient:
 
     def delete_prefix(self, prefix: str) -> None:
         raise NotImplementedError
-
-
-class _Boto3Client(ObjectClient):
-    def __init__(self, bucket: str, **kw: Any) -> None:
-        import boto3  # noqa: F401  (raises ImportError with a clear message when absent)
-
-        self.bucket = boto3.resource("s3", **{k: v for k, v in kw.items() if v is not None}).Bucket(bucket)
-
-    def upload_file(self, local: str, key: str) -> None:
-        self.bucket.upload_file(local, key)
-
-    def download_dir(self, prefix: str, local_dir: str) -> None:
-        for obj in self.bucket.objects.filter(Prefix=prefix):
-            dst = os.path.join(local_dir, os.path.relpath(obj.key, prefix))
-            if obj.key.endswith("/"):
-                os.makedirs(dst, exist_ok=True)
-                continue
-            os.makedirs(os.path.dirname(dst), exist_ok=True)
-            self.bucket.download_file(obj.key, dst)
-
-    def delete_prefix(self, prefix: str) -> None:
-        self.bucket.objects.filter(Prefix=prefix).delete()
 
 
 class _ObjectStoreManager(StorageManager):
@@ -82,8 +61,10 @@ class S3StorageManager(_ObjectStoreManager):
     @classmethod
     def from_config(cls, cfg: Dict[str, Any], client: Optional[ObjectClient] = None) -> "S3StorageManager":
         if client is None:
-            client = _Boto3Client(cfg["bucket"], aws_access_key_id=cfg.get("access_key"),
-                                  aws_secret_access_key=cfg.get("secret_key"), endpoint_url=cfg.get("endpoint_url"))
+            from determined_1_amd.storage.rest_clients import S3RestClient
+
+            client = S3RestClient(cfg["bucket"], access_key=cfg.get("access_key"), secret_key=cfg.get("secret_key"),
+                                  endpoint_url=cfg.get("endpoint_url"), region=cfg.get("region"))
         return cls(client, cfg.get("prefix", ""))
 
 
@@ -91,7 +72,9 @@ class GCSStorageManager(_ObjectStoreManager):
     @classmethod
     def from_config(cls, cfg: Dict[str, Any], client: Optional[ObjectClient] = None) -> "GCSStorageManager":
         if client is None:
-            raise ImportError("google-cloud-storage is not installed; inject an ObjectClient")
+            from determined_1_amd.storage.rest_clients import GCSRestClient
+
+            client = GCSRestClient(cfg["bucket"], endpoint_url=cfg.get("endpoint_url"), token=cfg.get("token"))
         return cls(client, cfg.get("prefix", ""))
 
 
@@ -99,7 +82,9 @@ class HDFSStorageManager(_ObjectStoreManager):
     @classmethod
     def from_config(cls, cfg: Dict[str, Any], client: Optional[ObjectClient] = None) -> "HDFSStorageManager":
         if client is None:
-            raise ImportError("hdfs is not installed; inject an ObjectClient")
+            from determined_1_amd.storage.rest_clients import WebHDFSClient
+
+            client = WebHDFSClient(cfg["hdfs_url"], user=cfg.get("user"))
         return cls(client, cfg.get("hdfs_path", ""))
 
 

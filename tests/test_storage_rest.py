@@ -1,0 +1,303 @@
+"""Object-store checkpoint storage over the stores' HTTP APIs (storage/rest_clients.py) against
+in-process fakes: an S3 endpoint that re-derives and checks every request's SigV4 signature and
+implements ListObjectsV2 pagination + multipart upload, a GCS JSON-API endpoint with bearer auth
+and page tokens, and a WebHDFS namenode/datanode pair with the CREATE redirect.  Each manager
+round-trips a checkpoint directory (store -> restore -> delete) like the reference's storage tests
+(harness/tests/storage/test_{s3,gcs,hdfs}.py, which mock the SDKs instead)."""
+import json
+import os
+import pathlib
+import re
+import threading
+import urllib.parse
+import uuid
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import pytest
+
+from determined_1_amd import storage
+from determined_1_amd.storage.base import list_directory
+from determined_1_amd.storage.rest_clients import sigv4_headers
+
+AK, SK = "AKIDEXAMPLE", "wJalrXUtnFEMI/K7MDENG+bPxRfiCYEXAMPLEKEY"
+
+
+class _Server:
+    def __init__(self, handler_cls):
+        self.objects = {}
+        self.srv = ThreadingHTTPServer(("127.0.0.1", 0), handler_cls)
+        self.srv.store = self
+        self.srv.daemon_threads = True
+        threading.Thread(target=self.srv.serve_forever, daemon=True).start()
+
+    @property
+    def url(self):
+        return f"http://127.0.0.1:{self.srv.server_address[1]}"
+
+    def close(self):
+        self.srv.shutdown()
+
+
+class _Base(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+
+    def log_message(self, *a):
+        pass
+
+    def send(self, code, body=b"", ctype="application/xml", headers=None):
+        if isinstance(body, str):
+            body = body.encode()
+        self.send_response(code)
+        self.send_header("Content-Type", ctype)
+        self.send_header("Content-Length", str(len(body)))
+        for k, v in (headers or {}).items():
+            self.send_header(k, v)
+        self.end_headers()
+        self.wfile.write(body)
+
+    def body(self):
+        n = int(self.headers.get("Content-Length", "0") or 0)
+        return self.rfile.read(n) if n else b""
+
+
+class S3Handler(_Base):
+    def _check_sig(self, payload: bytes) -> bool:
+        auth = self.headers.get("Authorization", "")
+        m = re.match(r"AWS4-HMAC-SHA256 Credential=([^/]+)/(\d{8})/([^/]+)/s3/aws4_request, SignedHeaders=([^,]+), "
+                     r"Signature=([0-9a-f]+)", auth)
+        if not m or m.group(1) != AK:
+            return False
+        import datetime
+        import hashlib
+
+        if self.headers.get("x-amz-content-sha256") != hashlib.sha256(payload).hexdigest():
+            return False
+        now = datetime.datetime.strptime(self.headers["x-amz-date"], "%Y%m%dT%H%M%SZ").replace(
+            tzinfo=datetime.timezone.utc)
+        url = f"http://{self.headers['Host']}{self.path}"
+        want = sigv4_headers(self.command, url, m.group(3), AK, SK, hashlib.sha256(payload).hexdigest(), now=now)
+        return want["Authorization"] == auth
+
+    def _key(self):
+        u = urllib.parse.urlsplit(self.path)
+        parts = urllib.parse.unquote(u.path).lstrip("/").split("/", 1)
+        return parts[0], (parts[1] if len(parts) > 1 else ""), dict(urllib.parse.parse_qsl(u.query, keep_blank_values=True))
+
+    def do_PUT(self):
+        data = self.body()
+        if not self._check_sig(data):
+            return self.send(403, "<Error><Code>SignatureDoesNotMatch</Code></Error>")
+        bucket, key, q = self._key()
+        st = self.server.store
+        if "uploadId" in q:
+            st.parts.setdefault(q["uploadId"], {})[int(q["partNumber"])] = data
+            return self.send(200, headers={"ETag": f'"p{q["partNumber"]}"'})
+        st.objects[key] = data
+        self.send(200, headers={"ETag": '"x"'})
+
+    def do_POST(self):
+        data = self.body()
+        if not self._check_sig(data):
+            return self.send(403, "<Error><Code>SignatureDoesNotMatch</Code></Error>")
+        bucket, key, q = self._key()
+        st = self.server.store
+        if "uploads" in q:
+            uid = uuid.uuid4().hex
+            st.parts[uid] = {}
+            return self.send(200, f'<InitiateMultipartUploadResult xmlns="http://s3.amazonaws.com/doc/2006-03-01/">'
+                                  f"<Bucket>{bucket}</Bucket><Key>{key}</Key><UploadId>{uid}</UploadId>"
+                                  f"</InitiateMultipartUploadResult>")
+        if "uploadId" in q:
+            parts = st.parts.pop(q["uploadId"])
+            nums = [int(x) for x in re.findall(rb"<PartNumber>(\d+)</PartNumber>", data)]
+            st.objects[key] = b"".join(parts[n] for n in nums)
+            st.multipart_completed += 1
+            return self.send(200, "<CompleteMultipartUploadResult/>")
+        self.send(400)
+
+    def do_GET(self):
+        if not self._check_sig(b""):
+            return self.send(403, "<Error><Code>SignatureDoesNotMatch</Code></Error>")
+        bucket, key, q = self._key()
+        st = self.server.store
+        if q.get("list-type") == "2":
+            keys = sorted(k for k in st.objects if k.startswith(q.get("prefix", "")))
+            start = int(q.get("continuation-token", "0"))
+            page = keys[start:start + 2]  # tiny pages exercise continuation
+            more = start + 2 < len(keys)
+            body = '<ListBucketResult xmlns="http://s3.amazonaws.com/doc/2006-03-01/">' + "".join(
+                f"<Contents><Key>{k}</Key></Contents>" for k in page) + \
+                f"<IsTruncated>{'true' if more else 'false'}</IsTruncated>" + \
+                (f"<NextContinuationToken>{start + 2}</NextContinuationToken>" if more else "") + "</ListBucketResult>"
+            return self.send(200, body)
+        if key not in st.objects:
+            return self.send(404, "<Error><Code>NoSuchKey</Code></Error>")
+        self.send(200, st.objects[key], "application/octet-stream")
+
+    def do_DELETE(self):
+        if not self._check_sig(b""):
+            return self.send(403)
+        bucket, key, q = self._key()
+        self.server.store.objects.pop(key, None)
+        self.send(204)
+
+
+class GCSHandler(_Base):
+    TOKEN = "ya29.test-token"
+
+    def _auth(self):
+        if self.headers.get("Authorization") != f"Bearer {self.TOKEN}":
+            self.send(401, json.dumps({"error": "unauthenticated"}), "application/json")
+            return False
+        return True
+
+    def do_POST(self):
+        if not self._auth():
+            return
+        u = urllib.parse.urlsplit(self.path)
+        q = dict(urllib.parse.parse_qsl(u.query))
+        if not u.path.startswith("/upload/storage/v1/b/") or q.get("uploadType") != "media":
+            return self.send(400)
+        self.server.store.objects[q["name"]] = self.body()
+        self.send(200, json.dumps({"name": q["name"]}), "application/json")
+
+    def do_GET(self):
+        if not self._auth():
+            return
+        u = urllib.parse.urlsplit(self.path)
+        q = dict(urllib.parse.parse_qsl(u.query))
+        m = re.match(r"^/storage/v1/b/([^/]+)/o(?:/(.+))?$", u.path)
+        st = self.server.store
+        if m and m.group(2) is None:
+            keys = sorted(k for k in st.objects if k.startswith(q.get("prefix", "")))
+            start = int(q.get("pageToken", "0"))
+            out = {"items": [{"name": k} for k in keys[start:start + 2]]}
+            if start + 2 < len(keys):
+                out["nextPageToken"] = str(start + 2)
+            return self.send(200, json.dumps(out), "application/json")
+        key = urllib.parse.unquote(m.group(2))
+        if key not in st.objects:
+            return self.send(404)
+        self.send(200, st.objects[key], "application/octet-stream")
+
+    def do_DELETE(self):
+        if not self._auth():
+            return
+        m = re.match(r"^/storage/v1/b/([^/]+)/o/(.+)$", urllib.parse.urlsplit(self.path).path)
+        self.server.store.objects.pop(urllib.parse.unquote(m.group(2)), None)
+        self.send(204)
+
+
+class HDFSHandler(_Base):
+    def _parse(self):
+        u = urllib.parse.urlsplit(self.path)
+        return "/" + urllib.parse.unquote(u.path)[len("/webhdfs/v1/"):], dict(urllib.parse.parse_qsl(u.query))
+
+    def do_PUT(self):
+        path, q = self._parse()
+        if q.get("op") == "CREATE" and q.get("datanode") != "1":
+            loc = f"http://{self.headers['Host']}{self.path}&datanode=1"
+            return self.send(307, headers={"Location": loc})
+        self.server.store.objects[path] = self.body()
+        self.send(201)
+
+    def do_GET(self):
+        path, q = self._parse()
+        st = self.server.store
+        if q.get("op") == "OPEN":
+            return self.send(200, st.objects[path], "application/octet-stream") if path in st.objects else self.send(404)
+        if q.get("op") == "LISTSTATUS":
+            pre = path.rstrip("/") + "/"
+            children = {}
+            for k in st.objects:
+                if k.startswith(pre):
+                    head, _, rest = k[len(pre):].partition("/")
+                    children[head] = "DIRECTORY" if rest else "FILE"
+            if not children:
+                return self.send(404, json.dumps({"RemoteException": {}}), "application/json")
+            fs = [{"pathSuffix": n, "type": t} for n, t in sorted(children.items())]
+            return self.send(200, json.dumps({"FileStatuses": {"FileStatus": fs}}), "application/json")
+        self.send(400)
+
+    def do_DELETE(self):
+        path, q = self._parse()
+        st = self.server.store
+        for k in [k for k in st.objects if k == path or k.startswith(path.rstrip("/") + "/")]:
+            del st.objects[k]
+        self.send(200, json.dumps({"boolean": True}), "application/json")
+
+
+def _ckpt(tmp_path, big=0):
+    d = tmp_path / "src"
+    (d / "code").mkdir(parents=True)
+    (d / "state_dict.pth").write_bytes(os.urandom(1000))
+    (d / "code" / "model_def.py").write_text("print('hi')\n")
+    (d / "metadata.json").write_text("{}")
+    if big:
+        (d / "big.bin").write_bytes(os.urandom(big))
+    return d
+
+
+def _roundtrip(mgr, tmp_path, big=0):
+    src = _ckpt(tmp_path, big)
+    with mgr.store_path() as (sid, path):  # on exit: post_store_path uploads
+        for f in src.rglob("*"):
+            if f.is_file():
+                dst = path / f.relative_to(src)
+                dst.parent.mkdir(parents=True, exist_ok=True)
+                dst.write_bytes(f.read_bytes())
+    md = storage.StorageMetadata(sid, list_directory(src))
+    with mgr.restore_path(md) as got:
+        for f in src.rglob("*"):
+            if f.is_file():
+                assert (pathlib.Path(got) / f.relative_to(src)).read_bytes() == f.read_bytes(), f
+    storage.validate_manager(mgr)  # the harness's write/read/delete probe
+    mgr.delete(md)
+    return sid
+
+
+@pytest.fixture()
+def s3():
+    s = _Server(S3Handler)
+    s.parts = {}
+    s.multipart_completed = 0
+    yield s
+    s.close()
+
+
+def test_s3_roundtrip_with_sigv4_and_multipart(s3, tmp_path):
+    mgr = storage.build({"type": "s3", "bucket": "ckpts", "access_key": AK, "secret_key": SK,
+                         "endpoint_url": s3.url, "prefix": "exp/1"})
+    mgr.client.multipart_threshold = 1 << 20
+    mgr.client.part_size = 256 << 10
+    _roundtrip(mgr, tmp_path, big=(1 << 20) + 12345)
+    assert s3.multipart_completed == 1
+    assert not s3.objects  # delete removed every key
+
+
+def test_s3_wrong_secret_is_rejected(s3, tmp_path):
+    mgr = storage.build({"type": "s3", "bucket": "ckpts", "access_key": AK, "secret_key": "wrong",
+                         "endpoint_url": s3.url})
+    with pytest.raises(IOError, match="403"):
+        _roundtrip(mgr, tmp_path)
+
+
+def test_gcs_roundtrip_with_bearer_token_and_paging(tmp_path):
+    s = _Server(GCSHandler)
+    try:
+        mgr = storage.build({"type": "gcs", "bucket": "b", "endpoint_url": s.url, "token": GCSHandler.TOKEN,
+                             "prefix": "p"})
+        _roundtrip(mgr, tmp_path)
+        assert not s.objects
+    finally:
+        s.close()
+
+
+def test_hdfs_roundtrip_with_datanode_redirect(tmp_path):
+    s = _Server(HDFSHandler)
+    try:
+        mgr = storage.build({"type": "hdfs", "hdfs_url": s.url, "hdfs_path": "/user/det/ckpt", "user": "det"})
+        _roundtrip(mgr, tmp_path)
+        assert not s.objects
+    finally:
+        s.close()
