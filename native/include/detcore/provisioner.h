@@ -47,6 +47,9 @@ struct ProvisionerConfig {
   int master_port = 8080;
   std::string python = "python3";
   std::string work_dir = "/tmp/det-provisioned";
+  std::string framework_root;      // cloud providers: PYTHONPATH of the provider coprocess
+  std::string cluster_id;
+  Json raw;                        // the provisioner config as given (cloud provider settings)
   static ProvisionerConfig FromJson(const Json& j);
 };
 
@@ -89,6 +92,28 @@ class LocalProvider : public Provider {
   std::string pool_;
   int next_ = 0;
   std::map<std::string, std::pair<int, Instance>> procs_;  // id -> (pid, instance)
+};
+
+// Cloud providers (aws, gcp): determined_1_amd/deploy/cloud_provider.py as a long-lived coprocess
+// speaking JSON lines over pipes (the clouds' REST APIs + request signing live there; the master
+// has no TLS stack).  Instance ids are the cloud's ids, which the started agents use as agent ids.
+class CommandProvider : public Provider {
+ public:
+  CommandProvider(ProvisionerConfig cfg, std::string pool);
+  ~CommandProvider() override;
+  std::vector<Instance> List() override;
+  void Launch(int n) override;
+  void Terminate(const std::vector<std::string>& ids) override;
+
+ private:
+  bool Call(const Json& req, Json* resp);
+  void Spawn();
+  ProvisionerConfig cfg_;
+  std::string pool_;
+  pid_t pid_ = -1;
+  int in_fd_ = -1, out_fd_ = -1;
+  std::string rbuf_;
+  std::map<std::string, Clock::time_point> launched_;
 };
 
 }  // namespace prov

@@ -1226,6 +1226,13 @@ int Master::Start() {
     pc.master_host = advertised_host_;
     pc.master_port = port_;
     pc.python = cfg_.python;
+    pc.cluster_id = cluster_id_;
+    if (pc.framework_root.empty()) {
+      char buf[4096];
+      ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+      std::string self = n > 0 ? std::string(buf, static_cast<size_t>(n)) : "det-master";
+      pc.framework_root = self.substr(0, self.rfind('/')) + "/../..";  // <root>/determined_1_amd/_native/
+    }
     if (pc.agent_binary.empty()) {
       char buf[4096];
       ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);

@@ -1019,7 +1019,10 @@ void TrialActor::SaveWorkloadEnd(const CompletedMessage& cm) {
 // =============================================================================== provisioner
 ProvisionerActor::ProvisionerActor(Master* m, std::string pool, prov::ProvisionerConfig cfg)
     : m_(m), pool_(std::move(pool)), cfg_(cfg), decider_(cfg) {
-  provider_ = std::make_unique<prov::LocalProvider>(cfg, pool_);
+  if (cfg.provider == "local")
+    provider_ = std::make_unique<prov::LocalProvider>(cfg, pool_);
+  else
+    provider_ = std::make_unique<prov::CommandProvider>(cfg, pool_);
 }
 
 void ProvisionerActor::Receive(Context& ctx) {

@@ -24,6 +24,7 @@ ProvisionerConfig ProvisionerConfig::FromJson(const Json& j) {
   c.agent_binary = j.get_string("agent_binary", "");
   c.artificial = j.get_bool("artificial_slots", true);
   c.work_dir = j.get_string("work_dir", c.work_dir);
+  c.raw = j;
   return c;
 }
 
@@ -129,6 +130,123 @@ void LocalProvider::Terminate(const std::vector<std::string>& ids) {
     waitpid(it->second.first, &st, 0);
     procs_.erase(it);
     std::fprintf(stderr, "[det-master] provisioner: terminated agent %s\n", id.c_str());
+  }
+}
+
+CommandProvider::CommandProvider(ProvisionerConfig cfg, std::string pool) : cfg_(std::move(cfg)), pool_(std::move(pool)) {
+  Spawn();
+}
+
+CommandProvider::~CommandProvider() {
+  if (in_fd_ >= 0) close(in_fd_);
+  if (out_fd_ >= 0) close(out_fd_);
+  if (pid_ > 0) {
+    ::kill(pid_, SIGTERM);
+    int st;
+    waitpid(pid_, &st, 0);
+  }
+}
+
+void CommandProvider::Spawn() {
+  int to_child[2], from_child[2];
+  if (pipe(to_child) != 0 || pipe(from_child) != 0) return;
+  Json raw = cfg_.raw;
+  raw["cluster_id"] = cfg_.cluster_id;
+  std::string conf = raw.dump();
+  std::vector<std::string> args = {cfg_.python, "-m", "determined_1_amd.deploy.cloud_provider", "--config", conf,
+                                   "--pool", pool_, "--master-host", cfg_.master_host, "--master-port",
+                                   std::to_string(cfg_.master_port)};
+  pid_t pid = fork();
+  if (pid == 0) {
+    dup2(to_child[0], 0);
+    dup2(from_child[1], 1);
+    close(to_child[1]);
+    close(from_child[0]);
+    if (!cfg_.framework_root.empty()) {
+      const char* old = getenv("PYTHONPATH");
+      std::string pp = cfg_.framework_root + (old && *old ? std::string(":") + old : "");
+      setenv("PYTHONPATH", pp.c_str(), 1);
+    }
+    std::vector<char*> argv;
+    for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
+    argv.push_back(nullptr);
+    execvp(argv[0], argv.data());
+    _exit(127);
+  }
+  close(to_child[0]);
+  close(from_child[1]);
+  pid_ = pid;
+  in_fd_ = to_child[1];
+  out_fd_ = from_child[0];
+}
+
+bool CommandProvider::Call(const Json& req, Json* resp) {
+  if (in_fd_ < 0) return false;
+  std::string line = req.dump() + "\n";
+  if (write(in_fd_, line.data(), line.size()) != static_cast<ssize_t>(line.size())) return false;
+  while (true) {
+    auto nl = rbuf_.find('\n');
+    if (nl != std::string::npos) {
+      std::string out = rbuf_.substr(0, nl);
+      rbuf_.erase(0, nl + 1);
+      try {
+        *resp = Json::parse(out);
+      } catch (const std::exception&) {
+        return false;
+      }
+      if (resp->has("error")) {
+        std::fprintf(stderr, "[det-master] provisioner (%s): %s\n", cfg_.provider.c_str(),
+                     resp->get_string("error", "").c_str());
+        return false;
+      }
+      return true;
+    }
+    char buf[4096];
+    ssize_t n = read(out_fd_, buf, sizeof(buf));
+    if (n <= 0) return false;
+    rbuf_.append(buf, static_cast<size_t>(n));
+  }
+}
+
+std::vector<Instance> CommandProvider::List() {
+  std::vector<Instance> out;
+  Json req = Json::object(), resp;
+  req["op"] = "list";
+  if (!Call(req, &resp)) return out;
+  for (auto& it : resp["instances"].as_array()) {
+    Instance inst;
+    inst.id = it.get_string("id", "");
+    inst.state = it.get_string("state", "Starting");
+    auto l = launched_.find(inst.id);
+    inst.launched = l == launched_.end() ? Clock::now() : l->second;
+    if (l == launched_.end()) launched_[inst.id] = inst.launched;
+    if (inst.state != "Stopped") out.push_back(inst);
+  }
+  return out;
+}
+
+void CommandProvider::Launch(int n) {
+  Json req = Json::object(), resp;
+  req["op"] = "launch";
+  req["n"] = n;
+  if (!Call(req, &resp)) return;
+  for (auto& id : resp["launched"].as_array()) {
+    launched_[id.as_string()] = Clock::now();
+    std::fprintf(stderr, "[det-master] provisioner (%s): launched instance %s\n", cfg_.provider.c_str(),
+                 id.as_string().c_str());
+  }
+}
+
+void CommandProvider::Terminate(const std::vector<std::string>& ids) {
+  Json req = Json::object(), resp;
+  req["op"] = "terminate";
+  Json arr = Json::array();
+  for (auto& i : ids) arr.push_back(i);
+  req["ids"] = arr;
+  if (!Call(req, &resp)) return;
+  for (auto& i : ids) {
+    launched_.erase(i);
+    std::fprintf(stderr, "[det-master] provisioner (%s): terminated instance %s\n", cfg_.provider.c_str(), i.c_str());
   }
 }
 
