@@ -11,6 +11,12 @@ them, or a dict of them).  The first caller materialises every sample once into 
 partial cache).  Later calls -- other ranks, restarts, other trials of the experiment -- memory-map
 the columns instead of re-running the (usually expensive) decode/pre-processing.
 
+Storage types (reference ``data_layer`` config): ``shared_fs`` (the cache lives under
+``container_storage_path``), and ``s3`` / ``gcs`` (reference yogadl's S3/GCS storage): the cache is
+written locally, uploaded under ``<bucket>/<bucket_directory_path>/<id>/<version>/`` with
+``meta.json`` last, and other nodes download it into ``local_cache_path`` instead of rebuilding it
+(object-store REST clients of ``storage/rest_clients.py``; no SDKs).
+
 The writer holds an exclusive lock and readers a shared one: through the master's RW coordinator
 (WS ``/ws/data-layer/*``, ``native/src/rw_coordinator.cc``) when the trial runs under a master, and
 an ``fcntl`` file lock in local mode.
@@ -43,7 +49,7 @@ from typing import Any, Callable, Dict, Iterator, List, Optional
 import numpy as np
 import torch
 
-SUPPORTED_TYPES = ("shared_fs",)
+SUPPORTED_TYPES = ("shared_fs", "s3", "gcs")
 
 
 def init_container_storage_path(configured: Optional[str]) -> pathlib.Path:
@@ -215,21 +221,45 @@ class _CacheableDecorator:
             raise RuntimeError("Dataset length not yet initialized.")
         return self._length
 
-    def _storage_root(self) -> pathlib.Path:
+    def _config(self) -> Dict[str, Any]:
         cfg = dict(self._env.experiment_config.get("data_layer", {}) or {})
         kind = cfg.get("type", "shared_fs")
         if kind not in SUPPORTED_TYPES:
-            raise ValueError(f"data_layer type {kind!r} is not supported here (object-store SDKs are absent); "
-                             f"supported: {list(SUPPORTED_TYPES)}")
-        return init_container_storage_path(cfg.get("container_storage_path"))
+            raise ValueError(f"data_layer type {kind!r} is not supported; supported: {list(SUPPORTED_TYPES)}")
+        return cfg
+
+    def _storage_root(self) -> pathlib.Path:
+        cfg = self._config()
+        if cfg.get("type", "shared_fs") == "shared_fs":
+            return init_container_storage_path(cfg.get("container_storage_path"))
+        return init_container_storage_path(cfg.get("local_cache_path"))
+
+    def _object_store(self) -> Optional[Any]:
+        """(client, remote prefix) for s3/gcs data layers, else None."""
+        cfg = self._config()
+        kind = cfg.get("type", "shared_fs")
+        if kind == "shared_fs":
+            return None
+        from determined_1_amd.storage import rest_clients
+
+        if kind == "s3":
+            client = rest_clients.S3RestClient(cfg["bucket"], access_key=cfg.get("access_key"),
+                                               secret_key=cfg.get("secret_key"), endpoint_url=cfg.get("endpoint_url"),
+                                               region=cfg.get("region"))
+        else:
+            client = rest_clients.GCSRestClient(cfg["bucket"], endpoint_url=cfg.get("endpoint_url"),
+                                                token=cfg.get("token"))
+        return client, str(cfg.get("bucket_directory_path", "")).strip("/")
 
     @contextlib.contextmanager
-    def _lock(self, path: pathlib.Path, read: bool):
+    def _lock(self, path: pathlib.Path, read: bool, key: Optional[str] = None):
+        """Master RW lock on ``key`` (the cache's shared identity) under a master, else an fcntl
+        lock next to the local cache ``path``."""
         master = getattr(self._env, "master_addr", "")
         if self._managed and master:
             from determined_1_amd.api.rw_lock import RWLock
 
-            with RWLock(f"{master}:{self._env.master_port}", str(path), read=read):
+            with RWLock(f"{master}:{self._env.master_port}", key or str(path), read=read):
                 yield
             return
         with open(str(path) + ".lock", "a+") as f:
@@ -250,19 +280,44 @@ class _CacheableDecorator:
         path = root / dataset_id / version
         path.parent.mkdir(parents=True, exist_ok=True)
 
+        store = self._object_store()
+        remote = None
+        if store is not None:
+            client, prefix = store
+            remote = "/".join(p for p in (prefix, dataset_id, version) if p)
+        lock_key = f"{self._config().get('bucket', '')}/{remote}" if remote else str(path)
+
+        def _fetch() -> bool:
+            """Download a complete remote cache into ``path`` (atomically); False if none."""
+            if remote is None or not list(client.list(remote + "/meta.json")):
+                return False
+            tmp = pathlib.Path(tempfile.mkdtemp(prefix=".tmp_", dir=str(path.parent)))
+            try:
+                client.download_dir(remote, str(tmp))
+                os.replace(tmp, path)
+            finally:
+                if tmp.exists():
+                    shutil.rmtree(tmp, ignore_errors=True)
+            logging.info(f"Downloaded cached dataset {dataset_id}:{version} from the object store.")
+            return True
+
         def _wrap(make_dataset_fn: Callable) -> Callable:
             @functools.wraps(make_dataset_fn)
             def _decorated(*args: Any, **kwargs: Any) -> Any:
-                with self._lock(path, read=True):
-                    hit = (path / "meta.json").exists()
+                with self._lock(path, read=True, key=lock_key):
+                    hit = (path / "meta.json").exists() or _fetch()
                 if not hit:
-                    with self._lock(path, read=False):
-                        if not (path / "meta.json").exists():
+                    with self._lock(path, read=False, key=lock_key):
+                        if not (path / "meta.json").exists() and not _fetch():
                             stale = remove_stale_temp_dirs(path)
                             if stale:
                                 logging.info(f"removed {stale} partial cache dir(s) of a killed writer")
                             logging.info(f"Caching dataset {dataset_id}:{version} to {path}.")
                             write_cache(make_dataset_fn(*args, **kwargs), path)
+                            if remote is not None:
+                                files = sorted(p.name for p in path.iterdir())
+                                for name in [f for f in files if f != "meta.json"] + ["meta.json"]:
+                                    client.upload_file(str(path / name), f"{remote}/{name}")
                 if self._map_style:
                     data = CachedDataset(path)
                     if shuffle:

@@ -153,3 +153,34 @@ def test_stale_writer_temp_dirs_removed(tmp_path):
     ds = ctx.cache_train_dataset("sq", "v9")(Squares)()
     assert isinstance(ds, _data_layer.CachedDataset) and len(ds) == 10
     assert not (tmp_path / "sq" / ".tmp_dead").exists()
+
+
+def test_s3_data_layer_shares_cache_across_nodes(tmp_path):
+    """data_layer type s3 (reference yogadl S3 storage): node A builds + uploads the cache (meta.json
+    last), node B with its own local_cache_path downloads it and never runs the dataset builder."""
+    from determined_1_amd.pytorch import PyTorchTrialContext
+    from tests.test_storage_rest import AK, SK, S3Handler, _Server
+
+    srv = _Server(S3Handler)
+    srv.parts, srv.multipart_completed = {}, 0
+    calls = []
+
+    def make():
+        calls.append(1)
+        return Squares()
+
+    try:
+        for node in ("a", "b"):
+            cfg = {"hyperparameters": {"global_batch_size": 4},
+                   "data_layer": {"type": "s3", "bucket": "dl", "bucket_directory_path": "cache",
+                                  "local_cache_path": str(tmp_path / node), "access_key": AK, "secret_key": SK,
+                                  "endpoint_url": srv.url}}
+            ctx = PyTorchTrialContext.from_config(cfg)
+            s = ctx.experimental.cache_train_dataset("sq", "v3")(make)()
+            assert len(s) == 10 and int(s[3]["y"]) == 9 and float(s[3]["x"][0]) == 3.0
+        assert calls == [1]  # built once, on node a
+        keys = sorted(srv.objects)
+        assert "cache/sq/v3_train/meta.json" in keys and any(k.endswith(".npy") for k in keys)
+        assert (tmp_path / "b" / "sq" / "v3_train" / "meta.json").exists()
+    finally:
+        srv.close()
