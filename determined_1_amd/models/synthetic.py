@@ -46,6 +46,46 @@ class SyntheticImages(tud.Dataset):
         return self.images.index_select(0, sel), self.labels.index_select(0, sel)
 
 
+class SyntheticImageClasses(tud.Dataset):
+    """Learnable uint8 image classification data in the layout CIFAR-10 / ImageNet decoders
+    produce (HWC uint8): a pool of ``pool`` images, each its class's fixed random template plus
+    noise, clipped to 0..255.  ``__getitems__`` returns a whole batch ``(uint8 [N,H,W,C], int64
+    [N])`` -- a zero-copy view of the pinned pool when the indices are consecutive -- so the host
+    does no per-sample work and normalisation runs on the GPU (``ops.functional.u8_normalize``).
+    Use with ``collate_fn=passthrough_collate``."""
+
+    def __init__(self, length: int, image_size: int = 32, channels: int = 3, num_classes: int = 10,
+                 pool: int = 4096, noise: float = 48.0, seed: int = 0, template_seed: int = 1234,
+                 pin: bool = True) -> None:
+        self.length = int(length)
+        self.pool = min(int(pool), self.length)
+        gt = torch.Generator().manual_seed(template_seed)
+        templates = torch.rand((num_classes, image_size, image_size, channels), generator=gt) * 255.0
+        g = torch.Generator().manual_seed(seed * 1000003 + 29)
+        labels = torch.randint(0, num_classes, (self.pool,), generator=g)
+        imgs = templates.index_select(0, labels) + noise * torch.randn((self.pool, image_size, image_size, channels),
+                                                                        generator=g)
+        imgs = imgs.clamp_(0, 255).round_().to(torch.uint8)
+        if pin and torch.cuda.is_available():
+            imgs, labels = imgs.pin_memory(), labels.pin_memory()
+        self.images, self.labels = imgs, labels
+
+    def __len__(self) -> int:
+        return self.length
+
+    def __getitem__(self, i: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        j = i % self.pool
+        return self.images[j], self.labels[j]
+
+    def __getitems__(self, idx: Sequence[int]) -> Tuple[torch.Tensor, torch.Tensor]:
+        n = len(idx)
+        j0 = idx[0] % self.pool
+        if j0 + n <= self.pool and all(idx[k] == idx[0] + k for k in range(n)):
+            return self.images[j0:j0 + n], self.labels[j0:j0 + n]
+        sel = torch.tensor([i % self.pool for i in idx], dtype=torch.int64)
+        return self.images.index_select(0, sel), self.labels.index_select(0, sel)
+
+
 def passthrough_collate(batch: Any) -> Any:
     """Collate for datasets whose ``__getitems__`` already returns a stacked batch."""
     return batch

@@ -1,6 +1,14 @@
 """CIFAR-10 CNN trial (reference examples/computer_vision/cifar10_pytorch/model_def.py:42-122):
-RMSprop, cross-entropy, epoch-based LR decay; synthetic 32x32x3 class-template data.  On MI355X
-the trial runs bf16 via ``configure_apex_amp`` when ``amp`` is set."""
+RMSprop, cross-entropy, the reference's three-conv-block network with dropout.
+
+Data: CIFAR-10 cannot be downloaded here, so a learnable synthetic stand-in in CIFAR's own storage
+layout (uint8 HWC images, class templates + noise) is used.  The reference decodes and normalises
+per sample on the host (``ToTensor`` + ``Normalize((0.5,)*3, (0.5,)*3)``); here each batch arrives
+as one uint8 tensor (no per-sample host work) and the same normalisation, (x/255 - 0.5)/0.5, runs
+on the GPU in the ``u8_normalize`` HIP kernel inside ``train_batch`` -- so with
+``optimizations.hip_graph`` it is part of the replayed graph.  On MI355X the trial runs bf16 via
+``configure_apex_amp`` when ``amp`` is set.
+"""
 from typing import Any, Dict
 
 import torch
@@ -8,7 +16,10 @@ import torch.nn as nn
 
 from determined_1_amd import pytorch
 from determined_1_amd.models import CIFAR10CNN
-from determined_1_amd.models.synthetic import SyntheticClassification
+from determined_1_amd.models.synthetic import SyntheticImageClasses, passthrough_collate
+from determined_1_amd.ops.functional import u8_normalize
+
+MEAN = STD = (127.5, 127.5, 127.5)  # ToTensor (/255) then Normalize(0.5, 0.5)
 
 
 class CIFARTrial(pytorch.PyTorchTrial):
@@ -25,17 +36,20 @@ class CIFARTrial(pytorch.PyTorchTrial):
         self.loss = nn.CrossEntropyLoss()
 
     def build_training_data_loader(self) -> pytorch.DataLoader:
-        # in-memory synthetic data: batched __getitems__ is cheaper than worker-process IPC
-        ds = SyntheticClassification(50000, (3, 32, 32), noise=3.0)
-        return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size(), shuffle=True)
+        return pytorch.DataLoader(SyntheticImageClasses(50000, 32), batch_size=self.context.get_per_slot_batch_size(),
+                                  collate_fn=passthrough_collate)
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:
-        ds = SyntheticClassification(10000, (3, 32, 32), noise=3.0, seed=1)
-        return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size())
+        return pytorch.DataLoader(SyntheticImageClasses(10000, 32, seed=1),
+                                  batch_size=self.context.get_per_slot_batch_size(), collate_fn=passthrough_collate)
+
+    def _images(self, x_u8: torch.Tensor) -> torch.Tensor:
+        dtype = next(self.model.parameters()).dtype
+        return u8_normalize(x_u8.contiguous(), MEAN, STD, out_dtype=dtype).contiguous()
 
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:
         x, y = batch
-        out = self.model(x)
+        out = self.model(self._images(x))
         loss = self.loss(out.float(), y)
         self.context.backward(loss)
         self.context.step_optimizer(self.opt)
@@ -43,6 +57,6 @@ class CIFARTrial(pytorch.PyTorchTrial):
 
     def evaluate_batch(self, batch: Any) -> Dict[str, Any]:
         x, y = batch
-        out = self.model(x).float()
+        out = self.model(self._images(x)).float()
         err = 1.0 - (out.argmax(1) == y).float().mean()
         return {"validation_loss": self.loss(out, y), "validation_error": err, "validation_accuracy": 1.0 - err}
