@@ -62,6 +62,7 @@ class PyTorchTrialController(trial.LoopTrialController):
         self.training_iterator = self._make_train_iterator()
         self._graph = None  # type: Optional[_graph.TrainStepGraph]
         self._graph_checked = False
+        self._eval_graph = None  # type: Optional[_graph.EvalStepGraph]
         # arenas / fused optimizers / bucketers, then restore, then rank-0 broadcast
         self.context._finalize()
         self._load()
@@ -316,11 +317,16 @@ class PyTorchTrialController(trial.LoopTrialController):
             batch_metrics = []
             loader = cast(torch.utils.data.DataLoader, self.validation_loader)
             check.gt(len(loader), 0)
+            if self._eval_graph is None and self._hip_graph_enabled() and self.context.device.type == "cuda":
+                self._eval_graph = _graph.EvalStepGraph(self.context, self.trial.evaluate_batch)
             for batch in loader:
                 num_inputs += data_length(batch)
                 batch = self.context.to_device(batch)
-                with self.context._autocast():
-                    vm = self.trial.evaluate_batch(batch=batch)
+                if self._eval_graph is not None:
+                    vm = self._eval_graph.run(batch)
+                else:
+                    with self.context._autocast():
+                        vm = self.trial.evaluate_batch(batch=batch)
                 check.is_instance(vm, dict, "evaluate_batch() must return a dictionary of string names to Tensor "
                                             "metrics")
                 if keys is None:

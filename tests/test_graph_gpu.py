@@ -80,6 +80,18 @@ def test_graph_replay_matches_eager(gpu, monkeypatch, hp):
     torch.testing.assert_close(torch.tensor(l_graph), torch.tensor(l_eager), rtol=1e-4, atol=1e-5)
 
 
+def test_eval_graph_matches_eager(gpu, monkeypatch):
+    results = []
+    for graph in (False, True):
+        monkeypatch.setenv("DET_HIP_GRAPH", "1" if graph else "0")
+        rec = Recorder().train(1, 4, 0).validate(1, 4)
+        ctrl, resp = run(ConvTrial, {"opt": "sgd", "global_batch_size": 16}, rec, use_gpu=True, records_per_epoch=160)
+        results.append(resp[1]["metrics"]["validation_metrics"]["validation_loss"])
+        if graph:
+            assert ctrl._eval_graph is not None and ctrl._eval_graph.replays >= 8, ctrl._eval_graph.__dict__
+    assert abs(results[0] - results[1]) <= 1e-4 * abs(results[0]) + 1e-5
+
+
 def test_graph_falls_back_for_adam(gpu, monkeypatch):
     ctrl, _, losses = _train({"opt": "adam"}, True, monkeypatch, batches=6)
     assert ctrl._graph is None and ctrl._graph_checked
