@@ -102,8 +102,15 @@ class LocalCluster:
 
     def wait_for_slots(self, n: int, timeout: float = 30.0) -> None:
         deadline = time.time() + timeout
+        headers = {}
         while time.time() < deadline:
-            agents = requests.get(f"http://{self.address}/agents", timeout=5).json()
+            r = requests.get(f"http://{self.address}/agents", timeout=5, headers=headers)
+            if r.status_code == 401:  # --require-auth: the built-in user has an empty password
+                tok = requests.post(f"http://{self.address}/login", json={"username": "determined", "password": ""},
+                                    timeout=5).json()["token"]
+                headers = {"Authorization": f"Bearer {tok}"}
+                continue
+            agents = r.json()
             if sum(len(a["slots"]) for a in agents) >= n:
                 return
             time.sleep(0.1)

@@ -55,12 +55,14 @@ class SyntheticImageClasses(tud.Dataset):
     Use with ``collate_fn=passthrough_collate``."""
 
     def __init__(self, length: int, image_size: int = 32, channels: int = 3, num_classes: int = 10,
-                 pool: int = 4096, noise: float = 48.0, seed: int = 0, template_seed: int = 1234,
+                 pool: int = 16384, noise: float = 60.0, seed: int = 0, template_seed: int = 1234,
                  pin: bool = True) -> None:
+        # template contrast 20 vs noise 60 (the 1:3 ratio of SyntheticClassification): learnable,
+        # but not separable within a few hundred batches
         self.length = int(length)
         self.pool = min(int(pool), self.length)
         gt = torch.Generator().manual_seed(template_seed)
-        templates = torch.rand((num_classes, image_size, image_size, channels), generator=gt) * 255.0
+        templates = 128.0 + 20.0 * torch.randn((num_classes, image_size, image_size, channels), generator=gt)
         g = torch.Generator().manual_seed(seed * 1000003 + 29)
         labels = torch.randint(0, num_classes, (self.pool,), generator=g)
         imgs = templates.index_select(0, labels) + noise * torch.randn((self.pool, image_size, image_size, channels),

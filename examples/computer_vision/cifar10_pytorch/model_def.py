@@ -26,8 +26,10 @@ class CIFARTrial(pytorch.PyTorchTrial):
     def __init__(self, context: pytorch.PyTorchTrialContext) -> None:
         self.context = context
         hp = context.get_hparams()
-        self.model = context.wrap_model(CIFAR10CNN(hp.get("layer1_dropout", 0.25), hp.get("layer2_dropout", 0.25),
-                                                   hp.get("layer3_dropout", 0.5)))
+        # channels_last end to end: the uint8 NHWC batch normalises straight into NHWC and MIOpen's
+        # NHWC implicit-GEMM convs run without the NCHW<->NHWC transpose kernels around every conv
+        net = CIFAR10CNN(hp.get("layer1_dropout", 0.25), hp.get("layer2_dropout", 0.25), hp.get("layer3_dropout", 0.5))
+        self.model = context.wrap_model(net.to(memory_format=torch.channels_last))
         self.opt = context.wrap_optimizer(torch.optim.RMSprop(
             self.model.parameters(), lr=hp.get("learning_rate", 1e-4), weight_decay=hp.get("learning_rate_decay", 1e-6)))
         amp = hp.get("amp")
@@ -45,7 +47,7 @@ class CIFARTrial(pytorch.PyTorchTrial):
 
     def _images(self, x_u8: torch.Tensor) -> torch.Tensor:
         dtype = next(self.model.parameters()).dtype
-        return u8_normalize(x_u8.contiguous(), MEAN, STD, out_dtype=dtype).contiguous()
+        return u8_normalize(x_u8.contiguous(), MEAN, STD, out_dtype=dtype)  # [N,C,H,W] channels_last
 
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:
         x, y = batch

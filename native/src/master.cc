@@ -412,6 +412,8 @@ void Master::InstallRoutes() {
   if (cfg_.require_auth) {
     http_.SetAuth([this](const net::Request& r) {
       if (r.path == "/login" || r.path == "/info" || r.path == "/trial_logs") return true;
+      if (r.path == "/" || r.path == "/det" || r.path.rfind("/det/", 0) == 0) return true;  // WebUI shell
+      if (r.path == "/api/v1/auth/login" || r.path == "/api/v1/master") return true;
       if (r.path.rfind("/experiments/", 0) == 0 && r.path.size() > 10 &&
           r.path.find("/model_def") != std::string::npos)
         return true;  // agents fetch model definitions
@@ -1038,6 +1040,30 @@ void Master::InstallRoutes() {
   http_.RouteWs("/ws/trial/:e/:t/:c", [this](const net::Request& r, net::WsPtr ws) { HandleTrialSocket(r, ws); });
   http_.RouteWs("/ws/data-layer/*", [this](const net::Request& r, net::WsPtr ws) { HandleRWLockSocket(r, ws); });
   InstallApiV1();
+
+  // WebUI (determined_1_amd/webui/index.html): a single-file app over /api/v1, served as-is
+  auto webui = [](const net::Request&) {
+    char buf[4096];
+    ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+    std::string self = n > 0 ? std::string(buf, static_cast<size_t>(n)) : "det-master";
+    std::ifstream f(self.substr(0, self.rfind('/')) + "/../webui/index.html", std::ios::binary);
+    if (!f) return net::Response::Text(404, "webui not installed");
+    std::stringstream ss;
+    ss << f.rdbuf();
+    net::Response r;
+    r.status = 200;
+    r.content_type = "text/html; charset=utf-8";
+    r.body = ss.str();
+    return r;
+  };
+  http_.Route("GET", "/det", webui);
+  http_.Route("GET", "/det/*", webui);
+  http_.Route("GET", "/", [](const net::Request&) {
+    net::Response r;
+    r.status = 302;
+    r.headers["Location"] = "/det/";
+    return r;
+  });
 }
 
 // One socket = one lock request; the lock is held until the socket closes (reference

@@ -190,11 +190,15 @@ static const char* StatusText(int s) {
     case 200: return "OK";
     case 201: return "Created";
     case 204: return "No Content";
+    case 302: return "Found";
+    case 403: return "Forbidden";
     case 400: return "Bad Request";
     case 401: return "Unauthorized";
     case 404: return "Not Found";
     case 405: return "Method Not Allowed";
     case 409: return "Conflict";
+    case 502: return "Bad Gateway";
+    case 504: return "Gateway Timeout";
     case 500: return "Internal Server Error";
     default: return "Status";
   }
