@@ -6,7 +6,7 @@ zero-copy views of the pinned pool, so the only per-batch host work is the DMA t
 ``DevicePrefetcher`` issues; normalisation to bf16 NCHW-channels_last happens on the GPU in one
 ``det_u8_normalize`` kernel pass.
 """
-from typing import Any, List, Sequence, Tuple
+from typing import Any, List, Optional, Sequence, Tuple
 
 import torch
 import torch.utils.data as tud
@@ -48,44 +48,52 @@ class SyntheticImages(tud.Dataset):
 
 class SyntheticImageClasses(tud.Dataset):
     """Learnable uint8 image classification data in the layout CIFAR-10 / ImageNet decoders
-    produce (HWC uint8): a pool of ``pool`` images, each its class's fixed random template plus
-    noise, clipped to 0..255.  ``__getitems__`` returns a whole batch ``(uint8 [N,H,W,C], int64
-    [N])`` -- a zero-copy view of the pinned pool when the indices are consecutive -- so the host
-    does no per-sample work and normalisation runs on the GPU (``ops.functional.u8_normalize``).
+    produce (HWC uint8).  Sample ``i`` is its class template (contrast 20 around 128) plus one of
+    1024 noise patterns (std 60: the 1:3 signal-to-noise of ``SyntheticClassification``), with the
+    label and pattern drawn from a hash of ``i`` -- every index is a distinct image, nothing is
+    materialised up front (trial start-up stays in milliseconds), and ``__getitems__`` builds a
+    whole batch ``(uint8 [N,H,W,C], int64 [N])`` with four vector ops in int16, so the host does
+    no per-sample work and normalisation runs on the GPU (``ops.functional.u8_normalize``).
     Use with ``collate_fn=passthrough_collate``."""
 
+    BANK = 1024
+
     def __init__(self, length: int, image_size: int = 32, channels: int = 3, num_classes: int = 10,
-                 pool: int = 16384, noise: float = 60.0, seed: int = 0, template_seed: int = 1234,
-                 pin: bool = True) -> None:
-        # template contrast 20 vs noise 60 (the 1:3 ratio of SyntheticClassification): learnable,
-        # but not separable within a few hundred batches
+                 noise: float = 60.0, seed: int = 0, template_seed: int = 1234) -> None:
         self.length = int(length)
-        self.pool = min(int(pool), self.length)
-        gt = torch.Generator().manual_seed(template_seed)
-        templates = 128.0 + 20.0 * torch.randn((num_classes, image_size, image_size, channels), generator=gt)
-        g = torch.Generator().manual_seed(seed * 1000003 + 29)
-        labels = torch.randint(0, num_classes, (self.pool,), generator=g)
-        imgs = templates.index_select(0, labels) + noise * torch.randn((self.pool, image_size, image_size, channels),
-                                                                        generator=g)
-        imgs = imgs.clamp_(0, 255).round_().to(torch.uint8)
-        if pin and torch.cuda.is_available():
-            imgs, labels = imgs.pin_memory(), labels.pin_memory()
-        self.images, self.labels = imgs, labels
+        self.num_classes = num_classes
+        self.seed = int(seed)
+        self.shape = (image_size, image_size, channels)
+        self.noise = noise
+        self.template_seed = template_seed
+        self._table: Optional[torch.Tensor] = None
+
+    def _build(self) -> torch.Tensor:
+        """Every (class, noise pattern) image, uint8 [num_classes * BANK, H, W, C]: built once on
+        first use (~70 ms for CIFAR's shape), then a batch is a single gather."""
+        gt = torch.Generator().manual_seed(self.template_seed)
+        templates = (128.0 + 20.0 * torch.randn((self.num_classes,) + self.shape, generator=gt)).to(torch.int16)
+        g = torch.Generator().manual_seed(self.seed * 1000003 + 29)
+        bank = (self.noise * torch.randn((self.BANK,) + self.shape, generator=g)).to(torch.int16)
+        table = (templates.view(self.num_classes, 1, -1) + bank.view(1, self.BANK, -1)).clamp_(0, 255)
+        return table.to(torch.uint8).view((self.num_classes * self.BANK,) + self.shape)
 
     def __len__(self) -> int:
         return self.length
 
+    def _keys(self, ii: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        h = (ii * 2654435761 + self.seed * 40503) & 0x7FFFFFFF  # Knuth multiplicative hash
+        return (h >> 7) % self.num_classes, h % self.BANK
+
     def __getitem__(self, i: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        j = i % self.pool
-        return self.images[j], self.labels[j]
+        x, y = self.__getitems__([i])
+        return x[0], y[0]
 
     def __getitems__(self, idx: Sequence[int]) -> Tuple[torch.Tensor, torch.Tensor]:
-        n = len(idx)
-        j0 = idx[0] % self.pool
-        if j0 + n <= self.pool and all(idx[k] == idx[0] + k for k in range(n)):
-            return self.images[j0:j0 + n], self.labels[j0:j0 + n]
-        sel = torch.tensor([i % self.pool for i in idx], dtype=torch.int64)
-        return self.images.index_select(0, sel), self.labels.index_select(0, sel)
+        if self._table is None:
+            self._table = self._build()
+        labels, pick = self._keys(torch.as_tensor(list(idx), dtype=torch.int64))
+        return self._table.index_select(0, labels * self.BANK + pick), labels
 
 
 def passthrough_collate(batch: Any) -> Any:
