@@ -190,6 +190,59 @@ def cmd_experiment_metrics(args: argparse.Namespace) -> None:
             return
 
 
+def cmd_experiment_config(args: argparse.Namespace) -> None:
+    print(yaml.safe_dump(MasterClient(args.master).experiment(args.experiment_id)["config"], sort_keys=False), end="")
+
+
+def cmd_experiment_list_trials(args: argparse.Namespace) -> None:
+    e = MasterClient(args.master).experiment(args.experiment_id)
+    rows = [{"id": t["id"], "state": t["state"], "batches": t.get("total_batches_processed", 0),
+             "best": t.get("best_validation_metric"), "hparams": json.dumps(t.get("hparams", {}))} for t in e["trials"]]
+    print(_table(rows, ["id", "state", "batches", "best", "hparams"]))
+
+
+def cmd_experiment_label(args: argparse.Namespace) -> None:
+    c = MasterClient(args.master)
+    e = c.experiment(args.experiment_id)
+    labels = list(e.get("labels") or e["config"].get("labels") or [])
+    if args.action == "add" and args.label not in labels:
+        labels.append(args.label)
+    elif args.action == "remove":
+        labels = [l for l in labels if l != args.label]
+    c.patch(f"/experiments/{args.experiment_id}", {"labels": labels})
+
+
+def cmd_experiment_set(args: argparse.Namespace) -> None:
+    """reference ``det experiment set {description,gc-policy,max-slots,weight,priority}``."""
+    c = MasterClient(args.master)
+    eid = args.experiment_id
+    if args.field == "description":
+        body = {"description": args.value}
+    elif args.field == "gc-policy":
+        keys = ("save_experiment_best", "save_trial_best", "save_trial_latest")
+        vals = dict(zip(keys, (int(v) for v in args.value.split(","))))
+        if len(vals) != 3:
+            sys.exit("gc-policy takes SAVE_EXPERIMENT_BEST,SAVE_TRIAL_BEST,SAVE_TRIAL_LATEST")
+        body = {"checkpoint_storage": vals}
+    elif args.field == "max-slots":
+        body = {"resources": {"max_slots": int(args.value)}}
+    elif args.field == "weight":
+        body = {"resources": {"weight": float(args.value)}}
+    else:
+        body = {"resources": {"priority": int(args.value)}}
+    c.patch(f"/experiments/{eid}", body)
+
+
+def cmd_experiment_download(args: argparse.Namespace) -> None:
+    """Download the experiment's top-N checkpoints (reference ``det experiment download``)."""
+    from determined_1_amd.experimental import Determined
+
+    exp = Determined(args.master).get_experiment(args.experiment_id)
+    for ck in exp.top_n_checkpoints(args.top_n):
+        path = ck.download(args.output_dir)
+        print(f"checkpoint {ck.uuid} -> {path}")
+
+
 def cmd_experiment_checkpoints(args: argparse.Namespace) -> None:
     rows = MasterClient(args.master).get(f"/experiments/{args.experiment_id}/checkpoints")
     if args.best is not None:
@@ -571,6 +624,27 @@ def build_parser() -> argparse.ArgumentParser:
     lc.add_argument("experiment_id", type=int)
     lc.add_argument("--best", type=int)
     lc.set_defaults(func=cmd_experiment_checkpoints)
+    x = e.add_parser("config")
+    x.add_argument("experiment_id", type=int)
+    x.set_defaults(func=cmd_experiment_config)
+    x = e.add_parser("list-trials", aliases=["lt"])
+    x.add_argument("experiment_id", type=int)
+    x.set_defaults(func=cmd_experiment_list_trials)
+    x = e.add_parser("label")
+    x.add_argument("action", choices=["add", "remove"])
+    x.add_argument("experiment_id", type=int)
+    x.add_argument("label")
+    x.set_defaults(func=cmd_experiment_label)
+    x = e.add_parser("set")
+    x.add_argument("field", choices=["description", "gc-policy", "max-slots", "weight", "priority"])
+    x.add_argument("experiment_id", type=int)
+    x.add_argument("value")
+    x.set_defaults(func=cmd_experiment_set)
+    x = e.add_parser("download")
+    x.add_argument("experiment_id", type=int)
+    x.add_argument("--top-n", type=int, default=1)
+    x.add_argument("--output-dir", default=None)
+    x.set_defaults(func=cmd_experiment_download)
     mt = e.add_parser("metrics", help="stream a metric's learning curves (TrialsSample)")
     mt.add_argument("experiment_id", type=int)
     mt.add_argument("--metric", required=True)

@@ -122,6 +122,9 @@ struct SetExperimentState {
   std::string state;
   bool kill = false;
 };
+struct PatchExperimentConfig {  // det experiment set gc-policy / weight / priority / max-slots
+  Json patch;
+};
 struct ReplayEvents {
   std::vector<Json> events;
 };

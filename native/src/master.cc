@@ -580,7 +580,36 @@ void Master::InstallRoutes() {
     if (body.has("archived")) patch["archived"] = body["archived"];
     if (body.has("description")) patch["description"] = body["description"];
     if (body.has("labels")) patch["labels"] = body["labels"];
+    // reference `det experiment set {weight,priority,max-slots,gc-policy}`: config changes that take
+    // effect now -- the pool's group weights/limits and an immediate checkpoint GC pass
+    Json cfg_patch = Json::object();
+    if (body["resources"].is_object()) {
+      for (const char* k : {"weight", "priority", "max_slots"})
+        if (body["resources"].has(k)) cfg_patch["resources"][k] = body["resources"][k];
+    }
+    if (body["checkpoint_storage"].is_object()) {
+      for (const char* k : {"save_experiment_best", "save_trial_best", "save_trial_latest"})
+        if (body["checkpoint_storage"].has(k)) cfg_patch["checkpoint_storage"][k] = body["checkpoint_storage"][k];
+    }
+    if (cfg_patch.size() > 0) {
+      Json cfg = DeepMerge(e["config"], cfg_patch);
+      patch["config"] = cfg;
+      if (Ref ex = ExperimentRef(id)) ex->AskSync(PatchExperimentConfig{cfg_patch});
+      if (cfg_patch.has("resources")) {
+        std::string pool = cfg["resources"].get_string("resource_pool", "");
+        Pool(pool.empty() ? cfg_.resource_pools[0] : pool)
+            ->Tell(SetGroup{std::to_string(id), cfg["resources"].get_double("weight", 1.0),
+                            cfg["resources"].has("priority") && !cfg["resources"]["priority"].is_null()
+                                ? std::optional<int>(static_cast<int>(cfg["resources"]["priority"].as_int()))
+                                : std::nullopt,
+                            static_cast<int>(cfg["resources"].get_int("max_slots", -1))});
+      }
+    }
     if (patch.size() > 0) store_->Update("experiments", id, patch);
+    if (cfg_patch.has("checkpoint_storage")) {
+      Json gc = CheckpointsToGC(*store_, id, patch["config"]);
+      if (gc.size() > 0) RunCheckpointGC(id, patch["config"], gc);
+    }
     if (body.has("state")) {
       Ref ex = ExperimentRef(id);
       if (!ex) return Err(409, "experiment is not running (state " + e.get_string("state", "") + ")");

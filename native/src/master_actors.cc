@@ -334,6 +334,9 @@ void ExperimentActor::Receive(Context& ctx) {
   } else if (auto cf = ctx.As<actor::ChildFailed>()) {
     Log("trial actor failed: " + cf->error);
     ChildGone(ctx, cf->child);
+  } else if (auto pc = ctx.As<PatchExperimentConfig>()) {
+    config_ = DeepMerge(config_, pc->patch);
+    ctx.Respond(true);
   } else if (auto st = ctx.As<SetExperimentState>()) {
     const std::string& want = st->state;
     std::string err;

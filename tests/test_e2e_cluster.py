@@ -398,3 +398,43 @@ def test_telemetry_events_written(cluster):
     created = [e for e in events if e["event"] == "experiment_created" and e["properties"]["id"] == exp_id]
     assert created and created[0]["properties"]["searcher"]["name"] == "single"
     assert all(e["cluster_id"] for e in events)
+
+
+def test_experiment_set_label_config_and_gc_policy(cluster, tmp_path):
+    """reference `det experiment {set,label,config,list-trials,download}` (cli/determined_cli/experiment.py)."""
+    cl, eid = submit(cluster, noop_config({"name": "single", "max_length": {"batches": 20}},
+                                          min_validation_period={"batches": 5}, checkpoint_policy="all",
+                                          checkpoint_storage={"save_trial_latest": 10, "save_trial_best": 10,
+                                                              "save_experiment_best": 10}))
+    assert cl.wait_for_experiment(eid, timeout=120) == "COMPLETED"
+
+    def det(*argv):
+        r = subprocess.run([sys.executable, "-m", "determined_1_amd.cli", "-m", cluster.address, *argv],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        return r.stdout
+
+    t = cl.get(f"/trials/{cl.experiment(eid)['trials'][0]['id']}")
+    assert sum(c["state"] == "COMPLETED" for c in t["checkpoints"]) == 4
+    det("experiment", "set", "gc-policy", str(eid), "0,1,0")  # keep only the trial's best
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        t = cl.get(f"/trials/{t['id']}")
+        if sum(c["state"] == "COMPLETED" for c in t["checkpoints"]) == 1:
+            break
+        time.sleep(0.2)
+    assert sum(c["state"] == "COMPLETED" for c in t["checkpoints"]) == 1
+    det("experiment", "set", "weight", str(eid), "2.5")
+    det("experiment", "set", "priority", str(eid), "7")
+    det("experiment", "set", "description", str(eid), "renamed")
+    det("experiment", "label", "add", str(eid), "blue")
+    e = cl.experiment(eid)
+    assert e["config"]["resources"]["weight"] == 2.5 and e["config"]["resources"]["priority"] == 7
+    assert e["config"]["checkpoint_storage"]["save_trial_best"] == 1 and e["description"] == "renamed"
+    assert "blue" in e["labels"]
+    det("experiment", "label", "remove", str(eid), "blue")
+    assert "blue" not in cl.experiment(eid)["labels"]
+    assert "save_trial_best: 1" in det("experiment", "config", str(eid))
+    assert str(t["id"]) in det("experiment", "list-trials", str(eid))
+    out = det("experiment", "download", str(eid), "--output-dir", str(tmp_path))
+    assert "checkpoint" in out and any(tmp_path.iterdir())
