@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/s23
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/s23/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/s23/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/s23/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/s23/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/s23/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s23/smoke.log 2>&1 || { tail -30 gpurun_out/s23/smoke.log; exit 1; }
 tail -1 gpurun_out/s23/smoke.log
