@@ -566,6 +566,12 @@ def cmd_master_config(args: argparse.Namespace) -> None:
     print(json.dumps(MasterClient(args.master).get("/master/config"), indent=2))
 
 
+def _cloud_deploy(cloud: str, rest: List[str]) -> int:
+    from determined_1_amd.deploy import cloud_deploy
+
+    return cloud_deploy.main([cloud] + rest)
+
+
 def cmd_deploy_local(args: argparse.Namespace) -> None:
     from determined_1_amd.deploy import LocalCluster
 
@@ -803,6 +809,11 @@ def build_parser() -> argparse.ArgumentParser:
     lo.add_argument("--checkpoint-dir")
     lo.add_argument("--scheduler", default="fair_share")
     lo.set_defaults(func=cmd_deploy_local)
+    for cloud in ("aws", "gcp"):
+        x = dp.add_parser(cloud, help=f"master VM on {cloud.upper()} with the {cloud} agent provisioner",
+                          add_help=False)
+        x.add_argument("rest", nargs=argparse.REMAINDER)
+        x.set_defaults(func=lambda a, cloud=cloud: sys.exit(_cloud_deploy(cloud, a.rest)))
     return p
 
 

@@ -227,3 +227,50 @@ def test_gcp_provider_against_fake_compute(tmp_path):
         assert [i["id"] for i in prov.list()] == [names[1]]
     finally:
         srv.shutdown()
+
+
+def test_det_deploy_aws_up_runs_experiment_and_down(tmp_path):
+    """`det deploy aws up`: the master VM's user-data starts det-master with the AWS provisioner;
+    the master then provisions its own agent VM for a pending trial; `down` terminates both."""
+    from determined_1_amd.deploy.local import free_port
+
+    ec2 = FakeEC2(str(tmp_path))
+    port = free_port()
+    prov_cfg = {"endpoint_url": ec2.url, "region": "us-west-2", "access_key": AK, "secret_key": SK,
+                "image_id": "ami-mi355x", "agent_command": native_binary("det-agent"),
+                "agent_args": ["--artificial-slots", "1", "--python", sys.executable, "--work-dir",
+                               str(tmp_path / "agentwork"), "--framework-root", REPO]}
+    base = [sys.executable, "-m", "determined_1_amd.cli", "deploy", "aws"]
+    common = ["--cluster-id", "c1", "--provider-config", json.dumps(prov_cfg)]
+    try:
+        r = subprocess.run(base + ["up"] + common + [
+            "--master-command", f"{native_binary('det-master')} --host 127.0.0.1 --python {sys.executable}",
+            "--master-port", str(port), "--store-dir", str(tmp_path / "store"), "--slots-per-agent", "1",
+            "--max-agents", "1", "--max-idle-agent-period-ms", "1500",
+            "--checkpoint-storage", json.dumps({"type": "shared_fs", "host_path": str(tmp_path / "ckpt")})],
+            capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        masters = json.loads(r.stdout)["master_instances"]
+        assert len(masters) == 1 and ec2.instances[masters[0]]["tags"]["determined-cluster"] == "c1"
+        cl = MasterClient(f"127.0.0.1:{port}")
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            try:
+                cl.get("/info")
+                break
+            except Exception:
+                time.sleep(0.2)
+        eid = cl.create_experiment({"description": "deploy", "entrypoint": "model_def:NoOpTrial",
+                                    "hyperparameters": {"global_batch_size": 4, "metrics_base": 0.9},
+                                    "searcher": {"name": "single", "metric": "validation_error",
+                                                 "max_length": {"batches": 5}}, "scheduling_unit": 5},
+                                   read_context(NOOP))["id"]
+        assert cl.wait_for_experiment(eid, timeout=180) == "COMPLETED"
+        agents = [i for i, d in ec2.instances.items() if d["tags"].get("determined-resource-pool") == "c1-default"]
+        assert len(agents) == 1
+        r = subprocess.run(base + ["down"] + common, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        assert set(json.loads(r.stdout)["terminated"]) >= set(masters)
+        assert all(d["state"] == "terminated" for d in ec2.instances.values())
+    finally:
+        ec2.close()
