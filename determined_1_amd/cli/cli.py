@@ -276,6 +276,26 @@ def cmd_trial_logs(args: argparse.Namespace) -> None:
         print(l["message"], flush=True)
 
 
+def cmd_trial_download(args: argparse.Namespace) -> None:
+    """reference ``det trial download``: the trial's best (default), latest or given checkpoint."""
+    from determined_1_amd.experimental import Determined
+
+    t = Determined(args.master).get_trial(args.trial_id)
+    ck = t.select_checkpoint(latest=args.latest, best=not args.latest and not args.uuid, uuid=args.uuid)
+    print(f"checkpoint {ck.uuid} -> {ck.download(args.output_dir)}")
+
+
+def cmd_master_logs(args: argparse.Namespace) -> None:
+    """Streams ``GET /api/v1/master/logs``; ``--tail N`` starts N lines before the end."""
+    c = MasterClient(args.master)
+    offset = 0
+    if args.tail:
+        ids = [l["logEntry"]["id"] for l in c.stream("/api/v1/master/logs", limit=100000)]
+        offset = ids[-args.tail] - 1 if len(ids) >= args.tail else 0
+    for l in c.stream("/api/v1/master/logs", offset=offset, follow=args.follow):
+        print(l["logEntry"]["message"], flush=True)
+
+
 def cmd_trial_kill(args: argparse.Namespace) -> None:
     MasterClient(args.master).post(f"/trials/{args.trial_id}/kill")
 
@@ -676,6 +696,14 @@ def build_parser() -> argparse.ArgumentParser:
     k = t.add_parser("kill")
     k.add_argument("trial_id", type=int)
     k.set_defaults(func=cmd_trial_kill)
+    x = t.add_parser("download")
+    x.add_argument("trial_id", type=int)
+    g = x.add_mutually_exclusive_group()
+    g.add_argument("--best", action="store_true", default=True)
+    g.add_argument("--latest", action="store_true")
+    g.add_argument("--uuid")
+    x.add_argument("--output-dir", default=None)
+    x.set_defaults(func=cmd_trial_download)
 
     ck = sub.add_parser("checkpoint", aliases=["c"]).add_subparsers(dest="sub")
     d = ck.add_parser("describe")
@@ -798,6 +826,10 @@ def build_parser() -> argparse.ArgumentParser:
     sub.add_parser("version").set_defaults(func=cmd_version)
     mc = sub.add_parser("master").add_subparsers(dest="sub")
     mc.add_parser("config").set_defaults(func=cmd_master_config)
+    x = mc.add_parser("logs")
+    x.add_argument("--follow", "-f", action="store_true")
+    x.add_argument("--tail", type=int, default=0)
+    x.set_defaults(func=cmd_master_logs)
 
     dp = sub.add_parser("deploy").add_subparsers(dest="sub")
     lo = dp.add_parser("local")

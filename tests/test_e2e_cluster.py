@@ -438,3 +438,7 @@ def test_experiment_set_label_config_and_gc_policy(cluster, tmp_path):
     assert str(t["id"]) in det("experiment", "list-trials", str(eid))
     out = det("experiment", "download", str(eid), "--output-dir", str(tmp_path))
     assert "checkpoint" in out and any(tmp_path.iterdir())
+    out = det("trial", "download", str(t["id"]), "--latest", "--output-dir", str(tmp_path / "t"))
+    assert "checkpoint" in out and any((tmp_path / "t").iterdir())
+    logs = det("master", "logs", "--tail", "3").strip().splitlines()
+    assert len(logs) == 3
