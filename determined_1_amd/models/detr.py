@@ -1,0 +1,294 @@
+"""DETR (Carion et al. 2020): ResNet-50 backbone with frozen BatchNorm, sine position encoding,
+post-norm transformer encoder/decoder, 100 object queries, class + 3-layer box heads, aux decoder
+outputs.  Reference: ``examples/computer_vision/detr_coco_pytorch/model.py:236-282``
+(``build_model``: num_classes 91 for COCO, weight dict incl. aux copies, losses labels / boxes /
+cardinality) and ``const_fake.yaml`` (hidden 256, 8 heads, 6+6 layers, FFN 2048, dropout 0.1).
+
+Written for MI355X rather than transcribed:
+  * **frozen BN folded into the convolutions.**  DETR's backbone BatchNorm is frozen (fixed
+    statistics and affine), so ``bn(conv(x, W)) == conv(x, W * s) + b`` with ``s, b`` per output
+    channel.  Each backbone conv therefore runs as ONE MIOpen convolution with the scale folded
+    into the (tiny) weight tensor and the shift as the conv bias -- no separate full-activation
+    normalisation pass over HBM, which for a 53-conv backbone is ~50 activation read+write passes
+    per step saved.  Gradients still reach the trainable ``W`` (layers 2-4) through the fold.
+  * activations stay ``channels_last`` through the backbone (MIOpen's NHWC bf16 kernels, no
+    layout transposes); the transformer consumes the flattened ``[B, HW, D]`` sequence directly;
+  * attention goes through ``F.scaled_dot_product_attention`` (fused flash-style kernel on
+    ROCm) with the key-padding mask as a boolean mask, q/k/v projected by one packed GEMM where
+    q and k share an input (self-attention);
+  * class and box heads run once over the stacked decoder outputs ``[L, B, Q, D]`` (one GEMM
+    each for all 6 layers).
+"""
+import math
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from determined_1_amd.models.detection import HungarianMatcher, SetCriterion
+
+
+# ------------------------------------------------------------------------------------------------
+# backbone
+# ------------------------------------------------------------------------------------------------
+class FrozenBNConv2d(nn.Module):
+    """``FrozenBatchNorm(conv(x))`` evaluated as one conv with the BN folded into weight/bias."""
+
+    def __init__(self, cin: int, cout: int, k: int, stride: int = 1, padding: int = 0, eps: float = 1e-5) -> None:
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        nn.init.kaiming_normal_(self.weight, mode="fan_out", nonlinearity="relu")
+        self.stride, self.padding, self.eps = stride, padding, eps
+        # frozen BatchNorm state (DETR's FrozenBatchNorm2d buffers)
+        self.register_buffer("bn_weight", torch.ones(cout))
+        self.register_buffer("bn_bias", torch.zeros(cout))
+        self.register_buffer("running_mean", torch.zeros(cout))
+        self.register_buffer("running_var", torch.ones(cout))
+
+    def folded(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        scale = self.bn_weight * (self.running_var + self.eps).rsqrt()
+        shift = self.bn_bias - self.running_mean * scale
+        return scale, shift
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        scale, shift = self.folded()
+        w = self.weight * scale.to(self.weight.dtype).view(-1, 1, 1, 1)
+        return F.conv2d(x, w, shift.to(x.dtype), self.stride, self.padding)
+
+
+class FrozenBottleneck(nn.Module):
+    def __init__(self, cin: int, planes: int, stride: int = 1) -> None:
+        super().__init__()
+        out = planes * 4
+        self.conv1 = FrozenBNConv2d(cin, planes, 1)
+        self.conv2 = FrozenBNConv2d(planes, planes, 3, stride, 1)
+        self.conv3 = FrozenBNConv2d(planes, out, 1)
+        self.downsample = FrozenBNConv2d(cin, out, 1, stride) if (stride != 1 or cin != out) else None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        idt = x if self.downsample is None else self.downsample(x)
+        y = F.relu(self.conv1(x), inplace=True)
+        y = F.relu(self.conv2(y), inplace=True)
+        return F.relu(self.conv3(y) + idt, inplace=True)
+
+
+class FrozenBNResNet(nn.Module):
+    """ResNet trunk (stride-32 feature map, no pooling / fc) with frozen, folded BatchNorm.  As in
+    DETR, only ``layer2``-``layer4`` train (when ``lr_backbone > 0``)."""
+
+    def __init__(self, layers: Tuple[int, ...] = (3, 4, 6, 3), train_backbone: bool = True) -> None:
+        super().__init__()
+        self.stem = FrozenBNConv2d(3, 64, 7, 2, 3)
+        cin = 64
+        stages = []
+        for i, (planes, n) in enumerate(zip((64, 128, 256, 512), layers)):
+            blocks = []
+            for b in range(n):
+                blocks.append(FrozenBottleneck(cin, planes, 2 if (b == 0 and i > 0) else 1))
+                cin = planes * 4
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.num_channels = cin
+        for name, p in self.named_parameters():
+            if not train_backbone or not any(s in name for s in ("layer2", "layer3", "layer4")):
+                p.requires_grad_(False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = F.max_pool2d(F.relu(self.stem(x), inplace=True), 3, 2, 1)
+        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+
+
+BACKBONE_LAYERS = {"resnet50": (3, 4, 6, 3), "resnet101": (3, 4, 23, 3), "resnet26": (2, 2, 2, 2)}
+
+
+def sine_position_encoding(mask: torch.Tensor, num_pos_feats: int, temperature: float = 10000.0) -> torch.Tensor:
+    """DETR's normalised 2-D sine embedding from the padding mask (True = padding): ``[B, 2F, H, W]``."""
+    not_mask = (~mask).to(torch.float32)
+    y = not_mask.cumsum(1)
+    x = not_mask.cumsum(2)
+    eps, scale = 1e-6, 2 * math.pi
+    y = y / (y[:, -1:, :] + eps) * scale
+    x = x / (x[:, :, -1:] + eps) * scale
+    dim_t = torch.arange(num_pos_feats, dtype=torch.float32, device=mask.device)
+    dim_t = temperature ** (2 * torch.div(dim_t, 2, rounding_mode="floor") / num_pos_feats)
+    px = x[..., None] / dim_t
+    py = y[..., None] / dim_t
+    px = torch.stack((px[..., 0::2].sin(), px[..., 1::2].cos()), dim=4).flatten(3)
+    py = torch.stack((py[..., 0::2].sin(), py[..., 1::2].cos()), dim=4).flatten(3)
+    return torch.cat((py, px), dim=3).permute(0, 3, 1, 2)
+
+
+# ------------------------------------------------------------------------------------------------
+# transformer
+# ------------------------------------------------------------------------------------------------
+class Attention(nn.Module):
+    """Multi-head attention on ``[B, L, D]`` tensors (batch-first) with a key-padding mask."""
+
+    def __init__(self, d: int, heads: int, dropout: float) -> None:
+        super().__init__()
+        self.d, self.h, self.p = d, heads, dropout
+        self.in_proj = nn.Linear(d, 3 * d)
+        self.out_proj = nn.Linear(d, d)
+        nn.init.xavier_uniform_(self.in_proj.weight)
+        nn.init.zeros_(self.in_proj.bias)
+        nn.init.zeros_(self.out_proj.bias)
+
+    def forward(self, q_in: torch.Tensor, k_in: torch.Tensor, v_in: torch.Tensor,
+                key_padding_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        b, lq, d = q_in.shape
+        w, bias = self.in_proj.weight, self.in_proj.bias
+        if q_in is k_in:  # self-attention: q and k from one packed GEMM
+            qk = F.linear(q_in, w[:2 * d], bias[:2 * d])
+            q, k = qk.split(d, -1)
+        else:
+            q = F.linear(q_in, w[:d], bias[:d])
+            k = F.linear(k_in, w[d:2 * d], bias[d:2 * d])
+        v = F.linear(v_in, w[2 * d:], bias[2 * d:])
+        hd = d // self.h
+
+        def heads(t: torch.Tensor) -> torch.Tensor:
+            return t.view(b, -1, self.h, hd).transpose(1, 2)
+
+        mask = None
+        if key_padding_mask is not None:
+            mask = (~key_padding_mask)[:, None, None, :]  # True = attend
+        o = F.scaled_dot_product_attention(heads(q), heads(k), heads(v), attn_mask=mask,
+                                           dropout_p=self.p if self.training else 0.0)
+        return self.out_proj(o.transpose(1, 2).reshape(b, lq, d))
+
+
+class EncoderLayer(nn.Module):
+    def __init__(self, d: int, heads: int, ffn: int, dropout: float) -> None:
+        super().__init__()
+        self.attn = Attention(d, heads, dropout)
+        self.lin1, self.lin2 = nn.Linear(d, ffn), nn.Linear(ffn, d)
+        self.norm1, self.norm2 = nn.LayerNorm(d), nn.LayerNorm(d)
+        self.drop = nn.Dropout(dropout)
+
+    def forward(self, src: torch.Tensor, pos: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        qk = src + pos
+        src = self.norm1(src + self.drop(self.attn(qk, qk, src, mask)))
+        return self.norm2(src + self.drop(self.lin2(self.drop(F.relu(self.lin1(src))))))
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, d: int, heads: int, ffn: int, dropout: float) -> None:
+        super().__init__()
+        self.self_attn = Attention(d, heads, dropout)
+        self.cross_attn = Attention(d, heads, dropout)
+        self.lin1, self.lin2 = nn.Linear(d, ffn), nn.Linear(ffn, d)
+        self.norm1, self.norm2, self.norm3 = nn.LayerNorm(d), nn.LayerNorm(d), nn.LayerNorm(d)
+        self.drop = nn.Dropout(dropout)
+
+    def forward(self, tgt: torch.Tensor, memory: torch.Tensor, mask: torch.Tensor, query_pos: torch.Tensor,
+                mem_k: torch.Tensor) -> torch.Tensor:
+        qk = tgt + query_pos
+        tgt = self.norm1(tgt + self.drop(self.self_attn(qk, qk, tgt)))
+        tgt = self.norm2(tgt + self.drop(self.cross_attn(tgt + query_pos, mem_k, memory, mask)))
+        return self.norm3(tgt + self.drop(self.lin2(self.drop(F.relu(self.lin1(tgt))))))
+
+
+class Transformer(nn.Module):
+    def __init__(self, d: int = 256, heads: int = 8, enc_layers: int = 6, dec_layers: int = 6, ffn: int = 2048,
+                 dropout: float = 0.1, pre_norm: bool = False) -> None:
+        super().__init__()
+        if pre_norm:
+            raise ValueError("pre_norm: true is not supported (the reference configs use post-norm)")
+        self.encoder = nn.ModuleList([EncoderLayer(d, heads, ffn, dropout) for _ in range(enc_layers)])
+        self.decoder = nn.ModuleList([DecoderLayer(d, heads, ffn, dropout) for _ in range(dec_layers)])
+        self.dec_norm = nn.LayerNorm(d)
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+
+    def forward(self, src: torch.Tensor, mask: torch.Tensor, query_embed: torch.Tensor, pos: torch.Tensor
+                ) -> torch.Tensor:
+        """``src/pos [B, HW, D]``, ``mask [B, HW]``, ``query_embed [Q, D]`` -> ``[L, B, Q, D]``."""
+        memory = src
+        for layer in self.encoder:
+            memory = layer(memory, pos, mask)
+        b = src.shape[0]
+        query_pos = query_embed.unsqueeze(0).expand(b, -1, -1)
+        tgt = torch.zeros_like(query_pos)
+        mem_k = memory + pos  # shared by every decoder layer's cross-attention keys
+        outs = []
+        for layer in self.decoder:
+            tgt = layer(tgt, memory, mask, query_pos, mem_k)
+            outs.append(tgt)
+        return self.dec_norm(torch.stack(outs))
+
+
+class MLP(nn.Module):
+    def __init__(self, din: int, hidden: int, dout: int, n: int) -> None:
+        super().__init__()
+        dims = [din] + [hidden] * (n - 1)
+        self.layers = nn.ModuleList(nn.Linear(i, o) for i, o in zip(dims, dims[1:] + [dout]))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        for i, lin in enumerate(self.layers):
+            x = lin(x) if i == len(self.layers) - 1 else F.relu(lin(x))
+        return x
+
+
+class DETR(nn.Module):
+    def __init__(self, num_classes: int = 91, num_queries: int = 100, hidden_dim: int = 256, nheads: int = 8,
+                 enc_layers: int = 6, dec_layers: int = 6, dim_feedforward: int = 2048, dropout: float = 0.1,
+                 aux_loss: bool = True, backbone: str = "resnet50", train_backbone: bool = True,
+                 pre_norm: bool = False, channels_last: bool = True) -> None:
+        super().__init__()
+        self.backbone = FrozenBNResNet(BACKBONE_LAYERS[backbone], train_backbone)
+        self.input_proj = nn.Conv2d(self.backbone.num_channels, hidden_dim, 1)
+        self.transformer = Transformer(hidden_dim, nheads, enc_layers, dec_layers, dim_feedforward, dropout, pre_norm)
+        self.query_embed = nn.Embedding(num_queries, hidden_dim)
+        self.class_embed = nn.Linear(hidden_dim, num_classes + 1)
+        self.bbox_embed = MLP(hidden_dim, hidden_dim, 4, 3)
+        self.aux_loss = aux_loss
+        self.hidden_dim = hidden_dim
+        self.channels_last = channels_last
+
+    def forward(self, samples: Dict[str, torch.Tensor]) -> Dict[str, Any]:
+        x, mask = samples["tensors"], samples["mask"]
+        p = next(self.parameters())
+        x = x.to(p.dtype)
+        if self.channels_last and x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
+        feat = self.backbone(x)
+        m = F.interpolate(mask[None].float(), size=feat.shape[-2:]).to(torch.bool)[0]
+        pos = sine_position_encoding(m, self.hidden_dim // 2).to(feat.dtype)
+        src = self.input_proj(feat)
+        b, d = src.shape[:2]
+        src = src.flatten(2).transpose(1, 2)  # [B, HW, D]
+        pos = pos.flatten(2).transpose(1, 2)
+        hs = self.transformer(src, m.flatten(1), self.query_embed.weight, pos)  # [L, B, Q, D]
+        logits = self.class_embed(hs)
+        boxes = self.bbox_embed(hs).sigmoid()
+        out: Dict[str, Any] = {"pred_logits": logits[-1], "pred_boxes": boxes[-1]}
+        if self.aux_loss:
+            out["aux_outputs"] = [{"pred_logits": a, "pred_boxes": bb} for a, bb in zip(logits[:-1], boxes[:-1])]
+        return out
+
+
+def build(hp: Dict[str, Any], num_classes: Optional[int] = None) -> Tuple[DETR, SetCriterion]:
+    """Model + criterion from the reference hyperparameter names (``const_fake.yaml``)."""
+    nc = num_classes if num_classes is not None else (91 if hp.get("dataset_file", "coco") == "coco" else 20)
+    if hp.get("masks"):
+        raise ValueError("masks: true (panoptic segmentation head) is not supported")
+    if hp.get("dilation"):
+        raise ValueError("dilation: true (DC5 backbone) is not supported")
+    model = DETR(num_classes=nc, num_queries=int(hp.get("num_queries", 100)), hidden_dim=int(hp.get("hidden_dim", 256)),
+                 nheads=int(hp.get("nheads", 8)), enc_layers=int(hp.get("enc_layers", 6)),
+                 dec_layers=int(hp.get("dec_layers", 6)), dim_feedforward=int(hp.get("dim_feedforward", 2048)),
+                 dropout=float(hp.get("dropout", 0.1)), aux_loss=bool(hp.get("aux_loss", True)),
+                 backbone=hp.get("backbone", "resnet50"), train_backbone=float(hp.get("lr_backbone", 1e-5)) > 0,
+                 pre_norm=bool(hp.get("pre_norm", False)))
+    matcher = HungarianMatcher(float(hp.get("set_cost_class", 1)), float(hp.get("set_cost_bbox", 5)),
+                               float(hp.get("set_cost_giou", 2)))
+    weight_dict = {"loss_ce": 1.0, "loss_bbox": float(hp.get("bbox_loss_coef", 5)),
+                   "loss_giou": float(hp.get("giou_loss_coef", 2))}
+    if model.aux_loss:
+        base = dict(weight_dict)
+        for i in range(int(hp.get("dec_layers", 6)) - 1):
+            weight_dict.update({f"{k}_{i}": v for k, v in base.items()})
+    criterion = SetCriterion(nc, matcher, weight_dict, float(hp.get("eos_coef", 0.1)))
+    return model, criterion

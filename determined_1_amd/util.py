@@ -2,6 +2,7 @@
 (reference ``harness/determined/util.py:29-166``)."""
 import datetime
 import enum
+import inspect
 import json
 import math
 import os
@@ -16,10 +17,14 @@ from determined_1_amd import check, workload
 
 
 def is_overridden(full_method: Any, parent_class: Any) -> bool:
-    """True if ``full_method`` (bound) is not the implementation defined on ``parent_class``."""
-    name = getattr(full_method, "__name__", None)
-    if name is None:
-        return True
+    """True if ``full_method`` (bound) is not the implementation defined on ``parent_class``.
+
+    A user attribute shadowing the method name (e.g. ``self.optimizer = AdamW(...)`` in a trial,
+    as the reference DETR example does) counts as *not* overridden, as in the reference
+    (``harness/determined/util.py:29-37``)."""
+    if not (inspect.ismethod(full_method) or inspect.isfunction(full_method)):
+        return False
+    name = full_method.__name__
     base = getattr(parent_class, name, None)
     impl = getattr(full_method, "__func__", full_method)
     return impl is not base
