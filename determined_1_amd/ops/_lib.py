@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -115,6 +115,17 @@ _SIGNATURES = {
         + [c_float, c_float, c_int, c_int] + [c_void_p] * 6,
         c_int,
     ),
+    # det_detect.hip: multi-level RoIAlign (NHWC) and device NMS
+    # stream, dtype, rois, level, K, n_levels, feats**, hs*, ws*, scales*, C, PH, PW, sampling, out
+    "det_roi_align_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4
+                          + [c_void_p], c_int),
+    # stream, dtype, rois, level, K, n_levels, grads**, hs*, ws*, scales*, C, PH, PW, sampling, dy
+    "det_roi_align_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4
+                          + [c_void_p], c_int),
+    "det_nms_mask_words": ([c_int], c_int),
+    "det_nms_max_boxes": ([], c_int),
+    # stream, boxes, n, thr, mask, keep
+    "det_nms": ([c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p], c_int),
     # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
     "det_conv_nt_rows_per_block": ([c_int], c_int),
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
