@@ -21,12 +21,23 @@ FUSED_BN = True
 # Stride-1 1x1 convs as hand-written MFMA GEMMs with the BN statistics in the forward epilogue
 # (ops/csrc/det_conv.hip); hparam ``native_conv1x1: false`` keeps them on MIOpen (A/B).
 NATIVE_CONV1X1 = True
+# Bottleneck bn2 applied inside conv3's GEMM prologue (stats-only BN pass, no normalised
+# activation in HBM); hparam ``bn_prologue: false`` materialises it (A/B).
+BN_PROLOGUE = True
 
 
 def c1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     if NATIVE_CONV1X1 and FUSED_BN:
         return native_conv.conv1x1(x, conv)
     return conv(x)
+
+
+def bn_relu_c1x1(x: torch.Tensor, bn_mod: BatchNormAct2d, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(relu(bn(x)))`` with the BN applied in the 1x1 GEMM's A-operand prologue (the normalised
+    activation is never written to HBM; ``ops.conv.bn_relu_conv1x1``)."""
+    if NATIVE_CONV1X1 and FUSED_BN and BN_PROLOGUE:
+        return native_conv.bn_relu_conv1x1(x, bn_mod, conv)
+    return c1x1(bn_mod(x), conv)
 
 
 def bn(c: int, relu: bool) -> BatchNormAct2d:
@@ -85,9 +96,9 @@ class Bottleneck(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
         out = self.bn1(c1x1(x, self.conv1))
-        out = self.bn2(self.conv2(out))
+        out = bn_relu_c1x1(self.conv2(out), self.bn2, self.conv3)
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
-        return self.bn3(c1x1(out, self.conv3), idt, shortcut_link=self.downsample is None)
+        return self.bn3(out, idt, shortcut_link=self.downsample is None)
 
 
 class ResNet(nn.Module):

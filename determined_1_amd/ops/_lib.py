@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -94,7 +94,12 @@ _SIGNATURES = {
         + [c_float, c_float, c_int] + [c_void_p] * 6,
         c_int,
     ),
-    # stream, dtype, x, res, y, M, C, scale, shift, relu
+    # stream, dtype, x, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
+    # save_mean, save_rstd, scale, shift, ws
+    "det_bn_stats_train": (
+        [c_void_p, c_int, c_void_p, c_i64, c_int] + [c_void_p] * 5 + [c_float, c_float] + [c_void_p] * 5,
+        c_int,
+    ),
     # stream, dtype, x, y, idx(u8), N, H, W, C
     "det_maxpool3s2_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
     # stream, dtype, dy, idx(u8), dx, N, H, W, C

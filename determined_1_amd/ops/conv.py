@@ -247,6 +247,104 @@ class _Conv1x1(torch.autograd.Function):
         return dx, dw, None
 
 
+class _BNReluConv1x1(torch.autograd.Function):
+    """``conv1x1(relu(bn(x)))`` for a training-mode BatchNorm whose only consumer is a stride-1 1x1
+    conv (ResNet bottleneck bn2 -> conv3).  The normalised activation is never materialised:
+
+    forward : stats pass over ``x`` (det_bn_stats_train, no apply) -> GEMM whose A-operand prologue
+              applies relu(x*scale+shift) while staging, with the output's BN statistics in its
+              epilogue (for bn3).  Saves the apply pass (read x + write z) and the conv's read of z
+              in exchange for reading x: 2 fewer activation passes per block.
+    backward: dgrad GEMM -> dz; wgrad GEMM re-applies the same prologue to ``x`` (bit-identical z);
+              det_bn_bwd with the ReLU mask recomputed from ``x`` (mask_mode 1) -> dx, dgamma, dbeta.
+    """
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, running_mean, running_var, nbt, momentum, eps, weight):
+        n, c, h, w_ = x.shape
+        cout = weight.shape[0]
+        m = n * h * w_
+        lib = _lib.get_lib()
+        x2 = x.permute(0, 2, 3, 1).reshape(m, c)
+        stats = torch.empty((4, c), dtype=torch.float32, device=x.device)
+        ws = torch.empty(int(lib.det_bn_ws_elems(m, c)), dtype=torch.float32, device=x.device)
+        _lib.check(lib.det_bn_stats_train(
+            _stream(x), 1, x.data_ptr(), m, c, _ptr(gamma), _ptr(beta), _ptr(running_mean), _ptr(running_var),
+            _ptr(nbt), float(-1.0 if momentum is None else momentum), float(eps),
+            stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), ws.data_ptr()),
+            "bn_stats_train")
+        wb = weight.reshape(cout, c)
+        wb = (wb if wb.dtype == torch.bfloat16 else wb.to(torch.bfloat16)).contiguous()
+        y2, parts = conv1x1_nt(x2, wb, scale=stats[2], shift=stats[3], stats=True)
+        y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
+        _attach_partials(y, parts)
+        ctx.save_for_backward(x, gamma, stats, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, stats, weight = ctx.saved_tensors
+        n, c, h, w_ = x.shape
+        cout = weight.shape[0]
+        m = n * h * w_
+        lib = _lib.get_lib()
+        dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(m, cout)
+        x2 = x.permute(0, 2, 3, 1).reshape(m, c)
+        dw = None
+        if ctx.needs_input_grad[8]:
+            from determined_1_amd.ops.arena import landing_buffer
+
+            buf = landing_buffer(weight)
+            if buf is not None and buf.is_contiguous() and buf.dtype in (torch.bfloat16, torch.float32):
+                dw = buf
+            else:
+                dw = torch.empty(weight.shape, dtype=weight.dtype if weight.dtype in (torch.bfloat16, torch.float32)
+                                 else torch.float32, device=weight.device)
+            conv1x1_wgrad(dy2, x2, dw.view(cout, c), scale=stats[2], shift=stats[3])
+            if dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
+        wt = weight.reshape(cout, c).to(torch.bfloat16).t().contiguous()
+        dz2, _ = conv1x1_nt(dy2, wt)  # gradient of relu(bn(x)), [m, c]
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dgb = torch.empty((2, c), dtype=torch.float32, device=x.device) if gamma is not None else None
+        ws = torch.empty(int(lib.det_bn_ws_elems(m, c)), dtype=torch.float32, device=x.device)
+        _lib.check(lib.det_bn_bwd(
+            _stream(x), 1, dz2.data_ptr(), None, x.data_ptr(), None, m, c, 1, _ptr(gamma),
+            stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), dx.data_ptr(), None,
+            None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(), ws.data_ptr()),
+            "bn_bwd")
+        dg = dgb[0] if dgb is not None and ctx.needs_input_grad[1] else None
+        db = dgb[1] if dgb is not None and ctx.needs_input_grad[2] else None
+        return dx, dg, db, None, None, None, None, None, dw
+
+
+FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0}
+
+
+def bn_relu_conv1x1(x: torch.Tensor, bn_mod: torch.nn.modules.batchnorm._BatchNorm,
+                    conv_mod: torch.nn.Conv2d) -> torch.Tensor:
+    """``conv_mod(relu(bn_mod(x)))``.  Training-mode BN on channels_last bf16 CUDA activations feeding a
+    bias-free stride-1 1x1 conv takes ``_BNReluConv1x1`` (BN applied in the GEMM prologue, the
+    normalised activation never written); anything else runs the two modules."""
+    assert getattr(bn_mod, "relu", False), "bn_relu_conv1x1 needs a BatchNormAct2d with relu=True"
+    w = conv_mod.weight
+    ok = (ENABLED and getattr(bn_mod, "fused", False) and x.device.type == "cuda" and x.dim() == 4
+          and x.dtype == torch.bfloat16 and torch.is_grad_enabled() and bn_mod.training and bn_mod.track_running_stats and bn_mod.affine
+          and bn_mod.weight.dtype == torch.float32
+          and conv_mod.bias is None and conv_mod.kernel_size == (1, 1) and conv_mod.stride == (1, 1)
+          and conv_mod.groups == 1 and conv_mod.padding in ((0, 0), 0, "valid")
+          and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
+          and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+          and not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") != torch.bfloat16))
+    if not ok:
+        FUSED_COUNTS["fallback"] += 1
+        return conv1x1(bn_mod(x), conv_mod)
+    FUSED_COUNTS["bn_relu_conv1x1"] += 1
+    with torch.autocast("cuda", enabled=False):
+        return _BNReluConv1x1.apply(x, bn_mod.weight, bn_mod.bias, bn_mod.running_mean, bn_mod.running_var,
+                                    bn_mod.num_batches_tracked, bn_mod.momentum, bn_mod.eps, w)
+
+
 def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> torch.Tensor:
     """``conv_mod(x)``; takes the native GEMM path for bias-free 1x1 stride-1 convs on channels_last
     bf16 CUDA activations (channels % 64 == 0), else the module itself."""

@@ -730,6 +730,32 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
   return static_cast<int>(hipGetLastError());
 }
 
+// Training statistics only (stats_partial + finalize + num_batches_tracked bump), no apply pass:
+// the consumer applies relu(x*scale + shift) itself in its GEMM prologue (det_conv.hip), so the
+// normalised activation is never written to HBM.  ResNet bottlenecks use it for bn2 -> conv3.
+int det_bn_stats_train(void* stream, int dtype, const void* x, int64_t M, int C, const float* gamma,
+                       const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                       float momentum, float eps, float* save_mean, float* save_rstd, float* scale, float* shift,
+                       float* ws) {
+  if (C % 8 != 0 || M <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Geom g = make_geom(M, C);
+  float* pmean = ws;
+  float* pm2 = ws + static_cast<int64_t>(g.nrb) * C;
+  dim3 grid(g.nrb, (C / 8 + g.tpr - 1) / g.tpr);
+  if (dtype == 1)
+    hipLaunchKernelGGL(bn_stats_partial<unsigned short>, grid, dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), g, pmean, pm2);
+  else
+    hipLaunchKernelGGL(bn_stats_partial<float>, grid, dim3(kThreads), 0, st, static_cast<const float*>(x), g,
+                       pmean, pm2);
+  FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+             save_mean, save_rstd, scale, shift};
+  launch_stats_finalize(st, pmean, pm2, g, fa, ws + 2 * static_cast<int64_t>(g.nrb) * C + 3 * static_cast<int64_t>(C));
+  if (num_batches_tracked) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, num_batches_tracked);
+  return static_cast<int>(hipGetLastError());
+}
+
 // Training forward when the producer already computed the statistics partials (det_conv.hip GEMM
 // epilogue): Chan-merge the [nrb, C] (mean, M2) partials over row-blocks of `rpb` rows, then apply.
 // ws (nullable, >= det_bn_fin_ws_elems(C) floats, 8-B aligned): scratch of the two-stage finalize.

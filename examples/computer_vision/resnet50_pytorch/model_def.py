@@ -36,6 +36,7 @@ class ResNetImageNetTrial(det_torch.PyTorchTrial):
         self.channels_last = bool(hp.get("channels_last", True))
         resnet.FUSED_BN = bool(hp.get("fused_bn", True))
         resnet.NATIVE_CONV1X1 = bool(hp.get("native_conv1x1", True))
+        resnet.BN_PROLOGUE = bool(hp.get("bn_prologue", True))
         model = getattr(resnet, arch)(num_classes=self.num_classes)
         if self.channels_last:
             model = model.to(memory_format=torch.channels_last)

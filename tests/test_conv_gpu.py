@@ -133,11 +133,12 @@ def test_resnet50_native_conv1x1_matches_miopen(gpu):
             losses.append(float(loss))
         return losses
 
-    before = nc.COUNTS["native"]
+    before = nc.COUNTS["native"] + nc.FUSED_COUNTS["bn_relu_conv1x1"]
     ref = run(False)
     got = run(True)
     resnet.NATIVE_CONV1X1 = True
-    assert nc.COUNTS["native"] - before >= 3 * 32  # 32 stride-1 1x1 convs per ResNet-50 forward
+    # 32 stride-1 1x1 convs per ResNet-50 forward (conv3 of each block with bn2 in its prologue)
+    assert nc.COUNTS["native"] + nc.FUSED_COUNTS["bn_relu_conv1x1"] - before >= 3 * 32
     for a, b in zip(got, ref):
         assert abs(a - b) < 0.05 * max(1.0, abs(b)), (got, ref)
 
@@ -167,3 +168,41 @@ def test_conv_stats_feed_bn_two_stage_finalize(gpu, m, cout):
     torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("n,c,h,cout", [(4, 64, 14, 256), (2, 128, 9, 512), (3, 256, 7, 64)])
+def test_bn_relu_conv1x1_matches_fp32_reference(gpu, n, c, h, cout):
+    """conv1x1(relu(bn(x))) with BN applied in the GEMM prologue (stats-only BN pass) vs the fp32
+    PyTorch composite: output, input/gamma/beta/weight gradients, running statistics."""
+    from determined_1_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(n * c + h)
+    x = (torch.randn(n, c, h, h, device=gpu) * 1.5 + 0.3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(c, relu=True).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    cv = torch.nn.Conv2d(c, cout, 1, bias=False).to(gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    dy = torch.randn(n, cout, h, h, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    xf = x.float().detach().requires_grad_(True)
+    bnr = torch.nn.BatchNorm2d(c).to(gpu)
+    bnr.load_state_dict({k: v for k, v in bn.state_dict().items()})
+    wf = cv.weight.float().detach().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(torch.relu(bnr(xf)), wf)
+    ref.backward(dy.float())
+
+    before = conv.FUSED_COUNTS["bn_relu_conv1x1"]
+    xg = x.detach().requires_grad_(True)
+    y = conv.bn_relu_conv1x1(xg, bn, cv)
+    y.backward(dy)
+    assert conv.FUSED_COUNTS["bn_relu_conv1x1"] == before + 1
+    tol = dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(y.float(), ref, **tol)
+    torch.testing.assert_close(xg.grad.float(), xf.grad, **tol)
+    torch.testing.assert_close(cv.weight.grad.float(), wf.grad, rtol=3e-2, atol=3e-2 * (n * h * h) ** 0.5)
+    torch.testing.assert_close(bn.weight.grad, bnr.weight.grad, rtol=3e-2, atol=3e-2 * (n * h * h) ** 0.5)
+    torch.testing.assert_close(bn.bias.grad, bnr.bias.grad, rtol=3e-2, atol=3e-2 * (n * h * h) ** 0.5)
+    torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn.running_var, bnr.running_var, rtol=1e-3, atol=1e-3)
+    assert int(bn.num_batches_tracked) == 1

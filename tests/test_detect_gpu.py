@@ -27,12 +27,12 @@ def test_roi_align_fwd_bwd_matches_reference(gpu, dtype):
     rois = _rois(g)
     levels = detect.map_levels(rois[:, 1:], 2, 5)
     scales = [0.25, 0.125, 0.0625, 0.03125]
-    ref_in = [f.float().requires_grad_(True) for f in feats]
+    ref_in = [f.detach().float().clone().requires_grad_(True) for f in feats]
     ref = detect.roi_align_multilevel(ref_in, rois, levels, scales, 7, 2)
     dy = torch.randn(ref.shape, generator=g)
     ref.backward(dy)
 
-    gin = [f.cuda().requires_grad_(True) for f in feats]
+    gin = [f.detach().cuda().requires_grad_(True) for f in feats]
     out = detect.roi_align_multilevel(gin, rois.cuda(), levels.cuda(), scales, 7, 2)
     assert detect.COUNTS["roi_align_native"] > 0
     # sample positions are computed in a different (equally valid) fp32 order than the reference,
