@@ -51,8 +51,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--no-fused-bn", action="store_true", help="stock MIOpen BN + separate add/ReLU (A/B)")
     ap.add_argument("--no-native-conv1x1", action="store_true", help="1x1 convs on MIOpen instead of det_conv GEMMs (A/B)")
-    ap.add_argument("--no-bn-prologue", action="store_true",
-                    help="materialise bottleneck bn2's output instead of applying it in conv3's GEMM prologue (A/B)")
+    ap.add_argument("--no-native-stem", action="store_true", help="7x7 stem conv on MIOpen instead of det_conv (A/B)")
+    ap.add_argument("--bn-prologue", action="store_true",
+                    help="apply bottleneck bn2 in conv3's GEMM prologue instead of materialising it (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
                     help="MIOpen find mode for the conv algorithms (tuned during the untimed warmup)")
     ap.add_argument("--launch-timeout", type=float, default=float(os.environ.get("DET_BENCH_LAUNCH_TIMEOUT", "0")),
@@ -181,7 +182,8 @@ def main() -> None:
             "channels_last": not args.no_channels_last,
             "fused_bn": not args.no_fused_bn,
             "native_conv1x1": not args.no_native_conv1x1,
-            "bn_prologue": not args.no_bn_prologue,
+            "bn_prologue": args.bn_prologue,
+            "native_stem": not args.no_native_stem,
             "image_size": args.image_size,
         },
         "resources": {"slots_per_trial": world},
@@ -272,7 +274,8 @@ def main() -> None:
                 "bucket_mb": args.bucket_mb,
                 "fused_bn": not args.no_fused_bn,
                 "native_conv1x1": not args.no_native_conv1x1,
-                "bn_prologue": not args.no_bn_prologue,
+                "bn_prologue": args.bn_prologue,
+                "native_stem": not args.no_native_stem,
                 "final_avg_loss": loss,
                 "world_size_seen": [e[2] for e in per_rank],
                 "backend": per_rank[0][3],

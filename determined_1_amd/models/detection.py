@@ -399,14 +399,18 @@ class SyntheticDetection(torch.utils.data.Dataset):
         return img, target
 
 
-def pad_collate(batch: Sequence[Tuple[torch.Tensor, Dict[str, torch.Tensor]]]) -> Tuple[Dict[str, torch.Tensor], List]:
-    """Pad a list of ``[3, h, w]`` images to the batch max (rounded up to 32, the backbone stride)
-    and return ``({"tensors": [B,3,H,W], "mask": [B,H,W] True on padding}, targets)`` -- the
-    reference's ``unwrap_collate_fn`` layout."""
+def pad_collate(batch: Sequence[Tuple[torch.Tensor, Dict[str, torch.Tensor]]],
+                multiple: int = 32) -> Tuple[Dict[str, torch.Tensor], List]:
+    """Pad a list of ``[3, h, w]`` images to the batch max (rounded up to ``multiple``, at least the
+    backbone stride 32) and return ``({"tensors": [B,3,H,W], "mask": [B,H,W] True on padding},
+    targets)`` -- the reference's ``unwrap_collate_fn`` layout.  A coarser ``multiple`` (e.g. 128)
+    buckets the padded shapes: the masked padding changes nothing the model reads, but far fewer
+    distinct conv shapes reach MIOpen (each new one costs a find / kernel build)."""
+    multiple = max(32, int(multiple))
     imgs, targets = zip(*batch)
     hm = max(i.shape[1] for i in imgs)
     wm = max(i.shape[2] for i in imgs)
-    hm, wm = (hm + 31) // 32 * 32, (wm + 31) // 32 * 32
+    hm, wm = (hm + multiple - 1) // multiple * multiple, (wm + multiple - 1) // multiple * multiple
     t = imgs[0].new_zeros(len(imgs), 3, hm, wm)
     mask = torch.ones(len(imgs), hm, wm, dtype=torch.bool)
     for k, im in enumerate(imgs):

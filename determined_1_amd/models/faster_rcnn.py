@@ -371,8 +371,11 @@ class RoIHeads(nn.Module):
 # ------------------------------------------------------------------------------------------------
 class FasterRCNN(nn.Module):
     def __init__(self, num_classes: int = 91, min_size: int = 800, max_size: int = 1333, arch: str = "resnet50",
-                 trainable_layers: int = 3, channels_last: bool = True) -> None:
+                 trainable_layers: int = 3, channels_last: bool = True, size_divisible: int = 32) -> None:
         super().__init__()
+        # size_divisible: the padded batch is rounded up to it (torchvision's 32 by default); a coarser
+        # bucket (128) keeps the set of conv shapes MIOpen sees small (each new one costs a find)
+        self.size_divisible = max(32, int(size_divisible))
         self.backbone = ResNetFPN(arch, trainable_layers)
         c = self.backbone.out_channels
         self.rpn = RPN(c, {"training": 2000, "testing": 1000}, {"training": 2000, "testing": 1000})
@@ -396,8 +399,9 @@ class FasterRCNN(nn.Module):
                 ry, rx = x.shape[-2] / h, x.shape[-1] / w
                 t["boxes"] = t["boxes"].float() * torch.tensor([rx, ry, rx, ry], device=x.device)
                 new_targets.append(t)
-        hm = (max(s[0] for s in sizes) + 31) // 32 * 32
-        wm = (max(s[1] for s in sizes) + 31) // 32 * 32
+        d = self.size_divisible
+        hm = (max(s[0] for s in sizes) + d - 1) // d * d
+        wm = (max(s[1] for s in sizes) + d - 1) // d * d
         batch = resized[0].new_zeros(len(resized), 3, hm, wm)
         for i, x in enumerate(resized):
             batch[i, :, :x.shape[-2], :x.shape[-1]] = x

@@ -22,8 +22,14 @@ FUSED_BN = True
 # (ops/csrc/det_conv.hip); hparam ``native_conv1x1: false`` keeps them on MIOpen (A/B).
 NATIVE_CONV1X1 = True
 # Bottleneck bn2 applied inside conv3's GEMM prologue (stats-only BN pass, no normalised
-# activation in HBM); hparam ``bn_prologue: false`` materialises it (A/B).
-BN_PROLOGUE = True
+# activation in HBM).  Off by default: measured 1.1 % slower end to end on the MI355X (9,949 vs
+# 10,056 samples/s, profiles/r2_bench_resnet50_bn_prologue_ab.jsonl) -- the prologue's VALU work
+# in the forward and wgrad GEMMs costs more than the two activation passes it saves.
+BN_PROLOGUE = False
+# 7x7/2 stem conv as an implicit GEMM on the det_conv MFMA tiles with the stem BN's statistics in
+# its epilogue (ops.conv.stem_conv; input channels padded to 4); hparam ``native_stem: false``
+# keeps it on MIOpen (A/B).
+NATIVE_STEM = True
 
 
 def c1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
@@ -141,8 +147,14 @@ class ResNet(nn.Module):
             layers.append(block(self.inplanes, planes))
         return nn.Sequential(*layers)
 
+    def _stem(self, x: torch.Tensor) -> torch.Tensor:
+        """conv1 on 3-channel images, or 4-channel ones with a zero 4th channel (``u8_normalize(pad4=True)``)."""
+        if NATIVE_STEM and FUSED_BN:
+            return native_conv.stem_conv(x, self.conv1)
+        return self.conv1(x[:, :3] if x.shape[1] == 4 and self.conv1.in_channels == 3 else x)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(self.bn1(self._stem(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -142,6 +142,12 @@ _SIGNATURES = {
     "det_igemm_conv": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2, c_int),
     # stream, dY, X, out, out_dtype, M, N, K, scale_x, shift_x, ws, out_scale, Ho, Wo, Hi, Wi
     "det_conv_tn": ([c_void_p] * 4 + [c_int, c_i64, c_int, c_int] + [c_void_p] * 3 + [c_float] + [c_int] * 4, c_int),
+    # stream, X, W, Y, M, Hi, Wi, Ho, Wo, pmean, pm2
+    "det_stem_conv_fwd": ([c_void_p] * 4 + [c_i64] + [c_int] * 4 + [c_void_p] * 2, c_int),
+    # stream, dY, X, out, out_dtype, M, Hi, Wi, Ho, Wo, ws, out_scale
+    "det_stem_conv_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 4 + [c_void_p, c_float], c_int),
+    # stream, in(u8 NHWC C<=3), out(NHWC 4), out_dtype, npix, C, mean, std
+    "det_u8_normalize_pad4": ([c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_void_p, c_void_p], c_int),
     # det_transformer.hip: fused LayerNorm / dropout / residual / GELU / bias-grad epilogues
     "det_tf_ln_max_hidden": ([], c_int),
     "det_tf_ln_ws_elems": ([c_i64, c_int], c_i64),

@@ -318,7 +318,109 @@ class _BNReluConv1x1(torch.autograd.Function):
         return dx, dg, db, None, None, None, None, None, dw
 
 
-FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0}
+FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0, "stem": 0, "stem_fallback": 0}
+
+
+# ------------------------------------------------------------------------------------------------
+# ResNet stem: 7x7 stride-2 pad-3 convolution, 64 filters, over channels padded to 4
+# ------------------------------------------------------------------------------------------------
+def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
+    """[64, C<=4, 7, 7] -> the [64, 256] bf16 im2col weight det_stem_conv reads: k = r*32 + s*4 + c
+    over an 8x8x4 box, zero outside the 7x7xC kernel."""
+    co, ci = w.shape[0], w.shape[1]
+    wp = torch.zeros(co, 8, 8, 4, dtype=torch.bfloat16, device=w.device)
+    wp[:, :7, :7, :ci] = w.detach().permute(0, 2, 3, 1).to(torch.bfloat16)
+    return wp.view(co, 256)
+
+
+def unpack_stem_grad(dwk: torch.Tensor, ci: int) -> torch.Tensor:
+    return dwk.view(-1, 8, 8, 4)[:, :7, :7, :ci].permute(0, 3, 1, 2)
+
+
+def pad_channels4(x: torch.Tensor) -> torch.Tensor:
+    """[N, 3, H, W] channels_last -> [N, 4, H, W] channels_last with a zero 4th channel."""
+    n, c, h, w = x.shape
+    out = torch.zeros((n, 4, h, w), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    out[:, :c] = x
+    return out
+
+
+class _StemConv(torch.autograd.Function):
+    """ResNet stem conv as an implicit GEMM on the det_conv MFMA tiles (csrc/det_conv.hip, GM_STEM):
+    forward with the stem BatchNorm's statistics in the epilogue (its stats pass over the largest
+    activation of the network disappears), weight gradient as a split-M implicit GEMM.  The input
+    (the image batch) needs no gradient; when it does, the input gradient comes from MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x4, weight, stats):
+        n, _, hi, wi = x4.shape
+        ho, wo = (hi - 1) // 2 + 1, (wi - 1) // 2 + 1
+        m = n * ho * wo
+        wk = pack_stem_weight(weight)
+        y = torch.empty((n, 64, ho, wo), dtype=torch.bfloat16, device=x4.device, memory_format=torch.channels_last)
+        parts = None
+        pm = pq = None
+        if stats:
+            rpb = rows_per_block(64)
+            nrb = (m + rpb - 1) // rpb
+            pm = torch.empty(nrb, 64, dtype=torch.float32, device=x4.device)
+            pq = torch.empty(nrb, 64, dtype=torch.float32, device=x4.device)
+            parts = (pm, pq, rpb)
+        _lib.check(_lib.get_lib().det_stem_conv_fwd(_stream(x4), x4.data_ptr(), wk.data_ptr(), y.data_ptr(), int(m),
+                                                    int(hi), int(wi), int(ho), int(wo), _ptr(pm), _ptr(pq)),
+                   "stem_conv_fwd")
+        _attach_partials(y, parts)
+        ctx.save_for_backward(x4, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x4, weight = ctx.saved_tensors
+        n, _, hi, wi = x4.shape
+        ho, wo = dy.shape[2], dy.shape[3]
+        m = n * ho * wo
+        dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            lib = _lib.get_lib()
+            ws = torch.empty(int(lib.det_conv_tn_ws_elems(m, 64, 256)), dtype=torch.float32, device=dy.device)
+            dwk = torch.empty(64, 256, dtype=torch.float32, device=dy.device)
+            _lib.check(lib.det_stem_conv_wgrad(_stream(dy), dyc.data_ptr(), x4.data_ptr(), dwk.data_ptr(), 0, int(m),
+                                               int(hi), int(wi), int(ho), int(wo), ws.data_ptr(), 1.0),
+                       "stem_conv_wgrad")
+            dw = unpack_stem_grad(dwk, weight.shape[1]).to(weight.dtype).contiguous(memory_format=torch.channels_last)
+        if ctx.needs_input_grad[0]:
+            w4 = torch.zeros((64, 4, 7, 7), dtype=torch.bfloat16, device=dy.device)
+            w4[:, :weight.shape[1]] = weight.detach().to(torch.bfloat16)
+            dx = torch.ops.aten.convolution_backward(dyc, x4, w4, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        return dx, dw, None
+
+
+def stem_conv(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> torch.Tensor:
+    """``conv_mod(x)`` for the ResNet stem (7x7/2, pad 3, 64 filters, no bias) on channels_last bf16
+    CUDA images with 3 channels or 4 (a zero 4th channel, as ``u8_normalize(pad4=True)`` emits).
+    Anything else runs the module (on the first 3 channels of a padded input)."""
+    w = conv_mod.weight
+    ok = (ENABLED and x.device.type == "cuda" and x.dim() == 4 and x.shape[1] in (3, 4) and w.shape[1] <= 4
+          and conv_mod.bias is None and conv_mod.kernel_size == (7, 7) and conv_mod.stride == (2, 2)
+          and conv_mod.padding in ((3, 3), 3) and conv_mod.dilation == (1, 1) and conv_mod.groups == 1
+          and w.shape[0] == 64 and conv_mod.padding_mode == "zeros"
+          and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+    if ok:
+        autocast = torch.is_autocast_enabled("cuda")
+        if x.dtype != torch.bfloat16 and not (autocast and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            ok = False
+    if not ok:
+        FUSED_COUNTS["stem_fallback"] += 1
+        return conv_mod(x[:, :w.shape[1]] if x.shape[1] > w.shape[1] else x)
+    FUSED_COUNTS["stem"] += 1
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    if x.shape[1] == 3:
+        x = pad_channels4(x)
+    with torch.autocast("cuda", enabled=False):
+        return _StemConv.apply(x, w, stats)
 
 
 def bn_relu_conv1x1(x: torch.Tensor, bn_mod: torch.nn.modules.batchnorm._BatchNorm,

@@ -65,6 +65,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // Input-row gather of a 1x1 stride-2 convolution: output row m = ((n*Ho)+ho)*Wo+wo reads input
 // row (n*Hi + 2ho)*Wi + 2wo.
+constexpr int kGmDirect = 0, kGmStride2 = 1, kGmStem = 2;  // A/X row gather modes
+
 struct Gather {
   int Ho, Wo, Hi, Wi;
   __device__ __forceinline__ int64_t row(int64_t m) const {
@@ -73,6 +75,32 @@ struct Gather {
     const int rem = static_cast<int>(m - n * hw);
     const int ho = rem / Wo, wo = rem - ho * Wo;
     return (n * Hi + 2 * ho) * Wi + 2 * wo;
+  }
+
+  // ResNet stem (7x7, stride 2, pad 3) over an NHWC input with channels padded to 4 (one pixel =
+  // 8 B).  K layout of the im2col row: k = r*32 + s*4 + c for r, s in 0..7 (tap 7 and channel 3
+  // carry zero weights), so one 16-B chunk q = k/8 is the pixel pair (r = q>>2, s = 2(q&3) + 0/1):
+  // adjacent pixels of one input row, contiguous in memory.
+  __device__ __forceinline__ const unsigned short* stem(int64_t m, int& ih0, int& iw0,
+                                                         const unsigned short* base) const {
+    const int64_t hw = static_cast<int64_t>(Ho) * Wo;
+    const int64_t n = m / hw;
+    const int rem = static_cast<int>(m - n * hw);
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    ih0 = 2 * ho - 3;
+    iw0 = 2 * wo - 3;
+    return base + n * static_cast<int64_t>(Hi) * Wi * 4;
+  }
+  __device__ __forceinline__ us8 stem_chunk(const unsigned short* img, bool valid, int ih0, int iw0, int q) const {
+    const int r = q >> 2, s = (q & 3) * 2;
+    const int ih = ih0 + r, iw = iw0 + s;
+    const bool rowok = valid && r < 7 && ih >= 0 && ih < Hi;
+    typedef __attribute__((ext_vector_type(4))) unsigned short us4;
+    us4 lo = us4{0, 0, 0, 0}, hi = us4{0, 0, 0, 0};
+    const unsigned short* p = img + (static_cast<int64_t>(ih) * Wi + iw) * 4;
+    if (rowok && iw >= 0 && iw < Wi) lo = *reinterpret_cast<const us4*>(p);
+    if (rowok && s + 1 < 7 && iw + 1 >= 0 && iw + 1 < Wi) hi = *reinterpret_cast<const us4*>(p + 4);
+    return us8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
 };
 
@@ -110,7 +138,7 @@ struct NtArgs {
 // OCC: workgroups per CU the register budget is sized for.  K == 64 (one K tile: layer1's
 // 64-channel side, every dgrad into a 64-channel input) is a pure streaming pass with no K loop
 // to overlap loads with, so it runs single-buffered (half the LDS) at higher occupancy instead.
-template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, bool STRIDE2, int OCC>
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC>
 __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
@@ -133,13 +161,18 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
 
   const unsigned short* aptr[ACH];
   bool aval[ACH];
+  int ih0[ACH], iw0[ACH];  // GM_STEM: top-left input pixel of the row's 7x7 window
 #pragma unroll
   for (int i = 0; i < ACH; ++i) {
     const int64_t m = m0 + r0 + 32 * i;
     aval[i] = m < a.M;
     int64_t row = aval[i] ? m : 0;
-    if (STRIDE2) row = a.g.row(row);
-    aptr[i] = a.A + row * K + kc * 8;
+    if (GM == kGmStride2) row = a.g.row(row);
+    if (GM == kGmStem) {
+      aptr[i] = a.g.stem(row, ih0[i], iw0[i], a.A);
+    } else {
+      aptr[i] = a.A + row * K + kc * 8;
+    }
   }
   const unsigned short* bptr = a.B + static_cast<int64_t>(n0 + r0) * K + kc * 8;
 
@@ -148,7 +181,8 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
     const int64_t k = static_cast<int64_t>(kt) * kBK;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      if (aval[i]) ra[i] = *reinterpret_cast<const us8*>(aptr[i] + k);
+      if (GM == kGmStem) ra[i] = a.g.stem_chunk(aptr[i], aval[i], ih0[i], iw0[i], kt * 8 + kc);
+      else if (aval[i]) ra[i] = *reinterpret_cast<const us8*>(aptr[i] + k);
       else ra[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
     }
 #pragma unroll
@@ -320,7 +354,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const unsigned char* tile, int k0, int
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BN, int BK, bool PRO, bool STRIDE2>
+template <int BN, int BK, bool PRO, int GM>
 __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
   constexpr int TN = BN / 2, TK = BK / 2, FN = TN / 16, FK = TK / 16;
   constexpr int YB = 64 * BN * 2, XB = 64 * BK * 2, BUF = YB + XB;
@@ -353,7 +387,13 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
       const int idx = tid + i * kThreads, r = idx / XCPR, c = idx - r * XCPR;
       const int64_t m = mb + r;
       xval[i] = m < mend;
-      const int64_t row = STRIDE2 ? a.g.row(xval[i] ? m : 0) : (xval[i] ? m : 0);
+      if (GM == kGmStem) {
+        int ih, iw;
+        const unsigned short* img = a.g.stem(xval[i] ? m : 0, ih, iw, a.X);
+        rx[i] = a.g.stem_chunk(img, xval[i], ih, iw, (k0 >> 3) + c);
+        continue;
+      }
+      const int64_t row = GM == kGmStride2 ? a.g.row(xval[i] ? m : 0) : (xval[i] ? m : 0);
       if (xval[i]) rx[i] = *reinterpret_cast<const us8*>(a.X + row * a.K + k0 + c * 8);
       else rx[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
     }
@@ -458,11 +498,11 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G, OCC>), dim3(static_cast<unsigned>(nwg)), \
                      dim3(kThreads), smem, st, a)
   if (stride2) {
-    if (pro) { if (stats) DET_NT(true, true, true); else DET_NT(true, false, true); }
-    else { if (stats) DET_NT(false, true, true); else DET_NT(false, false, true); }
+    if (pro) { if (stats) DET_NT(true, true, kGmStride2); else DET_NT(true, false, kGmStride2); }
+    else { if (stats) DET_NT(false, true, kGmStride2); else DET_NT(false, false, kGmStride2); }
   } else {
-    if (pro) { if (stats) DET_NT(true, true, false); else DET_NT(true, false, false); }
-    else { if (stats) DET_NT(false, true, false); else DET_NT(false, false, false); }
+    if (pro) { if (stats) DET_NT(true, true, kGmDirect); else DET_NT(true, false, kGmDirect); }
+    else { if (stats) DET_NT(false, true, kGmDirect); else DET_NT(false, false, kGmDirect); }
   }
 #undef DET_NT
   return static_cast<int>(hipGetLastError());
@@ -474,8 +514,8 @@ int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride
   constexpr int smem = 2 * 64 * (BN + BK) * 2;
 #define DET_TN(P, G) \
   hipLaunchKernelGGL((gemm_tn_kernel<BN, BK, P, G>), dim3(nwg), dim3(kThreads), smem, st, a)
-  if (stride2) { if (pro) DET_TN(true, true); else DET_TN(false, true); }
-  else { if (pro) DET_TN(true, false); else DET_TN(false, false); }
+  if (stride2) { if (pro) DET_TN(true, kGmStride2); else DET_TN(false, kGmStride2); }
+  else { if (pro) DET_TN(true, kGmDirect); else DET_TN(false, kGmDirect); }
 #undef DET_TN
   return static_cast<int>(hipGetLastError());
 }
@@ -544,6 +584,58 @@ int det_conv_tn(void* stream, const void* dY, const void* X, void* out, int out_
   else if (bk == 128) rc = launch_tn<64, 128>(st, a, splits, pro, stride2);
   else rc = launch_tn<64, 64>(st, a, splits, pro, stride2);
   if (rc != 0) return rc;
+  int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
+  if (grid > 2048) grid = 2048;
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
+                       static_cast<unsigned short*>(out));
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
+                       static_cast<float*>(out));
+  return static_cast<int>(hipGetLastError());
+}
+
+// ResNet stem convolution (7x7, stride 2, pad 3, 64 filters) as an implicit GEMM on the MFMA tiles
+// above: Y[M, 64] = im2col(X)[M, 256] . W[64, 256]^T, X NHWC bf16 with channels padded to 4, W in
+// the k = r*32 + s*4 + c layout with zero taps/channel (ops/conv.py pack_stem_weight).  pmean/pm2
+// (nullable): BN statistics partials of Y, consumed by the stem BatchNorm (no stats pass).
+int det_stem_conv_fwd(void* stream, const void* X, const void* W, void* Y, int64_t M, int Hi, int Wi, int Ho, int Wo,
+                      float* pmean, float* pm2) {
+  if (M <= 0 || Ho <= 0 || Wo <= 0 || M % (static_cast<int64_t>(Ho) * Wo) != 0) return -1;
+  if (Ho != (Hi + 6 - 7) / 2 + 1 || Wo != (Wi + 6 - 7) / 2 + 1) return -3;
+  if ((pmean == nullptr) != (pm2 == nullptr)) return -2;
+  NtArgs a{static_cast<const unsigned short*>(X), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(Y),
+           M, 64, 256, nullptr, nullptr, pmean, pm2, Gather{Ho, Wo, Hi, Wi}};
+  const int64_t nwg = (M + 127) / 128;
+  if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
+  constexpr int smem = nt_smem<128, 64, 2>();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (pmean)
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, true, kGmStem, 2>), dim3(static_cast<unsigned>(nwg)),
+                       dim3(kThreads), smem, st, a);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, false, kGmStem, 2>), dim3(static_cast<unsigned>(nwg)),
+                       dim3(kThreads), smem, st, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Stem weight gradient dW[64, 256] (out_dtype 0 fp32 / 1 bf16) = out_scale * dY[M, 64]^T . im2col(X),
+// split-M fp32 slabs in ws (>= det_conv_tn_ws_elems(M, 64, 256)) reduced by a second launch.
+int det_stem_conv_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int Hi,
+                        int Wi, int Ho, int Wo, float* ws, float out_scale) {
+  if (M <= 0 || Ho <= 0 || Wo <= 0 || M % (static_cast<int64_t>(Ho) * Wo) != 0) return -1;
+  if (Ho != (Hi + 6 - 7) / 2 + 1 || Wo != (Wi + 6 - 7) / 2 + 1) return -3;
+  constexpr int N = 64, K = 256;
+  const int64_t slab = static_cast<int64_t>(N) * K;
+  const int splits = static_cast<int>(det_conv_tn_ws_elems(M, N, K) / slab);
+  int64_t rps = (M + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  TnArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, N, K, rps,
+           nullptr, nullptr, Gather{Ho, Wo, Hi, Wi}};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int nwg = (N / 64) * (K / 128) * splits;
+  constexpr int smem = 2 * 64 * (64 + 128) * 2;
+  hipLaunchKernelGGL((gemm_tn_kernel<64, 128, false, kGmStem>), dim3(nwg), dim3(kThreads), smem, st, a);
   int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
   if (grid > 2048) grid = 2048;
   if (out_dtype == 1)

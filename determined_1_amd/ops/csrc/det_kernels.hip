@@ -419,6 +419,24 @@ struct ChanParams {
   float inv_std[4];
 };
 
+// uint8 NHWC (C <= 3) -> bf16 NHWC with the channels padded to 4 (zero 4th channel): one 8-B store
+// per pixel, the layout the ResNet stem implicit GEMM (det_conv.hip GM_STEM) reads.
+__global__ void __launch_bounds__(kBlock)
+u8_normalize_pad4_kernel(const uint8_t* __restrict__ in, ushort4* __restrict__ out, int64_t npix, int C,
+                         ChanParams cp) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += stride) {
+    float f[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < C; ++c) f[c] = (static_cast<float>(in[p * C + c]) - cp.mean[c]) * cp.inv_std[c];
+    ushort4 o;
+    o.x = __builtin_bit_cast(unsigned short, static_cast<__bf16>(f[0]));
+    o.y = __builtin_bit_cast(unsigned short, static_cast<__bf16>(f[1]));
+    o.z = __builtin_bit_cast(unsigned short, static_cast<__bf16>(f[2]));
+    o.w = __builtin_bit_cast(unsigned short, static_cast<__bf16>(f[3]));
+    out[p] = o;
+  }
+}
+
 template <typename TO>
 __global__ void __launch_bounds__(kBlock)
 u8_normalize_kernel(const uint8_t* __restrict__ in, TO* __restrict__ out, int64_t n, int C,
@@ -665,6 +683,22 @@ int det_u8_normalize(void* stream, const uint8_t* in, void* out, int out_dtype, 
   else
     hipLaunchKernelGGL(u8_normalize_kernel<float>, dim3(grid), dim3(kBlock), 0, st, in,
                        static_cast<float*>(out), n, C, cp);
+  return static_cast<int>(hipGetLastError());
+}
+
+
+int det_u8_normalize_pad4(void* stream, const uint8_t* in, void* out, int out_dtype, int64_t npix, int C,
+                          const float* mean, const float* stdv) {
+  if (npix <= 0) return 0;
+  if (C < 1 || C > 3 || out_dtype != kBF16) return -1;
+  ChanParams cp;
+  for (int c = 0; c < 4; ++c) {
+    cp.mean[c] = c < C ? mean[c] : 0.f;
+    cp.inv_std[c] = c < C ? 1.f / stdv[c] : 1.f;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(u8_normalize_pad4_kernel, dim3(grid_for(npix)), dim3(kBlock), 0, st, in,
+                     static_cast<ushort4*>(out), npix, C, cp);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -254,21 +254,27 @@ def u8_normalize(
     mean: Sequence[float],
     std: Sequence[float],
     out_dtype: torch.dtype = torch.bfloat16,
+    pad4: bool = False,
 ) -> torch.Tensor:
     """uint8 NHWC [N,H,W,C] -> normalized float tensor of logical shape [N,C,H,W] in
-    channels_last memory format (no transpose pass: NHWC bytes are already channels_last)."""
+    channels_last memory format (no transpose pass: NHWC bytes are already channels_last).
+    ``pad4`` (bf16, C <= 3): emit 4 channels, the last one zero -- the input layout of the native
+    ResNet stem (``ops.conv.stem_conv``)."""
     x = images_u8_nhwc
     assert x.dtype == torch.uint8 and x.dim() == 4 and x.is_contiguous()
     n, h, w, c = x.shape
-    out = torch.empty((n, c, h, w), dtype=out_dtype, device=x.device, memory_format=torch.channels_last)
+    pad4 = pad4 and c <= 3 and out_dtype == torch.bfloat16
+    co = 4 if pad4 else c
+    out = torch.empty((n, co, h, w), dtype=out_dtype, device=x.device, memory_format=torch.channels_last)
     if is_gpu(x):
         import ctypes
 
         m = (ctypes.c_float * 4)(*[float(v) for v in mean] + [0.0] * (4 - len(mean)))
         s = (ctypes.c_float * 4)(*[float(v) for v in std] + [1.0] * (4 - len(std)))
+        fn = _lib.get_lib().det_u8_normalize_pad4 if pad4 else _lib.get_lib().det_u8_normalize
         _lib.check(
-            _lib.get_lib().det_u8_normalize(
-                _stream_ptr(x), x.data_ptr(), out.data_ptr(), dtype_code(out_dtype), x.numel(), c,
+            fn(
+                _stream_ptr(x), x.data_ptr(), out.data_ptr(), dtype_code(out_dtype), n * h * w if pad4 else x.numel(), c,
                 ctypes.cast(m, ctypes.c_void_p), ctypes.cast(s, ctypes.c_void_p),
             ),
             "u8_normalize",
@@ -277,5 +283,7 @@ def u8_normalize(
         mt = torch.tensor(mean, dtype=torch.float32)
         st = torch.tensor(std, dtype=torch.float32)
         y = (x.float() - mt) / st  # NHWC
-        out.copy_(y.permute(0, 3, 1, 2))
+        if pad4:
+            out.zero_()
+        out[:, :c].copy_(y.permute(0, 3, 1, 2))
     return out

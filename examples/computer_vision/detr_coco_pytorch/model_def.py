@@ -13,6 +13,7 @@ MI355X notes: the backbone's frozen BatchNorm is folded into its convolutions (o
 layer), the matcher moves all decoder layers' cost matrices to the host in one copy per step, and
 ``clip_grads`` uses the fused gradient-norm kernel (``det.pytorch.ClipGradsNorm``).
 """
+import functools
 from collections import defaultdict
 from typing import Any, Dict
 
@@ -55,14 +56,19 @@ class DETRTrial(pytorch.PyTorchTrial):
         return SyntheticDetection(n, num_classes=91, min_size=int(self.hp.get("min_image_size", 480)),
                                   max_size=int(self.hp.get("max_image_size", 640)), seed=0 if train else 1)
 
+    @property
+    def _collate(self):
+        # padded shapes bucketed to 128 px (masked padding; few distinct conv shapes for MIOpen)
+        return functools.partial(pad_collate, multiple=int(self.hp.get("pad_multiple", 128)))
+
     def build_training_data_loader(self) -> pytorch.DataLoader:
         return pytorch.DataLoader(self._dataset(True), batch_size=self.context.get_per_slot_batch_size(),
-                                  collate_fn=pad_collate, shuffle=True,
+                                  collate_fn=self._collate, shuffle=True,
                                   num_workers=int(self.hp.get("num_workers", 0)))
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:
         return pytorch.DataLoader(self._dataset(False), batch_size=self.context.get_per_slot_batch_size(),
-                                  collate_fn=pad_collate, shuffle=False,
+                                  collate_fn=self._collate, shuffle=False,
                                   num_workers=int(self.hp.get("num_workers", 0)))
 
     def _losses(self, outputs: Dict[str, Any], targets: Any, eval: bool = False) -> Dict[str, torch.Tensor]:

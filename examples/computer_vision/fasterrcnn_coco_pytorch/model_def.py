@@ -35,7 +35,8 @@ class ObjectDetectionTrial(pytorch.PyTorchTrial):
         self.dataset_train, self.dataset_val = torch.utils.data.random_split(
             dataset, [train_size, len(dataset) - train_size], generator=torch.Generator().manual_seed(0))
         model = FasterRCNN(num_classes=2, min_size=int(hp.get("transform_min_size", 800)),
-                           max_size=int(hp.get("transform_max_size", 1333)), arch=hp.get("backbone", "resnet50"))
+                           max_size=int(hp.get("transform_max_size", 1333)), arch=hp.get("backbone", "resnet50"),
+                           size_divisible=int(hp.get("size_divisible", 128)))
         self.model = context.wrap_model(model)
         self.optimizer = context.wrap_optimizer(torch.optim.SGD(
             [p for p in self.model.parameters() if p.requires_grad], lr=float(hp["learning_rate"]),

@@ -36,7 +36,8 @@ class ResNetImageNetTrial(det_torch.PyTorchTrial):
         self.channels_last = bool(hp.get("channels_last", True))
         resnet.FUSED_BN = bool(hp.get("fused_bn", True))
         resnet.NATIVE_CONV1X1 = bool(hp.get("native_conv1x1", True))
-        resnet.BN_PROLOGUE = bool(hp.get("bn_prologue", True))
+        resnet.BN_PROLOGUE = bool(hp.get("bn_prologue", False))
+        resnet.NATIVE_STEM = bool(hp.get("native_stem", True))
         model = getattr(resnet, arch)(num_classes=self.num_classes)
         if self.channels_last:
             model = model.to(memory_format=torch.channels_last)
@@ -54,7 +55,9 @@ class ResNetImageNetTrial(det_torch.PyTorchTrial):
 
     def _inputs(self, images_u8: torch.Tensor) -> torch.Tensor:
         if images_u8.dtype == torch.uint8:
-            x = u8_normalize(images_u8, IMAGENET_MEAN, IMAGENET_STD, out_dtype=self.compute_dtype)
+            # the native stem reads 4-channel pixels (8 B): the normalize kernel pads for free
+            pad4 = self.channels_last and resnet.NATIVE_STEM and resnet.FUSED_BN and images_u8.is_cuda
+            x = u8_normalize(images_u8, IMAGENET_MEAN, IMAGENET_STD, out_dtype=self.compute_dtype, pad4=pad4)
             return x if self.channels_last else x.contiguous()
         return images_u8
 

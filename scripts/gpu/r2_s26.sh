@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/s26
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_conv_gpu.py tests/test_detect_gpu.py > gpurun_out/s26/conv.log 2>&1 || { tail -40 gpurun_out/s26/conv.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_detect_gpu.py tests/test_conv_gpu.py "tests/test_examples_gpu.py" -k "detect or roi or nms or conv or bn_relu or detr or fasterrcnn" > gpurun_out/s26/conv.log 2>&1 || { tail -40 gpurun_out/s26/conv.log; exit 1; }
 tail -2 gpurun_out/s26/conv.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/s26/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/s26/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/s26/pytest_gpu.log

@@ -206,3 +206,82 @@ def test_bn_relu_conv1x1_matches_fp32_reference(gpu, n, c, h, cout):
     torch.testing.assert_close(bn.running_mean, bnr.running_mean, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(bn.running_var, bnr.running_var, rtol=1e-3, atol=1e-3)
     assert int(bn.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9)])
+@pytest.mark.parametrize("cin", [3, 4])
+def test_stem_conv_matches_fp32_reference(gpu, n, h, w, cin):
+    """ResNet stem (7x7/2, pad 3, 64 filters) as the det_conv implicit GEMM vs fp32 conv2d: output,
+    BN statistics partials of the output, weight gradient; 3-channel input (padded inside) and
+    4-channel input with a zero 4th channel."""
+    torch.manual_seed(n * h + w + cin)
+    x3 = torch.randn(n, 3, h, w, device=gpu).to(torch.bfloat16)
+    x = x3 if cin == 3 else torch.cat([x3, torch.zeros_like(x3[:, :1])], 1)
+    x = x.contiguous(memory_format=torch.channels_last)
+    cv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(gpu).to(torch.bfloat16)
+    cv = cv.to(memory_format=torch.channels_last)
+    before = conv.FUSED_COUNTS["stem"]
+    y = conv.stem_conv(x, cv)
+    assert conv.FUSED_COUNTS["stem"] == before + 1
+    wf = cv.weight.float().detach().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(x3.float(), wf, stride=2, padding=3)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    m = y.shape[0] * y.shape[2] * y.shape[3]
+    parts = conv.take_partials(y)
+    assert parts is not None
+    mean, var = _merge(*parts, m)
+    yb = y.float().permute(0, 2, 3, 1).reshape(m, 64).double().cpu()
+    torch.testing.assert_close(mean, yb.mean(0), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(var, yb.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
+    dy = torch.randn_like(ref).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    ref.backward(dy.float())
+    torch.testing.assert_close(cv.weight.grad.float(), wf.grad, rtol=2e-2, atol=2e-3 * m ** 0.5)
+
+
+def test_u8_normalize_pad4(gpu):
+    from determined_1_amd.ops.functional import u8_normalize
+
+    g = torch.Generator().manual_seed(0)
+    u8 = torch.randint(0, 256, (3, 17, 19, 3), generator=g, dtype=torch.uint8)
+    mean, std = (0.485 * 255, 0.456 * 255, 0.406 * 255), (0.229 * 255, 0.224 * 255, 0.225 * 255)
+    ref = u8_normalize(u8, mean, std, out_dtype=torch.bfloat16, pad4=True)
+    got = u8_normalize(u8.to(gpu), mean, std, out_dtype=torch.bfloat16, pad4=True)
+    assert got.shape == (3, 4, 17, 19) and got.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(got.cpu().float(), ref.float(), rtol=1e-2, atol=1e-2)
+    assert float(got[:, 3].abs().max()) == 0.0
+
+
+def test_resnet50_native_stem_matches_miopen(gpu):
+    """Three SGD steps of ResNet-50 with the stem on det_conv (4-channel padded input) vs on MIOpen."""
+    from determined_1_amd.models import resnet
+
+    def run(native):
+        resnet.NATIVE_STEM = native
+        torch.manual_seed(0)
+        m = resnet.resnet50(num_classes=10).to(gpu).to(memory_format=torch.channels_last).to(torch.bfloat16)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.float()
+        opt = torch.optim.SGD(m.parameters(), lr=0.02, momentum=0.9)
+        g = torch.Generator(device="cpu").manual_seed(1)
+        x = torch.randn(8, 3, 64, 64, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if native:
+            x = conv.pad_channels4(x)
+        y = torch.randint(0, 10, (8,), generator=g).to(gpu)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = torch.nn.functional.cross_entropy(m(x).float(), y)
+            loss.backward()
+            opt.step()
+            losses.append(float(loss.detach()))
+        return losses
+
+    before = conv.FUSED_COUNTS["stem"]
+    ref = run(False)
+    got = run(True)
+    resnet.NATIVE_STEM = True
+    assert conv.FUSED_COUNTS["stem"] - before == 3
+    for a, b in zip(got, ref):
+        assert abs(a - b) < 0.05 * max(1.0, abs(b)), (got, ref)
