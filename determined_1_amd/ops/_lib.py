@@ -144,6 +144,7 @@ _SIGNATURES = {
     "det_conv_tn": ([c_void_p] * 4 + [c_int, c_i64, c_int, c_int] + [c_void_p] * 3 + [c_float] + [c_int] * 4, c_int),
     # stream, X, W, Y, M, Hi, Wi, Ho, Wo, pmean, pm2
     "det_stem_conv_fwd": ([c_void_p] * 4 + [c_i64] + [c_int] * 4 + [c_void_p] * 2, c_int),
+    "det_stem_conv_wgrad_ws_elems": ([c_i64], c_i64),
     # stream, dY, X, out, out_dtype, M, Hi, Wi, Ho, Wo, ws, out_scale
     "det_stem_conv_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 4 + [c_void_p, c_float], c_int),
     # stream, in(u8 NHWC C<=3), out(NHWC 4), out_dtype, npix, C, mean, std

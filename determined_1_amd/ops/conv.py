@@ -340,7 +340,8 @@ def unpack_stem_grad(dwk: torch.Tensor, ci: int) -> torch.Tensor:
 def pad_channels4(x: torch.Tensor) -> torch.Tensor:
     """[N, 3, H, W] channels_last -> [N, 4, H, W] channels_last with a zero 4th channel."""
     n, c, h, w = x.shape
-    out = torch.zeros((n, 4, h, w), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    out = torch.empty((n, 4, h, w), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    out[:, c:].zero_()
     out[:, :c] = x
     return out
 
@@ -383,7 +384,7 @@ class _StemConv(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[1]:
             lib = _lib.get_lib()
-            ws = torch.empty(int(lib.det_conv_tn_ws_elems(m, 64, 256)), dtype=torch.float32, device=dy.device)
+            ws = torch.empty(int(lib.det_stem_conv_wgrad_ws_elems(m)), dtype=torch.float32, device=dy.device)
             dwk = torch.empty(64, 256, dtype=torch.float32, device=dy.device)
             _lib.check(lib.det_stem_conv_wgrad(_stream(dy), dyc.data_ptr(), x4.data_ptr(), dwk.data_ptr(), 0, int(m),
                                                int(hi), int(wi), int(ho), int(wo), ws.data_ptr(), 1.0),

@@ -354,20 +354,24 @@ __device__ __forceinline__ bf16x8 tr_frag(const unsigned char* tile, int k0, int
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BN, int BK, bool PRO, int GM>
+// KSUB: K sub-tiles of BK columns per workgroup (each a separately swizzled [64][BK] LDS image);
+// KSUB = 2 lets one workgroup cover K = 2*BK so every dY row is streamed once (the stem's K = 256).
+template <int BN, int BK, bool PRO, int GM, int KSUB = 1>
 __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
-  constexpr int TN = BN / 2, TK = BK / 2, FN = TN / 16, FK = TK / 16;
-  constexpr int YB = 64 * BN * 2, XB = 64 * BK * 2, BUF = YB + XB;
-  constexpr int YCH = 64 * BN / 8 / kThreads, XCH = 64 * BK / 8 / kThreads;  // 16-B chunks per thread
-  constexpr int YCPR = BN / 8, XCPR = BK / 8;                                // chunks per row
+  constexpr int TN = BN / 2, TK = BK * KSUB / 2, FN = TN / 16, FK = TK / 16;
+  constexpr int XSUB = 64 * BK * 2;  // bytes of one X sub-tile
+  constexpr int YB = 64 * BN * 2, XB = XSUB * KSUB, BUF = YB + XB;
+  constexpr int YCH = 64 * BN / 8 / kThreads, XCH = 64 * BK * KSUB / 8 / kThreads;  // 16-B chunks per thread
+  constexpr int YCPR = BN / 8, XCPR = BK * KSUB / 8;                                // chunks per row
+  constexpr int SCPR = BK / 8;                                                      // chunks per sub-tile row
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wn = wid >> 1, wk = wid & 1;
-  const int ntn = a.N / BN, ntk = a.K / BK, ntiles = ntn * ntk;
+  const int ntn = a.N / BN, ntk = a.K / (BK * KSUB), ntiles = ntn * ntk;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid / ntiles, tile = bid - split * ntiles;
   const int nt = tile / ntk, kt_ = tile - nt * ntk;
-  const int n0 = nt * BN, k0 = kt_ * BK;
+  const int n0 = nt * BN, k0 = kt_ * BK * KSUB;
   const int64_t mbeg = static_cast<int64_t>(split) * a.rows_per_split;
   int64_t mend = mbeg + a.rows_per_split;
   if (mend > a.M) mend = a.M;
@@ -413,7 +417,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
         v = affine_relu8(v, a.scale, a.shift, k0 + c * 8);
         if (!xval[i]) v = us8{0, 0, 0, 0, 0, 0, 0, 0};
       }
-      *reinterpret_cast<us8*>(base + YB + tswz<BK>(r, c)) = v;
+      *reinterpret_cast<us8*>(base + YB + (c / SCPR) * XSUB + tswz<BK>(r, c % SCPR)) = v;
     }
   };
 
@@ -439,7 +443,10 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
 #pragma unroll
       for (int i = 0; i < FN; ++i) yf[i] = tr_frag<BN>(base, ks * 32, wn * TN + i * 16, lane);
 #pragma unroll
-      for (int j = 0; j < FK; ++j) xf[j] = tr_frag<BK>(base + YB, ks * 32, wk * TK + j * 16, lane);
+      for (int j = 0; j < FK; ++j) {
+        const int kc = wk * TK + j * 16;
+        xf[j] = tr_frag<BK>(base + YB + (kc / BK) * XSUB, ks * 32, kc % BK, lane);
+      }
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -619,23 +626,32 @@ int det_stem_conv_fwd(void* stream, const void* X, const void* W, void* Y, int64
   return static_cast<int>(hipGetLastError());
 }
 
+// fp32 workspace elements det_stem_conv_wgrad needs: 512 split-M slabs of [64, 256] (2 workgroups
+// per CU over 256 CUs), fewer for small M (>= 1024 rows per split).
+int64_t det_stem_conv_wgrad_ws_elems(int64_t M) {
+  int64_t splits = (M + 1023) / 1024;
+  if (splits > 512) splits = 512;
+  if (splits < 1) splits = 1;
+  return splits * 64 * 256;
+}
+
 // Stem weight gradient dW[64, 256] (out_dtype 0 fp32 / 1 bf16) = out_scale * dY[M, 64]^T . im2col(X),
-// split-M fp32 slabs in ws (>= det_conv_tn_ws_elems(M, 64, 256)) reduced by a second launch.
+// split-M fp32 slabs in ws (>= det_stem_conv_wgrad_ws_elems(M)) reduced by a second launch.
 int det_stem_conv_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int Hi,
                         int Wi, int Ho, int Wo, float* ws, float out_scale) {
   if (M <= 0 || Ho <= 0 || Wo <= 0 || M % (static_cast<int64_t>(Ho) * Wo) != 0) return -1;
   if (Ho != (Hi + 6 - 7) / 2 + 1 || Wo != (Wi + 6 - 7) / 2 + 1) return -3;
   constexpr int N = 64, K = 256;
   const int64_t slab = static_cast<int64_t>(N) * K;
-  const int splits = static_cast<int>(det_conv_tn_ws_elems(M, N, K) / slab);
+  const int splits = static_cast<int>(det_stem_conv_wgrad_ws_elems(M) / slab);
   int64_t rps = (M + splits - 1) / splits;
   rps = (rps + 63) / 64 * 64;
   TnArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, N, K, rps,
            nullptr, nullptr, Gather{Ho, Wo, Hi, Wi}};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int nwg = (N / 64) * (K / 128) * splits;
-  constexpr int smem = 2 * 64 * (64 + 128) * 2;
-  hipLaunchKernelGGL((gemm_tn_kernel<64, 128, false, kGmStem>), dim3(nwg), dim3(kThreads), smem, st, a);
+  const int nwg = splits;  // one 64 x 256 output tile: every dY row is read once
+  constexpr int smem = 2 * 64 * (64 + 2 * 128) * 2;
+  hipLaunchKernelGGL((gemm_tn_kernel<64, 128, false, kGmStem, 2>), dim3(nwg), dim3(kThreads), smem, st, a);
   int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
   if (grid > 2048) grid = 2048;
   if (out_dtype == 1)

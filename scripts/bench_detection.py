@@ -17,16 +17,24 @@
 The reference publishes no throughput for either example.
 """
 import argparse
+import importlib.util
 import json
 import os
 import sys
 import threading
 import time
 
-import torch
-
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+
+# the shipped MIOpen find-db / kernel cache (seeded for the bucketed detection shapes by
+# scripts/miopen_seed_detection.py), configured before torch initialises MIOpen
+_spec = importlib.util.spec_from_file_location("_det_miopen_db", os.path.join(REPO, "determined_1_amd", "ops", "miopen_db.py"))
+_mdb = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(_mdb)  # type: ignore
+_mdb.configure(os.environ)
+
+import torch  # noqa: E402
 
 
 def main() -> None:
