@@ -2,8 +2,11 @@
 gradient time with the input channels padded from 3 to 4 or 8 (zero channels, zero weights --
 the same convolution), channels_last bf16.  Prints one JSON line per variant."""
 import json
+import os
 import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 import torch.nn.functional as F
@@ -45,8 +48,22 @@ def main() -> None:
             ref = y.float()
         else:
             err = float((y.float() - ref).abs().max())
-        print(json.dumps({"cin": c, "batch": n, "fwd_ms": round(fwd, 4), "wgrad_ms": round(wgrad, 4),
+        print(json.dumps({"impl": "miopen", "cin": c, "batch": n, "fwd_ms": round(fwd, 4), "wgrad_ms": round(wgrad, 4),
                           "max_abs_diff_vs_c3": err}), flush=True)
+        if c == 4:
+            from determined_1_amd.ops import conv as nc
+
+            cv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(dev)
+            with torch.no_grad():
+                cv.weight.copy_(w3.float())
+            cv = cv.to(torch.bfloat16)
+            cvp = cv.weight.detach().requires_grad_(True)
+            fwd_n = timeit(lambda: nc._StemConv.apply(x, cvp, True))
+            yn = nc._StemConv.apply(x, cvp, True)
+            wgrad_n = timeit(lambda: torch.autograd.grad(yn, cvp, dy, retain_graph=True))
+            print(json.dumps({"impl": "det_conv GM_STEM (+BN stats)", "occ": os.environ.get("DET_STEM_OCC", "2"),
+                              "cin": 4, "batch": n, "fwd_ms": round(fwd_n, 4), "wgrad_ms": round(wgrad_n, 4),
+                              "max_abs_diff_vs_miopen": float((yn.float() - ref).abs().max())}), flush=True)
 
 
 if __name__ == "__main__":
