@@ -150,7 +150,7 @@ class ResNet(nn.Module):
     def _stem(self, x: torch.Tensor) -> torch.Tensor:
         """conv1 on 3-channel images, or 4-channel ones with a zero 4th channel (``u8_normalize(pad4=True)``)."""
         if NATIVE_STEM and FUSED_BN:
-            return native_conv.stem_conv(x, self.conv1)
+            return native_conv.stem_conv(x, self.conv1, stats=self.bn1.training)
         return self.conv1(x[:, :3] if x.shape[1] == 4 and self.conv1.in_channels == 3 else x)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
