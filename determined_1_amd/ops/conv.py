@@ -319,6 +319,10 @@ class _BNReluConv1x1(torch.autograd.Function):
 
 
 FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0, "stem": 0, "stem_fallback": 0}
+# Stem weight gradient: the det_conv split-M implicit GEMM (True) or MIOpen's NHWC C=4 kernel (False,
+# default: 0.49 vs 0.82 ms at batch 512, profiles/r2_stem_microbench.jsonl).  The forward stays native
+# (0.64 ms including the BN statistics vs MIOpen 0.70 + a 0.17 ms stats pass).
+STEM_NATIVE_WGRAD = False
 
 
 # ------------------------------------------------------------------------------------------------
@@ -382,19 +386,27 @@ class _StemConv(torch.autograd.Function):
         m = n * ho * wo
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        if ctx.needs_input_grad[1]:
+        ci = weight.shape[1]
+        native_wgrad = ctx.needs_input_grad[1] and STEM_NATIVE_WGRAD
+        if native_wgrad:
             lib = _lib.get_lib()
             ws = torch.empty(int(lib.det_stem_conv_wgrad_ws_elems(m)), dtype=torch.float32, device=dy.device)
             dwk = torch.empty(64, 256, dtype=torch.float32, device=dy.device)
             _lib.check(lib.det_stem_conv_wgrad(_stream(dy), dyc.data_ptr(), x4.data_ptr(), dwk.data_ptr(), 0, int(m),
                                                int(hi), int(wi), int(ho), int(wo), ws.data_ptr(), 1.0),
                        "stem_conv_wgrad")
-            dw = unpack_stem_grad(dwk, weight.shape[1]).to(weight.dtype).contiguous(memory_format=torch.channels_last)
-        if ctx.needs_input_grad[0]:
-            w4 = torch.zeros((64, 4, 7, 7), dtype=torch.bfloat16, device=dy.device)
-            w4[:, :weight.shape[1]] = weight.detach().to(torch.bfloat16)
-            dx = torch.ops.aten.convolution_backward(dyc, x4, w4, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
+            dw = unpack_stem_grad(dwk, ci).to(weight.dtype).contiguous(memory_format=torch.channels_last)
+        if ctx.needs_input_grad[0] or (ctx.needs_input_grad[1] and not native_wgrad):
+            # MIOpen on the 4-channel problem (its NHWC C=4 wgrad kernel beats the C=3 one 1.4x)
+            w4 = torch.empty((64, 4, 7, 7), dtype=torch.bfloat16, device=dy.device, memory_format=torch.channels_last)
+            w4[:, ci:].zero_()
+            w4[:, :ci] = weight.detach().to(torch.bfloat16)
+            gx, gw, _ = torch.ops.aten.convolution_backward(
+                dyc, x4, w4, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                [bool(ctx.needs_input_grad[0]), bool(ctx.needs_input_grad[1] and not native_wgrad), False])
+            dx = gx
+            if gw is not None:
+                dw = gw[:, :ci].to(weight.dtype).contiguous(memory_format=torch.channels_last)
         return dx, dw, None
 
 

@@ -32,7 +32,6 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 namespace {
 
@@ -616,18 +615,11 @@ int det_stem_conv_fwd(void* stream, const void* X, const void* W, void* Y, int64
            M, 64, 256, nullptr, nullptr, pmean, pm2, Gather{Ho, Wo, Hi, Wi}};
   const int64_t nwg = (M + 127) / 128;
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
-  constexpr int smem = nt_smem<128, 64, 2>();  // double-buffered (4 K tiles) at either occupancy
+  constexpr int smem = nt_smem<128, 64, 2>();  // double-buffered: 4 K tiles
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // DET_STEM_OCC=3: 3 workgroups per CU (register budget ~170 VGPRs) to hide more gather latency
-  static const bool occ3 = [] { const char* e = getenv("DET_STEM_OCC"); return e && e[0] == '3'; }();
   const dim3 grid(static_cast<unsigned>(nwg));
-  if (occ3) {
-    if (pmean) hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, true, kGmStem, 3>), grid, dim3(kThreads), smem, st, a);
-    else hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, false, kGmStem, 3>), grid, dim3(kThreads), smem, st, a);
-  } else {
-    if (pmean) hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, true, kGmStem, 2>), grid, dim3(kThreads), smem, st, a);
-    else hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, false, kGmStem, 2>), grid, dim3(kThreads), smem, st, a);
-  }
+  if (pmean) hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, true, kGmStem, 2>), grid, dim3(kThreads), smem, st, a);
+  else hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 2, 2, false, false, kGmStem, 2>), grid, dim3(kThreads), smem, st, a);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -60,8 +60,9 @@ def main() -> None:
             cvp = cv.weight.detach().requires_grad_(True)
             fwd_n = timeit(lambda: nc._StemConv.apply(x, cvp, True))
             yn = nc._StemConv.apply(x, cvp, True)
+            nc.STEM_NATIVE_WGRAD = True
             wgrad_n = timeit(lambda: torch.autograd.grad(yn, cvp, dy, retain_graph=True))
-            print(json.dumps({"impl": "det_conv GM_STEM (+BN stats)", "occ": os.environ.get("DET_STEM_OCC", "2"),
+            print(json.dumps({"impl": "det_conv GM_STEM (+BN stats; native split-M wgrad)",
                               "cin": 4, "batch": n, "fwd_ms": round(fwd_n, 4), "wgrad_ms": round(wgrad_n, 4),
                               "max_abs_diff_vs_miopen": float((yn.float() - ref).abs().max())}), flush=True)
 

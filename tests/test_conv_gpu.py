@@ -210,10 +210,12 @@ def test_bn_relu_conv1x1_matches_fp32_reference(gpu, n, c, h, cout):
 
 @pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9)])
 @pytest.mark.parametrize("cin", [3, 4])
-def test_stem_conv_matches_fp32_reference(gpu, n, h, w, cin):
+@pytest.mark.parametrize("native_wgrad", [True, False])
+def test_stem_conv_matches_fp32_reference(gpu, n, h, w, cin, native_wgrad, monkeypatch):
     """ResNet stem (7x7/2, pad 3, 64 filters) as the det_conv implicit GEMM vs fp32 conv2d: output,
     BN statistics partials of the output, weight gradient; 3-channel input (padded inside) and
     4-channel input with a zero 4th channel."""
+    monkeypatch.setattr(conv, "STEM_NATIVE_WGRAD", native_wgrad)
     torch.manual_seed(n * h + w + cin)
     x3 = torch.randn(n, 3, h, w, device=gpu).to(torch.bfloat16)
     x = x3 if cin == 3 else torch.cat([x3, torch.zeros_like(x3[:, :1])], 1)
