@@ -313,7 +313,7 @@ class RoIHeads(nn.Module):
         labels_t = reg_t = None
         if self.training:
             assert targets is not None
-            props, labs, regs = [], [], []
+            props, labs, regs, mids = [], [], [], []
             for p, t in zip(proposals, targets):
                 gt, gl = t["boxes"].to(p.dtype), t["labels"]
                 p = torch.cat([p, gt])
@@ -328,12 +328,15 @@ class RoIHeads(nn.Module):
                     mg = torch.zeros_like(p)
                 pos, neg = sample(lab, self.per_image, self.pos_fraction)
                 keep = torch.cat([pos, neg])
+                mid = m.clamp(min=0)[keep] if gt.numel() else torch.zeros_like(keep)
                 p, lab, mg = p[keep], lab[keep], mg[keep]
                 props.append(p)
                 labs.append(lab)
+                mids.append(mid)
                 regs.append(self.coder.encode(mg, p))
             proposals = props
             labels_t, reg_t = torch.cat(labs), torch.cat(regs)
+            self.sampled = (props, labs, mids)  # for heads that train on the same sample (masks)
         x = self._pool(feats, proposals, image_hw).flatten(1)
         x = F.relu(self.fc7(F.relu(self.fc6(x))))
         logits, box_reg = self.cls_score(x), self.bbox_pred(x)
@@ -366,6 +369,20 @@ class RoIHeads(nn.Module):
         return out
 
 
+def paste_masks(masks: torch.Tensor, boxes: torch.Tensor, image_hw: Tuple[int, int]) -> torch.Tensor:
+    """``masks [D, M, M]`` (probabilities over each box) -> ``[D, 1, H, W]`` full-image masks."""
+    h, w = int(image_hw[0]), int(image_hw[1])
+    out = masks.new_zeros((masks.shape[0], 1, h, w))
+    for i in range(masks.shape[0]):
+        x0, y0, x1, y1 = boxes[i].tolist()
+        x0, y0 = max(int(math.floor(x0)), 0), max(int(math.floor(y0)), 0)
+        x1, y1 = min(int(math.ceil(x1)), w), min(int(math.ceil(y1)), h)
+        if x1 > x0 and y1 > y0:
+            out[i, 0, y0:y1, x0:x1] = F.interpolate(masks[i][None, None], size=(y1 - y0, x1 - x0), mode="bilinear",
+                                                    align_corners=False)[0, 0]
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 # the detector
 # ------------------------------------------------------------------------------------------------
@@ -379,10 +396,13 @@ class FasterRCNN(nn.Module):
         self.backbone = ResNetFPN(arch, trainable_layers)
         c = self.backbone.out_channels
         self.rpn = RPN(c, {"training": 2000, "testing": 1000}, {"training": 2000, "testing": 1000})
-        self.roi_heads = RoIHeads(c, num_classes)
+        self.roi_heads = self._make_roi_heads(c, num_classes)
         self.min_size, self.max_size, self.channels_last = min_size, max_size, channels_last
         self.register_buffer("mean", torch.tensor(IMAGENET_MEAN).view(3, 1, 1), persistent=False)
         self.register_buffer("std", torch.tensor(IMAGENET_STD).view(3, 1, 1), persistent=False)
+
+    def _make_roi_heads(self, c: int, num_classes: int) -> RoIHeads:
+        return RoIHeads(c, num_classes)
 
     def _transform(self, images: Sequence[torch.Tensor], targets: Optional[List[Dict[str, torch.Tensor]]]):
         dtype = next(p for p in self.parameters()).dtype
@@ -398,6 +418,10 @@ class FasterRCNN(nn.Module):
                 t = dict(targets[i])
                 ry, rx = x.shape[-2] / h, x.shape[-1] / w
                 t["boxes"] = t["boxes"].float() * torch.tensor([rx, ry, rx, ry], device=x.device)
+                if "masks" in t:  # instance masks follow the image (nearest, as torchvision's transform)
+                    mk = t["masks"]
+                    t["masks"] = F.interpolate(mk[None].float(), size=x.shape[-2:], mode="nearest")[0].to(mk.dtype) \
+                        if mk.numel() else mk.new_zeros((0,) + tuple(x.shape[-2:]))
                 new_targets.append(t)
         d = self.size_divisible
         hm = (max(s[0] for s in sizes) + d - 1) // d * d
@@ -424,4 +448,6 @@ class FasterRCNN(nn.Module):
         for d, s, o in zip(dets, sizes, orig):
             ry, rx = o[0] / s[0], o[1] / s[1]
             d["boxes"] = d["boxes"] * torch.tensor([rx, ry, rx, ry], device=d["boxes"].device)
+            if "masks" in d:  # per-box 28x28 probabilities pasted into the original image
+                d["masks"] = paste_masks(d["masks"], d["boxes"], o)
         return dets

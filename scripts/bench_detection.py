@@ -5,6 +5,10 @@
                       COCO-shaped images (the reference's ``fake`` backend) of 480-640 px, padded
                       per batch.  A step = forward, Hungarian matching of all 6 decoder layers,
                       backward, clip, AdamW.
+  --model maskrcnn    ``maskrcnn_coco_pytorch/const.yaml`` (stands in for the reference's
+                      mmdetection ``maskrcnn.yaml``; it publishes 0.310 s/iter at 2 images per V100):
+                      Mask R-CNN R50-FPN, 2 images per GPU, SGD, COCO-shaped 480-640 px synthetic
+                      instances resized to 800 px short side.
   --model fasterrcnn  ``fasterrcnn_coco_pytorch/const.yaml``: Faster R-CNN R50-FPN, batch 2, SGD
                       momentum; PennFudan-sized synthetic images (300-500 px) resized to 800 px
                       short side as torchvision's transform does.  A step = full detector forward
@@ -43,7 +47,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-per-gpu", type=int, default=2)
     ap.add_argument("--amp", default="O0", help="O0 = fp32 as the reference config; O2 = bf16 weights + fp32 master")
-    ap.add_argument("--model", choices=["detr", "fasterrcnn"], default="detr")
+    ap.add_argument("--model", choices=["detr", "fasterrcnn", "maskrcnn"], default="detr")
     ap.add_argument("--min-size", type=int, default=0, help="synthetic image side range (0: model default)")
     ap.add_argument("--max-size", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny model (CPU smoke only)")
@@ -65,6 +69,12 @@ def main() -> None:
         cfg = yaml.safe_load(open(os.path.join(ex, "const_fake.yaml")))
         lo, hi = args.min_size or 480, args.max_size or 640
         metric, model_name = "mAP", "detr-r50 6enc/6dec/100q"
+    elif args.model == "maskrcnn":
+        ex = os.path.join(REPO, "examples", "computer_vision", "maskrcnn_coco_pytorch")
+        Trial = load_model_def(ex).MaskRCNNTrial
+        cfg = yaml.safe_load(open(os.path.join(ex, "const.yaml")))
+        lo, hi = args.min_size or 480, args.max_size or 640
+        metric, model_name = "val_mask_iou", "maskrcnn-r50-fpn 800px (mmdet mask_rcnn_r50_fpn_1x shape)"
     else:
         ex = os.path.join(REPO, "examples", "computer_vision", "fasterrcnn_coco_pytorch")
         Trial = load_model_def(ex).ObjectDetectionTrial
@@ -76,6 +86,8 @@ def main() -> None:
     hp.update(global_batch_size=gbs, amp=args.amp, min_image_size=lo, max_image_size=hi, num_workers=2)
     if args.model == "fasterrcnn":
         hp["num_images"] = max(int(hp.get("num_images", 170)), (args.steps + args.warmup) * gbs * 2)
+    if args.model == "maskrcnn":
+        hp["train_records"] = max(int(hp.get("train_records", 2000)), (args.steps + args.warmup) * gbs)
     if args.small:
         hp.update(backbone="resnet26", enc_layers=1, dec_layers=2, hidden_dim=32, nheads=2, dim_feedforward=64,
                   num_queries=10, num_workers=0, transform_min_size=96, transform_max_size=160)
@@ -123,6 +135,7 @@ def main() -> None:
             "data": f"synthetic detection images {lo}-{hi}px; random-init weights",
             "config": {"model": model_name, "per_gpu_batch": args.batch_per_gpu, "global_batch": gbs, "amp": args.amp,
                        "optimizer": "AdamW, backbone lr 1e-5, clip 0.1" if args.model == "detr" else "SGD momentum",
+                       "s_per_iter": round(el / steps, 4),
                        "parallelism": f"dp{world}"}}), flush=True)
     pdist.shutdown()
 

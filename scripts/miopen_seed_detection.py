@@ -55,6 +55,8 @@ class Resized(torch.utils.data.Dataset):
         t = dict(t)
         if self.absolute:
             t["boxes"] = t["boxes"] * torch.tensor([sx, sy, sx, sy])
+            if "masks" in t:
+                t["masks"] = F.interpolate(t["masks"][None].float(), size=(h, w), mode="nearest")[0].to(torch.uint8)
             t["area"] = (t["boxes"][:, 3] - t["boxes"][:, 1]) * (t["boxes"][:, 2] - t["boxes"][:, 0])
         else:
             t["orig_size"] = t["size"] = torch.tensor([h, w])
@@ -70,12 +72,34 @@ def frcnn_sizes():
     return out
 
 
+# Mask R-CNN: COCO-shaped 480-640 px originals -> 800 px short side, long side 800..1067 -> buckets
+# 896 / 1024 / 1152; an original short side of 480 scales by 5/3
+MRCNN_LONG = [None, 600, 640]
+
+
+def mrcnn_sizes():
+    out = []
+    for lh in MRCNN_LONG:
+        for lw in MRCNN_LONG:
+            out.append((480, 480) if lh is None else (lh, 480))
+            out.append((480, 480) if lw is None else (480, lw))
+    return out
+
+
 def detr_sizes():
     out = []
     for h in (500, 600):
         for w in (500, 600):
             out += [(h, w), (h, w)]
     return out
+
+
+def _example_module(ex: str, name: str):
+    """``<ex>/<name>.py`` loaded by path (several examples ship a ``data.py``)."""
+    spec = importlib.util.spec_from_file_location(f"_seed_{os.path.basename(ex)}_{name}", os.path.join(ex, name + ".py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)  # type: ignore
+    return mod
 
 
 def run(model: str, amp: str) -> None:
@@ -93,17 +117,31 @@ def run(model: str, amp: str) -> None:
 
         hp = dict(yaml.safe_load(open(os.path.join(ex, "const_fake.yaml")))["hyperparameters"])
         hp.update(global_batch_size=2, num_workers=0, amp=amp, train_records=len(sizes))
+    elif model == "maskrcnn":
+        ex = os.path.join(REPO, "examples", "computer_vision", "maskrcnn_coco_pytorch")
+        base_cls = load_model_def(ex).MaskRCNNTrial
+        sizes = mrcnn_sizes()
+        mdata = _example_module(ex, "data")
+
+        class Seed(base_cls):  # type: ignore
+            def build_training_data_loader(self):
+                return pytorch.DataLoader(Resized(mdata.SyntheticCocoInstances(len(sizes), num_classes=self.num_classes),
+                                                  sizes, True), batch_size=2, collate_fn=mdata.collate_fn)
+
+        import yaml
+
+        hp = dict(yaml.safe_load(open(os.path.join(ex, "const.yaml")))["hyperparameters"])
+        hp.update(global_batch_size=2, amp=amp)
     else:
         ex = os.path.join(REPO, "examples", "computer_vision", "fasterrcnn_coco_pytorch")
         base_cls = load_model_def(ex).ObjectDetectionTrial
         sizes = frcnn_sizes()
-        sys.path.insert(0, ex)
-        from data import SyntheticPedestrians, collate_fn  # noqa: E402
+        fdata = _example_module(ex, "data")
 
         class Seed(base_cls):  # type: ignore
             def build_training_data_loader(self):
-                return pytorch.DataLoader(Resized(SyntheticPedestrians(len(sizes)), sizes, True), batch_size=2,
-                                          collate_fn=collate_fn)
+                return pytorch.DataLoader(Resized(fdata.SyntheticPedestrians(len(sizes)), sizes, True), batch_size=2,
+                                          collate_fn=fdata.collate_fn)
 
         import yaml
 
@@ -122,7 +160,7 @@ def run(model: str, amp: str) -> None:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--models", default="detr,fasterrcnn")
+    ap.add_argument("--models", default="detr,fasterrcnn,maskrcnn")
     ap.add_argument("--amps", default="O0,O2")
     ap.add_argument("--harvest", default="", help="copy the db + kernel cache here (e.g. gpurun_out/miopen_db)")
     args = ap.parse_args()
