@@ -203,17 +203,9 @@ def load_model_def(model_dir: str, name: str = "model_def") -> Any:
     modname = "det_model_def_" + hashlib.sha1(path.encode()).hexdigest()[:12]
     if modname in sys.modules:
         return sys.modules[modname]
-    d = os.path.dirname(path)
-    if d in sys.path:
-        sys.path.remove(d)
-    sys.path.insert(0, d)
-    # sibling modules (e.g. ``data``) another example directory already imported under the same name
-    # must not shadow this directory's own
-    for f in os.listdir(d):
-        sib = f[:-3] if f.endswith(".py") else None
-        m = sys.modules.get(sib) if sib else None
-        if m is not None and os.path.dirname(os.path.abspath(getattr(m, "__file__", "") or "")) != d:
-            del sys.modules[sib]
+    from determined_1_amd.harness.load import isolate_model_dir
+
+    isolate_model_dir(os.path.dirname(path))
     spec = importlib.util.spec_from_file_location(modname, path)
     assert spec is not None and spec.loader is not None, path
     mod = importlib.util.module_from_spec(spec)

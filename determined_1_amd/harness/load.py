@@ -2,6 +2,7 @@
 and ``load/_load_trial_controller.py:10-143``)."""
 import importlib
 import logging
+import os
 import pathlib
 import sys
 from typing import Any, Optional, Type
@@ -31,6 +32,21 @@ def notebook_to_py(ipynb: pathlib.Path) -> pathlib.Path:
     return out
 
 
+def isolate_model_dir(d: str) -> None:
+    """Put model directory ``d`` first on ``sys.path`` and evict cached modules named like one of its
+    ``*.py`` files but loaded from elsewhere (two example directories that both ship a ``data.py``,
+    loaded into one process, must each import their own)."""
+    if d in sys.path:
+        sys.path.remove(d)
+    sys.path.insert(0, d)
+    for f in os.listdir(d):
+        if not f.endswith(".py"):
+            continue
+        m = sys.modules.get(f[:-3])
+        if m is not None and os.path.dirname(os.path.abspath(getattr(m, "__file__", None) or "")) != d:
+            del sys.modules[f[:-3]]
+
+
 def load_trial_class(entrypoint: str, model_dir: Optional[str] = None) -> Type[trial.Trial]:
     """``"module.sub:Class[.Inner]"`` -> the class.  The module is re-imported fresh (the reference
     pops it from ``sys.modules`` so a changed model definition is picked up)."""
@@ -38,9 +54,7 @@ def load_trial_class(entrypoint: str, model_dir: Optional[str] = None) -> Type[t
         raise ValueError(f"entrypoint must look like 'module:TrialClass', got {entrypoint!r}")
     mod_name, qual = entrypoint.split(":", 1)
     if model_dir:
-        d = str(pathlib.Path(model_dir).resolve())
-        if d not in sys.path:
-            sys.path.insert(0, d)
+        isolate_model_dir(str(pathlib.Path(model_dir).resolve()))
     base = pathlib.Path(model_dir or ".")
     nb = base.joinpath(*mod_name.split(".")).with_suffix(".ipynb")
     if nb.exists() and not nb.with_suffix(".py").exists():
