@@ -1,36 +1,33 @@
-"""Mask R-CNN R50-FPN instance segmentation (reference ``examples/computer_vision/mmdetection_pytorch``
-with ``maskrcnn.yaml``, which wraps mmdetection's ``mask_rcnn_r50_fpn_1x_coco``): 2 images per GPU,
-SGD lr 0.02 per 16 images with momentum 0.9 and weight decay 1e-4, linear warmup over the first 500
-iterations, the sum of the RPN, box and mask losses as the training signal.  Validation reports
-the mean best box IoU and mask IoU over ground-truth instances.
+"""RetinaNet R50-FPN detection (reference ``examples/computer_vision/mmdetection_pytorch`` with
+``retinanet.yaml``, which wraps mmdetection's ``retinanet_r50_fpn_1x_coco``): 2 images per GPU, SGD
+lr 0.01 per 16 images with momentum 0.9 and weight decay 1e-4, linear warmup over the first 500
+iterations, focal + L1 losses.  Validation reports the mean best box IoU over ground-truth boxes.
 
-mmdetection is not in this image; the model is the framework's own ``models.mask_rcnn`` on the MI355X
-detection ops (one-launch NHWC RoIAlign for box, mask and mask-target pooling; device NMS), with
-padded batch shapes and the mask-head batch bucketed so MIOpen's find-db covers every conv shape.
-Data: synthetic COCO-shaped instances (``models.detection.SyntheticCocoInstances``); weights random-init.
+mmdetection is not in this image; the model is the framework's own ``models.retinanet`` (device
+NMS, padded batch shapes bucketed so MIOpen's find-db covers every conv shape).  Data: synthetic
+COCO-shaped instances (``models.detection.SyntheticCocoInstances``); weights random-init.
 """
 from typing import Any, Dict
 
 import torch
 
 from determined_1_amd import pytorch
-from determined_1_amd.models.detection import SyntheticCocoInstances, list_collate as collate_fn
+from determined_1_amd.models.detection import SyntheticCocoInstances, list_collate
 from determined_1_amd.models.faster_rcnn import box_iou
-from determined_1_amd.models.mask_rcnn import MaskRCNN
+from determined_1_amd.models.retinanet import RetinaNet
 
 
-class MaskRCNNTrial(pytorch.PyTorchTrial):
+class RetinaNetTrial(pytorch.PyTorchTrial):
     def __init__(self, context: pytorch.PyTorchTrialContext) -> None:
         self.context = context
         hp = context.get_hparams()
         self.hp = hp
         self.num_classes = int(hp.get("num_classes", 81))
-        model = MaskRCNN(num_classes=self.num_classes, min_size=int(hp.get("transform_min_size", 800)),
-                         max_size=int(hp.get("transform_max_size", 1333)), arch=hp.get("backbone", "resnet50"),
-                         size_divisible=int(hp.get("size_divisible", 128)),
-                         mask_bucket=int(hp.get("mask_bucket", 64)))
+        model = RetinaNet(num_classes=self.num_classes, min_size=int(hp.get("transform_min_size", 800)),
+                          max_size=int(hp.get("transform_max_size", 1333)), arch=hp.get("backbone", "resnet50"),
+                          size_divisible=int(hp.get("size_divisible", 128)))
         self.model = context.wrap_model(model)
-        lr = float(hp.get("lr_per_16_images", 0.02)) * context.get_global_batch_size() / 16.0
+        lr = float(hp.get("lr_per_16_images", 0.01)) * context.get_global_batch_size() / 16.0
         self.optimizer = context.wrap_optimizer(torch.optim.SGD(
             [p for p in self.model.parameters() if p.requires_grad], lr=lr, momentum=float(hp.get("momentum", 0.9)),
             weight_decay=float(hp.get("weight_decay", 1e-4))))
@@ -51,11 +48,11 @@ class MaskRCNNTrial(pytorch.PyTorchTrial):
 
     def build_training_data_loader(self) -> pytorch.DataLoader:
         return pytorch.DataLoader(self._data(True), batch_size=self.context.get_per_slot_batch_size(),
-                                  collate_fn=collate_fn, shuffle=True, num_workers=int(self.hp.get("num_workers", 0)))
+                                  collate_fn=list_collate, shuffle=True, num_workers=int(self.hp.get("num_workers", 0)))
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:
         return pytorch.DataLoader(self._data(False), batch_size=self.context.get_per_slot_batch_size(),
-                                  collate_fn=collate_fn, num_workers=int(self.hp.get("num_workers", 0)))
+                                  collate_fn=list_collate, num_workers=int(self.hp.get("num_workers", 0)))
 
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:
         images, targets = batch
@@ -68,18 +65,10 @@ class MaskRCNNTrial(pytorch.PyTorchTrial):
     def evaluate_batch(self, batch: Any) -> Dict[str, Any]:
         images, targets = batch
         out = self.model(list(images))
-        box_iou_sum = mask_iou_sum = 0.0
-        n = 0
+        s, n = 0.0, 0
         for o, t in zip(out, targets):
-            gb, gm = t["boxes"].float(), t["masks"].bool()
+            gb = t["boxes"].float()
             n += gb.shape[0]
-            if o["boxes"].numel() == 0:
-                continue
-            iou = box_iou(gb, o["boxes"].float().to(gb.device))
-            best = iou.max(1)
-            box_iou_sum += float(best.values.sum())
-            pm = o["masks"][best.indices, 0].to(gm.device) >= 0.5  # [G, H, W]
-            inter = (pm & gm).flatten(1).sum(1).float()
-            union = (pm | gm).flatten(1).sum(1).float().clamp(min=1)
-            mask_iou_sum += float((inter / union).sum())
-        return {"val_box_iou": box_iou_sum / max(n, 1), "val_mask_iou": mask_iou_sum / max(n, 1)}
+            if o["boxes"].numel():
+                s += float(box_iou(gb, o["boxes"].float().to(gb.device)).max(1).values.sum())
+        return {"val_box_iou": s / max(n, 1)}

@@ -47,7 +47,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch-per-gpu", type=int, default=2)
     ap.add_argument("--amp", default="O0", help="O0 = fp32 as the reference config; O2 = bf16 weights + fp32 master")
-    ap.add_argument("--model", choices=["detr", "fasterrcnn", "maskrcnn"], default="detr")
+    ap.add_argument("--model", choices=["detr", "fasterrcnn", "maskrcnn", "retinanet"], default="detr")
     ap.add_argument("--min-size", type=int, default=0, help="synthetic image side range (0: model default)")
     ap.add_argument("--max-size", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny model (CPU smoke only)")
@@ -69,6 +69,12 @@ def main() -> None:
         cfg = yaml.safe_load(open(os.path.join(ex, "const_fake.yaml")))
         lo, hi = args.min_size or 480, args.max_size or 640
         metric, model_name = "mAP", "detr-r50 6enc/6dec/100q"
+    elif args.model == "retinanet":
+        ex = os.path.join(REPO, "examples", "computer_vision", "retinanet_coco_pytorch")
+        Trial = load_model_def(ex).RetinaNetTrial
+        cfg = yaml.safe_load(open(os.path.join(ex, "const.yaml")))
+        lo, hi = args.min_size or 480, args.max_size or 640
+        metric, model_name = "val_box_iou", "retinanet-r50-fpn 800px (mmdet retinanet_r50_fpn_1x shape)"
     elif args.model == "maskrcnn":
         ex = os.path.join(REPO, "examples", "computer_vision", "maskrcnn_coco_pytorch")
         Trial = load_model_def(ex).MaskRCNNTrial
@@ -86,7 +92,7 @@ def main() -> None:
     hp.update(global_batch_size=gbs, amp=args.amp, min_image_size=lo, max_image_size=hi, num_workers=2)
     if args.model == "fasterrcnn":
         hp["num_images"] = max(int(hp.get("num_images", 170)), (args.steps + args.warmup) * gbs * 2)
-    if args.model == "maskrcnn":
+    if args.model in ("maskrcnn", "retinanet"):
         hp["train_records"] = max(int(hp.get("train_records", 2000)), (args.steps + args.warmup) * gbs)
     if args.small:
         hp.update(backbone="resnet26", enc_layers=1, dec_layers=2, hidden_dim=32, nheads=2, dim_feedforward=64,

@@ -117,16 +117,17 @@ def run(model: str, amp: str) -> None:
 
         hp = dict(yaml.safe_load(open(os.path.join(ex, "const_fake.yaml")))["hyperparameters"])
         hp.update(global_batch_size=2, num_workers=0, amp=amp, train_records=len(sizes))
-    elif model == "maskrcnn":
-        ex = os.path.join(REPO, "examples", "computer_vision", "maskrcnn_coco_pytorch")
-        base_cls = load_model_def(ex).MaskRCNNTrial
+    elif model in ("maskrcnn", "retinanet"):
+        ex = os.path.join(REPO, "examples", "computer_vision", f"{model}_coco_pytorch")
+        mod = load_model_def(ex)
+        base_cls = mod.MaskRCNNTrial if model == "maskrcnn" else mod.RetinaNetTrial
         sizes = mrcnn_sizes()
-        mdata = _example_module(ex, "data")
+        from determined_1_amd.models import detection as mdata  # SyntheticCocoInstances, list_collate
 
         class Seed(base_cls):  # type: ignore
             def build_training_data_loader(self):
                 return pytorch.DataLoader(Resized(mdata.SyntheticCocoInstances(len(sizes), num_classes=self.num_classes),
-                                                  sizes, True), batch_size=2, collate_fn=mdata.collate_fn)
+                                                  sizes, True), batch_size=2, collate_fn=mdata.list_collate)
 
         import yaml
 
@@ -160,7 +161,7 @@ def run(model: str, amp: str) -> None:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--models", default="detr,fasterrcnn,maskrcnn")
+    ap.add_argument("--models", default="detr,fasterrcnn,maskrcnn,retinanet")
     ap.add_argument("--amps", default="O0,O2")
     ap.add_argument("--harvest", default="", help="copy the db + kernel cache here (e.g. gpurun_out/miopen_db)")
     args = ap.parse_args()

@@ -43,6 +43,9 @@ SHRINK = {
                           "dim_feedforward": 64, "num_queries": 10, "min_image_size": 64, "max_image_size": 96,
                           "train_records": 8, "validation_records": 4, "num_workers": 0, "global_batch_size": 2},
     "gan_mnist_pytorch": {"global_batch_size": 4},
+    "retinanet_coco_pytorch": {"backbone": "resnet26", "train_records": 6, "validation_records": 2,
+                               "min_image_size": 60, "max_image_size": 90, "transform_min_size": 96,
+                               "transform_max_size": 160, "num_classes": 5, "global_batch_size": 2},
     "maskrcnn_coco_pytorch": {"backbone": "resnet26", "train_records": 6, "validation_records": 2,
                               "min_image_size": 60, "max_image_size": 90, "transform_min_size": 96,
                               "transform_max_size": 160, "num_classes": 5, "global_batch_size": 2,
