@@ -386,23 +386,18 @@ def paste_masks(masks: torch.Tensor, boxes: torch.Tensor, image_hw: Tuple[int, i
 # ------------------------------------------------------------------------------------------------
 # the detector
 # ------------------------------------------------------------------------------------------------
-class FasterRCNN(nn.Module):
-    def __init__(self, num_classes: int = 91, min_size: int = 800, max_size: int = 1333, arch: str = "resnet50",
-                 trainable_layers: int = 3, channels_last: bool = True, size_divisible: int = 32) -> None:
+class ImageBatchTransform(nn.Module):
+    """torchvision's ``GeneralizedRCNNTransform`` for the detectors here: normalise, resize each image
+    so its short side is ``min_size`` (long side <= ``max_size``), resize boxes / masks along, and pad
+    the batch to a multiple of ``size_divisible`` (torchvision's 32 by default; a coarser bucket, e.g.
+    128, keeps the set of conv shapes MIOpen sees small -- each new one costs a find)."""
+
+    def __init__(self, min_size: int, max_size: int, size_divisible: int, channels_last: bool) -> None:
         super().__init__()
-        # size_divisible: the padded batch is rounded up to it (torchvision's 32 by default); a coarser
-        # bucket (128) keeps the set of conv shapes MIOpen sees small (each new one costs a find)
         self.size_divisible = max(32, int(size_divisible))
-        self.backbone = ResNetFPN(arch, trainable_layers)
-        c = self.backbone.out_channels
-        self.rpn = RPN(c, {"training": 2000, "testing": 1000}, {"training": 2000, "testing": 1000})
-        self.roi_heads = self._make_roi_heads(c, num_classes)
         self.min_size, self.max_size, self.channels_last = min_size, max_size, channels_last
         self.register_buffer("mean", torch.tensor(IMAGENET_MEAN).view(3, 1, 1), persistent=False)
         self.register_buffer("std", torch.tensor(IMAGENET_STD).view(3, 1, 1), persistent=False)
-
-    def _make_roi_heads(self, c: int, num_classes: int) -> RoIHeads:
-        return RoIHeads(c, num_classes)
 
     def _transform(self, images: Sequence[torch.Tensor], targets: Optional[List[Dict[str, torch.Tensor]]]):
         dtype = next(p for p in self.parameters()).dtype
@@ -433,6 +428,19 @@ class FasterRCNN(nn.Module):
         if self.channels_last and batch.is_cuda:
             batch = batch.contiguous(memory_format=torch.channels_last)
         return batch, sizes, (new_targets if targets is not None else None)
+
+
+class FasterRCNN(ImageBatchTransform):
+    def __init__(self, num_classes: int = 91, min_size: int = 800, max_size: int = 1333, arch: str = "resnet50",
+                 trainable_layers: int = 3, channels_last: bool = True, size_divisible: int = 32) -> None:
+        super().__init__(min_size, max_size, size_divisible, channels_last)
+        self.backbone = ResNetFPN(arch, trainable_layers)
+        c = self.backbone.out_channels
+        self.rpn = RPN(c, {"training": 2000, "testing": 1000}, {"training": 2000, "testing": 1000})
+        self.roi_heads = self._make_roi_heads(c, num_classes)
+
+    def _make_roi_heads(self, c: int, num_classes: int) -> RoIHeads:
+        return RoIHeads(c, num_classes)
 
     def forward(self, images: Sequence[torch.Tensor], targets: Optional[List[Dict[str, torch.Tensor]]] = None):
         if self.training and targets is None:

@@ -16,8 +16,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from determined_1_amd.models.detr import BACKBONE_LAYERS, FrozenBNResNet
-from determined_1_amd.models.faster_rcnn import (IMAGENET_MEAN, IMAGENET_STD, BELOW, BETWEEN, AnchorGenerator, BoxCoder,
-                                                 FasterRCNN, box_iou, match)
+from determined_1_amd.models.faster_rcnn import (BELOW, BETWEEN, AnchorGenerator, BoxCoder, ImageBatchTransform,
+                                                 box_iou, match)
 from determined_1_amd.ops import detect
 
 
@@ -113,20 +113,16 @@ def sigmoid_focal_loss(logits: torch.Tensor, targets: torch.Tensor, alpha: float
     return (alpha * targets + (1 - alpha) * (1 - targets)) * loss
 
 
-class RetinaNet(FasterRCNN):
+class RetinaNet(ImageBatchTransform):
     """``forward(images, targets)`` -> ``{"classification", "bbox_regression"}`` losses in training,
-    per-image ``boxes``/``scores``/``labels`` in eval.  Reuses ``FasterRCNN``'s resize/normalise/pad
-    transform (``size_divisible`` buckets the padded batch shape)."""
+    per-image ``boxes``/``scores``/``labels`` in eval.  Same resize/normalise/pad transform as the
+    two-stage detectors (``size_divisible`` buckets the padded batch shape)."""
 
     def __init__(self, num_classes: int = 91, min_size: int = 800, max_size: int = 1333, arch: str = "resnet50",
                  trainable_layers: int = 3, channels_last: bool = True, size_divisible: int = 128,
                  score_thresh: float = 0.05, nms_thresh: float = 0.5, detections_per_img: int = 100,
                  topk_candidates: int = 1000, fg_iou: float = 0.5, bg_iou: float = 0.4) -> None:
-        nn.Module.__init__(self)
-        self.size_divisible = max(32, int(size_divisible))
-        self.min_size, self.max_size, self.channels_last = min_size, max_size, channels_last
-        self.register_buffer("mean", torch.tensor(IMAGENET_MEAN).view(3, 1, 1), persistent=False)
-        self.register_buffer("std", torch.tensor(IMAGENET_STD).view(3, 1, 1), persistent=False)
+        super().__init__(min_size, max_size, size_divisible, channels_last)
         self.backbone = RetinaFPN(arch, trainable_layers)
         self.anchors = RetinaAnchors()
         self.head = RetinaHead(self.backbone.out_channels, self.anchors.num_anchors(), num_classes)
