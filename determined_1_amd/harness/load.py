@@ -39,11 +39,19 @@ def isolate_model_dir(d: str) -> None:
     if d in sys.path:
         sys.path.remove(d)
     sys.path.insert(0, d)
+    import sysconfig
+
+    installed = tuple(os.path.abspath(p) for p in {sysconfig.get_paths()[k] for k in ("stdlib", "purelib", "platlib")})
     for f in os.listdir(d):
         if not f.endswith(".py"):
             continue
         m = sys.modules.get(f[:-3])
-        if m is not None and os.path.dirname(os.path.abspath(getattr(m, "__file__", None) or "")) != d:
+        mf = getattr(m, "__file__", None) if m is not None else None
+        if not mf:
+            continue
+        mf = os.path.abspath(mf)
+        # only user-code siblings from other model dirs, never installed or standard-library modules
+        if os.path.dirname(mf) != d and not mf.startswith(installed):
             del sys.modules[f[:-3]]
 
 
