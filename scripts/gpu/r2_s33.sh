@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 session 33: final rehearsal on the final tree (fresh box): full GPU test tier (incl. the
+# Round-2 session 33 (re-run after the RetinaNet commits as well): final rehearsal on the final tree (fresh box): full GPU test tier (incl. the
 # Mask R-CNN example), smoke(), 1-GPU ResNet-50 bench, Mask R-CNN from the shipped find-db.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
