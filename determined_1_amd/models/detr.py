@@ -46,29 +46,15 @@ class FrozenBNConv2d(nn.Module):
         self.register_buffer("running_mean", torch.zeros(cout))
         self.register_buffer("running_var", torch.ones(cout))
 
-        self._fold_key = None
-        self._fold_val = None
-
     def folded(self) -> Tuple[torch.Tensor, torch.Tensor]:
         scale = self.bn_weight * (self.running_var + self.eps).rsqrt()
         shift = self.bn_bias - self.running_mean * scale
         return scale, shift
 
-    def _folded_cast(self, wdt: torch.dtype, xdt: torch.dtype) -> Tuple[torch.Tensor, torch.Tensor]:
-        """(scale as the weight dtype [cout,1,1,1], shift as the input dtype), cached: the frozen BN
-        buffers change only through in-place loads (which bump their versions) or moves (new
-        storage), so the ~5 small launches per conv per step are paid once."""
-        bufs = (self.bn_weight, self.bn_bias, self.running_mean, self.running_var)
-        key = tuple((b.data_ptr(), b._version) for b in bufs) + (wdt, xdt, self.eps)
-        if key != self._fold_key or torch.is_grad_enabled() and any(b.requires_grad for b in bufs):
-            scale, shift = self.folded()
-            self._fold_val = (scale.to(wdt).view(-1, 1, 1, 1), shift.to(xdt))
-            self._fold_key = key
-        return self._fold_val
-
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        scale, shift = self._folded_cast(self.weight.dtype, x.dtype)
-        return F.conv2d(x, self.weight * scale, shift, self.stride, self.padding)
+        scale, shift = self.folded()
+        w = self.weight * scale.to(self.weight.dtype).view(-1, 1, 1, 1)
+        return F.conv2d(x, w, shift.to(x.dtype), self.stride, self.padding)
 
 
 class FrozenBottleneck(nn.Module):
