@@ -288,13 +288,19 @@ class _CacheableDecorator:
         lock_key = f"{self._config().get('bucket', '')}/{remote}" if remote else str(path)
 
         def _fetch() -> bool:
-            """Download a complete remote cache into ``path`` (atomically); False if none."""
+            """Download a complete remote cache into ``path`` (atomically); False if none.  Called only
+            under the exclusive lock; a replace that loses to a concurrent writer outside this lock's
+            reach (another node's local-mode fcntl lock) still counts as a hit once meta.json is there."""
             if remote is None or not list(client.list(remote + "/meta.json")):
                 return False
             tmp = pathlib.Path(tempfile.mkdtemp(prefix=".tmp_", dir=str(path.parent)))
             try:
                 client.download_dir(remote, str(tmp))
-                os.replace(tmp, path)
+                try:
+                    os.replace(tmp, path)
+                except OSError:
+                    if not (path / "meta.json").exists():
+                        raise
             finally:
                 if tmp.exists():
                     shutil.rmtree(tmp, ignore_errors=True)
@@ -304,8 +310,10 @@ class _CacheableDecorator:
         def _wrap(make_dataset_fn: Callable) -> Callable:
             @functools.wraps(make_dataset_fn)
             def _decorated(*args: Any, **kwargs: Any) -> Any:
+                # readers only look; every download or build happens under the exclusive lock, which
+                # re-checks first, so concurrent same-node readers never race on the rename
                 with self._lock(path, read=True, key=lock_key):
-                    hit = (path / "meta.json").exists() or _fetch()
+                    hit = (path / "meta.json").exists()
                 if not hit:
                     with self._lock(path, read=False, key=lock_key):
                         if not (path / "meta.json").exists() and not _fetch():
@@ -320,6 +328,12 @@ class _CacheableDecorator:
                                     client.upload_file(str(path / name), f"{remote}/{name}")
                 if self._map_style:
                     data = CachedDataset(path)
+                    if shuffle and not skip_shuffle_at_epoch_end:
+                        logging.warning(
+                            "cache_train/validation_dataset(shuffle=True) on a PyTorchTrial applies ONE fixed "
+                            "permutation (skip_shuffle_at_epoch_end=True semantics): a map-style dataset cannot "
+                            "see epoch boundaries.  Pass shuffle=True to det.pytorch.DataLoader for a per-epoch "
+                            "reshuffle (docs/PARITY.md, data layer).")
                     if shuffle:
                         seed = int(getattr(self._env, "trial_seed", 0)) % (2 ** 32)
                         data.order = np.random.RandomState(seed).permutation(len(data))

@@ -477,11 +477,12 @@ def cmd_command_kill(args: argparse.Namespace) -> None:
     MasterClient(args.master).post(f"/commands/{args.command_id}/kill")
 
 
-def _start_task(client: MasterClient, kind: str, argv: List[str], env: List[str], slots: int,
+def _start_task(client: MasterClient, kind: str, argv: List[str], secret_env: List[str], slots: int,
                 description: str, wait: float) -> int:
-    cfg = {"entrypoint": argv, "type": kind, "resources": {"slots": slots}, "description": description,
-           "environment": {"environment_variables": env}}
-    cid = client.post("/commands", {"config": cfg, "context": []})["id"]
+    """Start a command task; ``secret_env`` ("K=V") reaches only the container's environment -- the
+    master keeps it out of the stored config that GET /commands returns."""
+    cfg = {"entrypoint": argv, "type": kind, "resources": {"slots": slots}, "description": description}
+    cid = client.post("/commands", {"config": cfg, "context": [], "secret_environment": secret_env})["id"]
     deadline = time.time() + wait
     while time.time() < deadline:
         c = client.get(f"/commands/{cid}")

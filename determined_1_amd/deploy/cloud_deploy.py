@@ -14,7 +14,18 @@ from typing import Any, Dict, List
 from determined_1_amd.deploy.cloud_provider import AWSProvider, GCPProvider, STATE
 
 
+# Credentials the deploying user passed for THIS client; they must never be rendered into the master
+# VM's user-data / startup-script (readable through instance metadata and DescribeInstanceAttribute).
+# The master VM authenticates with its instance profile (AWS) or service account (GCP) instead.
+SECRET_KEYS = ("access_key", "secret_key", "session_token", "token")
+
+
+def _strip_secrets(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    return {k: v for k, v in cfg.items() if k not in SECRET_KEYS}
+
+
 def master_script(args: argparse.Namespace, provider_cfg: Dict[str, Any]) -> str:
+    provider_cfg = _strip_secrets(provider_cfg)
     prov = {"provider": args.provider, "max_instances": args.max_agents, "slots_per_instance": args.slots_per_agent,
             "max_idle_agent_period_ms": args.max_idle_agent_period_ms, args.provider: provider_cfg}
     cfg = {"port": args.master_port, "store_dir": args.store_dir, "provisioner": prov,
@@ -33,7 +44,7 @@ class AWSDeployment(AWSProvider):
         self.args = args
 
     def up(self) -> List[str]:
-        agent_cfg = dict(self.cfg)
+        agent_cfg = _strip_secrets(self.cfg)
         agent_cfg.pop("tag_value", None)
         agent_cfg["tag_key"] = "determined-resource-pool"
         agent_cfg["cluster_id"] = self.args.cluster_id
@@ -57,7 +68,7 @@ class GCPDeployment(GCPProvider):
         self.args = args
 
     def up(self) -> List[str]:
-        agent_cfg = dict(self.cfg)
+        agent_cfg = _strip_secrets(self.cfg)
         agent_cfg.pop("label_value", None)
         agent_cfg["cluster_id"] = self.args.cluster_id
         self.script = master_script(self.args, agent_cfg)

@@ -62,12 +62,32 @@ class AWSProvider:
         self.ak = cfg.get("access_key") or os.environ.get("AWS_ACCESS_KEY_ID", "")
         self.sk = cfg.get("secret_key") or os.environ.get("AWS_SECRET_ACCESS_KEY", "")
         self.token = cfg.get("session_token") or os.environ.get("AWS_SESSION_TOKEN")
+        # no static keys (the deployed master VM): the instance profile's rotating credentials from the
+        # instance metadata service, refreshed ahead of their expiry
+        self._imds = None if self.ak else (cfg.get("instance_metadata_url") or "http://169.254.169.254").rstrip("/")
+        self._creds_expire = 0.0
         self.tag_key = cfg.get("tag_key", "determined-resource-pool")
         self.tag_value = cfg.get("tag_value") or f"{cfg.get('cluster_id', 'det')}-{pool}"
         self.user_data = startup_script(cfg, pool, master_host, master_port,
                                         "curl -s http://169.254.169.254/latest/meta-data/instance-id")
 
+    def _refresh_instance_credentials(self) -> None:
+        """IMDSv2: session token, then the role's temporary credentials (AccessKeyId/SecretAccessKey/Token)."""
+        import time
+
+        if self._imds is None or time.time() < self._creds_expire:
+            return
+        t = requests.put(f"{self._imds}/latest/api/token", headers={"X-aws-ec2-metadata-token-ttl-seconds": "300"},
+                         timeout=5)
+        h = {"X-aws-ec2-metadata-token": t.text} if t.status_code == 200 else {}
+        base = f"{self._imds}/latest/meta-data/iam/security-credentials/"
+        role = requests.get(base, headers=h, timeout=5).text.strip().splitlines()[0]
+        c = requests.get(base + role, headers=h, timeout=5).json()
+        self.ak, self.sk, self.token = c["AccessKeyId"], c["SecretAccessKey"], c.get("Token") or None
+        self._creds_expire = time.time() + 600  # re-read well inside the credentials' hour-long lifetime
+
     def _call(self, params: Dict[str, str]) -> ET.Element:
+        self._refresh_instance_credentials()
         params = dict(params, Version=self.VERSION)
         body = urllib.parse.urlencode(sorted(params.items())).encode()
         h = sigv4_headers("POST", self.endpoint, self.region, self.ak, self.sk, _sha256(body), self.token,

@@ -48,7 +48,10 @@ def sigv4_headers(method: str, url: str, region: str, access_key: str, secret_ke
     date = amz_date[:8]
     u = urllib.parse.urlsplit(url)
     host = u.netloc
-    canon_uri = urllib.parse.quote(u.path or "/", safe="/~-_.")
+    # S3 canonical URI = the path URI-encoded ONCE (RFC 3986 unreserved kept, '/' kept).  ``url`` comes
+    # from ``_url`` already encoded, so normalise through unquote (a second quote would turn '%3D'
+    # into '%253D' and every key with '=', '+' or a space would fail SignatureDoesNotMatch).
+    canon_uri = urllib.parse.quote(urllib.parse.unquote(u.path or "/"), safe="/~-_.")
     q = urllib.parse.parse_qsl(u.query, keep_blank_values=True)
     canon_q = "&".join(f"{urllib.parse.quote(k, safe='~-_.')}={urllib.parse.quote(v, safe='~-_.')}"
                        for k, v in sorted(q))

@@ -204,7 +204,9 @@ struct ServiceReady {  // a command's HTTP service is listening (POST /commands/
 };
 class CommandActor : public actor::Actor {
  public:
-  CommandActor(Master* m, int64_t id, Json config);
+  // secret_env: "K=V" entries (e.g. DET_SHELL_TOKEN) handed to the container's environment only;
+  // never written to the store, so no API response can return them.
+  CommandActor(Master* m, int64_t id, Json config, Json secret_env = Json::array());
   void Receive(actor::Context& ctx) override;
 
  private:
@@ -212,6 +214,7 @@ class CommandActor : public actor::Actor {
   Master* m_;
   int64_t id_;
   Json config_;
+  Json secret_env_;
   std::string pool_;
   std::string task_id_;
   std::string container_;

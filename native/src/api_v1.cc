@@ -1366,6 +1366,7 @@ void Master::InstallApiV1() {
       Json legacy = Json::object();
       legacy["config"] = cfg;
       legacy["context"] = body.has("files") ? body["files"] : Json::array();
+      if (body["secretEnvironment"].is_array()) legacy["secret_environment"] = body["secretEnvironment"];
       auto res = call(r, "POST", "/commands", legacy.dump());
       Json j;
       if (!unwrap(res, &j)) return relay_err(res);

@@ -896,7 +896,10 @@ void Master::InstallRoutes() {
     Json ctxrow = Json::object();
     ctxrow["files"] = body["context"].is_array() ? body["context"] : Json::array();
     store_->Put("command_contexts", id, ctxrow);
-    sys_->ActorOf("commands/" + std::to_string(id), std::make_unique<CommandActor>(this, id, cfg));
+    // Secrets (task auth tokens) travel beside the config, not in it: the stored row -- and with it
+    // every GET /commands and /api/v1/{shells,notebooks,...} response -- never holds them.
+    Json secret = body["secret_environment"].is_array() ? body["secret_environment"] : Json::array();
+    sys_->ActorOf("commands/" + std::to_string(id), std::make_unique<CommandActor>(this, id, cfg, secret));
     Json out = Json::object();
     out["id"] = id;
     return J(201, out);

@@ -1049,7 +1049,8 @@ void ProvisionerActor::Receive(Context& ctx) {
 }
 
 // =================================================================================== command
-CommandActor::CommandActor(Master* m, int64_t id, Json config) : m_(m), id_(id), config_(std::move(config)) {
+CommandActor::CommandActor(Master* m, int64_t id, Json config, Json secret_env)
+    : m_(m), id_(id), config_(std::move(config)), secret_env_(std::move(secret_env)) {
   pool_ = config_["resources"].get_string("resource_pool", "");
   if (pool_.empty()) pool_ = m_->config().resource_pools.empty() ? "default" : m_->config().resource_pools[0];
 }
@@ -1087,13 +1088,13 @@ void CommandActor::Receive(Context& ctx) {
     Json env = Json::object();
     env["DET_TASK_ID"] = task_id_;
     env["DET_MASTER"] = m_->master_host() + ":" + std::to_string(m_->port());
-    const Json& ev = config_["environment"]["environment_variables"];
-    if (ev.is_array())
-      for (auto& kv : ev.as_array()) {
-        const std::string& str = kv.as_string();
-        auto eq = str.find('=');
-        if (eq != std::string::npos) env[str.substr(0, eq)] = str.substr(eq + 1);
-      }
+    for (const Json* ev : {&config_["environment"]["environment_variables"], &secret_env_})
+      if (ev->is_array())
+        for (auto& kv : ev->as_array()) {
+          const std::string& str = kv.as_string();
+          auto eq = str.find('=');
+          if (eq != std::string::npos) env[str.substr(0, eq)] = str.substr(eq + 1);
+        }
     Json spec = Json::object();
     spec["env"] = env;
     spec["files"] = Json::array();

@@ -38,6 +38,7 @@ class FakeEC2:
     def __init__(self, workdir):
         self.instances = {}  # id -> {"state", "tags", "proc"}
         self.calls = []
+        self.imds_reads = 0
         self.workdir = workdir
         ec2 = self
 
@@ -57,13 +58,30 @@ class FakeEC2:
                 now = datetime.datetime.strptime(self.headers["x-amz-date"], "%Y%m%dT%H%M%SZ").replace(
                     tzinfo=datetime.timezone.utc)
                 want = sigv4_headers("POST", f"http://{self.headers['Host']}{self.path}", m.group(2) if m else "x",
-                                     AK, SK, _sha256(body), service="ec2", now=now,
+                                     AK, SK, _sha256(body), self.headers.get("x-amz-security-token"),
+                                     service="ec2", now=now,
                                      extra={"content-type": self.headers["Content-Type"]})
                 if not m or want["Authorization"] != auth:
                     return self._send(403, "<Response><Errors><Error><Code>AuthFailure</Code></Error></Errors></Response>")
                 q = dict(urllib.parse.parse_qsl(body.decode()))
                 ec2.calls.append(q["Action"])
                 self._send(200, getattr(ec2, q["Action"])(q))
+
+            # instance metadata service (IMDSv2) of the fake "VM": the instance profile's credentials
+            def do_PUT(self):
+                self._send(200, "imds-session") if self.path == "/latest/api/token" else self._send(404, "")
+
+            def do_GET(self):
+                if self.headers.get("X-aws-ec2-metadata-token") != "imds-session":
+                    return self._send(401, "")
+                base = "/latest/meta-data/iam/security-credentials/"
+                if self.path == base:
+                    return self._send(200, "det-master-role")
+                if self.path == base + "det-master-role":
+                    ec2.imds_reads += 1
+                    return self._send(200, json.dumps({"AccessKeyId": AK, "SecretAccessKey": SK,
+                                                       "Token": "session-tok"}))
+                self._send(404, "")
 
             def _send(self, code, text):
                 b = text.encode()
@@ -237,6 +255,7 @@ def test_det_deploy_aws_up_runs_experiment_and_down(tmp_path):
     ec2 = FakeEC2(str(tmp_path))
     port = free_port()
     prov_cfg = {"endpoint_url": ec2.url, "region": "us-west-2", "access_key": AK, "secret_key": SK,
+                "instance_metadata_url": ec2.url,
                 "image_id": "ami-mi355x", "agent_command": native_binary("det-agent"),
                 "agent_args": ["--artificial-slots", "1", "--python", sys.executable, "--work-dir",
                                str(tmp_path / "agentwork"), "--framework-root", REPO]}
@@ -268,9 +287,28 @@ def test_det_deploy_aws_up_runs_experiment_and_down(tmp_path):
         assert cl.wait_for_experiment(eid, timeout=180) == "COMPLETED"
         agents = [i for i, d in ec2.instances.items() if d["tags"].get("determined-resource-pool") == "c1-default"]
         assert len(agents) == 1
+        assert ec2.imds_reads >= 1  # the master signed with its instance-profile credentials
         r = subprocess.run(base + ["down"] + common, capture_output=True, text=True, timeout=60)
         assert r.returncode == 0, r.stderr
         assert set(json.loads(r.stdout)["terminated"]) >= set(masters)
         assert all(d["state"] == "terminated" for d in ec2.instances.values())
     finally:
         ec2.close()
+
+
+def test_deploy_master_script_never_embeds_credentials():
+    """--provider-config credentials stay with the deploying client; the master VM's
+    user-data (readable via instance metadata) carries none of them."""
+    import argparse
+
+    from determined_1_amd.deploy import cloud_deploy
+
+    args = argparse.Namespace(provider="aws", max_agents=2, slots_per_agent=8, max_idle_agent_period_ms=1000,
+                              master_port=8080, store_dir="/var/det", checkpoint_storage='{"type": "shared_fs"}',
+                              startup_script="", master_command="det-master", cluster_id="c1")
+    cfg = {"region": "us-east-1", "access_key": "AKIDSECRET1", "secret_key": "SKSECRET2",
+           "session_token": "STSECRET3", "image_id": "ami-1"}
+    script = cloud_deploy.master_script(args, cfg)
+    for secret in ("AKIDSECRET1", "SKSECRET2", "STSECRET3"):
+        assert secret not in script
+    assert "ami-1" in script and "us-east-1" in script

@@ -184,3 +184,41 @@ def test_s3_data_layer_shares_cache_across_nodes(tmp_path):
         assert (tmp_path / "b" / "sq" / "v3_train" / "meta.json").exists()
     finally:
         srv.close()
+
+
+def test_s3_data_layer_concurrent_same_node_readers(tmp_path):
+    """Several ranks of one node miss the local cache at once: the download happens once,
+    under the exclusive lock; no rank fails on the rename."""
+    import threading
+
+    from determined_1_amd.pytorch import PyTorchTrialContext
+    from tests.test_storage_rest import AK, SK, S3Handler, _Server
+
+    srv = _Server(S3Handler)
+    srv.parts, srv.multipart_completed = {}, 0
+    try:
+        cfg = {"hyperparameters": {"global_batch_size": 4},
+               "data_layer": {"type": "s3", "bucket": "dl", "bucket_directory_path": "cache",
+                              "local_cache_path": str(tmp_path / "seed"), "access_key": AK, "secret_key": SK,
+                              "endpoint_url": srv.url}}
+        PyTorchTrialContext.from_config(cfg).experimental.cache_train_dataset("sq", "v4")(Squares)()
+        cfg["data_layer"]["local_cache_path"] = str(tmp_path / "node")
+        errors, sizes = [], []
+
+        def rank():
+            try:
+                ctx = PyTorchTrialContext.from_config(cfg)
+                sizes.append(len(ctx.experimental.cache_train_dataset("sq", "v4")(Squares)()))
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ts = [threading.Thread(target=rank) for _ in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not errors, errors
+        assert sizes == [10] * 6
+        assert not [p for p in (tmp_path / "node" / "sq").iterdir() if p.name.startswith(".tmp_")]
+    finally:
+        srv.close()

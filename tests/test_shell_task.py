@@ -52,3 +52,25 @@ def test_notebook_without_jupyter_fails_loudly(cluster, tmp_path):
     assert r.returncode != 0 and "neither jupyter_server nor notebook is installed" in r.stderr
     rows = MasterClient(cluster.address).get("/commands", type="notebook")
     assert rows and rows[-1]["state"] == "TERMINATED"
+
+
+def test_shell_token_never_returned_by_the_api(cluster, tmp_path):
+    """The per-shell token reaches only the task's environment: no command/shell listing returns it
+    (it used to sit in environment.environment_variables of the stored config)."""
+    r = _det(cluster, tmp_path, "shell", "start", "-d")
+    assert r.returncode == 0, r.stderr
+    sid = int(re.search(r"Shell (\d+) ready", r.stderr).group(1))
+    import json
+
+    token_file = tmp_path / ".det-mi355x" / ("shells-" + cluster.address.replace(":", "_") + ".json")
+    token = json.loads(token_file.read_text())[str(sid)]
+    client = MasterClient(cluster.address)
+    bodies = [client.get("/commands"), client.get(f"/commands/{sid}"),
+              requests.get(f"http://{cluster.address}/api/v1/shells", timeout=10).text,
+              requests.get(f"http://{cluster.address}/api/v1/shells/{sid}", timeout=10).text]
+    for b in bodies:
+        assert token not in (b if isinstance(b, str) else json.dumps(b))
+    # ... and the shell still authenticates with it
+    ok = requests.get(f"http://{cluster.address}/proxy/cmd-{sid}/status", params={"token": token}, timeout=10)
+    assert ok.status_code == 200, ok.text
+    client.post(f"/commands/{sid}/kill")
