@@ -91,11 +91,11 @@ def self_launch(args: argparse.Namespace) -> int:
     n = args.gpus
     port = _free_port()
     base = dict(os.environ)
-    miopen_db.configure(base)
     procs = []
     for r in range(n):
         env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DET_BENCH_CHILD="1")
+        miopen_db.configure(env)  # a db copy per rank (ranks never share a writable MIOpen db)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
                                       start_new_session=True))
@@ -158,6 +158,10 @@ def main() -> None:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if os.environ.get("DET_BENCH_CHILD") != "1":
         _miopen_db().configure(os.environ)
+    if world > 1:
+        # phase timers (forward / backward / exposed comm / optimizer) on every multi-GPU run: DP
+        # steps are never hipGraph-captured, so the events add no synchronisation to the path
+        os.environ.setdefault("DET_STEP_TIMERS", "1")
     import torch
 
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
@@ -241,7 +245,8 @@ def main() -> None:
     import torch.distributed as tdist
 
     seen = (tdist.get_world_size(), tdist.get_backend()) if tdist.is_initialized() else (1, None)
-    per_rank = pdist.allgather_object((elapsed, warmup_s, seen[0], seen[1]))
+    phases = getattr(ctrl, "last_step_timers", None) or {}
+    per_rank = pdist.allgather_object((elapsed, warmup_s, seen[0], seen[1], phases))
     t = max(e[0] for e in per_rank)
     value = args.steps * gbs / t
     loss = None
@@ -285,9 +290,15 @@ def main() -> None:
                 "miopen_find_db": os.environ.get("MIOPEN_USER_DB_PATH"),
             },
         }
-        phases = getattr(ctrl, "last_step_timers", None)
         if phases:  # DET_STEP_TIMERS=1: per-batch device phases of the timed window (forward/backward/comm/opt)
             out["config"]["phase_ms"] = {k.split("/", 1)[1]: round(v, 3) for k, v in phases.items()}
+        if world > 1:
+            steps_ms = [1000.0 * e[0] / args.steps for e in per_rank]
+            out["config"]["rank_ms_per_step"] = [round(x, 3) for x in steps_ms]
+            out["config"]["rank_skew_pct"] = round(100.0 * (max(steps_ms) - min(steps_ms)) / max(steps_ms), 2)
+            exposed = [e[4].get("timer/comm_exposed_ms") for e in per_rank if e[4]]
+            if exposed:
+                out["config"]["rank_comm_exposed_ms"] = [round(x, 3) for x in exposed]
         print(json.dumps(out), flush=True)
     pdist.shutdown()
 

@@ -285,8 +285,8 @@ def validate_experiment_config(cfg: Dict[str, Any], require_entrypoint: bool = T
     opt = cfg.get("optimizations", {})
     if opt.get("aggregation_frequency", 1) < 1:
         errs.append("aggregation_frequency must be >= 1")
-    if opt.get("grad_reduction", "fp32_accum") not in ("fp32_accum", "allreduce"):
-        errs.append("optimizations.grad_reduction must be fp32_accum or allreduce")
+    if opt.get("grad_reduction", "fp32_accum") not in ("fp32_accum", "allreduce", "auto"):
+        errs.append("optimizations.grad_reduction must be fp32_accum, allreduce or auto")
     if not isinstance(opt.get("rccl", {}) or {}, dict):
         errs.append("optimizations.rccl must be a mapping")
     if opt.get("mixed_precision", "O0") not in ("O0", "O1", "O2", "O3"):

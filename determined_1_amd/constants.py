@@ -45,3 +45,6 @@ SHARED_FS_CONTAINER_PATH = "/determined_shared_fs"
 
 # Context packaging limit (common/determined_common/constants.py:5-18).
 MAX_CONTEXT_SIZE = 95 * 1024 * 1024
+
+# tensor-fusion autotune CSV (reference HOROVOD_AUTOTUNE_LOG_FILEPATH)
+FUSION_AUTOTUNE_LOG_FILEPATH = "/tmp/autotune_log.csv"

@@ -73,6 +73,8 @@ struct IgArgs {
   int64_t M;
   int N, K, Cin;
   int Hi, Wi, Ho, Wo, stride, pad, S;
+  int R;
+  int64_t x_bytes;  // X extent for the buffer resource (v2 fetch; < 2^31)
 };
 
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
@@ -294,6 +296,256 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// v2: the same LDS-DMA ring, with the fragment reads software-pipelined against the MFMAs.
+//
+// v1 issues all of a K tile's 16 fragment reads and then all 32 MFMAs, and every wave of the block
+// meets at one barrier per K tile, so the whole CU alternates between an LDS-read phase (matrix pipe
+// idle) and an MFMA phase (LDS idle).  v2 keeps two fragment register sets, one per 32-deep k half:
+//
+//   read F1 = half 1 of tile kt      || MFMAs on F0 (half 0 of tile kt, read last iteration)
+//   wait tile kt+1 (counted vmcnt), barrier, issue tile kt+NS-1 into the buffer tile kt-1 vacated
+//   read F0 = half 0 of tile kt+1    || MFMAs on F1
+//
+// so every ds_read burst has an independent MFMA cluster beside it (s_setprio(1) around the
+// clusters, cdna_hip_programming.md T5).  WAR on the ring: tile kt-1's fragments were all consumed
+// by MFMAs issued before this iteration's barrier, so every wave is past its reads of that buffer.
+// RAW: each wave's vmcnt retires its own DMAs of tile kt+1 and the barrier publishes all waves'.
+// ------------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int NS, bool DENSE, bool STATS, int OCC>
+__global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
+  constexpr int NW = WM * WN, kThreads = NW * 64;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);
+  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile rows split evenly over the waves");
+  static_assert(NS >= 3, "the prefetch distance needs >= 3 ring stages");
+  constexpr int NI = AI + BI;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int LDC = BN + 16;
+  static_assert(BM * LDC * 2 + 4 * WM * BN <= NS * STAGE, "C tile + stats scratch fit in the ring");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);  // [WM][BN], after the C tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = a.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int64_t m0 = static_cast<int64_t>(mt) * BM;
+  const int n0 = nt * BN;
+  const int64_t K = a.K;
+  const int lrow = lane >> 3;
+  const int gch = (lane & 7) ^ lrow;
+
+  // Operand fetch through buffer_load ... lds (raw buffer resources, 32-bit offsets): per A row the
+  // byte offset of its top-left input pixel (may be negative: padding) and a bitmask of the R*S
+  // taps that land inside the image; per K tile the tap offset is a wave-uniform scalar, so each
+  // A fetch costs an add, a bit test and a select, and an invalid tap or a row past M fetches at
+  // an out-of-range offset, which the buffer unit returns as zeros (no zero page, no branches).
+  // B offsets are fixed per lane; the K advance rides in the scalar soffset.
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(a.X), 0, static_cast<int>(a.x_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(a.W), 0, static_cast<int>(static_cast<int64_t>(a.N) * K * 2), 0x00020000);
+  constexpr unsigned kOOB = 0xFFFFFFF0u;
+  int aoff[AI];
+  unsigned amask[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (i * NW + wid) * 8 + lrow;
+    const int64_t m = m0 + row;
+    aoff[i] = 0;
+    amask[i] = 0;
+    if (m < a.M) {
+      const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
+      const int64_t n = m / hw;
+      const int rem = static_cast<int>(m - n * hw);
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
+      aoff[i] = static_cast<int>(((n * a.Hi + hi0) * a.Wi + wi0) * a.Cin * 2 + gch * 16);
+      for (int r = 0; r < a.R; ++r)
+        for (int s2 = 0; s2 < a.S; ++s2) {
+          const int hi = hi0 + r, wi = wi0 + s2;
+          if (hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi) amask[i] |= 1u << (r * a.S + s2);
+        }
+    }
+  }
+  unsigned boff[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j)
+    boff[j] = static_cast<unsigned>(((static_cast<int64_t>(n0) + (j * NW + wid) * 8 + lrow) * K + gch * 8) * 2);
+
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NS) * STAGE;
+    const int k0 = kt * kBK;
+    const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
+    const int r = tap / a.S, s2 = tap - r * a.S;
+    const int toff = ((r * a.Wi + s2) * a.Cin + c0) * 2;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const unsigned v = ((amask[i] >> tap) & 1u) ? static_cast<unsigned>(aoff[i] + toff) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(st + ((i * NW + wid) * 8) * 128), 16, v, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(st + A_BYTES + ((j * NW + wid) * 8) * 128), 16, boff[j],
+                                               k0 * 2, 0, 0);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  auto read_half = [&](const unsigned char* base, int ks, bf16x8* af, bf16x8* bfr) {
+    const int ch = ks * 4 + (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(base + swz(wm * TM + i * 16 + (lane & 15), ch));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+  };
+  auto mfma_half = [&](const bf16x8* af, const bf16x8* bfr) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = a.K / kBK;
+  // prologue: NS-1 tiles in flight, wait for tile 0
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
+  if (nk >= NS - 1) wait_vmcnt<NI * (NS - 2)>();
+  else wait_vmcnt<0>();
+  block_barrier();
+  read_half(smem, 0, a0, b0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // loop entry with nothing pending on lgkm (see the loop tail)
+  // every iteration but the last, with no data-dependent join between a read burst and the MFMA
+  // cluster that consumes the burst before it (a join makes the waitcnt pass fall back to lgkmcnt(0))
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    read_half(smem + (kt % NS) * STAGE, 1, a1, b1);
+    mfma_half(a0, b0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // F1 landed under the F0 cluster: nothing pending past here
+    // tiles issued so far: 0 .. min(nk-1, kt+NS-2); tile kt+1 must land, the younger may fly
+    if (kt + NS - 2 < nk) wait_vmcnt<NI * (NS - 3)>();
+    else wait_vmcnt<0>();
+    block_barrier();
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);
+    read_half(smem + ((kt + 1) % NS) * STAGE, 0, a0, b0);
+    mfma_half(a1, b1);
+    // retire F0's reads (they ran under the F1 cluster) with a real S_WAITCNT the waitcnt pass sees:
+    // otherwise it merges the back edge conservatively and puts lgkmcnt(0) AFTER the next F1 reads,
+    // i.e. in front of the F0 MFMAs, serialising every read burst with its cluster
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched
+  }
+  read_half(smem + ((nk - 1) % NS) * STAGE, 1, a1, b1);
+  mfma_half(a0, b0);
+  mfma_half(a1, b1);
+  __syncthreads();  // every wave's last fragment reads are done before the ring holds the C tile
+
+  unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
+  const int64_t rows_left = a.M - m0;
+  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * TN + j * 16 + (lane & 15);
+        ct[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  if (STATS) {
+    float cs[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (row < nvalid) s += round_bf(acc[i][j][r]);
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      cs[j] = s;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + j * 16 + lane] = cs[j];
+    }
+    __syncthreads();
+    const float inv_n = 1.f / static_cast<float>(nvalid);
+    float mu[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * TN + j * 16 + (lane & 15);
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += red[w * BN + col];
+      mu[j] = s * inv_n;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          const float d = round_bf(acc[i][j][r]) - mu[j];
+          if (row < nvalid) q += d * d;
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) red[wm * BN + wn * TN + j * 16 + lane] = q;
+      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
+    }
+  }
+  __syncthreads();
+  if (STATS && tid < BN) {
+    float q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
+    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
+  }
+  constexpr int CPR = BN / 8;
+#pragma unroll
+  for (int q = 0; q < (BM * CPR + kThreads - 1) / kThreads; ++q) {
+    const int idx = tid + q * kThreads;
+    const int row = idx / CPR, cc = idx - row * CPR;
+    if (idx < BM * CPR && row < nvalid)
+      *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+  }
+#endif
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int OCC>
+int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+  constexpr int kThreads = WM * WN * 64;
+  if (a.N % BN != 0) return -6;
+  const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
+  constexpr int smem = NS * (BM + BN) * 128;
+#define DET_IG2(D, S)                                                                                          \
+  hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, NS, D, S, OCC>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), \
+                     smem, st, a)
+  (void)dense;  // the tap-mask fetch covers 1x1 / strided / padded alike
+  if (stats) DET_IG2(false, true); else DET_IG2(false, false);
+#undef DET_IG2
+  return static_cast<int>(hipGetLastError());
+}
+
 template <int BM, int BN, int WM, int WN>
 int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
   constexpr int kThreads = WM * WN * 64;
@@ -308,19 +560,57 @@ int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
   return static_cast<int>(hipGetLastError());
 }
 
+// Tile configurations (det_igemm_conv_cfg): 0 = automatic; 1 = v1 (256 x BN, 8 waves); 2..7 = v2:
+//   2: 256x128, 8 waves (4x2, 64x64 wave tiles), 3-stage ring (144 KiB), 1 block/CU
+//   3: 256x64,  4 waves (4x1, 64x64), 3 stages (120 KiB)
+//   4: 128x128, 4 waves (2x2, 64x64), 4 stages (128 KiB)
+//   5: 256x64,  8 waves (8x1, 32x64), 3 stages (120 KiB)
+//   6: 128x64,  4 waves (2x2, 64x32), 3 stages (72 KiB), 2 blocks/CU
+//   7: 128x128, 4 waves (2x2, 64x64), 3 stages (96 KiB)
+static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+  switch (cfg) {
+    case 1:
+      if (a.N % 128 == 0) return launch<256, 128, 4, 2>(st, a, dense, stats);
+      return launch<256, 64, 8, 1>(st, a, dense, stats);
+    case 2: return launch2<256, 128, 4, 2, 3, 1>(st, a, dense, stats);
+    case 3: return launch2<256, 64, 4, 1, 3, 1>(st, a, dense, stats);
+    case 4: return launch2<128, 128, 2, 2, 4, 1>(st, a, dense, stats);
+    case 5: return launch2<256, 64, 8, 1, 3, 1>(st, a, dense, stats);
+    case 6: return launch2<128, 64, 2, 2, 3, 2>(st, a, dense, stats);
+    case 7: return launch2<128, 128, 2, 2, 3, 1>(st, a, dense, stats);
+    default: return -7;
+  }
+}
+
+static int auto_cfg(const IgArgs& a) {
+  static const int forced = [] {
+    const char* e = std::getenv("DET_IGEMM_CFG");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0) return forced;
+  return a.N % 128 == 0 ? 2 : 3;
+}
+
 }  // namespace
 
 extern "C" {
 
-// Rows per statistics block of det_igemm (the BN finalize needs it).
+// Rows per statistics block of det_igemm for configuration cfg (0 = the automatic choice for N).
+int det_igemm_rows_per_block_cfg(int N, int cfg) {
+  IgArgs a{};
+  a.N = N;
+  const int c = cfg > 0 ? cfg : auto_cfg(a);
+  return (c == 4 || c == 6 || c == 7) ? 128 : 256;
+}
 int det_igemm_rows_per_block() { return 256; }
 
 // Y[M, N] = conv(X, W) as described at the top.  bf16 NHWC.  Requirements (checked): Cin % 64 == 0,
 // N % 64 == 0, K == R*S*Cin, pointers 16-B aligned, zero -> >= 128 zero bytes.  R == S == 1,
-// stride 1, pad 0 with Hi*Wi == Ho*Wo takes the dense path.  pmean/pm2 (nullable, [ceil(M/256), N]):
-// BatchNorm statistics partials of the bf16-rounded Y.
-int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,
-                   int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* pmean, float* pm2) {
+// stride 1, pad 0 with Hi*Wi == Ho*Wo takes the dense path.  pmean/pm2 (nullable, [ceil(M/rpb), N],
+// rpb = det_igemm_rows_per_block_cfg(N, cfg)): BatchNorm statistics partials of the bf16-rounded Y.
+int det_igemm_conv_cfg(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,
+                       int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* pmean, float* pm2,
+                       int cfg) {
   if (M <= 0 || N <= 0 || N % 64 != 0 || Cin <= 0 || Cin % 64 != 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
     return -1;
   if ((pmean == nullptr) != (pm2 == nullptr) || zero == nullptr) return -2;
@@ -329,23 +619,22 @@ int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const vo
     return -5;
   const int64_t hw = static_cast<int64_t>(Ho) * Wo;
   if (hw <= 0 || M % hw != 0) return -3;
+  if (Ho != (Hi + 2 * pad - R) / stride + 1 || Wo != (Wi + 2 * pad - S) / stride + 1) return -3;
   const int K = R * S * Cin;
+  const int64_t x_bytes = (M / hw) * Hi * static_cast<int64_t>(Wi) * Cin * 2;
+  if (cfg != 1 && (x_bytes >= (static_cast<int64_t>(1) << 31) || static_cast<int64_t>(N) * K * 2 >= (static_cast<int64_t>(1) << 31)))
+    return -8;  // 32-bit buffer offsets
+  if (R * S > 32) return -1;
   IgArgs a{static_cast<const unsigned short*>(X), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(Y),
-           static_cast<const unsigned short*>(zero), pmean, pm2, M, N, K, Cin, Hi, Wi, Ho, Wo, stride, pad, S};
+           static_cast<const unsigned short*>(zero), pmean, pm2, M, N, K, Cin, Hi, Wi, Ho, Wo, stride, pad, S, R, x_bytes};
   const bool dense = R == 1 && S == 1 && stride == 1 && pad == 0 && Hi == Ho && Wi == Wo;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const bool stats = pmean != nullptr;
-  static const int waves = [] {
-    const char* e = std::getenv("DET_IGEMM_WAVES");
-    return e ? std::atoi(e) : 8;
-  }();
-  if (waves == 4) {  // A/B: one wave per SIMD, 128 x 64 wave tiles (measured ~25 % slower: the
-                     // per-K-step barrier + fragment-read latency is exposed with no partner wave)
-    if (N % 128 == 0) return launch<256, 128, 2, 2>(st, a, dense, stats);
-    return launch<256, 64, 4, 1>(st, a, dense, stats);
-  }
-  if (N % 128 == 0) return launch<256, 128, 4, 2>(st, a, dense, stats);
-  return launch<256, 64, 8, 1>(st, a, dense, stats);
+  return run_cfg(cfg > 0 ? cfg : auto_cfg(a), st, a, dense, pmean != nullptr);
+}
+
+int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,
+                   int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* pmean, float* pm2) {
+  return det_igemm_conv_cfg(stream, X, W, Y, zero, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, pmean, pm2, 1);
 }
 
 }  // extern "C"

@@ -30,13 +30,30 @@ bucket.  Bytes on the wire equal a ring all-reduce: 2 (N-1)/N x bucket.  ``grad_
 allreduce`` selects the plain RCCL all-reduce instead.  fp32 buckets always use the RCCL
 all-reduce.
 
+``grad_reduction: auto`` measures both algorithms on every bucket size of this model at the
+bucketer's construction (a few ms of collectives on scratch buffers, all ranks together), takes
+the MAX over ranks of each timing with one all-reduce -- so every rank holds bit-identical
+numbers and picks the identical per-bucket mode without a broadcast -- and keeps ``fp32_accum``
+(one rounding) unless the RCCL all-reduce is at least ``AUTO_MARGIN`` faster.
+
+Tensor-fusion autotune (``optimizations.auto_tune_tensor_fusion``, reference ``horovod.py:98-103``
+``--autotune --autotune-log-file``): the bucket cap is searched over ``AUTOTUNE_CAPS_MB`` during
+the first aggregation windows.  Each candidate runs ``AUTOTUNE_WINDOWS`` windows (the first is
+discarded); a window's time is the device time from the start of its backward to the end of the
+gradient synchronisation (HIP events).  The decision is taken at a fixed window index on every
+rank from MAX-all-reduced timings, the buckets are re-planned (``replan``; the GradSink groups
+follow through ``replan_listeners``) and every candidate is logged as CSV like Horovod's
+autotune log.  ``tensor_fusion_cycle_time`` has no analogue: buckets launch the moment backward
+completes them (no background cycle), so the key is accepted and ignored with an info line.
+
 RCCL knobs (the analogue of Horovod's fusion/cycle knobs, reference ``horovod.py:92-110``) come
 from ``optimizations.rccl`` and are applied as NCCL_* environment before the communicator is
 created (``apply_rccl_env``).
 """
 import logging
 import os
-from typing import Any, Dict, List, MutableMapping, Optional, Sequence, Tuple
+import time
+from typing import Any, Callable, Dict, List, MutableMapping, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -47,7 +64,10 @@ from determined_1_amd.ops.functional import scale_cast_, sum_rows_
 MB = 1024 * 1024
 MIN_BUCKET_BYTES = 2 * MB
 TARGET_BUCKETS = 8
-REDUCTIONS = ("fp32_accum", "allreduce")
+REDUCTIONS = ("fp32_accum", "allreduce", "auto")
+AUTO_MARGIN = 0.10  # auto keeps fp32_accum unless the all-reduce is >= 10 % faster
+AUTOTUNE_CAPS_MB = (0.5, 1, 2, 4, 8, 16, 32, 64, 128)
+AUTOTUNE_WINDOWS = 3  # per candidate; the first is warmup
 
 
 def auto_bucket_cap(total_bytes: int, threshold_bytes: int) -> int:
@@ -141,6 +161,8 @@ class GradientBucketer:
         group: Any = None,
         reduction: str = "fp32_accum",
         rank: Optional[int] = None,
+        autotune: bool = False,
+        autotune_log: Optional[str] = None,
     ) -> None:
         if reduction not in REDUCTIONS:
             raise ValueError(f"grad_reduction must be one of {REDUCTIONS}, got {reduction!r}")
@@ -149,35 +171,106 @@ class GradientBucketer:
         self.rank = dist.get_rank(group) if rank is None and dist.is_initialized() else (rank or 0)
         self.group = group
         self.compression = compression
-        total = sum(a.numel * a.flat_grad.element_size() for a in self.arenas)
-        self.cap_bytes = auto_bucket_cap(total, int(cap_mb * MB))
-        self.buckets = plan_buckets(self.arenas, self.cap_bytes)
+        self.reduction = reduction
+        self.total_bytes = sum(a.numel * a.flat_grad.element_size() for a in self.arenas)
+        self.threshold_bytes = int(cap_mb * MB)
+        self.auto_choice = {}  # type: Dict[int, Dict[str, Any]]  # bucket numel -> timings + mode
+        self.replan_listeners = []  # type: List[Callable[["GradientBucketer"], None]]
         self._side = None  # type: Any
+        self._handles = []  # type: List[Any]
+        self._sink = None  # type: Any
+        self._comm = False
+        self._launched_any = False
+        self._plan(auto_bucket_cap(self.total_bytes, self.threshold_bytes))
+        for a in self.arenas:
+            for p in a.params:
+                self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
+        self._tuner = _FusionAutotuner(self, autotune_log) if autotune else None
+
+    # ------------------------------------------------------------------------------------------
+    def _wire_dtype(self, b: _Bucket) -> torch.dtype:
+        return self.compression if self.compression is not None else b.arena.flat_grad.dtype
+
+    def _plan(self, cap_bytes: int) -> None:
+        """(Re)build the bucket list for ``cap_bytes`` and pick each bucket's reduction."""
+        self.cap_bytes = int(cap_bytes)
+        self.buckets = plan_buckets(self.arenas, self.cap_bytes)
+        if self.reduction == "auto":
+            self._calibrate()
+        downgraded = []
         for b in self.buckets:
-            if compression is not None:
-                b.comp = torch.empty(b.hi - b.lo, dtype=compression, device=b.arena.device)
-            wire_dtype = compression if compression is not None else b.arena.flat_grad.dtype
+            if self.compression is not None:
+                b.comp = torch.empty(b.hi - b.lo, dtype=self.compression, device=b.arena.device)
+            wire_dtype = self._wire_dtype(b)
             n = b.hi - b.lo
-            if reduction == "fp32_accum" and wire_dtype in (torch.bfloat16, torch.float16) and n % world_size == 0:
-                b.mode = "fp32_accum"
-                b.recv = torch.empty(n, dtype=wire_dtype, device=b.arena.device)
+            want = self.reduction
+            if want == "auto":
+                want = self.auto_choice.get(n, {}).get("mode", "fp32_accum")
+            if want == "fp32_accum" and wire_dtype in (torch.bfloat16, torch.float16):
+                if n % self.world_size == 0:
+                    b.mode = "fp32_accum"
+                    b.recv = torch.empty(n, dtype=wire_dtype, device=b.arena.device)
+                else:
+                    downgraded.append(n)
+        if downgraded:
+            # 64-element arena alignment keeps 2/4/8 ranks exact; other world sizes can miss
+            logging.warning(
+                "grad_reduction fp32_accum: %d of %d buckets (numel %s) are not divisible by world size %d "
+                "and fall back to a %s ring all-reduce (one rounding per hop)", len(downgraded), len(self.buckets),
+                downgraded[:8], self.world_size, self._wire_dtype(self.buckets[0]))
+        self.downgraded = downgraded
         self._pending = [0] * len(self.buckets)
         self._ready = [False] * len(self.buckets)
         self._next = 0
-        self._comm = False
-        self._launched_any = False
-        self._handles = []
-        self._sink = None  # type: Any
         self._bucket_of = {}  # type: Dict[int, int]
         for bi, b in enumerate(self.buckets):
             for pi in b.params:
                 self._bucket_of[id(b.arena.params[pi])] = bi
-        for a in self.arenas:
-            for p in a.params:
-                self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
         logging.info("gradient bucketer: %d buckets (cap %.1f MB of %.1f MB), reduction=%s, compression=%s",
-                     len(self.buckets), self.cap_bytes / MB, total / MB,
-                     sorted({b.mode for b in self.buckets}), compression)
+                     len(self.buckets), self.cap_bytes / MB, self.total_bytes / MB,
+                     sorted({b.mode for b in self.buckets}), self.compression)
+
+    def replan(self, cap_bytes: int) -> None:
+        """Re-cut the buckets with a new cap between aggregation windows (no collective in flight)."""
+        assert not self._comm, "replan only between aggregation windows"
+        self._plan(cap_bytes)
+        for fn in self.replan_listeners:
+            fn(self)
+
+    def _calibrate(self, iters: int = 4) -> None:
+        """``grad_reduction: auto``: time the RCCL all-reduce against all-to-all + fp32 sum +
+        all-gather on each distinct bucket size (scratch buffers), MAX over ranks, pick per size."""
+        sizes = sorted({b.hi - b.lo for b in self.buckets} - set(self.auto_choice))
+        if not sizes:
+            return
+        dev = self.buckets[0].arena.device
+        dt = self.compression if self.compression is not None else self.buckets[0].arena.flat_grad.dtype
+        if dt not in (torch.bfloat16, torch.float16) or self.world_size == 1:
+            for n in sizes:
+                self.auto_choice[n] = {"mode": "fp32_accum" if dt in (torch.bfloat16, torch.float16) else "allreduce"}
+            return
+        times = []
+        for n in sizes:
+            npad = n - n % self.world_size if n % self.world_size else n
+            buf = torch.randn(n, device=dev).to(dt)
+            recv = torch.empty(npad, dtype=dt, device=dev)
+            times.append(_time_collective(lambda: dist.all_reduce(buf, group=self.group), dev, iters))
+            times.append(_time_collective(lambda: self._fp32_accum_blocking(buf[:npad], recv), dev, iters))
+        t = torch.tensor(times, dtype=torch.float64, device=dev if dev.type == "cuda" else torch.device("cpu"))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        t = t.cpu().tolist()
+        for i, n in enumerate(sizes):
+            ar, fa = t[2 * i], t[2 * i + 1]
+            mode = "allreduce" if ar < (1.0 - AUTO_MARGIN) * fa else "fp32_accum"
+            self.auto_choice[n] = {"mode": mode, "allreduce_ms": round(1e3 * ar, 4), "fp32_accum_ms": round(1e3 * fa, 4)}
+        logging.info("grad_reduction auto: %s", {n: v for n, v in self.auto_choice.items() if n in sizes})
+
+    def _fp32_accum_blocking(self, wire: torch.Tensor, recv: torch.Tensor) -> None:
+        n = wire.numel() // self.world_size
+        shard = wire[self.rank * n:(self.rank + 1) * n]
+        dist.all_to_all_single(recv, wire, group=self.group)
+        sum_rows_(recv, self.world_size, shard)
+        dist.all_gather_into_tensor(wire, shard, group=self.group)
 
     def describe(self) -> List[Dict[str, Any]]:
         return [{"params": len(b.params), "mb": round(b.nbytes / MB, 3), "mode": b.mode} for b in self.buckets]
@@ -203,6 +296,8 @@ class GradientBucketer:
     def prepare_backward(self, communicate: bool) -> None:
         """Called before every backward pass; ``communicate`` says whether this pass ends an
         aggregation window (then buckets are reduced as they complete)."""
+        if communicate and self._tuner is not None:
+            self._tuner.window_start()
         self._comm = communicate
         if self._comm:
             for bi, b in enumerate(self.buckets):
@@ -274,7 +369,101 @@ class GradientBucketer:
         if self._side is not None:
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         self._comm = False
+        if self._tuner is not None:
+            self._tuner.window_end()
         return True
+
+
+def _time_collective(fn: Callable[[], None], dev: torch.device, iters: int) -> float:
+    """Median seconds of ``fn`` (a blocking collective sequence) after one warmup call."""
+    def sync() -> None:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    fn()
+    sync()
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        fn()
+        sync()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+class _FusionAutotuner:
+    """Bucket-cap search over the first aggregation windows (see the module docstring)."""
+
+    def __init__(self, bucketer: GradientBucketer, log_path: Optional[str]) -> None:
+        self.b = bucketer
+        self.log_path = log_path
+        self.caps = [int(c * MB) for c in AUTOTUNE_CAPS_MB if c * MB <= bucketer.total_bytes] or [bucketer.cap_bytes]
+        self.window = 0
+        self.marks = []  # type: List[Tuple[int, Any, Any]]  # (cap, start, end) per window
+        self.cur = None  # type: Any
+        self.done = False
+        self.result = {}  # type: Dict[int, float]
+        if self.caps[0] != bucketer.cap_bytes:
+            bucketer.replan(self.caps[0])
+
+    def _now(self) -> Any:
+        dev = self.b.buckets[0].arena.device
+        if dev.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def window_start(self) -> None:
+        if self.done:
+            return
+        w, per = self.window, AUTOTUNE_WINDOWS
+        if w > 0 and w % per == 0:
+            k = w // per
+            if k >= len(self.caps):
+                self._decide()
+                return
+            self.b.replan(self.caps[k])
+        self.cur = self._now()
+
+    def window_end(self) -> None:
+        if self.done or self.cur is None:
+            return
+        self.marks.append((self.b.cap_bytes, self.cur, self._now()))
+        self.cur = None
+        self.window += 1
+
+    def _decide(self) -> None:
+        """At the same window index on every rank: resolve the timings, MAX over ranks, keep the fastest."""
+        per = {}  # type: Dict[int, List[float]]
+        for i, (cap, t0, t1) in enumerate(self.marks):
+            if i % AUTOTUNE_WINDOWS == 0:
+                continue  # first window of each candidate: re-plan / warmup
+            if isinstance(t0, float):
+                dt = 1e3 * (t1 - t0)
+            else:
+                t1.synchronize()
+                dt = t0.elapsed_time(t1)
+            per.setdefault(cap, []).append(dt)
+        caps = list(self.caps)
+        mean = [sum(per.get(c, [0.0])) / max(1, len(per.get(c, []))) for c in caps]
+        dev = self.b.buckets[0].arena.device
+        t = torch.tensor(mean, dtype=torch.float64, device=dev if dev.type == "cuda" else torch.device("cpu"))
+        if self.b.world_size > 1 and dist.is_initialized():
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.b.group)
+        mean = t.cpu().tolist()
+        self.result = {c / MB: m for c, m in zip(caps, mean)}
+        best = caps[min(range(len(caps)), key=lambda i: mean[i])]
+        logging.info("tensor fusion autotune: window ms by cap MB %s -> %g MB", self.result, best / MB)
+        if self.log_path and self.b.rank == 0:
+            with open(self.log_path, "w") as f:
+                f.write("cap_mb,window_ms,chosen\n")
+                for c, m in zip(caps, mean):
+                    f.write(f"{c / MB:g},{m:.4f},{int(c == best)}\n")
+        self.done = True
+        if best != self.b.cap_bytes:
+            self.b.replan(best)
 
 
 def broadcast_arenas(arenas: Sequence[Arena], src: int = 0, group: Any = None) -> None:

@@ -87,6 +87,13 @@ class DistributedConfig:
             rccl=opt.get("rccl") or {},
         )
 
+    def log_inapplicable(self) -> None:
+        """``tensor_fusion_cycle_time`` is Horovod's background-thread cycle; buckets here launch the
+        moment backward completes them, so a non-default value is accepted and has no effect."""
+        if self.use and self.cycle_time_ms != 5:
+            logging.info("optimizations.tensor_fusion_cycle_time=%s has no effect: gradient buckets are "
+                         "launched as soon as backward completes them (no fusion cycle)", self.cycle_time_ms)
+
     @staticmethod
     def single() -> "DistributedConfig":
         return DistributedConfig(use=False)

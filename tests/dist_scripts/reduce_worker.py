@@ -27,12 +27,20 @@ def main() -> None:
     g = torch.Generator().manual_seed(1234 + rank)
     full = torch.randn(arena.numel, generator=g) * (1.0 + rank)
     arena.flat_grad.copy_(full.to(dtype))
+    autotune = os.environ.get("DET_TEST_AUTOTUNE") == "1"
     b = GradientBucketer([arena], world_size=world, cap_mb=1.0, reduction=reduction,
-                         compression=torch.bfloat16 if compress else None)
-    b.prepare_backward(True)
-    b.synchronize()
+                         compression=torch.bfloat16 if compress else None, autotune=autotune,
+                         autotune_log=f"{out}.autotune.csv" if autotune else None)
+    caps = []
+    windows = int(os.environ.get("DET_TEST_WINDOWS", "1"))
+    for _ in range(windows):
+        arena.flat_grad.copy_(full.to(dtype))
+        b.prepare_backward(True)
+        b.synchronize()
+        caps.append(b.cap_bytes)
     torch.save({"reduced": arena.flat_grad.clone(), "modes": [x.mode for x in b.buckets],
-                "nbuckets": len(b.buckets)}, f"{out}.{rank}.pt")
+                "nbuckets": len(b.buckets), "auto_choice": b.auto_choice, "downgraded": b.downgraded,
+                "caps": caps, "tuned": None if b._tuner is None else b._tuner.result}, f"{out}.{rank}.pt")
     dist.destroy_process_group()
 
 

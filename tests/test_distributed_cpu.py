@@ -97,6 +97,53 @@ def test_bench_self_launch_plain_invocation():
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["config"]["world_size_seen"] == [2, 2] and out["config"]["backend"] == "gloo"
     assert out["config"]["warmup_s"] >= 0 and out["value"] > 0
+    # multi-rank runs always report per-rank step time and skew (first-contact diagnostics)
+    assert len(out["config"]["rank_ms_per_step"]) == 2 and out["config"]["rank_skew_pct"] >= 0
+
+
+def test_bench_collectives_cpu_two_ranks():
+    """scripts/bench_collectives.py self-launches its ranks (gloo here) and prints one line per
+    (size, algorithm) plus the auto-rule summary."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(repo, "scripts", "bench_collectives.py"), "--gpus", "2", "--cpu",
+                        "--sizes-mb", "0.5,1", "--iters", "2"], capture_output=True, text=True, timeout=300, cwd=repo,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    algos = {(x["size_mb"], x["algo"]) for x in recs if "algo" in x}
+    assert algos == {(m, a) for m in (0.5, 1.0) for a in ("allreduce_bf16", "allreduce_fp32", "fp32_accum_bf16")}
+    assert all(x["ms"] > 0 and x["world"] == 2 for x in recs if "algo" in x)
+    summary = [x for x in recs if "summary" in x]
+    assert summary and set(summary[0]["choice_by_mb"].values()) <= {"allreduce", "fp32_accum"}
+
+
+def test_miopen_db_per_rank_and_key_merge(tmp_path, monkeypatch):
+    """Each local rank of a multi-rank job gets its own writable db; seeding merges by key and never
+    overwrites an entry the user already tuned; a changed shipped db is merged in again."""
+    import importlib
+
+    from determined_1_amd.ops import miopen_db
+
+    shipped = tmp_path / "shipped"
+    (shipped / "db").mkdir(parents=True)
+    (shipped / "cache").mkdir()
+    (shipped / "db" / "x.ufdb.txt").write_text("k1=shipped1\nk2=shipped2\n")
+    (shipped / "cache" / "k.ukdb").write_bytes(b"bin")
+    monkeypatch.setattr(miopen_db, "SHIPPED", str(shipped))
+    envs = [{"DET_MIOPEN_DIR": str(tmp_path / "run"), "WORLD_SIZE": "2", "LOCAL_RANK": str(r)} for r in range(2)]
+    dbs = [miopen_db.configure(e) for e in envs]
+    assert dbs[0] != dbs[1] and dbs[0].endswith("rank0/db") and dbs[1].endswith("rank1/db")
+    user = tmp_path / "run" / "rank0" / "db" / "x.ufdb.txt"
+    user.write_text("k1=user_tuned\n")
+    (shipped / "db" / "x.ufdb.txt").write_text("k1=shipped1\nk2=shipped2\nk3=shipped3\n")
+    import os as _os
+    _os.utime(shipped / "db" / "x.ufdb.txt", (1, 1))  # shipped db changed -> new stamp
+    e0 = {"DET_MIOPEN_DIR": str(tmp_path / "run"), "WORLD_SIZE": "2", "LOCAL_RANK": "0"}
+    miopen_db.configure(e0)
+    got = dict(l.split("=", 1) for l in user.read_text().splitlines())
+    assert got == {"k1": "user_tuned", "k2": "shipped2", "k3": "shipped3"}
+    importlib.reload(miopen_db)
 
 
 def test_bench_rejects_mismatched_world():

@@ -25,18 +25,29 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(out: str, world: int, reduction: str, dtype: str = "bfloat16", compress: bool = False) -> list:
+def _run(out: str, world: int, reduction: str, dtype: str = "bfloat16", compress: bool = False,
+         extra_env: dict = None, logs: list = None) -> list:
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   OMP_NUM_THREADS="1")
+                   OMP_NUM_THREADS="1", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, WORKER, out, reduction, dtype, "1" if compress else "0"],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     for p in procs:
         o, _ = p.communicate(timeout=240)
         assert p.returncode == 0, o.decode()[-3000:]
-    return [torch.load(f"{out}.{r}.pt") for r in range(world)]
+        if logs is not None:
+            logs.append(o.decode())
+    return [torch.load(f"{out}.{r}.pt", weights_only=False) for r in range(world)]
+
+
+def _abs_sum(world: int, numel: int, dtype: torch.dtype) -> torch.Tensor:
+    tot = torch.zeros(numel, dtype=torch.float64)
+    for r in range(world):
+        g = torch.Generator().manual_seed(1234 + r)
+        tot += (torch.randn(numel, generator=g) * (1.0 + r)).to(dtype).double().abs()
+    return tot
 
 
 def _exact_sum(world: int, numel: int, dtype: torch.dtype) -> torch.Tensor:
@@ -103,3 +114,51 @@ def test_fp32_arena_uses_allreduce_and_compression_accumulates(tmp_path):
     err = (comp[0]["reduced"].double() - exact).abs()
     # inputs rounded to bf16 once (2^-9 relative each), the fp32 sum rounded once
     assert float((err / exact.abs().clamp_min(1e-3)).median()) < 2.0 ** -7
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_auto_reduction_agrees_across_ranks(tmp_path, world):
+    """grad_reduction: auto times both algorithms collectively; every rank must pick identical
+    per-bucket modes (else the collective sequences diverge and the job hangs)."""
+    res = _run(str(tmp_path / "auto"), world, "auto")
+    choice0 = res[0]["auto_choice"]
+    assert choice0 and all(v["mode"] in ("fp32_accum", "allreduce") for v in choice0.values())
+    assert all("allreduce_ms" in v and "fp32_accum_ms" in v for v in choice0.values())
+    for r in range(1, world):
+        assert res[r]["auto_choice"] == choice0
+        assert res[r]["modes"] == res[0]["modes"]
+        assert torch.equal(res[0]["reduced"], res[r]["reduced"])
+    red = res[0]["reduced"].double()
+    exact = _exact_sum(world, red.numel(), torch.bfloat16)
+    # either algorithm: within a bf16 ring's worst case (world-1 roundings of partial sums)
+    assert bool(((red - exact).abs() <= _abs_sum(world, red.numel(), torch.bfloat16) * world * 2.0 ** -8).all())
+
+
+def test_fp32_accum_downgrade_warns_at_world_3(tmp_path):
+    logs = []
+    res = _run(str(tmp_path / "w3"), 3, "fp32_accum", logs=logs)
+    assert res[0]["downgraded"], "64-element-aligned buckets are not divisible by 3"
+    assert "allreduce" in res[0]["modes"]
+    assert any("fall back to a" in o and "not divisible by world size 3" in o for o in logs), logs[0][-2000:]
+    n = res[0]["reduced"].numel()
+    exact = _exact_sum(3, n, torch.bfloat16)
+    assert bool(((res[0]["reduced"].double() - exact).abs() <= _abs_sum(3, n, torch.bfloat16) * 3 * 2.0 ** -8).all())
+
+
+def test_tensor_fusion_autotune_converges_identically(tmp_path):
+    """auto_tune_tensor_fusion: caps searched over the first windows, decision identical on every
+    rank at the same window, CSV log written by rank 0, reduction still exact afterwards."""
+    from determined_1_amd.parallel import ddp
+
+    windows = len(ddp.AUTOTUNE_CAPS_MB) * ddp.AUTOTUNE_WINDOWS + 3
+    out = str(tmp_path / "tune")
+    res = _run(out, 2, "fp32_accum", extra_env={"DET_TEST_AUTOTUNE": "1", "DET_TEST_WINDOWS": str(windows)})
+    assert res[0]["tuned"] and res[0]["tuned"] == res[1]["tuned"]
+    assert res[0]["caps"] == res[1]["caps"]
+    assert len(set(res[0]["caps"])) >= 2  # the search visited several caps
+    assert res[0]["caps"][-1] == res[0]["caps"][-2]  # settled
+    lines = open(out + ".autotune.csv").read().strip().splitlines()
+    assert lines[0] == "cap_mb,window_ms,chosen" and sum(int(l.split(",")[2]) for l in lines[1:]) == 1
+    exact = _exact_sum(2, res[0]["reduced"].numel(), torch.bfloat16)
+    err = (res[0]["reduced"].double() - exact).abs()
+    assert bool((err <= exact.abs() * 2.0 ** -8 + 1e-30).all())
