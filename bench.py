@@ -52,6 +52,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--no-fused-bn", action="store_true", help="stock MIOpen BN + separate add/ReLU (A/B)")
     ap.add_argument("--no-native-conv1x1", action="store_true", help="1x1 convs on MIOpen instead of det_conv GEMMs (A/B)")
     ap.add_argument("--no-native-stem", action="store_true", help="7x7 stem conv on MIOpen instead of det_conv (A/B)")
+    ap.add_argument("--no-native-conv3x3", action="store_true", help="3x3 convs on MIOpen instead of det_igemm (A/B)")
     ap.add_argument("--bn-prologue", action="store_true",
                     help="apply bottleneck bn2 in conv3's GEMM prologue instead of materialising it (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
@@ -188,6 +189,7 @@ def main() -> None:
             "native_conv1x1": not args.no_native_conv1x1,
             "bn_prologue": args.bn_prologue,
             "native_stem": not args.no_native_stem,
+            "native_conv3x3": not args.no_native_conv3x3,
             "image_size": args.image_size,
         },
         "resources": {"slots_per_trial": world},
@@ -281,6 +283,7 @@ def main() -> None:
                 "native_conv1x1": not args.no_native_conv1x1,
                 "bn_prologue": args.bn_prologue,
                 "native_stem": not args.no_native_stem,
+                "native_conv3x3": not args.no_native_conv3x3,
                 "final_avg_loss": loss,
                 "world_size_seen": [e[2] for e in per_rank],
                 "backend": per_rank[0][3],

@@ -30,6 +30,16 @@ BN_PROLOGUE = False
 # its epilogue (ops.conv.stem_conv; input channels padded to 4); hparam ``native_stem: false``
 # keeps it on MIOpen (A/B).
 NATIVE_STEM = True
+# 3x3 convs on the det_igemm implicit GEMM (forward with the BN statistics in its epilogue, stride-1
+# input gradient through the flipped weight, im2col weight gradient; ops.conv.conv_rs); hparam
+# ``native_conv3x3: false`` keeps them on MIOpen (A/B).
+NATIVE_CONV3X3 = True
+
+
+def c3x3(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    if NATIVE_CONV3X3 and FUSED_BN:
+        return native_conv.conv_rs(x, conv)
+    return conv(x)
 
 
 def c1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
@@ -81,8 +91,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), idt, shortcut_link=self.downsample is None)
+        out = self.bn1(c3x3(x, self.conv1))
+        return self.bn2(c3x3(out, self.conv2), idt, shortcut_link=self.downsample is None)
 
 
 class Bottleneck(nn.Module):
@@ -102,7 +112,7 @@ class Bottleneck(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
         out = self.bn1(c1x1(x, self.conv1))
-        out = bn_relu_c1x1(self.conv2(out), self.bn2, self.conv3)
+        out = bn_relu_c1x1(c3x3(out, self.conv2), self.bn2, self.conv3)
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
         return self.bn3(out, idt, shortcut_link=self.downsample is None)
 

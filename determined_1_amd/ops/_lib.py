@@ -140,6 +140,13 @@ _SIGNATURES = {
     "det_igemm_rows_per_block": ([], c_int),
     # stream, X, W, Y, zero, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, pmean, pm2
     "det_igemm_conv": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2, c_int),
+    "det_igemm_rows_per_block_cfg": ([c_int, c_int], c_int),
+    # stream, W (KRSC), in_dtype (0 fp32 / 1 bf16), out [C, R*S*K] bf16, K, C, R, S
+    "det_conv_dgrad_weight": ([c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 4, c_int),
+    # ... + cfg (0 = automatic per shape)
+    "det_igemm_conv_cfg": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2 + [c_int], c_int),
+    # stream, dY, X, out, out_dtype, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, ws, out_scale
+    "det_conv_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 10 + [c_void_p, c_float], c_int),
     # stream, dY, X, out, out_dtype, M, N, K, scale_x, shift_x, ws, out_scale, Ho, Wo, Hi, Wi
     "det_conv_tn": ([c_void_p] * 4 + [c_int, c_i64, c_int, c_int] + [c_void_p] * 3 + [c_float] + [c_int] * 4, c_int),
     # stream, X, W, Y, M, Hi, Wi, Ho, Wo, pmean, pm2

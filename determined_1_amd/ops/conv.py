@@ -146,10 +146,11 @@ def igemm_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
-               w_krsc: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
-    """``conv2d(x, w, stride, pad)`` for channels_last bf16 ``x`` (Cin % 64 == 0) and Cout % 64 == 0.
+               w_krsc: Optional[torch.Tensor] = None, cfg: int = 0) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
+    """``conv2d(x, w, stride, pad)`` for channels_last bf16 ``x`` (Cin % 32 == 0) and Cout % 64 == 0.
     Returns (y channels_last bf16, BN statistics partials of y when ``stats``).  ``w_krsc``: the
-    weight already in [Cout, R*S*Cin] form (e.g. the flipped/transposed dgrad weight)."""
+    weight already in [Cout, R*S*Cin] form (e.g. the flipped/transposed dgrad weight).  ``cfg``:
+    det_igemm tile configuration (0 = the measured per-shape choice)."""
     nb, cin, hi, wi = x.shape
     cout, _, r, s = w.shape
     ho = (hi + 2 * pad - r) // stride + 1
@@ -169,17 +170,53 @@ def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, 
     parts = None
     pm = pq = None
     if stats:
-        rpb = int(_lib.get_lib().det_igemm_rows_per_block())
+        rpb = int(_lib.get_lib().det_igemm_rows_per_block_cfg(int(cout), int(cfg)))
         nrb = (m + rpb - 1) // rpb
         pm = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
         pq = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
         parts = (pm, pq, rpb)
-    _lib.check(_lib.get_lib().det_igemm_conv(_stream(x), x.data_ptr(), wk.data_ptr(), y.data_ptr(),
-                                             _zero_page(x.device).data_ptr(), int(m), int(cout), int(cin), int(hi),
-                                             int(wi), int(ho), int(wo), int(r), int(s), int(stride), int(pad),
-                                             _ptr(pm), _ptr(pq)),
+    _lib.check(_lib.get_lib().det_igemm_conv_cfg(_stream(x), x.data_ptr(), wk.data_ptr(), y.data_ptr(),
+                                                 _zero_page(x.device).data_ptr(), int(m), int(cout), int(cin), int(hi),
+                                                 int(wi), int(ho), int(wo), int(r), int(s), int(stride), int(pad),
+                                                 _ptr(pm), _ptr(pq), int(cfg)),
                "igemm_conv")
     return y, parts
+
+
+def dgrad_weight(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, R, S] -> the [Cin, R*S*Cout] KRSC weight whose forward conv (stride 1, pad
+    (R-1)/2) of dY is the input gradient: W'[c][r][s][k] = W[k][c][R-1-r][S-1-s].  One HIP
+    transpose launch for channels_last fp32/bf16 weights on the GPU."""
+    k, c, r, s = w.shape
+    if is_gpu(w) and w.dtype in (torch.float32, torch.bfloat16) and w.is_contiguous(memory_format=torch.channels_last):
+        out = torch.empty(c, r * s * k, dtype=torch.bfloat16, device=w.device)
+        _lib.check(_lib.get_lib().det_conv_dgrad_weight(_stream(w), w.data_ptr(), 1 if w.dtype == torch.bfloat16 else 0,
+                                                         out.data_ptr(), int(k), int(c), int(r), int(s)),
+                   "conv_dgrad_weight")
+        return out
+    return w.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).to(torch.bfloat16).contiguous()
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, r: int, s: int, stride: int, pad: int,
+               out_scale: float = 1.0) -> torch.Tensor:
+    """Weight gradient of a conv: ``out`` (contiguous [Cout, R*S*Cin] KRSC view, bf16 or fp32) =
+    out_scale * dY^T . im2col(X), split-M fp32 slabs on det_conv's transposed-read MFMA tiles."""
+    nb, cin, hi, wi = x.shape
+    cout, ho, wo = dy.shape[1], dy.shape[2], dy.shape[3]
+    m = nb * ho * wo
+    if not is_gpu(dy):
+        g = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, r, s), dy.float(), stride=stride, padding=pad)
+        out.copy_((g * out_scale).permute(0, 2, 3, 1).reshape(out.shape))
+        return out
+    assert out.dtype in (torch.bfloat16, torch.float32) and out.is_contiguous() and out.numel() == cout * r * s * cin
+    lib = _lib.get_lib()
+    ws = torch.empty(int(lib.det_conv_tn_ws_elems(m, cout, r * s * cin)), dtype=torch.float32, device=dy.device)
+    _lib.check(lib.det_conv_wgrad(_stream(dy), dy.data_ptr(), x.data_ptr(), out.data_ptr(),
+                                  1 if out.dtype == torch.bfloat16 else 0, int(m), int(cout), int(cin), int(hi), int(wi),
+                                  int(ho), int(wo), int(r), int(s), int(stride), int(pad), ws.data_ptr(),
+                                  float(out_scale)),
+               "conv_wgrad")
+    return out
 
 
 # ------------------------------------------------------------------------------------------------
@@ -319,6 +356,105 @@ class _BNReluConv1x1(torch.autograd.Function):
 
 
 FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0, "stem": 0, "stem_fallback": 0}
+
+
+# ------------------------------------------------------------------------------------------------
+# autograd: 3x3 (and other R x S) convolutions on the det_igemm implicit GEMM
+# ------------------------------------------------------------------------------------------------
+CONV3X3_COUNTS = {"native": 0, "fallback": 0, "dgrad_native": 0, "dgrad_miopen": 0, "wgrad_native": 0,
+                  "wgrad_miopen": 0}
+# 3x3 weight gradient on det_conv's split-M implicit GEMM (True) or MIOpen's wrw kernels (False,
+# default: 5.15 vs ~4.1 ms/step for ResNet-50's 16 3x3 wgrads at batch 512,
+# profiles/r3_resnet50_native3x3_steady.csv); the forward and stride-1 input gradient stay native.
+NATIVE_WGRAD_RS = False
+
+
+class _ConvRS(torch.autograd.Function):
+    """``conv2d(x, w, stride, pad)`` (R x S, no bias, groups 1) on channels_last bf16 activations:
+    forward = det_igemm implicit GEMM with the output's BatchNorm statistics in its epilogue;
+    input gradient = det_igemm forward conv of dY against the flipped/transposed weight (stride 1;
+    strided convs keep MIOpen's transposed conv for the input gradient); weight gradient = det_conv
+    split-M implicit GEMM with the im2col gather, written straight into the arena slot."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, stats):
+        wk = krsc(weight.to(torch.bfloat16) if weight.dtype != torch.bfloat16 else weight)
+        y, parts = igemm_conv(x, weight, stride=stride, pad=pad, stats=stats, w_krsc=wk)
+        _attach_partials(y, parts)
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.pad = stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, pad = ctx.stride, ctx.pad
+        cout, cin, r, s = weight.shape
+        dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if stride == 1 and 2 * pad == r - 1 and r == s:
+                wd = dgrad_weight(weight)
+                # (on the GPU only the shape of the second argument is read; the CPU reference
+                # path convolves with it, so it gets the real flipped weight there)
+                wt = weight.transpose(0, 1) if is_gpu(dyc) else weight.flip(2, 3).transpose(0, 1)
+                dx, _ = igemm_conv(dyc, wt, stride=1, pad=r - 1 - pad, w_krsc=wd)
+                CONV3X3_COUNTS["dgrad_native"] += 1
+            else:
+                wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                         [0, 0], 1, [True, False, False])[0]
+                CONV3X3_COUNTS["dgrad_miopen"] += 1
+        if ctx.needs_input_grad[1] and not NATIVE_WGRAD_RS:
+            wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            gw = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                     [0, 0], 1, [False, True, False])[1]
+            dw = gw.to(weight.dtype)
+            CONV3X3_COUNTS["wgrad_miopen"] += 1
+        elif ctx.needs_input_grad[1]:
+            from determined_1_amd.ops.arena import landing_buffer
+
+            buf = landing_buffer(weight)
+            if buf is not None and buf.is_contiguous(memory_format=torch.channels_last) and \
+                    buf.dtype in (torch.bfloat16, torch.float32):
+                dw = buf
+                out = buf.permute(0, 2, 3, 1).reshape(cout, -1)  # KRSC view of channels_last memory
+            else:
+                dt = weight.dtype if weight.dtype in (torch.bfloat16, torch.float32) else torch.float32
+                dw = torch.empty(weight.shape, dtype=dt, device=weight.device, memory_format=torch.channels_last)
+                out = dw.permute(0, 2, 3, 1).reshape(cout, -1)
+            assert out.data_ptr() == dw.data_ptr() and out.is_contiguous()
+            conv_wgrad(dyc, x, out, r, s, stride, pad)
+            CONV3X3_COUNTS["wgrad_native"] += 1
+            if dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
+        return dx, dw, None, None, None
+
+
+def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> torch.Tensor:
+    """``conv_mod(x)`` for bias-free square R x S convs (groups 1, dilation 1, symmetric zero padding)
+    on channels_last bf16 CUDA activations with Cin % 64 == 0 and Cout % 64 == 0 (every ResNet 3x3);
+    anything else runs the module."""
+    w = conv_mod.weight
+    k = conv_mod.kernel_size
+    st = conv_mod.stride
+    pd = conv_mod.padding
+    ok = (ENABLED and x.device.type == "cuda" and x.dim() == 4 and conv_mod.bias is None and k[0] == k[1]
+          and isinstance(pd, tuple) and pd[0] == pd[1] and st[0] == st[1] and conv_mod.dilation == (1, 1)
+          and conv_mod.groups == 1 and conv_mod.padding_mode == "zeros" and x.shape[1] % 64 == 0
+          and w.shape[0] % 64 == 0 and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+    if ok:
+        autocast = torch.is_autocast_enabled("cuda")
+        if x.dtype != torch.bfloat16 and not (autocast and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            ok = False
+    if not ok:
+        CONV3X3_COUNTS["fallback"] += 1
+        return conv_mod(x)
+    CONV3X3_COUNTS["native"] += 1
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    with torch.autocast("cuda", enabled=False):
+        return _ConvRS.apply(x, w, int(st[0]), int(pd[0]), stats)
 # Stem weight gradient: the det_conv split-M implicit GEMM (True) or MIOpen's NHWC C=4 kernel (False,
 # default: 0.49 vs 0.82 ms at batch 512, profiles/r2_stem_microbench.jsonl).  The forward stays native
 # (0.64 ms including the BN statistics vs MIOpen 0.70 + a 0.17 ms stats pass).

@@ -65,10 +65,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 // Input-row gather of a 1x1 stride-2 convolution: output row m = ((n*Ho)+ho)*Wo+wo reads input
 // row (n*Hi + 2ho)*Wi + 2wo.
-constexpr int kGmDirect = 0, kGmStride2 = 1, kGmStem = 2;  // A/X row gather modes
+constexpr int kGmDirect = 0, kGmStride2 = 1, kGmStem = 2, kGmConv = 3;  // A/X row gather modes
 
 struct Gather {
   int Ho, Wo, Hi, Wi;
+  // kGmConv (wgrad of an R x S conv): channels per input pixel, kernel width, stride, padding
+  int cin, ks, cstride, cpad;
   __device__ __forceinline__ int64_t row(int64_t m) const {
     const int64_t hw = static_cast<int64_t>(Ho) * Wo;
     const int64_t n = m / hw;
@@ -378,6 +380,29 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
 
   us8 ry[YCH], rx[XCH];
   bool xval[XCH];
+  // kGmConv: each X chunk row tracks its output pixel (n, ho, wo) and advances it by the 64 rows of
+  // an M step with carries (no per-step divisions); the tile's tap (r, s) and channel offset are
+  // fixed (one tile never straddles taps: cin % (BK * KSUB) == 0)
+  int cn[XCH], cho[XCH], cwo[XCH];
+  int ctap_r = 0, ctap_s = 0, cc0 = 0, adv_h = 0, adv_w = 0;
+  if (GM == kGmConv) {
+    const int tap = k0 / a.g.cin;
+    cc0 = k0 - tap * a.g.cin;
+    ctap_r = tap / a.g.ks;
+    ctap_s = tap - ctap_r * a.g.ks;
+    adv_h = 64 / a.g.Wo;
+    adv_w = 64 - adv_h * a.g.Wo;
+    const int hw = a.g.Ho * a.g.Wo;
+#pragma unroll
+    for (int i = 0; i < XCH; ++i) {
+      const int idx = tid + i * kThreads, r = idx / XCPR;
+      const int m = static_cast<int>(mbeg) + r;
+      cn[i] = m / hw;
+      const int rem = m - cn[i] * hw;
+      cho[i] = rem / a.g.Wo;
+      cwo[i] = rem - cho[i] * a.g.Wo;
+    }
+  }
   auto gload = [&](int64_t mb) {
 #pragma unroll
     for (int i = 0; i < YCH; ++i) {
@@ -395,6 +420,25 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
         int ih, iw;
         const unsigned short* img = a.g.stem(xval[i] ? m : 0, ih, iw, a.X);
         rx[i] = a.g.stem_chunk(img, xval[i], ih, iw, (k0 >> 3) + c);
+        continue;
+      }
+      if (GM == kGmConv) {
+        const int hi = cho[i] * a.g.cstride - a.g.cpad + ctap_r, wi = cwo[i] * a.g.cstride - a.g.cpad + ctap_s;
+        const bool ok = xval[i] && hi >= 0 && hi < a.g.Hi && wi >= 0 && wi < a.g.Wi;
+        if (ok)
+          rx[i] = *reinterpret_cast<const us8*>(
+              a.X + ((static_cast<int64_t>(cn[i]) * a.g.Hi + hi) * a.g.Wi + wi) * a.g.cin + cc0 + c * 8);
+        else
+          rx[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+        // advance this row's pixel by one M step (64 rows)
+        cwo[i] += adv_w;
+        int carry = cwo[i] >= a.g.Wo;
+        cwo[i] -= carry ? a.g.Wo : 0;
+        cho[i] += adv_h + carry;
+        while (cho[i] >= a.g.Ho) {
+          cho[i] -= a.g.Ho;
+          ++cn[i];
+        }
         continue;
       }
       const int64_t row = GM == kGmStride2 ? a.g.row(xval[i] ? m : 0) : (xval[i] ? m : 0);
@@ -516,12 +560,13 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
 }
 
 template <int BN, int BK>
-int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride2) {
+int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride2, bool conv = false) {
   const int nwg = (a.N / BN) * (a.K / BK) * splits;
   constexpr int smem = 2 * 64 * (BN + BK) * 2;
 #define DET_TN(P, G) \
   hipLaunchKernelGGL((gemm_tn_kernel<BN, BK, P, G>), dim3(nwg), dim3(kThreads), smem, st, a)
-  if (stride2) { if (pro) DET_TN(true, kGmStride2); else DET_TN(false, kGmStride2); }
+  if (conv) DET_TN(false, kGmConv);
+  else if (stride2) { if (pro) DET_TN(true, kGmStride2); else DET_TN(false, kGmStride2); }
   else { if (pro) DET_TN(true, kGmDirect); else DET_TN(false, kGmDirect); }
 #undef DET_TN
   return static_cast<int>(hipGetLastError());
@@ -590,6 +635,42 @@ int det_conv_tn(void* stream, const void* dY, const void* X, void* out, int out_
   else if (bn == 128) rc = launch_tn<128, 64>(st, a, splits, pro, stride2);
   else if (bk == 128) rc = launch_tn<64, 128>(st, a, splits, pro, stride2);
   else rc = launch_tn<64, 64>(st, a, splits, pro, stride2);
+  if (rc != 0) return rc;
+  int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
+  if (grid > 2048) grid = 2048;
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
+                       static_cast<unsigned short*>(out));
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
+                       static_cast<float*>(out));
+  return static_cast<int>(hipGetLastError());
+}
+
+// Weight gradient of an R x S convolution (stride, pad) over NHWC bf16:
+//   dW[N, R*S*Cin] (KRSC; out_dtype 0 fp32 / 1 bf16) = out_scale * dY[M, N]^T . im2col(X)[M, R*S*Cin]
+// as split-M fp32 slabs in ws (>= det_conv_tn_ws_elems(M, N, R*S*Cin)) reduced by a second launch.
+// Cin % 64 == 0, N % 64 == 0.
+int det_conv_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int N, int Cin,
+                   int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* ws, float out_scale) {
+  if (M <= 0 || N % 64 != 0 || Cin % 64 != 0 || R <= 0 || S <= 0) return -1;
+  if (M % (static_cast<int64_t>(Ho) * Wo) != 0 || M >= (static_cast<int64_t>(1) << 31)) return -3;
+  if (Ho != (Hi + 2 * pad - R) / stride + 1 || Wo != (Wi + 2 * pad - S) / stride + 1) return -3;
+  const int K = R * S * Cin;
+  const int bn = N % 128 == 0 ? 128 : 64, bk = Cin % 128 == 0 ? 128 : 64;
+  const int64_t slab = static_cast<int64_t>(N) * K;
+  const int splits = static_cast<int>(det_conv_tn_ws_elems(M, N, K) / slab);
+  int64_t rps = (M + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  Gather g{Ho, Wo, Hi, Wi, Cin, S, stride, pad};
+  TnArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, N, K, rps, nullptr,
+           nullptr, g};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int rc;
+  if (bn == 128 && bk == 128) rc = launch_tn<128, 128>(st, a, splits, false, false, true);
+  else if (bn == 128) rc = launch_tn<128, 64>(st, a, splits, false, false, true);
+  else if (bk == 128) rc = launch_tn<64, 128>(st, a, splits, false, false, true);
+  else rc = launch_tn<64, 64>(st, a, splits, false, false, true);
   if (rc != 0) return rc;
   int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
   if (grid > 2048) grid = 2048;

@@ -38,6 +38,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -530,10 +531,282 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// v3: 32-deep K tiles and 256 x 256 block tiles (8 waves, 128 x 64 wave tiles).
+//
+// v2's 256 x 128 tile stages (256 + 128) rows per 2 * 256 * 128 * K FLOP; its 6 LDS-DMA pieces per
+// wave per 32 MFMAs cost ~60-185 issue cycles each among the MFMAs (MI355X_MICROARCH.md, "LDS-DMA
+// piece issue cost"), which is what held it at ~35 % of the MFMA rate.  A 256 x 256 tile stages
+// 1.5x fewer bytes per FLOP: 4 pieces per wave per 32 MFMAs.  At BK = 64 a 256 x 256 stage is
+// 64 KiB, two stages are all the ring LDS allows, which leaves no prefetch distance in this loop
+// structure; at BK = 32 a stage is 32 KiB and a 4-stage ring keeps two tiles in flight.
+//
+// LDS rows are 64 B: a ds_read_b128 fragment read (16 rows, one 16-B chunk each, lane groups
+// {0-3,12-15,20-27} ...) is conflict-free with the chunk XOR f(row) = (-(row >> 2)) & 3 (each group
+// then covers 16 distinct (row & 3, chunk') bank slots); as everywhere the LDS image is lane-linear
+// and the XOR is applied to the per-lane source address.
+//
+// Software pipeline per K tile: the wave tile is cut into its upper and lower A halves;
+//   read A_hi(kt)                  || MFMAs A_lo(kt) x B(kt)
+//   wait tile kt+1, barrier, issue tile kt+NS-1
+//   read A_lo(kt+1)                || MFMAs A_hi(kt) x B(kt), then read B(kt+1) into the B registers
+//                                     as the j-outer cluster releases them
+// (acc 128 + 3 x 16 fragment VGPRs: a second B set would push the 256 x 256 tile past 256 VGPRs).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int swz64(int row, int ch) { return row * 64 + ((ch ^ ((-(row >> 2)) & 3)) << 4); }
+
+template <int BM, int BN, int WM, int WN, int NS, bool STATS>
+__global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int BK = 32;
+  constexpr int NW = WM * WN, kThreads = NW * 64;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16, FH = FM / 2;
+  static_assert(FM % 2 == 0, "two A halves");
+  // 16 rows of 64 B per LDS-DMA piece.  When B has fewer pieces than there are waves (BN = 64 at 8
+  // waves) only waves wid < BP fetch B, one piece each, and count their own extra piece in vmcnt.
+  constexpr int AI = BM / (16 * NW), BP = BN / 16, BI = BP >= NW ? BP / NW : 1;
+  static_assert(AI * 16 * NW == BM && (BP >= NW ? BI * NW == BP : NW % BP == 0), "tile rows split over the waves");
+  static_assert(NS >= 3, "prefetch distance");
+  constexpr bool BPART = BP < NW;
+  constexpr int NI = AI + BI, NIA = AI;  // pieces per tile of a B-fetching / a non-fetching wave
+  constexpr int A_BYTES = BM * 64, STAGE = (BM + BN) * 64;
+  constexpr int LDC = BN + 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = a.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int64_t m0 = static_cast<int64_t>(mt) * BM;
+  const int n0 = nt * BN;
+  const int64_t K = a.K;
+  const int lrow = lane >> 2;                       // row within a 16-row piece
+  const int gch = (lane & 3) ^ ((-(lrow >> 2)) & 3);  // source chunk of this lane's LDS slot
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(a.X), 0, static_cast<int>(a.x_bytes), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(a.W), 0, static_cast<int>(static_cast<int64_t>(a.N) * K * 2), 0x00020000);
+  constexpr unsigned kOOB = 0xFFFFFFF0u;
+  int aoff[AI];
+  unsigned amask[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (i * NW + wid) * 16 + lrow;
+    const int64_t m = m0 + row;
+    aoff[i] = 0;
+    amask[i] = 0;
+    if (m < a.M) {
+      const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
+      const int64_t n = m / hw;
+      const int rem = static_cast<int>(m - n * hw);
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
+      aoff[i] = static_cast<int>(((n * a.Hi + hi0) * a.Wi + wi0) * a.Cin * 2 + gch * 16);
+      for (int r = 0; r < a.R; ++r)
+        for (int s2 = 0; s2 < a.S; ++s2) {
+          const int hi = hi0 + r, wi = wi0 + s2;
+          if (hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi) amask[i] |= 1u << (r * a.S + s2);
+        }
+    }
+  }
+  unsigned boff[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j)
+    boff[j] = static_cast<unsigned>(((static_cast<int64_t>(n0) + ((j * NW + wid) % BP) * 16 + lrow) * K + gch * 8) * 2);
+
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NS) * STAGE;
+    const int k0 = kt * BK;
+    const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
+    const int r = tap / a.S, s2 = tap - r * a.S;
+    const int toff = ((r * a.Wi + s2) * a.Cin + c0) * 2;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const unsigned v = ((amask[i] >> tap) & 1u) ? static_cast<unsigned>(aoff[i] + toff) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(st + ((i * NW + wid) * 16) * 64), 16, v, 0, 0, 0);
+    }
+    if (!BPART || wid < BP) {
+#pragma unroll
+      for (int j = 0; j < BI; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(st + A_BYTES + ((j * NW + wid) * 16) * 64), 16, boff[j],
+                                                 k0 * 2, 0, 0);
+    }
+  };
+  const bool bwave = !BPART || __builtin_amdgcn_readfirstlane(wid) < BP;
+  // counted waits on this wave's own LDS-DMA pieces: `tiles` younger tiles may stay in flight
+  auto wait_tiles = [&](auto tiles) {
+    constexpr int T = decltype(tiles)::value;
+    if (bwave) wait_vmcnt<NI * T>();
+    else wait_vmcnt<NIA * T>();
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ch = lane >> 4;
+  auto read_a = [&](const unsigned char* base, int h, bf16x8* af) {
+#pragma unroll
+    for (int i = 0; i < FH; ++i) af[i] = *reinterpret_cast<const bf16x8*>(base + swz64(wm * TM + (h * FH + i) * 16 + (lane & 15), ch));
+  };
+  auto read_b = [&](const unsigned char* base, bf16x8* bfr) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz64(wn * TN + j * 16 + (lane & 15), ch));
+  };
+  // h = 0: i-outer; h = 1: j-outer, so each b[j] dies after its FH MFMAs and the next tile's B
+  // reads (issued after the cluster in source order) can be scheduled into the cluster's tail
+  auto mfma = [&](int h, const bf16x8* af, const bf16x8* bfr) {
+    __builtin_amdgcn_s_setprio(1);
+    if (h == 0) {
+#pragma unroll
+      for (int i = 0; i < FH; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FH; ++i)
+          acc[FH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[FH + i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  bf16x8 alo[FH], ahi[FH], bf[FN];
+  const int nk = a.K / BK;
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
+  if (nk >= NS - 1) wait_tiles(std::integral_constant<int, NS - 2>{});
+  else wait_vmcnt<0>();
+  block_barrier();
+  read_a(smem, 0, alo);
+  read_b(smem, bf);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    read_a(smem + (kt % NS) * STAGE, 1, ahi);
+    mfma(0, alo, bf);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (kt + NS - 2 < nk) wait_tiles(std::integral_constant<int, NS - 3>{});
+    else wait_vmcnt<0>();
+    block_barrier();
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);
+    const unsigned char* nb = smem + ((kt + 1) % NS) * STAGE;
+    read_a(nb, 0, alo);
+    mfma(1, ahi, bf);
+    read_b(nb, bf);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  read_a(smem + ((nk - 1) % NS) * STAGE, 1, ahi);
+  mfma(0, alo, bf);
+  mfma(1, ahi, bf);
+  __syncthreads();
+
+  unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
+  const int64_t rows_left = a.M - m0;
+  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * TN + j * 16 + (lane & 15);
+        ct[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  if (STATS) {
+    float cs[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          if (row < nvalid) sm += round_bf(acc[i][j][r]);
+        }
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      cs[j] = sm;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + j * 16 + lane] = cs[j];
+    }
+    __syncthreads();
+    const float inv_n = 1.f / static_cast<float>(nvalid);
+    float mu[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wn * TN + j * 16 + (lane & 15);
+      float sm = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) sm += red[w * BN + col];
+      mu[j] = sm * inv_n;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+          const float d = round_bf(acc[i][j][r]) - mu[j];
+          if (row < nvalid) q += d * d;
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) red[wm * BN + wn * TN + j * 16 + lane] = q;
+      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
+    }
+  }
+  __syncthreads();
+  if (STATS && tid < BN) {
+    float q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
+    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
+  }
+  constexpr int CPR = BN / 8;
+#pragma unroll
+  for (int q = 0; q < (BM * CPR + kThreads - 1) / kThreads; ++q) {
+    const int idx = tid + q * kThreads;
+    const int row = idx / CPR, cc = idx - row * CPR;
+    if (idx < BM * CPR && row < nvalid)
+      *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+  }
+#endif
+}
+
+template <int BM, int BN, int WM, int WN, int NS>
+int launch3(hipStream_t st, const IgArgs& a, bool stats) {
+  constexpr int kThreads = WM * WN * 64;
+  if (a.N % BN != 0 || a.Cin % 32 != 0) return -6;
+  const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
+  constexpr int ring = NS * (BM + BN) * 64, ctile = BM * (BN + 16) * 2 + 4 * WM * BN;
+  constexpr int smem = ring > ctile ? ring : ctile;
+  static_assert(smem <= 163840, "LDS");
+  if (stats)
+    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, true>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+  else
+    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+  return static_cast<int>(hipGetLastError());
+}
+
 template <int BM, int BN, int WM, int WN, int NS, int OCC>
 int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
   constexpr int kThreads = WM * WN * 64;
-  if (a.N % BN != 0) return -6;
+  if (a.N % BN != 0 || a.Cin % 64 != 0) return -6;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int smem = NS * (BM + BN) * 128;
@@ -570,6 +843,7 @@ int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
 static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool stats) {
   switch (cfg) {
     case 1:
+      if (a.Cin % 64) return -6;
       if (a.N % 128 == 0) return launch<256, 128, 4, 2>(st, a, dense, stats);
       return launch<256, 64, 8, 1>(st, a, dense, stats);
     case 2: return launch2<256, 128, 4, 2, 3, 1>(st, a, dense, stats);
@@ -578,6 +852,14 @@ static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool st
     case 5: return launch2<256, 64, 8, 1, 3, 1>(st, a, dense, stats);
     case 6: return launch2<128, 64, 2, 2, 3, 2>(st, a, dense, stats);
     case 7: return launch2<128, 128, 2, 2, 3, 1>(st, a, dense, stats);
+    case 8: return launch3<256, 256, 2, 4, 4>(st, a, stats);   // 128x64 wave tiles, BK 32, 4 stages
+    case 9: return launch3<256, 128, 4, 2, 4>(st, a, stats);   // 64x64 wave tiles, BK 32
+    case 10: return launch3<256, 256, 2, 4, 3>(st, a, stats);  // 3 stages
+    case 11: return launch3<256, 64, 4, 1, 4>(st, a, stats);   // 4 waves, 64x64 wave tiles (N = 64)
+    case 12: return launch3<512, 128, 4, 2, 3>(st, a, stats);  // 128x64 wave tiles at N = 128
+    case 13: return launch3<512, 128, 4, 2, 4>(st, a, stats);
+    case 14: return launch3<512, 64, 8, 1, 4>(st, a, stats);   // 64x64 wave tiles at N = 64, 8 waves
+    case 15: return launch3<512, 64, 4, 1, 4>(st, a, stats);   // 128x64 wave tiles at N = 64, 4 waves
     default: return -7;
   }
 }
@@ -588,19 +870,63 @@ static int auto_cfg(const IgArgs& a) {
     return e ? std::atoi(e) : 0;
   }();
   if (forced > 0) return forced;
-  return a.N % 128 == 0 ? 2 : 3;
+  // measured per ResNet-50 shape (profiles/r3_igemm_cfgs.jsonl): 256 x 256 / BK 32 wherever N
+  // allows, 256 x 128 / BK 64 at N = 128, 256 x 64 / BK 32 (4 waves) at N = 64
+  if (a.N % 256 == 0 && a.Cin % 32 == 0) return 8;
+  if (a.N % 128 == 0 && a.Cin % 64 == 0) return 2;
+  return a.Cin % 32 == 0 ? 11 : 1;
+}
+
+// Input-gradient weight of an R x S conv in one pass: out[c][r][s][k] = W[k][R-1-r][S-1-s][c]
+// (W in KRSC = channels_last memory, fp32 or bf16 in, bf16 out), 64 x 64 LDS-tiled transpose per tap.
+template <typename TI>
+__global__ void __launch_bounds__(256) dgrad_weight_kernel(const TI* __restrict__ W, unsigned short* __restrict__ out,
+                                                           int K, int C, int R, int S) {
+  __shared__ float tile[64][65];
+  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int r = tap / S, s2 = tap - r * S;
+  const int src_tap = (R - 1 - r) * S + (S - 1 - s2);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int k = k0 + i, c = c0 + tx;
+    float v = 0.f;
+    if (k < K && c < C) {
+      const TI x = W[(static_cast<int64_t>(k) * R * S + src_tap) * C + c];
+      if constexpr (sizeof(TI) == 2) v = bf2f(x); else v = x;
+    }
+    tile[i][tx] = v;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, k = k0 + tx;
+    if (c < C && k < K) out[(static_cast<int64_t>(c) * R * S + tap) * K + k] = f2bf(tile[tx][i]);
+  }
 }
 
 }  // namespace
 
 extern "C" {
 
+// out[C][R*S*K] bf16 = the flipped, transposed KRSC weight the stride-1 input gradient convolves with.
+int det_conv_dgrad_weight(void* stream, const void* W, int in_dtype, void* out, int K, int C, int R, int S) {
+  if (K <= 0 || C <= 0 || R <= 0 || S <= 0) return -1;
+  const dim3 grid((C + 63) / 64, (K + 63) / 64, R * S);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (in_dtype == 1)
+    hipLaunchKernelGGL(dgrad_weight_kernel<unsigned short>, grid, dim3(256), 0, st,
+                       static_cast<const unsigned short*>(W), static_cast<unsigned short*>(out), K, C, R, S);
+  else
+    hipLaunchKernelGGL(dgrad_weight_kernel<float>, grid, dim3(256), 0, st, static_cast<const float*>(W),
+                       static_cast<unsigned short*>(out), K, C, R, S);
+  return static_cast<int>(hipGetLastError());
+}
+
 // Rows per statistics block of det_igemm for configuration cfg (0 = the automatic choice for N).
 int det_igemm_rows_per_block_cfg(int N, int cfg) {
   IgArgs a{};
   a.N = N;
   const int c = cfg > 0 ? cfg : auto_cfg(a);
-  return (c == 4 || c == 6 || c == 7) ? 128 : 256;
+  return (c == 4 || c == 6 || c == 7) ? 128 : (c >= 12 ? 512 : 256);
 }
 int det_igemm_rows_per_block() { return 256; }
 
@@ -611,7 +937,7 @@ int det_igemm_rows_per_block() { return 256; }
 int det_igemm_conv_cfg(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,
                        int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* pmean, float* pm2,
                        int cfg) {
-  if (M <= 0 || N <= 0 || N % 64 != 0 || Cin <= 0 || Cin % 64 != 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
+  if (M <= 0 || N <= 0 || N % 64 != 0 || Cin <= 0 || Cin % 32 != 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
     return -1;
   if ((pmean == nullptr) != (pm2 == nullptr) || zero == nullptr) return -2;
   if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y) |

@@ -38,6 +38,7 @@ class ResNetImageNetTrial(det_torch.PyTorchTrial):
         resnet.NATIVE_CONV1X1 = bool(hp.get("native_conv1x1", True))
         resnet.BN_PROLOGUE = bool(hp.get("bn_prologue", False))
         resnet.NATIVE_STEM = bool(hp.get("native_stem", True))
+        resnet.NATIVE_CONV3X3 = bool(hp.get("native_conv3x3", True))
         model = getattr(resnet, arch)(num_classes=self.num_classes)
         if self.channels_last:
             model = model.to(memory_format=torch.channels_last)

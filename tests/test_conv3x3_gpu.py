@@ -1,0 +1,127 @@
+"""Numerics of the 3x3 conv path (ops.conv.conv_rs / _ConvRS on det_igemm v2/v3 + det_conv's
+im2col weight gradient) against plain PyTorch fp32 references: every det_igemm tile configuration
+on ragged / strided / padded shapes, exact small-integer operands (a tap, row or swizzle mix-up
+shows exactly), BN statistics partials of the 256- and 512-row block variants, the weight
+gradient, and the autograd function end to end with its FALLBACK counters."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from determined_1_amd.ops import _lib, conv
+
+pytestmark = pytest.mark.gpu
+
+CFG_SHAPES = [  # (Nb, Cin, H, W, Cout, R, stride, pad)
+    (3, 128, 7, 9, 128, 3, 1, 1),      # M = 189 < one block
+    (2, 256, 15, 15, 256, 3, 2, 1),    # stride 2, odd input
+    (4, 64, 28, 28, 64, 3, 1, 1),      # N = 64, several blocks + tail
+    (2, 512, 7, 7, 512, 3, 1, 1),
+    (2, 256, 9, 9, 512, 1, 2, 0),      # 1x1 stride-2 gather
+]
+
+
+def _data(case, gpu, seed=0, integer=False):
+    nb, cin, h, w, cout, r, st, pad = case
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    if integer:
+        x = torch.randint(-2, 3, (nb, cin, h, w), generator=g).to(torch.bfloat16)
+        wt = torch.randint(-2, 3, (cout, cin, r, r), generator=g).to(torch.bfloat16)
+    else:
+        x = torch.randn(nb, cin, h, w, generator=g).to(torch.bfloat16)
+        wt = (torch.randn(cout, cin, r, r, generator=g) / (cin * r * r) ** 0.5).to(torch.bfloat16)
+    return x, wt, x.to(gpu).contiguous(memory_format=torch.channels_last), wt.to(gpu).contiguous(
+        memory_format=torch.channels_last)
+
+
+def _run_cfg(xg, wg, st, pad, cfg, stats=False):
+    try:
+        return conv.igemm_conv(xg, wg, stride=st, pad=pad, cfg=cfg, stats=stats)
+    except RuntimeError as e:
+        if "-6" in str(e) or "-7" in str(e):
+            pytest.skip(f"cfg {cfg} does not cover this shape")
+        raise
+
+
+@pytest.mark.parametrize("cfg", list(range(1, 16)))
+@pytest.mark.parametrize("case", CFG_SHAPES)
+def test_every_cfg_exact_on_integer_operands(gpu, case, cfg):
+    nb, cin, h, w, cout, r, st, pad = case
+    x, wt, xg, wg = _data(case, gpu, integer=True)
+    y, _ = _run_cfg(xg, wg, st, pad, cfg)
+    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    # integer sums up to 9 * 512 * 4 = 18432 are exact in fp32; bf16 rounds above 256
+    torch.testing.assert_close(y.float().cpu(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("cfg", [0, 2, 8, 11, 13])
+def test_cfg_stats_partials(gpu, cfg):
+    case = (4, 256, 28, 28, 256, 3, 1, 1)  # M = 3136: ragged last block for 256 and 512 rows
+    nb, cin, h, w, cout, r, st, pad = case
+    _, _, xg, wg = _data(case, gpu, seed=3)
+    y, (pm, pq, rpb) = _run_cfg(xg, wg, st, pad, cfg, stats=True)
+    yr = y.permute(0, 2, 3, 1).reshape(-1, cout).double().cpu()
+    m = yr.shape[0]
+    nrb = pm.shape[0]
+    assert nrb == (m + rpb - 1) // rpb and rpb == int(_lib.get_lib().det_igemm_rows_per_block_cfg(cout, cfg))
+    cnt = torch.full((nrb, 1), float(rpb), dtype=torch.float64)
+    cnt[-1, 0] = float(m - (nrb - 1) * rpb)
+    pmd, pqd = pm.double().cpu(), pq.double().cpu()
+    mean = (pmd * cnt).sum(0) / m
+    var = (pqd + cnt * (pmd - mean) ** 2).sum(0) / m
+    torch.testing.assert_close(mean, yr.mean(0), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(var, yr.var(0, unbiased=False), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("case", [(3, 64, 9, 11, 128, 3, 1, 1), (2, 128, 15, 15, 128, 3, 2, 1),
+                                  (2, 256, 7, 7, 64, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0)])
+def test_conv_wgrad_matches_torch(gpu, case):
+    nb, cin, h, w, cout, r, st, pad = case
+    x, wt, xg, _ = _data(case, gpu, seed=7)
+    ho = (h + 2 * pad - r) // st + 1
+    g = torch.Generator(device="cpu").manual_seed(8)
+    dy = torch.randn(nb, cout, ho, (w + 2 * pad - r) // st + 1, generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, r, r), dy.float(), stride=st, padding=pad)
+    for dt in (torch.float32, torch.bfloat16):
+        out = torch.empty(cout, r * r * cin, dtype=dt, device=gpu)
+        conv.conv_wgrad(dy.to(gpu).contiguous(memory_format=torch.channels_last), xg, out, r, r, st, pad)
+        got = out.view(cout, r, r, cin).permute(0, 3, 1, 2).float().cpu()
+        tol = 1e-3 if dt == torch.float32 else 1e-2
+        torch.testing.assert_close(got, ref, rtol=tol, atol=tol * float(ref.abs().max()))
+
+
+def test_dgrad_weight_kernel_matches_torch(gpu):
+    for dt in (torch.float32, torch.bfloat16):
+        w = torch.randn(96, 64, 3, 3, device=gpu).to(dt).contiguous(memory_format=torch.channels_last)
+        got = conv.dgrad_weight(w)
+        ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(64, -1).to(torch.bfloat16)
+        assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("native_wgrad", [False, True])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv_rs_autograd_end_to_end(gpu, stride, native_wgrad, monkeypatch):
+    monkeypatch.setattr(conv, "NATIVE_WGRAD_RS", native_wgrad)
+    torch.manual_seed(0)
+    m = torch.nn.Conv2d(128, 128, 3, stride=stride, padding=1, bias=False).to(gpu).to(
+        memory_format=torch.channels_last)
+    x = torch.randn(4, 128, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    before = dict(conv.CONV3X3_COUNTS)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv.conv_rs(x, m)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    assert conv.CONV3X3_COUNTS["native"] == before["native"] + 1
+    assert conv.CONV3X3_COUNTS["fallback"] == before["fallback"]
+    wkey = "wgrad_native" if native_wgrad else "wgrad_miopen"
+    assert conv.CONV3X3_COUNTS[wkey] == before[wkey] + 1
+    key = "dgrad_native" if stride == 1 else "dgrad_miopen"
+    assert conv.CONV3X3_COUNTS[key] == before[key] + 1
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=stride, padding=1)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=2e-2 * float(wr.grad.abs().max()))
