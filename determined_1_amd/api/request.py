@@ -3,23 +3,38 @@
 import json
 import os
 import time
-from typing import Any, Dict, Iterator, List, Optional, Tuple
+from typing import Any, Dict, Iterator, List, Optional, Tuple, Union
 
 import requests
 
 
 def parse_master_address(addr: Optional[str]) -> Tuple[str, int]:
     addr = addr or os.environ.get("DET_MASTER", "127.0.0.1:8080")
-    addr = addr.replace("http://", "").rstrip("/")
+    addr = addr.replace("https://", "").replace("http://", "").rstrip("/")
     if ":" in addr:
         h, p = addr.rsplit(":", 1)
         return h, int(p)
     return addr, 8080
 
 
+def _truthy(v: Optional[str]) -> bool:
+    return (v or "").strip().lower() in ("1", "true", "yes", "on")
+
+
+def master_tls(master: Optional[str] = None) -> Tuple[bool, Union[bool, str]]:
+    """(use TLS, requests ``verify``) for the master.  TLS when the address is ``https://...`` or
+    ``DET_USE_TLS`` is true (the master sets it, with ``DET_MASTER_CERT_FILE``, in every task it
+    starts: reference ``harness/determined/exec/harness.py:161-163``); the server certificate is
+    verified against ``DET_MASTER_CERT_FILE`` when set, else the system CA bundle."""
+    addr = master or os.environ.get("DET_MASTER", "")
+    use = addr.startswith("https://") or _truthy(os.environ.get("DET_USE_TLS"))
+    cert = os.environ.get("DET_MASTER_CERT_FILE")
+    return use, (cert if cert else True)
+
+
 def make_url(master: str, path: str) -> str:
     h, p = parse_master_address(master)
-    return f"http://{h}:{p}{path}"
+    return f"{'https' if master_tls(master)[0] else 'http'}://{h}:{p}{path}"
 
 
 class APIError(RuntimeError):
@@ -62,6 +77,9 @@ class MasterClient:
         self.master = master or os.environ.get("DET_MASTER", "127.0.0.1:8080")
         self.timeout = timeout
         self.session = requests.Session()
+        # passed per request: requests lets $REQUESTS_CA_BUNDLE override a session-level verify
+        self.verify = master_tls(self.master)[1]
+        self.session.verify = self.verify
         tok = _load_token(self.master)
         if tok:
             self.session.headers["Authorization"] = f"Bearer {tok}"
@@ -75,7 +93,7 @@ class MasterClient:
     def _call(self, method: str, path: str, body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
         r = self.session.request(method, make_url(self.master, path), params=params,
                                  data=None if body is None else json.dumps(body), timeout=self.timeout,
-                                 headers={"Content-Type": "application/json"})
+                                 headers={"Content-Type": "application/json"}, verify=self.verify)
         if r.status_code >= 300:
             try:
                 msg = r.json().get("error", r.text)
@@ -131,7 +149,8 @@ class MasterClient:
         """A server-streaming /api/v1 RPC: one ``{"result": ...}`` JSON object per line over a
         chunked response (grpc-gateway framing); yields each ``result``."""
         q = {k: ("true" if v is True else "false" if v is False else v) for k, v in params.items() if v is not None}
-        r = self.session.get(make_url(self.master, path), params=q, stream=True, timeout=(self.timeout, None))
+        r = self.session.get(make_url(self.master, path), params=q, stream=True, timeout=(self.timeout, None),
+                             verify=self.verify)
         try:
             if r.status_code >= 300:
                 try:

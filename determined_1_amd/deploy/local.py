@@ -43,8 +43,10 @@ class LocalCluster:
                  store_dir: Optional[str] = None, checkpoint_dir: Optional[str] = None,
                  scheduler: str = "fair_share", work_dir: Optional[str] = None, gpu: bool = False,
                  log_dir: Optional[str] = None, tick_ms: int = 100, master_args: Optional[List[str]] = None,
-                 visible_gpus: Optional[str] = None, agent_args: Optional[List[str]] = None) -> None:
+                 visible_gpus: Optional[str] = None, agent_args: Optional[List[str]] = None,
+                 tls_cert: Optional[str] = None, tls_key: Optional[str] = None) -> None:
         self.port = port or free_port()
+        self.tls_cert, self.tls_key = tls_cert, tls_key  # serve the API over TLS (security.tls)
         self.tmp = tempfile.mkdtemp(prefix="det-local-")
         self.store_dir = store_dir or os.path.join(self.tmp, "store")
         self.checkpoint_dir = checkpoint_dir or os.path.join(self.tmp, "checkpoints")
@@ -63,7 +65,13 @@ class LocalCluster:
 
     @property
     def address(self) -> str:
-        return f"127.0.0.1:{self.port}"
+        return f"{'https://' if self.tls_cert else ''}127.0.0.1:{self.port}"
+
+    def _url(self, path: str) -> str:
+        return f"{'https' if self.tls_cert else 'http'}://127.0.0.1:{self.port}{path}"
+
+    def _verify(self):
+        return self.tls_cert if self.tls_cert else True
 
     def start_master(self) -> None:
         os.makedirs(self.checkpoint_dir, exist_ok=True)
@@ -71,12 +79,13 @@ class LocalCluster:
         self.master_proc = subprocess.Popen(
             [native_binary("det-master"), "--host", "127.0.0.1", "--port", str(self.port), "--store-dir",
              self.store_dir, "--scheduler", self.scheduler, "--checkpoint-host-path", self.checkpoint_dir,
-             "--python", sys.executable, "--scheduler-tick-ms", str(self.tick_ms)] + self.master_args,
+             "--python", sys.executable, "--scheduler-tick-ms", str(self.tick_ms)] + self.master_args
+            + (["--tls-cert", self.tls_cert, "--tls-key", self.tls_key] if self.tls_cert else []),
             stdout=log, stderr=subprocess.STDOUT)
         deadline = time.time() + 30
         while time.time() < deadline:
             try:
-                requests.get(f"http://{self.address}/info", timeout=1)
+                requests.get(self._url("/info"), timeout=1, verify=self._verify())
                 return
             except requests.RequestException:
                 if self.master_proc.poll() is not None:
@@ -96,6 +105,8 @@ class LocalCluster:
             if self.visible_gpus:
                 args += ["--visible-gpus", self.visible_gpus]
         args += self.agent_args
+        if self.tls_cert:
+            args += ["--master-cert-file", self.tls_cert]
         p = subprocess.Popen(args, stdout=log, stderr=subprocess.STDOUT)
         self.agent_procs.append(p)
         return p
@@ -104,10 +115,10 @@ class LocalCluster:
         deadline = time.time() + timeout
         headers = {}
         while time.time() < deadline:
-            r = requests.get(f"http://{self.address}/agents", timeout=5, headers=headers)
+            r = requests.get(self._url("/agents"), timeout=5, headers=headers, verify=self._verify())
             if r.status_code == 401:  # --require-auth: the built-in user has an empty password
-                tok = requests.post(f"http://{self.address}/login", json={"username": "determined", "password": ""},
-                                    timeout=5).json()["token"]
+                tok = requests.post(self._url("/login"), json={"username": "determined", "password": ""},
+                                    timeout=5, verify=self._verify()).json()["token"]
                 headers = {"Authorization": f"Bearer {tok}"}
                 continue
             agents = r.json()

@@ -25,11 +25,13 @@ from typing import Any, Dict, List
 
 import requests
 
+from determined_1_amd.api.request import make_url, master_tls
+
 
 def materialize(spec: Dict[str, Any], workdir: pathlib.Path, master: str) -> None:
     exp_id = spec.get("experiment_id", 0)
     url = spec.get("context_url") or f"/experiments/{exp_id}/model_def"
-    r = requests.get(f"http://{master}{url}", timeout=60)
+    r = requests.get(make_url(master, url), timeout=60, verify=master_tls(master)[1])
     r.raise_for_status()
     for f in r.json().get("files", []):
         rel = f.get("path", "")

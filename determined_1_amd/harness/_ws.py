@@ -17,9 +17,20 @@ class WebSocketError(RuntimeError):
 
 
 class WebSocket:
-    def __init__(self, host: str, port: int, path: str, timeout: Optional[float] = 30.0) -> None:
-        self.sock = socket.create_connection((host, port), timeout=timeout)
-        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    def __init__(self, host: str, port: int, path: str, timeout: Optional[float] = 30.0,
+                 tls: Optional[bool] = None) -> None:
+        """``tls=None``: TLS iff the task/CLI environment says the master speaks it (``DET_USE_TLS``,
+        ``DET_MASTER_CERT_FILE``; ``DET_MASTER_CERT_NAME`` overrides the name checked)."""
+        raw = socket.create_connection((host, port), timeout=timeout)
+        raw.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        if tls is None:
+            tls = (os.environ.get("DET_USE_TLS", "") or "").strip().lower() in ("1", "true", "yes", "on")
+        if tls:
+            import ssl
+
+            ctx = ssl.create_default_context(cafile=os.environ.get("DET_MASTER_CERT_FILE") or None)
+            raw = ctx.wrap_socket(raw, server_hostname=os.environ.get("DET_MASTER_CERT_NAME") or host)
+        self.sock = raw
         key = base64.b64encode(os.urandom(16)).decode()
         req = (f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
                f"Sec-WebSocket-Key: {key}\r\nSec-WebSocket-Version: 13\r\n\r\n")

@@ -68,7 +68,29 @@ struct Envelope {
   Ref sender;
   std::shared_ptr<std::promise<Message>> reply;
   bool stop = false;
+  std::chrono::steady_clock::time_point enq{};  // Post time (mailbox latency)
 };
+
+// Introspection (reference pprof + master/pkg/actor/trace.go): per-actor mailbox and processing
+// statistics, and a ring of the most recent processed messages across the system.
+struct CellStats {
+  std::string address;
+  size_t mailbox = 0;       // current depth
+  size_t max_mailbox = 0;   // high-water mark
+  uint64_t processed = 0;
+  double busy_ms = 0;       // total time inside Receive
+  double max_ms = 0;        // slowest Receive
+  double wait_ms = 0;       // total time messages sat in the mailbox
+  double max_wait_ms = 0;
+  uint64_t hist[16] = {0};  // Receive latency histogram: bucket b = [2^(b-1), 2^b) microseconds
+  std::map<std::string, uint64_t> by_type;
+};
+struct TraceRecord {
+  std::string address, type;
+  double wait_ms = 0, run_ms = 0;
+  int64_t at_ms = 0;  // unix ms when processing finished
+};
+std::string MessageTypeName(const Message& m);
 
 class Context {
  public:
@@ -137,6 +159,7 @@ class Cell : public std::enable_shared_from_this<Cell> {
   State state_ = State::Running;  // guarded by mu_ for readers; mutated by the worker
   std::map<std::string, Ref> children_;  // worker-only
   std::string error_;
+  CellStats stats_;  // guarded by mu_
 };
 
 class System {
@@ -148,6 +171,9 @@ class System {
   // Deliver msg to ref after delay (reference actors.NotifyAfter).
   void NotifyAfter(const Ref& ref, std::chrono::milliseconds delay, Message msg);
   void Shutdown();  // stop every top-level actor, then the workers
+  std::vector<CellStats> Stats() const;       // every live actor
+  std::vector<TraceRecord> Trace() const;     // most recent processed messages, oldest first
+  static constexpr size_t kTraceRing = 512;
 
  private:
   friend class Cell;
@@ -173,6 +199,10 @@ class System {
     Message msg;
     bool operator<(const Timer& o) const { return at != o.at ? at > o.at : seq > o.seq; }
   };
+  mutable std::mutex trace_mu_;
+  std::vector<TraceRecord> trace_;  // ring of kTraceRing
+  size_t trace_next_ = 0;
+  void Record(TraceRecord r);
   std::mutex tmu_;
   std::condition_variable tcv_;
   std::vector<Timer> timers_;  // heap

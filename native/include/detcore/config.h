@@ -42,8 +42,19 @@ struct MasterConfig {
   std::string telemetry_file;
   Json kubernetes;   // resource_manager {type: kubernetes, api_server, namespace, max_slots_per_pod, ...}; empty = agents
   Json provisioner;  // {max_instances, min_instances, slots_per_instance, ...}; empty = disabled  // security.authentication: tokens required on the REST API
+  // security.tls.{cert,key} (reference master/internal/config.go:118,249-260): PEM files; when both
+  // are set the REST/WebSocket API is served over TLS and tasks get DET_USE_TLS/DET_MASTER_CERT_FILE
+  std::string tls_cert, tls_key;
+  // task_container_defaults (reference master/pkg/model/task_container_defaults.go:19-70)
+  int64_t shm_size_bytes = 4294967296;  // 4 GiB, the reference default
+  std::string network_mode = "bridge";
+  std::string dtrain_network_interface;  // "" = auto-detect
+  std::string nccl_port_range, gloo_port_range;  // "MIN:MAX"
   static MasterConfig FromJson(const Json& j);
   Json ToJson() const;
+  std::vector<std::string> Validate() const;
+  // config keys DET_* environment variables may set beyond the defaults' leaves
+  static std::vector<std::string> EnvPaths();
 };
 
 }  // namespace detcore

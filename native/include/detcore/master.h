@@ -12,6 +12,8 @@
 //   including the experiment event log replayed on master restart.
 #pragma once
 
+#include <chrono>
+
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -59,6 +61,9 @@ class Master {
   LogStore& logs() { return *logs_; }
   actor::System& system() { return *sys_; }
   const MasterConfig& config() const { return cfg_; }
+  // task_container_defaults (+ TLS trust material) into a task's env / shipped files
+  void AddTaskDefaults(Json& env, Json& files) const;
+  bool tls() const { return !tls_cert_pem_.empty(); }
   actor::Ref Pool(const std::string& name);
   bool SendToAgent(const std::string& agent_id, const Json& msg);
   std::string AgentHost(const std::string& agent_id);
@@ -114,6 +119,8 @@ class Master {
   std::atomic<bool> shutting_down_{false};
   std::mutex telemetry_mu_;
   std::unique_ptr<KubernetesRM> kube_;
+  std::string tls_cert_pem_;  // security.tls.cert contents, shipped to tasks
+  std::chrono::steady_clock::time_point started_ = std::chrono::steady_clock::now();
 };
 
 // Helpers shared by the master translation units.

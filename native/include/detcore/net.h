@@ -1,6 +1,7 @@
 // Minimal HTTP/1.1 + WebSocket (RFC 6455) server and client over POSIX sockets for the control
 // plane (master REST API, master<->harness and master<->agent WebSockets).
-// No TLS; JSON bodies.  One thread per connection: the control plane carries tens of
+// Optional TLS (OpenSSL): HttpServer::EnableTls serves HTTPS/WSS; clients speak TLS to the
+// endpoints registered with RegisterTlsEndpoint (the agent -> master link).  JSON bodies.  One thread per connection: the control plane carries tens of
 // connections, not thousands.
 #pragma once
 
@@ -105,6 +106,9 @@ class HttpServer {
   void RouteWs(const std::string& pattern, WsHandler h);
   // Optional authorisation hook for plain HTTP routes: return false -> 401.
   void SetAuth(std::function<bool(const Request&)> auth) { auth_ = std::move(auth); }
+  // Serve every connection over TLS with this PEM certificate chain and key (call before Start).
+  bool EnableTls(const std::string& cert_file, const std::string& key_file, std::string* error);
+  bool tls() const { return tls_ctx_ != nullptr; }
   // Binds host:port (port 0 = ephemeral); returns the bound port.
   int Listen(const std::string& host, int port);
   void Start();  // accept loop on a background thread
@@ -135,6 +139,7 @@ class HttpServer {
   std::condition_variable conns_cv_;
   std::vector<int> conn_fds_;
   int active_conns_ = 0;
+  void* tls_ctx_ = nullptr;  // SSL_CTX*
 };
 
 // Client helpers.
@@ -150,6 +155,11 @@ ClientResponse HttpCall(const std::string& host, int port, const std::string& me
 WsPtr WsConnect(const std::string& host, int port, const std::string& path, std::string* error = nullptr);
 
 int ConnectTcp(const std::string& host, int port, int timeout_ms, std::string* error);
+// Client-side TLS for one endpoint: HttpCall / WsConnect to host:port then handshake TLS, verifying
+// the server against ca_file (a PEM bundle; the master's self-signed cert works), and the name
+// server_name when non-empty.
+bool RegisterTlsEndpoint(const std::string& host, int port, const std::string& ca_file, const std::string& server_name,
+                         std::string* error);
 std::string LocalIPForPeer(const std::string& host, int port);
 
 }  // namespace net

@@ -1,6 +1,12 @@
 // Actor runtime (see include/detcore/actor.h).
 #include "detcore/actor.h"
 
+#include <cxxabi.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 #include <algorithm>
 #include <exception>
 #include <stdexcept>
@@ -76,8 +82,20 @@ std::string Cell::error() const {
   return error_;
 }
 
+std::string MessageTypeName(const Message& m) {
+  const char* n = m.type().name();
+  int st = 0;
+  char* d = abi::__cxa_demangle(n, nullptr, nullptr, &st);
+  std::string out = (st == 0 && d) ? d : n;
+  std::free(d);
+  for (const char* pre : {"detcore::master::", "detcore::actor::", "detcore::"})
+    if (out.rfind(pre, 0) == 0) out = out.substr(std::strlen(pre));
+  return out;
+}
+
 void Cell::Post(Envelope e) {
   bool schedule = false;
+  e.enq = std::chrono::steady_clock::now();
   {
     std::lock_guard<std::mutex> g(mu_);
     if (state_ == State::Stopped) {
@@ -85,6 +103,7 @@ void Cell::Post(Envelope e) {
       return;
     }
     inbox_.push_back(std::move(e));
+    if (inbox_.size() > stats_.max_mailbox) stats_.max_mailbox = inbox_.size();
     if (!scheduled_) {
       scheduled_ = true;
       schedule = true;
@@ -150,7 +169,32 @@ void Cell::RunBatch() {
       e = std::move(inbox_.front());
       inbox_.pop_front();
     }
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string type = e.stop ? "Stop" : MessageTypeName(e.msg);
     Process(e);
+    const auto t1 = std::chrono::steady_clock::now();
+    const double run = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const double wait = e.enq.time_since_epoch().count() ? std::chrono::duration<double, std::milli>(t0 - e.enq).count() : 0.0;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      CellStats& st = stats_;
+      ++st.processed;
+      st.busy_ms += run;
+      st.max_ms = std::max(st.max_ms, run);
+      st.wait_ms += wait;
+      st.max_wait_ms = std::max(st.max_wait_ms, wait);
+      int b = 0;
+      for (double us = run * 1000.0; us >= 1.0 && b < 15; us /= 2) ++b;
+      ++st.hist[b];
+      ++st.by_type[type];
+    }
+    TraceRecord tr;
+    tr.address = address_;
+    tr.type = std::move(type);
+    tr.wait_ms = wait;
+    tr.run_ms = run;
+    tr.at_ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch()).count();
+    sys_->Record(std::move(tr));
   }
   bool again;
   {
@@ -350,6 +394,42 @@ void System::Shutdown() {
     if (w.joinable()) w.join();
   workers_.clear();
   if (timer_thread_.joinable()) timer_thread_.join();
+}
+
+void System::Record(TraceRecord r) {
+  std::lock_guard<std::mutex> g(trace_mu_);
+  if (trace_.size() < kTraceRing) {
+    trace_.push_back(std::move(r));
+  } else {
+    trace_[trace_next_] = std::move(r);
+  }
+  trace_next_ = (trace_next_ + 1) % kTraceRing;
+}
+
+std::vector<TraceRecord> System::Trace() const {
+  std::lock_guard<std::mutex> g(trace_mu_);
+  if (trace_.size() < kTraceRing) return trace_;
+  std::vector<TraceRecord> out(trace_.begin() + static_cast<long>(trace_next_), trace_.end());
+  out.insert(out.end(), trace_.begin(), trace_.begin() + static_cast<long>(trace_next_));
+  return out;
+}
+
+std::vector<CellStats> System::Stats() const {
+  std::vector<Ref> cells;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : registry_)
+      if (auto c = kv.second.lock()) cells.push_back(c);
+  }
+  std::vector<CellStats> out;
+  for (auto& c : cells) {
+    std::lock_guard<std::mutex> g(c->mu_);
+    CellStats s = c->stats_;
+    s.address = c->address_;
+    s.mailbox = c->inbox_.size();
+    out.push_back(std::move(s));
+  }
+  return out;
 }
 
 }  // namespace actor

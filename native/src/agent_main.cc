@@ -52,6 +52,9 @@ namespace {
 struct Options {
   std::string master_host = "127.0.0.1";
   int master_port = 8080;
+  // TLS to the master (reference agent --security-tls-*): verify its cert against this PEM
+  bool master_tls = false;
+  std::string master_cert_file, master_cert_name;
   std::string id;
   std::string pool;
   std::string label;
@@ -622,6 +625,9 @@ int main(int argc, char** argv) {
     else if (a == "--work-dir") o.work_dir = next();
     else if (a == "--framework-root") o.framework_root = next();
     else if (a == "--advertise-host") o.advertise_host = next();
+    else if (a == "--master-cert-file") o.master_cert_file = next();
+    else if (a == "--master-cert-name") o.master_cert_name = next();
+    else if (a == "--master-tls") o.master_tls = true;
     else if (a == "--no-zygote") o.zygote = false;
     else if (a == "--detect-only") {
       std::printf("%s\n", DetectDevices(o).dump().c_str());
@@ -630,12 +636,20 @@ int main(int argc, char** argv) {
       std::fprintf(stderr,
                    "usage: det-agent --master-host H --master-port P [--agent-id ID] [--resource-pool P]\n"
                    "                 [--label L] [--artificial-slots N] [--slot-type auto|gpu|cpu|none]\n"
-                   "                 [--visible-gpus 0,1] [--python PY] [--work-dir DIR] [--no-zygote] [--detect-only]\n");
+                   "                 [--visible-gpus 0,1] [--python PY] [--work-dir DIR] [--no-zygote] [--detect-only]\n"
+                   "                 [--master-tls] [--master-cert-file PEM] [--master-cert-name NAME]\n");
       return a == "-h" || a == "--help" ? 0 : 2;
     }
   }
   MkdirP(o.work_dir);
   signal(SIGPIPE, SIG_IGN);
+  if (o.master_tls || !o.master_cert_file.empty()) {
+    std::string err;
+    if (!net::RegisterTlsEndpoint(o.master_host, o.master_port, o.master_cert_file, o.master_cert_name, &err)) {
+      std::fprintf(stderr, "det-agent: %s\n", err.c_str());
+      return 2;
+    }
+  }
   Agent agent(o);
   g_agent = &agent;
   signal(SIGINT, OnSignal);

@@ -1,6 +1,9 @@
 // Experiment/master config (see include/detcore/config.h).
 #include "detcore/config.h"
 
+#include <cctype>
+#include <stdexcept>
+
 #include <algorithm>
 #include <set>
 
@@ -284,7 +287,57 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
   if (j["security"].is_object()) c.require_auth = j["security"].get_bool("authentication", c.require_auth);
   if (j["telemetry"].is_object() && j["telemetry"].get_bool("enabled", true))
     c.telemetry_file = j["telemetry"].get_string("file", "");
+  if (j["security"]["tls"].is_object()) {
+    c.tls_cert = j["security"]["tls"].get_string("cert", "");
+    c.tls_key = j["security"]["tls"].get_string("key", "");
+  }
+  const Json& tcd = j["task_container_defaults"];
+  if (tcd.is_object()) {
+    c.shm_size_bytes = tcd.get_int("shm_size_bytes", c.shm_size_bytes);
+    c.network_mode = tcd.get_string("network_mode", c.network_mode);
+    c.dtrain_network_interface = tcd.get_string("dtrain_network_interface", "");
+    c.nccl_port_range = tcd.get_string("nccl_port_range", "");
+    c.gloo_port_range = tcd.get_string("gloo_port_range", "");
+  }
+  auto errs = c.Validate();
+  if (!errs.empty()) {
+    std::string m = "invalid master config:";
+    for (auto& e : errs) m += " " + e + ";";
+    throw std::invalid_argument(m);
+  }
   return c;
+}
+
+static bool ValidPortRange(const std::string& r) {
+  if (r.empty()) return true;
+  auto colon = r.find(':');
+  if (colon == std::string::npos || colon == 0 || colon + 1 == r.size()) return false;
+  for (size_t i = 0; i < r.size(); ++i)
+    if (i != colon && !std::isdigit(static_cast<unsigned char>(r[i]))) return false;
+  const long lo = std::stol(r.substr(0, colon)), hi = std::stol(r.substr(colon + 1));
+  return lo <= hi && hi <= 65535;
+}
+
+std::vector<std::string> MasterConfig::Validate() const {
+  // reference TaskContainerDefaultsConfig.Validate + TLS pairing
+  std::vector<std::string> e;
+  if (shm_size_bytes < 0) e.push_back("task_container_defaults.shm_size_bytes must be >= 0");
+  if (network_mode.empty()) e.push_back("task_container_defaults.network_mode must be set");
+  if (!ValidPortRange(nccl_port_range)) e.push_back("task_container_defaults.nccl_port_range must be \"MIN:MAX\"");
+  if (!ValidPortRange(gloo_port_range)) e.push_back("task_container_defaults.gloo_port_range must be \"MIN:MAX\"");
+  if (tls_cert.empty() != tls_key.empty()) e.push_back("security.tls needs both cert and key");
+  if (port <= 0 || port > 65535) e.push_back("port must be in 1..65535");
+  return e;
+}
+
+std::vector<std::string> MasterConfig::EnvPaths() {
+  return {"security.tls.cert", "security.tls.key", "security.authentication", "task_container_defaults.shm_size_bytes",
+          "task_container_defaults.network_mode", "task_container_defaults.dtrain_network_interface",
+          "task_container_defaults.nccl_port_range", "task_container_defaults.gloo_port_range",
+          "checkpoint_storage.type", "checkpoint_storage.host_path", "checkpoint_storage.storage_path",
+          "checkpoint_storage.bucket", "checkpoint_storage.save_experiment_best",
+          "checkpoint_storage.save_trial_best", "checkpoint_storage.save_trial_latest", "telemetry.file",
+          "telemetry.enabled", "scheduler.type", "scheduler.fitting_policy", "resource_pools"};
 }
 
 Json MasterConfig::ToJson() const {
@@ -313,6 +366,17 @@ Json MasterConfig::ToJson() const {
   tel["enabled"] = !telemetry_file.empty();
   tel["file"] = telemetry_file;
   j["telemetry"] = tel;
+  Json tls = Json::object();
+  tls["cert"] = tls_cert;
+  tls["key"] = tls_key;
+  j["security"]["tls"] = tls;
+  Json tcd = Json::object();
+  tcd["shm_size_bytes"] = static_cast<long long>(shm_size_bytes);
+  tcd["network_mode"] = network_mode;
+  tcd["dtrain_network_interface"] = dtrain_network_interface;
+  tcd["nccl_port_range"] = nccl_port_range;
+  tcd["gloo_port_range"] = gloo_port_range;
+  j["task_container_defaults"] = tcd;
   return j;
 }
 

@@ -28,6 +28,8 @@
 //   WS     /ws/data-layer/*?read_lock=true|false   readers-writer lock per resource path (M24)
 #include "detcore/master.h"
 
+#include <dirent.h>
+
 #include <signal.h>
 #include <spawn.h>
 #include <sys/stat.h>
@@ -491,6 +493,81 @@ void Master::InstallRoutes() {
     return Err(404, "user not found");
   });
 
+  // ---------------------------------------------------------------- introspection (/debug)
+  // The reference exposes Go's pprof (master/internal/core.go:564-568) and actor message tracing
+  // (master/pkg/actor/trace.go:17-60).  Here: per-actor mailbox depth / high-water mark, message
+  // counts by type, Receive latency (total, max, log2-microsecond histogram) and mailbox wait, the
+  // ring of the last processed messages, and process-level stats from /proc.
+  http_.Route("GET", "/debug/actors", [this](const net::Request& r) {
+    const std::string prefix = r.Query("prefix", "");
+    auto stats = sys_->Stats();
+    std::sort(stats.begin(), stats.end(), [](const actor::CellStats& a, const actor::CellStats& b) {
+      return a.busy_ms > b.busy_ms;
+    });
+    Json out = Json::array();
+    for (auto& st : stats) {
+      if (!prefix.empty() && st.address.rfind(prefix, 0) != 0) continue;
+      Json a = Json::object();
+      a["address"] = st.address;
+      a["mailbox"] = static_cast<long long>(st.mailbox);
+      a["max_mailbox"] = static_cast<long long>(st.max_mailbox);
+      a["processed"] = static_cast<long long>(st.processed);
+      a["busy_ms"] = st.busy_ms;
+      a["max_ms"] = st.max_ms;
+      a["mean_ms"] = st.processed ? st.busy_ms / static_cast<double>(st.processed) : 0.0;
+      a["mean_wait_ms"] = st.processed ? st.wait_ms / static_cast<double>(st.processed) : 0.0;
+      a["max_wait_ms"] = st.max_wait_ms;
+      Json h = Json::object();
+      for (int b = 0; b < 16; ++b)
+        if (st.hist[b]) h[b == 0 ? std::string("<1us") : "<" + std::to_string(1LL << b) + "us"] = static_cast<long long>(st.hist[b]);
+      a["latency_histogram"] = h;
+      Json bt = Json::object();
+      for (auto& kv : st.by_type) bt[kv.first] = static_cast<long long>(kv.second);
+      a["messages"] = bt;
+      out.push_back(a);
+    }
+    return J(200, out);
+  });
+  http_.Route("GET", "/debug/trace", [this](const net::Request& r) {
+    const std::string prefix = r.Query("prefix", "");
+    Json out = Json::array();
+    for (auto& t : sys_->Trace()) {
+      if (!prefix.empty() && t.address.rfind(prefix, 0) != 0) continue;
+      Json e = Json::object();
+      e["address"] = t.address;
+      e["type"] = t.type;
+      e["wait_ms"] = t.wait_ms;
+      e["run_ms"] = t.run_ms;
+      e["at_ms"] = static_cast<long long>(t.at_ms);
+      out.push_back(e);
+    }
+    return J(200, out);
+  });
+  http_.Route("GET", "/debug/stats", [this](const net::Request&) {
+    Json out = Json::object();
+    std::ifstream st("/proc/self/status");
+    std::string line;
+    while (std::getline(st, line)) {
+      for (const char* k : {"Threads", "VmRSS", "VmHWM", "VmSize", "voluntary_ctxt_switches", "nonvoluntary_ctxt_switches"}) {
+        const std::string key = std::string(k) + ":";
+        if (line.rfind(key, 0) == 0) {
+          std::string v = line.substr(key.size());
+          v.erase(0, v.find_first_not_of(" \t"));
+          out[k] = v;
+        }
+      }
+    }
+    long fds = 0;
+    if (DIR* d = opendir("/proc/self/fd")) {
+      while (readdir(d)) ++fds;
+      closedir(d);
+    }
+    out["open_fds"] = static_cast<long long>(fds > 2 ? fds - 2 : fds);
+    out["uptime_s"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - started_).count();
+    out["actors"] = static_cast<long long>(sys_->Stats().size());
+    out["tls"] = tls();
+    return J(200, out);
+  });
   http_.Route("GET", "/info", [this](const net::Request&) {
     Json j = Json::object();
     j["cluster_id"] = cluster_id_;
@@ -1272,8 +1349,41 @@ void Master::RestoreExperiments() {
   }
 }
 
+void Master::AddTaskDefaults(Json& env, Json& files) const {
+  // task_container_defaults -> container env (reference master/pkg/tasks/task.go:224-248).  The agent
+  // runs tasks as process groups, not Docker containers: shm size and network mode are advisory here
+  // and exported for the task (and any container runtime wrapping the agent) to honour.
+  env["DET_TRIAL_RUNNER_NETWORK_INTERFACE"] =
+      cfg_.dtrain_network_interface.empty() ? "DET_AUTO_DETECT_NETWORK_INTERFACE" : cfg_.dtrain_network_interface;
+  if (!cfg_.dtrain_network_interface.empty()) {
+    env["NCCL_SOCKET_IFNAME"] = cfg_.dtrain_network_interface;  // RCCL bootstrap / socket transport
+    env["GLOO_SOCKET_IFNAME"] = cfg_.dtrain_network_interface;  // the gloo control plane
+  }
+  if (!cfg_.nccl_port_range.empty()) env["NCCL_PORT_RANGE"] = cfg_.nccl_port_range;
+  if (!cfg_.gloo_port_range.empty()) env["GLOO_PORT_RANGE"] = cfg_.gloo_port_range;
+  env["DET_SHM_SIZE_BYTES"] = std::to_string(cfg_.shm_size_bytes);
+  env["DET_NETWORK_MODE"] = cfg_.network_mode;
+  if (!tls_cert_pem_.empty()) {  // reference addTLSVars: tasks talk TLS to the master
+    env["DET_USE_TLS"] = "true";
+    env["DET_MASTER_CERT_FILE"] = ".det/master.crt";
+    Json f = Json::object();
+    f["path"] = ".det/master.crt";
+    f["content"] = net::Base64Encode(tls_cert_pem_);
+    files.push_back(f);
+  }
+}
+
 int Master::Start() {
   for (auto& p : cfg_.resource_pools) pools_[p] = sys_->ActorOf("pools/" + p, std::make_unique<ResourcePoolActor>(this, p));
+  if (!cfg_.tls_cert.empty()) {
+    std::string err;
+    if (!http_.EnableTls(cfg_.tls_cert, cfg_.tls_key, &err)) throw std::runtime_error(err);
+    std::ifstream f(cfg_.tls_cert);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    tls_cert_pem_ = ss.str();
+    Log("serving the API over TLS (" + cfg_.tls_cert + ")");
+  }
   InstallRoutes();
   port_ = http_.Listen(cfg_.listen_host, cfg_.port);
   if (port_ < 0) throw std::runtime_error("cannot bind port " + std::to_string(cfg_.port));

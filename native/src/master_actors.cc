@@ -633,7 +633,6 @@ void TrialActor::OnAllocated(Context& ctx, const ResourcesAllocated& ra) {
     int offset = c.devices.empty() ? 0 : *std::min_element(c.devices.begin(), c.devices.end());
     env["DET_TRIAL_UNIQUE_PORT_OFFSET"] = std::to_string(offset);
     env["DET_RENDEZVOUS_PORTS"] = std::to_string(1734 + offset) + "," + std::to_string(1734 + offset + 16);
-    env["DET_TRIAL_RUNNER_NETWORK_INTERFACE"] = "DET_AUTO_DETECT_NETWORK_INTERFACE";
     env["DET_NUM_CONTAINERS"] = std::to_string(order_.size());
     env["DET_CONTAINER_RANK"] = std::to_string(c.rank);
     env["DET_TOTAL_SLOTS"] = std::to_string(total);
@@ -648,9 +647,10 @@ void TrialActor::OnAllocated(Context& ctx, const ResourcesAllocated& ra) {
         if (eq != std::string::npos) env[s.substr(0, eq)] = s.substr(eq + 1);
       }
     };
+    Json files = Json::array();
+    m_->AddTaskDefaults(env, files);  // task_container_defaults first: the user's env wins
     if (ev.is_array()) add_env(ev);
     else if (ev.is_object()) add_env(ev[c.devices.empty() ? "cpu" : "gpu"]);
-    Json files = Json::array();
     const Json& latest = seq_->LatestCheckpoint();
     if (!latest.is_null() && latest.is_object() && latest.has("uuid")) {
       Json f = Json::object();
@@ -1088,6 +1088,8 @@ void CommandActor::Receive(Context& ctx) {
     Json env = Json::object();
     env["DET_TASK_ID"] = task_id_;
     env["DET_MASTER"] = m_->master_host() + ":" + std::to_string(m_->port());
+    Json files = Json::array();
+    m_->AddTaskDefaults(env, files);
     for (const Json* ev : {&config_["environment"]["environment_variables"], &secret_env_})
       if (ev->is_array())
         for (auto& kv : ev->as_array()) {
@@ -1097,7 +1099,7 @@ void CommandActor::Receive(Context& ctx) {
         }
     Json spec = Json::object();
     spec["env"] = env;
-    spec["files"] = Json::array();
+    spec["files"] = files;
     spec["cmd"] = config_["entrypoint"];
     spec["task_id"] = task_id_;
     spec["context_url"] = "/commands/" + std::to_string(id_) + "/context";

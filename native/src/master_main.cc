@@ -1,14 +1,23 @@
-// det-master entrypoint (reference master/cmd/determined-master/root.go): flags + optional JSON
-// config file (YAML configs are converted by the Python launcher `det-master` wrapper).
+// det-master entrypoint (reference master/cmd/determined-master/root.go + master/internal/config.go):
+// layered config, lowest to highest precedence:
+//   built-in defaults < config file (--config-file FILE.yaml|json, else /etc/determined/master.yaml
+//   when present, or $DET_MASTER_CONFIG_FILE) < DET_* environment (viper-style: security.tls.cert ->
+//   DET_SECURITY_TLS_CERT) < command-line flags.
 #include <signal.h>
+#include <unistd.h>
 
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <map>
 #include <sstream>
 #include <string>
 
+#include "detcore/config.h"
 #include "detcore/master.h"
+#include "detcore/yaml.h"
+
+extern char** environ;
 
 static detcore::master::Master* g_master = nullptr;
 
@@ -24,7 +33,8 @@ static void OnSignal(int) {
 
 static void Usage() {
   std::fprintf(stderr,
-               "usage: det-master [--config-file FILE.json] [--host H] [--port P] [--store-dir DIR]\n"
+               "usage: det-master [--config-file FILE.yaml|FILE.json] [--host H] [--port P] [--store-dir DIR]\n"
+               "                  [--tls-cert PEM --tls-key PEM]\n"
                "                  [--scheduler fair_share|priority|round_robin] [--fitting-policy best|worst]\n"
                "                  [--resource-pools a,b] [--checkpoint-host-path DIR] [--python PY]\n"
                "                  [--kubernetes-api HOST:PORT [--kubernetes-namespace NS]\n"
@@ -32,8 +42,29 @@ static void Usage() {
                "                   [--kubernetes-cpu-slots-per-node N] [--kubernetes-master-host H]]\n");
 }
 
+static detcore::Json LoadConfigFile(const std::string& path) {
+  std::ifstream f(path);
+  if (!f) {
+    std::fprintf(stderr, "cannot read config file %s\n", path.c_str());
+    std::exit(2);
+  }
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string text = ss.str();
+  size_t b = text.find_first_not_of(" \t\r\n");
+  try {
+    if (b != std::string::npos && text[b] == '{') return detcore::Json::parse(text);
+    detcore::Json j = detcore::ParseYaml(text);
+    return j.is_object() ? j : detcore::Json::object();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "config file %s: %s\n", path.c_str(), e.what());
+    std::exit(2);
+  }
+}
+
 int main(int argc, char** argv) {
-  detcore::Json cfgj = detcore::Json::object();
+  detcore::Json cfgj = detcore::Json::object();  // command-line flags (highest precedence)
+  std::string config_file;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -44,11 +75,11 @@ int main(int argc, char** argv) {
       return argv[++i];
     };
     if (a == "--config-file") {
-      std::ifstream f(next());
-      std::stringstream ss;
-      ss << f.rdbuf();
-      detcore::Json file = detcore::Json::parse(ss.str());
-      for (auto& kv : file.as_object()) cfgj[kv.first] = kv.second;
+      config_file = next();
+    } else if (a == "--tls-cert") {
+      cfgj["security"]["tls"]["cert"] = next();
+    } else if (a == "--tls-key") {
+      cfgj["security"]["tls"]["key"] = next();
     } else if (a == "--host") {
       cfgj["listen_host"] = next();
     } else if (a == "--port") {
@@ -108,6 +139,22 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
+  if (config_file.empty()) {
+    const char* e = std::getenv("DET_MASTER_CONFIG_FILE");
+    if (e && *e) config_file = e;
+    else if (access("/etc/determined/master.yaml", R_OK) == 0) config_file = "/etc/determined/master.yaml";
+  }
+  detcore::Json file = config_file.empty() ? detcore::Json::object() : LoadConfigFile(config_file);
+  std::map<std::string, std::string> env;
+  for (char** e = environ; e && *e; ++e) {
+    std::string kv = *e;
+    auto eq = kv.find('=');
+    if (eq != std::string::npos && kv.compare(0, 4, "DET_") == 0) env[kv.substr(0, eq)] = kv.substr(eq + 1);
+  }
+  const detcore::Json defaults = detcore::MasterConfig().ToJson();
+  const detcore::Json base = detcore::DeepMerge(defaults, file);
+  const detcore::Json envj = detcore::EnvOverlay(base, detcore::MasterConfig::EnvPaths(), env);
+  cfgj = detcore::DeepMerge(detcore::DeepMerge(base, envj), cfgj);
   signal(SIGPIPE, SIG_IGN);
   detcore::master::Master m(detcore::MasterConfig::FromJson(cfgj));
   g_master = &m;

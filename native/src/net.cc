@@ -17,6 +17,10 @@
 #include <cstring>
 #include <random>
 #include <sstream>
+#include <unordered_map>
+
+#include <openssl/err.h>
+#include <openssl/ssl.h>
 
 namespace detcore {
 namespace net {
@@ -120,8 +124,164 @@ std::string UrlDecode(const std::string& s) {
   return out;
 }
 
+// ---------------------------------------------------------------------------------------- TLS
+// TLS (reference master security.tls, master/internal/config.go:118,249-260): OpenSSL on the same
+// fd-based I/O.  A connection fd that carries TLS is registered here with its SSL object; the
+// socket is switched to non-blocking and every SSL call runs under the connection's mutex (an
+// SSL object must not be used from two threads at once, and a WebSocket is read on one thread
+// while other threads send), waiting in poll() -- never inside the lock -- for WANT_READ /
+// WANT_WRITE.  Plain fds take the old blocking send/recv paths untouched.
+namespace {
+struct TlsConn {
+  SSL* ssl = nullptr;
+  std::mutex mu;
+  int rcv_timeout_ms = -1;  // emulates SO_RCVTIMEO for client calls
+};
+std::mutex g_tls_mu;
+std::unordered_map<int, std::shared_ptr<TlsConn>> g_tls;
+struct TlsEndpoint {
+  SSL_CTX* ctx = nullptr;
+  std::string server_name;
+};
+std::mutex g_ep_mu;
+std::map<std::string, TlsEndpoint> g_endpoints;  // "host:port" -> client context
+
+std::shared_ptr<TlsConn> TlsOf(int fd) {
+  std::lock_guard<std::mutex> g(g_tls_mu);
+  auto it = g_tls.find(fd);
+  return it == g_tls.end() ? nullptr : it->second;
+}
+
+std::string SslErrors() {
+  std::string out;
+  unsigned long e;
+  char buf[256];
+  while ((e = ERR_get_error()) != 0) {
+    ERR_error_string_n(e, buf, sizeof(buf));
+    if (!out.empty()) out += "; ";
+    out += buf;
+  }
+  return out.empty() ? "tls error" : out;
+}
+
+// Run an SSL operation to completion on a non-blocking fd; >0 result, 0 = clean close, -1 = error
+// or timeout.
+template <typename F>
+int TlsCall(TlsConn* t, int fd, F op, int timeout_ms) {
+  for (;;) {
+    int r, err;
+    {
+      std::lock_guard<std::mutex> g(t->mu);
+      ERR_clear_error();
+      r = op(t->ssl);
+      if (r > 0) return r;
+      err = SSL_get_error(t->ssl, r);
+    }
+    short ev;
+    if (err == SSL_ERROR_WANT_READ) ev = POLLIN;
+    else if (err == SSL_ERROR_WANT_WRITE) ev = POLLOUT;
+    else if (err == SSL_ERROR_ZERO_RETURN) return 0;
+    else return -1;
+    pollfd p{fd, ev, 0};
+    int pr = poll(&p, 1, timeout_ms < 0 ? 1000 : timeout_ms);
+    if (pr < 0 && errno == EINTR) continue;
+    if (pr == 0 && timeout_ms >= 0) return -1;
+    if (pr > 0 && (p.revents & (POLLERR | POLLNVAL))) return -1;
+  }
+}
+
+bool AttachTls(int fd, SSL_CTX* ctx, bool server, const std::string& server_name, int timeout_ms, std::string* error) {
+  SSL* ssl = SSL_new(ctx);
+  if (!ssl) {
+    if (error) *error = SslErrors();
+    return false;
+  }
+  SSL_set_fd(ssl, fd);
+  if (!server && !server_name.empty()) {
+    SSL_set_tlsext_host_name(ssl, server_name.c_str());
+    SSL_set1_host(ssl, server_name.c_str());
+  }
+  fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK);
+  auto t = std::make_shared<TlsConn>();
+  t->ssl = ssl;
+  int r = TlsCall(t.get(), fd, [server](SSL* s) { return server ? SSL_accept(s) : SSL_connect(s); }, timeout_ms);
+  if (r <= 0) {
+    if (error) *error = "tls handshake failed: " + SslErrors();
+    SSL_free(ssl);
+    return false;
+  }
+  std::lock_guard<std::mutex> g(g_tls_mu);
+  g_tls[fd] = t;
+  return true;
+}
+}  // namespace
+
+static void CloseFd(int fd) {
+  std::shared_ptr<TlsConn> t;
+  {
+    std::lock_guard<std::mutex> g(g_tls_mu);
+    auto it = g_tls.find(fd);
+    if (it != g_tls.end()) {
+      t = it->second;
+      g_tls.erase(it);
+    }
+  }
+  if (t) {
+    std::lock_guard<std::mutex> g(t->mu);
+    SSL_shutdown(t->ssl);  // best effort close_notify; non-blocking
+    SSL_free(t->ssl);
+    t->ssl = nullptr;
+  }
+  ::close(fd);
+}
+
+bool RegisterTlsEndpoint(const std::string& host, int port, const std::string& ca_file, const std::string& server_name,
+                         std::string* error) {
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  if (!ctx) {
+    if (error) *error = SslErrors();
+    return false;
+  }
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  if (!ca_file.empty()) {
+    if (SSL_CTX_load_verify_locations(ctx, ca_file.c_str(), nullptr) != 1) {
+      if (error) *error = "cannot load CA file " + ca_file + ": " + SslErrors();
+      SSL_CTX_free(ctx);
+      return false;
+    }
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+  } else {
+    SSL_CTX_set_default_verify_paths(ctx);
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+  }
+  std::lock_guard<std::mutex> g(g_ep_mu);
+  TlsEndpoint& ep = g_endpoints[(host == "localhost" ? "127.0.0.1" : host) + ":" + std::to_string(port)];
+  if (ep.ctx) SSL_CTX_free(ep.ctx);
+  ep.ctx = ctx;
+  ep.server_name = server_name;
+  return true;
+}
+
+static SSL_CTX* EndpointCtx(const std::string& host, int port, std::string* name) {
+  std::lock_guard<std::mutex> g(g_ep_mu);
+  auto it = g_endpoints.find((host == "localhost" ? "127.0.0.1" : host) + ":" + std::to_string(port));
+  if (it == g_endpoints.end()) return nullptr;
+  *name = it->second.server_name;
+  return it->second.ctx;
+}
+
 // -------------------------------------------------------------------------------- socket utils
 static bool WriteAll(int fd, const char* p, size_t n) {
+  if (auto t = TlsOf(fd)) {
+    while (n > 0) {
+      const int chunk = static_cast<int>(std::min<size_t>(n, 1 << 20));
+      int w = TlsCall(t.get(), fd, [p, chunk](SSL* s) { return SSL_write(s, p, chunk); }, 30000);
+      if (w <= 0) return false;
+      p += w;
+      n -= static_cast<size_t>(w);
+    }
+    return true;
+  }
   while (n > 0) {
     ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
     if (w < 0) {
@@ -134,12 +294,22 @@ static bool WriteAll(int fd, const char* p, size_t n) {
   return true;
 }
 
+// one read of at most n bytes: >0 bytes, 0 EOF, <0 error (recv semantics)
+static ssize_t RecvSome(int fd, char* buf, size_t n) {
+  if (auto t = TlsOf(fd)) {
+    const int want = static_cast<int>(std::min<size_t>(n, 1 << 20));
+    int r = TlsCall(t.get(), fd, [buf, want](SSL* s) { return SSL_read(s, buf, want); }, t->rcv_timeout_ms);
+    return r;
+  }
+  return ::recv(fd, buf, n, 0);
+}
+
 // Read into buf until it contains `delim`; returns false on EOF/error.
 static bool ReadUntil(int fd, std::string& buf, const std::string& delim, size_t max_bytes = 1 << 20) {
   char tmp[8192];
   while (buf.find(delim) == std::string::npos) {
     if (buf.size() > max_bytes) return false;
-    ssize_t r = ::recv(fd, tmp, sizeof(tmp), 0);
+    ssize_t r = RecvSome(fd, tmp, sizeof(tmp));
     if (r < 0 && errno == EINTR) continue;
     if (r <= 0) return false;
     buf.append(tmp, static_cast<size_t>(r));
@@ -151,12 +321,26 @@ static bool ReadN(int fd, std::string& buf, size_t n) {
   char tmp[65536];
   while (buf.size() < n) {
     size_t want = std::min(sizeof(tmp), n - buf.size());
-    ssize_t r = ::recv(fd, tmp, want, 0);
+    ssize_t r = RecvSome(fd, tmp, want);
     if (r < 0 && errno == EINTR) continue;
     if (r <= 0) return false;
     buf.append(tmp, static_cast<size_t>(r));
   }
   return true;
+}
+
+// Client connect: TCP, plus TLS when host:port was registered with RegisterTlsEndpoint.
+static int ConnectMaybeTls(const std::string& host, int port, int timeout_ms, std::string* error) {
+  int fd = ConnectTcp(host, port, timeout_ms, error);
+  if (fd < 0) return fd;
+  std::string name;
+  if (SSL_CTX* ctx = EndpointCtx(host, port, &name)) {
+    if (!AttachTls(fd, ctx, false, name, timeout_ms, error)) {
+      ::close(fd);
+      return -1;
+    }
+  }
+  return fd;
 }
 
 static std::string Lower(std::string s) {
@@ -315,7 +499,7 @@ void WsConn::Close() {
       WriteAll(fd_, f.data(), f.size());
     }
     ::shutdown(fd_, SHUT_RDWR);
-    ::close(fd_);
+    CloseFd(fd_);
   }
 }
 
@@ -482,6 +666,14 @@ Response HttpServer::Dispatch(Request req) const {
 }
 
 void HttpServer::Serve(int fd, std::string peer) {
+  if (tls_ctx_) {
+    std::string err;
+    if (!AttachTls(fd, static_cast<SSL_CTX*>(tls_ctx_), true, "", 10000, &err)) {
+      ::shutdown(fd, SHUT_RDWR);
+      ::close(fd);
+      return;
+    }
+  }
   std::string buf;
   for (;;) {
     if (!ReadUntil(fd, buf, "\r\n\r\n")) break;
@@ -592,7 +784,24 @@ void HttpServer::Serve(int fd, std::string peer) {
     if (!WriteAll(fd, out.data(), out.size()) || close_after) break;
   }
   ::shutdown(fd, SHUT_RDWR);
-  ::close(fd);
+  CloseFd(fd);
+}
+
+bool HttpServer::EnableTls(const std::string& cert_file, const std::string& key_file, std::string* error) {
+  SSL_CTX* ctx = SSL_CTX_new(TLS_server_method());
+  if (!ctx) {
+    if (error) *error = SslErrors();
+    return false;
+  }
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  if (SSL_CTX_use_certificate_chain_file(ctx, cert_file.c_str()) != 1 ||
+      SSL_CTX_use_PrivateKey_file(ctx, key_file.c_str(), SSL_FILETYPE_PEM) != 1 || SSL_CTX_check_private_key(ctx) != 1) {
+    if (error) *error = "cannot load TLS cert/key: " + SslErrors();
+    SSL_CTX_free(ctx);
+    return false;
+  }
+  tls_ctx_ = ctx;
+  return true;
 }
 
 // ------------------------------------------------------------------------------------- clients
@@ -614,23 +823,24 @@ std::string UrlEncode(const std::string& s) {
 ClientResponse HttpCall(const std::string& host, int port, const std::string& method, const std::string& path,
                         const std::string& body, int timeout_ms, const std::string& content_type) {
   ClientResponse out;
-  int fd = ConnectTcp(host, port, timeout_ms, &out.error);
+  int fd = ConnectMaybeTls(host, port, timeout_ms, &out.error);
   if (fd < 0) return out;
   timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
   setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  if (auto t = TlsOf(fd)) t->rcv_timeout_ms = timeout_ms;
   std::ostringstream os;
   os << method << " " << path << " HTTP/1.1\r\nHost: " << host << ":" << port
      << "\r\nConnection: close\r\nContent-Type: " << content_type << "\r\nContent-Length: " << body.size() << "\r\n\r\n"
      << body;
   std::string req = os.str();
   if (!WriteAll(fd, req.data(), req.size())) {
-    ::close(fd);
+    CloseFd(fd);
     out.error = "write failed";
     return out;
   }
   std::string buf;
   if (!ReadUntil(fd, buf, "\r\n\r\n")) {
-    ::close(fd);
+    CloseFd(fd);
     out.error = "no response";
     return out;
   }
@@ -653,15 +863,15 @@ ClientResponse HttpCall(const std::string& host, int port, const std::string& me
   else {
     char tmp[8192];
     ssize_t r;
-    while ((r = ::recv(fd, tmp, sizeof(tmp), 0)) > 0) buf.append(tmp, static_cast<size_t>(r));
+    while ((r = RecvSome(fd, tmp, sizeof(tmp))) > 0) buf.append(tmp, static_cast<size_t>(r));
   }
   out.body = buf;
-  ::close(fd);
+  CloseFd(fd);
   return out;
 }
 
 WsPtr WsConnect(const std::string& host, int port, const std::string& path, std::string* error) {
-  int fd = ConnectTcp(host, port, 10000, error);
+  int fd = ConnectMaybeTls(host, port, 10000, error);
   if (fd < 0) return nullptr;
   std::string key = Base64Encode(std::to_string(std::random_device{}()) + "detcore-ws-key!!");
   std::ostringstream os;
@@ -672,7 +882,7 @@ WsPtr WsConnect(const std::string& host, int port, const std::string& path, std:
   std::string buf;
   if (!WriteAll(fd, req.data(), req.size()) || !ReadUntil(fd, buf, "\r\n\r\n") || buf.find(" 101 ") == std::string::npos) {
     if (error) *error = "websocket upgrade failed: " + buf.substr(0, 64);
-    ::close(fd);
+    CloseFd(fd);
     return nullptr;
   }
   size_t he = buf.find("\r\n\r\n");

@@ -1,0 +1,176 @@
+"""Master operability (reference master/internal/config.go:24-86,118,249-260,
+master/pkg/model/task_container_defaults.go, master/pkg/tasks/task.go:224-248,
+harness/determined/exec/harness.py:161-163):
+
+  * a TLS cluster: det-master serves HTTPS/WSS with security.tls, the agent verifies it with
+    --master-cert-file, the trial harness reaches the master over TLS (DET_USE_TLS /
+    DET_MASTER_CERT_FILE shipped by the master) -- an experiment completes end to end, and plain
+    HTTP is refused;
+  * YAML master config layered under DET_* environment variables and flags;
+  * task_container_defaults turned into task environment variables;
+  * master introspection endpoints (/debug/actors, /debug/stats).
+"""
+import json
+import os
+import pathlib
+import subprocess
+import sys
+
+import pytest
+import requests
+
+from determined_1_amd.api import MasterClient, read_context
+from determined_1_amd.deploy import LocalCluster
+from determined_1_amd.deploy.local import free_port, native_binary
+
+FIXTURES = pathlib.Path(__file__).resolve().parent / "fixtures"
+NOOP = FIXTURES / "no_op"
+
+
+def _self_signed(tmp: pathlib.Path):
+    cert, key = tmp / "master.crt", tmp / "master.key"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(cert),
+                    "-days", "2", "-subj", "/CN=127.0.0.1", "-addext", "subjectAltName=IP:127.0.0.1"],
+                   check=True, capture_output=True)
+    return str(cert), str(key)
+
+
+def _noop(max_batches=4, env=None):
+    cfg = {"description": "ops", "entrypoint": "model_def:NoOpTrial",
+           "hyperparameters": {"global_batch_size": 4, "metrics_base": 0.9},
+           "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": max_batches}},
+           "scheduling_unit": 2}
+    if env:
+        cfg["environment"] = {"environment_variables": env}
+    return cfg
+
+
+def test_tls_cluster_runs_experiment(tmp_path, monkeypatch):
+    cert, key = _self_signed(tmp_path)
+    with LocalCluster(agents=1, slots_per_agent=1, log_dir=str(tmp_path), tick_ms=50, tls_cert=cert,
+                      tls_key=key) as c:
+        monkeypatch.setenv("DET_MASTER_CERT_FILE", cert)
+        assert c.address.startswith("https://")
+        with pytest.raises(requests.RequestException):
+            requests.get(f"http://127.0.0.1:{c.port}/info", timeout=3)
+        with pytest.raises(requests.exceptions.SSLError):  # untrusted without the cert
+            requests.get(f"https://127.0.0.1:{c.port}/info", timeout=3, verify=True)
+        cl = MasterClient(c.address)
+        eid = cl.create_experiment(_noop(), read_context(NOOP))["id"]
+        assert cl.wait_for_experiment(eid, timeout=240) == "COMPLETED"
+        trials = cl.experiment(eid)["trials"]
+        assert trials and trials[0]["state"] == "COMPLETED"
+        # the task environment carried the TLS trust material
+        logs = "\n".join(l["message"] for l in cl.get(f"/trials/{trials[0]['id']}/logs"))
+        assert "Traceback" not in logs
+
+
+def test_yaml_config_env_and_flag_layering(tmp_path):
+    cfg = tmp_path / "master.yaml"
+    cfg.write_text(f"""# master config (reference /etc/determined/master.yaml)
+port: 1            # overridden by --port
+scheduler:
+  type: priority
+  fitting_policy: worst
+resource_pools:
+  - default
+  - big
+checkpoint_storage:
+  type: shared_fs
+  host_path: {tmp_path}/ckpt
+  save_trial_best: 2
+task_container_defaults:
+  shm_size_bytes: 1073741824
+  network_mode: host
+  dtrain_network_interface: lo
+  nccl_port_range: "20000:20100"
+telemetry: {{enabled: false}}
+""")
+    port = free_port()
+    env = dict(os.environ, DET_SCHEDULER_FITTING_POLICY="best", DET_TASK_CONTAINER_DEFAULTS_GLOO_PORT_RANGE="30000:30100",
+               DET_CHECKPOINT_STORAGE_SAVE_TRIAL_BEST="5")
+    p = subprocess.Popen([native_binary("det-master"), "--config-file", str(cfg), "--host", "127.0.0.1", "--port",
+                          str(port), "--scheduler", "round_robin"], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT)
+    try:
+        import time
+
+        deadline = time.time() + 20
+        out = None
+        while time.time() < deadline:
+            try:
+                out = requests.get(f"http://127.0.0.1:{port}/api/v1/master/config", timeout=1).json()["config"]
+                break
+            except requests.RequestException:
+                time.sleep(0.1)
+        assert out is not None, p.stdout.read1().decode() if p.poll() is not None else "no master"
+        assert out["port"] == port                                   # flag > file
+        assert out["scheduler"]["type"] == "round_robin"             # flag > file
+        assert out["scheduler"]["fitting_policy"] == "best"          # env > file
+        assert out["resource_pools"] == ["default", "big"]           # file
+        assert out["checkpoint_storage"]["host_path"] == f"{tmp_path}/ckpt"
+        assert out["checkpoint_storage"]["save_trial_best"] == 5     # env (typed as an int) > file
+        tcd = out["task_container_defaults"]
+        assert tcd["shm_size_bytes"] == 1073741824 and tcd["network_mode"] == "host"
+        assert tcd["nccl_port_range"] == "20000:20100" and tcd["gloo_port_range"] == "30000:30100"
+    finally:
+        p.terminate()
+        p.wait(10)
+
+
+def test_invalid_task_container_defaults_rejected(tmp_path):
+    cfg = tmp_path / "bad.yaml"
+    cfg.write_text("task_container_defaults:\n  nccl_port_range: 5000-6000\n")
+    r = subprocess.run([native_binary("det-master"), "--config-file", str(cfg), "--port", str(free_port())],
+                       capture_output=True, text=True, timeout=20)
+    assert r.returncode != 0 and "nccl_port_range" in (r.stdout + r.stderr)
+
+
+def test_task_container_defaults_reach_the_task_env(tmp_path):
+    cfg = tmp_path / "m.yaml"
+    cfg.write_text("task_container_defaults:\n  dtrain_network_interface: lo\n  nccl_port_range: 21000:21010\n"
+                   "  gloo_port_range: 22000:22010\n  shm_size_bytes: 2147483648\n")
+    with LocalCluster(agents=1, slots_per_agent=1, log_dir=str(tmp_path), tick_ms=50,
+                      master_args=["--config-file", str(cfg)]) as c:
+        cl = MasterClient(c.address)
+        out = tmp_path / "env.json"
+        cmd = {"entrypoint": [sys.executable, "-c",
+                              "import json,os; json.dump({k: v for k, v in os.environ.items() "
+                              "if k.startswith(('NCCL_', 'GLOO_', 'DET_SHM', 'DET_NETWORK', 'DET_TRIAL_RUNNER'))}, "
+                              f"open({str(out)!r}, 'w'))"],
+               "resources": {"slots": 0}, "description": "env"}
+        cid = cl.post("/commands", {"config": cmd, "context": []})["id"]
+        import time
+
+        deadline = time.time() + 60
+        while time.time() < deadline and cl.get(f"/commands/{cid}")["state"] != "TERMINATED":
+            time.sleep(0.2)
+        env = json.loads(out.read_text())
+        assert env["NCCL_SOCKET_IFNAME"] == "lo" and env["GLOO_SOCKET_IFNAME"] == "lo"
+        assert env["NCCL_PORT_RANGE"] == "21000:21010" and env["GLOO_PORT_RANGE"] == "22000:22010"
+        assert env["DET_SHM_SIZE_BYTES"] == "2147483648" and env["DET_NETWORK_MODE"] == "bridge"
+
+
+def test_debug_introspection_endpoints(tmp_path):
+    """pprof / actor-trace analogue: per-actor mailbox and latency stats, the processed-message ring
+    and process stats."""
+    with LocalCluster(agents=1, slots_per_agent=1, log_dir=str(tmp_path), tick_ms=50) as c:
+        cl = MasterClient(c.address)
+        eid = cl.create_experiment(_noop(), read_context(NOOP))["id"]
+        assert cl.wait_for_experiment(eid, timeout=240) == "COMPLETED"
+        actors = cl.get("/debug/actors")
+        by_addr = {a["address"]: a for a in actors}
+        exp = by_addr.get(f"/experiments/{eid}")
+        pool = [a for a in actors if a["address"].startswith("/pools/")]
+        assert pool and pool[0]["processed"] > 0 and "SchedulerTick" in " ".join(pool[0]["messages"])
+        for a in actors:
+            assert a["mailbox"] >= 0 and a["max_mailbox"] >= a["mailbox"] and a["max_ms"] >= a["mean_ms"] >= 0
+            assert sum(a["latency_histogram"].values()) == a["processed"]
+        assert exp is None or exp["processed"] > 0  # a finished experiment's actor may be gone
+        only_pools = cl.get("/debug/actors", prefix="/pools")
+        assert only_pools and all(a["address"].startswith("/pools") for a in only_pools)
+        trace = cl.get("/debug/trace")
+        assert 0 < len(trace) <= 512 and all(t["run_ms"] >= 0 and t["type"] for t in trace)
+        assert [t["at_ms"] for t in trace] == sorted(t["at_ms"] for t in trace)
+        st = cl.get("/debug/stats")
+        assert int(st["Threads"]) > 1 and "kB" in st["VmRSS"] and st["open_fds"] > 0 and st["uptime_s"] > 0
