@@ -42,9 +42,9 @@ def c3x3(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     return conv(x)
 
 
-def c1x1(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+def c1x1(x: torch.Tensor, conv: nn.Conv2d, bn_exclusive: bool = False) -> torch.Tensor:
     if NATIVE_CONV1X1 and FUSED_BN:
-        return native_conv.conv1x1(x, conv)
+        return native_conv.conv1x1(x, conv, bn_exclusive=bn_exclusive)
     return conv(x)
 
 
@@ -53,7 +53,7 @@ def bn_relu_c1x1(x: torch.Tensor, bn_mod: BatchNormAct2d, conv: nn.Conv2d) -> to
     activation is never written to HBM; ``ops.conv.bn_relu_conv1x1``)."""
     if NATIVE_CONV1X1 and FUSED_BN and BN_PROLOGUE:
         return native_conv.bn_relu_conv1x1(x, bn_mod, conv)
-    return c1x1(bn_mod(x), conv)
+    return c1x1(bn_mod(x), conv, bn_exclusive=True)  # bn2's output feeds only conv3
 
 
 def bn(c: int, relu: bool) -> BatchNormAct2d:
@@ -66,6 +66,18 @@ def conv3x3(cin: int, cout: int, stride: int = 1, groups: int = 1, dilation: int
 
 def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+def _shortcut_linked(downsample: Optional[nn.Module], x: torch.Tensor) -> bool:
+    """True when ``x``'s shortcut consumer hands its gradient through the BN link, not autograd."""
+    from determined_1_amd.ops import norm as _norm
+
+    if not _norm.SHORTCUT_LINK:
+        return False
+    if downsample is None:
+        return True  # identity: bn3(..., idt, shortcut_link=True)
+    return (isinstance(downsample, nn.Sequential) and len(downsample) == 2
+            and isinstance(downsample[0], nn.Conv2d) and isinstance(downsample[1], BatchNormAct2d))
 
 
 def _shortcut(downsample: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -111,7 +123,9 @@ class Bottleneck(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
-        out = self.bn1(c1x1(x, self.conv1))
+        # x (the previous block's output) reaches autograd only through conv1: the shortcut's
+        # gradient is handed to its producer through the BN link (identity or _LinkedConv)
+        out = self.bn1(c1x1(x, self.conv1, bn_exclusive=FUSED_BN and _shortcut_linked(self.downsample, x)))
         out = bn_relu_c1x1(c3x3(out, self.conv2), self.bn2, self.conv3)
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
         return self.bn3(out, idt, shortcut_link=self.downsample is None)

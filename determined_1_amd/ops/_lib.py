@@ -85,6 +85,9 @@ _SIGNATURES = {
         c_int,
     ),
     # det_norm.hip: fused BatchNorm(+add)(+ReLU), channels_last
+    # stream, dtype, d, x, M, C, gamma, mean, rstd, psum, psumx, nrb, rpb, dx, dgamma, dbeta, coef
+    "det_bn_bwd_from_partials": ([c_void_p, c_int, c_void_p, c_void_p, c_i64, c_int] + [c_void_p] * 5 + [c_int, c_i64]
+                                 + [c_void_p] * 4, c_int),
     "det_bn_ws_elems": ([c_i64, c_int], c_i64),
     "det_bn_fin_ws_elems": ([c_int], c_i64),
     # stream, dtype, x, res, y, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
@@ -136,6 +139,8 @@ _SIGNATURES = {
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
     "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4, c_int),
     "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),
+    # stream, A, B, C, M, N, K, x, mean, scale, shift, mbits, add, psum, psumx, mode
+    "det_conv_nt_bnbwd": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 8 + [c_int], c_int),
     # det_igemm.hip: pipelined implicit-GEMM conv (LDS-DMA ring)
     "det_igemm_rows_per_block": ([], c_int),
     # stream, X, W, Y, zero, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, pmean, pm2

@@ -239,13 +239,65 @@ def take_partials(x: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor,
     return p[1]
 
 
+# BatchNorm-backward fusion into the input-gradient GEMM of a 1x1 conv whose input is the output of
+# a fused training BatchNorm(+add)(+ReLU) that has no other autograd consumer (ResNet bottleneck
+# bn2 -> conv3; block output -> next block's conv1, whose identity / projection shortcut gradient
+# arrives through the BN link).  The dgrad epilogue applies the ReLU mask (and adds the shortcut
+# gradient), writes that masked gradient d and the BN's backward partial sums, so the BN backward
+# is finalize + an unmasked apply and d doubles as the shortcut's gradient (det_conv_nt_bnbwd,
+# det_bn_bwd_from_partials).  False: the separate partial pass (A/B).
+FUSE_BN_BWD = True
+BN_BWD_COUNTS = {"fused": 0, "unfused": 0}
+
+
+def _bn_producer(x: torch.Tensor):
+    """The fused-BN autograd node that produced ``x`` (None if not such an output)."""
+    from determined_1_amd.ops.norm import _BNActTrain
+
+    gf = x.grad_fn
+    return gf if isinstance(gf, _BNActTrain._backward_cls) else None
+
+
+def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) -> Optional[torch.Tensor]:
+    """dgrad with the producer BN's backward partials in the epilogue, or None when the producer
+    cannot take it (no ReLU, the shortcut gradient not in yet, already fused, layout/dtype)."""
+    mode = getattr(prod, "mask_mode", 0)
+    if mode not in (1, 2) or getattr(prod, "fused_bwd", None) is not None:
+        return None
+    if mode == 2 and getattr(prod, "extra_dy", None) is None:
+        return None  # the identity/projection shortcut gradient has not been linked yet
+    try:
+        xb, mbits, _, stats = prod.saved_tensors
+    except RuntimeError:
+        return None
+    if xb.dtype != torch.bfloat16 or xb.numel() != m * c or not xb.is_contiguous(memory_format=torch.channels_last):
+        return None
+    add = prod.extra_dy if mode == 2 else None
+    if add is not None and (add.dtype != torch.bfloat16 or not add.is_contiguous(memory_format=torch.channels_last)):
+        return None
+    rpb = rows_per_block(c)
+    nrb = (m + rpb - 1) // rpb
+    psum = torch.empty(nrb, c, dtype=torch.float32, device=dy2d.device)
+    psumx = torch.empty(nrb, c, dtype=torch.float32, device=dy2d.device)
+    d = torch.empty(m, c, dtype=torch.bfloat16, device=dy2d.device)
+    _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
+        _stream(dy2d), dy2d.data_ptr(), wt.data_ptr(), d.data_ptr(), int(m), int(c), int(wt.shape[1]), xb.data_ptr(),
+        stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits), _ptr(add), psum.data_ptr(),
+        psumx.data_ptr(), int(mode)), "conv_nt_bnbwd")
+    prod.fused_bwd = (psum, psumx, rpb)
+    if mode == 2:
+        prod.extra_dy = None  # consumed: summed into d
+    return d
+
+
 class _Conv1x1(torch.autograd.Function):
     """``conv2d(x, w)`` for a 1x1 stride-1 kernel as det_conv GEMMs: forward with the output's
-    BatchNorm statistics in the epilogue, dgrad through the transposed weight, split-M wgrad that
+    BatchNorm statistics in the epilogue, dgrad through the transposed weight (with the input's
+    BatchNorm-backward partials in its epilogue when ``bn_producer`` is given), split-M wgrad that
     writes the weight gradient straight into its arena slot when the parameter has one."""
 
     @staticmethod
-    def forward(ctx, x, weight, stats):
+    def forward(ctx, x, weight, stats, bn_producer=None):
         n, c, h, w_ = x.shape
         cout = weight.shape[0]
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # channels_last: a free view
@@ -255,6 +307,7 @@ class _Conv1x1(torch.autograd.Function):
         y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
         _attach_partials(y, parts)
         ctx.save_for_backward(x, weight)
+        ctx.bn_producer = bn_producer
         return y
 
     @staticmethod
@@ -265,9 +318,16 @@ class _Conv1x1(torch.autograd.Function):
         dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)
         dx = dw = None
+        prod, ctx.bn_producer = ctx.bn_producer, None
         if ctx.needs_input_grad[0]:
             wt = weight.reshape(cout, c).to(torch.bfloat16).t().contiguous()
-            dx2, _ = conv1x1_nt(dy2, wt)
+            dx2 = _fused_bn_dgrad(prod, dy2, wt, n * h * w_, c) if (prod is not None and is_gpu(dy2)) else None
+            if dx2 is None:
+                dx2, _ = conv1x1_nt(dy2, wt)
+                if prod is not None:
+                    BN_BWD_COUNTS["unfused"] += 1
+            else:
+                BN_BWD_COUNTS["fused"] += 1
             dx = dx2.view(n, h, w_, c).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             from determined_1_amd.ops.arena import landing_buffer
@@ -281,7 +341,7 @@ class _Conv1x1(torch.autograd.Function):
             conv1x1_wgrad(dy2, x2, dw.view(cout, c))
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class _BNReluConv1x1(torch.autograd.Function):
@@ -596,9 +656,11 @@ def bn_relu_conv1x1(x: torch.Tensor, bn_mod: torch.nn.modules.batchnorm._BatchNo
                                     bn_mod.num_batches_tracked, bn_mod.momentum, bn_mod.eps, w)
 
 
-def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_exclusive: bool = False) -> torch.Tensor:
     """``conv_mod(x)``; takes the native GEMM path for bias-free 1x1 stride-1 convs on channels_last
-    bf16 CUDA activations (channels % 64 == 0), else the module itself."""
+    bf16 CUDA activations (channels % 64 == 0), else the module itself.  ``bn_exclusive``: the
+    caller guarantees this conv is the only autograd consumer of ``x`` (shortcut consumers go
+    through the BN link), which allows the BN-backward fusion into the dgrad (``FUSE_BN_BWD``)."""
     w = conv_mod.weight
     ok = (ENABLED and x.device.type == "cuda" and x.dim() == 4 and conv_mod.bias is None
           and conv_mod.kernel_size == (1, 1) and conv_mod.stride == (1, 1) and conv_mod.groups == 1
@@ -614,5 +676,6 @@ def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> t
     COUNTS["native"] += 1
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
+    prod = _bn_producer(x) if (bn_exclusive and FUSE_BN_BWD and torch.is_grad_enabled()) else None
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1.apply(x, w, stats)
+        return _Conv1x1.apply(x, w, stats, prod)

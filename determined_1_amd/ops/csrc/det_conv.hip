@@ -121,6 +121,25 @@ __device__ __forceinline__ us8 affine_relu8(us8 v, const float* __restrict__ sca
   return o;
 }
 
+// BN-backward epilogue of an input-gradient GEMM whose output feeds a training BatchNorm's backward
+// (C = dL/dy of y = act(bn(x) [+ res])):  d = mask * (C [+ add]) is written instead of C, and the
+// BN's backward partial sums over this block's rows, psum = sum d and psumx = sum d (x - mean), go
+// to [ceil(M/BM), N] -- the BN backward then needs only its finalize and an unmasked apply
+// (det_norm.hip det_bn_bwd_from_partials), and with an identity shortcut d IS the residual's
+// gradient, so that pass writes no second tensor.  mode 1: mask = (x*scale + shift > 0);
+// mode 2: mask bits of the forward (1 bit per element, with the residual in the sum).
+struct BnBwdEpi {
+  const unsigned short* x;     // BN input [M, N]
+  const float* mean;           // [N]
+  const float* scale;          // mode 1
+  const float* shift;
+  const uint8_t* mbits;        // mode 2: [M*N/8]
+  const unsigned short* add;   // nullable: identity-shortcut gradient summed before the mask
+  float* psum;
+  float* psumx;
+  int mode;
+};
+
 struct NtArgs {
   const unsigned short* A;  // [rows, K]
   const unsigned short* B;  // [N, K]
@@ -132,6 +151,7 @@ struct NtArgs {
   float* pmean;  // STATS: [ceil(M/BM), N] block mean / M2 of the bf16-rounded C
   float* pm2;
   Gather g;  // STRIDE2
+  BnBwdEpi bn;  // BNB
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -140,7 +160,7 @@ struct NtArgs {
 // OCC: workgroups per CU the register budget is sized for.  K == 64 (one K tile: layer1's
 // 64-channel side, every dgrad into a 64-channel input) is a pure streaming pass with no K loop
 // to overlap loads with, so it runs single-buffered (half the LDS) at higher occupancy instead.
-template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC>
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false>
 __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
@@ -309,6 +329,64 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
     a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
   }
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
+  if constexpr (BNB) {
+    // each thread owns one 8-column chunk (kThreads % CPR == 0) over rows tid/CPR + q*kThreads/CPR
+    static_assert(kThreads % CPR == 0, "fixed chunk column per thread");
+    const int cc = tid % CPR;
+    const int c0 = n0 + cc * 8;
+    float mu[8], sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = a.bn.mean[c0 + j];
+      sc[j] = a.bn.mode == 1 ? a.bn.scale[c0 + j] : 0.f;
+      sh[j] = a.bn.mode == 1 ? a.bn.shift[c0 + j] : 0.f;
+      s1[j] = 0.f;
+      s2[j] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < BM * CPR / kThreads; ++q) {
+      const int row = (tid + q * kThreads) / CPR;
+      if (row >= nvalid) continue;
+      const int64_t off = (m0 + row) * a.N + c0;
+      const us8 cv = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+      const us8 xv = *reinterpret_cast<const us8*>(a.bn.x + off);
+      us8 av = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (a.bn.add) av = *reinterpret_cast<const us8*>(a.bn.add + off);
+      const unsigned bits = a.bn.mode == 2 ? a.bn.mbits[off >> 3] : 0u;
+      us8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xf = bf2f(xv[j]);
+        float d = bf2f(cv[j]) + (a.bn.add ? bf2f(av[j]) : 0.f);
+        const bool on = a.bn.mode == 2 ? ((bits >> j) & 1u) != 0 : __fmaf_rn(xf, sc[j], sh[j]) > 0.f;
+        d = on ? d : 0.f;
+        o[j] = f2bf(d);
+        const float dr = bf2f(o[j]);  // the sums see exactly what the BN apply reads back
+        s1[j] += dr;
+        s2[j] += dr * (xf - mu[j]);
+      }
+      *reinterpret_cast<us8*>(a.C + off) = o;
+    }
+    float* scratch = reinterpret_cast<float*>(smem + BM * LDC * 2);  // [kThreads][16], past the C tile
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      scratch[tid * 16 + j] = s1[j];
+      scratch[tid * 16 + 8 + j] = s2[j];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int ccol = tid / 8, j = tid % 8;
+      float t1 = 0.f, t2 = 0.f;
+      for (int g = 0; g < kThreads / CPR; ++g) {
+        t1 += scratch[(g * CPR + ccol) * 16 + j];
+        t2 += scratch[(g * CPR + ccol) * 16 + 8 + j];
+      }
+      a.bn.psum[static_cast<int64_t>(mt) * a.N + n0 + tid] = t1;
+      a.bn.psumx[static_cast<int64_t>(mt) * a.N + n0 + tid] = t2;
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < BM * CPR / kThreads; ++q) {
     const int idx = tid + q * kThreads;
@@ -540,11 +618,17 @@ constexpr int nt_smem() {
 }
 
 template <int BM, int BN, int WM, int WN, int OCC>
-int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2) {
+int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2, bool bnb = false) {
   const int64_t mtiles = (a.M + BM - 1) / BM;
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int smem = nt_smem<BM, BN, OCC == 2 ? 2 : 1>();
+  if (bnb) {  // input-gradient GEMM with the BN-backward epilogue (no prologue / stats / gather)
+    constexpr int smem_b = smem > BM * (BN + 16) * 2 + kThreads * 16 * 4 ? smem : BM * (BN + 16) * 2 + kThreads * 16 * 4;
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true>),
+                       dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
+    return static_cast<int>(hipGetLastError());
+  }
 #define DET_NT(P, S, G)                                                                               \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G, OCC>), dim3(static_cast<unsigned>(nwg)), \
                      dim3(kThreads), smem, st, a)
@@ -598,6 +682,27 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
   }
   if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, pro, stats, stride2);
   return launch_nt<128, 64, 2, 2, 2>(st, a, pro, stats, stride2);
+}
+
+// dX[M, N] = dY[M, K] . W^T[N, K]^T with the BN-backward epilogue (BnBwdEpi above): writes
+// d = mask * (dX [+ add]) and the BN's backward partials psum / psumx [ceil(M/128), N].
+// mode 1: x, mean, scale, shift; mode 2: x, mean, mbits (add nullable).
+int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
+                      const float* mean, const float* scale, const float* shift, const void* mbits, const void* add,
+                      float* psum, float* psumx, int mode) {
+  if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
+  if (!x || !mean || !psum || !psumx || (mode == 1 && (!scale || !shift)) || (mode == 2 && !mbits) || mode < 1 || mode > 2)
+    return -2;
+  NtArgs a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C),
+           M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}, BnBwdEpi{static_cast<const unsigned short*>(x), mean, scale,
+           shift, static_cast<const uint8_t*>(mbits), static_cast<const unsigned short*>(add), psum, psumx, mode}};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (K == kBK) {
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, true);
+    return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, true);
+  }
+  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, false, false, false, true);
+  return launch_nt<128, 64, 2, 2, 2>(st, a, false, false, false, true);
 }
 
 // fp32 workspace elements det_conv_tn needs (slabs) for an [N, K] output from M rows.

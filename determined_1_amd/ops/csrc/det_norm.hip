@@ -832,6 +832,37 @@ int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* 
 // add over the whole activation (read 2, write 1) before this backward.
 // dres may be null.
 // dgamma/dbeta may be null.  ws >= det_bn_ws_elems(M, C).
+// BatchNorm backward whose partial sums (psum = sum d, psumx = sum d * (x - mean) over row-blocks of
+// rpb rows, [nrb, C]) were produced by the epilogue of the GEMM that computed d (the dgrad of the
+// consuming conv, with the ReLU mask and the identity-shortcut gradient already applied:
+// det_conv_nt's BN-backward epilogue).  Runs the finalize and an unmasked apply: dx = A d + B x + C.
+int det_bn_bwd_from_partials(void* stream, int dtype, const void* d, const void* x, int64_t M, int C, const float* gamma,
+                             const float* save_mean, const float* save_rstd, const float* psum, const float* psumx,
+                             int nrb, int64_t rpb, void* dx, float* dgamma, float* dbeta, float* coef) {
+  if (C % 8 != 0 || M <= 0 || nrb <= 0) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Geom g = make_geom(M, C);
+  g.nrb = nrb;
+  g.rpb = rpb;
+  BwdFin bf{gamma, save_rstd, save_mean, dgamma, dbeta, coef};
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, psum, psumx, g, bf);
+  const int64_t nvec = M * C / 8;
+  const int grid2 = apply_grid(nvec, 2);
+  if (dtype == 1)
+    hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false>), dim3(grid2), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(d), static_cast<const unsigned short*>(nullptr),
+                       static_cast<const unsigned short*>(x), static_cast<const uint8_t*>(nullptr), coef,
+                       static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
+                       static_cast<unsigned short*>(dx), static_cast<unsigned short*>(nullptr), nvec, C);
+  else
+    hipLaunchKernelGGL((bn_apply_bwd<float, 0, false>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
+                       static_cast<const float*>(nullptr), static_cast<const float*>(x),
+                       static_cast<const uint8_t*>(nullptr), coef, static_cast<const float*>(nullptr),
+                       static_cast<const float*>(nullptr), static_cast<float*>(dx), static_cast<float*>(nullptr), nvec, C);
+  return static_cast<int>(hipGetLastError());
+}
+
 int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const void* x, const void* mbits, int64_t M, int C,
                int mask_mode, const float* gamma, const float* save_mean, const float* save_rstd,
                const float* scale, const float* shift, void* dx, void* dres, float* dgamma, float* dbeta,

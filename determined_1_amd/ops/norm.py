@@ -129,21 +129,39 @@ class _BNActTrain(torch.autograd.Function):
         dy2, ctx.extra_dy = ctx.extra_dy, None
         dx = torch.empty_like(x, memory_format=ctx.fmt)
         want_res = ctx.has_res and (ctx.needs_input_grad[1] or ctx.link is not None)
-        dres = torch.empty_like(x, memory_format=ctx.fmt) if want_res else None
         dgb = None
         if weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
             dgb = torch.empty((2, C), dtype=torch.float32, device=x.device)
-        ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
-        _lib.check(
-            lib.det_bn_bwd(
-                _stream(x), _DT[x.dtype], dy.data_ptr(), _ptr(dy2), x.data_ptr(), _ptr(mbits), M, C, ctx.mask_mode,
-                _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
-                dx.data_ptr(), _ptr(dres),
-                None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(),
-                ws.data_ptr(),
-            ),
-            "bn_bwd",
-        )
+        fused, ctx.fused_bwd = getattr(ctx, "fused_bwd", None), None
+        if fused is not None:
+            # the consuming conv's dgrad epilogue already masked dy (and summed the shortcut
+            # gradient into it) and wrote the partial sums: finalize + unmasked apply; the masked
+            # gradient is also the residual's gradient (no second tensor)
+            assert dy2 is None, "shortcut gradient arrived after the fused dgrad consumed it"
+            psum, psumx, rpb = fused
+            coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+            _lib.check(
+                lib.det_bn_bwd_from_partials(
+                    _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), M, C, _ptr(weight), stats[0].data_ptr(),
+                    stats[1].data_ptr(), psum.data_ptr(), psumx.data_ptr(), int(psum.shape[0]), int(rpb),
+                    dx.data_ptr(), None if dgb is None else dgb[0].data_ptr(),
+                    None if dgb is None else dgb[1].data_ptr(), coef.data_ptr()),
+                "bn_bwd_from_partials",
+            )
+            dres = dy if want_res else None
+        else:
+            dres = torch.empty_like(x, memory_format=ctx.fmt) if want_res else None
+            ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
+            _lib.check(
+                lib.det_bn_bwd(
+                    _stream(x), _DT[x.dtype], dy.data_ptr(), _ptr(dy2), x.data_ptr(), _ptr(mbits), M, C, ctx.mask_mode,
+                    _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
+                    dx.data_ptr(), _ptr(dres),
+                    None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(),
+                    ws.data_ptr(),
+                ),
+                "bn_bwd",
+            )
         _dbg("bwd", x)
         if ctx.has_res and dres is None and ctx.needs_input_grad[1]:
             raise RuntimeError("residual grad requested but not produced")
