@@ -31,15 +31,50 @@ def test_webui_served_and_its_api_calls_exist(tmp_path):
                                    read_context(NOOP))["id"]
         assert cl.wait_for_experiment(eid, timeout=120) == "COMPLETED"
         tid = cl.experiment(eid)["trials"][0]["id"]
+        # the mutations the page issues: create a model, register a checkpoint (registerCheckpoint),
+        # archive / unarchive (act), kill a trial (killTrial)
+        ck = requests.get(base + f"/api/v1/experiments/{eid}/checkpoints", headers=h).json()["checkpoints"]
+        assert ck, "the no-op trial checkpoints at the end"
+        assert requests.post(base + "/api/v1/models/ui-model", json={"description": "from the UI"},
+                             headers=h).status_code == 200
+        r = requests.post(base + "/api/v1/models/ui-model/versions", json={"checkpointUuid": ck[0]["uuid"]}, headers=h)
+        assert r.status_code == 200 and r.json()["modelVersion"]["version"] == 1
+        vers = requests.get(base + "/api/v1/models/ui-model/versions", headers=h).json()
+        assert vers["modelVersions"][0]["checkpoint"]["uuid"] == ck[0]["uuid"]
+        for verb in ("archive", "unarchive"):
+            assert requests.post(base + f"/api/v1/experiments/{eid}/{verb}", headers=h).status_code == 200
+        assert requests.post(base + f"/api/v1/trials/{tid}/kill", headers=h).status_code in (200, 409)
         js = WEBUI.read_text()
+        for route in ("#/models", "#/compare/", "checkpointTable", "compareSelected", "registerCheckpoint", "killTrial"):
+            assert route in js
         paths = set(re.findall(r'[`"](/api/v1/[^`"?]*)', js))
         assert len(paths) >= 10, paths
         for p in sorted(paths):
-            concrete = re.sub(r"\$\{[^}]*\}", lambda m: {"${kind}": "commands", "${verb}": "archive"}.get(
+            concrete = re.sub(r"\$\{[^}]*\}", lambda m: {"${kind}": "commands", "${verb}": "archive",
+                                                           "${encodeURIComponent(name)}": "ui-model"}.get(
                 m.group(0), str(tid) if "/trials/" in p and "experiments" not in p else str(eid)), p)
-            if "metrics-stream" in p or "/logs" in p or "auth/login" in p or "/archive" in concrete:
-                continue  # streams and mutations are covered by tests/test_api_v1.py
+            if "metrics-stream" in p or "/logs" in p or "auth/login" in p or "/archive" in concrete or p.endswith("/kill"):
+                continue  # streams and mutations are covered above and by tests/test_api_v1.py
             r = requests.get(base + concrete, headers=h, timeout=10)
             assert r.status_code == 200, (p, concrete, r.status_code, r.text[:200])
         # without a token the API refuses, so the page falls back to its login form
         assert requests.get(base + "/api/v1/experiments", timeout=10).status_code == 401
+
+
+def test_webui_script_parses(tmp_path):
+    """The page script is syntactically valid JavaScript (node --check; this image's node 12 lacks
+    ``??``, which every supported browser has, so it is rewritten for the check only)."""
+    import shutil
+    import subprocess
+
+    node = shutil.which("node") or shutil.which("nodejs")
+    if node is None:
+        import pytest
+
+        pytest.skip("node not installed")
+    html = WEBUI.read_text()
+    js = html[html.index("<script>") + len("<script>"):html.index("</script>")].replace("??", "||")
+    f = tmp_path / "ui.js"
+    f.write_text(js)
+    r = subprocess.run([node, "--check", str(f)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
