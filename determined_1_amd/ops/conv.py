@@ -247,6 +247,7 @@ def take_partials(x: torch.Tensor) -> Optional[Tuple[torch.Tensor, torch.Tensor,
 # is finalize + an unmasked apply and d doubles as the shortcut's gradient (det_conv_nt_bnbwd,
 # det_bn_bwd_from_partials).  False: the separate partial pass (A/B).
 FUSE_BN_BWD = True
+FUSE_BN_BWD_MODES = (1, 2)  # 1: ReLU mask from x (bn2 -> conv3); 2: forward mask bits + shortcut gradient
 BN_BWD_COUNTS = {"fused": 0, "unfused": 0}
 
 
@@ -262,7 +263,7 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) 
     """dgrad with the producer BN's backward partials in the epilogue, or None when the producer
     cannot take it (no ReLU, the shortcut gradient not in yet, already fused, layout/dtype)."""
     mode = getattr(prod, "mask_mode", 0)
-    if mode not in (1, 2) or getattr(prod, "fused_bwd", None) is not None:
+    if mode not in FUSE_BN_BWD_MODES or getattr(prod, "fused_bwd", None) is not None:
         return None
     if mode == 2 and getattr(prod, "extra_dy", None) is None:
         return None  # the identity/projection shortcut gradient has not been linked yet

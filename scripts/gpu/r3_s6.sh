@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/r3s6
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bn_bwd_fusion_gpu.py tests/test_conv_gpu.py tests/test_norm_gpu.py > gpurun_out/r3s6/pytest.log 2>&1 || { tail -40 gpurun_out/r3s6/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bn_bwd_fusion_gpu.py tests/test_conv_gpu.py tests/test_norm_gpu.py tests/test_conv3x3_gpu.py > gpurun_out/r3s6/pytest.log 2>&1 || { tail -40 gpurun_out/r3s6/pytest.log; exit 1; }
 tail -2 gpurun_out/r3s6/pytest.log
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 10 > gpurun_out/r3s6/bench.json 2> gpurun_out/r3s6/bench.err || { tail -30 gpurun_out/r3s6/bench.err; exit 1; }
 cat gpurun_out/r3s6/bench.json

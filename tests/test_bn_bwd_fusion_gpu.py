@@ -54,34 +54,74 @@ def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k):
     torch.testing.assert_close(psumx.double().sum(0).cpu(), sx_ref, rtol=1e-4, atol=1e-3)
 
 
-def test_resnet50_grads_with_and_without_bn_bwd_fusion(gpu):
-    """One backward of ResNet-50 (bf16, fused BN, native convs) from identical weights and data:
-    every parameter gradient with the fusion matches the unfused path."""
+def _ref_block(blk, x, weights):
+    """fp32 PyTorch composite of a Bottleneck (training-mode BN) with the given weights."""
+    import torch.nn.functional as F
+
+    def bn(t, name):
+        return F.batch_norm(t, None, None, weights[name + ".weight"], weights[name + ".bias"], True, 0.0, blk.bn1.eps)
+
+    out = F.relu(bn(F.conv2d(x, weights["conv1.weight"]), "bn1"))
+    out = F.relu(bn(F.conv2d(out, weights["conv2.weight"], stride=blk.conv2.stride, padding=1), "bn2"))
+    out = bn(F.conv2d(out, weights["conv3.weight"]), "bn3")
+    if blk.downsample is not None:
+        idt = bn(F.conv2d(x, weights["downsample.0.weight"], stride=blk.downsample[0].stride), "downsample.1")
+    else:
+        idt = x
+    return F.relu(out + idt)
+
+
+def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
+    """Stem-less chain of two ResNet bottlenecks (projection + identity shortcut) at a well-
+    conditioned batch-norm size: every gradient with the fusion (both mask modes exercised) and
+    without it against an fp32 PyTorch composite with the same weights.  (Run-to-run comparisons
+    of the whole network are not used: library kernels on the path are not bit-deterministic and
+    tiny late-layer BN batches amplify that.)"""
     from determined_1_amd.models import resnet
+    from determined_1_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(0)
+    stem_bn = BatchNormAct2d(64, relu=True, fused=True)
+    b0 = resnet.Bottleneck(64, 64, 1, torch.nn.Sequential(resnet.conv1x1(64, 256), resnet.bn(256, relu=False)))
+    b1 = resnet.Bottleneck(256, 64)
+    mods = torch.nn.ModuleList([stem_bn, b0, b1]).to(gpu).to(memory_format=torch.channels_last)
+    for mod in mods.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.to(torch.bfloat16)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    z = torch.randn(4, 64, 28, 28, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dout = torch.randn(4, 256, 28, 28, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     def run(fuse):
         conv.FUSE_BN_BWD = fuse
-        torch.manual_seed(0)
-        m = resnet.resnet50(num_classes=10, zero_init_residual=False).to(gpu).to(
-            memory_format=torch.channels_last).to(torch.bfloat16)
-        for mod in m.modules():
-            if isinstance(mod, torch.nn.BatchNorm2d):
-                mod.float()
-        g = torch.Generator(device="cpu").manual_seed(1)
-        x = torch.randn(4, 3, 64, 64, generator=g).to(gpu).to(torch.bfloat16).contiguous(
-            memory_format=torch.channels_last)
-        y = torch.randint(0, 10, (4,), generator=g).to(gpu)
-        loss = torch.nn.functional.cross_entropy(m(conv.pad_channels4(x)).float(), y)
-        loss.backward()
-        return {n: p.grad.float().clone() for n, p in m.named_parameters()}
+        for p in mods.parameters():
+            p.grad = None
+        zz = z.clone().requires_grad_(True)
+        out = b1(b0(stem_bn(zz)))
+        out.backward(dout)
+        return zz.grad.float().clone(), {n: p.grad.float().clone() for n, p in mods.named_parameters()}
 
     before = dict(conv.BN_BWD_COUNTS)
-    ref = run(False)
-    got = run(True)
+    dz_u, gr_u = run(False)
+    dz_f, gr_f = run(True)
     conv.FUSE_BN_BWD = True
-    fused = conv.BN_BWD_COUNTS["fused"] - before["fused"]
-    assert fused >= 16 + 12  # bn2 -> conv3 in all 16 blocks, block outputs -> next conv1 (>= 12 identity links)
-    for n in ref:
-        a, b = got[n], ref[n]
-        scale = float(b.abs().max()) + 1e-6
-        assert float((a - b).abs().max()) <= 0.05 * scale, (n, float((a - b).abs().max()), scale)
+    assert conv.BN_BWD_COUNTS["fused"] - before["fused"] >= 3  # bn2->conv3 x2, b0 output->b1.conv1 (mode 2)
+
+    # fp32 reference with the same (bf16-valued) weights
+    w = {n: p.detach().float().clone().requires_grad_(True) for n, p in mods.named_parameters()}
+    zr = z.float().clone().requires_grad_(True)
+    import torch.nn.functional as F
+
+    y = F.relu(F.batch_norm(zr, None, None, w["0.weight"], w["0.bias"], True, 0.0, stem_bn.eps))
+    y = _ref_block(b0, y, {k[2:]: v for k, v in w.items() if k.startswith("1.")})
+    y = _ref_block(b1, y, {k[2:]: v for k, v in w.items() if k.startswith("2.")})
+    y.backward(dout.float())
+    for tag, dz, gr in (("unfused", dz_u, gr_u), ("fused", dz_f, gr_f)):
+        err = float((dz - zr.grad).abs().max()) / float(zr.grad.abs().max())
+        assert err < 0.05, (tag, "input grad", err)
+        for n in gr:
+            ref = w[n].grad
+            e = float((gr[n] - ref).abs().max()) / (float(ref.abs().max()) + 1e-12)
+            assert e < 0.06, (tag, n, e)
+    # and the two native paths agree closer than either does with fp32
+    assert float((dz_f - dz_u).abs().max()) / float(dz_u.abs().max()) < 0.03
