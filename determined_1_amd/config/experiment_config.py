@@ -70,6 +70,7 @@ def default_experiment_config(experiment_seed: Optional[int] = None) -> Dict[str
             "grad_reduction": "fp32_accum",
             "rccl": {},
             "hip_graph": False,
+            "hip_graph_batches": 1,
         },
         "perform_initial_validation": False,
         "min_checkpoint_period": {"batches": 0},
@@ -285,6 +286,9 @@ def validate_experiment_config(cfg: Dict[str, Any], require_entrypoint: bool = T
     opt = cfg.get("optimizations", {})
     if opt.get("aggregation_frequency", 1) < 1:
         errs.append("aggregation_frequency must be >= 1")
+    hgb = opt.get("hip_graph_batches", 1)
+    if not isinstance(hgb, int) or isinstance(hgb, bool) or hgb < 1:
+        errs.append("optimizations.hip_graph_batches must be an integer >= 1")
     if opt.get("grad_reduction", "fp32_accum") not in ("fp32_accum", "allreduce", "auto"):
         errs.append("optimizations.grad_reduction must be fp32_accum, allreduce or auto")
     if not isinstance(opt.get("rccl", {}) or {}, dict):

@@ -13,9 +13,9 @@ Written for MI355X rather than transcribed:
     per step saved.  Gradients still reach the trainable ``W`` (layers 2-4) through the fold.
   * activations stay ``channels_last`` through the backbone (MIOpen's NHWC bf16 kernels, no
     layout transposes); the transformer consumes the flattened ``[B, HW, D]`` sequence directly;
-  * attention goes through ``F.scaled_dot_product_attention`` (fused flash-style kernel on
-    ROCm) with the key-padding mask as a boolean mask, q/k/v projected by one packed GEMM where
-    q and k share an input (self-attention);
+  * attention runs on ``det_attention.hip`` (``ops.transformer.attention``: fp32 or bf16 MFMA
+    flash attention, head_dim 32, any sequence length, the key-padding mask as a per-key bias row)
+    reading q and k in place from one packed GEMM where they share an input (self-attention);
   * class and box heads run once over the stacked decoder outputs ``[L, B, Q, D]`` (one GEMM
     each for all 6 layers).
 """
@@ -27,6 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from determined_1_amd.models.detection import HungarianMatcher, SetCriterion
+from determined_1_amd.ops import transformer as tfops
 
 
 # ------------------------------------------------------------------------------------------------
@@ -145,17 +146,13 @@ class Attention(nn.Module):
             q = F.linear(q_in, w[:d], bias[:d])
             k = F.linear(k_in, w[d:2 * d], bias[d:2 * d])
         v = F.linear(v_in, w[2 * d:], bias[2 * d:])
-        hd = d // self.h
-
-        def heads(t: torch.Tensor) -> torch.Tensor:
-            return t.view(b, -1, self.h, hd).transpose(1, 2)
-
         mask = None
         if key_padding_mask is not None:
             mask = (~key_padding_mask)[:, None, None, :]  # True = attend
-        o = F.scaled_dot_product_attention(heads(q), heads(k), heads(v), attn_mask=mask,
-                                           dropout_p=self.p if self.training else 0.0)
-        return self.out_proj(o.transpose(1, 2).reshape(b, lq, d))
+        # det_attention.hip (fp32 or bf16, head_dim 32, any length; Q/K read in place from the
+        # packed projection), composite SDPA on CPU
+        o = tfops.attention(q, k, v, self.h, attn_bias=mask, p=self.p, training=self.training)
+        return self.out_proj(o)
 
 
 class EncoderLayer(nn.Module):

@@ -96,9 +96,7 @@ class SyntheticImageClasses(tud.Dataset):
         return self._table.index_select(0, labels * self.BANK + pick), labels
 
 
-def passthrough_collate(batch: Any) -> Any:
-    """Collate for datasets whose ``__getitems__`` already returns a stacked batch."""
-    return batch
+from determined_1_amd.pytorch._data import passthrough_collate  # noqa: E402,F401  (re-export)
 
 
 class SyntheticTokens(tud.Dataset):

@@ -182,17 +182,15 @@ _SIGNATURES = {
     "det_tf_gelu_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, x, rows, C, out, ws
     "det_tf_colsum": ([c_void_p, c_int, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
-    # stream, dtype, gq, gk, gv, strides9 (host int64[9]), out, B, S, nh, hd
-    "det_tf_pack_qkv": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int],
-                        c_int),
-    # det_attention.hip: MFMA attention (head_dim 64, S <= 512)
-    "det_attn_supported": ([c_int, c_int], c_int),
-    # stream, qkv, bias, out, lse, B, S, nh, p, seed, offset
-    "det_attn_fwd": ([c_void_p] * 5 + [c_int, c_int, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64], c_int),
-    # stream, qkv, bias, out, dout, lse, delta, dqkv, B, S, nh, p, seed, offset
-    "det_attn_bwd": ([c_void_p] * 8 + [c_int, c_int, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64], c_int),
-    "det_attn_dropout_mask": ([c_void_p, c_int, c_int, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p],
-                              c_int),
+    # det_attention.hip: MFMA flash attention (bf16 head_dim 32/64/128, fp32 32/64, any length)
+    # dtype (0 bf16, 1 fp32), head_dim, Lq, Lk
+    "det_attn_supported": ([c_int, c_int, c_int, c_int], c_int),
+    # stream, const DetAttnParams* (transformer._AttnParams)
+    "det_attn_forward": ([c_void_p, c_void_p], c_int),
+    "det_attn_backward": ([c_void_p, c_void_p], c_int),
+    # stream, B, nh, Lq, Lk, p, seed, offset, out
+    "det_attn_dropout_mask": ([c_void_p, c_int, c_int, c_int, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64,
+                               c_void_p], c_int),
     "det_tf_dropout_mask": ([c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p], c_int),
 }
 

@@ -265,7 +265,8 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) 
     mode = getattr(prod, "mask_mode", 0)
     if mode not in FUSE_BN_BWD_MODES or getattr(prod, "fused_bwd", None) is not None:
         return None
-    if mode == 2 and getattr(prod, "extra_dy", None) is None:
+    expects = getattr(prod, "expects_extra", False)  # a linked shortcut also consumes the output
+    if expects and getattr(prod, "extra_dy", None) is None:
         return None  # the identity/projection shortcut gradient has not been linked yet
     try:
         xb, mbits, _, stats = prod.saved_tensors
@@ -273,7 +274,7 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) 
         return None
     if xb.dtype != torch.bfloat16 or xb.numel() != m * c or not xb.is_contiguous(memory_format=torch.channels_last):
         return None
-    add = prod.extra_dy if mode == 2 else None
+    add = prod.extra_dy if expects else None
     if add is not None and (add.dtype != torch.bfloat16 or not add.is_contiguous(memory_format=torch.channels_last)):
         return None
     rpb = rows_per_block(c)
@@ -286,7 +287,7 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) 
         stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits), _ptr(add), psum.data_ptr(),
         psumx.data_ptr(), int(mode)), "conv_nt_bnbwd")
     prod.fused_bwd = (psum, psumx, rpb)
-    if mode == 2:
+    if expects:
         prod.extra_dy = None  # consumed: summed into d
     return d
 

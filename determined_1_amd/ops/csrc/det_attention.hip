@@ -1,50 +1,68 @@
-// det_attention.hip — MFMA self-attention for encoder shapes (head_dim 64, S % 64 == 0, S <= 2048)
-// on gfx950, forward and backward, with regenerable dropout on the probabilities.
+// det_attention.hip — MFMA flash attention on gfx950, forward and backward, for every attention the
+// framework's models run: bf16 head_dim 32/64/128 and fp32 head_dim 32/64, any query/key length
+// (masked tail blocks), separate query/key lengths (cross-attention), an additive per-key bias
+// ([B, Lk], BERT/DETR padding masks) and/or a full additive bias with arbitrary broadcast strides
+// ([B|1, nh|1, Lq, Lk]), and regenerable dropout on the probabilities.
 //
 // Why this exists: BERT-base SQuAD-shape (B 12, S 384, 12 heads x 64) spent 2.2 ms/step in the
-// AOTriton attention kernels (profiles/r1_bert_native_bs12_o2_steady.csv), ~105 TFLOP/s; these
-// kernels take 0.99 ms (profiles/r1_bert_native_fa_bs12_o2_per_step.txt).
+// AOTriton attention kernels (profiles/r1_bert_native_bs12_o2_steady.csv), ~105 TFLOP/s; the
+// bf16/64 instance takes 0.99 ms (profiles/r1_bert_native_fa_bs12_o2_per_step.txt).  Round 3 made
+// the kernels generic so no example falls back to AOTriton or a composite SDPA (DETR: fp32,
+// head_dim 32, S = feature-map pixels; ALBERT fp32 reference config: head_dim 64).
 //
-// Layout: Q/K/V are read straight from the fused QKV GEMM output [B, S, 3, nh, 64] (token stride
-// 3H) and dQ/dK/dV written straight into its gradient, so no split/pack copies exist; the key bias
-// is an additive per-key row [B, S] (BERT's padding mask).  O is [B, S, nh*64]; LSE [B, nh, S] is
-// the natural-log normaliser the backward recomputes P from.
+// Layout: Q/K/V are token-major strided views — element (b, token, head, d) at
+// base + b*sb + token*st + head*HD + d — so the fused [B, S, 3, nh, HD] QKV GEMM output is read in
+// place (token stride 3H) and dQ/dK/dV are written straight into its gradient; DETR's separate
+// projections are the same with token stride H.  O/dO are [B, Lq, nh, HD] views the same way.
+// LSE [B, nh, Lq] is the natural-log normaliser the backward recomputes P from.
 //
 // All three kernels share one structure: a workgroup = 4 waves = 128 rows (queries, or keys for
-// dK/dV) of one (batch, head), one row per lane (v_mfma_f32_32x32x16_bf16 with the row on the
-// accumulator COLUMN, i.e. S^T = K . Q^T, so softmax reductions are in-lane plus one lane^32
-// exchange), and the other operand streamed in 64-token blocks that are double-buffered in LDS:
-// the next block is loaded into registers before the current block's MFMAs and written to the
-// other buffer after them (one barrier per block).  Row-major tiles use an XOR-swizzled 16-B chunk
-// layout (conflict-free A-fragment reads); operands consumed along the token axis get a
-// transposed [64][64+4] image written in the same pass.  An accumulator converted to bf16 in
-// registers is directly the B operand of the next product (k order permuted to match,
-// frag_from_image / pack_frag).
+// dK/dV) of one (batch, head), one row per lane (32x32 MFMA with the row on the accumulator COLUMN,
+// i.e. S^T = K . Q^T, so softmax reductions are in-lane plus one lane^32 exchange), and the other
+// operand streamed in 64-token blocks double-buffered in LDS: the next block is loaded into
+// registers before the current block's MFMAs and written to the other buffer after them (one
+// barrier per block).  Row-major tiles use an XOR-swizzled 16-B chunk layout (conflict-free
+// A-fragment reads); operands consumed along the token axis get a transposed [HD][64+4] image
+// written in the same pass.  An accumulator (converted to bf16 in registers on the bf16 path) is
+// directly the B operand of the next product with the k order permuted to match (Elt::mma_img).
+// bf16 uses v_mfma_f32_32x32x16_bf16 (one 16-B chunk per lane per MFMA); fp32 uses
+// v_mfma_f32_32x32x2_f32 over the same chunks (4 MFMAs per chunk), so the fp32 path keeps fp32
+// operands end to end rather than rounding through bf16.
 //   forward : per key block S^T, online softmax (running max/sum in the log2 domain), O^T += V^T P^T
 //   dQ      : per key block S^T, dP^T, dS^T = P o (dP^T o Z/(1-p) - D), dQ^T += K^T dS^T; writes D
 //   dK, dV  : per query block S, dP, dV^T += dO^T Pd, dK^T += Q^T dS (no cross-workgroup sums)
-// Dropout keep masks come from a keyed 32-bit hash of (b, h, q*S + key) (two 16-bit draws per
-// hash), regenerated bit-exactly in the backward pass.
+// Tails: key rows past Lk are clamped loads whose scores get a -inf bias (P = 0 exactly); query rows
+// past Lq are clamped loads with LSE = +inf in the dK/dV kernel (P = 0) and are never stored.
+// Dropout keep masks come from a keyed 32-bit hash of (b, h, q*LkE + key), LkE = Lk rounded up to
+// a multiple of 4 (two 16-bit draws per hash), regenerated bit-exactly in the backward pass.
 //
-// Reference parity: the reference runs attention inside HuggingFace BERT/ALBERT on torch
-// (examples/nlp/bert_squad_pytorch/model_def.py, examples/nlp/albert_squad_pytorch/model_def.py);
-// semantics = softmax(QK^T/sqrt(d) + bias) with dropout on the probabilities, as
+// Reference parity: the reference runs attention inside HuggingFace BERT/ALBERT and DETR's
+// nn.MultiheadAttention on torch (examples/nlp/bert_squad_pytorch/model_def.py,
+// examples/nlp/albert_squad_pytorch/model_def.py, examples/computer_vision/detr_coco_pytorch/
+// model.py); semantics = softmax(QK^T * scale + bias) V with dropout on the probabilities, as
 // torch.nn.functional.scaled_dot_product_attention.
 
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 namespace {
 
-constexpr int kHD = 64;        // head dim
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kQB = 32 * kWaves;  // queries per workgroup
+constexpr int kQB = 32 * kWaves;  // rows (queries, or keys for dK/dV) per workgroup
+constexpr int kKB = 64;           // streamed tokens per block
+constexpr int kTS = kKB + 4;      // transposed-image row stride (elements)
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kMaxLds = 160 * 1024;
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) unsigned short us4;
 typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+// 16-B chunk in registers (an ext vector, not HIP's uint4 union, so SROA keeps tile arrays in VGPRs)
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 __device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
 // RNE conversion; the compiler pairs adjacent conversions into gfx950's v_cvt_pk_bf16_f32 (one VALU
@@ -67,139 +85,257 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x, uint32_t key) {
   return x;
 }
 
-struct AttnArgs {
-  const unsigned short* qkv;  // [B, S, 3, nh, 64] bf16
-  const float* bias;          // [B, S] additive key bias (natural units) or null
-  unsigned short* out;        // [B, S, nh, 64] bf16
-  float* lse;                 // [B, nh, S]
-  int B, S, nh;
-  float scale_log2;           // log2(e) / sqrt(64)
-  uint32_t drop_thr;          // drop if 16-bit draw < thr (0: no dropout)
-  float drop_scale;           // 65536 / (65536 - thr)
+struct Args {
+  const void *q, *k, *v;        // token-major views, see header
+  const void* dout;             // dO (backward)
+  void* out;                    // O (written by the forward, read by the backward)
+  void *dq, *dk, *dv;           // gradients (backward)
+  float* lse;                   // [B, nh, Lq]
+  float* delta;                 // [B, nh, Lq] (backward workspace)
+  const float* kbias;           // [B, Lk] additive per-key bias (natural units) or null
+  const float* mbias;           // full additive bias, element (b, h, q, k) at b*mbb + h*mbh + q*mbq + k
+  int64_t qsb, qst, ksb, kst, vsb, vst, osb, ost, dosb, dost, dqsb, dqst, dksb, dkst, dvsb, dvst;
+  int64_t mbb, mbh, mbq;
+  int B, Lq, Lk, nh;
+  float scale, scale_log2;      // softmax scale (natural) and scale * log2(e)
+  uint32_t drop_thr;            // drop if 16-bit draw < thr (0: no dropout)
+  float drop_scale;             // 65536 / (65536 - thr)
   uint32_t rng_key;
 };
 
 __device__ __forceinline__ uint32_t rng_key_for(uint32_t base_key, int b, int head) {
   return base_key ^ (static_cast<uint32_t>(b * 977 + head) * 0x9E3779B9u);
 }
+__host__ __device__ __forceinline__ int lk_even4(int Lk) { return (Lk + 3) & ~3; }
 
-// ---- forward tiles: 64 keys per block, double-buffered in LDS -----------------------------------
-constexpr int kKB = 64;                                     // keys per block
-constexpr int kVtStride = kKB + 4;                          // V^T tile row stride (bf16): 136 B
-constexpr int kKTileBytes = kKB * kHD * 2;                  // K tile [64 keys][64 d], 128-B rows
-constexpr int kVTileBytes = kHD * kVtStride * 2;            // V^T tile [64 d][64 keys + 4]
-constexpr int kFwdBufBytes = kKTileBytes + kVTileBytes;
+// ---- element traits: the two MFMA shapes -------------------------------------------------------
+template <typename E>
+struct Elt;
 
-// byte offset of 16-B chunk `ch` (0..7) of K-tile row `row`: XOR swizzle so that the 32 rows an
-// MFMA A-fragment read touches (same chunk, consecutive rows) spread over all LDS banks
-__device__ __forceinline__ int kswz(int row, int ch) { return row * 128 + 16 * (ch ^ (row & 7)); }
-
-struct TileRegs {
-  us8 k[2], v[2];
+template <>
+struct Elt<unsigned short> {  // bf16
+  // acc += A . B over one 16-B chunk per lane: lane half hh holds k = 8hh..8hh+7
+  __device__ static __forceinline__ void mma_chunk(f32x16& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                  acc, 0, 0, 0);
+  }
+  // acc += Img[row][k0 .. k0+32) . P^T, P an accumulator over those 32 tokens (lane half hh holds
+  // tokens 8g + 4hh + e): bf16 pack of elements 8s..8s+7 = tokens 8(2s + j/4) + 4hh + j%4, and the
+  // image fragment read with the same permutation
+  __device__ static __forceinline__ void mma_img(f32x16& acc, const unsigned short* img, int row, int k0,
+                                                 const f32x16& p, int hh) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const unsigned short* src = img + row * kTS + k0 + 16 * s + 4 * hh;
+      const us4 lo = *reinterpret_cast<const us4*>(src);
+      const us4 hi = *reinterpret_cast<const us4*>(src + 8);
+      bf16x8 af, bf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        af[j] = static_cast<short>(lo[j]);
+        af[4 + j] = static_cast<short>(hi[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bf[j] = static_cast<short>(f2bf(p[8 * s + j]));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+    }
+  }
+  __device__ static __forceinline__ void store4(unsigned short* dst, float v0, float v1, float v2, float v3) {
+    us4 w;
+    w[0] = f2bf(v0);
+    w[1] = f2bf(v1);
+    w[2] = f2bf(v2);
+    w[3] = f2bf(v3);
+    *reinterpret_cast<us4*>(dst) = w;
+  }
+  __device__ static __forceinline__ float chunk_dot(const u32x4& a, const u32x4& b) {
+    const us8 x = __builtin_bit_cast(us8, a), y = __builtin_bit_cast(us8, b);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s = fmaf(bf2f(x[j]), bf2f(y[j]), s);
+    return s;
+  }
 };
 
-// thread i: K chunk (i & 7) of keys i>>3 and (i>>3)+32; V d-group (i & 7) of the key pair 2(i>>3), 2(i>>3)+1
-__device__ __forceinline__ void load_tile(TileRegs& t, const unsigned short* kbase, const unsigned short* vbase,
-                                          int64_t tok, int key0) {
-  const int c = threadIdx.x & 7, kr = threadIdx.x >> 3;
-  t.k[0] = *reinterpret_cast<const us8*>(kbase + static_cast<int64_t>(key0 + kr) * tok + 8 * c);
-  t.k[1] = *reinterpret_cast<const us8*>(kbase + static_cast<int64_t>(key0 + kr + 32) * tok + 8 * c);
-  t.v[0] = *reinterpret_cast<const us8*>(vbase + static_cast<int64_t>(key0 + 2 * kr) * tok + 8 * c);
-  t.v[1] = *reinterpret_cast<const us8*>(vbase + static_cast<int64_t>(key0 + 2 * kr + 1) * tok + 8 * c);
-}
-
-__device__ __forceinline__ void store_tile(const TileRegs& t, unsigned char* buf) {
-  const int c = threadIdx.x & 7, kr = threadIdx.x >> 3;
-  *reinterpret_cast<us8*>(buf + kswz(kr, c)) = t.k[0];
-  *reinterpret_cast<us8*>(buf + kswz(kr + 32, c)) = t.k[1];
-  unsigned short* vt = reinterpret_cast<unsigned short*>(buf + kKTileBytes);
+template <>
+struct Elt<float> {  // fp32: 4 MFMAs 32x32x2 per 16-B chunk; lane half hh holds k column 4c + e
+  __device__ static __forceinline__ void mma_chunk(f32x16& acc, const u32x4& a, const u32x4& b) {
+    const f32x4 x = __builtin_bit_cast(f32x4, a), y = __builtin_bit_cast(f32x4, b);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint32_t w = static_cast<uint32_t>(t.v[0][e]) | (static_cast<uint32_t>(t.v[1][e]) << 16);
-    *reinterpret_cast<uint32_t*>(vt + (8 * c + e) * kVtStride + 2 * kr) = w;
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], y[e], acc, 0, 0, 0);
   }
-}
-
-// A operand of an X^T image: lane (r, h) elements j = X[k0 + 8(j>>2) + 4h + (j&3)][row] (k-permuted
-// to match an accumulator packed as a B operand, see pack_frag)
-__device__ __forceinline__ bf16x8 frag_from_image(const unsigned short* img, int stride, int row, int k0, int hh) {
-  const unsigned short* p = img + row * stride + k0 + 4 * hh;
-  const us4 lo = *reinterpret_cast<const us4*>(p);
-  const us4 hi = *reinterpret_cast<const us4*>(p + 8);
-  bf16x8 f;
+  __device__ static __forceinline__ void mma_img(f32x16& acc, const float* img, int row, int k0, const f32x16& p,
+                                                 int hh) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    f[j] = static_cast<short>(lo[j]);
-    f[4 + j] = static_cast<short>(hi[j]);
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(img + row * kTS + k0 + 8 * g + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x[e], p[4 * g + e], acc, 0, 0, 0);
+    }
   }
-  return f;
-}
+  __device__ static __forceinline__ void store4(float* dst, float v0, float v1, float v2, float v3) {
+    *reinterpret_cast<f32x4*>(dst) = f32x4{v0, v1, v2, v3};
+  }
+  __device__ static __forceinline__ float chunk_dot(const u32x4& a, const u32x4& b) {
+    const f32x4 x = __builtin_bit_cast(f32x4, a), y = __builtin_bit_cast(f32x4, b);
+    return x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3];
+  }
+};
 
-__device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
-  bf16x8 f;
+// ---- streamed 64-token tiles --------------------------------------------------------------------
+// Work unit = 16-B chunk c of the token pair (2kp, 2kp+1); the row image is XOR-swizzled by chunk,
+// the transposed image [HD][64 + 4] gets token pairs as one 32-bit (bf16) or 64-bit (fp32) store.
+template <typename E, int HD>
+struct Tile {
+  static constexpr int RB = HD * static_cast<int>(sizeof(E));  // bytes per token row
+  static constexpr int NCH = RB / 16;
+  static constexpr int CH = 16 / static_cast<int>(sizeof(E));
+  static constexpr int UNITS = 32 * NCH;
+  static constexpr int NP = (UNITS + kThreads - 1) / kThreads;
+  static constexpr int SWM = (NCH < 16 ? NCH : 16) - 1;
+  static constexpr int ROW_BYTES = kKB * RB;
+  static constexpr int T_BYTES = HD * kTS * static_cast<int>(sizeof(E));
+  static_assert(RB % 16 == 0 && NCH >= 4, "head_dim too small");
+
+  u32x4 x[NP][2];
+
+  __device__ static __forceinline__ int off(int row, int ch) { return row * RB + 16 * (ch ^ (row & SWM)); }
+  __device__ static __forceinline__ bool live(int w) { return UNITS % kThreads == 0 || w < UNITS; }
+
+  // rows row0 .. row0+63 of src (row stride `tok` elements), rows >= nrows clamped to nrows-1
+  __device__ __forceinline__ void load(const E* src, int64_t tok, int row0, int nrows) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = static_cast<short>(f2bf(x[8 * s + j]));
-  return f;
+    for (int p = 0; p < NP; ++p) {
+      const int w = threadIdx.x + p * kThreads;
+      if (!live(w)) continue;
+      const int kp = w / NCH, c = w % NCH;
+      const int r0 = min(row0 + 2 * kp, nrows - 1), r1 = min(row0 + 2 * kp + 1, nrows - 1);
+      x[p][0] = *reinterpret_cast<const u32x4*>(src + static_cast<int64_t>(r0) * tok + c * CH);
+      x[p][1] = *reinterpret_cast<const u32x4*>(src + static_cast<int64_t>(r1) * tok + c * CH);
+    }
+  }
+  __device__ __forceinline__ void store_rows(unsigned char* dst) const {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int w = threadIdx.x + p * kThreads;
+      if (!live(w)) continue;
+      const int kp = w / NCH, c = w % NCH;
+      *reinterpret_cast<u32x4*>(dst + off(2 * kp, c)) = x[p][0];
+      *reinterpret_cast<u32x4*>(dst + off(2 * kp + 1, c)) = x[p][1];
+    }
+  }
+  __device__ __forceinline__ void store_t(E* dst) const {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int w = threadIdx.x + p * kThreads;
+      if (!live(w)) continue;
+      const int kp = w / NCH, c = w % NCH;
+      if constexpr (sizeof(E) == 2) {
+        const us8 a = __builtin_bit_cast(us8, x[p][0]), b = __builtin_bit_cast(us8, x[p][1]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          *reinterpret_cast<uint32_t*>(dst + (c * CH + e) * kTS + 2 * kp) =
+              static_cast<uint32_t>(a[e]) | (static_cast<uint32_t>(b[e]) << 16);
+      } else {
+        const f32x4 a = __builtin_bit_cast(f32x4, x[p][0]), b = __builtin_bit_cast(f32x4, x[p][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          typedef __attribute__((ext_vector_type(2))) float f32x2;
+          *reinterpret_cast<f32x2*>(dst + (c * CH + e) * kTS + 2 * kp) = f32x2{a[e], b[e]};
+        }
+      }
+    }
+  }
+  __device__ static __forceinline__ u32x4 frag(const unsigned char* img, int row, int ch) {
+    return *reinterpret_cast<const u32x4*>(img + off(row, ch));
+  }
+};
+
+// per-key bias row in LDS, log2 units: real keys clamped finite (fully masked rows degrade to
+// uniform like fp32 torch), tail keys -inf
+__device__ __forceinline__ void fill_key_bias(float* dst, const float* kbias, int Lk, int LkP) {
+  for (int i = threadIdx.x; i < LkP; i += kThreads)
+    dst[i] = i < Lk ? (kbias ? fmaxf(kbias[i] * kLog2e, -1e30f) : 0.f) : -INFINITY;
+}
+__device__ __forceinline__ float mbias_log2(const float* m, int64_t i) { return fmaxf(m[i] * kLog2e, -1e30f); }
+
+// dropout keep factors for tokens k0..k0+3 (k0 % 4 == 0) of the row with index base rowidx
+__device__ __forceinline__ void drop4(float z[4], uint32_t rowidx, int k0, uint32_t key, uint32_t thr, float dscale) {
+  const uint32_t h0 = mix32((rowidx + k0) >> 1, key), h1 = mix32((rowidx + k0 + 2) >> 1, key);
+  const uint32_t d4[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) z[e] = d4[e] < thr ? 0.f : dscale;
 }
 
-// Flash-style forward: one workgroup = 4 waves = 128 queries of one (batch, head), wave = 32
-// queries, lane = one query (its 32 keys of a 64-key block in two S^T accumulators).  Per key block:
-//   S^T = K . Q^T (8 MFMA 32x32x16, K fragments from the swizzled LDS tile, Q^T in registers),
-//   online softmax in the log2 domain (running max m / partial sum l per lane, one lane^32 max
-//   exchange per block), O^T = O^T * alpha + V^T . P^T (8 MFMA, P packed to bf16 in registers).
-// The next block's K/V are loaded into registers before the current block's MFMAs and written to
-// the other LDS buffer after them: one barrier per block, global latency behind the math.
-// Register footprint is independent of S (~110 VGPR): two workgroups per CU-SIMD pair.
-__global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnArgs a) {
+// =============================================================================================
+// Forward: one workgroup = 128 queries of one (batch, head), wave = 32 queries, lane = one query
+// (its 32 keys of a 64-key block in two S^T accumulators).  Per key block: S^T = K . Q^T (K
+// fragments from the swizzled LDS tile, Q^T in registers), online softmax in the log2 domain (one
+// lane^32 max exchange), O^T = O^T * alpha + V^T . P^T.
+// =============================================================================================
+template <typename E, int HD, bool MB>
+__global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) attn_fwd_kernel(Args a) {
+  using TL = Tile<E, HD>;
+  using EL = Elt<E>;
+  constexpr int QCH = TL::NCH / 2, NU = HD / 32;
+  constexpr int BUF = TL::ROW_BYTES + TL::T_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int S = a.S;
-  float* biasl = reinterpret_cast<float*>(smem + 2 * kFwdBufBytes);
+  const int Lq = a.Lq, Lk = a.Lk, nkb = (Lk + kKB - 1) / kKB;
+  float* biasl = reinterpret_cast<float*>(smem + 2 * BUF);
   const int b = blockIdx.z, head = blockIdx.y;
-  const int H = a.nh * kHD;
-  const int64_t tok = 3LL * H;  // elements between consecutive tokens
-  const unsigned short* base = a.qkv + static_cast<int64_t>(b) * S * tok + head * kHD;
-  const unsigned short* kbase = base + H;
-  const unsigned short* vbase = base + 2 * H;
+  const E* qbase = static_cast<const E*>(a.q) + b * a.qsb + head * HD;
+  const E* kbase = static_cast<const E*>(a.k) + b * a.ksb + head * HD;
+  const E* vbase = static_cast<const E*>(a.v) + b * a.vsb + head * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int q0 = blockIdx.x * kQB + wave * 32;
-  const bool active = q0 < S;  // inactive waves still stage tiles (no early return: barriers below)
-  const int q = active ? q0 + r : S - 1;
+  const int qv = blockIdx.x * kQB + wave * 32 + r;
+  const int q = qv < Lq ? qv : Lq - 1;  // past-the-end lanes compute a clamped row, store nothing
 
-  TileRegs tr;
-  load_tile(tr, kbase, vbase, tok, 0);
-  for (int i = threadIdx.x; i < S; i += kThreads) {
-    const float bv = a.bias ? a.bias[static_cast<int64_t>(b) * S + i] * 1.4426950408889634f : 0.f;
-    biasl[i] = fmaxf(bv, -1e30f);  // finite: fully masked rows degrade to uniform, like fp32 torch
-  }
-  bf16x8 qf[4];
+  TL kt, vt;
+  kt.load(kbase, a.kst, 0, Lk);
+  vt.load(vbase, a.vst, 0, Lk);
+  fill_key_bias(biasl, a.kbias ? a.kbias + static_cast<int64_t>(b) * Lk : nullptr, Lk, nkb * kKB);
+  u32x4 qf[QCH];
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
-    qf[s] = *reinterpret_cast<const bf16x8*>(base + static_cast<int64_t>(q) * tok + 16 * s + 8 * hh);
-  store_tile(tr, smem);
+  for (int j = 0; j < QCH; ++j)
+    qf[j] = *reinterpret_cast<const u32x4*>(qbase + static_cast<int64_t>(q) * a.qst + (2 * j + hh) * TL::CH);
+  const float* mrow = MB ? a.mbias + b * a.mbb + head * a.mbh + static_cast<int64_t>(q) * a.mbq : nullptr;
+  kt.store_rows(smem);
+  vt.store_t(reinterpret_cast<E*>(smem + TL::ROW_BYTES));
   __syncthreads();
 
   const uint32_t key = rng_key_for(a.rng_key, b, head);
-  const uint32_t rowidx = static_cast<uint32_t>(q) * static_cast<uint32_t>(S);
+  const uint32_t rowidx = static_cast<uint32_t>(q) * static_cast<uint32_t>(lk_even4(Lk));
   float m = -INFINITY, l = 0.f;
-  f32x16 o[2] = {f32x16{0}, f32x16{0}};
-  const int nkb = S / kKB;
+  f32x16 o[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) o[u] = f32x16{0};
   for (int kb = 0; kb < nkb; ++kb) {
-    const unsigned char* buf = smem + (kb & 1) * kFwdBufBytes;
-    const unsigned short* vt = reinterpret_cast<const unsigned short*>(buf + kKTileBytes);
-    if (kb + 1 < nkb) load_tile(tr, kbase, vbase, tok, (kb + 1) * kKB);
-
+    const unsigned char* buf = smem + (kb & 1) * BUF;
+    const E* vti = reinterpret_cast<const E*>(buf + TL::ROW_BYTES);
+    if (kb + 1 < nkb) {
+      kt.load(kbase, a.kst, (kb + 1) * kKB, Lk);
+      vt.load(vbase, a.vst, (kb + 1) * kKB, Lk);
+    }
+    float mb[2][16];
+    if constexpr (MB) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kk = kb * kKB + 32 * t + 8 * (i >> 2) + 4 * hh + (i & 3);
+          mb[t][i] = kk < Lk ? mbias_log2(mrow, kk) : 0.f;
+        }
+    }
     f32x16 sc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       sc[t] = f32x16{0};
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        sc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            *reinterpret_cast<const bf16x8*>(buf + kswz(32 * t + r, 2 * s + hh)), qf[s], sc[t], 0, 0, 0);
+      for (int j = 0; j < QCH; ++j) EL::mma_chunk(sc[t], TL::frag(buf, 32 * t + r, 2 * j + hh), qf[j]);
     }
-    // scores in log2 units + key bias; block max over the lane pair (q, q^32)
-    float mb = -INFINITY;
+    // scores in log2 units + biases; block max over the lane pair (q, q^32)
+    float mx = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -208,13 +344,14 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnArgs a) {
         const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = fmaf(sc[t][4 * g + e], a.scale_log2, bb[e]);
+          float x = fmaf(sc[t][4 * g + e], a.scale_log2, bb[e]);
+          if constexpr (MB) x += mb[t][4 * g + e];
           sc[t][4 * g + e] = x;
-          mb = fmaxf(mb, x);
+          mx = fmaxf(mx, x);
         }
       }
-    mb = fmaxf(mb, __shfl_xor(mb, 32, 64));
-    const float mn = fmaxf(m, mb);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
     const float alpha = fast_exp2(m - mn);
     m = mn;
     float ls = 0.f;
@@ -229,168 +366,125 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnArgs a) {
     l = fmaf(l, alpha, ls);
     if (__any(alpha != 1.f)) {  // no lane's running max moved: the rescale is an exact no-op
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[u][i] *= alpha;
     }
-    if (a.drop_thr) {  // keys 4g..4g+3 of each 32-key tile = 2 hashes (same draws as the backward)
+    if (a.drop_thr) {  // same draws as the backward
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const uint32_t k0 = kb * kKB + 32 * t + 8 * g + 4 * hh;
-          const uint32_t h0 = mix32((rowidx + k0) >> 1, key), h1 = mix32((rowidx + k0 + 2) >> 1, key);
-          const uint32_t d4[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
+          float z[4];
+          drop4(z, rowidx, kb * kKB + 32 * t + 8 * g + 4 * hh, key, a.drop_thr, a.drop_scale);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sc[t][4 * g + e] *= d4[e] < a.drop_thr ? 0.f : a.drop_scale;
+          for (int e = 0; e < 4; ++e) sc[t][4 * g + e] *= z[e];
         }
     }
     // O^T += V^T . P^T
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = pack_frag(sc[t], s);
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          o[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_from_image(vt, kVtStride, 32 * u + r, 32 * t + 16 * s, hh),
-                                                         pf, o[u], 0, 0, 0);
-      }
-    if (kb + 1 < nkb) store_tile(tr, smem + ((kb + 1) & 1) * kFwdBufBytes);
+      for (int u = 0; u < NU; ++u) EL::mma_img(o[u], vti, 32 * u + r, 32 * t, sc[t], hh);
+    if (kb + 1 < nkb) {
+      unsigned char* nb = smem + ((kb + 1) & 1) * BUF;
+      kt.store_rows(nb);
+      vt.store_t(reinterpret_cast<E*>(nb + TL::ROW_BYTES));
+    }
     __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
-  if (!active) return;
-  if (hh == 0) a.lse[(static_cast<int64_t>(b) * a.nh + head) * S + q] = (m + log2f(l)) * 0.6931471805599453f;
-  // ---- O = O^T / l -> [B, S, nh, 64] ---------------------------------------------------------
+  if (qv >= Lq) return;
+  if (hh == 0) a.lse[(static_cast<int64_t>(b) * a.nh + head) * Lq + qv] = (m + log2f(l)) * 0.6931471805599453f;
   const float inv_l = 1.f / l;
-  unsigned short* orow = a.out + ((static_cast<int64_t>(b) * S + q) * a.nh + head) * kHD;
+  E* orow = static_cast<E*>(a.out) + b * a.osb + static_cast<int64_t>(qv) * a.ost + head * HD;
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      us4 w;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = f2bf(o[u][4 * g + e] * inv_l);
-      *reinterpret_cast<us4*>(orow + 32 * u + 8 * g + 4 * hh) = w;
-    }
+    for (int g = 0; g < 4; ++g)
+      EL::store4(orow + 32 * u + 8 * g + 4 * hh, o[u][4 * g] * inv_l, o[u][4 * g + 1] * inv_l,
+                 o[u][4 * g + 2] * inv_l, o[u][4 * g + 3] * inv_l);
 }
-
 
 // =============================================================================================
 // Backward.  With Pd = P o Z/(1-p) (dropout keep mask Z), D_q = sum_d dO o O (= sum_k Pd dPd):
-//   dV = Pd^T dO,  dPd = dO V^T,  dS = P o (dPd o Z/(1-p) - D),  dQ = dS K / 8,  dK = dS^T Q / 8.
+//   dV = Pd^T dO,  dPd = dO V^T,  dS = P o (dPd o Z/(1-p) - D),  dQ = dS K * scale,  dK = dS^T Q * scale.
 // Two kernels so that no gradient needs a cross-workgroup sum:
 //   attn_bwd_dq  (query on the lane, like the forward): S^T, dPd^T per key tile, dQ^T += K^T dS^T
 //                with a K^T LDS image; also writes D (consumed by the next kernel);
 //   attn_bwd_dkv (key on the lane): S, dPd per query tile, dV^T += dO^T Pd and dK^T += Q^T dS with
-//                Q^T / dO^T LDS images of the whole head.
-// Both write straight into the packed dQKV [B, S, 3, nh, 64] gradient of the fused QKV GEMM.
+//                Q^T / dO^T LDS images.
 // =============================================================================================
-struct BwdArgs {
-  const unsigned short* qkv;   // [B, S, 3, nh, 64]
-  const float* bias;           // [B, S] or null
-  const unsigned short* out;   // O  [B, S, nh, 64]
-  const unsigned short* dout;  // dO [B, S, nh, 64]
-  const float* lse;            // [B, nh, S]
-  float* delta;                // [B, nh, S]
-  unsigned short* dqkv;        // [B, S, 3, nh, 64]
-  int B, S, nh;
-  float scale_log2;
-  uint32_t drop_thr;
-  float drop_scale;
-  uint32_t rng_key;
-};
-
-// ---- backward tiles: 64 tokens x 64 dims, rows (swizzled) and/or a transposed image -------------
-// thread i holds chunk (i & 7) of the token pair 2(i>>3), 2(i>>3)+1 of the block
-__device__ __forceinline__ void load_pair(us8 (&x)[2], const unsigned short* src, int64_t tok, int row0) {
-  const int c = threadIdx.x & 7, kp = threadIdx.x >> 3;
-  x[0] = *reinterpret_cast<const us8*>(src + static_cast<int64_t>(row0 + 2 * kp) * tok + 8 * c);
-  x[1] = *reinterpret_cast<const us8*>(src + static_cast<int64_t>(row0 + 2 * kp + 1) * tok + 8 * c);
-}
-__device__ __forceinline__ void store_rows(const us8 (&x)[2], unsigned char* dst) {
-  const int c = threadIdx.x & 7, kp = threadIdx.x >> 3;
-  *reinterpret_cast<us8*>(dst + kswz(2 * kp, c)) = x[0];
-  *reinterpret_cast<us8*>(dst + kswz(2 * kp + 1, c)) = x[1];
-}
-__device__ __forceinline__ void store_t(const us8 (&x)[2], unsigned short* dst) {  // [64 dims][64 tokens + 4]
-  const int c = threadIdx.x & 7, kp = threadIdx.x >> 3;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint32_t w = static_cast<uint32_t>(x[0][e]) | (static_cast<uint32_t>(x[1][e]) << 16);
-    *reinterpret_cast<uint32_t*>(dst + (8 * c + e) * kVtStride + 2 * kp) = w;
-  }
-}
-__device__ __forceinline__ bf16x8 row_frag(const unsigned char* img, int row, int s, int hh) {
-  return *reinterpret_cast<const bf16x8*>(img + kswz(row, 2 * s + hh));
-}
-
-// dQ (query on the lane, like the forward).  Per 64-key block (double-buffered: K rows, V rows,
-// K^T image): S^T = K.Q^T, dPd^T = V.dO^T, dS^T = P o (dPd^T o Z/(1-p) - D), dQ^T += K^T . dS^T.
-// Also writes D = rowsum(dO o O) for the dK/dV kernel.
-constexpr int kDqBuf = 2 * kKTileBytes + kVTileBytes;
-__global__ void __launch_bounds__(kThreads, 2) attn_bwd_dq_kernel(BwdArgs a) {
+template <typename E, int HD, bool MB>
+__global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_dq_kernel(Args a) {
+  using TL = Tile<E, HD>;
+  using EL = Elt<E>;
+  constexpr int QCH = TL::NCH / 2, NU = HD / 32;
+  constexpr int BUF = 2 * TL::ROW_BYTES + TL::T_BYTES;  // K rows, V rows, K^T
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int S = a.S;
-  float* biasl = reinterpret_cast<float*>(smem + 2 * kDqBuf);
+  const int Lq = a.Lq, Lk = a.Lk, nkb = (Lk + kKB - 1) / kKB;
+  float* biasl = reinterpret_cast<float*>(smem + 2 * BUF);
   const int b = blockIdx.z, head = blockIdx.y;
-  const int H = a.nh * kHD;
-  const int64_t tok = 3LL * H;
-  const unsigned short* base = a.qkv + static_cast<int64_t>(b) * S * tok + head * kHD;
-  const unsigned short* kbase = base + H;
-  const unsigned short* vbase = base + 2 * H;
+  const E* qbase = static_cast<const E*>(a.q) + b * a.qsb + head * HD;
+  const E* kbase = static_cast<const E*>(a.k) + b * a.ksb + head * HD;
+  const E* vbase = static_cast<const E*>(a.v) + b * a.vsb + head * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int q0 = blockIdx.x * kQB + wave * 32;
-  const bool active = q0 < S;
-  const int q = active ? q0 + r : S - 1;
+  const int qv = blockIdx.x * kQB + wave * 32 + r;
+  const int q = qv < Lq ? qv : Lq - 1;
 
-  us8 kx[2], vx[2];
-  load_pair(kx, kbase, tok, 0);
-  load_pair(vx, vbase, tok, 0);
-  for (int i = threadIdx.x; i < S; i += kThreads) {
-    const float bv = a.bias ? a.bias[static_cast<int64_t>(b) * S + i] * 1.4426950408889634f : 0.f;
-    biasl[i] = fmaxf(bv, -1e30f);
-  }
-  const int64_t orow = ((static_cast<int64_t>(b) * S + q) * a.nh + head) * kHD;
-  bf16x8 qf[4], df[4];
+  TL kt, vt;
+  kt.load(kbase, a.kst, 0, Lk);
+  vt.load(vbase, a.vst, 0, Lk);
+  fill_key_bias(biasl, a.kbias ? a.kbias + static_cast<int64_t>(b) * Lk : nullptr, Lk, nkb * kKB);
+  const E* orow = static_cast<const E*>(a.out) + b * a.osb + static_cast<int64_t>(q) * a.ost + head * HD;
+  const E* dorow = static_cast<const E*>(a.dout) + b * a.dosb + static_cast<int64_t>(q) * a.dost + head * HD;
+  u32x4 qf[QCH], df[QCH];
   float dsum = 0.f;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = *reinterpret_cast<const bf16x8*>(base + static_cast<int64_t>(q) * tok + 16 * s + 8 * hh);
-    df[s] = *reinterpret_cast<const bf16x8*>(a.dout + orow + 16 * s + 8 * hh);
-    const us8 ov = *reinterpret_cast<const us8*>(a.out + orow + 16 * s + 8 * hh);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dsum = fmaf(bf2f(static_cast<unsigned short>(df[s][j])), bf2f(ov[j]), dsum);
+  for (int j = 0; j < QCH; ++j) {
+    const int c = (2 * j + hh) * TL::CH;
+    qf[j] = *reinterpret_cast<const u32x4*>(qbase + static_cast<int64_t>(q) * a.qst + c);
+    df[j] = *reinterpret_cast<const u32x4*>(dorow + c);
+    dsum += EL::chunk_dot(df[j], *reinterpret_cast<const u32x4*>(orow + c));
   }
   const float D = dsum + __shfl_xor(dsum, 32, 64);
-  const int64_t li = (static_cast<int64_t>(b) * a.nh + head) * S + q;
-  if (active && hh == 0) a.delta[li] = D;
-  const float lse2 = a.lse[li] * 1.4426950408889634f;
+  const int64_t li = (static_cast<int64_t>(b) * a.nh + head) * Lq + q;
+  if (qv < Lq && hh == 0) a.delta[li] = D;
+  const float lse2 = a.lse[li] * kLog2e;
+  const float* mrow = MB ? a.mbias + b * a.mbb + head * a.mbh + static_cast<int64_t>(q) * a.mbq : nullptr;
   const uint32_t key = rng_key_for(a.rng_key, b, head);
-  const uint32_t rowidx = static_cast<uint32_t>(q) * static_cast<uint32_t>(S);
-  store_rows(kx, smem);
-  store_rows(vx, smem + kKTileBytes);
-  store_t(kx, reinterpret_cast<unsigned short*>(smem + 2 * kKTileBytes));
+  const uint32_t rowidx = static_cast<uint32_t>(q) * static_cast<uint32_t>(lk_even4(Lk));
+  kt.store_rows(smem);
+  vt.store_rows(smem + TL::ROW_BYTES);
+  kt.store_t(reinterpret_cast<E*>(smem + 2 * TL::ROW_BYTES));
   __syncthreads();
 
-  f32x16 dqt[2] = {f32x16{0}, f32x16{0}};
-  const int nkb = S / kKB;
+  f32x16 dqt[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) dqt[u] = f32x16{0};
   for (int kb = 0; kb < nkb; ++kb) {
-    const unsigned char* buf = smem + (kb & 1) * kDqBuf;
-    const unsigned short* kt = reinterpret_cast<const unsigned short*>(buf + 2 * kKTileBytes);
+    const unsigned char* buf = smem + (kb & 1) * BUF;
+    const E* kti = reinterpret_cast<const E*>(buf + 2 * TL::ROW_BYTES);
     if (kb + 1 < nkb) {
-      load_pair(kx, kbase, tok, (kb + 1) * kKB);
-      load_pair(vx, vbase, tok, (kb + 1) * kKB);
+      kt.load(kbase, a.kst, (kb + 1) * kKB, Lk);
+      vt.load(vbase, a.vst, (kb + 1) * kKB, Lk);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      float mb[16];
+      if constexpr (MB) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kk = kb * kKB + 32 * t + 8 * (i >> 2) + 4 * hh + (i & 3);
+          mb[i] = kk < Lk ? mbias_log2(mrow, kk) : 0.f;
+        }
+      }
       f32x16 sa = f32x16{0}, dp = f32x16{0};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(buf, 32 * t + r, s, hh), qf[s], sa, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(buf + kKTileBytes, 32 * t + r, s, hh), df[s], dp, 0, 0, 0);
+      for (int j = 0; j < QCH; ++j) {
+        EL::mma_chunk(sa, TL::frag(buf, 32 * t + r, 2 * j + hh), qf[j]);
+        EL::mma_chunk(dp, TL::frag(buf + TL::ROW_BYTES, 32 * t + r, 2 * j + hh), df[j]);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -398,263 +492,311 @@ __global__ void __launch_bounds__(kThreads, 2) attn_bwd_dq_kernel(BwdArgs a) {
         const float4 bv = *reinterpret_cast<const float4*>(biasl + k0);
         const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
         float z[4] = {1.f, 1.f, 1.f, 1.f};
-        if (a.drop_thr) {
-          const uint32_t h0 = mix32((rowidx + k0) >> 1, key), h1 = mix32((rowidx + k0 + 2) >> 1, key);
-          const uint32_t d4[4] = {h0 & 0xffffu, h0 >> 16, h1 & 0xffffu, h1 >> 16};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) z[e] = d4[e] < a.drop_thr ? 0.f : a.drop_scale;
-        }
+        if (a.drop_thr) drop4(z, rowidx, k0, key, a.drop_thr, a.drop_scale);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g + e;
-          const float pr = fast_exp2(fmaf(sa[i], a.scale_log2, bb[e]) - lse2);
+          float x = fmaf(sa[i], a.scale_log2, bb[e]);
+          if constexpr (MB) x += mb[i];
+          const float pr = fast_exp2(x - lse2);
           sa[i] = pr * fmaf(dp[i], z[e], -D);  // dS^T
         }
       }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 dsf = pack_frag(sa, s);
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          dqt[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_from_image(kt, kVtStride, 32 * u + r, 32 * t + 16 * s, hh),
-                                                           dsf, dqt[u], 0, 0, 0);
-      }
+      for (int u = 0; u < NU; ++u) EL::mma_img(dqt[u], kti, 32 * u + r, 32 * t, sa, hh);
     }
     if (kb + 1 < nkb) {
-      unsigned char* nb = smem + ((kb + 1) & 1) * kDqBuf;
-      store_rows(kx, nb);
-      store_rows(vx, nb + kKTileBytes);
-      store_t(kx, reinterpret_cast<unsigned short*>(nb + 2 * kKTileBytes));
+      unsigned char* nb = smem + ((kb + 1) & 1) * BUF;
+      kt.store_rows(nb);
+      vt.store_rows(nb + TL::ROW_BYTES);
+      kt.store_t(reinterpret_cast<E*>(nb + 2 * TL::ROW_BYTES));
     }
     __syncthreads();
   }
-  if (!active) return;
-  unsigned short* dq = a.dqkv + (static_cast<int64_t>(b) * S + q) * tok + head * kHD;
+  if (qv >= Lq) return;
+  E* dq = static_cast<E*>(a.dq) + b * a.dqsb + static_cast<int64_t>(qv) * a.dqst + head * HD;
+  const float sc = a.scale;
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      us4 w;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = f2bf(dqt[u][4 * g + e] * 0.125f);
-      *reinterpret_cast<us4*>(dq + 32 * u + 8 * g + 4 * hh) = w;
-    }
+    for (int g = 0; g < 4; ++g)
+      EL::store4(dq + 32 * u + 8 * g + 4 * hh, dqt[u][4 * g] * sc, dqt[u][4 * g + 1] * sc, dqt[u][4 * g + 2] * sc,
+                 dqt[u][4 * g + 3] * sc);
 }
 
-// dK, dV (key on the lane).  Per 64-query block (double-buffered: Q rows, Q^T, dO rows, dO^T):
-// S = Q.K^T, dPd = dO.V^T (accumulator column = the lane's key), Pd = P o Z/(1-p),
-// dS = P o (dPd o Z/(1-p) - D), dV^T += dO^T . Pd, dK^T += Q^T . dS.
-constexpr int kDkvBuf = 2 * (kKTileBytes + kVTileBytes);
-__global__ void __launch_bounds__(kThreads, 2) attn_bwd_dkv_kernel(BwdArgs a) {
+template <typename E, int HD, bool MB>  // a full bias adds a per-element load row: one wave per SIMD
+__global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_dkv_kernel(Args a) {
+  using TL = Tile<E, HD>;
+  using EL = Elt<E>;
+  constexpr int QCH = TL::NCH / 2, NU = HD / 32;
+  constexpr int BUF = 2 * (TL::ROW_BYTES + TL::T_BYTES);  // Q rows, Q^T, dO rows, dO^T
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int S = a.S;
-  float* lse2 = reinterpret_cast<float*>(smem + 2 * kDkvBuf);
-  float* dl = lse2 + S;
+  const int Lq = a.Lq, Lk = a.Lk, nqb = (Lq + kKB - 1) / kKB;
+  float* lse2 = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* dl = lse2 + nqb * kKB;
   const int b = blockIdx.z, head = blockIdx.y;
-  const int H = a.nh * kHD;
-  const int64_t tok = 3LL * H;
-  const unsigned short* base = a.qkv + static_cast<int64_t>(b) * S * tok + head * kHD;
-  const unsigned short* dobase = a.dout + static_cast<int64_t>(b) * S * H + head * kHD;
+  const E* qbase = static_cast<const E*>(a.q) + b * a.qsb + head * HD;
+  const E* dobase = static_cast<const E*>(a.dout) + b * a.dosb + head * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int k0w = blockIdx.x * kQB + wave * 32;
-  const bool active = k0w < S;
-  const int kk = active ? k0w + r : S - 1;  // this lane's key
+  const int kv = blockIdx.x * kQB + wave * 32 + r;
+  const int kk = kv < Lk ? kv : Lk - 1;  // this lane's key
 
-  us8 qx[2], dx[2];
-  load_pair(qx, base, tok, 0);
-  load_pair(dx, dobase, H, 0);
-  const int64_t lrow = (static_cast<int64_t>(b) * a.nh + head) * S;
-  for (int i = threadIdx.x; i < S; i += kThreads) {
-    lse2[i] = a.lse[lrow + i] * 1.4426950408889634f;
-    dl[i] = a.delta[lrow + i];
+  TL qt, dt;
+  qt.load(qbase, a.qst, 0, Lq);
+  dt.load(dobase, a.dost, 0, Lq);
+  const int64_t lrow = (static_cast<int64_t>(b) * a.nh + head) * Lq;
+  for (int i = threadIdx.x; i < nqb * kKB; i += kThreads) {
+    lse2[i] = i < Lq ? a.lse[lrow + i] * kLog2e : INFINITY;  // tail queries: P = 0
+    dl[i] = i < Lq ? a.delta[lrow + i] : 0.f;
   }
-  bf16x8 kf[4], vf[4];
+  const E* krow = static_cast<const E*>(a.k) + b * a.ksb + static_cast<int64_t>(kk) * a.kst + head * HD;
+  const E* vrow = static_cast<const E*>(a.v) + b * a.vsb + static_cast<int64_t>(kk) * a.vst + head * HD;
+  u32x4 kf[QCH], vf[QCH];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = *reinterpret_cast<const bf16x8*>(base + H + static_cast<int64_t>(kk) * tok + 16 * s + 8 * hh);
-    vf[s] = *reinterpret_cast<const bf16x8*>(base + 2 * H + static_cast<int64_t>(kk) * tok + 16 * s + 8 * hh);
+  for (int j = 0; j < QCH; ++j) {
+    kf[j] = *reinterpret_cast<const u32x4*>(krow + (2 * j + hh) * TL::CH);
+    vf[j] = *reinterpret_cast<const u32x4*>(vrow + (2 * j + hh) * TL::CH);
   }
-  const float bk = a.bias ? fmaxf(a.bias[static_cast<int64_t>(b) * S + kk] * 1.4426950408889634f, -1e30f) : 0.f;
+  const float bk = a.kbias ? fmaxf(a.kbias[static_cast<int64_t>(b) * Lk + kk] * kLog2e, -1e30f) : 0.f;
+  const float* mcol = MB ? a.mbias + b * a.mbb + head * a.mbh + kk : nullptr;
   const uint32_t key = rng_key_for(a.rng_key, b, head);
-  store_rows(qx, smem);
-  store_t(qx, reinterpret_cast<unsigned short*>(smem + kKTileBytes));
-  store_rows(dx, smem + kKTileBytes + kVTileBytes);
-  store_t(dx, reinterpret_cast<unsigned short*>(smem + 2 * kKTileBytes + kVTileBytes));
+  const uint32_t lke = static_cast<uint32_t>(lk_even4(Lk));
+  qt.store_rows(smem);
+  qt.store_t(reinterpret_cast<E*>(smem + TL::ROW_BYTES));
+  dt.store_rows(smem + TL::ROW_BYTES + TL::T_BYTES);
+  dt.store_t(reinterpret_cast<E*>(smem + 2 * TL::ROW_BYTES + TL::T_BYTES));
   __syncthreads();
 
-  f32x16 dkt[2] = {f32x16{0}, f32x16{0}}, dvt[2] = {f32x16{0}, f32x16{0}};
-  const int nqb = S / kKB;
+  f32x16 dkt[NU], dvt[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) dkt[u] = dvt[u] = f32x16{0};
   for (int qb = 0; qb < nqb; ++qb) {
-    const unsigned char* buf = smem + (qb & 1) * kDkvBuf;
-    const unsigned short* qt = reinterpret_cast<const unsigned short*>(buf + kKTileBytes);
-    const unsigned char* dorows = buf + kKTileBytes + kVTileBytes;
-    const unsigned short* dot = reinterpret_cast<const unsigned short*>(buf + 2 * kKTileBytes + kVTileBytes);
+    const unsigned char* buf = smem + (qb & 1) * BUF;
+    const E* qti = reinterpret_cast<const E*>(buf + TL::ROW_BYTES);
+    const unsigned char* dorows = buf + TL::ROW_BYTES + TL::T_BYTES;
+    const E* doti = reinterpret_cast<const E*>(buf + 2 * TL::ROW_BYTES + TL::T_BYTES);
     if (qb + 1 < nqb) {
-      load_pair(qx, base, tok, (qb + 1) * kKB);
-      load_pair(dx, dobase, H, (qb + 1) * kKB);
+      qt.load(qbase, a.qst, (qb + 1) * kKB, Lq);
+      dt.load(dobase, a.dost, (qb + 1) * kKB, Lq);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      float mb[16];
+      if constexpr (MB) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qq = qb * kKB + 32 * t + 8 * (i >> 2) + 4 * hh + (i & 3);
+          mb[i] = qq < Lq ? mbias_log2(mcol, static_cast<int64_t>(qq) * a.mbq) : 0.f;
+        }
+      }
       f32x16 sa = f32x16{0}, dp = f32x16{0};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(buf, 32 * t + r, s, hh), kf[s], sa, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(dorows, 32 * t + r, s, hh), vf[s], dp, 0, 0, 0);
+      for (int j = 0; j < QCH; ++j) {
+        EL::mma_chunk(sa, TL::frag(buf, 32 * t + r, 2 * j + hh), kf[j]);
+        EL::mma_chunk(dp, TL::frag(dorows, 32 * t + r, 2 * j + hh), vf[j]);
       }
       f32x16 pd;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int qq = qb * kKB + 32 * t + 8 * g + 4 * hh;
-        const float4 lv = *reinterpret_cast<const float4*>(lse2 + qq);
-        const float4 dv = *reinterpret_cast<const float4*>(dl + qq);
+        const int q0 = qb * kKB + 32 * t + 8 * g + 4 * hh;
+        const float4 lv = *reinterpret_cast<const float4*>(lse2 + q0);
+        const float4 dv = *reinterpret_cast<const float4*>(dl + q0);
         const float ll[4] = {lv.x, lv.y, lv.z, lv.w}, dd[4] = {dv.x, dv.y, dv.z, dv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g + e;
           float z = 1.f;
           if (a.drop_thr) {
-            const uint32_t idx = static_cast<uint32_t>(qq + e) * static_cast<uint32_t>(S) + kk;
+            const uint32_t idx = static_cast<uint32_t>(q0 + e) * lke + static_cast<uint32_t>(kk);
             const uint32_t hsh = mix32(idx >> 1, key);
-            z = ((kk & 1) ? (hsh >> 16) : (hsh & 0xffffu)) < a.drop_thr ? 0.f : a.drop_scale;
+            z = ((idx & 1) ? (hsh >> 16) : (hsh & 0xffffu)) < a.drop_thr ? 0.f : a.drop_scale;
           }
-          const float pr = fast_exp2(fmaf(sa[i], a.scale_log2, bk) - ll[e]);
+          float x = fmaf(sa[i], a.scale_log2, bk);
+          if constexpr (MB) x += mb[i];
+          const float pr = fast_exp2(x - ll[e]);
           pd[i] = pr * z;
           sa[i] = pr * fmaf(dp[i], z, -dd[e]);  // dS
         }
       }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pf = pack_frag(pd, s), dsf = pack_frag(sa, s);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          dvt[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_from_image(dot, kVtStride, 32 * u + r, 32 * t + 16 * s, hh),
-                                                           pf, dvt[u], 0, 0, 0);
-          dkt[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_from_image(qt, kVtStride, 32 * u + r, 32 * t + 16 * s, hh),
-                                                           dsf, dkt[u], 0, 0, 0);
-        }
+      for (int u = 0; u < NU; ++u) {
+        EL::mma_img(dvt[u], doti, 32 * u + r, 32 * t, pd, hh);
+        EL::mma_img(dkt[u], qti, 32 * u + r, 32 * t, sa, hh);
       }
     }
     if (qb + 1 < nqb) {
-      unsigned char* nb = smem + ((qb + 1) & 1) * kDkvBuf;
-      store_rows(qx, nb);
-      store_t(qx, reinterpret_cast<unsigned short*>(nb + kKTileBytes));
-      store_rows(dx, nb + kKTileBytes + kVTileBytes);
-      store_t(dx, reinterpret_cast<unsigned short*>(nb + 2 * kKTileBytes + kVTileBytes));
+      unsigned char* nb = smem + ((qb + 1) & 1) * BUF;
+      qt.store_rows(nb);
+      qt.store_t(reinterpret_cast<E*>(nb + TL::ROW_BYTES));
+      dt.store_rows(nb + TL::ROW_BYTES + TL::T_BYTES);
+      dt.store_t(reinterpret_cast<E*>(nb + 2 * TL::ROW_BYTES + TL::T_BYTES));
     }
     __syncthreads();
   }
-  if (!active) return;
-  unsigned short* dk = a.dqkv + (static_cast<int64_t>(b) * S + kk) * tok + H + head * kHD;
-  unsigned short* dv = dk + H;
+  if (kv >= Lk) return;
+  E* dk = static_cast<E*>(a.dk) + b * a.dksb + static_cast<int64_t>(kv) * a.dkst + head * HD;
+  E* dv = static_cast<E*>(a.dv) + b * a.dvsb + static_cast<int64_t>(kv) * a.dvst + head * HD;
+  const float sc = a.scale;
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      us4 wk, wv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        wk[e] = f2bf(dkt[u][4 * g + e] * 0.125f);
-        wv[e] = f2bf(dvt[u][4 * g + e]);
-      }
-      *reinterpret_cast<us4*>(dk + 32 * u + 8 * g + 4 * hh) = wk;
-      *reinterpret_cast<us4*>(dv + 32 * u + 8 * g + 4 * hh) = wv;
+      EL::store4(dk + 32 * u + 8 * g + 4 * hh, dkt[u][4 * g] * sc, dkt[u][4 * g + 1] * sc, dkt[u][4 * g + 2] * sc,
+                 dkt[u][4 * g + 3] * sc);
+      EL::store4(dv + 32 * u + 8 * g + 4 * hh, dvt[u][4 * g], dvt[u][4 * g + 1], dvt[u][4 * g + 2], dvt[u][4 * g + 3]);
     }
 }
 
-__global__ void attn_mask_kernel(int B, int nh, int S, uint32_t thr, uint32_t base_key, uint8_t* out) {
-  const int64_t n = static_cast<int64_t>(B) * nh * S * S;
+__global__ void attn_mask_kernel(int B, int nh, int Lq, int Lk, uint32_t thr, uint32_t base_key, uint8_t* out) {
+  const int64_t n = static_cast<int64_t>(B) * nh * Lq * Lk;
+  const uint32_t lke = static_cast<uint32_t>(lk_even4(Lk));
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int key = static_cast<int>(i % S);
-    const int q = static_cast<int>((i / S) % S);
-    const int head = static_cast<int>((i / S / S) % nh);
-    const int b = static_cast<int>(i / S / S / nh);
-    const uint32_t idx = static_cast<uint32_t>(q) * static_cast<uint32_t>(S) + key;
+    const int key = static_cast<int>(i % Lk);
+    const int q = static_cast<int>((i / Lk) % Lq);
+    const int head = static_cast<int>((i / Lk / Lq) % nh);
+    const int b = static_cast<int>(i / Lk / Lq / nh);
+    const uint32_t idx = static_cast<uint32_t>(q) * lke + static_cast<uint32_t>(key);
     const uint32_t h = mix32(idx >> 1, rng_key_for(base_key, b, head));
     const uint32_t d = (idx & 1) ? (h >> 16) : (h & 0xffffu);
     out[i] = d >= thr;
   }
 }
 
-void fill_args(AttnArgs& a, const void* qkv, const float* bias, void* out, float* lse, int B, int S, int nh,
-               float p, uint64_t seed, uint64_t offset) {
-  a.qkv = static_cast<const unsigned short*>(qkv);
-  a.bias = bias;
-  a.out = static_cast<unsigned short*>(out);
-  a.lse = lse;
-  a.B = B;
-  a.S = S;
-  a.nh = nh;
-  a.scale_log2 = 1.4426950408889634f * 0.125f;
-  uint32_t thr = p > 0.f ? static_cast<uint32_t>(p * 65536.0f + 0.5f) : 0u;
-  if (thr > 65535u) thr = 65535u;
-  a.drop_thr = thr;
-  a.drop_scale = thr ? 65536.0f / static_cast<float>(65536u - thr) : 1.f;
-  a.rng_key = static_cast<uint32_t>(seed) ^ static_cast<uint32_t>(seed >> 32) * 0x85ebca6bu ^
-              static_cast<uint32_t>(offset) * 0xc2b2ae35u ^ static_cast<uint32_t>(offset >> 32);
+// ---- host side ----------------------------------------------------------------------------------
+template <typename E, int HD>
+struct Cfg {
+  using TL = Tile<E, HD>;
+  static size_t fwd(int Lk) {
+    return 2 * static_cast<size_t>(TL::ROW_BYTES + TL::T_BYTES) + 4 * static_cast<size_t>((Lk + kKB - 1) / kKB * kKB);
+  }
+  static size_t dq(int Lk) {
+    return 2 * static_cast<size_t>(2 * TL::ROW_BYTES + TL::T_BYTES) +
+           4 * static_cast<size_t>((Lk + kKB - 1) / kKB * kKB);
+  }
+  static size_t dkv(int Lq) {
+    return 2 * static_cast<size_t>(2 * (TL::ROW_BYTES + TL::T_BYTES)) +
+           8 * static_cast<size_t>((Lq + kKB - 1) / kKB * kKB);
+  }
+  static bool fits(int Lq, int Lk) {
+    return fwd(Lk) <= kMaxLds && dq(Lk) <= kMaxLds && dkv(Lq) <= kMaxLds;
+  }
+  static void launch_fwd(hipStream_t st, const Args& a) {
+    dim3 grid((a.Lq + kQB - 1) / kQB, a.nh, a.B);
+    if (a.mbias)
+      hipLaunchKernelGGL((attn_fwd_kernel<E, HD, true>), grid, dim3(kThreads), fwd(a.Lk), st, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<E, HD, false>), grid, dim3(kThreads), fwd(a.Lk), st, a);
+  }
+  static void launch_bwd(hipStream_t st, const Args& a) {
+    dim3 gq((a.Lq + kQB - 1) / kQB, a.nh, a.B), gk((a.Lk + kQB - 1) / kQB, a.nh, a.B);
+    if (a.mbias) {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<E, HD, true>), gq, dim3(kThreads), dq(a.Lk), st, a);
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, HD, true>), gk, dim3(kThreads), dkv(a.Lq), st, a);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<E, HD, false>), gq, dim3(kThreads), dq(a.Lk), st, a);
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, HD, false>), gk, dim3(kThreads), dkv(a.Lq), st, a);
+    }
+  }
+};
+
+// dtype 0 = bf16, 1 = fp32
+template <typename F>
+bool dispatch(int dtype, int hd, F&& f) {
+  if (dtype == 0 && hd == 32) return f(Cfg<unsigned short, 32>{}), true;
+  if (dtype == 0 && hd == 64) return f(Cfg<unsigned short, 64>{}), true;
+  if (dtype == 0 && hd == 128) return f(Cfg<unsigned short, 128>{}), true;
+  if (dtype == 1 && hd == 32) return f(Cfg<float, 32>{}), true;
+  if (dtype == 1 && hd == 64) return f(Cfg<float, 64>{}), true;
+  return false;
 }
 
-size_t fwd_lds(int S) { return 2 * static_cast<size_t>(kFwdBufBytes) + static_cast<size_t>(S) * 4; }
+uint32_t drop_threshold(float p) {
+  uint32_t thr = p > 0.f ? static_cast<uint32_t>(p * 65536.0f + 0.5f) : 0u;
+  return thr > 65535u ? 65535u : thr;
+}
+uint32_t mix_key(uint64_t seed, uint64_t offset) {
+  return static_cast<uint32_t>(seed) ^ static_cast<uint32_t>(seed >> 32) * 0x85ebca6bu ^
+         static_cast<uint32_t>(offset) * 0xc2b2ae35u ^ static_cast<uint32_t>(offset >> 32);
+}
 
 }  // namespace
 
 extern "C" {
 
-// Shapes the MFMA path covers: head_dim 64, S a multiple of 64 up to 2048 (the per-head key bias /
-// LSE / delta rows live in LDS next to the double-buffered tiles).
-int det_attn_supported(int S, int head_dim) {
-  return head_dim == kHD && S >= 64 && S % kKB == 0 && S <= 2048;
+// mirrored by determined_1_amd/ops/transformer.py:_AttnParams (field order matters)
+struct DetAttnParams {
+  const void *q, *k, *v, *dout;
+  void *out, *dq, *dk, *dv;
+  float *lse, *delta;
+  const float *kbias, *mbias;
+  int64_t qsb, qst, ksb, kst, vsb, vst, osb, ost, dosb, dost, dqsb, dqst, dksb, dkst, dvsb, dvst;
+  int64_t mbb, mbh, mbq;
+  int32_t B, Lq, Lk, nh, hd, dtype;
+  float p, scale;
+  uint64_t seed, offset;
+};
+
+// Which (dtype, head_dim, Lq, Lk) the MFMA kernels cover (LDS holds the double-buffered tiles plus
+// the key-bias / LSE / delta rows).
+int det_attn_supported(int dtype, int hd, int Lq, int Lk) {
+  if (Lq <= 0 || Lk <= 0) return 0;
+  bool ok = false;
+  dispatch(dtype, hd, [&](auto cfg) { ok = decltype(cfg)::fits(Lq, Lk); });
+  return ok ? 1 : 0;
 }
 
-// qkv [B, S, 3, nh, 64] bf16; bias [B, S] fp32 (nullable); out [B, S, nh*64] bf16; lse [B, nh, S].
-int det_attn_fwd(void* stream, const void* qkv, const float* bias, void* out, float* lse, int B, int S, int nh,
-                 float p, uint64_t seed, uint64_t offset) {
-  if (!det_attn_supported(S, kHD) || B <= 0 || nh <= 0) return -1;
-  AttnArgs a;
-  fill_args(a, qkv, bias, out, lse, B, S, nh, p, seed, offset);
+static int fill(Args& a, const DetAttnParams* P) {
+  if (!P || P->B <= 0 || P->nh <= 0 || !det_attn_supported(P->dtype, P->hd, P->Lq, P->Lk)) return -1;
+  a.q = P->q;
+  a.k = P->k;
+  a.v = P->v;
+  a.dout = P->dout;
+  a.out = P->out;
+  a.dq = P->dq;
+  a.dk = P->dk;
+  a.dv = P->dv;
+  a.lse = P->lse;
+  a.delta = P->delta;
+  a.kbias = P->kbias;
+  a.mbias = P->mbias;
+  a.qsb = P->qsb, a.qst = P->qst, a.ksb = P->ksb, a.kst = P->kst, a.vsb = P->vsb, a.vst = P->vst;
+  a.osb = P->osb, a.ost = P->ost, a.dosb = P->dosb, a.dost = P->dost;
+  a.dqsb = P->dqsb, a.dqst = P->dqst, a.dksb = P->dksb, a.dkst = P->dkst, a.dvsb = P->dvsb, a.dvst = P->dvst;
+  a.mbb = P->mbb, a.mbh = P->mbh, a.mbq = P->mbq;
+  a.B = P->B, a.Lq = P->Lq, a.Lk = P->Lk, a.nh = P->nh;
+  a.scale = P->scale;
+  a.scale_log2 = P->scale * kLog2e;
+  a.drop_thr = drop_threshold(P->p);
+  a.drop_scale = a.drop_thr ? 65536.0f / static_cast<float>(65536u - a.drop_thr) : 1.f;
+  a.rng_key = mix_key(P->seed, P->offset);
+  return 0;
+}
+
+// out = softmax(q k^T * scale + bias) v (dropout p), lse [B, nh, Lq] fp32.
+int det_attn_forward(void* stream, const DetAttnParams* P) {
+  Args a;
+  if (fill(a, P) || !a.out || !a.lse) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  dim3 grid((S + kQB - 1) / kQB, nh, B);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(kThreads), fwd_lds(S), st, a);
+  dispatch(P->dtype, P->hd, [&](auto cfg) { decltype(cfg)::launch_fwd(st, a); });
   return static_cast<int>(hipGetLastError());
 }
 
-// Backward: dqkv [B, S, 3, nh, 64] (fully overwritten); delta: [B, nh, S] fp32 workspace.
-int det_attn_bwd(void* stream, const void* qkv, const float* bias, const void* out, const void* dout, const float* lse,
-                 float* delta, void* dqkv, int B, int S, int nh, float p, uint64_t seed, uint64_t offset) {
-  if (!det_attn_supported(S, kHD) || B <= 0 || nh <= 0) return -1;
-  AttnArgs f;
-  fill_args(f, qkv, bias, nullptr, nullptr, B, S, nh, p, seed, offset);
-  BwdArgs a;
-  a.qkv = static_cast<const unsigned short*>(qkv);
-  a.bias = bias;
-  a.out = static_cast<const unsigned short*>(out);
-  a.dout = static_cast<const unsigned short*>(dout);
-  a.lse = lse;
-  a.delta = delta;
-  a.dqkv = static_cast<unsigned short*>(dqkv);
-  a.B = B;
-  a.S = S;
-  a.nh = nh;
-  a.scale_log2 = f.scale_log2;
-  a.drop_thr = f.drop_thr;
-  a.drop_scale = f.drop_scale;
-  a.rng_key = f.rng_key;
+// dq/dk/dv fully overwritten (rows < Lq / Lk); delta [B, nh, Lq] fp32 workspace.
+int det_attn_backward(void* stream, const DetAttnParams* P) {
+  Args a;
+  if (fill(a, P) || !a.dout || !a.dq || !a.dk || !a.dv || !a.delta) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  dim3 grid((S + kQB - 1) / kQB, nh, B);
-  const size_t lds_dq = 2 * static_cast<size_t>(kDqBuf) + static_cast<size_t>(S) * 4;
-  const size_t lds_dkv = 2 * static_cast<size_t>(kDkvBuf) + 2 * static_cast<size_t>(S) * 4;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(kThreads), lds_dq, st, a);
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(kThreads), lds_dkv, st, a);
+  dispatch(P->dtype, P->hd, [&](auto cfg) { decltype(cfg)::launch_bwd(st, a); });
   return static_cast<int>(hipGetLastError());
 }
 
-// The keep mask (1 = kept) the kernels derive for (p, seed, offset): [B, nh, S, S] uint8 (tests).
-int det_attn_dropout_mask(void* stream, int B, int nh, int S, float p, uint64_t seed, uint64_t offset, uint8_t* out) {
-  AttnArgs a;
-  fill_args(a, nullptr, nullptr, nullptr, nullptr, B, S, nh, p, seed, offset);
-  hipLaunchKernelGGL(attn_mask_kernel, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), B, nh, S,
-                     a.drop_thr, a.rng_key, out);
+// The keep mask (1 = kept) the kernels derive for (p, seed, offset): [B, nh, Lq, Lk] uint8 (tests).
+int det_attn_dropout_mask(void* stream, int B, int nh, int Lq, int Lk, float p, uint64_t seed, uint64_t offset,
+                          uint8_t* out) {
+  hipLaunchKernelGGL(attn_mask_kernel, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), B, nh, Lq, Lk,
+                     drop_threshold(p), mix_key(seed, offset), out);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -724,37 +724,6 @@ __global__ void __launch_bounds__(kThreads) dropout_mask_kernel(int64_t ngroups,
   }
 }
 
-// dqkv[b, s, j, h, :] = g_j[b, h, s, :] for j = q, k, v: the backward of reading Q/K/V as strided
-// views of one [B, S, 3, nh, hd] GEMM output.  One 16 B vector per thread.
-struct PackArgs {
-  const void* g[3];
-  int64_t sb[3], sh[3], ss[3];  // element strides of each [B, nh, S, hd] input (hd stride 1)
-  void* out;
-  int B, S, nh, hd;
-};
-
-template <typename T>
-__global__ void __launch_bounds__(kThreads) pack_qkv_kernel(PackArgs a, int64_t nvec) {
-  const int v8 = a.hd / 8;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
-       i += static_cast<int64_t>(gridDim.x) * kThreads) {
-    int64_t r = i;
-    const int dv = static_cast<int>(r % v8); r /= v8;
-    const int h = static_cast<int>(r % a.nh); r /= a.nh;
-    const int j = static_cast<int>(r % 3); r /= 3;
-    const int s = static_cast<int>(r % a.S);
-    const int b = static_cast<int>(r / a.S);
-    const T* src = static_cast<const T*>(a.g[j]) + b * a.sb[j] + h * a.sh[j] + s * a.ss[j] + dv * 8;
-    T* dst = static_cast<T*>(a.out) + i * 8;
-    if (sizeof(T) == 2) {
-      *reinterpret_cast<us8*>(dst) = *reinterpret_cast<const us8*>(src);
-    } else {
-      reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
-      reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
-    }
-  }
-}
-
 Rng make_rng(float p, uint64_t seed, uint64_t offset) {
   Rng g;
   g.k0 = static_cast<uint32_t>(seed);
@@ -964,28 +933,6 @@ int det_tf_colsum(void* stream, int dtype, const void* x, int64_t rows, int C, v
     hipLaunchKernelGGL(colsum_finalize<float>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
                        g.nrb, C, C, static_cast<float*>(out), nullptr, nullptr);
   }
-  return static_cast<int>(hipGetLastError());
-}
-
-// Pack the three attention input gradients ([B, nh, S, hd] with arbitrary batch/head/seq strides,
-// unit hd stride, hd % 8 == 0) into one contiguous [B, S, 3, nh, hd] tensor.
-int det_tf_pack_qkv(void* stream, int dtype, const void* gq, const void* gk, const void* gv, const int64_t* strides9,
-                    void* out, int B, int S, int nh, int hd) {
-  if (hd % 8 != 0 || B <= 0 || S <= 0) return -1;
-  PackArgs a;
-  a.g[0] = gq; a.g[1] = gk; a.g[2] = gv;
-  for (int j = 0; j < 3; ++j) {
-    a.sb[j] = strides9[3 * j];
-    a.sh[j] = strides9[3 * j + 1];
-    a.ss[j] = strides9[3 * j + 2];
-  }
-  a.out = out;
-  a.B = B; a.S = S; a.nh = nh; a.hd = hd;
-  const int64_t nvec = static_cast<int64_t>(B) * S * 3 * nh * (hd / 8);
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const int grid = grid_for(nvec, kThreads * 4);
-  if (dtype == 1) hipLaunchKernelGGL(pack_qkv_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, a, nvec);
-  else hipLaunchKernelGGL(pack_qkv_kernel<float>, dim3(grid), dim3(kThreads), 0, st, a, nvec);
   return static_cast<int>(hipGetLastError());
 }
 

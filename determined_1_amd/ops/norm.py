@@ -115,6 +115,8 @@ class _BNActTrain(torch.autograd.Function):
         ctx.mask_mode = mask_mode
         ctx.has_res = residual is not None
         ctx.link = link  # producer ctx of the residual (identity shortcut) or None
+        if link is not None:
+            link.expects_extra = True  # a fused dgrad into the producer must wait for this gradient
         ctx.extra_dy = None  # set by the consumer of this output as identity shortcut
         ctx.fmt = fmt
         ctx.save_for_backward(x, mbits, weight, stats)
@@ -192,6 +194,7 @@ class _LinkedConv(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.conv = (stride, padding, dilation, groups)
         ctx.link = link
+        link.expects_extra = True  # a fused dgrad into the producer must wait for this gradient
         return F.conv2d(x, weight, None, stride, padding, dilation, groups)
 
     @staticmethod

@@ -27,7 +27,6 @@ from determined_1_amd.ops.arena import landing_buffer
 FALLBACKS = {"count": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 _MAX_H = 8192  # det_tf_ln_max_hidden() (workgroup-per-row kernels above 2048, e.g. ALBERT-xxlarge)
-ctypes_i64 = ctypes.c_int64
 _offsets = itertools.count(1)
 _seed = []  # lazily cached: the trial seeds torch before the first dropout call
 
@@ -269,80 +268,139 @@ def _split_qkv(qkv: torch.Tensor, nh: int):
     return qkv.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)  # 3 x [B, nh, S, hd] views
 
 
-class _MFMAAttention(torch.autograd.Function):
-    """``det_attention.hip``: hand-written MFMA forward/backward (head_dim 64, S in 128..512).
-    Reads Q/K/V straight from the fused [B, S, 3H] GEMM output and writes dQ/dK/dV straight into
-    its gradient; dropout masks are regenerated from (seed, offset) in the backward."""
+class _AttnParams(ctypes.Structure):
+    """Mirror of ``DetAttnParams`` (det_attention.hip)."""
+    _fields_ = ([(n, ctypes.c_void_p) for n in ("q", "k", "v", "dout", "out", "dq", "dk", "dv", "lse", "delta",
+                                                "kbias", "mbias")]
+                + [(n, ctypes.c_int64) for n in ("qsb", "qst", "ksb", "kst", "vsb", "vst", "osb", "ost", "dosb",
+                                                 "dost", "dqsb", "dqst", "dksb", "dkst", "dvsb", "dvst", "mbb", "mbh",
+                                                 "mbq")]
+                + [(n, ctypes.c_int32) for n in ("B", "Lq", "Lk", "nh", "hd", "dtype")]
+                + [("p", ctypes.c_float), ("scale", ctypes.c_float), ("seed", ctypes.c_uint64),
+                   ("offset", ctypes.c_uint64)])
+
+
+_ATTN_DT = {torch.bfloat16: 0, torch.float32: 1}
+
+
+def mfma_attention_supported(Lq: int, head_dim: int, dtype: torch.dtype = torch.bfloat16,
+                             Lk: Optional[int] = None) -> bool:
+    """Whether ``det_attention.hip`` covers the shape (bf16 head_dim 32/64/128, fp32 32/64, any
+    length up to what the LDS tiles allow).  ``DET_ATTN=composite`` forces the PyTorch path."""
+    import os
+
+    if os.environ.get("DET_ATTN", "mfma") != "mfma" or dtype not in _ATTN_DT:
+        return False
+    return bool(_lib.get_lib().det_attn_supported(_ATTN_DT[dtype], head_dim, Lq, Lq if Lk is None else Lk))
+
+
+def _view_ok(t: torch.Tensor, hd: int) -> bool:
+    """[B, L, nh*hd] token-major view the kernels read in place: unit inner stride, 16-B aligned rows."""
+    es = t.element_size()
+    return (t.dim() == 3 and t.stride(2) == 1 and t.data_ptr() % 16 == 0 and (t.stride(1) * es) % 16 == 0
+            and (t.stride(0) * es) % 16 == 0)
+
+
+def _bias_args(bias: Optional[torch.Tensor], B: int, nh: int, Lq: int, Lk: int):
+    """Split an additive / boolean SDPA mask into the kernels' per-key row [B, Lk] (padding masks)
+    or a strided full bias (element (b, h, q, k) at b*sb + h*sh + q*sq + k).  -> (kbias, mbias, strides)"""
+    if bias is None:
+        return None, None, (0, 0, 0)
+    if bias.dtype == torch.bool:  # SDPA semantics: True = attend
+        bias = torch.zeros(bias.shape, dtype=torch.float32, device=bias.device).masked_fill_(~bias, float("-inf"))
+    bias = bias.float()
+    while bias.dim() < 4:
+        bias = bias.unsqueeze(0)
+    if bias.shape[1] == 1 and bias.shape[2] == 1:  # [B|1, 1, 1, Lk]: a per-key row
+        return bias.reshape(bias.shape[0], Lk).expand(B, Lk).contiguous(), None, (0, 0, 0)
+    full = bias.expand(B, nh, Lq, Lk)
+    if full.stride(3) != 1:
+        full = bias.contiguous().expand(B, nh, Lq, Lk)
+    return None, full, (full.stride(0), full.stride(1), full.stride(2))
+
+
+def _attn_params(q, k, v, nh: int, kbias, mbias, mstrides, p: float, scale: float) -> _AttnParams:
+    B, Lq, H = q.shape
+    P = _AttnParams()
+    P.q, P.k, P.v = q.data_ptr(), k.data_ptr(), v.data_ptr()
+    P.qsb, P.qst = q.stride(0), q.stride(1)
+    P.ksb, P.kst = k.stride(0), k.stride(1)
+    P.vsb, P.vst = v.stride(0), v.stride(1)
+    P.kbias, P.mbias = _ptr(kbias), _ptr(mbias)
+    P.mbb, P.mbh, P.mbq = mstrides
+    P.B, P.Lq, P.Lk, P.nh, P.hd, P.dtype = B, Lq, k.shape[1], nh, H // nh, _ATTN_DT[q.dtype]
+    P.p, P.scale = p, scale
+    return P
+
+
+def _attn_forward(q, k, v, nh, kbias, mbias, mstrides, p, scale):
+    B, Lq, H = q.shape
+    out = torch.empty(B, Lq, H, dtype=q.dtype, device=q.device)
+    lse = torch.empty(B, nh, Lq, dtype=torch.float32, device=q.device)
+    seed, off = next_rng() if p > 0 else (0, 0)
+    P = _attn_params(q, k, v, nh, kbias, mbias, mstrides, p, scale)
+    P.out, P.lse, P.osb, P.ost = out.data_ptr(), lse.data_ptr(), out.stride(0), out.stride(1)
+    P.seed, P.offset = seed, off
+    _lib.check(_lib.get_lib().det_attn_forward(_stream(q), ctypes.byref(P)), "det_attn_forward")
+    return out, lse, seed, off
+
+
+def _attn_backward(ctx, dout, q, k, v, out, lse, kbias, mbias, dq, dk, dv):
+    dout = dout if _view_ok(dout, 1) else dout.contiguous()
+    P = _attn_params(q, k, v, ctx.nh, kbias, mbias, ctx.mstrides, ctx.p, ctx.scale)
+    delta = torch.empty_like(lse)
+    P.out, P.lse, P.delta, P.dout = out.data_ptr(), lse.data_ptr(), delta.data_ptr(), dout.data_ptr()
+    P.osb, P.ost, P.dosb, P.dost = out.stride(0), out.stride(1), dout.stride(0), dout.stride(1)
+    P.dq, P.dk, P.dv = dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+    P.dqsb, P.dqst, P.dksb, P.dkst, P.dvsb, P.dvst = (dq.stride(0), dq.stride(1), dk.stride(0), dk.stride(1),
+                                                      dv.stride(0), dv.stride(1))
+    P.seed, P.offset = ctx.seed, ctx.off
+    _lib.check(_lib.get_lib().det_attn_backward(_stream(q), ctypes.byref(P)), "det_attn_backward")
+
+
+class _PackedQKVAttention(torch.autograd.Function):
+    """``det_attention.hip`` on the fused [B, S, 3H] QKV GEMM output: Q/K/V read in place as strided
+    views, dQ/dK/dV written straight into the [B, S, 3H] gradient (no split/pack copies); dropout
+    masks are regenerated from (seed, offset) in the backward."""
 
     @staticmethod
-    def forward(ctx, qkv, bias, p, nh):
-        B, S, H3 = qkv.shape
-        lib = _lib.get_lib()
-        out = torch.empty(B, S, H3 // 3, dtype=qkv.dtype, device=qkv.device)
-        lse = torch.empty(B, nh, S, dtype=torch.float32, device=qkv.device)
-        seed, off = next_rng() if p > 0 else (0, 0)
-        _lib.check(lib.det_attn_fwd(_stream(qkv), qkv.data_ptr(), _ptr(bias), out.data_ptr(), lse.data_ptr(), B, S, nh,
-                                    p, seed, off), "det_attn_fwd")
-        ctx.save_for_backward(qkv, bias, out, lse)
-        ctx.p, ctx.nh, ctx.seed, ctx.off = p, nh, seed, off
+    def forward(ctx, qkv, kbias, mbias, mstrides, p, nh, scale):
+        H = qkv.shape[2] // 3
+        q, k, v = qkv[..., :H], qkv[..., H:2 * H], qkv[..., 2 * H:]
+        out, lse, ctx.seed, ctx.off = _attn_forward(q, k, v, nh, kbias, mbias, mstrides, p, scale)
+        ctx.save_for_backward(qkv, kbias, mbias, out, lse)
+        ctx.p, ctx.nh, ctx.scale, ctx.mstrides = p, nh, scale, mstrides
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, bias, out, lse = ctx.saved_tensors
-        B, S, H3 = qkv.shape
-        lib = _lib.get_lib()
-        dout = dout.contiguous()
-        delta = torch.empty_like(lse)
+        qkv, kbias, mbias, out, lse = ctx.saved_tensors
+        H = qkv.shape[2] // 3
         dqkv = torch.empty_like(qkv)
-        _lib.check(lib.det_attn_bwd(_stream(qkv), qkv.data_ptr(), _ptr(bias), out.data_ptr(), dout.data_ptr(),
-                                    lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), B, S, ctx.nh, ctx.p, ctx.seed,
-                                    ctx.off), "det_attn_bwd")
-        return dqkv, None, None, None
+        _attn_backward(ctx, dout, qkv[..., :H], qkv[..., H:2 * H], qkv[..., 2 * H:], out, lse, kbias, mbias,
+                       dqkv[..., :H], dqkv[..., H:2 * H], dqkv[..., 2 * H:])
+        return dqkv, None, None, None, None, None, None
 
 
-def mfma_attention_supported(S: int, head_dim: int) -> bool:
-    import os
-
-    if os.environ.get("DET_ATTN", "mfma") != "mfma":
-        return False
-    return bool(_lib.get_lib().det_attn_supported(S, head_dim))
-
-
-class _QKVAttention(torch.autograd.Function):
-    """Self-attention reading Q/K/V as strided views of the fused QKV GEMM output.  Forward and
-    backward call the AOTriton memory-efficient attention ops directly; the backward packs dQ/dK/dV
-    straight into the [B, S, 3H] gradient of the GEMM output with one ``det_tf_pack_qkv`` pass
-    instead of autograd's unbind->stack->permute copies (two full passes per layer)."""
+class _Attention(torch.autograd.Function):
+    """``det_attention.hip`` on separate Q [B, Lq, H] and K/V [B, Lk, H] views (cross-attention,
+    DETR's projections with positional embeddings)."""
 
     @staticmethod
-    def forward(ctx, qkv, mask_bias, p, nh):
-        B, S, H3 = qkv.shape
-        q, k, v = _split_qkv(qkv, nh)
-        bias = mask_bias.expand(B, nh, S, S) if mask_bias is not None else None
-        out, lse, seed, off = torch.ops.aten._scaled_dot_product_efficient_attention(q, k, v, bias, True, p, False)
-        ctx.save_for_backward(qkv, mask_bias, out, lse, seed, off)
-        ctx.p, ctx.nh = p, nh
-        return out.transpose(1, 2).reshape(B, S, H3 // 3)
+    def forward(ctx, q, k, v, kbias, mbias, mstrides, p, nh, scale):
+        out, lse, ctx.seed, ctx.off = _attn_forward(q, k, v, nh, kbias, mbias, mstrides, p, scale)
+        ctx.save_for_backward(q, k, v, kbias, mbias, out, lse)
+        ctx.p, ctx.nh, ctx.scale, ctx.mstrides = p, nh, scale, mstrides
+        return out
 
     @staticmethod
-    def backward(ctx, dctx):
-        qkv, mask_bias, out, lse, seed, off = ctx.saved_tensors
-        B, S, H3 = qkv.shape
-        nh = ctx.nh
-        hd = H3 // 3 // nh
-        q, k, v = _split_qkv(qkv, nh)
-        bias = mask_bias.expand(B, nh, S, S) if mask_bias is not None else None
-        dout = dctx.contiguous().view(B, S, nh, hd).transpose(1, 2)
-        gq, gk, gv, _ = torch.ops.aten._scaled_dot_product_efficient_attention_backward(
-            dout, q, k, v, bias, out, lse, seed, off, ctx.p, [True, True, True, False], False)
-        dqkv = torch.empty_like(qkv)
-        strides = (ctypes_i64 * 9)(*[st for g in (gq, gk, gv) for st in g.stride()[:3]])
-        for g in (gq, gk, gv):
-            assert g.stride(3) == 1 and g.dtype == qkv.dtype
-        _lib.check(_lib.get_lib().det_tf_pack_qkv(_stream(qkv), _DT[qkv.dtype], gq.data_ptr(), gk.data_ptr(), gv.data_ptr(),
-                                                  strides, dqkv.data_ptr(), B, S, nh, hd), "det_tf_pack_qkv")
-        return dqkv, None, None, None
+    def backward(ctx, dout):
+        q, k, v, kbias, mbias, out, lse = ctx.saved_tensors
+        dq = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+        dk = torch.empty(k.shape, dtype=k.dtype, device=k.device)
+        dv = torch.empty(v.shape, dtype=v.dtype, device=v.device)
+        _attn_backward(ctx, dout, q, k, v, out, lse, kbias, mbias, dq, dk, dv)
+        return dq, dk, dv, None, None, None, None, None, None
 
 
 # ------------------------------------------------------------------------------------------------
@@ -389,37 +447,71 @@ def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: fl
         return _LayerNorm.apply(x, gamma, beta, float(eps))
 
 
+def _composite_attention(q, k, v, nh, bias, p, scale):
+    B, Lq, H = q.shape
+    hd = H // nh
+
+    def heads(t):
+        return t.reshape(B, t.shape[1], nh, hd).transpose(1, 2)
+
+    ctx = F.scaled_dot_product_attention(heads(q), heads(k), heads(v), attn_mask=bias, dropout_p=p, scale=scale)
+    return ctx.transpose(1, 2).reshape(B, Lq, H)
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, num_heads: int, *,
+              attn_bias: Optional[torch.Tensor] = None, p: float = 0.0, training: bool = True,
+              scale: Optional[float] = None) -> torch.Tensor:
+    """Multi-head attention on token-major tensors: q [B, Lq, H], k/v [B, Lk, H] (H = heads x
+    head_dim; any token stride, e.g. slices of a packed projection) -> [B, Lq, H].  ``attn_bias``
+    is an SDPA ``attn_mask`` (additive float or boolean keep-mask) broadcastable to
+    [B, heads, Lq, Lk]; a [B, 1, 1, Lk] mask takes the per-key-row path."""
+    p = float(p) if training else 0.0
+    (q, k, v, attn_bias), ac = _autocast(q, k, v, attn_bias)
+    B, Lq, H = q.shape
+    Lk, hd = k.shape[1], H // num_heads
+    scale = hd ** -0.5 if scale is None else float(scale)
+    if not (q.is_cuda and q.dtype == k.dtype == v.dtype and q.dtype in _ATTN_DT
+            and all(_view_ok(t, hd) for t in (q, k, v)) and v.shape[1] == Lk
+            and (attn_bias is None or not attn_bias.requires_grad)
+            and mfma_attention_supported(Lq, hd, q.dtype, Lk)):
+        if q.is_cuda:
+            FALLBACKS["count"] += 1
+        return _composite_attention(q, k, v, num_heads, attn_bias, p, scale)
+    kbias, mbias, mstrides = _bias_args(attn_bias, B, num_heads, Lq, Lk)
+    with torch.autocast("cuda", enabled=False) if ac else _null():
+        return _Attention.apply(q, k, v, kbias, mbias, mstrides, p, num_heads, scale)
+
+
 def qkv_self_attention(qkv: torch.Tensor, num_heads: int, mask_bias: Optional[torch.Tensor] = None, p: float = 0.0,
                        training: bool = True) -> torch.Tensor:
     """softmax(Q K^T / sqrt(d) + mask_bias) V over the heads of a fused [B, S, 3H] QKV tensor -> [B, S, H].
-    ``mask_bias`` is additive, broadcastable as [B, 1, 1, S]."""
+    ``mask_bias`` is an SDPA mask broadcastable to [B, heads, S, S] ([B, 1, 1, S] padding masks
+    take the per-key-row path)."""
     p = float(p) if training else 0.0
     (qkv, mask_bias), ac = _autocast(qkv, mask_bias)
     B, S, H3 = qkv.shape
-    hd = H3 // 3 // num_heads
-    if mask_bias is not None and mask_bias.dtype != qkv.dtype:
-        mask_bias = mask_bias.to(qkv.dtype)
-    # AOTriton efficient attention: bf16 (fp32 keeps the composite path)
-    if qkv.dtype != torch.bfloat16 or not _native(qkv, mask_bias, width=hd) or S % 16 != 0:
-        q, k, v = _split_qkv(qkv, num_heads)
-        ctx = F.scaled_dot_product_attention(q, k, v, attn_mask=mask_bias, dropout_p=p)
-        return ctx.transpose(1, 2).reshape(B, S, H3 // 3)
+    H = H3 // 3
+    hd = H // num_heads
+    if not (qkv.is_cuda and qkv.dtype in _ATTN_DT and _view_ok(qkv, hd) and (H * qkv.element_size()) % 16 == 0
+            and (mask_bias is None or not mask_bias.requires_grad)
+            and mfma_attention_supported(S, hd, qkv.dtype)):
+        if qkv.is_cuda:
+            FALLBACKS["count"] += 1
+        return _composite_attention(qkv[..., :H], qkv[..., H:2 * H], qkv[..., 2 * H:], num_heads, mask_bias, p, None)
+    kbias, mbias, mstrides = _bias_args(mask_bias, B, num_heads, S, S)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        if qkv.is_contiguous() and mfma_attention_supported(S, hd) and \
-                (mask_bias is None or mask_bias.numel() == B * S):
-            bias = None if mask_bias is None else mask_bias.reshape(B, S).float().contiguous()
-            return _MFMAAttention.apply(qkv, bias, p, num_heads)
-        return _QKVAttention.apply(qkv, mask_bias, p, num_heads)
+        return _PackedQKVAttention.apply(qkv, kbias, mbias, mstrides, p, num_heads, hd ** -0.5)
 
 
 def attention_dropout_mask(B: int, nh: int, S: int, p: float, seed: int, offset: int,
-                           device: torch.device) -> torch.Tensor:
-    """Keep mask [B, nh, S, S] the MFMA attention kernels use for (p, seed, offset) (tests)."""
+                           device: torch.device, Lk: Optional[int] = None) -> torch.Tensor:
+    """Keep mask [B, nh, S, Lk] the MFMA attention kernels use for (p, seed, offset) (tests)."""
+    Lk = S if Lk is None else Lk
     lib = _lib.get_lib()
-    out = torch.empty(B, nh, S, S, dtype=torch.uint8, device=device)
+    out = torch.empty(B, nh, S, Lk, dtype=torch.uint8, device=device)
     with torch.cuda.device(device):
-        _lib.check(lib.det_attn_dropout_mask(torch.cuda.current_stream(device).cuda_stream, B, nh, S, p, seed, offset,
-                                             out.data_ptr()), "det_attn_dropout_mask")
+        _lib.check(lib.det_attn_dropout_mask(torch.cuda.current_stream(device).cuda_stream, B, nh, S, Lk, p, seed,
+                                             offset, out.data_ptr()), "det_attn_dropout_mask")
     return out.bool()
 
 

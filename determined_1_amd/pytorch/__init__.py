@@ -1,6 +1,9 @@
 """PyTorch Trial API (``determined.pytorch`` equivalent)."""
 from determined_1_amd.pytorch._callback import ClipGradsL2Norm, ClipGradsL2Value, PyTorchCallback
 from determined_1_amd.pytorch._data import (
+    BatchChunk,
+    ChunkedBatches,
+    ChunkPrefetcher,
     DataLoader,
     DevicePrefetcher,
     DistributedBatchSampler,
@@ -10,6 +13,7 @@ from determined_1_amd.pytorch._data import (
     _Data,
     adapt_batch_sampler,
     data_length,
+    passthrough_collate,
     to_device,
 )
 from determined_1_amd.pytorch._lr_scheduler import LRScheduler
@@ -23,6 +27,10 @@ __all__ = [
     "ClipGradsNorm",
     "DataLoader",
     "DevicePrefetcher",
+    "BatchChunk",
+    "ChunkedBatches",
+    "ChunkPrefetcher",
+    "passthrough_collate",
     "DistributedBatchSampler",
     "LRScheduler",
     "PyTorchCallback",

@@ -12,9 +12,15 @@ The skip is counted in *sharded* batches, applied after sharding (reference ``_d
 MI355X addition: ``DevicePrefetcher`` moves the next batches host->device on a side HIP stream
 (pinned memory, non_blocking copies) so the H2D transfer of batch k+1 overlaps compute of batch
 k instead of stalling the training stream (the reference copies synchronously in the loop).
+
+Batch chunks (``optimizations.hip_graph_batches``): for datasets whose ``__getitems__`` returns
+stacked rows (``collate_fn=passthrough_collate``), ``ChunkedBatches`` fetches K consecutive
+batches with ONE dataset call and ``ChunkPrefetcher`` moves them with one pinned H2D copy per
+leaf, so a small model's per-batch host cost (sampler, dataset call, pinning, copy, event) is paid
+once per K batches; the trial controller then replays K train steps as one hipGraph.
 """
 import logging
-from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Set, Type, Union
+from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Set, Tuple, Type, Union
 
 import numpy as np
 import torch
@@ -178,6 +184,95 @@ class SkipBatchSampler(tud.Sampler):
         yield from it
 
 
+def passthrough_collate(batch: Any) -> Any:
+    """Collate for datasets whose ``__getitems__`` already returns a stacked batch.  Contract (what
+    makes batch chunking valid): ``__getitems__(idx)`` returns rows that depend only on their own
+    index, stacked along dim 0 of every leaf."""
+    return batch
+
+
+def stacked_rows_loader(loader: Any) -> bool:
+    """Whether a built torch DataLoader can be fetched K batches per dataset call."""
+    return (getattr(loader, "num_workers", 1) == 0 and getattr(loader, "collate_fn", None) is passthrough_collate
+            and hasattr(loader.dataset, "__getitems__") and getattr(loader, "batch_sampler", None) is not None)
+
+
+def _split_rows(data: Any, sizes: Sequence[int]) -> List[Any]:
+    """Per-batch dim-0 views of a stacked batch."""
+    if isinstance(data, np.ndarray):
+        data = torch.from_numpy(data)
+    if isinstance(data, torch.Tensor):
+        return list(torch.split(data, list(sizes)))
+    if isinstance(data, dict):
+        parts = {k: _split_rows(v, sizes) for k, v in data.items()}
+        return [{k: parts[k][i] for k in data} for i in range(len(sizes))]
+    if isinstance(data, (list, tuple)):
+        parts = [_split_rows(v, sizes) for v in data]
+        return [type(data)(p[i] for p in parts) for i in range(len(sizes))]
+    return [data] * len(sizes)
+
+
+class BatchChunk:
+    """K consecutive batches: ``stacked`` (every leaf holds the K batches' rows back to back),
+    ``sizes`` (rows per batch) and ``batches`` (per-batch views, built on first use)."""
+
+    def __init__(self, stacked: Any, sizes: Sequence[int]) -> None:
+        self.stacked = stacked
+        self.sizes = tuple(sizes)
+        self._batches = None  # type: Optional[List[Any]]
+
+    def __len__(self) -> int:
+        return len(self.sizes)
+
+    @property
+    def batches(self) -> List[Any]:
+        if self._batches is None:
+            self._batches = _split_rows(self.stacked, self.sizes)
+        return self._batches
+
+    def split(self, r: int) -> Tuple["BatchChunk", "BatchChunk"]:
+        """(first r batches, the rest) as chunks over row views of the same storage."""
+        rows = sum(self.sizes[:r])
+        total = sum(self.sizes)
+        head, tail = _split_rows(self.stacked, [rows, total - rows])
+        return BatchChunk(head, self.sizes[:r]), BatchChunk(tail, self.sizes[r:])
+
+
+class ChunkedBatches:
+    """Iterator of ``BatchChunk``: up to ``k`` batches of ``loader.batch_sampler`` per ONE
+    ``dataset.__getitems__`` call.  Chunks never cross an epoch boundary (``epoch_len`` batches
+    from batch index ``start``), so every batch of a chunk shares its epoch index."""
+
+    def __init__(self, loader: Any, k: int, epoch_len: Optional[int] = None, start: int = 0) -> None:
+        self.dataset = loader.dataset
+        self._it = iter(loader.batch_sampler)
+        self.k = max(1, int(k))
+        self.epoch_len = epoch_len
+        self.next_idx = start
+
+    def __iter__(self) -> "ChunkedBatches":
+        return self
+
+    def __next__(self) -> BatchChunk:
+        n = self.k
+        if self.epoch_len:
+            n = min(n, self.epoch_len - self.next_idx % self.epoch_len)
+        idx = []  # type: List[int]
+        sizes = []  # type: List[int]
+        for _ in range(n):
+            try:
+                b = next(self._it)
+            except StopIteration:
+                break
+            b = list(b)
+            idx.extend(b)
+            sizes.append(len(b))
+        if not sizes:
+            raise StopIteration
+        self.next_idx += len(sizes)
+        return BatchChunk(self.dataset.__getitems__(idx), sizes)
+
+
 def data_length(data: _Data) -> int:
     """Batch size of a (possibly nested) batch: length of the first array/tensor leaf."""
     if isinstance(data, (np.ndarray, torch.Tensor)):
@@ -285,3 +380,73 @@ class DevicePrefetcher:
             cur.wait_event(ev)
             _record_stream(dev, cur)
         return n, dev
+
+
+class ChunkPrefetcher:
+    """``DevicePrefetcher`` for ``BatchChunk`` streams: one pinned H2D copy per leaf per chunk on a
+    side stream, ``depth`` chunks ahead, from a reused ring of pinned staging buffers (no
+    per-batch ``pin_memory`` allocation).  Yields device ``BatchChunk``s ordered on the consumer's
+    current stream.  On the CPU it yields the host chunks unchanged."""
+
+    def __init__(self, chunks: Iterator[BatchChunk], device: torch.device, depth: int = 2) -> None:
+        self._it = chunks
+        self._device = device
+        self._depth = max(1, depth)
+        self._cuda = device.type == "cuda"
+        self._stream = torch.cuda.Stream(device=device) if self._cuda else None
+        self._queue = []  # type: List[Any]
+        self._ring = []  # type: List[Any]  # (leaf signature, pinned leaves, event) per slot
+        self._slot = 0
+
+    def _stage(self, leaves: List[torch.Tensor]) -> List[torch.Tensor]:
+        sig = [(tuple(t.shape), t.dtype) for t in leaves]
+        if len(self._ring) < self._depth + 1:
+            self._ring.append(None)
+        slot = self._slot
+        self._slot = (self._slot + 1) % (self._depth + 1)
+        ent = self._ring[slot]
+        if ent is not None:
+            ent[2].synchronize()  # the copy that last read this slot (normally long done)
+        if ent is None or ent[0] != sig:
+            ent = [sig, [torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in leaves], None]
+            self._ring[slot] = ent
+        for dst, src in zip(ent[1], leaves):
+            dst.copy_(src)
+        return ent
+
+    def _fetch_one(self) -> None:
+        from torch.utils import _pytree as pytree
+
+        c = next(self._it)
+        if not self._cuda:
+            self._queue.append((c, None))
+            return
+        leaves, spec = pytree.tree_flatten(c.stacked)
+        tensors = [torch.from_numpy(x) if isinstance(x, np.ndarray) else x for x in leaves]
+        is_t = [isinstance(x, torch.Tensor) for x in tensors]
+        ent = self._stage([x for x, t in zip(tensors, is_t) if t])
+        with torch.cuda.stream(self._stream):
+            it = iter(ent[1])
+            dev = [next(it).to(self._device, non_blocking=True) if t else x for x, t in zip(tensors, is_t)]
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        ent[2] = ev
+        self._queue.append((BatchChunk(pytree.tree_unflatten(dev, spec), c.sizes), ev))
+
+    def __iter__(self) -> "ChunkPrefetcher":
+        return self
+
+    def __next__(self) -> BatchChunk:
+        while len(self._queue) < self._depth:
+            try:
+                self._fetch_one()
+            except StopIteration:
+                break
+        if not self._queue:
+            raise StopIteration
+        c, ev = self._queue.pop(0)
+        if ev is not None:
+            cur = torch.cuda.current_stream(self._device)
+            cur.wait_event(ev)
+            _record_stream(c.stacked, cur)
+        return c

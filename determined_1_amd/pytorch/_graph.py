@@ -25,6 +25,14 @@ values other than the epoch index and must not synchronise (``.item()``) -- the 
 CUDA graphs.  Eligibility is checked once: one process (no data-parallel bucketer), aggregation
 frequency 1, no dynamic loss scaler, every optimizer fused with step-invariant kernel arguments.
 Anything else runs eagerly, logged once.
+
+Multi-batch graphs (``optimizations.hip_graph_batches: K``): even one replay per batch leaves the
+CIFAR trial host-bound (data fetch, input copy, replay launch, metric clones: ~0.8 ms/batch against
+~0.1 ms of GPU work, ``profiles/r2_asha_baseline_shape_seed1_hipgraph_u8_cl.json``).
+``run_chunk`` captures K consecutive ``train_batch`` calls over the K batch views of one
+``BatchChunk`` input buffer into ONE graph whose metric outputs are stacked [K] tensors, so the
+host cost -- one input copy per leaf, one replay, one clone per metric -- is paid once per K
+batches.  Chunks never cross an epoch (the epoch index is part of the key).
 """
 import logging
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -36,6 +44,8 @@ WARMUP = 2        # eager batches per key before capturing (lazy init, MIOpen fi
 MAX_GRAPHS = 2    # live graphs (the epoch's full batch + its tail batch)
 THRASH_LIMIT = 8  # captures that replayed fewer than THRASH_MIN times -> graphs off
 THRASH_MIN = 4
+CHUNK_WARMUP = 1  # per-batch chunks per multi-batch key before capturing it
+CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 
 
 def _leaf_sig(x: Any) -> Any:
@@ -75,6 +85,10 @@ class TrainStepGraph:
         self.replays = 0
         self.disabled_reason: Optional[str] = None
         self.pool = None
+        self.chunk_graphs: Dict[Any, _Graph] = {}
+        self.chunk_disabled: Optional[str] = None
+        self.chunk_replays = 0
+        self.last_chunk_metrics: Optional[List[Any]] = None
 
     # ------------------------------------------------------------------------------------------
     @staticmethod
@@ -182,10 +196,88 @@ class TrainStepGraph:
             logging.warning("hip_graph: running train_batch eagerly: %s", reason)
         self.disabled_reason = reason
         self.graphs.clear()
+        self.chunk_graphs.clear()
+
+    # ---- multi-batch graphs ------------------------------------------------------------------
+    def run_chunk(self, chunk: Any, epoch_idx: int, batch_idx: int) -> Optional[Dict[str, torch.Tensor]]:
+        """K train steps over ``chunk`` (a device ``BatchChunk``) as one replay; returns stacked [K]
+        metrics, or None when the chunk ran batch by batch (warm-up / ineligible) -- then the
+        per-batch metrics are in ``self.last_chunk_metrics``."""
+        self.last_chunk_metrics = None
+        if self.disabled_reason is None and self.chunk_disabled is None:
+            leaves, spec = pytree.tree_flatten(chunk.stacked)
+            if all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
+                key = ("chunk", chunk.sizes, self._key(leaves, epoch_idx))
+                g = self.chunk_graphs.get(key)
+                if g is not None:
+                    for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
+                        dst.copy_(src, non_blocking=True)
+                    g.graph.replay()
+                    for f in self.fused:
+                        for _ in chunk.sizes:
+                            f.graph_replayed()
+                    self.replays += 1
+                    self.chunk_replays += 1
+                    g.replays += 1
+                    return self._clone_out(g.out)
+                n = self.seen.get(key, 0) + 1
+                self.seen[key] = n
+                if n > CHUNK_WARMUP:
+                    g = self._capture_chunk(key, leaves, spec, chunk.sizes, epoch_idx, batch_idx)
+                    if g is not None:
+                        g.graph.replay()  # the capture advanced host state but executed nothing
+                        self.replays += 1
+                        self.chunk_replays += 1
+                        g.replays += 1
+                        return self._clone_out(g.out)
+        self.last_chunk_metrics = [self.run(b, epoch_idx, batch_idx + i) for i, b in enumerate(chunk.batches)]
+        return None
+
+    def _capture_chunk(self, key: Any, leaves: List[Any], spec: Any, sizes: Tuple[int, ...], epoch_idx: int,
+                       batch_idx: int) -> Optional[_Graph]:
+        from determined_1_amd.pytorch._data import BatchChunk
+
+        while len(self.chunk_graphs) >= CHUNK_MAX_GRAPHS:
+            del self.chunk_graphs[next(iter(self.chunk_graphs))]
+        static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
+        it = iter(static_in)
+        views = BatchChunk(pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x for x in leaves],
+                                                 spec), sizes).batches
+        host = [f.host_state() for f in self.fused]
+        graph = torch.cuda.CUDAGraph()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        try:
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph, pool=self.pool):
+                outs = []
+                for i, b in enumerate(views):
+                    o = self._eager(b, epoch_idx, batch_idx + i)
+                    o = {"loss": o} if isinstance(o, torch.Tensor) else o
+                    if not isinstance(o, dict) or not all(isinstance(v, torch.Tensor) and v.dim() == 0
+                                                          for v in o.values()):
+                        raise TypeError("train_batch metrics are not all scalar tensors")
+                    outs.append(o)
+                names = list(outs[0].keys())
+                if any(list(o.keys()) != names for o in outs):
+                    raise TypeError("train_batch metric names differ between batches")
+                out = {k: torch.stack([o[k].detach().float() for o in outs]) for k in names}
+        except Exception as e:  # noqa: BLE001 - stay on per-batch replays
+            for f, h in zip(self.fused, host):
+                f.set_host_state(h)
+            self.chunk_disabled = f"{type(e).__name__}: {e}"
+            logging.warning("hip_graph: multi-batch capture failed, replaying per batch: %s", self.chunk_disabled)
+            torch.cuda.synchronize()
+            return None
+        self.captures += 1
+        g = _Graph(graph, static_in, spec, out)
+        self.chunk_graphs[key] = g
+        return g
 
     def stats(self) -> Dict[str, Any]:
         return {"captures": self.captures, "replays": self.replays, "failed_captures": self.failed_captures,
-                "disabled": self.disabled_reason}
+                "disabled": self.disabled_reason, "chunk_replays": self.chunk_replays,
+                "chunk_disabled": self.chunk_disabled}
 
 
 class EvalStepGraph:
@@ -248,6 +340,55 @@ class EvalStepGraph:
         g.graph.replay()
         self.replays += 1
         return TrainStepGraph._clone_out(g.out)
+
+    def run_chunk(self, chunk: Any) -> Optional[Dict[str, torch.Tensor]]:
+        """``evaluate_batch`` over the K batches of a device ``BatchChunk`` as one replay -> stacked
+        [K] metrics; None when it ran per batch (metrics in ``last_chunk_metrics``)."""
+        from determined_1_amd.pytorch._data import BatchChunk
+
+        self.last_chunk_metrics = None
+        leaves, spec = pytree.tree_flatten(chunk.stacked)
+        if self.disabled_reason is None and getattr(self, "chunk_disabled", None) is None and \
+                all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
+            key = ("chunk", chunk.sizes, tuple(_leaf_sig(x) for x in leaves))
+            g = self.graphs.get(key)
+            if g is None and self.seen.get(key, 0) >= self.WARMUP:
+                while len(self.graphs) >= CHUNK_MAX_GRAPHS:
+                    del self.graphs[next(iter(self.graphs))]
+                static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
+                it = iter(static_in)
+                views = BatchChunk(pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x
+                                                          for x in leaves], spec), chunk.sizes).batches
+                graph = torch.cuda.CUDAGraph()
+                if self.pool is None:
+                    self.pool = torch.cuda.graph_pool_handle()
+                try:
+                    torch.cuda.synchronize()
+                    with torch.cuda.graph(graph, pool=self.pool):
+                        outs = [self._eager(b) for b in views]
+                        if not all(isinstance(o, dict) and all(isinstance(v, torch.Tensor) and v.dim() == 0
+                                                               for v in o.values()) for o in outs):
+                            raise TypeError("evaluate_batch metrics are not all scalar tensors")
+                        out = {k: torch.stack([o[k].detach().float() for o in outs]) for k in outs[0]}
+                except Exception as e:  # noqa: BLE001
+                    self.chunk_disabled = f"{type(e).__name__}: {e}"
+                    logging.warning("hip_graph: multi-batch evaluate capture failed: %s", self.chunk_disabled)
+                    torch.cuda.synchronize()
+                    g = None
+                else:
+                    self.captures += 1
+                    g = self.graphs[key] = _Graph(graph, static_in, spec, out)
+            else:
+                self.seen[key] = self.seen.get(key, 0) + 1
+                if g is not None:
+                    for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
+                        dst.copy_(src, non_blocking=True)
+            if g is not None:
+                g.graph.replay()
+                self.replays += 1
+                return TrainStepGraph._clone_out(g.out)
+        self.last_chunk_metrics = [self.run(b) for b in chunk.batches]
+        return None
 
 
 def build(context: Any, train_batch: Callable[..., Any], enabled: bool) -> Tuple[Optional[TrainStepGraph], Optional[str]]:

@@ -29,7 +29,8 @@ from determined_1_amd import check, errors, trial, util, workload
 from determined_1_amd.parallel import dist as pdist
 from determined_1_amd.pytorch import _callback, _graph
 from determined_1_amd.pytorch._context import PyTorchTrialContext
-from determined_1_amd.pytorch._data import DataLoader, DevicePrefetcher, TorchData, data_length
+from determined_1_amd.pytorch._data import (BatchChunk, ChunkedBatches, ChunkPrefetcher, DataLoader, DevicePrefetcher,
+                                            TorchData, data_length, stacked_rows_loader)
 from determined_1_amd.pytorch._lr_scheduler import LRScheduler
 from determined_1_amd.pytorch._reducer import Reducer, _reduce_metrics
 
@@ -187,9 +188,18 @@ class PyTorchTrialController(trial.LoopTrialController):
         elif self.is_chief:
             self.validation_loader = vds.get_data_loader(repeat=False, skip=0, num_replicas=1, rank=0)
 
-    def _make_train_iterator(self) -> Iterator[Tuple[int, Any]]:
-        it = iter(self.training_loader)
+    def _make_train_iterator(self) -> Iterator[Any]:
+        """Per-batch ``(n, device_batch)`` iterator, or -- with ``optimizations.hip_graph_batches``
+        K > 1 and a stacked-rows loader -- an iterator of device ``BatchChunk``s of up to K batches
+        (one dataset call and one H2D copy per leaf per chunk; chunks never cross an epoch)."""
         dev = self.context.device
+        self._pending = None  # type: Optional[BatchChunk]  # rest of a chunk split at a step end
+        self._chunked = self._graph_batches() > 1 and stacked_rows_loader(self.training_loader)
+        if self._chunked:
+            chunks = ChunkedBatches(self.training_loader, self._graph_batches(), epoch_len=len(self.training_loader),
+                                    start=self.env.initial_workload.total_batches_processed)
+            return ChunkPrefetcher(chunks, dev, depth=2)
+        it = iter(self.training_loader)
         if dev.type == "cuda":
             return DevicePrefetcher(it, dev, depth=2)
 
@@ -198,6 +208,18 @@ class PyTorchTrialController(trial.LoopTrialController):
                 yield data_length(b), self.context.to_device(b)
 
         return _sync()
+
+    def _graph_batches(self) -> int:
+        env = os.environ.get("DET_GRAPH_BATCHES")
+        if env:
+            return max(1, int(env))
+        opt = self.env.experiment_config.get("optimizations", {}) or {}
+        return max(1, int(opt.get("hip_graph_batches", 1) or 1))
+
+    def _chunk_graph_ok(self) -> bool:
+        """K steps in one replay apply one set of hyper-parameters: no per-batch LR schedules."""
+        return self._graph is not None and all(
+            s._step_mode == LRScheduler.StepMode.STEP_EVERY_EPOCH for s in self.context.lr_schedulers)
 
     # ------------------------------------------------------------------------------------------
     def run(self) -> None:
@@ -243,32 +265,40 @@ class PyTorchTrialController(trial.LoopTrialController):
         per_batch = []  # type: List[Dict[str, Any]]
         num_inputs = 0
         timers = self.context._timers
-        for batch_idx in range(start, end):
+        batch_idx = start
+        while batch_idx < end:
             t_data = time.perf_counter()
-            n, batch = next(self.training_iterator)
-            timers.batch_start(time.perf_counter() - t_data)
-            num_inputs += n
-            self.context._current_batch_idx = batch_idx
-            self.context._loss_ids = {}
-            if self._graph is not None:
-                tr_metrics = self._graph.run(batch, self.get_epoch_idx(batch_idx), batch_idx)
-            else:
-                with self.context._autocast():
-                    tr_metrics = self.trial.train_batch(batch=batch, epoch_idx=self.get_epoch_idx(batch_idx),
-                                                        batch_idx=batch_idx)
-                if not self._graph_checked and self.context._finalized:
-                    self._graph_checked = True
-                    self._graph, _ = _graph.build(self.context, self.trial.train_batch, self._hip_graph_enabled())
-            if isinstance(tr_metrics, torch.Tensor):
-                tr_metrics = {"loss": tr_metrics}
-            check.is_instance(tr_metrics, dict, "train_batch() must return a dictionary mapping string names to "
-                                                f"Tensor metrics, got {type(tr_metrics)}")
-            for lr_scheduler in self.context.lr_schedulers:
-                self._auto_step_lr_scheduler_per_batch(batch_idx, lr_scheduler)
-            per_batch.append({k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in tr_metrics.items()})
-            # drop the last batch's autograd graph now: a live graph keeps its AccumulateGrad
-            # nodes bound to this stream, which breaks a hipGraph capture of the next batch
-            del tr_metrics
+            if not self._chunked:
+                n, batch = next(self.training_iterator)
+                num_inputs += n
+                per_batch.append(self._train_one(batch, batch_idx, time.perf_counter() - t_data))
+                batch_idx += 1
+                continue
+            chunk = self._pending if self._pending is not None else next(self.training_iterator)
+            self._pending = None
+            if batch_idx + len(chunk) > end:  # the step ends inside this chunk: the rest opens the next step
+                chunk, self._pending = chunk.split(end - batch_idx)
+            k = len(chunk)
+            num_inputs += sum(chunk.sizes)
+            if self._chunk_graph_ok():
+                assert self._graph is not None
+                timers.batch_start(time.perf_counter() - t_data)
+                self.context._current_batch_idx = batch_idx
+                self.context._loss_ids = {}
+                stacked = self._graph.run_chunk(chunk, self.get_epoch_idx(batch_idx), batch_idx)
+                if stacked is not None:
+                    per_batch.append(_StackedMetrics(stacked, k))
+                else:
+                    per_batch.extend(_detach_metrics(m) for m in self._graph.last_chunk_metrics or [])
+                for i in range(k):
+                    for lr_scheduler in self.context.lr_schedulers:
+                        self._auto_step_lr_scheduler_per_batch(batch_idx + i, lr_scheduler)
+            else:  # no multi-batch graph (CPU, ineligible, first batch): the chunk's batches one by one
+                for i, b in enumerate(chunk.batches):
+                    per_batch.append(self._train_one(b, batch_idx + i, time.perf_counter() - t_data))
+                    t_data = time.perf_counter()
+            batch_idx += k
+        per_batch = _expand_stacked(per_batch)
         per_batch = _metrics_to_host(per_batch)
         self.last_step_timers = timers.report(step_id)
         if self.dist_config.use and self.dist_config.average_training_metrics:
@@ -280,6 +310,25 @@ class PyTorchTrialController(trial.LoopTrialController):
             return workload.Skipped()
         logging.debug(f"Done training step: {num_inputs} records in {num_batches} batches.")
         return metrics
+
+    def _train_one(self, batch: Any, batch_idx: int, data_seconds: float) -> Dict[str, Any]:
+        self.context._timers.batch_start(data_seconds)
+        self.context._current_batch_idx = batch_idx
+        self.context._loss_ids = {}
+        if self._graph is not None:
+            tr_metrics = self._graph.run(batch, self.get_epoch_idx(batch_idx), batch_idx)
+        else:
+            with self.context._autocast():
+                tr_metrics = self.trial.train_batch(batch=batch, epoch_idx=self.get_epoch_idx(batch_idx),
+                                                    batch_idx=batch_idx)
+            if not self._graph_checked and self.context._finalized:
+                self._graph_checked = True
+                self._graph, _ = _graph.build(self.context, self.trial.train_batch, self._hip_graph_enabled())
+        for lr_scheduler in self.context.lr_schedulers:
+            self._auto_step_lr_scheduler_per_batch(batch_idx, lr_scheduler)
+        # detached copies only: a live autograd graph keeps its AccumulateGrad nodes bound to this
+        # stream, which breaks a hipGraph capture of the next batch
+        return _detach_metrics(tr_metrics)
 
     def _average_training_metrics(self, per_batch_metrics: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
         gathered = pdist.gather_to_chief(per_batch_metrics)
@@ -319,14 +368,7 @@ class PyTorchTrialController(trial.LoopTrialController):
             check.gt(len(loader), 0)
             if self._eval_graph is None and self._hip_graph_enabled() and self.context.device.type == "cuda":
                 self._eval_graph = _graph.EvalStepGraph(self.context, self.trial.evaluate_batch)
-            for batch in loader:
-                num_inputs += data_length(batch)
-                batch = self.context.to_device(batch)
-                if self._eval_graph is not None:
-                    vm = self._eval_graph.run(batch)
-                else:
-                    with self.context._autocast():
-                        vm = self.trial.evaluate_batch(batch=batch)
+            for vm in self._validation_batches(loader):
                 check.is_instance(vm, dict, "evaluate_batch() must return a dictionary of string names to Tensor "
                                             "metrics")
                 if keys is None:
@@ -335,6 +377,7 @@ class PyTorchTrialController(trial.LoopTrialController):
                     check.eq(keys, vm.keys(), "Validation metric names must match across all batches of data.")
                 batch_metrics.append({k: (v.detach().float() if isinstance(v, torch.Tensor) else v)
                                       for k, v in vm.items()})
+            num_inputs += self._val_inputs
             batch_metrics = _metrics_to_host(batch_metrics)
             metrics = self._reduce_metrics(batch_metrics, keys, self._prepare_metrics_reducers(keys))
             if self.dist_config.use:
@@ -360,6 +403,35 @@ class PyTorchTrialController(trial.LoopTrialController):
         if not self.is_chief:
             return workload.Skipped()
         return {"num_inputs": num_inputs, "validation_metrics": metrics}
+
+    def _validation_batches(self, loader: Any) -> Iterator[Any]:
+        """evaluate_batch metrics per validation batch; K batches per dataset call / H2D copy /
+        hipGraph replay when ``hip_graph_batches`` > 1 and the loader yields stacked rows."""
+        self._val_inputs = 0
+        k = self._graph_batches()
+        if k > 1 and stacked_rows_loader(loader):
+            for chunk in ChunkedBatches(loader, k):
+                self._val_inputs += sum(chunk.sizes)
+                dev = BatchChunk(self.context.to_device(chunk.stacked), chunk.sizes)
+                if self._eval_graph is not None:
+                    stacked = self._eval_graph.run_chunk(dev)
+                    if stacked is not None:
+                        yield from _expand_stacked([_StackedMetrics(stacked, len(chunk))])
+                    else:
+                        yield from self._eval_graph.last_chunk_metrics or []
+                else:
+                    for b in dev.batches:
+                        with self.context._autocast():
+                            yield self.trial.evaluate_batch(batch=b)
+            return
+        for batch in loader:
+            self._val_inputs += data_length(batch)
+            batch = self.context.to_device(batch)
+            if self._eval_graph is not None:
+                yield self._eval_graph.run(batch)
+            else:
+                with self.context._autocast():
+                    yield self.trial.evaluate_batch(batch=batch)
 
     def _prepare_metrics_reducers(self, keys: Any) -> Dict[str, Reducer]:
         red = self.trial.evaluation_reducer()
@@ -482,6 +554,33 @@ class PyTorchTrialController(trial.LoopTrialController):
         for cb in self.callbacks.values():
             cb.on_checkpoint_end(str(path))
         return {"framework": f"torch-{torch.__version__}", "format": "cloudpickle"}
+
+
+class _StackedMetrics:
+    """Metrics of K batches from one multi-batch replay: {name: [K] tensor}."""
+
+    def __init__(self, stacked: Dict[str, torch.Tensor], k: int) -> None:
+        self.stacked = stacked
+        self.k = k
+
+
+def _detach_metrics(tr_metrics: Any) -> Dict[str, Any]:
+    if isinstance(tr_metrics, torch.Tensor):
+        tr_metrics = {"loss": tr_metrics}
+    check.is_instance(tr_metrics, dict, "train_batch() must return a dictionary mapping string names to "
+                                        f"Tensor metrics, got {type(tr_metrics)}")
+    return {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in tr_metrics.items()}
+
+
+def _expand_stacked(per_batch: List[Any]) -> List[Dict[str, Any]]:
+    """Per-batch metric dicts, multi-batch entries split into 0-d views (no device work)."""
+    out = []  # type: List[Dict[str, Any]]
+    for m in per_batch:
+        if isinstance(m, _StackedMetrics):
+            out.extend({k: v[i] for k, v in m.stacked.items()} for i in range(m.k))
+        else:
+            out.append(m)
+    return out
 
 
 def _metrics_to_host(batch_metrics: List[Dict[str, Any]]) -> List[Dict[str, Any]]:

@@ -42,7 +42,8 @@ class CIFARTrial(pytorch.PyTorchTrial):
                                   collate_fn=passthrough_collate)
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:
-        return pytorch.DataLoader(SyntheticImageClasses(10000, 32, seed=1),
+        n = int(self.context.get_hparams().get("validation_records", 10000))  # CIFAR-10 test split size
+        return pytorch.DataLoader(SyntheticImageClasses(n, 32, seed=1),
                                   batch_size=self.context.get_per_slot_batch_size(), collate_fn=passthrough_collate)
 
     def _images(self, x_u8: torch.Tensor) -> torch.Tensor:

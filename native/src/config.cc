@@ -26,7 +26,8 @@ Json DefaultExperimentConfig(uint32_t seed) {
                       "average_training_metrics": false, "gradient_compression": false,
                       "mixed_precision": "O0", "tensor_fusion_threshold": 64,
                       "tensor_fusion_cycle_time": 5, "auto_tune_tensor_fusion": false,
-                      "grad_reduction": "fp32_accum", "rccl": {}, "hip_graph": false},
+                      "grad_reduction": "fp32_accum", "rccl": {}, "hip_graph": false,
+                      "hip_graph_batches": 1},
     "perform_initial_validation": false,
     "min_checkpoint_period": {"batches": 0},
     "min_validation_period": {"batches": 0},
@@ -259,6 +260,8 @@ std::vector<std::string> ValidateExperimentConfig(const Json& cfg) {
   if (cp != "best" && cp != "all" && cp != "none") errs.push_back("checkpoint_policy must be one of best, all, none");
   if (cfg["resources"].get_int("slots_per_trial", 1) < 0) errs.push_back("slots_per_trial must be >= 0");
   if (cfg["optimizations"].get_int("aggregation_frequency", 1) < 1) errs.push_back("aggregation_frequency must be >= 1");
+  if (cfg["optimizations"].get_int("hip_graph_batches", 1) < 1)
+    errs.push_back("optimizations.hip_graph_batches must be >= 1");
   if (cfg.get_int("scheduling_unit", 100) <= 0) errs.push_back("scheduling_unit must be > 0");
   return errs;
 }

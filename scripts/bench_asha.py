@@ -74,6 +74,11 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=1, help="reproducibility.experiment_seed (fixes the sampled hparams)")
     ap.add_argument("--no-hip-graph", action="store_true", help="eager train_batch (A/B)")
     ap.add_argument("--artificial-slots", type=int, default=0, help="CPU dry run without GPUs")
+    ap.add_argument("--validation-records", type=int, default=0,
+                    help="shrink the validation set (scaled-down CPU runs; 0 = CIFAR-10's 10,000)")
+    ap.add_argument("--amp", default=None, help="override hyperparameters.amp (O0 = fp32, the reference precision)")
+    ap.add_argument("--graph-batches", type=int, default=0,
+                    help="override optimizations.hip_graph_batches (train steps per hipGraph replay)")
     args = ap.parse_args()
     from determined_1_amd import gpu
     from determined_1_amd.api import MasterClient, read_context
@@ -85,6 +90,12 @@ def main() -> None:
     cfg.setdefault("reproducibility", {})["experiment_seed"] = args.seed
     if args.no_hip_graph:
         cfg.setdefault("optimizations", {})["hip_graph"] = False
+    if args.graph_batches:
+        cfg.setdefault("optimizations", {})["hip_graph_batches"] = args.graph_batches
+    if args.amp:
+        cfg["hyperparameters"]["amp"] = args.amp
+    if args.validation_records:
+        cfg["hyperparameters"]["validation_records"] = args.validation_records
     if args.max_length_batches:
         cfg["searcher"]["max_length"] = {"batches": args.max_length_batches}
         # validate only where the searcher asks (end of each rung); the real config validates every
@@ -94,6 +105,8 @@ def main() -> None:
         cfg.pop("records_per_epoch", None)
     env_vars = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
     env_vars.append("DET_TIMELINE=1")
+    if args.artificial_slots:
+        env_vars.append("OMP_NUM_THREADS=1")  # N CPU trial processes share the host's cores
     busy = []
     stop = threading.Event()
 
@@ -116,9 +129,11 @@ def main() -> None:
         eid = cl.create_experiment(cfg, read_context(ex))["id"]
         state = None
         last = 0.0
+        peak_busy = 0
         while time.time() - t0 < args.timeout:  # progress line every 20 s (long runs must not look hung)
             ex = cl.experiment(eid)
             state = ex["state"]
+            peak_busy = max(peak_busy, sum(1 for a in cl.get("/agents") for sl in a["slots"] if sl.get("task")))
             if state in ("COMPLETED", "CANCELED", "ERROR"):
                 break
             if time.time() - last > 20:
@@ -144,8 +159,10 @@ def main() -> None:
                           "containers": containers, "train_records": records,
                           "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
                           "slot_occupancy": round(occupancy, 3), "scheduler_idle_frac": round(1 - occupancy, 3),
+                          "peak_busy_slots": peak_busy,
                           "zygote": not args.no_zygote, "per_container_s": timeline,
                           "hip_graph": bool((cfg.get("optimizations") or {}).get("hip_graph", False)),
+                          "hip_graph_batches": (cfg.get("optimizations") or {}).get("hip_graph_batches", 1),
                           "experiment_seed": args.seed,
                           "config": {"max_length": cfg["searcher"]["max_length"], "max_trials": args.max_trials,
                                      "records_per_epoch": cfg.get("records_per_epoch"),

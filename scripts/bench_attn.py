@@ -1,40 +1,65 @@
-"""Microbenchmark of the MFMA attention kernels (det_attention.hip) at BERT / ALBERT shapes,
-with and without probability dropout.  Prints ms per fwd and per fwd+bwd and TFLOP/s."""
+"""Microbenchmark of the MFMA attention kernels (det_attention.hip) against torch SDPA (AOTriton /
+math on ROCm) at the BERT, ALBERT, DETR and head_dim-128 shapes, with and without probability
+dropout.  Prints ms per fwd and per fwd+bwd and TFLOP/s, one JSON line per case."""
+import json
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 
 from determined_1_amd.ops import transformer as tfops  # noqa: E402
 
 
-def bench(B, S, nh, p, iters=50):
-    H = nh * 64
-    qkv = torch.randn(B, S, 3 * H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-    mb = torch.zeros(B, 1, 1, S, device="cuda", dtype=torch.bfloat16)
-    dy = torch.randn(B, S, H, device="cuda", dtype=torch.bfloat16)
+def _time(fn, iters):
     for _ in range(3):
-        tfops.qkv_self_attention(qkv, nh, mb, p, training=True).backward(dy)
+        fn()
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters
+
+
+def bench(B, S, nh, hd=64, dt=torch.bfloat16, p=0.0, iters=30, Lk=None):
+    Lk = S if Lk is None else Lk
+    H = nh * hd
+    q, k, v = (torch.randn(B, L, H, device="cuda", dtype=dt, requires_grad=True) for L in (S, Lk, Lk))
+    mb = torch.zeros(B, 1, 1, Lk, device="cuda", dtype=dt)
+    dy = torch.randn(B, S, H, device="cuda", dtype=dt)
+
+    def native(bwd):
+        o = tfops.attention(q, k, v, nh, attn_bias=mb, p=p, training=True)
+        if bwd:
+            o.backward(dy)
+
+    def heads(t):
+        return t.view(B, t.shape[1], nh, hd).transpose(1, 2)
+
+    def sdpa(bwd):
+        o = F.scaled_dot_product_attention(heads(q), heads(k), heads(v), attn_mask=mb, dropout_p=p)
+        if bwd:
+            o.transpose(1, 2).reshape(B, S, H).backward(dy)
+
+    flop = 4 * B * nh * S * Lk * hd
+    res = {"B": B, "Lq": S, "Lk": Lk, "nh": nh, "hd": hd, "dtype": str(dt).split(".")[-1], "p": p}
+    for name, fn in (("native", native), ("sdpa", sdpa)):
         with torch.no_grad():
-            tfops.qkv_self_attention(qkv, nh, mb, p, training=True)
-    torch.cuda.synchronize()
-    tf = (time.perf_counter() - t) / iters
-    t = time.perf_counter()
-    for _ in range(iters):
-        tfops.qkv_self_attention(qkv, nh, mb, p, training=True).backward(dy)
-    torch.cuda.synchronize()
-    tfb = (time.perf_counter() - t) / iters
-    flop = 4 * B * nh * S * S * 64
-    print(f"B{B} S{S} nh{nh} p={p}: fwd {tf * 1e3:.3f} ms ({flop / tf / 1e12:.0f} TF/s)  "
-          f"fwd+bwd {tfb * 1e3:.3f} ms ({3.5 * flop / tfb / 1e12:.0f} TF/s)", flush=True)
+            tf = _time(lambda: fn(False), iters)
+        tfb = _time(lambda: fn(True), iters)
+        res[name] = {"fwd_ms": round(tf * 1e3, 4), "fwd_tflops": round(flop / tf / 1e12, 1),
+                     "fwd_bwd_ms": round(tfb * 1e3, 4), "fwd_bwd_tflops": round(3.5 * flop / tfb / 1e12, 1)}
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":
     for p in (0.0, 0.1):
-        bench(12, 384, 12, p)
-    bench(8, 384, 64, 0.0)
+        bench(12, 384, 12, p=p)  # BERT-base SQuAD
+    bench(8, 384, 64, p=0.0)  # ALBERT-xxlarge
+    bench(8, 384, 64, dt=torch.float32)  # ALBERT-xxlarge fp32 (reference const.yaml precision)
+    bench(2, 850, 8, hd=32, dt=torch.float32)  # DETR encoder fp32
+    bench(2, 100, 8, hd=32, dt=torch.float32, Lk=850)  # DETR cross-attention fp32
+    bench(4, 1024, 16, hd=128)  # head_dim 128

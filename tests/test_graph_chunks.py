@@ -1,0 +1,119 @@
+"""Multi-batch chunks (optimizations.hip_graph_batches, pytorch/_data.py ChunkedBatches /
+ChunkPrefetcher, pytorch/_graph.py run_chunk): a chunked run must see exactly the batches of the
+unchunked run, in order, never mixing epochs, through steps that end inside a chunk, a restore
+offset and validation -- on the CPU (eager) here, and as multi-batch hipGraph replays on the GPU."""
+import pytest
+import torch
+import torch.nn as nn
+
+from determined_1_amd import pytorch
+from determined_1_amd.pytorch._data import ChunkedBatches
+from tests.utils import Recorder, run
+
+
+class StackedRows(torch.utils.data.Dataset):
+    """Rows depend only on their index; ``__getitems__`` returns them stacked."""
+
+    def __init__(self, n: int, seed: int = 1) -> None:
+        g = torch.Generator().manual_seed(seed)
+        self.x = torch.randn(n, 3, 16, 16, generator=g)
+        self.y = torch.randint(0, 10, (n,), generator=g)
+        self.calls = 0
+
+    def __len__(self) -> int:
+        return len(self.y)
+
+    def __getitems__(self, idx):
+        self.calls += 1
+        i = torch.as_tensor(list(idx))
+        return self.x[i], self.y[i]
+
+
+class StackedTrial(pytorch.PyTorchTrial):
+    def __init__(self, context):
+        self.context = context
+        torch.manual_seed(0)
+        net = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.ReLU(), nn.AdaptiveAvgPool2d(1), nn.Flatten(),
+                            nn.Linear(8, 10))
+        self.model = context.wrap_model(net)
+        self.opt = context.wrap_optimizer(torch.optim.RMSprop(self.model.parameters(), lr=1e-3))
+        self.seen = []
+
+    def build_training_data_loader(self):
+        self.train_ds = StackedRows(160)
+        return pytorch.DataLoader(self.train_ds, batch_size=self.context.get_per_slot_batch_size(),
+                                  collate_fn=pytorch.passthrough_collate)
+
+    def build_validation_data_loader(self):
+        return pytorch.DataLoader(StackedRows(72, seed=2), batch_size=self.context.get_per_slot_batch_size(),
+                                  collate_fn=pytorch.passthrough_collate)
+
+    def train_batch(self, batch, epoch_idx, batch_idx):
+        x, y = batch
+        if not x.is_cuda:  # (a host read would break a hipGraph capture)
+            self.seen.append((epoch_idx, batch_idx, float(x[0, 0, 0, 0])))
+        loss = nn.functional.cross_entropy(self.model(x).float(), y)
+        self.context.backward(loss)
+        self.context.step_optimizer(self.opt)
+        return {"loss": loss}
+
+    def evaluate_batch(self, batch):
+        x, y = batch
+        return {"validation_loss": nn.functional.cross_entropy(self.model(x).float(), y)}
+
+
+def test_chunked_batches_respect_epochs_and_offsets():
+    dl = pytorch.DataLoader(StackedRows(100), batch_size=10, collate_fn=pytorch.passthrough_collate)
+    loader = dl.get_data_loader(repeat=True, skip=3)
+    ds = loader.dataset
+    it = ChunkedBatches(loader, 4, epoch_len=len(loader), start=3)
+    sizes = [len(next(it)) for _ in range(5)]
+    assert sizes == [4, 3, 4, 4, 2]  # batches 3-6, 7-9 | 10-13, 14-17, 18-19
+    assert ds.calls == 5
+    ref = iter(dl.get_data_loader(repeat=True, skip=3))
+    it = ChunkedBatches(dl.get_data_loader(repeat=True, skip=3), 4, epoch_len=10, start=3)
+    for _ in range(4):
+        for b in next(it).batches:
+            x, y = next(ref)
+            assert torch.equal(b[0], x) and torch.equal(b[1], y)
+
+
+def _run(monkeypatch, k, use_gpu=False, graph=False):
+    monkeypatch.setenv("DET_GRAPH_BATCHES", str(k))
+    monkeypatch.setenv("DET_HIP_GRAPH", "1" if graph else "0")
+    rec = Recorder().train(1, 13, 0).validate(1, 13).train(2, 9, 13).train(3, 11, 22).validate(3, 33)
+    ctrl, resp = run(StackedTrial, {"global_batch_size": 16}, rec, use_gpu=use_gpu, records_per_epoch=160)
+    if use_gpu:
+        torch.cuda.synchronize()
+    params = torch.cat([p.detach().float().reshape(-1) for p in ctrl.context.models[0].parameters()]).cpu()
+    losses = [float(b["loss"]) for r in resp if "batch_metrics" in r.get("metrics", {})
+              for b in r["metrics"]["batch_metrics"]]
+    vals = [r["metrics"]["validation_metrics"]["validation_loss"] for r in resp
+            if "validation_metrics" in r.get("metrics", {})]
+    return ctrl, params, losses, vals
+
+
+def test_chunked_training_matches_unchunked_on_cpu(monkeypatch):
+    c1, p1, l1, v1 = _run(monkeypatch, 1)
+    c4, p4, l4, v4 = _run(monkeypatch, 4)
+    assert c4._chunked and not c1._chunked
+    assert len(l1) == len(l4) == 33 and len(v1) == len(v4) == 2
+    assert [s[:2] for s in c1.trial.seen] == [s[:2] for s in c4.trial.seen]
+    assert [s[2] for s in c1.trial.seen] == [s[2] for s in c4.trial.seen]
+    torch.testing.assert_close(p4, p1, rtol=0, atol=0)
+    assert l1 == l4
+    assert v1 == pytest.approx(v4, rel=1e-6)
+    # one dataset call per chunk (chunks of <= 4 batches, split at epoch ends 10/20/30)
+    assert c4.trial.train_ds.calls <= 12
+
+
+@pytest.mark.gpu
+def test_multibatch_graph_replay_matches_eager(gpu, monkeypatch):
+    _, p_e, l_e, v_e = _run(monkeypatch, 1, use_gpu=True, graph=False)
+    c, p_g, l_g, v_g = _run(monkeypatch, 4, use_gpu=True, graph=True)
+    assert c._graph is not None and c._graph.chunk_replays > 0, c._graph.stats() if c._graph else None
+    assert c._eval_graph is not None and c._eval_graph.replays > 0
+    assert len(l_g) == len(l_e)
+    torch.testing.assert_close(torch.tensor(l_g), torch.tensor(l_e), rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(p_g, p_e, rtol=2e-3, atol=2e-3)
+    assert v_g == pytest.approx(v_e, rel=2e-3)

@@ -139,6 +139,7 @@ def test_bert_layer_fused_matches_composite(gpu, monkeypatch):
     loss_f, g_f = run()
     assert tfops.FALLBACKS["count"] == before
     monkeypatch.setattr(tfops, "_native", lambda *a, **k: False)
+    monkeypatch.setenv("DET_ATTN", "composite")
     loss_c, g_c = run()
     torch.testing.assert_close(loss_f, loss_c, atol=1e-5, rtol=1e-5)
     for k in g_c:
@@ -170,69 +171,11 @@ def test_albert_fused_matches_composite(gpu, monkeypatch):
     loss_f, g_f = run()
     assert tfops.FALLBACKS["count"] == before
     monkeypatch.setattr(tfops, "_native", lambda *a, **k: False)
+    monkeypatch.setenv("DET_ATTN", "composite")
     loss_c, g_c = run()
     torch.testing.assert_close(loss_f, loss_c, atol=1e-5, rtol=1e-5)
     for k in g_c:
         torch.testing.assert_close(g_f[k], g_c[k], atol=1e-4, rtol=1e-3, msg=k)
-
-
-@pytest.mark.parametrize("B,S,nh,hd,masked", [(4, 384, 12, 64, True), (2, 128, 4, 64, False)])
-def test_qkv_self_attention(gpu, B, S, nh, hd, masked):
-    """Fused-QKV attention (AOTriton fwd/bwd + det_tf_pack_qkv) vs fp32 SDPA on CPU, dropout off."""
-    torch.manual_seed(5)
-    H = nh * hd
-    qkv = torch.randn(B, S, 3 * H).to(torch.bfloat16).float()
-    am = torch.ones(B, S)
-    if masked:
-        am[0, -37:] = 0
-    bias = ((1.0 - am[:, None, None, :]) * -1e9) if masked else None
-    dy = torch.randn(B, S, H).to(torch.bfloat16).float()
-    ref_in = qkv.clone().requires_grad_(True)
-    q, k, v = ref_in.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)
-    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=bias).transpose(1, 2).reshape(B, S, H)
-    ref.backward(dy)
-    dut_in = qkv.to(gpu, torch.bfloat16).requires_grad_(True)
-    before = tfops.FALLBACKS["count"]
-    out = tfops.qkv_self_attention(dut_in, nh, None if bias is None else bias.to(gpu, torch.bfloat16), 0.0)
-    out.backward(dy.to(gpu, torch.bfloat16))
-    assert tfops.FALLBACKS["count"] == before
-    torch.testing.assert_close(out.float().cpu(), ref.detach(), atol=3e-2, rtol=3e-2)
-    torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, atol=5e-2, rtol=5e-2)
-
-
-@pytest.mark.parametrize("B,S,nh,p", [(2, 384, 4, 0.0), (3, 256, 2, 0.1), (1, 512, 2, 0.2), (2, 128, 3, 0.1),
-                                      (2, 192, 2, 0.1), (1, 1024, 2, 0.0), (2, 64, 2, 0.0)])
-def test_mfma_attention_with_dropout(gpu, monkeypatch, B, S, nh, p):
-    """det_attention.hip fwd+bwd vs an fp32 composite using the kernels' own dropout mask."""
-    hd = 64
-    H = nh * hd
-    assert tfops.mfma_attention_supported(S, hd)
-    torch.manual_seed(6)
-    qkv = (torch.randn(B, S, 3 * H) * 1.5).to(torch.bfloat16).float()
-    am = torch.ones(B, S)
-    am[-1, S - 19:] = 0
-    bias = (1.0 - am) * -10000.0
-    dy = torch.randn(B, S, H).to(torch.bfloat16).float()
-    seed, off = 4242, 9
-    monkeypatch.setattr(tfops, "next_rng", lambda: (seed, off))
-    ref_in = qkv.clone().requires_grad_(True)
-    q, k, v = ref_in.view(B, S, 3, nh, hd).permute(2, 0, 3, 1, 4).unbind(0)
-    probs = torch.softmax(q @ k.transpose(-1, -2) / 8.0 + bias[:, None, None, :], dim=-1)
-    if p > 0:
-        keep = tfops.attention_dropout_mask(B, nh, S, p, seed, off, torch.device(gpu)).cpu()
-        thr = min(65535, int(p * 65536 + 0.5))
-        assert abs(keep.float().mean().item() - (1 - thr / 65536)) < 5e-3
-        probs = probs * keep.float() * (65536.0 / (65536 - thr))
-    ref = (probs @ v).transpose(1, 2).reshape(B, S, H)
-    ref.backward(dy)
-    dut_in = qkv.to(gpu, torch.bfloat16).requires_grad_(True)
-    mb = bias.to(gpu, torch.bfloat16)[:, None, None, :]
-    out = tfops.qkv_self_attention(dut_in, nh, mb, p, training=True)
-    out.backward(dy.to(gpu, torch.bfloat16))
-    torch.testing.assert_close(out.float().cpu(), ref.detach(), atol=3e-2, rtol=3e-2)
-    g, gr = dut_in.grad.float().cpu(), ref_in.grad
-    scale = gr.abs().max().item()
-    torch.testing.assert_close(g / scale, gr / scale, atol=2e-2, rtol=2e-2)
 
 
 def test_bert_trial_direct_gradient_landing(gpu, monkeypatch):
