@@ -61,6 +61,7 @@ def _warm_gpu() -> None:
 
 def main() -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s [harness] %(levelname)s %(message)s")
+    faulthandler.enable()  # a crashing trial process leaves its Python stack in the trial log
     if os.environ.get("DET_ZYGOTE_PID"):
         logging.info("trial process forked from warm zygote %s", os.environ["DET_ZYGOTE_PID"])
     timeline.mark("imports done")

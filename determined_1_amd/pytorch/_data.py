@@ -241,13 +241,18 @@ class BatchChunk:
 class ChunkedBatches:
     """Iterator of ``BatchChunk``: up to ``k`` batches of ``loader.batch_sampler`` per ONE
     ``dataset.__getitems__`` call.  Chunks never cross an epoch boundary (``epoch_len`` batches
-    from batch index ``start``), so every batch of a chunk shares its epoch index."""
+    from batch index 0; the iterator starts at batch ``start``), so every batch of a chunk shares
+    its epoch index, nor a multiple of ``unit`` batches after ``start`` (the scheduling unit: the
+    training steps a container runs), so a step ends on a chunk boundary."""
 
-    def __init__(self, loader: Any, k: int, epoch_len: Optional[int] = None, start: int = 0) -> None:
+    def __init__(self, loader: Any, k: int, epoch_len: Optional[int] = None, start: int = 0,
+                 unit: Optional[int] = None) -> None:
         self.dataset = loader.dataset
         self._it = iter(loader.batch_sampler)
         self.k = max(1, int(k))
         self.epoch_len = epoch_len
+        self.unit = unit
+        self.start = start
         self.next_idx = start
 
     def __iter__(self) -> "ChunkedBatches":
@@ -257,6 +262,8 @@ class ChunkedBatches:
         n = self.k
         if self.epoch_len:
             n = min(n, self.epoch_len - self.next_idx % self.epoch_len)
+        if self.unit:
+            n = min(n, self.unit - (self.next_idx - self.start) % self.unit)
         idx = []  # type: List[int]
         sizes = []  # type: List[int]
         for _ in range(n):

@@ -48,6 +48,25 @@ CHUNK_WARMUP = 1  # per-batch chunks per multi-batch key before capturing it
 CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 
 
+def reads_argument(fn: Callable[..., Any], name: str) -> bool:
+    """Whether ``fn``'s body can observe its argument ``name`` (conservatively True when the code is
+    not inspectable or it uses locals()/frames).  A ``train_batch`` that never reads ``epoch_idx``
+    lets one graph serve every epoch instead of re-capturing at each epoch boundary."""
+    import dis
+    import inspect
+
+    fn = inspect.unwrap(getattr(fn, "__func__", fn))
+    code = getattr(fn, "__code__", None)
+    if code is None or name not in code.co_varnames[:code.co_argcount + code.co_kwonlyargcount]:
+        return True
+    if "locals" in code.co_names or "vars" in code.co_names or "_getframe" in code.co_names:
+        return True
+    if name in code.co_cellvars:  # captured by a nested function
+        return True
+    return any(ins.argval == name for ins in dis.get_instructions(code)
+               if ins.opname in ("LOAD_FAST", "LOAD_DEREF", "LOAD_CLOSURE", "DELETE_FAST", "STORE_FAST"))
+
+
 def _leaf_sig(x: Any) -> Any:
     if isinstance(x, torch.Tensor):
         return ("T", tuple(x.shape), x.dtype, x.device.type)
@@ -68,9 +87,13 @@ class TrainStepGraph:
     """Per-controller graph cache.  ``run(batch, epoch_idx, batch_idx)`` returns the train_batch
     metrics, eagerly or from a replay."""
 
-    def __init__(self, context: Any, train_batch: Callable[..., Any]) -> None:
+    def __init__(self, context: Any, train_batch: Callable[..., Any],
+                 epoch_sensitive: Optional[bool] = None) -> None:
         self.context = context
         self.train_batch = train_batch
+        # the epoch index is part of the key only when train_batch can read it
+        self.epoch_sensitive = reads_argument(train_batch, "epoch_idx") if epoch_sensitive is None \
+            else epoch_sensitive
         self.fused = [st.fused for st in context._opt_states if st.fused is not None]
         for f in self.fused:
             # in a graph the per-parameter accumulate launches cost nothing on the host, and the
@@ -113,7 +136,8 @@ class TrainStepGraph:
         return None
 
     def _key(self, leaves: List[Any], epoch_idx: int) -> Any:
-        return (tuple(_leaf_sig(x) for x in leaves), epoch_idx, tuple(f.graph_signature() for f in self.fused))
+        return (tuple(_leaf_sig(x) for x in leaves), epoch_idx if self.epoch_sensitive else None,
+                tuple(f.graph_signature() for f in self.fused))
 
     def _eager(self, batch: Any, epoch_idx: int, batch_idx: int) -> Any:
         with self.context._autocast():
@@ -164,9 +188,10 @@ class TrainStepGraph:
         if self.captures - len(self.graphs) >= THRASH_LIMIT and len(stale) == len(self.graphs):
             self._disable("graph key changes every few batches (per-batch hyper-parameter schedule?)")
             return None
-        while len(self.graphs) >= MAX_GRAPHS:
-            oldest = next(iter(self.graphs))
-            del self.graphs[oldest]
+        if len(self.graphs) >= MAX_GRAPHS:
+            torch.cuda.synchronize()  # never destroy a graph exec that may still be running
+            while len(self.graphs) >= MAX_GRAPHS:
+                del self.graphs[next(iter(self.graphs))]
         static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
         it = iter(static_in)
         static_leaves = [next(it) if isinstance(x, torch.Tensor) else x for x in leaves]
@@ -199,12 +224,14 @@ class TrainStepGraph:
         self.chunk_graphs.clear()
 
     # ---- multi-batch graphs ------------------------------------------------------------------
-    def run_chunk(self, chunk: Any, epoch_idx: int, batch_idx: int) -> Optional[Dict[str, torch.Tensor]]:
+    def run_chunk(self, chunk: Any, epoch_idx: int, batch_idx: int,
+                  capture: bool = True) -> Optional[Dict[str, torch.Tensor]]:
         """K train steps over ``chunk`` (a device ``BatchChunk``) as one replay; returns stacked [K]
-        metrics, or None when the chunk ran batch by batch (warm-up / ineligible) -- then the
-        per-batch metrics are in ``self.last_chunk_metrics``."""
+        metrics, or None when the chunk ran batch by batch (warm-up / ineligible / ``capture``
+        False: partial chunks at epoch ends replay per batch rather than growing one multi-batch
+        graph per odd size) -- then the per-batch metrics are in ``self.last_chunk_metrics``."""
         self.last_chunk_metrics = None
-        if self.disabled_reason is None and self.chunk_disabled is None:
+        if capture and self.disabled_reason is None and self.chunk_disabled is None:
             leaves, spec = pytree.tree_flatten(chunk.stacked)
             if all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
                 key = ("chunk", chunk.sizes, self._key(leaves, epoch_idx))
@@ -230,15 +257,23 @@ class TrainStepGraph:
                         self.chunk_replays += 1
                         g.replays += 1
                         return self._clone_out(g.out)
-        self.last_chunk_metrics = [self.run(b, epoch_idx, batch_idx + i) for i, b in enumerate(chunk.batches)]
+        outs = []
+        for i, b in enumerate(chunk.batches):
+            # detached: an eager batch's metrics hold its autograd graph, whose AccumulateGrad nodes
+            # (bound to this stream) would break the next capture
+            outs.append(pytree.tree_map(lambda t: t.detach() if isinstance(t, torch.Tensor) else t,
+                                        self.run(b, epoch_idx, batch_idx + i)))
+        self.last_chunk_metrics = outs
         return None
 
     def _capture_chunk(self, key: Any, leaves: List[Any], spec: Any, sizes: Tuple[int, ...], epoch_idx: int,
                        batch_idx: int) -> Optional[_Graph]:
         from determined_1_amd.pytorch._data import BatchChunk
 
-        while len(self.chunk_graphs) >= CHUNK_MAX_GRAPHS:
-            del self.chunk_graphs[next(iter(self.chunk_graphs))]
+        if len(self.chunk_graphs) >= CHUNK_MAX_GRAPHS:
+            torch.cuda.synchronize()  # never destroy a graph exec that may still be running
+            while len(self.chunk_graphs) >= CHUNK_MAX_GRAPHS:
+                del self.chunk_graphs[next(iter(self.chunk_graphs))]
         static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
         it = iter(static_in)
         views = BatchChunk(pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x for x in leaves],
@@ -315,8 +350,10 @@ class EvalStepGraph:
             self.seen[key] = n
             if n <= self.WARMUP:
                 return self._eager(batch)
-            while len(self.graphs) >= MAX_GRAPHS:
-                del self.graphs[next(iter(self.graphs))]
+            if len(self.graphs) >= MAX_GRAPHS:
+                torch.cuda.synchronize()
+                while len(self.graphs) >= MAX_GRAPHS:
+                    del self.graphs[next(iter(self.graphs))]
             static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
             it = iter(static_in)
             static_batch = pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x for x in leaves], spec)
@@ -353,8 +390,10 @@ class EvalStepGraph:
             key = ("chunk", chunk.sizes, tuple(_leaf_sig(x) for x in leaves))
             g = self.graphs.get(key)
             if g is None and self.seen.get(key, 0) >= self.WARMUP:
-                while len(self.graphs) >= CHUNK_MAX_GRAPHS:
-                    del self.graphs[next(iter(self.graphs))]
+                if len(self.graphs) >= CHUNK_MAX_GRAPHS:
+                    torch.cuda.synchronize()
+                    while len(self.graphs) >= CHUNK_MAX_GRAPHS:
+                        del self.graphs[next(iter(self.graphs))]
                 static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
                 it = iter(static_in)
                 views = BatchChunk(pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x
@@ -391,11 +430,12 @@ class EvalStepGraph:
         return None
 
 
-def build(context: Any, train_batch: Callable[..., Any], enabled: bool) -> Tuple[Optional[TrainStepGraph], Optional[str]]:
+def build(context: Any, train_batch: Callable[..., Any], enabled: bool,
+          epoch_sensitive: Optional[bool] = None) -> Tuple[Optional[TrainStepGraph], Optional[str]]:
     if not enabled:
         return None, None
     reason = TrainStepGraph.ineligible_reason(context)
     if reason is not None:
         logging.warning("optimizations.hip_graph is set but train_batch will run eagerly: %s", reason)
         return None, reason
-    return TrainStepGraph(context, train_batch), None
+    return TrainStepGraph(context, train_batch, epoch_sensitive), None

@@ -196,8 +196,9 @@ class PyTorchTrialController(trial.LoopTrialController):
         self._pending = None  # type: Optional[BatchChunk]  # rest of a chunk split at a step end
         self._chunked = self._graph_batches() > 1 and stacked_rows_loader(self.training_loader)
         if self._chunked:
+            unit = int(self.env.experiment_config.get("scheduling_unit", 100) or 100)
             chunks = ChunkedBatches(self.training_loader, self._graph_batches(), epoch_len=len(self.training_loader),
-                                    start=self.env.initial_workload.total_batches_processed)
+                                    start=self.env.initial_workload.total_batches_processed, unit=unit)
             return ChunkPrefetcher(chunks, dev, depth=2)
         it = iter(self.training_loader)
         if dev.type == "cuda":
@@ -285,7 +286,8 @@ class PyTorchTrialController(trial.LoopTrialController):
                 timers.batch_start(time.perf_counter() - t_data)
                 self.context._current_batch_idx = batch_idx
                 self.context._loss_ids = {}
-                stacked = self._graph.run_chunk(chunk, self.get_epoch_idx(batch_idx), batch_idx)
+                stacked = self._graph.run_chunk(chunk, self.get_epoch_idx(batch_idx), batch_idx,
+                                                capture=k == self._graph_batches())
                 if stacked is not None:
                     per_batch.append(_StackedMetrics(stacked, k))
                 else:

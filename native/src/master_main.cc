@@ -126,6 +126,7 @@ int main(int argc, char** argv) {
       cfgj["resource_manager"]["master_service_host"] = next();
     } else if (a == "--telemetry-file") {
       cfgj["telemetry"]["file"] = next();
+      cfgj["telemetry"]["enabled"] = true;
     } else if (a == "--require-auth") {
       cfgj["security"]["authentication"] = true;
     } else if (a == "--scheduler-tick-ms") {

@@ -105,6 +105,7 @@ def main() -> None:
         cfg.pop("records_per_epoch", None)
     env_vars = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
     env_vars.append("DET_TIMELINE=1")
+    env_vars.append("PYTHONFAULTHANDLER=1")  # a crashing trial logs its Python stack
     if args.artificial_slots:
         env_vars.append("OMP_NUM_THREADS=1")  # N CPU trial processes share the host's cores
     busy = []
@@ -148,6 +149,13 @@ def main() -> None:
         e = cl.experiment(eid)
         done = sum(1 for t in e["trials"] if t["state"] == "COMPLETED")
         timeline = summarize_timelines(cl, e["trials"], t0)
+        restarted = [t for t in e["trials"] if t.get("restarts", 0) or t["state"] != "COMPLETED"]
+        if restarted:  # keep the tail of every failing trial's log next to the timeline
+            with open(os.path.join(os.environ.get("DET_BENCH_LOGDIR", "/tmp"), "asha_failed_trials.txt"), "w") as f:
+                for t in restarted:
+                    recs = cl.get(f"/trials/{t['id']}/logs")
+                    f.write(f"==== trial {t['id']} state={t['state']} restarts={t.get('restarts')}\n")
+                    f.write("\n".join(r.get("message", "").rstrip() for r in recs[-150:]) + "\n")
         slots = sum(len(a["slots"]) for a in cl.get("/agents"))
         containers = timeline.pop("_containers", 0)
         occupancy = timeline.get("total", 0.0) * containers / max(1e-9, wall * slots)

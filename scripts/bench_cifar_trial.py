@@ -23,6 +23,7 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=500)
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
+    ap.add_argument("--graph-batches", type=int, default=1, help="optimizations.hip_graph_batches")
     args = ap.parse_args()
     t0 = time.time()
     import torch
@@ -37,7 +38,7 @@ def main() -> None:
                                "amp": args.amp},
            "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": args.batches}},
            "records_per_epoch": 50000, "scheduling_unit": args.chunk,
-           "optimizations": {"hip_graph": bool(args.hip_graph)}}
+           "optimizations": {"hip_graph": bool(args.hip_graph), "hip_graph_batches": args.graph_batches}}
     marks = []
     res = {}
 
