@@ -108,6 +108,11 @@ def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, out: torch.Tensor, scal
         res = (dy2d.float().t() @ xg.float()) * out_scale
         out.copy_(res.view_as(out))
         return out
+    if WGRAD_RING and scale is None and gather is None and ring_wgrad_1x1(n, k) and \
+            int(_lib.get_lib().det_igemm_wgrad_ws_elems(m, n, k, 0)) > 0:
+        # a stride-1 1x1 conv is the R = S = 1 case of the ring wgrad over one [1, M] "image"
+        return conv_wgrad(dy2d.view(1, 1, m, n).permute(0, 3, 1, 2), x2d.view(1, 1, m, k).permute(0, 3, 1, 2),
+                          out.view(n, k), 1, 1, 1, 0, out_scale=out_scale)
     ws = torch.empty(int(_lib.get_lib().det_conv_tn_ws_elems(m, n, k)), dtype=torch.float32, device=dy2d.device)
     g = gather or (0, 0, 0, 0)
     code = 1 if out.dtype == torch.bfloat16 else 0
@@ -197,10 +202,26 @@ def dgrad_weight(w: torch.Tensor) -> torch.Tensor:
     return w.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).to(torch.bfloat16).contiguous()
 
 
+WGRAD_RING = True  # det_igemm_wgrad (LDS-DMA ring, transposed reads) vs det_conv's register-staged gemm_tn
+WGRAD_COUNTS = {"ring": 0, "slab": 0}
+# 1x1 weight-gradient shapes (Cout, Cin) where the ring clearly beats gemm_tn at ResNet-50 / batch 512
+# (0.105 vs 0.198 ms at 64x64 / 56x56, 0.088 vs 0.20 ms at 2048x512 / 7x7,
+# profiles/r3_wgrad_ring_sweep.jsonl); the others stay on gemm_tn (within +-5 %, and the in-step A/B
+# of routing them all to the ring lost 1.4 ms, profiles/r3_resnet50_ring_wgrad_all_steady.csv).
+_RING_WGRAD_1X1 = {(64, 64), (2048, 512), (512, 2048)}
+RING_WGRAD_1X1_ALL = False
+
+
+def ring_wgrad_1x1(cout: int, cin: int) -> bool:
+    return WGRAD_RING and (RING_WGRAD_1X1_ALL or (cout, cin) in _RING_WGRAD_1X1)
+
+
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, r: int, s: int, stride: int, pad: int,
-               out_scale: float = 1.0) -> torch.Tensor:
+               out_scale: float = 1.0, cfg: int = 0) -> torch.Tensor:
     """Weight gradient of a conv: ``out`` (contiguous [Cout, R*S*Cin] KRSC view, bf16 or fp32) =
-    out_scale * dY^T . im2col(X), split-M fp32 slabs on det_conv's transposed-read MFMA tiles."""
+    out_scale * dY^T . im2col(X) as split-pixel fp32 slabs reduced by a second launch: on
+    det_igemm_wgrad (``WGRAD_RING``; ``cfg`` its tile configuration, 0 = automatic, -1 = force the
+    older det_conv gemm_tn path) when a tile fits the shape, else on det_conv's gemm_tn."""
     nb, cin, hi, wi = x.shape
     cout, ho, wo = dy.shape[1], dy.shape[2], dy.shape[3]
     m = nb * ho * wo
@@ -210,6 +231,20 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, r: int, s: 
         return out
     assert out.dtype in (torch.bfloat16, torch.float32) and out.is_contiguous() and out.numel() == cout * r * s * cin
     lib = _lib.get_lib()
+    if WGRAD_RING and cfg >= 0:
+        n_ws = int(lib.det_igemm_wgrad_ws_elems(m, cout, r * s * cin, int(cfg)))
+        if n_ws > 0 and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0:
+            ws = torch.empty(n_ws, dtype=torch.float32, device=dy.device)
+            _lib.check(lib.det_igemm_wgrad(_stream(dy), dy.data_ptr(), x.data_ptr(), out.data_ptr(),
+                                           1 if out.dtype == torch.bfloat16 else 0, int(m), int(cout), int(cin), int(hi),
+                                           int(wi), int(ho), int(wo), int(r), int(s), int(stride), int(pad), ws.data_ptr(),
+                                           float(out_scale), int(cfg)),
+                       "igemm_wgrad")
+            WGRAD_COUNTS["ring"] += 1
+            return out
+        if cfg > 0:
+            _lib.check(-6, "igemm_wgrad (cfg %d does not tile [%d, %d])" % (cfg, cout, r * s * cin))
+    WGRAD_COUNTS["slab"] += 1
     ws = torch.empty(int(lib.det_conv_tn_ws_elems(m, cout, r * s * cin)), dtype=torch.float32, device=dy.device)
     _lib.check(lib.det_conv_wgrad(_stream(dy), dy.data_ptr(), x.data_ptr(), out.data_ptr(),
                                   1 if out.dtype == torch.bfloat16 else 0, int(m), int(cout), int(cin), int(hi), int(wi),
@@ -425,10 +460,11 @@ FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0, "stem": 0, "stem_fallback":
 # ------------------------------------------------------------------------------------------------
 CONV3X3_COUNTS = {"native": 0, "fallback": 0, "dgrad_native": 0, "dgrad_miopen": 0, "wgrad_native": 0,
                   "wgrad_miopen": 0}
-# 3x3 weight gradient on det_conv's split-M implicit GEMM (True) or MIOpen's wrw kernels (False,
-# default: 5.15 vs ~4.1 ms/step for ResNet-50's 16 3x3 wgrads at batch 512,
-# profiles/r3_resnet50_native3x3_steady.csv); the forward and stride-1 input gradient stay native.
-NATIVE_WGRAD_RS = False
+# R x S weight gradient: "auto" = det_igemm_wgrad (LDS-DMA ring) at Cin >= 256, where it beats MIOpen's
+# wrw kernels (0.178 vs 0.202 ms at 256 ch / 14x14, and needs none of their zero-fill / cast launches),
+# MIOpen's wrw below (0.33 vs 0.44 ms at 64 ch / 56x56; level at 128 ch in isolation, slower in the
+# step; profiles/r3_wgrad_ring_sweep.jsonl); "native" forces the ring / gemm_tn path, "miopen" MIOpen.
+WGRAD_RS_MODE = "auto"
 
 
 class _ConvRS(torch.autograd.Function):
@@ -467,7 +503,8 @@ class _ConvRS(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
                 CONV3X3_COUNTS["dgrad_miopen"] += 1
-        if ctx.needs_input_grad[1] and not NATIVE_WGRAD_RS:
+        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 256)
+        if ctx.needs_input_grad[1] and not native_wgrad:
             wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             gw = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [False, True, False])[1]

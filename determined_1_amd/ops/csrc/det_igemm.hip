@@ -903,9 +903,375 @@ __global__ void __launch_bounds__(256) dgrad_weight_kernel(const TI* __restrict_
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Weight gradient on the LDS-DMA ring: P[split][N][RSC] (fp32 slab per pixel split) =
+//   sum_{m in split} dY[m][n] . im2col(X)[m][rsc]            (rsc = (r*S + s)*Cin + c, KRSC order)
+//
+// Both operands arrive pixel-major ([m][channel], channels contiguous), i.e. K-major for this GEMM,
+// so they are staged as they sit in HBM and read K-contiguous with ds_read_b64_tr_b16 (T10).  Each
+// operand image is a stack of [32 pixels][64 channels] sub-tiles (128-B rows, 4 KiB), filled by
+// buffer_load ... lds (16-B pieces, lane-linear: one instruction = 8 rows of one sub-tile) with the
+// transposed-read swizzle applied on the SOURCE chunk; any multiple of 64 works for both tile
+// sides, so the 9-tap column dimension (576 = 9 x 64 at Cin 64) needs no padding.
+//   * dY pieces: fixed column per lane, the row advances 32 pixels per K step (one VALU add);
+//   * X pieces: per lane a fixed (tap r,s, channel c) and an output pixel (n, ho, wo) advanced 32
+//     pixels per step with carries (no divisions in the loop); padding taps and the split tail
+//     fetch at an out-of-range offset, which the buffer unit returns as zeros;
+//   * NS-stage ring with a counted vmcnt and raw s_barrier (as igemm3);
+//   * blocks of one pixel split are consecutive in the XCD remap, so the N tiles that re-read the
+//     same dY/X rows share an XCD's L2.
+// ------------------------------------------------------------------------------------------------
+struct WgArgs {
+  const unsigned short* dY;  // [M, N]
+  const unsigned short* X;   // NHWC [Nb, Hi, Wi, Cin]
+  float* P;                  // [splits, N, RSC]
+  int64_t M;
+  int N, RSC, Cin;
+  int Hi, Wi, Ho, Wo, stride, pad, S;
+  int rows_per_split;  // multiple of 32
+  int dy_bytes, x_bytes;
+};
+
+__device__ __forceinline__ int wswz(int row, int ch) {
+  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
+}
+
+// MFMA operand (16 columns x 32 pixels) of a [32][64] sub-tile via two transposed 4x16 reads: lane
+// (g = lane>>4, i = lane&15) gets pixels 8g + 0..7 of column c0 + i.
+__device__ __forceinline__ bf16x8 wtr_frag(const unsigned char* sub, int c0, int lane) {
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = c0 + 4 * p;
+  const int o0 = wswz(8 * g + q, col >> 3) + ((col & 4) << 1);
+  const int o1 = wswz(8 * g + 4 + q, col >> 3) + ((col & 4) << 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sub + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sub + o1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BM, int BN, int WM, int WN, int NS, int KB, int OCC>
+__global__ void __launch_bounds__(WM * WN * 64, OCC) wgrad3_kernel(WgArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // a stage = KB groups of 32 pixels (KB > 1: fewer barriers / waits per MFMA for small tiles)
+  constexpr int BK = 32, SK = BK * KB;
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int PA = BM / 16, PB = BN / 16, PT = PA + PB;  // 1-KiB pieces per 32-pixel group
+  static_assert(BM % 64 == 0 && BN % 64 == 0 && TM % 16 == 0 && TN % 16 == 0, "tile shape");
+  static_assert(PT % NW == 0, "pieces split evenly over the waves");
+  static_assert(NS >= 3, "prefetch distance");
+  constexpr int PW = PT / NW;  // pieces per wave per group
+  constexpr int A_BYTES = BM * 64, GROUP = (BM + BN) * 64, STAGE = GROUP * KB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: piece kinds branch per wave
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = a.N / BM, ntn = a.RSC / BN, ntiles = ntm * ntn;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int mt = tile / ntn, nt = tile - mt * ntn;
+  const int n0 = mt * BM, k0 = nt * BN;
+  const int64_t mbeg = static_cast<int64_t>(split) * a.rows_per_split;
+  int64_t mend = mbeg + a.rows_per_split;
+  if (mend > a.M) mend = a.M;
+  const int nk = mend > mbeg ? static_cast<int>((mend - mbeg + SK - 1) / SK) : 0;
+
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.dY), 0, a.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.X), 0, a.x_bytes, 0x00020000);
+  constexpr unsigned kOOB = 0xFFFFFFF0u;
+
+  // per piece: LDS slot (row, slot chunk) of this lane and the source it stands for
+  const int prow = lane >> 3;  // row within the piece's 8
+  int row_[PW];                // pixel row within a 32-pixel group
+  bool isa[PW];
+  int yoff[PW];                // A: byte offset of (mbeg + row, column)
+  int xc[PW], xr_[PW], xs[PW]; // B: channel, tap row/col
+  int xn[PW], xho[PW], xwo[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int p = i * NW + wid;
+    const bool pa = p < PA;
+    const int q = pa ? p : p - PA;  // piece within the operand
+    const int sub = q >> 2, row = (q & 3) * 8 + prow;
+    const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2));
+    row_[i] = row;
+    isa[i] = pa;
+    yoff[i] = 0;
+    xc[i] = xr_[i] = xs[i] = xn[i] = xho[i] = xwo[i] = 0;
+    if (pa) {
+      yoff[i] = static_cast<int>(((mbeg + row) * a.N + n0 + sub * 64 + ch * 8) * 2);
+    } else {
+      const int k = k0 + sub * 64 + ch * 8;
+      const int tap = k / a.Cin;
+      xc[i] = k - tap * a.Cin;
+      xr_[i] = tap / a.S;
+      xs[i] = tap - xr_[i] * a.S;
+      const int64_t m = mbeg + row;
+      const int hw = a.Ho * a.Wo;
+      xn[i] = static_cast<int>(m / hw);
+      const int rem = static_cast<int>(m - static_cast<int64_t>(xn[i]) * hw);
+      xho[i] = rem / a.Wo;
+      xwo[i] = rem - xho[i] * a.Wo;
+    }
+  }
+  const int adv_h = BK / a.Wo, adv_w = BK - adv_h * a.Wo;
+  const int ystep = BK * a.N * 2;
+
+  // issue stage kt's pieces (kt advances monotonically: the X pixel state is stepped here, 32
+  // pixels per group)
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NS) * STAGE;
+#pragma unroll
+    for (int g = 0; g < KB; ++g) {
+      const int grp = kt * KB + g;
+      const int64_t mrow0 = mbeg + static_cast<int64_t>(grp) * BK;
+#pragma unroll
+      for (int i = 0; i < PW; ++i) {
+        const int p = i * NW + wid;
+        const bool valid = mrow0 + row_[i] < mend;
+        unsigned v;
+        if (isa[i]) {
+          v = valid ? static_cast<unsigned>(yoff[i] + grp * ystep) : kOOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void*)(st + g * GROUP + p * 1024), 16, v, 0, 0, 0);
+        } else {
+          const int hi = xho[i] * a.stride - a.pad + xr_[i], wi = xwo[i] * a.stride - a.pad + xs[i];
+          const bool ok = valid && hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi;
+          v = ok ? static_cast<unsigned>((((xn[i] * a.Hi + hi) * a.Wi + wi) * a.Cin + xc[i]) * 2) : kOOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(st + g * GROUP + p * 1024), 16, v, 0, 0, 0);
+          // advance this row's output pixel by one group
+          xwo[i] += adv_w;
+          const int carry = xwo[i] >= a.Wo;
+          xwo[i] -= carry ? a.Wo : 0;
+          xho[i] += adv_h + carry;
+          while (xho[i] >= a.Ho) {
+            xho[i] -= a.Ho;
+            ++xn[i];
+          }
+        }
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stages issued: 0 .. min(nk-1, kt+NS-2); stage kt must land, the younger may stay in flight
+    if (kt + NS - 2 < nk) wait_vmcnt<KB * PW * (NS - 2)>();
+    else wait_vmcnt<0>();
+    block_barrier();  // every wave's stage-kt pieces landed; every wave is done reading stage kt-1
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);  // into stage kt-1's buffer
+#pragma unroll
+    for (int g = 0; g < KB; ++g) {
+      const unsigned char* base = smem + (kt % NS) * STAGE + g * GROUP;
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int c = wm * TM + i * 16;
+        af[i] = wtr_frag(base + (c >> 6) * 4096, c & 63, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * TN + j * 16;
+        bfr[j] = wtr_frag(base + A_BYTES + (c >> 6) * 4096, c & 63, lane);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  float* out = a.P + static_cast<int64_t>(split) * a.N * a.RSC;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wn * TN + j * 16 + (lane & 15);
+        out[static_cast<int64_t>(n) * a.RSC + k] = acc[i][j][r];
+      }
+#endif
+}
+
+// out[i] = scale * sum_s P[s][i]  (fp32 slabs -> bf16 or fp32), deterministic: a block owns E float4
+// columns and L = 256 / E split lanes (lane l sums splits l, l+L, ...), then lane 0 of each column
+// adds the L lane sums in order.  L > 1 when the output is small and the split count large (the
+// layer-1 shapes: 4096 outputs x ~1000 splits would otherwise run on a handful of workgroups).
+template <typename TO>
+__global__ void __launch_bounds__(256) wg_reduce_kernel(const float* __restrict__ P, int S, int64_t n, float scale,
+                                                        TO* __restrict__ out, int E) {
+  __shared__ float4 part[256];
+  const int L = 256 / E;
+  const int e = threadIdx.x % E, l = threadIdx.x / E;
+  const int64_t n4 = n >> 2;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * E + e;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    for (int s = l; s < S; s += L) {
+      const float4 v = reinterpret_cast<const float4*>(P + s * n)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (l != 0 || i >= n4) return;
+  for (int j = 1; j < L; ++j) {
+    const float4 v = part[j * E + e];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if constexpr (sizeof(TO) == 4) {
+    reinterpret_cast<float4*>(out)[i] = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
+  } else {
+    ushort4 o;
+    o.x = f2bf(acc.x * scale); o.y = f2bf(acc.y * scale); o.z = f2bf(acc.z * scale); o.w = f2bf(acc.w * scale);
+    reinterpret_cast<ushort4*>(out)[i] = o;
+  }
+}
+
+// wgrad tile configurations: {BM (output channels), BN (R*S*Cin columns), waves, occupancy, KB}
+struct WgCfg {
+  int bm, bn, nw, occ, kb;
+};
+constexpr WgCfg kWgCfgs[] = {
+    {0, 0, 0, 0, 0},
+    {64, 192, 4, 2, 1},    // 1: 1 x 4 waves of 64 x 48 (Cout 64 at 3 x 3: 576 = 3 x 192)
+    {128, 384, 8, 1, 1},   // 2: 2 x 4 waves of 64 x 96 (Cout 128 at 3 x 3: 1152 = 3 x 384)
+    {256, 256, 8, 1, 1},   // 3: 2 x 4 waves of 128 x 64
+    {128, 128, 4, 2, 1},   // 4: 2 x 2 waves of 64 x 64
+    {64, 256, 4, 2, 1},    // 5: 1 x 4 waves of 64 x 64
+    {256, 128, 8, 1, 1},   // 6: 4 x 2 waves of 64 x 64
+    {128, 256, 8, 1, 1},   // 7: 2 x 4 waves of 64 x 64
+    {64, 128, 4, 1, 2},    // 8: 1 x 4 waves of 64 x 32, 64 pixels per stage
+    {64, 64, 4, 2, 2},     // 9: 2 x 2 waves of 32 x 32, 64 pixels per stage
+    {256, 64, 4, 2, 1},    // 10: 4 x 1 waves of 64 x 64
+    {128, 64, 4, 1, 2},    // 11: 2 x 2 waves of 64 x 32, 64 pixels per stage
+    {64, 192, 4, 1, 2},    // 12: cfg 1 at 64 pixels per stage
+    {64, 64, 4, 1, 4},     // 13: cfg 9 at 128 pixels per stage
+};
+constexpr int kWgNumCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
+
+int wg_auto_cfg(int N, int RSC) {
+  static const int forced = [] {
+    const char* e = std::getenv("DET_WGRAD_CFG");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto fits = [&](int c) { return N % kWgCfgs[c].bm == 0 && RSC % kWgCfgs[c].bn == 0; };
+  if (forced > 0 && forced < kWgNumCfgs && fits(forced)) return forced;
+  for (int c : {3, 2, 7, 6, 10, 1, 5, 4, 11, 8, 9})
+    if (fits(c)) return c;
+  return 0;
+}
+
+int wg_splits(int64_t M, int N, int RSC, int cfg) {
+  const WgCfg& c = kWgCfgs[cfg];
+  const int64_t tiles = static_cast<int64_t>(N / c.bm) * (RSC / c.bn);
+  static const int target = [] {
+    const char* e = std::getenv("DET_WGRAD_WGS");
+    return e ? std::atoi(e) : 512;
+  }();
+  // ~two waves of workgroups over the 256 CUs (one wave: -20 % at Cout 128, profiles/r3_wgrad_ring_sweep.jsonl)
+  int64_t splits = (target * c.occ + tiles - 1) / tiles;
+  const int64_t max_rows = (M + 511) / 512;                  // >= 512 pixels (16 K steps) per split
+  // fp32 slab traffic (write + reduce read) at most the operand bytes ...
+  const int64_t max_bytes = (M * (static_cast<int64_t>(N) + RSC) * 2) / (8 * static_cast<int64_t>(N) * RSC);
+  if (splits > max_bytes) splits = max_bytes;
+  // ... but never fewer workgroups than one per CU slot (small-M deep layers)
+  const int64_t one_wave = (256 * c.occ + tiles - 1) / tiles;
+  if (splits < one_wave) splits = one_wave;
+  if (splits > max_rows) splits = max_rows;
+  if (splits < 1) splits = 1;
+  return static_cast<int>(splits);
+}
+
+template <int BM, int BN, int WM, int WN, int OCC, int KB>
+void launch_wg(hipStream_t st, const WgArgs& a, int nwg) {
+  constexpr int NS = 4;
+  constexpr int smem = NS * KB * (BM + BN) * 64;
+  static_assert(smem * OCC <= 163840, "LDS");
+  hipLaunchKernelGGL((wgrad3_kernel<BM, BN, WM, WN, NS, KB, OCC>), dim3(nwg), dim3(WM * WN * 64), smem, st, a);
+}
+
 }  // namespace
 
 extern "C" {
+
+// fp32 workspace elements det_igemm_wgrad needs for an [N, R*S*Cin] output from M pixels.
+int64_t det_igemm_wgrad_ws_elems(int64_t M, int N, int RSC, int cfg) {
+  const int c = cfg > 0 && cfg < kWgNumCfgs ? cfg : wg_auto_cfg(N, RSC);
+  if (c == 0 || N % kWgCfgs[c].bm != 0 || RSC % kWgCfgs[c].bn != 0) return 0;  // no tile fits
+  return static_cast<int64_t>(wg_splits(M, N, RSC, c)) * N * RSC;
+}
+
+// Weight gradient of an R x S convolution (stride, pad) over NHWC bf16 on the LDS-DMA ring:
+//   dW[N, R*S*Cin] (KRSC; out_dtype 0 fp32 / 1 bf16) = out_scale * dY[M, N]^T . im2col(X)[M, R*S*Cin]
+// as split-pixel fp32 slabs in ws (>= det_igemm_wgrad_ws_elems) reduced by a second launch.
+// N % 64 == 0, R*S*Cin divisible by the tile, Cin % 8 == 0, operands < 2 GiB, 16-B aligned.
+int det_igemm_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int N, int Cin,
+                    int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, float* ws, float out_scale,
+                    int cfg) {
+  if (M <= 0 || N <= 0 || Cin <= 0 || Cin % 8 != 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0) return -1;
+  const int64_t hw = static_cast<int64_t>(Ho) * Wo;
+  if (hw <= 0 || M % hw != 0) return -3;
+  if (Ho != (Hi + 2 * pad - R) / stride + 1 || Wo != (Wi + 2 * pad - S) / stride + 1) return -3;
+  if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X)) & 15) != 0) return -5;
+  const int RSC = R * S * Cin;
+  const int c = cfg > 0 && cfg < kWgNumCfgs ? cfg : wg_auto_cfg(N, RSC);
+  if (c == 0 || N % kWgCfgs[c].bm != 0 || RSC % kWgCfgs[c].bn != 0) return -6;
+  const int64_t dy_bytes = M * N * 2, x_bytes = (M / hw) * Hi * static_cast<int64_t>(Wi) * Cin * 2;
+  if (dy_bytes >= (static_cast<int64_t>(1) << 31) || x_bytes >= (static_cast<int64_t>(1) << 31)) return -8;
+  const int splits = wg_splits(M, N, RSC, c);
+  int64_t rps = (M + splits - 1) / splits;
+  const int sk = 32 * kWgCfgs[c].kb;
+  rps = (rps + sk - 1) / sk * sk;
+  const int real_splits = static_cast<int>((M + rps - 1) / rps);
+  WgArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, N, RSC, Cin, Hi, Wi,
+           Ho, Wo, stride, pad, S, static_cast<int>(rps), static_cast<int>(dy_bytes), static_cast<int>(x_bytes)};
+  const int nwg = (N / kWgCfgs[c].bm) * (RSC / kWgCfgs[c].bn) * real_splits;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (c) {
+    case 1: launch_wg<64, 192, 1, 4, 2, 1>(st, a, nwg); break;
+    case 2: launch_wg<128, 384, 2, 4, 1, 1>(st, a, nwg); break;
+    case 3: launch_wg<256, 256, 2, 4, 1, 1>(st, a, nwg); break;
+    case 4: launch_wg<128, 128, 2, 2, 2, 1>(st, a, nwg); break;
+    case 5: launch_wg<64, 256, 1, 4, 2, 1>(st, a, nwg); break;
+    case 6: launch_wg<256, 128, 4, 2, 1, 1>(st, a, nwg); break;
+    case 7: launch_wg<128, 256, 2, 4, 1, 1>(st, a, nwg); break;
+    case 8: launch_wg<64, 128, 1, 4, 1, 2>(st, a, nwg); break;
+    case 9: launch_wg<64, 64, 2, 2, 2, 2>(st, a, nwg); break;
+    case 10: launch_wg<256, 64, 4, 1, 2, 1>(st, a, nwg); break;
+    case 11: launch_wg<128, 64, 2, 2, 1, 2>(st, a, nwg); break;
+    case 12: launch_wg<64, 192, 1, 4, 1, 2>(st, a, nwg); break;
+    case 13: launch_wg<64, 64, 2, 2, 1, 4>(st, a, nwg); break;
+    default: return -7;
+  }
+  const int rc = static_cast<int>(hipGetLastError());
+  if (rc != 0) return rc;
+  const int64_t slab = static_cast<int64_t>(N) * RSC, n4 = slab / 4;
+  int lanes = 1;  // split lanes per output column: enough workgroups for small outputs
+  while (lanes < 256 && lanes < real_splits && n4 / (256 / lanes) < 2048) lanes *= 2;
+  const int E = 256 / lanes;
+  const int grid = static_cast<int>((n4 + E - 1) / E);
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(wg_reduce_kernel<unsigned short>, dim3(grid), dim3(256), 0, st, ws, real_splits, slab, out_scale,
+                       static_cast<unsigned short*>(out), E);
+  else
+    hipLaunchKernelGGL(wg_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, ws, real_splits, slab, out_scale,
+                       static_cast<float*>(out), E);
+  return static_cast<int>(hipGetLastError());
+}
 
 // out[C][R*S*K] bf16 = the flipped, transposed KRSC weight the stride-1 input gradient convolves with.
 int det_conv_dgrad_weight(void* stream, const void* W, int in_dtype, void* out, int K, int C, int R, int S) {

@@ -90,6 +90,54 @@ def test_conv_wgrad_matches_torch(gpu, case):
         torch.testing.assert_close(got, ref, rtol=tol, atol=tol * float(ref.abs().max()))
 
 
+WGRAD_SHAPES = [  # (Nb, Cin, H, W, Cout, R, stride, pad)
+    (3, 64, 9, 11, 64, 3, 1, 1),       # M = 297: ragged last K step
+    (8, 64, 28, 28, 64, 3, 1, 1),      # many splits, multi-row pixel carries
+    (2, 128, 15, 15, 128, 3, 2, 1),    # stride 2, odd input
+    (2, 256, 7, 7, 256, 3, 1, 1),      # Ho*Wo = 49 > 32: image carries inside a step
+    (2, 128, 14, 14, 256, 1, 2, 0),    # 1x1 stride-2
+    (4, 256, 7, 7, 64, 1, 1, 0),       # 1x1, N = 64
+]
+
+
+@pytest.mark.parametrize("cfg", list(range(1, 14)))
+@pytest.mark.parametrize("case", WGRAD_SHAPES)
+def test_ring_wgrad_every_cfg_exact(gpu, case, cfg):
+    """det_igemm_wgrad (LDS-DMA ring + transposed reads) per tile configuration on small-integer
+    operands: every product and partial sum is exact in fp32, so any tap / swizzle / split /
+    carry error shows as an exact mismatch against torch's fp32 weight gradient."""
+    nb, cin, h, w, cout, r, st, pad = case
+    x, _, xg, _ = _data(case, gpu, seed=5, integer=True)
+    ho, wo = (h + 2 * pad - r) // st + 1, (w + 2 * pad - r) // st + 1
+    g = torch.Generator(device="cpu").manual_seed(6)
+    dy = torch.randint(-2, 3, (nb, cout, ho, wo), generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, r, r), dy.float(), stride=st, padding=pad)
+    out = torch.full((cout, r * r * cin), float("nan"), dtype=torch.float32, device=gpu)
+    before = dict(conv.WGRAD_COUNTS)
+    try:
+        conv.conv_wgrad(dy.to(gpu).contiguous(memory_format=torch.channels_last), xg, out, r, r, st, pad, cfg=cfg)
+    except RuntimeError as e:
+        if "-6" in str(e):
+            pytest.skip(f"wgrad cfg {cfg} does not cover this shape")
+        raise
+    assert conv.WGRAD_COUNTS["ring"] == before["ring"] + 1
+    got = out.view(cout, r, r, cin).permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, rtol=0, atol=0)
+
+
+def test_ring_wgrad_scale_and_bf16_out(gpu):
+    case = (4, 128, 14, 14, 128, 3, 1, 1)
+    nb, cin, h, w, cout, r, st, pad = case
+    x, _, xg, _ = _data(case, gpu, seed=9)
+    g = torch.Generator(device="cpu").manual_seed(10)
+    dy = torch.randn(nb, cout, h, w, generator=g).to(torch.bfloat16)
+    ref = 0.25 * torch.nn.grad.conv2d_weight(x.float(), (cout, cin, r, r), dy.float(), stride=st, padding=pad)
+    out = torch.empty(cout, r * r * cin, dtype=torch.bfloat16, device=gpu)
+    conv.conv_wgrad(dy.to(gpu).contiguous(memory_format=torch.channels_last), xg, out, r, r, st, pad, out_scale=0.25)
+    got = out.view(cout, r, r, cin).permute(0, 3, 1, 2).float().cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+
+
 def test_dgrad_weight_kernel_matches_torch(gpu):
     for dt in (torch.float32, torch.bfloat16):
         w = torch.randn(96, 64, 3, 3, device=gpu).to(dt).contiguous(memory_format=torch.channels_last)
@@ -98,10 +146,11 @@ def test_dgrad_weight_kernel_matches_torch(gpu):
         assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("native_wgrad", [False, True])
+@pytest.mark.parametrize("wgrad_mode", ["miopen", "auto", "native"])
 @pytest.mark.parametrize("stride", [1, 2])
-def test_conv_rs_autograd_end_to_end(gpu, stride, native_wgrad, monkeypatch):
-    monkeypatch.setattr(conv, "NATIVE_WGRAD_RS", native_wgrad)
+def test_conv_rs_autograd_end_to_end(gpu, stride, wgrad_mode, monkeypatch):
+    monkeypatch.setattr(conv, "WGRAD_RS_MODE", wgrad_mode)
+    native_wgrad = wgrad_mode == "native"  # auto: Cin 128 stays on MIOpen
     torch.manual_seed(0)
     m = torch.nn.Conv2d(128, 128, 3, stride=stride, padding=1, bias=False).to(gpu).to(
         memory_format=torch.channels_last)
