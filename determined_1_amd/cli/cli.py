@@ -608,6 +608,18 @@ def cmd_deploy_local(args: argparse.Namespace) -> None:
         c.down()
 
 
+def cmd_tunnel(args: argparse.Namespace) -> None:
+    from determined_1_amd.cli import tunnel
+
+    argv = [args.master, args.service]
+    if args.listen is not None:
+        argv += ["--listen", str(args.listen)]
+    for k in ("cert_file", "cert_name"):
+        if getattr(args, k):
+            argv += ["--" + k.replace("_", "-"), getattr(args, k)]
+    tunnel.main(argv)
+
+
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="det", description="Determined (MI355X-native) command line")
     p.add_argument("-m", "--master", default=os.environ.get("DET_MASTER", "127.0.0.1:8080"))
@@ -819,6 +831,13 @@ def build_parser() -> argparse.ArgumentParser:
             x = grp.add_parser(name)
             x.add_argument("command_id", type=int)
             x.set_defaults(func=fn)
+
+    tn = sub.add_parser("tunnel", help="TCP stream to a task service through the master (stdio or --listen PORT)")
+    tn.add_argument("service", help="command id or cmd-<id>")
+    tn.add_argument("--listen", type=int, default=None)
+    tn.add_argument("--cert-file")
+    tn.add_argument("--cert-name")
+    tn.set_defaults(func=cmd_tunnel)
 
     ps = sub.add_parser("preview-search")
     ps.add_argument("config_file")

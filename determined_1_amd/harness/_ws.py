@@ -1,4 +1,5 @@
-"""Minimal synchronous WebSocket client (RFC 6455, text frames) for the harness <-> master channel.
+"""Minimal synchronous WebSocket client (RFC 6455, text + binary frames) for the harness <-> master
+channel and the ``det tunnel`` byte stream.
 
 The reference uses ``lomond`` (``harness/determined/layers/_socket_manager.py:41-69``); it is not
 installed here and the protocol needs only text frames, ping/pong and close, so this is ~100 lines
@@ -81,8 +82,18 @@ class WebSocket:
             raise WebSocketError("send on closed websocket")
         self._send_frame(0x1, text.encode())
 
+    def send_binary(self, data: bytes) -> None:
+        if self.closed:
+            raise WebSocketError("send on closed websocket")
+        self._send_frame(0x2, data)
+
     def recv(self) -> Optional[str]:
         """Next text message, or None when the peer closed the connection."""
+        m = self.recv_bytes()
+        return None if m is None else m.decode()
+
+    def recv_bytes(self) -> Optional[bytes]:
+        """Next text or binary message as bytes, or None when the peer closed the connection."""
         message = b""
         while True:
             try:
@@ -99,7 +110,8 @@ class WebSocket:
             mask = self._read_exact(4) if b1 & 0x80 else None
             payload = self._read_exact(n)
             if mask:
-                payload = bytes(c ^ mask[i % 4] for i, c in enumerate(payload))
+                m = (mask * (n // 4 + 1))[:n]
+                payload = (int.from_bytes(payload, "little") ^ int.from_bytes(m, "little")).to_bytes(n, "little") if n else b""
             if opcode == 0x8:
                 self.close()
                 return None
@@ -110,7 +122,7 @@ class WebSocket:
                 continue
             message += payload
             if fin:
-                return message.decode()
+                return message
 
     def close(self) -> None:
         if self.closed:

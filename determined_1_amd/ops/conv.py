@@ -259,6 +259,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, r: int, s: 
 # ------------------------------------------------------------------------------------------------
 COUNTS = {"native": 0, "fallback": 0}
 ENABLED = True  # A/B switch (models.resnet.NATIVE_CONV1X1 toggles it)
+DGRAD_BT = True  # 1x1 input gradients read the weight untransposed (no per-call transpose copy)
 
 
 def _attach_partials(y: torch.Tensor, parts: Optional[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:
@@ -294,7 +295,20 @@ def _bn_producer(x: torch.Tensor):
     return gf if isinstance(gf, _BNActTrain._backward_cls) else None
 
 
-def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) -> Optional[torch.Tensor]:
+def dgrad_1x1(dy2d: torch.Tensor, w2d: torch.Tensor) -> torch.Tensor:
+    """dX[M, Cin] = dY[M, Cout] . W[Cout, Cin] for a 1x1 conv.  On the GPU with ``DGRAD_BT`` the GEMM
+    reads the weight as stored (transposed LDS reads), else through a transposed copy."""
+    if DGRAD_BT and is_gpu(dy2d) and w2d.dtype == torch.bfloat16 and w2d.is_contiguous():
+        m, k = dy2d.shape
+        n = w2d.shape[1]
+        dx = torch.empty(m, n, dtype=torch.bfloat16, device=dy2d.device)
+        _lib.check(_lib.get_lib().det_conv_dgrad(_stream(dy2d), dy2d.data_ptr(), w2d.data_ptr(), dx.data_ptr(), int(m),
+                                                 int(n), int(k)), "conv_dgrad")
+        return dx
+    return conv1x1_nt(dy2d, w2d.t().contiguous())[0]
+
+
+def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int) -> Optional[torch.Tensor]:
     """dgrad with the producer BN's backward partials in the epilogue, or None when the producer
     cannot take it (no ReLU, the shortcut gradient not in yet, already fused, layout/dtype)."""
     mode = getattr(prod, "mask_mode", 0)
@@ -317,10 +331,11 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, wt: torch.Tensor, m: int, c: int) 
     psum = torch.empty(nrb, c, dtype=torch.float32, device=dy2d.device)
     psumx = torch.empty(nrb, c, dtype=torch.float32, device=dy2d.device)
     d = torch.empty(m, c, dtype=torch.bfloat16, device=dy2d.device)
+    wb = w2d if DGRAD_BT else w2d.t().contiguous()  # [Cout, Cin] as stored, or the transposed copy
     _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
-        _stream(dy2d), dy2d.data_ptr(), wt.data_ptr(), d.data_ptr(), int(m), int(c), int(wt.shape[1]), xb.data_ptr(),
+        _stream(dy2d), dy2d.data_ptr(), wb.data_ptr(), d.data_ptr(), int(m), int(c), int(w2d.shape[0]), xb.data_ptr(),
         stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits), _ptr(add), psum.data_ptr(),
-        psumx.data_ptr(), int(mode)), "conv_nt_bnbwd")
+        psumx.data_ptr(), int(mode), 1 if DGRAD_BT else 0), "conv_nt_bnbwd")
     prod.fused_bwd = (psum, psumx, rpb)
     if expects:
         prod.extra_dy = None  # consumed: summed into d
@@ -357,10 +372,10 @@ class _Conv1x1(torch.autograd.Function):
         dx = dw = None
         prod, ctx.bn_producer = ctx.bn_producer, None
         if ctx.needs_input_grad[0]:
-            wt = weight.reshape(cout, c).to(torch.bfloat16).t().contiguous()
-            dx2 = _fused_bn_dgrad(prod, dy2, wt, n * h * w_, c) if (prod is not None and is_gpu(dy2)) else None
+            w2 = weight.reshape(cout, c).to(torch.bfloat16).contiguous()
+            dx2 = _fused_bn_dgrad(prod, dy2, w2, n * h * w_, c) if (prod is not None and is_gpu(dy2)) else None
             if dx2 is None:
-                dx2, _ = conv1x1_nt(dy2, wt)
+                dx2 = dgrad_1x1(dy2, w2)
                 if prod is not None:
                     BN_BWD_COUNTS["unfused"] += 1
             else:
@@ -437,8 +452,7 @@ class _BNReluConv1x1(torch.autograd.Function):
             conv1x1_wgrad(dy2, x2, dw.view(cout, c), scale=stats[2], shift=stats[3])
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
-        wt = weight.reshape(cout, c).to(torch.bfloat16).t().contiguous()
-        dz2, _ = conv1x1_nt(dy2, wt)  # gradient of relu(bn(x)), [m, c]
+        dz2 = dgrad_1x1(dy2, weight.reshape(cout, c).to(torch.bfloat16).contiguous())  # gradient of relu(bn(x))
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dgb = torch.empty((2, c), dtype=torch.float32, device=x.device) if gamma is not None else None
         ws = torch.empty(int(lib.det_bn_ws_elems(m, c)), dtype=torch.float32, device=x.device)

@@ -121,6 +121,29 @@ __device__ __forceinline__ us8 affine_relu8(us8 v, const float* __restrict__ sca
   return o;
 }
 
+// byte offset of 16-B chunk ch of row `row` in a [64][W] bf16 tile (W = 64 or 128): XOR pattern
+// that makes the ds_read_b64_tr_b16 fragment reads (4 rows x 2 chunks per 16-lane group, two such
+// groups 8 rows apart per 32-lane half) hit distinct banks
+template <int W>
+__device__ __forceinline__ int tswz(int row, int ch) {
+  if (W == 128) return row * 256 + ((ch ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3))) << 4);
+  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
+}
+
+// MFMA operand (16 columns x 32 k-rows) via two transposed 4x16 reads: lane (g = lane>>4, i = lane&15)
+// gets rows k0 + 8g + 0..7 of column c0 + i.
+template <int W>
+__device__ __forceinline__ bf16x8 tr_frag(const unsigned char* tile, int k0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = c0 + 4 * p;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int o0 = tswz<W>(k0 + 8 * g + q, col >> 3) + ((col & 4) << 1);
+  const int o1 = tswz<W>(k0 + 8 * g + 4 + q, col >> 3) + ((col & 4) << 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + o0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + o1));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // BN-backward epilogue of an input-gradient GEMM whose output feeds a training BatchNorm's backward
 // (C = dL/dy of y = act(bn(x) [+ res])):  d = mask * (C [+ add]) is written instead of C, and the
 // BN's backward partial sums over this block's rows, psum = sum d and psumx = sum d (x - mean), go
@@ -160,7 +183,10 @@ struct NtArgs {
 // OCC: workgroups per CU the register budget is sized for.  K == 64 (one K tile: layer1's
 // 64-channel side, every dgrad into a 64-channel input) is a pure streaming pass with no K loop
 // to overlap loads with, so it runs single-buffered (half the LDS) at higher occupancy instead.
-template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false>
+// BT: B is given as [K, N] (N contiguous: the conv weight [Cout, Cin] itself for an input gradient),
+// staged as it sits ([64 k][BN] image, the wgrad swizzle) and read with ds_read_b64_tr_b16 -- no
+// transposed weight copy per call.
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false, bool BT = false>
 __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
@@ -197,6 +223,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
     }
   }
   const unsigned short* bptr = a.B + static_cast<int64_t>(n0 + r0) * K + kc * 8;
+  constexpr int BCPR = BN / 8;  // BT: 16-B chunks per B image row
 
   us8 ra[ACH], rb[BCH];
   auto gload = [&](int kt) {
@@ -208,7 +235,14 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       else ra[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
     }
 #pragma unroll
-    for (int j = 0; j < BCH; ++j) rb[j] = *reinterpret_cast<const us8*>(bptr + 32 * j * K + k);
+    for (int j = 0; j < BCH; ++j) {
+      if (BT) {
+        const int idx = tid + j * kThreads, r = idx / BCPR, c = idx - r * BCPR;
+        rb[j] = *reinterpret_cast<const us8*>(a.B + (k + r) * a.N + n0 + c * 8);
+      } else {
+        rb[j] = *reinterpret_cast<const us8*>(bptr + 32 * j * K + k);
+      }
+    }
   };
   auto lstore = [&](int buf, int kt) {
     unsigned char* base = smem + buf * BUF;
@@ -222,7 +256,14 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       *reinterpret_cast<us8*>(base + swz(r0 + 32 * i, kc)) = v;
     }
 #pragma unroll
-    for (int j = 0; j < BCH; ++j) *reinterpret_cast<us8*>(base + A_BYTES + swz(r0 + 32 * j, kc)) = rb[j];
+    for (int j = 0; j < BCH; ++j) {
+      if (BT) {
+        const int idx = tid + j * kThreads, r = idx / BCPR, c = idx - r * BCPR;
+        *reinterpret_cast<us8*>(base + A_BYTES + tswz<BN>(r, c)) = rb[j];
+      } else {
+        *reinterpret_cast<us8*>(base + A_BYTES + swz(r0 + 32 * j, kc)) = rb[j];
+      }
+    }
   };
 
   f32x4 acc[FM][FN];
@@ -247,8 +288,10 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       for (int i = 0; i < FM; ++i)
         af[i] = *reinterpret_cast<const bf16x8*>(base + swz(wm * TM + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+      for (int j = 0; j < FN; ++j) {
+        if (BT) bfr[j] = tr_frag<BN>(base + A_BYTES, ks * 32, wn * TN + j * 16, lane);
+        else bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_BYTES + swz(wn * TN + j * 16 + (lane & 15), ch));
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -410,29 +453,6 @@ struct TnArgs {
   const float* shift;
   Gather g;
 };
-
-// byte offset of 16-B chunk ch of row `row` in a [64][W] bf16 tile (W = 64 or 128): XOR pattern
-// that makes the ds_read_b64_tr_b16 fragment reads (4 rows x 2 chunks per 16-lane group, two such
-// groups 8 rows apart per 32-lane half) hit distinct banks
-template <int W>
-__device__ __forceinline__ int tswz(int row, int ch) {
-  if (W == 128) return row * 256 + ((ch ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3))) << 4);
-  return row * 128 + ((ch ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2))) << 4);
-}
-
-// MFMA operand (16 columns x 32 k-rows) via two transposed 4x16 reads: lane (g = lane>>4, i = lane&15)
-// gets rows k0 + 8g + 0..7 of column c0 + i.
-template <int W>
-__device__ __forceinline__ bf16x8 tr_frag(const unsigned char* tile, int k0, int c0, int lane) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int col = c0 + 4 * p;
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const int o0 = tswz<W>(k0 + 8 * g + q, col >> 3) + ((col & 4) << 1);
-  const int o1 = tswz<W>(k0 + 8 * g + 4 + q, col >> 3) + ((col & 4) << 1);
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + o0));
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + o1));
-  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
 
 // KSUB: K sub-tiles of BK columns per workgroup (each a separately swizzled [64][BK] LDS image);
 // KSUB = 2 lets one workgroup cover K = 2*BK so every dY row is streamed once (the stem's K = 256).
@@ -618,15 +638,24 @@ constexpr int nt_smem() {
 }
 
 template <int BM, int BN, int WM, int WN, int OCC>
-int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2, bool bnb = false) {
+int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2, bool bnb = false, bool bt = false) {
   const int64_t mtiles = (a.M + BM - 1) / BM;
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int smem = nt_smem<BM, BN, OCC == 2 ? 2 : 1>();
   if (bnb) {  // input-gradient GEMM with the BN-backward epilogue (no prologue / stats / gather)
     constexpr int smem_b = smem > BM * (BN + 16) * 2 + kThreads * 16 * 4 ? smem : BM * (BN + 16) * 2 + kThreads * 16 * 4;
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true>),
-                       dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
+    if (bt)
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true>),
+                         dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true>),
+                         dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
+    return static_cast<int>(hipGetLastError());
+  }
+  if (bt) {  // plain input-gradient GEMM against the untransposed weight
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true>),
+                       dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
     return static_cast<int>(hipGetLastError());
   }
 #define DET_NT(P, S, G)                                                                               \
@@ -684,12 +713,28 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
   return launch_nt<128, 64, 2, 2, 2>(st, a, pro, stats, stride2);
 }
 
+// dX[M, N] = dY[M, K] . W[K, N]: the input gradient of a 1x1 conv against its weight W = [Cout, Cin]
+// as stored (no transposed copy).  bf16, N % 64 == 0, K % 64 == 0.
+int det_conv_dgrad(void* stream, const void* dY, const void* W, void* dX, int64_t M, int N, int K) {
+  if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
+  NtArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(dX),
+           M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (K == kBK) {
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, false, true);
+    return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, false, true);
+  }
+  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, false, false, false, false, true);
+  return launch_nt<128, 64, 2, 2, 2>(st, a, false, false, false, false, true);
+}
+
 // dX[M, N] = dY[M, K] . W^T[N, K]^T with the BN-backward epilogue (BnBwdEpi above): writes
 // d = mask * (dX [+ add]) and the BN's backward partials psum / psumx [ceil(M/128), N].
 // mode 1: x, mean, scale, shift; mode 2: x, mean, mbits (add nullable).
+// b_kn: B is the untransposed weight [K, N] (the gemm reads it with transposed LDS reads).
 int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
                       const float* mean, const float* scale, const float* shift, const void* mbits, const void* add,
-                      float* psum, float* psumx, int mode) {
+                      float* psum, float* psumx, int mode, int b_kn) {
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
   if (!x || !mean || !psum || !psumx || (mode == 1 && (!scale || !shift)) || (mode == 2 && !mbits) || mode < 1 || mode > 2)
     return -2;
@@ -697,12 +742,13 @@ int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64
            M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}, BnBwdEpi{static_cast<const unsigned short*>(x), mean, scale,
            shift, static_cast<const uint8_t*>(mbits), static_cast<const unsigned short*>(add), psum, psumx, mode}};
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool bt = b_kn != 0;
   if (K == kBK) {
-    if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, true);
-    return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, true);
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, true, bt);
+    return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, true, bt);
   }
-  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, false, false, false, true);
-  return launch_nt<128, 64, 2, 2, 2>(st, a, false, false, false, true);
+  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, false, false, false, true, bt);
+  return launch_nt<128, 64, 2, 2, 2>(st, a, false, false, false, true, bt);
 }
 
 // fp32 workspace elements det_conv_tn needs (slabs) for an [N, K] output from M rows.

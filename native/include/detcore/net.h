@@ -74,6 +74,7 @@ class WsConn : public std::enable_shared_from_this<WsConn> {
   WsConn(int fd, bool client_side, std::string peer, std::string initial = "");
   ~WsConn();
   bool Send(const std::string& text);
+  bool SendBinary(const std::string& data);  // opcode 2 (byte streams: the TCP tunnel)
   void Close();
   bool closed() const { return closed_.load(); }
   const std::string& peer() const { return peer_; }

@@ -32,12 +32,14 @@
 
 #include <signal.h>
 #include <spawn.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cctype>
+#include <cerrno>
 #include <chrono>
 #include <cstdio>
 #include <ctime>
@@ -46,6 +48,7 @@
 #include <mutex>
 #include <random>
 #include <sstream>
+#include <thread>
 
 #include "detcore/config.h"
 #include "detcore/lttb.h"
@@ -1032,6 +1035,61 @@ void Master::InstallRoutes() {
     http_.Route(m, "/proxy/:task/*", proxy);
     http_.Route(m, "/proxy/:task", proxy);
   }
+  // TCP tunnel (reference cli/determined_cli/tunnel.py over master/internal/proxy's WebSocket
+  // upgrade): a WebSocket upgrade on /proxy/<task>/ is spliced onto a raw TCP connection to the
+  // service, binary frames both ways, so any TCP protocol (not just HTTP) reaches the task;
+  // `det tunnel` is the client.
+  auto tunnel = [this](const net::Request& r, net::WsPtr ws) {
+    std::string task = r.Param("task");
+    int64_t id = 0;
+    try {
+      id = std::stoll(task.rfind("cmd-", 0) == 0 ? task.substr(4) : task);
+    } catch (const std::exception&) {
+      ws->Close();
+      return;
+    }
+    Json c;
+    if (!store_->Get("commands", id, &c) || c.get_string("service_address", "").empty() ||
+        c.get_string("state", "") == "TERMINATED") {
+      ws->Close();
+      return;
+    }
+    std::string addr = c.get_string("service_address", "");
+    auto colon = addr.rfind(':');
+    std::string err;
+    int fd = net::ConnectTcp(addr.substr(0, colon), std::stoi(addr.substr(colon + 1)), 10000, &err);
+    if (fd < 0) {
+      ws->Close();
+      return;
+    }
+    std::thread up([fd, ws] {  // service -> client
+      std::string buf(65536, '\0');
+      for (;;) {
+        ssize_t n = ::recv(fd, &buf[0], buf.size(), 0);
+        if (n < 0 && errno == EINTR) continue;
+        if (n <= 0 || !ws->SendBinary(buf.substr(0, static_cast<size_t>(n)))) break;
+      }
+      ws->Close();
+    });
+    ws->ReadLoop([fd](const std::string& m) {  // client -> service; an empty frame = client EOF
+      if (m.empty()) {
+        ::shutdown(fd, SHUT_WR);  // half-close: the service sees EOF and can still answer
+        return;
+      }
+      size_t off = 0;
+      while (off < m.size()) {
+        ssize_t n = ::send(fd, m.data() + off, m.size() - off, MSG_NOSIGNAL);
+        if (n < 0 && errno == EINTR) continue;
+        if (n <= 0) return;
+        off += static_cast<size_t>(n);
+      }
+    });
+    ::shutdown(fd, SHUT_RDWR);
+    up.join();
+    ::close(fd);
+  };
+  http_.RouteWs("/proxy/:task/*", tunnel);
+  http_.RouteWs("/proxy/:task", tunnel);
   http_.Route("GET", "/commands/:id", [this](const net::Request& r) {
     Json c;
     if (!store_->Get("commands", IntParam(r, "id"), &c)) return Err(404, "command not found");

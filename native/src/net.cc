@@ -486,6 +486,7 @@ bool WsConn::SendFrame(int opcode, const std::string& payload) {
 }
 
 bool WsConn::Send(const std::string& text) { return SendFrame(0x1, text); }
+bool WsConn::SendBinary(const std::string& data) { return SendFrame(0x2, data); }
 
 void WsConn::Close() {
   bool was = closed_.exchange(true);

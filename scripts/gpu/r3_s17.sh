@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 session 17: ring wgrad only where it clearly wins (3x3 Cin >= 256, three 1x1 shapes): conv GPU tests,
+# Round-3 session 17: ring wgrad only where it clearly wins (3x3 Cin >= 256, three 1x1 shapes) + 1x1 dgrad on the untransposed weight: conv GPU tests,
 # wgrad sweep at the final split rule, ResNet bench + steady profile.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1

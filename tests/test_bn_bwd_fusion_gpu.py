@@ -10,9 +10,10 @@ from determined_1_amd.ops import _lib, conv
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("b_kn", [0, 1])
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("m,c,k", [(1000, 128, 256), (4096, 64, 64), (777, 256, 512)])
-def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k):
+def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k, b_kn):
     g = torch.Generator(device="cpu").manual_seed(m + c + mode)
     dy = torch.randn(m, k, generator=g).to(torch.bfloat16)
     w = (torch.randn(c, k, generator=g) / k ** 0.5).to(torch.bfloat16)  # B operand = the transposed conv weight
@@ -38,11 +39,13 @@ def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k):
     psumx = torch.empty(nrb, c, device=gpu)
     d = torch.empty(m, c, dtype=torch.bfloat16, device=gpu)
     dev = lambda t: None if t is None else t.to(gpu).contiguous()  # noqa: E731
-    dyg, wg, xg, meang, scg, shg, addg, bitsg = (dev(t) for t in (dy, w, x, mean, scale, shift, add, bits))
+    # b_kn = 1: the GEMM reads the conv weight [k, c] as stored (transposed LDS reads)
+    wop = w.t().contiguous() if b_kn else w
+    dyg, wg, xg, meang, scg, shg, addg, bitsg = (dev(t) for t in (dy, wop, x, mean, scale, shift, add, bits))
     _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
         torch.cuda.current_stream().cuda_stream, dyg.data_ptr(), wg.data_ptr(), d.data_ptr(), m, c, k,
         xg.data_ptr(), meang.data_ptr(), scg.data_ptr(), shg.data_ptr(), None if bitsg is None else bitsg.data_ptr(),
-        None if addg is None else addg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), mode), "bnbwd")
+        None if addg is None else addg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), mode, b_kn), "bnbwd")
     torch.cuda.synchronize()
     got = d.float().cpu()
     # one bf16 rounding of the accumulated product may differ by an ulp from torch's rounding

@@ -74,6 +74,17 @@ def test_conv_dgrad_via_transposed_weight(gpu, m, cin, cout):
     torch.testing.assert_close(dx.float(), dy.float() @ w.float(), rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("m,cin,cout", SHAPES + [(777, 128, 64), (4096, 64, 64)])
+def test_conv_dgrad_untransposed_weight_exact(gpu, m, cin, cout):
+    """det_conv_dgrad (weight read as stored with transposed LDS reads) on small-integer operands:
+    exact against the fp32 product, so a swizzle or k/n mix-up shows as a mismatch."""
+    g = torch.Generator(device="cpu").manual_seed(m + cin)
+    dy = torch.randint(-2, 3, (m, cout), generator=g).to(torch.bfloat16)
+    w = torch.randint(-2, 3, (cout, cin), generator=g).to(torch.bfloat16)
+    dx = conv.dgrad_1x1(dy.to(gpu), w.to(gpu))
+    torch.testing.assert_close(dx.float().cpu(), (dy.float() @ w.float()).to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("m,cin,cout", SHAPES + [(50000, 64, 256)])
 @pytest.mark.parametrize("pro", [False, True])
 def test_conv_wgrad(gpu, m, cin, cout, pro):
