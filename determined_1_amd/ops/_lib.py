@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -87,7 +87,8 @@ _SIGNATURES = {
     # det_norm.hip: fused BatchNorm(+add)(+ReLU), channels_last
     # stream, dtype, d, x, M, C, gamma, mean, rstd, psum, psumx, nrb, rpb, dx, dgamma, dbeta, coef
     "det_bn_bwd_from_partials": ([c_void_p, c_int, c_void_p, c_void_p, c_i64, c_int] + [c_void_p] * 5 + [c_int, c_i64]
-                                 + [c_void_p] * 4, c_int),
+                                 + [c_void_p] * 5, c_int),
+    "det_bn_bwd_scratch_elems": ([c_int], c_i64),
     "det_bn_ws_elems": ([c_i64, c_int], c_i64),
     "det_bn_fin_ws_elems": ([c_int], c_i64),
     # stream, dtype, x, res, y, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,

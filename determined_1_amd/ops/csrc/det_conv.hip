@@ -610,26 +610,55 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_tn_kernel(TnArgs a) {
       }
 }
 
-// out[i] = scale * sum_s P[s][i]  (fp32 slabs -> bf16 or fp32)
+// out[i] = scale * sum_s P[s][i]  (fp32 slabs -> bf16 or fp32), deterministic: a block owns E float4
+// columns and L = 256 / E split lanes (lane l sums slabs l, l+L, ...), lane 0 of each column adds the
+// L lane sums in order.  L > 1 for small outputs with many slabs (a 64 x 64 weight from 512 slabs
+// ran on 4 workgroups).
 template <typename TO>
 __global__ void __launch_bounds__(kThreads) slab_reduce_kernel(const float* __restrict__ P, int S, int64_t n, float scale,
-                                                                TO* __restrict__ out) {
+                                                                TO* __restrict__ out, int E) {
+  __shared__ float4 part[kThreads];
+  const int L = kThreads / E;
+  const int e = threadIdx.x % E, l = threadIdx.x / E;
   const int64_t n4 = n >> 2;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n4;
-       i += static_cast<int64_t>(gridDim.x) * kThreads) {
-    float4 acc = reinterpret_cast<const float4*>(P)[i];
-    for (int s = 1; s < S; ++s) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * E + e;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    for (int s = l; s < S; s += L) {
       const float4 v = reinterpret_cast<const float4*>(P + s * n)[i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    if constexpr (sizeof(TO) == 4) {
-      reinterpret_cast<float4*>(out)[i] = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
-    } else {
-      ushort4 o;
-      o.x = f2bf(acc.x * scale); o.y = f2bf(acc.y * scale); o.z = f2bf(acc.z * scale); o.w = f2bf(acc.w * scale);
-      reinterpret_cast<ushort4*>(out)[i] = o;
-    }
   }
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (l != 0 || i >= n4) return;
+  for (int j = 1; j < L; ++j) {
+    const float4 v = part[j * E + e];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if constexpr (sizeof(TO) == 4) {
+    reinterpret_cast<float4*>(out)[i] = make_float4(acc.x * scale, acc.y * scale, acc.z * scale, acc.w * scale);
+  } else {
+    ushort4 o;
+    o.x = f2bf(acc.x * scale); o.y = f2bf(acc.y * scale); o.z = f2bf(acc.z * scale); o.w = f2bf(acc.w * scale);
+    reinterpret_cast<ushort4*>(out)[i] = o;
+  }
+}
+
+// launch the slab reduce with enough workgroups: split lanes per column while the output is small
+void launch_slab_reduce(hipStream_t st, const float* ws, int splits, int64_t slab, float scale, void* out,
+                        int out_dtype) {
+  const int64_t n4 = slab / 4;
+  int lanes = 1;
+  while (lanes < kThreads && lanes < splits && n4 / (kThreads / lanes) < 2048) lanes *= 2;
+  const int E = kThreads / lanes;
+  const int grid = static_cast<int>((n4 + E - 1) / E);
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, scale,
+                       static_cast<unsigned short*>(out), E);
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, scale,
+                       static_cast<float*>(out), E);
 }
 
 template <int BM, int BN, int NBUF>
@@ -787,14 +816,7 @@ int det_conv_tn(void* stream, const void* dY, const void* X, void* out, int out_
   else if (bk == 128) rc = launch_tn<64, 128>(st, a, splits, pro, stride2);
   else rc = launch_tn<64, 64>(st, a, splits, pro, stride2);
   if (rc != 0) return rc;
-  int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
-  if (grid > 2048) grid = 2048;
-  if (out_dtype == 1)
-    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
-                       static_cast<unsigned short*>(out));
-  else
-    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
-                       static_cast<float*>(out));
+  launch_slab_reduce(st, ws, splits, slab, out_scale, out, out_dtype);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -823,14 +845,7 @@ int det_conv_wgrad(void* stream, const void* dY, const void* X, void* out, int o
   else if (bk == 128) rc = launch_tn<64, 128>(st, a, splits, false, false, true);
   else rc = launch_tn<64, 64>(st, a, splits, false, false, true);
   if (rc != 0) return rc;
-  int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
-  if (grid > 2048) grid = 2048;
-  if (out_dtype == 1)
-    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
-                       static_cast<unsigned short*>(out));
-  else
-    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
-                       static_cast<float*>(out));
+  launch_slab_reduce(st, ws, splits, slab, out_scale, out, out_dtype);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -881,14 +896,7 @@ int det_stem_conv_wgrad(void* stream, const void* dY, const void* X, void* out, 
   const int nwg = splits;  // one 64 x 256 output tile: every dY row is read once
   constexpr int smem = 2 * 64 * (64 + 2 * 128) * 2;
   hipLaunchKernelGGL((gemm_tn_kernel<64, 128, false, kGmStem, 2>), dim3(nwg), dim3(kThreads), smem, st, a);
-  int grid = static_cast<int>((slab / 4 + kThreads - 1) / kThreads);
-  if (grid > 2048) grid = 2048;
-  if (out_dtype == 1)
-    hipLaunchKernelGGL(slab_reduce_kernel<unsigned short>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
-                       static_cast<unsigned short*>(out));
-  else
-    hipLaunchKernelGGL(slab_reduce_kernel<float>, dim3(grid), dim3(kThreads), 0, st, ws, splits, slab, out_scale,
-                       static_cast<float*>(out));
+  launch_slab_reduce(st, ws, splits, slab, out_scale, out, out_dtype);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -333,6 +334,60 @@ bn_stats_reduce(const float* __restrict__ pmean, const float* __restrict__ pm2, 
   }
 }
 
+// Combine of the S slices (fp64 pairs) per channel, 16 lanes per channel in a fixed order
+// (deterministic): a lane walks S / 16 slices instead of one thread walking all S (the serial
+// 256-thread combine took ~10 us per call).  A one-launch variant that merged in the last-arriving
+// reduce block was slower (41 vs 16 us per BN: every block's agent-scope fence writes back L2,
+// profiles/r3_resnet50_lastblock_finalize_negative_steady.csv).
+__global__ void __launch_bounds__(kFinThreads)
+bn_stats_combine_par(const double* __restrict__ part, int S, Geom g, FinArgs a) {
+  __shared__ double red1[kFinLanes][kFinCh];
+  __shared__ double red2[kFinLanes][kFinCh];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  double t1 = 0, t2 = 0;
+  if (ok) {
+    for (int q = lane; q < S; q += kFinLanes) {
+      const int64_t o = (static_cast<int64_t>(q) * g.C + c) * 2;
+      t1 += part[o];
+      t2 += part[o + 1];
+    }
+  }
+  red1[lane][cl] = t1;
+  red2[lane][cl] = t2;
+  __syncthreads();
+  if (lane != 0 || !ok) return;
+  t1 = 0;
+  t2 = 0;
+#pragma unroll
+  for (int q = 0; q < kFinLanes; ++q) {
+    t1 += red1[q][cl];
+    t2 += red2[q][cl];
+  }
+  const double M = static_cast<double>(g.M);
+  const double meand = t1 / M;
+  double m2 = t2 - M * meand * meand;
+  if (m2 < 0) m2 = 0;
+  const float mean = static_cast<float>(meand);
+  const float var = static_cast<float>(m2 / M);
+  const float rstd = rsqrtf(var + a.eps);
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  const float bt = a.beta ? a.beta[c] : 0.f;
+  const float sc = gm * rstd;
+  a.save_mean[c] = mean;
+  a.save_rstd[c] = rstd;
+  a.scale[c] = sc;
+  a.shift[c] = bt - mean * sc;
+  if (a.running_mean) {
+    float f = a.momentum;
+    if (f < 0.f) f = a.num_batches_tracked ? 1.f / static_cast<float>(*a.num_batches_tracked + 1) : 0.f;
+    const float unbiased = g.M > 1 ? static_cast<float>(m2 / (M - 1.0)) : var;
+    a.running_mean[c] = (1.f - f) * a.running_mean[c] + f * mean;
+    a.running_var[c] = (1.f - f) * a.running_var[c] + f * unbiased;
+  }
+}
+
 __global__ void __launch_bounds__(256)
 bn_stats_combine(const double* __restrict__ part, int S, Geom g, FinArgs a) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -385,7 +440,7 @@ void launch_stats_finalize(hipStream_t st, const float* pmean, const float* pm2,
   S = (g.nrb + per - 1) / per;
   double* part = reinterpret_cast<double*>(scratch);
   hipLaunchKernelGGL(bn_stats_reduce, dim3(cb, S), dim3(kFinThreads), 0, st, pmean, pm2, g, per, part);
-  hipLaunchKernelGGL(bn_stats_combine, dim3((g.C + 255) / 256), dim3(256), 0, st, part, S, g, fa);
+  hipLaunchKernelGGL(bn_stats_combine_par, dim3(cb), dim3(kFinThreads), 0, st, part, S, g, fa);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -594,6 +649,107 @@ bn_bwd_finalize(const float* __restrict__ psum, const float* __restrict__ psumx,
   }
 }
 
+// Sliced backward finalize: blocks (channel block, slice) sum their slice of the [nrb, C] partials
+// into part[S][C][2]; a combine launch merges the slices (16 lanes per channel, fixed order) and
+// writes dgamma, dbeta and the apply coefficients (the single-block finalize walked 12,544 partial
+// rows serially for a layer-1 activation: ~22 us).
+__global__ void __launch_bounds__(kFinThreads)
+bn_bwd_reduce(const float* __restrict__ psum, const float* __restrict__ psumx, Geom g, int per_slice,
+              float* __restrict__ part) {
+  __shared__ float r1[kFinLanes][kFinCh];
+  __shared__ float r2[kFinLanes][kFinCh];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  const int b0 = blockIdx.y * per_slice;
+  const int b1 = min(g.nrb, b0 + per_slice);
+  float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    int b = b0 + lane;
+    for (; b + 3 * kFinLanes < b1; b += 4 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = static_cast<int64_t>(b + u * kFinLanes) * g.C + c;
+        sa[u] += psum[o];
+        sb[u] += psumx[o];
+      }
+    }
+    for (; b < b1; b += kFinLanes) {
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      sa[0] += psum[o];
+      sb[0] += psumx[o];
+    }
+  }
+  r1[lane][cl] = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+  r2[lane][cl] = (sb[0] + sb[1]) + (sb[2] + sb[3]);
+  __syncthreads();
+  if (lane == 0 && ok) {
+    float ts = 0.f, tsx = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) { ts += r1[q][cl]; tsx += r2[q][cl]; }
+    const int64_t o = (static_cast<int64_t>(blockIdx.y) * g.C + c) * 2;
+    part[o] = ts;
+    part[o + 1] = tsx;
+  }
+}
+
+__global__ void __launch_bounds__(kFinThreads)
+bn_bwd_combine(const float* __restrict__ part, int S, Geom g, BwdFin a) {
+  __shared__ float r1[kFinLanes][kFinCh];
+  __shared__ float r2[kFinLanes][kFinCh];
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  float ts = 0.f, tsx = 0.f;
+  if (ok) {
+    for (int q = lane; q < S; q += kFinLanes) {
+      const int64_t o = (static_cast<int64_t>(q) * g.C + c) * 2;
+      ts += part[o];
+      tsx += part[o + 1];
+    }
+  }
+  r1[lane][cl] = ts;
+  r2[lane][cl] = tsx;
+  __syncthreads();
+  if (lane != 0 || !ok) return;
+  ts = 0.f;
+  tsx = 0.f;
+#pragma unroll
+  for (int q = 0; q < kFinLanes; ++q) { ts += r1[q][cl]; tsx += r2[q][cl]; }
+  const float rstd = a.rstd[c], mu = a.mean[c];
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  const float dbeta = ts;
+  const float dgamma = tsx * rstd;
+  if (a.dgamma) a.dgamma[c] = dgamma;
+  if (a.dbeta) a.dbeta[c] = dbeta;
+  const float invM = 1.f / static_cast<float>(g.M);
+  const float A = gm * rstd;
+  const float B = -gm * rstd * rstd * dgamma * invM;
+  const float C0 = -A * dbeta * invM - B * mu;
+  a.coef[c] = A;
+  a.coef[g.C + c] = B;
+  a.coef[2 * g.C + c] = C0;
+}
+
+// Backward finalize: sliced reduce + parallel combine when the partial list is long and scratch
+// (>= 2 * kMaxSlices * C floats) is given, else the single-launch walk.
+void launch_bwd_finalize(hipStream_t st, const float* psum, const float* psumx, const Geom& g, const BwdFin& bf,
+                         float* scratch) {
+  const int cb = (g.C + kFinCh - 1) / kFinCh;
+  int S = 1024 / cb;
+  if (S > kMaxSlices) S = kMaxSlices;
+  const int by_rows = g.nrb / (4 * kFinLanes);
+  if (S > by_rows) S = by_rows;
+  if (!scratch || S < 4) {
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(cb), dim3(kFinThreads), 0, st, psum, psumx, g, bf);
+    return;
+  }
+  const int per = (g.nrb + S - 1) / S;
+  S = (g.nrb + per - 1) / per;
+  hipLaunchKernelGGL(bn_bwd_reduce, dim3(cb, S), dim3(kFinThreads), 0, st, psum, psumx, g, per, scratch);
+  hipLaunchKernelGGL(bn_bwd_combine, dim3(cb), dim3(kFinThreads), 0, st, scratch, S, g, bf);
+}
+
 template <typename T, int MASK, bool DRES>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ dy2, const T* __restrict__ x,
@@ -686,6 +842,9 @@ int64_t det_bn_ws_elems(int64_t M, int C) {
 
 // fp32 workspace elements det_bn_fwd_from_partials needs (two-stage finalize scratch).
 int64_t det_bn_fin_ws_elems(int C) { return fin_scratch_elems(C); }
+
+// fp32 scratch elements of det_bn_bwd_from_partials' sliced finalize.
+int64_t det_bn_bwd_scratch_elems(int C) { return 2 * static_cast<int64_t>(kMaxSlices) * C; }
 
 // dtype: 0 = fp32, 1 = bf16.  res may be null.  Outputs save_mean/save_rstd/scale/shift [C].
 int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
@@ -838,7 +997,7 @@ int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* 
 // det_conv_nt's BN-backward epilogue).  Runs the finalize and an unmasked apply: dx = A d + B x + C.
 int det_bn_bwd_from_partials(void* stream, int dtype, const void* d, const void* x, int64_t M, int C, const float* gamma,
                              const float* save_mean, const float* save_rstd, const float* psum, const float* psumx,
-                             int nrb, int64_t rpb, void* dx, float* dgamma, float* dbeta, float* coef) {
+                             int nrb, int64_t rpb, void* dx, float* dgamma, float* dbeta, float* coef, float* scratch) {
   if (C % 8 != 0 || M <= 0 || nrb <= 0) return -1;
   if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -846,7 +1005,7 @@ int det_bn_bwd_from_partials(void* stream, int dtype, const void* d, const void*
   g.nrb = nrb;
   g.rpb = rpb;
   BwdFin bf{gamma, save_rstd, save_mean, dgamma, dbeta, coef};
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, psum, psumx, g, bf);
+  launch_bwd_finalize(st, psum, psumx, g, bf, scratch);
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 2);
   if (dtype == 1)
@@ -890,8 +1049,7 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const v
   }
 #undef DET_BN_P
   BwdFin bf{gamma, save_rstd, save_mean, dgamma, dbeta, coef};
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinThreads), 0, st, psum, psumx, g,
-                     bf);
+  launch_bwd_finalize(st, psum, psumx, g, bf, coef + 3 * static_cast<int64_t>(C));
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 2);
 #define DET_BN_B(T, MK, DR)                                                                            \

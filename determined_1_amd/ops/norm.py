@@ -141,13 +141,14 @@ class _BNActTrain(torch.autograd.Function):
             # gradient is also the residual's gradient (no second tensor)
             assert dy2 is None, "shortcut gradient arrived after the fused dgrad consumed it"
             psum, psumx, rpb = fused
-            coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+            # [3][C] apply coefficients, then the sliced finalize's scratch
+            coef = torch.empty(3 * C + int(lib.det_bn_bwd_scratch_elems(C)), dtype=torch.float32, device=x.device)
             _lib.check(
                 lib.det_bn_bwd_from_partials(
                     _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), M, C, _ptr(weight), stats[0].data_ptr(),
                     stats[1].data_ptr(), psum.data_ptr(), psumx.data_ptr(), int(psum.shape[0]), int(rpb),
                     dx.data_ptr(), None if dgb is None else dgb[0].data_ptr(),
-                    None if dgb is None else dgb[1].data_ptr(), coef.data_ptr()),
+                    None if dgb is None else dgb[1].data_ptr(), coef.data_ptr(), coef[3 * C:].data_ptr()),
                 "bn_bwd_from_partials",
             )
             dres = dy if want_res else None

@@ -212,3 +212,58 @@ def test_resnet50_fused_shortcut_link_and_pool_match_stock(gpu, monkeypatch):
     # median: the fused BN sums in a different fp32 order than MIOpen's BN, which 50 layers amplify
     # to ~1 % at batch 8 (observed 0.3-1.0 % across boxes); the stock-vs-stock noise sets the scale
     assert e[len(e) // 2] < 2 * noise[len(noise) // 2] + 1e-2, (e[len(e) // 2], noise[len(noise) // 2])
+
+
+def test_sliced_finalize_repeatable(gpu):
+    """The sliced finalizes (slice reduce + 16-lane fixed-order combine, forward statistics and
+    backward sums) are deterministic: bit-identical results on repeated launches."""
+    torch.manual_seed(1)
+    n, c, h, w = 8, 64, 224, 224  # 401k rows: sliced statistics + backward finalize
+    base = norm.BatchNormAct2d(c, relu=True, fused=True).to(gpu)
+    x = (torch.randn(n, c, h, w, device=gpu) * 2 + 0.7).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, c, h, w, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for _ in range(3):
+        mod = copy.deepcopy(base)
+        outs.append(_run(mod, x, None, dy) + (mod.running_mean.clone(), mod.running_var.clone()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            if a is not None:
+                assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("c", [64, 256])
+def test_bwd_from_partials_sliced_matches_fp64(gpu, c):
+    """det_bn_bwd_from_partials with a long partial list (2000 row-blocks: the sliced finalize) vs
+    an fp64 reference of dgamma, dbeta and dx = A d + B x + C; twice (scratch reuse)."""
+    from determined_1_amd.ops import _lib
+
+    lib = _lib.get_lib()
+    nrb, rpb = 2000, 128
+    m = nrb * rpb
+    g = torch.Generator(device="cpu").manual_seed(c)
+    d = torch.randn(m, c, generator=g).to(torch.bfloat16)
+    x = torch.randn(m, c, generator=g).to(torch.bfloat16)
+    psum = torch.randn(nrb, c, generator=g)
+    psumx = torch.randn(nrb, c, generator=g)
+    gamma = torch.rand(c, generator=g) + 0.5
+    mean = torch.randn(c, generator=g) * 0.1
+    rstd = torch.rand(c, generator=g) + 0.5
+    ts, tsx = psum.double().sum(0), psumx.double().sum(0)
+    dbeta_r, dgamma_r = ts, tsx * rstd.double()
+    A = gamma.double() * rstd.double()
+    B = -gamma.double() * rstd.double() ** 2 * dgamma_r / m
+    C0 = -A * dbeta_r / m - B * mean.double()
+    dx_r = A * d.double() + B * x.double() + C0
+    dev = [t.to(gpu).contiguous() for t in (d, x, psum, psumx, gamma, mean, rstd)]
+    for _ in range(2):
+        dx = torch.empty(m, c, dtype=torch.bfloat16, device=gpu)
+        dgb = torch.empty(2, c, device=gpu)
+        coef = torch.empty(3 * c + int(lib.det_bn_bwd_scratch_elems(c)), device=gpu)
+        _lib.check(lib.det_bn_bwd_from_partials(
+            torch.cuda.current_stream().cuda_stream, 1, dev[0].data_ptr(), dev[1].data_ptr(), m, c, dev[4].data_ptr(),
+            dev[5].data_ptr(), dev[6].data_ptr(), dev[2].data_ptr(), dev[3].data_ptr(), nrb, rpb, dx.data_ptr(),
+            dgb[0].data_ptr(), dgb[1].data_ptr(), coef.data_ptr(), coef[3 * c:].data_ptr()), "bwd_from_partials")
+        torch.testing.assert_close(dgb[1].double().cpu(), dbeta_r, rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(dgb[0].double().cpu(), dgamma_r, rtol=1e-5, atol=1e-3)
+        torch.testing.assert_close(dx.double().cpu(), dx_r, rtol=2e-2, atol=2e-2)
