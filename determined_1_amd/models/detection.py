@@ -20,9 +20,11 @@ MI355X-first differences:
     thresholds .50:.05:.95, 101-point interpolated precision, area ranges small/medium/large,
     at most 100 detections per image.
 """
+import math
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -401,16 +403,45 @@ class SyntheticDetection(torch.utils.data.Dataset):
 
 class SyntheticCocoInstances(torch.utils.data.Dataset):
     """Synthetic COCO-shaped instance-segmentation data (the COCO download is unavailable offline):
-    images of ``min_size``-``max_size`` px per side (landscape and portrait), 1-``max_objects``
-    instances each -- filled ellipses or rectangles of a per-class colour over a noisy background --
-    with absolute xyxy ``boxes``, ``labels`` and uint8 instance ``masks``.  Deterministic per index;
-    images are float RGB in [0, 1] (the detectors normalise them themselves)."""
+    images of ``min_size``-``max_size`` px per side (landscape and portrait), filled ellipses or
+    rectangles of a per-class colour over a noisy background, with absolute xyxy ``boxes``,
+    ``labels`` and uint8 instance ``masks``.  Deterministic per index; images are float RGB in
+    [0, 1] (the detectors normalise them themselves).
+
+    ``instance_dist``: "uniform" = 1-``max_objects`` large instances (w/10-w/2 per side);
+    "coco" = COCO train2017-like load: a geometric instance count with COCO's mean of 7.3 per
+    image, capped at 93 (COCO's maximum), and log-uniform object areas from 8x8 px to half the
+    image (COCO is ~41 % small objects), aspect ratios 1:2-2:1.  Later instances occlude earlier
+    ones; fully occluded instances are dropped."""
+
+    COCO_MEAN_INSTANCES = 7.3
+    COCO_MAX_INSTANCES = 93
 
     def __init__(self, length: int, num_classes: int = 81, min_size: int = 480, max_size: int = 640,
-                 max_objects: int = 6, seed: int = 0) -> None:
+                 max_objects: int = 6, seed: int = 0, instance_dist: str = "uniform") -> None:
+        if instance_dist not in ("uniform", "coco"):
+            raise ValueError(f"instance_dist must be 'uniform' or 'coco', got {instance_dist!r}")
         self.length, self.num_classes, self.min_size, self.max_size = length, num_classes, min_size, max_size
-        self.max_objects, self.seed = max_objects, seed
+        self.max_objects, self.seed, self.instance_dist = max_objects, seed, instance_dist
         self.colors = torch.rand(num_classes, 3, generator=torch.Generator().manual_seed(4321))
+
+    def _coco_boxes(self, g: torch.Generator, h: int, w: int) -> List[Tuple[int, int, int, int]]:
+        p = 1.0 / self.COCO_MEAN_INSTANCES
+        u = float(torch.rand(1, generator=g)) or 1e-12
+        n = min(self.COCO_MAX_INSTANCES, 1 + int(math.log(u) / math.log(1.0 - p)))
+        lo, hi = math.log(64.0 / (h * w)), math.log(0.25)  # area fraction: 8x8 px .. (1/2)^2
+        out = []
+        for _ in range(n):
+            a, r = torch.rand(2, generator=g).tolist()
+            area = math.exp(lo + a * (hi - lo)) * h * w
+            ar = math.exp((r - 0.5) * 2 * math.log(2.0))
+            bw = int(min(w, max(4, round(math.sqrt(area * ar)))))
+            bh = int(min(h, max(4, round(math.sqrt(area / ar)))))
+            x0 = int(torch.randint(0, w - bw + 1, (1,), generator=g))
+            y0 = int(torch.randint(0, h - bh + 1, (1,), generator=g))
+            c = int(torch.randint(1, self.num_classes, (1,), generator=g))
+            out.append((x0, y0, bw, bh, c, float(torch.rand(1, generator=g)) < 0.5))
+        return out
 
     def __len__(self) -> int:
         return self.length
@@ -420,29 +451,39 @@ class SyntheticCocoInstances(torch.utils.data.Dataset):
         h = int(torch.randint(self.min_size, self.max_size + 1, (1,), generator=g))
         w = int(torch.randint(self.min_size, self.max_size + 1, (1,), generator=g))
         img = torch.rand(3, h, w, generator=g) * 0.2 + 0.4
-        n = int(torch.randint(1, self.max_objects + 1, (1,), generator=g))
-        yy = torch.arange(h).view(h, 1).float()
-        xx = torch.arange(w).view(1, w).float()
-        boxes, labels, masks = [], [], []
-        for _ in range(n):
-            bw = int(torch.randint(max(8, w // 10), max(9, w // 2), (1,), generator=g))
-            bh = int(torch.randint(max(8, h // 10), max(9, h // 2), (1,), generator=g))
-            x0 = int(torch.randint(0, w - bw + 1, (1,), generator=g))
-            y0 = int(torch.randint(0, h - bh + 1, (1,), generator=g))
-            c = int(torch.randint(1, self.num_classes, (1,), generator=g))
-            if float(torch.rand(1, generator=g)) < 0.5:  # ellipse inscribed in the box
-                cy, cx, ry, rx = y0 + bh / 2, x0 + bw / 2, bh / 2, bw / 2
-                m = (((yy + 0.5 - cy) / ry) ** 2 + ((xx + 0.5 - cx) / rx) ** 2) <= 1.0
+        if self.instance_dist == "coco":
+            geo = self._coco_boxes(g, h, w)
+        else:
+            geo = []
+            for _ in range(int(torch.randint(1, self.max_objects + 1, (1,), generator=g))):
+                bw = int(torch.randint(max(8, w // 10), max(9, w // 2), (1,), generator=g))
+                bh = int(torch.randint(max(8, h // 10), max(9, h // 2), (1,), generator=g))
+                x0 = int(torch.randint(0, w - bw + 1, (1,), generator=g))
+                y0 = int(torch.randint(0, h - bh + 1, (1,), generator=g))
+                c = int(torch.randint(1, self.num_classes, (1,), generator=g))
+                geo.append((x0, y0, bw, bh, c, float(torch.rand(1, generator=g)) < 0.5))
+        # owner map: later instances occlude earlier ones (O(n * box area), not O(n^2 * image))
+        owner = torch.full((h, w), -1, dtype=torch.int16)
+        boxes, labels = [], []
+        for i, (x0, y0, bw, bh, c, ellipse) in enumerate(geo):
+            if ellipse:  # inscribed in the box
+                yy = torch.arange(bh).view(bh, 1).float() + 0.5 - bh / 2
+                xx = torch.arange(bw).view(1, bw).float() + 0.5 - bw / 2
+                m = ((yy / (bh / 2)) ** 2 + (xx / (bw / 2)) ** 2) <= 1.0
             else:
-                m = torch.zeros(h, w, dtype=torch.bool)
-                m[y0:y0 + bh, x0:x0 + bw] = True
-            img[:, m] = self.colors[c].view(3, 1)
-            for prev in masks:  # later instances occlude earlier ones
-                prev &= ~m
-            masks.append(m)
+                m = torch.ones(bh, bw, dtype=torch.bool)
+            sub = img[:, y0:y0 + bh, x0:x0 + bw]
+            sub[:, m] = self.colors[c].view(3, 1)
+            owner[y0:y0 + bh, x0:x0 + bw][m] = i
             boxes.append([float(x0), float(y0), float(x0 + bw), float(y0 + bh)])
             labels.append(c)
-        mk = torch.stack(masks).to(torch.uint8)
+        ids = torch.arange(len(geo), dtype=torch.int16).view(-1, 1, 1)
+        mk = (owner.unsqueeze(0) == ids).to(torch.uint8)
+        keep = mk.flatten(1).sum(1) > 0  # fully occluded instances are dropped
+        if not bool(keep.all()):
+            mk = mk[keep]
+            boxes = [b for b, k in zip(boxes, keep.tolist()) if k]
+            labels = [c for c, k in zip(labels, keep.tolist()) if k]
         target = {"boxes": torch.tensor(boxes), "labels": torch.tensor(labels, dtype=torch.int64), "masks": mk,
                   "image_id": torch.tensor([idx])}
         return img, target

@@ -47,7 +47,8 @@ class MaskRCNNTrial(pytorch.PyTorchTrial):
     def _data(self, train: bool) -> SyntheticCocoInstances:
         n = int(self.hp.get("train_records" if train else "validation_records", 1000 if train else 16))
         return SyntheticCocoInstances(n, num_classes=self.num_classes, min_size=int(self.hp.get("min_image_size", 480)),
-                                      max_size=int(self.hp.get("max_image_size", 640)), seed=0 if train else 1)
+                                      max_size=int(self.hp.get("max_image_size", 640)), seed=0 if train else 1,
+                                      instance_dist=str(self.hp.get("instance_dist", "uniform")))
 
     def build_training_data_loader(self) -> pytorch.DataLoader:
         return pytorch.DataLoader(self._data(True), batch_size=self.context.get_per_slot_batch_size(),

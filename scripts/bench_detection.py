@@ -51,6 +51,8 @@ def main() -> None:
     ap.add_argument("--min-size", type=int, default=0, help="synthetic image side range (0: model default)")
     ap.add_argument("--max-size", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny model (CPU smoke only)")
+    ap.add_argument("--coco-instances", action="store_true",
+                    help="COCO-like instance load (mean 7.3 per image, heavy tail, small objects) for Mask R-CNN / RetinaNet")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -94,6 +96,9 @@ def main() -> None:
         hp["num_images"] = max(int(hp.get("num_images", 170)), (args.steps + args.warmup) * gbs * 2)
     if args.model in ("maskrcnn", "retinanet"):
         hp["train_records"] = max(int(hp.get("train_records", 2000)), (args.steps + args.warmup) * gbs)
+        if args.coco_instances:
+            hp["instance_dist"] = "coco"
+            model_name += ", COCO-like instance load"
     if args.small:
         hp.update(backbone="resnet26", enc_layers=1, dec_layers=2, hidden_dim=32, nheads=2, dim_feedforward=64,
                   num_queries=10, num_workers=0, transform_min_size=96, transform_max_size=160)

@@ -48,3 +48,30 @@ def test_tiny_mask_rcnn_trains_and_predicts():
     for o, img in zip(out, imgs):
         assert o["masks"].shape[1:] == (1,) + tuple(img.shape[1:])
         assert o["masks"].shape[0] == o["boxes"].shape[0]
+
+
+def test_synthetic_coco_instance_load():
+    """instance_dist="coco": COCO train2017-like instance counts (mean 7.3, capped at 93) and small
+    objects; masks, boxes and labels stay aligned after occlusion drops, every mask is non-empty
+    and inside its box.  The default "uniform" load is unchanged (1..max_objects)."""
+    from determined_1_amd.models.detection import SyntheticCocoInstances
+
+    ds = SyntheticCocoInstances(300, min_size=200, max_size=260, instance_dist="coco")
+    counts, small = [], 0
+    for i in range(len(ds)):
+        img, t = ds[i]
+        n = t["labels"].shape[0]
+        assert t["boxes"].shape == (n, 4) and t["masks"].shape[0] == n and n >= 1
+        counts.append(n)
+        areas = t["masks"].flatten(1).sum(1)
+        assert bool((areas > 0).all())
+        for b, m in zip(t["boxes"].tolist(), t["masks"]):
+            ys, xs = torch.nonzero(m, as_tuple=True)
+            assert xs.min() >= b[0] and xs.max() < b[2] and ys.min() >= b[1] and ys.max() < b[3]
+        small += int(((t["boxes"][:, 2] - t["boxes"][:, 0]) * (t["boxes"][:, 3] - t["boxes"][:, 1]) < 32 * 32).sum())
+    mean = sum(counts) / len(counts)
+    assert 5.5 < mean < 8.5, mean  # geometric(1/7.3) less the fully occluded
+    assert max(counts) > 15 and max(counts) <= SyntheticCocoInstances.COCO_MAX_INSTANCES
+    assert small / sum(counts) > 0.2  # COCO: ~41 % small objects
+    uni = SyntheticCocoInstances(50, min_size=200, max_size=260)
+    assert all(1 <= uni[i][1]["labels"].shape[0] <= uni.max_objects for i in range(50))
