@@ -36,9 +36,9 @@ NATIVE_STEM = True
 NATIVE_CONV3X3 = True
 
 
-def c3x3(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+def c3x3(x: torch.Tensor, conv: nn.Conv2d, bn_exclusive: bool = False) -> torch.Tensor:
     if NATIVE_CONV3X3 and FUSED_BN:
-        return native_conv.conv_rs(x, conv)
+        return native_conv.conv_rs(x, conv, bn_exclusive=bn_exclusive)
     return conv(x)
 
 
@@ -126,7 +126,7 @@ class Bottleneck(nn.Module):
         # x (the previous block's output) reaches autograd only through conv1: the shortcut's
         # gradient is handed to its producer through the BN link (identity or _LinkedConv)
         out = self.bn1(c1x1(x, self.conv1, bn_exclusive=FUSED_BN and _shortcut_linked(self.downsample, x)))
-        out = bn_relu_c1x1(c3x3(out, self.conv2), self.bn2, self.conv3)
+        out = bn_relu_c1x1(c3x3(out, self.conv2, bn_exclusive=True), self.bn2, self.conv3)  # bn1 feeds only conv2
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
         return self.bn3(out, idt, shortcut_link=self.downsample is None)
 

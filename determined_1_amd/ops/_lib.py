@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -152,6 +152,7 @@ _SIGNATURES = {
     "det_conv_dgrad_weight": ([c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 4, c_int),
     # ... + cfg (0 = automatic per shape)
     "det_igemm_conv_cfg": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2 + [c_int], c_int),
+    "det_igemm_conv_bnbwd": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 6 + [c_int], c_int),
     # stream, dY, X, out, out_dtype, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, ws, out_scale
     "det_conv_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 10 + [c_void_p, c_float], c_int),
     "det_igemm_wgrad_ws_elems": ([c_i64, c_int, c_int, c_int], c_i64),

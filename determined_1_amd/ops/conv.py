@@ -342,6 +342,38 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int)
     return d
 
 
+def _fused_bn_dgrad_rs(prod, dyc: torch.Tensor, wt: torch.Tensor, wd: torch.Tensor, pad: int) -> Optional[torch.Tensor]:
+    """Stride-1 R x S input gradient on det_igemm with the producer BN's backward partials in its
+    epilogue (mask mode 1: ReLU recomputed from the BN input; ResNet bn1 -> conv2), or None when the
+    producer cannot take it."""
+    if getattr(prod, "mask_mode", 0) != 1 or getattr(prod, "fused_bwd", None) is not None:
+        return None
+    try:
+        xb, _, _, stats = prod.saved_tensors
+    except RuntimeError:
+        return None
+    nb, cout, h, w_ = dyc.shape
+    cin = wt.shape[0]
+    m = nb * h * w_
+    if xb.dtype != torch.bfloat16 or xb.shape != (nb, cin, h, w_) or not xb.is_contiguous(memory_format=torch.channels_last):
+        return None
+    lib = _lib.get_lib()
+    cfg = 0
+    rpb = int(lib.det_igemm_rows_per_block_cfg(int(cin), cfg))
+    nrb = (m + rpb - 1) // rpb
+    psum = torch.empty(nrb, cin, dtype=torch.float32, device=dyc.device)
+    psumx = torch.empty(nrb, cin, dtype=torch.float32, device=dyc.device)
+    d = torch.empty((nb, cin, h, w_), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
+    r, s = wt.shape[2], wt.shape[3]
+    _lib.check(lib.det_igemm_conv_bnbwd(_stream(dyc), dyc.data_ptr(), wd.data_ptr(), d.data_ptr(),
+                                        _zero_page(dyc.device).data_ptr(), int(m), int(cin), int(cout), int(h), int(w_),
+                                        int(h), int(w_), int(r), int(s), 1, int(pad), xb.data_ptr(), stats[0].data_ptr(),
+                                        stats[2].data_ptr(), stats[3].data_ptr(), psum.data_ptr(), psumx.data_ptr(),
+                                        cfg), "igemm_conv_bnbwd")
+    prod.fused_bwd = (psum, psumx, rpb)
+    return d
+
+
 class _Conv1x1(torch.autograd.Function):
     """``conv2d(x, w)`` for a 1x1 stride-1 kernel as det_conv GEMMs: forward with the output's
     BatchNorm statistics in the epilogue, dgrad through the transposed weight (with the input's
@@ -489,12 +521,13 @@ class _ConvRS(torch.autograd.Function):
     split-M implicit GEMM with the im2col gather, written straight into the arena slot."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, stats):
+    def forward(ctx, x, weight, stride, pad, stats, bn_producer=None):
         wk = krsc(weight.to(torch.bfloat16) if weight.dtype != torch.bfloat16 else weight)
         y, parts = igemm_conv(x, weight, stride=stride, pad=pad, stats=stats, w_krsc=wk)
         _attach_partials(y, parts)
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
+        ctx.bn_producer = bn_producer
         return y
 
     @staticmethod
@@ -510,7 +543,14 @@ class _ConvRS(torch.autograd.Function):
                 # (on the GPU only the shape of the second argument is read; the CPU reference
                 # path convolves with it, so it gets the real flipped weight there)
                 wt = weight.transpose(0, 1) if is_gpu(dyc) else weight.flip(2, 3).transpose(0, 1)
-                dx, _ = igemm_conv(dyc, wt, stride=1, pad=r - 1 - pad, w_krsc=wd)
+                prod, ctx.bn_producer = ctx.bn_producer, None
+                dx = _fused_bn_dgrad_rs(prod, dyc, wt, wd, r - 1 - pad) if (prod is not None and is_gpu(dyc)) else None
+                if dx is None:
+                    dx, _ = igemm_conv(dyc, wt, stride=1, pad=r - 1 - pad, w_krsc=wd)
+                    if prod is not None:
+                        BN_BWD_COUNTS["unfused"] += 1
+                else:
+                    BN_BWD_COUNTS["fused"] += 1
                 CONV3X3_COUNTS["dgrad_native"] += 1
             else:
                 wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -541,13 +581,16 @@ class _ConvRS(torch.autograd.Function):
             CONV3X3_COUNTS["wgrad_native"] += 1
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
-        return dx, dw, None, None, None
+        ctx.bn_producer = None
+        return dx, dw, None, None, None, None
 
 
-def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> torch.Tensor:
+def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_exclusive: bool = False) -> torch.Tensor:
     """``conv_mod(x)`` for bias-free square R x S convs (groups 1, dilation 1, symmetric zero padding)
     on channels_last bf16 CUDA activations with Cin % 64 == 0 and Cout % 64 == 0 (every ResNet 3x3);
-    anything else runs the module."""
+    anything else runs the module.  ``bn_exclusive``: this conv is the only autograd consumer of
+    ``x``, the output of a fused BatchNorm+ReLU, whose backward partials can then come from the
+    stride-1 input-gradient GEMM's epilogue (``FUSE_BN_BWD``)."""
     w = conv_mod.weight
     k = conv_mod.kernel_size
     st = conv_mod.stride
@@ -566,8 +609,9 @@ def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True) -> t
     CONV3X3_COUNTS["native"] += 1
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
+    prod = _bn_producer(x) if (bn_exclusive and FUSE_BN_BWD and torch.is_grad_enabled() and st[0] == 1) else None
     with torch.autocast("cuda", enabled=False):
-        return _ConvRS.apply(x, w, int(st[0]), int(pd[0]), stats)
+        return _ConvRS.apply(x, w, int(st[0]), int(pd[0]), stats, prod)
 # Stem weight gradient: the det_conv split-M implicit GEMM (True) or MIOpen's NHWC C=4 kernel (False,
 # default: 0.49 vs 0.82 ms at batch 512, profiles/r2_stem_microbench.jsonl).  The forward stays native
 # (0.64 ms including the BN statistics vs MIOpen 0.70 + a 0.17 ms stats pass).

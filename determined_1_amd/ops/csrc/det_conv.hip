@@ -386,16 +386,30 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       s1[j] = 0.f;
       s2[j] = 0.f;
     }
+    // all of this thread's loads (BN input, shortcut gradient, mask bits) are issued before the
+    // first store: the stores may alias them as far as the compiler knows, which would otherwise
+    // serialise every row on the HBM latency
+    constexpr int NQ = BM * CPR / kThreads;
+    us8 xs[NQ], as[NQ];
+    unsigned bs[NQ];
 #pragma unroll
-    for (int q = 0; q < BM * CPR / kThreads; ++q) {
+    for (int q = 0; q < NQ; ++q) {
+      const int row = (tid + q * kThreads) / CPR;
+      const bool ok = row < nvalid;
+      const int64_t off = (m0 + (ok ? row : 0)) * a.N + c0;
+      xs[q] = ok ? *reinterpret_cast<const us8*>(a.bn.x + off) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+      as[q] = (ok && a.bn.add) ? *reinterpret_cast<const us8*>(a.bn.add + off) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+      bs[q] = (ok && a.bn.mode == 2) ? a.bn.mbits[off >> 3] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
       const int row = (tid + q * kThreads) / CPR;
       if (row >= nvalid) continue;
       const int64_t off = (m0 + row) * a.N + c0;
       const us8 cv = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
-      const us8 xv = *reinterpret_cast<const us8*>(a.bn.x + off);
-      us8 av = us8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (a.bn.add) av = *reinterpret_cast<const us8*>(a.bn.add + off);
-      const unsigned bits = a.bn.mode == 2 ? a.bn.mbits[off >> 3] : 0u;
+      const us8 xv = xs[q];
+      const us8 av = as[q];
+      const unsigned bits = bs[q];
       us8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {

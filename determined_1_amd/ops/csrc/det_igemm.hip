@@ -76,7 +76,84 @@ struct IgArgs {
   int Hi, Wi, Ho, Wo, stride, pad, S;
   int R;
   int64_t x_bytes;  // X extent for the buffer resource (v2 fetch; < 2^31)
+  // BNB (input gradient feeding a training BatchNorm+ReLU backward, mask recomputed from the BN
+  // input): Y <- d = (bn_x * bn_scale + bn_shift > 0) ? dX : 0, and the BN's backward partials
+  // psum = sum d, psumx = sum d (bn_x - bn_mean) per (BM-row block, column)
+  const unsigned short* bn_x;
+  const float* bn_mean;
+  const float* bn_scale;
+  const float* bn_shift;
+  float* psum;
+  float* psumx;
 };
+
+// BN-backward epilogue of a BM x BN output tile held as bf16 in LDS (ct, row stride LDC): each
+// thread owns one 8-column chunk over rows tid/CPR + q*NT/CPR, writes the masked gradient and
+// accumulates the two sums of exactly what it wrote; the per-thread sums then overlay the C tile
+// ([NT][16] floats) and the NT/CPR threads of a column are added in a fixed order.
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void bnb_epilogue(const IgArgs& a, unsigned char* smem, const unsigned short* ct, int LDC,
+                                             int64_t m0, int n0, int mt, int nvalid, int tid) {
+  constexpr int CPR = BN / 8;
+  static_assert(NT % CPR == 0, "fixed chunk column per thread");
+  const int cc = tid % CPR;
+  const int c0 = n0 + cc * 8;
+  float mu[8], sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = a.bn_mean[c0 + j];
+    sc[j] = a.bn_scale[c0 + j];
+    sh[j] = a.bn_shift[c0 + j];
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
+  // every BN-input load of this thread is issued before the first store (the stores could alias
+  // the loads as far as the compiler knows, which would serialise each row on the HBM latency)
+  constexpr int NQ = BM * CPR / NT;
+  us8 xs[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int row = (tid + q * NT) / CPR;
+    xs[q] = row < nvalid ? *reinterpret_cast<const us8*>(a.bn_x + (m0 + row) * a.N + c0) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int row = (tid + q * NT) / CPR;
+    if (row >= nvalid) continue;
+    const int64_t off = (m0 + row) * a.N + c0;
+    const us8 cv = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+    const us8 xv = xs[q];
+    us8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xf = bf2f(xv[j]);
+      const float d = __fmaf_rn(xf, sc[j], sh[j]) > 0.f ? bf2f(cv[j]) : 0.f;
+      o[j] = f2bf(d);
+      const float dr = bf2f(o[j]);  // the sums see exactly what the BN apply reads back
+      s1[j] += dr;
+      s2[j] += dr * (xf - mu[j]);
+    }
+    *reinterpret_cast<us8*>(a.Y + off) = o;
+  }
+  float* scratch = reinterpret_cast<float*>(smem);  // overlays the consumed C tile
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    scratch[tid * 16 + j] = s1[j];
+    scratch[tid * 16 + 8 + j] = s2[j];
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const int ccol = tid / 8, j = tid % 8;
+    float t1 = 0.f, t2 = 0.f;
+    for (int g = 0; g < NT / CPR; ++g) {
+      t1 += scratch[(g * CPR + ccol) * 16 + j];
+      t2 += scratch[(g * CPR + ccol) * 16 + 8 + j];
+    }
+    a.psum[static_cast<int64_t>(mt) * a.N + n0 + tid] = t1;
+    a.psumx[static_cast<int64_t>(mt) * a.N + n0 + tid] = t2;
+  }
+}
 
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void*)(const_cast<void*>(g)), (lds_void*)(lds_wave_base), 16, 0, 0);
@@ -313,7 +390,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
 // by MFMAs issued before this iteration's barrier, so every wave is past its reads of that buffer.
 // RAW: each wave's vmcnt retires its own DMAs of tile kt+1 and the barrier publishes all waves'.
 // ------------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int NS, bool DENSE, bool STATS, int OCC>
+template <int BM, int BN, int WM, int WN, int NS, bool DENSE, bool STATS, int OCC, bool BNB = false>
 __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
   constexpr int NW = WM * WN, kThreads = NW * 64;
@@ -520,6 +597,10 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
     for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
     a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
   }
+  if constexpr (BNB) {
+    bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
+    return;
+  }
   constexpr int CPR = BN / 8;
 #pragma unroll
   for (int q = 0; q < (BM * CPR + kThreads - 1) / kThreads; ++q) {
@@ -555,7 +636,7 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int swz64(int row, int ch) { return row * 64 + ((ch ^ ((-(row >> 2)) & 3)) << 4); }
 
-template <int BM, int BN, int WM, int WN, int NS, bool STATS>
+template <int BM, int BN, int WM, int WN, int NS, bool STATS, bool BNB = false>
 __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int BK = 32;
@@ -776,6 +857,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
     for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
     a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
   }
+  if constexpr (BNB) {
+    bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
+    return;
+  }
   constexpr int CPR = BN / 8;
 #pragma unroll
   for (int q = 0; q < (BM * CPR + kThreads - 1) / kThreads; ++q) {
@@ -788,7 +873,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
 }
 
 template <int BM, int BN, int WM, int WN, int NS>
-int launch3(hipStream_t st, const IgArgs& a, bool stats) {
+int launch3(hipStream_t st, const IgArgs& a, bool stats, bool bnb = false) {
   constexpr int kThreads = WM * WN * 64;
   if (a.N % BN != 0 || a.Cin % 32 != 0) return -6;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
@@ -796,7 +881,11 @@ int launch3(hipStream_t st, const IgArgs& a, bool stats) {
   constexpr int ring = NS * (BM + BN) * 64, ctile = BM * (BN + 16) * 2 + 4 * WM * BN;
   constexpr int smem = ring > ctile ? ring : ctile;
   static_assert(smem <= 163840, "LDS");
-  if (stats)
+  static_assert(BM * (BN + 16) * 2 >= kThreads * 16 * 4, "BN-backward scratch fits in the C tile");
+  if (bnb)
+    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false, true>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem,
+                       st, a);
+  else if (stats)
     hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, true>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
   else
     hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
@@ -804,7 +893,7 @@ int launch3(hipStream_t st, const IgArgs& a, bool stats) {
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int OCC>
-int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats, bool bnb = false) {
   constexpr int kThreads = WM * WN * 64;
   if (a.N % BN != 0 || a.Cin % 64 != 0) return -6;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
@@ -814,7 +903,11 @@ int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
   hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, NS, D, S, OCC>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), \
                      smem, st, a)
   (void)dense;  // the tap-mask fetch covers 1x1 / strided / padded alike
-  if (stats) DET_IG2(false, true); else DET_IG2(false, false);
+  static_assert(BM * (BN + 16) * 2 >= kThreads * 16 * 4, "BN-backward scratch fits in the C tile");
+  if (bnb)
+    hipLaunchKernelGGL((igemm2_kernel<BM, BN, WM, WN, NS, false, false, OCC, true>), dim3(static_cast<unsigned>(nwg)),
+                       dim3(kThreads), smem, st, a);
+  else if (stats) DET_IG2(false, true); else DET_IG2(false, false);
 #undef DET_IG2
   return static_cast<int>(hipGetLastError());
 }
@@ -840,26 +933,26 @@ int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
 //   5: 256x64,  8 waves (8x1, 32x64), 3 stages (120 KiB)
 //   6: 128x64,  4 waves (2x2, 64x32), 3 stages (72 KiB), 2 blocks/CU
 //   7: 128x128, 4 waves (2x2, 64x64), 3 stages (96 KiB)
-static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool stats, bool bnb = false) {
   switch (cfg) {
     case 1:
-      if (a.Cin % 64) return -6;
+      if (a.Cin % 64 || bnb) return -6;
       if (a.N % 128 == 0) return launch<256, 128, 4, 2>(st, a, dense, stats);
       return launch<256, 64, 8, 1>(st, a, dense, stats);
-    case 2: return launch2<256, 128, 4, 2, 3, 1>(st, a, dense, stats);
-    case 3: return launch2<256, 64, 4, 1, 3, 1>(st, a, dense, stats);
-    case 4: return launch2<128, 128, 2, 2, 4, 1>(st, a, dense, stats);
-    case 5: return launch2<256, 64, 8, 1, 3, 1>(st, a, dense, stats);
-    case 6: return launch2<128, 64, 2, 2, 3, 2>(st, a, dense, stats);
-    case 7: return launch2<128, 128, 2, 2, 3, 1>(st, a, dense, stats);
-    case 8: return launch3<256, 256, 2, 4, 4>(st, a, stats);   // 128x64 wave tiles, BK 32, 4 stages
-    case 9: return launch3<256, 128, 4, 2, 4>(st, a, stats);   // 64x64 wave tiles, BK 32
-    case 10: return launch3<256, 256, 2, 4, 3>(st, a, stats);  // 3 stages
-    case 11: return launch3<256, 64, 4, 1, 4>(st, a, stats);   // 4 waves, 64x64 wave tiles (N = 64)
-    case 12: return launch3<512, 128, 4, 2, 3>(st, a, stats);  // 128x64 wave tiles at N = 128
-    case 13: return launch3<512, 128, 4, 2, 4>(st, a, stats);
-    case 14: return launch3<512, 64, 8, 1, 4>(st, a, stats);   // 64x64 wave tiles at N = 64, 8 waves
-    case 15: return launch3<512, 64, 4, 1, 4>(st, a, stats);   // 128x64 wave tiles at N = 64, 4 waves
+    case 2: return launch2<256, 128, 4, 2, 3, 1>(st, a, dense, stats, bnb);
+    case 3: return launch2<256, 64, 4, 1, 3, 1>(st, a, dense, stats, bnb);
+    case 4: return launch2<128, 128, 2, 2, 4, 1>(st, a, dense, stats, bnb);
+    case 5: return launch2<256, 64, 8, 1, 3, 1>(st, a, dense, stats, bnb);
+    case 6: return launch2<128, 64, 2, 2, 3, 2>(st, a, dense, stats, bnb);
+    case 7: return launch2<128, 128, 2, 2, 3, 1>(st, a, dense, stats, bnb);
+    case 8: return launch3<256, 256, 2, 4, 4>(st, a, stats, bnb);   // 128x64 wave tiles, BK 32, 4 stages
+    case 9: return launch3<256, 128, 4, 2, 4>(st, a, stats, bnb);   // 64x64 wave tiles, BK 32
+    case 10: return launch3<256, 256, 2, 4, 3>(st, a, stats, bnb);  // 3 stages
+    case 11: return launch3<256, 64, 4, 1, 4>(st, a, stats, bnb);   // 4 waves, 64x64 wave tiles (N = 64)
+    case 12: return launch3<512, 128, 4, 2, 3>(st, a, stats, bnb);  // 128x64 wave tiles at N = 128
+    case 13: return launch3<512, 128, 4, 2, 4>(st, a, stats, bnb);
+    case 14: return launch3<512, 64, 8, 1, 4>(st, a, stats, bnb);   // 64x64 wave tiles at N = 64, 8 waves
+    case 15: return launch3<512, 64, 4, 1, 4>(st, a, stats, bnb);   // 128x64 wave tiles at N = 64, 4 waves
     default: return -7;
   }
 }
@@ -1322,6 +1415,35 @@ int det_igemm_conv_cfg(void* stream, const void* X, const void* W, void* Y, cons
   const bool dense = R == 1 && S == 1 && stride == 1 && pad == 0 && Hi == Ho && Wi == Wo;
   hipStream_t st = static_cast<hipStream_t>(stream);
   return run_cfg(cfg > 0 ? cfg : auto_cfg(a), st, a, dense, pmean != nullptr);
+}
+
+// det_igemm_conv_cfg for an input gradient whose output feeds a training BatchNorm(+ReLU) backward:
+// Y <- the ReLU-masked gradient d (mask = bn_x*bn_scale + bn_shift > 0) and psum / psumx
+// [ceil(M/rpb), N] (rpb = det_igemm_rows_per_block_cfg(N, cfg)) = sum d, sum d (bn_x - bn_mean)
+// per row block: the BN backward is then finalize + unmasked apply (det_bn_bwd_from_partials).
+int det_igemm_conv_bnbwd(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,
+                         int Hi, int Wi, int Ho, int Wo, int R, int S, int stride, int pad, const void* bn_x,
+                         const float* bn_mean, const float* bn_scale, const float* bn_shift, float* psum, float* psumx,
+                         int cfg) {
+  if (M <= 0 || N <= 0 || N % 64 != 0 || Cin <= 0 || Cin % 32 != 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
+    return -1;
+  if (!bn_x || !bn_mean || !bn_scale || !bn_shift || !psum || !psumx || zero == nullptr) return -2;
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y) |
+        reinterpret_cast<uintptr_t>(zero) | reinterpret_cast<uintptr_t>(bn_x)) & 15) != 0)
+    return -5;
+  const int64_t hw = static_cast<int64_t>(Ho) * Wo;
+  if (hw <= 0 || M % hw != 0) return -3;
+  if (Ho != (Hi + 2 * pad - R) / stride + 1 || Wo != (Wi + 2 * pad - S) / stride + 1) return -3;
+  const int K = R * S * Cin;
+  const int64_t x_bytes = (M / hw) * Hi * static_cast<int64_t>(Wi) * Cin * 2;
+  if (x_bytes >= (static_cast<int64_t>(1) << 31) || static_cast<int64_t>(N) * K * 2 >= (static_cast<int64_t>(1) << 31))
+    return -8;
+  if (R * S > 32) return -1;
+  IgArgs a{static_cast<const unsigned short*>(X), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(Y),
+           static_cast<const unsigned short*>(zero), nullptr, nullptr, M, N, K, Cin, Hi, Wi, Ho, Wo, stride, pad, S, R, x_bytes,
+           static_cast<const unsigned short*>(bn_x), bn_mean, bn_scale, bn_shift, psum, psumx};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  return run_cfg(cfg > 0 ? cfg : auto_cfg(a), st, a, false, false, true);
 }
 
 int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,

@@ -108,7 +108,8 @@ def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
     dz_u, gr_u = run(False)
     dz_f, gr_f = run(True)
     conv.FUSE_BN_BWD = True
-    assert conv.BN_BWD_COUNTS["fused"] - before["fused"] >= 3  # bn2->conv3 x2, b0 output->b1.conv1 (mode 2)
+    # bn2->conv3 x2, bn1->conv2 (3x3 dgrad epilogue) x2, b0 output->b1.conv1 (mode 2)
+    assert conv.BN_BWD_COUNTS["fused"] - before["fused"] >= 5
 
     # fp32 reference with the same (bf16-valued) weights
     w = {n: p.detach().float().clone().requires_grad_(True) for n, p in mods.named_parameters()}
@@ -130,3 +131,46 @@ def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
     for n in errs_u:
         assert errs_u[n] < 0.35 and errs_f[n] < 0.35, (n, errs_u[n], errs_f[n])
         assert errs_f[n] <= 1.5 * errs_u[n] + 0.02, (n, errs_u[n], errs_f[n])
+
+
+@pytest.mark.parametrize("cfg,c,k", [(11, 64, 64), (2, 128, 128), (8, 256, 256), (0, 128, 64)])
+def test_igemm_bnbwd_epilogue_matches_composite(gpu, cfg, c, k):
+    """3x3 stride-1 input gradient (det_igemm_conv_bnbwd) with the ReLU-masked gradient and the BN's
+    backward partial sums in its epilogue, per tile configuration, against an fp32 composite."""
+    import torch.nn.functional as F
+
+    nb, h, w_ = 3, 13, 11  # M = 429: a ragged last row block
+    g = torch.Generator(device="cpu").manual_seed(c + k + cfg)
+    dy = torch.randn(nb, k, h, w_, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(k, c, 3, 3, generator=g) / (9 * k) ** 0.5).to(torch.bfloat16)  # conv weight [Cout=k, Cin=c]
+    x = torch.randn(nb, c, h, w_, generator=g).to(torch.bfloat16)  # the BN input (pre-normalisation)
+    mean = torch.randn(c, generator=g) * 0.1
+    scale = torch.rand(c, generator=g) + 0.5
+    shift = torch.randn(c, generator=g) * 0.2
+    dxr = F.conv_transpose2d(dy.float(), wt.float(), padding=1).to(torch.bfloat16).float()
+    mask = (x.float() * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)) > 0
+    d_ref = torch.where(mask, dxr, torch.zeros_like(dxr))
+    cl = torch.channels_last
+    dyg = dy.to(gpu).contiguous(memory_format=cl)
+    wg = wt.to(gpu).contiguous(memory_format=cl)
+    xg = x.to(gpu).contiguous(memory_format=cl)
+    wd = conv.dgrad_weight(wg)
+    m = nb * h * w_
+    lib = _lib.get_lib()
+    rpb = int(lib.det_igemm_rows_per_block_cfg(c, cfg))
+    nrb = (m + rpb - 1) // rpb
+    psum = torch.empty(nrb, c, device=gpu)
+    psumx = torch.empty(nrb, c, device=gpu)
+    d = torch.empty(nb, c, h, w_, dtype=torch.bfloat16, device=gpu, memory_format=cl)
+    mg, sg, hg = mean.to(gpu), scale.to(gpu), shift.to(gpu)
+    _lib.check(lib.det_igemm_conv_bnbwd(
+        torch.cuda.current_stream().cuda_stream, dyg.data_ptr(), wd.data_ptr(), d.data_ptr(),
+        conv._zero_page(dyg.device).data_ptr(), m, c, k, h, w_, h, w_, 3, 3, 1, 1, xg.data_ptr(), mg.data_ptr(),
+        sg.data_ptr(), hg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), cfg), "igemm_conv_bnbwd")
+    torch.cuda.synchronize()
+    got = d.float().cpu()
+    torch.testing.assert_close(got, d_ref, rtol=2e-2, atol=2e-2)
+    g2 = got.permute(0, 2, 3, 1).reshape(m, c).double()
+    x2 = x.permute(0, 2, 3, 1).reshape(m, c).double()
+    torch.testing.assert_close(psum.double().sum(0).cpu(), g2.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(psumx.double().sum(0).cpu(), (g2 * (x2 - mean.double())).sum(0), rtol=1e-4, atol=1e-3)
