@@ -40,7 +40,7 @@ class StackedTrial(pytorch.PyTorchTrial):
         self.seen = []
 
     def build_training_data_loader(self):
-        self.train_ds = StackedRows(160)
+        self.train_ds = StackedRows(int(self.context.get_hparam("train_rows")))
         return pytorch.DataLoader(self.train_ds, batch_size=self.context.get_per_slot_batch_size(),
                                   collate_fn=pytorch.passthrough_collate)
 
@@ -78,11 +78,12 @@ def test_chunked_batches_respect_epochs_and_offsets():
             assert torch.equal(b[0], x) and torch.equal(b[1], y)
 
 
-def _run(monkeypatch, k, use_gpu=False, graph=False):
+def _run(monkeypatch, k, use_gpu=False, graph=False, rows=160):
     monkeypatch.setenv("DET_GRAPH_BATCHES", str(k))
     monkeypatch.setenv("DET_HIP_GRAPH", "1" if graph else "0")
     rec = Recorder().train(1, 13, 0).validate(1, 13).train(2, 9, 13).train(3, 11, 22).validate(3, 33)
-    ctrl, resp = run(StackedTrial, {"global_batch_size": 16}, rec, use_gpu=use_gpu, records_per_epoch=160)
+    ctrl, resp = run(StackedTrial, {"global_batch_size": 16, "train_rows": rows}, rec, use_gpu=use_gpu,
+                     records_per_epoch=rows)
     if use_gpu:
         torch.cuda.synchronize()
     params = torch.cat([p.detach().float().reshape(-1) for p in ctrl.context.models[0].parameters()]).cpu()
@@ -109,8 +110,11 @@ def test_chunked_training_matches_unchunked_on_cpu(monkeypatch):
 
 @pytest.mark.gpu
 def test_multibatch_graph_replay_matches_eager(gpu, monkeypatch):
-    _, p_e, l_e, v_e = _run(monkeypatch, 1, use_gpu=True, graph=False)
-    c, p_g, l_g, v_g = _run(monkeypatch, 4, use_gpu=True, graph=True)
+    # 30-batch epochs: train_batch reads epoch_idx (graphs are keyed per epoch) and only full
+    # 4-batch chunks are captured, after one per-batch warm-up of their key, so an epoch needs
+    # several full chunks to replay any (10-batch epochs have one full chunk after the first)
+    _, p_e, l_e, v_e = _run(monkeypatch, 1, use_gpu=True, graph=False, rows=480)
+    c, p_g, l_g, v_g = _run(monkeypatch, 4, use_gpu=True, graph=True, rows=480)
     assert c._graph is not None and c._graph.chunk_replays > 0, c._graph.stats() if c._graph else None
     assert c._eval_graph is not None and c._eval_graph.replays > 0
     assert len(l_g) == len(l_e)
