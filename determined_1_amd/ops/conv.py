@@ -6,6 +6,7 @@ multiples of 64 (every 1x1 conv of ResNet-50 qualifies); ``supported()`` says wh
 can take the HIP path.  On CPU tensors the functions compute the same result with torch ops
 (fp32 accumulate), which is what the unit tests compare against.
 """
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -295,20 +296,54 @@ def _bn_producer(x: torch.Tensor):
     return gf if isinstance(gf, _BNActTrain._backward_cls) else None
 
 
-def dgrad_1x1(dy2d: torch.Tensor, w2d: torch.Tensor) -> torch.Tensor:
+def dgrad_1x1(dy2d: torch.Tensor, w2d: torch.Tensor, abn=None) -> torch.Tensor:
     """dX[M, Cin] = dY[M, Cout] . W[Cout, Cin] for a 1x1 conv.  On the GPU with ``DGRAD_BT`` the GEMM
-    reads the weight as stored (transposed LDS reads), else through a transposed copy."""
+    reads the weight as stored (transposed LDS reads), else through a transposed copy.  ``abn`` =
+    (d, x, coef, out): dY is the deferred BN-backward apply of the consuming BN (see
+    ``take_pending_apply``), staged by the GEMM and written to ``out`` (the 2-D view of dY)."""
     if DGRAD_BT and is_gpu(dy2d) and w2d.dtype == torch.bfloat16 and w2d.is_contiguous():
         m, k = dy2d.shape
         n = w2d.shape[1]
         dx = torch.empty(m, n, dtype=torch.bfloat16, device=dy2d.device)
-        _lib.check(_lib.get_lib().det_conv_dgrad(_stream(dy2d), dy2d.data_ptr(), w2d.data_ptr(), dx.data_ptr(), int(m),
-                                                 int(n), int(k)), "conv_dgrad")
+        a_src, ax, acoef, aout = (dy2d, None, None, None) if abn is None else abn
+        _lib.check(_lib.get_lib().det_conv_dgrad(_stream(dy2d), a_src.data_ptr(), w2d.data_ptr(), dx.data_ptr(), int(m),
+                                                 int(n), int(k), _ptr(ax), _ptr(acoef), _ptr(aout)), "conv_dgrad")
         return dx
+    assert abn is None
     return conv1x1_nt(dy2d, w2d.t().contiguous())[0]
 
 
-def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int) -> Optional[torch.Tensor]:
+# Deferred BatchNorm-backward apply (``DEFER_BN_APPLY``): a fused training BN whose input is the
+# output of a native 1x1 conv (ResNet bn3 <- conv3) runs only its finalize and hands (d, x, coef) to
+# that conv's backward, whose input-gradient GEMM computes dY = A d + B x + C while staging its A
+# operand and writes it for the weight gradient: the apply pass and the GEMM's read of dY become one.
+DEFER_BN_APPLY = os.environ.get("DET_DEFER_BN_APPLY", "1") != "0"
+BN_APPLY_COUNTS = {"deferred": 0, "in_gemm": 0, "materialized": 0}
+
+
+def take_pending_apply(ctx, dy: torch.Tensor):
+    """(d, x, coef) of a BN backward deferred onto this conv node, checked against the gradient
+    buffer ``dy`` it returned (None if nothing is pending)."""
+    pend = getattr(ctx, "pending_bn_apply", None)
+    ctx.pending_bn_apply = None
+    if pend is None:
+        return None
+    buf, d, x, coef = pend
+    if buf.data_ptr() != dy.data_ptr() or dy.shape != buf.shape:
+        raise RuntimeError("deferred BN-backward apply: the gradient reached the conv in a different buffer")
+    return d, x, coef
+
+
+def materialize_pending_apply(dy: torch.Tensor, pend) -> None:
+    d, x, coef = pend
+    m = d.numel() // d.shape[1]
+    _lib.check(_lib.get_lib().det_bn_bwd_apply_coef(_stream(d), 1 if d.dtype == torch.bfloat16 else 0, d.data_ptr(),
+                                                    x.data_ptr(), int(m), int(d.shape[1]), coef.data_ptr(),
+                                                    dy.data_ptr()), "bn_bwd_apply_coef")
+    BN_APPLY_COUNTS["materialized"] += 1
+
+
+def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int, abn=None) -> Optional[torch.Tensor]:
     """dgrad with the producer BN's backward partials in the epilogue, or None when the producer
     cannot take it (no ReLU, the shortcut gradient not in yet, already fused, layout/dtype)."""
     mode = getattr(prod, "mask_mode", 0)
@@ -331,11 +366,14 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int)
     psum = torch.empty(nrb, c, dtype=torch.float32, device=dy2d.device)
     psumx = torch.empty(nrb, c, dtype=torch.float32, device=dy2d.device)
     d = torch.empty(m, c, dtype=torch.bfloat16, device=dy2d.device)
+    if abn is not None and not DGRAD_BT:
+        return None
     wb = w2d if DGRAD_BT else w2d.t().contiguous()  # [Cout, Cin] as stored, or the transposed copy
+    a_src, ax, acoef, aout = (dy2d, None, None, None) if abn is None else abn
     _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
-        _stream(dy2d), dy2d.data_ptr(), wb.data_ptr(), d.data_ptr(), int(m), int(c), int(w2d.shape[0]), xb.data_ptr(),
+        _stream(dy2d), a_src.data_ptr(), wb.data_ptr(), d.data_ptr(), int(m), int(c), int(w2d.shape[0]), xb.data_ptr(),
         stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits), _ptr(add), psum.data_ptr(),
-        psumx.data_ptr(), int(mode), 1 if DGRAD_BT else 0), "conv_nt_bnbwd")
+        psumx.data_ptr(), int(mode), 1 if DGRAD_BT else 0, _ptr(ax), _ptr(acoef), _ptr(aout)), "conv_nt_bnbwd")
     prod.fused_bwd = (psum, psumx, rpb)
     if expects:
         prod.extra_dy = None  # consumed: summed into d
@@ -392,6 +430,12 @@ class _Conv1x1(torch.autograd.Function):
         _attach_partials(y, parts)
         ctx.save_for_backward(x, weight)
         ctx.bn_producer = bn_producer
+        # a consuming fused BN may defer its backward apply onto this node (take_pending_apply):
+        # expansion convs only (ResNet conv3, Cout = 4 Cin), whose dgrad reads each staged A element
+        # once; a reducing conv (conv1, Cout = Cin / 4) re-stages A per N tile and measured slower
+        # than the separate apply (profiles/r3_bench_resnet50_defer_bn_apply_ab.jsonl)
+        ctx.accepts_bn_apply = is_gpu(x) and DGRAD_BT and cout >= 2 * c
+        ctx.pending_bn_apply = None
         return y
 
     @staticmethod
@@ -399,19 +443,30 @@ class _Conv1x1(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         n, c, h, w_ = x.shape
         cout = weight.shape[0]
+        pend = take_pending_apply(ctx, dy)
+        if pend is not None and not (ctx.needs_input_grad[0] and dy.dtype == torch.bfloat16
+                                     and dy.is_contiguous(memory_format=torch.channels_last)):
+            materialize_pending_apply(dy, pend)
+            pend = None
         dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)
         dx = dw = None
         prod, ctx.bn_producer = ctx.bn_producer, None
+        abn = None
+        if pend is not None:  # dY = the deferred BN apply, computed in the dgrad's A staging into dy2
+            d, bx, coef = pend
+            abn = (d.permute(0, 2, 3, 1).reshape(-1, cout), bx, coef, dy2)
         if ctx.needs_input_grad[0]:
             w2 = weight.reshape(cout, c).to(torch.bfloat16).contiguous()
-            dx2 = _fused_bn_dgrad(prod, dy2, w2, n * h * w_, c) if (prod is not None and is_gpu(dy2)) else None
+            dx2 = _fused_bn_dgrad(prod, dy2, w2, n * h * w_, c, abn) if (prod is not None and is_gpu(dy2)) else None
             if dx2 is None:
-                dx2 = dgrad_1x1(dy2, w2)
+                dx2 = dgrad_1x1(dy2, w2, abn)
                 if prod is not None:
                     BN_BWD_COUNTS["unfused"] += 1
             else:
                 BN_BWD_COUNTS["fused"] += 1
+            if abn is not None:
+                BN_APPLY_COUNTS["in_gemm"] += 1
             dx = dx2.view(n, h, w_, c).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             from determined_1_amd.ops.arena import landing_buffer

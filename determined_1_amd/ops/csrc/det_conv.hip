@@ -175,6 +175,14 @@ struct NtArgs {
   float* pm2;
   Gather g;  // STRIDE2
   BnBwdEpi bn;  // BNB
+  // ABN (input gradient of the conv that produced a training BatchNorm's input): the A operand is
+  // the BN backward's apply, dY = coef[0][k] * A + coef[1][k] * A2 + coef[2][k] (A = the BN's
+  // masked output gradient, A2 = the BN input), computed while staging; the blocks of the first
+  // N tile also write it to Aout (the weight gradient's operand) -- the separate apply pass
+  // (read A, A2, write dY) and this GEMM's read of dY become one pass.
+  const unsigned short* A2;
+  const float* acoef;  // [3][K]
+  unsigned short* Aout;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -186,7 +194,8 @@ struct NtArgs {
 // BT: B is given as [K, N] (N contiguous: the conv weight [Cout, Cin] itself for an input gradient),
 // staged as it sits ([64 k][BN] image, the wgrad swizzle) and read with ds_read_b64_tr_b16 -- no
 // transposed weight copy per call.
-template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false, bool BT = false>
+template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false, bool BT = false,
+          bool ABN = false>
 __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
@@ -206,6 +215,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   const int n0 = nt * BN;
   const int kc = tid & 7, r0 = tid >> 3;
   const int64_t K = a.K;
+  const bool first_ntile = nt == 0;  // ABN: these blocks write the staged A operand out
 
   const unsigned short* aptr[ACH];
   bool aval[ACH];
@@ -225,7 +235,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   const unsigned short* bptr = a.B + static_cast<int64_t>(n0 + r0) * K + kc * 8;
   constexpr int BCPR = BN / 8;  // BT: 16-B chunks per B image row
 
-  us8 ra[ACH], rb[BCH];
+  us8 ra[ACH], rb[BCH], ra2[ABN ? ACH : 1];
   auto gload = [&](int kt) {
     const int64_t k = static_cast<int64_t>(kt) * kBK;
 #pragma unroll
@@ -233,6 +243,10 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       if (GM == kGmStem) ra[i] = a.g.stem_chunk(aptr[i], aval[i], ih0[i], iw0[i], kt * 8 + kc);
       else if (aval[i]) ra[i] = *reinterpret_cast<const us8*>(aptr[i] + k);
       else ra[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (ABN) {
+        if (aval[i]) ra2[i] = *reinterpret_cast<const us8*>(a.A2 + (aptr[i] - a.A) + k);
+        else ra2[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
 #pragma unroll
     for (int j = 0; j < BCH; ++j) {
@@ -246,12 +260,34 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   };
   auto lstore = [&](int buf, int kt) {
     unsigned char* base = smem + buf * BUF;
+    // ABN: this thread's 8 channels of the apply coefficients, loaded once per K tile (before the
+    // Aout stores, which the compiler could not move them across)
+    float ca[8], cb[8], cc[8];
+    if constexpr (ABN) {
+      const int k0 = kt * kBK + kc * 8;
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        const float4 A0 = *reinterpret_cast<const float4*>(a.acoef + k0 + j);
+        const float4 B0 = *reinterpret_cast<const float4*>(a.acoef + a.K + k0 + j);
+        const float4 C0 = *reinterpret_cast<const float4*>(a.acoef + 2 * a.K + k0 + j);
+        ca[j] = A0.x; ca[j + 1] = A0.y; ca[j + 2] = A0.z; ca[j + 3] = A0.w;
+        cb[j] = B0.x; cb[j + 1] = B0.y; cb[j + 2] = B0.z; cb[j + 3] = B0.w;
+        cc[j] = C0.x; cc[j + 1] = C0.y; cc[j + 2] = C0.z; cc[j + 3] = C0.w;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       us8 v = ra[i];
       if (PRO) {
         v = affine_relu8(v, a.scale, a.shift, kt * kBK + kc * 8);
         if (!aval[i]) v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+      if constexpr (ABN) {
+        // exactly det_norm.hip bn_apply_bwd<MASK 0>: fma(A, d, fma(B, x, C)) in fp32, one rounding
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = f2bf(__fmaf_rn(ca[j], bf2f(ra[i][j]), __fmaf_rn(cb[j], bf2f(ra2[i][j]), cc[j])));
+        if (!aval[i]) v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+        else if (first_ntile) *reinterpret_cast<us8*>(a.Aout + (aptr[i] - a.A) + static_cast<int64_t>(kt) * kBK) = v;
       }
       *reinterpret_cast<us8*>(base + swz(r0 + 32 * i, kc)) = v;
     }
@@ -686,9 +722,14 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int smem = nt_smem<BM, BN, OCC == 2 ? 2 : 1>();
+  const bool abn = a.A2 != nullptr;
+  if (abn && (!bt || pro || stats || stride2)) return -2;  // the A-apply prologue: input gradients only
   if (bnb) {  // input-gradient GEMM with the BN-backward epilogue (no prologue / stats / gather)
     constexpr int smem_b = smem > BM * (BN + 16) * 2 + kThreads * 16 * 4 ? smem : BM * (BN + 16) * 2 + kThreads * 16 * 4;
-    if (bt)
+    if (abn)
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true, true>),
+                         dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
+    else if (bt)
       hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true>),
                          dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
     else
@@ -697,8 +738,12 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
     return static_cast<int>(hipGetLastError());
   }
   if (bt) {  // plain input-gradient GEMM against the untransposed weight
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true>),
-                       dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+    if (abn)
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true, true>),
+                         dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true>),
+                         dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
     return static_cast<int>(hipGetLastError());
   }
 #define DET_NT(P, S, G)                                                                               \
@@ -758,10 +803,15 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
 
 // dX[M, N] = dY[M, K] . W[K, N]: the input gradient of a 1x1 conv against its weight W = [Cout, Cin]
 // as stored (no transposed copy).  bf16, N % 64 == 0, K % 64 == 0.
-int det_conv_dgrad(void* stream, const void* dY, const void* W, void* dX, int64_t M, int N, int K) {
+// abn_x (nullable): with abn_coef [3][K] and abn_out, dY is the BN backward's apply of A = dY (the
+// BN's masked gradient) and abn_x (the BN input), computed in the A staging and written to abn_out.
+int det_conv_dgrad(void* stream, const void* dY, const void* W, void* dX, int64_t M, int N, int K, const void* abn_x,
+                   const float* abn_coef, void* abn_out) {
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
+  if (abn_x && (!abn_coef || !abn_out)) return -2;
   NtArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(dX),
-           M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}};
+           M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}, BnBwdEpi{},
+           static_cast<const unsigned short*>(abn_x), abn_coef, static_cast<unsigned short*>(abn_out)};
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (K == kBK) {
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, false, true);
@@ -777,13 +827,16 @@ int det_conv_dgrad(void* stream, const void* dY, const void* W, void* dX, int64_
 // b_kn: B is the untransposed weight [K, N] (the gemm reads it with transposed LDS reads).
 int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
                       const float* mean, const float* scale, const float* shift, const void* mbits, const void* add,
-                      float* psum, float* psumx, int mode, int b_kn) {
+                      float* psum, float* psumx, int mode, int b_kn, const void* abn_x, const float* abn_coef,
+                      void* abn_out) {
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
   if (!x || !mean || !psum || !psumx || (mode == 1 && (!scale || !shift)) || (mode == 2 && !mbits) || mode < 1 || mode > 2)
     return -2;
   NtArgs a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C),
            M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}, BnBwdEpi{static_cast<const unsigned short*>(x), mean, scale,
-           shift, static_cast<const uint8_t*>(mbits), static_cast<const unsigned short*>(add), psum, psumx, mode}};
+           shift, static_cast<const uint8_t*>(mbits), static_cast<const unsigned short*>(add), psum, psumx, mode},
+           static_cast<const unsigned short*>(abn_x), abn_coef, static_cast<unsigned short*>(abn_out)};
+  if (abn_x && (!abn_coef || !abn_out)) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool bt = b_kn != 0;
   if (K == kBK) {

@@ -1022,6 +1022,44 @@ int det_bn_bwd_from_partials(void* stream, int dtype, const void* d, const void*
   return static_cast<int>(hipGetLastError());
 }
 
+// det_bn_bwd_from_partials split in two for a consumer that applies the BN backward itself (the
+// input-gradient GEMM of the conv that produced x stages dx = A d + B x + C as its A operand,
+// det_conv.hip ABN): the finalize only (dgamma, dbeta, coef [3][C]) ...
+int det_bn_bwd_finalize_partials(void* stream, int64_t M, int C, const float* gamma, const float* save_mean,
+                                 const float* save_rstd, const float* psum, const float* psumx, int nrb, int64_t rpb,
+                                 float* dgamma, float* dbeta, float* coef, float* scratch) {
+  if (C % 8 != 0 || M <= 0 || nrb <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Geom g = make_geom(M, C);
+  g.nrb = nrb;
+  g.rpb = rpb;
+  BwdFin bf{gamma, save_rstd, save_mean, dgamma, dbeta, coef};
+  launch_bwd_finalize(st, psum, psumx, g, bf, scratch);
+  return static_cast<int>(hipGetLastError());
+}
+
+// ... and the unmasked apply alone, dx = A d + B x + C (the fallback when that consumer cannot).
+int det_bn_bwd_apply_coef(void* stream, int dtype, const void* d, const void* x, int64_t M, int C, const float* coef,
+                          void* dx) {
+  if (C % 8 != 0 || M <= 0) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t nvec = M * C / 8;
+  const int grid2 = apply_grid(nvec, 2);
+  if (dtype == 1)
+    hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false>), dim3(grid2), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(d), static_cast<const unsigned short*>(nullptr),
+                       static_cast<const unsigned short*>(x), static_cast<const uint8_t*>(nullptr), coef,
+                       static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
+                       static_cast<unsigned short*>(dx), static_cast<unsigned short*>(nullptr), nvec, C);
+  else
+    hipLaunchKernelGGL((bn_apply_bwd<float, 0, false>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
+                       static_cast<const float*>(nullptr), static_cast<const float*>(x),
+                       static_cast<const uint8_t*>(nullptr), coef, static_cast<const float*>(nullptr),
+                       static_cast<const float*>(nullptr), static_cast<float*>(dx), static_cast<float*>(nullptr), nvec, C);
+  return static_cast<int>(hipGetLastError());
+}
+
 int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const void* x, const void* mbits, int64_t M, int C,
                int mask_mode, const float* gamma, const float* save_mean, const float* save_rstd,
                const float* scale, const float* shift, void* dx, void* dres, float* dgamma, float* dbeta,

@@ -18,6 +18,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from determined_1_amd.ops import _lib
+from determined_1_amd.ops import conv as _conv
 
 FALLBACKS = {"count": 0}
 SHORTCUT_LINK = True  # identity-shortcut gradients through the producer's BN backward (A/B switch)
@@ -143,6 +144,24 @@ class _BNActTrain(torch.autograd.Function):
             psum, psumx, rpb = fused
             # [3][C] apply coefficients, then the sliced finalize's scratch
             coef = torch.empty(3 * C + int(lib.det_bn_bwd_scratch_elems(C)), dtype=torch.float32, device=x.device)
+            conv_node = x.grad_fn
+            if (_conv.DEFER_BN_APPLY and getattr(conv_node, "accepts_bn_apply", False)
+                    and getattr(conv_node, "pending_bn_apply", "x") is None and x.dtype == torch.bfloat16
+                    and ctx.fmt == torch.channels_last and dy.is_contiguous(memory_format=torch.channels_last)):
+                # x came from a native 1x1 conv whose input-gradient GEMM computes dx = A d + B x + C
+                # while staging its A operand (ops/conv.py take_pending_apply): finalize only here
+                _lib.check(
+                    lib.det_bn_bwd_finalize_partials(
+                        _stream(x), M, C, _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), psum.data_ptr(),
+                        psumx.data_ptr(), int(psum.shape[0]), int(rpb), None if dgb is None else dgb[0].data_ptr(),
+                        None if dgb is None else dgb[1].data_ptr(), coef.data_ptr(), coef[3 * C:].data_ptr()),
+                    "bn_bwd_finalize_partials",
+                )
+                conv_node.pending_bn_apply = (dx, dy, x, coef)
+                _conv.BN_APPLY_COUNTS["deferred"] += 1
+                dres = dy if want_res else None
+                fused = "deferred"
+        if fused is not None and fused != "deferred":
             _lib.check(
                 lib.det_bn_bwd_from_partials(
                     _stream(x), _DT[x.dtype], dy.data_ptr(), x.data_ptr(), M, C, _ptr(weight), stats[0].data_ptr(),
@@ -152,7 +171,7 @@ class _BNActTrain(torch.autograd.Function):
                 "bn_bwd_from_partials",
             )
             dres = dy if want_res else None
-        else:
+        elif fused is None:
             dres = torch.empty_like(x, memory_format=ctx.fmt) if want_res else None
             ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
             _lib.check(

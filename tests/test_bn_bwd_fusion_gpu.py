@@ -45,7 +45,8 @@ def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k, b_kn):
     _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
         torch.cuda.current_stream().cuda_stream, dyg.data_ptr(), wg.data_ptr(), d.data_ptr(), m, c, k,
         xg.data_ptr(), meang.data_ptr(), scg.data_ptr(), shg.data_ptr(), None if bitsg is None else bitsg.data_ptr(),
-        None if addg is None else addg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), mode, b_kn), "bnbwd")
+        None if addg is None else addg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), mode, b_kn, None, None, None),
+        "bnbwd")
     torch.cuda.synchronize()
     got = d.float().cpu()
     # one bf16 rounding of the accumulated product may differ by an ulp from torch's rounding
@@ -105,11 +106,18 @@ def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
         return zz.grad.float().clone(), {n: p.grad.float().clone() for n, p in mods.named_parameters()}
 
     before = dict(conv.BN_BWD_COUNTS)
+    before_apply = dict(conv.BN_APPLY_COUNTS)
     dz_u, gr_u = run(False)
     dz_f, gr_f = run(True)
     conv.FUSE_BN_BWD = True
     # bn2->conv3 x2, bn1->conv2 (3x3 dgrad epilogue) x2, b0 output->b1.conv1 (mode 2)
     assert conv.BN_BWD_COUNTS["fused"] - before["fused"] >= 5
+    # deferred BN applies computed in the conv dgrad's A staging: b0.bn3 -> b0.conv3 (the expansion
+    # conv; b1.bn3 has no fused dgrad downstream here)
+    assert conv.BN_APPLY_COUNTS["in_gemm"] - before_apply["in_gemm"] >= 1
+    assert conv.BN_APPLY_COUNTS["deferred"] - before_apply["deferred"] == \
+        conv.BN_APPLY_COUNTS["in_gemm"] - before_apply["in_gemm"] + conv.BN_APPLY_COUNTS["materialized"] - \
+        before_apply["materialized"]
 
     # fp32 reference with the same (bf16-valued) weights
     w = {n: p.detach().float().clone().requires_grad_(True) for n, p in mods.named_parameters()}
@@ -174,3 +182,24 @@ def test_igemm_bnbwd_epilogue_matches_composite(gpu, cfg, c, k):
     x2 = x.permute(0, 2, 3, 1).reshape(m, c).double()
     torch.testing.assert_close(psum.double().sum(0).cpu(), g2.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(psumx.double().sum(0).cpu(), (g2 * (x2 - mean.double())).sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("m,c,k", [(1000, 64, 256), (777, 128, 512), (4096, 256, 64)])
+def test_dgrad_with_bn_apply_prologue(gpu, m, c, k):
+    """det_conv_dgrad with the deferred BN-backward apply in its A staging (ABN): the staged operand
+    written out equals the standalone apply kernel bitwise, and dX equals dgrad(apply) ."""
+    lib = _lib.get_lib()
+    g = torch.Generator(device="cpu").manual_seed(m + c)
+    d = torch.randn(m, k, generator=g).to(torch.bfloat16).to(gpu)
+    x = torch.randn(m, k, generator=g).to(torch.bfloat16).to(gpu)
+    coef = torch.cat([torch.rand(k, generator=g) + 0.5, torch.randn(k, generator=g) * 0.1,
+                      torch.randn(k, generator=g) * 0.1]).to(gpu)
+    w = (torch.randn(k, c, generator=g) / k ** 0.5).to(torch.bfloat16).to(gpu)  # conv weight [Cout=k, Cin=c]
+    ref_dy = torch.empty(m, k, dtype=torch.bfloat16, device=gpu)
+    _lib.check(lib.det_bn_bwd_apply_coef(torch.cuda.current_stream().cuda_stream, 1, d.data_ptr(), x.data_ptr(), m, k,
+                                         coef.data_ptr(), ref_dy.data_ptr()), "apply_coef")
+    out = torch.full((m, k), float("nan"), dtype=torch.bfloat16, device=gpu)
+    dx = conv.dgrad_1x1(d, w, (d, x, coef, out))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref_dy)
+    torch.testing.assert_close(dx.float(), (ref_dy.float() @ w.float()).to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2)
