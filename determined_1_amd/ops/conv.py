@@ -261,6 +261,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, r: int, s: 
 COUNTS = {"native": 0, "fallback": 0}
 ENABLED = True  # A/B switch (models.resnet.NATIVE_CONV1X1 toggles it)
 DGRAD_BT = True  # 1x1 input gradients read the weight untransposed (no per-call transpose copy)
+# 1x1 forward shapes (Cin, Cout) -> det_igemm tile configuration where the LDS-DMA implicit GEMM
+# beat the register-staged gemm_nt by >= 7 % at ResNet-50 / batch 512 (profiles/r3_igemm_cfgs_1x1.jsonl:
+# 0.063 vs 0.084 ms at 2048->512, 0.123 vs 0.136 at 256->1024, ...); the rest stay on gemm_nt.
+IGEMM_FWD_1X1 = {(256, 1024): 8, (2048, 512): 8, (1024, 512): 8, (512, 256): 8, (1024, 256): 8}
 
 
 def _attach_partials(y: torch.Tensor, parts: Optional[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:
@@ -425,8 +429,13 @@ class _Conv1x1(torch.autograd.Function):
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # channels_last: a free view
         w2 = weight.reshape(cout, c)
         wb = w2 if w2.dtype == torch.bfloat16 else w2.to(torch.bfloat16)
-        y2, parts = conv1x1_nt(x2, wb.contiguous(), stats=stats)
-        y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
+        cfg = IGEMM_FWD_1X1.get((c, cout)) if is_gpu(x) else None
+        if cfg is not None and x.data_ptr() % 16 == 0:
+            # LDS-DMA implicit GEMM (same BN-statistics epilogue, 256-row partial blocks)
+            y, parts = igemm_conv(x, weight, stats=stats, w_krsc=wb.contiguous(), cfg=cfg)
+        else:
+            y2, parts = conv1x1_nt(x2, wb.contiguous(), stats=stats)
+            y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
         _attach_partials(y, parts)
         ctx.save_for_backward(x, weight)
         ctx.bn_producer = bn_producer
