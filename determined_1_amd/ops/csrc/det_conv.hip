@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "det_stats.h"
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -204,7 +206,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   static_assert(WM * WN == 4, "4 waves");
   static_assert(FM >= 1 && FN >= 1 && ACH >= 1 && BCH >= 1, "tile");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ float red[WM][BN];
+  __shared__ float red[WM * BN * 3];  // STATS: per (wave row, column) mean, M2, count
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -352,61 +354,10 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
   if (STATS) {
-    float cs[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          if (row < nvalid) s += round_bf(acc[i][j][r]);
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      cs[j] = s;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm][wn * TN + j * 16 + lane] = cs[j];
-    }
-    __syncthreads();
-    const float inv_n = 1.f / static_cast<float>(nvalid);
-    float mu[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = wn * TN + j * 16 + (lane & 15);
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w][col];
-      mu[j] = s * inv_n;
-    }
-    __syncthreads();  // every lane has read red[] before it is reused for M2
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          const float d = round_bf(acc[i][j][r]) - mu[j];
-          if (row < nvalid) q += d * d;
-        }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16) red[wm][wn * TN + j * 16 + lane] = q;
-      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
-    }
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   }
   __syncthreads();
-  if (STATS && tid < BN) {
-    float q = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) q += red[w][tid];
-    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
-  }
   constexpr int CPR = BN / 8;  // 16-B chunks per output row
   if constexpr (BNB) {
     // each thread owns one 8-column chunk (kThreads % CPR == 0) over rows tid/CPR + q*kThreads/CPR

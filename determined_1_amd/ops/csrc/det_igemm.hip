@@ -40,6 +40,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "det_stats.h"
+
 namespace {
 
 constexpr int kBK = 64;       // K tile: one 128-B LDS row per operand row
@@ -307,63 +309,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
   if (STATS) {
-    // per-lane (mean, M2) over its rows of each column, Chan-merged across the 4 row groups of the
-    // wave by shuffles and across the WM waves through LDS
-    float cs[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          if (row < nvalid) s += round_bf(acc[i][j][r]);
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      cs[j] = s;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + j * 16 + lane] = cs[j];
-    }
-    __syncthreads();
-    const float inv_n = 1.f / static_cast<float>(nvalid);
-    float mu[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = wn * TN + j * 16 + (lane & 15);
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w * BN + col];
-      mu[j] = s * inv_n;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          const float d = round_bf(acc[i][j][r]) - mu[j];
-          if (row < nvalid) q += d * d;
-        }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16) red[wm * BN + wn * TN + j * 16 + lane] = q;
-      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
-    }
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   }
   __syncthreads();
-  if (STATS && tid < BN) {
-    float q = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
-    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
-  }
   constexpr int CPR = BN / 8;
 #pragma unroll
   for (int q = 0; q < BM * CPR / kThreads; ++q) {
@@ -401,7 +350,7 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
   constexpr int NI = AI + BI;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int LDC = BN + 16;
-  static_assert(BM * LDC * 2 + 4 * WM * BN <= NS * STAGE, "C tile + stats scratch fit in the ring");
+  static_assert(BM * LDC * 2 + 12 * WM * BN <= NS * STAGE, "C tile + stats scratch fit in the ring");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);  // [WM][BN], after the C tile
 
@@ -542,61 +491,10 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
   if (STATS) {
-    float cs[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          if (row < nvalid) s += round_bf(acc[i][j][r]);
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      cs[j] = s;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + j * 16 + lane] = cs[j];
-    }
-    __syncthreads();
-    const float inv_n = 1.f / static_cast<float>(nvalid);
-    float mu[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = wn * TN + j * 16 + (lane & 15);
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) s += red[w * BN + col];
-      mu[j] = s * inv_n;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          const float d = round_bf(acc[i][j][r]) - mu[j];
-          if (row < nvalid) q += d * d;
-        }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16) red[wm * BN + wn * TN + j * 16 + lane] = q;
-      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
-    }
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   }
   __syncthreads();
-  if (STATS && tid < BN) {
-    float q = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
-    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
-  }
   if constexpr (BNB) {
     bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
     return;
@@ -802,61 +700,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
   if (STATS) {
-    float cs[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float sm = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          if (row < nvalid) sm += round_bf(acc[i][j][r]);
-        }
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
-      cs[j] = sm;
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) red[wm * BN + wn * TN + j * 16 + lane] = cs[j];
-    }
-    __syncthreads();
-    const float inv_n = 1.f / static_cast<float>(nvalid);
-    float mu[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = wn * TN + j * 16 + (lane & 15);
-      float sm = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) sm += red[w * BN + col];
-      mu[j] = sm * inv_n;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-          const float d = round_bf(acc[i][j][r]) - mu[j];
-          if (row < nvalid) q += d * d;
-        }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16) red[wm * BN + wn * TN + j * 16 + lane] = q;
-      if (lane < 16 && wm == 0) a.pmean[static_cast<int64_t>(mt) * a.N + n0 + wn * TN + j * 16 + lane] = mu[j];
-    }
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   }
   __syncthreads();
-  if (STATS && tid < BN) {
-    float q = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) q += red[w * BN + tid];
-    a.pm2[static_cast<int64_t>(mt) * a.N + n0 + tid] = q;
-  }
   if constexpr (BNB) {
     bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
     return;
@@ -878,7 +725,7 @@ int launch3(hipStream_t st, const IgArgs& a, bool stats, bool bnb = false) {
   if (a.N % BN != 0 || a.Cin % 32 != 0) return -6;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
-  constexpr int ring = NS * (BM + BN) * 64, ctile = BM * (BN + 16) * 2 + 4 * WM * BN;
+  constexpr int ring = NS * (BM + BN) * 64, ctile = BM * (BN + 16) * 2 + 12 * WM * BN;
   constexpr int smem = ring > ctile ? ring : ctile;
   static_assert(smem <= 163840, "LDS");
   static_assert(BM * (BN + 16) * 2 >= kThreads * 16 * 4, "BN-backward scratch fits in the C tile");
@@ -917,7 +764,7 @@ int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
   constexpr int kThreads = WM * WN * 64;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
-  constexpr int smem = kStages * (BM + BN) * 128 + 4 * WM * BN;
+  constexpr int smem = kStages * (BM + BN) * 128 + 12 * WM * BN;
 #define DET_IG(D, S) \
   hipLaunchKernelGGL((igemm_kernel<BM, BN, WM, WN, D, S>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a)
   if (dense) { if (stats) DET_IG(true, true); else DET_IG(true, false); }
