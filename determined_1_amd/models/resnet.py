@@ -45,6 +45,7 @@ def c3x3(x: torch.Tensor, conv: nn.Conv2d, bn_exclusive: bool = False) -> torch.
 def c1x1(x: torch.Tensor, conv: nn.Conv2d, bn_exclusive: bool = False) -> torch.Tensor:
     if NATIVE_CONV1X1 and FUSED_BN:
         return native_conv.conv1x1(x, conv, bn_exclusive=bn_exclusive)
+    native_conv.materialize_fwd_apply(x)  # a deferred bn3 apply of the previous block
     return conv(x)
 
 
@@ -120,6 +121,9 @@ class Bottleneck(nn.Module):
         self.bn3 = bn(planes * self.expansion, relu=True)  # relu(bn3(conv3) + identity), fused
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
+        # set by ResNet when the next block is an identity-shortcut Bottleneck, whose conv1 is the
+        # first reader of this block's output and stages bn3's apply itself (ops.conv DEFER_FWD_APPLY)
+        self.defer_out = False
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
@@ -128,7 +132,8 @@ class Bottleneck(nn.Module):
         out = self.bn1(c1x1(x, self.conv1, bn_exclusive=FUSED_BN and _shortcut_linked(self.downsample, x)))
         out = bn_relu_c1x1(c3x3(out, self.conv2, bn_exclusive=True), self.bn2, self.conv3)  # bn1 feeds only conv2
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
-        return self.bn3(out, idt, shortcut_link=self.downsample is None)
+        return self.bn3(out, idt, shortcut_link=self.downsample is None,
+                        defer_apply=self.defer_out and NATIVE_CONV1X1 and FUSED_BN)
 
 
 class ResNet(nn.Module):
@@ -169,6 +174,9 @@ class ResNet(nn.Module):
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
             layers.append(block(self.inplanes, planes))
+        for blk, nxt in zip(layers[:-1], layers[1:]):  # identity-shortcut successor: conv1 reads first
+            if isinstance(blk, Bottleneck) and isinstance(nxt, Bottleneck) and nxt.downsample is None:
+                blk.defer_out = True
         return nn.Sequential(*layers)
 
     def _stem(self, x: torch.Tensor) -> torch.Tensor:

@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -91,6 +91,7 @@ _SIGNATURES = {
     "det_bn_bwd_scratch_elems": ([c_int], c_i64),
     "det_bn_bwd_finalize_partials": ([c_void_p, c_i64, c_int] + [c_void_p] * 5 + [c_int, c_i64] + [c_void_p] * 4, c_int),
     "det_bn_bwd_apply_coef": ([c_void_p, c_int, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
+    "det_bn_apply_res_mbits": ([c_void_p] * 3 + [c_void_p, c_i64, c_int] + [c_void_p] * 3, c_int),
     "det_bn_ws_elems": ([c_i64, c_int], c_i64),
     "det_bn_fin_ws_elems": ([c_int], c_i64),
     # stream, dtype, x, res, y, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
@@ -140,7 +141,7 @@ _SIGNATURES = {
     # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
     "det_conv_nt_rows_per_block": ([c_int], c_int),
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
-    "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4, c_int),
+    "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 3, c_int),
     "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),
     # stream, A, B, C, M, N, K, x, mean, scale, shift, mbits, add, psum, psumx, mode
     "det_conv_nt_bnbwd": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 8 + [c_int, c_int] + [c_void_p] * 3, c_int),

@@ -53,7 +53,8 @@ def _affine_relu_ref(x: torch.Tensor, scale: Optional[torch.Tensor], shift: Opti
 
 def conv1x1_nt(a2d: torch.Tensor, b2d: torch.Tensor, m: Optional[int] = None, scale: Optional[torch.Tensor] = None,
                shift: Optional[torch.Tensor] = None, stats: bool = False, gather: Optional[Gather] = None,
-               out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
+               out: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None, aout: Optional[torch.Tensor] = None,
+               abits: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
     """``C = op(A) . B^T`` with ``op(A) = relu(A*scale+shift)`` when scale/shift are given.
 
     Returns ``(C [M, N] bf16, partials)`` where partials is ``(pmean, pm2, rows_per_block)`` of the
@@ -93,7 +94,8 @@ def conv1x1_nt(a2d: torch.Tensor, b2d: torch.Tensor, m: Optional[int] = None, sc
         parts = (pm, pq, rpb)
     g = gather or (0, 0, 0, 0)
     _lib.check(_lib.get_lib().det_conv_nt(_stream(a2d), a2d.data_ptr(), b2d.data_ptr(), c.data_ptr(), int(m), int(n),
-                                          int(k), _ptr(scale), _ptr(shift), _ptr(pm), _ptr(pq), *[int(v) for v in g]),
+                                          int(k), _ptr(scale), _ptr(shift), _ptr(pm), _ptr(pq), *[int(v) for v in g],
+                                          _ptr(res), _ptr(aout), _ptr(abits)),
                "conv_nt")
     return c, parts
 
@@ -347,6 +349,30 @@ def materialize_pending_apply(dy: torch.Tensor, pend) -> None:
     BN_APPLY_COUNTS["materialized"] += 1
 
 
+# Deferred BatchNorm forward apply (``DEFER_FWD_APPLY``): a fused training BN(+residual)+ReLU whose
+# output's first consumer is a native 1x1 conv (ResNet bn3 -> the next identity block's conv1;
+# ``models.resnet`` marks those blocks) runs only its finalize and returns its output buffer
+# unwritten, tagged ``_det_fwd_apply = (x, residual, scale, shift, mbits)``; the conv's forward GEMM
+# computes relu(x*scale + shift + residual) while staging its A operand and writes it and its mask
+# bits into the tagged buffers (det_conv.hip AFWD).  Any other first consumer materialises it.
+DEFER_FWD_APPLY = os.environ.get("DET_DEFER_FWD_APPLY", "1") != "0"
+FWD_APPLY_COUNTS = {"deferred": 0, "in_gemm": 0, "materialized": 0}
+
+
+def materialize_fwd_apply(t: Optional[torch.Tensor]) -> None:
+    """Write a deferred BN forward apply into ``t`` (no-op for untagged tensors)."""
+    pend = getattr(t, "_det_fwd_apply", None) if t is not None else None
+    if pend is None:
+        return
+    t._det_fwd_apply = None
+    x, res, scale, shift, mbits = pend
+    m = x.numel() // x.shape[1]
+    _lib.check(_lib.get_lib().det_bn_apply_res_mbits(_stream(x), x.data_ptr(), res.data_ptr(), t.data_ptr(), int(m),
+                                                     int(x.shape[1]), scale.data_ptr(), shift.data_ptr(),
+                                                     mbits.data_ptr()), "bn_apply_res_mbits")
+    FWD_APPLY_COUNTS["materialized"] += 1
+
+
 def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int, abn=None) -> Optional[torch.Tensor]:
     """dgrad with the producer BN's backward partials in the epilogue, or None when the producer
     cannot take it (no ReLU, the shortcut gradient not in yet, already fused, layout/dtype)."""
@@ -423,14 +449,22 @@ class _Conv1x1(torch.autograd.Function):
     writes the weight gradient straight into its arena slot when the parameter has one."""
 
     @staticmethod
-    def forward(ctx, x, weight, stats, bn_producer=None):
+    def forward(ctx, x, weight, stats, bn_producer=None, fwd_apply=None):
         n, c, h, w_ = x.shape
         cout = weight.shape[0]
         x2 = x.permute(0, 2, 3, 1).reshape(-1, c)  # channels_last: a free view
         w2 = weight.reshape(cout, c)
         wb = w2 if w2.dtype == torch.bfloat16 else w2.to(torch.bfloat16)
         cfg = IGEMM_FWD_1X1.get((c, cout)) if is_gpu(x) else None
-        if cfg is not None and x.data_ptr() % 16 == 0:
+        if fwd_apply is not None:
+            # x is the unwritten output of the producing BN: stage relu(bx*scale + shift + res) as
+            # the A operand and write it (and its mask bits) into x (DEFER_FWD_APPLY)
+            bx, res, scale, shift, mbits = fwd_apply
+            y2, parts = conv1x1_nt(bx.permute(0, 2, 3, 1).reshape(-1, c), wb.contiguous(), scale=scale, shift=shift,
+                                   stats=stats, res=res.permute(0, 2, 3, 1).reshape(-1, c), aout=x2, abits=mbits)
+            y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
+            FWD_APPLY_COUNTS["in_gemm"] += 1
+        elif cfg is not None and x.data_ptr() % 16 == 0:
             # LDS-DMA implicit GEMM (same BN-statistics epilogue, 256-row partial blocks)
             y, parts = igemm_conv(x, weight, stats=stats, w_krsc=wb.contiguous(), cfg=cfg)
         else:
@@ -489,7 +523,7 @@ class _Conv1x1(torch.autograd.Function):
             conv1x1_wgrad(dy2, x2, dw.view(cout, c))
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class _BNReluConv1x1(torch.autograd.Function):
@@ -831,12 +865,20 @@ def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_e
         autocast = torch.is_autocast_enabled("cuda")
         if x.dtype != torch.bfloat16 and not (autocast and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             ok = False
+    pend = getattr(x, "_det_fwd_apply", None)
+    # (a staged apply saves a full pass over x: it outweighs det_igemm's edge on the IGEMM_FWD_1X1
+    # shapes, so those take the gemm_nt prologue here)
+    if pend is not None and not (ok and x.dtype == torch.bfloat16 and w.shape[0] % 64 == 0):
+        materialize_fwd_apply(x)  # this conv cannot stage the producer's BN apply itself
+        pend = None
     if not ok:
         COUNTS["fallback"] += 1
         return conv_mod(x)
     COUNTS["native"] += 1
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
+    if pend is not None:
+        x._det_fwd_apply = None
     prod = _bn_producer(x) if (bn_exclusive and FUSE_BN_BWD and torch.is_grad_enabled()) else None
     with torch.autocast("cuda", enabled=False):
-        return _Conv1x1.apply(x, w, stats, prod)
+        return _Conv1x1.apply(x, w, stats, prod, pend)

@@ -185,6 +185,7 @@ struct NtArgs {
   const unsigned short* A2;
   const float* acoef;  // [3][K]
   unsigned short* Aout;
+  uint8_t* abits;  // AFWD: ReLU mask bits of Aout (1 per element)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -196,8 +197,13 @@ struct NtArgs {
 // BT: B is given as [K, N] (N contiguous: the conv weight [Cout, Cin] itself for an input gradient),
 // staged as it sits ([64 k][BN] image, the wgrad swizzle) and read with ds_read_b64_tr_b16 -- no
 // transposed weight copy per call.
+// AFWD (forward of the conv that consumes a training BatchNorm(+residual)+ReLU output, ResNet
+// bn3 -> the next block's conv1): the A operand is the BN apply itself, relu(A*scale[k] + shift[k]
+// + A2) with A = the BN input and A2 = the residual, and the first N tile's blocks write it (Aout)
+// and its ReLU mask bits (abits) for the residual add and the backward: the separate apply pass
+// and this GEMM's read of its output become one pass.
 template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false, bool BT = false,
-          bool ABN = false>
+          bool ABN = false, bool AFWD = false>
 __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
@@ -237,7 +243,8 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   const unsigned short* bptr = a.B + static_cast<int64_t>(n0 + r0) * K + kc * 8;
   constexpr int BCPR = BN / 8;  // BT: 16-B chunks per B image row
 
-  us8 ra[ACH], rb[BCH], ra2[ABN ? ACH : 1];
+  constexpr bool A2IN = ABN || AFWD;
+  us8 ra[ACH], rb[BCH], ra2[A2IN ? ACH : 1];
   auto gload = [&](int kt) {
     const int64_t k = static_cast<int64_t>(kt) * kBK;
 #pragma unroll
@@ -245,7 +252,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       if (GM == kGmStem) ra[i] = a.g.stem_chunk(aptr[i], aval[i], ih0[i], iw0[i], kt * 8 + kc);
       else if (aval[i]) ra[i] = *reinterpret_cast<const us8*>(aptr[i] + k);
       else ra[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
-      if constexpr (ABN) {
+      if constexpr (A2IN) {
         if (aval[i]) ra2[i] = *reinterpret_cast<const us8*>(a.A2 + (aptr[i] - a.A) + k);
         else ra2[i] = us8{0, 0, 0, 0, 0, 0, 0, 0};
       }
@@ -265,6 +272,16 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
     // ABN: this thread's 8 channels of the apply coefficients, loaded once per K tile (before the
     // Aout stores, which the compiler could not move them across)
     float ca[8], cb[8], cc[8];
+    if constexpr (AFWD) {  // scale, shift of this thread's 8 channels
+      const int k0 = kt * kBK + kc * 8;
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        const float4 S0 = *reinterpret_cast<const float4*>(a.scale + k0 + j);
+        const float4 H0 = *reinterpret_cast<const float4*>(a.shift + k0 + j);
+        ca[j] = S0.x; ca[j + 1] = S0.y; ca[j + 2] = S0.z; ca[j + 3] = S0.w;
+        cb[j] = H0.x; cb[j + 1] = H0.y; cb[j + 2] = H0.z; cb[j + 3] = H0.w;
+      }
+    }
     if constexpr (ABN) {
       const int k0 = kt * kBK + kc * 8;
 #pragma unroll
@@ -290,6 +307,23 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
         for (int j = 0; j < 8; ++j) v[j] = f2bf(__fmaf_rn(ca[j], bf2f(ra[i][j]), __fmaf_rn(cb[j], bf2f(ra2[i][j]), cc[j])));
         if (!aval[i]) v = us8{0, 0, 0, 0, 0, 0, 0, 0};
         else if (first_ntile) *reinterpret_cast<us8*>(a.Aout + (aptr[i] - a.A) + static_cast<int64_t>(kt) * kBK) = v;
+      }
+      if constexpr (AFWD) {
+        // exactly det_norm.hip bn_apply_fwd<RELU, RES>: z = fma(x, scale, shift) + res, relu, mask bits
+        unsigned bits = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = __fmaf_rn(bf2f(ra[i][j]), ca[j], cb[j]) + bf2f(ra2[i][j]);
+          v[j] = f2bf(fmaxf(z, 0.f));
+          bits |= (z > 0.f ? 1u : 0u) << j;
+        }
+        if (!aval[i]) {
+          v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+        } else if (first_ntile) {
+          const int64_t off = (aptr[i] - a.A) + static_cast<int64_t>(kt) * kBK;
+          *reinterpret_cast<us8*>(a.Aout + off) = v;
+          a.abits[off >> 3] = static_cast<uint8_t>(bits);
+        }
       }
       *reinterpret_cast<us8*>(base + swz(r0 + 32 * i, kc)) = v;
     }
@@ -673,6 +707,20 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int smem = nt_smem<BM, BN, OCC == 2 ? 2 : 1>();
+  if (a.abits != nullptr) {  // AFWD: forward with the BN apply (+ residual, ReLU) in the A staging
+    if (!a.A2 || !a.Aout || !a.scale || !a.shift || pro || bt || bnb || stride2) return -2;
+    if constexpr (OCC > 2) {
+      return -6;  // the occupancy-3 single-K-tile variant has no register room for it (K = 64 only)
+    } else {
+      if (stats)
+        hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, true, kGmDirect, OCC, false, false, false, true>),
+                           dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, false, false, true>),
+                           dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   const bool abn = a.A2 != nullptr;
   if (abn && (!bt || pro || stats || stride2)) return -2;  // the A-apply prologue: input gradients only
   if (bnb) {  // input-gradient GEMM with the BN-backward epilogue (no prologue / stats / gather)
@@ -734,16 +782,24 @@ int det_conv_nt_rows_per_block(int N) { return 128; }
 // C[M,N] = op(A)[M,K] . B[N,K]^T.  bf16.  N % 64 == 0, K % 64 == 0, pointers 16-B aligned.
 // scale/shift (nullable): prologue relu(A*scale+shift) per K channel.  pmean/pm2 (nullable):
 // BN statistics partials [ceil(M/rpb), N].  Ho..Wi > 0 selects the 1x1 stride-2 row gather.
+// res / aout / abits (all or none; with scale, shift): AFWD -- op(A) = relu(A*scale + shift + res),
+// written to aout with its mask bits to abits by the first N tile (the consuming conv applies the
+// producing BatchNorm; see the AFWD note at gemm_nt_kernel).
 int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K,
-                const float* scale, const float* shift, float* pmean, float* pm2, int Ho, int Wo, int Hi, int Wi) {
+                const float* scale, const float* shift, float* pmean, float* pm2, int Ho, int Wo, int Hi, int Wi,
+                const void* res, void* aout, void* abits) {
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
   if ((scale == nullptr) != (shift == nullptr) || (pmean == nullptr) != (pm2 == nullptr)) return -2;
   const bool stride2 = Ho > 0;
   if (stride2 && M != static_cast<int64_t>(M / (static_cast<int64_t>(Ho) * Wo)) * Ho * Wo) return -3;
+  if ((res == nullptr) != (aout == nullptr) || (res == nullptr) != (abits == nullptr)) return -2;
+  if (res && (!scale || stride2)) return -2;
   NtArgs a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C),
-           M, N, K, scale, shift, pmean, pm2, Gather{Ho, Wo, Hi, Wi}};
+           M, N, K, scale, shift, pmean, pm2, Gather{Ho, Wo, Hi, Wi}, BnBwdEpi{},
+           static_cast<const unsigned short*>(res), nullptr, static_cast<unsigned short*>(aout),
+           static_cast<uint8_t*>(abits)};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const bool pro = scale != nullptr, stats = pmean != nullptr;
+  const bool pro = scale != nullptr && res == nullptr, stats = pmean != nullptr;
   if (K == kBK) {
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
     return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);

@@ -960,6 +960,20 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
   return static_cast<int>(hipGetLastError());
 }
 
+// Training apply with precomputed scale/shift: y = relu(x*scale + shift + res) and its mask bits
+// (the materialisation of a BN apply deferred onto a consuming conv that could not take it).
+int det_bn_apply_res_mbits(void* stream, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
+                           const float* shift, uint8_t* mbits) {
+  if (C % 8 != 0 || M <= 0 || !res || !mbits) return -1;
+  if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t nvec = M * C / 8;
+  hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, true>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+                     static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                     static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits);
+  return static_cast<int>(hipGetLastError());
+}
+
 // Inference / frozen-stats path: y = act(x*scale + shift [+ res]) with host-prepared scale/shift.
 int det_bn_apply(void* stream, int dtype, const void* x, const void* res, void* y, int64_t M, int C,
                  const float* scale, const float* shift, int relu) {

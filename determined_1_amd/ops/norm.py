@@ -72,7 +72,8 @@ class _BNActTrain(torch.autograd.Function):
     the conv's input gradient with a separate elementwise pass over the whole activation."""
 
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, link=None):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, link=None,
+                defer=False):
         M, C = _rows(x)
         lib = _lib.get_lib()
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
@@ -87,6 +88,8 @@ class _BNActTrain(torch.autograd.Function):
         parts = take_partials(x)  # statistics already computed by the producing GEMM's epilogue
         ws = torch.empty(int(lib.det_bn_fin_ws_elems(C) if parts is not None else lib.det_bn_ws_elems(M, C)),
                          dtype=torch.float32, device=x.device)
+        defer = bool(defer and parts is not None and relu and residual is not None and mbits is not None
+                     and x.dtype == torch.bfloat16 and fmt == torch.channels_last)
         if parts is not None:
             pm, pq, rpb = parts
             _lib.check(
@@ -94,7 +97,7 @@ class _BNActTrain(torch.autograd.Function):
                     _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C, int(rpb),
                     int(pm.shape[0]), pm.data_ptr(), pq.data_ptr(),
                     _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
-                    float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)), 1,
+                    float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)), 0 if defer else 1,
                     stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits),
                     ws.data_ptr(),
                 ),
@@ -121,6 +124,11 @@ class _BNActTrain(torch.autograd.Function):
         ctx.extra_dy = None  # set by the consumer of this output as identity shortcut
         ctx.fmt = fmt
         ctx.save_for_backward(x, mbits, weight, stats)
+        if defer:
+            # y stays unwritten: the consuming conv stages (and writes) the apply (ops/conv.py
+            # DEFER_FWD_APPLY); bn_act tags the returned tensor
+            _DEFERRED["last"] = (y.data_ptr(), (x, residual, stats[2], stats[3], mbits))
+            _conv.FWD_APPLY_COUNTS["deferred"] += 1
         return y
 
     @staticmethod
@@ -197,7 +205,7 @@ class _BNActTrain(torch.autograd.Function):
             dres = None
         dw = dgb[0] if dgb is not None and ctx.needs_input_grad[2] else None
         db = dgb[1] if dgb is not None and ctx.needs_input_grad[3] else None
-        return dx, dres, dw, db, None, None, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None, None, None
 
 
 class _LinkedConv(torch.autograd.Function):
@@ -265,8 +273,11 @@ def linked_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     return conv(x)
 
 
+_DEFERRED = {"last": None}  # (data_ptr of the unwritten output, apply arguments) of the last deferred forward
+
+
 def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optional[torch.Tensor] = None,
-           relu: bool = True, shortcut_link: bool = False) -> torch.Tensor:
+           relu: bool = True, shortcut_link: bool = False, defer_apply: bool = False) -> torch.Tensor:
     """``act(bn(x) + residual)`` with the module's parameters/buffers and train/eval semantics.
 
     ``shortcut_link``: the caller guarantees ``residual`` is an identity shortcut, i.e. also the
@@ -276,6 +287,8 @@ def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optio
     rm = bn.running_mean if (bn.track_running_stats and bn.training) else None
     rv = bn.running_var if (bn.track_running_stats and bn.training) else None
     res_ok = residual is None or (residual.shape == x.shape and residual.device == x.device)
+    _conv.materialize_fwd_apply(x)  # inputs whose producing BN apply was deferred but never staged
+    _conv.materialize_fwd_apply(residual)
     if _nhwc_ok(x) and res_ok:
         if use_batch_stats:
             nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
@@ -286,7 +299,15 @@ def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optio
                                                else torch.contiguous_format)):
                 link = residual.grad_fn
                 residual = residual.detach()
-            return _BNActTrain.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, bn.momentum, bn.eps, relu, link)
+            defer = bool(defer_apply and _conv.DEFER_FWD_APPLY and torch.is_grad_enabled())
+            out = _BNActTrain.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, bn.momentum, bn.eps, relu, link,
+                                    defer)
+            last, _DEFERRED["last"] = _DEFERRED["last"], None
+            if last is not None:
+                if last[0] != out.data_ptr():
+                    raise RuntimeError("deferred BN apply: output buffer changed across autograd")
+                out._det_fwd_apply = last[1]
+            return out
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or (residual is not None and residual.requires_grad)
             or (bn.weight is not None and bn.weight.requires_grad))
@@ -333,9 +354,9 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.fused = fused  # False: stock torch/MIOpen BN + separate add/ReLU (A/B comparisons)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,  # type: ignore[override]
-                shortcut_link: bool = False) -> torch.Tensor:
+                shortcut_link: bool = False, defer_apply: bool = False) -> torch.Tensor:
         if self.fused:
-            return bn_act(x, self, residual, self.relu, shortcut_link)
+            return bn_act(x, self, residual, self.relu, shortcut_link, defer_apply)
         y = super().forward(x)
         if residual is not None:
             y = y + residual
