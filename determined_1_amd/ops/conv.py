@@ -866,9 +866,10 @@ def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_e
         if x.dtype != torch.bfloat16 and not (autocast and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             ok = False
     pend = getattr(x, "_det_fwd_apply", None)
-    # (a staged apply saves a full pass over x: it outweighs det_igemm's edge on the IGEMM_FWD_1X1
-    # shapes, so those take the gemm_nt prologue here)
-    if pend is not None and not (ok and x.dtype == torch.bfloat16 and w.shape[0] % 64 == 0):
+    # (the det_igemm-routed shapes keep det_igemm + the separate apply: staging the apply in
+    # gemm_nt there measured 0.5 ms/step slower, profiles/r3_bench_resnet50_defer_fwd_apply.jsonl)
+    if pend is not None and not (ok and x.dtype == torch.bfloat16 and w.shape[0] % 64 == 0
+                                 and (x.shape[1], w.shape[0]) not in IGEMM_FWD_1X1):
         materialize_fwd_apply(x)  # this conv cannot stage the producer's BN apply itself
         pend = None
     if not ok:
