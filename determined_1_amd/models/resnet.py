@@ -126,11 +126,14 @@ class Bottleneck(nn.Module):
         self.defer_out = False
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.downsample is None else _shortcut(self.downsample, x)
         # x (the previous block's output) reaches autograd only through conv1: the shortcut's
-        # gradient is handed to its producer through the BN link (identity or _LinkedConv)
+        # gradient is handed to its producer through the BN link (identity or projection)
         out = self.bn1(c1x1(x, self.conv1, bn_exclusive=FUSED_BN and _shortcut_linked(self.downsample, x)))
         out = bn_relu_c1x1(c3x3(out, self.conv2, bn_exclusive=True), self.bn2, self.conv3)  # bn1 feeds only conv2
+        # the projection runs after the main branch: autograd then runs its backward first (later
+        # nodes go first among ready ones), so its input gradient is linked before conv1's dgrad,
+        # whose epilogue sums it into the producer's BN-backward partials
+        idt = x if self.downsample is None else _shortcut(self.downsample, x)
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
         return self.bn3(out, idt, shortcut_link=self.downsample is None,
                         defer_apply=self.defer_out and NATIVE_CONV1X1 and FUSED_BN)

@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -144,7 +144,8 @@ _SIGNATURES = {
     "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 3, c_int),
     "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),
     # stream, A, B, C, M, N, K, x, mean, scale, shift, mbits, add, psum, psumx, mode
-    "det_conv_nt_bnbwd": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 8 + [c_int, c_int] + [c_void_p] * 3, c_int),
+    "det_conv_nt_bnbwd": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 8 + [c_int, c_int] + [c_void_p] * 3
+                          + [c_int] * 4, c_int),
     "det_conv_dgrad": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 3, c_int),
     # det_igemm.hip: pipelined implicit-GEMM conv (LDS-DMA ring)
     "det_igemm_rows_per_block": ([], c_int),

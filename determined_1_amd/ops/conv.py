@@ -7,7 +7,7 @@ can take the HIP path.  On CPU tensors the functions compute the same result wit
 (fp32 accumulate), which is what the unit tests compare against.
 """
 import os
-from typing import Optional, Tuple
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 
@@ -373,6 +373,26 @@ def materialize_fwd_apply(t: Optional[torch.Tensor]) -> None:
     FWD_APPLY_COUNTS["materialized"] += 1
 
 
+class StridedGrad(NamedTuple):
+    """Input gradient of a 1x1 stride-2 conv kept on its stride-2 grid: ``t`` [N, C, Ho, Wo]
+    (channels_last) holds the values at the even (h, w) positions of the [N, C, Hi, Wi] input,
+    zero elsewhere.  A producer's fused BN-backward epilogue reads it in place (det_conv.hip
+    BnBwdEpi add_*); anything else materialises it (``full_res_grad``)."""
+    t: torch.Tensor
+    g: Gather  # (Ho, Wo, Hi, Wi)
+
+
+def full_res_grad(extra, like: Optional[torch.Tensor] = None):
+    """A shortcut gradient at the resolution of its input (``StridedGrad`` scattered into zeros)."""
+    if not isinstance(extra, StridedGrad):
+        return extra
+    ho, wo, hi, wi = extra.g
+    nb, c = extra.t.shape[0], extra.t.shape[1]
+    full = torch.zeros((nb, hi, wi, c), dtype=extra.t.dtype, device=extra.t.device).permute(0, 3, 1, 2)
+    full[:, :, ::2, ::2] = extra.t
+    return full
+
+
 def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int, abn=None) -> Optional[torch.Tensor]:
     """dgrad with the producer BN's backward partials in the epilogue, or None when the producer
     cannot take it (no ReLU, the shortcut gradient not in yet, already fused, layout/dtype)."""
@@ -389,6 +409,9 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int,
     if xb.dtype != torch.bfloat16 or xb.numel() != m * c or not xb.is_contiguous(memory_format=torch.channels_last):
         return None
     add = prod.extra_dy if expects else None
+    sub = (0, 0, 0, 0)
+    if isinstance(add, StridedGrad):  # a stride-2 projection shortcut's gradient, read on its grid
+        sub, add = add.g, add.t
     if add is not None and (add.dtype != torch.bfloat16 or not add.is_contiguous(memory_format=torch.channels_last)):
         return None
     rpb = rows_per_block(c)
@@ -403,7 +426,8 @@ def _fused_bn_dgrad(prod, dy2d: torch.Tensor, w2d: torch.Tensor, m: int, c: int,
     _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
         _stream(dy2d), a_src.data_ptr(), wb.data_ptr(), d.data_ptr(), int(m), int(c), int(w2d.shape[0]), xb.data_ptr(),
         stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits), _ptr(add), psum.data_ptr(),
-        psumx.data_ptr(), int(mode), 1 if DGRAD_BT else 0, _ptr(ax), _ptr(acoef), _ptr(aout)), "conv_nt_bnbwd")
+        psumx.data_ptr(), int(mode), 1 if DGRAD_BT else 0, _ptr(ax), _ptr(acoef), _ptr(aout), *[int(v) for v in sub]),
+        "conv_nt_bnbwd")
     prod.fused_bwd = (psum, psumx, rpb)
     if expects:
         prod.extra_dy = None  # consumed: summed into d
@@ -883,3 +907,104 @@ def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_e
     prod = _bn_producer(x) if (bn_exclusive and FUSE_BN_BWD and torch.is_grad_enabled()) else None
     with torch.autocast("cuda", enabled=False):
         return _Conv1x1.apply(x, w, stats, prod, pend)
+
+
+# ------------------------------------------------------------------------------------------------
+# projection shortcut: 1x1 conv, stride 1 or 2 (ResNet downsample)
+# ------------------------------------------------------------------------------------------------
+# Native projection shortcuts (hparam-free A/B switch): forward on the det_igemm implicit GEMM /
+# det_conv gemm_nt with the downsample BN's statistics in the epilogue, input gradient as a 1x1 GEMM
+# on the output grid (a stride-2 conv's gradient stays on its stride-2 grid, ``StridedGrad``),
+# weight gradient on det_conv's gathered gemm_tn.  Off: MIOpen conv + a separate statistics pass.
+NATIVE_SHORTCUT = os.environ.get("DET_NATIVE_SHORTCUT", "1") != "0"
+# stride-2 forward tile configuration per (Cin, Cout) (profiles/r3_igemm_cfgs_1x1.jsonl: cfg 8 is the
+# fastest det_igemm tile on all three ResNet-50 stride-2 projections)
+SHORTCUT_S2_CFG = {}
+SHORTCUT_COUNTS = {"native": 0, "fallback": 0}
+
+
+def shortcut_native_ok(x: torch.Tensor, conv_mod: torch.nn.Conv2d) -> bool:
+    w = conv_mod.weight
+    return (NATIVE_SHORTCUT and ENABLED and x.device.type == "cuda" and x.dim() == 4 and conv_mod.bias is None
+            and conv_mod.kernel_size == (1, 1) and conv_mod.stride in ((1, 1), (2, 2)) and conv_mod.groups == 1
+            and conv_mod.padding in ((0, 0), 0, "valid") and conv_mod.dilation == (1, 1)
+            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0
+            and w.shape[0] % 64 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.data_ptr() % 16 == 0 and not torch.is_autocast_enabled("cuda"))
+
+
+class _Shortcut1x1(torch.autograd.Function):
+    """``conv2d(x, w, stride)`` of a 1x1 projection shortcut (stride 1 or 2) on channels_last bf16.
+
+    ``link``: ``x`` is the output of a fused training BN that also feeds the block's conv1; the input
+    gradient then goes to that producer's backward (``link.extra_dy``, summed in its kernels -- for
+    stride 2 read on the stride-2 grid by the fused dgrad epilogue) and autograd gets None for ``x``
+    (reference behaviour: norm._LinkedConv).  Without a link the gradient returns to autograd at
+    full resolution."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, stats, link):
+        n, c, h, w_ = x.shape
+        cout = weight.shape[0]
+        wk = weight.reshape(cout, c).contiguous()
+        if stride == 2:
+            y, parts = igemm_conv(x, weight, stride=2, stats=stats, w_krsc=wk, cfg=SHORTCUT_S2_CFG.get((c, cout), 8))
+        elif (c, cout) in IGEMM_FWD_1X1:
+            y, parts = igemm_conv(x, weight, stats=stats, w_krsc=wk, cfg=IGEMM_FWD_1X1[(c, cout)])
+        else:
+            y2, parts = conv1x1_nt(x.permute(0, 2, 3, 1).reshape(-1, c), wk, stats=stats)
+            y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
+        _attach_partials(y, parts)
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        ctx.link = link
+        if link is not None:
+            link.expects_extra = True  # a fused dgrad into the producer must wait for this gradient
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        n, c, h, w_ = x.shape
+        cout, ho, wo = dy.shape[1], dy.shape[2], dy.shape[3]
+        st = ctx.stride
+        g = (ho, wo, h, w_) if st == 2 else None
+        dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
+        link, ctx.link = ctx.link, None
+        dx = dw = None
+        if ctx.needs_input_grad[0] or link is not None:
+            w2 = weight.reshape(cout, c).contiguous()
+            dxs = dgrad_1x1(dy2, w2).view(n, ho, wo, c).permute(0, 3, 1, 2)  # on the output grid
+            extra = StridedGrad(dxs, g) if st == 2 else dxs
+            if link is not None:
+                if link.extra_dy is not None:
+                    raise RuntimeError("second upstream gradient linked twice to one producer")
+                link.extra_dy = extra
+            else:
+                dx = full_res_grad(extra)
+        if ctx.needs_input_grad[1]:
+            from determined_1_amd.ops.arena import landing_buffer
+
+            buf = landing_buffer(weight)
+            if buf is not None and buf.is_contiguous() and buf.dtype in (torch.bfloat16, torch.float32):
+                dw = buf
+            else:
+                dw = torch.empty(weight.shape, dtype=weight.dtype if weight.dtype in (torch.bfloat16, torch.float32)
+                                 else torch.float32, device=weight.device)
+            if st == 2 and WGRAD_RING and int(_lib.get_lib().det_igemm_wgrad_ws_elems(dy2.shape[0], cout, c, 0)) > 0:
+                # stride 2: the ring's strided im2col beats the gathered gemm_tn on all three ResNet-50
+                # projections (0.209 / 0.185 / 0.243 vs 0.228 / 0.208 / 0.316 ms,
+                # profiles/r3_shortcut_microbench.jsonl); stride 1 stays on gemm_tn (0.188 vs 0.243)
+                dyc = dy2.view(n, ho, wo, cout).permute(0, 3, 1, 2)
+                conv_wgrad(dyc, x, dw.view(cout, c), 1, 1, 2, 0)
+            else:
+                conv1x1_wgrad(dy2, x.permute(0, 2, 3, 1).reshape(-1, c), dw.view(cout, c), gather=g)
+            if dw.dtype != weight.dtype:
+                dw = dw.to(weight.dtype)
+        return dx, dw, None, None, None
+
+
+def shortcut_conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, link=None, stats: bool = True) -> torch.Tensor:
+    """Projection-shortcut conv on the native path (``shortcut_native_ok`` must hold)."""
+    SHORTCUT_COUNTS["native"] += 1
+    return _Shortcut1x1.apply(x, conv_mod.weight, int(conv_mod.stride[0]), stats, link)

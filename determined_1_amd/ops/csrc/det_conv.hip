@@ -163,6 +163,10 @@ struct BnBwdEpi {
   float* psum;
   float* psumx;
   int mode;
+  // add_hi > 0: add is given on the stride-2 grid [M/(Hi*Wi)*Ho*Wo, N] of a 1x1 stride-2 projection
+  // shortcut (its input gradient is zero off the even (h, w) positions) -- never materialised at
+  // the full resolution
+  int add_ho, add_wo, add_hi, add_wi;
 };
 
 struct NtArgs {
@@ -419,7 +423,20 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       const bool ok = row < nvalid;
       const int64_t off = (m0 + (ok ? row : 0)) * a.N + c0;
       xs[q] = ok ? *reinterpret_cast<const us8*>(a.bn.x + off) : us8{0, 0, 0, 0, 0, 0, 0, 0};
-      as[q] = (ok && a.bn.add) ? *reinterpret_cast<const us8*>(a.bn.add + off) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+      as[q] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (ok && a.bn.add) {
+        int64_t aoff = off;
+        bool on = true;
+        if (a.bn.add_hi > 0) {
+          const int64_t r = m0 + row, hw = static_cast<int64_t>(a.bn.add_hi) * a.bn.add_wi;
+          const int64_t img = r / hw;
+          const int rem = static_cast<int>(r - img * hw);
+          const int h = rem / a.bn.add_wi, w = rem - h * a.bn.add_wi;
+          on = ((h | w) & 1) == 0;
+          aoff = ((img * a.bn.add_ho + (h >> 1)) * a.bn.add_wo + (w >> 1)) * a.N + c0;
+        }
+        if (on) as[q] = *reinterpret_cast<const us8*>(a.bn.add + aoff);
+      }
       bs[q] = (ok && a.bn.mode == 2) ? a.bn.mbits[off >> 3] : 0u;
     }
 #pragma unroll
@@ -835,13 +852,17 @@ int det_conv_dgrad(void* stream, const void* dY, const void* W, void* dX, int64_
 int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K, const void* x,
                       const float* mean, const float* scale, const float* shift, const void* mbits, const void* add,
                       float* psum, float* psumx, int mode, int b_kn, const void* abn_x, const float* abn_coef,
-                      void* abn_out) {
+                      void* abn_out, int add_ho, int add_wo, int add_hi, int add_wi) {
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
+  if (add_hi > 0 && (add_wi <= 0 || add_ho != (add_hi + 1) / 2 || add_wo != (add_wi + 1) / 2 ||
+                     M % (static_cast<int64_t>(add_hi) * add_wi) != 0))
+    return -3;
   if (!x || !mean || !psum || !psumx || (mode == 1 && (!scale || !shift)) || (mode == 2 && !mbits) || mode < 1 || mode > 2)
     return -2;
   NtArgs a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C),
            M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}, BnBwdEpi{static_cast<const unsigned short*>(x), mean, scale,
-           shift, static_cast<const uint8_t*>(mbits), static_cast<const unsigned short*>(add), psum, psumx, mode},
+           shift, static_cast<const uint8_t*>(mbits), static_cast<const unsigned short*>(add), psum, psumx, mode,
+           add_ho, add_wo, add_hi > 0 ? add_hi : 0, add_wi},
            static_cast<const unsigned short*>(abn_x), abn_coef, static_cast<unsigned short*>(abn_out)};
   if (abn_x && (!abn_coef || !abn_out)) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);

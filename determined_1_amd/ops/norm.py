@@ -138,6 +138,7 @@ class _BNActTrain(torch.autograd.Function):
         lib = _lib.get_lib()
         dy = dy.to(x.dtype).contiguous(memory_format=ctx.fmt)
         dy2, ctx.extra_dy = ctx.extra_dy, None
+        dy2 = _conv.full_res_grad(dy2)  # a stride-2 projection shortcut's gradient, unfused path
         dx = torch.empty_like(x, memory_format=ctx.fmt)
         want_res = ctx.has_res and (ctx.needs_input_grad[1] or ctx.link is not None)
         dgb = None
@@ -262,14 +263,20 @@ def linked_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     Limitation of the link: autograd sees no gradient for ``x`` from this conv (it is added inside
     the producer's backward), so ``torch.autograd.grad(loss, x)`` taken *without* running the full
     backward would miss this consumer's share.  ``x.retain_grad()`` and ``x.register_hook`` are
-    detected and fall back to plain ``conv(x)`` (``_observed``)."""
+    detected and fall back to plain ``conv(x)`` (``_observed``).  1x1 stride-1/2 convs on channels_last
+    bf16 take the native path (``ops.conv.shortcut_conv1x1``), with or without the link."""
+    _conv.materialize_fwd_apply(x)
     if (SHORTCUT_LINK and conv.bias is None and torch.is_grad_enabled() and x.requires_grad
             and not _observed(x)
             and isinstance(x.grad_fn, _BNActTrain._backward_cls) and x.dim() == 4
             and x.dtype == conv.weight.dtype and _autocast_keeps(x)
             and x.is_contiguous(memory_format=torch.channels_last) and conv.padding_mode == "zeros"
             and getattr(x.grad_fn, "extra_dy", None) is None):
+        if _conv.shortcut_native_ok(x, conv):
+            return _conv.shortcut_conv1x1(x, conv, link=x.grad_fn)
         return _LinkedConv.apply(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, x.grad_fn)
+    if torch.is_grad_enabled() and _conv.shortcut_native_ok(x, conv):
+        return _conv.shortcut_conv1x1(x, conv)  # e.g. ResNet layer1's projection of the max-pool output
     return conv(x)
 
 

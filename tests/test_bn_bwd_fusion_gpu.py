@@ -45,8 +45,8 @@ def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k, b_kn):
     _lib.check(_lib.get_lib().det_conv_nt_bnbwd(
         torch.cuda.current_stream().cuda_stream, dyg.data_ptr(), wg.data_ptr(), d.data_ptr(), m, c, k,
         xg.data_ptr(), meang.data_ptr(), scg.data_ptr(), shg.data_ptr(), None if bitsg is None else bitsg.data_ptr(),
-        None if addg is None else addg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), mode, b_kn, None, None, None),
-        "bnbwd")
+        None if addg is None else addg.data_ptr(), psum.data_ptr(), psumx.data_ptr(), mode, b_kn, None, None, None,
+        0, 0, 0, 0), "bnbwd")
     torch.cuda.synchronize()
     got = d.float().cpu()
     # one bf16 rounding of the accumulated product may differ by an ulp from torch's rounding
@@ -56,6 +56,48 @@ def test_bnbwd_epilogue_matches_composite(gpu, mode, m, c, k, b_kn):
     sx_ref = (got.double() * (x.double() - mean.double())).sum(0)
     torch.testing.assert_close(psum.double().sum(0).cpu(), s_ref, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(psumx.double().sum(0).cpu(), sx_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("nb,hi,wi,c,k", [(2, 14, 14, 64, 128), (3, 7, 9, 128, 64), (1, 28, 28, 256, 512)])
+def test_bnbwd_epilogue_strided_shortcut_gradient(gpu, nb, hi, wi, c, k):
+    """Mode-2 epilogue with the shortcut gradient of a 1x1 stride-2 projection given on its stride-2
+    grid (add_ho/wo/hi/wi): equals the epilogue fed the zero-scattered full-resolution gradient."""
+    ho, wo = (hi + 1) // 2, (wi + 1) // 2
+    m = nb * hi * wi
+    g = torch.Generator(device="cpu").manual_seed(m + c)
+    dy = torch.randn(m, k, generator=g).to(torch.bfloat16).to(gpu)
+    w = (torch.randn(k, c, generator=g) / k ** 0.5).to(torch.bfloat16).to(gpu)  # [K, N] as stored (b_kn)
+    x = torch.randn(m, c, generator=g).to(torch.bfloat16).to(gpu)
+    mean = (torch.randn(c, generator=g) * 0.1).to(gpu)
+    mask = torch.rand(m, c, generator=g) > 0.3
+    bits = (mask.reshape(-1, 8).to(torch.int32) * (2 ** torch.arange(8, dtype=torch.int32))).sum(1).to(torch.uint8).to(gpu)
+    sub = torch.randn(nb, ho, wo, c, generator=g).to(torch.bfloat16).to(gpu)
+    full = torch.zeros(nb, hi, wi, c, dtype=torch.bfloat16, device=gpu)
+    full[:, ::2, ::2, :] = sub
+    lib = _lib.get_lib()
+    rpb = conv.rows_per_block(c)
+    nrb = (m + rpb - 1) // rpb
+    outs = []
+    for add, dims in ((full, (0, 0, 0, 0)), (sub, (ho, wo, hi, wi))):
+        psum = torch.empty(nrb, c, device=gpu)
+        psumx = torch.empty(nrb, c, device=gpu)
+        d = torch.empty(m, c, dtype=torch.bfloat16, device=gpu)
+        _lib.check(lib.det_conv_nt_bnbwd(
+            torch.cuda.current_stream().cuda_stream, dy.data_ptr(), w.data_ptr(), d.data_ptr(), m, c, k, x.data_ptr(),
+            mean.data_ptr(), None, None, bits.data_ptr(), add.data_ptr(), psum.data_ptr(), psumx.data_ptr(), 2, 1, None,
+            None, None, *dims), "bnbwd")
+        outs.append((d, psum, psumx))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    # and against the composite
+    ref = torch.where(mask.to(gpu), ((dy.float() @ w.float()).to(torch.bfloat16).float() + full.view(m, c).float()),
+                      torch.zeros(m, c, device=gpu))
+    torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2)
+    # an inconsistent grid is refused
+    assert lib.det_conv_nt_bnbwd(torch.cuda.current_stream().cuda_stream, dy.data_ptr(), w.data_ptr(), d.data_ptr(), m,
+                                 c, k, x.data_ptr(), mean.data_ptr(), None, None, bits.data_ptr(), sub.data_ptr(),
+                                 psum.data_ptr(), psumx.data_ptr(), 2, 1, None, None, None, ho + 1, wo, hi, wi) == -3
 
 
 def _ref_block(blk, x, weights):
@@ -75,7 +117,8 @@ def _ref_block(blk, x, weights):
     return F.relu(out + idt)
 
 
-def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
+@pytest.mark.parametrize("stride", [1, 2])
+def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu, stride):
     """Stem-less chain of two ResNet bottlenecks (projection + identity shortcut) at a well-
     conditioned batch-norm size: every gradient with the fusion (both mask modes exercised) and
     without it against an fp32 PyTorch composite with the same weights.  (Run-to-run comparisons
@@ -86,7 +129,10 @@ def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
 
     torch.manual_seed(0)
     stem_bn = BatchNormAct2d(64, relu=True, fused=True)
-    b0 = resnet.Bottleneck(64, 64, 1, torch.nn.Sequential(resnet.conv1x1(64, 256), resnet.bn(256, relu=False)))
+    # stride 2: a projection shortcut whose input gradient stays on its stride-2 grid (StridedGrad),
+    # read in place by the fused conv1 dgrad epilogue (fusion on) or scattered (fusion off)
+    b0 = resnet.Bottleneck(64, 64, stride, torch.nn.Sequential(resnet.conv1x1(64, 256, stride),
+                                                               resnet.bn(256, relu=False)))
     b1 = resnet.Bottleneck(256, 64)
     mods = torch.nn.ModuleList([stem_bn, b0, b1]).to(gpu).to(memory_format=torch.channels_last)
     for mod in mods.modules():
@@ -94,7 +140,8 @@ def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
             mod.to(torch.bfloat16)
     g = torch.Generator(device="cpu").manual_seed(2)
     z = torch.randn(4, 64, 28, 28, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    dout = torch.randn(4, 256, 28, 28, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ho = 28 // stride
+    dout = torch.randn(4, 256, ho, ho, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     def run(fuse):
         conv.FUSE_BN_BWD = fuse
@@ -107,9 +154,11 @@ def test_bottleneck_chain_grads_with_bn_bwd_fusion(gpu):
 
     before = dict(conv.BN_BWD_COUNTS)
     before_apply = dict(conv.BN_APPLY_COUNTS)
+    before_sc = conv.SHORTCUT_COUNTS["native"]
     dz_u, gr_u = run(False)
     dz_f, gr_f = run(True)
     conv.FUSE_BN_BWD = True
+    assert conv.SHORTCUT_COUNTS["native"] - before_sc == 2  # the projection conv ran natively both times
     # bn2->conv3 x2, bn1->conv2 (3x3 dgrad epilogue) x2, b0 output->b1.conv1 (mode 2)
     assert conv.BN_BWD_COUNTS["fused"] - before["fused"] >= 5
     # deferred BN applies computed in the conv dgrad's A staging: b0.bn3 -> b0.conv3 (the expansion
