@@ -917,8 +917,9 @@ def conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_e
 # on the output grid (a stride-2 conv's gradient stays on its stride-2 grid, ``StridedGrad``),
 # weight gradient on det_conv's gathered gemm_tn.  Off: MIOpen conv + a separate statistics pass.
 NATIVE_SHORTCUT = os.environ.get("DET_NATIVE_SHORTCUT", "1") != "0"
-# stride-2 forward tile configuration per (Cin, Cout) (profiles/r3_igemm_cfgs_1x1.jsonl: cfg 8 is the
-# fastest det_igemm tile on all three ResNet-50 stride-2 projections)
+# stride-2 forward tile configuration per (Cin, Cout); default cfg 8 where Cout % 256 == 0
+# (profiles/r3_igemm_cfgs_1x1.jsonl: the fastest det_igemm tile on all three ResNet-50 stride-2
+# projections), else the automatic choice
 SHORTCUT_S2_CFG = {}
 SHORTCUT_COUNTS = {"native": 0, "fallback": 0}
 
@@ -948,7 +949,8 @@ class _Shortcut1x1(torch.autograd.Function):
         cout = weight.shape[0]
         wk = weight.reshape(cout, c).contiguous()
         if stride == 2:
-            y, parts = igemm_conv(x, weight, stride=2, stats=stats, w_krsc=wk, cfg=SHORTCUT_S2_CFG.get((c, cout), 8))
+            cfg = SHORTCUT_S2_CFG.get((c, cout), 8 if cout % 256 == 0 else 0)  # cfg 8: 256-wide N tiles
+            y, parts = igemm_conv(x, weight, stride=2, stats=stats, w_krsc=wk, cfg=cfg)
         elif (c, cout) in IGEMM_FWD_1X1:
             y, parts = igemm_conv(x, weight, stats=stats, w_krsc=wk, cfg=IGEMM_FWD_1X1[(c, cout)])
         else:

@@ -4,7 +4,7 @@ import copy
 import pytest
 import torch
 
-from determined_1_amd.ops import norm
+from determined_1_amd.ops import conv, norm
 
 pytestmark = pytest.mark.gpu
 
@@ -133,12 +133,14 @@ def test_linked_projection_conv_matches_autograd_sum(gpu, dtype, monkeypatch):
     outs = []
     for link in (False, True):
         monkeypatch.setattr(norm, "SHORTCUT_LINK", link)
+        monkeypatch.setattr(conv, "NATIVE_SHORTCUT", link)  # reference: plain conv, autograd sum
         for m in (bn, conv_a, conv_b):
             m.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
         h = bn(x)
         b = norm.linked_conv2d(h, conv_b)
-        assert (type(b.grad_fn).__name__ == "_LinkedConvBackward") == link
+        # linked: the MIOpen conv (fp32) or the native projection (bf16, ops.conv._Shortcut1x1)
+        assert (type(b.grad_fn).__name__ in ("_LinkedConvBackward", "_Shortcut1x1Backward")) == link
         torch.autograd.backward([conv_a(h), b], [ga, gb])
         outs.append([x.grad, bn.weight.grad, bn.bias.grad, conv_a.weight.grad, conv_b.weight.grad])
     tol = dict(atol=1e-4, rtol=1e-4) if dtype == torch.float32 else dict(atol=3e-2, rtol=3e-2)
@@ -198,6 +200,7 @@ def test_resnet50_fused_shortcut_link_and_pool_match_stock(gpu, monkeypatch):
     losses = []
     for m, link in ((ref, False), (ref2, False), (dut, True)):
         monkeypatch.setattr(norm, "SHORTCUT_LINK", link)
+        monkeypatch.setattr(conv, "NATIVE_SHORTCUT", link)  # reference: plain conv, autograd sum
         loss = torch.nn.functional.cross_entropy(m(x), t)
         loss.backward()
         losses.append(loss.item())
