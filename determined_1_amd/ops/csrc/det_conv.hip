@@ -31,6 +31,7 @@
 // (examples/computer_vision/*); semantics are torch.nn.functional.conv2d's.
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "det_stats.h"
@@ -348,6 +349,46 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // BNB: the epilogue's operand loads (BN input, shortcut gradient, mask bits) are issued before
+  // the K loop, so their HBM latency overlaps the GEMM instead of following it (these dgrads have
+  // short K loops and stream 3 activation-sized tensors through the epilogue)
+  constexpr int CPR = BN / 8;  // 16-B chunks per output row
+  const int64_t rows_left = a.M - m0;
+  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+  constexpr int NQE = BNB ? BM * CPR / kThreads : 1;
+  // hoisted only where the registers allow it (occupancy-2 tiles without the ABN staging: the
+  // others spill); elsewhere the loads are issued at the start of the epilogue
+  constexpr bool EPRE = BNB && OCC <= 2 && !ABN;
+  us8 xs[NQE], as[NQE];
+  unsigned bs[NQE];
+  auto eload = [&]() {
+    static_assert(!BNB || kThreads % CPR == 0, "fixed chunk column per thread");
+    const int c0 = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int q = 0; q < NQE; ++q) {
+      const int row = (tid + q * kThreads) / CPR;
+      const bool ok = row < nvalid;
+      const int64_t off = (m0 + (ok ? row : 0)) * a.N + c0;
+      xs[q] = ok ? *reinterpret_cast<const us8*>(a.bn.x + off) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+      as[q] = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (ok && a.bn.add) {
+        int64_t aoff = off;
+        bool on = true;
+        if (a.bn.add_hi > 0) {
+          const int64_t r = m0 + row, hw = static_cast<int64_t>(a.bn.add_hi) * a.bn.add_wi;
+          const int64_t img = r / hw;
+          const int rem = static_cast<int>(r - img * hw);
+          const int h = rem / a.bn.add_wi, w = rem - h * a.bn.add_wi;
+          on = ((h | w) & 1) == 0;
+          aoff = ((img * a.bn.add_ho + (h >> 1)) * a.bn.add_wo + (w >> 1)) * a.N + c0;
+        }
+        if (on) as[q] = *reinterpret_cast<const us8*>(a.bn.add + aoff);
+      }
+      bs[q] = (ok && a.bn.mode == 2) ? a.bn.mbits[off >> 3] : 0u;
+    }
+  };
+  if constexpr (EPRE) eload();
+
   const int nk = a.K / kBK;
   gload(0);
   lstore(0, 0);
@@ -379,8 +420,6 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
 
   // ---- epilogue: bf16 tile through LDS (coalesced 16-B row stores) + BN statistics ----
   unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
-  const int64_t rows_left = a.M - m0;
-  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -396,10 +435,8 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
                                                 static_cast<int64_t>(mt) * a.N + n0);
   }
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 16-B chunks per output row
   if constexpr (BNB) {
     // each thread owns one 8-column chunk (kThreads % CPR == 0) over rows tid/CPR + q*kThreads/CPR
-    static_assert(kThreads % CPR == 0, "fixed chunk column per thread");
     const int cc = tid % CPR;
     const int c0 = n0 + cc * 8;
     float mu[8], sc[8], sh[8], s1[8], s2[8];
@@ -411,34 +448,8 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       s1[j] = 0.f;
       s2[j] = 0.f;
     }
-    // all of this thread's loads (BN input, shortcut gradient, mask bits) are issued before the
-    // first store: the stores may alias them as far as the compiler knows, which would otherwise
-    // serialise every row on the HBM latency
-    constexpr int NQ = BM * CPR / kThreads;
-    us8 xs[NQ], as[NQ];
-    unsigned bs[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int row = (tid + q * kThreads) / CPR;
-      const bool ok = row < nvalid;
-      const int64_t off = (m0 + (ok ? row : 0)) * a.N + c0;
-      xs[q] = ok ? *reinterpret_cast<const us8*>(a.bn.x + off) : us8{0, 0, 0, 0, 0, 0, 0, 0};
-      as[q] = us8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (ok && a.bn.add) {
-        int64_t aoff = off;
-        bool on = true;
-        if (a.bn.add_hi > 0) {
-          const int64_t r = m0 + row, hw = static_cast<int64_t>(a.bn.add_hi) * a.bn.add_wi;
-          const int64_t img = r / hw;
-          const int rem = static_cast<int>(r - img * hw);
-          const int h = rem / a.bn.add_wi, w = rem - h * a.bn.add_wi;
-          on = ((h | w) & 1) == 0;
-          aoff = ((img * a.bn.add_ho + (h >> 1)) * a.bn.add_wo + (w >> 1)) * a.N + c0;
-        }
-        if (on) as[q] = *reinterpret_cast<const us8*>(a.bn.add + aoff);
-      }
-      bs[q] = (ok && a.bn.mode == 2) ? a.bn.mbits[off >> 3] : 0u;
-    }
+    constexpr int NQ = NQE;
+    if constexpr (!EPRE) eload();  // all loads before the first store (they may alias it)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int row = (tid + q * kThreads) / CPR;
@@ -867,7 +878,13 @@ int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64
   if (abn_x && (!abn_coef || !abn_out)) return -2;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool bt = b_kn != 0;
-  if (K == kBK) {
+  // K == 64 (one K tile): the occupancy-3 single-buffer variant, or (DET_BNB_SINGLE_OCC=0) the
+  // occupancy-2 one, whose BN-backward epilogue loads are issued before the K loop (EPRE)
+  static const bool single = [] {
+    const char* e = std::getenv("DET_BNB_SINGLE_OCC");
+    return !(e && e[0] == '0');
+  }();
+  if (K == kBK && (single || abn_x)) {
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, true, bt);
     return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, true, bt);
   }
