@@ -50,6 +50,9 @@ struct MasterConfig {
   std::string network_mode = "bridge";
   std::string dtrain_network_interface;  // "" = auto-detect
   std::string nccl_port_range, gloo_port_range;  // "MIN:MAX"
+  // logging.{type: default | elastic, host, port, index} (reference master/internal/config/elastic.go):
+  // with elastic, trial and task logs live in Elasticsearch instead of the local segments
+  Json logging;
   static MasterConfig FromJson(const Json& j);
   Json ToJson() const;
   std::vector<std::string> Validate() const;

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -71,10 +72,28 @@ class Store {
 // line per entry, with only the byte offset of each line kept in memory (8 B/line), so a long
 // HP search with millions of log lines costs disk, not master RSS.  Entry ids are 1-based line
 // numbers per stream (the cursor clients follow).  Memory-only when dir is empty (tests).
+// Remote log index behind a LogStore (reference master/internal/elastic/elastic_trial_logs.go:
+// trial logs in Elasticsearch instead of the database).  Rows carry the LogStore's per-stream id.
+class LogBackend {
+ public:
+  virtual ~LogBackend() = default;
+  virtual void Index(const std::string& stream, const std::vector<Json>& rows) = 0;
+  // Rows with after_id < id < before_id, `limit` of them from the low end (or the high end when
+  // desc), returned in ascending id order.
+  virtual std::vector<Json> Search(const std::string& stream, int64_t after_id, int64_t before_id, int64_t limit,
+                                   bool desc) = 0;
+  virtual int64_t MaxId(const std::string& stream) = 0;  // 0 for an empty / unknown stream
+  virtual void Delete(const std::string& stream) = 0;
+};
+// Elasticsearch backend over its REST API (_bulk / _search / _delete_by_query on one index).
+std::unique_ptr<LogBackend> MakeElasticLogBackend(const std::string& host, int port, const std::string& index);
+
 class LogStore {
  public:
   explicit LogStore(std::string dir = "");
   ~LogStore();
+  // Route every stream to `b` (local segments are then not written).
+  void SetBackend(std::unique_ptr<LogBackend> b) { backend_ = std::move(b); }
   // Appends rows to `stream`, setting row["id"]; returns the last id.
   int64_t Append(const std::string& stream, std::vector<Json> rows);
   // Entries with id > after_id passing `pred`, at most `limit` (the last `limit` when tail).
@@ -94,6 +113,9 @@ class LogStore {
   std::string dir_;
   mutable std::mutex mu_;
   std::map<std::string, Stream> streams_;
+  std::unique_ptr<LogBackend> backend_;
+  std::map<std::string, int64_t> remote_next_;  // next id per stream on the backend
+  int64_t RemoteMax(const std::string& stream);
 };
 
 }  // namespace detcore

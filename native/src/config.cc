@@ -294,6 +294,7 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
     c.tls_cert = j["security"]["tls"].get_string("cert", "");
     c.tls_key = j["security"]["tls"].get_string("key", "");
   }
+  if (j["logging"].is_object()) c.logging = j["logging"];
   const Json& tcd = j["task_container_defaults"];
   if (tcd.is_object()) {
     c.shm_size_bytes = tcd.get_int("shm_size_bytes", c.shm_size_bytes);
@@ -330,6 +331,13 @@ std::vector<std::string> MasterConfig::Validate() const {
   if (!ValidPortRange(gloo_port_range)) e.push_back("task_container_defaults.gloo_port_range must be \"MIN:MAX\"");
   if (tls_cert.empty() != tls_key.empty()) e.push_back("security.tls needs both cert and key");
   if (port <= 0 || port > 65535) e.push_back("port must be in 1..65535");
+  if (logging.is_object()) {
+    const std::string t = logging.get_string("type", "default");
+    if (t != "default" && t != "elastic") e.push_back("logging.type must be default or elastic");
+    if (t == "elastic" && logging.get_string("host", "").empty()) e.push_back("logging.host is required for elastic");
+    if (t == "elastic" && (logging.get_int("port", 9200) <= 0 || logging.get_int("port", 9200) > 65535))
+      e.push_back("logging.port must be in 1..65535");
+  }
   return e;
 }
 
@@ -340,7 +348,7 @@ std::vector<std::string> MasterConfig::EnvPaths() {
           "checkpoint_storage.type", "checkpoint_storage.host_path", "checkpoint_storage.storage_path",
           "checkpoint_storage.bucket", "checkpoint_storage.save_experiment_best",
           "checkpoint_storage.save_trial_best", "checkpoint_storage.save_trial_latest", "telemetry.file",
-          "telemetry.enabled", "scheduler.type", "scheduler.fitting_policy", "resource_pools"};
+          "telemetry.enabled", "logging.type", "logging.host", "logging.port", "scheduler.type", "scheduler.fitting_policy", "resource_pools"};
 }
 
 Json MasterConfig::ToJson() const {
@@ -380,6 +388,11 @@ Json MasterConfig::ToJson() const {
   tcd["nccl_port_range"] = nccl_port_range;
   tcd["gloo_port_range"] = gloo_port_range;
   j["task_container_defaults"] = tcd;
+  if (logging.is_object()) {
+    j["logging"] = logging;
+  } else {
+    j["logging"]["type"] = "default";
+  }
   return j;
 }
 

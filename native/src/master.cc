@@ -190,6 +190,10 @@ Json CheckpointsToGC(Store& store, int64_t experiment_id, const Json& cfg) {
 Master::Master(MasterConfig cfg) : cfg_(std::move(cfg)) {
   store_ = std::make_unique<Store>(cfg_.store_dir);
   logs_ = std::make_unique<LogStore>(cfg_.store_dir.empty() ? std::string() : cfg_.store_dir + "/logs");
+  if (cfg_.logging.is_object() && cfg_.logging.get_string("type", "default") == "elastic")
+    logs_->SetBackend(MakeElasticLogBackend(cfg_.logging.get_string("host", ""),
+                                            static_cast<int>(cfg_.logging.get_int("port", 9200)),
+                                            cfg_.logging.get_string("index", "determined-logs")));
   sys_ = std::make_unique<actor::System>(8);
   Json cid;
   if (store_->Get("cluster_id", 1, &cid)) {

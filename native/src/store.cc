@@ -7,6 +7,8 @@
 #include <dirent.h>
 
 #include <algorithm>
+#include <climits>
+#include <iterator>
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
@@ -285,8 +287,21 @@ LogStore::Stream& LogStore::Open(const std::string& stream) {
   return s;
 }
 
+int64_t LogStore::RemoteMax(const std::string& stream) {
+  auto it = remote_next_.find(stream);
+  if (it == remote_next_.end()) it = remote_next_.emplace(stream, backend_->MaxId(stream) + 1).first;
+  return it->second - 1;
+}
+
 int64_t LogStore::Append(const std::string& stream, std::vector<Json> rows) {
   std::lock_guard<std::mutex> g(mu_);
+  if (backend_) {
+    int64_t id = RemoteMax(stream);
+    for (auto& r : rows) r["id"] = ++id;
+    backend_->Index(stream, rows);
+    remote_next_[stream] = id + 1;
+    return id;
+  }
   Stream& s = Open(stream);
   std::string buf;
   for (auto& r : rows) {
@@ -310,8 +325,39 @@ int64_t LogStore::Append(const std::string& stream, std::vector<Json> rows) {
 std::vector<Json> LogStore::Read(const std::string& stream, int64_t after_id, int64_t limit,
                                  const std::function<bool(const Json&)>& pred, bool tail) {
   std::lock_guard<std::mutex> g(mu_);
-  Stream& s = Open(stream);
   std::vector<Json> out;
+  if (backend_) {
+    if (after_id < 0) after_id = 0;
+    if (limit <= 0) return out;
+    const int64_t page = std::min<int64_t>(std::max<int64_t>(limit, 256), 5000);
+    if (!tail) {  // ascending pages from after_id until `limit` rows pass the filter
+      for (int64_t cur = after_id;;) {
+        auto rows = backend_->Search(stream, cur, INT64_MAX, page, false);
+        for (auto& r : rows) {
+          cur = r.get_int("id", cur);
+          if (pred && !pred(r)) continue;
+          out.push_back(std::move(r));
+          if (static_cast<int64_t>(out.size()) >= limit) return out;
+        }
+        if (static_cast<int64_t>(rows.size()) < page) return out;
+      }
+    }
+    // tail: descending pages from the end until `limit` rows pass the filter
+    std::vector<Json> rev;
+    for (int64_t before = INT64_MAX;;) {
+      auto rows = backend_->Search(stream, after_id, before, page, true);
+      for (auto it = rows.rbegin(); it != rows.rend(); ++it) {
+        before = it->get_int("id", before);
+        if (pred && !pred(*it)) continue;
+        rev.push_back(std::move(*it));
+        if (static_cast<int64_t>(rev.size()) >= limit) break;
+      }
+      if (static_cast<int64_t>(rev.size()) >= limit || static_cast<int64_t>(rows.size()) < page) break;
+    }
+    out.assign(std::make_move_iterator(rev.rbegin()), std::make_move_iterator(rev.rend()));
+    return out;
+  }
+  Stream& s = Open(stream);
   const int64_t n = static_cast<int64_t>(s.offsets.size());
   if (after_id < 0) after_id = 0;
   if (after_id >= n || limit <= 0) return out;
@@ -340,6 +386,7 @@ std::vector<Json> LogStore::Read(const std::string& stream, int64_t after_id, in
 
 int64_t LogStore::Count(const std::string& stream) const {
   std::lock_guard<std::mutex> g(mu_);
+  if (backend_) return const_cast<LogStore*>(this)->RemoteMax(stream);
   auto it = streams_.find(stream);
   if (it != streams_.end()) return static_cast<int64_t>(it->second.offsets.size());
   return const_cast<LogStore*>(this)->Open(stream).offsets.size();
@@ -347,6 +394,11 @@ int64_t LogStore::Count(const std::string& stream) const {
 
 void LogStore::Delete(const std::string& stream) {
   std::lock_guard<std::mutex> g(mu_);
+  if (backend_) {
+    backend_->Delete(stream);
+    remote_next_.erase(stream);
+    return;
+  }
   streams_.erase(stream);
   if (!dir_.empty()) ::unlink(Path(stream).c_str());
 }
