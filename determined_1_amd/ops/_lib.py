@@ -110,7 +110,7 @@ _SIGNATURES = {
     # stream, dtype, x, y, idx(u8), N, H, W, C
     "det_maxpool3s2_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
     # stream, dtype, dy, idx(u8), dx, N, H, W, C
-    "det_maxpool3s2_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
+    "det_maxpool3s2_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
     "det_bn_apply": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, dy, x, mask_bits, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws

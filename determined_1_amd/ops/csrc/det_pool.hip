@@ -111,9 +111,12 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x,
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy, const uint8_t* __restrict__ idx,
-                                                        T* __restrict__ dx, PoolGeom g, int64_t nvec) {
+// kTwo: a second upstream gradient dy2 of the pooled output (a linked projection shortcut that also
+// reads it, ops/norm.py linked_conv2d) is summed in the gather instead of by a separate add pass.
+template <typename T, bool kTwo>
+__global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                        const uint8_t* __restrict__ idx, T* __restrict__ dx, PoolGeom g,
+                                                        int64_t nvec) {
   const int cv = g.C / 8;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
        i += static_cast<int64_t>(gridDim.x) * kThreads) {
@@ -145,6 +148,12 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy
         if (!any) continue;
         float d[8];
         Vec8<T>::load(dy + o, d);
+        if constexpr (kTwo) {
+          float d2[8];
+          Vec8<T>::load(dy2 + o, d2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] += d2[j];
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += av[j] == me ? d[j] : 0.f;
       }
@@ -179,19 +188,32 @@ int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t*
   return static_cast<int>(hipGetLastError());
 }
 
-// dy [N, Ho, Wo, C], idx from the forward -> dx [N, H, W, C] (fully overwritten).
-int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const uint8_t* idx, void* dx, int N, int H, int W,
-                       int C) {
+// dy [N, Ho, Wo, C] (+ optional dy2 of the same shape, summed), idx from the forward -> dx [N, H, W, C]
+// (fully overwritten).
+int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int N,
+                       int H, int W, int C) {
   if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0) return -1;
   PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
   const int64_t nvec = static_cast<int64_t>(N) * H * W * (C / 8);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (dtype == 1)
-    hipLaunchKernelGGL(maxpool_bwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
-                       static_cast<const unsigned short*>(dy), idx, static_cast<unsigned short*>(dx), g, nvec);
-  else
-    hipLaunchKernelGGL(maxpool_bwd<float>, dim3(grid_for(nvec)), dim3(kThreads), 0, st, static_cast<const float*>(dy),
-                       idx, static_cast<float*>(dx), g, nvec);
+  const dim3 grid(grid_for(nvec)), block(kThreads);
+  if (dtype == 1) {
+    auto* a = static_cast<const unsigned short*>(dy);
+    auto* b = static_cast<const unsigned short*>(dy2);
+    auto* o = static_cast<unsigned short*>(dx);
+    if (dy2)
+      hipLaunchKernelGGL((maxpool_bwd<unsigned short, true>), grid, block, 0, st, a, b, idx, o, g, nvec);
+    else
+      hipLaunchKernelGGL((maxpool_bwd<unsigned short, false>), grid, block, 0, st, a, b, idx, o, g, nvec);
+  } else {
+    auto* a = static_cast<const float*>(dy);
+    auto* b = static_cast<const float*>(dy2);
+    auto* o = static_cast<float*>(dx);
+    if (dy2)
+      hipLaunchKernelGGL((maxpool_bwd<float, true>), grid, block, 0, st, a, b, idx, o, g, nvec);
+    else
+      hipLaunchKernelGGL((maxpool_bwd<float, false>), grid, block, 0, st, a, b, idx, o, g, nvec);
+  }
   return static_cast<int>(hipGetLastError());
 }
 

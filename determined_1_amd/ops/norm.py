@@ -13,6 +13,8 @@ composite path and are counted in ``FALLBACKS`` so a benchmark can assert it sta
 """
 from typing import Optional, Tuple
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -256,6 +258,18 @@ def _observed(x: torch.Tensor) -> bool:
     return bool(x.retains_grad or getattr(x, "_backward_hooks", None))
 
 
+# Link a stride-1 projection of the stem max-pool output (ResNet layer1) to the pool's backward,
+# which sums the shortcut's input gradient in its gather kernel (no separate autograd add pass).
+MAXPOOL_LINK = os.environ.get("DET_MAXPOOL_LINK", "0") == "1"  # off until its A/B is measured on hardware
+
+
+def _maxpool_link_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    from determined_1_amd.ops import pool as _pool
+
+    return (MAXPOOL_LINK and isinstance(x.grad_fn, _pool._MaxPool3s2._backward_cls)
+            and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (0, 0) and conv.kernel_size == (1, 1))
+
+
 def linked_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)``; when ``x`` came from the fused BN-act op and feeds another consumer too, the
     conv's input gradient is summed inside the producer's BN-backward kernels (``_LinkedConv``).
@@ -268,7 +282,7 @@ def linked_conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     _conv.materialize_fwd_apply(x)
     if (SHORTCUT_LINK and conv.bias is None and torch.is_grad_enabled() and x.requires_grad
             and not _observed(x)
-            and isinstance(x.grad_fn, _BNActTrain._backward_cls) and x.dim() == 4
+            and (isinstance(x.grad_fn, _BNActTrain._backward_cls) or _maxpool_link_ok(x, conv)) and x.dim() == 4
             and x.dtype == conv.weight.dtype and _autocast_keeps(x)
             and x.is_contiguous(memory_format=torch.channels_last) and conv.padding_mode == "zeros"
             and getattr(x.grad_fn, "extra_dy", None) is None):

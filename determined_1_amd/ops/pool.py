@@ -11,6 +11,7 @@ import torch.nn.functional as F
 from determined_1_amd.ops import _lib
 
 FALLBACKS = {"count": 0}
+LINKED = {"count": 0}  # backward passes that summed a linked shortcut gradient
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
@@ -38,10 +39,23 @@ class _MaxPool3s2(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         N, C, H, W = ctx.shape
         dy = dy.contiguous(memory_format=torch.channels_last)
+        # a linked projection shortcut of the pooled output (ops/norm.py linked_conv2d, ResNet layer1)
+        # handed its input gradient here instead of to autograd: summed in the gather kernel
+        extra, ctx.extra_dy = getattr(ctx, "extra_dy", None), None
+        if extra is not None:
+            if not isinstance(extra, torch.Tensor):
+                from determined_1_amd.ops.conv import full_res_grad
+
+                extra = full_res_grad(extra)
+            extra = extra.to(dy.dtype).contiguous(memory_format=torch.channels_last)
+            if extra.shape != dy.shape:
+                raise RuntimeError(f"linked max-pool gradient shape {tuple(extra.shape)} != {tuple(dy.shape)}")
+            LINKED["count"] += 1
         dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         st = torch._C._cuda_getCurrentRawStream(dy.device.index)
-        _lib.check(_lib.get_lib().det_maxpool3s2_bwd(st, _DT[dy.dtype], dy.data_ptr(), idx.data_ptr(), dx.data_ptr(),
-                                                     N, H, W, C), "det_maxpool3s2_bwd")
+        _lib.check(_lib.get_lib().det_maxpool3s2_bwd(st, _DT[dy.dtype], dy.data_ptr(),
+                                                     None if extra is None else extra.data_ptr(), idx.data_ptr(),
+                                                     dx.data_ptr(), N, H, W, C), "det_maxpool3s2_bwd")
         return dx
 
 

@@ -28,3 +28,47 @@ def test_maxpool3s2_matches_torch(gpu, N, C, H, W, dt):
     # fp32: up to 4 overlapping windows summed in a different order than torch's scatter
     tol = dict(atol=1e-6, rtol=1e-5) if dt == torch.float32 else dict(atol=2e-2, rtol=1e-2)
     torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, **tol)
+
+
+@pytest.mark.parametrize("native_shortcut", [True, False])
+def test_maxpool_linked_projection_gradient(gpu, native_shortcut, monkeypatch):
+    """ResNet layer1: the pooled stem output feeds conv1 and a stride-1 projection shortcut; the
+    shortcut's input gradient is linked to the pool's backward (ops/norm.py linked_conv2d) and summed
+    in its gather kernel.  Checked against the fp32 CPU composite with autograd's add."""
+    from determined_1_amd.ops import conv as convops
+    from determined_1_amd.ops import norm
+
+    monkeypatch.setattr(norm, "MAXPOOL_LINK", True)
+    torch.manual_seed(0)
+    N, C, H, W, Co = 8, 64, 56, 56, 256
+    x = torch.randn(N, C, H, W).to(torch.bfloat16).float()
+    w1 = (torch.randn(64, C, 1, 1) / C ** 0.5).to(torch.bfloat16)
+    ws = (torch.randn(Co, C, 1, 1) / C ** 0.5).to(torch.bfloat16)
+    g1 = torch.randn(N, 64, H // 2, W // 2).to(torch.bfloat16)
+    gs = torch.randn(N, Co, H // 2, W // 2).to(torch.bfloat16)
+
+    ref_in = x.clone().requires_grad_(True)
+    p = F.max_pool2d(ref_in, 3, 2, 1)
+    ((F.conv2d(p, w1.float()) * g1.float()).sum() + (F.conv2d(p, ws.float()) * gs.float()).sum()).backward()
+    ref_x = ref_in.grad
+
+    conv1 = torch.nn.Conv2d(C, 64, 1, bias=False).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    sc = torch.nn.Conv2d(C, Co, 1, bias=False).to(gpu, torch.bfloat16).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv1.weight.copy_(w1)
+        sc.weight.copy_(ws)
+    dut_in = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    pooled = pool.max_pool_3x3s2(dut_in)
+    old = convops.ENABLED
+    linked_before = pool.LINKED["count"]
+    try:
+        if not native_shortcut:
+            convops.ENABLED = False  # _LinkedConv (MIOpen conv) path instead of the native shortcut
+        ys = norm.linked_conv2d(pooled, sc)
+        y1 = conv1(pooled)
+        torch.autograd.backward([y1, ys], [g1.to(gpu).contiguous(memory_format=torch.channels_last),
+                                           gs.to(gpu).contiguous(memory_format=torch.channels_last)])
+    finally:
+        convops.ENABLED = old
+    assert pool.LINKED["count"] == linked_before + 1, "shortcut gradient was not linked to the pool"
+    torch.testing.assert_close(dut_in.grad.float().cpu(), ref_x, atol=5e-2, rtol=2e-2)
