@@ -32,6 +32,7 @@ class _MaxPool3s2(torch.autograd.Function):
                                                      N, H, W, C), "det_maxpool3s2_fwd")
         ctx.save_for_backward(idx)
         ctx.shape = (N, C, H, W)
+        ctx.extra_dy = None  # set by a linked shortcut consumer (ops/norm.py linked_conv2d)
         return y
 
     @staticmethod
