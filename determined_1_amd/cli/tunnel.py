@@ -31,10 +31,17 @@ def _split_master(master: str):
     return (host or m), int(port or 8080)
 
 
-def open_tunnel(master: str, service: str, tls: Optional[bool] = None) -> WebSocket:
+def open_tunnel(master: str, service: str, tls: Optional[bool] = None, token: Optional[str] = None) -> WebSocket:
+    """The tunnel WebSocket to ``service``.  The master gates the upgrade on the session like any
+    user route (``--require-auth``): the token is the CLI's saved login for ``master`` (or
+    ``DET_USER_TOKEN``) unless given."""
+    from determined_1_amd.api.request import _load_token
+
     host, port = _split_master(master)
     svc = service if service.startswith("cmd-") else f"cmd-{service}"
-    return WebSocket(host, port, f"/proxy/{svc}/", timeout=30.0, tls=tls)
+    tok = token if token is not None else _load_token(master)
+    headers = {"Authorization": f"Bearer {tok}"} if tok else None
+    return WebSocket(host, port, f"/proxy/{svc}/", timeout=30.0, tls=tls, headers=headers)
 
 
 def splice(ws: WebSocket, read: Callable[[], bytes], write: Callable[[bytes], None],

@@ -10,7 +10,7 @@ import os
 import socket
 import struct
 import threading
-from typing import Optional
+from typing import Dict, Optional
 
 
 class WebSocketError(RuntimeError):
@@ -19,9 +19,10 @@ class WebSocketError(RuntimeError):
 
 class WebSocket:
     def __init__(self, host: str, port: int, path: str, timeout: Optional[float] = 30.0,
-                 tls: Optional[bool] = None) -> None:
+                 tls: Optional[bool] = None, headers: Optional[Dict[str, str]] = None) -> None:
         """``tls=None``: TLS iff the task/CLI environment says the master speaks it (``DET_USE_TLS``,
-        ``DET_MASTER_CERT_FILE``; ``DET_MASTER_CERT_NAME`` overrides the name checked)."""
+        ``DET_MASTER_CERT_FILE``; ``DET_MASTER_CERT_NAME`` overrides the name checked).  ``headers``:
+        extra request headers of the upgrade (e.g. ``Authorization`` for auth-gated sockets)."""
         raw = socket.create_connection((host, port), timeout=timeout)
         raw.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         if tls is None:
@@ -34,7 +35,8 @@ class WebSocket:
         self.sock = raw
         key = base64.b64encode(os.urandom(16)).decode()
         req = (f"GET {path} HTTP/1.1\r\nHost: {host}:{port}\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
-               f"Sec-WebSocket-Key: {key}\r\nSec-WebSocket-Version: 13\r\n\r\n")
+               f"Sec-WebSocket-Key: {key}\r\nSec-WebSocket-Version: 13\r\n"
+               + "".join(f"{k}: {v}\r\n" for k, v in (headers or {}).items()) + "\r\n")
         self.sock.sendall(req.encode())
         self._buf = b""
         while b"\r\n\r\n" not in self._buf:

@@ -6,6 +6,7 @@ format, which is the layout MIOpen's fastest bf16 convolution/batch-norm kernels
 gfx950, and the input pipeline kernel (``ops.u8_normalize``) produces NHWC directly.
 ``zero_init_residual`` zeroes the last BN gamma of each block (standard large-batch recipe).
 """
+import threading
 from typing import List, Optional, Type, Union
 
 import torch
@@ -21,6 +22,22 @@ FUSED_BN = True
 # Stride-1 1x1 convs as hand-written MFMA GEMMs with the BN statistics in the forward epilogue
 # (ops/csrc/det_conv.hip); hparam ``native_conv1x1: false`` keeps them on MIOpen (A/B).
 NATIVE_CONV1X1 = True
+
+# Deferred BN forward applies (ops.conv DEFER_FWD_APPLY) hand the NEXT block an unwritten output
+# buffer that its conv1 fills while staging its GEMM operand.  Only this file's own code may see such
+# a buffer, so a block defers only inside ResNet.forward (blocks called one by one from user code
+# never do) and only while no forward hook, forward pre-hook of its successor, or global module hook
+# could observe the intermediate output (feature extraction, activation statistics, TensorBoard
+# histogram callbacks).
+_FWD = threading.local()
+
+
+def _unobserved(block: nn.Module, nxt: Optional[nn.Module]) -> bool:
+    from torch.nn.modules import module as _m
+
+    if block._forward_hooks or _m._global_forward_hooks or _m._global_forward_pre_hooks:
+        return False
+    return nxt is None or not (nxt._forward_pre_hooks or nxt._forward_hooks)
 # Bottleneck bn2 applied inside conv3's GEMM prologue (stats-only BN pass, no normalised
 # activation in HBM).  Off by default: measured 1.1 % slower end to end on the MI355X (9,949 vs
 # 10,056 samples/s, profiles/r2_bench_resnet50_bn_prologue_ab.jsonl) -- the prologue's VALU work
@@ -124,6 +141,7 @@ class Bottleneck(nn.Module):
         # set by ResNet when the next block is an identity-shortcut Bottleneck, whose conv1 is the
         # first reader of this block's output and stages bn3's apply itself (ops.conv DEFER_FWD_APPLY)
         self.defer_out = False
+        self._defer_next: List[nn.Module] = []  # [successor block] (a list: not registered as a submodule)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # x (the previous block's output) reaches autograd only through conv1: the shortcut's
@@ -135,8 +153,9 @@ class Bottleneck(nn.Module):
         # whose epilogue sums it into the producer's BN-backward partials
         idt = x if self.downsample is None else _shortcut(self.downsample, x)
         # identity shortcut: its gradient goes straight to the previous block's fused BN backward
-        return self.bn3(out, idt, shortcut_link=self.downsample is None,
-                        defer_apply=self.defer_out and NATIVE_CONV1X1 and FUSED_BN)
+        defer = (self.defer_out and NATIVE_CONV1X1 and FUSED_BN and getattr(_FWD, "depth", 0) > 0
+                 and _unobserved(self, self._defer_next[0] if self._defer_next else None))
+        return self.bn3(out, idt, shortcut_link=self.downsample is None, defer_apply=defer)
 
 
 class ResNet(nn.Module):
@@ -180,6 +199,7 @@ class ResNet(nn.Module):
         for blk, nxt in zip(layers[:-1], layers[1:]):  # identity-shortcut successor: conv1 reads first
             if isinstance(blk, Bottleneck) and isinstance(nxt, Bottleneck) and nxt.downsample is None:
                 blk.defer_out = True
+                blk._defer_next = [nxt]
         return nn.Sequential(*layers)
 
     def _stem(self, x: torch.Tensor) -> torch.Tensor:
@@ -189,8 +209,12 @@ class ResNet(nn.Module):
         return self.conv1(x[:, :3] if x.shape[1] == 4 and self.conv1.in_channels == 3 else x)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self._stem(x)))
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        _FWD.depth = getattr(_FWD, "depth", 0) + 1  # blocks may defer their output applies (see _FWD)
+        try:
+            x = self.maxpool(self.bn1(self._stem(x)))
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        finally:
+            _FWD.depth -= 1
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 

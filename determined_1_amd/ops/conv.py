@@ -979,9 +979,9 @@ class _Shortcut1x1(torch.autograd.Function):
             dxs = dgrad_1x1(dy2, w2).view(n, ho, wo, c).permute(0, 3, 1, 2)  # on the output grid
             extra = StridedGrad(dxs, g) if st == 2 else dxs
             if link is not None:
-                if link.extra_dy is not None:
-                    raise RuntimeError("second upstream gradient linked twice to one producer")
-                link.extra_dy = extra
+                from determined_1_amd.ops.norm import hand_linked_grad
+
+                hand_linked_grad(link, extra)
             else:
                 dx = full_res_grad(extra)
         if ctx.needs_input_grad[1]:

@@ -23,7 +23,7 @@ from determined_1_amd.ops import _lib
 from determined_1_amd.ops import conv as _conv
 
 FALLBACKS = {"count": 0}
-SHORTCUT_LINK = True  # identity-shortcut gradients through the producer's BN backward (A/B switch)
+SHORTCUT_LINK = os.environ.get("DET_SHORTCUT_LINK", "1") != "0"  # identity-shortcut gradients through the producer's BN backward (A/B switch)
 _SYNC_DEBUG = bool(__import__("os").environ.get("DET_SYNC_DEBUG"))
 
 
@@ -201,9 +201,7 @@ class _BNActTrain(torch.autograd.Function):
         if ctx.link is not None:
             # the producer runs later (its output also feeds our block's first conv, whose input
             # gradient it waits for); it sums dres in its own backward kernels
-            if ctx.link.extra_dy is not None:
-                raise RuntimeError("identity-shortcut gradient linked twice to one producer")
-            ctx.link.extra_dy = dres
+            hand_linked_grad(ctx.link, dres)
             ctx.link = None
             dres = None
         dw = dgb[0] if dgb is not None and ctx.needs_input_grad[2] else None
@@ -238,9 +236,7 @@ class _LinkedConv(torch.autograd.Function):
         link, ctx.link = ctx.link, None
         if link is None:  # a repeated backward (retain_graph): plain autograd accumulation
             return dx, dw, None, None, None, None, None
-        if link.extra_dy is not None:
-            raise RuntimeError("second upstream gradient linked twice to one producer")
-        link.extra_dy = dx.contiguous(memory_format=torch.channels_last)
+        hand_linked_grad(link, dx.contiguous(memory_format=torch.channels_last))
         return None, dw, None, None, None, None, None
 
 
@@ -258,9 +254,37 @@ def _observed(x: torch.Tensor) -> bool:
     return bool(x.retains_grad or getattr(x, "_backward_hooks", None))
 
 
+def hand_linked_grad(link, grad) -> None:
+    """Hand ``grad`` (a second upstream gradient of ``link``'s output) to the producer node ``link``,
+    whose backward sums it in its own kernels, and check at the end of this backward pass that the
+    producer did run and consume it.  It does not when autograd stops at the linked activation
+    (``torch.autograd.grad(loss, x)`` / ``backward(inputs=[x])``): the gradient autograd reports for
+    ``x`` would then silently lack this consumer's share, so the pass raises instead (and the stale
+    gradient is dropped, never summed into a later backward).  ``DET_SHORTCUT_LINK=0`` turns the
+    links off for code that needs such partial gradients."""
+    if link.extra_dy is not None:
+        raise RuntimeError("second upstream gradient linked twice to one producer")
+    link.extra_dy = grad
+
+    def check() -> None:
+        if getattr(link, "extra_dy", None) is not None:
+            link.extra_dy = None
+            LINK_COUNTS["unconsumed"] += 1
+            raise RuntimeError(
+                "a linked shortcut gradient was not consumed: autograd stopped at an activation whose "
+                "gradient is summed inside its producer's backward (torch.autograd.grad / backward(inputs=) "
+                "on a fused ResNet activation). Set DET_SHORTCUT_LINK=0 to compute such partial gradients.")
+
+    torch.autograd.Variable._execution_engine.queue_callback(check)
+
+
+LINK_COUNTS = {"unconsumed": 0}
+
+
 # Link a stride-1 projection of the stem max-pool output (ResNet layer1) to the pool's backward,
 # which sums the shortcut's input gradient in its gather kernel (no separate autograd add pass).
-MAXPOOL_LINK = os.environ.get("DET_MAXPOOL_LINK", "0") == "1"  # off until its A/B is measured on hardware
+# measured on: +0.16 % (3 interleaved pairs, every pair positive; profiles/r4_maxpool_link_ab.jsonl)
+MAXPOOL_LINK = os.environ.get("DET_MAXPOOL_LINK", "1") == "1"
 
 
 def _maxpool_link_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:

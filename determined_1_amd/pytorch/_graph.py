@@ -22,7 +22,8 @@ capture.  What is NOT in the graph and is handled on the host:
 
 Requirements on user code (documented in the README): ``train_batch`` must not branch on host
 values other than the epoch index and must not synchronise (``.item()``) -- the same contract as
-CUDA graphs.  Eligibility is checked once: one process (no data-parallel bucketer), aggregation
+CUDA graphs.  A ``train_batch`` that reads ``batch_idx`` at all runs eagerly (checked from its
+bytecode by ``reads_argument``, logged once).  Eligibility is checked once: one process (no data-parallel bucketer), aggregation
 frequency 1, no dynamic loss scaler, every optimizer fused with step-invariant kernel arguments.
 Anything else runs eagerly, logged once.
 
@@ -435,6 +436,10 @@ def build(context: Any, train_batch: Callable[..., Any], enabled: bool,
     if not enabled:
         return None, None
     reason = TrainStepGraph.ineligible_reason(context)
+    if reason is None and reads_argument(train_batch, "batch_idx"):
+        # a replay re-runs the captured kernels with the batch_idx of the capture: a train_batch
+        # that branches on it (or feeds it to a kernel) would train silently wrong
+        reason = "train_batch reads batch_idx (a graph replay would reuse the captured value)"
     if reason is not None:
         logging.warning("optimizations.hip_graph is set but train_batch will run eagerly: %s", reason)
         return None, reason

@@ -104,8 +104,10 @@ class HttpServer {
   ~HttpServer();
   // Pattern segments starting with ':' capture; a trailing "*" matches the rest.
   void Route(const std::string& method, const std::string& pattern, Handler h);
-  void RouteWs(const std::string& pattern, WsHandler h);
-  // Optional authorisation hook for plain HTTP routes: return false -> 401.
+  // require_auth: the auth hook (SetAuth) also gates the upgrade (401 before switching protocols);
+  // used for user-facing sockets (the TCP tunnel), not for agent / trial sockets.
+  void RouteWs(const std::string& pattern, WsHandler h, bool require_auth = false);
+  // Optional authorisation hook for plain HTTP routes (and auth-gated WebSocket routes): false -> 401.
   void SetAuth(std::function<bool(const Request&)> auth) { auth_ = std::move(auth); }
   // Serve every connection over TLS with this PEM certificate chain and key (call before Start).
   bool EnableTls(const std::string& cert_file, const std::string& key_file, std::string* error);
@@ -126,6 +128,7 @@ class HttpServer {
     std::vector<std::string> segs;
     Handler h;
     WsHandler ws;
+    bool ws_auth = false;
   };
   bool Match(const RouteEntry& r, const std::vector<std::string>& segs, std::map<std::string, std::string>* params) const;
   const RouteEntry* Find(Request* req, bool want_ws, bool* path_hit) const;

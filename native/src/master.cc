@@ -1092,8 +1092,9 @@ void Master::InstallRoutes() {
     up.join();
     ::close(fd);
   };
-  http_.RouteWs("/proxy/:task/*", tunnel);
-  http_.RouteWs("/proxy/:task", tunnel);
+  // a raw TCP stream into a task's service: gated by the same session check as /proxy
+  http_.RouteWs("/proxy/:task/*", tunnel, /*require_auth=*/true);
+  http_.RouteWs("/proxy/:task", tunnel, /*require_auth=*/true);
   http_.Route("GET", "/commands/:id", [this](const net::Request& r) {
     Json c;
     if (!store_->Get("commands", IntParam(r, "id"), &c)) return Err(404, "command not found");

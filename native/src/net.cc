@@ -132,10 +132,17 @@ std::string UrlDecode(const std::string& s) {
 // while other threads send), waiting in poll() -- never inside the lock -- for WANT_READ /
 // WANT_WRITE.  Plain fds take the old blocking send/recv paths untouched.
 namespace {
+// The SSL object lives as long as the last reference to its TlsConn: a thread that looked the
+// connection up before another thread closed the fd (a WebSocket ReadLoop woken by the shutdown()
+// of WsConn::Close) still holds a valid SSL*, and sees `closed` instead of a freed pointer.
 struct TlsConn {
   SSL* ssl = nullptr;
+  bool closed = false;
   std::mutex mu;
   int rcv_timeout_ms = -1;  // emulates SO_RCVTIMEO for client calls
+  ~TlsConn() {
+    if (ssl) SSL_free(ssl);
+  }
 };
 std::mutex g_tls_mu;
 std::unordered_map<int, std::shared_ptr<TlsConn>> g_tls;
@@ -172,6 +179,7 @@ int TlsCall(TlsConn* t, int fd, F op, int timeout_ms) {
     int r, err;
     {
       std::lock_guard<std::mutex> g(t->mu);
+      if (t->closed || !t->ssl) return -1;  // closed by another thread
       ERR_clear_error();
       r = op(t->ssl);
       if (r > 0) return r;
@@ -198,8 +206,14 @@ bool AttachTls(int fd, SSL_CTX* ctx, bool server, const std::string& server_name
   }
   SSL_set_fd(ssl, fd);
   if (!server && !server_name.empty()) {
-    SSL_set_tlsext_host_name(ssl, server_name.c_str());
-    SSL_set1_host(ssl, server_name.c_str());
+    // SNI for names only; the certificate must match the name (or the literal IP) that was dialed
+    in6_addr a6;
+    in_addr a4;
+    const bool is_ip = inet_pton(AF_INET, server_name.c_str(), &a4) == 1 || inet_pton(AF_INET6, server_name.c_str(), &a6) == 1;
+    if (!is_ip) SSL_set_tlsext_host_name(ssl, server_name.c_str());
+    X509_VERIFY_PARAM* vp = SSL_get0_param(ssl);
+    if (is_ip) X509_VERIFY_PARAM_set1_ip_asc(vp, server_name.c_str());
+    else SSL_set1_host(ssl, server_name.c_str());
   }
   fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK);
   auto t = std::make_shared<TlsConn>();
@@ -207,8 +221,7 @@ bool AttachTls(int fd, SSL_CTX* ctx, bool server, const std::string& server_name
   int r = TlsCall(t.get(), fd, [server](SSL* s) { return server ? SSL_accept(s) : SSL_connect(s); }, timeout_ms);
   if (r <= 0) {
     if (error) *error = "tls handshake failed: " + SslErrors();
-    SSL_free(ssl);
-    return false;
+    return false;  // ~TlsConn frees the SSL
   }
   std::lock_guard<std::mutex> g(g_tls_mu);
   g_tls[fd] = t;
@@ -228,9 +241,8 @@ static void CloseFd(int fd) {
   }
   if (t) {
     std::lock_guard<std::mutex> g(t->mu);
-    SSL_shutdown(t->ssl);  // best effort close_notify; non-blocking
-    SSL_free(t->ssl);
-    t->ssl = nullptr;
+    if (!t->closed && t->ssl) SSL_shutdown(t->ssl);  // best effort close_notify; non-blocking
+    t->closed = true;  // the SSL itself is freed with the last TlsConn reference
   }
   ::close(fd);
 }
@@ -335,7 +347,9 @@ static int ConnectMaybeTls(const std::string& host, int port, int timeout_ms, st
   if (fd < 0) return fd;
   std::string name;
   if (SSL_CTX* ctx = EndpointCtx(host, port, &name)) {
-    if (!AttachTls(fd, ctx, false, name, timeout_ms, error)) {
+    // the peer certificate is checked against --master-cert-name when given, else against the
+    // host that was dialed (a chain-only check accepted any trusted certificate)
+    if (!AttachTls(fd, ctx, false, name.empty() ? host : name, timeout_ms, error)) {
       ::close(fd);
       return -1;
     }
@@ -563,8 +577,8 @@ void HttpServer::Route(const std::string& method, const std::string& pattern, Ha
   routes_.push_back(RouteEntry{method, SplitPath(pattern), std::move(h), nullptr});
 }
 
-void HttpServer::RouteWs(const std::string& pattern, WsHandler h) {
-  routes_.push_back(RouteEntry{"GET", SplitPath(pattern), nullptr, std::move(h)});
+void HttpServer::RouteWs(const std::string& pattern, WsHandler h, bool require_auth) {
+  routes_.push_back(RouteEntry{"GET", SplitPath(pattern), nullptr, std::move(h), require_auth});
 }
 
 bool HttpServer::Match(const RouteEntry& r, const std::vector<std::string>& segs,
@@ -720,6 +734,13 @@ void HttpServer::Serve(int fd, std::string peer) {
     bool path_hit = false;
     bool want_ws = Lower(req.headers["upgrade"]) == "websocket";
     const RouteEntry* hit = Find(&req, want_ws, &path_hit);
+    if (hit && hit->ws && hit->ws_auth && auth_ && !auth_(req)) {
+      const std::string body = R"({"error":"unauthenticated: log in with POST /login"})";
+      std::string resp = "HTTP/1.1 401 Unauthorized\r\nContent-Type: application/json\r\nContent-Length: " +
+                         std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body;
+      WriteAll(fd, resp.data(), resp.size());
+      break;
+    }
     if (hit && hit->ws) {
       std::string key = req.headers["sec-websocket-key"];
       std::string accept = Base64Encode(Sha1(key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11"));

@@ -65,6 +65,24 @@ def test_tls_cluster_runs_experiment(tmp_path, monkeypatch):
         assert "Traceback" not in logs
 
 
+def test_agent_checks_master_cert_hostname(tmp_path):
+    """det-agent verifies the master certificate against the host it dialed (or
+    --master-cert-name), not only the chain: a trusted certificate issued for another name is refused."""
+    cert, key = tmp_path / "other.crt", tmp_path / "other.key"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out", str(cert),
+                    "-days", "2", "-subj", "/CN=other.example", "-addext", "subjectAltName=DNS:other.example"],
+                   check=True, capture_output=True)
+    c = LocalCluster(agents=0, slots_per_agent=1, log_dir=str(tmp_path), tick_ms=50, tls_cert=str(cert), tls_key=str(key))
+    c._verify = lambda: False  # this test's own client skips verification; the agent does not
+    with c:
+        c.start_agent(0)
+        with pytest.raises(RuntimeError):
+            c.wait_for_slots(1, timeout=8)  # dialed 127.0.0.1; the certificate names other.example
+        c.agent_args = ["--master-cert-name", "other.example"]
+        c.start_agent(1)
+        c.wait_for_slots(1, timeout=30)
+
+
 def test_yaml_config_env_and_flag_layering(tmp_path):
     cfg = tmp_path / "master.yaml"
     cfg.write_text(f"""# master config (reference /etc/determined/master.yaml)

@@ -174,6 +174,34 @@ def test_linked_conv_falls_back_when_input_grad_is_observed(gpu):
         torch.testing.assert_close(got, want, atol=1e-4, rtol=1e-4)
 
 
+def test_linked_gradient_unconsumed_raises(gpu, monkeypatch):
+    """torch.autograd.grad(loss, h) on a linked activation stops before the producer,
+    which would have summed the linked conv's share -- the pass must raise (not return a partial
+    gradient), and the stale share must not leak into the next full backward."""
+    torch.manual_seed(5)
+    bn = norm.BatchNormAct2d(64, relu=True).to(gpu)
+    conv_a = torch.nn.Conv2d(64, 32, 1, bias=False).to(gpu).to(memory_format=torch.channels_last)
+    conv_b = torch.nn.Conv2d(64, 128, 1, stride=2, bias=False).to(gpu).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 64, 14, 14, device=gpu).to(memory_format=torch.channels_last).requires_grad_(True)
+    h = bn(x)
+    b = norm.linked_conv2d(h, conv_b)
+    assert type(b.grad_fn).__name__ == "_LinkedConvBackward"
+    loss = conv_a(h).float().square().mean() + b.float().square().mean()
+    n0 = norm.LINK_COUNTS["unconsumed"]
+    with pytest.raises(RuntimeError, match="not consumed"):
+        torch.autograd.grad(loss, [h], retain_graph=True)
+    assert norm.LINK_COUNTS["unconsumed"] == n0 + 1
+    assert h.grad_fn.extra_dy is None  # dropped, not carried into the next backward
+    # the full backward after it is still exact (vs the same graph built without the link)
+    loss.backward()
+    got = x.grad.clone()
+    x.grad = None
+    monkeypatch.setattr(norm, "SHORTCUT_LINK", False)
+    h2 = bn(x)
+    (conv_a(h2).float().square().mean() + norm.linked_conv2d(h2, conv_b).float().square().mean()).backward()
+    torch.testing.assert_close(got, x.grad, atol=1e-4, rtol=1e-4)
+
+
 def test_resnet50_fused_shortcut_link_and_pool_match_stock(gpu, monkeypatch):
     """Fused BN with identity-shortcut gradient links (dy2 summed in the BN backward) and the HIP
     stem max-pool vs stock modules; non-zero residual gammas so every branch carries gradient.

@@ -114,3 +114,29 @@ def test_tunnel_to_missing_service_is_refused(cluster):
         # the master accepts the upgrade only to close it at once: the first read sees the close
         if ws.recv_bytes() is None:
             raise WebSocketError("closed")
+
+
+def test_tunnel_requires_a_session_under_require_auth(tmp_path):
+    """the tunnel's WebSocket upgrade is gated like /proxy -- without a session token the
+    master answers 401 before switching protocols; with the CLI's token the stream works."""
+    with LocalCluster(agents=1, slots_per_agent=1, log_dir=str(tmp_path), tick_ms=50,
+                      master_args=["--require-auth"]) as c:
+        client = MasterClient(c.address)
+        tok = client.login("determined", "")
+        cid = client.post("/commands", {"config": {"entrypoint": [sys.executable, "-c", ECHO], "resources": {"slots": 0},
+                                                   "description": "tcp echo"}, "context": [],
+                                        "secret_environment": [f"DET_USER_TOKEN={tok}"]})["id"]
+        deadline = time.time() + 60
+        while time.time() < deadline and not client.get(f"/commands/{cid}").get("service_address"):
+            time.sleep(0.2)
+        try:
+            with pytest.raises(WebSocketError, match="401"):
+                tunnel.open_tunnel(c.address, f"cmd-{cid}", token="")
+            with pytest.raises(WebSocketError, match="401"):
+                tunnel.open_tunnel(c.address, f"cmd-{cid}", token="not-a-session")
+            ws = tunnel.open_tunnel(c.address, f"cmd-{cid}", token=tok)
+            ws.send_binary(b"abc")
+            assert ws.recv_bytes() == b"cba"
+            ws.close()
+        finally:
+            client.post(f"/commands/{cid}/kill")
