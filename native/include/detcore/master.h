@@ -102,6 +102,9 @@ class Master {
 
   MasterConfig cfg_;
   std::unique_ptr<Store> store_;
+  std::mutex state_lat_mu_;  // agent ContainerStateChanged send -> handled (/debug/stats)
+  double state_lat_max_ms_ = 0, state_lat_sum_ms_ = 0;
+  int64_t state_lat_n_ = 0;
   std::unique_ptr<LogStore> logs_;  // trial-<id> / task-<id> log segments
   std::unique_ptr<actor::System> sys_;
   RWCoordinator rw_coordinator_;  // before http_: socket threads use it until the server stops

@@ -347,12 +347,19 @@ class Agent {
     auto ws = ws_;
     if (ws) ws->Send(m.dump());
   }
+  // wall-clock send time of a state change: the master reports how long state changes wait
+  // behind other traffic on this socket (/debug/stats agent_state_latency_ms)
+  static long long NowUs() {
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::system_clock::now().time_since_epoch())
+        .count();
+  }
 
   void State(const std::string& cid, const std::string& state, int exit_code = 0, const std::string& failure = "") {
     Json m = Json::object();
     m["type"] = "ContainerStateChanged";
     m["container_id"] = cid;
     m["state"] = state;
+    m["sent_us"] = NowUs();
     m["exit_code"] = exit_code;
     if (!failure.empty()) m["failure"] = failure;
     Send(m);
@@ -505,6 +512,7 @@ class Agent {
     Json running = Json::object();
     running["type"] = "ContainerStateChanged";
     running["container_id"] = cid;
+    running["sent_us"] = NowUs();
     running["state"] = "Running";
     running["address"] = o_.advertise_host;
     Send(running);

@@ -573,6 +573,15 @@ void Master::InstallRoutes() {
     out["uptime_s"] = std::chrono::duration<double>(std::chrono::steady_clock::now() - started_).count();
     out["actors"] = static_cast<long long>(sys_->Stats().size());
     out["tls"] = tls();
+    out["log_shipping"] = logs_->Stats();
+    {
+      std::lock_guard<std::mutex> g(state_lat_mu_);
+      Json lat = Json::object();
+      lat["count"] = static_cast<long long>(state_lat_n_);
+      lat["max"] = state_lat_max_ms_;
+      lat["mean"] = state_lat_n_ ? state_lat_sum_ms_ / static_cast<double>(state_lat_n_) : 0.0;
+      out["agent_state_latency_ms"] = lat;
+    }
     return J(200, out);
   });
   http_.Route("GET", "/info", [this](const net::Request&) {
@@ -1337,6 +1346,15 @@ void Master::OnAgentMessage(const std::shared_ptr<AgentConn>& conn, const Json& 
     }
     Pool(conn->pool)->Tell(AddAgent{a});
   } else if (t == "ContainerStateChanged") {
+    if (m.get_int("sent_us", 0) > 0) {
+      const double ms = (std::chrono::duration_cast<std::chrono::microseconds>(
+                             std::chrono::system_clock::now().time_since_epoch()).count() -
+                         m.get_int("sent_us", 0)) / 1000.0;
+      std::lock_guard<std::mutex> g(state_lat_mu_);
+      state_lat_max_ms_ = std::max(state_lat_max_ms_, ms);
+      state_lat_sum_ms_ += ms;
+      ++state_lat_n_;
+    }
     std::string cid = m.get_string("container_id", "");
     Ref tr = TrialForContainer(cid);
     if (tr)

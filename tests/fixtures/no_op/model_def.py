@@ -5,7 +5,8 @@ metrics, checkpoints are a small JSON file, optional chaos (random failures) to 
 Hyperparameters: ``metrics_base`` (0.9), ``metrics_progression`` (decreasing|increasing|constant),
 ``chaos_probability{,_train,_validate,_checkpoint}``, ``fail_on_first_validation``,
 ``fail_on_checkpoint_save``, ``validation_set_size`` (num_inputs), ``sleep`` (s per step),
-``invalid_hp`` (raise InvalidHP at construction).
+``invalid_hp`` (raise InvalidHP at construction), ``log_lines`` / ``log_seconds`` (print that
+many stdout lines per step, spread over that many seconds: log-shipping load tests).
 """
 import json
 import os
@@ -52,6 +53,13 @@ class NoOpTrialController(trial.CallbackTrialController):
     def train_for_step(self, step_id: int, num_batches: int) -> Dict[str, Any]:
         self._chaos("train")
         time.sleep(float(self.context.get_hparams().get("sleep", 0.0)))
+        n = int(self.context.get_hparams().get("log_lines", 0))
+        if n:
+            t0, span = time.time(), float(self.context.get_hparams().get("log_seconds", 0.0))
+            for i in range(n):
+                print(f"spam step={step_id} line={i}", flush=True)
+                if span and i % 100 == 99:
+                    time.sleep(max(0.0, t0 + span * (i + 1) / n - time.time()))
         self.trained_steps += 1
         m = self._step_metric()
         print(f"finished train_batch for rank {self.context.distributed.get_rank()}", flush=True)
