@@ -52,6 +52,8 @@ for c, st, hin, mult in SHAPES:
     if st == 1:
         r["dgrad_native"] = timeit(lambda: conv.igemm_conv(dy, w.transpose(0, 1), stride=1, pad=1,
                                                            w_krsc=conv.dgrad_weight(w)))
+    else:  # parity-class implicit GEMMs (incl. the flip kernel)
+        r["dgrad_native"] = timeit(lambda: conv.igemm_dgrad_s2(dy, w, hin, hin))
     r["dgrad_miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
         dy, x, w, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
     out = torch.empty(c, 9 * c, dtype=torch.bfloat16, device=dev)

@@ -165,8 +165,8 @@ def test_conv_rs_autograd_end_to_end(gpu, stride, wgrad_mode, monkeypatch):
     assert conv.CONV3X3_COUNTS["fallback"] == before["fallback"]
     wkey = "wgrad_native" if native_wgrad else "wgrad_miopen"
     assert conv.CONV3X3_COUNTS[wkey] == before[wkey] + 1
-    key = "dgrad_native" if stride == 1 else "dgrad_miopen"
-    assert conv.CONV3X3_COUNTS[key] == before[key] + 1
+    assert conv.CONV3X3_COUNTS["dgrad_native"] == before["dgrad_native"] + 1  # stride 2: parity classes
+    assert conv.CONV3X3_COUNTS["dgrad_miopen"] == before["dgrad_miopen"]
     xr = x.detach().float().requires_grad_(True)
     wr = m.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
     yr = F.conv2d(xr, wr, stride=stride, padding=1)
@@ -174,3 +174,59 @@ def test_conv_rs_autograd_end_to_end(gpu, stride, wgrad_mode, monkeypatch):
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=2e-2 * float(wr.grad.abs().max()))
+
+
+S2_SHAPES = [  # (Nb, Cout, Ho, Wo, Cin): ResNet's three stride-2 3x3 convs (reduced batch) + ragged tails
+    (2, 128, 28, 28, 128),
+    (3, 256, 14, 14, 256),
+    (2, 512, 7, 7, 512),
+    (1, 64, 5, 9, 192),    # Cin 192 -> BN 64 tiles, odd output grid, M < one block
+]
+
+
+@pytest.mark.parametrize("case", S2_SHAPES)
+def test_dgrad_s2_exact_on_integer_operands(gpu, case):
+    """det_igemm_dgrad_s2 (four parity-class implicit GEMMs over dY) == conv2d_input of the stride-2
+    3x3 conv, exactly: small-integer operands keep every sum exact in fp32, so a wrong tap, class
+    scatter or row offset shows as a mismatch."""
+    nb, cout, ho, wo, cin = case
+    g = torch.Generator(device="cpu").manual_seed(11)
+    dy = torch.randint(-2, 3, (nb, cout, ho, wo), generator=g).to(torch.bfloat16)
+    wt = torch.randint(-2, 3, (cout, cin, 3, 3), generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_input((nb, cin, 2 * ho, 2 * wo), wt.float(), dy.float(), stride=2, padding=1)
+    got = conv.igemm_dgrad_s2(dy.to(gpu).contiguous(memory_format=torch.channels_last),
+                              wt.to(gpu).contiguous(memory_format=torch.channels_last), 2 * ho, 2 * wo)
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(got.float().cpu(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+def test_dgrad_s2_bn_backward_epilogue_matches_unfused(gpu):
+    """The fused path: the BN(+ReLU) that produced the stride-2 conv's input takes its backward
+    partials from the class GEMMs' epilogue; x.grad, dgamma, dbeta equal the unfused backward."""
+    from determined_1_amd.ops import norm
+
+    torch.manual_seed(2)
+    bn = norm.BatchNormAct2d(128, relu=True).to(gpu)
+    m = torch.nn.Conv2d(128, 128, 3, stride=2, padding=1, bias=False).to(gpu).to(memory_format=torch.channels_last)
+    x0 = torch.randn(4, 128, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = None
+    outs = []
+    for fuse in (False, True):
+        conv.FUSE_BN_BWD = fuse
+        try:
+            bn.zero_grad(set_to_none=True)
+            m.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            before = dict(conv.BN_BWD_COUNTS)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = conv.conv_rs(bn(x), m, bn_exclusive=True)
+            if dy is None:
+                dy = torch.randn_like(y)
+            y.backward(dy)
+            if fuse:
+                assert conv.BN_BWD_COUNTS["fused"] == before["fused"] + 1
+            outs.append([x.grad.float(), bn.weight.grad, bn.bias.grad, m.weight.grad.float()])
+        finally:
+            conv.FUSE_BN_BWD = True
+    for a, b in zip(*outs):
+        torch.testing.assert_close(b, a, rtol=2e-2, atol=2e-2 * float(a.abs().max()) + 1e-6)

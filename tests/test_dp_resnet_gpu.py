@@ -1,0 +1,89 @@
+"""The fused ResNet-50 data-parallel path, numerically.
+
+Two ranks share this GPU over gloo (DET_DIST_SHARE_GPU=1; RCCL refuses two ranks on one device,
+so the collective backend is the only difference from the driver's 8-GPU run) and train the
+benchmark trial with every default fusion on: linked shortcut gradients, deferred BN applies,
+GradSink landing, the bucketed all-reduce (fp32_accum for the O2 bf16 arena; bf16 wire
+compression for the O0 fp32 arena).  Two checks, each at O2 and at O0 + compression:
+
+* identical batches on both ranks: the fp32 master weights after 4 SGD-momentum steps equal the
+  single-process run on the same batches (the average of two equal gradients is that gradient);
+* different batches: one plain-SGD step (lr 1, no momentum) moves the weights by exactly minus the
+  mean of the two single-rank gradients, computed from two single-process runs in fp32.
+
+Reference: harness/determined/pytorch/_pytorch_context.py:152-204 (hvd.DistributedOptimizer
+averaging) and e2e_tests/tests/experiment/test_pytorch.py:89-104 (DP vs single-slot parity)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "dist_scripts", "resnet_dp_worker.py")
+REPO = os.path.dirname(HERE)
+
+
+def _run(out, amp, compress, data, steps, lr, mom, ranks):
+    from determined_1_amd.deploy.local import free_port
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                             "DET_FORCE_DISTRIBUTED")}
+    args = [out, amp, "1" if compress else "0", data, str(steps), str(lr), str(mom)]
+    if ranks == 1:
+        cmd = [sys.executable, WORKER] + args
+    else:
+        env.update(DET_DIST_SHARE_GPU="1", DET_DIST_BACKEND="gloo")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), WORKER] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return torch.load(out + ".pt")
+
+
+def _fusions_on(info):
+    c = info["counts"]
+    assert c["fwd_apply"]["in_gemm"] > 0, c  # deferred BN forward applies staged by the next conv1
+    assert c["bn_bwd"]["fused"] > 0, c        # BN-backward partials from dgrad epilogues
+    assert c["conv3x3"]["fallback"] == 0 and c["bn_fallbacks"] == 0, c
+
+
+CASES = [("O2", False), ("O0", True)]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("amp,compress", CASES)
+def test_identical_batches_match_single_process(gpu, tmp_path, amp, compress):
+    ref = _run(str(tmp_path / "ref"), amp, compress, "seq", 4, 0.05, 0.9, 1)
+    dp = _run(str(tmp_path / "dp"), amp, compress, "dup", 4, 0.05, 0.9, 2)
+    assert dp["world"] == 2 and dp["dist"] and not ref["dist"]
+    modes = {b["mode"] for bs in dp["buckets"] for b in bs}
+    assert modes == {"fp32_accum"}, dp["buckets"]
+    _fusions_on(dp)
+    assert torch.equal(dp["init"], ref["init"])  # the same seeded initialisation
+    moved = (ref["params"] - ref["init"]).abs()
+    diff = (dp["params"] - ref["params"]).abs()
+    # bf16 compute; the wire compression rounds each gradient to bf16 once more
+    tol = 2e-2 if compress else 1e-2
+    assert float(diff.max()) <= tol * float(moved.max()) + 1e-6, (float(diff.max()), float(moved.max()))
+    assert float(diff.norm()) <= tol * float(moved.norm()), (float(diff.norm()), float(moved.norm()))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("amp,compress", CASES)
+def test_split_batches_average_the_gradients(gpu, tmp_path, amp, compress):
+    r0 = _run(str(tmp_path / "b0"), amp, compress, "b0", 1, 1.0, 0.0, 1)
+    r1 = _run(str(tmp_path / "b1"), amp, compress, "b1", 1, 1.0, 0.0, 1)
+    dp = _run(str(tmp_path / "dp"), amp, compress, "pair", 1, 1.0, 0.0, 2)
+    _fusions_on(dp)
+    init = r0["init"].double()
+    assert torch.equal(r1["init"], r0["init"]) and torch.equal(dp["init"], r0["init"])
+    g0, g1 = init - r0["params"].double(), init - r1["params"].double()
+    got = init - dp["params"].double()
+    want = (g0 + g1) / 2
+    err = (got - want).norm() / want.norm()
+    assert float(err) < (2e-2 if compress else 1e-2), float(err)
+    # and it is not either rank's gradient alone
+    assert float((got - g0).norm() / want.norm()) > 5 * float(err)
