@@ -398,7 +398,11 @@ def cmd_user_whoami(args: argparse.Namespace) -> None:
 
 
 def cmd_user_list(args: argparse.Namespace) -> None:
-    print(_table(MasterClient(args.master).get("/users"), ["username", "admin", "active"]))
+    rows = MasterClient(args.master).get("/users")
+    for r in rows:
+        g = r.get("agent_user_group") or {}
+        r["agent_user"] = f"{g['user']}:{g['group']} ({g['uid']}:{g['gid']})" if g else ""
+    print(_table(rows, ["username", "admin", "active", "agent_user"]))
 
 
 def cmd_user_create(args: argparse.Namespace) -> None:
@@ -408,6 +412,18 @@ def cmd_user_create(args: argparse.Namespace) -> None:
 
 def cmd_user_change_password(args: argparse.Namespace) -> None:
     MasterClient(args.master).patch(f"/users/{args.username}", {"password": args.password})
+
+
+def cmd_user_link_with_agent_user(args: argparse.Namespace) -> None:
+    """Tasks of ``det_username`` run on agents as this host account (reference
+    cli/determined_cli/user.py:165-185 link_with_agent_user); admin only."""
+    for flag in ("agent_uid", "agent_user", "agent_gid", "agent_group"):
+        if getattr(args, flag) is None:
+            raise SystemExit(f"--{flag.replace('_', '-')} argument required")
+    MasterClient(args.master).patch(f"/users/{args.det_username}", {"agent_user_group": {
+        "uid": args.agent_uid, "user": args.agent_user, "gid": args.agent_gid, "group": args.agent_group}})
+    print(f"linked {args.det_username} with {args.agent_user}:{args.agent_group} "
+          f"({args.agent_uid}:{args.agent_gid}) on the agents")
 
 
 # ----------------------------------------------------------------------------- commands
@@ -785,6 +801,13 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("username")
     x.add_argument("password")
     x.set_defaults(func=cmd_user_change_password)
+    x = us.add_parser("link-with-agent-user", help="link a user with a UID/GID on the agents")
+    x.add_argument("det_username")
+    x.add_argument("--agent-uid", type=int, help="UID on the agent to run tasks as")
+    x.add_argument("--agent-user", help="user on the agent to run tasks as")
+    x.add_argument("--agent-gid", type=int, help="GID on the agent to run tasks as")
+    x.add_argument("--agent-group", help="group on the agent to run tasks as")
+    x.set_defaults(func=cmd_user_link_with_agent_user)
 
     cm = sub.add_parser("command", aliases=["cmd"]).add_subparsers(dest="sub")
     x = cm.add_parser("run")

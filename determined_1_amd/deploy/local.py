@@ -44,10 +44,14 @@ class LocalCluster:
                  scheduler: str = "fair_share", work_dir: Optional[str] = None, gpu: bool = False,
                  log_dir: Optional[str] = None, tick_ms: int = 100, master_args: Optional[List[str]] = None,
                  visible_gpus: Optional[str] = None, agent_args: Optional[List[str]] = None,
-                 tls_cert: Optional[str] = None, tls_key: Optional[str] = None) -> None:
+                 tls_cert: Optional[str] = None, tls_key: Optional[str] = None,
+                 framework_root: Optional[str] = None) -> None:
         self.port = port or free_port()
         self.tls_cert, self.tls_key = tls_cert, tls_key  # serve the API over TLS (security.tls)
+        # where agents (and the tasks they start) import the framework from; default: this checkout
+        self.framework_root = framework_root or str(NATIVE_DIR.parent.parent)
         self.tmp = tempfile.mkdtemp(prefix="det-local-")
+        os.chmod(self.tmp, 0o711)  # tasks may run as other host accounts (agent user groups)
         self.store_dir = store_dir or os.path.join(self.tmp, "store")
         self.checkpoint_dir = checkpoint_dir or os.path.join(self.tmp, "checkpoints")
         self.work_dir = work_dir or os.path.join(self.tmp, "agents")
@@ -97,7 +101,7 @@ class LocalCluster:
         log = open(os.path.join(self.log_dir, f"agent-{i}.log"), "ab")
         args = [native_binary("det-agent"), "--master-host", "127.0.0.1", "--master-port", str(self.port),
                 "--agent-id", f"agent-{i}", "--work-dir", os.path.join(self.work_dir, f"agent-{i}"),
-                "--python", sys.executable, "--framework-root", str(NATIVE_DIR.parent.parent)]
+                "--python", sys.executable, "--framework-root", self.framework_root]
         if self.slots_per_agent > 0 and not self.gpu:
             args += ["--artificial-slots", str(self.slots_per_agent)]
         elif self.gpu:
@@ -107,7 +111,8 @@ class LocalCluster:
         args += self.agent_args
         if self.tls_cert:
             args += ["--master-cert-file", self.tls_cert]
-        p = subprocess.Popen(args, stdout=log, stderr=subprocess.STDOUT)
+        p = subprocess.Popen(args, stdout=log, stderr=subprocess.STDOUT,
+                             cwd=self.tmp if self.framework_root != str(NATIVE_DIR.parent.parent) else None)
         self.agent_procs.append(p)
         return p
 

@@ -99,6 +99,11 @@ def _child(req: Dict, fds: List[int], close: List[int]) -> None:
                     os.close(fd)
         sys.stdout = os.fdopen(1, "w", buffering=1, closefd=False)
         sys.stderr = os.fdopen(2, "w", buffering=1, closefd=False)
+        if req.get("uid") is not None and int(req["uid"]) != os.geteuid():
+            # the task owner's host account (agent user group): drop privileges before any user code
+            os.setgroups([int(req["gid"])])
+            os.setgid(int(req["gid"]))
+            os.setuid(int(req["uid"]))
         cwd = req.get("cwd") or os.getcwd()
         os.chdir(cwd)
         env = req.get("env") or {}

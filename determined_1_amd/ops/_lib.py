@@ -157,6 +157,13 @@ _SIGNATURES = {
     # ... + cfg (0 = automatic per shape)
     "det_igemm_conv_cfg": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2 + [c_int], c_int),
     "det_igemm_conv_bnbwd": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 6 + [c_int], c_int),
+    # stream, dY, Wd [Cin][9*Cout], dX, zero, Nb, Ho, Wo, Cout, Cin, bn_x, bn_mean, bn_scale, bn_shift,
+    # psum, psumx (nullable BNB epilogue), cfg
+    "det_igemm_dgrad_s2": ([c_void_p] * 5 + [c_int] * 5 + [c_void_p] * 6 + [c_int], c_int),
+    "det_igemm_dgrad_s2_rows_per_block": ([c_int, c_int], c_int),
+    # stream, X, W [N][9][Cin], Y, Nb, H, W, Cin, N, pro_scale, pro_shift, pmean, pm2, bn_x, bn_mean,
+    # bn_scale, bn_shift, psum, psumx, grid (0 = one persistent block per CU)
+    "det_conv3p": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 10 + [c_int], c_int),
     # stream, dY, X, out, out_dtype, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, ws, out_scale
     "det_conv_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 10 + [c_void_p, c_float], c_int),
     "det_igemm_wgrad_ws_elems": ([c_i64, c_int, c_int, c_int], c_i64),

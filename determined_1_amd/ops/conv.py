@@ -153,6 +153,53 @@ def igemm_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
             and x.is_contiguous(memory_format=torch.channels_last))
 
 
+# 3x3 / stride-1 convolutions with at most this many output channels run on the halo-patch kernel
+# (det_igemm.hip conv3p: the input staged once per 256-pixel tile instead of once per tap); wider
+# ones stay on igemm3, whose 256 x 256 tiles already reuse each staged row over 256 columns.
+CONV3P_MAX_N = int(os.environ.get("DET_CONV3P_MAX_N", "128"))
+CONV3P_COUNTS = {"fwd": 0, "dgrad": 0}
+
+
+def conv3p_ok(cin: int, cout: int, r: int, s: int, stride: int, pad: int) -> bool:
+    return (r == 3 and s == 3 and stride == 1 and pad == 1 and cin % 32 == 0 and cout % 64 == 0
+            and cout <= CONV3P_MAX_N)
+
+
+def conv3p(x: torch.Tensor, wk: torch.Tensor, cout: int, stats: bool = False, pro=None, bnb=None):
+    """3x3 / stride-1 / pad-1 conv of channels_last bf16 ``x`` with the KRSC weight ``wk``
+    [Cout, 9*Cin] on det_conv3p.  ``pro`` = (scale, shift): the input operand is relu(x*scale+shift)
+    (a BatchNorm+ReLU applied while staging).  ``bnb`` = (bn_x, mean, scale, shift): the output is the
+    input gradient feeding that BN's backward; returns (masked gradient, (psum, psumx, 256)).
+    Otherwise returns (y, BN statistics partials of y or None).  Returns None when a tile's halo
+    patch does not fit (very wide images)."""
+    nb, cin, h, w = x.shape
+    m = nb * h * w
+    lib = _lib.get_lib()
+    y = torch.empty((nb, cout, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    nrb = (m + 255) // 256
+    pm = pq = None
+    bn = [None] * 6
+    if stats:
+        pm = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
+        pq = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
+    if bnb is not None:
+        bx, mean, sc, sh = bnb
+        pm_b = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
+        pq_b = torch.empty(nrb, cout, dtype=torch.float32, device=x.device)
+        bn = [bx.data_ptr(), mean.data_ptr(), sc.data_ptr(), sh.data_ptr(), pm_b.data_ptr(), pq_b.data_ptr()]
+    rc = lib.det_conv3p(_stream(x), x.data_ptr(), wk.data_ptr(), y.data_ptr(), int(nb), int(h), int(w), int(cin),
+                        int(cout), _ptr(pro[0]) if pro else None, _ptr(pro[1]) if pro else None, _ptr(pm), _ptr(pq),
+                        *bn, 0)
+    if rc == -6:
+        return None
+    _lib.check(rc, "conv3p")
+    if bnb is not None:
+        CONV3P_COUNTS["dgrad"] += 1
+        return y, (pm_b, pq_b, 256)
+    CONV3P_COUNTS["fwd"] += 1
+    return y, ((pm, pq, 256) if stats else None)
+
+
 def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
                w_krsc: Optional[torch.Tensor] = None, cfg: int = 0) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
     """``conv2d(x, w, stride, pad)`` for channels_last bf16 ``x`` (Cin % 32 == 0) and Cout % 64 == 0.
@@ -174,6 +221,10 @@ def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, 
         return y, parts
     wk = krsc(w) if w_krsc is None else w_krsc
     assert wk.dtype == torch.bfloat16 and wk.is_contiguous() and wk.shape == (cout, r * s * cin)
+    if cfg == 0 and conv3p_ok(cin, cout, r, s, stride, pad) and x.data_ptr() % 16 == 0:
+        res = conv3p(x, wk, cout, stats=stats)
+        if res is not None:
+            return res
     y = torch.empty((nb, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
     parts = None
     pm = pq = None
@@ -449,6 +500,13 @@ def _fused_bn_dgrad_rs(prod, dyc: torch.Tensor, wt: torch.Tensor, wd: torch.Tens
     m = nb * h * w_
     if xb.dtype != torch.bfloat16 or xb.shape != (nb, cin, h, w_) or not xb.is_contiguous(memory_format=torch.channels_last):
         return None
+    r, s = wt.shape[2], wt.shape[3]
+    if conv3p_ok(cout, cin, r, s, 1, pad):
+        res = conv3p(dyc, wd, cin, bnb=(xb, stats[0], stats[2], stats[3]))
+        if res is not None:
+            d, fb = res
+            prod.fused_bwd = fb
+            return d
     lib = _lib.get_lib()
     cfg = 0
     rpb = int(lib.det_igemm_rows_per_block_cfg(int(cin), cfg))
@@ -456,7 +514,6 @@ def _fused_bn_dgrad_rs(prod, dyc: torch.Tensor, wt: torch.Tensor, wd: torch.Tens
     psum = torch.empty(nrb, cin, dtype=torch.float32, device=dyc.device)
     psumx = torch.empty(nrb, cin, dtype=torch.float32, device=dyc.device)
     d = torch.empty((nb, cin, h, w_), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
-    r, s = wt.shape[2], wt.shape[3]
     _lib.check(lib.det_igemm_conv_bnbwd(_stream(dyc), dyc.data_ptr(), wd.data_ptr(), d.data_ptr(),
                                         _zero_page(dyc.device).data_ptr(), int(m), int(cin), int(cout), int(h), int(w_),
                                         int(h), int(w_), int(r), int(s), 1, int(pad), xb.data_ptr(), stats[0].data_ptr(),
@@ -464,6 +521,57 @@ def _fused_bn_dgrad_rs(prod, dyc: torch.Tensor, wt: torch.Tensor, wd: torch.Tens
                                         cfg), "igemm_conv_bnbwd")
     prod.fused_bwd = (psum, psumx, rpb)
     return d
+
+
+DGRAD_S2_NATIVE = os.environ.get("DET_DGRAD_S2_NATIVE", "1") != "0"  # A/B switch: MIOpen's transposed conv
+
+
+def dgrad_s2_ok(x: torch.Tensor, weight: torch.Tensor, stride: int, pad: int) -> bool:
+    """The stride-2 3x3/pad-1 input gradient can run on det_igemm_dgrad_s2 (parity classes)."""
+    cout, cin, r, s = weight.shape
+    return (DGRAD_S2_NATIVE and stride == 2 and pad == 1 and r == 3 and s == 3 and cin % 64 == 0 and cout % 32 == 0
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
+
+
+def igemm_dgrad_s2(dyc: torch.Tensor, weight: torch.Tensor, hi: int, wi: int, prod=None) -> torch.Tensor:
+    """Input gradient [N, Cin, Hi, Wi] (channels_last bf16) of a 3x3 / stride-2 / pad-1 conv from dY
+    (channels_last bf16): det_igemm_dgrad_s2, four parity-class implicit GEMMs over dY against taps of
+    the flipped weight.  ``prod``: the fused BN(+ReLU) that produced the conv input (mask mode 1):
+    its backward partials come from the GEMM epilogue (``prod.fused_bwd``) and the ReLU mask is
+    applied to the returned gradient."""
+    nb, cout, ho, wo = dyc.shape
+    cin = weight.shape[1]
+    if not is_gpu(dyc):  # CPU reference of the same computation
+        g = torch.nn.grad.conv2d_input((nb, cin, hi, wi), weight.float(), dyc.float(), stride=2, padding=1)
+        return g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    lib = _lib.get_lib()
+    wd = dgrad_weight(weight)  # [Cin, 9 * Cout]
+    dx = torch.empty((nb, cin, hi, wi), dtype=torch.bfloat16, device=dyc.device, memory_format=torch.channels_last)
+    bn = [None] * 6
+    if prod is not None:
+        xb, _, _, stats = prod.saved_tensors
+        rpb = int(lib.det_igemm_dgrad_s2_rows_per_block(int(cin), 0))
+        nrb = 4 * ((nb * ho * wo + rpb - 1) // rpb)
+        psum = torch.empty(nrb, cin, dtype=torch.float32, device=dyc.device)
+        psumx = torch.empty(nrb, cin, dtype=torch.float32, device=dyc.device)
+        bn = [xb.data_ptr(), stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), psum.data_ptr(),
+              psumx.data_ptr()]
+    _lib.check(lib.det_igemm_dgrad_s2(_stream(dyc), dyc.data_ptr(), wd.data_ptr(), dx.data_ptr(),
+                                      _zero_page(dyc.device).data_ptr(), int(nb), int(ho), int(wo), int(cout), int(cin),
+                                      *bn, 0), "igemm_dgrad_s2")
+    if prod is not None:
+        prod.fused_bwd = (psum, psumx, rpb)  # the BN backward sums the partials (any row order)
+    return dx
+
+
+def _bn_producer_s2_ok(prod, x: torch.Tensor) -> bool:
+    if prod is None or getattr(prod, "mask_mode", 0) != 1 or getattr(prod, "fused_bwd", None) is not None:
+        return False
+    try:
+        xb = prod.saved_tensors[0]
+    except RuntimeError:
+        return False
+    return xb.dtype == torch.bfloat16 and xb.shape == x.shape and xb.is_contiguous(memory_format=torch.channels_last)
 
 
 class _Conv1x1(torch.autograd.Function):
@@ -674,6 +782,13 @@ class _ConvRS(torch.autograd.Function):
                 else:
                     BN_BWD_COUNTS["fused"] += 1
                 CONV3X3_COUNTS["dgrad_native"] += 1
+            elif dgrad_s2_ok(x, weight, stride, pad) and is_gpu(dyc):
+                prod, ctx.bn_producer = ctx.bn_producer, None
+                fuse = _bn_producer_s2_ok(prod, x)
+                dx = igemm_dgrad_s2(dyc, weight, x.shape[2], x.shape[3], prod if fuse else None)
+                if prod is not None:
+                    BN_BWD_COUNTS["fused" if fuse else "unfused"] += 1
+                CONV3X3_COUNTS["dgrad_native"] += 1
             else:
                 wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
                 dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
@@ -731,7 +846,8 @@ def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_e
     CONV3X3_COUNTS["native"] += 1
     if x.dtype != torch.bfloat16:
         x = x.to(torch.bfloat16)
-    prod = _bn_producer(x) if (bn_exclusive and FUSE_BN_BWD and torch.is_grad_enabled() and st[0] == 1) else None
+    prod = _bn_producer(x) if (bn_exclusive and FUSE_BN_BWD and torch.is_grad_enabled()
+                               and (st[0] == 1 or dgrad_s2_ok(x, w, st[0], pd[0]))) else None
     with torch.autocast("cuda", enabled=False):
         return _ConvRS.apply(x, w, int(st[0]), int(pd[0]), stats, prod)
 # Stem weight gradient: the det_conv split-M implicit GEMM (True) or MIOpen's NHWC C=4 kernel (False,

@@ -87,7 +87,27 @@ struct IgArgs {
   const float* bn_shift;
   float* psum;
   float* psumx;
+  // Input gradient of a stride-2 3x3/pad-1 conv as four parity-class convs (igemm3 only; see
+  // det_igemm_dgrad_s2): kb_stride = the B row stride (0: K), tapmap = 4-bit B tap per class tap
+  // (0: identity), oscat = 1 + 2*ph + pw scatters output row (q = n*Ho + i, j) to the full-resolution
+  // row (2q + ph) * 2Wo + 2j + pw, mt_base = first statistics block row of this class.
+  int kb_stride;
+  unsigned tapmap;
+  int oscat;
+  int mt_base;
+  // conv3p prologue: the input operand is relu(X * pro_scale[c] + pro_shift[c]) (padding stays 0)
+  const float* pro_scale;
+  const float* pro_shift;
 };
+
+// the row of Y (and of the BN input in the BNB epilogue) that GEMM row m writes
+__device__ __forceinline__ int64_t out_row(const IgArgs& a, int64_t m) {
+  if (a.oscat == 0) return m;
+  const int cls = a.oscat - 1, ph = cls >> 1, pw = cls & 1;
+  const int64_t q = m / a.Wo;
+  const int j = static_cast<int>(m - q * a.Wo);
+  return (2 * q + ph) * (2 * static_cast<int64_t>(a.Wo)) + 2 * j + pw;
+}
 
 // BN-backward epilogue of a BM x BN output tile held as bf16 in LDS (ct, row stride LDC): each
 // thread owns one 8-column chunk over rows tid/CPR + q*NT/CPR, writes the masked gradient and
@@ -116,13 +136,13 @@ __device__ __forceinline__ void bnb_epilogue(const IgArgs& a, unsigned char* sme
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int row = (tid + q * NT) / CPR;
-    xs[q] = row < nvalid ? *reinterpret_cast<const us8*>(a.bn_x + (m0 + row) * a.N + c0) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+    xs[q] = row < nvalid ? *reinterpret_cast<const us8*>(a.bn_x + out_row(a, m0 + row) * a.N + c0) : us8{0, 0, 0, 0, 0, 0, 0, 0};
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int row = (tid + q * NT) / CPR;
     if (row >= nvalid) continue;
-    const int64_t off = (m0 + row) * a.N + c0;
+    const int64_t off = out_row(a, m0 + row) * a.N + c0;
     const us8 cv = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
     const us8 xv = xs[q];
     us8 o;
@@ -152,8 +172,8 @@ __device__ __forceinline__ void bnb_epilogue(const IgArgs& a, unsigned char* sme
       t1 += scratch[(g * CPR + ccol) * 16 + j];
       t2 += scratch[(g * CPR + ccol) * 16 + 8 + j];
     }
-    a.psum[static_cast<int64_t>(mt) * a.N + n0 + tid] = t1;
-    a.psumx[static_cast<int64_t>(mt) * a.N + n0 + tid] = t2;
+    a.psum[static_cast<int64_t>(a.mt_base + mt) * a.N + n0 + tid] = t1;
+    a.psumx[static_cast<int64_t>(a.mt_base + mt) * a.N + n0 + tid] = t2;
   }
 }
 
@@ -566,8 +586,9 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned short*>(a.X), 0, static_cast<int>(a.x_bytes), 0x00020000);
+  const int64_t KB = a.kb_stride > 0 ? a.kb_stride : K;  // B row stride (elements)
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<unsigned short*>(a.W), 0, static_cast<int>(static_cast<int64_t>(a.N) * K * 2), 0x00020000);
+      const_cast<unsigned short*>(a.W), 0, static_cast<int>(static_cast<int64_t>(a.N) * KB * 2), 0x00020000);
   constexpr unsigned kOOB = 0xFFFFFFF0u;
   int aoff[AI];
   unsigned amask[AI];
@@ -594,7 +615,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
   unsigned boff[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j)
-    boff[j] = static_cast<unsigned>(((static_cast<int64_t>(n0) + ((j * NW + wid) % BP) * 16 + lrow) * K + gch * 8) * 2);
+    boff[j] = static_cast<unsigned>(((static_cast<int64_t>(n0) + ((j * NW + wid) % BP) * 16 + lrow) * KB + gch * 8) * 2);
 
   auto issue = [&](int kt) {
     unsigned char* st = smem + (kt % NS) * STAGE;
@@ -602,6 +623,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
     const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
     const int r = tap / a.S, s2 = tap - r * a.S;
     const int toff = ((r * a.Wi + s2) * a.Cin + c0) * 2;
+    const int kb = a.tapmap ? static_cast<int>((a.tapmap >> (4 * tap)) & 15u) * a.Cin + c0 : k0;  // B column
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const unsigned v = ((amask[i] >> tap) & 1u) ? static_cast<unsigned>(aoff[i] + toff) : kOOB;
@@ -611,7 +633,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
 #pragma unroll
       for (int j = 0; j < BI; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_void*)(st + A_BYTES + ((j * NW + wid) * 16) * 64), 16, boff[j],
-                                                 k0 * 2, 0, 0);
+                                                 kb * 2, 0, 0);
     }
   };
   const bool bwave = !BPART || __builtin_amdgcn_readfirstlane(wid) < BP;
@@ -714,7 +736,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
     const int idx = tid + q * kThreads;
     const int row = idx / CPR, cc = idx - row * CPR;
     if (idx < BM * CPR && row < nvalid)
-      *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+      *reinterpret_cast<us8*>(a.Y + out_row(a, m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
 #endif
 }
@@ -815,6 +837,248 @@ static int auto_cfg(const IgArgs& a) {
   if (a.N % 256 == 0 && a.Cin % 32 == 0) return 8;
   if (a.N % 128 == 0 && a.Cin % 64 == 0) return 2;
   return a.Cin % 32 == 0 ? 11 : 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// v5 (conv3p): 3x3 / stride-1 / pad-1 convolution with the input staged ONCE per tile as a halo
+// patch, for the thin-N layers (ResNet layer1/2: N = 64/128, K = 9 x 64/128).
+//
+// igemm3 gathers the im2col A operand tap by tap: every output pixel's row is staged 9 times per
+// channel slice, and with N = 64 the 16 KiB of A per K tile carry only 256 x 64 x 32 MACs -- the
+// LDS-DMA issue cost per KiB (MI355X_MICROARCH.md "LDS-DMA piece issue cost") then exceeds the MFMA
+// time (layer1 3x3 forward at ~400 TF/s, profiles/r3_conv3x3_passes.jsonl).  Here a 256-pixel output
+// tile stages, per 32-channel slice, the padded input rows it touches (<= 512 pixels x 64 B) and the
+// slice's 9-tap weights [9][64][32] once; the 9 taps then read their A fragments from the patch at
+// a row offset of r * (W + 2) + s (per-lane patch rows, the 64-B-row swizzle of igemm3).  Staging
+// is register-path (global_load -> ds_write), which lets the preceding BatchNorm + ReLU be applied
+// on the way in (PRO: the normalised activation is never written to HBM; padding stays zero).
+//   * 256 x 64 block tile, 8 waves of 32 x 64 (v_mfma_f32_16x16x32_bf16), one block per CU (the
+//     staged slice is held in registers while the MFMAs run: 4 waves of 64 x 64 spill);
+//   * persistent blocks over a contiguous chunk of (M tile, N tile) pairs, N fastest: the next
+//     slice (or the next tile's first) is loaded into registers while the current one computes;
+//   * epilogues of igemm3: bf16 tile via LDS, BN statistics (STATS) or the BN-backward partials
+//     of the producing BatchNorm (BNB, for the stride-1 input gradient over the flipped weight).
+// ------------------------------------------------------------------------------------------------
+constexpr int kP3BM = 256, kP3BN = 64, kP3BK = 32, kP3PMAX = 512;
+constexpr int kP3PATCH = kP3PMAX * 64, kP3BT = 9 * kP3BN * 64;
+constexpr int kP3SMEM = kP3PATCH + kP3BT;  // 69632 B
+
+struct P3Tile {
+  int64_t m0;
+  int n0, g0;  // first padded input row ((H + 2) per image) the tile reads
+  int rows;    // padded rows in the patch
+};
+
+__device__ __forceinline__ P3Tile p3_tile(const IgArgs& a, int t, int ntn) {
+  P3Tile T;
+  const int mt = t / ntn;
+  T.n0 = (t - mt * ntn) * kP3BN;
+  T.m0 = static_cast<int64_t>(mt) * kP3BM;
+  const int64_t hw = static_cast<int64_t>(a.Hi) * a.Wi;
+  int64_t mlast = T.m0 + kP3BM - 1;
+  if (mlast >= a.M) mlast = a.M - 1;
+  const int64_t na = T.m0 / hw, nb = mlast / hw;
+  const int ha = static_cast<int>((T.m0 - na * hw) / a.Wi), hb = static_cast<int>((mlast - nb * hw) / a.Wi);
+  T.g0 = static_cast<int>(na * (a.Hi + 2) + ha);
+  T.rows = static_cast<int>(nb * (a.Hi + 2) + hb + 2) - T.g0 + 1;
+  return T;
+}
+
+template <bool PRO, bool STATS, bool BNB>
+__global__ void __launch_bounds__(512, 2) conv3p_kernel(IgArgs a, int ntiles, int ntn) {
+  constexpr int BM = kP3BM, BN = kP3BN, NT = 512, WM = 8, TM = 32, TN = 64, FM = 2, FN = 4;
+  constexpr int PCH = kP3PMAX * 4 / NT;  // patch 16-B chunks per thread (max)
+  constexpr int BCHUNKS = 9 * BN * 4, BCH = (BCHUNKS + NT - 1) / NT;  // weight chunks (per thread)
+  static_assert(kP3PMAX * 4 % NT == 0, "patch chunks split evenly");
+  constexpr int LDC = BN + 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* patch = smem;
+  unsigned char* bt = smem + kP3PATCH;
+  float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wm = tid >> 6;
+  const int Wp = a.Wi + 2;
+  const int ns = a.Cin / kP3BK;  // channel slices per tile
+  // this block's contiguous chunk of tiles (N tile fastest)
+  const int G = gridDim.x;
+  const int tbeg = static_cast<int>((static_cast<int64_t>(ntiles) * blockIdx.x) / G);
+  const int tend = static_cast<int>((static_cast<int64_t>(ntiles) * (blockIdx.x + 1)) / G);
+  const int items = (tend - tbeg) * ns;
+  if (items <= 0) return;
+
+  us8 rp[PCH], rw[BCH];
+  const int cch = tid & 3;  // the 16-B channel chunk every patch chunk of this thread carries
+  auto gload = [&](int it) {
+    const int t = tbeg + it / ns, sl = it - (it / ns) * ns;
+    const P3Tile T = p3_tile(a, t, ntn);
+    const int c0 = sl * kP3BK;
+    const int np = T.rows * Wp;
+#pragma unroll
+    for (int q = 0; q < PCH; ++q) {
+      const int idx = tid + q * NT, p = idx >> 2;
+      us8 v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (p < np) {
+        const int gr = T.g0 + p / Wp, wp = p - (p / Wp) * Wp;
+        const int n = gr / (a.Hi + 2), h = gr - n * (a.Hi + 2) - 1, w = wp - 1;
+        if (h >= 0 && h < a.Hi && w >= 0 && w < a.Wi)
+          v = *reinterpret_cast<const us8*>(a.X + ((static_cast<int64_t>(n) * a.Hi + h) * a.Wi + w) * a.Cin + c0 + cch * 8);
+      }
+      rp[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < BCH; ++q) {
+      const int idx = tid + q * NT, row = idx >> 2, ch = idx & 3;  // row = tap * BN + n
+      const int tap = row / BN, n = row - tap * BN;
+      if (BCHUNKS % NT == 0 || idx < BCHUNKS)
+        rw[q] = *reinterpret_cast<const us8*>(a.W + (static_cast<int64_t>(T.n0 + n) * 9 + tap) * a.Cin + c0 + ch * 8);
+    }
+  };
+  auto lstore = [&](int it) {
+    const int t = tbeg + it / ns, sl = it - (it / ns) * ns;
+    const P3Tile T = p3_tile(a, t, ntn);
+    const int np = T.rows * Wp;
+    float psc[8], psh[8];  // (loaded here, not with the slice: no registers held across the MFMAs)
+    if constexpr (PRO) {
+      const int c = sl * kP3BK + cch * 8;
+#pragma unroll
+      for (int j = 0; j < 8; j += 4) {
+        const float4 s4 = *reinterpret_cast<const float4*>(a.pro_scale + c + j);
+        const float4 h4 = *reinterpret_cast<const float4*>(a.pro_shift + c + j);
+        psc[j] = s4.x; psc[j + 1] = s4.y; psc[j + 2] = s4.z; psc[j + 3] = s4.w;
+        psh[j] = h4.x; psh[j + 1] = h4.y; psh[j + 2] = h4.z; psh[j + 3] = h4.w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PCH; ++q) {
+      const int idx = tid + q * NT, p = idx >> 2;
+      if (p >= np) continue;
+      us8 v = rp[q];
+      if constexpr (PRO) {
+        const int gr = T.g0 + p / Wp, wp = p - (p / Wp) * Wp;
+        const int h = gr - (gr / (a.Hi + 2)) * (a.Hi + 2) - 1, w = wp - 1;
+        if (h >= 0 && h < a.Hi && w >= 0 && w < a.Wi) {  // the BN output of real pixels; padding stays 0
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = f2bf(fmaxf(__fmaf_rn(bf2f(v[j]), psc[j], psh[j]), 0.f));
+        }
+      }
+      *reinterpret_cast<us8*>(patch + swz64(p, cch)) = v;
+    }
+#pragma unroll
+    for (int q = 0; q < BCH; ++q) {
+      const int idx = tid + q * NT, row = idx >> 2, ch = idx & 3;
+      if (BCHUNKS % NT == 0 || idx < BCHUNKS) *reinterpret_cast<us8*>(bt + swz64(row, ch)) = rw[q];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+  int abase[FM];  // patch row of this lane's A rows at tap (0, 0)
+  const int ch = lane >> 4;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int it = 0; it < items; ++it) {
+    const int t = tbeg + it / ns, sl = it - (it / ns) * ns;
+    if (sl == 0) {
+      const P3Tile T = p3_tile(a, t, ntn);
+      const int64_t hw = static_cast<int64_t>(a.Hi) * a.Wi;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        int64_t m = T.m0 + wm * TM + i * 16 + (lane & 15);
+        if (m >= a.M) m = a.M - 1;  // tail rows read a real pixel; their outputs are not stored
+        const int64_t n = m / hw;
+        const int rem = static_cast<int>(m - n * hw);
+        const int ho = rem / a.Wi, wo = rem - ho * a.Wi;
+        abase[i] = static_cast<int>(n * (a.Hi + 2) + ho - T.g0) * Wp + wo;
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (it + 1 < items) gload(it + 1);  // in flight under the 9 x 16 MFMAs below
+    // taps software-pipelined over two fragment sets: the reads of tap+1 are in flight under the
+    // 16 MFMAs of tap (sched_barrier keeps the compiler from hoisting further reads: registers)
+    bf16x8 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+    auto rd = [&](int tap, bf16x8* fa, bf16x8* fb) {
+      const int toff = (tap / 3) * Wp + (tap % 3);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(patch + swz64(abase[i] + toff, ch));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(bt + swz64(tap * BN + j * 16 + (lane & 15), ch));
+    };
+    auto mm = [&](const bf16x8* fa, const bf16x8* fb) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    rd(0, fa0, fb0);
+#pragma unroll
+    for (int tap = 0; tap < 9; tap += 2) {
+      if (tap + 1 < 9) rd(tap + 1, fa1, fb1);
+      mm(fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (tap + 1 < 9) {
+        if (tap + 2 < 9) rd(tap + 2, fa0, fb0);
+        mm(fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();  // every wave is done with this slice's patch and weights
+    if (sl == ns - 1) {
+      const P3Tile T = p3_tile(a, t, ntn);
+      const int64_t m0 = T.m0;
+      const int n0 = T.n0, mt = static_cast<int>(m0 / BM);
+      unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
+      const int64_t rows_left = a.M - m0;
+      const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(wm * TM + i * 16 + (lane >> 4) * 4 + r) * LDC + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+      if (STATS)
+        det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, 0, lane, tid, nvalid, a.pmean, a.pm2,
+                                                    static_cast<int64_t>(mt) * a.N + n0);
+      __syncthreads();
+      if constexpr (BNB) {
+        bnb_epilogue<BM, BN, NT>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
+      } else {
+        constexpr int CPR = BN / 8;
+#pragma unroll
+        for (int q = 0; q < BM * CPR / NT; ++q) {
+          const int idx = tid + q * NT, row = idx / CPR, cc = idx - row * CPR;
+          if (row < nvalid)
+            *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+        }
+      }
+      __syncthreads();  // the C tile (LDS) is consumed before the next slice lands there
+    }
+    if (it + 1 < items) {
+      lstore(it + 1);
+      __syncthreads();
+    }
+  }
+}
+
+// Largest patch (pixels) any 256-pixel tile of an Nb x H x W image batch needs (host side).
+static int64_t p3_max_patch(int64_t M, int H, int W) {
+  const int64_t hw = static_cast<int64_t>(H) * W;
+  int64_t best = 0;
+  for (int64_t m0 = 0; m0 < M; m0 += kP3BM) {
+    int64_t ml = m0 + kP3BM - 1;
+    if (ml >= M) ml = M - 1;
+    const int64_t na = m0 / hw, nb = ml / hw;
+    const int64_t ga = na * (H + 2) + (m0 - na * hw) / W, gb = nb * (H + 2) + (ml - nb * hw) / W + 2;
+    const int64_t p = (gb - ga + 1) * (W + 2);
+    if (p > best) best = p;
+    if (best > kP3PMAX) break;
+  }
+  return best;
 }
 
 // Input-gradient weight of an R x S conv in one pass: out[c][r][s][k] = W[k][R-1-r][S-1-s][c]
@@ -1291,6 +1555,126 @@ int det_igemm_conv_bnbwd(void* stream, const void* X, const void* W, void* Y, co
            static_cast<const unsigned short*>(bn_x), bn_mean, bn_scale, bn_shift, psum, psumx};
   hipStream_t st = static_cast<hipStream_t>(stream);
   return run_cfg(cfg > 0 ? cfg : auto_cfg(a), st, a, false, false, true);
+}
+
+// igemm3 tile configuration of the stride-2 input gradient for Cin output channels (the launch3
+// family: the class gather needs the 32-deep K tiles); rows per statistics block follow from it.
+static int s2_cfg(int cin, int cfg) {
+  if (cfg > 0) return cfg;
+  return cin % 256 == 0 ? 8 : (cin % 128 == 0 ? 9 : 11);
+}
+int det_igemm_dgrad_s2_rows_per_block(int Cin, int cfg) {
+  const int c = s2_cfg(Cin, cfg);
+  return c >= 12 ? 512 : 256;
+}
+
+// Input gradient of a 3x3 / stride-2 / pad-1 convolution (Hi = 2 Ho, Wi = 2 Wo) without MIOpen:
+//   dX[n, h, w, c] = sum_{r,s,k} dY[n, (h+1-r)/2, (w+1-s)/2, k] W[k][c][r][s]   ((h+1-r), (w+1-s) even)
+// Output pixels of one parity class (h % 2, w % 2) = (ph, pw) see only the taps r == ph + 1 (mod 2):
+// ph = 0 -> r = 1; ph = 1 -> r in {2, 0} at dY rows i, i + 1 (h = 2i + ph), likewise for w.  So each
+// class is a stride-1, pad-0 implicit GEMM over dY with a (1+ph) x (1+pw) kernel whose B taps are
+// gathered from the flipped dgrad weight Wd [Cin][9 * Cout] (det_conv_dgrad_weight: tap r' = 2 - r)
+// through `tapmap`, and whose output rows scatter to the class's pixels (`oscat`): 2.25 taps per
+// pixel on average, no zero-inserted MACs (a dilated stride-1 conv would do 9).  Four launches.
+// bn_x..psumx (all or none): the BNB epilogue of the BatchNorm(+ReLU) whose output this is (mask
+// mode 1), partials [4 * ceil(Nb*Ho*Wo / rpb), Cin], rpb = det_igemm_dgrad_s2_rows_per_block.
+int det_igemm_dgrad_s2(void* stream, const void* dY, const void* Wd, void* dX, const void* zero, int Nb, int Ho, int Wo,
+                       int Cout, int Cin, const void* bn_x, const float* bn_mean, const float* bn_scale,
+                       const float* bn_shift, float* psum, float* psumx, int cfg) {
+  if (Nb <= 0 || Ho <= 0 || Wo <= 0 || Cout <= 0 || Cout % 32 != 0 || Cin <= 0 || Cin % 64 != 0) return -1;
+  const bool bnb = bn_x != nullptr;
+  if (bnb && (!bn_mean || !bn_scale || !bn_shift || !psum || !psumx)) return -2;
+  if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(Wd) | reinterpret_cast<uintptr_t>(dX) |
+        reinterpret_cast<uintptr_t>(zero) | reinterpret_cast<uintptr_t>(bn_x)) & 15) != 0)
+    return -5;
+  const int64_t M = static_cast<int64_t>(Nb) * Ho * Wo;
+  const int64_t dy_bytes = M * Cout * 2;
+  if (dy_bytes >= (static_cast<int64_t>(1) << 31) || static_cast<int64_t>(Cin) * 9 * Cout * 2 >= (static_cast<int64_t>(1) << 31))
+    return -8;
+  const int c = s2_cfg(Cin, cfg);
+  if (c < 8) return -7;
+  const int rpb = det_igemm_dgrad_s2_rows_per_block(Cin, cfg);
+  const int nblk = static_cast<int>((M + rpb - 1) / rpb);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  for (int cls = 0; cls < 4; ++cls) {
+    const int ph = cls >> 1, pw = cls & 1;
+    const int R = 1 + ph, S = 1 + pw;
+    unsigned tapmap = 0;
+    for (int rr = 0; rr < R; ++rr)
+      for (int ss = 0; ss < S; ++ss) {
+        const int rp = ph ? 2 * rr : 1, sp = pw ? 2 * ss : 1;  // flipped-weight tap of class tap (rr, ss)
+        tapmap |= static_cast<unsigned>(rp * 3 + sp) << (4 * (rr * S + ss));
+      }
+    IgArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(Wd), static_cast<unsigned short*>(dX),
+             static_cast<const unsigned short*>(zero), nullptr, nullptr, M, Cin, R * S * Cout, Cout, Ho, Wo, Ho, Wo, 1, 0,
+             S, R, dy_bytes, static_cast<const unsigned short*>(bn_x), bn_mean, bn_scale, bn_shift, psum, psumx,
+             9 * Cout, tapmap, 1 + cls, cls * nblk};
+    const int rc = run_cfg(c, st, a, false, false, bnb);
+    if (rc != 0) return rc;
+  }
+  return 0;
+}
+
+// 3x3 / stride-1 / pad-1 convolution on the halo-patch kernel (conv3p, see above): Y[M, N] (M = Nb*H*W)
+// = conv(op(X), W) with W in KRSC [N][9][Cin], op = relu(x * pro_scale + pro_shift) when given (the
+// preceding BatchNorm + ReLU; zero padding is not transformed).  pmean/pm2 (nullable, [ceil(M/256),
+// N]): BN statistics partials of Y.  bn_x..psumx (all or none): the BN-backward epilogue of a BN
+// whose output X this conv's input gradient is (mask mode 1), partials [ceil(M/256), N].  Cin % 32,
+// N % 64, 16-B aligned; -6 when a tile's patch would exceed 512 pixels (very wide images).
+int det_conv3p(void* stream, const void* X, const void* W, void* Y, int Nb, int H, int Wd, int Cin, int N,
+               const float* pro_scale, const float* pro_shift, float* pmean, float* pm2, const void* bn_x,
+               const float* bn_mean, const float* bn_scale, const float* bn_shift, float* psum, float* psumx,
+               int grid) {
+  if (Nb <= 0 || H <= 0 || Wd <= 0 || Cin <= 0 || Cin % 32 != 0 || N <= 0 || N % kP3BN != 0) return -1;
+  if ((pro_scale == nullptr) != (pro_shift == nullptr) || (pmean == nullptr) != (pm2 == nullptr)) return -2;
+  const bool bnb = bn_x != nullptr;
+  if (bnb && (!bn_mean || !bn_scale || !bn_shift || !psum || !psumx || pmean || pro_scale)) return -2;
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y) |
+        reinterpret_cast<uintptr_t>(bn_x)) & 15) != 0)
+    return -5;
+  const int64_t M = static_cast<int64_t>(Nb) * H * Wd;
+  if (p3_max_patch(M, H, Wd) > kP3PMAX) return -6;
+  IgArgs a{};
+  a.X = static_cast<const unsigned short*>(X);
+  a.W = static_cast<const unsigned short*>(W);
+  a.Y = static_cast<unsigned short*>(Y);
+  a.pmean = pmean;
+  a.pm2 = pm2;
+  a.M = M;
+  a.N = N;
+  a.K = 9 * Cin;
+  a.Cin = Cin;
+  a.Hi = a.Ho = H;
+  a.Wi = a.Wo = Wd;
+  a.stride = 1;
+  a.pad = 1;
+  a.R = a.S = 3;
+  a.bn_x = static_cast<const unsigned short*>(bn_x);
+  a.bn_mean = bn_mean;
+  a.bn_scale = bn_scale;
+  a.bn_shift = bn_shift;
+  a.psum = psum;
+  a.psumx = psumx;
+  a.pro_scale = pro_scale;
+  a.pro_shift = pro_shift;
+  const int ntn = N / kP3BN;
+  const int64_t ntiles64 = ((M + kP3BM - 1) / kP3BM) * ntn;
+  if (ntiles64 >= (static_cast<int64_t>(1) << 31)) return -4;
+  const int ntiles = static_cast<int>(ntiles64);
+  static const int env_grid = [] {
+    const char* e = std::getenv("DET_CONV3P_GRID");
+    return e ? std::atoi(e) : 0;
+  }();
+  int g = grid > 0 ? grid : (env_grid > 0 ? env_grid : 256);  // one persistent block per CU
+  if (g > ntiles) g = ntiles;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 gd(static_cast<unsigned>(g)), bd(512);
+  if (bnb) hipLaunchKernelGGL((conv3p_kernel<false, false, true>), gd, bd, kP3SMEM, st, a, ntiles, ntn);
+  else if (pro_scale && pmean) hipLaunchKernelGGL((conv3p_kernel<true, true, false>), gd, bd, kP3SMEM, st, a, ntiles, ntn);
+  else if (pro_scale) hipLaunchKernelGGL((conv3p_kernel<true, false, false>), gd, bd, kP3SMEM, st, a, ntiles, ntn);
+  else if (pmean) hipLaunchKernelGGL((conv3p_kernel<false, true, false>), gd, bd, kP3SMEM, st, a, ntiles, ntn);
+  else hipLaunchKernelGGL((conv3p_kernel<false, false, false>), gd, bd, kP3SMEM, st, a, ntiles, ntn);
+  return static_cast<int>(hipGetLastError());
 }
 
 int det_igemm_conv(void* stream, const void* X, const void* W, void* Y, const void* zero, int64_t M, int N, int Cin,

@@ -73,7 +73,9 @@ class MetricWriter:
 
 
 def build(env: Any, checkpoint_storage: Dict[str, Any]) -> TensorboardManager:
-    base = os.path.join(tempfile.gettempdir(), "tensorboard", f"{env.det_experiment_id}-{env.det_trial_id}-{os.getpid()}")
+    # per host account: trial processes of different users (agent user groups) share the host's /tmp
+    base = os.path.join(tempfile.gettempdir(), f"tensorboard-{os.getuid()}",
+                        f"{env.det_experiment_id}-{env.det_trial_id}-{os.getpid()}")
     sync = None
     if checkpoint_storage.get("type", "shared_fs") == "shared_fs":
         sync = get_base_path(checkpoint_storage, env.det_experiment_id, env.det_trial_id)

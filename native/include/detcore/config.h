@@ -24,6 +24,9 @@ std::vector<std::string> ValidateExperimentConfig(const Json& cfg);
 
 // Master config (reference master/internal/config.go:24-86): port, store dir, scheduler,
 // fitting policy, resource pools, checkpoint storage, task defaults.
+// "" when g is a valid agent user group {uid, gid, user, group}, else why not.
+std::string ValidateAgentUserGroup(const Json& g);
+
 struct MasterConfig {
   std::string listen_host = "0.0.0.0";
   int port = 8080;
@@ -53,6 +56,9 @@ struct MasterConfig {
   // logging.{type: default | elastic, host, port, index} (reference master/internal/config/elastic.go):
   // with elastic, trial and task logs live in Elasticsearch instead of the local segments
   Json logging;
+  // security.default_agent_user_group {uid, gid, user, group}: the host account tasks of users with no
+  // linked agent user run as (reference model.AgentUserGroup); null = the agent's own account
+  Json default_agent_user_group;
   static MasterConfig FromJson(const Json& j);
   Json ToJson() const;
   std::vector<std::string> Validate() const;

@@ -63,6 +63,10 @@ class Master {
   const MasterConfig& config() const { return cfg_; }
   // task_container_defaults (+ TLS trust material) into a task's env / shipped files
   void AddTaskDefaults(Json& env, Json& files) const;
+  // The host account {uid, gid, user, group} a task of `username` runs as: the user's linked agent
+  // user group, else security.default_agent_user_group, else null (the agent's own account).
+  Json AgentUserGroupFor(const std::string& username);
+  Json AgentUserGroupForExperiment(int64_t experiment_id);
   bool tls() const { return !tls_cert_pem_.empty(); }
   actor::Ref Pool(const std::string& name);
   bool SendToAgent(const std::string& agent_id, const Json& msg);

@@ -27,6 +27,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <ftw.h>
+#include <grp.h>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -264,7 +266,7 @@ class Agent {
   // Returns the connected socket (the exit status arrives on it later) and sets *child; -1 when the
   // zygote is unavailable or refused, in which case the caller fork/execs.
   int ZygoteSpawn(const std::vector<std::string>& args, const std::map<std::string, std::string>& env,
-                  const std::string& cwd, int out_fd, int err_fd, pid_t* child) {
+                  const std::string& cwd, int out_fd, int err_fd, pid_t* child, int uid = -1, int gid = -1) {
     if (zygote_pid_ <= 0 || args.size() < 3 || args[1] != "-m") return -1;
     int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (fd < 0) return -1;
@@ -287,6 +289,10 @@ class Agent {
     for (auto& kv : env) je[kv.first] = kv.second;
     req["env"] = je;
     req["cwd"] = cwd;
+    if (uid >= 0) {  // the zygote child switches to the task owner's account after fork
+      req["uid"] = uid;
+      req["gid"] = gid;
+    }
     std::string body = req.dump();
     std::string msg(4, '\0');
     uint32_t n = static_cast<uint32_t>(body.size());
@@ -330,6 +336,20 @@ class Agent {
     }
     *child = static_cast<pid_t>(std::atol(line.c_str() + 4));
     return *child > 0 ? fd : (close(fd), -1);
+  }
+
+  // chown -R (no symlink following): the task's work dir belongs to the account it runs as
+  static void ChownTree(const std::string& root, uid_t uid, gid_t gid) {
+    static uid_t s_uid;
+    static gid_t s_gid;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> g(mu);
+    s_uid = uid;
+    s_gid = gid;
+    nftw(root.c_str(), [](const char* p, const struct stat*, int, struct FTW*) -> int {
+      if (lchown(p, s_uid, s_gid) != 0) return 0;  // best effort per entry
+      return 0;
+    }, 32, FTW_PHYS);
   }
 
   static std::string ReadLine(int fd) {
@@ -459,6 +479,44 @@ class Agent {
     if (env.count("PYTHONPATH") && !env["PYTHONPATH"].empty()) pp += ":" + env["PYTHONPATH"];
     env["PYTHONPATH"] = pp;
     env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0";
+    // the task owner's host account (reference master/pkg/tasks/task.go:60-100 getUser +
+    // injectUserArchive): passwd/group/shadow entries for it, the work dir handed over to it, and
+    // the process started as uid:gid (setgroups/setgid/setuid after fork, here or in the zygote)
+    int run_uid = -1, run_gid = -1;
+    if (spec["user"].is_object()) {
+      const Json& u = spec["user"];
+      run_uid = static_cast<int>(u.get_int("uid", -1));
+      run_gid = static_cast<int>(u.get_int("gid", -1));
+      const std::string uname = u.get_string("user", ""), gname = u.get_string("group", "");
+      if (run_uid < 0 || run_gid < 0 || uname.empty() || gname.empty()) {
+        State(cid, "Terminated", 1, "invalid agent user group in the container spec");
+        return;
+      }
+      if (geteuid() != 0 && static_cast<uid_t>(run_uid) != geteuid()) {
+        State(cid, "Terminated", 1, "det-agent runs as uid " + std::to_string(geteuid()) +
+                                        ", not root: cannot start a task as uid " + std::to_string(run_uid));
+        return;
+      }
+      const std::string etc = dir + "/.det/etc";
+      MkdirP(etc);
+      std::ofstream(etc + "/passwd") << uname << ":x:" << run_uid << ":" << run_gid << "::" << dir << ":/bin/sh\n";
+      std::ofstream(etc + "/group") << gname << ":x:" << run_gid << ":\n";
+      std::ofstream(etc + "/shadow") << uname << ":!!:::::::\n";
+      ::chmod((etc + "/shadow").c_str(), 0600);
+      env["USER"] = env["LOGNAME"] = uname;
+      env["HOME"] = dir;
+      env["DET_AGENT_USER"] = uname;
+      env["DET_AGENT_GROUP"] = gname;
+      env["DET_TASK_ETC"] = etc;
+      if (geteuid() == 0) {
+        ChownTree(dir, static_cast<uid_t>(run_uid), static_cast<gid_t>(run_gid));
+        // the task account must be able to reach its own work dir through the agent's
+        for (const std::string& d : {o_.work_dir, dir.substr(0, dir.rfind('/'))}) {
+          struct stat st {};
+          if (::stat(d.c_str(), &st) == 0) ::chmod(d.c_str(), (st.st_mode & 07777) | 0111);
+        }
+      }
+    }
     std::vector<std::string> envs;
     for (auto& kv : env) envs.push_back(kv.first + "=" + kv.second);
     std::vector<char*> envp;
@@ -481,7 +539,7 @@ class Agent {
     pid_t pid = -1;
     int zfd = spec["cmd"].is_array() && spec["cmd"].size() > 0
                   ? -1
-                  : ZygoteSpawn(args, env, dir, out_pipe[1], err_pipe[1], &pid);
+                  : ZygoteSpawn(args, env, dir, out_pipe[1], err_pipe[1], &pid, run_uid, run_gid);
     if (zfd < 0) pid = fork();
     if (pid == 0) {
       setpgid(0, 0);
@@ -489,7 +547,17 @@ class Agent {
       dup2(err_pipe[1], 2);
       close(out_pipe[0]);
       close(err_pipe[0]);
-      if (chdir(dir.c_str()) != 0) _exit(127);
+      if (run_uid >= 0 && static_cast<uid_t>(run_uid) != geteuid()) {
+        const gid_t g = static_cast<gid_t>(run_gid);
+        if (setgroups(1, &g) != 0 || setgid(g) != 0 || setuid(static_cast<uid_t>(run_uid)) != 0) {
+          std::fprintf(stderr, "det-agent: cannot switch to uid %d gid %d: %s\n", run_uid, run_gid, std::strerror(errno));
+          _exit(126);
+        }
+      }
+      if (chdir(dir.c_str()) != 0) {
+        std::fprintf(stderr, "det-agent: cannot enter the work dir %s: %s\n", dir.c_str(), std::strerror(errno));
+        _exit(127);
+      }
       execvpe(argv[0], argv.data(), envp.data());
       _exit(127);
     }

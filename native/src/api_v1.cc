@@ -367,6 +367,14 @@ void Master::InstallApiV1() {
     for (auto& row : store_->Where("users", "username", Json(name))) {
       Json u = Json::object();
       for (const char* k : {"id", "username", "admin", "active"}) u[k] = row[k];
+      if (row["agent_user_group"].is_object()) {
+        Json g = Json::object();
+        g["agentUid"] = row["agent_user_group"]["uid"];
+        g["agentGid"] = row["agent_user_group"]["gid"];
+        g["agentUser"] = row["agent_user_group"]["user"];
+        g["agentGroup"] = row["agent_user_group"]["group"];
+        u["agentUserGroup"] = g;
+      }
       Json out = Json::object();
       out["user"] = u;
       return JV(200, out);
@@ -389,6 +397,14 @@ void Master::InstallApiV1() {
     for (auto& row : store_->Where("users", "username", Json(r.Param("username")))) {
       Json u = Json::object();
       for (const char* k : {"id", "username", "admin", "active"}) u[k] = row[k];
+      if (row["agent_user_group"].is_object()) {
+        Json g = Json::object();
+        g["agentUid"] = row["agent_user_group"]["uid"];
+        g["agentGid"] = row["agent_user_group"]["gid"];
+        g["agentUser"] = row["agent_user_group"]["user"];
+        g["agentGroup"] = row["agent_user_group"]["group"];
+        u["agentUserGroup"] = g;
+      }
       Json out = Json::object();
       out["user"] = u;
       return JV(200, out);

@@ -295,6 +295,8 @@ MasterConfig MasterConfig::FromJson(const Json& j) {
     c.tls_key = j["security"]["tls"].get_string("key", "");
   }
   if (j["logging"].is_object()) c.logging = j["logging"];
+  if (j["security"]["default_agent_user_group"].is_object())
+    c.default_agent_user_group = j["security"]["default_agent_user_group"];
   const Json& tcd = j["task_container_defaults"];
   if (tcd.is_object()) {
     c.shm_size_bytes = tcd.get_int("shm_size_bytes", c.shm_size_bytes);
@@ -322,6 +324,19 @@ static bool ValidPortRange(const std::string& r) {
   return lo <= hi && hi <= 65535;
 }
 
+// reference master/internal/user/service.go:28-45 (agentUserGroup.Validate) and
+// master/pkg/model/agent_user_group.go:27-47: all four fields set, ids non-negative
+std::string ValidateAgentUserGroup(const Json& g) {
+  if (!g.is_object()) return "must be an object {uid, gid, user, group}";
+  if (!g["uid"].is_number()) return "uid must be set";
+  if (!g["gid"].is_number()) return "gid must be set";
+  if (g.get_string("user", "").empty()) return "user must be set";
+  if (g.get_string("group", "").empty()) return "group must be set";
+  if (g.get_int("uid", -1) < 0) return "uid less than zero";
+  if (g.get_int("gid", -1) < 0) return "gid less than zero";
+  return "";
+}
+
 std::vector<std::string> MasterConfig::Validate() const {
   // reference TaskContainerDefaultsConfig.Validate + TLS pairing
   std::vector<std::string> e;
@@ -331,6 +346,10 @@ std::vector<std::string> MasterConfig::Validate() const {
   if (!ValidPortRange(gloo_port_range)) e.push_back("task_container_defaults.gloo_port_range must be \"MIN:MAX\"");
   if (tls_cert.empty() != tls_key.empty()) e.push_back("security.tls needs both cert and key");
   if (port <= 0 || port > 65535) e.push_back("port must be in 1..65535");
+  if (default_agent_user_group.is_object()) {
+    const std::string why = ValidateAgentUserGroup(default_agent_user_group);
+    if (!why.empty()) e.push_back("security.default_agent_user_group: " + why);
+  }
   if (logging.is_object()) {
     const std::string t = logging.get_string("type", "default");
     if (t != "default" && t != "elastic") e.push_back("logging.type must be default or elastic");
@@ -381,6 +400,7 @@ Json MasterConfig::ToJson() const {
   tls["cert"] = tls_cert;
   tls["key"] = tls_key;
   j["security"]["tls"] = tls;
+  j["security"]["default_agent_user_group"] = default_agent_user_group;
   Json tcd = Json::object();
   tcd["shm_size_bytes"] = static_cast<long long>(shm_size_bytes);
   tcd["network_mode"] = network_mode;

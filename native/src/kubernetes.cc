@@ -320,6 +320,10 @@ void KubernetesRM::CreatePod(const std::string& agent, const Json& msg) {
   container["command"] = cmd;
   container["env"] = env;
   container["workingDir"] = "/run/determined/workdir";
+  if (spec["user"].is_object()) {  // the task owner's agent user group (reference kubernetes/spec.go)
+    container["securityContext"]["runAsUser"] = spec["user"].get_int("uid", 0);
+    container["securityContext"]["runAsGroup"] = spec["user"].get_int("gid", 0);
+  }
   Json mounts = Json::array();
   Json mount = Json::object();
   mount["name"] = "det-spec";

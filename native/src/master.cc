@@ -469,6 +469,7 @@ void Master::InstallRoutes() {
     for (auto& u : store_->Scan("users")) {
       Json v = Json::object();
       for (const char* k : {"id", "username", "admin", "active"}) v[k] = u[k];
+      if (u["agent_user_group"].is_object()) v["agent_user_group"] = u["agent_user_group"];
       out.push_back(v);
     }
     return J(200, out);
@@ -489,11 +490,32 @@ void Master::InstallRoutes() {
   });
   http_.Route("PATCH", "/users/:name", [this](const net::Request& r) {
     Json body = Json::parse(r.body);
+    // with authentication on, only an admin changes another user, admin/active flags or the agent
+    // user group (reference user/service.go:248-280, AdminCanBeModifiedBy)
+    bool caller_admin = true;
+    std::string caller;
+    if (cfg_.require_auth) {
+      caller = UserForRequest(r);
+      caller_admin = false;
+      for (auto& cu : store_->Where("users", "username", Json(caller))) caller_admin = cu.get_bool("admin", false);
+    }
+    const bool privileged = body.has("active") || body.has("admin") || body.has("agent_user_group");
+    if (!caller_admin && (privileged || caller != r.Param("name"))) return Err(403, "only an admin can do that");
     for (auto& u : store_->Where("users", "username", Json(r.Param("name")))) {
       Json patch = Json::object();
       if (body.has("password")) patch["password_hash"] = HashPassword(u.get_string("salt", ""), body["password"].as_string());
       if (body.has("active")) patch["active"] = body["active"];
       if (body.has("admin")) patch["admin"] = body["admin"];
+      if (body.has("agent_user_group")) {
+        const std::string why = ValidateAgentUserGroup(body["agent_user_group"]);
+        if (!why.empty()) return Err(400, why);
+        Json g = Json::object();
+        g["uid"] = body["agent_user_group"].get_int("uid", 0);
+        g["gid"] = body["agent_user_group"].get_int("gid", 0);
+        g["user"] = body["agent_user_group"].get_string("user", "");
+        g["group"] = body["agent_user_group"].get_string("group", "");
+        patch["agent_user_group"] = g;
+      }
       store_->Update("users", u["id"].as_int(), patch);
       return J(200, Json::object());
     }
@@ -985,6 +1007,7 @@ void Master::InstallRoutes() {
     row["start_time"] = NowRFC3339();
     row["description"] = cfg.get_string("description", "");
     row["type"] = cfg.get_string("type", "command");
+    row["owner"] = UserForRequest(r).empty() ? std::string("determined") : UserForRequest(r);
     int64_t id = store_->Insert("commands", row);
     Json ctxrow = Json::object();
     ctxrow["files"] = body["context"].is_array() ? body["context"] : Json::array();
@@ -1428,6 +1451,19 @@ void Master::RestoreExperiments() {
     ex->Tell(ReplayEvents{events});
     Log("restoring experiment " + std::to_string(id) + " from " + std::to_string(events.size()) + " events");
   }
+}
+
+Json Master::AgentUserGroupFor(const std::string& username) {
+  if (!username.empty())
+    for (auto& u : store_->Where("users", "username", Json(username)))
+      if (u["agent_user_group"].is_object()) return u["agent_user_group"].clone();
+  return cfg_.default_agent_user_group.is_object() ? cfg_.default_agent_user_group.clone() : Json();
+}
+
+Json Master::AgentUserGroupForExperiment(int64_t experiment_id) {
+  Json e;
+  if (!store_->Get("experiments", experiment_id, &e)) return AgentUserGroupFor("");
+  return AgentUserGroupFor(e.get_string("owner", ""));
 }
 
 void Master::AddTaskDefaults(Json& env, Json& files) const {

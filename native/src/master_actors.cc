@@ -667,6 +667,9 @@ void TrialActor::OnAllocated(Context& ctx, const ResourcesAllocated& ra) {
     spec["experiment_id"] = exp_id_;
     spec["trial_id"] = trial_id_;
     spec["rank"] = c.rank;
+    // the owner's host account (reference tasks/task.go:60-100: passwd/group files + run as uid:gid)
+    Json aug = m_->AgentUserGroupForExperiment(exp_id_);
+    if (aug.is_object()) spec["user"] = aug;
     Json dev = Json::array();
     for (int d : c.devices) dev.push_back(d);
     Json msg = Json::object();
@@ -1101,6 +1104,11 @@ void CommandActor::Receive(Context& ctx) {
     spec["env"] = env;
     spec["files"] = files;
     spec["cmd"] = config_["entrypoint"];
+    {
+      Json row;
+      Json aug = m_->AgentUserGroupFor(m_->store().Get("commands", id_, &row) ? row.get_string("owner", "") : "");
+      if (aug.is_object()) spec["user"] = aug;
+    }
     spec["task_id"] = task_id_;
     spec["context_url"] = "/commands/" + std::to_string(id_) + "/context";
     Json dev = Json::array();

@@ -30,6 +30,8 @@ class NoOpTrialController(trial.CallbackTrialController):
             raise errors.InvalidHP("invalid hyperparameter configuration")
         self.metric = float(hp.get("metrics_base", 0.9)) if self.load_path is None else self.metric
         self.chaos = random.Random(int(self.env.trial_seed) * 7919 + int(time.time() * 1000) % 100000)
+        if os.environ.get("DET_PRINT_UID"):  # agent user groups: which host account runs the trial
+            print(f"trial process uid={os.getuid()} gid={os.getgid()}", flush=True)
 
     @staticmethod
     def from_trial(trial_inst: Any, context: Any, env: Any, workloads: Any, load_path: Any, rendezvous_info: Any,

@@ -342,7 +342,7 @@ def test_deferred_forward_apply_never_reaches_hooks_or_user_code(gpu):
     torch.manual_seed(0)
     model = resnet.resnet50(num_classes=10, zero_init_residual=False).to(gpu).to(memory_format=torch.channels_last)
     for mod in model.modules():
-        if isinstance(mod, torch.nn.Conv2d):
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
             mod.to(torch.bfloat16)
     x = torch.randn(4, 4, 64, 64, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     assert model.layer1[0].defer_out and model.layer1[1].defer_out

@@ -230,3 +230,86 @@ def test_dgrad_s2_bn_backward_epilogue_matches_unfused(gpu):
             conv.FUSE_BN_BWD = True
     for a, b in zip(*outs):
         torch.testing.assert_close(b, a, rtol=2e-2, atol=2e-2 * float(a.abs().max()) + 1e-6)
+
+
+P3_SHAPES = [  # (Nb, Cin, H, W, Cout)
+    (2, 64, 56, 56, 64),    # ResNet layer1 (reduced batch)
+    (3, 128, 28, 28, 128),  # layer2: two N tiles per pixel tile
+    (4, 64, 14, 14, 64),    # 256-pixel tiles span images (patch with per-image padding rows)
+    (1, 32, 7, 9, 64),      # Cin 32 (one slice), odd width, M < one tile
+    (6, 64, 7, 7, 128),     # tiles spanning 5+ images
+]
+
+
+@pytest.mark.parametrize("case", P3_SHAPES)
+def test_conv3p_exact_on_integer_operands(gpu, case):
+    """det_conv3p (input staged once per tile as a halo patch, 9 taps read at row offsets) ==
+    F.conv2d exactly on small-integer operands, with and without the BN+ReLU prologue (integer
+    scale/shift keep it exact; the zero padding must not be transformed)."""
+    nb, cin, h, w, cout = case
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randint(-2, 3, (nb, cin, h, w), generator=g).to(torch.bfloat16)
+    wt = torch.randint(-2, 3, (cout, cin, 3, 3), generator=g).to(torch.bfloat16)
+    xg = x.to(gpu).contiguous(memory_format=torch.channels_last)
+    wk = conv.krsc(wt.to(gpu).contiguous(memory_format=torch.channels_last))
+    y, _ = conv.conv3p(xg, wk, cout)
+    ref = F.conv2d(x.float(), wt.float(), padding=1)
+    torch.testing.assert_close(y.float().cpu(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
+    sc = torch.randint(-1, 3, (cin,), generator=g).float()
+    sh = torch.randint(-2, 2, (cin,), generator=g).float()
+    yp, _ = conv.conv3p(xg, wk, cout, pro=(sc.to(gpu), sh.to(gpu)))
+    z = torch.relu(x.float() * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    refp = F.conv2d(z, wt.float(), padding=1)
+    torch.testing.assert_close(yp.float().cpu(), refp.to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+def test_conv3p_stats_and_bn_backward_epilogues(gpu):
+    nb, cin, h, w, cout = 4, 64, 28, 28, 128  # M = 3136: ragged last 256-row block
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = (torch.randn(nb, cin, h, w, generator=g)).to(torch.bfloat16)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) / 24).to(torch.bfloat16)
+    xg = x.to(gpu).contiguous(memory_format=torch.channels_last)
+    wk = conv.krsc(wt.to(gpu).contiguous(memory_format=torch.channels_last))
+    y, (pm, pq, rpb) = conv.conv3p(xg, wk, cout, stats=True)
+    yr = y.permute(0, 2, 3, 1).reshape(-1, cout).double().cpu()
+    m = yr.shape[0]
+    cnt = torch.full((pm.shape[0], 1), float(rpb), dtype=torch.float64)
+    cnt[-1, 0] = float(m - (pm.shape[0] - 1) * rpb)
+    mean = (pm.double().cpu() * cnt).sum(0) / m
+    var = (pq.double().cpu() + cnt * (pm.double().cpu() - mean) ** 2).sum(0) / m
+    torch.testing.assert_close(mean, yr.mean(0), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(var, yr.var(0, unbiased=False), rtol=1e-4, atol=1e-5)
+    # BNB: the output is the gradient reaching a BN(+ReLU) with input bx: masked, with partial sums
+    bx = torch.randn(nb, cout, h, w, generator=g).to(torch.bfloat16).to(gpu).contiguous(memory_format=torch.channels_last)
+    bmean = torch.randn(cout, generator=g).to(gpu)
+    bsc = torch.rand(cout, generator=g).add(0.5).to(gpu)
+    bsh = torch.randn(cout, generator=g).to(gpu)
+    d, (ps, psx, _) = conv.conv3p(xg, wk, cout, bnb=(bx, bmean, bsc, bsh))
+    mask = (bx.float() * bsc.view(1, -1, 1, 1) + bsh.view(1, -1, 1, 1)) > 0
+    want = torch.where(mask, y.float(), torch.zeros_like(y.float())).to(torch.bfloat16)
+    assert torch.equal(d, want)
+    df = d.float().permute(0, 2, 3, 1).reshape(-1, cout).double()
+    xf = bx.float().permute(0, 2, 3, 1).reshape(-1, cout).double()
+    torch.testing.assert_close(ps.double().sum(0), df.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(psx.double().sum(0), (df * (xf - bmean.double())).sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_conv_rs_routes_thin_3x3_to_conv3p(gpu):
+    """The autograd 3x3 path runs conv3p for N <= CONV3P_MAX_N (forward and stride-1 dgrad) and the
+    result matches the fp32 reference."""
+    torch.manual_seed(0)
+    m = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).to(gpu).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 64, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    before = dict(conv.CONV3P_COUNTS)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv.conv_rs(x, m)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    assert conv.CONV3P_COUNTS["fwd"] == before["fwd"] + 1
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=1)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)

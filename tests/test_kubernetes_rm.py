@@ -110,3 +110,27 @@ def test_gpu_pod_requests_amd_gpus(tmp_path):
         assert env["DET_USE_GPU"] == "true" and env["DET_SLOT_IDS"] == "[0,1,2,3]"
         cl.post(f"/experiments/{eid}/kill")
         cl.wait_for_experiment(eid, timeout=60)
+
+
+def test_pod_runs_as_the_owners_agent_user_group(tmp_path):
+    """Agent user groups on the Kubernetes RM: the pod's container securityContext carries the
+    experiment owner's linked uid/gid (the default account of security.default_agent_user_group
+    here, as the experiment is created without a session)."""
+    cfgfile = tmp_path / "master.yaml"
+    cfgfile.write_text("security:\n  default_agent_user_group: {uid: 1234, gid: 5678, user: u, group: g}\n")
+    with FakeKube(nodes=1) as kube:
+        args = ["--kubernetes-api", kube.address, "--kubernetes-namespace", "det", "--kubernetes-slot-type", "cpu",
+                "--kubernetes-max-slots-per-pod", "8", "--kubernetes-cpu-slots-per-node", "1",
+                "--kubernetes-master-host", "127.0.0.1", "--config-file", str(cfgfile)]
+        with LocalCluster(agents=0, store_dir=str(tmp_path / "store"), checkpoint_dir=str(tmp_path / "ckpt"),
+                          log_dir=str(tmp_path), tick_ms=50, master_args=args) as c:
+            cl = MasterClient(c.address)
+            eid = cl.create_experiment(_cfg({"name": "single", "max_length": {"batches": 10}}), read_context(NOOP))["id"]
+            deadline = time.time() + 60
+            while time.time() < deadline and not kube.created:
+                time.sleep(0.1)
+            assert kube.created
+            sc = kube.created[0]["spec"]["containers"][0]["securityContext"]
+            assert sc == {"runAsUser": 1234, "runAsGroup": 5678}
+            cl.post(f"/experiments/{eid}/kill")
+            cl.wait_for_experiment(eid, timeout=60)
