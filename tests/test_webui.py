@@ -78,3 +78,70 @@ def test_webui_script_parses(tmp_path):
     f.write_text(js)
     r = subprocess.run([node, "--check", str(f)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_webui_hp_visualization_and_master_logs(tmp_path):
+    """The HP-visualization tab (parallel coordinates / scatter plots at the best validation or at a
+    training length from the TrialsSnapshot stream), the master-logs page (MasterLogs stream) and
+    the dashboard: their endpoints answer on a live master, and the page's drawing code turns an
+    adaptive search's trials into one line / point per trial (run under node with DOM stubs)."""
+    import json
+    import shutil
+    import subprocess
+
+    import pytest
+
+    with LocalCluster(agents=1, slots_per_agent=1, log_dir=str(tmp_path), tick_ms=50) as c:
+        base = f"http://{c.address}"
+        cl = MasterClient(c.address)
+        eid = cl.create_experiment({"description": "hp", "entrypoint": "model_def:NoOpTrial",
+                                    "hyperparameters": {"global_batch_size": 4,
+                                                        "metrics_base": {"type": "double", "minval": 0.5,
+                                                                         "maxval": 0.9}},
+                                    "searcher": {"name": "random", "metric": "validation_error", "max_trials": 3,
+                                                 "max_length": {"batches": 4}}, "scheduling_unit": 2},
+                                   read_context(NOOP))["id"]
+        assert cl.wait_for_experiment(eid, timeout=180) == "COMPLETED"
+        trials = requests.get(base + f"/api/v1/experiments/{eid}/trials", timeout=10).json()["trials"]
+        assert len(trials) == 3 and all(t["bestValidation"] for t in trials)
+        r = requests.get(base + f"/api/v1/experiments/{eid}/metrics-stream/trials-snapshot",
+                         params={"metric_name": "validation_error", "metric_type": "METRIC_TYPE_VALIDATION",
+                                 "batches_processed": 4, "period_seconds": 1}, timeout=30, stream=True)
+        snap = json.loads(next(l for l in r.iter_lines() if l))["result"]["trials"]
+        assert sorted(t["trialId"] for t in snap) == sorted(t["id"] for t in trials)
+        assert all("metrics_base" in t["hparams"] and isinstance(t["metric"], float) for t in snap)
+        r.close()
+        logs = [json.loads(l)["result"]["logEntry"]["message"] for l in
+                requests.get(base + "/api/v1/master/logs", params={"limit": 5}, timeout=10).iter_lines() if l]
+        assert 1 <= len(logs) <= 5 and any("experiment" in l for l in logs), logs
+        config = requests.get(base + f"/api/v1/experiments/{eid}", timeout=10).json()["config"]
+    html = WEBUI.read_text()
+    for needle in ("#/logs", "#/dashboard", "/hp/parcoords", "/hp/scatter", "trials-snapshot", "/api/v1/master/logs"):
+        assert needle in html, needle
+    node = shutil.which("node") or shutil.which("nodejs")
+    if node is None:
+        pytest.skip("node not installed")
+    js = html[html.index("<script>") + len("<script>"):html.index("</script>")].replace("??", "||")
+    stubs = """
+const el = () => ({textContent: "", innerHTML: "", replaceChildren() {}, set onclick(f) {}});
+const document = {getElementById: el, createElement: el};
+const localStorage = {getItem: () => null, setItem() {}};
+const window = {addEventListener() {}};
+const location = {hash: "#/"};
+function setInterval() {}
+async function fetch() { return {status: 401, ok: false, json: async () => ({})}; }
+"""
+    check = f"""
+const config = {json.dumps(config)}, trials = {json.dumps(trials)};
+const axes = hpAxes(config, trials);
+if (axes.length !== 1 || axes[0].name !== "metrics_base") throw new Error("axes " + JSON.stringify(axes));
+const pts = trials.map((t) => ({{trialId: t.id, hparams: t.hparams, metric: t.bestValidation.searcherMetric}}));
+const pc = parcoords(axes, pts, "validation_error", true), sc = scatterPlots(axes, pts, "validation_error", true);
+if ((pc.match(/<polyline/g) || []).length !== 3) throw new Error("parcoords " + pc);
+if ((sc.match(/<circle/g) || []).length !== 3) throw new Error("scatter " + sc);
+console.log("ok");
+"""
+    f = tmp_path / "ui_test.js"
+    f.write_text(stubs + js + check)
+    r = subprocess.run([node, str(f)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
