@@ -164,6 +164,9 @@ _SIGNATURES = {
     # stream, X, W [N][9][Cin], Y, Nb, H, W, Cin, N, pro_scale, pro_shift, pmean, pm2, bn_x, bn_mean,
     # bn_scale, bn_shift, psum, psumx, grid (0 = one persistent block per CU)
     "det_conv3p": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 10 + [c_int], c_int),
+    "det_conv3p_wgrad_ws_elems": ([c_i64, c_int, c_int], c_i64),
+    # stream, dY, X, out, out_dtype, Nb, H, W, Cin, N, ws, out_scale
+    "det_conv3p_wgrad": ([c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_float], c_int),
     # stream, dY, X, out, out_dtype, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, ws, out_scale
     "det_conv_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 10 + [c_void_p, c_float], c_int),
     "det_igemm_wgrad_ws_elems": ([c_i64, c_int, c_int, c_int], c_i64),

@@ -157,7 +157,7 @@ def igemm_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
 # (det_igemm.hip conv3p: the input staged once per 256-pixel tile instead of once per tap); wider
 # ones stay on igemm3, whose 256 x 256 tiles already reuse each staged row over 256 columns.
 CONV3P_MAX_N = int(os.environ.get("DET_CONV3P_MAX_N", "128"))
-CONV3P_COUNTS = {"fwd": 0, "dgrad": 0}
+CONV3P_COUNTS = {"fwd": 0, "dgrad": 0, "wgrad": 0}
 
 
 def conv3p_ok(cin: int, cout: int, r: int, s: int, stride: int, pad: int) -> bool:
@@ -198,6 +198,33 @@ def conv3p(x: torch.Tensor, wk: torch.Tensor, cout: int, stats: bool = False, pr
         return y, (pm_b, pq_b, 256)
     CONV3P_COUNTS["fwd"] += 1
     return y, ((pm, pq, 256) if stats else None)
+
+
+CONV3P_WGRAD = os.environ.get("DET_CONV3P_WGRAD", "1") != "0"  # A/B switch: MIOpen's wrw kernels
+
+
+def conv3p_wgrad_ok(cin: int, cout: int, r: int, s: int, stride: int, pad: int) -> bool:
+    return (CONV3P_WGRAD and r == 3 and s == 3 and stride == 1 and pad == 1 and cin % 64 == 0 and cout % 64 == 0
+            and cin <= 128)
+
+
+def conv3p_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, out_scale: float = 1.0) -> bool:
+    """Weight gradient of a 3x3 / stride-1 / pad-1 conv into ``out`` (contiguous [Cout, 9*Cin] KRSC
+    view, bf16 or fp32) on det_conv3p_wgrad (the halo patch staged once for all 9 taps).  False when
+    a chunk's patch does not fit (the caller falls back)."""
+    nb, cin, h, w = x.shape
+    cout = dy.shape[1]
+    m = nb * h * w
+    lib = _lib.get_lib()
+    ws = torch.empty(int(lib.det_conv3p_wgrad_ws_elems(m, cout, cin)), dtype=torch.float32, device=dy.device)
+    rc = lib.det_conv3p_wgrad(_stream(dy), dy.data_ptr(), x.data_ptr(), out.data_ptr(),
+                              1 if out.dtype == torch.bfloat16 else 0, int(nb), int(h), int(w), int(cin), int(cout),
+                              ws.data_ptr(), float(out_scale))
+    if rc == -6:
+        return False
+    _lib.check(rc, "conv3p_wgrad")
+    CONV3P_COUNTS["wgrad"] += 1
+    return True
 
 
 def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, stats: bool = False,
@@ -794,7 +821,8 @@ class _ConvRS(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
                 CONV3X3_COUNTS["dgrad_miopen"] += 1
-        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 256)
+        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 256) or \
+            (WGRAD_RS_MODE == "auto" and conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc))
         if ctx.needs_input_grad[1] and not native_wgrad:
             wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             gw = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
@@ -814,7 +842,9 @@ class _ConvRS(torch.autograd.Function):
                 dw = torch.empty(weight.shape, dtype=dt, device=weight.device, memory_format=torch.channels_last)
                 out = dw.permute(0, 2, 3, 1).reshape(cout, -1)
             assert out.data_ptr() == dw.data_ptr() and out.is_contiguous()
-            conv_wgrad(dyc, x, out, r, s, stride, pad)
+            if not (conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc) and x.data_ptr() % 16 == 0
+                    and conv3p_wgrad(dyc, x, out)):
+                conv_wgrad(dyc, x, out, r, s, stride, pad)
             CONV3X3_COUNTS["wgrad_native"] += 1
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)

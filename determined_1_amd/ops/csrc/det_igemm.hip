@@ -1310,6 +1310,166 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) wgrad3_kernel(WgArgs a) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// conv3p_wgrad: weight gradient of a 3x3 / stride-1 / pad-1 convolution on the halo patch.
+//   P[split][n][tap * Cin + c] = sum_{m in split} dY[m][n] . Xpad[patch(m) + off(tap)][c]
+// A 512-thread block owns one 64 (Cout) x 9 x 64 (Cin) tile of the weight gradient and a range of
+// output pixels, staged 256 at a time: dY [256][64] and the input patch those pixels read
+// (<= 512 padded pixels x 64 channels) once for all 9 taps -- the per-tap im2col gather of the
+// ring wgrad (wgrad3) stages each input row 9 times, which is what left it behind MIOpen at 64/128
+// channels (profiles/r3_wgrad_ring_sweep.jsonl: 0.44 vs 0.33 ms).  Both MFMA operands are read
+// K(pixel)-major with ds_read_b64_tr_b16: dY from 32-pixel sub-tiles (wtr_frag), the input from the
+// patch at per-lane rows (the pixel's patch row + the tap offset, from a per-stage row table).
+// Wave w holds Cout rows 16 (w & 3) .. +16 and Cin columns 32 (w >> 2) .. +32 of all 9 taps: 18
+// accumulator tiles, one dY fragment per 32-pixel step shared by all of them.
+// ------------------------------------------------------------------------------------------------
+struct WpArgs {
+  const unsigned short* dY;  // [M, N]
+  const unsigned short* X;   // NHWC [Nb, H, W, Cin]
+  float* P;                  // [splits, N, 9 * Cin]
+  int64_t M;
+  int N, Cin, H, W;
+  int rows_per_split;        // multiple of 256
+  int ntiles;                // (N / 64) * (Cin / 64)
+};
+constexpr int kWpDY = 256 * 128, kWpPATCH = kP3PMAX * 128;
+constexpr int kWpSMEM = kWpDY + kWpPATCH + 256 * 4;  // dY [256][64] + patch [512][64] + row table
+
+__global__ void __launch_bounds__(512, 1) conv3p_wgrad_kernel(WpArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  constexpr int NT = 512, DYCH = 256 * 8 / NT, XCH = kP3PMAX * 8 / NT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* dys = smem;
+  unsigned char* xps = smem + kWpDY;
+  int* prow = reinterpret_cast<int*>(smem + kWpDY + kWpPATCH);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nb = w & 3, ch2 = w >> 2;  // Cout 16-block, Cin 32-column half
+  const int tile = blockIdx.x % a.ntiles, split = blockIdx.x / a.ntiles;
+  const int ntc = a.Cin / 64;
+  const int n0 = (tile / ntc) * 64, c0 = (tile % ntc) * 64;
+  const int64_t pbeg = static_cast<int64_t>(split) * a.rows_per_split;
+  int64_t pend = pbeg + a.rows_per_split;
+  if (pend > a.M) pend = a.M;
+  const int nst = pend > pbeg ? static_cast<int>((pend - pbeg + 255) / 256) : 0;
+  const int Wp = a.W + 2;
+  const int64_t hw = static_cast<int64_t>(a.H) * a.W;
+  const int RSC = 9 * a.Cin;
+
+  us8 ry[DYCH], rx[XCH];
+  int g0s = 0, rows_s = 0;  // patch geometry of the staged chunk
+  auto geom = [&](int64_t m0, int& g0, int& rows) {
+    int64_t ml = m0 + 255;
+    if (ml >= a.M) ml = a.M - 1;
+    const int64_t na = m0 / hw, nbb = ml / hw;
+    g0 = static_cast<int>(na * (a.H + 2) + (m0 - na * hw) / a.W);
+    rows = static_cast<int>(nbb * (a.H + 2) + (ml - nbb * hw) / a.W + 2) - g0 + 1;
+  };
+  auto gload = [&](int st) {
+    const int64_t m0 = pbeg + static_cast<int64_t>(st) * 256;
+    int g0, rows;
+    geom(m0, g0, rows);
+#pragma unroll
+    for (int q = 0; q < DYCH; ++q) {
+      const int idx = tid + q * NT, r = idx >> 3, cc = idx & 7;
+      const int64_t m = m0 + r;
+      ry[q] = m < pend ? *reinterpret_cast<const us8*>(a.dY + m * a.N + n0 + cc * 8) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    const int np = rows * Wp;
+#pragma unroll
+    for (int q = 0; q < XCH; ++q) {
+      const int idx = tid + q * NT, pp = idx >> 3, cc = idx & 7;
+      us8 v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (pp < np) {
+        const int gr = g0 + pp / Wp, wp = pp - (pp / Wp) * Wp;
+        const int n = gr / (a.H + 2), h = gr - n * (a.H + 2) - 1, x = wp - 1;
+        if (h >= 0 && h < a.H && x >= 0 && x < a.W)
+          v = *reinterpret_cast<const us8*>(a.X + ((static_cast<int64_t>(n) * a.H + h) * a.W + x) * a.Cin + c0 + cc * 8);
+      }
+      rx[q] = v;
+    }
+  };
+  auto lstore = [&](int st) {
+    const int64_t m0 = pbeg + static_cast<int64_t>(st) * 256;
+    geom(m0, g0s, rows_s);
+#pragma unroll
+    for (int q = 0; q < DYCH; ++q) {
+      const int idx = tid + q * NT, r = idx >> 3, cc = idx & 7;
+      *reinterpret_cast<us8*>(dys + (r >> 5) * 4096 + wswz(r & 31, cc)) = ry[q];
+    }
+    const int np = rows_s * Wp;
+#pragma unroll
+    for (int q = 0; q < XCH; ++q) {
+      const int idx = tid + q * NT, pp = idx >> 3, cc = idx & 7;
+      if (pp < np) *reinterpret_cast<us8*>(xps + wswz(pp, cc)) = rx[q];
+    }
+    if (tid < 256) {  // patch row of output pixel m0 + tid at tap (0, 0); rows past M read row 0 (dY = 0)
+      int64_t m = m0 + tid;
+      int r = 0;
+      if (m < pend) {
+        const int64_t n = m / hw;
+        const int rem = static_cast<int>(m - n * hw);
+        const int ho = rem / a.W, wo = rem - ho * a.W;
+        r = static_cast<int>(n * (a.H + 2) + ho - g0s) * Wp + wo;
+      }
+      prow[tid] = r;
+    }
+  };
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  if (nst > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) gload(st + 1);
+#pragma unroll 1
+    for (int ks = 0; ks < 8; ++ks) {
+      const bf16x8 af = wtr_frag(dys + ks * 4096, nb * 16, lane);  // dY^T: 16 Cout x 32 pixels
+      // this lane's two K rows (pixels) of the B reads: 8g + q4 and 8g + 4 + q4
+      const int r0 = prow[ks * 32 + 8 * g + q4], r1 = prow[ks * 32 + 8 * g + 4 + q4];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = (tap / 3) * Wp + (tap % 3);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int col = ch2 * 32 + i * 16 + 4 * p4;
+          const int o0 = wswz(r0 + toff, col >> 3) + ((col & 4) << 1);
+          const int o1 = wswz(r1 + toff, col >> 3) + ((col & 4) << 1);
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + o0));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + o1));
+          const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[i][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i][tap], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (st + 1 < nst) {
+      lstore(st + 1);
+      __syncthreads();
+    }
+  }
+  float* out = a.P + static_cast<int64_t>(split) * a.N * RSC;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + nb * 16 + (lane >> 4) * 4 + r;
+        const int c = c0 + ch2 * 32 + i * 16 + (lane & 15);
+        out[static_cast<int64_t>(n) * RSC + t * a.Cin + c] = acc[i][t][r];
+      }
+#endif
+}
+
 // out[i] = scale * sum_s P[s][i]  (fp32 slabs -> bf16 or fp32), deterministic: a block owns E float4
 // columns and L = 256 / E split lanes (lane l sums splits l, l+L, ...), then lane 0 of each column
 // adds the L lane sums in order.  L > 1 when the output is small and the split count large (the
@@ -1473,6 +1633,53 @@ int det_igemm_wgrad(void* stream, const void* dY, const void* X, void* out, int 
                        static_cast<unsigned short*>(out), E);
   else
     hipLaunchKernelGGL(wg_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, ws, real_splits, slab, out_scale,
+                       static_cast<float*>(out), E);
+  return static_cast<int>(hipGetLastError());
+}
+
+// conv3p_wgrad splits: enough (tile, pixel-range) blocks for the 256 CUs, >= 8 stages of 256 pixels each.
+static int wp_splits(int64_t M, int ntiles) {
+  int64_t s = (256 + ntiles - 1) / ntiles;
+  const int64_t max_s = (M + 2047) / 2048;
+  if (s > max_s) s = max_s;
+  return static_cast<int>(s < 1 ? 1 : s);
+}
+int64_t det_conv3p_wgrad_ws_elems(int64_t M, int N, int Cin) {
+  if (N % 64 || Cin % 64) return 0;
+  return static_cast<int64_t>(wp_splits(M, (N / 64) * (Cin / 64))) * N * 9 * Cin;
+}
+
+// Weight gradient of a 3x3 / stride-1 / pad-1 convolution (NHWC bf16 dY [M, N] and X) on the halo
+// patch (conv3p_wgrad above): out [N, 9 * Cin] (KRSC; out_dtype 0 fp32 / 1 bf16) = out_scale *
+// dY^T . im2col(X), as split-pixel fp32 slabs in ws (>= det_conv3p_wgrad_ws_elems) reduced by a
+// second launch.  N % 64 == 0, Cin % 64 == 0; -6 when a 256-pixel chunk's patch exceeds 512 pixels.
+int det_conv3p_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int Nb, int H, int W, int Cin,
+                     int N, float* ws, float out_scale) {
+  if (Nb <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cin % 64 != 0 || N <= 0 || N % 64 != 0) return -1;
+  if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X)) & 15) != 0) return -5;
+  const int64_t M = static_cast<int64_t>(Nb) * H * W;
+  if (p3_max_patch(M, H, W) > kP3PMAX) return -6;
+  const int ntiles = (N / 64) * (Cin / 64);
+  const int splits = wp_splits(M, ntiles);
+  int64_t rps = (M + splits - 1) / splits;
+  rps = (rps + 255) / 256 * 256;
+  const int real = static_cast<int>((M + rps - 1) / rps);
+  WpArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, N, Cin, H, W,
+           static_cast<int>(rps), ntiles};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(conv3p_wgrad_kernel, dim3(static_cast<unsigned>(ntiles * real)), dim3(512), kWpSMEM, st, a);
+  int rc = static_cast<int>(hipGetLastError());
+  if (rc != 0) return rc;
+  const int64_t slab = static_cast<int64_t>(N) * 9 * Cin, n4 = slab / 4;
+  int lanes = 1;
+  while (lanes < 256 && lanes < real && n4 / (256 / lanes) < 2048) lanes *= 2;
+  const int E = 256 / lanes;
+  const int grid = static_cast<int>((n4 + E - 1) / E);
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(wg_reduce_kernel<unsigned short>, dim3(grid), dim3(256), 0, st, ws, real, slab, out_scale,
+                       static_cast<unsigned short*>(out), E);
+  else
+    hipLaunchKernelGGL(wg_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, ws, real, slab, out_scale,
                        static_cast<float*>(out), E);
   return static_cast<int>(hipGetLastError());
 }

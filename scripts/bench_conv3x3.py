@@ -48,6 +48,12 @@ for c, st, hin, mult in SHAPES:
     wk = conv.krsc(w)
     r = {"c": c, "stride": st, "hin": hin, "mult": mult}
     r["fwd_native"] = timeit(lambda: conv.igemm_conv(x, w, stride=st, pad=1, stats=True, w_krsc=wk))
+    if conv.conv3p_ok(c, c, 3, 3, st, 1):  # the igemm3 path it replaces, for the record
+        keep, conv.CONV3P_MAX_N = conv.CONV3P_MAX_N, 0
+        r["fwd_igemm3"] = timeit(lambda: conv.igemm_conv(x, w, stride=st, pad=1, stats=True, w_krsc=wk))
+        r["dgrad_igemm3"] = timeit(lambda: conv.igemm_conv(dy, w.transpose(0, 1), stride=1, pad=1,
+                                                           w_krsc=conv.dgrad_weight(w)))
+        conv.CONV3P_MAX_N = keep
     r["fwd_miopen"] = timeit(lambda: F.conv2d(x, w, stride=st, padding=1))
     if st == 1:
         r["dgrad_native"] = timeit(lambda: conv.igemm_conv(dy, w.transpose(0, 1), stride=1, pad=1,
@@ -61,7 +67,7 @@ for c, st, hin, mult in SHAPES:
     r["wgrad_miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
         dy, x, w, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
     for k in list(r):
-        if k.endswith("_native") or k.endswith("_miopen"):
+        if k.endswith("_native") or k.endswith("_miopen") or k.endswith("_igemm3"):
             tot[k] = tot.get(k, 0.0) + mult * r[k]
             r[k.replace("native", "TFs_native").replace("miopen", "TFs_miopen") if False else k] = round(r[k], 4)
             r[k + "_TFs"] = round(flops / r[k] / 1e9, 1)

@@ -150,7 +150,7 @@ def test_dgrad_weight_kernel_matches_torch(gpu):
 @pytest.mark.parametrize("stride", [1, 2])
 def test_conv_rs_autograd_end_to_end(gpu, stride, wgrad_mode, monkeypatch):
     monkeypatch.setattr(conv, "WGRAD_RS_MODE", wgrad_mode)
-    native_wgrad = wgrad_mode == "native"  # auto: Cin 128 stays on MIOpen
+    native_wgrad = wgrad_mode == "native" or (wgrad_mode == "auto" and stride == 1)  # auto: conv3p_wgrad at stride 1
     torch.manual_seed(0)
     m = torch.nn.Conv2d(128, 128, 3, stride=stride, padding=1, bias=False).to(gpu).to(
         memory_format=torch.channels_last)
@@ -313,3 +313,28 @@ def test_conv_rs_routes_thin_3x3_to_conv3p(gpu):
     yr.backward(dy.float())
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)
+
+
+WP_SHAPES = [  # (Nb, Cin, H, W, Cout)
+    (2, 64, 56, 56, 64),
+    (3, 128, 28, 28, 128),  # 2 x 2 weight tiles
+    (4, 64, 14, 14, 128),   # chunks spanning images
+    (1, 64, 7, 9, 64),      # one partial chunk
+]
+
+
+@pytest.mark.parametrize("case", WP_SHAPES)
+def test_conv3p_wgrad_exact_on_integer_operands(gpu, case):
+    """det_conv3p_wgrad (dY and the input patch staged once per 256 pixels for all 9 taps, transposed
+    reads at per-lane patch rows) == torch's conv2d_weight exactly on small-integer operands (sums
+    stay exact in fp32; fp32 output)."""
+    nb, cin, h, w, cout = case
+    g = torch.Generator(device="cpu").manual_seed(13)
+    x = torch.randint(-2, 3, (nb, cin, h, w), generator=g).to(torch.bfloat16)
+    dy = torch.randint(-2, 3, (nb, cout, h, w), generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, 3, 3), dy.float(), padding=1)
+    out = torch.empty(cout, 9 * cin, dtype=torch.float32, device=gpu)
+    assert conv.conv3p_wgrad(dy.to(gpu).contiguous(memory_format=torch.channels_last),
+                             x.to(gpu).contiguous(memory_format=torch.channels_last), out)
+    got = out.view(cout, 3, 3, cin).permute(0, 3, 1, 2).cpu()
+    torch.testing.assert_close(got, ref, rtol=0, atol=0)
