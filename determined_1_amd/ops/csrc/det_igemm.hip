@@ -847,7 +847,7 @@ static int auto_cfg(const IgArgs& a) {
 // channel slice, and with N = 64 the 16 KiB of A per K tile carry only 256 x 64 x 32 MACs -- the
 // LDS-DMA issue cost per KiB (MI355X_MICROARCH.md "LDS-DMA piece issue cost") then exceeds the MFMA
 // time (layer1 3x3 forward at ~400 TF/s, profiles/r3_conv3x3_passes.jsonl).  Here a 256-pixel output
-// tile stages, per 32-channel slice, the padded input rows it touches (<= 512 pixels x 64 B) and the
+// tile stages, per 32-channel slice, the padded input rows it touches (<= 640 pixels x 64 B) and the
 // slice's 9-tap weights [9][64][32] once; the 9 taps then read their A fragments from the patch at
 // a row offset of r * (W + 2) + s (per-lane patch rows, the 64-B-row swizzle of igemm3).  Staging
 // is register-path (global_load -> ds_write), which lets the preceding BatchNorm + ReLU be applied
@@ -859,7 +859,7 @@ static int auto_cfg(const IgArgs& a) {
 //   * epilogues of igemm3: bf16 tile via LDS, BN statistics (STATS) or the BN-backward partials
 //     of the producing BatchNorm (BNB, for the stride-1 input gradient over the flipped weight).
 // ------------------------------------------------------------------------------------------------
-constexpr int kP3BM = 256, kP3BN = 64, kP3BK = 32, kP3PMAX = 512;
+constexpr int kP3BM = 256, kP3BN = 64, kP3BK = 32, kP3PMAX = 640;  // PMAX: a 56-wide tile across an image boundary needs 580
 constexpr int kP3PATCH = kP3PMAX * 64, kP3BT = 9 * kP3BN * 64;
 constexpr int kP3SMEM = kP3PATCH + kP3BT;  // 69632 B
 
@@ -1315,7 +1315,7 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) wgrad3_kernel(WgArgs a) {
 //   P[split][n][tap * Cin + c] = sum_{m in split} dY[m][n] . Xpad[patch(m) + off(tap)][c]
 // A 512-thread block owns one 64 (Cout) x 9 x 64 (Cin) tile of the weight gradient and a range of
 // output pixels, staged 256 at a time: dY [256][64] and the input patch those pixels read
-// (<= 512 padded pixels x 64 channels) once for all 9 taps -- the per-tap im2col gather of the
+// (<= 640 padded pixels x 64 channels) once for all 9 taps -- the per-tap im2col gather of the
 // ring wgrad (wgrad3) stages each input row 9 times, which is what left it behind MIOpen at 64/128
 // channels (profiles/r3_wgrad_ring_sweep.jsonl: 0.44 vs 0.33 ms).  Both MFMA operands are read
 // K(pixel)-major with ds_read_b64_tr_b16: dY from 32-pixel sub-tiles (wtr_frag), the input from the
@@ -1652,7 +1652,7 @@ int64_t det_conv3p_wgrad_ws_elems(int64_t M, int N, int Cin) {
 // Weight gradient of a 3x3 / stride-1 / pad-1 convolution (NHWC bf16 dY [M, N] and X) on the halo
 // patch (conv3p_wgrad above): out [N, 9 * Cin] (KRSC; out_dtype 0 fp32 / 1 bf16) = out_scale *
 // dY^T . im2col(X), as split-pixel fp32 slabs in ws (>= det_conv3p_wgrad_ws_elems) reduced by a
-// second launch.  N % 64 == 0, Cin % 64 == 0; -6 when a 256-pixel chunk's patch exceeds 512 pixels.
+// second launch.  N % 64 == 0, Cin % 64 == 0; -6 when a 256-pixel chunk's patch exceeds 640 pixels.
 int det_conv3p_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int Nb, int H, int W, int Cin,
                      int N, float* ws, float out_scale) {
   if (Nb <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cin % 64 != 0 || N <= 0 || N % 64 != 0) return -1;
@@ -1827,7 +1827,7 @@ int det_igemm_dgrad_s2(void* stream, const void* dY, const void* Wd, void* dX, c
 // preceding BatchNorm + ReLU; zero padding is not transformed).  pmean/pm2 (nullable, [ceil(M/256),
 // N]): BN statistics partials of Y.  bn_x..psumx (all or none): the BN-backward epilogue of a BN
 // whose output X this conv's input gradient is (mask mode 1), partials [ceil(M/256), N].  Cin % 32,
-// N % 64, 16-B aligned; -6 when a tile's patch would exceed 512 pixels (very wide images).
+// N % 64, 16-B aligned; -6 when a tile's patch would exceed 640 pixels (very wide images).
 int det_conv3p(void* stream, const void* X, const void* W, void* Y, int Nb, int H, int Wd, int Cin, int N,
                const float* pro_scale, const float* pro_shift, float* pmean, float* pm2, const void* bn_x,
                const float* bn_mean, const float* bn_scale, const float* bn_shift, float* psum, float* psumx,

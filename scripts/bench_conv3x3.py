@@ -64,10 +64,12 @@ for c, st, hin, mult in SHAPES:
         dy, x, w, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
     out = torch.empty(c, 9 * c, dtype=torch.bfloat16, device=dev)
     r["wgrad_native"] = timeit(lambda: conv.conv_wgrad(dy, x, out, 3, 3, st, 1))
+    if conv.conv3p_wgrad_ok(c, c, 3, 3, st, 1):  # halo-patch wgrad (the model's choice at these shapes)
+        r["wgrad_conv3p"] = timeit(lambda: conv.conv3p_wgrad(dy, x, out))
     r["wgrad_miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
         dy, x, w, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
     for k in list(r):
-        if k.endswith("_native") or k.endswith("_miopen") or k.endswith("_igemm3"):
+        if k.endswith("_native") or k.endswith("_miopen") or k.endswith("_igemm3") or k.endswith("_conv3p"):
             tot[k] = tot.get(k, 0.0) + mult * r[k]
             r[k.replace("native", "TFs_native").replace("miopen", "TFs_miopen") if False else k] = round(r[k], 4)
             r[k + "_TFs"] = round(flops / r[k] / 1e9, 1)
