@@ -165,6 +165,9 @@ _SIGNATURES = {
     # bn_scale, bn_shift, psum, psumx, grid (0 = one persistent block per CU)
     "det_conv3p": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 10 + [c_int], c_int),
     "det_conv3p_wgrad_ws_elems": ([c_i64, c_int, c_int], c_i64),
+    "det_stemp_wgrad_ws_elems": ([c_i64], c_i64),
+    # stream, dY, X4, out, out_dtype, M, Hi, Wi, Ho, Wo, ws, out_scale
+    "det_stemp_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 4 + [c_void_p, c_float], c_int),
     # stream, dY, X, out, out_dtype, Nb, H, W, Cin, N, ws, out_scale
     "det_conv3p_wgrad": ([c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_float], c_int),
     # stream, dY, X, out, out_dtype, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, ws, out_scale

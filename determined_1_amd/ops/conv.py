@@ -755,7 +755,7 @@ class _BNReluConv1x1(torch.autograd.Function):
         return dx, dg, db, None, None, None, None, None, dw
 
 
-FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0, "stem": 0, "stem_fallback": 0}
+FUSED_COUNTS = {"bn_relu_conv1x1": 0, "fallback": 0, "stem": 0, "stem_fallback": 0, "stem_wgrad_patch": 0}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -821,7 +821,11 @@ class _ConvRS(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
                 CONV3X3_COUNTS["dgrad_miopen"] += 1
+        # auto: the ring at >= 256 channels and for the stride-2 3x3 at 128 (0.253 vs MIOpen 0.249 ms,
+        # profiles/r3_wgrad_ring_sweep.jsonl: a tie, and no library launch), the halo patch for
+        # stride-1 3x3 at 64/128 channels
         native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 256) or \
+            (WGRAD_RS_MODE == "auto" and WGRAD_RING and stride == 2 and cin >= 128) or \
             (WGRAD_RS_MODE == "auto" and conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc))
         if ctx.needs_input_grad[1] and not native_wgrad:
             wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -884,6 +888,9 @@ def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_e
 # default: 0.49 vs 0.82 ms at batch 512, profiles/r2_stem_microbench.jsonl).  The forward stays native
 # (0.64 ms including the BN statistics vs MIOpen 0.70 + a 0.17 ms stats pass).
 STEM_NATIVE_WGRAD = False
+# Stem weight gradient on the patch kernel (det_igemm.hip stemp_wgrad: dY and the input rows of a
+# 256-pixel chunk staged once, transposed operand reads straight from the patch), ahead of both.
+STEM_PATCH_WGRAD = os.environ.get("DET_STEM_PATCH_WGRAD", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -948,8 +955,21 @@ class _StemConv(torch.autograd.Function):
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         ci = weight.shape[1]
-        native_wgrad = ctx.needs_input_grad[1] and STEM_NATIVE_WGRAD
-        if native_wgrad:
+        native_wgrad = False
+        if ctx.needs_input_grad[1] and STEM_PATCH_WGRAD:
+            # the patch kernel (det_igemm.hip stemp_wgrad): each input row staged once per chunk
+            lib = _lib.get_lib()
+            ws = torch.empty(int(lib.det_stemp_wgrad_ws_elems(m)), dtype=torch.float32, device=dy.device)
+            dwk = torch.empty(64, 256, dtype=torch.float32, device=dy.device)
+            rc = lib.det_stemp_wgrad(_stream(dy), dyc.data_ptr(), x4.data_ptr(), dwk.data_ptr(), 0, int(m), int(hi),
+                                     int(wi), int(ho), int(wo), ws.data_ptr(), 1.0)
+            if rc != -6:
+                _lib.check(rc, "stemp_wgrad")
+                dw = unpack_stem_grad(dwk, ci).to(weight.dtype).contiguous(memory_format=torch.channels_last)
+                native_wgrad = True
+                FUSED_COUNTS["stem_wgrad_patch"] += 1
+        if not native_wgrad and ctx.needs_input_grad[1] and STEM_NATIVE_WGRAD:
+            native_wgrad = True
             lib = _lib.get_lib()
             ws = torch.empty(int(lib.det_stem_conv_wgrad_ws_elems(m)), dtype=torch.float32, device=dy.device)
             dwk = torch.empty(64, 256, dtype=torch.float32, device=dy.device)

@@ -1320,8 +1320,10 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) wgrad3_kernel(WgArgs a) {
 // channels (profiles/r3_wgrad_ring_sweep.jsonl: 0.44 vs 0.33 ms).  Both MFMA operands are read
 // K(pixel)-major with ds_read_b64_tr_b16: dY from 32-pixel sub-tiles (wtr_frag), the input from the
 // patch at per-lane rows (the pixel's patch row + the tap offset, from a per-stage row table).
-// Wave w holds Cout rows 16 (w & 3) .. +16 and Cin columns 32 (w >> 2) .. +32 of all 9 taps: 18
-// accumulator tiles, one dY fragment per 32-pixel step shared by all of them.
+// Wave w holds Cout rows 32 (w & 1) .. +32 and Cin columns 16 (w >> 1) .. +16 of all 9 taps: 18
+// accumulator tiles per 32-pixel step from 2 dY fragments and 9 input fragments, each input
+// fragment feeding 2 MFMAs (LDS reads ~0.6 of the MFMA time; 16 x 32 wave columns would need 19
+// fragments per 18 MFMAs and be LDS-bound).
 // ------------------------------------------------------------------------------------------------
 struct WpArgs {
   const unsigned short* dY;  // [M, N]
@@ -1345,7 +1347,7 @@ __global__ void __launch_bounds__(512, 1) conv3p_wgrad_kernel(WpArgs a) {
   unsigned char* xps = smem + kWpDY;
   int* prow = reinterpret_cast<int*>(smem + kWpDY + kWpPATCH);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nb = w & 3, ch2 = w >> 2;  // Cout 16-block, Cin 32-column half
+  const int nh = w & 1, cb = w >> 1;  // Cout 32-row half, Cin 16-column block
   const int tile = blockIdx.x % a.ntiles, split = blockIdx.x / a.ntiles;
   const int ntc = a.Cin / 64;
   const int n0 = (tile / ntc) * 64, c0 = (tile % ntc) * 64;
@@ -1432,22 +1434,22 @@ __global__ void __launch_bounds__(512, 1) conv3p_wgrad_kernel(WpArgs a) {
     if (st + 1 < nst) gload(st + 1);
 #pragma unroll 1
     for (int ks = 0; ks < 8; ++ks) {
-      const bf16x8 af = wtr_frag(dys + ks * 4096, nb * 16, lane);  // dY^T: 16 Cout x 32 pixels
+      bf16x8 af[2];  // dY^T: 2 x (16 Cout x 32 pixels)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = wtr_frag(dys + ks * 4096, nh * 32 + i * 16, lane);
       // this lane's two K rows (pixels) of the B reads: 8g + q4 and 8g + 4 + q4
       const int r0 = prow[ks * 32 + 8 * g + q4], r1 = prow[ks * 32 + 8 * g + 4 + q4];
+      const int col = cb * 16 + 4 * p4;
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int toff = (tap / 3) * Wp + (tap % 3);
+        const int o0 = wswz(r0 + toff, col >> 3) + ((col & 4) << 1);
+        const int o1 = wswz(r1 + toff, col >> 3) + ((col & 4) << 1);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + o0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + o1));
+        const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int col = ch2 * 32 + i * 16 + 4 * p4;
-          const int o0 = wswz(r0 + toff, col >> 3) + ((col & 4) << 1);
-          const int o1 = wswz(r1 + toff, col >> 3) + ((col & 4) << 1);
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + o0));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + o1));
-          const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          acc[i][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i][tap], 0, 0, 0);
-        }
+        for (int i = 0; i < 2; ++i) acc[i][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][tap], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -1463,9 +1465,168 @@ __global__ void __launch_bounds__(512, 1) conv3p_wgrad_kernel(WpArgs a) {
     for (int t = 0; t < 9; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + nb * 16 + (lane >> 4) * 4 + r;
-        const int c = c0 + ch2 * 32 + i * 16 + (lane & 15);
+        const int n = n0 + nh * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int c = c0 + cb * 16 + (lane & 15);
         out[static_cast<int64_t>(n) * RSC + t * a.Cin + c] = acc[i][t][r];
+      }
+#endif
+}
+
+// ------------------------------------------------------------------------------------------------
+// stemp_wgrad: weight gradient of the ResNet stem (7x7 / stride 2 / pad 3 over 4-channel NHWC
+// images) in the packed layout of det_conv's stem GEMM: P[split][n][k], k = r*32 + s*4 + c over an
+// 8x8x4 box (tap 7 and channel 3 carry zero weights; their gradient is computed and dropped).
+// Per 256-output-pixel chunk the block stages dY [256][64] and the input rows the chunk reads
+// (<= 14 padded rows x (W + 6) pixels x 8 B) once; the B fragment of column block (r, s0..s0+3) is
+// 4 transposed reads per lane pair straight from the patch: lane (q, p) addresses the input pixel
+// (2 ho - 3 + r, 2 wo - 3 + s0 + p) of K row q -- its 4 channels are the 8 contiguous bytes the
+// transposed read takes.  Replaces MIOpen's NHWC C=4 wrw kernel (0.46 ms/step at batch 512).
+// Wave w: Cout rows 32 (w & 1) .. +32, packed columns 64 (w >> 1) .. +64 (two r values).
+// ------------------------------------------------------------------------------------------------
+struct SpArgs {
+  const unsigned short* dY;  // [M, 64]
+  const unsigned short* X;   // [Nb, Hi, Wi, 4]
+  float* P;                  // [splits, 64, 256]
+  int64_t M;
+  int Hi, Wi, Ho, Wo;
+  int rows_per_split;        // multiple of 256
+};
+constexpr int kSpPMAX = 14 * 240;  // padded input pixels per chunk (Wi <= 234)
+constexpr int kSpSMEM = 256 * 128 + kSpPMAX * 8 + 256 * 4;
+
+__global__ void __launch_bounds__(512, 1) stemp_wgrad_kernel(SpArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef __attribute__((ext_vector_type(4))) unsigned short us4;
+  constexpr int NT = 512, DYCH = 256 * 8 / NT, XCH = (kSpPMAX * 8 / 16 + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* dys = smem;
+  unsigned char* xps = smem + 256 * 128;
+  int* prow = reinterpret_cast<int*>(smem + 256 * 128 + kSpPMAX * 8);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nh = w & 1, cq = w >> 1;
+  const int64_t pbeg = static_cast<int64_t>(blockIdx.x) * a.rows_per_split;
+  int64_t pend = pbeg + a.rows_per_split;
+  if (pend > a.M) pend = a.M;
+  const int nst = pend > pbeg ? static_cast<int>((pend - pbeg + 255) / 256) : 0;
+  const int Hp = a.Hi + 6, Wp = a.Wi + 6;  // 3 pixels of zero padding on every side
+  const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
+
+  us8 ry[DYCH], rx[XCH];
+  auto geom = [&](int64_t m0, int& g0, int& rows) {
+    int64_t ml = m0 + 255;
+    if (ml >= a.M) ml = a.M - 1;
+    const int64_t na = m0 / hw, nb = ml / hw;
+    g0 = static_cast<int>(na * Hp + 2 * ((m0 - na * hw) / a.Wo));
+    rows = static_cast<int>(nb * Hp + 2 * ((ml - nb * hw) / a.Wo) + 7) - g0 + 1;
+  };
+  auto gload = [&](int st) {
+    const int64_t m0 = pbeg + static_cast<int64_t>(st) * 256;
+    int g0, rows;
+    geom(m0, g0, rows);
+#pragma unroll
+    for (int q = 0; q < DYCH; ++q) {
+      const int idx = tid + q * NT, r = idx >> 3, cc = idx & 7;
+      const int64_t m = m0 + r;
+      ry[q] = m < pend ? *reinterpret_cast<const us8*>(a.dY + m * 64 + cc * 8) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    // the patch in 16-B pieces = 2 padded pixels of 4 channels
+    const int npc = (rows * Wp + 1) / 2;
+#pragma unroll
+    for (int q = 0; q < XCH; ++q) {
+      const int idx = tid + q * NT;
+      us8 v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (idx < npc) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int pp = 2 * idx + h2;
+          const int gr = g0 + pp / Wp, wp = pp - (pp / Wp) * Wp;
+          const int n = gr / Hp, h = gr - n * Hp - 3, x = wp - 3;
+          if (pp < rows * Wp && h >= 0 && h < a.Hi && x >= 0 && x < a.Wi) {
+            const us4 px = *reinterpret_cast<const us4*>(a.X + ((static_cast<int64_t>(n) * a.Hi + h) * a.Wi + x) * 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[h2 * 4 + j] = px[j];
+          }
+        }
+      }
+      rx[q] = v;
+    }
+  };
+  auto lstore = [&](int st) {
+    const int64_t m0 = pbeg + static_cast<int64_t>(st) * 256;
+    int g0, rows;
+    geom(m0, g0, rows);
+#pragma unroll
+    for (int q = 0; q < DYCH; ++q) {
+      const int idx = tid + q * NT, r = idx >> 3, cc = idx & 7;
+      *reinterpret_cast<us8*>(dys + (r >> 5) * 4096 + wswz(r & 31, cc)) = ry[q];
+    }
+    const int npc = (rows * Wp + 1) / 2;
+#pragma unroll
+    for (int q = 0; q < XCH; ++q) {
+      const int idx = tid + q * NT;
+      if (idx < npc) *reinterpret_cast<us8*>(xps + idx * 16) = rx[q];
+    }
+    if (tid < 256) {  // padded-patch pixel of (row 2 ho, col 2 wo) for output pixel m0 + tid
+      const int64_t m = m0 + tid;
+      int r = 0;
+      if (m < pend) {
+        const int64_t n = m / hw;
+        const int rem = static_cast<int>(m - n * hw);
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+        r = static_cast<int>(n * Hp + 2 * ho - g0) * Wp + 2 * wo;
+      }
+      prow[tid] = r;
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  if (nst > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) gload(st + 1);
+#pragma unroll 1
+    for (int ks = 0; ks < 8; ++ks) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = wtr_frag(dys + ks * 4096, nh * 32 + i * 16, lane);
+      const int r0 = prow[ks * 32 + 8 * g + q4], r1 = prow[ks * 32 + 8 * g + 4 + q4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cb = cq * 4 + j;            // 16-column block: r = cb / 2, s0 = 4 (cb % 2)
+        const int off = (cb >> 1) * Wp + (cb & 1) * 4 + p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + (r0 + off) * 8));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xps + (r1 + off) * 8));
+        const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (st + 1 < nst) {
+      lstore(st + 1);
+      __syncthreads();
+    }
+  }
+  float* out = a.P + static_cast<int64_t>(blockIdx.x) * 64 * 256;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nh * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int k = (cq * 4 + j) * 16 + (lane & 15);
+        out[n * 256 + k] = acc[i][j][r];
       }
 #endif
 }
@@ -1671,6 +1832,47 @@ int det_conv3p_wgrad(void* stream, const void* dY, const void* X, void* out, int
   int rc = static_cast<int>(hipGetLastError());
   if (rc != 0) return rc;
   const int64_t slab = static_cast<int64_t>(N) * 9 * Cin, n4 = slab / 4;
+  int lanes = 1;
+  while (lanes < 256 && lanes < real && n4 / (256 / lanes) < 2048) lanes *= 2;
+  const int E = 256 / lanes;
+  const int grid = static_cast<int>((n4 + E - 1) / E);
+  if (out_dtype == 1)
+    hipLaunchKernelGGL(wg_reduce_kernel<unsigned short>, dim3(grid), dim3(256), 0, st, ws, real, slab, out_scale,
+                       static_cast<unsigned short*>(out), E);
+  else
+    hipLaunchKernelGGL(wg_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, ws, real, slab, out_scale,
+                       static_cast<float*>(out), E);
+  return static_cast<int>(hipGetLastError());
+}
+
+static int sp_splits(int64_t M) {
+  int64_t s = 256;
+  const int64_t max_s = (M + 4095) / 4096;  // >= 16 chunks of 256 pixels per block
+  if (s > max_s) s = max_s;
+  return static_cast<int>(s < 1 ? 1 : s);
+}
+int64_t det_stemp_wgrad_ws_elems(int64_t M) { return static_cast<int64_t>(sp_splits(M)) * 64 * 256; }
+
+// ResNet stem weight gradient (7x7 / stride 2 / pad 3, 64 filters, NHWC input padded to 4 channels)
+// on the patch kernel above: out [64, 256] (packed k = r*32 + s*4 + c; fp32 or bf16) = out_scale *
+// sum over pixels, via split fp32 slabs in ws (>= det_stemp_wgrad_ws_elems(M)).  -6 for widths the
+// patch cannot hold (Wi > 234).
+int det_stemp_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int Hi, int Wi,
+                    int Ho, int Wo, float* ws, float out_scale) {
+  if (M <= 0 || Hi <= 0 || Wi <= 0 || Ho != (Hi - 1) / 2 + 1 || Wo != (Wi - 1) / 2 + 1) return -1;
+  if (Wi + 6 > 240) return -6;
+  if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X)) & 15) != 0) return -5;
+  const int splits = sp_splits(M);
+  int64_t rps = (M + splits - 1) / splits;
+  rps = (rps + 255) / 256 * 256;
+  const int real = static_cast<int>((M + rps - 1) / rps);
+  SpArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, Hi, Wi, Ho, Wo,
+           static_cast<int>(rps)};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(stemp_wgrad_kernel, dim3(static_cast<unsigned>(real)), dim3(512), kSpSMEM, st, a);
+  int rc = static_cast<int>(hipGetLastError());
+  if (rc != 0) return rc;
+  const int64_t slab = 64 * 256, n4 = slab / 4;
   int lanes = 1;
   while (lanes < 256 && lanes < real && n4 / (256 / lanes) < 2048) lanes *= 2;
   const int E = 256 / lanes;

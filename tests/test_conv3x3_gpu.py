@@ -150,7 +150,7 @@ def test_dgrad_weight_kernel_matches_torch(gpu):
 @pytest.mark.parametrize("stride", [1, 2])
 def test_conv_rs_autograd_end_to_end(gpu, stride, wgrad_mode, monkeypatch):
     monkeypatch.setattr(conv, "WGRAD_RS_MODE", wgrad_mode)
-    native_wgrad = wgrad_mode == "native" or (wgrad_mode == "auto" and stride == 1)  # auto: conv3p_wgrad at stride 1
+    native_wgrad = wgrad_mode in ("native", "auto")  # auto: conv3p_wgrad at stride 1, the ring at stride 2
     torch.manual_seed(0)
     m = torch.nn.Conv2d(128, 128, 3, stride=stride, padding=1, bias=False).to(gpu).to(
         memory_format=torch.channels_last)

@@ -221,12 +221,14 @@ def test_bn_relu_conv1x1_matches_fp32_reference(gpu, n, c, h, cout):
 
 @pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9)])
 @pytest.mark.parametrize("cin", [3, 4])
-@pytest.mark.parametrize("native_wgrad", [True, False])
-def test_stem_conv_matches_fp32_reference(gpu, n, h, w, cin, native_wgrad, monkeypatch):
+@pytest.mark.parametrize("wgrad", ["patch", "gemm", "miopen"])
+def test_stem_conv_matches_fp32_reference(gpu, n, h, w, cin, wgrad, monkeypatch):
     """ResNet stem (7x7/2, pad 3, 64 filters) as the det_conv implicit GEMM vs fp32 conv2d: output,
-    BN statistics partials of the output, weight gradient; 3-channel input (padded inside) and
-    4-channel input with a zero 4th channel."""
-    monkeypatch.setattr(conv, "STEM_NATIVE_WGRAD", native_wgrad)
+    BN statistics partials of the output, weight gradient (patch kernel, split-M GEMM or MIOpen);
+    3-channel input (padded inside) and 4-channel input with a zero 4th channel."""
+    monkeypatch.setattr(conv, "STEM_PATCH_WGRAD", wgrad == "patch")
+    monkeypatch.setattr(conv, "STEM_NATIVE_WGRAD", wgrad == "gemm")
+    before_patch = conv.FUSED_COUNTS["stem_wgrad_patch"]
     torch.manual_seed(n * h + w + cin)
     x3 = torch.randn(n, 3, h, w, device=gpu).to(torch.bfloat16)
     x = x3 if cin == 3 else torch.cat([x3, torch.zeros_like(x3[:, :1])], 1)
@@ -250,6 +252,30 @@ def test_stem_conv_matches_fp32_reference(gpu, n, h, w, cin, native_wgrad, monke
     y.backward(dy)
     ref.backward(dy.float())
     torch.testing.assert_close(cv.weight.grad.float(), wf.grad, rtol=2e-2, atol=2e-3 * m ** 0.5)
+    assert conv.FUSED_COUNTS["stem_wgrad_patch"] == before_patch + (1 if wgrad == "patch" else 0)
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9)])
+def test_stem_patch_wgrad_exact_on_integer_operands(gpu, n, h, w):
+    """det_stemp_wgrad (dY and the chunk's input rows staged once; 4-channel pixels read as the
+    8-byte rows of transposed fragment reads) == conv2d_weight exactly on small integers."""
+    from determined_1_amd.ops import _lib
+
+    g = torch.Generator(device="cpu").manual_seed(n + h + w)
+    x = torch.randint(-2, 3, (n, 4, h, w), generator=g).to(torch.bfloat16)
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    dy = torch.randint(-2, 3, (n, 64, ho, wo), generator=g).to(torch.bfloat16)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (64, 4, 7, 7), dy.float(), stride=2, padding=3)
+    lib = _lib.get_lib()
+    m = n * ho * wo
+    xg = x.to(gpu).contiguous(memory_format=torch.channels_last)
+    dyg = dy.to(gpu).contiguous(memory_format=torch.channels_last)
+    ws = torch.empty(int(lib.det_stemp_wgrad_ws_elems(m)), dtype=torch.float32, device=gpu)
+    out = torch.empty(64, 256, dtype=torch.float32, device=gpu)
+    _lib.check(lib.det_stemp_wgrad(torch.cuda.current_stream().cuda_stream, dyg.data_ptr(), xg.data_ptr(),
+                                   out.data_ptr(), 0, m, h, w, ho, wo, ws.data_ptr(), 1.0), "stemp")
+    got = conv.unpack_stem_grad(out, 4).cpu()
+    torch.testing.assert_close(got, ref, rtol=0, atol=0)
 
 
 def test_u8_normalize_pad4(gpu):
