@@ -154,9 +154,11 @@ def igemm_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 # 3x3 / stride-1 convolutions with at most this many output channels run on the halo-patch kernel
-# (det_igemm.hip conv3p: the input staged once per 256-pixel tile instead of once per tap); wider
-# ones stay on igemm3, whose 256 x 256 tiles already reuse each staged row over 256 columns.
-CONV3P_MAX_N = int(os.environ.get("DET_CONV3P_MAX_N", "128"))
+# (det_igemm.hip conv3p: the input staged once per 256-pixel tile instead of once per tap).  Off by
+# default: measured slower than igemm3 at every ResNet-50 shape (64 ch @56: fwd 0.317 vs 0.292 ms,
+# dgrad 0.279 vs 0.259; 128 ch @28: fwd 0.253 vs 0.184) and -1.5 % on the whole step
+# (profiles/r4_conv3x3_microbench.jsonl, r4_conv3p_ab.jsonl).
+CONV3P_MAX_N = int(os.environ.get("DET_CONV3P_MAX_N", "0"))
 CONV3P_COUNTS = {"fwd": 0, "dgrad": 0, "wgrad": 0}
 
 
@@ -201,11 +203,13 @@ def conv3p(x: torch.Tensor, wk: torch.Tensor, cout: int, stats: bool = False, pr
 
 
 CONV3P_WGRAD = os.environ.get("DET_CONV3P_WGRAD", "1") != "0"  # A/B switch: MIOpen's wrw kernels
+CONV3P_WGRAD_MAX_C = int(os.environ.get("DET_CONV3P_WGRAD_MAX_C", "64"))
 
 
 def conv3p_wgrad_ok(cin: int, cout: int, r: int, s: int, stride: int, pad: int) -> bool:
+    # 64 channels only: 0.272 ms vs MIOpen 0.334 at 56x56; at 128 the ring (0.224) is ahead (0.255)
     return (CONV3P_WGRAD and r == 3 and s == 3 and stride == 1 and pad == 1 and cin % 64 == 0 and cout % 64 == 0
-            and cin <= 128)
+            and cin <= CONV3P_WGRAD_MAX_C)
 
 
 def conv3p_wgrad(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor, out_scale: float = 1.0) -> bool:
@@ -821,11 +825,10 @@ class _ConvRS(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
                 CONV3X3_COUNTS["dgrad_miopen"] += 1
-        # auto: the ring at >= 256 channels and for the stride-2 3x3 at 128 (0.253 vs MIOpen 0.249 ms,
-        # profiles/r3_wgrad_ring_sweep.jsonl: a tie, and no library launch), the halo patch for
-        # stride-1 3x3 at 64/128 channels
-        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 256) or \
-            (WGRAD_RS_MODE == "auto" and WGRAD_RING and stride == 2 and cin >= 128) or \
+        # auto: the ring at >= 128 channels (at 128 a tie with MIOpen, 0.224 / 0.253 ms at stride 1 / 2,
+        # profiles/r4_conv3x3_microbench.jsonl, and no library launch), the halo patch for the stride-1
+        # 3x3 at 64 channels
+        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 128) or \
             (WGRAD_RS_MODE == "auto" and conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc))
         if ctx.needs_input_grad[1] and not native_wgrad:
             wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)

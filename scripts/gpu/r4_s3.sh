@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r4s3
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_conv3x3_gpu.py tests/test_bn_bwd_fusion_gpu.py tests/test_norm_gpu.py > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_conv3x3_gpu.py tests/test_conv_gpu.py tests/test_bn_bwd_fusion_gpu.py tests/test_norm_gpu.py > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python -u scripts/bench_conv3x3.py > $O/conv3x3.jsonl 2> $O/conv3x3.err || { tail -20 $O/conv3x3.err; exit 1; }
 cut -c1-420 $O/conv3x3.jsonl

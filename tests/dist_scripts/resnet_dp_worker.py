@@ -8,6 +8,7 @@ arena, bf16 wire compression for the fp32 one) on 64x64 images, 8 per rank.  DAT
 per-rank batches: "seq" batch i at step i; "dup" each batch twice in a row, so with 2 ranks both
 see batch i at step i; "b0"/"b1" only batch 0 / 1; "pair" batches 0, 1 (2 ranks: one each).
 Writes the flat fp32 master weights (the arena's, O2) or fp32 parameters (O0) to OUT.pt."""
+import json
 import os
 import sys
 
@@ -79,11 +80,12 @@ def main() -> None:
     from determined_1_amd.ops import conv, norm
 
     info = {"params": flat(), "init": init, "world": world, "dist": dist.is_initialized(),
-            "buckets": [st.bucketer.describe() for st in ctx._opt_states if st.bucketer is not None],
+            "buckets": json.loads(json.dumps([st.bucketer.describe() for st in ctx._opt_states if st.bucketer is not None],
+                                          default=float)),
             "counts": {"fwd_apply": dict(conv.FWD_APPLY_COUNTS), "bn_bwd": dict(conv.BN_BWD_COUNTS),
                        "conv3x3": dict(conv.CONV3X3_COUNTS), "bn_apply": dict(conv.BN_APPLY_COUNTS),
                        "bn_fallbacks": norm.FALLBACKS["count"]},
-            "loss": [m["loss"] for r in resp if "metrics" in r for m in r["metrics"]["batch_metrics"]]}
+            "loss": [float(m["loss"]) for r in resp if "metrics" in r for m in r["metrics"]["batch_metrics"]]}
     if int(os.environ.get("RANK", "0")) == 0:
         torch.save(info, out + ".pt")
     from determined_1_amd.parallel import dist as pdist

@@ -294,9 +294,10 @@ def test_conv3p_stats_and_bn_backward_epilogues(gpu):
     torch.testing.assert_close(psx.double().sum(0), (df * (xf - bmean.double())).sum(0), rtol=1e-4, atol=1e-3)
 
 
-def test_conv_rs_routes_thin_3x3_to_conv3p(gpu):
+def test_conv_rs_routes_thin_3x3_to_conv3p(gpu, monkeypatch):
     """The autograd 3x3 path runs conv3p for N <= CONV3P_MAX_N (forward and stride-1 dgrad) and the
-    result matches the fp32 reference."""
+    result matches the fp32 reference (conv3p is opt-in: DET_CONV3P_MAX_N)."""
+    monkeypatch.setattr(conv, "CONV3P_MAX_N", 128)
     torch.manual_seed(0)
     m = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).to(gpu).to(memory_format=torch.channels_last)
     x = torch.randn(4, 64, 28, 28, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
