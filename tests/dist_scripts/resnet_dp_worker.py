@@ -60,7 +60,7 @@ def main() -> None:
           "momentum": float(mom), "weight_decay": 0.0}
     cfg = base_config(hp, resources={"slots_per_trial": world},
                       optimizations={"gradient_compression": compress == "1", "grad_reduction": "fp32_accum"})
-    ctrl = make_controller(Trial, cfg, rec.stream(), trial_seed=3, use_gpu=True,
+    ctrl = make_controller(Trial, cfg, rec.stream(), trial_seed=3, use_gpu=os.environ.get("RDP_CPU") != "1",
                            initial_workload=workload.train_workload(1, num_batches=1, total_batches_processed=0))
     ctx = ctrl.context
     ctx._finalize()  # arenas (+ fp32 masters at O2) exist from here on; idempotent
@@ -74,7 +74,8 @@ def main() -> None:
     init = flat()
     ctrl.run()
     resp = rec.responses
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     import torch.distributed as dist
 
     from determined_1_amd.ops import conv, norm
@@ -85,7 +86,8 @@ def main() -> None:
             "counts": {"fwd_apply": dict(conv.FWD_APPLY_COUNTS), "bn_bwd": dict(conv.BN_BWD_COUNTS),
                        "conv3x3": dict(conv.CONV3X3_COUNTS), "bn_apply": dict(conv.BN_APPLY_COUNTS),
                        "bn_fallbacks": norm.FALLBACKS["count"]},
-            "loss": [float(m["loss"]) for r in resp if "metrics" in r for m in r["metrics"]["batch_metrics"]]}
+            "loss": [float(m["loss"]) for r in resp if isinstance(r, dict) and "metrics" in r
+                     for m in r["metrics"]["batch_metrics"]]}
     if int(os.environ.get("RANK", "0")) == 0:
         torch.save(info, out + ".pt")
     from determined_1_amd.parallel import dist as pdist

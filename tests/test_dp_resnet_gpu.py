@@ -60,7 +60,8 @@ def test_identical_batches_match_single_process(gpu, tmp_path, amp, compress):
     dp = _run(str(tmp_path / "dp"), amp, compress, "dup", 4, 0.05, 0.9, 2)
     assert dp["world"] == 2 and dp["dist"] and not ref["dist"]
     modes = {b["mode"] for bs in dp["buckets"] for b in bs}
-    assert modes == {"fp32_accum"}, dp["buckets"]
+    # the bf16 arena reduces through fp32_accum; a small fp32 arena (O2's BatchNorm parameters) as-is
+    assert "fp32_accum" in modes and modes <= {"fp32_accum", "allreduce"}, dp["buckets"]
     _fusions_on(dp)
     assert torch.equal(dp["init"], ref["init"])  # the same seeded initialisation
     moved = (ref["params"] - ref["init"]).abs()
