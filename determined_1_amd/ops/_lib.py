@@ -140,6 +140,7 @@ _SIGNATURES = {
     "det_nms": ([c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p], c_int),
     # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
     "det_conv_nt_rows_per_block": ([c_int], c_int),
+    "det_conv_nt_set_pf": ([c_int], c_int),
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
     "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 3, c_int),
     "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),

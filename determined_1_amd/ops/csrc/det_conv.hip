@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include <stdint.h>
+#include <type_traits>
 
 #include "det_stats.h"
 
@@ -207,8 +208,12 @@ struct NtArgs {
 // + A2) with A = the BN input and A2 = the residual, and the first N tile's blocks write it (Aout)
 // and its ReLU mask bits (abits) for the residual add and the backward: the separate apply pass
 // and this GEMM's read of its output become one pass.
+// PF: register staging sets -- the global loads of K tiles kt+1 .. kt+PF are in flight while tile kt
+// is multiplied (PF = 1: one tile ahead).  The short-K, wide-N GEMMs (layer 2-4 expansions, K =
+// 128..512) spend most of a block's life waiting for each K tile's loads; deeper prefetch overlaps
+// those latencies instead of paying them one after another.
 template <int BM, int BN, int WM, int WN, bool PRO, bool STATS, int GM, int OCC, bool BNB = false, bool BT = false,
-          bool ABN = false, bool AFWD = false>
+          bool ABN = false, bool AFWD = false, int PF = 1>
 __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int ACH = BM * 8 / kThreads, BCH = BN * 8 / kThreads;
@@ -249,8 +254,14 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int BCPR = BN / 8;  // BT: 16-B chunks per B image row
 
   constexpr bool A2IN = ABN || AFWD;
-  us8 ra[ACH], rb[BCH], ra2[A2IN ? ACH : 1];
-  auto gload = [&](int kt) {
+  static_assert(PF >= 1 && PF <= 4, "prefetch depth");
+  us8 ra_[PF][ACH], rb_[PF][BCH], ra2_[PF][A2IN ? ACH : 1];
+  // S: the register set (a compile-time index, std::integral_constant) that holds K tile kt
+  auto gload = [&](auto S, int kt) {
+    constexpr int s = decltype(S)::value;
+    us8* ra = ra_[s];
+    us8* rb = rb_[s];
+    us8* ra2 = ra2_[s];
     const int64_t k = static_cast<int64_t>(kt) * kBK;
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
@@ -272,7 +283,11 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       }
     }
   };
-  auto lstore = [&](int buf, int kt) {
+  auto lstore = [&](auto S, int buf, int kt) {
+    constexpr int s = decltype(S)::value;
+    const us8* ra = ra_[s];
+    const us8* rb = rb_[s];
+    const us8* ra2 = ra2_[s];
     unsigned char* base = smem + buf * BUF;
     // ABN: this thread's 8 channels of the apply coefficients, loaded once per K tile (before the
     // Aout stores, which the compiler could not move them across)
@@ -390,13 +405,18 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   if constexpr (EPRE) eload();
 
   const int nk = a.K / kBK;
-  gload(0);
-  lstore(0, 0);
+  using I0 = std::integral_constant<int, 0>;
+  gload(I0{}, 0);
+  if constexpr (PF > 1) if (1 < nk) gload(std::integral_constant<int, 1 % PF>{}, 1);
+  if constexpr (PF > 2) if (2 < nk) gload(std::integral_constant<int, 2 % PF>{}, 2);
+  if constexpr (PF > 3) if (3 < nk) gload(std::integral_constant<int, 3 % PF>{}, 3);
+  lstore(I0{}, 0, 0);
+  if (PF < nk) gload(I0{}, PF);  // set 0 is free again: tile PF
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
-    const unsigned char* base = smem + cur * BUF;
+  // one K tile: multiply buffer kt & 1, stage tile kt+1 (register set S) into the other buffer and
+  // refill S with tile kt+1+PF
+  auto step = [&](auto S, int kt) {
+    const unsigned char* base = smem + (kt & 1) * BUF;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + (lane >> 4);
@@ -414,8 +434,18 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1, kt + 1);
+    const int nx = kt + 1;
+    if (nx < nk) {
+      lstore(S, nx & 1, nx);
+      if (nx + PF < nk) gload(S, nx + PF);
+    }
     __syncthreads();
+  };
+  for (int kb = 0; kb < nk; kb += PF) {  // unrolled by PF so every register set index is static
+    step(std::integral_constant<int, 1 % PF>{}, kb);
+    if constexpr (PF > 1) if (kb + 1 < nk) step(std::integral_constant<int, 2 % PF>{}, kb + 1);
+    if constexpr (PF > 2) if (kb + 2 < nk) step(std::integral_constant<int, 3 % PF>{}, kb + 2);
+    if constexpr (PF > 3) if (kb + 3 < nk) step(std::integral_constant<int, 4 % PF>{}, kb + 3);
   }
 
   // ---- epilogue: bf16 tile through LDS (coalesced 16-B row stores) + BN statistics ----
@@ -729,7 +759,9 @@ constexpr int nt_smem() {
   return (NBUF * (BM + BN) * 128) > (BM * (BN + 16) * 2) ? NBUF * (BM + BN) * 128 : BM * (BN + 16) * 2;
 }
 
-template <int BM, int BN, int WM, int WN, int OCC>
+// PF (prefetch depth) applies to the plain forward / input-gradient variants; the fused ones
+// (AFWD, ABN, BNB) already use their registers for the extra operands and stay at PF = 1.
+template <int BM, int BN, int WM, int WN, int OCC, int PF = 1>
 int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2, bool bnb = false, bool bt = false) {
   const int64_t mtiles = (a.M + BM - 1) / BM;
   const int64_t nwg = mtiles * (a.N / BN);
@@ -769,13 +801,13 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
       hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true, true>),
                          dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true>),
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, false, true, false, false, PF>),
                          dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
     return static_cast<int>(hipGetLastError());
   }
-#define DET_NT(P, S, G)                                                                               \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G, OCC>), dim3(static_cast<unsigned>(nwg)), \
-                     dim3(kThreads), smem, st, a)
+#define DET_NT(P, S, G)                                                                                           \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, P, S, G, OCC, false, false, false, false, PF>),               \
+                     dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a)
   if (stride2) {
     if (pro) { if (stats) DET_NT(true, true, kGmStride2); else DET_NT(true, false, kGmStride2); }
     else { if (stats) DET_NT(false, true, kGmStride2); else DET_NT(false, false, kGmStride2); }
@@ -800,9 +832,43 @@ int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride
   return static_cast<int>(hipGetLastError());
 }
 
+// Prefetch depth of the OCC-2 plain GEMMs: DET_NT_PF (1..3, default 1 = one K tile ahead), capped
+// at the K tile count.
+int g_nt_pf = -1;  // det_conv_nt_set_pf
+int nt_pf(int K) {
+  static const int env_pf = [] {
+    const char* e = std::getenv("DET_NT_PF");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 1 ? 1 : (v > 3 ? 3 : v);
+  }();
+  const int pf = g_nt_pf > 0 ? g_nt_pf : env_pf;
+  const int nk = K / kBK;
+  return nk < pf ? nk : pf;
+}
+
+template <int BM, int BN>
+int launch_nt_pf(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2, bool bt) {
+  const bool fused = a.abits != nullptr || a.A2 != nullptr;
+  int pf = fused ? 1 : nt_pf(a.K);
+  if (bt && pf > 2) pf = 2;  // the transposed-B variant spills at 3
+  switch (pf) {
+    case 3: return launch_nt<BM, BN, 2, 2, 2, 3>(st, a, pro, stats, stride2, false, bt);
+    case 2: return launch_nt<BM, BN, 2, 2, 2, 2>(st, a, pro, stats, stride2, false, bt);
+    default: return launch_nt<BM, BN, 2, 2, 2, 1>(st, a, pro, stats, stride2, false, bt);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// Prefetch depth of the plain GEMMs (1..3; 0 = back to DET_NT_PF / the default).  Returns the previous
+// override.  For benchmarks and tests; not thread-safe against concurrent launches.
+int det_conv_nt_set_pf(int pf) {
+  const int old = g_nt_pf;
+  g_nt_pf = pf <= 0 ? -1 : (pf > 3 ? 3 : pf);
+  return old;
+}
 
 // Rows per statistics block of det_conv_nt for an N-column output (the BN finalize needs it).
 int det_conv_nt_rows_per_block(int N) { return 128; }
@@ -832,8 +898,8 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
     return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
   }
-  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, pro, stats, stride2);
-  return launch_nt<128, 64, 2, 2, 2>(st, a, pro, stats, stride2);
+  if (N % 128 == 0) return launch_nt_pf<128, 128>(st, a, pro, stats, stride2, false);
+  return launch_nt_pf<128, 64>(st, a, pro, stats, stride2, false);
 }
 
 // dX[M, N] = dY[M, K] . W[K, N]: the input gradient of a 1x1 conv against its weight W = [Cout, Cin]
@@ -852,8 +918,8 @@ int det_conv_dgrad(void* stream, const void* dY, const void* W, void* dX, int64_
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, false, true);
     return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, false, true);
   }
-  if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, false, false, false, false, true);
-  return launch_nt<128, 64, 2, 2, 2>(st, a, false, false, false, false, true);
+  if (N % 128 == 0) return launch_nt_pf<128, 128>(st, a, false, false, false, true);
+  return launch_nt_pf<128, 64>(st, a, false, false, false, true);
 }
 
 // dX[M, N] = dY[M, K] . W^T[N, K]^T with the BN-backward epilogue (BnBwdEpi above): writes

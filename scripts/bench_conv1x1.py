@@ -1,6 +1,8 @@
 """Per-shape timing of ResNet-50's 1x1 convolutions at batch 512 (bf16, NHWC): the hand-written
 det_conv GEMMs (forward + fused BN stats, dgrad, wgrad) vs torch/MIOpen conv2d forward and backward.
-Prints one JSON line per shape plus totals (x multiplicity in the network)."""
+Prints one JSON line per shape plus totals (x multiplicity in the network).  The forward is timed at
+each register prefetch depth of the plain GEMM (det_conv_nt_set_pf 1..3), GEMM-only (no statistics
+epilogue) and fused; TF/s and % of the 2.5 PF/s dense bf16 peak are reported for each."""
 import json
 import sys
 import time
@@ -9,7 +11,9 @@ import torch
 import torch.nn.functional as F
 
 sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
-from determined_1_amd.ops import conv  # noqa: E402
+from determined_1_amd.ops import _lib, conv  # noqa: E402
+
+PEAK_TF = 2500.0
 
 torch.backends.cudnn.benchmark = True
 dev = torch.device("cuda")
@@ -46,7 +50,8 @@ def timeit(fn, iters=10):
     return e0.elapsed_time(e1) / iters
 
 
-tot = {"mine_fwd": 0.0, "mine_dgrad": 0.0, "mine_wgrad": 0.0, "miopen_fwd": 0.0, "miopen_bwd": 0.0}
+tot = {"mine_fwd": 0.0, "mine_fwd_gemm_only": 0.0, "mine_fwd_pf1": 0.0, "mine_dgrad": 0.0, "mine_wgrad": 0.0,
+       "miopen_fwd": 0.0, "miopen_bwd": 0.0}
 for (ci, co, s, h), mult in shapes.items():
     ho = h // s
     m = N * ho * ho
@@ -57,22 +62,38 @@ for (ci, co, s, h), mult in shapes.items():
     dw = torch.empty(co, ci, device=dev, dtype=torch.bfloat16)
     g = (ho, ho, h, h) if s == 2 else None
     x2 = x.view(-1, ci)
-    t_f = timeit(lambda: conv.conv1x1_nt(x2, w, m=m, stats=True, gather=g))
-    t_d = timeit(lambda: conv.conv1x1_nt(dy, wt)) if s == 1 else float("nan")
+    fl = 2.0 * m * ci * co
+    by_pf = {}
+    for pf in (1, 2, 3):
+        _lib.get_lib().det_conv_nt_set_pf(pf)
+        by_pf[pf] = (timeit(lambda: conv.conv1x1_nt(x2, w, m=m, stats=True, gather=g)),
+                     timeit(lambda: conv.conv1x1_nt(x2, w, m=m, stats=False, gather=g)),
+                     timeit(lambda: conv.dgrad_1x1(dy, w)) if s == 1 else float("nan"))
+    _lib.get_lib().det_conv_nt_set_pf(0)
+    best = min(by_pf, key=lambda p: by_pf[p][0])
+    t_f, t_g = by_pf[best][0], by_pf[best][1]
+    t_d = min(v[2] for v in by_pf.values()) if s == 1 else float("nan")
     t_w = timeit(lambda: conv.conv1x1_wgrad(dy, x2, dw, gather=g))
     xc = x.permute(0, 3, 1, 2).requires_grad_()  # channels_last NCHW view
     wc = w.view(co, ci, 1, 1).contiguous(memory_format=torch.channels_last).requires_grad_()
     gy = dy.view(N, ho, ho, co).permute(0, 3, 1, 2)
     t_mf = timeit(lambda: F.conv2d(xc, wc, stride=s))
     t_mb = timeit(lambda: torch.autograd.grad(F.conv2d(xc, wc, stride=s), (xc, wc), gy)) - t_mf
-    fl = 2.0 * m * ci * co
     byt_f = (m * ci * (1 if s == 1 else 1) + m * co) * 2
     rec = {"ci": ci, "co": co, "s": s, "h": h, "mult": mult, "M": m,
-           "mine_fwd_ms": round(t_f, 4), "mine_dgrad_ms": round(t_d, 4), "mine_wgrad_ms": round(t_w, 4),
+           "mine_fwd_ms": round(t_f, 4), "mine_fwd_gemm_only_ms": round(t_g, 4), "best_pf": best,
+           "fwd_ms_by_pf": {p: round(v[0], 4) for p, v in by_pf.items()},
+           "gemm_only_ms_by_pf": {p: round(v[1], 4) for p, v in by_pf.items()},
+           "dgrad_bt_ms_by_pf": {p: round(v[2], 4) for p, v in by_pf.items()},
+           "mine_dgrad_ms": round(t_d, 4), "mine_wgrad_ms": round(t_w, 4),
            "miopen_fwd_ms": round(t_mf, 4), "miopen_bwd_ms": round(t_mb, 4),
-           "mine_fwd_TBs": round(byt_f / t_f / 1e9, 2), "mine_fwd_TFs": round(fl / t_f / 1e9, 1)}
+           "mine_fwd_TBs": round(byt_f / t_f / 1e9, 2), "mine_fwd_TFs": round(fl / t_f / 1e9, 1),
+           "gemm_only_TFs": round(fl / t_g / 1e9, 1), "gemm_only_pct_peak": round(100 * fl / t_g / 1e9 / PEAK_TF, 1),
+           "miopen_fwd_TFs": round(fl / t_mf / 1e9, 1), "miopen_pct_peak": round(100 * fl / t_mf / 1e9 / PEAK_TF, 1)}
     print(json.dumps(rec), flush=True)
     tot["mine_fwd"] += t_f * mult
+    tot["mine_fwd_gemm_only"] += t_g * mult
+    tot["mine_fwd_pf1"] += by_pf[1][0] * mult
     tot["mine_dgrad"] += (t_d if s == 1 else 0.0) * mult
     tot["mine_wgrad"] += t_w * mult
     tot["miopen_fwd"] += t_mf * mult

@@ -85,6 +85,40 @@ def test_conv_dgrad_untransposed_weight_exact(gpu, m, cin, cout):
     torch.testing.assert_close(dx.float().cpu(), (dy.float() @ w.float()).to(torch.bfloat16).float(), rtol=0, atol=0)
 
 
+@pytest.fixture
+def nt_pf():
+    from determined_1_amd.ops import _lib
+
+    lib = _lib.get_lib()
+    yield lib.det_conv_nt_set_pf
+    lib.det_conv_nt_set_pf(0)
+
+
+PF_SHAPES = [  # (M, K, N): K tiles 2..10 cover every prefetch-ring phase at depths 1-3
+    (777, 128, 256), (1000, 192, 128), (4096 + 77, 256, 512), (640, 320, 64), (1500, 512, 128), (333, 640, 256),
+]
+
+
+@pytest.mark.parametrize("pf", [1, 2, 3])
+@pytest.mark.parametrize("m,k,n", PF_SHAPES)
+def test_conv_nt_prefetch_depths_exact(gpu, nt_pf, pf, m, k, n):
+    """det_conv_nt / det_conv_dgrad at every register prefetch depth (the K-tile ring of the plain
+    GEMMs): integer operands whose fp32 sums are exact, so the bf16 output must equal the rounded
+    fp32 product bit for bit -- a ring slot staged from the wrong K tile shows."""
+    nt_pf(pf)
+    g = torch.Generator(device="cpu").manual_seed(m + k + pf)
+    a = torch.randint(-2, 3, (m, k), generator=g).to(torch.bfloat16)
+    b = torch.randint(-2, 3, (n, k), generator=g).to(torch.bfloat16)
+    want = (a.float() @ b.float().t()).to(torch.bfloat16)
+    y, parts = conv.conv1x1_nt(a.to(gpu), b.to(gpu), stats=True)
+    assert torch.equal(y.cpu(), want)
+    mean, _ = _merge(*parts, m)
+    torch.testing.assert_close(mean, y.double().cpu().mean(0), rtol=1e-6, atol=1e-6)
+    # input gradient against the untransposed [K, N] weight (transposed LDS reads; depth capped at 2)
+    dx = conv.dgrad_1x1(a.to(gpu), b.t().contiguous().to(gpu))
+    assert torch.equal(dx.cpu(), want)
+
+
 @pytest.mark.parametrize("m,cin,cout", SHAPES + [(50000, 64, 256)])
 @pytest.mark.parametrize("pro", [False, True])
 def test_conv_wgrad(gpu, m, cin, cout, pro):

@@ -43,8 +43,12 @@ def _run(out, amp, compress, data, steps, lr, mom, ranks):
     return torch.load(out + ".pt")
 
 
-def _fusions_on(info):
+def _fusions_on(info, amp):
+    """At O2 every bf16 fusion runs; O0 (fp32 activations, the reference's precision) runs the fp32
+    library convs and BatchNorm, so there the test covers the bucketer, compression and GradSink."""
     c = info["counts"]
+    if amp != "O2":
+        return
     assert c["fwd_apply"]["in_gemm"] > 0, c  # deferred BN forward applies staged by the next conv1
     assert c["bn_bwd"]["fused"] > 0, c        # BN-backward partials from dgrad epilogues
     assert c["conv3x3"]["fallback"] == 0 and c["bn_fallbacks"] == 0, c
@@ -62,7 +66,7 @@ def test_identical_batches_match_single_process(gpu, tmp_path, amp, compress):
     modes = {b["mode"] for bs in dp["buckets"] for b in bs}
     # the bf16 arena reduces through fp32_accum; a small fp32 arena (O2's BatchNorm parameters) as-is
     assert "fp32_accum" in modes and modes <= {"fp32_accum", "allreduce"}, dp["buckets"]
-    _fusions_on(dp)
+    _fusions_on(dp, amp)
     assert torch.equal(dp["init"], ref["init"])  # the same seeded initialisation
     moved = (ref["params"] - ref["init"]).abs()
     diff = (dp["params"] - ref["params"]).abs()
@@ -78,7 +82,7 @@ def test_split_batches_average_the_gradients(gpu, tmp_path, amp, compress):
     r0 = _run(str(tmp_path / "b0"), amp, compress, "b0", 1, 1.0, 0.0, 1)
     r1 = _run(str(tmp_path / "b1"), amp, compress, "b1", 1, 1.0, 0.0, 1)
     dp = _run(str(tmp_path / "dp"), amp, compress, "pair", 1, 1.0, 0.0, 2)
-    _fusions_on(dp)
+    _fusions_on(dp, amp)
     init = r0["init"].double()
     assert torch.equal(r1["init"], r0["init"]) and torch.equal(dp["init"], r0["init"])
     g0, g1 = init - r0["params"].double(), init - r1["params"].double()
