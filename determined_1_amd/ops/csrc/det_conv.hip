@@ -832,13 +832,14 @@ int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride
   return static_cast<int>(hipGetLastError());
 }
 
-// Prefetch depth of the OCC-2 plain GEMMs: DET_NT_PF (1..3, default 1 = one K tile ahead), capped
-// at the K tile count.
+// Prefetch depth of the OCC-2 plain GEMMs: DET_NT_PF (1..3), capped at the K tile count.  Default 3:
+// GEMM-only 2-10 % faster than depth 1 on most ResNet 1x1 shapes (profiles/r4_conv1x1_pf_sweep.jsonl);
+// neutral on the whole step, where the fused variants carry most calls (r4_nt_pf_ab.jsonl).
 int g_nt_pf = -1;  // det_conv_nt_set_pf
 int nt_pf(int K) {
   static const int env_pf = [] {
     const char* e = std::getenv("DET_NT_PF");
-    const int v = e ? std::atoi(e) : 1;
+    const int v = e ? std::atoi(e) : 3;
     return v < 1 ? 1 : (v > 3 ? 3 : v);
   }();
   const int pf = g_nt_pf > 0 ? g_nt_pf : env_pf;

@@ -53,6 +53,11 @@ class Trial(ResNetImageNetTrial):
 
 def main() -> None:
     out, amp, compress, data, steps, lr, mom = sys.argv[1:8]
+    # O0 runs the fp32 convolutions on MIOpen: deterministic solvers only, so that two processes on
+    # the same batches agree to rounding (the weight-gradient solvers with atomics otherwise add
+    # run-to-run noise the comparison would mistake for a reduction error)
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
     os.environ["RDP_DATA"], os.environ["RDP_STEPS"] = data, steps
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rec = Recorder().train(1, int(steps), 0)
