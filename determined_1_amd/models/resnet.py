@@ -211,7 +211,9 @@ class ResNet(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _FWD.depth = getattr(_FWD, "depth", 0) + 1  # blocks may defer their output applies (see _FWD)
         try:
-            x = self.maxpool(self.bn1(self._stem(x)))
+            x = self.bn1(self._stem(x))
+            # the stem BN's output feeds only the pool: its backward partials come from the pool's
+            x = self.maxpool(x, bn_exclusive=True) if isinstance(self.maxpool, MaxPool3x3s2) else self.maxpool(x)
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             _FWD.depth -= 1

@@ -110,7 +110,10 @@ _SIGNATURES = {
     # stream, dtype, x, y, idx(u8), N, H, W, C
     "det_maxpool3s2_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
     # stream, dtype, dy, idx(u8), dx, N, H, W, C
-    "det_maxpool3s2_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
+    # ... + bn_x, bn_mean, bn_scale, bn_shift, psum, psumx (nullable BN-backward epilogue)
+    "det_maxpool3s2_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p] * 6,
+                           c_int),
+    "det_maxpool3s2_bwd_rows_per_block": ([], c_int),
     "det_bn_apply": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, dy, x, mask_bits, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws
@@ -167,8 +170,8 @@ _SIGNATURES = {
     "det_conv3p": ([c_void_p] * 4 + [c_int] * 5 + [c_void_p] * 10 + [c_int], c_int),
     "det_conv3p_wgrad_ws_elems": ([c_i64, c_int, c_int], c_i64),
     "det_stemp_wgrad_ws_elems": ([c_i64], c_i64),
-    # stream, dY, X4, out, out_dtype, M, Hi, Wi, Ho, Wo, ws, out_scale
-    "det_stemp_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 4 + [c_void_p, c_float], c_int),
+    # stream, dY, X4, out, out_dtype, M, Hi, Wi, Ho, Wo, ws, out_scale, bn_x, coef (nullable deferred BN apply)
+    "det_stemp_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 4 + [c_void_p, c_float] + [c_void_p] * 2, c_int),
     # stream, dY, X, out, out_dtype, Nb, H, W, Cin, N, ws, out_scale
     "det_conv3p_wgrad": ([c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_float], c_int),
     # stream, dY, X, out, out_dtype, M, N, Cin, Hi, Wi, Ho, Wo, R, S, stride, pad, ws, out_scale

@@ -947,6 +947,10 @@ class _StemConv(torch.autograd.Function):
                    "stem_conv_fwd")
         _attach_partials(y, parts)
         ctx.save_for_backward(x4, weight)
+        # the stem BatchNorm may defer its backward apply onto this node (take_pending_apply): the
+        # patch wgrad stages it, and the image batch needs no input gradient
+        ctx.accepts_bn_apply = is_gpu(x4) and STEM_PATCH_WGRAD and not x4.requires_grad
+        ctx.pending_bn_apply = None
         return y
 
     @staticmethod
@@ -955,22 +959,33 @@ class _StemConv(torch.autograd.Function):
         n, _, hi, wi = x4.shape
         ho, wo = dy.shape[2], dy.shape[3]
         m = n * ho * wo
+        pend = take_pending_apply(ctx, dy)
+        if pend is not None and (ctx.needs_input_grad[0] or not ctx.needs_input_grad[1]):
+            materialize_pending_apply(dy, pend)
+            pend = None
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         ci = weight.shape[1]
         native_wgrad = False
         if ctx.needs_input_grad[1] and STEM_PATCH_WGRAD:
-            # the patch kernel (det_igemm.hip stemp_wgrad): each input row staged once per chunk
+            # the patch kernel (det_igemm.hip stemp_wgrad): each input row staged once per chunk;
+            # with a deferred BN-backward apply, dY = coef . (d, x) is computed while staging
             lib = _lib.get_lib()
             ws = torch.empty(int(lib.det_stemp_wgrad_ws_elems(m)), dtype=torch.float32, device=dy.device)
             dwk = torch.empty(64, 256, dtype=torch.float32, device=dy.device)
-            rc = lib.det_stemp_wgrad(_stream(dy), dyc.data_ptr(), x4.data_ptr(), dwk.data_ptr(), 0, int(m), int(hi),
-                                     int(wi), int(ho), int(wo), ws.data_ptr(), 1.0)
+            src, bx, coef = (dyc, None, None) if pend is None else pend
+            rc = lib.det_stemp_wgrad(_stream(dy), src.data_ptr(), x4.data_ptr(), dwk.data_ptr(), 0, int(m), int(hi),
+                                     int(wi), int(ho), int(wo), ws.data_ptr(), 1.0, _ptr(bx), _ptr(coef))
             if rc != -6:
                 _lib.check(rc, "stemp_wgrad")
                 dw = unpack_stem_grad(dwk, ci).to(weight.dtype).contiguous(memory_format=torch.channels_last)
                 native_wgrad = True
                 FUSED_COUNTS["stem_wgrad_patch"] += 1
+                if pend is not None:
+                    BN_APPLY_COUNTS["in_gemm"] += 1
+            elif pend is not None:  # the patch does not fit: the apply is needed in HBM after all
+                materialize_pending_apply(dy, pend)
+                pend = None
         if not native_wgrad and ctx.needs_input_grad[1] and STEM_NATIVE_WGRAD:
             native_wgrad = True
             lib = _lib.get_lib()

@@ -1490,10 +1490,16 @@ struct SpArgs {
   int64_t M;
   int Hi, Wi, Ho, Wo;
   int rows_per_split;        // multiple of 256
+  // ABN (nullable): dY is the stem BatchNorm's backward apply, computed while staging:
+  // dY = coef[0][c] * dY_in + coef[1][c] * bn_x + coef[2][c] (dY_in = the BN's masked output gradient,
+  // bn_x = its input [M, 64]); the materialised input gradient of the BN is never written
+  const unsigned short* bn_x;
+  const float* coef;  // [3][64]
 };
 constexpr int kSpPMAX = 14 * 240;  // padded input pixels per chunk (Wi <= 234)
 constexpr int kSpSMEM = 256 * 128 + kSpPMAX * 8 + 256 * 4;
 
+template <bool ABN>
 __global__ void __launch_bounds__(512, 1) stemp_wgrad_kernel(SpArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -1513,7 +1519,17 @@ __global__ void __launch_bounds__(512, 1) stemp_wgrad_kernel(SpArgs a) {
   const int Hp = a.Hi + 6, Wp = a.Wi + 6;  // 3 pixels of zero padding on every side
   const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
 
-  us8 ry[DYCH], rx[XCH];
+  us8 ry[DYCH], rx[XCH], rz[ABN ? DYCH : 1];
+  float ca[8], cb[8], cc8[8];  // ABN: this thread's 8 channels (tid & 7) of the apply coefficients
+  if constexpr (ABN) {
+    const int c0 = (tid & 7) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = a.coef[c0 + j];
+      cb[j] = a.coef[64 + c0 + j];
+      cc8[j] = a.coef[128 + c0 + j];
+    }
+  }
   auto geom = [&](int64_t m0, int& g0, int& rows) {
     int64_t ml = m0 + 255;
     if (ml >= a.M) ml = a.M - 1;
@@ -1530,6 +1546,8 @@ __global__ void __launch_bounds__(512, 1) stemp_wgrad_kernel(SpArgs a) {
       const int idx = tid + q * NT, r = idx >> 3, cc = idx & 7;
       const int64_t m = m0 + r;
       ry[q] = m < pend ? *reinterpret_cast<const us8*>(a.dY + m * 64 + cc * 8) : us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if constexpr (ABN)
+        rz[q] = m < pend ? *reinterpret_cast<const us8*>(a.bn_x + m * 64 + cc * 8) : us8{0, 0, 0, 0, 0, 0, 0, 0};
     }
     // the patch in 16-B pieces = 2 padded pixels of 4 channels
     const int npc = (rows * Wp + 1) / 2;
@@ -1560,7 +1578,17 @@ __global__ void __launch_bounds__(512, 1) stemp_wgrad_kernel(SpArgs a) {
 #pragma unroll
     for (int q = 0; q < DYCH; ++q) {
       const int idx = tid + q * NT, r = idx >> 3, cc = idx & 7;
-      *reinterpret_cast<us8*>(dys + (r >> 5) * 4096 + wswz(r & 31, cc)) = ry[q];
+      us8 v = ry[q];
+      if constexpr (ABN) {
+        // exactly det_norm.hip bn_apply_bwd<MASK 0>: fma(A, d, fma(B, x, C)) in fp32, one rounding;
+        // rows past the end stay zero
+        if (m0 + r < pend) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = f2bf(__fmaf_rn(ca[j], bf2f(ry[q][j]), __fmaf_rn(cb[j], bf2f(rz[q][j]), cc8[j])));
+        }
+      }
+      *reinterpret_cast<us8*>(dys + (r >> 5) * 4096 + wswz(r & 31, cc)) = v;
     }
     const int npc = (rows * Wp + 1) / 2;
 #pragma unroll
@@ -1857,19 +1885,26 @@ int64_t det_stemp_wgrad_ws_elems(int64_t M) { return static_cast<int64_t>(sp_spl
 // on the patch kernel above: out [64, 256] (packed k = r*32 + s*4 + c; fp32 or bf16) = out_scale *
 // sum over pixels, via split fp32 slabs in ws (>= det_stemp_wgrad_ws_elems(M)).  -6 for widths the
 // patch cannot hold (Wi > 234).
+// bn_x / coef (nullable, both or neither): dY is the stem BatchNorm's backward apply of the given
+// masked gradient (SpArgs ABN).
 int det_stemp_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int Hi, int Wi,
-                    int Ho, int Wo, float* ws, float out_scale) {
+                    int Ho, int Wo, float* ws, float out_scale, const void* bn_x, const float* coef) {
   if (M <= 0 || Hi <= 0 || Wi <= 0 || Ho != (Hi - 1) / 2 + 1 || Wo != (Wi - 1) / 2 + 1) return -1;
   if (Wi + 6 > 240) return -6;
-  if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X)) & 15) != 0) return -5;
+  if ((bn_x == nullptr) != (coef == nullptr)) return -2;
+  if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(bn_x)) & 15) != 0)
+    return -5;
   const int splits = sp_splits(M);
   int64_t rps = (M + splits - 1) / splits;
   rps = (rps + 255) / 256 * 256;
   const int real = static_cast<int>((M + rps - 1) / rps);
   SpArgs a{static_cast<const unsigned short*>(dY), static_cast<const unsigned short*>(X), ws, M, Hi, Wi, Ho, Wo,
-           static_cast<int>(rps)};
+           static_cast<int>(rps), static_cast<const unsigned short*>(bn_x), coef};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(stemp_wgrad_kernel, dim3(static_cast<unsigned>(real)), dim3(512), kSpSMEM, st, a);
+  if (bn_x)
+    hipLaunchKernelGGL(stemp_wgrad_kernel<true>, dim3(static_cast<unsigned>(real)), dim3(512), kSpSMEM, st, a);
+  else
+    hipLaunchKernelGGL(stemp_wgrad_kernel<false>, dim3(static_cast<unsigned>(real)), dim3(512), kSpSMEM, st, a);
   int rc = static_cast<int>(hipGetLastError());
   if (rc != 0) return rc;
   const int64_t slab = 64 * 256, n4 = slab / 4;

@@ -64,15 +64,15 @@ struct PoolGeom {
 
 template <typename T>
 __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x, T* __restrict__ y,
-                                                        uint8_t* __restrict__ idx, PoolGeom g, int64_t nvec) {
+                                                        uint8_t* __restrict__ idx, PoolGeom g, int nvec) {
   const int cv = g.C / 8;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
-       i += static_cast<int64_t>(gridDim.x) * kThreads) {
-    int64_t t = i;
-    const int c8 = static_cast<int>(t % cv); t /= cv;
-    const int ow = static_cast<int>(t % g.Wo); t /= g.Wo;
-    const int oh = static_cast<int>(t % g.Ho);
-    const int n = static_cast<int>(t / g.Ho);
+  // 32-bit index math (nvec < 2^31, checked by the host): 64-bit division is a long software sequence
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < nvec; i += gridDim.x * kThreads) {
+    int t = i;
+    const int c8 = t % cv; t /= cv;
+    const int ow = t % g.Wo; t /= g.Wo;
+    const int oh = t % g.Ho;
+    const int n = t / g.Ho;
     // torch semantics: start from -inf with the window's first valid slot, take v if v > max
     // or v is NaN (the first NaN then sticks)
     const uint8_t slot0 = static_cast<uint8_t>(3 * (oh == 0 ? 1 : 0) + (ow == 0 ? 1 : 0));
@@ -103,28 +103,59 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x,
         }
       }
     }
-    Vec8<T>::store(y + i * 8, m);
+    Vec8<T>::store(y + static_cast<int64_t>(i) * 8, m);
     uc8 av;
 #pragma unroll
     for (int j = 0; j < 8; ++j) av[j] = a[j];
-    *reinterpret_cast<uc8*>(idx + i * 8) = av;
+    *reinterpret_cast<uc8*>(idx + static_cast<int64_t>(i) * 8) = av;
   }
 }
 
+// One block = kBwdRows consecutive INPUT pixels (all channels); thread t owns channel group
+// t % (C/8) of pixels t / (C/8), + 256 / (C/8), ...  Pixel coordinates in 32-bit math (the input has
+// < 2^31 pixels; 64-bit division is a long software sequence per element).
 // kTwo: a second upstream gradient dy2 of the pooled output (a linked projection shortcut that also
 // reads it, ops/norm.py linked_conv2d) is summed in the gather instead of by a separate add pass.
-template <typename T, bool kTwo>
+// BNB: the pooled tensor is the output of a training BatchNorm + ReLU (the ResNet stem): the gathered
+// gradient is masked with relu'(x * scale + shift) (x = the BN input) and each block writes the BN
+// backward's partial sums psum = sum d, psumx = sum d (x - mean) over its pixels -- the BN backward
+// is then a finalize and an apply (ops/norm.py fused_bwd), with no partial pass over the tensor.
+constexpr int kBwdRows = 512;
+
+struct BnbArgs {
+  const unsigned short* x;  // BN input [pixels, C]
+  const float* mean;
+  const float* scale;
+  const float* shift;
+  float* psum;   // [blocks, C]
+  float* psumx;  // [blocks, C]
+};
+
+template <typename T, bool kTwo, bool BNB>
 __global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                         const uint8_t* __restrict__ idx, T* __restrict__ dx, PoolGeom g,
-                                                        int64_t nvec) {
+                                                        BnbArgs bn) {
   const int cv = g.C / 8;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
-       i += static_cast<int64_t>(gridDim.x) * kThreads) {
-    int64_t t = i;
-    const int c8 = static_cast<int>(t % cv); t /= cv;
-    const int w = static_cast<int>(t % g.W); t /= g.W;
-    const int h = static_cast<int>(t % g.H);
-    const int n = static_cast<int>(t / g.H);
+  const int c8 = threadIdx.x % cv, lanes = kThreads / cv;
+  const int npix = g.N * g.H * g.W;
+  const int p0 = blockIdx.x * kBwdRows;
+  const int p1 = min(npix, p0 + kBwdRows);
+  float mu[8], sc[8], sh[8], s1[8], s2[8];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = bn.mean[8 * c8 + j];
+      sc[j] = bn.scale[8 * c8 + j];
+      sh[j] = bn.shift[8 * c8 + j];
+      s1[j] = 0.f;
+      s2[j] = 0.f;
+    }
+  }
+  for (int p = p0 + static_cast<int>(threadIdx.x) / cv; p < p1; p += lanes) {
+    const int w = p % g.W;
+    const int t = p / g.W;
+    const int h = t % g.H;
+    const int n = t / g.H;
     float acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
@@ -139,7 +170,7 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy
         const int ow = (w + 1) / 2 - dw;
         const int kw = w - (2 * ow - 1);
         if (ow < 0 || ow >= g.Wo || kw < 0 || kw > 2) continue;
-        const int64_t o = ((static_cast<int64_t>(n) * g.Ho + oh) * g.Wo + ow) * g.C + 8 * c8;
+        const int64_t o = (static_cast<int64_t>(n * g.Ho + oh) * g.Wo + ow) * g.C + 8 * c8;
         const uc8 av = *reinterpret_cast<const uc8*>(idx + o);
         const uint8_t me = static_cast<uint8_t>(3 * kh + kw);
         bool any = false;
@@ -158,7 +189,39 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy
         for (int j = 0; j < 8; ++j) acc[j] += av[j] == me ? d[j] : 0.f;
       }
     }
-    Vec8<T>::store(dx + i * 8, acc);
+    const int64_t e = static_cast<int64_t>(p) * g.C + 8 * c8;
+    if constexpr (BNB) {
+      float xv[8];
+      Vec8<unsigned short>::load(bn.x + e, xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dm = __fmaf_rn(xv[j], sc[j], sh[j]) > 0.f ? acc[j] : 0.f;
+        const float dr = __uint_as_float(static_cast<uint32_t>(f2bf(dm)) << 16);  // what the apply reads back
+        acc[j] = dr;
+        s1[j] += dr;
+        s2[j] += dr * (xv[j] - mu[j]);
+      }
+    }
+    Vec8<T>::store(dx + e, acc);
+  }
+  if constexpr (BNB) {
+    __shared__ float red[kThreads][17];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[threadIdx.x][j] = s1[j];
+      red[threadIdx.x][8 + j] = s2[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < g.C; c += kThreads) {  // channel c = 8 * group + j
+      const int grp = c / 8, j = c % 8;
+      float t1 = 0.f, t2 = 0.f;
+      for (int l = 0; l < lanes; ++l) {
+        t1 += red[l * cv + grp][j];
+        t2 += red[l * cv + grp][8 + j];
+      }
+      bn.psum[static_cast<int64_t>(blockIdx.x) * g.C + c] = t1;
+      bn.psumx[static_cast<int64_t>(blockIdx.x) * g.C + c] = t2;
+    }
   }
 }
 
@@ -178,41 +241,55 @@ int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t*
   if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0) return -1;
   PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
   const int64_t nvec = static_cast<int64_t>(N) * g.Ho * g.Wo * (C / 8);
+  if (nvec >= (static_cast<int64_t>(1) << 31)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (dtype == 1)
     hipLaunchKernelGGL(maxpool_fwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
-                       static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g, nvec);
+                       static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g,
+                       static_cast<int>(nvec));
   else
     hipLaunchKernelGGL(maxpool_fwd<float>, dim3(grid_for(nvec)), dim3(kThreads), 0, st, static_cast<const float*>(x),
-                       static_cast<float*>(y), idx, g, nvec);
+                       static_cast<float*>(y), idx, g, static_cast<int>(nvec));
   return static_cast<int>(hipGetLastError());
 }
 
+// Input pixels per partial-sum block of det_maxpool3s2_bwd's BN-backward epilogue.
+int det_maxpool3s2_bwd_rows_per_block() { return kBwdRows; }
+
 // dy [N, Ho, Wo, C] (+ optional dy2 of the same shape, summed), idx from the forward -> dx [N, H, W, C]
-// (fully overwritten).
+// (fully overwritten).  C % 8 == 0 and 256 % (C / 8) == 0; N*H*W < 2^31.
+// bn_x (nullable, bf16 only): with bn_mean/scale/shift [C] and psum/psumx [ceil(N*H*W / rows), C],
+// dx = relu'(bn_x * scale + shift) * gradient and the BN-backward partials (see maxpool_bwd BNB).
 int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int N,
-                       int H, int W, int C) {
-  if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0) return -1;
+                       int H, int W, int C, const void* bn_x, const float* bn_mean, const float* bn_scale,
+                       const float* bn_shift, float* psum, float* psumx) {
+  if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0 || kThreads % (C / 8) != 0) return -1;
+  if (static_cast<int64_t>(N) * H * W >= (static_cast<int64_t>(1) << 31)) return -3;
+  if (bn_x && (dtype != 1 || !bn_mean || !bn_scale || !bn_shift || !psum || !psumx)) return -2;
   PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
-  const int64_t nvec = static_cast<int64_t>(N) * H * W * (C / 8);
+  const int64_t npix = static_cast<int64_t>(N) * H * W;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const dim3 grid(grid_for(nvec)), block(kThreads);
+  const dim3 grid(static_cast<unsigned>((npix + kBwdRows - 1) / kBwdRows)), block(kThreads);
+  const BnbArgs bn{static_cast<const unsigned short*>(bn_x), bn_mean, bn_scale, bn_shift, psum, psumx};
   if (dtype == 1) {
     auto* a = static_cast<const unsigned short*>(dy);
     auto* b = static_cast<const unsigned short*>(dy2);
     auto* o = static_cast<unsigned short*>(dx);
-    if (dy2)
-      hipLaunchKernelGGL((maxpool_bwd<unsigned short, true>), grid, block, 0, st, a, b, idx, o, g, nvec);
-    else
-      hipLaunchKernelGGL((maxpool_bwd<unsigned short, false>), grid, block, 0, st, a, b, idx, o, g, nvec);
+    if (bn_x) {
+      if (dy2) hipLaunchKernelGGL((maxpool_bwd<unsigned short, true, true>), grid, block, 0, st, a, b, idx, o, g, bn);
+      else hipLaunchKernelGGL((maxpool_bwd<unsigned short, false, true>), grid, block, 0, st, a, b, idx, o, g, bn);
+    } else {
+      if (dy2) hipLaunchKernelGGL((maxpool_bwd<unsigned short, true, false>), grid, block, 0, st, a, b, idx, o, g, bn);
+      else hipLaunchKernelGGL((maxpool_bwd<unsigned short, false, false>), grid, block, 0, st, a, b, idx, o, g, bn);
+    }
   } else {
     auto* a = static_cast<const float*>(dy);
     auto* b = static_cast<const float*>(dy2);
     auto* o = static_cast<float*>(dx);
     if (dy2)
-      hipLaunchKernelGGL((maxpool_bwd<float, true>), grid, block, 0, st, a, b, idx, o, g, nvec);
+      hipLaunchKernelGGL((maxpool_bwd<float, true, false>), grid, block, 0, st, a, b, idx, o, g, bn);
     else
-      hipLaunchKernelGGL((maxpool_bwd<float, false>), grid, block, 0, st, a, b, idx, o, g, nvec);
+      hipLaunchKernelGGL((maxpool_bwd<float, false, false>), grid, block, 0, st, a, b, idx, o, g, bn);
   }
   return static_cast<int>(hipGetLastError());
 }

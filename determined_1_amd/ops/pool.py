@@ -4,6 +4,8 @@ GPU path: one-byte argmax per output element and a gather backward (no zero fill
 CPU tensors and layouts the kernel does not cover (C % 8 != 0, not channels_last, fp16) use
 ``F.max_pool2d``, which is also the numerics reference of the GPU tests.
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -12,7 +14,24 @@ from determined_1_amd.ops import _lib
 
 FALLBACKS = {"count": 0}
 LINKED = {"count": 0}  # backward passes that summed a linked shortcut gradient
+# the pooled tensor is a fused training BN + ReLU output read by nothing else (the ResNet stem): the
+# backward gather applies the ReLU mask and writes that BN's backward partial sums (det_pool.hip
+# maxpool_bwd BNB), so the BN backward skips its partial pass over the largest activation
+FUSE_BN_BWD = os.environ.get("DET_POOL_BN_BWD", "1") != "0"
+BN_BWD_COUNTS = {"fused": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
+
+
+def _bn_producer(x: torch.Tensor):
+    """The fused BN(+ReLU, no residual) node that produced ``x`` when its backward can take its
+    partial sums from this pool's backward, else None."""
+    from determined_1_amd.ops.norm import _BNActTrain, _observed
+
+    gf = x.grad_fn
+    if not (FUSE_BN_BWD and isinstance(gf, _BNActTrain._backward_cls) and getattr(gf, "mask_mode", 0) == 1
+            and x.dtype == torch.bfloat16 and not _observed(x)):
+        return None
+    return gf
 
 
 def _ok(x: torch.Tensor) -> bool:
@@ -22,7 +41,7 @@ def _ok(x: torch.Tensor) -> bool:
 
 class _MaxPool3s2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, bn_exclusive=False):
         N, C, H, W = x.shape
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
@@ -33,6 +52,7 @@ class _MaxPool3s2(torch.autograd.Function):
         ctx.save_for_backward(idx)
         ctx.shape = (N, C, H, W)
         ctx.extra_dy = None  # set by a linked shortcut consumer (ops/norm.py linked_conv2d)
+        ctx.bn_producer = _bn_producer(x) if (bn_exclusive and torch.is_grad_enabled()) else None
         return y
 
     @staticmethod
@@ -54,16 +74,36 @@ class _MaxPool3s2(torch.autograd.Function):
             LINKED["count"] += 1
         dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         st = torch._C._cuda_getCurrentRawStream(dy.device.index)
-        _lib.check(_lib.get_lib().det_maxpool3s2_bwd(st, _DT[dy.dtype], dy.data_ptr(),
-                                                     None if extra is None else extra.data_ptr(), idx.data_ptr(),
-                                                     dx.data_ptr(), N, H, W, C), "det_maxpool3s2_bwd")
-        return dx
+        lib = _lib.get_lib()
+        prod, ctx.bn_producer = ctx.bn_producer, None
+        bn = [None] * 6
+        if prod is not None and getattr(prod, "fused_bwd", None) is None and dy.dtype == torch.bfloat16:
+            try:
+                xb, _, _, stats = prod.saved_tensors
+            except RuntimeError:  # already freed (a second backward)
+                xb = None
+            if xb is not None and xb.shape == dx.shape and xb.is_contiguous(memory_format=torch.channels_last):
+                rpb = int(lib.det_maxpool3s2_bwd_rows_per_block())
+                nrb = (N * H * W + rpb - 1) // rpb
+                psum = torch.empty(nrb, C, dtype=torch.float32, device=dy.device)
+                psumx = torch.empty(nrb, C, dtype=torch.float32, device=dy.device)
+                bn = [xb.data_ptr(), stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), psum.data_ptr(),
+                      psumx.data_ptr()]
+        _lib.check(lib.det_maxpool3s2_bwd(st, _DT[dy.dtype], dy.data_ptr(), None if extra is None else extra.data_ptr(),
+                                          idx.data_ptr(), dx.data_ptr(), N, H, W, C, *bn), "det_maxpool3s2_bwd")
+        if bn[0] is not None:
+            # dx is the masked gradient; the BN backward finalizes these partials (ops/norm.py fused_bwd)
+            prod.fused_bwd = (psum, psumx, rpb)
+            BN_BWD_COUNTS["fused"] += 1
+        return dx, None
 
 
-def max_pool_3x3s2(x: torch.Tensor) -> torch.Tensor:
-    """``F.max_pool2d(x, 3, 2, 1)``."""
+def max_pool_3x3s2(x: torch.Tensor, bn_exclusive: bool = False) -> torch.Tensor:
+    """``F.max_pool2d(x, 3, 2, 1)``.  ``bn_exclusive``: this pool is the only autograd consumer of
+    ``x``, the output of a fused BatchNorm+ReLU, whose backward partials can then come from the
+    pool's backward (``FUSE_BN_BWD``)."""
     if _ok(x):
-        return _MaxPool3s2.apply(x)
+        return _MaxPool3s2.apply(x, bn_exclusive)
     if x.device.type == "cuda":
         FALLBACKS["count"] += 1
     return F.max_pool2d(x, 3, 2, 1)
@@ -72,5 +112,5 @@ def max_pool_3x3s2(x: torch.Tensor) -> torch.Tensor:
 class MaxPool3x3s2(nn.Module):
     """Drop-in for ``nn.MaxPool2d(3, stride=2, padding=1)`` (the ResNet stem)."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return max_pool_3x3s2(x)
+    def forward(self, x: torch.Tensor, bn_exclusive: bool = False) -> torch.Tensor:
+        return max_pool_3x3s2(x, bn_exclusive)

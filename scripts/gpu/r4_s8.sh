@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 session 8: stem BN backward fused into the max-pool gather (partials) + the stem weight
+# gradient (deferred apply); faster pool indexing.  Tests, bench A/B (DET_POOL_BN_BWD), bn-prologue A/B,
+# steady profile, then the DP equivalence tests (O0 now with deterministic MIOpen + noise floor).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r4s8
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_pool_gpu.py tests/test_conv_gpu.py tests/test_bn_bwd_fusion_gpu.py tests/test_norm_gpu.py > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for cfg in "on:1:" "off:0:" "on:1:" "off:0:" "pro:1:--bn-prologue" "pro:1:--bn-prologue"; do
+  name=${cfg%%:*}; rest=${cfg#*:}; v=${rest%%:*}; args=${rest#*:}
+  DET_POOL_BN_BWD=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 $args > $O/bench_$name.json 2> $O/bench_$name.err || { tail -30 $O/bench_$name.err; exit 1; }
+  echo "$name $(python3 -c "import json;d=json.load(open('$O/bench_$name.json'));print(d['value'],d['ms_per_step'])")"
+done
+timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 8 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
+f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
+python3 scripts/prof_summarize.py "$f" --out $O/steady.csv > $O/steady.txt 2>&1 || { tail -5 $O/steady.txt; exit 1; }
+head -3 $O/steady.txt
+rm -rf $O/prof
+timeout -k 10 900 python -u -m pytest -x -v -s --timeout 900 --timeout-method thread -p no:cacheprovider -m gpu tests/test_dp_resnet_gpu.py > $O/pytest_dp.log 2>&1 || { tail -60 $O/pytest_dp.log; exit 1; }
+grep "dp-vs-single\|passed\|failed" $O/pytest_dp.log | tail -6

@@ -307,9 +307,26 @@ def test_stem_patch_wgrad_exact_on_integer_operands(gpu, n, h, w):
     ws = torch.empty(int(lib.det_stemp_wgrad_ws_elems(m)), dtype=torch.float32, device=gpu)
     out = torch.empty(64, 256, dtype=torch.float32, device=gpu)
     _lib.check(lib.det_stemp_wgrad(torch.cuda.current_stream().cuda_stream, dyg.data_ptr(), xg.data_ptr(),
-                                   out.data_ptr(), 0, m, h, w, ho, wo, ws.data_ptr(), 1.0), "stemp")
+                                   out.data_ptr(), 0, m, h, w, ho, wo, ws.data_ptr(), 1.0, None, None), "stemp")
     got = conv.unpack_stem_grad(out, 4).cpu()
     torch.testing.assert_close(got, ref, rtol=0, atol=0)
+    # ABN: dY staged as the BN-backward apply coef0 * d + coef1 * x + coef2 (small integers and
+    # halves: every product and sum exact, so the staged bf16 dY equals the reference apply)
+    d = torch.randint(-2, 3, (n, 64, ho, wo), generator=g).to(torch.bfloat16)
+    bx = torch.randint(-2, 3, (n, 64, ho, wo), generator=g).to(torch.bfloat16)
+    coef = torch.stack([torch.randint(-2, 3, (64,), generator=g).float() / 2,
+                        torch.randint(-2, 3, (64,), generator=g).float() / 2,
+                        torch.randint(-2, 3, (64,), generator=g).float() / 2])
+    dy_apply = (coef[0].view(1, 64, 1, 1) * d.float() + coef[1].view(1, 64, 1, 1) * bx.float()
+                + coef[2].view(1, 64, 1, 1)).to(torch.bfloat16)
+    ref2 = torch.nn.grad.conv2d_weight(x.float(), (64, 4, 7, 7), dy_apply.float(), stride=2, padding=3)
+    dg = d.to(gpu).contiguous(memory_format=torch.channels_last)
+    bxg = bx.to(gpu).contiguous(memory_format=torch.channels_last)
+    cg = coef.to(gpu).contiguous()
+    _lib.check(lib.det_stemp_wgrad(torch.cuda.current_stream().cuda_stream, dg.data_ptr(), xg.data_ptr(),
+                                   out.data_ptr(), 0, m, h, w, ho, wo, ws.data_ptr(), 1.0, bxg.data_ptr(),
+                                   cg.data_ptr()), "stemp abn")
+    torch.testing.assert_close(conv.unpack_stem_grad(out, 4).cpu(), ref2, rtol=0, atol=0)
 
 
 def test_u8_normalize_pad4(gpu):

@@ -72,3 +72,65 @@ def test_maxpool_linked_projection_gradient(gpu, native_shortcut, monkeypatch):
         convops.ENABLED = old
     assert pool.LINKED["count"] == linked_before + 1, "shortcut gradient was not linked to the pool"
     torch.testing.assert_close(dut_in.grad.float().cpu(), ref_x, atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(4, 64, 56, 56), (3, 32, 17, 9)])
+def test_maxpool_bn_backward_epilogue(gpu, N, C, H, W):
+    """Stem BN + ReLU -> max-pool with the BN's backward partial sums written by the pool's gather
+    (det_pool.hip maxpool_bwd BNB): input, weight and bias gradients vs the fp32 CPU composite."""
+    from determined_1_amd.ops.norm import BatchNormAct2d
+
+    torch.manual_seed(1)
+    x = (torch.randn(N, C, H, W) * 2 + 0.3).to(torch.bfloat16).float()
+    dy = torch.randn(N, C, (H - 1) // 2 + 1, (W - 1) // 2 + 1).to(torch.bfloat16).float()
+    bn = BatchNormAct2d(C, relu=True, fused=True).to(gpu)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C) + 0.5)
+        bn.bias.copy_(torch.randn(C) * 0.2)
+    ref_in = x.clone().requires_grad_(True)
+    wr, br = bn.weight.detach().cpu().clone().requires_grad_(True), bn.bias.detach().cpu().clone().requires_grad_(True)
+    F.max_pool2d(F.relu(F.batch_norm(ref_in, None, None, wr, br, True)), 3, 2, 1).backward(dy)
+
+    dut_in = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    before = pool.BN_BWD_COUNTS["fused"]
+    out = pool.max_pool_3x3s2(bn(dut_in), bn_exclusive=True)
+    out.backward(dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    assert pool.BN_BWD_COUNTS["fused"] == before + 1, "the pool's BN-backward epilogue did not run"
+    torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(bn.weight.grad.cpu(), wr.grad, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(bn.bias.grad.cpu(), br.grad, atol=2e-2, rtol=2e-2)
+
+
+def test_stem_chain_defers_bn_apply_into_patch_wgrad(gpu):
+    """ResNet stem: conv -> BN + ReLU -> pool.  The pool's backward writes the BN partials, the BN
+    backward only finalizes, and the stem weight gradient stages the BN apply (stemp_wgrad ABN).
+    The weight gradient matches the same chain with both fusions off."""
+    from determined_1_amd.models import resnet
+    from determined_1_amd.ops import conv as convops
+
+    torch.manual_seed(2)
+    img = torch.randn(4, 3, 64, 64)
+
+    def run(fused):
+        torch.manual_seed(3)
+        m = resnet.resnet50(num_classes=10).to(gpu).to(memory_format=torch.channels_last).to(torch.bfloat16)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.float()
+        old = (pool.FUSE_BN_BWD, convops.DEFER_BN_APPLY)
+        pool.FUSE_BN_BWD = convops.DEFER_BN_APPLY = fused
+        try:
+            x = img.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            y = m.maxpool(m.bn1(m._stem(x)), bn_exclusive=True)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device=gpu).view_as(y)).sum().backward()
+        finally:
+            pool.FUSE_BN_BWD, convops.DEFER_BN_APPLY = old
+        return m.conv1.weight.grad.float().cpu(), m.bn1.weight.grad.cpu()
+
+    before = (pool.BN_BWD_COUNTS["fused"], convops.BN_APPLY_COUNTS["in_gemm"])
+    wf, gf = run(True)
+    assert pool.BN_BWD_COUNTS["fused"] == before[0] + 1
+    assert convops.BN_APPLY_COUNTS["in_gemm"] == before[1] + 1, "the stem wgrad did not stage the BN apply"
+    wu, gu = run(False)
+    torch.testing.assert_close(wf, wu, atol=2e-2 * float(wu.abs().max()), rtol=2e-2)
+    torch.testing.assert_close(gf, gu, atol=1e-3, rtol=1e-3)
