@@ -98,12 +98,24 @@ def _shortcut_linked(downsample: Optional[nn.Module], x: torch.Tensor) -> bool:
             and isinstance(downsample[0], nn.Conv2d) and isinstance(downsample[1], BatchNormAct2d))
 
 
+def _quiet(mod: nn.Module) -> bool:
+    """No forward hook anywhere on ``mod`` (or a global one) could observe an intermediate output."""
+    from torch.nn.modules import module as _m
+
+    if _m._global_forward_hooks or _m._global_forward_pre_hooks:
+        return False
+    return not any(m._forward_hooks or m._forward_pre_hooks for m in mod.modules())
+
+
 def _shortcut(downsample: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """Projection shortcut; its conv's input gradient is summed inside the producer's fused BN
-    backward (``linked_conv2d``) rather than added to conv1's input gradient by autograd."""
+    backward (``linked_conv2d``) rather than added to conv1's input gradient by autograd.  Inside
+    ResNet.forward (the block's residual BN is then its only reader) the shortcut BN's apply is
+    deferred into that residual apply (ops.conv DEFER_AFFINE_APPLY)."""
     if (FUSED_BN and isinstance(downsample, nn.Sequential) and len(downsample) == 2
             and isinstance(downsample[0], nn.Conv2d) and isinstance(downsample[1], BatchNormAct2d)):
-        return downsample[1](linked_conv2d(x, downsample[0]))
+        defer = getattr(_FWD, "depth", 0) > 0 and _quiet(downsample)
+        return downsample[1](linked_conv2d(x, downsample[0]), defer_affine=defer)
     return downsample(x)
 
 

@@ -91,7 +91,7 @@ _SIGNATURES = {
     "det_bn_bwd_scratch_elems": ([c_int], c_i64),
     "det_bn_bwd_finalize_partials": ([c_void_p, c_i64, c_int] + [c_void_p] * 5 + [c_int, c_i64] + [c_void_p] * 4, c_int),
     "det_bn_bwd_apply_coef": ([c_void_p, c_int, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p], c_int),
-    "det_bn_apply_res_mbits": ([c_void_p] * 3 + [c_void_p, c_i64, c_int] + [c_void_p] * 3, c_int),
+    "det_bn_apply_res_mbits": ([c_void_p] * 3 + [c_void_p, c_i64, c_int] + [c_void_p] * 5, c_int),
     "det_bn_ws_elems": ([c_i64, c_int], c_i64),
     "det_bn_fin_ws_elems": ([c_int], c_i64),
     # stream, dtype, x, res, y, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
@@ -124,10 +124,10 @@ _SIGNATURES = {
         c_int,
     ),
     # stream, dtype, x, res, y, M, C, rpb, nrb, pmean, pm2, gamma, beta, rmean, rvar, nbt, momentum, eps, relu,
-    # apply, save_mean, save_rstd, scale, shift, mbits, ws
+    # apply, save_mean, save_rstd, scale, shift, mbits, ws, res_scale, res_shift
     "det_bn_fwd_from_partials": (
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int, c_int] + [c_void_p] * 7
-        + [c_float, c_float, c_int, c_int] + [c_void_p] * 6,
+        + [c_float, c_float, c_int, c_int] + [c_void_p] * 8,
         c_int,
     ),
     # det_detect.hip: multi-level RoIAlign (NHWC) and device NMS
@@ -145,7 +145,8 @@ _SIGNATURES = {
     "det_conv_nt_rows_per_block": ([c_int], c_int),
     "det_conv_nt_set_pf": ([c_int], c_int),
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
-    "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 3, c_int),
+    # ... + res, aout, abits, res_scale, res_shift
+    "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 5, c_int),
     "det_conv_tn_ws_elems": ([c_i64, c_int, c_int], c_i64),
     # stream, A, B, C, M, N, K, x, mean, scale, shift, mbits, add, psum, psumx, mode
     "det_conv_nt_bnbwd": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 8 + [c_int, c_int] + [c_void_p] * 3

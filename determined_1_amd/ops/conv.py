@@ -54,7 +54,9 @@ def _affine_relu_ref(x: torch.Tensor, scale: Optional[torch.Tensor], shift: Opti
 def conv1x1_nt(a2d: torch.Tensor, b2d: torch.Tensor, m: Optional[int] = None, scale: Optional[torch.Tensor] = None,
                shift: Optional[torch.Tensor] = None, stats: bool = False, gather: Optional[Gather] = None,
                out: Optional[torch.Tensor] = None, res: Optional[torch.Tensor] = None, aout: Optional[torch.Tensor] = None,
-               abits: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
+               abits: Optional[torch.Tensor] = None, res_scale: Optional[torch.Tensor] = None,
+               res_shift: Optional[torch.Tensor] = None
+               ) -> Tuple[torch.Tensor, Optional[Tuple[torch.Tensor, torch.Tensor, int]]]:
     """``C = op(A) . B^T`` with ``op(A) = relu(A*scale+shift)`` when scale/shift are given.
 
     Returns ``(C [M, N] bf16, partials)`` where partials is ``(pmean, pm2, rows_per_block)`` of the
@@ -95,7 +97,7 @@ def conv1x1_nt(a2d: torch.Tensor, b2d: torch.Tensor, m: Optional[int] = None, sc
     g = gather or (0, 0, 0, 0)
     _lib.check(_lib.get_lib().det_conv_nt(_stream(a2d), a2d.data_ptr(), b2d.data_ptr(), c.data_ptr(), int(m), int(n),
                                           int(k), _ptr(scale), _ptr(shift), _ptr(pm), _ptr(pq), *[int(v) for v in g],
-                                          _ptr(res), _ptr(aout), _ptr(abits)),
+                                          _ptr(res), _ptr(aout), _ptr(abits), _ptr(res_scale), _ptr(res_shift)),
                "conv_nt")
     return c, parts
 
@@ -443,16 +445,42 @@ FWD_APPLY_COUNTS = {"deferred": 0, "in_gemm": 0, "materialized": 0}
 
 def materialize_fwd_apply(t: Optional[torch.Tensor]) -> None:
     """Write a deferred BN forward apply into ``t`` (no-op for untagged tensors)."""
-    pend = getattr(t, "_det_fwd_apply", None) if t is not None else None
+    if t is None:
+        return
+    aff = getattr(t, "_det_affine_apply", None)
+    if aff is not None:
+        t._det_affine_apply = None
+        materialize_affine_apply(t, aff)
+    pend = getattr(t, "_det_fwd_apply", None)
     if pend is None:
         return
     t._det_fwd_apply = None
-    x, res, scale, shift, mbits = pend
+    x, res, scale, shift, mbits, rs, rh = pend
     m = x.numel() // x.shape[1]
     _lib.check(_lib.get_lib().det_bn_apply_res_mbits(_stream(x), x.data_ptr(), res.data_ptr(), t.data_ptr(), int(m),
                                                      int(x.shape[1]), scale.data_ptr(), shift.data_ptr(),
-                                                     mbits.data_ptr()), "bn_apply_res_mbits")
+                                                     mbits.data_ptr(), _ptr(rs), _ptr(rh)), "bn_apply_res_mbits")
     FWD_APPLY_COUNTS["materialized"] += 1
+
+
+# Deferred affine BN apply (``DEFER_AFFINE_APPLY``): a training BN without ReLU or residual whose only
+# consumer is a residual BN(+ReLU) apply -- ResNet's projection-shortcut BN, read only by bn3 -- runs
+# only its finalize and returns its output unwritten, tagged ``_det_affine_apply = (x, scale, shift)``;
+# the consumer computes relu(bn3 + x * scale + shift) from x (det_norm.hip bn_apply_fwd RES 2, or
+# det_conv.hip AFWD when bn3's apply is itself deferred onto the next conv): the shortcut BN's apply
+# pass (read x, write y) and the consumer's read of y become one read of x.
+DEFER_AFFINE_APPLY = os.environ.get("DET_DEFER_AFFINE_APPLY", "1") != "0"
+AFFINE_APPLY_COUNTS = {"deferred": 0, "in_residual": 0, "materialized": 0}
+
+
+def materialize_affine_apply(t: torch.Tensor, aff) -> None:
+    """Write ``t = x * scale + shift`` (a deferred affine BN apply, see ``DEFER_AFFINE_APPLY``)."""
+    x, scale, shift = aff
+    m = x.numel() // x.shape[1]
+    _lib.check(_lib.get_lib().det_bn_apply(_stream(x), 1 if x.dtype == torch.bfloat16 else 0, x.data_ptr(), None,
+                                           t.data_ptr(), int(m), int(x.shape[1]), scale.data_ptr(), shift.data_ptr(), 0),
+               "bn_apply")
+    AFFINE_APPLY_COUNTS["materialized"] += 1
 
 
 class StridedGrad(NamedTuple):
@@ -622,9 +650,10 @@ class _Conv1x1(torch.autograd.Function):
         if fwd_apply is not None:
             # x is the unwritten output of the producing BN: stage relu(bx*scale + shift + res) as
             # the A operand and write it (and its mask bits) into x (DEFER_FWD_APPLY)
-            bx, res, scale, shift, mbits = fwd_apply
+            bx, res, scale, shift, mbits, rs, rh = fwd_apply
             y2, parts = conv1x1_nt(bx.permute(0, 2, 3, 1).reshape(-1, c), wb.contiguous(), scale=scale, shift=shift,
-                                   stats=stats, res=res.permute(0, 2, 3, 1).reshape(-1, c), aout=x2, abits=mbits)
+                                   stats=stats, res=res.permute(0, 2, 3, 1).reshape(-1, c), aout=x2, abits=mbits,
+                                   res_scale=rs, res_shift=rh)
             y = y2.view(n, h, w_, cout).permute(0, 3, 1, 2)
             FWD_APPLY_COUNTS["in_gemm"] += 1
         elif cfg is not None and x.data_ptr() % 16 == 0:

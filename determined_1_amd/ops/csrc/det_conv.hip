@@ -192,6 +192,10 @@ struct NtArgs {
   const float* acoef;  // [3][K]
   unsigned short* Aout;
   uint8_t* abits;  // AFWD: ReLU mask bits of Aout (1 per element)
+  // AFWD (nullable): A2 is itself a BatchNorm output whose apply was deferred (ResNet's projection
+  // shortcut BN): the residual is A2 * a2scale[k] + a2shift[k] (det_norm.hip bn_apply_fwd RES 2)
+  const float* a2scale;
+  const float* a2shift;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -291,8 +295,9 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
     unsigned char* base = smem + buf * BUF;
     // ABN: this thread's 8 channels of the apply coefficients, loaded once per K tile (before the
     // Aout stores, which the compiler could not move them across)
-    float ca[8], cb[8], cc[8];
-    if constexpr (AFWD) {  // scale, shift of this thread's 8 channels
+    float ca[8], cb[8], cc[8], ra_s[8], ra_h[8];
+    const bool a2aff = AFWD && a.a2scale != nullptr;
+    if constexpr (AFWD) {  // scale, shift of this thread's 8 channels (and of the residual's BN)
       const int k0 = kt * kBK + kc * 8;
 #pragma unroll
       for (int j = 0; j < 8; j += 4) {
@@ -300,6 +305,13 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
         const float4 H0 = *reinterpret_cast<const float4*>(a.shift + k0 + j);
         ca[j] = S0.x; ca[j + 1] = S0.y; ca[j + 2] = S0.z; ca[j + 3] = S0.w;
         cb[j] = H0.x; cb[j + 1] = H0.y; cb[j + 2] = H0.z; cb[j + 3] = H0.w;
+        float4 S2 = make_float4(1.f, 1.f, 1.f, 1.f), H2 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a2aff) {
+          S2 = *reinterpret_cast<const float4*>(a.a2scale + k0 + j);
+          H2 = *reinterpret_cast<const float4*>(a.a2shift + k0 + j);
+        }
+        ra_s[j] = S2.x; ra_s[j + 1] = S2.y; ra_s[j + 2] = S2.z; ra_s[j + 3] = S2.w;
+        ra_h[j] = H2.x; ra_h[j + 1] = H2.y; ra_h[j + 2] = H2.z; ra_h[j + 3] = H2.w;
       }
     }
     if constexpr (ABN) {
@@ -330,10 +342,12 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       }
       if constexpr (AFWD) {
         // exactly det_norm.hip bn_apply_fwd<RELU, RES>: z = fma(x, scale, shift) + res, relu, mask bits
+        // (RES 2: res = fma(r, rscale, rshift) of the deferred residual BN)
         unsigned bits = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float z = __fmaf_rn(bf2f(ra[i][j]), ca[j], cb[j]) + bf2f(ra2[i][j]);
+          const float r2 = bf2f(ra2[i][j]);
+          const float z = __fmaf_rn(bf2f(ra[i][j]), ca[j], cb[j]) + (a2aff ? __fmaf_rn(r2, ra_s[j], ra_h[j]) : r2);
           v[j] = f2bf(fmaxf(z, 0.f));
           bits |= (z > 0.f ? 1u : 0u) << j;
         }
@@ -879,10 +893,12 @@ int det_conv_nt_rows_per_block(int N) { return 128; }
 // BN statistics partials [ceil(M/rpb), N].  Ho..Wi > 0 selects the 1x1 stride-2 row gather.
 // res / aout / abits (all or none; with scale, shift): AFWD -- op(A) = relu(A*scale + shift + res),
 // written to aout with its mask bits to abits by the first N tile (the consuming conv applies the
-// producing BatchNorm; see the AFWD note at gemm_nt_kernel).
+// producing BatchNorm; see the AFWD note at gemm_nt_kernel).  res_scale / res_shift (nullable): the
+// residual is res * res_scale + res_shift (a deferred projection-shortcut BN apply).
 int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, int N, int K,
                 const float* scale, const float* shift, float* pmean, float* pm2, int Ho, int Wo, int Hi, int Wi,
-                const void* res, void* aout, void* abits) {
+                const void* res, void* aout, void* abits, const float* res_scale, const float* res_shift) {
+  if ((res_scale == nullptr) != (res_shift == nullptr) || (res_scale && !res)) return -2;
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
   if ((scale == nullptr) != (shift == nullptr) || (pmean == nullptr) != (pm2 == nullptr)) return -2;
   const bool stride2 = Ho > 0;
@@ -892,7 +908,7 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
   NtArgs a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C),
            M, N, K, scale, shift, pmean, pm2, Gather{Ho, Wo, Hi, Wi}, BnBwdEpi{},
            static_cast<const unsigned short*>(res), nullptr, static_cast<unsigned short*>(aout),
-           static_cast<uint8_t*>(abits)};
+           static_cast<uint8_t*>(abits), res_scale, res_shift};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const bool pro = scale != nullptr && res == nullptr, stats = pmean != nullptr;
   if (K == kBK) {

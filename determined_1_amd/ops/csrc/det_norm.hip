@@ -445,13 +445,16 @@ void launch_stats_finalize(hipStream_t st, const float* pmean, const float* pm2,
 
 // ---------------------------------------------------------------------------------------------
 // Elementwise apply: y = act(x*scale + shift [+ res]); grid-stride over 8-element vectors, 4 in
-// flight per thread.
+// flight per thread.  RES 2: the residual is itself a BatchNorm output whose apply was deferred
+// (ResNet's projection-shortcut BN): res = r * rscale + rshift, computed here from its input r --
+// that BN's own apply pass (read r, write res) and this pass's read of res become one read of r.
 // ---------------------------------------------------------------------------------------------
-template <typename T, bool RELU, bool RES>
+template <typename T, bool RELU, int RES>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
              const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int C,
-             int64_t* __restrict__ bump, uint8_t* __restrict__ mbits) {
+             int64_t* __restrict__ bump, uint8_t* __restrict__ mbits, const float* __restrict__ rscale = nullptr,
+             const float* __restrict__ rshift = nullptr) {
   // num_batches_tracked += 1 rides on this launch (stream-ordered after the finalize that read it)
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
   const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
@@ -471,14 +474,19 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
       if (v < nvec) {
         // vector index -> first channel; 32-bit modulo (nvec < 2^32 checked on the host)
         const int c0 = static_cast<int>(static_cast<uint32_t>(v) % static_cast<uint32_t>(C >> 3)) << 3;
-        float sc[8], sh[8], o[8];
+        float sc[8], sh[8], o[8], rsc[8], rsh[8];
         load8f(scale + c0, sc);
         load8f(shift + c0, sh);
+        if (RES == 2) {
+          load8f(rscale + c0, rsc);
+          load8f(rshift + c0, rsh);
+        }
         unsigned bits = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float z = __fmaf_rn(xv[u][j], sc[j], sh[j]);
-          if (RES) z += rv[u][j];
+          if (RES == 1) z += rv[u][j];
+          if (RES == 2) z += __fmaf_rn(rv[u][j], rsc[j], rsh[j]);
           o[j] = RELU ? fmaxf(z, 0.f) : z;
           bits |= (z > 0.f ? 1u : 0u) << j;
         }
@@ -925,8 +933,9 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
                              const float* beta, float* running_mean, float* running_var,
                              int64_t* num_batches_tracked, float momentum, float eps, int relu, int apply,
                              float* save_mean, float* save_rstd, float* scale, float* shift, uint8_t* mbits,
-                             float* ws) {
+                             float* ws, const float* res_scale, const float* res_shift) {
   if (C % 8 != 0 || M <= 0 || rpb <= 0 || nrb != static_cast<int>((M + rpb - 1) / rpb)) return -1;
+  if ((res_scale == nullptr) != (res_shift == nullptr) || (res_scale && (!res || dtype != 1 || !relu))) return -2;
   if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   Geom g = make_geom(M, C);
@@ -942,6 +951,12 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
   }
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
+  if (res_scale) {  // the residual is a deferred BN apply of its input res (RES 2)
+    hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2>), dim3(grid2), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                       static_cast<unsigned short*>(y), scale, shift, nvec, C, bump, mbits, res_scale, res_shift);
+    return static_cast<int>(hipGetLastError());
+  }
 #define DET_BN_FWD(T, RL, RS)                                                                          \
   hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                    \
                      static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, shift, \
@@ -962,15 +977,23 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
 
 // Training apply with precomputed scale/shift: y = relu(x*scale + shift + res) and its mask bits
 // (the materialisation of a BN apply deferred onto a consuming conv that could not take it).
+// res_scale / res_shift (nullable): the residual is a deferred BN apply of res (bn_apply_fwd RES 2).
 int det_bn_apply_res_mbits(void* stream, const void* x, const void* res, void* y, int64_t M, int C, const float* scale,
-                           const float* shift, uint8_t* mbits) {
+                           const float* shift, uint8_t* mbits, const float* res_scale, const float* res_shift) {
   if (C % 8 != 0 || M <= 0 || !res || !mbits) return -1;
+  if ((res_scale == nullptr) != (res_shift == nullptr)) return -2;
   if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nvec = M * C / 8;
-  hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, true>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
-                     static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
-                     static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits);
+  if (res_scale)
+    hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                       static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits,
+                       res_scale, res_shift);
+  else
+    hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 1>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                       static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -75,7 +75,7 @@ class _BNActTrain(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, nbt, momentum, eps, relu, link=None,
-                defer=False):
+                defer=False, res_affine=None, defer_affine=False):
         M, C = _rows(x)
         lib = _lib.get_lib()
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
@@ -92,16 +92,27 @@ class _BNActTrain(torch.autograd.Function):
                          dtype=torch.float32, device=x.device)
         defer = bool(defer and parts is not None and relu and residual is not None and mbits is not None
                      and x.dtype == torch.bfloat16 and fmt == torch.channels_last)
+        # res_affine = (r, scale, shift): the residual is a BN output whose apply was deferred (the
+        # projection shortcut's, below); this apply computes it from r (det_norm.hip RES 2)
+        if res_affine is not None and not (parts is not None and relu and x.dtype == torch.bfloat16):
+            _conv.materialize_affine_apply(residual, res_affine)
+            res_affine = None
+        res_src, rs, rh = (residual, None, None) if res_affine is None else res_affine
+        # defer_affine: a BN without ReLU or residual whose only consumer is a residual BN apply that
+        # takes res_affine (ResNet's projection-shortcut BN): finalize only, the output stays unwritten
+        defer_affine = bool(defer_affine and parts is not None and not relu and residual is None
+                            and x.dtype == torch.bfloat16 and fmt == torch.channels_last)
         if parts is not None:
             pm, pq, rpb = parts
             _lib.check(
                 lib.det_bn_fwd_from_partials(
-                    _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(residual), y.data_ptr(), M, C, int(rpb),
+                    _stream(x), _DT[x.dtype], x.data_ptr(), _ptr(res_src), y.data_ptr(), M, C, int(rpb),
                     int(pm.shape[0]), pm.data_ptr(), pq.data_ptr(),
                     _ptr(weight), _ptr(bias), _ptr(running_mean), _ptr(running_var), _ptr(nbt),
-                    float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)), 0 if defer else 1,
+                    float(-1.0 if momentum is None else momentum), float(eps), int(bool(relu)),
+                    0 if (defer or defer_affine) else 1,
                     stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), _ptr(mbits),
-                    ws.data_ptr(),
+                    ws.data_ptr(), _ptr(rs), _ptr(rh),
                 ),
                 "bn_fwd_from_partials",
             )
@@ -129,8 +140,13 @@ class _BNActTrain(torch.autograd.Function):
         if defer:
             # y stays unwritten: the consuming conv stages (and writes) the apply (ops/conv.py
             # DEFER_FWD_APPLY); bn_act tags the returned tensor
-            _DEFERRED["last"] = (y.data_ptr(), (x, residual, stats[2], stats[3], mbits))
+            _DEFERRED["last"] = (y.data_ptr(), (x, res_src, stats[2], stats[3], mbits, rs, rh))
             _conv.FWD_APPLY_COUNTS["deferred"] += 1
+        elif defer_affine:
+            _DEFERRED["last"] = (y.data_ptr(), ("affine", x, stats[2], stats[3]))
+            _conv.AFFINE_APPLY_COUNTS["deferred"] += 1
+        if res_affine is not None:
+            _conv.AFFINE_APPLY_COUNTS["in_residual"] += 1
         return y
 
     @staticmethod
@@ -206,7 +222,7 @@ class _BNActTrain(torch.autograd.Function):
             dres = None
         dw = dgb[0] if dgb is not None and ctx.needs_input_grad[2] else None
         db = dgb[1] if dgb is not None and ctx.needs_input_grad[3] else None
-        return dx, dres, dw, db, None, None, None, None, None, None, None, None
+        return dx, dres, dw, db, None, None, None, None, None, None, None, None, None, None
 
 
 class _LinkedConv(torch.autograd.Function):
@@ -322,7 +338,8 @@ _DEFERRED = {"last": None}  # (data_ptr of the unwritten output, apply arguments
 
 
 def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optional[torch.Tensor] = None,
-           relu: bool = True, shortcut_link: bool = False, defer_apply: bool = False) -> torch.Tensor:
+           relu: bool = True, shortcut_link: bool = False, defer_apply: bool = False,
+           defer_affine: bool = False) -> torch.Tensor:
     """``act(bn(x) + residual)`` with the module's parameters/buffers and train/eval semantics.
 
     ``shortcut_link``: the caller guarantees ``residual`` is an identity shortcut, i.e. also the
@@ -333,7 +350,16 @@ def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optio
     rv = bn.running_var if (bn.track_running_stats and bn.training) else None
     res_ok = residual is None or (residual.shape == x.shape and residual.device == x.device)
     _conv.materialize_fwd_apply(x)  # inputs whose producing BN apply was deferred but never staged
-    _conv.materialize_fwd_apply(residual)
+    # a residual whose BN apply was deferred (defer_affine) is computed inside this apply when the
+    # fused training path runs; anything else materialises it
+    aff = getattr(residual, "_det_affine_apply", None) if residual is not None else None
+    res_affine = None
+    if (aff is not None and _nhwc_ok(x) and res_ok and use_batch_stats and relu and not shortcut_link
+            and x.dtype == torch.bfloat16 and residual.dtype == x.dtype):
+        residual._det_affine_apply = None
+        res_affine = aff
+    else:
+        _conv.materialize_fwd_apply(residual)
     if _nhwc_ok(x) and res_ok:
         if use_batch_stats:
             nbt = bn.num_batches_tracked if (bn.training and bn.track_running_stats) else None
@@ -345,13 +371,17 @@ def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optio
                 link = residual.grad_fn
                 residual = residual.detach()
             defer = bool(defer_apply and _conv.DEFER_FWD_APPLY and torch.is_grad_enabled())
+            daff = bool(defer_affine and _conv.DEFER_AFFINE_APPLY and torch.is_grad_enabled() and residual is None)
             out = _BNActTrain.apply(x, residual, bn.weight, bn.bias, rm, rv, nbt, bn.momentum, bn.eps, relu, link,
-                                    defer)
+                                    defer, res_affine, daff)
             last, _DEFERRED["last"] = _DEFERRED["last"], None
             if last is not None:
                 if last[0] != out.data_ptr():
                     raise RuntimeError("deferred BN apply: output buffer changed across autograd")
-                out._det_fwd_apply = last[1]
+                if last[1][0] == "affine":
+                    out._det_affine_apply = last[1][1:]
+                else:
+                    out._det_fwd_apply = last[1]
             return out
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or (residual is not None and residual.requires_grad)
@@ -399,9 +429,10 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.fused = fused  # False: stock torch/MIOpen BN + separate add/ReLU (A/B comparisons)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,  # type: ignore[override]
-                shortcut_link: bool = False, defer_apply: bool = False) -> torch.Tensor:
+                shortcut_link: bool = False, defer_apply: bool = False, defer_affine: bool = False) -> torch.Tensor:
         if self.fused:
-            return bn_act(x, self, residual, self.relu, shortcut_link, defer_apply)
+            return bn_act(x, self, residual, self.relu, shortcut_link, defer_apply, defer_affine)
+        _conv.materialize_fwd_apply(residual)
         y = super().forward(x)
         if residual is not None:
             y = y + residual

@@ -377,3 +377,40 @@ def test_deferred_forward_apply_never_reaches_hooks_or_user_code(gpu):
         assert conv.FWD_APPLY_COUNTS["deferred"] == before["deferred"]
     finally:
         conv.DEFER_FWD_APPLY = True
+
+
+def test_projection_shortcut_bn_apply_deferred_into_residual(gpu):
+    """The projection-shortcut BN (no ReLU) of each layer's first block finalizes only; bn3's apply
+    computes relu(bn3(x) + xs * scale + shift) from the shortcut conv's output xs (det_norm.hip RES 2,
+    or det_conv.hip AFWD when bn3's apply is itself staged by the next conv1).  Outputs and gradients
+    match the materialised path (which rounds the shortcut BN's output to bf16 once more)."""
+    from determined_1_amd.models import resnet
+
+    torch.manual_seed(0)
+    model = resnet.resnet50(num_classes=10, zero_init_residual=False).to(gpu).to(memory_format=torch.channels_last)
+    for mod in model.modules():
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
+            mod.to(torch.bfloat16)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(8, 4, 64, 64, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y_lab = torch.randint(0, 10, (8,), generator=g).to(gpu)
+
+    def run(defer):
+        conv.DEFER_AFFINE_APPLY = defer
+        model.zero_grad(set_to_none=True)
+        before = dict(conv.AFFINE_APPLY_COUNTS)
+        out = model(x)
+        torch.nn.functional.cross_entropy(out.float(), y_lab).backward()
+        d = {k: conv.AFFINE_APPLY_COUNTS[k] - before[k] for k in before}
+        return out.float(), {k: p.grad.float().clone() for k, p in model.named_parameters()}, d
+
+    try:
+        o_m, g_m, c_m = run(False)
+        o_d, g_d, c_d = run(True)
+    finally:
+        conv.DEFER_AFFINE_APPLY = True
+    assert c_m == {"deferred": 0, "in_residual": 0, "materialized": 0}, c_m
+    assert c_d == {"deferred": 4, "in_residual": 4, "materialized": 0}, c_d
+    torch.testing.assert_close(o_d, o_m, rtol=3e-2, atol=3e-2 * float(o_m.abs().max()))
+    rel = {k: float((g_d[k] - g_m[k]).norm() / (g_m[k].norm() + 1e-12)) for k in g_m}
+    assert max(rel.values()) < 5e-2, sorted(rel.items(), key=lambda kv: -kv[1])[:5]
