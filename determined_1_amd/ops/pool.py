@@ -41,7 +41,7 @@ def _ok(x: torch.Tensor) -> bool:
 
 class _MaxPool3s2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bn_exclusive=False):
+    def forward(ctx, x, bn_producer=None):
         N, C, H, W = x.shape
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
@@ -52,7 +52,7 @@ class _MaxPool3s2(torch.autograd.Function):
         ctx.save_for_backward(idx)
         ctx.shape = (N, C, H, W)
         ctx.extra_dy = None  # set by a linked shortcut consumer (ops/norm.py linked_conv2d)
-        ctx.bn_producer = _bn_producer(x) if (bn_exclusive and torch.is_grad_enabled()) else None
+        ctx.bn_producer = bn_producer
         return y
 
     @staticmethod
@@ -103,7 +103,9 @@ def max_pool_3x3s2(x: torch.Tensor, bn_exclusive: bool = False) -> torch.Tensor:
     ``x``, the output of a fused BatchNorm+ReLU, whose backward partials can then come from the
     pool's backward (``FUSE_BN_BWD``)."""
     if _ok(x):
-        return _MaxPool3s2.apply(x, bn_exclusive)
+        # (decided here: autograd runs Function.forward with grad mode off)
+        prod = _bn_producer(x) if (bn_exclusive and torch.is_grad_enabled()) else None
+        return _MaxPool3s2.apply(x, prod)
     if x.device.type == "cuda":
         FALLBACKS["count"] += 1
     return F.max_pool2d(x, 3, 2, 1)

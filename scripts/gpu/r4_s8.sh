@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 session 8: stem BN backward fused into the max-pool gather (partials) + the stem weight
-# gradient (deferred apply); faster pool indexing.  Tests, bench A/B (DET_POOL_BN_BWD), bn-prologue A/B,
+# gradient (deferred apply); faster pool indexing; projection-shortcut BN apply deferred into bn3's.  Tests, bench A/B (DET_POOL_BN_BWD), bn-prologue A/B,
 # steady profile, then the DP equivalence tests (O0 now with deterministic MIOpen + noise floor).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -9,9 +9,9 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_pool_gpu.py tests/test_conv_gpu.py tests/test_bn_bwd_fusion_gpu.py tests/test_norm_gpu.py > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-for cfg in "on:1:" "off:0:" "on:1:" "off:0:" "pro:1:--bn-prologue" "pro:1:--bn-prologue"; do
-  name=${cfg%%:*}; rest=${cfg#*:}; v=${rest%%:*}; args=${rest#*:}
-  DET_POOL_BN_BWD=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 $args > $O/bench_$name.json 2> $O/bench_$name.err || { tail -30 $O/bench_$name.err; exit 1; }
+for cfg in "on::" "off:DET_POOL_BN_BWD=0 DET_DEFER_AFFINE_APPLY=0:" "pool:DET_DEFER_AFFINE_APPLY=0:" "on::" "off:DET_POOL_BN_BWD=0 DET_DEFER_AFFINE_APPLY=0:" "pool:DET_DEFER_AFFINE_APPLY=0:" "pro::--bn-prologue" "pro::--bn-prologue"; do
+  name=${cfg%%:*}; rest=${cfg#*:}; envs=${rest%%:*}; args=${rest#*:}
+  env $envs timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 $args > $O/bench_$name.json 2> $O/bench_$name.err || { tail -30 $O/bench_$name.err; exit 1; }
   echo "$name $(python3 -c "import json;d=json.load(open('$O/bench_$name.json'));print(d['value'],d['ms_per_step'])")"
 done
 timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 8 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
