@@ -75,9 +75,12 @@ def test_maxpool_linked_projection_gradient(gpu, native_shortcut, monkeypatch):
 
 
 @pytest.mark.parametrize("N,C,H,W", [(4, 64, 56, 56), (3, 32, 17, 9)])
-def test_maxpool_bn_backward_epilogue(gpu, N, C, H, W):
+def test_maxpool_bn_backward_epilogue(gpu, N, C, H, W, monkeypatch):
     """Stem BN + ReLU -> max-pool with the BN's backward partial sums written by the pool's gather
-    (det_pool.hip maxpool_bwd BNB): input, weight and bias gradients vs the fp32 CPU composite."""
+    (det_pool.hip maxpool_bwd BNB) vs the same GPU chain with the fusion off (the plain gather and
+    the BN's own partial pass): the same forward, so the same argmax, and gradients equal up to the
+    summation order of the partials.  Also near the fp32 CPU composite, where bf16 rounding of the
+    pooled values moves an argmax now and then (a handful of elements)."""
     from determined_1_amd.ops.norm import BatchNormAct2d
 
     torch.manual_seed(1)
@@ -87,18 +90,30 @@ def test_maxpool_bn_backward_epilogue(gpu, N, C, H, W):
     with torch.no_grad():
         bn.weight.copy_(torch.rand(C) + 0.5)
         bn.bias.copy_(torch.randn(C) * 0.2)
+
+    def run(fused):
+        monkeypatch.setattr(pool, "FUSE_BN_BWD", fused)
+        bn.zero_grad(set_to_none=True)
+        xin = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+        before = pool.BN_BWD_COUNTS["fused"]
+        out = pool.max_pool_3x3s2(bn(xin), bn_exclusive=True)
+        out.backward(dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        assert pool.BN_BWD_COUNTS["fused"] == before + int(fused)
+        return xin.grad.float().cpu(), bn.weight.grad.cpu(), bn.bias.grad.cpu()
+
+    dx_f, dw_f, db_f = run(True)
+    dx_u, dw_u, db_u = run(False)
+    torch.testing.assert_close(dw_f, dw_u, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(db_f, db_u, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(dx_f, dx_u, atol=2e-2, rtol=2e-2)
+
     ref_in = x.clone().requires_grad_(True)
     wr, br = bn.weight.detach().cpu().clone().requires_grad_(True), bn.bias.detach().cpu().clone().requires_grad_(True)
     F.max_pool2d(F.relu(F.batch_norm(ref_in, None, None, wr, br, True)), 3, 2, 1).backward(dy)
-
-    dut_in = x.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
-    before = pool.BN_BWD_COUNTS["fused"]
-    out = pool.max_pool_3x3s2(bn(dut_in), bn_exclusive=True)
-    out.backward(dy.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last))
-    assert pool.BN_BWD_COUNTS["fused"] == before + 1, "the pool's BN-backward epilogue did not run"
-    torch.testing.assert_close(dut_in.grad.float().cpu(), ref_in.grad, atol=5e-2, rtol=5e-2)
-    torch.testing.assert_close(bn.weight.grad.cpu(), wr.grad, atol=2e-2, rtol=2e-2)
-    torch.testing.assert_close(bn.bias.grad.cpu(), br.grad, atol=2e-2, rtol=2e-2)
+    bad = ~torch.isclose(dx_f, ref_in.grad, atol=5e-2, rtol=5e-2)
+    assert int(bad.sum()) <= max(8, dx_f.numel() // 2000), int(bad.sum())
+    torch.testing.assert_close(dw_f, wr.grad, atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(db_f, br.grad, atol=5e-2, rtol=5e-2)
 
 
 def test_stem_chain_defers_bn_apply_into_patch_wgrad(gpu):
