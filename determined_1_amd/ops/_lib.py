@@ -120,9 +120,10 @@ _SIGNATURES = {
     # stream, dtype, dy, dy2, x, mbits, M, C, mask_mode, gamma, mean, rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws
     "det_bn_bwd": (
-        [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int] + [c_void_p] * 10,
+        [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_int] + [c_void_p] * 10 + [c_int],
         c_int,
     ),
+    "det_bn_bwd_coef_offset": ([c_i64, c_int], c_i64),
     # stream, dtype, x, res, y, M, C, rpb, nrb, pmean, pm2, gamma, beta, rmean, rvar, nbt, momentum, eps, relu,
     # apply, save_mean, save_rstd, scale, shift, mbits, ws, res_scale, res_shift
     "det_bn_fwd_from_partials": (

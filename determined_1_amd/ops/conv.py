@@ -781,7 +781,7 @@ class _BNReluConv1x1(torch.autograd.Function):
         _lib.check(lib.det_bn_bwd(
             _stream(x), 1, dz2.data_ptr(), None, x.data_ptr(), None, m, c, 1, _ptr(gamma),
             stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), dx.data_ptr(), None,
-            None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(), ws.data_ptr()),
+            None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(), ws.data_ptr(), 1),
             "bn_bwd")
         dg = dgb[0] if dgb is not None and ctx.needs_input_grad[1] else None
         db = dgb[1] if dgb is not None and ctx.needs_input_grad[2] else None
@@ -1175,6 +1175,10 @@ class _Shortcut1x1(torch.autograd.Function):
         ctx.link = link
         if link is not None:
             link.expects_extra = True  # a fused dgrad into the producer must wait for this gradient
+        # the shortcut BN may defer its backward apply onto this node (take_pending_apply): the input
+        # gradient GEMM stages it (ABN) and writes it for the weight gradient
+        ctx.accepts_bn_apply = DGRAD_BT and is_gpu(x)
+        ctx.pending_bn_apply = None
         return y
 
     @staticmethod
@@ -1184,12 +1188,22 @@ class _Shortcut1x1(torch.autograd.Function):
         cout, ho, wo = dy.shape[1], dy.shape[2], dy.shape[3]
         st = ctx.stride
         g = (ho, wo, h, w_) if st == 2 else None
-        dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
         link, ctx.link = ctx.link, None
+        pend = take_pending_apply(ctx, dy)
+        if pend is not None and not ((ctx.needs_input_grad[0] or link is not None) and dy.dtype == torch.bfloat16
+                                     and dy.is_contiguous(memory_format=torch.channels_last)):
+            materialize_pending_apply(dy, pend)
+            pend = None
+        dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
         dx = dw = None
         if ctx.needs_input_grad[0] or link is not None:
             w2 = weight.reshape(cout, c).contiguous()
-            dxs = dgrad_1x1(dy2, w2).view(n, ho, wo, c).permute(0, 3, 1, 2)  # on the output grid
+            abn = None
+            if pend is not None:  # dY = the deferred BN apply, staged by the dgrad and written into dy2
+                d, bx, coef = pend
+                abn = (d.permute(0, 2, 3, 1).reshape(-1, cout), bx, coef, dy2)
+                BN_APPLY_COUNTS["in_gemm"] += 1
+            dxs = dgrad_1x1(dy2, w2, abn).view(n, ho, wo, c).permute(0, 3, 1, 2)  # on the output grid
             extra = StridedGrad(dxs, g) if st == 2 else dxs
             if link is not None:
                 from determined_1_amd.ops.norm import hand_linked_grad

@@ -1097,10 +1097,13 @@ int det_bn_bwd_apply_coef(void* stream, int dtype, const void* d, const void* x,
   return static_cast<int>(hipGetLastError());
 }
 
+// Offset (floats) of the [3][C] apply coefficients inside det_bn_bwd's workspace.
+int64_t det_bn_bwd_coef_offset(int64_t M, int C) { return 2 * static_cast<int64_t>(make_geom(M, C).nrb) * C; }
+
 int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const void* x, const void* mbits, int64_t M, int C,
                int mask_mode, const float* gamma, const float* save_mean, const float* save_rstd,
                const float* scale, const float* shift, void* dx, void* dres, float* dgamma, float* dbeta,
-               float* ws) {
+               float* ws, int apply) {
   if (C % 8 != 0 || M <= 0) return -1;
   if (M * (C / 8) >= (static_cast<int64_t>(1) << 32)) return -3;  // 32-bit vector indexing in apply
   if (mask_mode == 2 && !mbits) return -2;
@@ -1125,6 +1128,9 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const v
 #undef DET_BN_P
   BwdFin bf{gamma, save_rstd, save_mean, dgamma, dbeta, coef};
   launch_bwd_finalize(st, psum, psumx, g, bf, coef + 3 * static_cast<int64_t>(C));
+  // apply = 0: stop at the coefficients (ws + det_bn_bwd_coef_offset): a consuming GEMM stages the
+  // apply dx = coef[0] dy + coef[1] x + coef[2] itself (mask mode 0, no dy2 / dres)
+  if (!apply) return (mask_mode == 0 && !dy2 && !dres) ? static_cast<int>(hipGetLastError()) : -2;
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 2);
 #define DET_BN_B(T, MK, DR)                                                                            \

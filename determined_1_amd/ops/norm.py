@@ -201,16 +201,28 @@ class _BNActTrain(torch.autograd.Function):
         elif fused is None:
             dres = torch.empty_like(x, memory_format=ctx.fmt) if want_res else None
             ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=x.device)
+            # an affine BN (no ReLU, no residual: ResNet's projection-shortcut BN) whose input came
+            # from a native conv that stages the apply in its input-gradient GEMM: partials and
+            # finalize here, the apply there (ops/conv.py take_pending_apply)
+            conv_node = x.grad_fn
+            defer = (ctx.mask_mode == 0 and dy2 is None and dres is None and _conv.DEFER_BN_APPLY
+                     and getattr(conv_node, "accepts_bn_apply", False)
+                     and getattr(conv_node, "pending_bn_apply", "x") is None and x.dtype == torch.bfloat16
+                     and ctx.fmt == torch.channels_last and dy.is_contiguous(memory_format=torch.channels_last))
             _lib.check(
                 lib.det_bn_bwd(
                     _stream(x), _DT[x.dtype], dy.data_ptr(), _ptr(dy2), x.data_ptr(), _ptr(mbits), M, C, ctx.mask_mode,
                     _ptr(weight), stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(),
                     dx.data_ptr(), _ptr(dres),
                     None if dgb is None else dgb[0].data_ptr(), None if dgb is None else dgb[1].data_ptr(),
-                    ws.data_ptr(),
+                    ws.data_ptr(), 0 if defer else 1,
                 ),
                 "bn_bwd",
             )
+            if defer:
+                off = int(lib.det_bn_bwd_coef_offset(M, C))
+                conv_node.pending_bn_apply = (dx, dy, x, ws[off:off + 3 * C])
+                _conv.BN_APPLY_COUNTS["deferred"] += 1
         _dbg("bwd", x)
         if ctx.has_res and dres is None and ctx.needs_input_grad[1]:
             raise RuntimeError("residual grad requested but not produced")

@@ -122,6 +122,8 @@ def main() -> None:
         m, c, mode, n = a[6], a[7], a[8], a[6] * a[7] * el(a[1])
         # partial pass (dy [+dy2], x [+mbits]) then apply pass (the same again, writes dx [+dres])
         rd = n + (n if a[3] else 0) + n + (m * c // 8 if mode == 2 and a[5] else 0)
+        if len(a) > 19 and not a[19]:  # apply deferred into the consuming GEMM: the partial pass only
+            return (f"bn bwd partials (apply deferred) mask{mode}", rd, 0, 0)
         return (f"bn bwd (partials+apply) mask{mode}", 2 * rd, n + (n if a[15] else 0), 0)
 
     def bn_bwd_parts(a):

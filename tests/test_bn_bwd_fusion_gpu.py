@@ -414,3 +414,38 @@ def test_projection_shortcut_bn_apply_deferred_into_residual(gpu):
     torch.testing.assert_close(o_d, o_m, rtol=3e-2, atol=3e-2 * float(o_m.abs().max()))
     rel = {k: float((g_d[k] - g_m[k]).norm() / (g_m[k].norm() + 1e-12)) for k in g_m}
     assert max(rel.values()) < 5e-2, sorted(rel.items(), key=lambda kv: -kv[1])[:5]
+
+
+def test_projection_shortcut_bn_backward_apply_in_dgrad(gpu):
+    """The projection-shortcut BN's backward (no ReLU) stops at its coefficients; the shortcut conv's
+    input-gradient GEMM stages dY = coef . (d, x) (ABN) and writes it for the weight gradient.
+    ResNet-50 gradients match the materialised apply."""
+    from determined_1_amd.models import resnet
+
+    torch.manual_seed(0)
+    model = resnet.resnet50(num_classes=10, zero_init_residual=False).to(gpu).to(memory_format=torch.channels_last)
+    for mod in model.modules():
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
+            mod.to(torch.bfloat16)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x = torch.randn(8, 4, 64, 64, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y_lab = torch.randint(0, 10, (8,), generator=g).to(gpu)
+
+    def run(defer):
+        conv.DEFER_BN_APPLY = defer
+        model.zero_grad(set_to_none=True)
+        before = dict(conv.BN_APPLY_COUNTS)
+        torch.nn.functional.cross_entropy(model(x).float(), y_lab).backward()
+        return {k: p.grad.float().clone() for k, p in model.named_parameters()}, \
+            {k: conv.BN_APPLY_COUNTS[k] - before[k] for k in before}
+
+    try:
+        g_m, c_m = run(False)
+        g_d, c_d = run(True)
+    finally:
+        conv.DEFER_BN_APPLY = True
+    assert c_m["in_gemm"] == 0 and c_d["in_gemm"] == c_d["deferred"] and c_d["materialized"] == 0, c_d
+    # bn3 of every block (16), the stem BN (1) and the four projection-shortcut BNs
+    assert c_d["deferred"] >= 4 + 1, c_d
+    rel = {k: float((g_d[k] - g_m[k]).norm() / (g_m[k].norm() + 1e-12)) for k in g_m}
+    assert max(rel.values()) < 5e-2, sorted(rel.items(), key=lambda kv: -kv[1])[:5]
