@@ -269,7 +269,7 @@ def test_conv_nt_with_bn_apply_prologue(gpu, m, k, n):
     bits_ref = torch.empty(m * k // 8, dtype=torch.uint8, device=gpu)
     _lib.check(lib.det_bn_apply_res_mbits(torch.cuda.current_stream().cuda_stream, x.data_ptr(), res.data_ptr(),
                                           z_ref.data_ptr(), m, k, scale.data_ptr(), shift.data_ptr(),
-                                          bits_ref.data_ptr()), "apply_res_mbits")
+                                          bits_ref.data_ptr(), None, None), "apply_res_mbits")
     z = torch.full((m, k), float("nan"), dtype=torch.bfloat16, device=gpu)
     bits = torch.zeros(m * k // 8, dtype=torch.uint8, device=gpu)
     y, (pm, pq, rpb) = conv.conv1x1_nt(x, w, scale=scale, shift=shift, stats=True, res=res, aout=z, abits=bits)
