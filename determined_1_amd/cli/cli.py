@@ -617,10 +617,18 @@ def cmd_deploy_local(args: argparse.Namespace) -> None:
                      scheduler=args.scheduler)
     c.up()
     print(f"cluster up: DET_MASTER={c.address}  (Ctrl-C to stop)")
+    grpc_server = None
+    if args.grpc_port is not None:  # the gRPC wire protocol of the master API (determined_1_amd/rpc)
+        from determined_1_amd.rpc.server import serve
+
+        grpc_server, gport = serve(c.address, args.grpc_port)
+        print(f"gRPC determined.api.v1.Determined on 127.0.0.1:{gport}")
     try:
         while True:
             time.sleep(3600)
     except KeyboardInterrupt:
+        if grpc_server is not None:
+            grpc_server.stop(0)
         c.down()
 
 
@@ -883,6 +891,8 @@ def build_parser() -> argparse.ArgumentParser:
     lo.add_argument("--store-dir")
     lo.add_argument("--checkpoint-dir")
     lo.add_argument("--scheduler", default="fair_share")
+    lo.add_argument("--grpc-port", type=int, default=None,
+                    help="also serve the master API over gRPC (determined.api.v1.Determined) on this port")
     lo.set_defaults(func=cmd_deploy_local)
     for cloud in ("aws", "gcp"):
         x = dp.add_parser(cloud, help=f"master VM on {cloud.upper()} with the {cloud} agent provisioner",
