@@ -382,8 +382,10 @@ def test_deferred_forward_apply_never_reaches_hooks_or_user_code(gpu):
 def test_projection_shortcut_bn_apply_deferred_into_residual(gpu):
     """The projection-shortcut BN (no ReLU) of each layer's first block finalizes only; bn3's apply
     computes relu(bn3(x) + xs * scale + shift) from the shortcut conv's output xs (det_norm.hip RES 2,
-    or det_conv.hip AFWD when bn3's apply is itself staged by the next conv1).  Outputs and gradients
-    match the materialised path (which rounds the shortcut BN's output to bf16 once more)."""
+    or det_conv.hip AFWD when bn3's apply is itself staged by the next conv1).  Each ResNet-50 layer
+    (stride-1 and stride-2 projections) matches the materialised path, which rounds the shortcut
+    BN's output to bf16 once more, per layer (a whole-network comparison at a tiny batch mostly
+    measures how batch-statistics BN amplifies that rounding), and the counters see the deferral."""
     from determined_1_amd.models import resnet
 
     torch.manual_seed(0)
@@ -392,28 +394,36 @@ def test_projection_shortcut_bn_apply_deferred_into_residual(gpu):
         if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
             mod.to(torch.bfloat16)
     g = torch.Generator(device="cpu").manual_seed(5)
-    x = torch.randn(8, 4, 64, 64, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    y_lab = torch.randint(0, 10, (8,), generator=g).to(gpu)
-
-    def run(defer):
-        conv.DEFER_AFFINE_APPLY = defer
-        model.zero_grad(set_to_none=True)
-        before = dict(conv.AFFINE_APPLY_COUNTS)
-        out = model(x)
-        torch.nn.functional.cross_entropy(out.float(), y_lab).backward()
-        d = {k: conv.AFFINE_APPLY_COUNTS[k] - before[k] for k in before}
-        return out.float(), {k: p.grad.float().clone() for k, p in model.named_parameters()}, d
-
+    shapes = {"layer1": (8, 64, 32, 32), "layer2": (8, 256, 32, 32), "layer3": (8, 512, 16, 16),
+              "layer4": (8, 1024, 8, 8)}
+    resnet._FWD.depth = 1  # as inside ResNet.forward
     try:
-        o_m, g_m, c_m = run(False)
-        o_d, g_d, c_d = run(True)
+        for name, shp in shapes.items():
+            layer = getattr(model, name)
+            xin = torch.randn(*shp, generator=g).to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            gout = None
+            res = {}
+            for defer in (False, True):
+                conv.DEFER_AFFINE_APPLY = defer
+                layer.zero_grad(set_to_none=True)
+                before = dict(conv.AFFINE_APPLY_COUNTS)
+                xi = xin.clone().requires_grad_(True)
+                out = layer(xi)
+                if gout is None:
+                    gout = torch.randn(out.shape, generator=g).to(gpu).to(out.dtype).contiguous(
+                        memory_format=torch.channels_last)
+                out.backward(gout)
+                res[defer] = (out.float().clone(), xi.grad.float().clone(),
+                              {k: conv.AFFINE_APPLY_COUNTS[k] - before[k] for k in before})
+            (o_m, dx_m, c_m), (o_d, dx_d, c_d) = res[False], res[True]
+            assert c_m == {"deferred": 0, "in_residual": 0, "materialized": 0}, (name, c_m)
+            assert c_d == {"deferred": 1, "in_residual": 1, "materialized": 0}, (name, c_d)
+            e_o = float((o_d - o_m).norm() / o_m.norm())
+            e_dx = float((dx_d - dx_m).norm() / dx_m.norm())
+            assert e_o < 1e-2 and e_dx < 3e-2, (name, e_o, e_dx)
     finally:
         conv.DEFER_AFFINE_APPLY = True
-    assert c_m == {"deferred": 0, "in_residual": 0, "materialized": 0}, c_m
-    assert c_d == {"deferred": 4, "in_residual": 4, "materialized": 0}, c_d
-    torch.testing.assert_close(o_d, o_m, rtol=3e-2, atol=3e-2 * float(o_m.abs().max()))
-    rel = {k: float((g_d[k] - g_m[k]).norm() / (g_m[k].norm() + 1e-12)) for k in g_m}
-    assert max(rel.values()) < 5e-2, sorted(rel.items(), key=lambda kv: -kv[1])[:5]
+        resnet._FWD.depth = 0
 
 
 def test_projection_shortcut_bn_backward_apply_in_dgrad(gpu):
