@@ -342,12 +342,12 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       }
       if constexpr (AFWD) {
         // exactly det_norm.hip bn_apply_fwd<RELU, RES>: z = fma(x, scale, shift) + res, relu, mask bits
-        // (RES 2: res = fma(r, rscale, rshift) of the deferred residual BN)
+        // (RES 2: res = bf16(fma(r, rscale, rshift)) of the deferred residual BN)
         unsigned bits = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float r2 = bf2f(ra2[i][j]);
-          const float z = __fmaf_rn(bf2f(ra[i][j]), ca[j], cb[j]) + (a2aff ? __fmaf_rn(r2, ra_s[j], ra_h[j]) : r2);
+          const float z = __fmaf_rn(bf2f(ra[i][j]), ca[j], cb[j]) + (a2aff ? round_bf(__fmaf_rn(r2, ra_s[j], ra_h[j])) : r2);
           v[j] = f2bf(fmaxf(z, 0.f));
           bits |= (z > 0.f ? 1u : 0u) << j;
         }

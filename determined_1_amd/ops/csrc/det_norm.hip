@@ -446,8 +446,8 @@ void launch_stats_finalize(hipStream_t st, const float* pmean, const float* pm2,
 // ---------------------------------------------------------------------------------------------
 // Elementwise apply: y = act(x*scale + shift [+ res]); grid-stride over 8-element vectors, 4 in
 // flight per thread.  RES 2: the residual is itself a BatchNorm output whose apply was deferred
-// (ResNet's projection-shortcut BN): res = r * rscale + rshift, computed here from its input r --
-// that BN's own apply pass (read r, write res) and this pass's read of res become one read of r.
+// (ResNet's projection-shortcut BN): res = bf16(r * rscale + rshift), computed here from its input r
+// -- that BN's own apply pass (read r, write res) and this pass's read of res become one read of r.
 // ---------------------------------------------------------------------------------------------
 template <typename T, bool RELU, int RES>
 __global__ void __launch_bounds__(kThreads)
@@ -486,7 +486,8 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
         for (int j = 0; j < 8; ++j) {
           float z = __fmaf_rn(xv[u][j], sc[j], sh[j]);
           if (RES == 1) z += rv[u][j];
-          if (RES == 2) z += __fmaf_rn(rv[u][j], rsc[j], rsh[j]);
+          // rounded to bf16 like the materialised shortcut-BN output: bit-identical to that path
+          if (RES == 2) z += __uint_as_float(static_cast<uint32_t>(f2bf(__fmaf_rn(rv[u][j], rsc[j], rsh[j]))) << 16);
           o[j] = RELU ? fmaxf(z, 0.f) : z;
           bits |= (z > 0.f ? 1u : 0u) << j;
         }
