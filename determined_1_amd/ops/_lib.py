@@ -216,6 +216,7 @@ _SIGNATURES = {
     # stream, const DetAttnParams* (transformer._AttnParams)
     "det_attn_forward": ([c_void_p, c_void_p], c_int),
     "det_attn_backward": ([c_void_p, c_void_p], c_int),
+    "det_attn_set_bwd_merged": ([c_int], c_int),
     # stream, B, nh, Lq, Lk, p, seed, offset, out
     "det_attn_dropout_mask": ([c_void_p, c_int, c_int, c_int, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64,
                                c_void_p], c_int),

@@ -43,6 +43,7 @@
 // torch.nn.functional.scaled_dot_product_attention.
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <math.h>
 #include <stdint.h>
 
@@ -415,13 +416,14 @@ __global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) att
 //   attn_bwd_dkv (key on the lane): S, dPd per query tile, dV^T += dO^T Pd and dK^T += Q^T dS with
 //                Q^T / dO^T LDS images.
 // =============================================================================================
-template <typename E, int HD, bool MB>
-__global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_dq_kernel(Args a) {
+// bx: the workgroup's row-tile index (blockIdx.x in the two-launch form; see attn_bwd_kernel).
+// WRITE_D: this pass also writes D for the dK/dV pass (the merged form has attn_delta_kernel do it).
+template <typename E, int HD, bool MB, bool WRITE_D>
+__device__ __forceinline__ void attn_bwd_dq_body(const Args& a, int bx, unsigned char* smem) {
   using TL = Tile<E, HD>;
   using EL = Elt<E>;
   constexpr int QCH = TL::NCH / 2, NU = HD / 32;
   constexpr int BUF = 2 * TL::ROW_BYTES + TL::T_BYTES;  // K rows, V rows, K^T
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lq = a.Lq, Lk = a.Lk, nkb = (Lk + kKB - 1) / kKB;
   float* biasl = reinterpret_cast<float*>(smem + 2 * BUF);
   const int b = blockIdx.z, head = blockIdx.y;
@@ -430,7 +432,7 @@ __global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) att
   const E* vbase = static_cast<const E*>(a.v) + b * a.vsb + head * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int qv = blockIdx.x * kQB + wave * 32 + r;
+  const int qv = bx * kQB + wave * 32 + r;
   const int q = qv < Lq ? qv : Lq - 1;
 
   TL kt, vt;
@@ -450,7 +452,7 @@ __global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) att
   }
   const float D = dsum + __shfl_xor(dsum, 32, 64);
   const int64_t li = (static_cast<int64_t>(b) * a.nh + head) * Lq + q;
-  if (qv < Lq && hh == 0) a.delta[li] = D;
+  if (WRITE_D && qv < Lq && hh == 0) a.delta[li] = D;
   const float lse2 = a.lse[li] * kLog2e;
   const float* mrow = MB ? a.mbias + b * a.mbb + head * a.mbh + static_cast<int64_t>(q) * a.mbq : nullptr;
   const uint32_t key = rng_key_for(a.rng_key, b, head);
@@ -524,13 +526,18 @@ __global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) att
                  dqt[u][4 * g + 3] * sc);
 }
 
-template <typename E, int HD, bool MB>  // a full bias adds a per-element load row: one wave per SIMD
-__global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_dkv_kernel(Args a) {
+template <typename E, int HD, bool MB>
+__global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_dq_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  attn_bwd_dq_body<E, HD, MB, true>(a, blockIdx.x, smem);
+}
+
+template <typename E, int HD, bool MB>
+__device__ __forceinline__ void attn_bwd_dkv_body(const Args& a, int bx, unsigned char* smem) {
   using TL = Tile<E, HD>;
   using EL = Elt<E>;
   constexpr int QCH = TL::NCH / 2, NU = HD / 32;
   constexpr int BUF = 2 * (TL::ROW_BYTES + TL::T_BYTES);  // Q rows, Q^T, dO rows, dO^T
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lq = a.Lq, Lk = a.Lk, nqb = (Lq + kKB - 1) / kKB;
   float* lse2 = reinterpret_cast<float*>(smem + 2 * BUF);
   float* dl = lse2 + nqb * kKB;
@@ -539,7 +546,7 @@ __global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2
   const E* dobase = static_cast<const E*>(a.dout) + b * a.dosb + head * HD;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int kv = blockIdx.x * kQB + wave * 32 + r;
+  const int kv = bx * kQB + wave * 32 + r;
   const int kk = kv < Lk ? kv : Lk - 1;  // this lane's key
 
   TL qt, dt;
@@ -648,6 +655,61 @@ __global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2
     }
 }
 
+template <typename E, int HD, bool MB>  // a full bias adds a per-element load row: one wave per SIMD
+__global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_dkv_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  attn_bwd_dkv_body<E, HD, MB>(a, blockIdx.x, smem);
+}
+
+// D[b, h, q] = sum_d dO o O, summed exactly as attn_bwd_dq_body does (chunk-sequential fmaf per lane
+// half, halves added): the pre-pass of the merged backward.  One 64-lane wave per 32 rows.
+template <typename E, int HD>
+__global__ void __launch_bounds__(kThreads) attn_delta_kernel(Args a) {
+  using TL = Tile<E, HD>;
+  using EL = Elt<E>;
+  constexpr int QCH = TL::NCH / 2;
+  const int lane = threadIdx.x & 63, r = lane & 31, hh = lane >> 5;
+  const int64_t rows = static_cast<int64_t>(a.B) * a.nh * a.Lq;
+  for (int64_t row0 = (static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * 32; row0 < rows;
+       row0 += static_cast<int64_t>(gridDim.x) * kWaves * 32) {
+    const int64_t li = row0 + r;
+    const int64_t lc = li < rows ? li : rows - 1;
+    const int q = static_cast<int>(lc % a.Lq);
+    const int head = static_cast<int>((lc / a.Lq) % a.nh);
+    const int b = static_cast<int>(lc / a.Lq / a.nh);
+    const E* orow = static_cast<const E*>(a.out) + b * a.osb + static_cast<int64_t>(q) * a.ost + head * HD;
+    const E* dorow = static_cast<const E*>(a.dout) + b * a.dosb + static_cast<int64_t>(q) * a.dost + head * HD;
+    float dsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < QCH; ++j) {
+      const int c = (2 * j + hh) * TL::CH;
+      dsum += EL::chunk_dot(*reinterpret_cast<const u32x4*>(dorow + c), *reinterpret_cast<const u32x4*>(orow + c));
+    }
+    const float D = dsum + __shfl_xor(dsum, 32, 64);
+    if (li < rows && hh == 0) a.delta[li] = D;
+  }
+}
+
+// The whole backward in one grid: the first nqt row tiles run the dQ pass, the rest the dK/dV pass
+// (no dependency between them once D exists), so the two passes share the chip instead of running
+// back to back -- at BERT shape (B 12, S 384, 12 heads) each pass alone is 432 workgroups, under two
+// per CU at one wave per SIMD, latency-bound.
+template <typename E, int HD, bool MB>
+__global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2)) attn_bwd_kernel(Args a, int nqt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (static_cast<int>(blockIdx.x) < nqt) attn_bwd_dq_body<E, HD, MB, false>(a, blockIdx.x, smem);
+  else attn_bwd_dkv_body<E, HD, MB>(a, blockIdx.x - nqt, smem);
+}
+
+bool g_bwd_merged_set = false, g_bwd_merged = true;
+bool bwd_merged() {
+  static const bool env = [] {
+    const char* e = std::getenv("DET_ATTN_BWD_MERGED");
+    return !(e && e[0] == '0');
+  }();
+  return g_bwd_merged_set ? g_bwd_merged : env;
+}
+
 __global__ void attn_mask_kernel(int B, int nh, int Lq, int Lk, uint32_t thr, uint32_t base_key, uint8_t* out) {
   const int64_t n = static_cast<int64_t>(B) * nh * Lq * Lk;
   const uint32_t lke = static_cast<uint32_t>(lk_even4(Lk));
@@ -691,6 +753,18 @@ struct Cfg {
   }
   static void launch_bwd(hipStream_t st, const Args& a) {
     dim3 gq((a.Lq + kQB - 1) / kQB, a.nh, a.B), gk((a.Lk + kQB - 1) / kQB, a.nh, a.B);
+    if (bwd_merged()) {
+      const int64_t rows = static_cast<int64_t>(a.B) * a.nh * a.Lq;
+      const int64_t dgrid = (rows + kWaves * 32 - 1) / (kWaves * 32);
+      hipLaunchKernelGGL((attn_delta_kernel<E, HD>), dim3(static_cast<unsigned>(dgrid < 65536 ? dgrid : 65536)),
+                         dim3(kThreads), 0, st, a);
+      const int nqt = static_cast<int>(gq.x);
+      const dim3 g(gq.x + gk.x, a.nh, a.B);
+      const size_t lds = dq(a.Lk) > dkv(a.Lq) ? dq(a.Lk) : dkv(a.Lq);
+      if (a.mbias) hipLaunchKernelGGL((attn_bwd_kernel<E, HD, true>), g, dim3(kThreads), lds, st, a, nqt);
+      else hipLaunchKernelGGL((attn_bwd_kernel<E, HD, false>), g, dim3(kThreads), lds, st, a, nqt);
+      return;
+    }
     if (a.mbias) {
       hipLaunchKernelGGL((attn_bwd_dq_kernel<E, HD, true>), gq, dim3(kThreads), dq(a.Lk), st, a);
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<E, HD, true>), gk, dim3(kThreads), dkv(a.Lq), st, a);
@@ -790,6 +864,16 @@ int det_attn_backward(void* stream, const DetAttnParams* P) {
   hipStream_t st = static_cast<hipStream_t>(stream);
   dispatch(P->dtype, P->hd, [&](auto cfg) { decltype(cfg)::launch_bwd(st, a); });
   return static_cast<int>(hipGetLastError());
+}
+
+// Backward as one merged grid after a D pre-pass (1, default; DET_ATTN_BWD_MERGED) or as the dQ
+// and dK/dV launches back to back (0); < 0 restores the environment's choice.  For benchmarks and
+// tests.  Returns the previous effective setting.
+int det_attn_set_bwd_merged(int on) {
+  const int old = bwd_merged() ? 1 : 0;
+  g_bwd_merged_set = on >= 0;
+  g_bwd_merged = on > 0;
+  return old;
 }
 
 // The keep mask (1 = kept) the kernels derive for (p, seed, offset): [B, nh, Lq, Lk] uint8 (tests).

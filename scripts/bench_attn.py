@@ -1,6 +1,8 @@
 """Microbenchmark of the MFMA attention kernels (det_attention.hip) against torch SDPA (AOTriton /
 math on ROCm) at the BERT, ALBERT, DETR and head_dim-128 shapes, with and without probability
-dropout.  Prints ms per fwd and per fwd+bwd and TFLOP/s, one JSON line per case."""
+dropout.  Prints ms per fwd and per fwd+bwd and TFLOP/s, one JSON line per case; the native
+backward both as one merged grid (default) and as two launches.  ``--graph``: GPU time of hipGraph
+replays instead of the host loop."""
 import json
 import os
 import sys
@@ -74,7 +76,12 @@ def bench(B, S, nh, hd=64, dt=torch.bfloat16, p=0.0, iters=30, Lk=None):
     flop = 4 * B * nh * S * Lk * hd
     res = {"B": B, "Lq": S, "Lk": Lk, "nh": nh, "hd": hd, "dtype": str(dt).split(".")[-1], "p": p,
            "timing": "hipgraph replay" if GRAPH else "host loop"}
-    for name, fn in (("native", native), ("sdpa", sdpa)):
+    from determined_1_amd.ops import _lib
+
+    lib = _lib.get_lib()
+    for name, fn in (("native", native), ("native_2launch", native), ("sdpa", sdpa)):
+        # native: merged backward grid (default); native_2launch: dQ then dK/dV launches
+        lib.det_attn_set_bwd_merged(0 if name == "native_2launch" else -1)
         if GRAPH:
             if p > 0:
                 continue  # dropout RNG state is not graph-safe here

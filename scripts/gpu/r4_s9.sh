@@ -1,12 +1,15 @@
 #!/bin/bash
 # Round-4 session 9: ResNet-50 per-call step roofline (read/write stream bounds); BERT-base SQuAD
 # re-bench on the round-3 attention kernels (+ aggregation 2) with a steady rocprof profile; the
-# attention microbench timed as hipGraph replays (GPU time, not host launch rate).
+# attention microbench timed as hipGraph replays (GPU time, not host launch rate), merged backward
+# grid vs two launches.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r4s9
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_attention_gpu.py tests/test_transformer_gpu.py > $O/pytest_attn.log 2>&1 || { tail -40 $O/pytest_attn.log; exit 1; }
+tail -1 $O/pytest_attn.log
 timeout -k 10 300 python -u scripts/step_roofline.py --iters 3 --out $O/step_roofline.csv > $O/step_roofline.txt 2>&1 || { tail -30 $O/step_roofline.txt; exit 1; }
 sed -n '/per family/,$p' $O/step_roofline.txt
 timeout -k 10 300 python -u scripts/bench_attn.py --graph > $O/attn_graph.jsonl 2> $O/attn.err || { tail -20 $O/attn.err; exit 1; }

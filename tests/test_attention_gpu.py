@@ -170,3 +170,34 @@ def test_zero_attention_fallbacks_at_model_shapes(gpu):
     hs.float().pow(2).mean().backward()
     assert tfops.FALLBACKS["count"] == before
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("dt,hd,B,nh,Lq,Lk,mask", [
+    (torch.bfloat16, 64, 4, 12, 384, 384, "key"),     # BERT-base SQuAD
+    (torch.bfloat16, 128, 2, 4, 333, 200, "full_b"),  # cross-attention, full bias, tails
+    (torch.float32, 32, 2, 8, 100, 850, None),        # DETR decoder cross-attention
+])
+def test_merged_backward_equals_two_launch_backward(gpu, dt, hd, B, nh, Lq, Lk, mask):
+    """The merged backward (D pre-pass, then dQ and dK/dV work in one grid) computes exactly what the
+    dQ-then-dK/dV launches do: the same D (same summation order) and the same per-tile work."""
+    from determined_1_amd.ops import _lib
+
+    lib = _lib.get_lib()
+    g = torch.Generator().manual_seed(7)
+    H = nh * hd
+    ins = [(torch.randn(B, L, H, generator=g) * 1.5).to(dt) for L in (Lq, Lk, Lk)]
+    dy = torch.randn(B, Lq, H, generator=g).to(dt)
+    dev_mask, _ = _bias(mask, B, nh, Lq, Lk, g)
+    m = None if dev_mask is None else dev_mask.to(gpu, dt)
+    res = {}
+    try:
+        for merged in (0, 1):
+            lib.det_attn_set_bwd_merged(merged)
+            d_ins = [t.to(gpu).requires_grad_(True) for t in ins]
+            out = tfops.attention(*d_ins, nh, attn_bias=m)
+            out.backward(dy.to(gpu))
+            res[merged] = [out.detach().clone()] + [t.grad.clone() for t in d_ins]
+    finally:
+        lib.det_attn_set_bwd_merged(-1)
+    for name, a, b in zip(("out", "dq", "dk", "dv"), res[0], res[1]):
+        assert torch.equal(a, b), name
