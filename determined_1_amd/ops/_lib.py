@@ -145,6 +145,8 @@ _SIGNATURES = {
     # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
     "det_conv_nt_rows_per_block": ([c_int], c_int),
     "det_conv_nt_set_pf": ([c_int], c_int),
+    # stream, X, W, bias (nullable), Y, M, N, K
+    "det_linear_fwd": ([c_void_p] * 5 + [c_i64, c_int, c_int], c_int),
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
     # ... + res, aout, abits, res_scale, res_shift
     "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 5, c_int),

@@ -196,6 +196,8 @@ struct NtArgs {
   // shortcut BN): the residual is A2 * a2scale[k] + a2shift[k] (det_norm.hip bn_apply_fwd RES 2)
   const float* a2scale;
   const float* a2shift;
+  // nullable: C = op(A) . B^T + bias[n] (bf16 [N]; added to the fp32 accumulators, one rounding)
+  const unsigned short* bias;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -463,6 +465,18 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   }
 
   // ---- epilogue: bf16 tile through LDS (coalesced 16-B row stores) + BN statistics ----
+  if constexpr (!BNB) {
+    if (a.bias != nullptr) {  // a Linear layer's bias (det_linear_fwd)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const float bj = bf2f(a.bias[n0 + wn * TN + j * 16 + (lane & 15)]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += bj;
+      }
+    }
+  }
   unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -917,6 +931,24 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
   }
   if (N % 128 == 0) return launch_nt_pf<128, 128>(st, a, pro, stats, stride2, false);
   return launch_nt_pf<128, 64>(st, a, pro, stats, stride2, false);
+}
+
+// Linear layer forward: Y[M, N] = X[M, K] . W[N, K]^T (+ bias[N]), bf16, N % 64 == 0, K % 64 == 0
+// (a transformer's dense layers on the same MFMA tiles as the 1x1 convs).  Small grids (fewer than
+// two 128 x 128 tiles per CU: BERT's M = 4608 token rows against N = 768) take 128 x 64 tiles.
+int det_linear_fwd(void* stream, const void* X, const void* W, const void* bias, void* Y, int64_t M, int N, int K) {
+  if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
+  NtArgs a{static_cast<const unsigned short*>(X), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(Y),
+           M, N, K, nullptr, nullptr, nullptr, nullptr, Gather{}, BnBwdEpi{}, nullptr, nullptr, nullptr, nullptr,
+           nullptr, nullptr, static_cast<const unsigned short*>(bias)};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t tiles128 = ((M + 127) / 128) * (N / 128);
+  if (K == kBK) {
+    if (N % 128 == 0 && tiles128 >= 512) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false);
+    return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false);
+  }
+  if (N % 128 == 0 && tiles128 >= 512) return launch_nt_pf<128, 128>(st, a, false, false, false, false);
+  return launch_nt_pf<128, 64>(st, a, false, false, false, false);
 }
 
 // dX[M, N] = dY[M, K] . W[K, N]: the input gradient of a 1x1 conv against its weight W = [Cout, Cin]

@@ -5,7 +5,9 @@
     linear_dropout_add_layernorm(x, W, b, r, g, be)   y = LN(dropout(x W^T + b) + r)
     layer_norm(x, g, be)                              y = LN(x)
 
-GEMMs stay on hipBLASLt (``torch.addmm`` / ``torch.mm``); everything between them is one HIP
+GEMMs run on hipBLASLt (``torch.addmm`` / ``torch.mm``) or, with ``DET_NATIVE_LINEAR=1``, on the
+hand-written MFMA tiles of ``det_conv.hip`` (forward with the bias in the epilogue, input gradient
+against the weight as stored, split-M weight gradient); everything between them is one HIP
 pass per direction, and every Linear's bias gradient is produced inside the kernel that already
 reads the gradient (LayerNorm bwd, GELU bwd) instead of a separate reduction.  Dropout masks are
 regenerated from a Philox (seed, offset) pair in the backward pass rather than stored.
@@ -16,6 +18,7 @@ fallbacks are counted in ``FALLBACKS`` so benchmarks can assert the native path 
 """
 import ctypes
 import itertools
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -99,10 +102,29 @@ class SharedWeightGrads:
         return out
 
 
+# Dense layers on the hand-written det_conv.hip GEMMs instead of hipBLASLt (A/B switch, see module doc)
+NATIVE_LINEAR = os.environ.get("DET_NATIVE_LINEAR", "0") == "1"
+LINEAR_COUNTS = {"native_fwd": 0, "native_dgrad": 0, "native_wgrad": 0}
+
+
+def _native_linear(x2: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (NATIVE_LINEAR and x2.is_cuda and x2.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and x2.dim() == 2 and x2.is_contiguous() and weight.is_contiguous() and weight.shape[0] % 64 == 0
+            and weight.shape[1] % 64 == 0 and x2.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
+
+
 def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     """dW = dz^T x, written straight into the parameter's gradient-arena slot when that is where
     it will land (ops.arena.landing_buffer): no separate landing copy for the largest gradients."""
     buf = landing_buffer(weight) if weight.is_cuda else None
+    if _native_linear(x2, weight) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
+        from determined_1_amd.ops.conv import conv1x1_wgrad
+
+        out = buf if (buf is not None and buf.dtype in (torch.bfloat16, torch.float32) and buf.is_contiguous()) \
+            else torch.empty(weight.shape, dtype=weight.dtype, device=weight.device)
+        conv1x1_wgrad(dz, x2, out.view(weight.shape[0], -1))
+        LINEAR_COUNTS["native_wgrad"] += 1
+        return out
     if buf is not None and buf.dtype == dz.dtype and buf.is_contiguous():
         return torch.mm(dz.t(), x2, out=buf)
     return dz.t() @ x2
@@ -110,7 +132,13 @@ def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> to
 
 def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool,
                  acc: Optional[SharedWeightGrads] = None):
-    dx = dz @ weight if need_x else None
+    if need_x and _native_linear(x2, weight) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
+        from determined_1_amd.ops.conv import dgrad_1x1
+
+        dx = dgrad_1x1(dz, weight)  # dz [M, N] . W [N, K], the weight read as stored
+        LINEAR_COUNTS["native_dgrad"] += 1
+    else:
+        dx = dz @ weight if need_x else None
     dw = None
     if need_w:
         dw = acc.accumulate(weight, dz, x2) if acc is not None else _weight_grad(weight, dz, x2)
@@ -124,6 +152,13 @@ def _track(acc: Optional[SharedWeightGrads], weight: torch.Tensor) -> Optional[S
 
 
 def _addmm(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    if _native_linear(x2, weight) and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous())):
+        y = torch.empty(x2.shape[0], weight.shape[0], dtype=torch.bfloat16, device=x2.device)
+        _lib.check(_lib.get_lib().det_linear_fwd(_stream(x2), x2.data_ptr(), weight.data_ptr(), _ptr(bias), y.data_ptr(),
+                                                 int(x2.shape[0]), int(weight.shape[0]), int(x2.shape[1])),
+                   "det_linear_fwd")
+        LINEAR_COUNTS["native_fwd"] += 1
+        return y
     return torch.addmm(bias, x2, weight.t()) if bias is not None else x2 @ weight.t()
 
 

@@ -216,3 +216,52 @@ def test_bert_trial_direct_gradient_landing(gpu, monkeypatch):
                        len(landed))
     assert out[False][1] == 0 and out[True][1] > 0
     torch.testing.assert_close(out[True][0], out[False][0], atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("rows,K,N", [(4608, 768, 2304), (4608, 3072, 768), (4608, 768, 768), (333, 128, 192),
+                                      (200, 64, 128)])
+def test_native_linear_exact_on_integer_operands(gpu, monkeypatch, rows, K, N):
+    """DET_NATIVE_LINEAR: a Linear's forward (bias in the GEMM epilogue), input gradient (weight read
+    as stored) and weight gradient on the det_conv.hip tiles, integer operands whose fp32 sums are
+    exact: forward / input gradient bit-equal to the rounded fp32 product, weight gradient exact."""
+    monkeypatch.setattr(tfops, "NATIVE_LINEAR", True)
+    g = torch.Generator().manual_seed(rows + K + N)
+    x = torch.randint(-2, 3, (rows, K), generator=g).to(torch.bfloat16)
+    w = torch.randint(-2, 3, (N, K), generator=g).to(torch.bfloat16)
+    b = torch.randint(-4, 5, (N,), generator=g).to(torch.bfloat16)
+    dy = torch.randint(-2, 3, (rows, N), generator=g).to(torch.bfloat16)
+    before = dict(tfops.LINEAR_COUNTS)
+    xd, wd, bd = _leaf(x, gpu), _leaf(w, gpu), _leaf(b, gpu)
+    y = tfops.linear(xd, wd, bd)
+    y.backward(dy.to(gpu))
+    assert all(tfops.LINEAR_COUNTS[k] == before[k] + 1 for k in before), tfops.LINEAR_COUNTS
+    assert torch.equal(y.cpu(), (x.float() @ w.float().t() + b.float()).to(torch.bfloat16))
+    assert torch.equal(xd.grad.cpu(), (dy.float() @ w.float()).to(torch.bfloat16))
+    assert torch.equal(wd.grad.float().cpu(), (dy.float().t() @ x.float()).to(torch.bfloat16).float())
+    torch.testing.assert_close(bd.grad.float().cpu(), dy.float().sum(0), rtol=1e-2, atol=1e-2)
+
+
+def test_bert_layer_native_linear_matches_hipblaslt(gpu, monkeypatch):
+    """The BERT encoder layer with its dense layers on the hand-written GEMMs vs on hipBLASLt."""
+    from determined_1_amd.models.bert import BertEncoderConfig, BertLayer
+
+    torch.manual_seed(0)
+    cfg = BertEncoderConfig(hidden_size=256, num_attention_heads=4, intermediate_size=1024,
+                            hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    layer = BertLayer(cfg).to(gpu).to(torch.bfloat16)
+    x = torch.randn(2, 128, 256, device=gpu).to(torch.bfloat16)
+    mask = torch.zeros(2, 1, 1, 128, device=gpu, dtype=torch.bfloat16)
+    outs = {}
+    for native in (False, True):
+        monkeypatch.setattr(tfops, "NATIVE_LINEAR", native)
+        layer.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        y = layer(xi, mask)
+        y.float().square().sum().backward()
+        outs[native] = (y.float(), xi.grad.float(), {k: p.grad.float() for k, p in layer.named_parameters()})
+    (y0, dx0, g0), (y1, dx1, g1) = outs[False], outs[True]
+    torch.testing.assert_close(y1, y0, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(dx1, dx0, rtol=5e-2, atol=5e-2 * float(dx0.abs().max()))
+    for k in g0:
+        rel = float((g1[k] - g0[k]).norm() / (g0[k].norm() + 1e-12))
+        assert rel < 3e-2, (k, rel)
