@@ -248,7 +248,16 @@ def test_bert_layer_native_linear_matches_hipblaslt(gpu, monkeypatch):
     torch.manual_seed(0)
     cfg = BertEncoderConfig(hidden_size=256, num_attention_heads=4, intermediate_size=1024,
                             hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
-    layer = BertLayer(cfg).to(gpu).to(torch.bfloat16)
+    layer = BertLayer(cfg)
+    for name, p in layer.named_parameters():  # the BertForQA initialisation (torch.empty otherwise)
+        with torch.no_grad():
+            if name.endswith("weight") and p.dim() == 2:
+                p.normal_(0.0, 0.02)
+            elif "ln" in name and name.endswith("weight"):
+                p.fill_(1.0)
+            else:
+                p.normal_(0.0, 0.02)
+    layer = layer.to(gpu).to(torch.bfloat16)
     x = torch.randn(2, 128, 256, device=gpu).to(torch.bfloat16)
     mask = torch.zeros(2, 1, 1, 128, device=gpu, dtype=torch.bfloat16)
     outs = {}
