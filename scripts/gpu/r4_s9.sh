@@ -17,3 +17,5 @@ head -16 $O/bert_steady.txt
 rm -rf $O/prof
 timeout -k 10 900 python -u -m pytest -x -v -s --timeout 900 --timeout-method thread -p no:cacheprovider -m gpu tests/test_dp_resnet_gpu.py > $O/pytest_dp.log 2>&1 || { tail -60 $O/pytest_dp.log; exit 1; }
 grep "dp-vs-single\|passed\|failed" $O/pytest_dp.log | tail -6
+timeout -k 10 300 python -u scripts/probe_small_launches.py --steps 3 --warmup 3 > $O/small_launches.txt 2>&1 || { tail -20 $O/small_launches.txt; exit 1; }
+grep -A3 "copy_\|add\|fill" $O/small_launches.txt | head -30
