@@ -701,13 +701,19 @@ __global__ void __launch_bounds__(kThreads, (MB || HD * sizeof(E) >= 256 ? 1 : 2
   else attn_bwd_dkv_body<E, HD, MB>(a, blockIdx.x - nqt, smem);
 }
 
-bool g_bwd_merged_set = false, g_bwd_merged = true;
-bool bwd_merged() {
-  static const bool env = [] {
+// -1 auto, 0 two launches, 1 merged (det_attn_set_bwd_merged, else DET_ATTN_BWD_MERGED=0/1).
+// auto: merged when the two passes together have at most two workgroups per CU (measured, graph
+// replays, profiles/r4_attention_graph.jsonl: DETR fp32 encoder 0.139 vs 0.191 ms fwd+bwd, cross-
+// attention 0.110 vs 0.121; at BERT shape, 864 workgroups, the merged grid is 6 % slower).
+int g_bwd_mode = -2;
+bool bwd_merged(int64_t workgroups) {
+  static const int env = [] {
     const char* e = std::getenv("DET_ATTN_BWD_MERGED");
-    return !(e && e[0] == '0');
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
   }();
-  return g_bwd_merged_set ? g_bwd_merged : env;
+  const int mode = g_bwd_mode >= -1 ? g_bwd_mode : env;
+  if (mode >= 0) return mode == 1;
+  return workgroups <= 2 * 256;
 }
 
 __global__ void attn_mask_kernel(int B, int nh, int Lq, int Lk, uint32_t thr, uint32_t base_key, uint8_t* out) {
@@ -753,7 +759,7 @@ struct Cfg {
   }
   static void launch_bwd(hipStream_t st, const Args& a) {
     dim3 gq((a.Lq + kQB - 1) / kQB, a.nh, a.B), gk((a.Lk + kQB - 1) / kQB, a.nh, a.B);
-    if (bwd_merged()) {
+    if (bwd_merged(static_cast<int64_t>(gq.x + gk.x) * a.nh * a.B)) {
       const int64_t rows = static_cast<int64_t>(a.B) * a.nh * a.Lq;
       const int64_t dgrid = (rows + kWaves * 32 - 1) / (kWaves * 32);
       hipLaunchKernelGGL((attn_delta_kernel<E, HD>), dim3(static_cast<unsigned>(dgrid < 65536 ? dgrid : 65536)),
@@ -866,13 +872,12 @@ int det_attn_backward(void* stream, const DetAttnParams* P) {
   return static_cast<int>(hipGetLastError());
 }
 
-// Backward as one merged grid after a D pre-pass (1, default; DET_ATTN_BWD_MERGED) or as the dQ
-// and dK/dV launches back to back (0); < 0 restores the environment's choice.  For benchmarks and
-// tests.  Returns the previous effective setting.
+// Backward as one merged grid after a D pre-pass (1) or as the dQ and dK/dV launches back to back
+// (0); -1 picks by grid size (auto, the default), < -1 restores DET_ATTN_BWD_MERGED.  For benchmarks
+// and tests.  Returns the previous override.
 int det_attn_set_bwd_merged(int on) {
-  const int old = bwd_merged() ? 1 : 0;
-  g_bwd_merged_set = on >= 0;
-  g_bwd_merged = on > 0;
+  const int old = g_bwd_mode;
+  g_bwd_mode = on < -1 ? -2 : (on > 1 ? 1 : on);
   return old;
 }
 

@@ -63,6 +63,45 @@ def summarize_timelines(cl, trials, t0):
     return out
 
 
+def _ts(s):
+    from datetime import datetime
+
+    return datetime.strptime(s.rstrip("Z")[:26], "%Y-%m-%dT%H:%M:%S.%f").timestamp() if s else None
+
+
+def idle_breakdown(cl, trials, slots, t_start, t_end):
+    """Split idle slot-seconds into "no trial exists to run" (searcher-bound: ASHA has not created or
+    promoted work for the slot) and "a live trial has no running container" (scheduling, container
+    start, or a trial parked between rungs until ASHA promotes it), from the master's trial
+    start/end times and the first / last log record of each trial container."""
+    from collections import defaultdict
+
+    alive, busy = [], []
+    for t in trials:
+        a, b = _ts(t.get("start_time")), _ts(t.get("end_time")) or t_end
+        if a is not None:
+            alive.append((a, b))
+        spans = defaultdict(list)
+        for rec in cl.get(f"/trials/{t['id']}/logs"):
+            ts = _ts(rec.get("timestamp"))
+            if ts is not None:
+                spans[rec.get("container_id")].append(ts)
+        busy += [(min(v), max(v)) for v in spans.values() if v]
+    step = 0.05
+    n = int((t_end - t_start) / step) + 1
+    idle = searcher = parked = 0.0
+    for i in range(n):
+        t = t_start + i * step
+        nb = sum(1 for a, b in busy if a <= t < b)
+        na = sum(1 for a, b in alive if a <= t < b)
+        idle += max(0, slots - nb) * step
+        searcher += max(0, slots - max(na, nb)) * step
+        parked += max(0, min(na, slots) - nb) * step
+    tot = slots * (t_end - t_start)
+    return {"idle_frac": round(idle / tot, 3), "idle_no_trial_frac": round(searcher / tot, 3),
+            "idle_trial_without_container_frac": round(parked / tot, 3)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-length-batches", type=int, default=0,
@@ -108,6 +147,9 @@ def main() -> None:
     env_vars.append("PYTHONFAULTHANDLER=1")  # a crashing trial logs its Python stack
     if args.artificial_slots:
         env_vars.append("OMP_NUM_THREADS=1")  # N CPU trial processes share the host's cores
+        # a scheduler dry run: a 10k-record validation pass per rung on one CPU thread per trial
+        # would dominate the wall time it measures
+        cfg["hyperparameters"]["validation_records"] = 512
     busy = []
     stop = threading.Event()
 
@@ -157,6 +199,10 @@ def main() -> None:
                     f.write(f"==== trial {t['id']} state={t['state']} restarts={t.get('restarts')}\n")
                     f.write("\n".join(r.get("message", "").rstrip() for r in recs[-150:]) + "\n")
         slots = sum(len(a["slots"]) for a in cl.get("/agents"))
+        try:
+            idle = idle_breakdown(cl, e["trials"], slots, t0, t0 + wall)
+        except Exception as ex:  # diagnostics only
+            idle = {"error": f"{type(ex).__name__}: {ex}"[:200]}
         containers = timeline.pop("_containers", 0)
         occupancy = timeline.get("total", 0.0) * containers / max(1e-9, wall * slots)
         records = sum(t.get("total_batches_processed", 0) * t.get("hparams", {}).get("global_batch_size", 0)
@@ -167,7 +213,7 @@ def main() -> None:
                           "containers": containers, "train_records": records,
                           "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
                           "slot_occupancy": round(occupancy, 3), "scheduler_idle_frac": round(1 - occupancy, 3),
-                          "peak_busy_slots": peak_busy,
+                          "peak_busy_slots": peak_busy, "idle_breakdown": idle,
                           "zygote": not args.no_zygote, "per_container_s": timeline,
                           "hip_graph": bool((cfg.get("optimizations") or {}).get("hip_graph", False)),
                           "hip_graph_batches": (cfg.get("optimizations") or {}).get("hip_graph_batches", 1),

@@ -79,9 +79,10 @@ def bench(B, S, nh, hd=64, dt=torch.bfloat16, p=0.0, iters=30, Lk=None):
     from determined_1_amd.ops import _lib
 
     lib = _lib.get_lib()
-    for name, fn in (("native", native), ("native_2launch", native), ("sdpa", sdpa)):
-        # native: merged backward grid (default); native_2launch: dQ then dK/dV launches
-        lib.det_attn_set_bwd_merged(0 if name == "native_2launch" else -1)
+    for name, fn in (("native", native), ("native_2launch", native), ("native_merged", native), ("sdpa", sdpa)):
+        # native: the default (merged backward grid for small grids); native_2launch: dQ then dK/dV
+        # launches; native_merged: always merged
+        lib.det_attn_set_bwd_merged({"native": -1, "native_2launch": 0, "native_merged": 1}.get(name, -1))
         if GRAPH:
             if p > 0:
                 continue  # dropout RNG state is not graph-safe here

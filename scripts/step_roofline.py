@@ -30,20 +30,30 @@ def _bucket(nbytes: int) -> int:
     return max(1 << 20, 1 << int(nbytes).bit_length())  # power-of-two buckets
 
 
-def stream_tbs(dev, nbytes: int, kind: str) -> float:
-    """Device bandwidth of a pure read ("r": a sum over a freshly written buffer, as a producer kernel
-    leaves its output) or a pure write ("w": a fill) of ``nbytes`` (its power-of-two bucket)."""
+def stream_tbs(dev, nbytes: int, kind: str, lib=None) -> float:
+    """Device bandwidth of a pure read ("r") or a pure write ("w": a fill) of ``nbytes`` (its
+    power-of-two bucket), over a freshly written buffer (as a producer kernel leaves its output).
+    The read stream is det_bn_stats_train over a [M, 256] bf16 tensor (one read, per-block partial
+    sums out): torch's generic reduction reads at ~3-4 TB/s and would under-state the bound."""
     key = (kind, _bucket(nbytes))
     if key not in _BW:
         n = key[1] // 4
         a = torch.empty(n, dtype=torch.float32, device=dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        C = 256
+        M = key[1] // (2 * C)
+        f = torch.empty(6, C, dtype=torch.float32, device=dev)
+        nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ws = torch.empty(int(lib.det_bn_ws_elems(M, C)), dtype=torch.float32, device=dev) if kind == "r" else None
+        st = torch.cuda.current_stream().cuda_stream
         t = 0.0
         for _ in range(5):
             a.fill_(1.0)
             e0.record()
             if kind == "r":
-                a.sum()
+                lib.det_bn_stats_train(st, 1, a.data_ptr(), M, C, f[0].data_ptr(), f[1].data_ptr(), f[2].data_ptr(),
+                                       f[3].data_ptr(), nbt.data_ptr(), 0.1, 1e-5, f[4].data_ptr(), f[5].data_ptr(),
+                                       f[0].data_ptr(), f[1].data_ptr(), ws.data_ptr())
             else:
                 a.fill_(2.0)
             e1.record()
@@ -53,13 +63,13 @@ def stream_tbs(dev, nbytes: int, kind: str) -> float:
     return _BW[key]
 
 
-def ref_ms(dev, rb: int, wb: int) -> float:
+def ref_ms(dev, rb: int, wb: int, lib) -> float:
     """Time the same bytes take as a pure read plus a pure write of the same sizes."""
     ms = 0.0
     if rb:
-        ms += rb / (stream_tbs(dev, rb, "r") * 1e12) * 1e3
+        ms += rb / (stream_tbs(dev, rb, "r", lib) * 1e12) * 1e3
     if wb:
-        ms += wb / (stream_tbs(dev, wb, "w") * 1e12) * 1e3
+        ms += wb / (stream_tbs(dev, wb, "w", lib) * 1e12) * 1e3
     return ms
 
 
@@ -72,6 +82,7 @@ def main() -> None:
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = _lib.get_lib()
+    raw = lib  # (the same object; the reference runs while the wrappers are switched off)
     recs = []
     state = {"on": False}
 
@@ -292,7 +303,7 @@ def main() -> None:
         ms = sum(g[4].elapsed_time(g[5]) for g in grp) / len(grp)
         nb = rb + wb
         tbs = nb / (ms * 1e-3) / 1e12
-        rms = ref_ms(dev, rb, wb)
+        rms = ref_ms(dev, rb, wb, raw)
         rows.append((i, name, kind, nb, fl, ms, tbs, 100 * rms / ms, rms, fl / (ms * 1e-3) / 1e12 if fl else 0.0, rb, wb))
     fam = defaultdict(lambda: [0, 0.0, 0, 0.0, 0.0])
     for r in rows:

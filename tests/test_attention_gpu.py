@@ -198,6 +198,6 @@ def test_merged_backward_equals_two_launch_backward(gpu, dt, hd, B, nh, Lq, Lk, 
             out.backward(dy.to(gpu))
             res[merged] = [out.detach().clone()] + [t.grad.clone() for t in d_ins]
     finally:
-        lib.det_attn_set_bwd_merged(-1)
+        lib.det_attn_set_bwd_merged(-2)
     for name, a, b in zip(("out", "dq", "dk", "dv"), res[0], res[1]):
         assert torch.equal(a, b), name
