@@ -156,43 +156,53 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy
     const int t = p / g.W;
     const int h = t % g.H;
     const int n = t / g.H;
-    float acc[8];
+    const int64_t e = static_cast<int64_t>(p) * g.C + 8 * c8;
+    // every operand of the (at most 2 x 2) windows that contain this pixel is loaded up front, with no
+    // branch on loaded data (an argmax test before the dy load made each window two dependent
+    // round trips): windows oh with 2*oh-1 <= h <= 2*oh+1 -> oh in {(h+1)/2 - d : d = 0,1}
+    int64_t off[4];
+    bool ok[4];
+    uint8_t me[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    // windows oh with 2*oh-1 <= h <= 2*oh+1  ->  oh in {(h+1)/2 - 1 + d : d = 0,1} (>= 0, < Ho)
+    for (int q = 0; q < 4; ++q) {
+      const int oh = (h + 1) / 2 - (q >> 1), kh = h - (2 * oh - 1);
+      const int ow = (w + 1) / 2 - (q & 1), kw = w - (2 * ow - 1);
+      ok[q] = oh >= 0 && oh < g.Ho && kh >= 0 && kh <= 2 && ow >= 0 && ow < g.Wo && kw >= 0 && kw <= 2;
+      off[q] = ok[q] ? (static_cast<int64_t>(n * g.Ho + oh) * g.Wo + ow) * g.C + 8 * c8 : 0;
+      me[q] = static_cast<uint8_t>(3 * kh + kw);
+    }
+    uc8 av[4];
+    float d[4][8];
+    float xv[8];
+    if constexpr (BNB) Vec8<unsigned short>::load(bn.x + e, xv);
 #pragma unroll
-    for (int dh = 0; dh < 2; ++dh) {
-      const int oh = (h + 1) / 2 - dh;
-      const int kh = h - (2 * oh - 1);
-      if (oh < 0 || oh >= g.Ho || kh < 0 || kh > 2) continue;
-#pragma unroll
-      for (int dw = 0; dw < 2; ++dw) {
-        const int ow = (w + 1) / 2 - dw;
-        const int kw = w - (2 * ow - 1);
-        if (ow < 0 || ow >= g.Wo || kw < 0 || kw > 2) continue;
-        const int64_t o = (static_cast<int64_t>(n * g.Ho + oh) * g.Wo + ow) * g.C + 8 * c8;
-        const uc8 av = *reinterpret_cast<const uc8*>(idx + o);
-        const uint8_t me = static_cast<uint8_t>(3 * kh + kw);
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) any |= av[j] == me;
-        if (!any) continue;
-        float d[8];
-        Vec8<T>::load(dy + o, d);
+    for (int q = 0; q < 4; ++q) {
+      if (ok[q]) {
+        av[q] = *reinterpret_cast<const uc8*>(idx + off[q]);
+        Vec8<T>::load(dy + off[q], d[q]);
         if constexpr (kTwo) {
           float d2[8];
-          Vec8<T>::load(dy2 + o, d2);
+          Vec8<T>::load(dy2 + off[q], d2);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) d[j] += d2[j];
+          for (int j = 0; j < 8; ++j) d[q][j] += d2[j];
         }
+      } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += av[j] == me ? d[j] : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          av[q][j] = 0xff;
+          d[q][j] = 0.f;
+        }
       }
     }
-    const int64_t e = static_cast<int64_t>(p) * g.C + 8 * c8;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a += av[q][j] == me[q] ? d[q][j] : 0.f;
+      acc[j] = a;
+    }
     if constexpr (BNB) {
-      float xv[8];
-      Vec8<unsigned short>::load(bn.x + e, xv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float dm = __fmaf_rn(xv[j], sc[j], sh[j]) > 0.f ? acc[j] : 0.f;
