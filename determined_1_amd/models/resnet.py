@@ -223,9 +223,11 @@ class ResNet(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         _FWD.depth = getattr(_FWD, "depth", 0) + 1  # blocks may defer their output applies (see _FWD)
         try:
-            x = self.bn1(self._stem(x))
-            # the stem BN's output feeds only the pool: its backward partials come from the pool's
-            x = self.maxpool(x, bn_exclusive=True) if isinstance(self.maxpool, MaxPool3x3s2) else self.maxpool(x)
+            # the stem BN's output feeds only the pool: the pool applies it (forward) and writes its
+            # backward partials, unless a hook could observe that activation
+            pool_fused = isinstance(self.maxpool, MaxPool3x3s2)
+            x = self.bn1(self._stem(x), defer_affine=pool_fused and _quiet(self.bn1) and _quiet(self.maxpool))
+            x = self.maxpool(x, bn_exclusive=True) if pool_fused else self.maxpool(x)
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             _FWD.depth -= 1

@@ -108,7 +108,8 @@ _SIGNATURES = {
         c_int,
     ),
     # stream, dtype, x, y, idx(u8), N, H, W, C
-    "det_maxpool3s2_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 4, c_int),
+    # ... + bn_scale, bn_shift (nullable: the pooled tensor's BN + ReLU applied in the pool)
+    "det_maxpool3s2_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p] * 2, c_int),
     # stream, dtype, dy, idx(u8), dx, N, H, W, C
     # ... + bn_x, bn_mean, bn_scale, bn_shift, psum, psumx (nullable BN-backward epilogue)
     "det_maxpool3s2_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p] * 6,

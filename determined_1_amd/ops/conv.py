@@ -463,23 +463,26 @@ def materialize_fwd_apply(t: Optional[torch.Tensor]) -> None:
     FWD_APPLY_COUNTS["materialized"] += 1
 
 
-# Deferred affine BN apply (``DEFER_AFFINE_APPLY``): a training BN without ReLU or residual whose only
-# consumer is a residual BN(+ReLU) apply -- ResNet's projection-shortcut BN, read only by bn3 -- runs
-# only its finalize and returns its output unwritten, tagged ``_det_affine_apply = (x, scale, shift)``;
-# the consumer computes relu(bn3 + x * scale + shift) from x (det_norm.hip bn_apply_fwd RES 2, or
-# det_conv.hip AFWD when bn3's apply is itself deferred onto the next conv): the shortcut BN's apply
-# pass (read x, write y) and the consumer's read of y become one read of x.
+# Deferred affine BN apply (``DEFER_AFFINE_APPLY``): a training BN without residual whose only
+# consumer applies it itself runs only its finalize and returns its output unwritten, tagged
+# ``_det_affine_apply = (x, scale, shift, relu)``.  Consumers: a residual BN(+ReLU) apply for ResNet's
+# projection-shortcut BN (no ReLU, read only by bn3), which computes relu(bn3 + x * scale + shift)
+# from x (det_norm.hip bn_apply_fwd RES 2, or det_conv.hip AFWD when bn3's apply is itself deferred
+# onto the next conv); the stem max-pool for the stem BN + ReLU (det_pool.hip maxpool_fwd BNP).  The
+# BN's apply pass (read x, write y) and the consumer's read of y become one read of x.
 DEFER_AFFINE_APPLY = os.environ.get("DET_DEFER_AFFINE_APPLY", "1") != "0"
 AFFINE_APPLY_COUNTS = {"deferred": 0, "in_residual": 0, "materialized": 0}
 
 
 def materialize_affine_apply(t: torch.Tensor, aff) -> None:
-    """Write ``t = x * scale + shift`` (a deferred affine BN apply, see ``DEFER_AFFINE_APPLY``)."""
-    x, scale, shift = aff
+    """Write ``t = [relu](x * scale + shift)`` (a deferred BN apply without residual, see
+    ``DEFER_AFFINE_APPLY``)."""
+    x, scale, shift = aff[:3]
+    relu = len(aff) > 3 and bool(aff[3])
     m = x.numel() // x.shape[1]
     _lib.check(_lib.get_lib().det_bn_apply(_stream(x), 1 if x.dtype == torch.bfloat16 else 0, x.data_ptr(), None,
-                                           t.data_ptr(), int(m), int(x.shape[1]), scale.data_ptr(), shift.data_ptr(), 0),
-               "bn_apply")
+                                           t.data_ptr(), int(m), int(x.shape[1]), scale.data_ptr(), shift.data_ptr(),
+                                           int(relu)), "bn_apply")
     AFFINE_APPLY_COUNTS["materialized"] += 1
 
 

@@ -62,9 +62,14 @@ struct PoolGeom {
   int N, H, W, C, Ho, Wo;
 };
 
-template <typename T>
+// BNP: x is the input of the training BatchNorm + ReLU whose output is pooled (the ResNet stem); the
+// pool applies relu(x * scale + shift), rounded to bf16 exactly like det_norm.hip's apply, to each
+// window value, so that activation is never written to HBM or read back.
+template <typename T, bool BNP = false>
 __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x, T* __restrict__ y,
-                                                        uint8_t* __restrict__ idx, PoolGeom g, int nvec) {
+                                                        uint8_t* __restrict__ idx, PoolGeom g, int nvec,
+                                                        const float* __restrict__ bn_scale = nullptr,
+                                                        const float* __restrict__ bn_shift = nullptr) {
   const int cv = g.C / 8;
   // 32-bit index math (nvec < 2^31, checked by the host): 64-bit division is a long software sequence
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < nvec; i += gridDim.x * kThreads) {
@@ -76,6 +81,14 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x,
     // torch semantics: start from -inf with the window's first valid slot, take v if v > max
     // or v is NaN (the first NaN then sticks)
     const uint8_t slot0 = static_cast<uint8_t>(3 * (oh == 0 ? 1 : 0) + (ow == 0 ? 1 : 0));
+    float bsc[8], bsh[8];
+    if constexpr (BNP) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bsc[j] = bn_scale[8 * c8 + j];
+        bsh[j] = bn_shift[8 * c8 + j];
+      }
+    }
     float m[8];
     uint8_t a[8];
 #pragma unroll
@@ -93,6 +106,11 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x,
         if (w < 0 || w >= g.W) continue;
         float v[8];
         Vec8<T>::load(x + ((static_cast<int64_t>(n) * g.H + h) * g.W + w) * g.C + 8 * c8, v);
+        if constexpr (BNP) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = __uint_as_float(static_cast<uint32_t>(f2bf(fmaxf(__fmaf_rn(v[j], bsc[j], bsh[j]), 0.f))) << 16);
+        }
         const uint8_t slot = static_cast<uint8_t>(3 * kh + kw);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -247,13 +265,21 @@ extern "C" {
 
 // x [N, H, W, C] (channels_last) -> y [N, Ho, Wo, C], idx [N, Ho, Wo, C] uint8 (window slot 0..8).
 // dtype 0 = fp32, 1 = bf16; C % 8 == 0.  Ho = (H - 1) / 2 + 1 (kernel 3, stride 2, pad 1).
-int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t* idx, int N, int H, int W, int C) {
+// bn_scale / bn_shift (nullable, bf16 only): x is the input of a BatchNorm + ReLU and the pool reads
+// relu(x * scale + shift) (the BN's apply deferred into the pool, maxpool_fwd BNP).
+int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t* idx, int N, int H, int W, int C,
+                       const float* bn_scale, const float* bn_shift) {
   if (C % 8 != 0 || N <= 0 || H <= 0 || W <= 0) return -1;
+  if ((bn_scale == nullptr) != (bn_shift == nullptr) || (bn_scale && dtype != 1)) return -2;
   PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
   const int64_t nvec = static_cast<int64_t>(N) * g.Ho * g.Wo * (C / 8);
   if (nvec >= (static_cast<int64_t>(1) << 31)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (dtype == 1)
+  if (dtype == 1 && bn_scale)
+    hipLaunchKernelGGL((maxpool_fwd<unsigned short, true>), dim3(grid_for(nvec)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g,
+                       static_cast<int>(nvec), bn_scale, bn_shift);
+  else if (dtype == 1)
     hipLaunchKernelGGL(maxpool_fwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g,
                        static_cast<int>(nvec));

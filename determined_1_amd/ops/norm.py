@@ -98,9 +98,10 @@ class _BNActTrain(torch.autograd.Function):
             _conv.materialize_affine_apply(residual, res_affine)
             res_affine = None
         res_src, rs, rh = (residual, None, None) if res_affine is None else res_affine
-        # defer_affine: a BN without ReLU or residual whose only consumer is a residual BN apply that
-        # takes res_affine (ResNet's projection-shortcut BN): finalize only, the output stays unwritten
-        defer_affine = bool(defer_affine and parts is not None and not relu and residual is None
+        # defer_affine: a BN without residual whose only consumer applies it itself -- a residual BN
+        # apply taking res_affine (ResNet's projection-shortcut BN, no ReLU) or the max-pool forward
+        # (the stem BN + ReLU): finalize only, the output stays unwritten
+        defer_affine = bool(defer_affine and parts is not None and residual is None
                             and x.dtype == torch.bfloat16 and fmt == torch.channels_last)
         if parts is not None:
             pm, pq, rpb = parts
@@ -143,7 +144,7 @@ class _BNActTrain(torch.autograd.Function):
             _DEFERRED["last"] = (y.data_ptr(), (x, res_src, stats[2], stats[3], mbits, rs, rh))
             _conv.FWD_APPLY_COUNTS["deferred"] += 1
         elif defer_affine:
-            _DEFERRED["last"] = (y.data_ptr(), ("affine", x, stats[2], stats[3]))
+            _DEFERRED["last"] = (y.data_ptr(), ("affine", x, stats[2], stats[3], bool(relu)))
             _conv.AFFINE_APPLY_COUNTS["deferred"] += 1
         if res_affine is not None:
             _conv.AFFINE_APPLY_COUNTS["in_residual"] += 1
@@ -366,10 +367,10 @@ def bn_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: Optio
     # fused training path runs; anything else materialises it
     aff = getattr(residual, "_det_affine_apply", None) if residual is not None else None
     res_affine = None
-    if (aff is not None and _nhwc_ok(x) and res_ok and use_batch_stats and relu and not shortcut_link
+    if (aff is not None and not aff[3] and _nhwc_ok(x) and res_ok and use_batch_stats and relu and not shortcut_link
             and x.dtype == torch.bfloat16 and residual.dtype == x.dtype):
         residual._det_affine_apply = None
-        res_affine = aff
+        res_affine = aff[:3]
     else:
         _conv.materialize_fwd_apply(residual)
     if _nhwc_ok(x) and res_ok:

@@ -19,6 +19,7 @@ LINKED = {"count": 0}  # backward passes that summed a linked shortcut gradient
 # maxpool_bwd BNB), so the BN backward skips its partial pass over the largest activation
 FUSE_BN_BWD = os.environ.get("DET_POOL_BN_BWD", "1") != "0"
 BN_BWD_COUNTS = {"fused": 0}
+BN_FWD_COUNTS = {"in_pool": 0}  # forwards that applied the producer's deferred BN + ReLU
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 
 
@@ -41,14 +42,18 @@ def _ok(x: torch.Tensor) -> bool:
 
 class _MaxPool3s2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bn_producer=None):
+    def forward(ctx, x, bn_producer=None, bn_apply=None):
         N, C, H, W = x.shape
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         idx = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device)
         st = torch._C._cuda_getCurrentRawStream(x.device.index)
-        _lib.check(_lib.get_lib().det_maxpool3s2_fwd(st, _DT[x.dtype], x.data_ptr(), y.data_ptr(), idx.data_ptr(),
-                                                     N, H, W, C), "det_maxpool3s2_fwd")
+        # bn_apply = (bn_x, scale, shift): x is the unwritten output of the producing BN + ReLU, which
+        # the pool applies to each window value itself (ops/conv.py DEFER_AFFINE_APPLY)
+        src, sc, sh = (x, None, None) if bn_apply is None else bn_apply
+        _lib.check(_lib.get_lib().det_maxpool3s2_fwd(st, _DT[x.dtype], src.data_ptr(), y.data_ptr(), idx.data_ptr(),
+                                                     N, H, W, C, None if sc is None else sc.data_ptr(),
+                                                     None if sh is None else sh.data_ptr()), "det_maxpool3s2_fwd")
         ctx.save_for_backward(idx)
         ctx.shape = (N, C, H, W)
         ctx.extra_dy = None  # set by a linked shortcut consumer (ops/norm.py linked_conv2d)
@@ -95,17 +100,26 @@ class _MaxPool3s2(torch.autograd.Function):
             # dx is the masked gradient; the BN backward finalizes these partials (ops/norm.py fused_bwd)
             prod.fused_bwd = (psum, psumx, rpb)
             BN_BWD_COUNTS["fused"] += 1
-        return dx, None
+        return dx, None, None
 
 
 def max_pool_3x3s2(x: torch.Tensor, bn_exclusive: bool = False) -> torch.Tensor:
     """``F.max_pool2d(x, 3, 2, 1)``.  ``bn_exclusive``: this pool is the only autograd consumer of
     ``x``, the output of a fused BatchNorm+ReLU, whose backward partials can then come from the
     pool's backward (``FUSE_BN_BWD``)."""
+    aff = getattr(x, "_det_affine_apply", None)
+    if aff is not None and not (bn_exclusive and _ok(x) and aff[3] and x.dtype == torch.bfloat16):
+        from determined_1_amd.ops.conv import materialize_fwd_apply
+
+        materialize_fwd_apply(x)  # a deferred BN apply this pool cannot stage
+        aff = None
     if _ok(x):
         # (decided here: autograd runs Function.forward with grad mode off)
         prod = _bn_producer(x) if (bn_exclusive and torch.is_grad_enabled()) else None
-        return _MaxPool3s2.apply(x, prod)
+        if aff is not None:
+            x._det_affine_apply = None
+            BN_FWD_COUNTS["in_pool"] += 1
+        return _MaxPool3s2.apply(x, prod, None if aff is None else aff[:3])
     if x.device.type == "cuda":
         FALLBACKS["count"] += 1
     return F.max_pool2d(x, 3, 2, 1)

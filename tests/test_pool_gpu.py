@@ -117,9 +117,10 @@ def test_maxpool_bn_backward_epilogue(gpu, N, C, H, W, monkeypatch):
 
 
 def test_stem_chain_defers_bn_apply_into_patch_wgrad(gpu):
-    """ResNet stem: conv -> BN + ReLU -> pool.  The pool's backward writes the BN partials, the BN
-    backward only finalizes, and the stem weight gradient stages the BN apply (stemp_wgrad ABN).
-    The weight gradient matches the same chain with both fusions off."""
+    """ResNet stem: conv -> BN + ReLU -> pool.  The pool applies the BN + ReLU while reading its
+    windows (the activation is never written), its backward writes the BN partials, the BN backward
+    only finalizes, and the stem weight gradient stages the BN's backward apply (stemp_wgrad ABN).
+    Pooled output bit-equal, weight gradient close to the same chain with the fusions off."""
     from determined_1_amd.models import resnet
     from determined_1_amd.ops import conv as convops
 
@@ -132,20 +133,24 @@ def test_stem_chain_defers_bn_apply_into_patch_wgrad(gpu):
         for mod in m.modules():
             if isinstance(mod, torch.nn.BatchNorm2d):
                 mod.float()
-        old = (pool.FUSE_BN_BWD, convops.DEFER_BN_APPLY)
-        pool.FUSE_BN_BWD = convops.DEFER_BN_APPLY = fused
+        old = (pool.FUSE_BN_BWD, convops.DEFER_BN_APPLY, convops.DEFER_AFFINE_APPLY)
+        pool.FUSE_BN_BWD = convops.DEFER_BN_APPLY = convops.DEFER_AFFINE_APPLY = fused
+        resnet._FWD.depth = 1  # as inside ResNet.forward
         try:
             x = img.to(gpu, torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            y = m.maxpool(m.bn1(m._stem(x)), bn_exclusive=True)
+            y = m.maxpool(m.bn1(m._stem(x), defer_affine=True), bn_exclusive=True)
             (y.float() * torch.linspace(-1, 1, y.numel(), device=gpu).view_as(y)).sum().backward()
         finally:
-            pool.FUSE_BN_BWD, convops.DEFER_BN_APPLY = old
-        return m.conv1.weight.grad.float().cpu(), m.bn1.weight.grad.cpu()
+            pool.FUSE_BN_BWD, convops.DEFER_BN_APPLY, convops.DEFER_AFFINE_APPLY = old
+            resnet._FWD.depth = 0
+        return m.conv1.weight.grad.float().cpu(), m.bn1.weight.grad.cpu(), y.detach().cpu()
 
-    before = (pool.BN_BWD_COUNTS["fused"], convops.BN_APPLY_COUNTS["in_gemm"])
-    wf, gf = run(True)
+    before = (pool.BN_BWD_COUNTS["fused"], convops.BN_APPLY_COUNTS["in_gemm"], pool.BN_FWD_COUNTS["in_pool"])
+    wf, gf, yf = run(True)
     assert pool.BN_BWD_COUNTS["fused"] == before[0] + 1
     assert convops.BN_APPLY_COUNTS["in_gemm"] == before[1] + 1, "the stem wgrad did not stage the BN apply"
-    wu, gu = run(False)
+    assert pool.BN_FWD_COUNTS["in_pool"] == before[2] + 1, "the pool did not apply the stem BN"
+    wu, gu, yu = run(False)
+    assert torch.equal(yf, yu)  # the pool's BN + ReLU rounds exactly like the materialised apply
     torch.testing.assert_close(wf, wu, atol=2e-2 * float(wu.abs().max()), rtol=2e-2)
     torch.testing.assert_close(gf, gu, atol=1e-3, rtol=1e-3)
