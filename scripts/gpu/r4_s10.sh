@@ -20,6 +20,6 @@ head -3 $O/steady.txt
 rm -rf $O/prof
 for cfg in "gb20:" "o0:--amp O0"; do
   name=${cfg%%:*}; args=${cfg#*:}
-  DET_BENCH_LOGDIR=$O/asha_$name timeout -k 10 360 python -u scripts/bench_asha.py --slots 1 $args > $O/asha_$name.json 2> $O/asha_$name.err || { tail -30 $O/asha_$name.err; exit 1; }
+  mkdir -p $O/asha_$name && DET_BENCH_LOGDIR=$O/asha_$name timeout -k 10 360 python -u scripts/bench_asha.py --slots 1 $args > $O/asha_$name.json 2> $O/asha_$name.err || { tail -30 $O/asha_$name.err; exit 1; }
   echo "asha $name $(cut -c1-300 $O/asha_$name.json)"
 done
