@@ -176,6 +176,8 @@ _SIGNATURES = {
     "det_conv3p_wgrad_ws_elems": ([c_i64, c_int, c_int], c_i64),
     "det_stemp_wgrad_ws_elems": ([c_i64], c_i64),
     # stream, dY, X4, out, out_dtype, M, Hi, Wi, Ho, Wo, ws, out_scale, bn_x, coef (nullable deferred BN apply)
+    "det_stemp_fwd": ([c_void_p] * 4 + [c_i64] + [c_int] * 4 + [c_void_p] * 2, c_int),
+    "det_stemp_fwd_rows_per_block": ([], c_int),
     "det_stemp_wgrad": ([c_void_p] * 4 + [c_int, c_i64] + [c_int] * 4 + [c_void_p, c_float] + [c_void_p] * 2, c_int),
     # stream, dY, X, out, out_dtype, Nb, H, W, Cin, N, ws, out_scale
     "det_conv3p_wgrad": ([c_void_p] * 4 + [c_int] * 6 + [c_void_p, c_float], c_int),

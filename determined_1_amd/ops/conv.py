@@ -926,6 +926,11 @@ STEM_NATIVE_WGRAD = False
 # Stem weight gradient on the patch kernel (det_igemm.hip stemp_wgrad: dY and the input rows of a
 # 256-pixel chunk staged once, transposed operand reads straight from the patch), ahead of both.
 STEM_PATCH_WGRAD = os.environ.get("DET_STEM_PATCH_WGRAD", "1") != "0"
+# Stem forward on the patch kernel (det_igemm.hip stemp_fwd: the input rows of a 256-pixel chunk
+# staged once in LDS, weights resident) instead of det_conv's gathering implicit GEMM (GM_STEM);
+# bit-identical outputs, statistics partials per 256 rows.
+STEM_PATCH_FWD = os.environ.get("DET_STEM_PATCH_FWD", "1") != "0"
+STEM_FWD_COUNTS = {"patch": 0, "gemm": 0}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -966,17 +971,29 @@ class _StemConv(torch.autograd.Function):
         m = n * ho * wo
         wk = pack_stem_weight(weight)
         y = torch.empty((n, 64, ho, wo), dtype=torch.bfloat16, device=x4.device, memory_format=torch.channels_last)
-        parts = None
-        pm = pq = None
-        if stats:
-            rpb = rows_per_block(64)
+        lib = _lib.get_lib()
+
+        def partials(rpb):
+            if not stats:
+                return None, None, None
             nrb = (m + rpb - 1) // rpb
             pm = torch.empty(nrb, 64, dtype=torch.float32, device=x4.device)
             pq = torch.empty(nrb, 64, dtype=torch.float32, device=x4.device)
-            parts = (pm, pq, rpb)
-        _lib.check(_lib.get_lib().det_stem_conv_fwd(_stream(x4), x4.data_ptr(), wk.data_ptr(), y.data_ptr(), int(m),
-                                                    int(hi), int(wi), int(ho), int(wo), _ptr(pm), _ptr(pq)),
-                   "stem_conv_fwd")
+            return pm, pq, (pm, pq, rpb)
+
+        rc = -6
+        if STEM_PATCH_FWD:
+            pm, pq, parts = partials(int(lib.det_stemp_fwd_rows_per_block()))
+            rc = lib.det_stemp_fwd(_stream(x4), x4.data_ptr(), wk.data_ptr(), y.data_ptr(), int(m), int(hi), int(wi),
+                                   int(ho), int(wo), _ptr(pm), _ptr(pq))
+            if rc != -6:
+                _lib.check(rc, "stemp_fwd")
+                STEM_FWD_COUNTS["patch"] += 1
+        if rc == -6:  # the gathering GEMM (any width)
+            pm, pq, parts = partials(rows_per_block(64))
+            _lib.check(lib.det_stem_conv_fwd(_stream(x4), x4.data_ptr(), wk.data_ptr(), y.data_ptr(), int(m), int(hi),
+                                             int(wi), int(ho), int(wo), _ptr(pm), _ptr(pq)), "stem_conv_fwd")
+            STEM_FWD_COUNTS["gemm"] += 1
         _attach_partials(y, parts)
         ctx.save_for_backward(x4, weight)
         # the stem BatchNorm may defer its backward apply onto this node (take_pending_apply): the

@@ -1759,6 +1759,188 @@ void launch_wg(hipStream_t st, const WgArgs& a, int nwg) {
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------------
+// stemp_fwd: the ResNet stem forward Y[M, 64] = im2col(X) . W^T (7x7 / stride 2 / pad 3 over
+// 4-channel NHWC images, W packed k = r*32 + s*4 + c) on stemp_wgrad's input patch.  The implicit
+// GEMM of det_conv (GM_STEM) gathers every A fragment from global memory -- each input pixel is
+// fetched ~12 times (49 taps / stride 4) through L2 and the MFMAs wait on it (0.58 ms/step at batch
+// 512, 27 % of the bandwidth bound).  Here a block stages the <= 14 padded input rows of a 256-pixel
+// chunk once into LDS; an A fragment (row m, k-group g of k-step r) is then the 16 contiguous bytes
+// of padded pixels (2 ho + r, 2 wo + 2g .. 2g + 1) -- two 8-B LDS reads, no transposes.  The weights
+// (32 KB) stay resident in LDS for the whole run: persistent blocks walk a contiguous range of chunks
+// (the next chunk's halo rows are this chunk's, so their re-read hits L2), prefetching the next
+// patch into registers under the MFMAs.  The k order (8 steps of 32) is the GEMM kernel's, so the
+// outputs are bit-identical to det_stem_conv_fwd.  Epilogue: BN statistics partials per 256 rows
+// (det_stats.h) and a C tile restaged in LDS for coalesced 16-B row stores.
+// Wave w: rows 32 w .. +32, all 64 filters (2 x 4 MFMA 16x16x32 tiles).
+// ------------------------------------------------------------------------------------------------
+struct SfArgs {
+  const unsigned short* X;  // [Nb, Hi, Wi, 4]
+  const unsigned short* W;  // [64, 256] packed
+  unsigned short* Y;        // [M, 64]
+  float* pmean;             // [ceil(M / 256), 64] (nullable, with pm2)
+  float* pm2;
+  int64_t M;
+  int Hi, Wi, Ho, Wo;
+  int chunks_per_block;
+};
+constexpr int kSfLDC = 72;                     // C tile row pitch (elements): 16-B stores conflict-free
+constexpr int kSfU = 256 * kSfLDC * 2;         // patch + prow while computing, the C tile after
+static_assert(kSpPMAX * 8 + 256 * 4 <= kSfU, "patch region");
+constexpr int kSfSMEM = 64 * 256 * 2 + kSfU + 3 * 8 * 64 * 4;  // weights | patch / C tile | stats
+
+template <bool STATS>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) stemp_fwd_kernel(SfArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((ext_vector_type(4))) unsigned short us4;
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  constexpr int NT = 512, XCH = (kSpPMAX * 8 / 16 + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* wl = smem;
+  unsigned char* xps = smem + 64 * 256 * 2;
+  int* prow = reinterpret_cast<int*>(xps + kSpPMAX * 8);
+  unsigned short* ct = reinterpret_cast<unsigned short*>(xps);
+  float* red = reinterpret_cast<float*>(smem + 64 * 256 * 2 + kSfU);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int64_t nch = (a.M + 255) / 256;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * a.chunks_per_block;
+  int64_t c1 = c0 + a.chunks_per_block;
+  if (c1 > nch) c1 = nch;
+  if (c0 >= c1) return;  // uniform over the block, before any barrier
+  const int Hp = a.Hi + 6, Wp = a.Wi + 6;
+  const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
+
+  // the weights, [k-step][filter][4 x 16 B] swizzled: 2048 16-B pieces
+#pragma unroll
+  for (int q = 0; q < 64 * 32 / NT; ++q) {
+    const int idx = tid + q * NT, n = idx >> 5, ch = idx & 31;
+    *reinterpret_cast<us8*>(wl + (ch >> 2) * 4096 + swz64(n, ch & 3)) =
+        *reinterpret_cast<const us8*>(a.W + n * 256 + ch * 8);
+  }
+  us8 rx[XCH];
+  auto geom = [&](int64_t m0, int& g0, int& rows) {
+    int64_t ml = m0 + 255;
+    if (ml >= a.M) ml = a.M - 1;
+    const int64_t na = m0 / hw, nb = ml / hw;
+    g0 = static_cast<int>(na * Hp + 2 * ((m0 - na * hw) / a.Wo));
+    rows = static_cast<int>(nb * Hp + 2 * ((ml - nb * hw) / a.Wo) + 7) - g0 + 1;
+  };
+  auto gload = [&](int64_t m0) {
+    int g0, rows;
+    geom(m0, g0, rows);
+    const int npc = (rows * Wp + 1) / 2;  // 16-B pieces = 2 padded pixels of 4 channels
+#pragma unroll
+    for (int q = 0; q < XCH; ++q) {
+      const int idx = tid + q * NT;
+      us8 v = us8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (idx < npc) {
+        // one division pair per piece: the second pixel is the first's right neighbour
+        const int pp0 = 2 * idx, q0 = pp0 / Wp;
+        int gr = g0 + q0, wp = pp0 - q0 * Wp, n = gr / Hp, h = gr - n * Hp - 3;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          if (h2 == 1 && ++wp == Wp) {
+            wp = 0;
+            if (++h == a.Hi + 3) {
+              h = -3;
+              ++n;
+            }
+          }
+          const int x = wp - 3;
+          if (pp0 + h2 < rows * Wp && h >= 0 && h < a.Hi && x >= 0 && x < a.Wi) {
+            const us4 px = *reinterpret_cast<const us4*>(a.X + ((static_cast<int64_t>(n) * a.Hi + h) * a.Wi + x) * 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[h2 * 4 + j] = px[j];
+          }
+        }
+      }
+      rx[q] = v;
+    }
+  };
+  auto lstore = [&](int64_t m0) {
+    int g0, rows;
+    geom(m0, g0, rows);
+    const int npc = (rows * Wp + 1) / 2;
+#pragma unroll
+    for (int q = 0; q < XCH; ++q) {
+      const int idx = tid + q * NT;
+      if (idx < npc) *reinterpret_cast<us8*>(xps + idx * 16) = rx[q];
+    }
+    if (tid < 256) {  // padded-patch pixel (row 2 ho, col 2 wo) of output pixel m0 + tid
+      const int64_t m = m0 + tid;
+      int r = 0;
+      if (m < a.M) {
+        const int64_t n = m / hw;
+        const int rem = static_cast<int>(m - n * hw);
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+        r = static_cast<int>(n * Hp + 2 * ho - g0) * Wp + 2 * wo;
+      }
+      prow[tid] = r;
+    }
+  };
+
+  gload(c0 * 256);
+  lstore(c0 * 256);
+  __syncthreads();
+  for (int64_t c = c0; c < c1; ++c) {
+    const int64_t m0 = c * 256;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int pr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) pr[i] = prow[w * 32 + i * 16 + (lane & 15)] + 2 * g;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      bf16x8 fa[2], fb[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // 8-B aligned only (odd Wp): two 8-B reads
+        const unsigned char* p = xps + (pr[i] + ks * Wp) * 8;
+        const s16x4 lo = *reinterpret_cast<const s16x4*>(p), hi = *reinterpret_cast<const s16x4*>(p + 8);
+        fa[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(wl + ks * 4096 + swz64(j * 16 + (lane & 15), g));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // one k-step's fragments in flight (registers)
+    }
+    __syncthreads();  // every wave is done with the patch: the C tile overlays it
+    const int64_t rows_left = a.M - m0;
+    const int nvalid = rows_left < 256 ? static_cast<int>(rows_left) : 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ct[(w * 32 + i * 16 + g * 4 + r) * kSfLDC + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+    if constexpr (STATS)
+      det_block_bn_stats<2, 4, 8, 32, 64, 64>(acc, red, w, 0, lane, tid, nvalid, a.pmean, a.pm2, c * 64);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 256 * 8 / NT; ++q) {
+      const int idx = tid + q * NT, row = idx >> 3, cc = idx & 7;
+      if (row < nvalid)
+        *reinterpret_cast<us8*>(a.Y + (m0 + row) * 64 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * kSfLDC + cc * 8);
+    }
+    if (c + 1 < c1) {
+      // the next chunk's patch: fetched here, not under the MFMAs or the epilogue (both spill at
+      // 4 waves / SIMD); the other block on the CU computes meanwhile
+      gload(m0 + 256);
+      __syncthreads();  // the C tile is consumed before the next patch lands there
+      lstore(m0 + 256);
+      __syncthreads();
+    }
+  }
+#endif
+}
+
 extern "C" {
 
 // fp32 workspace elements det_igemm_wgrad needs for an [N, R*S*Cin] output from M pixels.
@@ -1873,6 +2055,8 @@ int det_conv3p_wgrad(void* stream, const void* dY, const void* X, void* out, int
   return static_cast<int>(hipGetLastError());
 }
 
+static bool sp_patch_fits(int64_t M, int Hi, int Wi, int Ho, int Wo);
+
 static int sp_splits(int64_t M) {
   int64_t s = 256;
   const int64_t max_s = (M + 4095) / 4096;  // >= 16 chunks of 256 pixels per block
@@ -1890,7 +2074,8 @@ int64_t det_stemp_wgrad_ws_elems(int64_t M) { return static_cast<int64_t>(sp_spl
 int det_stemp_wgrad(void* stream, const void* dY, const void* X, void* out, int out_dtype, int64_t M, int Hi, int Wi,
                     int Ho, int Wo, float* ws, float out_scale, const void* bn_x, const float* coef) {
   if (M <= 0 || Hi <= 0 || Wi <= 0 || Ho != (Hi - 1) / 2 + 1 || Wo != (Wi - 1) / 2 + 1) return -1;
-  if (Wi + 6 > 240) return -6;
+  if (M % (static_cast<int64_t>(Ho) * Wo) != 0) return -1;
+  if (!sp_patch_fits(M, Hi, Wi, Ho, Wo)) return -6;
   if ((bn_x == nullptr) != (coef == nullptr)) return -2;
   if (((reinterpret_cast<uintptr_t>(dY) | reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(bn_x)) & 15) != 0)
     return -5;
@@ -1918,6 +2103,60 @@ int det_stemp_wgrad(void* stream, const void* dY, const void* X, void* out, int 
   else
     hipLaunchKernelGGL(wg_reduce_kernel<float>, dim3(grid), dim3(256), 0, st, ws, real, slab, out_scale,
                        static_cast<float*>(out), E);
+  return static_cast<int>(hipGetLastError());
+}
+
+// Host side: do the input rows of every 256-pixel chunk fit the stem patch (kSpPMAX pixels)?  A
+// chunk that straddles two images spans both images' rows plus the padding between them; cached
+// per shape (one pass over the chunks, the first call of a shape only).
+static bool sp_patch_fits(int64_t M, int Hi, int Wi, int Ho, int Wo) {
+  thread_local int64_t key_m = -1;
+  thread_local int key_h = -1, key_w = -1;
+  thread_local bool key_ok = false;
+  if (M == key_m && Hi == key_h && Wi == key_w) return key_ok;
+  const int64_t Hp = Hi + 6, Wp = Wi + 6, hw = static_cast<int64_t>(Ho) * Wo;
+  bool ok = Wp <= 240;
+  for (int64_t m0 = 0; ok && m0 < M; m0 += 256) {
+    int64_t ml = m0 + 255;
+    if (ml >= M) ml = M - 1;
+    const int64_t na = m0 / hw, nb = ml / hw;
+    const int64_t rows = nb * Hp + 2 * ((ml - nb * hw) / Wo) + 8 - (na * Hp + 2 * ((m0 - na * hw) / Wo));
+    ok = rows * Wp <= kSpPMAX;
+  }
+  key_m = M;
+  key_h = Hi;
+  key_w = Wi;
+  key_ok = ok;
+  return ok;
+}
+
+int det_stemp_fwd_rows_per_block() { return 256; }
+
+// ResNet stem convolution on the patch kernel above (same contract as det_conv's det_stem_conv_fwd,
+// except that the statistics partials pmean / pm2 are per det_stemp_fwd_rows_per_block() rows).
+// -6: a chunk's input rows do not fit the patch (very wide images) -- use det_stem_conv_fwd.
+int det_stemp_fwd(void* stream, const void* X, const void* W, void* Y, int64_t M, int Hi, int Wi, int Ho, int Wo,
+                  float* pmean, float* pm2) {
+  if (M <= 0 || Hi <= 0 || Wi <= 0 || Ho != (Hi - 1) / 2 + 1 || Wo != (Wi - 1) / 2 + 1) return -1;
+  if (M % (static_cast<int64_t>(Ho) * Wo) != 0) return -1;
+  if ((pmean == nullptr) != (pm2 == nullptr)) return -2;
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y)) & 15) != 0)
+    return -5;
+  if (!sp_patch_fits(M, Hi, Wi, Ho, Wo)) return -6;
+  const int64_t nch = (M + 255) / 256;
+  // two blocks per CU over 256 CUs; at least 4 chunks a block so the weight staging amortises
+  int64_t blocks = 512;
+  if (blocks > (nch + 3) / 4) blocks = (nch + 3) / 4;
+  const int64_t cpb = (nch + blocks - 1) / blocks;
+  if (cpb >= (static_cast<int64_t>(1) << 30)) return -4;
+  blocks = (nch + cpb - 1) / cpb;
+  SfArgs a{static_cast<const unsigned short*>(X), static_cast<const unsigned short*>(W), static_cast<unsigned short*>(Y),
+           pmean, pm2, M, Hi, Wi, Ho, Wo, static_cast<int>(cpb)};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (pmean)
+    hipLaunchKernelGGL(stemp_fwd_kernel<true>, dim3(static_cast<unsigned>(blocks)), dim3(512), kSfSMEM, st, a);
+  else
+    hipLaunchKernelGGL(stemp_fwd_kernel<false>, dim3(static_cast<unsigned>(blocks)), dim3(512), kSfSMEM, st, a);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -264,7 +264,7 @@ def main() -> None:
                         ("det_conv_nt_bnbwd", conv_nt_bnbwd), ("det_conv_tn", conv_tn), ("det_conv_wgrad", conv_wgrad),
                         ("det_igemm_wgrad", igemm_wgrad), ("det_igemm_conv_cfg", igemm_conv),
                         ("det_igemm_conv_bnbwd", igemm_bnbwd), ("det_igemm_dgrad_s2", dgrad_s2), ("det_conv3p", conv3p),
-                        ("det_conv3p_wgrad", conv3p_wgrad), ("det_stem_conv_fwd", stem_fwd), ("det_stemp_wgrad", stemp),
+                        ("det_conv3p_wgrad", conv3p_wgrad), ("det_stem_conv_fwd", stem_fwd), ("det_stemp_fwd", stem_fwd), ("det_stemp_wgrad", stemp),
                         ("det_conv_dgrad_weight", dgrad_weight), ("det_maxpool3s2_fwd", maxpool_fwd),
                         ("det_maxpool3s2_bwd", maxpool_bwd)]:
         wrap(name, model)

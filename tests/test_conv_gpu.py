@@ -329,6 +329,56 @@ def test_stem_patch_wgrad_exact_on_integer_operands(gpu, n, h, w):
     torch.testing.assert_close(conv.unpack_stem_grad(out, 4).cpu(), ref2, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9), (5, 57, 57), (2, 225, 225)])
+def test_stem_patch_fwd_bit_identical_to_gemm(gpu, n, h, w):
+    """det_stemp_fwd (the chunk's input rows staged once in LDS, weights resident, persistent
+    blocks) == det_stem_conv_fwd (gathering implicit GEMM) bit for bit -- same k order -- including
+    chunks that straddle two images; its 256-row statistics partials merge to the output's."""
+    from determined_1_amd.ops import _lib
+
+    torch.manual_seed(n + h + w)
+    lib = _lib.get_lib()
+    x = torch.randn(n, 4, h, w, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = conv.pack_stem_weight((torch.randn(64, 4, 7, 7, device=gpu) * 0.1).to(torch.bfloat16))
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    m = n * ho * wo
+    s = torch.cuda.current_stream().cuda_stream
+    y0 = torch.empty(m, 64, dtype=torch.bfloat16, device=gpu)
+    y1 = torch.full((m, 64), float("nan"), dtype=torch.bfloat16, device=gpu)
+    _lib.check(lib.det_stem_conv_fwd(s, x.data_ptr(), wt.data_ptr(), y0.data_ptr(), m, h, w, ho, wo, None, None), "gemm")
+    rpb = int(lib.det_stemp_fwd_rows_per_block())
+    nrb = (m + rpb - 1) // rpb
+    pm = torch.empty(nrb, 64, dtype=torch.float32, device=gpu)
+    pq = torch.empty(nrb, 64, dtype=torch.float32, device=gpu)
+    _lib.check(lib.det_stemp_fwd(s, x.data_ptr(), wt.data_ptr(), y1.data_ptr(), m, h, w, ho, wo, pm.data_ptr(),
+                                 pq.data_ptr()), "stemp_fwd")
+    assert torch.equal(y0, y1)
+    mean, var = _merge(pm, pq, rpb, m)
+    yb = y1.double().cpu()
+    torch.testing.assert_close(mean, yb.mean(0), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(var, yb.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
+
+
+def test_stem_patch_fwd_wide_images_fall_back(gpu):
+    """Images too wide for the stem patch: det_stemp_fwd declines (-6) and stem_conv takes the
+    gathering GEMM."""
+    from determined_1_amd.ops import _lib
+
+    x = torch.randn(1, 3, 9, 480, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    cv = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(gpu).to(torch.bfloat16)
+    lib = _lib.get_lib()
+    x4 = conv.pad_channels4(x)
+    wt = conv.pack_stem_weight(cv.weight)
+    y = torch.empty(5 * 240, 64, dtype=torch.bfloat16, device=gpu)
+    assert lib.det_stemp_fwd(torch.cuda.current_stream().cuda_stream, x4.data_ptr(), wt.data_ptr(), y.data_ptr(),
+                             5 * 240, 9, 480, 5, 240, None, None) == -6
+    before = dict(conv.STEM_FWD_COUNTS)
+    out = conv.stem_conv(x, cv)
+    assert conv.STEM_FWD_COUNTS["gemm"] == before["gemm"] + 1
+    ref = torch.nn.functional.conv2d(x.float(), cv.weight.float(), stride=2, padding=3)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
 def test_u8_normalize_pad4(gpu):
     from determined_1_amd.ops.functional import u8_normalize
 
