@@ -13,11 +13,20 @@ for i in 1 2; do
   timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_$i.json 2> $O/bench_$i.err || { tail -30 $O/bench_$i.err; exit 1; }
   echo "bench $i $(python3 -c "import json;d=json.load(open('$O/bench_$i.json'));print(d['value'],d['ms_per_step'])")"
 done
+DET_STEM_PATCH_FWD=0 timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_stemgemm.json 2> $O/bench_stemgemm.err || { tail -30 $O/bench_stemgemm.err; exit 1; }
+echo "bench stem-gemm $(python3 -c "import json;d=json.load(open('$O/bench_stemgemm.json'));print(d['value'],d['ms_per_step'])")"
+timeout -k 10 300 python -u scripts/step_roofline.py --iters 3 --out $O/step_roofline.csv > $O/step_roofline.txt 2>&1 || { tail -30 $O/step_roofline.txt; exit 1; }
+grep -i "stem\|maxpool" $O/step_roofline.txt | head -12
 timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 8 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
 f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
 python3 scripts/prof_summarize.py "$f" --out $O/steady.csv > $O/steady.txt 2>&1 || { tail -5 $O/steady.txt; exit 1; }
 head -3 $O/steady.txt
 rm -rf $O/prof
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d $O/pmc -o run -- python3 -u bench.py --steps 2 --warmup 2 > $O/pmc_bench.json 2> $O/pmc_bench.err || { tail -20 $O/pmc_bench.err; exit 1; }
+f=$(find $O/pmc -name '*counter_collection.csv' | head -1)
+python3 scripts/pmc_summarize.py "$f" --top 40 --out $O/pmc_summary.csv > $O/pmc_summary.txt 2>&1 || { tail -5 $O/pmc_summary.txt; exit 1; }
+head -25 $O/pmc_summary.txt
+rm -rf $O/pmc
 for cfg in "gb20:" "o0:--amp O0"; do
   name=${cfg%%:*}; args=${cfg#*:}
   mkdir -p $O/asha_$name && DET_BENCH_LOGDIR=$O/asha_$name timeout -k 10 360 python -u scripts/bench_asha.py --slots 1 $args > $O/asha_$name.json 2> $O/asha_$name.err || { tail -30 $O/asha_$name.err; exit 1; }
