@@ -115,6 +115,7 @@ _SIGNATURES = {
     "det_maxpool3s2_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 4 + [c_void_p] * 6,
                            c_int),
     "det_maxpool3s2_bwd_rows_per_block": ([], c_int),
+    "det_maxpool3s2_bwd_partial_rows": ([c_int] * 4, c_i64),
     "det_bn_apply": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, dy, x, mask_bits, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws

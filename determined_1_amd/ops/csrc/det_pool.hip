@@ -253,6 +253,141 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd(const T* __restrict__ dy
   }
 }
 
+// Row-staged variant (the default where the window rows fit LDS): one block = one pooled row oh of
+// one image, i.e. the input rows 2 oh and 2 oh + 1, which read only the window rows oh and oh + 1.
+// Those two rows of dy (+ dy2, summed in fp32) and of the argmax bytes are staged once into LDS with
+// coalesced 16-B loads; each input pixel then gathers its (at most 2 x 2) windows from LDS.  The
+// per-pixel gather above issues ~12 vector-memory instructions per 8 input pixels (8-B argmax and
+// 16-B gradient pieces of up to four windows, re-fetched by the neighbouring pixels through the
+// texture path) -- 2.2 TB/s at the ResNet stem; here a block issues ~3 per 8 pixels, the rest is LDS.
+// Summation order per element is the gather kernel's (bit-identical results).  Blocks are mapped so
+// that consecutive pooled rows (which share a window row) run on the same XCD (its own L2).
+// BN partial sums are per block: [N * Ho, C].
+template <typename T, bool kTwo, bool BNB>
+__global__ void __launch_bounds__(kThreads) maxpool_bwd_rows(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                             const uint8_t* __restrict__ idx, T* __restrict__ dx,
+                                                             PoolGeom g, BnbArgs bn, int nblk) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  const int cv = g.C / 8, rowv = g.Wo * cv;  // 8-channel vectors per window row
+  float* ds = reinterpret_cast<float*>(psm);                               // [2][Wo][C] fp32
+  uint8_t* is = psm + static_cast<size_t>(2) * g.Wo * g.C * sizeof(float);  // [2][Wo][C]
+  const int b = blockIdx.x, per = nblk / 8, rem = nblk % 8, xcd = b % 8, bi = b / 8;
+  const int blk = xcd < rem ? xcd * (per + 1) + bi : rem * (per + 1) + (xcd - rem) * per + bi;
+  const int n = blk / g.Ho, oh = blk - n * g.Ho;
+  const int nrows = oh + 1 < g.Ho ? 2 : 1;
+  const int nv = nrows * rowv;
+  const int64_t wbase = static_cast<int64_t>(n * g.Ho + oh) * g.Wo * g.C;
+#pragma unroll 4
+  for (int v = threadIdx.x; v < nv; v += kThreads) {
+    const int64_t off = wbase + static_cast<int64_t>(v) * 8;
+    float d[8];
+    Vec8<T>::load(dy + off, d);
+    if constexpr (kTwo) {
+      float d2[8];
+      Vec8<T>::load(dy2 + off, d2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += d2[j];
+    }
+    const uc8 av = *reinterpret_cast<const uc8*>(idx + off);
+    float4* dst = reinterpret_cast<float4*>(ds + static_cast<int64_t>(v) * 8);
+    dst[0] = make_float4(d[0], d[1], d[2], d[3]);
+    dst[1] = make_float4(d[4], d[5], d[6], d[7]);
+    *reinterpret_cast<uc8*>(is + static_cast<int64_t>(v) * 8) = av;
+  }
+  const int c8 = threadIdx.x % cv, lanes = kThreads / cv;
+  float mu[8], sc[8], sh[8], s1[8], s2[8];
+  if constexpr (BNB) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = bn.mean[8 * c8 + j];
+      sc[j] = bn.scale[8 * c8 + j];
+      sh[j] = bn.shift[8 * c8 + j];
+      s1[j] = 0.f;
+      s2[j] = 0.f;
+    }
+  }
+  const int h0 = 2 * oh, hrows = min(2, g.H - h0), npx = hrows * g.W;
+  // the BN input of the block's input rows is contiguous: element offset of pixel p = xbase + p * C;
+  // its loads run one item ahead (the first under the staging barrier)
+  const int64_t xbase = static_cast<int64_t>(n * g.H + h0) * g.W * g.C + 8 * c8;
+  uint4 xnext = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (BNB) {
+    const int p = static_cast<int>(threadIdx.x) / cv;
+    if (p < npx) xnext = *reinterpret_cast<const uint4*>(bn.x + xbase + static_cast<int64_t>(p) * g.C);
+  }
+  __syncthreads();
+  for (int p = static_cast<int>(threadIdx.x) / cv; p < npx; p += lanes) {
+    const int hr = p >= g.W ? 1 : 0, w = p - hr * g.W, h = h0 + hr;
+    const int64_t e = xbase + static_cast<int64_t>(p) * g.C;
+    float xv[8];
+    if constexpr (BNB) {
+      const uint32_t wd[4] = {xnext.x, xnext.y, xnext.z, xnext.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xv[2 * k] = __uint_as_float(wd[k] << 16);
+        xv[2 * k + 1] = __uint_as_float(wd[k] & 0xffff0000u);
+      }
+      if (p + lanes < npx) xnext = *reinterpret_cast<const uint4*>(bn.x + e + static_cast<int64_t>(lanes) * g.C);
+    }
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // the gather kernel's window order
+      const int ohq = (h + 1) / 2 - (q >> 1), kh = h - (2 * ohq - 1);
+      const int owq = (w + 1) / 2 - (q & 1), kw = w - (2 * owq - 1);
+      if (ohq >= 0 && ohq < g.Ho && kh >= 0 && kh <= 2 && owq >= 0 && owq < g.Wo && kw >= 0 && kw <= 2) {
+        const int li = ((ohq - oh) * g.Wo + owq) * g.C + 8 * c8;
+        const float4 lo = *reinterpret_cast<const float4*>(ds + li), hi = *reinterpret_cast<const float4*>(ds + li + 4);
+        const float dv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const uc8 av = *reinterpret_cast<const uc8*>(is + li);
+        const uint8_t me = static_cast<uint8_t>(3 * kh + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += av[j] == me ? dv[j] : 0.f;
+      }
+    }
+    if constexpr (BNB) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dm = __fmaf_rn(xv[j], sc[j], sh[j]) > 0.f ? acc[j] : 0.f;
+        const float dr = __uint_as_float(static_cast<uint32_t>(f2bf(dm)) << 16);
+        acc[j] = dr;
+        s1[j] += dr;
+        s2[j] += dr * (xv[j] - mu[j]);
+      }
+    }
+    Vec8<T>::store(dx + e, acc);
+  }
+  if constexpr (BNB) {
+    __syncthreads();  // the staged rows are dead: the reduction reuses the LDS
+    float* red = ds;  // [kThreads][17]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[threadIdx.x * 17 + j] = s1[j];
+      red[threadIdx.x * 17 + 8 + j] = s2[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < g.C; c += kThreads) {
+      const int grp = c / 8, j = c % 8;
+      float t1 = 0.f, t2 = 0.f;
+      for (int l = 0; l < lanes; ++l) {
+        t1 += red[(l * cv + grp) * 17 + j];
+        t2 += red[(l * cv + grp) * 17 + 8 + j];
+      }
+      bn.psum[static_cast<int64_t>(blk) * g.C + c] = t1;
+      bn.psumx[static_cast<int64_t>(blk) * g.C + c] = t2;
+    }
+  }
+}
+
+// LDS bytes of maxpool_bwd_rows (two window rows, fp32 gradient + argmax byte; >= the BN reduction)
+size_t rows_lds(const PoolGeom& g) {
+  size_t b = static_cast<size_t>(2) * g.Wo * g.C * 5;
+  const size_t red = static_cast<size_t>(kThreads) * 17 * sizeof(float);
+  return b > red ? b : red;
+}
+constexpr size_t kRowsLdsMax = 64 * 1024;
+
 int grid_for(int64_t work) {
   int64_t b = (work + kThreads - 1) / kThreads;
   if (b > 16384) b = 16384;
@@ -289,12 +424,22 @@ int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t*
   return static_cast<int>(hipGetLastError());
 }
 
-// Input pixels per partial-sum block of det_maxpool3s2_bwd's BN-backward epilogue.
+// Input pixels per partial-sum block of the per-pixel gather kernel's BN-backward epilogue.
 int det_maxpool3s2_bwd_rows_per_block() { return kBwdRows; }
+
+// Rows of the BN partial sums det_maxpool3s2_bwd writes for this shape (psum / psumx [rows, C]):
+// N * Ho with the row-staged kernel, ceil(N*H*W / det_maxpool3s2_bwd_rows_per_block()) otherwise.
+int64_t det_maxpool3s2_bwd_partial_rows(int N, int H, int W, int C) {
+  const PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
+  if (rows_lds(g) <= kRowsLdsMax && static_cast<int64_t>(N) * g.Ho < (static_cast<int64_t>(1) << 31))
+    return static_cast<int64_t>(N) * g.Ho;
+  return (static_cast<int64_t>(N) * H * W + kBwdRows - 1) / kBwdRows;
+}
 
 // dy [N, Ho, Wo, C] (+ optional dy2 of the same shape, summed), idx from the forward -> dx [N, H, W, C]
 // (fully overwritten).  C % 8 == 0 and 256 % (C / 8) == 0; N*H*W < 2^31.
-// bn_x (nullable, bf16 only): with bn_mean/scale/shift [C] and psum/psumx [ceil(N*H*W / rows), C],
+// bn_x (nullable, bf16 only): with bn_mean/scale/shift [C] and psum/psumx
+// [det_maxpool3s2_bwd_partial_rows(N, H, W, C), C],
 // dx = relu'(bn_x * scale + shift) * gradient and the BN-backward partials (see maxpool_bwd BNB).
 int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const void* dy2, const uint8_t* idx, void* dx, int N,
                        int H, int W, int C, const void* bn_x, const float* bn_mean, const float* bn_scale,
@@ -305,8 +450,32 @@ int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const void* dy2,
   PoolGeom g{N, H, W, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
   const int64_t npix = static_cast<int64_t>(N) * H * W;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const dim3 grid(static_cast<unsigned>((npix + kBwdRows - 1) / kBwdRows)), block(kThreads);
   const BnbArgs bn{static_cast<const unsigned short*>(bn_x), bn_mean, bn_scale, bn_shift, psum, psumx};
+  if (rows_lds(g) <= kRowsLdsMax && static_cast<int64_t>(N) * g.Ho < (static_cast<int64_t>(1) << 31)) {
+    const int nblk = N * g.Ho;
+    const dim3 grid(static_cast<unsigned>(nblk)), block(kThreads);
+    const size_t lds = rows_lds(g);
+    if (dtype == 1) {
+      auto* a = static_cast<const unsigned short*>(dy);
+      auto* b = static_cast<const unsigned short*>(dy2);
+      auto* o = static_cast<unsigned short*>(dx);
+      if (bn_x) {
+        if (dy2) hipLaunchKernelGGL((maxpool_bwd_rows<unsigned short, true, true>), grid, block, lds, st, a, b, idx, o, g, bn, nblk);
+        else hipLaunchKernelGGL((maxpool_bwd_rows<unsigned short, false, true>), grid, block, lds, st, a, b, idx, o, g, bn, nblk);
+      } else {
+        if (dy2) hipLaunchKernelGGL((maxpool_bwd_rows<unsigned short, true, false>), grid, block, lds, st, a, b, idx, o, g, bn, nblk);
+        else hipLaunchKernelGGL((maxpool_bwd_rows<unsigned short, false, false>), grid, block, lds, st, a, b, idx, o, g, bn, nblk);
+      }
+    } else {
+      auto* a = static_cast<const float*>(dy);
+      auto* b = static_cast<const float*>(dy2);
+      auto* o = static_cast<float*>(dx);
+      if (dy2) hipLaunchKernelGGL((maxpool_bwd_rows<float, true, false>), grid, block, lds, st, a, b, idx, o, g, bn, nblk);
+      else hipLaunchKernelGGL((maxpool_bwd_rows<float, false, false>), grid, block, lds, st, a, b, idx, o, g, bn, nblk);
+    }
+    return static_cast<int>(hipGetLastError());
+  }
+  const dim3 grid(static_cast<unsigned>((npix + kBwdRows - 1) / kBwdRows)), block(kThreads);
   if (dtype == 1) {
     auto* a = static_cast<const unsigned short*>(dy);
     auto* b = static_cast<const unsigned short*>(dy2);

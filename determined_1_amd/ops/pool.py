@@ -88,8 +88,10 @@ class _MaxPool3s2(torch.autograd.Function):
             except RuntimeError:  # already freed (a second backward)
                 xb = None
             if xb is not None and xb.shape == dx.shape and xb.is_contiguous(memory_format=torch.channels_last):
-                rpb = int(lib.det_maxpool3s2_bwd_rows_per_block())
-                nrb = (N * H * W + rpb - 1) // rpb
+                # partial-sum rows: one per pooled row (row-staged kernel) or per 512 pixels; the
+                # BN finalize only sums them (rpb is informational)
+                nrb = int(lib.det_maxpool3s2_bwd_partial_rows(N, H, W, C))
+                rpb = (N * H * W + nrb - 1) // nrb
                 psum = torch.empty(nrb, C, dtype=torch.float32, device=dy.device)
                 psumx = torch.empty(nrb, C, dtype=torch.float32, device=dy.device)
                 bn = [xb.data_ptr(), stats[0].data_ptr(), stats[2].data_ptr(), stats[3].data_ptr(), psum.data_ptr(),

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r4s9
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_conv_gpu.py -k "stem" > $O/pytest_stem.log 2>&1 || { tail -40 $O/pytest_stem.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_pool_gpu.py tests/test_conv_gpu.py -k "stem or pool" > $O/pytest_stem.log 2>&1 || { tail -40 $O/pytest_stem.log; exit 1; }
 tail -2 $O/pytest_stem.log
 timeout -k 10 300 python -u scripts/step_roofline.py --iters 3 --out $O/step_roofline.csv > $O/step_roofline.txt 2>&1 || { tail -30 $O/step_roofline.txt; exit 1; }
 sed -n '/per family/,$p' $O/step_roofline.txt | head -40
