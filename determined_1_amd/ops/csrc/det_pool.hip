@@ -129,6 +129,89 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd(const T* __restrict__ x,
   }
 }
 
+// Row-staged forward (the default where three input rows fit LDS): one block = pooled row oh of one
+// image; the input rows 2 oh - 1 .. 2 oh + 1 are staged once into LDS (BNP: normalised + ReLU'd
+// and rounded while staging, once per element instead of once per window that reads it), then each
+// output vector takes its nine window values from LDS in maxpool_fwd's order (same max, same argmax
+// byte, same tie and NaN handling).  The gather above re-fetches every input vector ~2.25 times
+// through the texture path.  Consecutive pooled rows (sharing an input row) run on one XCD.
+template <typename T, bool BNP>
+__global__ void __launch_bounds__(kThreads) maxpool_fwd_rows(const T* __restrict__ x, T* __restrict__ y,
+                                                             uint8_t* __restrict__ idx, PoolGeom g, int nblk,
+                                                             const float* __restrict__ bn_scale,
+                                                             const float* __restrict__ bn_shift) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  T* xs = reinterpret_cast<T*>(psm);  // [3][W][C]
+  const int cv = g.C / 8, rowv = g.W * cv;
+  const int b = blockIdx.x, per = nblk / 8, rem = nblk % 8, xcd = b % 8, bi = b / 8;
+  const int blk = xcd < rem ? xcd * (per + 1) + bi : rem * (per + 1) + (xcd - rem) * per + bi;
+  const int n = blk / g.Ho, oh = blk - n * g.Ho;
+  const int hlo = max(0, 2 * oh - 1), hhi = min(g.H - 1, 2 * oh + 1);  // valid input rows
+  const int nv = (hhi - hlo + 1) * rowv;
+  const int64_t xbase = static_cast<int64_t>(n * g.H + hlo) * g.W * g.C;
+  const int c8s = threadIdx.x % cv;  // the staging thread's channel group is fixed (kThreads % cv == 0)
+  float bsc[8], bsh[8];
+  if constexpr (BNP) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bsc[j] = bn_scale[8 * c8s + j];
+      bsh[j] = bn_shift[8 * c8s + j];
+    }
+  }
+  // LDS row r holds input row 2 oh - 1 + r
+  const int r0 = hlo - (2 * oh - 1);
+#pragma unroll 4
+  for (int v = threadIdx.x; v < nv; v += kThreads) {
+    float val[8];
+    Vec8<T>::load(x + xbase + static_cast<int64_t>(v) * 8, val);
+    if constexpr (BNP) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        val[j] = __uint_as_float(static_cast<uint32_t>(f2bf(fmaxf(__fmaf_rn(val[j], bsc[j], bsh[j]), 0.f))) << 16);
+    }
+    Vec8<T>::store(xs + (static_cast<int64_t>(r0) * rowv + v) * 8, val);
+  }
+  __syncthreads();
+  const int nout = g.Wo * cv;
+  for (int i = threadIdx.x; i < nout; i += kThreads) {
+    const int ow = i / cv, c8 = i - ow * cv;
+    const uint8_t slot0 = static_cast<uint8_t>(3 * (oh == 0 ? 1 : 0) + (ow == 0 ? 1 : 0));
+    float m[8];
+    uint8_t a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      a[j] = slot0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = 2 * oh - 1 + kh;
+      if (h < 0 || h >= g.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = 2 * ow - 1 + kw;
+        if (w < 0 || w >= g.W) continue;
+        float v[8];
+        Vec8<T>::load(xs + (static_cast<int64_t>(kh) * rowv + w * cv + c8) * 8, v);
+        const uint8_t slot = static_cast<uint8_t>(3 * kh + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (v[j] > m[j] || (__builtin_isnan(v[j]) && !__builtin_isnan(m[j]))) {
+            m[j] = v[j];
+            a[j] = slot;
+          }
+        }
+      }
+    }
+    const int64_t o = (static_cast<int64_t>(n * g.Ho + oh) * g.Wo + ow) * g.C + 8 * c8;
+    Vec8<T>::store(y + o, m);
+    uc8 av;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) av[j] = a[j];
+    *reinterpret_cast<uc8*>(idx + o) = av;
+  }
+}
+
 // One block = kBwdRows consecutive INPUT pixels (all channels); thread t owns channel group
 // t % (C/8) of pixels t / (C/8), + 256 / (C/8), ...  Pixel coordinates in 32-bit math (the input has
 // < 2^31 pixels; 64-bit division is a long software sequence per element).
@@ -410,6 +493,23 @@ int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t*
   const int64_t nvec = static_cast<int64_t>(N) * g.Ho * g.Wo * (C / 8);
   if (nvec >= (static_cast<int64_t>(1) << 31)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t flds = static_cast<size_t>(3) * W * C * (dtype == 1 ? 2 : 4);
+  if (flds <= kRowsLdsMax && kThreads % (C / 8) == 0 && static_cast<int64_t>(N) * g.Ho < (static_cast<int64_t>(1) << 31)) {
+    const int nblk = N * g.Ho;
+    const dim3 grid(static_cast<unsigned>(nblk)), block(kThreads);
+    if (dtype == 1 && bn_scale)
+      hipLaunchKernelGGL((maxpool_fwd_rows<unsigned short, true>), grid, block, flds, st,
+                         static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g, nblk, bn_scale,
+                         bn_shift);
+    else if (dtype == 1)
+      hipLaunchKernelGGL((maxpool_fwd_rows<unsigned short, false>), grid, block, flds, st,
+                         static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g, nblk, nullptr,
+                         nullptr);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_rows<float, false>), grid, block, flds, st, static_cast<const float*>(x),
+                         static_cast<float*>(y), idx, g, nblk, nullptr, nullptr);
+    return static_cast<int>(hipGetLastError());
+  }
   if (dtype == 1 && bn_scale)
     hipLaunchKernelGGL((maxpool_fwd<unsigned short, true>), dim3(grid_for(nvec)), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), idx, g,
