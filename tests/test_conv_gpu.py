@@ -329,7 +329,7 @@ def test_stem_patch_wgrad_exact_on_integer_operands(gpu, n, h, w):
     torch.testing.assert_close(conv.unpack_stem_grad(out, 4).cpu(), ref2, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9), (5, 57, 57), (2, 225, 225)])
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 37, 50), (1, 8, 9), (5, 57, 57), (3, 99, 101)])
 def test_stem_patch_fwd_bit_identical_to_gemm(gpu, n, h, w):
     """det_stemp_fwd (the chunk's input rows staged once in LDS, weights resident, persistent
     blocks) == det_stem_conv_fwd (gathering implicit GEMM) bit for bit -- same k order -- including
@@ -372,6 +372,11 @@ def test_stem_patch_fwd_wide_images_fall_back(gpu):
     y = torch.empty(5 * 240, 64, dtype=torch.bfloat16, device=gpu)
     assert lib.det_stemp_fwd(torch.cuda.current_stream().cuda_stream, x4.data_ptr(), wt.data_ptr(), y.data_ptr(),
                              5 * 240, 9, 480, 5, 240, None, None) == -6
+    # 225 x 225: a 256-pixel chunk that straddles two images spans 17 padded rows of 231 pixels
+    x2 = torch.zeros(2, 4, 225, 225, device=gpu, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y2 = torch.empty(2 * 113 * 113, 64, dtype=torch.bfloat16, device=gpu)
+    assert lib.det_stemp_fwd(torch.cuda.current_stream().cuda_stream, x2.data_ptr(), wt.data_ptr(), y2.data_ptr(),
+                             2 * 113 * 113, 225, 225, 113, 113, None, None) == -6
     before = dict(conv.STEM_FWD_COUNTS)
     out = conv.stem_conv(x, cv)
     assert conv.STEM_FWD_COUNTS["gemm"] == before["gemm"] + 1
