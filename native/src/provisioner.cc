@@ -63,12 +63,20 @@ Decision ScaleDecider::Decide(int pending_slots, const std::vector<AgentInfo>& a
     idle_since_.erase(inst->id);
     --removable;
   }
-  // launch for unmet demand: instances still starting count as capacity on the way
-  int starting = 0;
-  for (auto& inst : instances)
-    if (inst.state != "Stopped" && !connected_idle.count(inst.id)) ++starting;
+  // launch for unmet demand: instances still starting count as capacity on the way, and so do the
+  // slots of connected idle instances that are kept (the scheduler places pending work on them at its
+  // next pass; without this an agent that connects between a scheduling pass and this decision
+  // looks like missing capacity and a second instance is launched)
+  int starting = 0, idle_kept = 0;
+  for (auto& inst : instances) {
+    if (inst.state == "Stopped") continue;
+    auto it = connected_idle.find(inst.id);
+    if (it == connected_idle.end()) ++starting;
+    else if (it->second && std::find(d.terminate.begin(), d.terminate.end(), inst.id) == d.terminate.end()) ++idle_kept;
+  }
   int spi = std::max(1, cfg_.slots_per_instance);
-  int want = (pending_slots + spi - 1) / spi - starting;
+  const int unmet = std::max(0, pending_slots - idle_kept * spi);
+  int want = (unmet + spi - 1) / spi - starting;
   int room = cfg_.max_instances - (live - static_cast<int>(d.terminate.size()));
   d.launch = std::max(0, std::min(want, room));
   if (live - static_cast<int>(d.terminate.size()) + d.launch < cfg_.min_instances)

@@ -188,3 +188,20 @@ TEST(scale_decider_launch_and_idle_terminate) {
   d = sd.Decide(0, {}, {{"z", "Starting", t0}}, t0 + std::chrono::milliseconds(6000));
   EXPECT_EQ(d.terminate.size(), size_t(1));  // never connected within the starting period
 }
+
+TEST(scale_decider_idle_connected_capacity_counts) {
+  using namespace detcore::prov;
+  ProvisionerConfig cfg;
+  cfg.max_instances = 2;
+  cfg.slots_per_instance = 1;
+  cfg.max_idle_period = std::chrono::milliseconds(1500);
+  ScaleDecider sd(cfg);
+  auto t0 = Clock::now();
+  // the launched instance's agent just connected (idle) while the trial's slot is still pending:
+  // the scheduler places it there next, so no second instance
+  auto d = sd.Decide(1, {{"a", true}}, {{"a", "Running", t0}}, t0 + std::chrono::milliseconds(10));
+  EXPECT_EQ(d.launch, 0);
+  // demand beyond the idle capacity still launches
+  d = sd.Decide(2, {{"a", true}}, {{"a", "Running", t0}}, t0 + std::chrono::milliseconds(20));
+  EXPECT_EQ(d.launch, 1);
+}
