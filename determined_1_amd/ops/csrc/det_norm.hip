@@ -194,6 +194,9 @@ struct FinArgs {
   float* save_rstd;
   float* scale;
   float* shift;
+  // nullable: a counter the finalize increments once (block 0, thread 0) -- num_batches_tracked when no
+  // apply kernel follows to bump it; only with momentum >= 0, where no block reads the counter
+  int64_t* bump;
 };
 
 // One block = 64 channels x 16 row-lanes (one wave per row-lane: 256 B coalesced partial rows).
@@ -202,6 +205,7 @@ struct FinArgs {
 // in flight per lane (the loop is L2-latency bound, not bandwidth bound).
 __global__ void __launch_bounds__(kFinThreads)
 bn_stats_finalize(const float* __restrict__ pmean, const float* __restrict__ pm2, Geom g, FinArgs a) {
+  if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) *a.bump += 1;
   __shared__ double red1[kFinLanes][kFinCh];
   __shared__ double red2[kFinLanes][kFinCh];
   const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
@@ -341,6 +345,7 @@ bn_stats_reduce(const float* __restrict__ pmean, const float* __restrict__ pm2, 
 // profiles/r3_resnet50_lastblock_finalize_negative_steady.csv).
 __global__ void __launch_bounds__(kFinThreads)
 bn_stats_combine_par(const double* __restrict__ part, int S, Geom g, FinArgs a) {
+  if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) *a.bump += 1;
   __shared__ double red1[kFinLanes][kFinCh];
   __shared__ double red2[kFinLanes][kFinCh];
   const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
@@ -919,8 +924,9 @@ int det_bn_stats_train(void* stream, int dtype, const void* x, int64_t M, int C,
                        pmean, pm2);
   FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
              save_mean, save_rstd, scale, shift};
+  if (momentum >= 0.f) fa.bump = num_batches_tracked;  // bumped by the finalize itself
   launch_stats_finalize(st, pmean, pm2, g, fa, ws + 2 * static_cast<int64_t>(g.nrb) * C + 3 * static_cast<int64_t>(C));
-  if (num_batches_tracked) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, num_batches_tracked);
+  if (num_batches_tracked && !fa.bump) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, num_batches_tracked);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -944,10 +950,11 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
   g.nrb = nrb;
   FinArgs fa{gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
              save_mean, save_rstd, scale, shift};
+  if (!apply && momentum >= 0.f) fa.bump = num_batches_tracked;  // no apply kernel to bump it
   launch_stats_finalize(st, pmean, pm2, g, fa, ws);
   int64_t* bump = num_batches_tracked;
   if (!apply) {
-    if (bump) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, bump);
+    if (bump && !fa.bump) hipLaunchKernelGGL(bump_counter, dim3(1), dim3(1), 0, st, bump);
     return static_cast<int>(hipGetLastError());
   }
   const int64_t nvec = M * C / 8;
