@@ -116,6 +116,7 @@ _SIGNATURES = {
                            c_int),
     "det_maxpool3s2_bwd_rows_per_block": ([], c_int),
     "det_maxpool3s2_bwd_partial_rows": ([c_int] * 4, c_i64),
+    "det_maxpool3s2_set_fwd_rows": ([c_int], None),
     "det_bn_apply": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, dy, x, mask_bits, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws

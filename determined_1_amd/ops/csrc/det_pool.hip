@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -479,7 +481,12 @@ int grid_for(int64_t work) {
 
 }  // namespace
 
+int g_fwd_rows = -1;  // -1: DET_POOL_FWD_ROWS decides on first use
+
 extern "C" {
+
+// 1: the row-staged forward (maxpool_fwd_rows) where it fits, 0: the per-output gather.
+void det_maxpool3s2_set_fwd_rows(int on) { g_fwd_rows = on ? 1 : 0; }
 
 // x [N, H, W, C] (channels_last) -> y [N, Ho, Wo, C], idx [N, Ho, Wo, C] uint8 (window slot 0..8).
 // dtype 0 = fp32, 1 = bf16; C % 8 == 0.  Ho = (H - 1) / 2 + 1 (kernel 3, stride 2, pad 1).
@@ -494,7 +501,13 @@ int det_maxpool3s2_fwd(void* stream, int dtype, const void* x, void* y, uint8_t*
   if (nvec >= (static_cast<int64_t>(1) << 31)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t flds = static_cast<size_t>(3) * W * C * (dtype == 1 ? 2 : 4);
-  if (flds <= kRowsLdsMax && kThreads % (C / 8) == 0 && static_cast<int64_t>(N) * g.Ho < (static_cast<int64_t>(1) << 31)) {
+  // the row-staged forward is opt-in (DET_POOL_FWD_ROWS=1): at the ResNet stem it ran 0.55 ms against
+  // the gather's 0.33 (LDS-bound occupancy of 3 blocks / CU and a load-all-then-compute block)
+  if (g_fwd_rows < 0) {
+    const char* e = std::getenv("DET_POOL_FWD_ROWS");
+    g_fwd_rows = e != nullptr && e[0] == '1' ? 1 : 0;
+  }
+  if (g_fwd_rows == 1 && flds <= kRowsLdsMax && kThreads % (C / 8) == 0 && static_cast<int64_t>(N) * g.Ho < (static_cast<int64_t>(1) << 31)) {
     const int nblk = N * g.Ho;
     const dim3 grid(static_cast<unsigned>(nblk)), block(kThreads);
     if (dtype == 1 && bn_scale)

@@ -24,6 +24,7 @@ def main() -> None:
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
     ap.add_argument("--impl", default="native", choices=["native", "hf"], help="fused MI355X encoder or HF BERT")
+    ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
     ap.add_argument("--cprof", default="", help="write a cProfile of the timed steps to this path")
     ap.add_argument("--autograd-threads", type=int, default=0,
                     help="1: stock multithreaded autograd engine (the controller disables it by default)")
@@ -50,7 +51,7 @@ def main() -> None:
         "hyperparameters": {"global_batch_size": gbs, "learning_rate": 3e-5, "max_seq_length": 384, "amp": args.amp,
                             "max_grad_norm": 1.0, "train_records": 100000, "impl": args.impl},
         "resources": {"slots_per_trial": world},
-        "optimizations": {"aggregation_frequency": args.agg},
+        "optimizations": {"aggregation_frequency": args.agg, "hip_graph": bool(args.hip_graph)},
         "searcher": {"name": "single", "metric": "f1", "max_length": {"batches": args.steps}, "smaller_is_better": False},
     }
     t = {}
@@ -84,6 +85,8 @@ def main() -> None:
 
     ctrl = make_controller(BertSQuADTrial, cfg, stream(), trial_seed=7)
     ctrl.run()
+    g = getattr(ctrl, "_graph", None)
+    graph_stats = {k: getattr(g, k, None) for k in ("captures", "failed_captures", "replays")} if g is not None else None
     el = max(pdist.allgather_object(t["t1"] - t["t0"]))
     from determined_1_amd.ops import transformer as tfops
 
@@ -94,6 +97,7 @@ def main() -> None:
                           "config": {"model": "bert-base (random init)", "seq_len": 384, "global_batch": gbs,
                                      "amp": args.amp, "aggregation_frequency": args.agg,
                                      "optimizer": "AdamW (fused arena HIP kernel)", "impl": args.impl,
+                                     "hip_graph": bool(args.hip_graph), "graph_stats": graph_stats,
                                      "tf_fallbacks": tfops.FALLBACKS["count"]}}), flush=True)
     pdist.shutdown()
 

@@ -1,4 +1,5 @@
 #!/bin/bash
+# Round-4 session 10: (+ stem patch forward and pool-forward A/Bs, roofline, PMC pass, BERT hipGraph)
 # Round-4 session 10: stem BN + ReLU applied inside the max-pool forward, max-pool backward with all
 # window operands loaded up front: tests, bench x2, steady profile; then ASHA trials/hr on one GPU
 # slot (the r3 default hip_graph_batches 20, and the reference precision O0).
@@ -15,6 +16,8 @@ for i in 1 2; do
 done
 DET_STEM_PATCH_FWD=0 timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_stemgemm.json 2> $O/bench_stemgemm.err || { tail -30 $O/bench_stemgemm.err; exit 1; }
 echo "bench stem-gemm $(python3 -c "import json;d=json.load(open('$O/bench_stemgemm.json'));print(d['value'],d['ms_per_step'])")"
+DET_POOL_FWD_ROWS=1 timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_poolrows.json 2> $O/bench_poolrows.err || { tail -30 $O/bench_poolrows.err; exit 1; }
+echo "bench pool-fwd-rows $(python3 -c "import json;d=json.load(open('$O/bench_poolrows.json'));print(d['value'],d['ms_per_step'])")"
 timeout -k 10 300 python -u scripts/step_roofline.py --iters 3 --out $O/step_roofline.csv > $O/step_roofline.txt 2>&1 || { tail -30 $O/step_roofline.txt; exit 1; }
 grep -i "stem\|maxpool" $O/step_roofline.txt | head -12
 timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 8 > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
@@ -27,6 +30,8 @@ f=$(find $O/pmc -name '*counter_collection.csv' | head -1)
 python3 scripts/pmc_summarize.py "$f" --top 40 --out $O/pmc_summary.csv > $O/pmc_summary.txt 2>&1 || { tail -5 $O/pmc_summary.txt; exit 1; }
 head -25 $O/pmc_summary.txt
 rm -rf $O/pmc
+timeout -k 10 400 python -u scripts/bench_bert.py --steps 30 --warmup 8 --hip-graph > $O/bert_graph.json 2> $O/bert_graph.err || { tail -20 $O/bert_graph.err; exit 1; }
+echo "bert hip_graph $(cut -c1-400 $O/bert_graph.json)"
 for cfg in "gb20:" "o0:--amp O0"; do
   name=${cfg%%:*}; args=${cfg#*:}
   mkdir -p $O/asha_$name && DET_BENCH_LOGDIR=$O/asha_$name timeout -k 10 360 python -u scripts/bench_asha.py --slots 1 $args > $O/asha_$name.json 2> $O/asha_$name.err || { tail -30 $O/asha_$name.err; exit 1; }

@@ -8,9 +8,20 @@ from determined_1_amd.ops import pool
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["gather", "rows"])
+def fwd_kernel(request):
+    """Both max-pool forwards: the per-output gather (default) and the row-staged one."""
+    from determined_1_amd.ops import _lib
+
+    lib = _lib.get_lib()
+    lib.det_maxpool3s2_set_fwd_rows(1 if request.param == "rows" else 0)
+    yield request.param
+    lib.det_maxpool3s2_set_fwd_rows(0)
+
+
 @pytest.mark.parametrize("N,C,H,W,dt", [(4, 64, 112, 112, torch.bfloat16), (2, 16, 15, 9, torch.float32),
                                         (3, 8, 8, 8, torch.bfloat16), (1, 32, 1, 5, torch.float32)])
-def test_maxpool3s2_matches_torch(gpu, N, C, H, W, dt):
+def test_maxpool3s2_matches_torch(gpu, fwd_kernel, N, C, H, W, dt):
     torch.manual_seed(0)
     x = torch.randn(N, C, H, W).to(dt).float()  # bf16 values: ties inside windows do occur
     dy_shape = F.max_pool2d(x, 3, 2, 1).shape
