@@ -182,14 +182,15 @@ class SyntheticSQuAD(tud.Dataset):
     def __getitem__(self, i: int) -> Tuple[torch.Tensor, ...]:
         g = torch.Generator().manual_seed(self.seed * 1000003 + i)
         L = self.seq_len
-        q = 64
-        ids = torch.randint(1000, self.vocab, (L,), generator=g)
-        ids[0], ids[q - 1], ids[L - 1] = 101, 102, 102
+        q = min(64, L // 4)  # question length (64 at SQuAD's 384; short sequences for tiny test models)
+        span = min(30, (L - q) // 4)
+        ids = torch.randint(min(1000, self.vocab // 2), self.vocab, (L,), generator=g)
+        ids[0], ids[q - 1], ids[L - 1] = min(101, self.vocab - 1), min(102, self.vocab - 1), min(102, self.vocab - 1)
         tt = torch.zeros(L, dtype=torch.int64)
         tt[q:] = 1
         am = torch.ones(L, dtype=torch.int64)
-        s = int(torch.randint(q, L - 31, (1,), generator=g))
-        e = s + int(torch.randint(0, 30, (1,), generator=g))
+        s = int(torch.randint(q, L - span - 1, (1,), generator=g))
+        e = s + int(torch.randint(0, span, (1,), generator=g))
         return ids, tt, am, torch.tensor(s), torch.tensor(e)
 
 

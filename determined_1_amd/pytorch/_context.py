@@ -80,6 +80,9 @@ class PyTorchTrialContext(trial.TrialContext):
         self._loss_ids = {}  # type: Dict[Any, int]
         self._last_backward_batch_idx = None  # type: Optional[int]
         self._current_batch_idx = None  # type: Optional[int]
+        # gradients of a partial aggregation window restored from a checkpoint (_trial._load), added
+        # before the next backward accumulates into them
+        self._restored_grads = None  # type: Optional[List[List[Optional[torch.Tensor]]]]
         self._finalized = False
         self._fuse = True
         # gradients land through one batched copy per bucket instead of per-parameter adds
@@ -283,6 +286,8 @@ class PyTorchTrialContext(trial.TrialContext):
                 # of a batch that ends an aggregation window (Horovod's
                 # backward_passes_per_step * aggregation_frequency, reference :192-198)
                 st.bucketer.prepare_backward(comm and st.calls == st.bpps)
+        if self._restored_grads is not None:
+            self._apply_restored_grads()
         if self._use_amp and self._amp is not None and self._amp.scaler is not None:
             if (self._last_backward_batch_idx is not None and self._current_batch_idx is not None
                     and self._last_backward_batch_idx >= self._current_batch_idx and self.dist_config.use):
@@ -297,6 +302,38 @@ class PyTorchTrialContext(trial.TrialContext):
         for st in self._opt_states:
             if st.fused is not None and st.fused.sink is not None:
                 st.fused.sink.end_backward()
+
+    def _partial_window_grads(self) -> Optional[List[List[Optional[torch.Tensor]]]]:
+        """The accumulated gradients of an unfinished aggregation window (checkpointed so that a
+        restored trial steps on the same sum as an uninterrupted one; the reference drops them), or
+        None.  Single-process only: with several ranks each holds its own partial sum."""
+        if self._restored_grads is not None:
+            return self._restored_grads  # restored and not consumed yet
+        agg = self.dist_config.aggregation_frequency
+        if agg <= 1 or self._current_batch_idx is None or (self._current_batch_idx + 1) % agg == 0:
+            return None
+        if self.dist_config.use and pdist.is_initialized() and self.distributed.get_size() > 1:
+            logging.warning("checkpoint inside an aggregation window: the partial gradient sums of %d ranks are "
+                            "not saved", self.distributed.get_size())
+            return None
+        return [[None if p.grad is None else p.grad.detach().to("cpu", copy=True) for p in m.parameters()]
+                for m in self.models]
+
+    @torch.no_grad()
+    def _apply_restored_grads(self) -> None:
+        saved, self._restored_grads = self._restored_grads, None
+        for st in self._opt_states:
+            sink = st.fused.sink if st.fused is not None else None
+            if sink is not None and sink.fresh:
+                sink.end_backward()  # land zeros: the window continues, it does not start here
+        for m, grads in zip(self.models, saved):
+            for p, g in zip(m.parameters(), grads):
+                if g is None:
+                    continue
+                if p.grad is None:
+                    p.grad = g.to(device=p.device, dtype=p.dtype).clone()
+                else:
+                    p.grad.copy_(g)
 
     def _grad_scale(self) -> float:
         s = 1.0

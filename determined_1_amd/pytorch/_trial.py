@@ -522,6 +522,8 @@ class PyTorchTrialController(trial.LoopTrialController):
                 logging.warning("There exists gpu_rng_state in checkpoint but the system has no gpu.")
         else:
             logging.warning("The checkpoint has no random state to restore.")
+        if checkpoint.get("accumulated_grads") is not None:
+            ctx._restored_grads = checkpoint["accumulated_grads"]
         cb_state = checkpoint.get("callbacks", {})
         for name, cb in self.callbacks.items():
             if name in cb_state:
@@ -552,6 +554,9 @@ class PyTorchTrialController(trial.LoopTrialController):
         }
         if ctx._amp is not None:
             ckpt["amp_state"] = ctx._amp_state_dict()
+        partial = ctx._partial_window_grads()
+        if partial is not None:
+            ckpt["accumulated_grads"] = partial
         torch.save(ckpt, str(path.joinpath(CHECKPOINT_FILE)), pickle_module=_pickle_module)
         for cb in self.callbacks.values():
             cb.on_checkpoint_end(str(path))

@@ -73,12 +73,14 @@ class BertSQuADTrial(det_torch.PyTorchTrial):
 
     def build_training_data_loader(self) -> det_torch.DataLoader:
         n = int(self.context.get_hparams().get("train_records", 88000))
-        return det_torch.DataLoader(SyntheticSQuAD(n, self.seq_len), batch_size=self.context.get_per_slot_batch_size(),
-                                    num_workers=2, drop_last=True)
+        vocab = int(self.context.get_hparams().get("vocab_size", 30522))
+        return det_torch.DataLoader(SyntheticSQuAD(n, self.seq_len, vocab_size=vocab),
+                                    batch_size=self.context.get_per_slot_batch_size(), num_workers=2, drop_last=True)
 
     def build_validation_data_loader(self) -> det_torch.DataLoader:
         n = int(self.context.get_hparams().get("validation_records", 1024))
-        return det_torch.DataLoader(SyntheticSQuAD(n, self.seq_len, seed=1),
+        vocab = int(self.context.get_hparams().get("vocab_size", 30522))
+        return det_torch.DataLoader(SyntheticSQuAD(n, self.seq_len, vocab_size=vocab, seed=1),
                                     batch_size=self.context.get_per_slot_batch_size(), num_workers=2)
 
 
