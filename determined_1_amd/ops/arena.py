@@ -201,8 +201,13 @@ class GradSink:
         self._landing_taken = set()  # type: set  # (group, index) slots handed out by landing_buffer
         self._tables = {}  # type: Dict[int, Any]
         self._handles = []
+        # per parameter, everything the hook compares against (one dict lookup instead of ~10
+        # tensor attribute reads per parameter per backward: the hook runs 150-160 times a step)
+        self._slot = {}  # type: Dict[int, Tuple[int, Arena, int, torch.Tensor, int, Any, Any, Any, Any]]
         for gi, (a, idx) in enumerate(self.groups):
             for i in idx:
+                v = a.grad_views[i]
+                self._slot[id(a.params[i])] = (gi, a, i, v, v.data_ptr(), v.shape, v.stride(), v.dtype, v.device)
                 self._handles.append(a.params[i].register_post_accumulate_grad_hook(self._hook))
                 a.params[i]._det_grad_slot = (self, gi, a, i)  # see landing_buffer()
 
@@ -244,29 +249,27 @@ class GradSink:
     def _hook(self, p: torch.Tensor) -> None:
         if not self.fresh:
             return
-        gi = self.group_of.get(id(p))
-        if gi is None:
+        slot = self._slot.get(id(p))
+        if slot is None:
             return
-        a, _ = self.groups[gi]
-        i = a.index[id(p)]
-        if i in self._seen[gi]:
+        gi, a, i, view, vptr, vshape, vstride, vdtype, vdev = slot
+        seen = self._seen[gi]
+        if i in seen:
             return
-        self._seen[gi].add(i)
+        seen.add(i)
         g = p.grad
-        view = a.grad_views[i]
-        if g is not None and g is not view and g.data_ptr() == view.data_ptr() and g.shape == view.shape \
-                and g.stride() == view.stride() and g.dtype == view.dtype:
-            p.grad = view  # produced in place by its backward (landing_buffer): nothing to move
-        elif g is not None and g is not view:
-            # same shape + the arena view's (dense) strides => g is dense with the same element order
-            if g.dtype == view.dtype and g.shape == view.shape and g.stride() == view.stride() \
-                    and g.device == view.device:
+        if g is None:
+            p.grad = view
+        elif g is not view:
+            same = g.dtype == vdtype and g.shape == vshape and g.stride() == vstride
+            if same and g.data_ptr() == vptr:
+                pass  # produced in place by its backward (landing_buffer): nothing to move
+            elif same and g.device == vdev:
+                # same shape + the arena view's (dense) strides => g is dense with the same element order
                 self._stolen[gi].append((i, g))
             else:
                 with torch.no_grad():
                     view.copy_(g)
-            p.grad = view
-        elif g is None:
             p.grad = view
         self._pending[gi] -= 1
         if self._pending[gi] == 0:
