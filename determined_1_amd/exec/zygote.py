@@ -30,6 +30,7 @@ import signal
 import socket
 import struct
 import sys
+import time
 from typing import Dict, List, Optional, Tuple
 
 ALLOWED_PREFIX = "determined_1_amd.exec."
@@ -80,6 +81,7 @@ def _recv_request(conn: socket.socket) -> Tuple[Dict, List[int]]:
 def _child(req: Dict, fds: List[int], close: List[int]) -> None:
     """Runs in the forked child; never returns."""
     code = 1
+    t_fork = time.time()
     try:
         os.setpgid(0, 0)
         for fd in close:
@@ -110,6 +112,7 @@ def _child(req: Dict, fds: List[int], close: List[int]) -> None:
         os.environ.clear()
         os.environ.update({str(k): str(v) for k, v in env.items()})
         os.environ["DET_ZYGOTE_PID"] = str(os.getppid())
+        os.environ["DET_PROCESS_T0"] = repr(t_fork)  # the harness timeline's origin (harness/timeline.py)
         pp = [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]
         sys.path[:] = [cwd] + pp + [p for p in sys.path if p and p not in pp and p != cwd]
         argv = list(req["argv"])

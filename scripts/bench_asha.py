@@ -204,7 +204,10 @@ def main() -> None:
         except Exception as ex:  # diagnostics only
             idle = {"error": f"{type(ex).__name__}: {ex}"[:200]}
         containers = timeline.pop("_containers", 0)
-        occupancy = timeline.get("total", 0.0) * containers / max(1e-9, wall * slots)
+        # slot occupancy from the container log spans (idle_breakdown); the per-container timeline
+        # totals are kept for the phase split only
+        occupancy = (1.0 - idle["idle_frac"]) if "idle_frac" in idle else \
+            timeline.get("total", 0.0) * containers / max(1e-9, wall * slots)
         records = sum(t.get("total_batches_processed", 0) * t.get("hparams", {}).get("global_batch_size", 0)
                       for t in e["trials"])
         print(json.dumps({"metric": "ASHA trials/hr (16-trial adaptive_asha CIFAR-10)",
