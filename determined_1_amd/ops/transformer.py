@@ -17,9 +17,8 @@ run the plain PyTorch composite, which is also the numerics reference of the GPU
 fallbacks are counted in ``FALLBACKS`` so benchmarks can assert the native path ran.
 """
 import ctypes
-import itertools
 import os
-from typing import Optional, Tuple
+from typing import Any, Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -30,8 +29,12 @@ from determined_1_amd.ops.arena import landing_buffer
 FALLBACKS = {"count": 0}
 _DT = {torch.float32: 0, torch.bfloat16: 1}
 _MAX_H = 8192  # det_tf_ln_max_hidden() (workgroup-per-row kernels above 2048, e.g. ALBERT-xxlarge)
-_offsets = itertools.count(1)
-_seed = []  # lazily cached: the trial seeds torch before the first dropout call
+# Philox (seed, offset) stream of the native dropout kernels (LayerNorm + residual dropout,
+# attention dropout).  Part of the trial's RNG state: reset when the trial seeds its RNGs and saved /
+# restored with its checkpoints (pytorch/_trial.py), so a resumed trial draws the masks an
+# uninterrupted one would.  The seed is taken lazily from torch's at the first call.
+_RNG = {"seed": None, "offset": 1}
+_MASK64 = 0xFFFFFFFFFFFFFFFF
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -44,10 +47,33 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 def next_rng() -> Tuple[int, int]:
     """(seed, offset) of the next dropout call: the seed follows the trial's torch seed, the offset
-    is unique per call within the process, so masks are reproducible run to run."""
-    if not _seed:
-        _seed.append(torch.initial_seed() & 0xFFFFFFFFFFFFFFFF)
-    return _seed[0], next(_offsets)
+    is unique per call, so masks are reproducible run to run and across checkpoint/restore."""
+    if _RNG["seed"] is None:
+        _RNG["seed"] = torch.initial_seed() & _MASK64
+    off = _RNG["offset"]
+    _RNG["offset"] = off + 1
+    return _RNG["seed"], off
+
+
+def reset_rng(seed: Optional[int] = None) -> None:
+    """Start a new stream (the trial controller calls this when it seeds torch)."""
+    _RNG["seed"] = None if seed is None else int(seed) & _MASK64
+    _RNG["offset"] = 1
+
+
+def rng_state() -> Dict[str, Any]:
+    return {"seed": _RNG["seed"], "offset": _RNG["offset"]}
+
+
+def set_rng_state(state: Dict[str, Any]) -> None:
+    _RNG["seed"] = state.get("seed")
+    _RNG["offset"] = int(state.get("offset", 1))
+
+
+def rng_calls() -> int:
+    """Native dropout calls so far (the hipGraph builder checks that a captured step makes none:
+    its (seed, offset) kernel arguments would replay the same masks every step)."""
+    return _RNG["offset"] - 1
 
 
 def _native(*ts: Optional[torch.Tensor], width: int, max_width: Optional[int] = None) -> bool:

@@ -35,8 +35,9 @@ CIFAR trial host-bound (data fetch, input copy, replay launch, metric clones: ~0
 host cost -- one input copy per leaf, one replay, one clone per metric -- is paid once per K
 batches.  Chunks never cross an epoch (the epoch index is part of the key).
 """
+import contextlib
 import logging
-from typing import Any, Callable, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
 import torch
 from torch.utils import _pytree as pytree
@@ -45,6 +46,19 @@ WARMUP = 2        # eager batches per key before capturing (lazy init, MIOpen fi
 MAX_GRAPHS = 2    # live graphs (the epoch's full batch + its tail batch)
 THRASH_LIMIT = 8  # captures that replayed fewer than THRASH_MIN times -> graphs off
 THRASH_MIN = 4
+
+
+@contextlib.contextmanager
+def _no_native_rng() -> Iterator[None]:
+    """Fail a train-step capture that draws native dropout masks (ops/transformer.py next_rng): their
+    Philox (seed, offset) are kernel arguments, so every replay would repeat the captured masks.
+    The capture then fails like any capture-unsafe op and the step runs eagerly."""
+    from determined_1_amd.ops import transformer as _tf
+
+    c0 = _tf.rng_calls()
+    yield
+    if _tf.rng_calls() != c0:
+        raise RuntimeError("train_batch draws native dropout masks, whose Philox offsets a replay would repeat")
 CHUNK_WARMUP = 1  # per-batch chunks per multi-batch key before capturing it
 CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 
@@ -203,7 +217,7 @@ class TrainStepGraph:
             self.pool = torch.cuda.graph_pool_handle()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self.pool):
+            with torch.cuda.graph(graph, pool=self.pool), _no_native_rng():
                 out = self._eager(static_batch, epoch_idx, batch_idx)
         except Exception as e:  # capture-unsafe op in user code or a library: stay eager
             for f, h in zip(self.fused, host):
@@ -285,7 +299,7 @@ class TrainStepGraph:
             self.pool = torch.cuda.graph_pool_handle()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self.pool):
+            with torch.cuda.graph(graph, pool=self.pool), _no_native_rng():
                 outs = []
                 for i, b in enumerate(views):
                     o = self._eager(b, epoch_idx, batch_idx + i)

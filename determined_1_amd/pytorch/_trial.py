@@ -94,6 +94,9 @@ class PyTorchTrialController(trial.LoopTrialController):
         random.seed(seed)
         np.random.seed(seed)
         torch.random.manual_seed(seed)
+        from determined_1_amd.ops import transformer as _tf
+
+        _tf.reset_rng()  # the native dropout stream follows the new torch seed
 
     @staticmethod
     def from_trial(*args: Any, **kwargs: Any) -> trial.TrialController:
@@ -520,6 +523,10 @@ class PyTorchTrialController(trial.LoopTrialController):
                     logging.warning("The system has a gpu but no gpu_rng_state exists in the checkpoint.")
             elif "gpu_rng_state" in rs:
                 logging.warning("There exists gpu_rng_state in checkpoint but the system has no gpu.")
+            if "det_dropout_rng" in rs:
+                from determined_1_amd.ops import transformer as _tf
+
+                _tf.set_rng_state(rs["det_dropout_rng"])
         else:
             logging.warning("The checkpoint has no random state to restore.")
         if checkpoint.get("accumulated_grads") is not None:
@@ -545,6 +552,9 @@ class PyTorchTrialController(trial.LoopTrialController):
         }
         if torch.cuda.is_available() and ctx.device.type == "cuda":
             rng_state["gpu_rng_state"] = torch.cuda.get_rng_state(ctx.device)
+        from determined_1_amd.ops import transformer as _tf
+
+        rng_state["det_dropout_rng"] = _tf.rng_state()
         ckpt = {
             "models_state_dict": [m.state_dict() for m in ctx.models],
             "optimizers_state_dict": [o.state_dict() for o in ctx.optimizers],
