@@ -147,6 +147,7 @@ _SIGNATURES = {
     "det_nms": ([c_void_p, c_void_p, c_int, c_float, c_void_p, c_void_p], c_int),
     # det_conv.hip: 1x1-conv GEMMs (MFMA) with fused BN statistics / BN-apply+ReLU prologue
     "det_conv_nt_rows_per_block": ([c_int], c_int),
+    "det_conv_nt_set_wide": ([c_int], c_int),
     "det_conv_nt_set_pf": ([c_int], c_int),
     # stream, X, W, bias (nullable), Y, M, N, K
     "det_linear_fwd": ([c_void_p] * 5 + [c_i64, c_int, c_int], c_int),

@@ -351,6 +351,8 @@ DGRAD_BT = True  # 1x1 input gradients read the weight untransposed (no per-call
 # beat the register-staged gemm_nt by >= 7 % at ResNet-50 / batch 512 (profiles/r3_igemm_cfgs_1x1.jsonl:
 # 0.063 vs 0.084 ms at 2048->512, 0.123 vs 0.136 at 256->1024, ...); the rest stay on gemm_nt.
 IGEMM_FWD_1X1 = {(256, 1024): 8, (2048, 512): 8, (1024, 512): 8, (512, 256): 8, (1024, 256): 8}
+if os.environ.get("DET_NT_WIDE") == "1":  # A/B: the layer-3 expansion on det_conv's occupancy-3 wide tiles
+    IGEMM_FWD_1X1.pop((256, 1024))
 
 
 def _attach_partials(y: torch.Tensor, parts: Optional[Tuple[torch.Tensor, torch.Tensor, int]]) -> None:

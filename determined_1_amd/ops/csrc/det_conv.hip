@@ -76,6 +76,14 @@ struct Gather {
   // kGmConv (wgrad of an R x S conv): channels per input pixel, kernel width, stride, padding
   int cin, ks, cstride, cpad;
   __device__ __forceinline__ int64_t row(int64_t m) const {
+    if (static_cast<uint64_t>(m) < (static_cast<uint64_t>(1) << 32)) {
+      // 32-bit unsigned divisions (every activation here has < 2^32 rows): the 64-bit ones are a
+      // long software sequence per gathered row
+      const uint32_t mu = static_cast<uint32_t>(m), hw = static_cast<uint32_t>(Ho) * static_cast<uint32_t>(Wo);
+      const uint32_t n = mu / hw, rem = mu - n * hw;
+      const uint32_t ho = rem / static_cast<uint32_t>(Wo), wo = rem - ho * static_cast<uint32_t>(Wo);
+      return (static_cast<int64_t>(n) * Hi + 2 * ho) * Wi + 2 * wo;
+    }
     const int64_t hw = static_cast<int64_t>(Ho) * Wo;
     const int64_t n = m / hw;
     const int rem = static_cast<int>(m - n * hw);
@@ -406,12 +414,15 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
         int64_t aoff = off;
         bool on = true;
         if (a.bn.add_hi > 0) {
-          const int64_t r = m0 + row, hw = static_cast<int64_t>(a.bn.add_hi) * a.bn.add_wi;
-          const int64_t img = r / hw;
-          const int rem = static_cast<int>(r - img * hw);
-          const int h = rem / a.bn.add_wi, w = rem - h * a.bn.add_wi;
-          on = ((h | w) & 1) == 0;
-          aoff = ((img * a.bn.add_ho + (h >> 1)) * a.bn.add_wo + (w >> 1)) * a.N + c0;
+          // 32-bit unsigned index math (M < 2^32, checked by the host): a 64-bit division is a long
+          // software sequence, and every thread does NQE of these before its first store
+          const uint32_t r = static_cast<uint32_t>(m0 + row);
+          const uint32_t hw = static_cast<uint32_t>(a.bn.add_hi) * static_cast<uint32_t>(a.bn.add_wi);
+          const uint32_t img = r / hw, rem = r - img * hw;
+          const uint32_t h = rem / static_cast<uint32_t>(a.bn.add_wi), w = rem - h * static_cast<uint32_t>(a.bn.add_wi);
+          on = ((h | w) & 1u) == 0;
+          aoff = (static_cast<int64_t>(img * static_cast<uint32_t>(a.bn.add_ho) + (h >> 1)) * a.bn.add_wo + (w >> 1)) *
+                     a.N + c0;
         }
         if (on) as[q] = *reinterpret_cast<const us8*>(a.bn.add + aoff);
       }
@@ -488,12 +499,11 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
-  if (STATS) {
-    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
-                                                static_cast<int64_t>(mt) * a.N + n0);
-  }
   __syncthreads();
   if constexpr (BNB) {
+    if (STATS)
+      det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                  static_cast<int64_t>(mt) * a.N + n0);
     // each thread owns one 8-column chunk (kThreads % CPR == 0) over rows tid/CPR + q*kThreads/CPR
     const int cc = tid % CPR;
     const int c0 = n0 + cc * 8;
@@ -558,6 +568,10 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
     if (row < nvalid)
       *reinterpret_cast<us8*>(a.C + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
+  // BN statistics after the stores are issued (red is a separate LDS array): they drain meanwhile
+  if (STATS)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -794,7 +808,10 @@ int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride
   const int64_t mtiles = (a.M + BM - 1) / BM;
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
-  constexpr int smem = nt_smem<BM, BN, OCC == 2 ? 2 : 1>();
+  // double-buffered at occupancy 2, and for the 128 x 64 occupancy-3 tiles of the short-K wide-N
+  // forwards (g_nt_wide: 48 KB x 3 fits the 160 KB LDS); the 128 x 128 occupancy-3 K == 64 variant
+  // has a single K tile and one buffer
+  constexpr int smem = nt_smem<BM, BN, (OCC == 2 || (OCC == 3 && BN == 64)) ? 2 : 1>();
   if (a.abits != nullptr) {  // AFWD: forward with the BN apply (+ residual, ReLU) in the A staging
     if (!a.A2 || !a.Aout || !a.scale || !a.shift || pro || bt || bnb || stride2) return -2;
     if constexpr (OCC > 2) {
@@ -864,6 +881,17 @@ int launch_tn(hipStream_t st, const TnArgs& a, int splits, bool pro, bool stride
 // GEMM-only 2-10 % faster than depth 1 on most ResNet 1x1 shapes (profiles/r4_conv1x1_pf_sweep.jsonl);
 // neutral on the whole step, where the fused variants carry most calls (r4_nt_pf_ab.jsonl).
 int g_nt_pf = -1;  // det_conv_nt_set_pf
+// Short-K wide-N plain forwards (the bottleneck expansions, K = 128..512) on 128 x 64 tiles at three
+// workgroups per CU instead of 128 x 128 at two: those GEMMs wait on each block's load latency (a
+// 2-8 K-tile loop), and a third resident block hides more of it.  -1: DET_NT_WIDE decides (default off).
+int g_nt_wide = -1;
+bool nt_wide(const NtArgs& a) {
+  if (g_nt_wide < 0) {
+    const char* e = std::getenv("DET_NT_WIDE");
+    g_nt_wide = e != nullptr && e[0] == '1' ? 1 : 0;
+  }
+  return g_nt_wide == 1 && a.K >= 128 && a.K <= 512 && a.N >= 4 * a.K && a.abits == nullptr && a.A2 == nullptr;
+}
 int nt_pf(int K) {
   static const int env_pf = [] {
     const char* e = std::getenv("DET_NT_PF");
@@ -893,6 +921,12 @@ extern "C" {
 
 // Prefetch depth of the plain GEMMs (1..3; 0 = back to DET_NT_PF / the default).  Returns the previous
 // override.  For benchmarks and tests; not thread-safe against concurrent launches.
+int det_conv_nt_set_wide(int on) {
+  const int prev = g_nt_wide;
+  g_nt_wide = on < 0 ? -1 : (on ? 1 : 0);
+  return prev;
+}
+
 int det_conv_nt_set_pf(int pf) {
   const int old = g_nt_pf;
   g_nt_pf = pf <= 0 ? -1 : (pf > 3 ? 3 : pf);
@@ -929,6 +963,7 @@ int det_conv_nt(void* stream, const void* A, const void* B, void* C, int64_t M, 
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
     return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, pro, stats, stride2);
   }
+  if (nt_wide(a)) return launch_nt<128, 64, 2, 2, 3, 2>(st, a, pro, stats, stride2);
   if (N % 128 == 0) return launch_nt_pf<128, 128>(st, a, pro, stats, stride2, false);
   return launch_nt_pf<128, 64>(st, a, pro, stats, stride2, false);
 }
@@ -981,7 +1016,7 @@ int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64
                       void* abn_out, int add_ho, int add_wo, int add_hi, int add_wi) {
   if (M <= 0 || N % 64 != 0 || K % 64 != 0 || N <= 0 || K <= 0) return -1;
   if (add_hi > 0 && (add_wi <= 0 || add_ho != (add_hi + 1) / 2 || add_wo != (add_wi + 1) / 2 ||
-                     M % (static_cast<int64_t>(add_hi) * add_wi) != 0))
+                     M % (static_cast<int64_t>(add_hi) * add_wi) != 0 || M >= (static_cast<int64_t>(1) << 32)))
     return -3;
   if (!x || !mean || !psum || !psumx || (mode == 1 && (!scale || !shift)) || (mode == 2 && !mbits) || mode < 1 || mode > 2)
     return -2;

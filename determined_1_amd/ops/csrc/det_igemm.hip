@@ -328,10 +328,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
-  if (STATS) {
-    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
-                                                static_cast<int64_t>(mt) * a.N + n0);
-  }
   __syncthreads();
   constexpr int CPR = BN / 8;
 #pragma unroll
@@ -341,6 +337,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
     if (row < nvalid)
       *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
+  // BN statistics after the stores are issued (red is its own LDS region): they drain meanwhile
+  if (STATS)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -510,12 +510,11 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
-  if (STATS) {
-    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
-                                                static_cast<int64_t>(mt) * a.N + n0);
-  }
   __syncthreads();
   if constexpr (BNB) {
+    if (STATS)
+      det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                  static_cast<int64_t>(mt) * a.N + n0);
     bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
     return;
   }
@@ -527,6 +526,10 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
     if (idx < BM * CPR && row < nvalid)
       *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
+  // BN statistics after the stores are issued (red is its own LDS region): they drain meanwhile
+  if (STATS)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
 #endif
 }
 
@@ -721,12 +724,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
-  if (STATS) {
-    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
-                                                static_cast<int64_t>(mt) * a.N + n0);
-  }
   __syncthreads();
   if constexpr (BNB) {
+    if (STATS)
+      det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                  static_cast<int64_t>(mt) * a.N + n0);
     bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
     return;
   }
@@ -738,6 +740,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
     if (idx < BM * CPR && row < nvalid)
       *reinterpret_cast<us8*>(a.Y + out_row(a, m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
+  // BN statistics after the stores are issued (red is its own LDS region): they drain meanwhile
+  if (STATS)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
 #endif
 }
 
@@ -1920,8 +1926,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           ct[(w * 32 + i * 16 + g * 4 + r) * kSfLDC + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
-    if constexpr (STATS)
-      det_block_bn_stats<2, 4, 8, 32, 64, 64>(acc, red, w, 0, lane, tid, nvalid, a.pmean, a.pm2, c * 64);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 256 * 8 / NT; ++q) {
@@ -1929,6 +1933,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       if (row < nvalid)
         *reinterpret_cast<us8*>(a.Y + (m0 + row) * 64 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * kSfLDC + cc * 8);
     }
+    if constexpr (STATS)  // after the stores are issued (red is its own LDS region)
+      det_block_bn_stats<2, 4, 8, 32, 64, 64>(acc, red, w, 0, lane, tid, nvalid, a.pmean, a.pm2, c * 64);
     if (c + 1 < c1) {
       // the next chunk's patch: fetched here, not under the MFMAs or the epilogue (both spill at
       // 4 waves / SIMD); the other block on the CU computes meanwhile

@@ -50,7 +50,7 @@ def timeit(fn, iters=10):
     return e0.elapsed_time(e1) / iters
 
 
-tot = {"mine_fwd": 0.0, "mine_fwd_gemm_only": 0.0, "mine_fwd_pf1": 0.0, "mine_dgrad": 0.0, "mine_wgrad": 0.0,
+tot = {"wide_fwd": 0.0, "mine_fwd": 0.0, "mine_fwd_gemm_only": 0.0, "mine_fwd_pf1": 0.0, "mine_dgrad": 0.0, "mine_wgrad": 0.0,
        "miopen_fwd": 0.0, "miopen_bwd": 0.0}
 for (ci, co, s, h), mult in shapes.items():
     ho = h // s
@@ -70,6 +70,11 @@ for (ci, co, s, h), mult in shapes.items():
                      timeit(lambda: conv.conv1x1_nt(x2, w, m=m, stats=False, gather=g)),
                      timeit(lambda: conv.dgrad_1x1(dy, w)) if s == 1 else float("nan"))
     _lib.get_lib().det_conv_nt_set_pf(0)
+    # the occupancy-3 128 x 64 tiles of the short-K wide-N forwards (det_conv_nt_set_wide)
+    _lib.get_lib().det_conv_nt_set_wide(1)
+    wide = (timeit(lambda: conv.conv1x1_nt(x2, w, m=m, stats=True, gather=g)),
+            timeit(lambda: conv.conv1x1_nt(x2, w, m=m, stats=False, gather=g)))
+    _lib.get_lib().det_conv_nt_set_wide(-1)
     best = min(by_pf, key=lambda p: by_pf[p][0])
     t_f, t_g = by_pf[best][0], by_pf[best][1]
     t_d = min(v[2] for v in by_pf.values()) if s == 1 else float("nan")
@@ -85,12 +90,14 @@ for (ci, co, s, h), mult in shapes.items():
            "fwd_ms_by_pf": {p: round(v[0], 4) for p, v in by_pf.items()},
            "gemm_only_ms_by_pf": {p: round(v[1], 4) for p, v in by_pf.items()},
            "dgrad_bt_ms_by_pf": {p: round(v[2], 4) for p, v in by_pf.items()},
+           "wide_fwd_ms": round(wide[0], 4), "wide_gemm_only_ms": round(wide[1], 4),
            "mine_dgrad_ms": round(t_d, 4), "mine_wgrad_ms": round(t_w, 4),
            "miopen_fwd_ms": round(t_mf, 4), "miopen_bwd_ms": round(t_mb, 4),
            "mine_fwd_TBs": round(byt_f / t_f / 1e9, 2), "mine_fwd_TFs": round(fl / t_f / 1e9, 1),
            "gemm_only_TFs": round(fl / t_g / 1e9, 1), "gemm_only_pct_peak": round(100 * fl / t_g / 1e9 / PEAK_TF, 1),
            "miopen_fwd_TFs": round(fl / t_mf / 1e9, 1), "miopen_pct_peak": round(100 * fl / t_mf / 1e9 / PEAK_TF, 1)}
     print(json.dumps(rec), flush=True)
+    tot["wide_fwd"] += min(wide[0], t_f) * mult
     tot["mine_fwd"] += t_f * mult
     tot["mine_fwd_gemm_only"] += t_g * mult
     tot["mine_fwd_pf1"] += by_pf[1][0] * mult

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-4 session 13: occupancy-3 128 x 64 tiles for the short-K wide-N 1x1 forwards (exact test,
+# per-shape sweep, step A/B), then the ResNet DP equivalence tests and the small-launch probe.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r4s13
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_conv_gpu.py -k "wide or prefetch or stats" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 400 python -u scripts/bench_conv1x1.py > $O/conv1x1_wide_sweep.jsonl 2> $O/conv1x1.err || { tail -20 $O/conv1x1.err; exit 1; }
+python3 -c "
+import json
+for l in open('$O/conv1x1_wide_sweep.jsonl'):
+    d=json.loads(l)
+    if 'M' in d: print(d['ci'], d['co'], d['s'], d['h'], 'x', d['mult'], 'fwd', d['mine_fwd_ms'], 'wide', d['wide_fwd_ms'], 'gemm', d['mine_fwd_gemm_only_ms'], 'wide-gemm', d['wide_gemm_only_ms'])
+    else: print(d)
+"
+for v in 0 1; do
+  DET_NT_WIDE=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_wide$v.json 2> $O/bench_wide$v.err || { tail -30 $O/bench_wide$v.err; exit 1; }
+  echo "bench wide=$v $(python3 -c "import json;d=json.load(open('$O/bench_wide$v.json'));print(d['value'],d['ms_per_step'])")"
+done
+timeout -k 10 1000 python -u -m pytest -x -v -s --timeout 900 --timeout-method thread -p no:cacheprovider -m gpu tests/test_dp_resnet_gpu.py > $O/pytest_dp.log 2>&1 || { tail -60 $O/pytest_dp.log; exit 1; }
+grep "dp-vs-single\|passed\|failed" $O/pytest_dp.log | tail -6

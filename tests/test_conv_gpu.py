@@ -119,6 +119,30 @@ def test_conv_nt_prefetch_depths_exact(gpu, nt_pf, pf, m, k, n):
     assert torch.equal(dx.cpu(), want)
 
 
+@pytest.mark.parametrize("m,k,n", [(777, 128, 512), (4096 + 77, 256, 1024), (1500, 512, 2048), (640, 128, 1024)])
+def test_conv_nt_wide_tiles_exact(gpu, m, k, n):
+    """The occupancy-3 128 x 64 tiles of the short-K wide-N forwards (det_conv_nt_set_wide): integer
+    operands, exact against the fp32 product; statistics partials per 128 rows merge to the output's."""
+    from determined_1_amd.ops import _lib
+
+    lib = _lib.get_lib()
+    g = torch.Generator(device="cpu").manual_seed(m + k)
+    a = torch.randint(-2, 3, (m, k), generator=g).to(torch.bfloat16)
+    b = torch.randint(-2, 3, (n, k), generator=g).to(torch.bfloat16)
+    want = (a.float() @ b.float().t()).to(torch.bfloat16)
+    lib.det_conv_nt_set_wide(1)
+    try:
+        y, parts = conv.conv1x1_nt(a.to(gpu), b.to(gpu), stats=True)
+        y2, _ = conv.conv1x1_nt(a.to(gpu), b.to(gpu), stats=False)
+    finally:
+        lib.det_conv_nt_set_wide(-1)
+    assert torch.equal(y.cpu(), want) and torch.equal(y2.cpu(), want)
+    mean, var = _merge(*parts, m)
+    yr = y.double().cpu()
+    torch.testing.assert_close(mean, yr.mean(0), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(var, yr.var(0, unbiased=False), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("m,cin,cout", SHAPES + [(50000, 64, 256)])
 @pytest.mark.parametrize("pro", [False, True])
 def test_conv_wgrad(gpu, m, cin, cout, pro):
