@@ -200,16 +200,17 @@ _SIGNATURES = {
     # det_transformer.hip: fused LayerNorm / dropout / residual / GELU / bias-grad epilogues
     "det_tf_ln_max_hidden": ([], c_int),
     "det_tf_ln_ws_elems": ([c_i64, c_int], c_i64),
-    # stream, dtype, h, r, y, rows, H, gamma, beta, eps, p, seed, offset, mean, rstd
+    # stream, dtype, h, r, y, rows, H, gamma, beta, eps, p, seed, offset, mean, rstd, offset base
     "det_tf_ln_fwd": (
         [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_float, c_float,
-         ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p],
+         ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p, c_void_p],
         c_int,
     ),
-    # stream, dtype, dy, h, r, mean, rstd, gamma, rows, H, p, seed, offset, dr, dh, dgamma, dbeta, dbias, ws
+    # stream, dtype, dy, h, r, mean, rstd, gamma, rows, H, p, seed, offset, dr, dh, dgamma, dbeta, dbias, ws,
+    # offset base
     "det_tf_ln_bwd": (
         [c_void_p, c_int] + [c_void_p] * 6 + [c_i64, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64]
-        + [c_void_p] * 6,
+        + [c_void_p] * 7,
         c_int,
     ),
     "det_tf_col_ws_elems": ([c_i64, c_int], c_i64),
@@ -225,10 +226,11 @@ _SIGNATURES = {
     "det_attn_forward": ([c_void_p, c_void_p], c_int),
     "det_attn_backward": ([c_void_p, c_void_p], c_int),
     "det_attn_set_bwd_merged": ([c_int], c_int),
-    # stream, B, nh, Lq, Lk, p, seed, offset, out
+    # stream, B, nh, Lq, Lk, p, seed, offset, out, offset base
     "det_attn_dropout_mask": ([c_void_p, c_int, c_int, c_int, c_int, c_float, ctypes.c_uint64, ctypes.c_uint64,
-                               c_void_p], c_int),
-    "det_tf_dropout_mask": ([c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p], c_int),
+                               c_void_p, c_void_p], c_int),
+    "det_tf_dropout_mask": ([c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p], c_int),
+    "det_tf_rng_bump": ([c_void_p, c_void_p], c_int),
 }
 
 

@@ -102,7 +102,14 @@ struct Args {
   uint32_t drop_thr;            // drop if 16-bit draw < thr (0: no dropout)
   float drop_scale;             // 65536 / (65536 - thr)
   uint32_t rng_key;
+  // nullable: device counter folded into the key when the kernel runs (a hipGraph replays its
+  // captured key; the captured step bumps the counter first -- ops/transformer.py rng_base)
+  const uint32_t* rng_base;
 };
+
+__device__ __forceinline__ uint32_t run_key(const Args& a) {
+  return a.rng_key ^ (a.rng_base != nullptr ? *a.rng_base * 0x2545F491u : 0u);
+}
 
 __device__ __forceinline__ uint32_t rng_key_for(uint32_t base_key, int b, int head) {
   return base_key ^ (static_cast<uint32_t>(b * 977 + head) * 0x9E3779B9u);
@@ -305,7 +312,7 @@ __global__ void __launch_bounds__(kThreads, (HD * sizeof(E) >= 256 ? 1 : 2)) att
   vt.store_t(reinterpret_cast<E*>(smem + TL::ROW_BYTES));
   __syncthreads();
 
-  const uint32_t key = rng_key_for(a.rng_key, b, head);
+  const uint32_t key = rng_key_for(run_key(a), b, head);
   const uint32_t rowidx = static_cast<uint32_t>(q) * static_cast<uint32_t>(lk_even4(Lk));
   float m = -INFINITY, l = 0.f;
   f32x16 o[NU];
@@ -455,7 +462,7 @@ __device__ __forceinline__ void attn_bwd_dq_body(const Args& a, int bx, unsigned
   if (WRITE_D && qv < Lq && hh == 0) a.delta[li] = D;
   const float lse2 = a.lse[li] * kLog2e;
   const float* mrow = MB ? a.mbias + b * a.mbb + head * a.mbh + static_cast<int64_t>(q) * a.mbq : nullptr;
-  const uint32_t key = rng_key_for(a.rng_key, b, head);
+  const uint32_t key = rng_key_for(run_key(a), b, head);
   const uint32_t rowidx = static_cast<uint32_t>(q) * static_cast<uint32_t>(lk_even4(Lk));
   kt.store_rows(smem);
   vt.store_rows(smem + TL::ROW_BYTES);
@@ -567,7 +574,7 @@ __device__ __forceinline__ void attn_bwd_dkv_body(const Args& a, int bx, unsigne
   }
   const float bk = a.kbias ? fmaxf(a.kbias[static_cast<int64_t>(b) * Lk + kk] * kLog2e, -1e30f) : 0.f;
   const float* mcol = MB ? a.mbias + b * a.mbb + head * a.mbh + kk : nullptr;
-  const uint32_t key = rng_key_for(a.rng_key, b, head);
+  const uint32_t key = rng_key_for(run_key(a), b, head);
   const uint32_t lke = static_cast<uint32_t>(lk_even4(Lk));
   qt.store_rows(smem);
   qt.store_t(reinterpret_cast<E*>(smem + TL::ROW_BYTES));
@@ -716,7 +723,9 @@ bool bwd_merged(int64_t workgroups) {
   return workgroups <= 2 * 256;
 }
 
-__global__ void attn_mask_kernel(int B, int nh, int Lq, int Lk, uint32_t thr, uint32_t base_key, uint8_t* out) {
+__global__ void attn_mask_kernel(int B, int nh, int Lq, int Lk, uint32_t thr, uint32_t key0, const uint32_t* rng_base,
+                                 uint8_t* out) {
+  const uint32_t base_key = key0 ^ (rng_base != nullptr ? *rng_base * 0x2545F491u : 0u);  // run_key
   const int64_t n = static_cast<int64_t>(B) * nh * Lq * Lk;
   const uint32_t lke = static_cast<uint32_t>(lk_even4(Lk));
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -816,6 +825,7 @@ struct DetAttnParams {
   int32_t B, Lq, Lk, nh, hd, dtype;
   float p, scale;
   uint64_t seed, offset;
+  const uint32_t* rng_base;  // nullable (Args::rng_base)
 };
 
 // Which (dtype, head_dim, Lq, Lk) the MFMA kernels cover (LDS holds the double-buffered tiles plus
@@ -851,6 +861,7 @@ static int fill(Args& a, const DetAttnParams* P) {
   a.drop_thr = drop_threshold(P->p);
   a.drop_scale = a.drop_thr ? 65536.0f / static_cast<float>(65536u - a.drop_thr) : 1.f;
   a.rng_key = mix_key(P->seed, P->offset);
+  a.rng_base = P->rng_base;
   return 0;
 }
 
@@ -883,9 +894,9 @@ int det_attn_set_bwd_merged(int on) {
 
 // The keep mask (1 = kept) the kernels derive for (p, seed, offset): [B, nh, Lq, Lk] uint8 (tests).
 int det_attn_dropout_mask(void* stream, int B, int nh, int Lq, int Lk, float p, uint64_t seed, uint64_t offset,
-                          uint8_t* out) {
+                          uint8_t* out, const uint32_t* rng_base) {
   hipLaunchKernelGGL(attn_mask_kernel, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), B, nh, Lq, Lk,
-                     drop_threshold(p), mix_key(seed, offset), out);
+                     drop_threshold(p), mix_key(seed, offset), rng_base, out);
   return static_cast<int>(hipGetLastError());
 }
 

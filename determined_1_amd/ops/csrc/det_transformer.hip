@@ -110,10 +110,15 @@ struct Rng {
   uint32_t k0, k1, o0, o1;  // key = seed, counter words 2/3 = offset
   uint32_t thresh;          // drop if u < thresh  (thresh = p * 2^32)
   float scale;              // 1 / (1 - p)
+  // nullable: device counter added to counter word 3 when the kernel runs.  A hipGraph replays the
+  // (seed, offset) kernel arguments it captured; the captured step bumps this counter first, so every
+  // replay draws fresh masks (ops/transformer.py rng_base / bump_rng_base)
+  const uint32_t* obase;
 };
 
 __device__ __forceinline__ void philox(uint64_t idx, const Rng& g, uint32_t (&u)[4]) {
-  uint32_t c0 = static_cast<uint32_t>(idx), c1 = static_cast<uint32_t>(idx >> 32), c2 = g.o0, c3 = g.o1;
+  uint32_t c0 = static_cast<uint32_t>(idx), c1 = static_cast<uint32_t>(idx >> 32), c2 = g.o0,
+           c3 = g.o1 + (g.obase != nullptr ? *g.obase : 0u);
   uint32_t k0 = g.k0, k1 = g.k1;
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
@@ -724,8 +729,13 @@ __global__ void __launch_bounds__(kThreads) dropout_mask_kernel(int64_t ngroups,
   }
 }
 
-Rng make_rng(float p, uint64_t seed, uint64_t offset) {
+__global__ void rng_bump_kernel(uint32_t* counter) {
+  if (threadIdx.x == 0) counter[threadIdx.x] += 1u;
+}
+
+Rng make_rng(float p, uint64_t seed, uint64_t offset, const uint32_t* obase) {
   Rng g;
+  g.obase = obase;
   g.k0 = static_cast<uint32_t>(seed);
   g.k1 = static_cast<uint32_t>(seed >> 32);
   g.o0 = static_cast<uint32_t>(offset);
@@ -762,9 +772,9 @@ int64_t det_tf_ln_ws_elems(int64_t rows, int H) { return ln_bwd_blocks(rows) * 3
 // applied to h (0 disables).  Writes y, mean[rows], rstd[rows].
 int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y, int64_t rows, int H,
                   const void* gamma, const void* beta, float eps, float p, uint64_t seed, uint64_t offset,
-                  float* mean, float* rstd) {
+                  float* mean, float* rstd, const uint32_t* obase) {
   if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
-  LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset)};
+  LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset, obase)};
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (H % 8 == 0) {  // workgroup per row (128 / 256 / 512 threads of 8 columns each)
     const dim3 wg(static_cast<unsigned>(rows < 65536 ? rows : 65536));
@@ -809,11 +819,12 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
 // produced h).  ws: det_tf_ln_ws_elems(rows, H) fp32.
 int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const void* r, const float* mean,
                   const float* rstd, const void* gamma, int64_t rows, int H, float p, uint64_t seed,
-                  uint64_t offset, void* dr, void* dh, void* dgamma, void* dbeta, void* dbias, float* ws) {
+                  uint64_t offset, void* dr, void* dh, void* dgamma, void* dbeta, void* dbias, float* ws,
+                  const uint32_t* obase) {
   if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   int blocks = static_cast<int>(ln_bwd_blocks(rows));
-  LnBwdArgs a{dy, h, r, mean, rstd, gamma, dr, dh, ws, rows, H, p > 0.f, make_rng(p, seed, offset)};
+  LnBwdArgs a{dy, h, r, mean, rstd, gamma, dr, dh, ws, rows, H, p > 0.f, make_rng(p, seed, offset, obase)};
   if (H > kMaxNarrowH) {
     if (H % 8 != 0) return -1;
     if (blocks > 256) blocks = 256;  // <= ln_bwd_blocks(rows): fits det_tf_ln_ws_elems
@@ -936,12 +947,21 @@ int det_tf_colsum(void* stream, int dtype, const void* x, int64_t rows, int C, v
   return static_cast<int>(hipGetLastError());
 }
 
+// One increment of a dropout offset counter (Rng::obase), stream-ordered: a captured train step
+// starts with it, so each replay of the graph draws new masks.
+int det_tf_rng_bump(void* stream, uint32_t* counter) {
+  if (!counter) return -1;
+  hipLaunchKernelGGL(rng_bump_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), counter);
+  return static_cast<int>(hipGetLastError());
+}
+
 // Materialise the keep-mask (1 = kept) the LN kernels use for [n] elements (n % 4 == 0); tests only.
-int det_tf_dropout_mask(void* stream, int64_t n, float p, uint64_t seed, uint64_t offset, uint8_t* out) {
+int det_tf_dropout_mask(void* stream, int64_t n, float p, uint64_t seed, uint64_t offset, uint8_t* out,
+                        const uint32_t* obase) {
   if (n % 4 != 0 || n <= 0) return -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n / 4, kThreads)), dim3(kThreads), 0, st, n / 4,
-                     make_rng(p, seed, offset), out);
+                     make_rng(p, seed, offset, obase), out);
   return static_cast<int>(hipGetLastError());
 }
 

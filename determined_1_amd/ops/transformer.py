@@ -55,6 +55,28 @@ def next_rng() -> Tuple[int, int]:
     return _RNG["seed"], off
 
 
+_RNG_BASE = {}  # type: Dict[int, torch.Tensor]  # device index -> int32 [1] offset counter
+
+
+def rng_base(device: torch.device) -> int:
+    """Device pointer of the dropout offset counter the kernels add to their captured (seed, offset)
+    (det_transformer.hip Rng::obase, det_attention.hip Args::rng_base)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _RNG_BASE.get(idx)
+    if t is None:
+        t = _RNG_BASE[idx] = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", idx))
+    return t.data_ptr()
+
+
+def bump_rng_base() -> None:
+    """Advance every device's dropout offset counter on the current stream.  A captured train step
+    starts with this, so each hipGraph replay draws new masks from the same captured arguments."""
+    lib = _lib.get_lib()
+    for idx, t in _RNG_BASE.items():
+        _lib.check(lib.det_tf_rng_bump(torch.cuda.current_stream(torch.device("cuda", idx)).cuda_stream,
+                                       t.data_ptr()), "det_tf_rng_bump")
+
+
 def reset_rng(seed: Optional[int] = None) -> None:
     """Start a new stream (the trial controller calls this when it seeds torch)."""
     _RNG["seed"] = None if seed is None else int(seed) & _MASK64
@@ -62,17 +84,21 @@ def reset_rng(seed: Optional[int] = None) -> None:
 
 
 def rng_state() -> Dict[str, Any]:
-    return {"seed": _RNG["seed"], "offset": _RNG["offset"]}
+    return {"seed": _RNG["seed"], "offset": _RNG["offset"],
+            "base": {idx: int(t.item()) for idx, t in _RNG_BASE.items()}}
 
 
 def set_rng_state(state: Dict[str, Any]) -> None:
     _RNG["seed"] = state.get("seed")
     _RNG["offset"] = int(state.get("offset", 1))
+    for idx, v in (state.get("base") or {}).items():
+        if torch.cuda.is_available() and int(idx) < torch.cuda.device_count():
+            rng_base(torch.device("cuda", int(idx)))
+            _RNG_BASE[int(idx)].fill_(int(v))
 
 
 def rng_calls() -> int:
-    """Native dropout calls so far (the hipGraph builder checks that a captured step makes none:
-    its (seed, offset) kernel arguments would replay the same masks every step)."""
+    """Native dropout calls so far."""
     return _RNG["offset"] - 1
 
 
@@ -256,7 +282,7 @@ def _ln_forward(h: torch.Tensor, r: Optional[torch.Tensor], gamma, beta, p: floa
     seed, off = next_rng() if p > 0 else (0, 0)
     _lib.check(lib.det_tf_ln_fwd(_stream(h), _DT[h.dtype], h.data_ptr(), _ptr(r), y.data_ptr(), rows, H,
                                  gamma.data_ptr(), beta.data_ptr(), eps, p, seed, off, mean.data_ptr(),
-                                 rstd.data_ptr()), "det_tf_ln_fwd")
+                                 rstd.data_ptr(), rng_base(h.device) if p > 0 else None), "det_tf_ln_fwd")
     return y, mean, rstd, seed, off
 
 
@@ -272,7 +298,8 @@ def _ln_backward(ctx, dy, h, r, gamma, mean, rstd, need_dh: bool, need_dr: bool,
     ws = torch.empty(int(lib.det_tf_ln_ws_elems(rows, H)), dtype=torch.float32, device=h.device)
     _lib.check(lib.det_tf_ln_bwd(_stream(h), _DT[h.dtype], dy2.data_ptr(), h.data_ptr(), _ptr(r), mean.data_ptr(),
                                  rstd.data_ptr(), gamma.data_ptr(), rows, H, ctx.p, ctx.seed, ctx.off, _ptr(dr),
-                                 _ptr(dh), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), ws.data_ptr()), "det_tf_ln_bwd")
+                                 _ptr(dh), _ptr(dgamma), _ptr(dbeta), _ptr(dbias), ws.data_ptr(),
+                                 rng_base(h.device) if ctx.p > 0 else None), "det_tf_ln_bwd")
     return dh, dr, dgamma, dbeta, dbias
 
 
@@ -338,7 +365,7 @@ class _AttnParams(ctypes.Structure):
                                                  "mbq")]
                 + [(n, ctypes.c_int32) for n in ("B", "Lq", "Lk", "nh", "hd", "dtype")]
                 + [("p", ctypes.c_float), ("scale", ctypes.c_float), ("seed", ctypes.c_uint64),
-                   ("offset", ctypes.c_uint64)])
+                   ("offset", ctypes.c_uint64), ("rng_base", ctypes.c_void_p)])
 
 
 _ATTN_DT = {torch.bfloat16: 0, torch.float32: 1}
@@ -402,6 +429,7 @@ def _attn_forward(q, k, v, nh, kbias, mbias, mstrides, p, scale):
     P = _attn_params(q, k, v, nh, kbias, mbias, mstrides, p, scale)
     P.out, P.lse, P.osb, P.ost = out.data_ptr(), lse.data_ptr(), out.stride(0), out.stride(1)
     P.seed, P.offset = seed, off
+    P.rng_base = rng_base(q.device) if p > 0 else None
     _lib.check(_lib.get_lib().det_attn_forward(_stream(q), ctypes.byref(P)), "det_attn_forward")
     return out, lse, seed, off
 
@@ -416,6 +444,7 @@ def _attn_backward(ctx, dout, q, k, v, out, lse, kbias, mbias, dq, dk, dv):
     P.dqsb, P.dqst, P.dksb, P.dkst, P.dvsb, P.dvst = (dq.stride(0), dq.stride(1), dk.stride(0), dk.stride(1),
                                                       dv.stride(0), dv.stride(1))
     P.seed, P.offset = ctx.seed, ctx.off
+    P.rng_base = rng_base(q.device) if ctx.p > 0 else None
     _lib.check(_lib.get_lib().det_attn_backward(_stream(q), ctypes.byref(P)), "det_attn_backward")
 
 
@@ -572,7 +601,7 @@ def attention_dropout_mask(B: int, nh: int, S: int, p: float, seed: int, offset:
     out = torch.empty(B, nh, S, Lk, dtype=torch.uint8, device=device)
     with torch.cuda.device(device):
         _lib.check(lib.det_attn_dropout_mask(torch.cuda.current_stream(device).cuda_stream, B, nh, S, Lk, p, seed,
-                                             offset, out.data_ptr()), "det_attn_dropout_mask")
+                                             offset, out.data_ptr(), rng_base(device)), "det_attn_dropout_mask")
     return out.bool()
 
 
@@ -582,7 +611,7 @@ def dropout_mask(n: int, p: float, seed: int, offset: int, device: torch.device)
     out = torch.empty(n, dtype=torch.uint8, device=device)
     with torch.cuda.device(device):
         _lib.check(lib.det_tf_dropout_mask(torch.cuda.current_stream(device).cuda_stream, n, p, seed, offset,
-                                           out.data_ptr()), "det_tf_dropout_mask")
+                                           out.data_ptr(), rng_base(device)), "det_tf_dropout_mask")
     return out.bool()
 
 

@@ -49,16 +49,19 @@ THRASH_MIN = 4
 
 
 @contextlib.contextmanager
-def _no_native_rng() -> Iterator[None]:
-    """Fail a train-step capture that draws native dropout masks (ops/transformer.py next_rng): their
-    Philox (seed, offset) are kernel arguments, so every replay would repeat the captured masks.
-    The capture then fails like any capture-unsafe op and the step runs eagerly."""
+def _native_rng_advance() -> Iterator[None]:
+    """Inside a train-step capture: the native dropout kernels (ops/transformer.py) take their
+    Philox (seed, offset) as kernel arguments, which a replay repeats; they also add a device offset
+    counter, and the captured step starts by bumping it, so every replay draws new masks."""
     from determined_1_amd.ops import transformer as _tf
 
-    c0 = _tf.rng_calls()
+    c0, existed = _tf.rng_calls(), set(_tf._RNG_BASE)
+    _tf.bump_rng_base()
     yield
-    if _tf.rng_calls() != c0:
-        raise RuntimeError("train_batch draws native dropout masks, whose Philox offsets a replay would repeat")
+    if _tf.rng_calls() != c0 and set(_tf._RNG_BASE) != existed:
+        # the counter was created inside the capture (its zero-fill would run on every replay): fail
+        # this capture; the eager step creates it and the next capture bumps it
+        raise RuntimeError("native dropout offset counter created during capture")
 CHUNK_WARMUP = 1  # per-batch chunks per multi-batch key before capturing it
 CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 
@@ -217,7 +220,7 @@ class TrainStepGraph:
             self.pool = torch.cuda.graph_pool_handle()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self.pool), _no_native_rng():
+            with torch.cuda.graph(graph, pool=self.pool), _native_rng_advance():
                 out = self._eager(static_batch, epoch_idx, batch_idx)
         except Exception as e:  # capture-unsafe op in user code or a library: stay eager
             for f, h in zip(self.fused, host):
@@ -299,7 +302,7 @@ class TrainStepGraph:
             self.pool = torch.cuda.graph_pool_handle()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self.pool), _no_native_rng():
+            with torch.cuda.graph(graph, pool=self.pool), _native_rng_advance():
                 outs = []
                 for i, b in enumerate(views):
                     o = self._eager(b, epoch_idx, batch_idx + i)

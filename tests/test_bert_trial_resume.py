@@ -84,11 +84,24 @@ def test_dropout_rng_stream_is_trial_state():
 
 
 @pytest.mark.gpu
-def test_hip_graph_refuses_native_dropout_steps(gpu):
-    """A captured step would replay its dropout masks (kernel-argument Philox offsets): the BERT
-    trial with dropout runs eagerly under optimizations.hip_graph, with the reason logged."""
+def test_hip_graph_replays_draw_fresh_dropout_masks(gpu):
+    """The native dropout kernels take (seed, offset) as kernel arguments, which a hipGraph replay
+    repeats; the captured step bumps a device offset counter the kernels add, so the BERT trial runs
+    as graph replays (no eager fallback) and every replay draws new masks -- the counter equals the
+    replay count, and a different counter value gives a different mask."""
+    import torch
+
+    from determined_1_amd.ops import transformer as tf
+
     trial = _trial()
     hp = dict(HP, amp="O2", max_seq_length=64)
-    ctrl, _ = run(trial, hp, Recorder().train(1, 4, 0), trial_seed=5, optimizations={"hip_graph": True}, use_gpu=True)
+    ctrl, _ = run(trial, hp, Recorder().train(1, 6, 0), trial_seed=5, optimizations={"hip_graph": True}, use_gpu=True)
     g = ctrl._graph
-    assert g is not None and g.replays == 0 and "dropout" in (g.disabled_reason or ""), g.disabled_reason
+    assert g is not None and g.disabled_reason is None and g.replays >= 3, (g.disabled_reason, g.replays)
+    idx = torch.cuda.current_device()
+    assert int(tf._RNG_BASE[idx].item()) >= g.replays
+    m0 = tf.dropout_mask(4096, 0.1, 123, 7, gpu)
+    tf._RNG_BASE[idx].add_(1)
+    m1 = tf.dropout_mask(4096, 0.1, 123, 7, gpu)
+    tf._RNG_BASE[idx].sub_(1)
+    assert not torch.equal(m0, m1)
