@@ -1,4 +1,5 @@
 #!/bin/bash
+# Round-4 session 13 (+ graph-safe native dropout: transformer/attention/BERT tests, BERT eager vs hipGraph):
 # Round-4 session 13: occupancy-3 128 x 64 tiles for the short-K wide-N 1x1 forwards (exact test,
 # per-shape sweep, step A/B), then the ResNet DP equivalence tests and the small-launch probe.
 set -o pipefail
@@ -8,6 +9,12 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_conv_gpu.py -k "wide or prefetch or stats" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests/test_transformer_gpu.py tests/test_attention_gpu.py tests/test_bert_trial_resume.py > $O/pytest_tf.log 2>&1 || { tail -60 $O/pytest_tf.log; exit 1; }
+tail -1 $O/pytest_tf.log
+for g in "" "--hip-graph"; do
+  timeout -k 10 400 python -u scripts/bench_bert.py --steps 30 --warmup 8 $g > $O/bert$g.json 2> $O/bert$g.err || { tail -20 $O/bert$g.err; exit 1; }
+  echo "bert $g $(cut -c1-120 $O/bert$g.json) $(grep -o '"graph_stats.*' $O/bert$g.json | cut -c1-100)"
+done
 timeout -k 10 400 python -u scripts/bench_conv1x1.py > $O/conv1x1_wide_sweep.jsonl 2> $O/conv1x1.err || { tail -20 $O/conv1x1.err; exit 1; }
 python3 -c "
 import json
