@@ -27,5 +27,3 @@ for v in 0 1; do
   DET_NT_WIDE=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_wide$v.json 2> $O/bench_wide$v.err || { tail -30 $O/bench_wide$v.err; exit 1; }
   echo "bench wide=$v $(python3 -c "import json;d=json.load(open('$O/bench_wide$v.json'));print(d['value'],d['ms_per_step'])")"
 done
-timeout -k 10 1000 python -u -m pytest -x -v -s --timeout 900 --timeout-method thread -p no:cacheprovider -m gpu tests/test_dp_resnet_gpu.py > $O/pytest_dp.log 2>&1 || { tail -60 $O/pytest_dp.log; exit 1; }
-grep "dp-vs-single\|passed\|failed" $O/pytest_dp.log | tail -6
