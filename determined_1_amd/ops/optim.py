@@ -202,6 +202,18 @@ class FusedOptimizer:
     def load_state_dict(self, state_dict: Dict[str, Any]) -> None:
         had = [g.initialized for g in self.groups]
         self._orig_load_state_dict(state_dict)
+        # torch casts floating state to its parameter's dtype on load (bf16 for O2 parameters), which
+        # would round the fp32 moments and master weights the arenas keep: put the saved values back
+        # at their own precision before they are copied into the arenas
+        params = [p for g in self.opt.param_groups for p in g["params"]]
+        saved = state_dict.get("state", {})
+        for k, p in enumerate(params):
+            sv = saved.get(k)
+            if not sv or p not in self.opt.state:
+                continue
+            for name, val in sv.items():
+                if isinstance(val, torch.Tensor) and val.is_floating_point() and name != "step":
+                    self.opt.state[p][name] = val.to(device=p.device)
         # torch replaced our state views with fresh tensors; copy them back into the arenas.
         for gi, gs in enumerate(self.groups):
             group = self.opt.param_groups[gi]
