@@ -9,7 +9,7 @@ mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_conv_gpu.py -k "wide or prefetch or stats" > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests/test_transformer_gpu.py tests/test_attention_gpu.py tests/test_bert_trial_resume.py > $O/pytest_tf.log 2>&1 || { tail -60 $O/pytest_tf.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests/test_transformer_gpu.py tests/test_attention_gpu.py > $O/pytest_tf.log 2>&1 || { tail -60 $O/pytest_tf.log; exit 1; }
 tail -1 $O/pytest_tf.log
 for g in "" "--hip-graph"; do
   timeout -k 10 400 python -u scripts/bench_bert.py --steps 30 --warmup 8 $g > $O/bert$g.json 2> $O/bert$g.err || { tail -20 $O/bert$g.err; exit 1; }
@@ -27,3 +27,7 @@ for v in 0 1; do
   DET_NT_WIDE=$v timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_wide$v.json 2> $O/bench_wide$v.err || { tail -30 $O/bench_wide$v.err; exit 1; }
   echo "bench wide=$v $(python3 -c "import json;d=json.load(open('$O/bench_wide$v.json'));print(d['value'],d['ms_per_step'])")"
 done
+# last: the BERT trial resume / dropout-graph tests (session 12 hung in the first of them and left
+# the GPU faulted; not reproduced on CPU): verbose, stack dumps of every thread after 90 s
+timeout -k 10 240 python -u -X faulthandler -m pytest -x -v -s --timeout 200 --timeout-method thread -o faulthandler_timeout=90 -p no:cacheprovider -m gpu tests/test_bert_trial_resume.py > $O/pytest_bert_resume.log 2>&1 || { tail -80 $O/pytest_bert_resume.log; exit 1; }
+tail -3 $O/pytest_bert_resume.log
