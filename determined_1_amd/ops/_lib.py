@@ -45,7 +45,7 @@ _SIGNATURES = {
     # amsgrad, bias_c1, bias_c2_sqrt, g_scale, g_scale_dev, found_inf
     "det_adam_step": (
         [c_void_p, c_int, c_int] + [c_void_p] * 6 + [c_i64] + [c_float] * 5
-        + [c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p],
+        + [c_int, c_int, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p],
         c_int,
     ),
     # stream, g_dtype, out_dtype, p, g, square_avg, momentum_buf, grad_avg, out_model, n, lr,

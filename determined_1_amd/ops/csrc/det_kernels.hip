@@ -112,6 +112,9 @@ struct AdamArgs {
   float lr, beta1, beta2, eps, wd;
   int adamw, amsgrad;
   float bias_c1, bias_c2_sqrt;  // 1-b1^t, sqrt(1-b2^t)
+  // nullable: [lr, bias_c1, bias_c2_sqrt] read from device memory at run time instead of the values
+  // above -- a hipGraph replays its kernel arguments, and these three change every step
+  const float* hyper;
 };
 struct RmsArgs {
   float lr, alpha, eps, wd, momentum;
@@ -142,9 +145,12 @@ struct AdamOp {
   AdamArgs a;
   __device__ __forceinline__ void operator()(float& p, float g, float* m, float* v,
                                              float* vmax) const {
+    const float lr = a.hyper ? a.hyper[0] : a.lr;
+    const float bc1 = a.hyper ? a.hyper[1] : a.bias_c1;
+    const float bc2s = a.hyper ? a.hyper[2] : a.bias_c2_sqrt;
     if (a.wd != 0.f) {
       if (a.adamw)
-        p = p * (1.f - a.lr * a.wd);
+        p = p * (1.f - lr * a.wd);
       else
         g = fmaf(a.wd, p, g);
     }
@@ -157,8 +163,8 @@ struct AdamOp {
       vd = fmaxf(*vmax, vv);
       *vmax = vd;
     }
-    float denom = sqrtf(vd) / a.bias_c2_sqrt + a.eps;
-    p = p - (a.lr / a.bias_c1) * (mm / denom);
+    float denom = sqrtf(vd) / bc2s + a.eps;
+    p = p - (lr / bc1) * (mm / denom);
   }
 };
 
@@ -520,8 +526,8 @@ int det_adam_step(void* stream, int g_dtype, int out_dtype, float* p, const void
                   float* v, float* vmax, void* out_model, int64_t n, float lr, float beta1,
                   float beta2, float eps, float wd, int adamw, int amsgrad, float bias_c1,
                   float bias_c2_sqrt, float g_scale, const float* g_scale_dev,
-                  const int* found_inf) {
-  AdamOp op{{lr, beta1, beta2, eps, wd, adamw, amsgrad, bias_c1, bias_c2_sqrt}};
+                  const int* found_inf, const float* hyper) {
+  AdamOp op{{lr, beta1, beta2, eps, wd, adamw, amsgrad, bias_c1, bias_c2_sqrt, hyper}};
   if (amsgrad)
     return launch_opt<AdamOp, 3>((hipStream_t)stream, g_dtype, out_dtype, p, g, m, v, vmax,
                                  out_model, n, g_scale, g_scale_dev, found_inf, op);

@@ -94,6 +94,9 @@ class _GroupState:
         self.initialized = False
         self.step = None  # type: Optional[torch.Tensor]  # shared CPU scalar (torch's layout)
         self.momentum_ready = False  # SGD: torch clones d_p on the first step
+        # Adam on the GPU: [lr, 1 - b1^t, sqrt(1 - b2^t)] in device memory, read by the kernel at run
+        # time (a hipGraph replays kernel arguments; these change every step)
+        self.hyper_dev = None  # type: Optional[torch.Tensor]
 
 
 class FusedOptimizer:
@@ -235,10 +238,8 @@ class FusedOptimizer:
     # scalar hyper-parameters baked in, so the graph is keyed by the values the NEXT step would
     # pass, and the host-side bookkeeping a replay skips is advanced explicitly.
     def graph_capturable(self) -> bool:
-        """Kernel arguments do not change from step to step by themselves (Adam's bias corrections
-        and Adagrad's lr decay do)."""
-        if self.kind in ("adam", "adamw"):
-            return False
+        """Kernel arguments do not change from step to step by themselves (Adagrad's lr decay does;
+        Adam's per-step lr and bias corrections are read from device memory, see graph_prepare)."""
         if self.kind == "adagrad":
             return all(float(g.get("lr_decay", 0.0)) == 0.0 for g in self.opt.param_groups)
         return True
@@ -250,8 +251,38 @@ class FusedOptimizer:
             h = self._hyper(group, gs) if gs.initialized else {"uninitialized": 1}
             if self.kind == "sgd" and gs.initialized:
                 h["first"] = int(not gs.momentum_ready)
+            if self.kind in ("adam", "adamw"):
+                for key in ("lr", "bc1", "bc2s"):  # device-side (graph_prepare)
+                    h.pop(key, None)
             sig.append(tuple(sorted(h.items())))
         return tuple(sig)
+
+    def chunk_capturable(self) -> bool:
+        """Several steps in one replay: Adam's device-side hyper-parameters hold one step's values."""
+        return self.kind not in ("adam", "adamw")
+
+    def capturing(self, on: bool) -> None:
+        """Inside a capture the step must not upload its hyper-parameters (the upload would be
+        recorded and replayed with stale host data); graph_prepare does it before each replay."""
+        self._capturing = on
+
+    def graph_prepare(self, advanced: bool = False) -> None:
+        """Before a replay: upload the hyper-parameters of the step it will run -- step count + 1, or
+        the count itself right after a capture (which advanced the host bookkeeping already)."""
+        if self.kind not in ("adam", "adamw"):
+            return
+        for gi, gs in enumerate(self.groups):
+            if gs.hyper_dev is None:
+                continue
+            group = self.opt.param_groups[gi]
+            t = (float(gs.step.item()) if gs.step is not None else 0.0) + (0.0 if advanced else 1.0)
+            b1, b2 = group["betas"]
+            self._upload_hyper(gs, float(group["lr"]), 1.0 - float(b1) ** t, math.sqrt(1.0 - float(b2) ** t))
+
+    @staticmethod
+    def _upload_hyper(gs: _GroupState, lr: float, bc1: float, bc2s: float) -> None:
+        host = torch.tensor([lr, bc1, bc2s], dtype=torch.float32).pin_memory()
+        gs.hyper_dev.copy_(host, non_blocking=True)  # the caching host allocator keeps it until copied
 
     def host_state(self) -> List[Tuple[Optional[float], bool]]:
         return [(float(gs.step) if gs.step is not None else None, gs.momentum_ready) for gs in self.groups]
@@ -340,8 +371,15 @@ class FusedOptimizer:
             rc = lib.det_sgd_step(st, gd, od, p, g, ptr(s[0]), om, n, h["lr"], h["momentum"], h["dampening"], h["wd"],
                                   h["nesterov"], h["first"], gsc, gsd, fi)
         elif k in ("adam", "adamw"):
+            if gs.hyper_dev is None:
+                if getattr(self, "_capturing", False):
+                    raise RuntimeError("first Adam step inside a graph capture (no eager step yet)")
+                gs.hyper_dev = torch.zeros(3, dtype=torch.float32, device=a.flat_param.device)
+            if not getattr(self, "_capturing", False) and a is gs.arenas[0]:
+                self._upload_hyper(gs, h["lr"], h["bc1"], h["bc2s"])
             rc = lib.det_adam_step(st, gd, od, p, g, ptr(s[0]), ptr(s[1]), ptr(s[2]), om, n, h["lr"], h["b1"], h["b2"],
-                                   h["eps"], h["wd"], int(k == "adamw"), h["amsgrad"], h["bc1"], h["bc2s"], gsc, gsd, fi)
+                                   h["eps"], h["wd"], int(k == "adamw"), h["amsgrad"], h["bc1"], h["bc2s"], gsc, gsd, fi,
+                                   gs.hyper_dev.data_ptr())
         elif k == "rmsprop":
             rc = lib.det_rmsprop_step(st, gd, od, p, g, ptr(s[0]), ptr(s[1]), ptr(s[2]), om, n, h["lr"], h["alpha"],
                                       h["eps"], h["wd"], h["momentum"], h["centered"], gsc, gsd, fi)

@@ -182,6 +182,8 @@ class TrainStepGraph:
             return self._eager(batch, epoch_idx, batch_idx)
         # the capture recorded but did not execute this batch's work: run it now (host state
         # was advanced during the capture itself)
+        for f in self.fused:
+            f.graph_prepare(advanced=True)
         g.graph.replay()
         self.replays += 1
         g.replays += 1
@@ -190,6 +192,8 @@ class TrainStepGraph:
     def _replay(self, g: _Graph, leaves: List[Any]) -> Any:
         for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
             dst.copy_(src, non_blocking=True)
+        for f in self.fused:
+            f.graph_prepare()
         g.graph.replay()
         for f in self.fused:
             f.graph_replayed()
@@ -220,8 +224,14 @@ class TrainStepGraph:
             self.pool = torch.cuda.graph_pool_handle()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self.pool), _native_rng_advance():
-                out = self._eager(static_batch, epoch_idx, batch_idx)
+            for f in self.fused:
+                f.capturing(True)
+            try:
+                with torch.cuda.graph(graph, pool=self.pool), _native_rng_advance():
+                    out = self._eager(static_batch, epoch_idx, batch_idx)
+            finally:
+                for f in self.fused:
+                    f.capturing(False)
         except Exception as e:  # capture-unsafe op in user code or a library: stay eager
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
@@ -249,6 +259,8 @@ class TrainStepGraph:
         False: partial chunks at epoch ends replay per batch rather than growing one multi-batch
         graph per odd size) -- then the per-batch metrics are in ``self.last_chunk_metrics``."""
         self.last_chunk_metrics = None
+        if self.chunk_disabled is None and not all(f.chunk_capturable() for f in self.fused):
+            self.chunk_disabled = "the optimizer's per-step hyper-parameters hold one step (replaying per batch)"
         if capture and self.disabled_reason is None and self.chunk_disabled is None:
             leaves, spec = pytree.tree_flatten(chunk.stacked)
             if all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
