@@ -206,6 +206,8 @@ struct NtArgs {
   const float* a2shift;
   // nullable: C = op(A) . B^T + bias[n] (bf16 [N]; added to the fp32 accumulators, one rounding)
   const unsigned short* bias;
+  // 1: BN statistics before the C stores (DET_STATS_FIRST=1 A/B); 0: after them (default)
+  int stats_first;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -499,6 +501,9 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
+  if (STATS && a.stats_first && !BNB)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   __syncthreads();
   if constexpr (BNB) {
     if (STATS)
@@ -569,7 +574,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
       *reinterpret_cast<us8*>(a.C + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
   // BN statistics after the stores are issued (red is a separate LDS array): they drain meanwhile
-  if (STATS)
+  if (STATS && !a.stats_first)
     det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
                                                 static_cast<int64_t>(mt) * a.N + n0);
 }
@@ -804,7 +809,13 @@ constexpr int nt_smem() {
 // PF (prefetch depth) applies to the plain forward / input-gradient variants; the fused ones
 // (AFWD, ABN, BNB) already use their registers for the extra operands and stay at PF = 1.
 template <int BM, int BN, int WM, int WN, int OCC, int PF = 1>
-int launch_nt(hipStream_t st, const NtArgs& a, bool pro, bool stats, bool stride2, bool bnb = false, bool bt = false) {
+int launch_nt(hipStream_t st, const NtArgs& a_in, bool pro, bool stats, bool stride2, bool bnb = false, bool bt = false) {
+  NtArgs a = a_in;
+  static const int stats_first = [] {
+    const char* e = std::getenv("DET_STATS_FIRST");
+    return e != nullptr && e[0] == '1' ? 1 : 0;
+  }();
+  a.stats_first = stats_first;
   const int64_t mtiles = (a.M + BM - 1) / BM;
   const int64_t nwg = mtiles * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;

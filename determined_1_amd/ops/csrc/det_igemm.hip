@@ -98,7 +98,19 @@ struct IgArgs {
   // conv3p prologue: the input operand is relu(X * pro_scale[c] + pro_shift[c]) (padding stays 0)
   const float* pro_scale;
   const float* pro_shift;
+  // 1: the BN-statistics epilogue runs before the C stores (the round-3 order, DET_STATS_FIRST=1 A/B);
+  // 0: after them, so the stores drain while the statistics are reduced
+  int stats_first;
 };
+
+// DET_STATS_FIRST (read once): the statistics-epilogue order of every GEMM with STATS
+inline int stats_first_flag() {
+  static const int v = [] {
+    const char* e = std::getenv("DET_STATS_FIRST");
+    return e != nullptr && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
 
 // the row of Y (and of the BN input in the BNB epilogue) that GEMM row m writes
 __device__ __forceinline__ int64_t out_row(const IgArgs& a, int64_t m) {
@@ -328,6 +340,9 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
+  if (STATS && a.stats_first)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   __syncthreads();
   constexpr int CPR = BN / 8;
 #pragma unroll
@@ -338,7 +353,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm_kernel(IgArgs a) {
       *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
   // BN statistics after the stores are issued (red is its own LDS region): they drain meanwhile
-  if (STATS)
+  if (STATS && !a.stats_first)
     det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
                                                 static_cast<int64_t>(mt) * a.N + n0);
 }
@@ -510,6 +525,9 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
+  if (STATS && a.stats_first && !BNB)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   __syncthreads();
   if constexpr (BNB) {
     if (STATS)
@@ -527,7 +545,7 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
       *reinterpret_cast<us8*>(a.Y + (m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
   // BN statistics after the stores are issued (red is its own LDS region): they drain meanwhile
-  if (STATS)
+  if (STATS && !a.stats_first)
     det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
                                                 static_cast<int64_t>(mt) * a.N + n0);
 #endif
@@ -724,6 +742,9 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
         const int col = wn * TN + j * 16 + (lane & 15);
         ct[row * LDC + col] = f2bf(acc[i][j][r]);
       }
+  if (STATS && a.stats_first && !BNB)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
   __syncthreads();
   if constexpr (BNB) {
     if (STATS)
@@ -741,14 +762,16 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
       *reinterpret_cast<us8*>(a.Y + out_row(a, m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
   }
   // BN statistics after the stores are issued (red is its own LDS region): they drain meanwhile
-  if (STATS)
+  if (STATS && !a.stats_first)
     det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
                                                 static_cast<int64_t>(mt) * a.N + n0);
 #endif
 }
 
 template <int BM, int BN, int WM, int WN, int NS>
-int launch3(hipStream_t st, const IgArgs& a, bool stats, bool bnb = false) {
+int launch3(hipStream_t st, const IgArgs& a_in, bool stats, bool bnb = false) {
+  IgArgs a = a_in;
+  a.stats_first = stats_first_flag();
   constexpr int kThreads = WM * WN * 64;
   if (a.N % BN != 0 || a.Cin % 32 != 0) return -6;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
@@ -768,7 +791,9 @@ int launch3(hipStream_t st, const IgArgs& a, bool stats, bool bnb = false) {
 }
 
 template <int BM, int BN, int WM, int WN, int NS, int OCC>
-int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats, bool bnb = false) {
+int launch2(hipStream_t st, const IgArgs& a_in, bool dense, bool stats, bool bnb = false) {
+  IgArgs a = a_in;
+  a.stats_first = stats_first_flag();
   constexpr int kThreads = WM * WN * 64;
   if (a.N % BN != 0 || a.Cin % 64 != 0) return -6;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
@@ -788,7 +813,9 @@ int launch2(hipStream_t st, const IgArgs& a, bool dense, bool stats, bool bnb = 
 }
 
 template <int BM, int BN, int WM, int WN>
-int launch(hipStream_t st, const IgArgs& a, bool dense, bool stats) {
+int launch(hipStream_t st, const IgArgs& a_in, bool dense, bool stats) {
+  IgArgs a = a_in;
+  a.stats_first = stats_first_flag();
   constexpr int kThreads = WM * WN * 64;
   const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
