@@ -29,10 +29,15 @@ PER_RANK, SIZE = 8, 64
 
 class Batches(torch.utils.data.Dataset):
     def __init__(self, order):
-        g = torch.Generator().manual_seed(11)
+        # batch b from its own generator: its content must not depend on how many batches the run
+        # uses ("b0" alone vs "pair"), or the split-batch check compares different data
         n = max(order) + 1
-        self.img = torch.randint(0, 256, (n, PER_RANK, SIZE, SIZE, 3), generator=g, dtype=torch.uint8)
-        self.lab = torch.randint(0, 10, (n, PER_RANK), generator=g)
+        self.img = torch.empty((n, PER_RANK, SIZE, SIZE, 3), dtype=torch.uint8)
+        self.lab = torch.empty((n, PER_RANK), dtype=torch.int64)
+        for b in range(n):
+            g = torch.Generator().manual_seed(11 + 1000 * b)
+            self.img[b] = torch.randint(0, 256, (PER_RANK, SIZE, SIZE, 3), generator=g, dtype=torch.uint8)
+            self.lab[b] = torch.randint(0, 10, (PER_RANK,), generator=g)
         self.order = order
 
     def __len__(self):
@@ -49,6 +54,16 @@ class Trial(ResNetImageNetTrial):
         order = {"seq": list(range(steps)), "dup": [i for i in range(steps) for _ in range(2)], "b0": [0], "b1": [1],
                  "pair": [0, 1]}[data]
         return det_torch.DataLoader(Batches(order), batch_size=self.context.get_per_slot_batch_size(), shuffle=False)
+
+
+if os.environ.get("RDP_DEBUG"):  # print each rank's batch labels (data-sharding checks)
+    _orig_tb = Trial.train_batch
+
+    def _tb(self, batch, epoch_idx, batch_idx):
+        print("RANK", os.environ.get("RANK", "0"), "batch", batch_idx, "labels", batch[1].tolist(), flush=True)
+        return _orig_tb(self, batch, epoch_idx, batch_idx)
+
+    Trial.train_batch = _tb
 
 
 def main() -> None:
