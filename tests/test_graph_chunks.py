@@ -62,6 +62,18 @@ class StackedTrial(pytorch.PyTorchTrial):
         return {"validation_loss": nn.functional.cross_entropy(self.model(x).float(), y)}
 
 
+class StackedTrialNoBatchIdx(StackedTrial):
+    """The same step without reading batch_idx: the hipGraph builder refuses a train_batch that
+    reads it (a replay would reuse the captured value); epoch_idx keys the graphs per epoch."""
+
+    def train_batch(self, batch, epoch_idx, batch_idx):
+        x, y = batch
+        loss = nn.functional.cross_entropy(self.model(x).float(), y) * (1.0 + 0.0 * epoch_idx)
+        self.context.backward(loss)
+        self.context.step_optimizer(self.opt)
+        return {"loss": loss}
+
+
 def test_chunked_batches_respect_epochs_and_offsets():
     dl = pytorch.DataLoader(StackedRows(100), batch_size=10, collate_fn=pytorch.passthrough_collate)
     loader = dl.get_data_loader(repeat=True, skip=3)
@@ -78,11 +90,11 @@ def test_chunked_batches_respect_epochs_and_offsets():
             assert torch.equal(b[0], x) and torch.equal(b[1], y)
 
 
-def _run(monkeypatch, k, use_gpu=False, graph=False, rows=160):
+def _run(monkeypatch, k, use_gpu=False, graph=False, rows=160, trial=StackedTrial):
     monkeypatch.setenv("DET_GRAPH_BATCHES", str(k))
     monkeypatch.setenv("DET_HIP_GRAPH", "1" if graph else "0")
     rec = Recorder().train(1, 13, 0).validate(1, 13).train(2, 9, 13).train(3, 11, 22).validate(3, 33)
-    ctrl, resp = run(StackedTrial, {"global_batch_size": 16, "train_rows": rows}, rec, use_gpu=use_gpu,
+    ctrl, resp = run(trial, {"global_batch_size": 16, "train_rows": rows}, rec, use_gpu=use_gpu,
                      records_per_epoch=rows)
     if use_gpu:
         torch.cuda.synchronize()
@@ -113,8 +125,8 @@ def test_multibatch_graph_replay_matches_eager(gpu, monkeypatch):
     # 30-batch epochs: train_batch reads epoch_idx (graphs are keyed per epoch) and only full
     # 4-batch chunks are captured, after one per-batch warm-up of their key, so an epoch needs
     # several full chunks to replay any (10-batch epochs have one full chunk after the first)
-    _, p_e, l_e, v_e = _run(monkeypatch, 1, use_gpu=True, graph=False, rows=480)
-    c, p_g, l_g, v_g = _run(monkeypatch, 4, use_gpu=True, graph=True, rows=480)
+    _, p_e, l_e, v_e = _run(monkeypatch, 1, use_gpu=True, graph=False, rows=480, trial=StackedTrialNoBatchIdx)
+    c, p_g, l_g, v_g = _run(monkeypatch, 4, use_gpu=True, graph=True, rows=480, trial=StackedTrialNoBatchIdx)
     assert c._graph is not None and c._graph.chunk_replays > 0, c._graph.stats() if c._graph else None
     assert c._eval_graph is not None and c._eval_graph.replays > 0
     assert len(l_g) == len(l_e)
