@@ -64,9 +64,20 @@ def main() -> None:
             r["mfma_util"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui / 8 * NCU) / 4, 3)
         if gui > 0:
             r["gui_active_M"] = round(gui / 1e6, 2)
+        # memory-side traffic (KB summed over dispatches; gfx950 FETCH_SIZE counts 64 B per 128-B
+        # request of a wide streaming read, so it is doubled -- MI355X_MICROARCH.md)
+        if "FETCH_SIZE" in c:
+            r["fetch_MB"] = round(2 * c["FETCH_SIZE"] / 1024.0, 1)
+        if "WRITE_SIZE" in c:
+            r["write_MB"] = round(c["WRITE_SIZE"] / 1024.0, 1)
+        hit, miss = c.get("TCC_HIT_sum", c.get("TCC_HIT")), c.get("TCC_MISS_sum", c.get("TCC_MISS"))
+        if hit is not None and miss is not None and hit + miss > 0:
+            r["l2_hit"] = round(hit / (hit + miss), 3)
+        if disp[k]:
+            r["dispatches"] = len(disp[k])
         rows.append(r)
     cols = ["kernel", "dispatches", "gui_active_M", "mfma_util", "wait_any", "wait_inst", "active", "wait_lds",
-            "lds_conflict", "lds_conflict_per_wave_cyc"]
+            "lds_conflict", "lds_conflict_per_wave_cyc", "fetch_MB", "write_MB", "l2_hit"]
     cols = [c for c in cols if any(c in r for r in rows)]
     for r in rows[:args.top]:
         print("  ".join(f"{c}={r[c]}" for c in cols if c in r))
