@@ -80,9 +80,11 @@ def main() -> None:
                       "import_s": round(t_import, 2), "controller_build_s": round(t_build, 2),
                       "hip_graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
                       "loss": res[names[-2]]["metrics"]["avg_metrics"].get("loss") if len(names) > 1 else None,
-                      "loss_per_chunk": [res[n]["metrics"]["avg_metrics"].get("loss") for n in names
-                                         if n.startswith("train")],
-                      "validation_error": res["val"]["metrics"]["validation_metrics"].get("validation_error")}),
+                      "loss_per_chunk": [float(res[n]["metrics"]["avg_metrics"].get("loss", float("nan")))
+                                         for n in names if n.startswith("train")],
+                      "validation_error": float(res["val"]["metrics"]["validation_metrics"].get("validation_error",
+                                                                                                float("nan")))},
+                     default=float),
           flush=True)
 
 
