@@ -24,6 +24,8 @@ def main() -> None:
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
     ap.add_argument("--graph-batches", type=int, default=1, help="optimizations.hip_graph_batches")
+    ap.add_argument("--no-dropout", action="store_true", help="dropout 0 (deterministic eager/graph comparison)")
+    ap.add_argument("--batch-losses", action="store_true", help="also print every batch's loss")
     args = ap.parse_args()
     t0 = time.time()
     import torch
@@ -34,7 +36,9 @@ def main() -> None:
 
     t_import = time.time() - t0
     cfg = {"hyperparameters": {"global_batch_size": args.batch, "learning_rate": 1e-3, "learning_rate_decay": 1e-6,
-                               "layer1_dropout": 0.25, "layer2_dropout": 0.25, "layer3_dropout": 0.5,
+                               "layer1_dropout": 0.0 if args.no_dropout else 0.25,
+                               "layer2_dropout": 0.0 if args.no_dropout else 0.25,
+                               "layer3_dropout": 0.0 if args.no_dropout else 0.5,
                                "amp": args.amp},
            "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": args.batches}},
            "records_per_epoch": 50000, "scheduling_unit": args.chunk,
@@ -82,6 +86,8 @@ def main() -> None:
                       "loss": res[names[-2]]["metrics"]["avg_metrics"].get("loss") if len(names) > 1 else None,
                       "loss_per_chunk": [float(res[n]["metrics"]["avg_metrics"].get("loss", float("nan")))
                                          for n in names if n.startswith("train")],
+                      "batch_losses": [float(m["loss"]) for n in names if n.startswith("train")
+                                       for m in res[n]["metrics"]["batch_metrics"]] if args.batch_losses else None,
                       "validation_error": float(res["val"]["metrics"]["validation_metrics"].get("validation_error",
                                                                                                 float("nan")))},
                      default=float),
