@@ -24,6 +24,8 @@ def main() -> None:
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
     ap.add_argument("--graph-batches", type=int, default=1, help="optimizations.hip_graph_batches")
+    ap.add_argument("--seed", type=int, default=0, help="trial seed")
+    ap.add_argument("--lr", type=float, default=1e-3, help="RMSprop learning rate (const.yaml: 1e-4)")
     ap.add_argument("--no-dropout", action="store_true", help="dropout 0 (deterministic eager/graph comparison)")
     ap.add_argument("--batch-losses", action="store_true", help="also print every batch's loss")
     args = ap.parse_args()
@@ -35,7 +37,7 @@ def main() -> None:
     import model_def
 
     t_import = time.time() - t0
-    cfg = {"hyperparameters": {"global_batch_size": args.batch, "learning_rate": 1e-3, "learning_rate_decay": 1e-6,
+    cfg = {"hyperparameters": {"global_batch_size": args.batch, "learning_rate": args.lr, "learning_rate_decay": 1e-6,
                                "layer1_dropout": 0.0 if args.no_dropout else 0.25,
                                "layer2_dropout": 0.0 if args.no_dropout else 0.25,
                                "layer3_dropout": 0.0 if args.no_dropout else 0.5,
@@ -66,7 +68,8 @@ def main() -> None:
         yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
 
     t1 = time.time()
-    ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=torch.cuda.is_available())
+    ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=torch.cuda.is_available(),
+                           trial_seed=args.seed)
     t_build = time.time() - t1
     t2 = time.time()
     ctrl.run()
@@ -78,7 +81,8 @@ def main() -> None:
     steady_batches = args.batches - (args.chunk if len(trains) > 1 else 0)
     ms_batch = 1000.0 * sum(steady) / max(1, steady_batches)
     print(json.dumps({"metric": "CIFAR-10 CNN PyTorchTrial train ms/batch", "value": round(ms_batch, 4),
-                      "unit": "ms/batch", "batch": args.batch, "amp": args.amp,
+                      "unit": "ms/batch", "batch": args.batch, "amp": args.amp, "lr": args.lr,
+                      "seed": args.seed,
                       "records_per_s": round(args.batch * 1000.0 / ms_batch, 1),
                       "first_chunk_s": round(trains[0], 3), "validation_10k_s": round(per["val"], 3),
                       "import_s": round(t_import, 2), "controller_build_s": round(t_build, 2),
