@@ -38,7 +38,8 @@ class CIFARTrial(pytorch.PyTorchTrial):
         self.loss = nn.CrossEntropyLoss()
 
     def build_training_data_loader(self) -> pytorch.DataLoader:
-        return pytorch.DataLoader(SyntheticImageClasses(50000, 32), batch_size=self.context.get_per_slot_batch_size(),
+        n = int(self.context.get_hparams().get("train_records", 50000))  # CIFAR-10 train split size
+        return pytorch.DataLoader(SyntheticImageClasses(n, 32), batch_size=self.context.get_per_slot_batch_size(),
                                   collate_fn=passthrough_collate)
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:

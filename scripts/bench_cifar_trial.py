@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--graph-batches", type=int, default=1, help="optimizations.hip_graph_batches")
     ap.add_argument("--seed", type=int, default=0, help="trial seed")
     ap.add_argument("--lr", type=float, default=1e-3, help="RMSprop learning rate (const.yaml: 1e-4)")
+    ap.add_argument("--train-records", type=int, default=50000, help="records per epoch")
     ap.add_argument("--no-dropout", action="store_true", help="dropout 0 (deterministic eager/graph comparison)")
     ap.add_argument("--batch-losses", action="store_true", help="also print every batch's loss")
     args = ap.parse_args()
@@ -37,13 +38,13 @@ def main() -> None:
     import model_def
 
     t_import = time.time() - t0
-    cfg = {"hyperparameters": {"global_batch_size": args.batch, "learning_rate": args.lr, "learning_rate_decay": 1e-6,
+    cfg = {"hyperparameters": {"global_batch_size": args.batch, "learning_rate": args.lr, "train_records": args.train_records, "learning_rate_decay": 1e-6,
                                "layer1_dropout": 0.0 if args.no_dropout else 0.25,
                                "layer2_dropout": 0.0 if args.no_dropout else 0.25,
                                "layer3_dropout": 0.0 if args.no_dropout else 0.5,
                                "amp": args.amp},
            "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": args.batches}},
-           "records_per_epoch": 50000, "scheduling_unit": args.chunk,
+           "records_per_epoch": args.train_records, "scheduling_unit": args.chunk,
            "optimizations": {"hip_graph": bool(args.hip_graph), "hip_graph_batches": args.graph_batches}}
     marks = []
     res = {}
