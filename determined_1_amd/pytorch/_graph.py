@@ -36,6 +36,7 @@ host cost -- one input copy per leaf, one replay, one clone per metric -- is pai
 batches.  Chunks never cross an epoch (the epoch index is part of the key).
 """
 import contextlib
+import os
 import logging
 from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
@@ -144,6 +145,16 @@ class TrainStepGraph:
             return "dynamic loss scaling syncs on overflow"
         if context._timers.enabled:
             return "DET_STEP_TIMERS synchronises the step"
+        if os.environ.get("DET_GRAPH_HALF_DROPOUT", "0") != "1":
+            for m in getattr(context, "models", []):
+                half = any(p.dtype in (torch.bfloat16, torch.float16) for p in m.parameters())
+                drop = any(isinstance(x, torch.nn.modules.dropout._DropoutNd) and x.p > 0 for x in m.modules())
+                if half and drop:
+                    # measured: the CIFAR trial at O2 went NaN late in every replayed run (per-batch
+                    # and chunked graphs, 3 seeds, 2 learning rates) and in no eager run; the same
+                    # trial without dropout, or at O0 with it, replays cleanly (README, round 4)
+                    return ("torch dropout in a half-precision model (replays of it diverged in measured runs; "
+                            "DET_GRAPH_HALF_DROPOUT=1 overrides)")
         if not context._opt_states:
             return "no wrapped optimizer"
         for st in context._opt_states:

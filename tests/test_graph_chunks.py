@@ -133,3 +133,24 @@ def test_multibatch_graph_replay_matches_eager(gpu, monkeypatch):
     torch.testing.assert_close(torch.tensor(l_g), torch.tensor(l_e), rtol=2e-3, atol=2e-3)
     torch.testing.assert_close(p_g, p_e, rtol=2e-3, atol=2e-3)
     assert v_g == pytest.approx(v_e, rel=2e-3)
+
+
+def test_half_precision_dropout_model_stays_eager(monkeypatch):
+    """A bf16 model with torch dropout layers is not replayed (README: replays of the CIFAR trial at
+    O2 diverged); fp32 with dropout, or bf16 without, stays eligible; the env override lifts it."""
+    from types import SimpleNamespace
+
+    from determined_1_amd.pytorch._graph import TrainStepGraph
+
+    def ctx(model):
+        return SimpleNamespace(device=torch.device("cuda"), dist_config=SimpleNamespace(use=False, aggregation_frequency=1),
+                               _amp=None, _timers=SimpleNamespace(enabled=False), _opt_states=[], models=[model])
+
+    drop = nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.5))
+    assert "dropout" in TrainStepGraph.ineligible_reason(ctx(drop.to(torch.bfloat16)))
+    assert TrainStepGraph.ineligible_reason(ctx(nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.5)))) == "no wrapped optimizer"
+    assert TrainStepGraph.ineligible_reason(ctx(nn.Sequential(nn.Linear(4, 4)).to(torch.bfloat16))) == "no wrapped optimizer"
+    assert TrainStepGraph.ineligible_reason(ctx(nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.0)).to(torch.bfloat16))) \
+        == "no wrapped optimizer"
+    monkeypatch.setenv("DET_GRAPH_HALF_DROPOUT", "1")
+    assert TrainStepGraph.ineligible_reason(ctx(drop)) == "no wrapped optimizer"
