@@ -13,6 +13,9 @@ from determined_1_amd.experimental.client import (
     Checkpoint,
     Determined,
     ExperimentReference,
+    Model,
+    ModelOrderBy,
+    ModelSortBy,
     TrialReference,
     load_checkpoint,
 )
@@ -24,6 +27,9 @@ __all__ = [
     "ExperimentReference",
     "TrialReference",
     "load_checkpoint",
+    "Model",
+    "ModelOrderBy",
+    "ModelSortBy",
     "load_model_def",
     "make_controller",
     "make_local_env",

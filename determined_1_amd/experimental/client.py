@@ -8,87 +8,261 @@
 (``{determined_version, framework, format, experiment_id, trial_id, hparams, experiment_config,
 metadata}``, reference ``_checkpoint.py:170-184``).
 """
+import enum
 import json
+import os
 import pathlib
+import re
 import shutil
-import tempfile
+import urllib.parse
 from typing import Any, Dict, List, Optional
 
 from determined_1_amd import __version__, storage
 from determined_1_amd.api import MasterClient
 
 
+def _snake(k: str) -> str:
+    return re.sub(r"(?<!^)([A-Z])", r"_\1", k).lower()
+
+
+def _norm(record: Dict[str, Any]) -> Dict[str, Any]:
+    """/api/v1 records are camelCase (grpc-gateway JSON); the legacy routes are snake_case."""
+    return {_snake(k): v for k, v in (record or {}).items()}
+
+
 class Checkpoint:
-    def __init__(self, client: MasterClient, record: Dict[str, Any]) -> None:
+    """A checkpoint of a trial (reference ``experimental/checkpoint/_checkpoint.py:15-251``)."""
+
+    def __init__(self, client: Optional[MasterClient], record: Dict[str, Any]) -> None:
+        record = _norm(record)
         self._client = client
         self.record = record
         self.uuid = record["uuid"]
         self.trial_id = record.get("trial_id")
         self.experiment_id = record.get("experiment_id")
         self.step_id = record.get("step_id")
+        self.batch_number = record.get("batch_number") or record.get("total_batches")
         self.resources = record.get("resources") or {}
         self.framework = record.get("framework")
         self.format = record.get("format")
         self.validation_metrics = record.get("validation_metrics")
         self.experiment_config = record.get("experiment_config")
         self.hparams = record.get("hparams")
+        self.metadata = dict(record.get("metadata") or {})  # type: Dict[str, Any]
+        self.model_version = record.get("model_version")
+        self.model_name = record.get("model_name")
+
+    @staticmethod
+    def from_json(data: Dict[str, Any], master: Optional[str] = None) -> "Checkpoint":
+        return Checkpoint(MasterClient(master) if master else None, data)
 
     def _full(self) -> None:
-        if self.experiment_config is None:
-            full = self._client.get(f"/checkpoints/{self.uuid}")
+        if self.experiment_config is None and self._client is not None:
+            full = _norm(self._client.get(f"/checkpoints/{self.uuid}"))
             self.experiment_config = full.get("experiment_config")
             self.hparams = full.get("hparams")
             self.validation_metrics = full.get("validation_metrics")
+            if not self.metadata:
+                self.metadata = dict(full.get("metadata") or {})
+
+    def _meta(self) -> Dict[str, Any]:
+        return {
+            "determined_version": __version__,
+            "framework": self.framework,
+            "format": self.format,
+            "experiment_id": self.experiment_id,
+            "trial_id": self.trial_id,
+            "hparams": self.hparams,
+            "experiment_config": self.experiment_config,
+            "metadata": self.metadata,
+        }
+
+    def _shared_fs_path(self) -> Optional[pathlib.Path]:
+        """The checkpoint's own directory when storage is a shared_fs mounted here too (reference
+        ``_find_shared_fs_path``): loading reads it in place instead of copying it."""
+        cs = (self.experiment_config or {}).get("checkpoint_storage") or {}
+        if cs.get("type") != "shared_fs":
+            return None
+        from determined_1_amd.storage import shared_fs_root
+
+        for root in shared_fs_root(cs):
+            p = pathlib.Path(root, self.uuid)
+            if p.is_dir():
+                return p
+        return None
 
     def download(self, path: Optional[str] = None) -> str:
         self._full()
-        dst = pathlib.Path(path or tempfile.mkdtemp(prefix="det-ckpt-")).joinpath(self.uuid) \
-            if path is None else pathlib.Path(path)
+        dst = pathlib.Path(path) if path is not None else pathlib.Path("checkpoints", self.uuid)
         if not dst.joinpath("metadata.json").exists():
-            mgr = storage.build((self.experiment_config or {}).get("checkpoint_storage", {}))
-            with mgr.restore_path(storage.StorageMetadata(self.uuid, self.resources)) as src:
-                shutil.copytree(str(src), str(dst), dirs_exist_ok=True)
-            meta = {
-                "determined_version": __version__,
-                "framework": self.framework,
-                "format": self.format,
-                "experiment_id": self.experiment_id,
-                "trial_id": self.trial_id,
-                "hparams": self.hparams,
-                "experiment_config": self.experiment_config,
-                "metadata": self.record.get("metadata") or {},
-            }
-            dst.joinpath("metadata.json").write_text(json.dumps(meta, indent=2))
+            src_dir = self._shared_fs_path()
+            if src_dir is not None:
+                shutil.copytree(str(src_dir), str(dst), dirs_exist_ok=True)
+            else:
+                mgr = storage.build((self.experiment_config or {}).get("checkpoint_storage", {}))
+                with mgr.restore_path(storage.StorageMetadata(self.uuid, self.resources)) as src:
+                    shutil.copytree(str(src), str(dst), dirs_exist_ok=True)
+            dst.joinpath("metadata.json").write_text(json.dumps(self._meta(), indent=2))
         return str(dst)
 
-    def load(self, path: Optional[str] = None, map_location: Any = None) -> Any:
-        return load_checkpoint(self.download(path), map_location=map_location)
+    def load(self, path: Optional[str] = None, map_location: Any = None, **kwargs: Any) -> Any:
+        """The trial's model with this checkpoint's weights.  On a shared_fs checkpoint visible from
+        this host (and no ``path``), it is read in place: no copy."""
+        self._full()
+        if path is None:
+            src = self._shared_fs_path()
+            if src is not None:
+                return load_checkpoint(str(src), map_location=map_location, meta=self._meta(), **kwargs)
+        return Checkpoint.load_from_path(self.download(path), map_location=map_location, **kwargs)
+
+    @staticmethod
+    def load_from_path(path: str, map_location: Any = None, **kwargs: Any) -> Any:
+        """Load a checkpoint directory (as written by ``download``) without a master."""
+        return load_checkpoint(path, map_location=map_location, **kwargs)
+
+    def _post_metadata(self) -> None:
+        if self._client is not None:
+            self._client.post(f"/api/v1/checkpoints/{self.uuid}/metadata", {"checkpoint": {"metadata": self.metadata}})
+
+    def add_metadata(self, metadata: Dict[str, Any]) -> None:
+        """Merge ``metadata`` (JSON-serialisable) into the checkpoint's user metadata."""
+        self.metadata.update(metadata)
+        self._post_metadata()
+
+    def remove_metadata(self, keys: List[str]) -> None:
+        for k in keys:
+            self.metadata.pop(k, None)
+        self._post_metadata()
 
     def __repr__(self) -> str:
         return f"Checkpoint(uuid={self.uuid}, trial_id={self.trial_id}, step_id={self.step_id})"
 
 
-def load_checkpoint(ckpt_dir: str, map_location: Any = None) -> Any:
+def load_checkpoint(ckpt_dir: str, map_location: Any = None, meta: Optional[Dict[str, Any]] = None,
+                    **kwargs: Any) -> Any:
     """Re-instantiate the trial from ``<ckpt>/code`` and load ``models_state_dict`` into it
-    (reference ``experimental/checkpoint/_torch.py:10``).  Returns the first wrapped model."""
+    (reference ``experimental/checkpoint/_torch.py:10``).  Returns the first wrapped model.  A
+    Native-API experiment (no entrypoint) is re-loaded by re-running its command under the loader."""
     import torch
 
     from determined_1_amd.experimental._local import make_controller
-    from determined_1_amd.harness.load import load_trial_class
+    from determined_1_amd.harness.load import load_native_implementation, load_trial_class, native_command
 
     ckpt = pathlib.Path(ckpt_dir)
-    meta = json.loads(ckpt.joinpath("metadata.json").read_text())
-    trial_class = load_trial_class(meta["experiment_config"]["entrypoint"], str(ckpt.joinpath("code")))
-    ctrl = make_controller(trial_class, meta["experiment_config"], iter([]), hparams=meta["hparams"],
+    if meta is None:
+        meta = json.loads(ckpt.joinpath("metadata.json").read_text())
+    cfg = meta["experiment_config"]
+    code = ckpt.joinpath("code")
+    cmd = native_command(cfg)
+    if cmd is not None:
+        cwd = os.getcwd()
+        os.chdir(str(code))
+        try:
+            trial_class = load_native_implementation(command=cmd)
+        finally:
+            os.chdir(cwd)
+    else:
+        trial_class = load_trial_class(cfg["entrypoint"], str(code))
+    ctrl = make_controller(trial_class, cfg, iter([]), hparams=meta["hparams"],
                            use_gpu=map_location not in ("cpu", torch.device("cpu")) and torch.cuda.is_available())
-    from determined_1_amd.pytorch._trial import CHECKPOINT_FILE, _pickle_module
+    from determined_1_amd.pytorch._trial import CHECKPOINT_FILE
 
-    state = torch.load(str(ckpt.joinpath(CHECKPOINT_FILE)), map_location=map_location, weights_only=False,
-                       pickle_module=_pickle_module)
+    # written by this framework's own controller (cloudpickle output is plain-pickle loadable)
+    state = torch.load(str(ckpt.joinpath(CHECKPOINT_FILE)), map_location=map_location, weights_only=False, **kwargs)
     models = ctrl.context.models
     for m, sd in zip(models, state["models_state_dict"]):
         m.load_state_dict(sd)
     return models[0] if len(models) == 1 else models
+
+
+class ModelSortBy(enum.Enum):
+    """Field a model listing is sorted on (reference ``model.py:10-25``)."""
+    UNSPECIFIED = 0
+    NAME = 1
+    DESCRIPTION = 2
+    CREATION_TIME = 4
+    LAST_UPDATED_TIME = 5
+
+
+class ModelOrderBy(enum.Enum):
+    ASCENDING = 1
+    ASC = 1
+    DESCENDING = 2
+    DESC = 2
+
+
+class Model:
+    """A model in the registry and its versions (reference ``experimental/model.py:47-218``)."""
+
+    def __init__(self, name: str, description: str = "", creation_time: Optional[str] = None,
+                 last_updated_time: Optional[str] = None, metadata: Optional[Dict[str, Any]] = None,
+                 client: Optional[MasterClient] = None) -> None:
+        self._client = client or MasterClient()
+        self.name = name
+        self.description = description or ""
+        self.creation_time = creation_time
+        self.last_updated_time = last_updated_time
+        self.metadata = dict(metadata or {})
+
+    @staticmethod
+    def from_json(data: Dict[str, Any], client: Optional[MasterClient] = None) -> "Model":
+        d = _norm(data)
+        return Model(d["name"], d.get("description", ""), d.get("creation_time"), d.get("last_updated_time"),
+                     d.get("metadata") or {}, client)
+
+    def _path(self) -> str:
+        return "/api/v1/models/" + urllib.parse.quote(self.name, safe="")
+
+    def _version_ckpt(self, v: Dict[str, Any]) -> Checkpoint:
+        v = _norm(v)
+        ck = v.get("checkpoint")
+        if not ck:
+            uuid = v.get("checkpoint_uuid")
+            ck = self._client.get(f"/api/v1/checkpoints/{uuid}")["checkpoint"]
+        rec = dict(_norm(ck))
+        rec["model_version"] = v.get("version")
+        rec["model_name"] = self.name
+        return Checkpoint(self._client, rec)
+
+    def get_versions(self, order_by: ModelOrderBy = ModelOrderBy.DESC) -> List[Checkpoint]:
+        """Checkpoints of every version, by version number (descending by default)."""
+        data = self._client.get(self._path() + "/versions")
+        vs = sorted(data.get("modelVersions") or [], key=lambda v: int(v.get("version", 0)),
+                    reverse=order_by == ModelOrderBy.DESC)
+        return [self._version_ckpt(v) for v in vs]
+
+    def get_version(self, version: int = 0) -> Optional[Checkpoint]:
+        """The checkpoint of ``version``; 0 means the latest (None if there is no version yet).
+        A missing explicit version raises."""
+        if version == 0:
+            vs = self.get_versions(ModelOrderBy.DESC)
+            return vs[0] if vs else None
+        return self._version_ckpt(self._client.get(f"{self._path()}/versions/{int(version)}")["modelVersion"])
+
+    def register_version(self, checkpoint_uuid: str) -> Checkpoint:
+        """Register a checkpoint as the next version of this model."""
+        v = self._client.post(self._path() + "/versions", {"checkpoint_uuid": checkpoint_uuid})["modelVersion"]
+        return self._version_ckpt(v)
+
+    def _patch(self) -> None:
+        m = self._client.patch(self._path(), {"model": {"metadata": self.metadata, "description": self.description}})
+        self.last_updated_time = _norm(m.get("model") or {}).get("last_updated_time", self.last_updated_time)
+
+    def add_metadata(self, metadata: Dict[str, Any]) -> None:
+        self.metadata.update(metadata)
+        self._patch()
+
+    def remove_metadata(self, keys: List[str]) -> None:
+        for k in keys:
+            self.metadata.pop(k, None)
+        self._patch()
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"name": self.name, "description": self.description, "creation_time": self.creation_time,
+                "last_updated_time": self.last_updated_time, "metadata": self.metadata}
+
+    def __repr__(self) -> str:
+        return f"Model(name={self.name}, metadata={json.dumps(self.metadata)})"
 
 
 class TrialReference:
@@ -183,13 +357,33 @@ class Determined:
         return TrialReference(self._client, trial_id)
 
     def get_checkpoint(self, uuid: str) -> Checkpoint:
-        return Checkpoint(self._client, self._client.get(f"/checkpoints/{uuid}"))
+        return Checkpoint(self._client, self._client.get(f"/api/v1/checkpoints/{uuid}")["checkpoint"])
 
-    def get_models(self) -> List[Dict[str, Any]]:
-        return self._client.get("/models")
+    def create_model(self, name: str, description: Optional[str] = "",
+                     metadata: Optional[Dict[str, Any]] = None) -> Model:
+        """Add a model (unique ``name``) to the registry."""
+        r = self._client.post("/api/v1/models/" + urllib.parse.quote(name, safe=""),
+                              {"description": description or "", "metadata": metadata or {}})
+        m = Model.from_json(r["model"], self._client)
+        if metadata and not m.metadata:  # a registry that took only the description
+            m.add_metadata(metadata)
+        return m
 
-    def create_model(self, name: str, description: str = "") -> Dict[str, Any]:
-        return self._client.post(f"/models/{name}", {"description": description})
+    def get_model(self, name: str) -> Model:
+        return Model.from_json(self._client.get("/api/v1/models/" + urllib.parse.quote(name, safe=""))["model"],
+                               self._client)
 
-    def register_model_version(self, name: str, checkpoint_uuid: str) -> Dict[str, Any]:
-        return self._client.post(f"/models/{name}/versions", {"checkpoint_uuid": checkpoint_uuid})
+    def get_models(self, sort_by: ModelSortBy = ModelSortBy.NAME, order_by: ModelOrderBy = ModelOrderBy.ASCENDING,
+                   name: str = "", description: str = "") -> List[Model]:
+        """Registry models, filtered by substring of ``name`` / ``description`` and sorted."""
+        params = {k: v for k, v in (("name", name), ("description", description)) if v}
+        models = [Model.from_json(m, self._client) for m in self._client.get("/api/v1/models", **params)["models"]]
+        key = {ModelSortBy.NAME: lambda m: m.name, ModelSortBy.DESCRIPTION: lambda m: m.description,
+               ModelSortBy.CREATION_TIME: lambda m: m.creation_time or "",
+               ModelSortBy.LAST_UPDATED_TIME: lambda m: m.last_updated_time or ""}.get(sort_by)
+        if key is not None:
+            models.sort(key=key, reverse=order_by == ModelOrderBy.DESCENDING)
+        return models
+
+    def register_model_version(self, name: str, checkpoint_uuid: str) -> Checkpoint:
+        return self.get_model(name).register_version(checkpoint_uuid)

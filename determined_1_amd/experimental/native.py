@@ -4,33 +4,49 @@
     det.experimental.create(MyTrial, config, local=True)              # full single-trial run, in-process
     det.experimental.create(MyTrial, config, context_dir=".", master_url="host:8080")  # cluster
 
-The trial class is resolved to ``module:QualName`` relative to ``context_dir`` for cluster
-submission, exactly like an ``entrypoint`` in a config file.
+Cluster mode works like the reference's (``experimental/_native.py:21-68,114-165``): the submitting
+script records itself as ``internal.native.command = [script relative to context_dir, *argv]`` (a
+notebook passes ``command=["nb.ipynb"]``), and every trial process re-runs that command under the
+harness loader (``harness/load.py`` ``RunpyGlobals``).  There ``create()`` hands ``trial_def`` back and
+raises ``StopLoadingImplementation`` instead of submitting again, so a script with a top-level
+``create()`` call and no ``__main__`` guard yields exactly one experiment.
 """
-import inspect
 import logging
 import os
 import pathlib
+import sys
 import tempfile
 import uuid
-from typing import Any, Dict, Iterator, Optional, Type
+from typing import Any, Dict, Iterator, List, Optional, Type
 
-from determined_1_amd import trial, workload
+from determined_1_amd import errors, trial, workload
 from determined_1_amd.config import merge_with_defaults
 from determined_1_amd.config.length import BATCHES, Length, UnitContext
 from determined_1_amd.experimental._local import make_controller, test_one_batch
 
 
-def _entrypoint_for(trial_def: Type[trial.Trial], context_dir: str) -> str:
-    mod = inspect.getmodule(trial_def)
-    assert mod is not None and getattr(mod, "__file__", None), "trial class must live in a module file"
-    rel = os.path.relpath(os.path.abspath(mod.__file__), os.path.abspath(context_dir))
-    if rel.startswith(".."):
-        raise ValueError(f"{mod.__file__} is not inside context_dir {context_dir}")
-    modname = rel[:-3].replace(os.sep, ".") if rel.endswith(".py") else rel.replace(os.sep, ".")
-    if modname.endswith(".__init__"):
-        modname = modname[: -len(".__init__")]
-    return f"{modname}:{trial_def.__qualname__}"
+def _set_command_default(context_dir: str, command: Optional[List[str]]) -> List[str]:
+    """``[script relative to context_dir, *sys.argv[1:]]`` unless the caller gave a command."""
+    if command:
+        cmd = [str(c) for c in command]
+        if not cmd[0].endswith((".py", ".ipynb")):
+            raise errors.InvalidExperimentException(f"command must start with a .py or .ipynb file, got {cmd}")
+        return cmd
+    import __main__
+
+    main_file = getattr(__main__, "__file__", None)
+    if not main_file:  # a notebook / REPL: there is no script to re-run
+        raise errors.InvalidExperimentException(
+            "Must specify the location of the notebook file relative to the context directory "
+            "(command=[\"notebook.ipynb\"]) when not running a script.")
+    try:
+        rel = pathlib.Path(main_file).resolve().relative_to(pathlib.Path(context_dir).resolve())
+    except ValueError:
+        raise errors.InvalidExperimentException(
+            f"the submitting script {main_file} is not inside context_dir {context_dir}") from None
+    if rel.suffix not in (".py", ".ipynb"):
+        raise errors.InvalidExperimentException(f"command must start with a .py or .ipynb file, got {rel}")
+    return [str(rel), *sys.argv[1:]]
 
 
 def local_training_workloads(cfg: Dict[str, Any], ckpt_root: pathlib.Path) -> Iterator:
@@ -60,8 +76,18 @@ def local_training_workloads(cfg: Dict[str, Any], ckpt_root: pathlib.Path) -> It
 
 
 def create(trial_def: Type[trial.Trial], config: Optional[Dict[str, Any]] = None, local: bool = False,
-           test: bool = False, context_dir: str = "", master_url: Optional[str] = None,
-           checkpoint_dir: Optional[str] = None) -> Any:
+           test: bool = False, context_dir: str = "", command: Optional[List[str]] = None,
+           master_url: Optional[str] = None, checkpoint_dir: Optional[str] = None, follow: bool = False) -> Any:
+    """Create an experiment from ``trial_def`` (reference ``experimental/_native.py:254-340``).
+
+    Inside a trial process (the harness re-running this script) it returns nothing: it hands the
+    class to the loader and stops the script.  ``follow`` waits for the cluster experiment to end,
+    printing trial logs, like the reference's ``create_experiment_and_follow_logs``.
+    """
+    from determined_1_amd.harness.load import RunpyGlobals
+
+    if RunpyGlobals.is_initialized():
+        RunpyGlobals.set_runpy_trial_result(trial_def)  # raises StopLoadingImplementation
     config = dict(config or {})
     if local and test:
         return test_one_batch(trial_def, config)
@@ -74,12 +100,21 @@ def create(trial_def: Type[trial.Trial], config: Optional[Dict[str, Any]] = None
     from determined_1_amd.experimental.client import Determined
 
     if not context_dir:
-        raise ValueError("cluster mode needs context_dir (the directory shipped as the model definition)")
-    config.setdefault("entrypoint", _entrypoint_for(trial_def, context_dir))
+        raise errors.InvalidExperimentException("Cannot specify the context directory to be empty.")
+    internal = dict(config.get("internal") or {})
+    internal["native"] = {"command": _set_command_default(context_dir, command)}
+    config["internal"] = internal
     if test:
         from determined_1_amd.cli.cli import make_test_config
 
         config = make_test_config(config)
-    exp = Determined(master_url).create_experiment(config, context_dir)
-    logging.info("created experiment %d", exp.id)
+    d = Determined(master_url)
+    exp = d.create_experiment(config, context_dir)
+    logging.info("created experiment %d (native command %s)", exp.id, internal["native"]["command"])
+    if follow or test:
+        from determined_1_amd.cli.cli import _follow
+
+        state = _follow(d._client, exp.id)
+        if test and state != "COMPLETED":
+            raise errors.InvalidExperimentException(f"test experiment {exp.id} ended in state {state}")
     return exp

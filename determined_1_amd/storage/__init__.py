@@ -32,7 +32,18 @@ def build(config: dict, container_path: str = None) -> StorageManager:
     return _TYPES[t].from_config(cfg)
 
 
+def shared_fs_root(config: dict) -> list:
+    """Candidate local directories of a shared_fs store (host view first, then the container
+    mount), for readers that use checkpoints in place (reference ``_find_shared_fs_path``)."""
+    from determined_1_amd import constants
+    from determined_1_amd.storage.shared import full_storage_path
+
+    host, sp = config.get("host_path", "/tmp"), config.get("storage_path")
+    return [full_storage_path(host, sp, None), full_storage_path(host, sp, constants.SHARED_FS_CONTAINER_PATH)]
+
+
 __all__ = [
+    "shared_fs_root",
     "GCSStorageManager",
     "HDFSStorageManager",
     "S3StorageManager",
