@@ -189,6 +189,9 @@ struct SimulationResult {
   std::map<RequestID, std::vector<Op>> results;  // runnable ops per trial
   std::vector<RequestID> order;                  // creation order
   Json Summary() const;                          // {"64000R V 128000R V": count, ...}
+  // reference experimentv1.ExperimentSimulation.trials: [{operations: [{type, length: {unit,
+  // count}}], occurrences}] in first-seen order (api_experiment.go:182-260)
+  Json TrialSimulations() const;
 };
 using ValidationFn = std::function<double(int trial_id, int op_index)>;
 // random_order: pick trials uniformly among those with pending ops (seeded by sim_seed);

@@ -762,6 +762,7 @@ void Master::InstallApiV1() {
     Json body = Json::parse(r.body.empty() ? "{}" : r.body);
     Json legacy = Json::object();
     legacy["config"] = body["config"];
+    if (body.has("seed")) legacy["seed"] = body["seed"];
     auto res = call(r, "POST", "/searcher/preview", legacy.dump());
     Json j;
     if (!unwrap(res, &j)) return relay_err(res);
@@ -773,7 +774,9 @@ void Master::InstallApiV1() {
       one["count"] = kv.second;
       results.push_back(one);
     }
-    sim["results"] = results;
+    sim["results"] = results;  // det-master extension: {units, count} per distinct sequence
+    sim["trials"] = j["trials"];
+    sim["config"] = j["config"];
     sim["seed"] = j["seed"];
     Json out = Json::object();
     out["simulation"] = sim;

@@ -1156,13 +1156,18 @@ void Master::InstallRoutes() {
     Json body = Json::parse(r.body);
     Json user = body["config"].is_string() ? Json::parse(body["config"].as_string()) : body["config"];
     Json cfg = MergeExperimentConfig(user, cfg_.checkpoint_storage, Json(), 0);
-    uint32_t seed = static_cast<uint32_t>(cfg["reproducibility"].get_int("experiment_seed", 0));
+    uint32_t seed = static_cast<uint32_t>(body.has("seed") && body["seed"].is_number()
+                                              ? body["seed"].as_int()
+                                              : cfg["reproducibility"].get_int("experiment_seed", 0));
     Searcher s(seed, NewSearchMethod(cfg["searcher"]), cfg["hyperparameters"]);
     std::mt19937_64 rng(seed);
     std::uniform_real_distribution<double> U(0.0, 1.0);
     auto res = Simulate(s, [&](int, int) { return U(rng); }, true, seed, cfg["searcher"].get_string("metric", "metric"));
     Json out = Json::object();
     out["results"] = res.Summary();
+    out["trials"] = res.TrialSimulations();
+    out["seed"] = static_cast<int64_t>(seed);
+    out["config"] = cfg;
     out["num_trials"] = static_cast<int64_t>(res.order.size());
     return J(200, out);
   });

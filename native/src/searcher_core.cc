@@ -595,6 +595,50 @@ Json SimulationResult::Summary() const {
   return j;
 }
 
+Json SimulationResult::TrialSimulations() const {
+  Json trials = Json::array();
+  std::map<std::string, size_t> index;
+  for (const auto& id : order) {
+    auto it = results.find(id);
+    if (it == results.end()) continue;
+    std::string key;
+    Json ops = Json::array();
+    for (const auto& op : it->second) {
+      Json o = Json::object();
+      if (op.kind == Op::Kind::Train) {
+        key += op.length.ShortString() + " ";
+        o["type"] = "RUNNABLE_TYPE_TRAIN";
+        Json len = Json::object();
+        len["unit"] = op.length.unit == Unit::Records ? "UNIT_RECORDS"
+                      : op.length.unit == Unit::Epochs ? "UNIT_EPOCHS" : "UNIT_BATCHES";
+        len["count"] = op.length.units;
+        o["length"] = len;
+      } else if (op.kind == Op::Kind::Validate) {
+        key += "V ";
+        o["type"] = "RUNNABLE_TYPE_VALIDATE";
+      } else if (op.kind == Op::Kind::Checkpoint) {
+        key += "C ";
+        o["type"] = "RUNNABLE_TYPE_CHECKPOINT";
+      } else {
+        continue;
+      }
+      ops.push_back(o);
+    }
+    auto f = index.find(key);
+    if (f != index.end()) {
+      Json& t = trials.as_array()[f->second];
+      t["occurrences"] = t["occurrences"].as_int() + 1;
+      continue;
+    }
+    index[key] = trials.size();
+    Json t = Json::object();
+    t["operations"] = ops;
+    t["occurrences"] = static_cast<int64_t>(1);
+    trials.push_back(t);
+  }
+  return trials;
+}
+
 SimulationResult Simulate(Searcher& s, const ValidationFn& valfn, bool random_order, uint64_t sim_seed,
                           const std::string& metric_name) {
   SimulationResult sim;
