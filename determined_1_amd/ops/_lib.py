@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -103,6 +103,8 @@ _SIGNATURES = {
     ),
     # stream, dtype, x, M, C, gamma, beta, running_mean, running_var, nbt, momentum, eps,
     # save_mean, save_rstd, scale, shift, ws
+    # stream, kind, src, dst, nbytes, blocks, unroll, value, sink  (det_stream.hip yardsticks)
+    "det_stream": ([c_void_p, c_int, c_void_p, c_void_p, c_i64, c_int, c_int, ctypes.c_uint32, c_void_p], c_int),
     "det_bn_stats_train": (
         [c_void_p, c_int, c_void_p, c_i64, c_int] + [c_void_p] * 5 + [c_float, c_float] + [c_void_p] * 5,
         c_int,

@@ -107,9 +107,13 @@ struct Args {
   const uint32_t* rng_base;
 };
 
-__device__ __forceinline__ uint32_t run_key(const Args& a) {
-  return a.rng_key ^ (a.rng_base != nullptr ? *a.rng_base * 0x2545F491u : 0u);
+// The replay counter enters the key through the mixer, not by XOR: a linear fold (key ^ base * C
+// with key itself linear in the offset) lets whole families of (offset, counter) pairs land on one
+// key, i.e. one mask; mixed, distinct pairs share a 32-bit key only by chance.
+__device__ __forceinline__ uint32_t fold_base(uint32_t key, const uint32_t* rng_base) {
+  return rng_base != nullptr ? mix32(*rng_base * 0x2545F491u + 0x632BE5ABu, key) : key;
 }
+__device__ __forceinline__ uint32_t run_key(const Args& a) { return fold_base(a.rng_key, a.rng_base); }
 
 __device__ __forceinline__ uint32_t rng_key_for(uint32_t base_key, int b, int head) {
   return base_key ^ (static_cast<uint32_t>(b * 977 + head) * 0x9E3779B9u);
@@ -725,7 +729,7 @@ bool bwd_merged(int64_t workgroups) {
 
 __global__ void attn_mask_kernel(int B, int nh, int Lq, int Lk, uint32_t thr, uint32_t key0, const uint32_t* rng_base,
                                  uint8_t* out) {
-  const uint32_t base_key = key0 ^ (rng_base != nullptr ? *rng_base * 0x2545F491u : 0u);  // run_key
+  const uint32_t base_key = fold_base(key0, rng_base);  // = run_key of the attention kernels
   const int64_t n = static_cast<int64_t>(B) * nh * Lq * Lk;
   const uint32_t lke = static_cast<uint32_t>(lk_even4(Lk));
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -805,9 +809,19 @@ uint32_t drop_threshold(float p) {
   uint32_t thr = p > 0.f ? static_cast<uint32_t>(p * 65536.0f + 0.5f) : 0u;
   return thr > 65535u ? 65535u : thr;
 }
-uint32_t mix_key(uint64_t seed, uint64_t offset) {
-  return static_cast<uint32_t>(seed) ^ static_cast<uint32_t>(seed >> 32) * 0x85ebca6bu ^
-         static_cast<uint32_t>(offset) * 0xc2b2ae35u ^ static_cast<uint32_t>(offset >> 32);
+uint32_t host_mix32(uint32_t x, uint32_t key) {  // = mix32, for the host
+  x ^= key;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+uint32_t mix_key(uint64_t seed, uint64_t offset) {  // all 128 bits through the mixer
+  uint32_t k = host_mix32(static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32) ^ 0x85ebca6bu);
+  k = host_mix32(static_cast<uint32_t>(offset), k);
+  return host_mix32(static_cast<uint32_t>(offset >> 32), k ^ 0xc2b2ae35u);
 }
 
 }  // namespace

@@ -306,18 +306,34 @@ class PyTorchTrialContext(trial.TrialContext):
     def _partial_window_grads(self) -> Optional[List[List[Optional[torch.Tensor]]]]:
         """The accumulated gradients of an unfinished aggregation window (checkpointed so that a
         restored trial steps on the same sum as an uninterrupted one; the reference drops them), or
-        None.  Single-process only: with several ranks each holds its own partial sum."""
+        None.  Every rank must call it (it is a collective with several ranks): each rank's partial
+        sum is still local mid-window (the bucketer communicates only on the window's last batch),
+        so the ranks' partials are summed into the chief's copy.  Restored, the chief continues the
+        window from that sum and the other ranks from zero, which all-reduces to the same total as
+        an uninterrupted run (the reduction is linear)."""
         if self._restored_grads is not None:
             return self._restored_grads  # restored and not consumed yet
         agg = self.dist_config.aggregation_frequency
         if agg <= 1 or self._current_batch_idx is None or (self._current_batch_idx + 1) % agg == 0:
             return None
+        grads = [[p.grad for p in m.parameters()] for m in self.models]
         if self.dist_config.use and pdist.is_initialized() and self.distributed.get_size() > 1:
-            logging.warning("checkpoint inside an aggregation window: the partial gradient sums of %d ranks are "
-                            "not saved", self.distributed.get_size())
-            return None
-        return [[None if p.grad is None else p.grad.detach().to("cpu", copy=True) for p in m.parameters()]
-                for m in self.models]
+            import torch.distributed as tdist
+
+            live = [g for gs in grads for g in gs if g is not None]
+            if live:
+                flat = torch.cat([g.detach().reshape(-1).float() for g in live])
+                tdist.all_reduce(flat)
+                off = 0
+                summed = []
+                for g in live:
+                    summed.append(flat[off:off + g.numel()].view_as(g).to(g.dtype))
+                    off += g.numel()
+                it = iter(summed)
+                grads = [[None if g is None else next(it) for g in gs] for gs in grads]
+            if self.distributed.get_rank() != 0:
+                return None
+        return [[None if g is None else g.detach().to("cpu", copy=True) for g in gs] for gs in grads]
 
     @torch.no_grad()
     def _apply_restored_grads(self) -> None:

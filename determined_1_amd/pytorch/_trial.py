@@ -529,7 +529,9 @@ class PyTorchTrialController(trial.LoopTrialController):
                 _tf.set_rng_state(rs["det_dropout_rng"])
         else:
             logging.warning("The checkpoint has no random state to restore.")
-        if checkpoint.get("accumulated_grads") is not None:
+        if checkpoint.get("accumulated_grads") is not None and self.is_chief:
+            # the chief holds the ranks' summed partial window (see _partial_window_grads); the other
+            # ranks continue the window from zero
             ctx._restored_grads = checkpoint["accumulated_grads"]
         cb_state = checkpoint.get("callbacks", {})
         for name, cb in self.callbacks.items():
@@ -540,6 +542,7 @@ class PyTorchTrialController(trial.LoopTrialController):
                                 "for that name when restoring from checkpoint.")
 
     def _save(self, path: pathlib.Path) -> workload.Response:
+        partial = self.context._partial_window_grads()  # a collective across ranks: before the chief check
         if not self.is_chief:
             return workload.Skipped()
         path.mkdir(parents=True, exist_ok=True)
@@ -564,7 +567,6 @@ class PyTorchTrialController(trial.LoopTrialController):
         }
         if ctx._amp is not None:
             ckpt["amp_state"] = ctx._amp_state_dict()
-        partial = ctx._partial_window_grads()
         if partial is not None:
             ckpt["accumulated_grads"] = partial
         torch.save(ckpt, str(path.joinpath(CHECKPOINT_FILE)), pickle_module=_pickle_module)

@@ -510,6 +510,9 @@ class Agent {
       env["DET_TASK_ETC"] = etc;
       if (geteuid() == 0) {
         ChownTree(dir, static_cast<uid_t>(run_uid), static_cast<gid_t>(run_gid));
+        // the task dir is its owner's alone: the +x added to the parents below only lets an
+        // account traverse to its own dir, never list or read another task's
+        ::chmod(dir.c_str(), 0700);
         // the task account must be able to reach its own work dir through the agent's
         for (const std::string& d : {o_.work_dir, dir.substr(0, dir.rfind('/'))}) {
           struct stat st {};
@@ -536,6 +539,12 @@ class Agent {
       State(cid, "Terminated", 1, "pipe failed");
       return;
     }
+    // the child's failure messages are formatted here, before fork(): after it this multithreaded
+    // process may only make async-signal-safe calls (no stdio locks, no strerror)
+    char msg_uid[160], msg_dir[512];
+    std::snprintf(msg_uid, sizeof msg_uid, "det-agent: cannot switch to uid %d gid %d\n", run_uid, run_gid);
+    std::snprintf(msg_dir, sizeof msg_dir, "det-agent: cannot enter the work dir %s\n", dir.c_str());
+    const size_t msg_uid_len = std::strlen(msg_uid), msg_dir_len = std::strlen(msg_dir);
     pid_t pid = -1;
     int zfd = spec["cmd"].is_array() && spec["cmd"].size() > 0
                   ? -1
@@ -550,12 +559,14 @@ class Agent {
       if (run_uid >= 0 && static_cast<uid_t>(run_uid) != geteuid()) {
         const gid_t g = static_cast<gid_t>(run_gid);
         if (setgroups(1, &g) != 0 || setgid(g) != 0 || setuid(static_cast<uid_t>(run_uid)) != 0) {
-          std::fprintf(stderr, "det-agent: cannot switch to uid %d gid %d: %s\n", run_uid, run_gid, std::strerror(errno));
+          ssize_t w = ::write(2, msg_uid, msg_uid_len);
+          (void)w;
           _exit(126);
         }
       }
       if (chdir(dir.c_str()) != 0) {
-        std::fprintf(stderr, "det-agent: cannot enter the work dir %s: %s\n", dir.c_str(), std::strerror(errno));
+        ssize_t w = ::write(2, msg_dir, msg_dir_len);
+        (void)w;
         _exit(127);
       }
       execvpe(argv[0], argv.data(), envp.data());

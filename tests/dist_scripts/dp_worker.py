@@ -19,8 +19,22 @@ def main() -> None:
     compress = len(sys.argv) > 4 and sys.argv[4] == "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     trial_cls = getattr(xor, trial_name)
-    rec = Recorder().train(1, 4, 0).train(2, 4, 4).validate(2, 8)
+    # MODE (env): "" the default 4+4 batches; "full" 8 batches; "ckpt" 3 batches then a checkpoint inside
+    # the aggregation window (to CKPT); "resume" the last 5 batches from CKPT
+    mode = os.environ.get("MODE", "")
+    import pathlib
+
+    load_path = None
+    if mode == "full":
+        rec = Recorder().train(1, 8, 0)
+    elif mode == "ckpt":
+        rec = Recorder().train(1, 3, 0).checkpoint(1, 3, pathlib.Path(os.environ["CKPT"]))
+    elif mode == "resume":
+        rec, load_path = Recorder().train(2, 5, 3), pathlib.Path(os.environ["CKPT"])
+    else:
+        rec = Recorder().train(1, 4, 0).train(2, 4, 4).validate(2, 8)
     ctrl, resp = run(trial_cls, {"global_batch_size": 8, "optimizer": "adam", "lr": 0.05}, rec, trial_seed=11,
+                     load_path=load_path, total_batches=3 if mode == "resume" else 0,
                      resources={"slots_per_trial": world},
                      optimizations={"aggregation_frequency": agg, "gradient_compression": compress,
                                     "average_training_metrics": True})

@@ -20,11 +20,11 @@ def _free_port() -> int:
     return p
 
 
-def _launch(out: str, world: int, agg: int, compress: bool = False) -> None:
+def _launch(out: str, world: int, agg: int, compress: bool = False, **extra_env: str) -> None:
     port = _free_port()
     procs = []
     for r in range(world):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+        env = dict(os.environ, **extra_env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         procs.append(subprocess.Popen([sys.executable, WORKER, out, "XORTrial", str(agg), "1" if compress else "0"],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -36,6 +36,20 @@ def _launch(out: str, world: int, agg: int, compress: bool = False) -> None:
                 q.kill()
             raise
         assert p.returncode == 0, o.decode()[-4000:]
+
+
+def test_dp2_checkpoint_inside_aggregation_window_resumes_exactly(tmp_path):
+    """a checkpoint taken mid-window keeps the ranks' partial sums (summed into the
+    chief's copy), so a restored 2-rank run steps on the same gradient sums as an uninterrupted one."""
+    ckpt = str(tmp_path / "ckpt")
+    _launch(str(tmp_path / "full"), 2, 2, MODE="full")
+    _launch(str(tmp_path / "first"), 2, 2, MODE="ckpt", CKPT=ckpt)
+    saved = torch.load(os.path.join(ckpt, "state_dict.pth"), weights_only=False)
+    assert saved.get("accumulated_grads") is not None  # batch 3 of a 2-batch window
+    _launch(str(tmp_path / "resumed"), 2, 2, MODE="resume", CKPT=ckpt)
+    full, res0, res1 = (torch.load(str(tmp_path / f)) for f in ("full.0.pt", "resumed.0.pt", "resumed.1.pt"))
+    torch.testing.assert_close(res0, res1, rtol=0, atol=0)
+    torch.testing.assert_close(res0, full, rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("agg", [1, 2])
