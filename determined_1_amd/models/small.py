@@ -7,6 +7,8 @@
 * ``MNISTNet``: the CNN of ``examples/tutorials/mnist_pytorch/model_def.py``.
 * ``CIFAR10CNN``: the CNN of ``examples/computer_vision/cifar10_pytorch/model_def.py:42-122``.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -51,13 +53,18 @@ class MNISTNet(nn.Module):
 
 
 class CIFAR10CNN(nn.Module):
+    """The reference's CIFAR-10 network (``cifar10_pytorch/model_def.py:47-65``).  On an MI355X the
+    whole forward and backward run on ``ops/cnn.py`` (csrc/det_cnn.hip: ~20 launches per training
+    batch); ``DET_NATIVE_CNN=0`` keeps the torch layers.  The logits come back fp32 on that path."""
+
     def __init__(self, layer1_dropout: float = 0.25, layer2_dropout: float = 0.25, layer3_dropout: float = 0.5,
                  num_classes: int = 10) -> None:
         super().__init__()
+        self.native = os.environ.get("DET_NATIVE_CNN", "1") != "0" and num_classes == 10
         self.net = nn.Sequential(
             nn.Conv2d(3, 32, kernel_size=(3, 3)), nn.ReLU(),
             nn.Conv2d(32, 32, kernel_size=(3, 3)), nn.ReLU(),
-            nn.MaxPool2d((2, 2)), nn.Dropout(layer1_dropout),
+            nn.MaxPool2d((2, 2)), nn.Dropout2d(layer1_dropout),
             nn.Conv2d(32, 64, (3, 3), padding=1), nn.ReLU(),
             nn.Conv2d(64, 64, (3, 3)), nn.ReLU(),
             nn.MaxPool2d((2, 2)), nn.Dropout2d(layer2_dropout),
@@ -67,4 +74,12 @@ class CIFAR10CNN(nn.Module):
         )
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.native and x.is_cuda:
+            from determined_1_amd.ops import cnn
+
+            layers = [self.net[i] for i in (0, 2, 6, 8, 13, 16)]
+            params = [t for m in layers for t in (m.weight, m.bias)]
+            if cnn.supported(x, params):
+                ps = (self.net[5].p, self.net[11].p, self.net[15].p)
+                return cnn.cifar_cnn(x, params, ps, self.training)
         return self.net(x)

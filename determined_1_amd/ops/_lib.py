@@ -262,7 +262,9 @@ def get_lib() -> ctypes.CDLL:
                 "(hipcc --offload-arch=gfx950).  GPU tensors never fall back to eager PyTorch."
             )
         lib = ctypes.CDLL(path)
-        for name, (argtypes, restype) in _SIGNATURES.items():
+        from determined_1_amd.ops.cnn import SIGNATURES as _CNN_SIGS
+
+        for name, (argtypes, restype) in list(_SIGNATURES.items()) + list(_CNN_SIGS.items()):
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = restype

@@ -1,0 +1,740 @@
+// det_cnn.hip — the CIFAR-10 CNN of the ASHA benchmark (BASELINE configs #2/#4) on one generic
+// gather-GEMM kernel: every conv / linear pass of forward and backward, with bias, ReLU, 2x2 max-pool,
+// dropout and the pooling / dropout backward folded into operand loaders and epilogues.
+//
+// Network (reference examples/computer_vision/cifar10_pytorch/model_def.py:47-65), NHWC:
+//   x [N,32,32,3] -> conv1 3->32 -> relu -> a1 [N,30,30,32]
+//   -> conv2 32->32 -> relu -> maxpool2 -> dropout2d -> a2 [N,14,14,32] (+ argmax idx2)
+//   -> conv3 32->64 pad 1 -> relu -> a3 [N,14,14,64]
+//   -> conv4 64->64 -> relu -> maxpool2 -> dropout2d -> a4 [N,6,6,64] (+ idx4)
+//   -> flatten (torch's NCHW order: k = c*36 + h*6 + w) -> fc1 2304->512 -> relu -> dropout -> a5
+//   -> fc2 512->10 -> logits (fp32)
+//
+// Why one generic kernel: at batch 16-64 every pass is a few microseconds of work on a few hundred
+// workgroups, so the step is launch- and latency-bound (round 4: ~130 library kernels per batch,
+// profiles/r4_cifar_trial_steady.txt).  What matters is the number of passes and that no activation
+// is written just to be re-read by an elementwise kernel: here the forward is 7 launches (masks +
+// 6 GEMMs, pooling/dropout in the conv epilogues), the backward 7 (each layer's weight- and input-
+// gradient GEMMs share one launch, one launch reduces every split-K weight gradient into the grad
+// arena), and the unpooling / ReLU / dropout backward never materialise: the gradient operand loader
+// routes the pooled gradient to the argmax position as it stages the tile.
+//
+// GEMM: C[M,N] = sum_k A[m,k] B[k,n], fp32 accumulate on the VALU (64x64 block tile, BK 16, 256 lanes
+// x 4x4 outputs, register-prefetched double buffer through LDS).  At these shapes the convolutions are
+// 25-460 MFLOP: a few microseconds each at VALU rates, well under the launch floor, so the matrix
+// cores would not change the step time (fp32 O0 and bf16 O2 storage share the code path).
+//
+// Dropout masks: one launch per forward draws every mask from Philox4x32-10 keyed by (seed, offset) +
+// the device offset counter (ops/transformer.py rng_base), so hipGraph replays draw fresh masks and
+// backward reads the masks the forward used.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int BM = 64, BN = 64, BK = 16, NT = 256;
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40u);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+// element access for T = float (dtype 0) or bf16 (dtype 1)
+__device__ __forceinline__ float ld(const void* p, int dt, int64_t i) {
+  return dt == 0 ? static_cast<const float*>(p)[i] : bf2f(static_cast<const uint16_t*>(p)[i]);
+}
+__device__ __forceinline__ void st(void* p, int dt, int64_t i, float v) {
+  if (dt == 0) static_cast<float*>(p)[i] = v;
+  else static_cast<uint16_t*>(p)[i] = f2bf(v);
+}
+
+// ---- operand loaders ---------------------------------------------------------------------------
+// Operand roles: ACT = an activation gathered as im2col (conv) or flattened (fc); GRAD = a gradient
+// w.r.t. a layer output; WGT = a weight through its strides; ONES is the bias column of a wgrad.
+enum Src : int {
+  S_ACT_CONV = 0,     // act[n][h][w][c], (pix, kk=(r*S+s)*C+c): h = ho*1 + r - pad (zero outside)
+  S_ACT_FLAT = 1,     // act[n][h][w][c] read in torch's NCHW flatten order: kk = c*HW + h*W + w
+  S_ACT_ROWS = 2,     // act[n][j] (fc input rows)
+  S_GRAD_ROWS = 3,    // g[n][j]
+  S_GRAD_CONV_T = 4,  // dgrad gather: g over output pixels, kk = (r*S+s)*Cg + o, input pixel (h, w):
+                      //   output (h + pad - r, w + pad - s)
+  S_WGT_CONV = 5,     // W[o][c][r][s] via strides: B[kk=(r*S+s)*C+c][n=o]        (forward)
+  S_WGT_CONV_T = 6,   // W[o][c][r][s]: B[kk=(r*S+s)*Cout+o][n=c]                 (dgrad)
+  S_WGT_FC = 7,       // W[o][j]: B[k=j][n=o]                                        (fc forward)
+  S_WGT_FC_T = 8,     // W[o][j]: B[k=o][n=j]                                        (fc dgrad)
+};
+
+struct Operand {
+  const void* p;     // tensor
+  int dt;            // 0 f32, 1 bf16, 2 f32 regardless of the GEMM's dtype (logits-side fp32)
+  int src;           // Src
+  // geometry of the tensor the index maps read (activation / gradient grid)
+  int H, W, C;       // grid of p (for GRAD_CONV_T: the output-gradient grid Ho, Wo, Cout)
+  int R, S, pad;     // conv kernel
+  int OH, OW;        // the GEMM's pixel grid (conv forward/wgrad: output grid; dgrad: input grid)
+  int pool;          // 1: the pixel grid is a 2x2-window-ordered pre-pool grid (m = win*4 + q)
+  // unpool (GRAD operands of a pooled layer): p holds the pooled gradient [n][OH/2][OW/2][C];
+  // idx the argmax (0..3) per pooled element; the value is routed to the argmax position only
+  const uint8_t* idx;
+  int64_t so, sc, sr, ss;  // weight strides (o, c, r, s) in elements / (o, j) for fc
+  int transpose;     // the operand is read as A[m][k] = T[k][m] (wgrad's gradient operand)
+};
+
+__device__ __forceinline__ float opval(const Operand& o, int64_t row, int64_t kk) {
+  // row: the GEMM row this operand element belongs to (A: m; B: n); kk: the reduction index.
+  // Returns the operand value A[row][kk] (or B[kk][row]).
+  switch (o.src) {
+    case S_ACT_CONV: {
+      // row = pixel index over (n, OH, OW) [window ordered if pool]; kk = (r*S+s)*C + c
+      int64_t pix = row;
+      int n, oh, ow;
+      if (o.pool) {
+        const int q = static_cast<int>(pix & 3);
+        int64_t win = pix >> 2;
+        const int PW = o.OW >> 1, PH = o.OH >> 1;
+        const int pw = static_cast<int>(win % PW);
+        win /= PW;
+        const int ph = static_cast<int>(win % PH);
+        n = static_cast<int>(win / PH);
+        oh = 2 * ph + (q >> 1);
+        ow = 2 * pw + (q & 1);
+      } else {
+        ow = static_cast<int>(pix % o.OW);
+        pix /= o.OW;
+        oh = static_cast<int>(pix % o.OH);
+        n = static_cast<int>(pix / o.OH);
+      }
+      const int c = static_cast<int>(kk % o.C);
+      const int rs = static_cast<int>(kk / o.C);
+      const int r = rs / o.S, s = rs - r * o.S;
+      const int h = oh + r - o.pad, w = ow + s - o.pad;
+      if (h < 0 || h >= o.H || w < 0 || w >= o.W) return 0.f;
+      return ld(o.p, o.dt, ((static_cast<int64_t>(n) * o.H + h) * o.W + w) * o.C + c);
+    }
+    case S_ACT_FLAT: {
+      const int64_t n = row;
+      const int hw = o.H * o.W;
+      const int c = static_cast<int>(kk / hw);
+      const int rem = static_cast<int>(kk - static_cast<int64_t>(c) * hw);
+      return ld(o.p, o.dt, (n * hw + rem) * o.C + c);
+    }
+    case S_ACT_ROWS:
+    case S_GRAD_ROWS:
+      return ld(o.p, o.dt == 2 ? 0 : o.dt, row * o.C + kk);
+    case S_GRAD_CONV_T: {
+      // input pixel `row` over (n, OH, OW) = the dgrad output grid; kk = (r*S+s)*C + og
+      int64_t pix = row;
+      const int iw = static_cast<int>(pix % o.OW);
+      pix /= o.OW;
+      const int ih = static_cast<int>(pix % o.OH);
+      const int n = static_cast<int>(pix / o.OH);
+      const int og = static_cast<int>(kk % o.C);
+      const int rs = static_cast<int>(kk / o.C);
+      const int r = rs / o.S, s = rs - r * o.S;
+      const int h = ih + o.pad - r, w = iw + o.pad - s;  // output-gradient position
+      if (h < 0 || h >= o.H || w < 0 || w >= o.W) return 0.f;
+      if (o.idx != nullptr) {  // unpool: gradient of the pre-pool grid (H, W) from the pooled one
+        const int PH = o.H >> 1, PW = o.W >> 1;
+        const int64_t pe = ((static_cast<int64_t>(n) * PH + (h >> 1)) * PW + (w >> 1)) * o.C + og;
+        return o.idx[pe] == ((h & 1) << 1 | (w & 1)) ? ld(o.p, o.dt, pe) : 0.f;
+      }
+      return ld(o.p, o.dt, ((static_cast<int64_t>(n) * o.H + h) * o.W + w) * o.C + og);
+    }
+    case S_WGT_CONV: {
+      const int c = static_cast<int>(kk % o.C);
+      const int rs = static_cast<int>(kk / o.C);
+      const int r = rs / o.S, s = rs - r * o.S;
+      return ld(o.p, o.dt, row * o.so + c * o.sc + r * o.sr + s * o.ss);
+    }
+    case S_WGT_CONV_T: {
+      // B[kk = (r*S+s)*Cout + o][n = c]: the flipped-weight dgrad operand
+      const int og = static_cast<int>(kk % o.C);  // o.C = Cout here
+      const int rs = static_cast<int>(kk / o.C);
+      const int r = rs / o.S, s = rs - r * o.S;
+      return ld(o.p, o.dt, og * o.so + row * o.sc + r * o.sr + s * o.ss);
+    }
+    case S_WGT_FC:
+      return ld(o.p, o.dt, row * o.so + kk * o.sc);
+    case S_WGT_FC_T:
+      return ld(o.p, o.dt, kk * o.so + row * o.sc);
+  }
+  return 0.f;
+}
+
+// gradient operand of a weight gradient: A[m = out channel][k = pixel] = g[pixel][m], with the
+// unpool routing for pooled layers (pixel over the pre-pool grid OH x OW, row-major)
+__device__ __forceinline__ float gradval(const Operand& o, int64_t m, int64_t pix) {
+  if (o.src == S_GRAD_ROWS) return ld(o.p, o.dt == 2 ? 0 : o.dt, pix * o.C + m);
+  if (o.idx != nullptr) {
+    int64_t p = pix;
+    const int w = static_cast<int>(p % o.OW);
+    p /= o.OW;
+    const int h = static_cast<int>(p % o.OH);
+    const int n = static_cast<int>(p / o.OH);
+    const int64_t pe = ((static_cast<int64_t>(n) * (o.OH >> 1) + (h >> 1)) * (o.OW >> 1) + (w >> 1)) * o.C + m;
+    return o.idx[pe] == ((h & 1) << 1 | (w & 1)) ? ld(o.p, o.dt, pe) : 0.f;
+  }
+  return ld(o.p, o.dt, pix * o.C + m);
+}
+
+// ---- epilogues ---------------------------------------------------------------------------------
+enum Epi : int {
+  E_BIAS_RELU = 0,       // out[m][n] = relu(acc + bias[n])                                 (T)
+  E_BIAS_RELU_POOL = 1,  // 2x2 windows of 4 consecutive m: out[m/4][n] = max * drop(img, n), idx
+  E_BIAS_RELU_DROP = 2,  // fc1: out[m][n] = relu(acc + bias) * drop(m, n)
+  E_BIAS = 3,            // fc2 logits: out[m][n] = acc + bias[n]                            (fp32)
+  E_MASK_POS = 4,        // dgrad into a ReLU output a: out = acc * (a[m][n] > 0)            (T)
+  E_DROP_POS = 5,        // dgrad into a dropout(relu) output a (pooled / fc): out = acc * drop * (a > 0)
+  E_DROP_POS_FLAT = 6,   // fc1 dgrad: as 5, written at the NHWC position of flat index n (c*HW + hw)
+  E_GRAD_FC = 7,         // weight gradient W[m][n] (+)= acc via (gso, gsc); n == N-1 with gbias: bias
+  E_GRAD_CONV = 8,       // weight gradient W[o=m][c][r][s] (+)= acc, n = (r*S+s)*C + c; bias column
+};
+
+struct Job {
+  Operand a, b;
+  int64_t M, N, K;
+  int tiles_m, tiles_n, splits;  // blocks = tiles_m * tiles_n * splits
+  int64_t k_per_split;           // multiple of BK
+  int epi;
+  void* out;
+  int out_dt;
+  const void* bias;              // [N] (epilogues 0-3), dtype bias_dt
+  int bias_dt;
+  const float* drop;             // dropout factors [rows of the image / batch][drop_cols] or null (1)
+  int drop_cols;
+  const void* act;               // E_MASK_POS / E_DROP_POS*: the activation a
+  uint8_t* idx;                  // E_BIAS_RELU_POOL: argmax out
+  int HW, C;                     // E_DROP_POS(_FLAT): pooled grid size, channels
+  int PW, PH;                    // E_BIAS_RELU_POOL: pooled grid (image = window / (PH*PW))
+  int64_t gso, gsc, gsr, gss;    // E_GRAD_*: weight-gradient strides
+  int gC, gS;                    // E_GRAD_CONV: kk = (r*gS+s)*gC + c
+  void* gbias;                   // bias gradient (its column is N-1) or null
+  int accumulate;                // E_GRAD_*: add into the existing gradient
+  float* slab;                   // split-K partials [splits][M][N] (splits > 1)
+};
+
+struct Launch {
+  Job job[2];
+  int nblocks0;
+};
+
+__device__ __forceinline__ float drop_factor(const Job& j, int64_t row, int64_t col) {
+  return j.drop == nullptr ? 1.f : j.drop[row * j.drop_cols + col];
+}
+
+// every epilogue but the pooling one, for one output element (GEMM or split-K finish)
+__device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, float v) {
+  switch (J.epi) {
+    case E_BIAS_RELU:
+      st(J.out, J.out_dt, m * J.N + n, fmaxf(v + ld(J.bias, J.bias_dt, n), 0.f));
+      break;
+    case E_BIAS_RELU_DROP: {
+      float r = fmaxf(v + ld(J.bias, J.bias_dt, n), 0.f);
+      r = J.out_dt == 1 ? bf2f(f2bf(r)) : r;  // the reference rounds the Linear output first
+      st(J.out, J.out_dt, m * J.N + n, r * drop_factor(J, m, n));
+      break;
+    }
+    case E_BIAS:
+      static_cast<float*>(J.out)[m * J.N + n] = v + ld(J.bias, J.bias_dt, n);
+      break;
+    case E_MASK_POS:
+      st(J.out, J.out_dt, m * J.N + n, ld(J.act, J.out_dt, m * J.N + n) > 0.f ? v : 0.f);
+      break;
+    case E_DROP_POS: {
+      const float a = ld(J.act, J.out_dt, m * J.N + n);
+      st(J.out, J.out_dt, m * J.N + n, a > 0.f ? v * drop_factor(J, m / J.HW, n) : 0.f);
+      break;
+    }
+    case E_DROP_POS_FLAT: {
+      const int c = static_cast<int>(n / J.HW);
+      const int hw = static_cast<int>(n - static_cast<int64_t>(c) * J.HW);
+      const int64_t e = (m * J.HW + hw) * J.C + c;
+      const float a = ld(J.act, J.out_dt, e);
+      st(J.out, J.out_dt, e, a > 0.f ? v * drop_factor(J, m, c) : 0.f);
+      break;
+    }
+    case E_GRAD_FC:
+    case E_GRAD_CONV: {
+      if (J.gbias != nullptr && n == J.N - 1) {
+        const float prev = J.accumulate ? ld(J.gbias, J.out_dt, m) : 0.f;
+        st(J.gbias, J.out_dt, m, prev + v);
+        break;
+      }
+      int64_t e;
+      if (J.epi == E_GRAD_FC) {
+        e = m * J.gso + n * J.gsc;
+      } else {
+        const int c = static_cast<int>(n % J.gC), rs = static_cast<int>(n / J.gC);
+        const int r = rs / J.gS, sx = rs - r * J.gS;
+        e = m * J.gso + c * J.gsc + r * J.gsr + sx * J.gss;
+      }
+      const float prev = J.accumulate ? ld(J.out, J.out_dt, e) : 0.f;
+      st(J.out, J.out_dt, e, prev + v);
+      break;
+    }
+  }
+}
+
+// ---- the GEMM core on MFMA ---------------------------------------------------------------------
+// 64 x 64 block tile, BK = 32, 4 waves of 32 x 32 (2 x 2 tiles of 16 x 16).  bf16 storage runs
+// v_mfma_f32_16x16x32_bf16 (lane l: A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]); fp32 storage runs the
+// exact-fp32 v_mfma_f32_16x16x4_f32 (A[l&15][l>>4], B[l>>4][l&15]), so O0 keeps fp32 products.
+// C/D: col = l&15, row = 4(l>>4) + i.  Staging: each lane gathers 8 consecutive k of one tile row
+// (the operand loaders above), double-buffered through LDS with the next tile's gathers issued
+// before the current tile's MFMAs.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+template <bool BF>
+struct Stage;
+template <>
+struct Stage<true> {
+  typedef uint16_t E;
+  static constexpr int PAD = 8;  // row stride 40 elements = 80 B (16-B fragment reads stay aligned)
+  __device__ static E cvt(float v) { return f2bf(v); }
+};
+template <>
+struct Stage<false> {
+  typedef float E;
+  static constexpr int PAD = 4;
+  __device__ static E cvt(float v) { return v; }
+};
+
+constexpr int GBK = 32;
+
+template <bool BF>
+__global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
+  using E = typename Stage<BF>::E;
+  constexpr int LDK = GBK + Stage<BF>::PAD;
+  const int jb = static_cast<int>(blockIdx.x) < L.nblocks0 ? 0 : 1;
+  const Job& J = L.job[jb];
+  int bid = jb == 0 ? blockIdx.x : blockIdx.x - L.nblocks0;
+  const int z = bid % J.splits;
+  bid /= J.splits;
+  const int tn = bid % J.tiles_n;
+  const int tm = bid / J.tiles_n;
+  const int64_t m0 = static_cast<int64_t>(tm) * BM, n0 = static_cast<int64_t>(tn) * BN;
+  const int64_t k_lo = static_cast<int64_t>(z) * J.k_per_split;
+  const int64_t k_hi = k_lo + J.k_per_split < J.K ? k_lo + J.k_per_split : J.K;
+
+  __shared__ __attribute__((aligned(16))) E As[2][BM][LDK];
+  __shared__ __attribute__((aligned(16))) E Bs[2][BN][LDK];
+  const int t = threadIdx.x;
+  const int lr = t >> 2, lk = (t & 3) * 8;  // staging: tile row lr, k = lk .. lk+7
+  const int lane = t & 63, w = t >> 6;
+  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
+  const bool wgrad = J.a.transpose != 0;
+  const bool bias_col = wgrad && J.gbias != nullptr;
+
+  float ra[8], rb[8];
+  auto gather = [&](int64_t k0) {
+    const int64_t m = m0 + lr, n = n0 + lr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t k = k0 + lk + i;
+      const bool kin = k < k_hi;
+      ra[i] = (m < J.M && kin) ? (wgrad ? gradval(J.a, m, k) : opval(J.a, m, k)) : 0.f;
+      float v = 0.f;
+      if (n < J.N && kin) {
+        if (wgrad) v = (bias_col && n == J.N - 1) ? 1.f : opval(J.b, k, n);
+        else v = opval(J.b, n, k);
+      }
+      rb[i] = v;
+    }
+  };
+  auto stash = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      As[b][lr][lk + i] = Stage<BF>::cvt(ra[i]);
+      Bs[b][lr][lk + i] = Stage<BF>::cvt(rb[i]);
+    }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int64_t k0 = k_lo;
+  gather(k0);
+  stash(0);
+  __syncthreads();
+  int buf = 0;
+  for (; k0 < k_hi; k0 += GBK) {
+    const bool more = k0 + GBK < k_hi;
+    if (more) gather(k0 + GBK);
+    if constexpr (BF) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(&As[buf][wm + i * 16 + (lane & 15)][8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn + j * 16 + (lane & 15)][8 * (lane >> 4)]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kq = 0; kq < GBK; kq += 4) {
+        float af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = As[buf][wm + i * 16 + (lane & 15)][kq + (lane >> 4)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = Bs[buf][wn + j * 16 + (lane & 15)][kq + (lane >> 4)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      stash(buf ^ 1);
+      buf ^= 1;
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds rows 4(lane>>4)+r, r = 0..3, of column lane&15 of each 16x16 tile
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t mrow = m0 + wm + i * 16 + 4 * (lane >> 4);
+      const int64_t n = n0 + wn + j * 16 + (lane & 15);
+      if (n >= J.N) continue;
+      const f32x4 v = acc[i][j];
+      if (J.splits > 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (mrow + r < J.M) J.slab[(static_cast<int64_t>(z) * J.M + mrow + r) * J.N + n] = v[r];
+        continue;
+      }
+      if (J.epi == E_BIAS_RELU_POOL) {
+        // the 4 rows are one 2x2 window (M window-ordered, M % 4 == 0)
+        if (mrow >= J.M) continue;
+        const int64_t win = mrow >> 2;
+        const int64_t img = win / (static_cast<int64_t>(J.PH) * J.PW);
+        const float bb = ld(J.bias, J.bias_dt, n);
+        float best = fmaxf(v[0] + bb, 0.f);
+        int arg = 0;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          const float x = fmaxf(v[q] + bb, 0.f);
+          if (x > best) {  // first maximum of the row-major window, as torch's max_pool2d
+            best = x;
+            arg = q;
+          }
+        }
+        best = J.out_dt == 1 ? bf2f(f2bf(best)) : best;
+        st(J.out, J.out_dt, win * J.N + n, best * drop_factor(J, img, n));
+        J.idx[win * J.N + n] = static_cast<uint8_t>(arg);
+        continue;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (mrow + r < J.M) epi_store(J, mrow + r, n, v[r]);
+    }
+  }
+}
+
+// ---- split-K finish: sum the slabs of up to 4 jobs and apply their epilogues --------------------
+constexpr int kMaxFin = 4;
+struct FinishLaunch {
+  Job job[kMaxFin];
+  int64_t first[kMaxFin];
+  int njobs;
+  int64_t total;
+};
+
+__global__ void __launch_bounds__(NT) cnn_finish_kernel(FinishLaunch L) {
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x; e < L.total;
+       e += static_cast<int64_t>(gridDim.x) * NT) {
+    int ji = 0;
+    while (ji + 1 < L.njobs && e >= L.first[ji + 1]) ++ji;
+    const Job& J = L.job[ji];
+    const int64_t i = e - L.first[ji];
+    const int64_t m = i / J.N, n = i - m * J.N;
+    float s = 0.f;
+    for (int zz = 0; zz < J.splits; ++zz) s += J.slab[(static_cast<int64_t>(zz) * J.M + m) * J.N + n];
+    epi_store(J, m, n, s);
+  }
+}
+
+// ---- dropout factors ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t philox_u0(uint64_t idx, uint32_t k0, uint32_t k1, uint32_t c2, uint32_t c3) {
+  uint32_t c0 = static_cast<uint32_t>(idx), c1 = static_cast<uint32_t>(idx >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
+struct MaskLaunch {
+  float* out[3];
+  int64_t n[3];
+  float p[3];
+  uint64_t seed, offset;
+  const uint32_t* rng_base;
+};
+
+__global__ void __launch_bounds__(NT) cnn_masks_kernel(MaskLaunch L) {
+  const uint32_t base = L.rng_base != nullptr ? *L.rng_base : 0u;
+  const uint32_t k0 = static_cast<uint32_t>(L.seed), k1 = static_cast<uint32_t>(L.seed >> 32);
+  for (int s = 0; s < 3; ++s) {
+    if (L.out[s] == nullptr) continue;
+    const float p = L.p[s];
+    const float keep = 1.f - p;
+    const uint32_t thr = p >= 1.f ? 0xffffffffu : static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x; i < L.n[s];
+         i += static_cast<int64_t>(gridDim.x) * NT) {
+      const uint32_t u = philox_u0(static_cast<uint64_t>(i), k0, k1, static_cast<uint32_t>(L.offset) + s * 0x9E3779B9u,
+                                   static_cast<uint32_t>(L.offset >> 32) + base);
+      L.out[s][i] = (p <= 0.f) ? 1.f : (u >= thr && keep > 0.f ? 1.f / keep : 0.f);
+    }
+  }
+}
+
+// ---- cross entropy -----------------------------------------------------------------------------
+// loss = mean_n (logsumexp(z_n) - z_n[y_n]); correct = #(argmax z_n == y_n) (first max, as torch);
+// backward dz = g * (softmax(z) - onehot(y)) / N.
+__global__ void __launch_bounds__(NT) cnn_xent_fwd_kernel(const float* z, const int64_t* y, int N, int C,
+                                                          float* loss_out, float* acc_out) {
+  __shared__ float sl[NT], sa[NT];
+  float l = 0.f, a = 0.f;
+  for (int n = threadIdx.x; n < N; n += NT) {
+    const float* r = z + static_cast<int64_t>(n) * C;
+    float mx = r[0];
+    int arg = 0;
+    for (int c = 1; c < C; ++c)
+      if (r[c] > mx) {
+        mx = r[c];
+        arg = c;
+      }
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(r[c] - mx);
+    const int yy = static_cast<int>(y[n]);
+    l += logf(se) + mx - r[yy];
+    a += arg == yy ? 1.f : 0.f;
+  }
+  sl[threadIdx.x] = l;
+  sa[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = NT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sl[threadIdx.x] += sl[threadIdx.x + o];
+      sa[threadIdx.x] += sa[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    loss_out[0] = sl[0] / N;
+    if (acc_out != nullptr) acc_out[0] = sa[0] / N;
+  }
+}
+
+__global__ void __launch_bounds__(NT) cnn_xent_bwd_kernel(const float* z, const int64_t* y, const float* g, int N,
+                                                          int C, float* dz) {
+  const float gs = g[0] / N;
+  for (int n = blockIdx.x * NT + threadIdx.x; n < N; n += gridDim.x * NT) {
+    const float* r = z + static_cast<int64_t>(n) * C;
+    float mx = r[0];
+    for (int c = 1; c < C; ++c) mx = fmaxf(mx, r[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(r[c] - mx);
+    const float inv = 1.f / se;
+    const int yy = static_cast<int>(y[n]);
+    for (int c = 0; c < C; ++c) dz[static_cast<int64_t>(n) * C + c] = gs * (expf(r[c] - mx) * inv - (c == yy ? 1.f : 0.f));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// mirrored by determined_1_amd/ops/cnn.py (ctypes Structures, field order matters)
+struct DetCnnOperand {
+  const void* p;
+  int32_t dt, src, H, W, C, R, S, pad, OH, OW, pool, transpose;
+  const uint8_t* idx;
+  int64_t so, sc, sr, ss;
+};
+struct DetCnnJob {
+  DetCnnOperand a, b;
+  int64_t M, N, K;
+  int32_t splits, epi, out_dt, bias_dt, drop_cols, HW, C, PW, PH, gC, gS, accumulate;
+  void* out;
+  const void* bias;
+  const float* drop;
+  const void* act;
+  uint8_t* idx;
+  int64_t gso, gsc, gsr, gss;
+  void* gbias;
+  float* slab;
+};
+
+static Operand to_operand(const DetCnnOperand& d) {
+  Operand o;
+  o.p = d.p;
+  o.dt = d.dt;
+  o.src = d.src;
+  o.H = d.H;
+  o.W = d.W;
+  o.C = d.C;
+  o.R = d.R;
+  o.S = d.S;
+  o.pad = d.pad;
+  o.OH = d.OH;
+  o.OW = d.OW;
+  o.pool = d.pool;
+  o.idx = d.idx;
+  o.so = d.so;
+  o.sc = d.sc;
+  o.sr = d.sr;
+  o.ss = d.ss;
+  o.transpose = d.transpose;
+  return o;
+}
+
+static int64_t k_per_split(int64_t K, int splits) {
+  int64_t kps = (K + splits - 1) / splits;
+  return (kps + GBK - 1) / GBK * GBK;
+}
+
+// the split count a job with reduction length K and requested splits runs with
+int det_cnn_splits(int64_t K, int32_t splits) {
+  if (splits < 1) splits = 1;
+  const int64_t kps = k_per_split(K, splits);
+  return static_cast<int>((K + kps - 1) / kps);
+}
+
+static int fill_job(const DetCnnJob& d, Job* j) {
+  if (d.M < 1 || d.N < 1 || d.K < 1) return -1;
+  j->a = to_operand(d.a);
+  j->b = to_operand(d.b);
+  j->M = d.M;
+  j->N = d.N;
+  j->K = d.K;
+  j->tiles_m = static_cast<int>((d.M + BM - 1) / BM);
+  j->tiles_n = static_cast<int>((d.N + BN - 1) / BN);
+  j->splits = det_cnn_splits(d.K, d.splits);
+  j->k_per_split = k_per_split(d.K, j->splits > 1 ? j->splits : 1);
+  if (j->splits == 1) j->k_per_split = d.K;
+  j->epi = d.epi;
+  j->out = d.out;
+  j->out_dt = d.out_dt;
+  j->bias = d.bias;
+  j->bias_dt = d.bias_dt;
+  j->drop = d.drop;
+  j->drop_cols = d.drop_cols;
+  j->act = d.act;
+  j->idx = d.idx;
+  j->HW = d.HW < 1 ? 1 : d.HW;
+  j->C = d.C;
+  j->PW = d.PW;
+  j->PH = d.PH;
+  j->gso = d.gso;
+  j->gsc = d.gsc;
+  j->gsr = d.gsr;
+  j->gss = d.gss;
+  j->gC = d.gC < 1 ? 1 : d.gC;
+  j->gS = d.gS < 1 ? 1 : d.gS;
+  j->gbias = d.gbias;
+  j->accumulate = d.accumulate;
+  j->slab = d.slab;
+  if (j->splits > 1 && (d.slab == nullptr || d.epi == E_BIAS_RELU_POOL)) return -1;
+  if (d.epi == E_BIAS_RELU_POOL && (d.M & 3)) return -1;
+  return j->tiles_m * j->tiles_n * j->splits;
+}
+
+// one launch running job0 and (optionally) job1 side by side (both of storage dtype `bf16`)
+int det_cnn_gemm(void* stream, int32_t bf16, const DetCnnJob* j0, const DetCnnJob* j1) {
+  Launch L;
+  const int b0 = fill_job(*j0, &L.job[0]);
+  if (b0 <= 0) return static_cast<int>(hipErrorInvalidValue);
+  int b1 = 0;
+  if (j1 != nullptr) {
+    b1 = fill_job(*j1, &L.job[1]);
+    if (b1 <= 0) return static_cast<int>(hipErrorInvalidValue);
+  } else {
+    L.job[1] = L.job[0];
+  }
+  L.nblocks0 = b0;
+  if (bf16) cnn_gemm_kernel<true><<<b0 + b1, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
+  else cnn_gemm_kernel<false><<<b0 + b1, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
+  return static_cast<int>(hipGetLastError());
+}
+
+// the split-K finish of up to 4 jobs (their slabs summed, their epilogues applied) in one launch
+int det_cnn_finish(void* stream, const DetCnnJob* jobs, int32_t njobs) {
+  if (njobs < 1 || njobs > kMaxFin) return static_cast<int>(hipErrorInvalidValue);
+  FinishLaunch L;
+  int64_t total = 0;
+  for (int i = 0; i < njobs; ++i) {
+    if (fill_job(jobs[i], &L.job[i]) <= 0 || L.job[i].splits < 2) return static_cast<int>(hipErrorInvalidValue);
+    L.first[i] = total;
+    total += L.job[i].M * L.job[i].N;
+  }
+  for (int i = njobs; i < kMaxFin; ++i) {
+    L.job[i] = L.job[0];
+    L.first[i] = total;
+  }
+  L.njobs = njobs;
+  L.total = total;
+  int blocks = static_cast<int>((total + NT - 1) / NT);
+  blocks = blocks > 2048 ? 2048 : blocks;
+  cnn_finish_kernel<<<blocks, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
+  return static_cast<int>(hipGetLastError());
+}
+
+int det_cnn_masks(void* stream, float* m0, int64_t n0, float p0, float* m1, int64_t n1, float p1, float* m2,
+                  int64_t n2, float p2, uint64_t seed, uint64_t offset, const uint32_t* rng_base) {
+  MaskLaunch L;
+  L.out[0] = m0;
+  L.out[1] = m1;
+  L.out[2] = m2;
+  L.n[0] = n0;
+  L.n[1] = n1;
+  L.n[2] = n2;
+  L.p[0] = p0;
+  L.p[1] = p1;
+  L.p[2] = p2;
+  L.seed = seed;
+  L.offset = offset;
+  L.rng_base = rng_base;
+  int64_t mx = n0 > n1 ? n0 : n1;
+  mx = mx > n2 ? mx : n2;
+  int blocks = static_cast<int>((mx + NT - 1) / NT);
+  blocks = blocks < 1 ? 1 : (blocks > 256 ? 256 : blocks);
+  cnn_masks_kernel<<<blocks, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
+  return static_cast<int>(hipGetLastError());
+}
+
+int det_cnn_xent_fwd(void* stream, const float* z, const int64_t* y, int32_t N, int32_t C, float* loss,
+                     float* acc) {
+  if (N < 1 || C < 1) return static_cast<int>(hipErrorInvalidValue);
+  cnn_xent_fwd_kernel<<<1, NT, 0, static_cast<hipStream_t>(stream)>>>(z, y, N, C, loss, acc);
+  return static_cast<int>(hipGetLastError());
+}
+
+int det_cnn_xent_bwd(void* stream, const float* z, const int64_t* y, const float* g, int32_t N, int32_t C,
+                     float* dz) {
+  if (N < 1 || C < 1) return static_cast<int>(hipErrorInvalidValue);
+  const int blocks = (N + NT - 1) / NT;
+  cnn_xent_bwd_kernel<<<blocks, NT, 0, static_cast<hipStream_t>(stream)>>>(z, y, g, N, C, dz);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

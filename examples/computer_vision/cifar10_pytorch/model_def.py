@@ -6,8 +6,9 @@ layout (uint8 HWC images, class templates + noise) is used.  The reference decod
 per sample on the host (``ToTensor`` + ``Normalize((0.5,)*3, (0.5,)*3)``); here each batch arrives
 as one uint8 tensor (no per-sample host work) and the same normalisation, (x/255 - 0.5)/0.5, runs
 on the GPU in the ``u8_normalize`` HIP kernel inside ``train_batch`` -- so with
-``optimizations.hip_graph`` it is part of the replayed graph.  On MI355X the trial runs bf16 via
-``configure_apex_amp`` when ``amp`` is set.
+``optimizations.hip_graph`` it is part of the replayed graph.  On MI355X the network runs on the
+native CNN kernels (``ops/cnn.py``; fp32 at O0, bf16 via ``configure_apex_amp`` at O2) and the loss
+and accuracy come from one fused cross-entropy launch.
 """
 from typing import Any, Dict
 
@@ -17,6 +18,7 @@ import torch.nn as nn
 from determined_1_amd import pytorch
 from determined_1_amd.models import CIFAR10CNN
 from determined_1_amd.models.synthetic import SyntheticImageClasses, passthrough_collate
+from determined_1_amd.ops.cnn import cross_entropy
 from determined_1_amd.ops.functional import u8_normalize
 
 MEAN = STD = (127.5, 127.5, 127.5)  # ToTensor (/255) then Normalize(0.5, 0.5)
@@ -31,7 +33,8 @@ class CIFARTrial(pytorch.PyTorchTrial):
         net = CIFAR10CNN(hp.get("layer1_dropout", 0.25), hp.get("layer2_dropout", 0.25), hp.get("layer3_dropout", 0.5))
         self.model = context.wrap_model(net.to(memory_format=torch.channels_last))
         self.opt = context.wrap_optimizer(torch.optim.RMSprop(
-            self.model.parameters(), lr=hp.get("learning_rate", 1e-4), weight_decay=hp.get("learning_rate_decay", 1e-6)))
+            self.model.parameters(), lr=hp.get("learning_rate", 1e-4), weight_decay=hp.get("learning_rate_decay", 1e-6),
+            alpha=0.9))
         amp = hp.get("amp")
         if amp and amp != "O0":
             self.model, self.opt = context.configure_apex_amp(self.model, self.opt, opt_level=amp)
@@ -54,13 +57,12 @@ class CIFARTrial(pytorch.PyTorchTrial):
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:
         x, y = batch
         out = self.model(self._images(x))
-        loss = self.loss(out.float(), y)
+        loss, acc = cross_entropy(out, y, with_accuracy=True)  # one fused launch on the GPU
         self.context.backward(loss)
         self.context.step_optimizer(self.opt)
-        return {"loss": loss, "train_error": 1.0 - (out.argmax(1) == y).float().mean()}
+        return {"loss": loss, "train_error": 1.0 - acc, "train_accuracy": acc}
 
     def evaluate_batch(self, batch: Any) -> Dict[str, Any]:
         x, y = batch
-        out = self.model(self._images(x)).float()
-        err = 1.0 - (out.argmax(1) == y).float().mean()
-        return {"validation_loss": self.loss(out, y), "validation_error": err, "validation_accuracy": 1.0 - err}
+        loss, acc = cross_entropy(self.model(self._images(x)), y, with_accuracy=True)
+        return {"validation_loss": loss, "validation_error": 1.0 - acc, "validation_accuracy": acc}

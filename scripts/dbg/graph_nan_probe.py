@@ -75,6 +75,10 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default="gpurun_out/nanprobe")
     ap.add_argument("--eager-trials", type=int, default=64)
+    ap.add_argument("--check-every", type=int, default=1,
+                    help="synchronise and check invariants every N replays (1: every replay, as round-5 s2)")
+    ap.add_argument("--r4-model", action="store_true",
+                    help="round-4 model: element Dropout after the first pool and RMSprop alpha 0.99")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     os.environ["DET_GRAPH_HALF_DROPOUT"] = "1"  # lift the round-4 guard: this probe is about that defect
@@ -102,8 +106,15 @@ def main():
             step += 1
         yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
 
+    os.environ["DET_NATIVE_CNN"] = "0"  # the torch layers: this probe is about torch dropout under replays
     ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=True, trial_seed=args.seed)
     trial = ctrl.trial
+    if args.r4_model:
+        import torch.nn as nn
+
+        trial.model.net[5] = nn.Dropout(trial.model.net[5].p)
+        for g in trial.opt.param_groups:
+            g["alpha"] = 0.99
     patch_dropout(trial.model, args.variant)
     ctx = ctrl.context
     state = {"batch": 0, "violation": None, "log": [], "t0": time.time()}
@@ -160,13 +171,15 @@ def main():
     pre = {"snap": None, "batch": None}
 
     def replay(self, g, leaves):
-        if state["violation"] is None:
+        every = args.check_every
+        due = (state["batch"] + 1) % every == 0
+        if state["violation"] is None and every == 1:
             pre["snap"] = snapshot()
             pre["batch"] = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
         out = orig_replay(self, g, leaves)
         state["batch"] += 1
-        if state["violation"] is None:
-            v = check("replay", out, g.static_in, pre["batch"])
+        if state["violation"] is None and due:
+            v = check("replay", out, g.static_in, pre["batch"]) if every == 1 else check("replay", out)
             if v:
                 state["violation"] = {"batch": state["batch"], "what": v, "tag": "replay"}
         return out
@@ -209,11 +222,12 @@ def main():
            "graph_batches": args.graph_batches, "no_graph": args.no_graph, "batches_seen": state["batch"],
            "graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
            "violation": state["violation"], "wall_s": round(time.time() - state["t0"], 1)}
-    tag = f"{args.variant}_{args.amp}_g{0 if args.no_graph else args.graph_batches}_s{args.seed}"
+    tag = (f"{args.variant}_{args.amp}_g{0 if args.no_graph else args.graph_batches}_s{args.seed}"
+           f"_c{args.check_every}{'_r4' if args.r4_model else ''}")
     with open(os.path.join(args.out, f"{tag}.log.jsonl"), "w") as fh:
         for r in state["log"]:
             fh.write(json.dumps(r) + "\n")
-    if state["violation"] is not None and pre["snap"] is not None:
+    if state["violation"] is not None and pre["snap"] is not None and args.check_every == 1:
         torch.save({"snap": pre["snap"], "batch": pre["batch"]}, os.path.join(args.out, f"{tag}_pre.pt"))
         res["eager_replays"] = eager_replays(pre, args, trial)
     print(json.dumps(res, default=str), flush=True)
