@@ -244,49 +244,54 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
         return dict(epi=E_GRAD_CONV, out=g[i].data_ptr(), out_dt=dt, gso=st[0], gsc=st[1], gsr=st[2], gss=st[3],
                     gC=cin, gS=3, gbias=g[i + 1].data_ptr(), accumulate=acc[i])
 
+    deferred = []  # type: List[Job]
+
+    def step(j0: Job, j1: Optional[Job] = None) -> None:
+        """Launch a (weight grad, input grad) pair; a split input gradient is finished before the
+        next layer reads it, split weight gradients are finished together at the end."""
+        split = R.gemm(j0, j1)
+        deferred.extend(j for j in split if j.epi in (E_GRAD_FC, E_GRAD_CONV))
+        R.finish([j for j in split if j.epi not in (E_GRAD_FC, E_GRAD_CONV)])
+
     # fc2: weight grad (K = batch) || input grad -> dz5 = d(a5) * drop * (a5 > 0)
-    fin = R.gemm(R.prepare(Job(a=Operand(p=dl.data_ptr(), dt=0, src=S_GRAD_ROWS, C=10, transpose=1),
-                               b=Operand(p=a5.data_ptr(), dt=dt, src=S_ACT_ROWS, C=512), M=10, N=513, K=n, **gfc(10, n))),
-                 R.prepare(Job(a=Operand(p=dl.data_ptr(), dt=0, src=S_GRAD_ROWS, C=10), b=_wgt(w6, dt, S_WGT_FC_T, 0),
-                               M=n, N=512, K=10, epi=E_DROP_POS, out=dz5.data_ptr(), out_dt=dt, act=a5.data_ptr(),
-                               drop=_p(m5), drop_cols=512, HW=1)))
-    R.finish(fin)
+    step(R.prepare(Job(a=Operand(p=dl.data_ptr(), dt=0, src=S_GRAD_ROWS, C=10, transpose=1),
+                       b=Operand(p=a5.data_ptr(), dt=dt, src=S_ACT_ROWS, C=512), M=10, N=513, K=n, **gfc(10, n))),
+         R.prepare(Job(a=Operand(p=dl.data_ptr(), dt=0, src=S_GRAD_ROWS, C=10), b=_wgt(w6, dt, S_WGT_FC_T, 0),
+                       M=n, N=512, K=10, epi=E_DROP_POS, out=dz5.data_ptr(), out_dt=dt, act=a5.data_ptr(),
+                       drop=_p(m5), drop_cols=512, HW=1)))
     # fc1: weight grad || input grad -> dp4 (NHWC) = d(a4) * drop2d * (a4 > 0)
-    fin = R.gemm(R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512, transpose=1),
-                               b=Operand(p=a4.data_ptr(), dt=dt, src=S_ACT_FLAT, H=6, W=6, C=64), M=512, N=2305, K=n,
-                               **gfc(8, n))),
-                 R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512), b=_wgt(w5, dt, S_WGT_FC_T, 0),
-                               M=n, N=2304, K=512, epi=E_DROP_POS_FLAT, out=dp4.data_ptr(), out_dt=dt,
-                               act=a4.data_ptr(), drop=_p(m4), drop_cols=64, HW=36, C=64)))
-    R.finish(fin)
+    step(R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512, transpose=1),
+                       b=Operand(p=a4.data_ptr(), dt=dt, src=S_ACT_FLAT, H=6, W=6, C=64), M=512, N=2305, K=n,
+                       **gfc(8, n))),
+         R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512), b=_wgt(w5, dt, S_WGT_FC_T, 0),
+                       M=n, N=2304, K=512, epi=E_DROP_POS_FLAT, out=dp4.data_ptr(), out_dt=dt,
+                       act=a4.data_ptr(), drop=_p(m4), drop_cols=64, HW=36, C=64)))
     # conv4: weight grad over the unpooled gradient || input grad -> dy3 = d(a3) * (a3 > 0)
     unpool4 = Operand(p=dp4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=12, W=12, C=64, R=3, S=3, pad=0, OH=12, OW=12,
                       idx=idx4.data_ptr(), transpose=1)
-    fin = R.gemm(R.prepare(Job(a=unpool4, b=_conv_act(a3, dt, 14, 64, 0, 12), M=64, N=577, K=n * 144, **gconv(6, 64))),
-                 R.prepare(Job(a=Operand(p=dp4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=12, W=12, C=64, R=3, S=3, pad=0,
-                                         OH=14, OW=14, idx=idx4.data_ptr()),
-                               b=_wgt(w4, dt, S_WGT_CONV_T, 64), M=n * 196, N=64, K=576, epi=E_MASK_POS,
-                               out=dy3.data_ptr(), out_dt=dt, act=a3.data_ptr())))
-    R.finish(fin)
+    step(R.prepare(Job(a=unpool4, b=_conv_act(a3, dt, 14, 64, 0, 12), M=64, N=577, K=n * 144, **gconv(6, 64))),
+         R.prepare(Job(a=Operand(p=dp4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=12, W=12, C=64, R=3, S=3, pad=0,
+                                 OH=14, OW=14, idx=idx4.data_ptr()),
+                       b=_wgt(w4, dt, S_WGT_CONV_T, 64), M=n * 196, N=64, K=576, epi=E_MASK_POS,
+                       out=dy3.data_ptr(), out_dt=dt, act=a3.data_ptr())))
     # conv3 (pad 1): weight grad || input grad -> dp2 = d(a2) * drop2d * (a2 > 0)
-    fin = R.gemm(R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=64, OH=14, OW=14, transpose=1),
-                               b=_conv_act(a2, dt, 14, 32, 1, 14), M=64, N=289, K=n * 196, **gconv(4, 32))),
-                 R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=14, W=14, C=64, R=3, S=3, pad=1,
-                                         OH=14, OW=14),
-                               b=_wgt(w3, dt, S_WGT_CONV_T, 64), M=n * 196, N=32, K=576, epi=E_DROP_POS,
-                               out=dp2.data_ptr(), out_dt=dt, act=a2.data_ptr(), drop=_p(m2), drop_cols=32, HW=196)))
-    R.finish(fin)
+    step(R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=64, OH=14, OW=14, transpose=1),
+                       b=_conv_act(a2, dt, 14, 32, 1, 14), M=64, N=289, K=n * 196, **gconv(4, 32))),
+         R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=14, W=14, C=64, R=3, S=3, pad=1,
+                                 OH=14, OW=14),
+                       b=_wgt(w3, dt, S_WGT_CONV_T, 64), M=n * 196, N=32, K=576, epi=E_DROP_POS,
+                       out=dp2.data_ptr(), out_dt=dt, act=a2.data_ptr(), drop=_p(m2), drop_cols=32, HW=196)))
     # conv2: weight grad over the unpooled gradient || input grad -> dy1 = d(a1) * (a1 > 0)
     unpool2 = Operand(p=dp2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=28, OW=28, idx=idx2.data_ptr(), transpose=1)
-    fin = R.gemm(R.prepare(Job(a=unpool2, b=_conv_act(a1, dt, 30, 32, 0, 28), M=32, N=289, K=n * 784, **gconv(2, 32))),
-                 R.prepare(Job(a=Operand(p=dp2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=28, W=28, C=32, R=3, S=3, pad=0,
-                                         OH=30, OW=30, idx=idx2.data_ptr()),
-                               b=_wgt(w2, dt, S_WGT_CONV_T, 32), M=n * 900, N=32, K=288, epi=E_MASK_POS,
-                               out=dy1.data_ptr(), out_dt=dt, act=a1.data_ptr())))
+    step(R.prepare(Job(a=unpool2, b=_conv_act(a1, dt, 30, 32, 0, 28), M=32, N=289, K=n * 784, **gconv(2, 32))),
+         R.prepare(Job(a=Operand(p=dp2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=28, W=28, C=32, R=3, S=3, pad=0,
+                                 OH=30, OW=30, idx=idx2.data_ptr()),
+                       b=_wgt(w2, dt, S_WGT_CONV_T, 32), M=n * 900, N=32, K=288, epi=E_MASK_POS,
+                       out=dy1.data_ptr(), out_dt=dt, act=a1.data_ptr())))
     # conv1: weight grad only (no input gradient)
-    fin += R.gemm(R.prepare(Job(a=Operand(p=dy1.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=30, OW=30, transpose=1),
-                                b=_conv_act(xh, dt, 32, 3, 0, 30), M=32, N=28, K=n * 900, **gconv(0, 3))))
-    R.finish(fin)
+    step(R.prepare(Job(a=Operand(p=dy1.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=30, OW=30, transpose=1),
+                        b=_conv_act(xh, dt, 32, 3, 0, 30), M=32, N=28, K=n * 900, **gconv(0, 3))))
+    R.finish(deferred)
     return [t[0] if t[1] else None for t in targets]
 
 

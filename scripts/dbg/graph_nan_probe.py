@@ -77,6 +77,9 @@ def main():
     ap.add_argument("--eager-trials", type=int, default=64)
     ap.add_argument("--check-every", type=int, default=1,
                     help="synchronise and check invariants every N replays (1: every replay, as round-5 s2)")
+    ap.add_argument("--loss", default="native", choices=("native", "torch", "torch_ce", "torch_acc"),
+                    help="torch: round-4 train_batch (F.cross_entropy on out.float() + argmax accuracy); torch_ce / "
+                         "torch_acc: only that half in torch, the other from the fused native kernel")
     ap.add_argument("--r4-model", action="store_true",
                     help="round-4 model: element Dropout after the first pool and RMSprop alpha 0.99")
     args = ap.parse_args()
@@ -109,6 +112,21 @@ def main():
     os.environ["DET_NATIVE_CNN"] = "0"  # the torch layers: this probe is about torch dropout under replays
     ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=True, trial_seed=args.seed)
     trial = ctrl.trial
+    if args.loss != "native":
+        import torch.nn.functional as F
+
+        native_ce = model_def.cross_entropy
+
+        def loss_fn(out, y, with_accuracy=False):
+            if args.loss == "torch":  # exactly round 4's train_batch
+                lt, at = F.cross_entropy(out.float(), y), (out.argmax(1) == y).float().mean()
+                return (lt, at) if with_accuracy else lt
+            ln, an = native_ce(out, y, with_accuracy=True)
+            lt = F.cross_entropy(out.float(), y) if args.loss in ("torch", "torch_ce") else ln
+            at = (out.argmax(1) == y).float().mean() if args.loss in ("torch", "torch_acc") else an
+            return (lt, at) if with_accuracy else lt
+
+        model_def.cross_entropy = loss_fn
     if args.r4_model:
         import torch.nn as nn
 
@@ -223,7 +241,7 @@ def main():
            "graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
            "violation": state["violation"], "wall_s": round(time.time() - state["t0"], 1)}
     tag = (f"{args.variant}_{args.amp}_g{0 if args.no_graph else args.graph_batches}_s{args.seed}"
-           f"_c{args.check_every}{'_r4' if args.r4_model else ''}")
+           f"_c{args.check_every}{'_r4' if args.r4_model else ''}_{args.loss}")
     with open(os.path.join(args.out, f"{tag}.log.jsonl"), "w") as fh:
         for r in state["log"]:
             fh.write(json.dumps(r) + "\n")
