@@ -30,6 +30,7 @@
 // (biased variance for normalisation, unbiased for running_var, momentum=None -> cumulative).
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 
@@ -57,6 +58,13 @@ template <> struct IO8<unsigned short> {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = bf2f(r[j]);
   }
+  // streaming read of data this pass alone consumes: the nt hint (det_stream.hip measured 6.4 vs
+  // 5.4 TB/s for 16-B/lane reads of 2 GiB, profiles/r5_hbm_stream.txt)
+  static __device__ __forceinline__ void load_nt(const unsigned short* p, float (&v)[8]) {
+    us8 r = __builtin_nontemporal_load(reinterpret_cast<const us8*>(p));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(r[j]);
+  }
   static __device__ __forceinline__ void store(unsigned short* p, const float (&v)[8]) {
     us8 r;
 #pragma unroll
@@ -71,6 +79,7 @@ template <> struct IO8<float> {
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   }
+  static __device__ __forceinline__ void load_nt(const float* p, float (&v)[8]) { load(p, v); }
   static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
     reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
     reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
@@ -78,6 +87,20 @@ template <> struct IO8<float> {
 };
 
 __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) { IO8<float>::load(p, v); }
+template <bool NT, typename T>
+__device__ __forceinline__ void sload8(const T* p, float (&v)[8]) {
+  if constexpr (NT) IO8<T>::load_nt(p, v);
+  else IO8<T>::load(p, v);
+}
+
+// DET_BN_NT=1: the BatchNorm apply passes read their activation streams with the nontemporal hint
+inline bool bn_nt() {
+  static const bool v = [] {
+    const char* e = std::getenv("DET_BN_NT");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
+}
 
 struct Geom {
   int64_t M;   // rows
@@ -454,7 +477,7 @@ void launch_stats_finalize(hipStream_t st, const float* pmean, const float* pm2,
 // (ResNet's projection-shortcut BN): res = bf16(r * rscale + rshift), computed here from its input r
 // -- that BN's own apply pass (read r, write res) and this pass's read of res become one read of r.
 // ---------------------------------------------------------------------------------------------
-template <typename T, bool RELU, int RES>
+template <typename T, bool RELU, int RES, bool NTL = false>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
              const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int C,
@@ -469,8 +492,8 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
     for (int u = 0; u < 4; ++u) {
       const int64_t v = v0 + u * S;
       if (v < nvec) {
-        IO8<T>::load(x + v * 8, xv[u]);
-        if (RES) IO8<T>::load(res + v * 8, rv[u]);
+        sload8<NTL>(x + v * 8, xv[u]);
+        if (RES) sload8<NTL>(res + v * 8, rv[u]);
       }
     }
 #pragma unroll
@@ -764,7 +787,7 @@ void launch_bwd_finalize(hipStream_t st, const float* psum, const float* psumx, 
   hipLaunchKernelGGL(bn_bwd_combine, dim3(cb), dim3(kFinThreads), 0, st, scratch, S, g, bf);
 }
 
-template <typename T, int MASK, bool DRES>
+template <typename T, int MASK, bool DRES, bool NTL = false>
 __global__ void __launch_bounds__(kThreads)
 bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ dy2, const T* __restrict__ x,
              const uint8_t* __restrict__ mbits,
@@ -779,11 +802,11 @@ bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ dy2, const T* __res
     for (int u = 0; u < 2; ++u) {
       const int64_t v = v0 + u * S;
       if (v < nvec) {
-        IO8<T>::load(dy + v * 8, dv[u]);
-        IO8<T>::load(x + v * 8, xv[u]);
+        sload8<NTL>(dy + v * 8, dv[u]);
+        sload8<NTL>(x + v * 8, xv[u]);
         if (dy2) {
           float e[8];
-          IO8<T>::load(dy2 + v * 8, e);
+          sload8<NTL>(dy2 + v * 8, e);
 #pragma unroll
           for (int j = 0; j < 8; ++j) dv[u][j] += e[j];
         }
@@ -886,9 +909,16 @@ int det_bn_fwd_train(void* stream, int dtype, const void* x, const void* res, vo
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
 #define DET_BN_FWD(T, RL, RS)                                                                          \
-  hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                    \
-                     static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, shift, \
-                     nvec, C, bump, mbits)
+  do {                                                                                                 \
+    if (bn_nt())                                                                                       \
+      hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS, true>), dim3(grid2), dim3(kThreads), 0, st,          \
+                         static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, \
+                         shift, nvec, C, bump, mbits);                                                 \
+    else                                                                                               \
+      hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                \
+                         static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, \
+                         shift, nvec, C, bump, mbits);                                                 \
+  } while (0)
   if (dtype == 1) {
     if (relu && res) DET_BN_FWD(unsigned short, true, true);
     else if (relu) DET_BN_FWD(unsigned short, true, false);
@@ -960,15 +990,27 @@ int det_bn_fwd_from_partials(void* stream, int dtype, const void* x, const void*
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 4);
   if (res_scale) {  // the residual is a deferred BN apply of its input res (RES 2)
-    hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2>), dim3(grid2), dim3(kThreads), 0, st,
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2, true>), dim3(grid2), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                       static_cast<unsigned short*>(y), scale, shift, nvec, C, bump, mbits, res_scale, res_shift);
+    else
+      hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2>), dim3(grid2), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
                        static_cast<unsigned short*>(y), scale, shift, nvec, C, bump, mbits, res_scale, res_shift);
     return static_cast<int>(hipGetLastError());
   }
 #define DET_BN_FWD(T, RL, RS)                                                                          \
-  hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                    \
-                     static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, shift, \
-                     nvec, C, bump, mbits)
+  do {                                                                                                 \
+    if (bn_nt())                                                                                       \
+      hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS, true>), dim3(grid2), dim3(kThreads), 0, st,          \
+                         static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, \
+                         shift, nvec, C, bump, mbits);                                                 \
+    else                                                                                               \
+      hipLaunchKernelGGL((bn_apply_fwd<T, RL, RS>), dim3(grid2), dim3(kThreads), 0, st,                \
+                         static_cast<const T*>(x), static_cast<const T*>(res), static_cast<T*>(y), scale, \
+                         shift, nvec, C, bump, mbits);                                                 \
+  } while (0)
   if (dtype == 1) {
     if (relu && res) DET_BN_FWD(unsigned short, true, true);
     else if (relu) DET_BN_FWD(unsigned short, true, false);
@@ -994,12 +1036,23 @@ int det_bn_apply_res_mbits(void* stream, const void* x, const void* res, void* y
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nvec = M * C / 8;
   if (res_scale)
-    hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2, true>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                       static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits,
+                       res_scale, res_shift);
+    else
+      hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 2>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
                        static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits,
                        res_scale, res_shift);
   else
-    hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 1>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 1, true>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
+                       static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits);
+    else
+      hipLaunchKernelGGL((bn_apply_fwd<unsigned short, true, 1>), dim3(apply_grid(nvec, 4)), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(res),
                        static_cast<unsigned short*>(y), scale, shift, nvec, C, static_cast<int64_t*>(nullptr), mbits);
   return static_cast<int>(hipGetLastError());
@@ -1054,13 +1107,26 @@ int det_bn_bwd_from_partials(void* stream, int dtype, const void* d, const void*
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 2);
   if (dtype == 1)
-    hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false>), dim3(grid2), dim3(kThreads), 0, st,
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false, true>), dim3(grid2), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(d), static_cast<const unsigned short*>(nullptr),
+                       static_cast<const unsigned short*>(x), static_cast<const uint8_t*>(nullptr), coef,
+                       static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
+                       static_cast<unsigned short*>(dx), static_cast<unsigned short*>(nullptr), nvec, C);
+    else
+      hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false>), dim3(grid2), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(d), static_cast<const unsigned short*>(nullptr),
                        static_cast<const unsigned short*>(x), static_cast<const uint8_t*>(nullptr), coef,
                        static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
                        static_cast<unsigned short*>(dx), static_cast<unsigned short*>(nullptr), nvec, C);
   else
-    hipLaunchKernelGGL((bn_apply_bwd<float, 0, false>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_bwd<float, 0, false, true>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
+                       static_cast<const float*>(nullptr), static_cast<const float*>(x),
+                       static_cast<const uint8_t*>(nullptr), coef, static_cast<const float*>(nullptr),
+                       static_cast<const float*>(nullptr), static_cast<float*>(dx), static_cast<float*>(nullptr), nvec, C);
+    else
+      hipLaunchKernelGGL((bn_apply_bwd<float, 0, false>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
                        static_cast<const float*>(nullptr), static_cast<const float*>(x),
                        static_cast<const uint8_t*>(nullptr), coef, static_cast<const float*>(nullptr),
                        static_cast<const float*>(nullptr), static_cast<float*>(dx), static_cast<float*>(nullptr), nvec, C);
@@ -1092,13 +1158,26 @@ int det_bn_bwd_apply_coef(void* stream, int dtype, const void* d, const void* x,
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 2);
   if (dtype == 1)
-    hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false>), dim3(grid2), dim3(kThreads), 0, st,
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false, true>), dim3(grid2), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(d), static_cast<const unsigned short*>(nullptr),
+                       static_cast<const unsigned short*>(x), static_cast<const uint8_t*>(nullptr), coef,
+                       static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
+                       static_cast<unsigned short*>(dx), static_cast<unsigned short*>(nullptr), nvec, C);
+    else
+      hipLaunchKernelGGL((bn_apply_bwd<unsigned short, 0, false>), dim3(grid2), dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(d), static_cast<const unsigned short*>(nullptr),
                        static_cast<const unsigned short*>(x), static_cast<const uint8_t*>(nullptr), coef,
                        static_cast<const float*>(nullptr), static_cast<const float*>(nullptr),
                        static_cast<unsigned short*>(dx), static_cast<unsigned short*>(nullptr), nvec, C);
   else
-    hipLaunchKernelGGL((bn_apply_bwd<float, 0, false>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
+    if (bn_nt())
+      hipLaunchKernelGGL((bn_apply_bwd<float, 0, false, true>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
+                       static_cast<const float*>(nullptr), static_cast<const float*>(x),
+                       static_cast<const uint8_t*>(nullptr), coef, static_cast<const float*>(nullptr),
+                       static_cast<const float*>(nullptr), static_cast<float*>(dx), static_cast<float*>(nullptr), nvec, C);
+    else
+      hipLaunchKernelGGL((bn_apply_bwd<float, 0, false>), dim3(grid2), dim3(kThreads), 0, st, static_cast<const float*>(d),
                        static_cast<const float*>(nullptr), static_cast<const float*>(x),
                        static_cast<const uint8_t*>(nullptr), coef, static_cast<const float*>(nullptr),
                        static_cast<const float*>(nullptr), static_cast<float*>(dx), static_cast<float*>(nullptr), nvec, C);
@@ -1142,10 +1221,18 @@ int det_bn_bwd(void* stream, int dtype, const void* dy, const void* dy2, const v
   const int64_t nvec = M * C / 8;
   const int grid2 = apply_grid(nvec, 2);
 #define DET_BN_B(T, MK, DR)                                                                            \
-  hipLaunchKernelGGL((bn_apply_bwd<T, MK, DR>), dim3(grid2), dim3(kThreads), 0, st,                     \
-                     static_cast<const T*>(dy), static_cast<const T*>(dy2), static_cast<const T*>(x),              \
-                     static_cast<const uint8_t*>(mbits), coef,                                                \
-                     scale, shift, static_cast<T*>(dx), static_cast<T*>(dres), nvec, C)
+  do {                                                                                                 \
+    if (bn_nt())                                                                                       \
+      hipLaunchKernelGGL((bn_apply_bwd<T, MK, DR, true>), dim3(grid2), dim3(kThreads), 0, st,          \
+                         static_cast<const T*>(dy), static_cast<const T*>(dy2), static_cast<const T*>(x), \
+                         static_cast<const uint8_t*>(mbits), coef, scale, shift, static_cast<T*>(dx),  \
+                         static_cast<T*>(dres), nvec, C);                                              \
+    else                                                                                               \
+      hipLaunchKernelGGL((bn_apply_bwd<T, MK, DR>), dim3(grid2), dim3(kThreads), 0, st,                \
+                         static_cast<const T*>(dy), static_cast<const T*>(dy2), static_cast<const T*>(x), \
+                         static_cast<const uint8_t*>(mbits), coef, scale, shift, static_cast<T*>(dx),  \
+                         static_cast<T*>(dres), nvec, C);                                              \
+  } while (0)
 #define DET_BN_B_MASK(T, DR)                 \
   if (mask_mode == 0) DET_BN_B(T, 0, DR);    \
   else if (mask_mode == 1) DET_BN_B(T, 1, DR); \

@@ -29,8 +29,10 @@ if [ $rc -eq 0 ]; then
     [ $rc -le 1 ] || { tail -30 $O/cifar_$amp.err; exit $rc; }
   done
 fi
-timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
-cat $O/bench.json
+for nt in 0 1 0 1; do  # BatchNorm apply passes with nontemporal activation reads (DET_BN_NT) A/B
+  DET_BN_NT=$nt timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $O/bench_nt$nt.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+  echo "bench DET_BN_NT=$nt $(cut -c1-160 $O/bench_nt$nt.json)"; cat $O/bench_nt$nt.json >> $O/bench_bn_nt_ab.jsonl
+done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 15 --warmup 5 \
   > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
 python3 scripts/prof_summarize.py $(find $O/prof -name "bench_kernel_trace.csv" | head -1) --out $O/steady.csv > $O/steady.txt
