@@ -25,6 +25,9 @@ def main() -> None:
     ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
     ap.add_argument("--impl", default="native", choices=["native", "hf"], help="fused MI355X encoder or HF BERT")
     ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
+    ap.add_argument("--loss-every", type=int, default=0,
+                    help="timed steps in workloads of this many batches, reporting each one's mean loss (long-run "
+                         "graph-vs-eager tracking)")
     ap.add_argument("--cprof", default="", help="write a cProfile of the timed steps to this path")
     ap.add_argument("--autograd-threads", type=int, default=0,
                     help="1: stock multithreaded autograd engine (the controller disables it by default)")
@@ -69,19 +72,36 @@ def main() -> None:
     if args.autograd_threads:
         os.environ["DET_AUTOGRAD_THREADS"] = "1"
 
+    losses = []
+
+    def keep_loss(r) -> None:
+        m = (r or {}).get("metrics", {}).get("avg_metrics", {}) if isinstance(r, dict) else {}
+        if "loss" in m:
+            losses.append(float(m["loss"]))
+
     def stream():
         yield workload.train_workload(1, num_batches=args.warmup), [], workload.ignore_response
         sync()
         if prof is not None:
             prof.enable()
         t["t0"] = time.perf_counter()
-        yield workload.train_workload(2, num_batches=args.steps, total_batches_processed=args.warmup), [], workload.ignore_response
+        if args.loss_every > 0:
+            done, step = 0, 2
+            while done < args.steps:
+                n = min(args.loss_every, args.steps - done)
+                yield (workload.train_workload(step, num_batches=n, total_batches_processed=args.warmup + done), [],
+                       keep_loss)
+                done += n
+                step += 1
+        else:
+            yield (workload.train_workload(2, num_batches=args.steps, total_batches_processed=args.warmup), [],
+                   workload.ignore_response)
         sync()
         t["t1"] = time.perf_counter()
         if prof is not None:
             prof.disable()
             prof.dump_stats(args.cprof)
-        yield workload.terminate_workload(3), [], workload.ignore_response
+        yield workload.terminate_workload(10 ** 6), [], workload.ignore_response
 
     ctrl = make_controller(BertSQuADTrial, cfg, stream(), trial_seed=7)
     ctrl.run()
@@ -98,7 +118,8 @@ def main() -> None:
                                      "amp": args.amp, "aggregation_frequency": args.agg,
                                      "optimizer": "AdamW (fused arena HIP kernel)", "impl": args.impl,
                                      "hip_graph": bool(args.hip_graph), "graph_stats": graph_stats,
-                                     "tf_fallbacks": tfops.FALLBACKS["count"]}}), flush=True)
+                                     "tf_fallbacks": tfops.FALLBACKS["count"]},
+                          "losses": [round(x, 5) for x in losses] if losses else None}), flush=True)
     pdist.shutdown()
 
 

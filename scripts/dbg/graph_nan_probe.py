@@ -100,11 +100,17 @@ def main():
            "records_per_epoch": 50000, "scheduling_unit": 250,
            "optimizations": {"hip_graph": not args.no_graph, "hip_graph_batches": args.graph_batches}}
 
+    step_losses = []
+
+    def keep(r):
+        m = r.get("metrics", {}).get("avg_metrics", {}) if isinstance(r, dict) else {}
+        step_losses.append(float(m.get("loss", float("nan"))))
+
     def stream():
         done, step = 0, 1
         while done < args.batches:
             n = min(250, args.batches - done)
-            yield workload.train_workload(step, num_batches=n, total_batches_processed=done), [], workload.ignore_response
+            yield workload.train_workload(step, num_batches=n, total_batches_processed=done), [], keep
             done += n
             step += 1
         yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
@@ -239,7 +245,9 @@ def main():
     res = {"variant": args.variant, "amp": args.amp, "seed": args.seed, "lr": args.lr,
            "graph_batches": args.graph_batches, "no_graph": args.no_graph, "batches_seen": state["batch"],
            "graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
-           "violation": state["violation"], "wall_s": round(time.time() - state["t0"], 1)}
+           "violation": state["violation"], "wall_s": round(time.time() - state["t0"], 1),
+           "step_losses": [round(x, 4) for x in step_losses],
+           "final_masters_finite": all(bool(torch.isfinite(a.master).all()) for f in fused() for a in f.arenas)}
     tag = (f"{args.variant}_{args.amp}_g{0 if args.no_graph else args.graph_batches}_s{args.seed}"
            f"_c{args.check_every}{'_r4' if args.r4_model else ''}_{args.loss}")
     with open(os.path.join(args.out, f"{tag}.log.jsonl"), "w") as fh:
