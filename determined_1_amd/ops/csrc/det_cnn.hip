@@ -83,101 +83,230 @@ struct Operand {
   int transpose;     // the operand is read as A[m][k] = T[k][m] (wgrad's gradient operand)
 };
 
-__device__ __forceinline__ float opval(const Operand& o, int64_t row, int64_t kk) {
-  // row: the GEMM row this operand element belongs to (A: m; B: n); kk: the reduction index.
-  // Returns the operand value A[row][kk] (or B[kk][row]).
-  switch (o.src) {
-    case S_ACT_CONV: {
-      // row = pixel index over (n, OH, OW) [window ordered if pool]; kk = (r*S+s)*C + c
-      int64_t pix = row;
-      int n, oh, ow;
-      if (o.pool) {
-        const int q = static_cast<int>(pix & 3);
-        int64_t win = pix >> 2;
-        const int PW = o.OW >> 1, PH = o.OH >> 1;
-        const int pw = static_cast<int>(win % PW);
-        win /= PW;
-        const int ph = static_cast<int>(win % PH);
-        n = static_cast<int>(win / PH);
-        oh = 2 * ph + (q >> 1);
-        ow = 2 * pw + (q & 1);
-      } else {
-        ow = static_cast<int>(pix % o.OW);
-        pix /= o.OW;
-        oh = static_cast<int>(pix % o.OH);
-        n = static_cast<int>(pix / o.OH);
-      }
-      const int c = static_cast<int>(kk % o.C);
-      const int rs = static_cast<int>(kk / o.C);
-      const int r = rs / o.S, s = rs - r * o.S;
-      const int h = oh + r - o.pad, w = ow + s - o.pad;
-      if (h < 0 || h >= o.H || w < 0 || w >= o.W) return 0.f;
-      return ld(o.p, o.dt, ((static_cast<int64_t>(n) * o.H + h) * o.W + w) * o.C + c);
-    }
-    case S_ACT_FLAT: {
-      const int64_t n = row;
-      const int hw = o.H * o.W;
-      const int c = static_cast<int>(kk / hw);
-      const int rem = static_cast<int>(kk - static_cast<int64_t>(c) * hw);
-      return ld(o.p, o.dt, (n * hw + rem) * o.C + c);
-    }
-    case S_ACT_ROWS:
-    case S_GRAD_ROWS:
-      return ld(o.p, o.dt == 2 ? 0 : o.dt, row * o.C + kk);
-    case S_GRAD_CONV_T: {
-      // input pixel `row` over (n, OH, OW) = the dgrad output grid; kk = (r*S+s)*C + og
-      int64_t pix = row;
-      const int iw = static_cast<int>(pix % o.OW);
-      pix /= o.OW;
-      const int ih = static_cast<int>(pix % o.OH);
-      const int n = static_cast<int>(pix / o.OH);
-      const int og = static_cast<int>(kk % o.C);
-      const int rs = static_cast<int>(kk / o.C);
-      const int r = rs / o.S, s = rs - r * o.S;
-      const int h = ih + o.pad - r, w = iw + o.pad - s;  // output-gradient position
-      if (h < 0 || h >= o.H || w < 0 || w >= o.W) return 0.f;
-      if (o.idx != nullptr) {  // unpool: gradient of the pre-pool grid (H, W) from the pooled one
-        const int PH = o.H >> 1, PW = o.W >> 1;
-        const int64_t pe = ((static_cast<int64_t>(n) * PH + (h >> 1)) * PW + (w >> 1)) * o.C + og;
-        return o.idx[pe] == ((h & 1) << 1 | (w & 1)) ? ld(o.p, o.dt, pe) : 0.f;
-      }
-      return ld(o.p, o.dt, ((static_cast<int64_t>(n) * o.H + h) * o.W + w) * o.C + og);
-    }
-    case S_WGT_CONV: {
-      const int c = static_cast<int>(kk % o.C);
-      const int rs = static_cast<int>(kk / o.C);
-      const int r = rs / o.S, s = rs - r * o.S;
-      return ld(o.p, o.dt, row * o.so + c * o.sc + r * o.sr + s * o.ss);
-    }
-    case S_WGT_CONV_T: {
-      // B[kk = (r*S+s)*Cout + o][n = c]: the flipped-weight dgrad operand
-      const int og = static_cast<int>(kk % o.C);  // o.C = Cout here
-      const int rs = static_cast<int>(kk / o.C);
-      const int r = rs / o.S, s = rs - r * o.S;
-      return ld(o.p, o.dt, og * o.so + row * o.sc + r * o.sr + s * o.ss);
-    }
-    case S_WGT_FC:
-      return ld(o.p, o.dt, row * o.so + kk * o.sc);
-    case S_WGT_FC_T:
-      return ld(o.p, o.dt, kk * o.so + row * o.sc);
+// All index math is 32-bit unsigned (every tensor here has < 2^31 elements; 64-bit divisions are a
+// long software sequence per element): the decomposition of the thread's fixed row is done once per
+// 8-element group, and 8 consecutive reduction indices that share one kernel tap (C % 8 == 0) are
+// one 16-B (bf16) / 32-B (fp32) vector load.
+
+// 8 consecutive elements at p[e .. e+7] (contiguous), converted to fp32
+__device__ __forceinline__ void ld8(const void* p, int dt, uint32_t e, float (&v)[8]) {
+  if (dt == 1) {
+    typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+    const u16x8 r = *reinterpret_cast<const u16x8*>(static_cast<const uint16_t*>(p) + e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(r[j]);
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + e);
+    const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + e + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   }
-  return 0.f;
+}
+__device__ __forceinline__ float ld32(const void* p, int dt, uint32_t e) {
+  return dt == 0 ? static_cast<const float*>(p)[e] : bf2f(static_cast<const uint16_t*>(p)[e]);
+}
+__device__ __forceinline__ int odt(const Operand& o) { return o.dt == 2 ? 0 : o.dt; }
+
+// pixel index -> (n, h, w) over an OH x OW grid (window-ordered 2x2 groups if pool)
+__device__ __forceinline__ void pix_nhw(const Operand& o, uint32_t pix, uint32_t& n, int& h, int& w) {
+  if (o.pool) {
+    const uint32_t q = pix & 3u, win = pix >> 2;
+    const uint32_t PW = static_cast<uint32_t>(o.OW) >> 1, PH = static_cast<uint32_t>(o.OH) >> 1;
+    const uint32_t t = win / PW, pw = win - t * PW;
+    n = t / PH;
+    const uint32_t ph = t - n * PH;
+    h = static_cast<int>(2 * ph + (q >> 1));
+    w = static_cast<int>(2 * pw + (q & 1u));
+  } else {
+    const uint32_t t = pix / static_cast<uint32_t>(o.OW);
+    w = static_cast<int>(pix - t * static_cast<uint32_t>(o.OW));
+    n = t / static_cast<uint32_t>(o.OH);
+    h = static_cast<int>(t - n * static_cast<uint32_t>(o.OH));
+  }
 }
 
-// gradient operand of a weight gradient: A[m = out channel][k = pixel] = g[pixel][m], with the
-// unpool routing for pooled layers (pixel over the pre-pool grid OH x OW, row-major)
-__device__ __forceinline__ float gradval(const Operand& o, int64_t m, int64_t pix) {
-  if (o.src == S_GRAD_ROWS) return ld(o.p, o.dt == 2 ? 0 : o.dt, pix * o.C + m);
-  if (o.idx != nullptr) {
-    int64_t p = pix;
-    const int w = static_cast<int>(p % o.OW);
-    p /= o.OW;
-    const int h = static_cast<int>(p % o.OH);
-    const int n = static_cast<int>(p / o.OH);
-    const int64_t pe = ((static_cast<int64_t>(n) * (o.OH >> 1) + (h >> 1)) * (o.OW >> 1) + (w >> 1)) * o.C + m;
-    return o.idx[pe] == ((h & 1) << 1 | (w & 1)) ? ld(o.p, o.dt, pe) : 0.f;
+// the unpooled gradient at pre-pool position (n, h, w, c): the pooled gradient routed to the argmax
+__device__ __forceinline__ float unpool_at(const Operand& o, uint32_t n, int h, int w, uint32_t c) {
+  const uint32_t PH = static_cast<uint32_t>(o.H) >> 1, PW = static_cast<uint32_t>(o.W) >> 1;
+  const uint32_t pe = ((n * PH + static_cast<uint32_t>(h >> 1)) * PW + static_cast<uint32_t>(w >> 1)) *
+                      static_cast<uint32_t>(o.C) + c;
+  return o.idx[pe] == static_cast<uint8_t>((h & 1) << 1 | (w & 1)) ? ld32(o.p, o.dt, pe) : 0.f;
+}
+
+// A[row][kk0 .. kk0+7] (or B[kk0 .. kk0+7][row]) for a fixed GEMM row; nk <= 8 of them are in range
+__device__ __forceinline__ void opval8(const Operand& o, uint32_t row, uint32_t kk0, int nk, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  const int dt = odt(o);
+  switch (o.src) {
+    case S_ACT_CONV: {
+      uint32_t n;
+      int oh, ow;
+      pix_nhw(o, row, n, oh, ow);
+      const uint32_t C = static_cast<uint32_t>(o.C);
+      if ((C & 7u) == 0 && nk == 8) {  // one tap, 8 consecutive channels: one vector load
+        const uint32_t rs = kk0 / C, c0 = kk0 - rs * C;
+        const int r = static_cast<int>(rs / static_cast<uint32_t>(o.S)), s = static_cast<int>(rs) - r * o.S;
+        const int h = oh + r - o.pad, w = ow + s - o.pad;
+        if (h >= 0 && h < o.H && w >= 0 && w < o.W)
+          ld8(o.p, dt, ((n * static_cast<uint32_t>(o.H) + h) * static_cast<uint32_t>(o.W) + w) * C + c0, v);
+        return;
+      }
+      for (int j = 0; j < nk; ++j) {
+        const uint32_t kk = kk0 + j, rs = kk / C, c = kk - rs * C;
+        const int r = static_cast<int>(rs / static_cast<uint32_t>(o.S)), s = static_cast<int>(rs) - r * o.S;
+        const int h = oh + r - o.pad, w = ow + s - o.pad;
+        if (h >= 0 && h < o.H && w >= 0 && w < o.W)
+          v[j] = ld32(o.p, dt, ((n * static_cast<uint32_t>(o.H) + h) * static_cast<uint32_t>(o.W) + w) * C + c);
+      }
+      return;
+    }
+    case S_ACT_FLAT: {  // torch's NCHW flatten order over an NHWC tensor
+      const uint32_t hw = static_cast<uint32_t>(o.H * o.W), C = static_cast<uint32_t>(o.C);
+      for (int j = 0; j < nk; ++j) {
+        const uint32_t kk = kk0 + j, c = kk / hw;
+        v[j] = ld32(o.p, dt, (row * hw + (kk - c * hw)) * C + c);
+      }
+      return;
+    }
+    case S_ACT_ROWS:
+    case S_GRAD_ROWS: {
+      const uint32_t e = row * static_cast<uint32_t>(o.C) + kk0;
+      if (nk == 8 && (o.C & 7) == 0) {
+        ld8(o.p, dt, e, v);
+        return;
+      }
+      for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, e + j);
+      return;
+    }
+    case S_GRAD_CONV_T: {  // input pixel `row` of the dgrad grid; kk = (r*S+s)*C + og
+      uint32_t n;
+      int ih, iw;
+      pix_nhw(o, row, n, ih, iw);
+      const uint32_t C = static_cast<uint32_t>(o.C);
+      const bool vec = (C & 7u) == 0 && nk == 8;
+      for (int j = 0; j < (vec ? 1 : nk); ++j) {
+        const uint32_t kk = kk0 + j, rs = kk / C, og = kk - rs * C;
+        const int r = static_cast<int>(rs / static_cast<uint32_t>(o.S)), s = static_cast<int>(rs) - r * o.S;
+        const int h = ih + o.pad - r, w = iw + o.pad - s;  // output-gradient position
+        if (h < 0 || h >= o.H || w < 0 || w >= o.W) continue;
+        if (o.idx != nullptr) {
+          if (vec) {
+            for (int q = 0; q < 8; ++q) v[q] = unpool_at(o, n, h, w, og + q);
+          } else {
+            v[j] = unpool_at(o, n, h, w, og);
+          }
+        } else {
+          const uint32_t e = ((n * static_cast<uint32_t>(o.H) + h) * static_cast<uint32_t>(o.W) + w) * C + og;
+          if (vec) ld8(o.p, dt, e, v);
+          else v[j] = ld32(o.p, dt, e);
+        }
+      }
+      return;
+    }
+    case S_WGT_CONV: {  // B[kk = (r*S+s)*C + c][n = o] = W[o][c][r][s]
+      const uint32_t C = static_cast<uint32_t>(o.C);
+      if ((C & 7u) == 0 && nk == 8 && o.sc == 1) {
+        const uint32_t rs = kk0 / C, c0 = kk0 - rs * C;
+        const uint32_t r = rs / static_cast<uint32_t>(o.S), s = rs - r * static_cast<uint32_t>(o.S);
+        ld8(o.p, dt, static_cast<uint32_t>(row * o.so + c0 + r * o.sr + s * o.ss), v);
+        return;
+      }
+      for (int j = 0; j < nk; ++j) {
+        const uint32_t kk = kk0 + j, rs = kk / C, c = kk - rs * C;
+        const uint32_t r = rs / static_cast<uint32_t>(o.S), s = rs - r * static_cast<uint32_t>(o.S);
+        v[j] = ld32(o.p, dt, static_cast<uint32_t>(row * o.so + c * o.sc + r * o.sr + s * o.ss));
+      }
+      return;
+    }
+    case S_WGT_CONV_T: {  // B[kk = (r*S+s)*Cout + og][n = c] = W[og][c][r][s]
+      const uint32_t C = static_cast<uint32_t>(o.C);
+      for (int j = 0; j < nk; ++j) {
+        const uint32_t kk = kk0 + j, rs = kk / C, og = kk - rs * C;
+        const uint32_t r = rs / static_cast<uint32_t>(o.S), s = rs - r * static_cast<uint32_t>(o.S);
+        v[j] = ld32(o.p, dt, static_cast<uint32_t>(og * o.so + row * o.sc + r * o.sr + s * o.ss));
+      }
+      return;
+    }
+    case S_WGT_FC: {  // B[k = j][n = o] = W[o][j]
+      const uint32_t e = static_cast<uint32_t>(row * o.so + kk0 * o.sc);
+      if (nk == 8 && o.sc == 1 && (o.so & 7) == 0) {
+        ld8(o.p, dt, e, v);
+        return;
+      }
+      for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, static_cast<uint32_t>(e + j * o.sc));
+      return;
+    }
+    case S_WGT_FC_T:  // B[k = o][n = j] = W[o][j]
+      for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, static_cast<uint32_t>((kk0 + j) * o.so + row * o.sc));
+      return;
   }
-  return ld(o.p, o.dt, pix * o.C + m);
+}
+
+// weight-gradient operands, 8 consecutive reduction indices (pixels / images) k0 .. k0+7:
+//   A[m = out channel][k] = g[k][m] (with the unpool routing of a pooled layer)
+__device__ __forceinline__ void gradval8(const Operand& o, uint32_t m, uint32_t k0, int nk, float (&v)[8]) {
+  const int dt = odt(o);
+  const uint32_t C = static_cast<uint32_t>(o.C);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  if (o.src == S_GRAD_ROWS || o.idx == nullptr) {
+    for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, (k0 + j) * C + m);
+    return;
+  }
+  uint32_t n;
+  int h, w;
+  Operand g = o;
+  g.pool = 0;
+  g.H = o.OH;  // unpool_at reads the pooled grid of the OH x OW pre-pool grid
+  g.W = o.OW;
+  pix_nhw(g, k0, n, h, w);
+  for (int j = 0; j < nk; ++j) {
+    v[j] = unpool_at(g, n, h, w, m);
+    if (++w == o.OW) {  // next pixel, row-major
+      w = 0;
+      if (++h == o.OH) {
+        h = 0;
+        ++n;
+      }
+    }
+  }
+}
+//   B[k][n = weight column] = the activation of pixel / image k at column n (conv: kk = n)
+__device__ __forceinline__ void actcol8(const Operand& o, uint32_t k0, uint32_t col, int nk, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  const int dt = odt(o);
+  if (o.src == S_ACT_ROWS) {
+    for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, (k0 + j) * static_cast<uint32_t>(o.C) + col);
+    return;
+  }
+  if (o.src == S_ACT_FLAT) {
+    const uint32_t hw = static_cast<uint32_t>(o.H * o.W), C = static_cast<uint32_t>(o.C);
+    const uint32_t c = col / hw, rem = col - c * hw;
+    for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, ((k0 + j) * hw + rem) * C + c);
+    return;
+  }
+  // S_ACT_CONV: the tap / channel of column `col` is fixed, the pixel advances
+  const uint32_t C = static_cast<uint32_t>(o.C);
+  const uint32_t rs = col / C, c = col - rs * C;
+  const int r = static_cast<int>(rs / static_cast<uint32_t>(o.S)), s = static_cast<int>(rs) - r * o.S;
+  uint32_t n;
+  int oh, ow;
+  Operand g = o;
+  g.pool = 0;
+  pix_nhw(g, k0, n, oh, ow);
+  for (int j = 0; j < nk; ++j) {
+    const int h = oh + r - o.pad, w = ow + s - o.pad;
+    if (h >= 0 && h < o.H && w >= 0 && w < o.W)
+      v[j] = ld32(o.p, dt, ((n * static_cast<uint32_t>(o.H) + h) * static_cast<uint32_t>(o.W) + w) * C + c);
+    if (++ow == o.OW) {
+      ow = 0;
+      if (++oh == o.OH) {
+        oh = 0;
+        ++n;
+      }
+    }
+  }
 }
 
 // ---- epilogues ---------------------------------------------------------------------------------
@@ -332,17 +461,27 @@ __global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
   float ra[8], rb[8];
   auto gather = [&](int64_t k0) {
     const int64_t m = m0 + lr, n = n0 + lr;
+    const int64_t kg = k0 + lk;  // first of this lane's 8 reduction indices
+    const int nk = kg >= k_hi ? 0 : (k_hi - kg < 8 ? static_cast<int>(k_hi - kg) : 8);
+    if (m < J.M && nk > 0) {
+      if (wgrad) gradval8(J.a, static_cast<uint32_t>(m), static_cast<uint32_t>(kg), nk, ra);
+      else opval8(J.a, static_cast<uint32_t>(m), static_cast<uint32_t>(kg), nk, ra);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t k = k0 + lk + i;
-      const bool kin = k < k_hi;
-      ra[i] = (m < J.M && kin) ? (wgrad ? gradval(J.a, m, k) : opval(J.a, m, k)) : 0.f;
-      float v = 0.f;
-      if (n < J.N && kin) {
-        if (wgrad) v = (bias_col && n == J.N - 1) ? 1.f : opval(J.b, k, n);
-        else v = opval(J.b, n, k);
+      for (int i = 0; i < 8; ++i) ra[i] = 0.f;
+    }
+    if (n < J.N && nk > 0) {
+      if (!wgrad) {
+        opval8(J.b, static_cast<uint32_t>(n), static_cast<uint32_t>(kg), nk, rb);
+      } else if (bias_col && n == J.N - 1) {  // weight gradient: the last column is the bias's
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rb[i] = i < nk ? 1.f : 0.f;
+      } else {
+        actcol8(J.b, static_cast<uint32_t>(kg), static_cast<uint32_t>(n), nk, rb);
       }
-      rb[i] = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rb[i] = 0.f;
     }
   };
   auto stash = [&](int b) {

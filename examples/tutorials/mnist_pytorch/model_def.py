@@ -19,11 +19,12 @@ class MNistTrial(pytorch.PyTorchTrial):
         self.opt = context.wrap_optimizer(torch.optim.Adadelta(self.model.parameters(), lr=hp.get("learning_rate", 1.0)))
 
     def build_training_data_loader(self) -> pytorch.DataLoader:
-        ds = SyntheticClassification(60000, (1, 28, 28), noise=2.0)
+        ds = SyntheticClassification(int(self.context.get_hparams().get("train_records", 60000)), (1, 28, 28), noise=2.0)
         return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size(), shuffle=True)
 
     def build_validation_data_loader(self) -> pytorch.DataLoader:
-        ds = SyntheticClassification(10000, (1, 28, 28), noise=2.0, seed=1)
+        ds = SyntheticClassification(int(self.context.get_hparams().get("validation_records", 10000)), (1, 28, 28),
+                                    noise=2.0, seed=1)
         return pytorch.DataLoader(ds, batch_size=self.context.get_per_slot_batch_size())
 
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:

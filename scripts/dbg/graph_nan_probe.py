@@ -38,6 +38,10 @@ def patch_dropout(model, variant):
     import torch.nn as nn
 
     mods = [m for m in model.modules() if isinstance(m, nn.modules.dropout._DropoutNd) and m.p > 0]
+    if variant == "none":
+        for m in mods:
+            m.p = 0.0
+        return mods
     if variant == "torch":
         return mods
 
@@ -65,7 +69,9 @@ def patch_dropout(model, variant):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", default="torch", choices=("torch", "randmask", "bankmask"))
+    ap.add_argument("--variant", default="torch", choices=("torch", "randmask", "bankmask", "none"))
+    ap.add_argument("--separate-pools", action="store_true", help="each chunk graph captures into its own memory pool")
+    ap.add_argument("--native", action="store_true", help="the native CNN kernels instead of torch layers")
     ap.add_argument("--amp", default="O2")
     ap.add_argument("--batches", type=int, default=2000)
     ap.add_argument("--graph-batches", type=int, default=1)
@@ -115,7 +121,8 @@ def main():
             step += 1
         yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
 
-    os.environ["DET_NATIVE_CNN"] = "0"  # the torch layers: this probe is about torch dropout under replays
+    # the torch layers by default: this probe is about torch dropout under replays
+    os.environ["DET_NATIVE_CNN"] = "1" if args.native else "0"
     ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=True, trial_seed=args.seed)
     trial = ctrl.trial
     if args.loss != "native":
@@ -222,6 +229,48 @@ def main():
                     state["violation"] = {"batch": state["batch"], "what": v, "tag": "eager"}
         return out
 
+    orig_chunk = _graph.TrainStepGraph.run_chunk
+    orig_cap_chunk = _graph.TrainStepGraph._capture_chunk
+    state["chunks"] = 0
+
+    def run_chunk(self, chunk, epoch_idx, batch_idx, capture=True):
+        out = orig_chunk(self, chunk, epoch_idx, batch_idx, capture)
+        if out is None:
+            return out
+        state["chunks"] += 1
+        state["batch"] += len(chunk)
+        if state["violation"] is None and state["chunks"] % max(1, args.check_every // 20) == 0:
+            torch.cuda.synchronize()
+            losses = out["loss"].float()
+            v = []
+            if not torch.isfinite(losses).all():
+                first = int((~torch.isfinite(losses)).nonzero()[0])
+                v.append(f"chunk loss non-finite from step {first} of {len(chunk)}")
+            for f in fused():
+                for a in f.arenas:
+                    if not torch.isfinite(a.master).all():
+                        v.append("master non-finite")
+            if state["chunks"] % 5 == 0 or v:
+                state["log"].append({"batch": state["batch"], "tag": "chunk", "loss": float(losses.mean()),
+                                     "chunk_losses": [round(float(x), 4) for x in losses],
+                                     "max_abs_master": max(float(a.master.abs().max()) for f in fused() for a in f.arenas)})
+            if v:
+                state["violation"] = {"batch": state["batch"], "what": v, "tag": "chunk", "epoch_idx": epoch_idx,
+                                      "batch_idx": batch_idx, "chunk_losses": [float(x) for x in losses]}
+        return out
+
+    def capture_chunk(self, *a, **kw):
+        if not args.separate_pools:
+            return orig_cap_chunk(self, *a, **kw)
+        keep = self.pool
+        self.pool = torch.cuda.graph_pool_handle()
+        try:
+            return orig_cap_chunk(self, *a, **kw)
+        finally:
+            self.pool = keep
+
+    _graph.TrainStepGraph.run_chunk = run_chunk
+    _graph.TrainStepGraph._capture_chunk = capture_chunk
     _graph.TrainStepGraph._replay = replay
     _graph.TrainStepGraph._eager = eager
     if args.no_graph:
@@ -247,9 +296,10 @@ def main():
            "graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
            "violation": state["violation"], "wall_s": round(time.time() - state["t0"], 1),
            "step_losses": [round(x, 4) for x in step_losses],
-           "final_masters_finite": all(bool(torch.isfinite(a.master).all()) for f in fused() for a in f.arenas)}
+           "chunks_checked": state.get("chunks"), "final_masters_finite": all(bool(torch.isfinite(a.master).all()) for f in fused() for a in f.arenas)}
     tag = (f"{args.variant}_{args.amp}_g{0 if args.no_graph else args.graph_batches}_s{args.seed}"
-           f"_c{args.check_every}{'_r4' if args.r4_model else ''}_{args.loss}")
+           f"_c{args.check_every}{'_r4' if args.r4_model else ''}_{args.loss}{'_sep' if args.separate_pools else ''}"
+           f"{'_native' if args.native else ''}")
     with open(os.path.join(args.out, f"{tag}.log.jsonl"), "w") as fh:
         for r in state["log"]:
             fh.write(json.dumps(r) + "\n")

@@ -17,7 +17,7 @@ REPO = pathlib.Path(__file__).resolve().parent.parent
 def test_bench_asha_eight_artificial_slots(tmp_path):
     env = dict(os.environ, DET_BENCH_LOGDIR=str(tmp_path), MASTER_ADDR="127.0.0.1")
     p = subprocess.run([sys.executable, str(REPO / "scripts" / "bench_asha.py"), "--artificial-slots", "8",
-                        "--max-length-batches", "40", "--max-trials", "16", "--amp", "O0", "--validation-records", "640", "--timeout", "600"],
+                        "--max-length-batches", "16", "--max-trials", "16", "--amp", "O0", "--validation-records", "128", "--timeout", "600"],
                        capture_output=True, text=True, timeout=800, env=env, cwd=str(REPO))
     assert p.returncode == 0, p.stderr[-3000:]
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])

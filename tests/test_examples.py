@@ -36,7 +36,7 @@ SHRINK = {
     "eval": {"num_classes": 10, "image_size": 32, "init_channels": 8, "layers": 3, "global_batch_size": 2,
              "train_records": 8, "validation_records": 4},  # nas/gaea_pytorch/eval
     "cifar10_pytorch": {"amp": "O0", "global_batch_size": 4, "validation_records": 64},  # not the 10k test split
-    "mnist_pytorch": {"global_batch_size": 4},
+    "mnist_pytorch": {"global_batch_size": 4, "validation_records": 64},  # not the 10k test split
     "fasterrcnn_coco_pytorch": {"backbone": "resnet26", "num_images": 10, "min_image_size": 60, "max_image_size": 90,
                                 "transform_min_size": 96, "transform_max_size": 160},
     "detr_coco_pytorch": {"backbone": "resnet26", "enc_layers": 1, "dec_layers": 2, "hidden_dim": 32, "nheads": 2,
