@@ -15,6 +15,7 @@ per parameter); elsewhere they are produced into ``arena.landing_buffer`` slots 
 returned to autograd.  CPU tensors and unsupported shapes use the torch module (``supported``).
 """
 import ctypes
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -28,7 +29,10 @@ c_void_p, c_i32, c_i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
 S_ACT_CONV, S_ACT_FLAT, S_ACT_ROWS, S_GRAD_ROWS, S_GRAD_CONV_T, S_WGT_CONV, S_WGT_CONV_T, S_WGT_FC, S_WGT_FC_T = range(9)
 (E_BIAS_RELU, E_BIAS_RELU_POOL, E_BIAS_RELU_DROP, E_BIAS, E_MASK_POS, E_DROP_POS, E_DROP_POS_FLAT, E_GRAD_FC,
  E_GRAD_CONV) = range(9)
-BLOCKS_TARGET = 320  # split-K sizing: at least this many workgroups per launch where K allows
+# split-K sizing: at least this many workgroups per launch where K allows.  Every pass here is
+# latency-bound (each K tile of a block costs a global round trip, ~2.4 us measured), so the K loop
+# is cut short and spread over more blocks; the finish launch that sums the slabs costs ~5 us.
+BLOCKS_TARGET = int(os.environ.get("DET_CNN_BLOCKS", "1024"))
 DEBUG = {"keep_masks": False, "masks": None}  # tests: the dropout factors of the last forward
 
 
@@ -109,7 +113,7 @@ class _Runner:
         self.keep = []  # type: List[torch.Tensor]
 
     def prepare(self, job: Job, split: bool = True) -> Job:
-        if split and job.epi != E_BIAS_RELU_POOL:
+        if split:
             s = _splits(self.lib, int(job.K), _tiles(int(job.M), int(job.N)))
         else:
             s = 1
@@ -171,26 +175,27 @@ def _forward(x: torch.Tensor, params: Sequence[torch.Tensor], ps, training: bool
     R.gemm(R.prepare(Job(a=_conv_act(xh, dt, 32, 3, 0, 30), b=_wgt(w1, dt, S_WGT_CONV, 3), M=n * 900, N=32, K=27,
                          epi=E_BIAS_RELU, out=a1.data_ptr(), out_dt=dt, bias=b1.data_ptr(), bias_dt=dt), split=False))
     # conv2 32->32 + bias + relu + maxpool + dropout2d (window-ordered rows)
-    R.gemm(R.prepare(Job(a=_conv_act(a1, dt, 30, 32, 0, 28, pool=1), b=_wgt(w2, dt, S_WGT_CONV, 32), M=n * 784, N=32,
-                         K=288, epi=E_BIAS_RELU_POOL, out=a2.data_ptr(), out_dt=dt, bias=b2.data_ptr(), bias_dt=dt,
-                         drop=_p(m2), drop_cols=32, idx=idx2.data_ptr(), PH=14, PW=14), split=False))
+    R.finish(R.gemm(R.prepare(Job(a=_conv_act(a1, dt, 30, 32, 0, 28, pool=1), b=_wgt(w2, dt, S_WGT_CONV, 32), M=n * 784,
+                                  N=32, K=288, epi=E_BIAS_RELU_POOL, out=a2.data_ptr(), out_dt=dt, bias=b2.data_ptr(),
+                                  bias_dt=dt, drop=_p(m2), drop_cols=32, idx=idx2.data_ptr(), PH=14, PW=14))))
     # conv3 32->64 pad 1 + bias + relu
-    R.gemm(R.prepare(Job(a=_conv_act(a2, dt, 14, 32, 1, 14), b=_wgt(w3, dt, S_WGT_CONV, 32), M=n * 196, N=64, K=288,
-                         epi=E_BIAS_RELU, out=a3.data_ptr(), out_dt=dt, bias=b3.data_ptr(), bias_dt=dt), split=False))
+    R.finish(R.gemm(R.prepare(Job(a=_conv_act(a2, dt, 14, 32, 1, 14), b=_wgt(w3, dt, S_WGT_CONV, 32), M=n * 196, N=64,
+                                  K=288, epi=E_BIAS_RELU, out=a3.data_ptr(), out_dt=dt, bias=b3.data_ptr(), bias_dt=dt))))
     # conv4 64->64 + bias + relu + maxpool + dropout2d
-    R.gemm(R.prepare(Job(a=_conv_act(a3, dt, 14, 64, 0, 12, pool=1), b=_wgt(w4, dt, S_WGT_CONV, 64), M=n * 144, N=64,
-                         K=576, epi=E_BIAS_RELU_POOL, out=a4.data_ptr(), out_dt=dt, bias=b4.data_ptr(), bias_dt=dt,
-                         drop=_p(m4), drop_cols=64, idx=idx4.data_ptr(), PH=6, PW=6), split=False))
+    R.finish(R.gemm(R.prepare(Job(a=_conv_act(a3, dt, 14, 64, 0, 12, pool=1), b=_wgt(w4, dt, S_WGT_CONV, 64), M=n * 144,
+                                  N=64, K=576, epi=E_BIAS_RELU_POOL, out=a4.data_ptr(), out_dt=dt, bias=b4.data_ptr(),
+                                  bias_dt=dt, drop=_p(m4), drop_cols=64, idx=idx4.data_ptr(), PH=6, PW=6))))
     # fc1 2304->512 (torch's NCHW flatten order) + bias + relu + dropout: split-K, finished by a launch
     fin = R.gemm(R.prepare(Job(a=Operand(p=a4.data_ptr(), dt=dt, src=S_ACT_FLAT, H=6, W=6, C=64),
                                b=_wgt(w5, dt, S_WGT_FC, 2304), M=n, N=512, K=2304, epi=E_BIAS_RELU_DROP,
                                out=a5.data_ptr(), out_dt=dt, bias=b5.data_ptr(), bias_dt=dt, drop=_p(m5),
                                drop_cols=512)))
     R.finish(fin)
-    # fc2 512->10 + bias -> fp32 logits
-    R.gemm(R.prepare(Job(a=Operand(p=a5.data_ptr(), dt=dt, src=S_ACT_ROWS, C=512), b=_wgt(w6, dt, S_WGT_FC, 512),
+    # fc2 512->10 + bias -> fp32 logits (split-K: one block would walk K serially)
+    fin = R.gemm(R.prepare(Job(a=Operand(p=a5.data_ptr(), dt=dt, src=S_ACT_ROWS, C=512), b=_wgt(w6, dt, S_WGT_FC, 512),
                          M=n, N=10, K=512, epi=E_BIAS, out=logits.data_ptr(), out_dt=dt, bias=b6.data_ptr(),
-                         bias_dt=dt), split=False))
+                         bias_dt=dt)))
+    R.finish(fin)
     saved = (xh, a1, a2, a3, a4, a5, idx2, idx4, m2, m4, m5)
     return logits, saved
 
@@ -229,9 +234,9 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
     kw = dict(dtype=xh.dtype, device=xh.device)
     dl = dlogits.contiguous().float()
     dz5 = torch.empty(n, 512, **kw)
-    dp4 = torch.empty(n, 6, 6, 64, **kw)
+    g4 = torch.empty(n, 12, 12, 64, **kw)  # conv4's output gradient: dp4 routed through the max-pool
     dy3 = torch.empty(n, 14, 14, 64, **kw)
-    dp2 = torch.empty(n, 14, 14, 32, **kw)
+    g2 = torch.empty(n, 28, 28, 32, **kw)  # conv2's output gradient (unpooled dp2)
     dy1 = torch.empty(n, 30, 30, 32, **kw)
 
     def gfc(i: int, K: int) -> dict:
@@ -259,33 +264,34 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
          R.prepare(Job(a=Operand(p=dl.data_ptr(), dt=0, src=S_GRAD_ROWS, C=10), b=_wgt(w6, dt, S_WGT_FC_T, 0),
                        M=n, N=512, K=10, epi=E_DROP_POS, out=dz5.data_ptr(), out_dt=dt, act=a5.data_ptr(),
                        drop=_p(m5), drop_cols=512, HW=1)))
-    # fc1: weight grad || input grad -> dp4 (NHWC) = d(a4) * drop2d * (a4 > 0)
+    # fc1: weight grad || input grad -> d(a4) * drop2d * (a4 > 0), written unpooled (the argmax of each
+    # 2x2 window, zeros elsewhere) as conv4's output gradient g4
     step(R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512, transpose=1),
                        b=Operand(p=a4.data_ptr(), dt=dt, src=S_ACT_FLAT, H=6, W=6, C=64), M=512, N=2305, K=n,
                        **gfc(8, n))),
          R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512), b=_wgt(w5, dt, S_WGT_FC_T, 0),
-                       M=n, N=2304, K=512, epi=E_DROP_POS_FLAT, out=dp4.data_ptr(), out_dt=dt,
-                       act=a4.data_ptr(), drop=_p(m4), drop_cols=64, HW=36, C=64)))
-    # conv4: weight grad over the unpooled gradient || input grad -> dy3 = d(a3) * (a3 > 0)
-    unpool4 = Operand(p=dp4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=12, W=12, C=64, R=3, S=3, pad=0, OH=12, OW=12,
-                      idx=idx4.data_ptr(), transpose=1)
-    step(R.prepare(Job(a=unpool4, b=_conv_act(a3, dt, 14, 64, 0, 12), M=64, N=577, K=n * 144, **gconv(6, 64))),
-         R.prepare(Job(a=Operand(p=dp4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=12, W=12, C=64, R=3, S=3, pad=0,
-                                 OH=14, OW=14, idx=idx4.data_ptr()),
+                       M=n, N=2304, K=512, epi=E_DROP_POS_FLAT, out=g4.data_ptr(), out_dt=dt,
+                       act=a4.data_ptr(), drop=_p(m4), drop_cols=64, HW=36, C=64, idx=idx4.data_ptr(), PH=6, PW=6)))
+    # conv4: weight grad || input grad -> dy3 = d(a3) * (a3 > 0)
+    step(R.prepare(Job(a=Operand(p=g4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=64, OH=12, OW=12, transpose=1),
+                       b=_conv_act(a3, dt, 14, 64, 0, 12), M=64, N=577, K=n * 144, **gconv(6, 64))),
+         R.prepare(Job(a=Operand(p=g4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=12, W=12, C=64, R=3, S=3, pad=0,
+                                 OH=14, OW=14),
                        b=_wgt(w4, dt, S_WGT_CONV_T, 64), M=n * 196, N=64, K=576, epi=E_MASK_POS,
                        out=dy3.data_ptr(), out_dt=dt, act=a3.data_ptr())))
-    # conv3 (pad 1): weight grad || input grad -> dp2 = d(a2) * drop2d * (a2 > 0)
+    # conv3 (pad 1): weight grad || input grad -> d(a2) * drop2d * (a2 > 0), unpooled: conv2's g2
     step(R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=64, OH=14, OW=14, transpose=1),
                        b=_conv_act(a2, dt, 14, 32, 1, 14), M=64, N=289, K=n * 196, **gconv(4, 32))),
          R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=14, W=14, C=64, R=3, S=3, pad=1,
                                  OH=14, OW=14),
                        b=_wgt(w3, dt, S_WGT_CONV_T, 64), M=n * 196, N=32, K=576, epi=E_DROP_POS,
-                       out=dp2.data_ptr(), out_dt=dt, act=a2.data_ptr(), drop=_p(m2), drop_cols=32, HW=196)))
-    # conv2: weight grad over the unpooled gradient || input grad -> dy1 = d(a1) * (a1 > 0)
-    unpool2 = Operand(p=dp2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=28, OW=28, idx=idx2.data_ptr(), transpose=1)
-    step(R.prepare(Job(a=unpool2, b=_conv_act(a1, dt, 30, 32, 0, 28), M=32, N=289, K=n * 784, **gconv(2, 32))),
-         R.prepare(Job(a=Operand(p=dp2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=28, W=28, C=32, R=3, S=3, pad=0,
-                                 OH=30, OW=30, idx=idx2.data_ptr()),
+                       out=g2.data_ptr(), out_dt=dt, act=a2.data_ptr(), drop=_p(m2), drop_cols=32, HW=196,
+                       idx=idx2.data_ptr(), PH=14, PW=14)))
+    # conv2: weight grad || input grad -> dy1 = d(a1) * (a1 > 0)
+    step(R.prepare(Job(a=Operand(p=g2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=28, OW=28, transpose=1),
+                       b=_conv_act(a1, dt, 30, 32, 0, 28), M=32, N=289, K=n * 784, **gconv(2, 32))),
+         R.prepare(Job(a=Operand(p=g2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=28, W=28, C=32, R=3, S=3, pad=0,
+                                 OH=30, OW=30),
                        b=_wgt(w2, dt, S_WGT_CONV_T, 32), M=n * 900, N=32, K=288, epi=E_MASK_POS,
                        out=dy1.data_ptr(), out_dt=dt, act=a1.data_ptr())))
     # conv1: weight grad only (no input gradient)

@@ -10,19 +10,20 @@
 //   -> flatten (torch's NCHW order: k = c*36 + h*6 + w) -> fc1 2304->512 -> relu -> dropout -> a5
 //   -> fc2 512->10 -> logits (fp32)
 //
-// Why one generic kernel: at batch 16-64 every pass is a few microseconds of work on a few hundred
+// Why gather-GEMMs: at batch 16-64 every pass is a few microseconds of work on a few hundred
 // workgroups, so the step is launch- and latency-bound (round 4: ~130 library kernels per batch,
 // profiles/r4_cifar_trial_steady.txt).  What matters is the number of passes and that no activation
-// is written just to be re-read by an elementwise kernel: here the forward is 7 launches (masks +
-// 6 GEMMs, pooling/dropout in the conv epilogues), the backward 7 (each layer's weight- and input-
-// gradient GEMMs share one launch, one launch reduces every split-K weight gradient into the grad
-// arena), and the unpooling / ReLU / dropout backward never materialise: the gradient operand loader
-// routes the pooled gradient to the argmax position as it stages the tile.
+// is written just to be re-read by an elementwise kernel: here the forward is 8 launches (masks +
+// 6 GEMMs + split-K finishes, pooling/dropout in the conv epilogues), the backward ~10 (each layer's
+// weight- and input-gradient GEMMs share one launch, one launch reduces every split-K weight
+// gradient into the grad arena), and the unpooling / ReLU / dropout backward never materialise: the
+// gradient operand loader routes the pooled gradient to the argmax position as it stages the tile.
 //
-// GEMM: C[M,N] = sum_k A[m,k] B[k,n], fp32 accumulate on the VALU (64x64 block tile, BK 16, 256 lanes
-// x 4x4 outputs, register-prefetched double buffer through LDS).  At these shapes the convolutions are
-// 25-460 MFLOP: a few microseconds each at VALU rates, well under the launch floor, so the matrix
-// cores would not change the step time (fp32 O0 and bf16 O2 storage share the code path).
+// GEMM: C[M,N] = sum_k A[m,k] B[k,n] on MFMA (64x64 block tile, BK 64, bf16 or exact-fp32 MFMA,
+// fp32 accumulate), one kernel instantiation per (A source, B source, epilogue) kind.  Every pass is
+// latency-bound (a tile's global loads take longer than its MFMAs), so the levers are loads in
+// flight per iteration (BK 64, 16-B gathers), split-K for launches with few tiles, and small
+// per-kind code (see gemm_tile).
 //
 // Dropout masks: one launch per forward draws every mask from Philox4x32-10 keyed by (seed, offset) +
 // the device offset counter (ops/transformer.py rng_base), so hipGraph replays draw fresh masks and
@@ -30,9 +31,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 16, NT = 256;
+constexpr int BM = 64, BN = 64, NT = 256;
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -133,11 +136,12 @@ __device__ __forceinline__ float unpool_at(const Operand& o, uint32_t n, int h, 
 }
 
 // A[row][kk0 .. kk0+7] (or B[kk0 .. kk0+7][row]) for a fixed GEMM row; nk <= 8 of them are in range
+template <int SRC>
 __device__ __forceinline__ void opval8(const Operand& o, uint32_t row, uint32_t kk0, int nk, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = 0.f;
   const int dt = odt(o);
-  switch (o.src) {
+  switch (SRC) {
     case S_ACT_CONV: {
       uint32_t n;
       int oh, ow;
@@ -244,12 +248,13 @@ __device__ __forceinline__ void opval8(const Operand& o, uint32_t row, uint32_t 
 
 // weight-gradient operands, 8 consecutive reduction indices (pixels / images) k0 .. k0+7:
 //   A[m = out channel][k] = g[k][m] (with the unpool routing of a pooled layer)
+template <int SRC>
 __device__ __forceinline__ void gradval8(const Operand& o, uint32_t m, uint32_t k0, int nk, float (&v)[8]) {
   const int dt = odt(o);
   const uint32_t C = static_cast<uint32_t>(o.C);
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = 0.f;
-  if (o.src == S_GRAD_ROWS || o.idx == nullptr) {
+  if (SRC == S_GRAD_ROWS || o.idx == nullptr) {
     for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, (k0 + j) * C + m);
     return;
   }
@@ -272,15 +277,16 @@ __device__ __forceinline__ void gradval8(const Operand& o, uint32_t m, uint32_t 
   }
 }
 //   B[k][n = weight column] = the activation of pixel / image k at column n (conv: kk = n)
+template <int SRC>
 __device__ __forceinline__ void actcol8(const Operand& o, uint32_t k0, uint32_t col, int nk, float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = 0.f;
   const int dt = odt(o);
-  if (o.src == S_ACT_ROWS) {
+  if (SRC == S_ACT_ROWS) {
     for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, (k0 + j) * static_cast<uint32_t>(o.C) + col);
     return;
   }
-  if (o.src == S_ACT_FLAT) {
+  if (SRC == S_ACT_FLAT) {
     const uint32_t hw = static_cast<uint32_t>(o.H * o.W), C = static_cast<uint32_t>(o.C);
     const uint32_t c = col / hw, rem = col - c * hw;
     for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, ((k0 + j) * hw + rem) * C + c);
@@ -316,8 +322,9 @@ enum Epi : int {
   E_BIAS_RELU_DROP = 2,  // fc1: out[m][n] = relu(acc + bias) * drop(m, n)
   E_BIAS = 3,            // fc2 logits: out[m][n] = acc + bias[n]                            (fp32)
   E_MASK_POS = 4,        // dgrad into a ReLU output a: out = acc * (a[m][n] > 0)            (T)
-  E_DROP_POS = 5,        // dgrad into a dropout(relu) output a (pooled / fc): out = acc * drop * (a > 0)
-  E_DROP_POS_FLAT = 6,   // fc1 dgrad: as 5, written at the NHWC position of flat index n (c*HW + hw)
+  E_DROP_POS = 5,        // dgrad into a dropout(relu) output a (pooled / fc): out = acc * drop * (a > 0);
+                         //   with idx: written unpooled (the 2x2 window of the pre-pool grid, see unpool_store)
+  E_DROP_POS_FLAT = 6,   // fc1 dgrad: as 5, written at the NHWC position of flat index n (c*HW + hw); idx: unpooled
   E_GRAD_FC = 7,         // weight gradient W[m][n] (+)= acc via (gso, gsc); n == N-1 with gbias: bias
   E_GRAD_CONV = 8,       // weight gradient W[o=m][c][r][s] (+)= acc, n = (r*S+s)*C + c; bias column
 };
@@ -354,9 +361,42 @@ __device__ __forceinline__ float drop_factor(const Job& j, int64_t row, int64_t 
   return j.drop == nullptr ? 1.f : j.drop[row * j.drop_cols + col];
 }
 
+// the gradient of one pooled element routed to its 2x2 window of the (2PH, 2PW) pre-pool grid: g at
+// the argmax q, zero at the other three (so the unpooled gradient needs no memset)
+__device__ __forceinline__ void unpool_store(const Job& J, uint32_t img, uint32_t ph, uint32_t pw, uint32_t c,
+                                             uint32_t C, float g, uint8_t q) {
+  const uint32_t W2 = 2u * static_cast<uint32_t>(J.PW), H2 = 2u * static_cast<uint32_t>(J.PH);
+  const uint32_t base = ((img * H2 + 2u * ph) * W2 + 2u * pw) * C + c;
+#pragma unroll
+  for (uint32_t d = 0; d < 4; ++d)
+    st(J.out, J.out_dt, base + ((d >> 1) * W2 + (d & 1u)) * C, d == q ? g : 0.f);
+}
+
+// bias + ReLU + 2x2 max-pool + channel dropout of one pooled output (win, n) from its 4 window rows,
+// with the argmax (first maximum of the row-major window, as torch's max_pool2d) to idx
+__device__ __forceinline__ void pool_store(const Job& J, uint32_t win, int64_t n, float v0, float v1, float v2, float v3) {
+  const uint32_t img = win / static_cast<uint32_t>(J.PH * J.PW);
+  const float bb = ld(J.bias, J.bias_dt, n);
+  const float v[4] = {v0, v1, v2, v3};
+  float best = fmaxf(v[0] + bb, 0.f);
+  int arg = 0;
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    const float x = fmaxf(v[q] + bb, 0.f);
+    if (x > best) {
+      best = x;
+      arg = q;
+    }
+  }
+  best = J.out_dt == 1 ? bf2f(f2bf(best)) : best;
+  st(J.out, J.out_dt, static_cast<int64_t>(win) * J.N + n, best * drop_factor(J, img, n));
+  J.idx[static_cast<int64_t>(win) * J.N + n] = static_cast<uint8_t>(arg);
+}
+
 // every epilogue but the pooling one, for one output element (GEMM or split-K finish)
-__device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, float v) {
-  switch (J.epi) {
+template <int EPI>
+__device__ __forceinline__ void epi_store_t(const Job& J, int64_t m, int64_t n, float v) {
+  switch (EPI) {
     case E_BIAS_RELU:
       st(J.out, J.out_dt, m * J.N + n, fmaxf(v + ld(J.bias, J.bias_dt, n), 0.f));
       break;
@@ -374,7 +414,15 @@ __device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, fl
       break;
     case E_DROP_POS: {
       const float a = ld(J.act, J.out_dt, m * J.N + n);
-      st(J.out, J.out_dt, m * J.N + n, a > 0.f ? v * drop_factor(J, m / J.HW, n) : 0.f);
+      const float g = a > 0.f ? v * drop_factor(J, m / J.HW, n) : 0.f;
+      if (J.idx == nullptr) {
+        st(J.out, J.out_dt, m * J.N + n, g);
+      } else {  // unpooled: m is a pooled pixel (img, ph, pw) of the HW = PH * PW grid
+        const uint32_t mu = static_cast<uint32_t>(m), hw = static_cast<uint32_t>(J.HW);
+        const uint32_t img = mu / hw, rem = mu - img * hw;
+        const uint32_t ph = rem / static_cast<uint32_t>(J.PW), pw = rem - ph * static_cast<uint32_t>(J.PW);
+        unpool_store(J, img, ph, pw, static_cast<uint32_t>(n), static_cast<uint32_t>(J.N), g, J.idx[m * J.N + n]);
+      }
       break;
     }
     case E_DROP_POS_FLAT: {
@@ -382,7 +430,14 @@ __device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, fl
       const int hw = static_cast<int>(n - static_cast<int64_t>(c) * J.HW);
       const int64_t e = (m * J.HW + hw) * J.C + c;
       const float a = ld(J.act, J.out_dt, e);
-      st(J.out, J.out_dt, e, a > 0.f ? v * drop_factor(J, m, c) : 0.f);
+      const float g = a > 0.f ? v * drop_factor(J, m, c) : 0.f;
+      if (J.idx == nullptr) {
+        st(J.out, J.out_dt, e, g);
+      } else {
+        const uint32_t ph = static_cast<uint32_t>(hw) / static_cast<uint32_t>(J.PW);
+        const uint32_t pw = static_cast<uint32_t>(hw) - ph * static_cast<uint32_t>(J.PW);
+        unpool_store(J, static_cast<uint32_t>(m), ph, pw, static_cast<uint32_t>(c), static_cast<uint32_t>(J.C), g, J.idx[e]);
+      }
       break;
     }
     case E_GRAD_FC:
@@ -393,7 +448,7 @@ __device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, fl
         break;
       }
       int64_t e;
-      if (J.epi == E_GRAD_FC) {
+      if (EPI == E_GRAD_FC) {
         e = m * J.gso + n * J.gsc;
       } else {
         const int c = static_cast<int>(n % J.gC), rs = static_cast<int>(n / J.gC);
@@ -406,14 +461,32 @@ __device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, fl
     }
   }
 }
+__device__ __forceinline__ void epi_store(const Job& J, int64_t m, int64_t n, float v) {
+  switch (J.epi) {
+    case E_BIAS_RELU: epi_store_t<E_BIAS_RELU>(J, m, n, v); break;
+    case E_BIAS_RELU_DROP: epi_store_t<E_BIAS_RELU_DROP>(J, m, n, v); break;
+    case E_BIAS: epi_store_t<E_BIAS>(J, m, n, v); break;
+    case E_MASK_POS: epi_store_t<E_MASK_POS>(J, m, n, v); break;
+    case E_DROP_POS: epi_store_t<E_DROP_POS>(J, m, n, v); break;
+    case E_DROP_POS_FLAT: epi_store_t<E_DROP_POS_FLAT>(J, m, n, v); break;
+    case E_GRAD_FC: epi_store_t<E_GRAD_FC>(J, m, n, v); break;
+    case E_GRAD_CONV: epi_store_t<E_GRAD_CONV>(J, m, n, v); break;
+  }
+}
 
 // ---- the GEMM core on MFMA ---------------------------------------------------------------------
-// 64 x 64 block tile, BK = 32, 4 waves of 32 x 32 (2 x 2 tiles of 16 x 16).  bf16 storage runs
+// 64 x 64 block tile, BK = 64, 4 waves of 32 x 32 (2 x 2 tiles of 16 x 16).  bf16 storage runs
 // v_mfma_f32_16x16x32_bf16 (lane l: A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]); fp32 storage runs the
 // exact-fp32 v_mfma_f32_16x16x4_f32 (A[l&15][l>>4], B[l>>4][l&15]), so O0 keeps fp32 products.
-// C/D: col = l&15, row = 4(l>>4) + i.  Staging: each lane gathers 8 consecutive k of one tile row
-// (the operand loaders above), double-buffered through LDS with the next tile's gathers issued
+// C/D: col = l&15, row = 4(l>>4) + i.  Staging: each lane gathers two groups of 8 consecutive k of
+// one tile row (the operand loaders above: one 16-B load per group where the layout allows),
+// double-buffered through LDS (one vector store per group) with the next tile's gathers issued
 // before the current tile's MFMAs.
+//
+// The kernel is specialised per (A source, B source, epilogue) at compile time -- a job's loaders
+// and epilogue are all a launch executes, so each instantiation stays a few KB of code: one generic
+// kernel with every path inlined was 148 KB, beyond the 64 KB instruction cache, and its small
+// launches ran 20-30 us on cold instruction fetches (round-5 trace, profiles/r5_cifar_native_trace.txt).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -421,26 +494,53 @@ template <bool BF>
 struct Stage;
 template <>
 struct Stage<true> {
+  static constexpr int LDK = 64 + 8;  // row stride 144 B: 16-B fragment reads stay aligned
   typedef uint16_t E;
-  static constexpr int PAD = 8;  // row stride 40 elements = 80 B (16-B fragment reads stay aligned)
   __device__ static E cvt(float v) { return f2bf(v); }
+  __device__ static void put8(E* dst, const float (&v)[8]) {
+    uint4 q;
+    q.x = static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16;
+    q.y = static_cast<uint32_t>(f2bf(v[2])) | static_cast<uint32_t>(f2bf(v[3])) << 16;
+    q.z = static_cast<uint32_t>(f2bf(v[4])) | static_cast<uint32_t>(f2bf(v[5])) << 16;
+    q.w = static_cast<uint32_t>(f2bf(v[6])) | static_cast<uint32_t>(f2bf(v[7])) << 16;
+    *reinterpret_cast<uint4*>(dst) = q;
+  }
 };
 template <>
 struct Stage<false> {
+  static constexpr int LDK = 64 + 4;
   typedef float E;
-  static constexpr int PAD = 4;
   __device__ static E cvt(float v) { return v; }
+  __device__ static void put8(E* dst, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
 };
 
-constexpr int GBK = 32;
+constexpr int GBK = 64;
+
+// a job kind: A source, B source, epilogue (weight-gradient jobs read A transposed)
+template <int SA_, int SB_, int EP_>
+struct Kind {
+  static constexpr int SA = SA_, SB = SB_, EP = EP_;
+  static constexpr bool WG = EP_ == E_GRAD_FC || EP_ == E_GRAD_CONV;
+};
+struct NoKind {};
 
 template <bool BF>
-__global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
-  using E = typename Stage<BF>::E;
-  constexpr int LDK = GBK + Stage<BF>::PAD;
-  const int jb = static_cast<int>(blockIdx.x) < L.nblocks0 ? 0 : 1;
-  const Job& J = L.job[jb];
-  int bid = jb == 0 ? blockIdx.x : blockIdx.x - L.nblocks0;
+struct Smem {
+  typename Stage<BF>::E As[2][BM][Stage<BF>::LDK];
+  typename Stage<BF>::E Bs[2][BN][Stage<BF>::LDK];
+};
+
+// Convolution operands address an element as (row's pixel) + (the k index's tap and channel): the
+// k part comes from a per-block LDS table built once (ktab: A delta, packed (dh, dw) offset, B
+// delta), the row part is decomposed once per tile, so the K loop does no integer division.
+constexpr int KTAB = 576;  // largest conv reduction of the network (3 x 3 x 64)
+
+template <bool BF, class KD>
+__device__ __forceinline__ void gemm_tile(const Job& J, int bid, Smem<BF>& sm, int4* ktab) {
+  constexpr int LDK = Stage<BF>::LDK;
   const int z = bid % J.splits;
   bid /= J.splits;
   const int tn = bid % J.tiles_n;
@@ -449,47 +549,247 @@ __global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
   const int64_t k_lo = static_cast<int64_t>(z) * J.k_per_split;
   const int64_t k_hi = k_lo + J.k_per_split < J.K ? k_lo + J.k_per_split : J.K;
 
-  __shared__ __attribute__((aligned(16))) E As[2][BM][LDK];
-  __shared__ __attribute__((aligned(16))) E Bs[2][BN][LDK];
   const int t = threadIdx.x;
-  const int lr = t >> 2, lk = (t & 3) * 8;  // staging: tile row lr, k = lk .. lk+7
+  const int lr = t >> 2, lk = (t & 3) * 8;  // staging: tile row lr, k = lk .. lk+7 and lk+32 .. lk+39
   const int lane = t & 63, w = t >> 6;
   const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
-  const bool wgrad = J.a.transpose != 0;
-  const bool bias_col = wgrad && J.gbias != nullptr;
+  const bool bias_col = KD::WG && J.gbias != nullptr;
 
-  float ra[8], rb[8];
+  constexpr bool ATAB = !KD::WG && (KD::SA == S_ACT_CONV || KD::SA == S_GRAD_CONV_T);
+  constexpr bool BTAB = !KD::WG && (KD::SB == S_WGT_CONV || KD::SB == S_WGT_CONV_T);
+  if constexpr (ATAB || BTAB) {
+    for (int k = t; k < J.K; k += NT) {
+      int4 e = make_int4(0, 0, 0, 0);
+      if constexpr (ATAB) {
+        const Operand& o = J.a;
+        const int rs = k / o.C, c = k - rs * o.C, r = rs / o.S, sx = rs - r * o.S;
+        const int dh = KD::SA == S_ACT_CONV ? r - o.pad : o.pad - r;
+        const int dw = KD::SA == S_ACT_CONV ? sx - o.pad : o.pad - sx;
+        e.x = (dh * o.W + dw) * o.C + c;
+        e.y = static_cast<int>(static_cast<uint32_t>(dh) << 16 | (static_cast<uint32_t>(dw) & 0xffffu));
+      }
+      if constexpr (BTAB) {
+        const Operand& o = J.b;
+        const int rs = k / o.C, c = k - rs * o.C, r = rs / o.S, sx = rs - r * o.S;
+        e.z = static_cast<int>((KD::SB == S_WGT_CONV ? c * o.sc : c * o.so) + r * o.sr + sx * o.ss);
+      }
+      ktab[k] = e;
+    }
+    __syncthreads();
+  }
+  // this thread's A row (a pixel of the conv's GEMM grid), decomposed once
+  int a_base = 0, a_h = 0, a_w = 0;
+  if constexpr (ATAB) {
+    const Operand& o = J.a;
+    if (m0 + lr < J.M) {
+      uint32_t n;
+      Operand g = o;
+      if (KD::SA == S_GRAD_CONV_T) g.pool = 0;
+      pix_nhw(g, static_cast<uint32_t>(m0 + lr), n, a_h, a_w);
+      a_base = ((static_cast<int>(n) * o.H + a_h) * o.W + a_w) * o.C;
+    }
+  }
+  auto tab_a = [&](int64_t kg, int nk, float (&v)[8]) {
+    const Operand& o = J.a;
+    const int dt = odt(o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    if (nk == 8 && (o.C & 7) == 0) {  // one tap, 8 channels
+      const int4 e = ktab[kg];
+      const int h = a_h + (e.y >> 16), w = a_w + static_cast<int>(static_cast<short>(e.y & 0xffff));
+      if (h >= 0 && h < o.H && w >= 0 && w < o.W) ld8(o.p, dt, static_cast<uint32_t>(a_base + e.x), v);
+      return;
+    }
+    for (int j = 0; j < nk; ++j) {
+      const int4 e = ktab[kg + j];
+      const int h = a_h + (e.y >> 16), w = a_w + static_cast<int>(static_cast<short>(e.y & 0xffff));
+      if (h >= 0 && h < o.H && w >= 0 && w < o.W) v[j] = ld32(o.p, dt, static_cast<uint32_t>(a_base + e.x));
+    }
+  };
+  auto tab_b = [&](uint32_t row, int64_t kg, int nk, float (&v)[8]) {
+    const Operand& o = J.b;
+    const int dt = odt(o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    const uint32_t rb = static_cast<uint32_t>(row * (KD::SB == S_WGT_CONV ? o.so : o.sc));
+    if (KD::SB == S_WGT_CONV && nk == 8 && o.sc == 1 && (o.C & 7) == 0) {
+      ld8(o.p, dt, rb + static_cast<uint32_t>(ktab[kg].z), v);
+      return;
+    }
+    for (int j = 0; j < nk; ++j) v[j] = ld32(o.p, dt, rb + static_cast<uint32_t>(ktab[kg + j].z));
+  };
+
+  // Operands whose 8 contiguous elements run along the GEMM row (not along k) are staged k-major:
+  // thread t takes k = t & 63 of the tile and rows 8 rg .. 8 rg + 7 (rg = t >> 6, then + 4), one 16-B
+  // load each, written to LDS transposed -- the weight-gradient operands (A = dY^T: channels
+  // contiguous; B = the activation column block: a tap's channels contiguous) and the input-gradient
+  // weights (W[o][c][r][s] with c contiguous).  The others are staged row-major (row lr, 8 k).
+  constexpr bool AKM = KD::WG;
+  constexpr bool BKM = KD::WG || KD::SB == S_WGT_CONV_T || KD::SB == S_WGT_FC_T;
+  const int kk = t & 63, rg = t >> 6;
+  // k-major B of a conv weight gradient: per row group, the tap offset and channel of its 8 columns
+  int bc_dh[2] = {0, 0}, bc_dw[2] = {0, 0}, bc_c0[2] = {0, 0};
+  bool bc_vec[2] = {false, false};
+  const int nreal = bias_col ? static_cast<int>(J.N) - 1 : static_cast<int>(J.N);  // non-bias columns
+  if constexpr (KD::WG && KD::SB == S_ACT_CONV) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int col0 = static_cast<int>(n0) + 8 * (rg + 4 * g);
+      const int C = J.b.C;
+      const int rs = col0 / C, c0 = col0 - rs * C, r = rs / J.b.S, sx = rs - r * J.b.S;
+      bc_dh[g] = r - J.b.pad;
+      bc_dw[g] = sx - J.b.pad;
+      bc_c0[g] = c0;
+      bc_vec[g] = (C & 7) == 0 && col0 + 8 <= nreal;
+    }
+  }
+  auto km_a = [&](int64_t k, int g, float (&v)[8]) {  // A[m][k] = dY[k][m], m = m0 + 8 (rg + 4g) + i
+    const Operand& o = J.a;
+    const int dt = odt(o);
+    const int mr = static_cast<int>(m0) + 8 * (rg + 4 * g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    if (k >= k_hi) return;
+    const uint32_t base = static_cast<uint32_t>(k) * static_cast<uint32_t>(o.C);
+    if ((o.C & 7) == 0 && mr + 8 <= J.M) {
+      ld8(o.p, dt, base + static_cast<uint32_t>(mr), v);
+    } else {
+      for (int i = 0; i < 8; ++i)
+        if (mr + i < J.M) v[i] = ld32(o.p, dt, base + static_cast<uint32_t>(mr + i));
+    }
+  };
+  // the pixel of k-major k (weight gradients of a conv: k runs over the OH x OW grid, row-major)
+  auto km_b = [&](int64_t k, int g, uint32_t pn, int ph, int pw, float (&v)[8]) {
+    const Operand& o = J.b;
+    const int dt = odt(o);
+    const int col0 = static_cast<int>(n0) + 8 * (rg + 4 * g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    if (k >= k_hi) return;
+    if constexpr (KD::WG) {
+      if constexpr (KD::SB == S_ACT_CONV) {
+        if (bc_vec[g]) {
+          const int h = ph + bc_dh[g], w = pw + bc_dw[g];
+          if (h >= 0 && h < o.H && w >= 0 && w < o.W)
+            ld8(o.p, dt, ((pn * static_cast<uint32_t>(o.H) + h) * static_cast<uint32_t>(o.W) + w) * o.C + bc_c0[g], v);
+          return;
+        }
+        for (int i = 0; i < 8; ++i) {
+          const int col = col0 + i;
+          if (col >= static_cast<int>(J.N)) break;
+          if (col == nreal) {  // the bias column
+            v[i] = 1.f;
+            continue;
+          }
+          const int rs = col / o.C, c = col - rs * o.C, r = rs / o.S, sx = rs - r * o.S;
+          const int h = ph + r - o.pad, w = pw + sx - o.pad;
+          if (h >= 0 && h < o.H && w >= 0 && w < o.W)
+            v[i] = ld32(o.p, dt, ((pn * static_cast<uint32_t>(o.H) + h) * static_cast<uint32_t>(o.W) + w) * o.C + c);
+        }
+      } else if constexpr (KD::SB == S_ACT_ROWS) {
+        const uint32_t base = static_cast<uint32_t>(k) * static_cast<uint32_t>(o.C);
+        if ((o.C & 7) == 0 && col0 + 8 <= nreal) {
+          ld8(o.p, dt, base + static_cast<uint32_t>(col0), v);
+          return;
+        }
+        for (int i = 0; i < 8; ++i) {
+          const int col = col0 + i;
+          if (col < nreal) v[i] = ld32(o.p, dt, base + static_cast<uint32_t>(col));
+          else if (col == nreal && col < static_cast<int>(J.N)) v[i] = 1.f;
+        }
+      } else {  // S_ACT_FLAT: column c*HW + hw of image k
+        const int hw = o.H * o.W;
+        for (int i = 0; i < 8; ++i) {
+          const int col = col0 + i;
+          if (col < nreal) {
+            const int c = col / hw, rem = col - c * hw;
+            v[i] = ld32(o.p, dt, (static_cast<uint32_t>(k) * static_cast<uint32_t>(hw) + rem) * o.C + c);
+          } else if (col == nreal && col < static_cast<int>(J.N)) {
+            v[i] = 1.f;
+          }
+        }
+      }
+    } else if constexpr (KD::SB == S_WGT_CONV_T) {  // B[k = (tap, o)][n = c] = W[o][c][r][s]
+      const uint32_t base = static_cast<uint32_t>(ktab[k].z);
+      if (o.sc == 1 && col0 + 8 <= static_cast<int>(J.N)) {
+        ld8(o.p, dt, base + static_cast<uint32_t>(col0), v);
+        return;
+      }
+      for (int i = 0; i < 8; ++i)
+        if (col0 + i < J.N) v[i] = ld32(o.p, dt, base + static_cast<uint32_t>((col0 + i) * o.sc));
+    } else {  // S_WGT_FC_T: B[k = o][n = j] = W[o][j]
+      const uint32_t base = static_cast<uint32_t>(k * o.so);
+      if (o.sc == 1 && col0 + 8 <= static_cast<int>(J.N) && (o.so & 7) == 0) {
+        ld8(o.p, dt, base + static_cast<uint32_t>(col0), v);
+        return;
+      }
+      for (int i = 0; i < 8; ++i)
+        if (col0 + i < J.N) v[i] = ld32(o.p, dt, base + static_cast<uint32_t>((col0 + i) * o.sc));
+    }
+  };
+
+  float ra[2][8], rb[2][8];
   auto gather = [&](int64_t k0) {
     const int64_t m = m0 + lr, n = n0 + lr;
-    const int64_t kg = k0 + lk;  // first of this lane's 8 reduction indices
-    const int nk = kg >= k_hi ? 0 : (k_hi - kg < 8 ? static_cast<int>(k_hi - kg) : 8);
-    if (m < J.M && nk > 0) {
-      if (wgrad) gradval8(J.a, static_cast<uint32_t>(m), static_cast<uint32_t>(kg), nk, ra);
-      else opval8(J.a, static_cast<uint32_t>(m), static_cast<uint32_t>(kg), nk, ra);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ra[i] = 0.f;
-    }
-    if (n < J.N && nk > 0) {
-      if (!wgrad) {
-        opval8(J.b, static_cast<uint32_t>(n), static_cast<uint32_t>(kg), nk, rb);
-      } else if (bias_col && n == J.N - 1) {  // weight gradient: the last column is the bias's
-#pragma unroll
-        for (int i = 0; i < 8; ++i) rb[i] = i < nk ? 1.f : 0.f;
-      } else {
-        actcol8(J.b, static_cast<uint32_t>(kg), static_cast<uint32_t>(n), nk, rb);
+    if constexpr (AKM || BKM) {
+      const int64_t k = k0 + kk;
+      uint32_t pn = 0;
+      int ph = 0, pw = 0;
+      if constexpr (KD::WG && KD::SB == S_ACT_CONV) {  // this thread's pixel, once per tile
+        const uint32_t ku = static_cast<uint32_t>(k), OW = static_cast<uint32_t>(J.b.OW);
+        const uint32_t q = ku / OW;
+        pw = static_cast<int>(ku - q * OW);
+        pn = q / static_cast<uint32_t>(J.b.OH);
+        ph = static_cast<int>(q - pn * static_cast<uint32_t>(J.b.OH));
       }
-    } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) rb[i] = 0.f;
+      for (int g = 0; g < 2; ++g) {
+        if constexpr (AKM) km_a(k, g, ra[g]);
+        if constexpr (BKM) km_b(k, g, pn, ph, pw, rb[g]);
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int64_t kg = k0 + lk + 32 * g;
+      const int nk = kg >= k_hi ? 0 : (k_hi - kg < 8 ? static_cast<int>(k_hi - kg) : 8);
+      if constexpr (!AKM) {
+        if (m < J.M && nk > 0) {
+          if constexpr (ATAB) tab_a(kg, nk, ra[g]);
+          else opval8<KD::SA>(J.a, static_cast<uint32_t>(m), static_cast<uint32_t>(kg), nk, ra[g]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ra[g][i] = 0.f;
+        }
+      }
+      if constexpr (!BKM) {
+        if (n < J.N && nk > 0) {
+          if constexpr (BTAB) tab_b(static_cast<uint32_t>(n), kg, nk, rb[g]);
+          else opval8<KD::SB>(J.b, static_cast<uint32_t>(n), static_cast<uint32_t>(kg), nk, rb[g]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) rb[g][i] = 0.f;
+        }
+      }
     }
   };
   auto stash = [&](int b) {
+    using E = typename Stage<BF>::E;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      As[b][lr][lk + i] = Stage<BF>::cvt(ra[i]);
-      Bs[b][lr][lk + i] = Stage<BF>::cvt(rb[i]);
+    for (int g = 0; g < 2; ++g) {
+      if constexpr (AKM) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm.As[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt(ra[g][i]);
+      } else {
+        Stage<BF>::put8(&sm.As[b][lr][lk + 32 * g], ra[g]);
+      }
+      if constexpr (BKM) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sm.Bs[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt(rb[g][i]);
+      } else {
+        Stage<BF>::put8(&sm.Bs[b][lr][lk + 32 * g], rb[g]);
+      }
     }
+    (void)sizeof(E);
   };
   f32x4 acc[2][2];
 #pragma unroll
@@ -497,46 +797,50 @@ __global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int64_t k0 = k_lo;
-  gather(k0);
-  stash(0);
-  __syncthreads();
-  int buf = 0;
-  for (; k0 < k_hi; k0 += GBK) {
-    const bool more = k0 + GBK < k_hi;
-    if (more) gather(k0 + GBK);
+  // one gather call site (the loaders are most of the code): iteration i gathers tile i, runs the
+  // MFMAs of tile i-1 (staged in the other buffer) while the loads are in flight, then stages tile i
+  auto compute = [&](int cb) {
     if constexpr (BF) {
-      bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(&As[buf][wm + i * 16 + (lane & 15)][8 * (lane >> 4)]);
+      for (int ks = 0; ks < GBK; ks += 32) {
+        bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn + j * 16 + (lane & 15)][8 * (lane >> 4)]);
+        for (int i = 0; i < 2; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(&sm.As[cb][wm + i * 16 + (lane & 15)][ks + 8 * (lane >> 4)]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&sm.Bs[cb][wn + j * 16 + (lane & 15)][ks + 8 * (lane >> 4)]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int kq = 0; kq < GBK; kq += 4) {
         float af[2], bfr[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = As[buf][wm + i * 16 + (lane & 15)][kq + (lane >> 4)];
+        for (int i = 0; i < 2; ++i) af[i] = sm.As[cb][wm + i * 16 + (lane & 15)][kq + (lane >> 4)];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = Bs[buf][wn + j * 16 + (lane & 15)][kq + (lane >> 4)];
+        for (int j = 0; j < 2; ++j) bfr[j] = sm.Bs[cb][wn + j * 16 + (lane & 15)][kq + (lane >> 4)];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (more) {
-      stash(buf ^ 1);
-      buf ^= 1;
-    }
-    __syncthreads();
+  };
+  int buf = 0;
+  for (int64_t k0 = k_lo; k0 < k_hi; k0 += GBK) {
+    gather(k0);
+    if (k0 > k_lo) compute(buf ^ 1);
+    stash(buf);
+    __syncthreads();  // tile i staged; every wave is past tile i-1's reads of the buffer i+1 reuses
+    buf ^= 1;
   }
+  compute(buf ^ 1);
+  (void)LDK;
 
   // ---- epilogue: lane holds rows 4(lane>>4)+r, r = 0..3, of column lane&15 of each 16x16 tile
 #pragma unroll
@@ -553,32 +857,73 @@ __global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
           if (mrow + r < J.M) J.slab[(static_cast<int64_t>(z) * J.M + mrow + r) * J.N + n] = v[r];
         continue;
       }
-      if (J.epi == E_BIAS_RELU_POOL) {
+      if constexpr (KD::EP == E_BIAS_RELU_POOL) {
         // the 4 rows are one 2x2 window (M window-ordered, M % 4 == 0)
         if (mrow >= J.M) continue;
-        const int64_t win = mrow >> 2;
-        const int64_t img = win / (static_cast<int64_t>(J.PH) * J.PW);
-        const float bb = ld(J.bias, J.bias_dt, n);
-        float best = fmaxf(v[0] + bb, 0.f);
-        int arg = 0;
+        pool_store(J, static_cast<uint32_t>(mrow >> 2), n, v[0], v[1], v[2], v[3]);
+      } else {
 #pragma unroll
-        for (int q = 1; q < 4; ++q) {
-          const float x = fmaxf(v[q] + bb, 0.f);
-          if (x > best) {  // first maximum of the row-major window, as torch's max_pool2d
-            best = x;
-            arg = q;
-          }
-        }
-        best = J.out_dt == 1 ? bf2f(f2bf(best)) : best;
-        st(J.out, J.out_dt, win * J.N + n, best * drop_factor(J, img, n));
-        J.idx[win * J.N + n] = static_cast<uint8_t>(arg);
-        continue;
+        for (int r = 0; r < 4; ++r)
+          if (mrow + r < J.M) epi_store_t<KD::EP>(J, mrow + r, n, v[r]);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (mrow + r < J.M) epi_store(J, mrow + r, n, v[r]);
     }
   }
+}
+
+// one launch runs job 0 (kind K0) and, if K1 is a Kind, job 1 side by side
+template <bool BF, class K0, class K1>
+__global__ void __launch_bounds__(NT) cnn_gemm_kernel(Launch L) {
+  __shared__ __attribute__((aligned(16))) Smem<BF> sm;
+  __shared__ int4 ktab[KTAB];
+  if constexpr (!std::is_same<K1, NoKind>::value) {
+    if (static_cast<int>(blockIdx.x) >= L.nblocks0) {
+      gemm_tile<BF, K1>(L.job[1], static_cast<int>(blockIdx.x) - L.nblocks0, sm, ktab);
+      return;
+    }
+  }
+  gemm_tile<BF, K0>(L.job[0], static_cast<int>(blockIdx.x), sm, ktab);
+}
+
+// the job kinds the network launches (ops/cnn.py): forward, then backward (weight grad, input grad)
+typedef Kind<S_ACT_CONV, S_WGT_CONV, E_BIAS_RELU> KConv;
+typedef Kind<S_ACT_CONV, S_WGT_CONV, E_BIAS_RELU_POOL> KConvPool;
+typedef Kind<S_ACT_FLAT, S_WGT_FC, E_BIAS_RELU_DROP> KFc1;
+typedef Kind<S_ACT_ROWS, S_WGT_FC, E_BIAS> KFc2;
+typedef Kind<S_GRAD_ROWS, S_ACT_ROWS, E_GRAD_FC> KFc2W;
+typedef Kind<S_GRAD_ROWS, S_WGT_FC_T, E_DROP_POS> KFc2D;
+typedef Kind<S_GRAD_ROWS, S_ACT_FLAT, E_GRAD_FC> KFc1W;
+typedef Kind<S_GRAD_ROWS, S_WGT_FC_T, E_DROP_POS_FLAT> KFc1D;
+typedef Kind<S_GRAD_CONV_T, S_ACT_CONV, E_GRAD_CONV> KConvW;
+typedef Kind<S_GRAD_CONV_T, S_WGT_CONV_T, E_MASK_POS> KConvD;
+typedef Kind<S_GRAD_CONV_T, S_WGT_CONV_T, E_DROP_POS> KConvDDrop;
+
+template <class KD>
+__host__ bool kind_is(const Job& j) {
+  const bool tab = !KD::WG && (KD::SA == S_ACT_CONV || KD::SA == S_GRAD_CONV_T || KD::SB == S_WGT_CONV ||
+                               KD::SB == S_WGT_CONV_T);
+  return j.a.src == KD::SA && j.b.src == KD::SB && j.epi == KD::EP && (j.a.transpose != 0) == KD::WG &&
+         (!tab || j.K <= KTAB);
+}
+
+template <bool BF, class K0, class K1>
+bool try_launch(const Launch& L, bool has1, int blocks, hipStream_t st) {
+  if (!kind_is<K0>(L.job[0])) return false;
+  if constexpr (std::is_same<K1, NoKind>::value) {
+    if (has1) return false;
+  } else {
+    if (!has1 || !kind_is<K1>(L.job[1])) return false;
+  }
+  cnn_gemm_kernel<BF, K0, K1><<<blocks, NT, 0, st>>>(L);
+  return true;
+}
+
+template <bool BF>
+bool launch_kinds(const Launch& L, bool has1, int blocks, hipStream_t st) {
+  return try_launch<BF, KConv, NoKind>(L, has1, blocks, st) || try_launch<BF, KConvPool, NoKind>(L, has1, blocks, st) ||
+         try_launch<BF, KFc1, NoKind>(L, has1, blocks, st) || try_launch<BF, KFc2, NoKind>(L, has1, blocks, st) ||
+         try_launch<BF, KFc2W, KFc2D>(L, has1, blocks, st) || try_launch<BF, KFc1W, KFc1D>(L, has1, blocks, st) ||
+         try_launch<BF, KConvW, KConvD>(L, has1, blocks, st) || try_launch<BF, KConvW, KConvDDrop>(L, has1, blocks, st) ||
+         try_launch<BF, KConvW, NoKind>(L, has1, blocks, st);
 }
 
 // ---- split-K finish: sum the slabs of up to 4 jobs and apply their epilogues --------------------
@@ -597,10 +942,30 @@ __global__ void __launch_bounds__(NT) cnn_finish_kernel(FinishLaunch L) {
     while (ji + 1 < L.njobs && e >= L.first[ji + 1]) ++ji;
     const Job& J = L.job[ji];
     const int64_t i = e - L.first[ji];
-    const int64_t m = i / J.N, n = i - m * J.N;
-    float s = 0.f;
-    for (int zz = 0; zz < J.splits; ++zz) s += J.slab[(static_cast<int64_t>(zz) * J.M + m) * J.N + n];
-    epi_store(J, m, n, s);
+    const int64_t stride = J.M * J.N;
+    // 8 independent slab loads in flight per step (a serial chain of dependent adds left every
+    // load's latency exposed: 76 us for the batched weight-gradient finish of round-5 session 6)
+    auto sum = [&](int64_t m, int64_t n) {
+      const float* sp = J.slab + m * J.N + n;
+      float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int zz = 0;
+      for (; zz + 8 <= J.splits; zz += 8) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc8[q] += sp[(zz + q) * stride];
+      }
+#pragma unroll
+      for (int q = 0; q < 7; ++q)
+        if (zz + q < J.splits) acc8[q] += sp[(zz + q) * stride];
+      return ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+    };
+    if (J.epi == E_BIAS_RELU_POOL) {  // i = (window, n): the window's 4 rows summed, then pooled
+      const int64_t win = i / J.N, n = i - win * J.N;
+      pool_store(J, static_cast<uint32_t>(win), n, sum(4 * win, n), sum(4 * win + 1, n), sum(4 * win + 2, n),
+                 sum(4 * win + 3, n));
+    } else {
+      const int64_t m = i / J.N, n = i - m * J.N;
+      epi_store(J, m, n, sum(m, n));
+    }
   }
 }
 
@@ -793,7 +1158,7 @@ static int fill_job(const DetCnnJob& d, Job* j) {
   j->gbias = d.gbias;
   j->accumulate = d.accumulate;
   j->slab = d.slab;
-  if (j->splits > 1 && (d.slab == nullptr || d.epi == E_BIAS_RELU_POOL)) return -1;
+  if (j->splits > 1 && d.slab == nullptr) return -1;
   if (d.epi == E_BIAS_RELU_POOL && (d.M & 3)) return -1;
   return j->tiles_m * j->tiles_n * j->splits;
 }
@@ -811,8 +1176,9 @@ int det_cnn_gemm(void* stream, int32_t bf16, const DetCnnJob* j0, const DetCnnJo
     L.job[1] = L.job[0];
   }
   L.nblocks0 = b0;
-  if (bf16) cnn_gemm_kernel<true><<<b0 + b1, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
-  else cnn_gemm_kernel<false><<<b0 + b1, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool ok = bf16 ? launch_kinds<true>(L, j1 != nullptr, b0 + b1, st) : launch_kinds<false>(L, j1 != nullptr, b0 + b1, st);
+  if (!ok) return static_cast<int>(hipErrorNotSupported);  // a job kind the network does not launch
   return static_cast<int>(hipGetLastError());
 }
 
@@ -824,7 +1190,7 @@ int det_cnn_finish(void* stream, const DetCnnJob* jobs, int32_t njobs) {
   for (int i = 0; i < njobs; ++i) {
     if (fill_job(jobs[i], &L.job[i]) <= 0 || L.job[i].splits < 2) return static_cast<int>(hipErrorInvalidValue);
     L.first[i] = total;
-    total += L.job[i].M * L.job[i].N;
+    total += (L.job[i].epi == E_BIAS_RELU_POOL ? L.job[i].M / 4 : L.job[i].M) * L.job[i].N;
   }
   for (int i = njobs; i < kMaxFin; ++i) {
     L.job[i] = L.job[0];

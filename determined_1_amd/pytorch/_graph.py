@@ -67,6 +67,57 @@ CHUNK_WARMUP = 1  # per-batch chunks per multi-batch key before capturing it
 CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 
 
+# Half-precision convolutions on the vendor library (MIOpen) do not replay correctly from a captured
+# graph once other MIOpen work runs between replays: the graph's results diverge from eager and go
+# non-finite within a few replays.  Reproduced without this framework (scripts/dbg/
+# miopen_graph_repro.py --step, round 5): a plain bf16 torch CNN trained K steps per graph with
+# eager steps in between goes NaN on the second replay; the same steps in fp32, with the convolutions
+# off MIOpen (torch.backends.cudnn.enabled = False), or with only Linear layers replay exactly; every
+# MIOpen op captured alone replays exactly.  This was the round-4 "O2 + dropout" NaN of the CIFAR
+# trial (dropout was incidental: the NaN stays with dropout removed and with masks from a fixed bank).
+# The first warm-up step of a graph key runs under this probe; a hit keeps train_batch eager.
+# DET_GRAPH_LIBRARY_CONVS=1 captures anyway (for the reproduction scripts).
+LIBRARY_CONV_OPS = ("aten::convolution", "aten::convolution_backward", "aten::_convolution",
+                    "aten::miopen_convolution", "aten::cudnn_convolution")
+
+
+class _LibraryConvProbe:
+    """TorchDispatchMode wrapper that notes the first half-precision convolution a step dispatches to
+    the vendor library (torch.backends.cudnn.enabled, a CUDA input in bf16/fp16)."""
+
+    def __init__(self) -> None:
+        from torch.utils._python_dispatch import TorchDispatchMode
+
+        probe = self
+
+        class _Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):  # noqa: ANN001
+                if probe.found is None and func.name() in LIBRARY_CONV_OPS and torch.backends.cudnn.enabled:
+                    x = args[0] if args else None
+                    if isinstance(x, torch.Tensor) and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
+                        probe.found = f"{func.name()} on {x.dtype}"
+                return func(*args, **(kwargs or {}))
+
+        self.found: Optional[str] = None
+        self.mode = _Mode()
+
+    def run(self, fn: Callable[[], Any]) -> Any:
+        with self.mode:
+            return fn()
+
+
+def library_conv_reason(fn: Callable[[], Any]) -> Tuple[Any, Optional[str]]:
+    """Run ``fn`` (one eager step) under the probe: (its result, a reason to stay eager or None)."""
+    if os.environ.get("DET_GRAPH_LIBRARY_CONVS", "0") == "1":
+        return fn(), None
+    probe = _LibraryConvProbe()
+    out = probe.run(fn)
+    if probe.found is None:
+        return out, None
+    return out, (f"half-precision MIOpen convolution ({probe.found}) -- these mis-replay from captured graphs "
+                 "(pytorch/_graph.py LIBRARY_CONV_OPS note; DET_GRAPH_LIBRARY_CONVS=1 captures anyway)")
+
+
 def reads_argument(fn: Callable[..., Any], name: str) -> bool:
     """Whether ``fn``'s body can observe its argument ``name`` (conservatively True when the code is
     not inspectable or it uses locals()/frames).  A ``train_batch`` that never reads ``epoch_idx``
@@ -131,6 +182,7 @@ class TrainStepGraph:
         self.chunk_disabled: Optional[str] = None
         self.chunk_replays = 0
         self.last_chunk_metrics: Optional[List[Any]] = None
+        self.probed = False  # the first warm-up step ran under the library-convolution probe
 
     # ------------------------------------------------------------------------------------------
     @staticmethod
@@ -145,16 +197,6 @@ class TrainStepGraph:
             return "dynamic loss scaling syncs on overflow"
         if context._timers.enabled:
             return "DET_STEP_TIMERS synchronises the step"
-        if os.environ.get("DET_GRAPH_HALF_DROPOUT", "0") != "1":
-            for m in getattr(context, "models", []):
-                half = any(p.dtype in (torch.bfloat16, torch.float16) for p in m.parameters())
-                drop = any(isinstance(x, torch.nn.modules.dropout._DropoutNd) and x.p > 0 for x in m.modules())
-                if half and drop:
-                    # measured: the CIFAR trial at O2 went NaN late in every replayed run (per-batch
-                    # and chunked graphs, 3 seeds, 2 learning rates) and in no eager run; the same
-                    # trial without dropout, or at O0 with it, replays cleanly (README, round 4)
-                    return ("torch dropout in a half-precision model (replays of it diverged in measured runs; "
-                            "DET_GRAPH_HALF_DROPOUT=1 overrides)")
         if not context._opt_states:
             return "no wrapped optimizer"
         for st in context._opt_states:
@@ -187,7 +229,13 @@ class TrainStepGraph:
         n = self.seen.get(key, 0) + 1
         self.seen[key] = n
         if n <= WARMUP:
-            return self._eager(batch, epoch_idx, batch_idx)
+            if self.probed:
+                return self._eager(batch, epoch_idx, batch_idx)
+            self.probed = True
+            out, reason = library_conv_reason(lambda: self._eager(batch, epoch_idx, batch_idx))
+            if reason is not None:
+                self._disable(reason)
+            return out
         g = self._capture(key, leaves, spec, epoch_idx, batch_idx)
         if g is None:
             return self._eager(batch, epoch_idx, batch_idx)
@@ -390,7 +438,14 @@ class EvalStepGraph:
             n = self.seen.get(key, 0) + 1
             self.seen[key] = n
             if n <= self.WARMUP:
-                return self._eager(batch)
+                if getattr(self, "probed", False):
+                    return self._eager(batch)
+                self.probed = True
+                out, reason = library_conv_reason(lambda: self._eager(batch))
+                if reason is not None:
+                    logging.warning("hip_graph: evaluate_batch runs eagerly: %s", reason)
+                    self.disabled_reason = reason
+                return out
             if len(self.graphs) >= MAX_GRAPHS:
                 torch.cuda.synchronize()
                 while len(self.graphs) >= MAX_GRAPHS:

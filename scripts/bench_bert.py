@@ -78,6 +78,8 @@ def main() -> None:
         m = (r or {}).get("metrics", {}).get("avg_metrics", {}) if isinstance(r, dict) else {}
         if "loss" in m:
             losses.append(float(m["loss"]))
+            print(f"[bench_bert] {len(losses) * args.loss_every} steps, loss {losses[-1]:.5f}, "
+                  f"{time.perf_counter() - t['t0']:.1f}s", file=sys.stderr, flush=True)
 
     def stream():
         yield workload.train_workload(1, num_batches=args.warmup), [], workload.ignore_response

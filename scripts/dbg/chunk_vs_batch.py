@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--out", default="gpurun_out/cvb")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
-    os.environ["DET_GRAPH_HALF_DROPOUT"] = "1"
+    os.environ["DET_GRAPH_LIBRARY_CONVS"] = "1"
     os.environ["DET_NATIVE_CNN"] = "1" if args.native else "0"
     import torch
 

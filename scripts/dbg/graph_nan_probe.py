@@ -90,7 +90,7 @@ def main():
                     help="round-4 model: element Dropout after the first pool and RMSprop alpha 0.99")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
-    os.environ["DET_GRAPH_HALF_DROPOUT"] = "1"  # lift the round-4 guard: this probe is about that defect
+    os.environ["DET_GRAPH_LIBRARY_CONVS"] = "1"  # capture the torch (MIOpen) layers anyway: this probe is about that defect
     import torch
     import torch.nn.functional as F
 

@@ -165,7 +165,6 @@ def test_graph_replays_train_the_native_cnn(gpu, monkeypatch):
     fresh masks per replay (the device offset counter), grads landing in the arena in place."""
     import sys
 
-    monkeypatch.setenv("DET_GRAPH_HALF_DROPOUT", "1")
     ex = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "computer_vision",
                       "cifar10_pytorch")
     sys.path.insert(0, ex)

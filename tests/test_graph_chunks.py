@@ -135,9 +135,10 @@ def test_multibatch_graph_replay_matches_eager(gpu, monkeypatch):
     assert v_g == pytest.approx(v_e, rel=2e-3)
 
 
-def test_half_precision_dropout_model_stays_eager(monkeypatch):
-    """A bf16 model with torch dropout layers is not replayed (README: replays of the CIFAR trial at
-    O2 diverged); fp32 with dropout, or bf16 without, stays eligible; the env override lifts it."""
+def test_half_precision_dropout_model_is_graph_eligible():
+    """The round-4 guard (half-precision model + torch dropout -> eager) is gone: its NaN was MIOpen
+    half-precision convolutions mis-replaying (pytorch/_graph.py LIBRARY_CONV_OPS note), which the
+    warm-up probe now detects instead.  Dropout itself never made a model ineligible again."""
     from types import SimpleNamespace
 
     from determined_1_amd.pytorch._graph import TrainStepGraph
@@ -146,11 +147,24 @@ def test_half_precision_dropout_model_stays_eager(monkeypatch):
         return SimpleNamespace(device=torch.device("cuda"), dist_config=SimpleNamespace(use=False, aggregation_frequency=1),
                                _amp=None, _timers=SimpleNamespace(enabled=False), _opt_states=[], models=[model])
 
-    drop = nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.5))
-    assert "dropout" in TrainStepGraph.ineligible_reason(ctx(drop.to(torch.bfloat16)))
-    assert TrainStepGraph.ineligible_reason(ctx(nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.5)))) == "no wrapped optimizer"
-    assert TrainStepGraph.ineligible_reason(ctx(nn.Sequential(nn.Linear(4, 4)).to(torch.bfloat16))) == "no wrapped optimizer"
-    assert TrainStepGraph.ineligible_reason(ctx(nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.0)).to(torch.bfloat16))) \
-        == "no wrapped optimizer"
-    monkeypatch.setenv("DET_GRAPH_HALF_DROPOUT", "1")
+    drop = nn.Sequential(nn.Linear(4, 4), nn.Dropout(0.5)).to(torch.bfloat16)
     assert TrainStepGraph.ineligible_reason(ctx(drop)) == "no wrapped optimizer"
+
+
+def test_library_conv_probe_passes_results_through_and_ignores_host_convs():
+    """The probe runs the warm-up step unchanged (same result) and only flags convolutions that would
+    go to MIOpen: CUDA inputs in bf16/fp16 (host convolutions, fp32 and Linear layers never)."""
+    from determined_1_amd.pytorch._graph import LIBRARY_CONV_OPS, library_conv_reason
+
+    conv = nn.Conv2d(3, 4, 3).to(torch.bfloat16)
+    x = torch.randn(2, 3, 8, 8, dtype=torch.bfloat16, requires_grad=True)
+
+    def step():
+        y = conv(x).float().sum()
+        y.backward()
+        return y.detach()
+
+    ref = step()
+    out, reason = library_conv_reason(step)
+    assert reason is None and torch.equal(out, ref)
+    assert "aten::convolution" in LIBRARY_CONV_OPS and "aten::convolution_backward" in LIBRARY_CONV_OPS

@@ -39,3 +39,39 @@ def test_graph_replays_draw_fresh_torch_dropout_masks(gpu, dtype, layer):
     for i in range(len(outs)):
         for j in range(i):
             assert not torch.equal(outs[i], outs[j]), f"replays {j} and {i} drew the same mask"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_two_dropout_layers_per_step_and_eager_steps_draw_distinct_masks(gpu, dtype):
+    """Two dropout layers in ONE captured step (module and functional form) and eager steps between
+    replays: every mask drawn -- per layer, per replay, per eager step -- is distinct, i.e. no two
+    draws share a Philox offset."""
+    torch.manual_seed(1)
+    mod = nn.Dropout(0.5)
+    x = torch.ones(16, 4096, device=gpu, dtype=dtype)
+
+    def step():
+        return mod(x), nn.functional.dropout(x, 0.5, training=True)
+
+    for _ in range(2):
+        step()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            ya, yb = step()
+    torch.cuda.current_stream().wait_stream(s)
+    masks = []
+    for _ in range(3):
+        g.replay()
+        masks += [ya.clone(), yb.clone()]
+        masks += [m.clone() for m in step()]
+    torch.cuda.synchronize()
+    for m in masks:
+        kept = (m != 0).float().mean().item()
+        assert 0.45 < kept < 0.55
+    for i in range(len(masks)):
+        for j in range(i):
+            assert not torch.equal(masks[i], masks[j]), f"draws {j} and {i} share a mask"
