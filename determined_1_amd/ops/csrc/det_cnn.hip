@@ -497,6 +497,16 @@ struct Stage<true> {
   static constexpr int LDK = 64 + 8;  // row stride 144 B: 16-B fragment reads stay aligned
   typedef uint16_t E;
   __device__ static E cvt(float v) { return f2bf(v); }
+  // values that came from bf16 storage convert back exactly: keep the high half (v_perm packs two)
+  __device__ static E cvt_exact(float v) { return static_cast<E>(__float_as_uint(v) >> 16); }
+  __device__ static void put8_exact(E* dst, const float (&v)[8]) {
+    uint4 q;
+    q.x = __builtin_amdgcn_perm(__float_as_uint(v[1]), __float_as_uint(v[0]), 0x07060302u);
+    q.y = __builtin_amdgcn_perm(__float_as_uint(v[3]), __float_as_uint(v[2]), 0x07060302u);
+    q.z = __builtin_amdgcn_perm(__float_as_uint(v[5]), __float_as_uint(v[4]), 0x07060302u);
+    q.w = __builtin_amdgcn_perm(__float_as_uint(v[7]), __float_as_uint(v[6]), 0x07060302u);
+    *reinterpret_cast<uint4*>(dst) = q;
+  }
   __device__ static void put8(E* dst, const float (&v)[8]) {
     uint4 q;
     q.x = static_cast<uint32_t>(f2bf(v[0])) | static_cast<uint32_t>(f2bf(v[1])) << 16;
@@ -511,10 +521,12 @@ struct Stage<false> {
   static constexpr int LDK = 64 + 4;
   typedef float E;
   __device__ static E cvt(float v) { return v; }
+  __device__ static E cvt_exact(float v) { return v; }
   __device__ static void put8(E* dst, const float (&v)[8]) {
     *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
+  __device__ static void put8_exact(E* dst, const float (&v)[8]) { put8(dst, v); }
 };
 
 constexpr int GBK = 64;
@@ -772,24 +784,36 @@ __device__ __forceinline__ void gemm_tile(const Job& J, int bid, Smem<BF>& sm, i
       }
     }
   };
+  // bf16-stored operands round-trip exactly (truncate); only fp32 ones (the logits gradient) round
+  const bool a_exact = J.a.dt == 1, b_exact = J.b.dt == 1;
   auto stash = [&](int b) {
-    using E = typename Stage<BF>::E;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       if constexpr (AKM) {
+        if (a_exact) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm.As[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt(ra[g][i]);
+          for (int i = 0; i < 8; ++i) sm.As[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt_exact(ra[g][i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) sm.As[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt(ra[g][i]);
+        }
       } else {
-        Stage<BF>::put8(&sm.As[b][lr][lk + 32 * g], ra[g]);
+        if (a_exact) Stage<BF>::put8_exact(&sm.As[b][lr][lk + 32 * g], ra[g]);
+        else Stage<BF>::put8(&sm.As[b][lr][lk + 32 * g], ra[g]);
       }
       if constexpr (BKM) {
+        if (b_exact) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sm.Bs[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt(rb[g][i]);
+          for (int i = 0; i < 8; ++i) sm.Bs[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt_exact(rb[g][i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) sm.Bs[b][8 * (rg + 4 * g) + i][kk] = Stage<BF>::cvt(rb[g][i]);
+        }
       } else {
-        Stage<BF>::put8(&sm.Bs[b][lr][lk + 32 * g], rb[g]);
+        if (b_exact) Stage<BF>::put8_exact(&sm.Bs[b][lr][lk + 32 * g], rb[g]);
+        else Stage<BF>::put8(&sm.Bs[b][lr][lk + 32 * g], rb[g]);
       }
     }
-    (void)sizeof(E);
   };
   f32x4 acc[2][2];
 #pragma unroll

@@ -399,7 +399,7 @@ __global__ void __launch_bounds__(kThreads, OCC) gemm_nt_kernel(NtArgs a) {
   constexpr int NQE = BNB ? BM * CPR / kThreads : 1;
   // hoisted only where the registers allow it (occupancy-2 tiles without the ABN staging: the
   // others spill); elsewhere the loads are issued at the start of the epilogue
-  constexpr bool EPRE = BNB && OCC <= 2 && !ABN;
+  constexpr bool EPRE = BNB && OCC <= 2 && !ABN && PF == 1;
   us8 xs[NQE], as[NQE];
   unsigned bs[NQE];
   auto eload = [&]() {
@@ -842,13 +842,13 @@ int launch_nt(hipStream_t st, const NtArgs& a_in, bool pro, bool stats, bool str
   if (bnb) {  // input-gradient GEMM with the BN-backward epilogue (no prologue / stats / gather)
     constexpr int smem_b = smem > BM * (BN + 16) * 2 + kThreads * 16 * 4 ? smem : BM * (BN + 16) * 2 + kThreads * 16 * 4;
     if (abn)
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true, true>),
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true, true, false, PF>),
                          dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
     else if (bt)
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true>),
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, true, false, false, PF>),
                          dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true>),
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, false, false, kGmDirect, OCC, true, false, false, false, PF>),
                          dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem_b, st, a);
     return static_cast<int>(hipGetLastError());
   }
@@ -1048,6 +1048,18 @@ int det_conv_nt_bnbwd(void* stream, const void* A, const void* B, void* C, int64
   if (K == kBK && (single || abn_x)) {
     if (N % 128 == 0) return launch_nt<128, 128, 2, 2, kSingleOcc>(st, a, false, false, false, true, bt);
     return launch_nt<128, 64, 2, 2, kSingleOcc>(st, a, false, false, false, true, bt);
+  }
+  // BN-backward GEMMs with a K loop of >= 4 tiles (layer 3/4 input gradients): DET_BNB_PF register
+  // sets of prefetch (the epilogue operand loads then wait for the loop's end instead of holding
+  // their registers through it)
+  static const int bnb_pf = [] {
+    const char* e = std::getenv("DET_BNB_PF");
+    const int v = e ? std::atoi(e) : 1;
+    return v < 1 ? 1 : (v > 2 ? 2 : v);
+  }();
+  if (bnb_pf == 2 && K >= 4 * kBK && !abn_x) {
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2, 2>(st, a, false, false, false, true, bt);
+    return launch_nt<128, 64, 2, 2, 2, 2>(st, a, false, false, false, true, bt);
   }
   if (N % 128 == 0) return launch_nt<128, 128, 2, 2, 2>(st, a, false, false, false, true, bt);
   return launch_nt<128, 64, 2, 2, 2>(st, a, false, false, false, true, bt);
