@@ -83,11 +83,10 @@ class BertEmbeddings(nn.Module):
         self.p = c.hidden_dropout_prob
 
     def forward(self, input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor]) -> torch.Tensor:
-        S = input_ids.shape[1]
-        pos = torch.arange(S, device=input_ids.device)
-        if token_type_ids is None:
-            token_type_ids = torch.zeros_like(input_ids)
-        e = self.word_embeddings(input_ids) + self.token_type_embeddings(token_type_ids) + self.position_embeddings(pos)
+        # one lookup-and-sum launch with a graph-safe backward on the GPU (ops/csrc/det_embed.hip)
+        e = tfops.bert_embeddings(input_ids, token_type_ids, self.word_embeddings.weight,
+                                  self.token_type_embeddings.weight, self.position_embeddings.weight,
+                                  self.word_embeddings.padding_idx)
         e = tfops.layer_norm(e, self.LayerNorm.weight, self.LayerNorm.bias, self.LayerNorm.eps)
         return F.dropout(e, self.p, self.training)
 

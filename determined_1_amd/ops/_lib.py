@@ -233,6 +233,11 @@ _SIGNATURES = {
                                c_void_p, c_void_p], c_int),
     "det_tf_dropout_mask": ([c_void_p, c_i64, c_float, ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p], c_int),
     "det_tf_rng_bump": ([c_void_p, c_void_p], c_int),
+    "det_embed_fwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int],
+                      c_int),
+    "det_embed_ws_floats": ([c_int, c_int, c_int], ctypes.c_int64),
+    "det_embed_bwd": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                       c_int, ctypes.c_int64, c_void_p, c_int], c_int),
 }
 
 

@@ -956,39 +956,53 @@ struct FinishLaunch {
   Job job[kMaxFin];
   int64_t first[kMaxFin];
   int njobs;
+  int tpe;  // threads per output element (power of two <= 32): they split the slab sum
   int64_t total;
 };
 
+// sum of the slabs of (m, n) taken by lane `sub` of a group of T: 4 independent partial sums
+__device__ __forceinline__ float slab_part(const Job& J, int64_t m, int64_t n, int sub, int T) {
+  const float* sp = J.slab + m * J.N + n;
+  const int64_t stride = J.M * J.N;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int zz = sub;
+  for (; zz + 3 * T < J.splits; zz += 4 * T) {
+    a0 += sp[zz * stride];
+    a1 += sp[(zz + T) * stride];
+    a2 += sp[(zz + 2 * T) * stride];
+    a3 += sp[(zz + 3 * T) * stride];
+  }
+  for (; zz < J.splits; zz += T) a0 += sp[zz * stride];
+  return (a0 + a1) + (a2 + a3);
+}
+
+__device__ __forceinline__ float group_sum(float v, int T) {
+  for (int o = T >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __global__ void __launch_bounds__(NT) cnn_finish_kernel(FinishLaunch L) {
-  for (int64_t e = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x; e < L.total;
-       e += static_cast<int64_t>(gridDim.x) * NT) {
+  // T adjacent lanes per output element, each summing every T-th slab (the weight-gradient slabs
+  // run to ~200 splits: one lane per element left that sum a serial chain of load latencies)
+  const int T = L.tpe;
+  const int sub = threadIdx.x & (T - 1);
+  const int64_t groups = static_cast<int64_t>(gridDim.x) * (NT / T);
+  for (int64_t e = (static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x) / T; e < L.total; e += groups) {
     int ji = 0;
     while (ji + 1 < L.njobs && e >= L.first[ji + 1]) ++ji;
     const Job& J = L.job[ji];
     const int64_t i = e - L.first[ji];
-    const int64_t stride = J.M * J.N;
-    // 8 independent slab loads in flight per step (a serial chain of dependent adds left every
-    // load's latency exposed: 76 us for the batched weight-gradient finish of round-5 session 6)
-    auto sum = [&](int64_t m, int64_t n) {
-      const float* sp = J.slab + m * J.N + n;
-      float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      int zz = 0;
-      for (; zz + 8 <= J.splits; zz += 8) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc8[q] += sp[(zz + q) * stride];
-      }
-#pragma unroll
-      for (int q = 0; q < 7; ++q)
-        if (zz + q < J.splits) acc8[q] += sp[(zz + q) * stride];
-      return ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
-    };
     if (J.epi == E_BIAS_RELU_POOL) {  // i = (window, n): the window's 4 rows summed, then pooled
       const int64_t win = i / J.N, n = i - win * J.N;
-      pool_store(J, static_cast<uint32_t>(win), n, sum(4 * win, n), sum(4 * win + 1, n), sum(4 * win + 2, n),
-                 sum(4 * win + 3, n));
+      const float s0 = group_sum(slab_part(J, 4 * win, n, sub, T), T);
+      const float s1 = group_sum(slab_part(J, 4 * win + 1, n, sub, T), T);
+      const float s2 = group_sum(slab_part(J, 4 * win + 2, n, sub, T), T);
+      const float s3 = group_sum(slab_part(J, 4 * win + 3, n, sub, T), T);
+      if (sub == 0) pool_store(J, static_cast<uint32_t>(win), n, s0, s1, s2, s3);
     } else {
       const int64_t m = i / J.N, n = i - m * J.N;
-      epi_store(J, m, n, sum(m, n));
+      const float sum = group_sum(slab_part(J, m, n, sub, T), T);
+      if (sub == 0) epi_store(J, m, n, sum);
     }
   }
 }
@@ -1222,8 +1236,13 @@ int det_cnn_finish(void* stream, const DetCnnJob* jobs, int32_t njobs) {
   }
   L.njobs = njobs;
   L.total = total;
-  int blocks = static_cast<int>((total + NT - 1) / NT);
-  blocks = blocks > 2048 ? 2048 : blocks;
+  int maxs = 1;
+  for (int i = 0; i < njobs; ++i) maxs = L.job[i].splits > maxs ? L.job[i].splits : maxs;
+  int T = 1;
+  while (T < 32 && T * 8 < maxs) T <<= 1;  // ~8 slabs per lane
+  L.tpe = T;
+  int64_t want = (total * T + NT - 1) / NT;
+  const int blocks = static_cast<int>(want > 2048 ? 2048 : want);
   cnn_finish_kernel<<<blocks, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
   return static_cast<int>(hipGetLastError());
 }

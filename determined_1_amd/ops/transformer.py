@@ -537,6 +537,68 @@ def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: fl
         return _LayerNorm.apply(x, gamma, beta, float(eps))
 
 
+class _Embed(torch.autograd.Function):
+    """word[ids] + type[tt] + pos[arange(S)] (det_embed.hip): a graph-safe, deterministic backward
+    (torch's sorts the ids and sizes launches from a host-read count, which a hipGraph freezes)."""
+
+    @staticmethod
+    def forward(ctx, ids, tt, ww, wt, wp, pad):  # type: ignore[override]
+        B, S = ids.shape
+        H = ww.shape[1]
+        out = torch.empty(B, S, H, dtype=ww.dtype, device=ww.device)
+        ids_c = ids.contiguous().long()
+        tt_c = tt.contiguous().long() if tt is not None else None
+        bf = 1 if ww.dtype == torch.bfloat16 else 0
+        _lib.check(_lib.get_lib().det_embed_fwd(_stream(ww), bf, ids_c.data_ptr(), tt_c.data_ptr() if tt_c is not None else None,
+                                                ww.data_ptr(), wt.data_ptr(), wp.data_ptr(), out.data_ptr(), B * S, S, H),
+                   "det_embed_fwd")
+        ctx.save_for_backward(ids_c, tt_c if tt_c is not None else torch.zeros_like(ids_c))
+        ctx.params = (ww, wt, wp)
+        ctx.pad = -1 if pad is None else int(pad)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):  # type: ignore[override]
+        ids, tt = ctx.saved_tensors
+        ww, wt, wp = ctx.params
+        B, S = ids.shape
+        H = ww.shape[1]
+        g = g.contiguous().to(ww.dtype)
+        # inside a capture with the gradients pinned to the arena: accumulate in place (the rows of
+        # absent ids stay as they are); otherwise fresh gradients back to autograd
+        direct = torch.cuda.is_current_stream_capturing() and all(
+            p.grad is not None and p.grad.is_contiguous() and p.grad.dtype == p.dtype for p in (ww, wt, wp))
+        if direct:
+            dww, dwt, dwp, acc = ww.grad, wt.grad, wp.grad, 1
+        else:
+            dww, dwt, dwp, acc = torch.zeros_like(ww), torch.empty_like(wt), torch.zeros_like(wp), 0
+        lib = _lib.get_lib()
+        ws = torch.empty(int(lib.det_embed_ws_floats(B * S, H, wt.shape[0])), dtype=torch.float32, device=g.device)
+        _lib.check(lib.det_embed_bwd(_stream(g), 1 if ww.dtype == torch.bfloat16 else 0, ids.data_ptr(), tt.data_ptr(),
+                                     g.data_ptr(), dww.data_ptr(), dwt.data_ptr(), dwp.data_ptr(), B * S, S, H, wt.shape[0],
+                                     ctx.pad, ws.data_ptr(), acc), "det_embed_bwd")
+        if direct:
+            return None, None, None, None, None, None
+        return None, None, dww, dwt, dwp, None
+
+
+def bert_embeddings(input_ids: torch.Tensor, token_type_ids: Optional[torch.Tensor], word: torch.Tensor,
+                    token_type: torch.Tensor, position: torch.Tensor, padding_idx: Optional[int]) -> torch.Tensor:
+    """word[input_ids] + token_type[token_type_ids] + position[arange(S)] -> [B, S, H] in one launch,
+    with the graph-safe native backward on the GPU (torch's composition elsewhere)."""
+    B, S = input_ids.shape
+    native = (input_ids.is_cuda and _lib.lib_available() and word.dtype in (torch.bfloat16, torch.float32)
+              and word.dtype == token_type.dtype == position.dtype and B * S <= 8192 and S <= position.shape[0]
+              and word.shape[0] < (1 << 18) and token_type.shape[0] <= 4 and word.is_contiguous()
+              and token_type.is_contiguous() and position.is_contiguous() and not torch.is_autocast_enabled())
+    if not native:
+        pos = torch.arange(S, device=input_ids.device)
+        if token_type_ids is None:
+            token_type_ids = torch.zeros_like(input_ids)
+        return F.embedding(input_ids, word, padding_idx) + F.embedding(token_type_ids, token_type) + F.embedding(pos, position)
+    return _Embed.apply(input_ids, token_type_ids, word, token_type, position, padding_idx)
+
+
 def _composite_attention(q, k, v, nh, bias, p, scale):
     B, Lq, H = q.shape
     hd = H // nh

@@ -79,6 +79,12 @@ CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 # DET_GRAPH_LIBRARY_CONVS=1 captures anyway (for the reproduction scripts).
 LIBRARY_CONV_OPS = ("aten::convolution", "aten::convolution_backward", "aten::_convolution",
                     "aten::miopen_convolution", "aten::cudnn_convolution")
+# torch's dense embedding backward over more than this many indices sorts them and sizes its later
+# launches from a segment count read back to the host: a replay keeps the captured batch's sizes and
+# a batch with more distinct ids runs out of bounds (the BERT replays faulted in rocprim's
+# partition_kernel after ~700 steps, round 5; models/bert.py now uses ops.transformer.bert_embeddings,
+# whose backward is shape-sized).  The probe keeps such a train_batch eager.
+EMBED_SORT_INDICES = 3072
 
 
 class _LibraryConvProbe:
@@ -92,10 +98,16 @@ class _LibraryConvProbe:
 
         class _Mode(TorchDispatchMode):
             def __torch_dispatch__(self, func, types, args=(), kwargs=None):  # noqa: ANN001
-                if probe.found is None and func.name() in LIBRARY_CONV_OPS and torch.backends.cudnn.enabled:
-                    x = args[0] if args else None
-                    if isinstance(x, torch.Tensor) and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
-                        probe.found = f"{func.name()} on {x.dtype}"
+                if probe.found is None:
+                    name = func.name()
+                    if name in LIBRARY_CONV_OPS and torch.backends.cudnn.enabled:
+                        x = args[0] if args else None
+                        if isinstance(x, torch.Tensor) and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
+                            probe.found = f"half-precision MIOpen convolution ({name} on {x.dtype})"
+                    elif name == "aten::embedding_dense_backward" and len(args) > 1:
+                        idx = args[1]
+                        if isinstance(idx, torch.Tensor) and idx.is_cuda and idx.numel() > EMBED_SORT_INDICES:
+                            probe.found = f"torch embedding backward over {idx.numel()} indices (host-sized sort path)"
                 return func(*args, **(kwargs or {}))
 
         self.found: Optional[str] = None
@@ -114,7 +126,7 @@ def library_conv_reason(fn: Callable[[], Any]) -> Tuple[Any, Optional[str]]:
     out = probe.run(fn)
     if probe.found is None:
         return out, None
-    return out, (f"half-precision MIOpen convolution ({probe.found}) -- these mis-replay from captured graphs "
+    return out, (f"{probe.found} -- not replay-safe from a captured graph "
                  "(pytorch/_graph.py LIBRARY_CONV_OPS note; DET_GRAPH_LIBRARY_CONVS=1 captures anyway)")
 
 

@@ -99,4 +99,4 @@ def test_half_precision_library_convs_keep_train_batch_eager(gpu):
         assert torch.isfinite(out)
         assert (reason is not None) == expect_hit, reason
         if expect_hit:
-            assert "MIOpen" in reason and "bfloat16" in reason
+            assert "MIOpen" in reason and "bfloat16" in reason and "not replay-safe" in reason
