@@ -102,6 +102,10 @@ inline bool bn_nt() {
   return v;
 }
 
+#ifndef DET_BN_CF
+#define DET_BN_CF 1  // channel-fixed apply mapping (0: the grid-stride vector mapping, for A/B builds)
+#endif
+
 struct Geom {
   int64_t M;   // rows
   int C;       // channels
@@ -485,6 +489,54 @@ bn_apply_fwd(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__
              const float* __restrict__ rshift = nullptr) {
   // num_batches_tracked += 1 rides on this launch (stream-ordered after the finalize that read it)
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
+#if DET_BN_CF
+  // channel-fixed mapping when C/8 divides the block: each thread keeps one 8-channel group for the
+  // whole pass (scale/shift loaded once, no per-vector channel modulo), a block covers 256/(C/8)
+  // whole rows per iteration (consecutive threads = consecutive 16-B chunks of a row)
+  const int cv = C >> 3;
+  if (cv <= kThreads && (kThreads % cv) == 0) {
+    const int lc = static_cast<int>(threadIdx.x) % cv, rpb = kThreads / cv, c0 = lc << 3;
+    float sc[8], sh[8], rsc[8], rsh[8];
+    load8f(scale + c0, sc);
+    load8f(shift + c0, sh);
+    if (RES == 2) {
+      load8f(rscale + c0, rsc);
+      load8f(rshift + c0, rsh);
+    }
+    const int64_t nrow = nvec / cv, RS = static_cast<int64_t>(gridDim.x) * rpb;
+    for (int64_t r0 = static_cast<int64_t>(blockIdx.x) * rpb + threadIdx.x / cv; r0 < nrow; r0 += 4 * RS) {
+      float xv[4][8], rv[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = r0 + u * RS;
+        if (r < nrow) {
+          sload8<NTL>(x + (r * cv + lc) * 8, xv[u]);
+          if (RES) sload8<NTL>(res + (r * cv + lc) * 8, rv[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = r0 + u * RS;
+        if (r < nrow) {
+          const int64_t v = r * cv + lc;
+          float o[8];
+          unsigned bits = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float z = __fmaf_rn(xv[u][j], sc[j], sh[j]);
+            if (RES == 1) z += rv[u][j];
+            if (RES == 2) z += __uint_as_float(static_cast<uint32_t>(f2bf(__fmaf_rn(rv[u][j], rsc[j], rsh[j]))) << 16);
+            o[j] = RELU ? fmaxf(z, 0.f) : z;
+            bits |= (z > 0.f ? 1u : 0u) << j;
+          }
+          IO8<T>::store(y + v * 8, o);
+          if (RELU && RES && mbits) mbits[v] = static_cast<uint8_t>(bits);
+        }
+      }
+    }
+    return;
+  }
+#endif
   const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v0 < nvec; v0 += 4 * S) {
     float xv[4][8], rv[4][8];
@@ -794,6 +846,60 @@ bn_apply_bwd(const T* __restrict__ dy, const T* __restrict__ dy2, const T* __res
              const float* __restrict__ coef, const float* __restrict__ scale,
              const float* __restrict__ shift, T* __restrict__ dx, T* __restrict__ dres,
              int64_t nvec, int C) {
+#if DET_BN_CF
+  const int cv = C >> 3;
+  if (cv <= kThreads && (kThreads % cv) == 0) {  // channel-fixed mapping (see bn_apply_fwd)
+    const int lc = static_cast<int>(threadIdx.x) % cv, rpb = kThreads / cv, c0 = lc << 3;
+    float A[8], B[8], Cc[8], sc[8], sh[8];
+    load8f(coef + c0, A);
+    load8f(coef + C + c0, B);
+    load8f(coef + 2 * C + c0, Cc);
+    if (MASK == 1) {
+      load8f(scale + c0, sc);
+      load8f(shift + c0, sh);
+    }
+    const int64_t nrow = nvec / cv, RS = static_cast<int64_t>(gridDim.x) * rpb;
+    for (int64_t r0 = static_cast<int64_t>(blockIdx.x) * rpb + threadIdx.x / cv; r0 < nrow; r0 += 2 * RS) {
+      float dv[2][8], xv[2][8];
+      unsigned mb[2] = {0xFFu, 0xFFu};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t r = r0 + u * RS;
+        if (r < nrow) {
+          const int64_t v = r * cv + lc;
+          sload8<NTL>(dy + v * 8, dv[u]);
+          sload8<NTL>(x + v * 8, xv[u]);
+          if (dy2) {
+            float e[8];
+            sload8<NTL>(dy2 + v * 8, e);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dv[u][j] += e[j];
+          }
+          if (MASK == 2) mb[u] = mbits[v];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t r = r0 + u * RS;
+        if (r < nrow) {
+          const int64_t v = r * cv + lc;
+          float o[8], dz[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float d = dv[u][j];
+            if (MASK == 1) d = __fmaf_rn(xv[u][j], sc[j], sh[j]) > 0.f ? d : 0.f;
+            else if (MASK == 2) d = (mb[u] >> j) & 1u ? d : 0.f;
+            dz[j] = d;
+            o[j] = __fmaf_rn(A[j], d, __fmaf_rn(B[j], xv[u][j], Cc[j]));
+          }
+          IO8<T>::store(dx + v * 8, o);
+          if (DRES) IO8<T>::store(dres + v * 8, dz);
+        }
+      }
+    }
+    return;
+  }
+#endif
   const int64_t S = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t v0 = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v0 < nvec; v0 += 2 * S) {
     float dv[2][8], xv[2][8];

@@ -29,6 +29,8 @@ def main() -> None:
     ap.add_argument("--step-kernel", default="opt_kernel")
     ap.add_argument("--skip-steps", type=int, default=3)
     ap.add_argument("--out")
+    ap.add_argument("--sequence", action="store_true",
+                    help="also print one mid-window step's kernel sequence (per-dispatch durations)")
     args = ap.parse_args()
     rows = []
     if args.trace.endswith(".db"):  # rocprofv3 >= 7 default output (rocpd sqlite)
@@ -62,6 +64,13 @@ def main() -> None:
           f"kernel busy {busy / 1e6 / n_steps:.3f} ms/step ({100.0 * busy / max(1, wall):.1f}%)")
     for k, (t, c) in out[:40]:
         print(f"{t / 1e6 / n_steps:8.3f} ms/step {c / n_steps:6.1f}/step {100.0 * t / busy:5.1f}%  {k}")
+    if args.sequence:
+        mid = steps[args.skip_steps + n_steps // 2]
+        nxt = steps[args.skip_steps + n_steps // 2 + 1]
+        seq = rows[mid + 1:nxt + 1]
+        print(f"one step ({len(seq)} kernels, {(rows[nxt][1] - rows[mid][1]) / 1e3:.1f} us):")
+        for s0, e0, n0 in seq:
+            print(f"  {(e0 - s0) / 1e3:8.2f} us  {short(n0)}")
     if args.out:
         with open(args.out, "w", newline="") as f:
             w = csv.writer(f)
