@@ -1083,7 +1083,10 @@ __global__ void __launch_bounds__(NT) cnn_xent_fwd_kernel(const float* z, const 
   }
   if (threadIdx.x == 0) {
     loss_out[0] = sl[0] / N;
-    if (acc_out != nullptr) acc_out[0] = sa[0] / N;
+    if (acc_out != nullptr) {  // accuracy, then the error rate in the next float
+      acc_out[0] = sa[0] / N;
+      acc_out[1] = 1.f - sa[0] / N;
+    }
   }
 }
 

@@ -57,12 +57,12 @@ class CIFARTrial(pytorch.PyTorchTrial):
     def train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, torch.Tensor]:
         x, y = batch
         out = self.model(self._images(x))
-        loss, acc = cross_entropy(out, y, with_accuracy=True)  # one fused launch on the GPU
+        loss, acc, err = cross_entropy(out, y, with_accuracy=True, with_error=True)  # one fused launch on the GPU
         self.context.backward(loss)
         self.context.step_optimizer(self.opt)
-        return {"loss": loss, "train_error": 1.0 - acc, "train_accuracy": acc}
+        return {"loss": loss, "train_error": err, "train_accuracy": acc}
 
     def evaluate_batch(self, batch: Any) -> Dict[str, Any]:
         x, y = batch
-        loss, acc = cross_entropy(self.model(self._images(x)), y, with_accuracy=True)
-        return {"validation_loss": loss, "validation_error": 1.0 - acc, "validation_accuracy": acc}
+        loss, acc, err = cross_entropy(self.model(self._images(x)), y, with_accuracy=True, with_error=True)
+        return {"validation_loss": loss, "validation_error": err, "validation_accuracy": acc}

@@ -130,14 +130,15 @@ def main():
 
         native_ce = model_def.cross_entropy
 
-        def loss_fn(out, y, with_accuracy=False):
+        def loss_fn(out, y, with_accuracy=False, with_error=False):
             if args.loss == "torch":  # exactly round 4's train_batch
                 lt, at = F.cross_entropy(out.float(), y), (out.argmax(1) == y).float().mean()
-                return (lt, at) if with_accuracy else lt
-            ln, an = native_ce(out, y, with_accuracy=True)
-            lt = F.cross_entropy(out.float(), y) if args.loss in ("torch", "torch_ce") else ln
-            at = (out.argmax(1) == y).float().mean() if args.loss in ("torch", "torch_acc") else an
-            return (lt, at) if with_accuracy else lt
+            else:
+                ln, an = native_ce(out, y, with_accuracy=True)
+                lt = F.cross_entropy(out.float(), y) if args.loss in ("torch", "torch_ce") else ln
+                at = (out.argmax(1) == y).float().mean() if args.loss in ("torch", "torch_acc") else an
+            outs = (lt,) + ((at,) if with_accuracy else ()) + ((1.0 - at,) if with_error else ())
+            return outs if len(outs) > 1 else lt
 
         model_def.cross_entropy = loss_fn
     if args.r4_model:

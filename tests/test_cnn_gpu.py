@@ -150,11 +150,12 @@ def test_cross_entropy_matches_torch(gpu):
     torch.manual_seed(3)
     z = torch.randn(48, 10, device=gpu, requires_grad=True)
     y = torch.randint(0, 10, (48,), device=gpu)
-    loss, acc = cross_entropy(z, y, with_accuracy=True)
+    loss, acc, err = cross_entropy(z, y, with_accuracy=True, with_error=True)
     z2 = z.detach().clone().requires_grad_(True)
     ref = torch.nn.functional.cross_entropy(z2, y)
     assert torch.allclose(loss, ref, rtol=1e-6, atol=1e-6)
     assert float(acc) == float((z.argmax(1) == y).float().mean())
+    assert float(err) == 1.0 - float(acc)
     loss.backward()
     ref.backward()
     assert torch.allclose(z.grad, z2.grad, rtol=1e-5, atol=1e-7)

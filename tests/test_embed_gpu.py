@@ -39,12 +39,18 @@ def test_forward_and_backward_match_torch(gpu, dtype):
     dy = (torch.randint(-2, 3, (B, S, w.shape[1]), generator=g).float() if integer
           else torch.randn(B, S, w.shape[1], generator=g)).to(gpu).to(dtype)
     out.backward(dy)
-    ref.backward(dy)
-    for a, b in ((w, w2), (t, t2), (p, p2)):
-        if integer:
+    if integer:
+        ref.backward(dy)
+        for a, b in ((w, w2), (t, t2), (p, p2)):
             assert torch.equal(a.grad, b.grad)
-        else:
-            torch.testing.assert_close(a.grad.float(), b.grad.float(), rtol=1e-2, atol=2e-2)
+        return
+    # bf16: each gradient row is summed in fp32 and rounded once, so it must equal the fp32 sum of
+    # the same bf16 gradient rows to bf16 rounding (torch's bf16 backward accumulates with more
+    # rounding; it is not the reference here)
+    w3, t3, p3 = [x.detach().float().requires_grad_(True) for x in (w, t, p)]
+    _ref(ids, tt, w3, t3, p3, 0).backward(dy.float())
+    for a, b in ((w, w3), (t, t3), (p, p3)):
+        torch.testing.assert_close(a.grad.float(), b.grad, rtol=8e-3, atol=1e-6)
 
 
 def test_backward_replays_with_varying_distinct_ids(gpu):
