@@ -176,9 +176,10 @@ def _forward(x: torch.Tensor, params: Sequence[torch.Tensor], ps, training: bool
                          epi=E_BIAS_RELU, out=a1.data_ptr(), out_dt=dt, bias=b1.data_ptr(), bias_dt=dt), split=False))
     # conv2 32->32 + bias + relu + maxpool + dropout2d (window-ordered rows)
     # (not split: 784 tiles already fill the chip; split + finish measured 30 vs 19 us)
-    R.gemm(R.prepare(Job(a=_conv_act(a1, dt, 30, 32, 0, 28, pool=1), b=_wgt(w2, dt, S_WGT_CONV, 32), M=n * 784,
-                         N=32, K=288, epi=E_BIAS_RELU_POOL, out=a2.data_ptr(), out_dt=dt, bias=b2.data_ptr(),
-                         bias_dt=dt, drop=_p(m2), drop_cols=32, idx=idx2.data_ptr(), PH=14, PW=14), split=n * 784 < 16384))
+    R.finish(R.gemm(R.prepare(Job(a=_conv_act(a1, dt, 30, 32, 0, 28, pool=1), b=_wgt(w2, dt, S_WGT_CONV, 32), M=n * 784,
+                                  N=32, K=288, epi=E_BIAS_RELU_POOL, out=a2.data_ptr(), out_dt=dt, bias=b2.data_ptr(),
+                                  bias_dt=dt, drop=_p(m2), drop_cols=32, idx=idx2.data_ptr(), PH=14, PW=14),
+                              split=n * 784 < 16384)))
     # conv3 32->64 pad 1 + bias + relu
     R.finish(R.gemm(R.prepare(Job(a=_conv_act(a2, dt, 14, 32, 1, 14), b=_wgt(w3, dt, S_WGT_CONV, 32), M=n * 196, N=64,
                                   K=288, epi=E_BIAS_RELU, out=a3.data_ptr(), out_dt=dt, bias=b3.data_ptr(), bias_dt=dt))))

@@ -8,7 +8,6 @@ native CNN kernels (no MIOpen), its graphs stay on, and the graph controller det
 half-precision convolutions in its first warm-up step and keeps such a train_batch eager.
 """
 import os
-import sys
 
 import pytest
 import torch
@@ -21,37 +20,34 @@ EX = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "
 
 
 def _run_cifar(amp, hip_graph, batches, seed=3, lr=1e-4):
-    sys.path.insert(0, EX)
-    try:
-        import model_def
-        from determined_1_amd import workload
-        from determined_1_amd.experimental import make_controller
+    from determined_1_amd import workload
+    from determined_1_amd.experimental import load_model_def, make_controller
 
-        cfg = {"hyperparameters": {"global_batch_size": 32, "learning_rate": lr, "train_records": 50000, "amp": amp,
-                                   "learning_rate_decay": 1e-6, "layer1_dropout": 0.25, "layer2_dropout": 0.25,
-                                   "layer3_dropout": 0.5},
-               "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": batches}},
-               "records_per_epoch": 50000, "scheduling_unit": 250,
-               "optimizations": {"hip_graph": hip_graph, "hip_graph_batches": 20}}
-        res = []
+    model_def = load_model_def(EX)  # a uniquely named module: other examples have a model_def too
 
-        def stream():
-            done, step = 0, 1
-            while done < batches:
-                n = min(250, batches - done)
-                yield workload.train_workload(step, num_batches=n, total_batches_processed=done), [], res.append
-                done += n
-                step += 1
-            yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
+    cfg = {"hyperparameters": {"global_batch_size": 32, "learning_rate": lr, "train_records": 50000, "amp": amp,
+                               "learning_rate_decay": 1e-6, "layer1_dropout": 0.25, "layer2_dropout": 0.25,
+                               "layer3_dropout": 0.5},
+           "searcher": {"name": "single", "metric": "validation_error", "max_length": {"batches": batches}},
+           "records_per_epoch": 50000, "scheduling_unit": 250,
+           "optimizations": {"hip_graph": hip_graph, "hip_graph_batches": 20}}
+    res = []
 
-        ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=True, trial_seed=seed)
-        ctrl.run()
-        losses = [r["metrics"]["avg_metrics"]["loss"] for r in res]
-        masters = [a.master for st in ctrl.context._opt_states if st.fused is not None for a in st.fused.arenas]
-        finite = all(bool(torch.isfinite(m).all()) for m in masters)
-        return losses, finite, ctrl._graph.stats() if ctrl._graph is not None else None
-    finally:
-        sys.path.remove(EX)
+    def stream():
+        done, step = 0, 1
+        while done < batches:
+            n = min(250, batches - done)
+            yield workload.train_workload(step, num_batches=n, total_batches_processed=done), [], res.append
+            done += n
+            step += 1
+        yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
+
+    ctrl = make_controller(model_def.CIFARTrial, cfg, stream(), use_gpu=True, trial_seed=seed)
+    ctrl.run()
+    losses = [r["metrics"]["avg_metrics"]["loss"] for r in res]
+    masters = [a.master for st in ctrl.context._opt_states if st.fused is not None for a in st.fused.arenas]
+    finite = all(bool(torch.isfinite(m).all()) for m in masters)
+    return losses, finite, ctrl._graph.stats() if ctrl._graph is not None else None
 
 
 def test_o2_cifar_with_dropout_replays_2000_batches_in_20_batch_chunks_tracking_eager(gpu):
