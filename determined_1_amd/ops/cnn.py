@@ -337,11 +337,14 @@ class _XEnt(torch.autograd.Function):
         ctx.dtype = logits.dtype
         loss, acc, err = out[0], out[1], out[2]
         ctx.mark_non_differentiable(acc, err)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the metrics (two fill launches)
         return loss, acc, err
 
     @staticmethod
     def backward(ctx, gloss, gacc, gerr):  # type: ignore[override]
         z, yy = ctx.saved_tensors
+        if gloss is None:
+            return None, None
         n, c = z.shape
         dz = torch.empty_like(z)
         g = gloss.reshape(1).float().contiguous()
