@@ -113,13 +113,17 @@ class BertLayer(nn.Module):
                 acc: Optional[tfops.SharedWeightGrads] = None) -> torch.Tensor:
         """``acc``: weight-gradient accumulator when this layer is applied repeatedly (ALBERT)."""
         B, S, H = x.shape
-        qkv = tfops.linear(x, self.qkv.weight, self.qkv.bias, acc=acc)  # [B, S, 3H]
+        # x and a are each read by a Linear and as a residual: the two gradients meet in one GEMM
+        lx, la = tfops.ResidualGradLink(), tfops.ResidualGradLink()
+        qkv = tfops.linear(x, self.qkv.weight, self.qkv.bias, acc=acc, link=lx)  # [B, S, 3H]
         ctx = tfops.qkv_self_attention(qkv, self.nh, mask_bias, self.p_attn, self.training)
         a = tfops.linear_dropout_add_layernorm(ctx, self.attn_out.weight, self.attn_out.bias, x, self.attn_ln.weight,
-                                               self.attn_ln.bias, self.p, self.attn_ln.eps, self.training, acc=acc)
-        i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias, self.gelu_approx, acc=acc)
+                                               self.attn_ln.bias, self.p, self.attn_ln.eps, self.training, acc=acc,
+                                               link=lx)
+        i = tfops.linear_gelu(a, self.ffn_in.weight, self.ffn_in.bias, self.gelu_approx, acc=acc, link=la)
         return tfops.linear_dropout_add_layernorm(i, self.ffn_out.weight, self.ffn_out.bias, a, self.ffn_ln.weight,
-                                                  self.ffn_ln.bias, self.p, self.ffn_ln.eps, self.training, acc=acc)
+                                                  self.ffn_ln.bias, self.p, self.ffn_ln.eps, self.training, acc=acc,
+                                                  link=la)
 
 
 class BertForQA(nn.Module):

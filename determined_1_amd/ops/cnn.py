@@ -32,7 +32,8 @@ S_ACT_CONV, S_ACT_FLAT, S_ACT_ROWS, S_GRAD_ROWS, S_GRAD_CONV_T, S_WGT_CONV, S_WG
 # split-K sizing: at least this many workgroups per launch where K allows.  Every pass here is
 # latency-bound (each K tile of a block costs a global round trip, ~2.4 us measured), so the K loop
 # is cut short and spread over more blocks; the finish launch that sums the slabs costs ~5 us.
-BLOCKS_TARGET = int(os.environ.get("DET_CNN_BLOCKS", "1024"))
+# 512: O2 batch-32 trial 0.269 ms/batch vs 0.296 (1024), 0.281 (768), 0.275 (384), r5s19.
+BLOCKS_TARGET = int(os.environ.get("DET_CNN_BLOCKS", "512"))
 DEBUG = {"keep_masks": False, "masks": None}  # tests: the dropout factors of the last forward
 
 

@@ -183,14 +183,23 @@ def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> to
 
 
 def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool,
-                 acc: Optional[SharedWeightGrads] = None):
+                 acc: Optional[SharedWeightGrads] = None, dr: Optional[torch.Tensor] = None):
+    """dr: a gradient of x2 from another use (ResidualGradLink), summed into dx by the GEMM."""
+    if dr is not None and not need_x:
+        raise RuntimeError("a linked residual gradient reached a Linear whose input needs no gradient")
     if need_x and _native_linear(x2, weight) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
         from determined_1_amd.ops.conv import dgrad_1x1
 
         dx = dgrad_1x1(dz, weight)  # dz [M, N] . W [N, K], the weight read as stored
         LINEAR_COUNTS["native_dgrad"] += 1
+        if dr is not None:
+            dx = dx.add_(dr)
+    elif need_x and dr is not None and dr.dtype == dz.dtype and dr.shape == x2.shape and dr.is_contiguous():
+        dx = dr.addmm_(dz, weight)  # dr + dz W: hipBLASLt beta = 1 instead of autograd's separate add
     else:
         dx = dz @ weight if need_x else None
+        if dr is not None:
+            dx = dx + dr.view(dx.shape)
     dw = None
     if need_w:
         dw = acc.accumulate(weight, dz, x2) if acc is not None else _weight_grad(weight, dz, x2)
@@ -214,12 +223,40 @@ def _addmm(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor])
     return torch.addmm(bias, x2, weight.t()) if bias is not None else x2 @ weight.t()
 
 
+class ResidualGradLink:
+    """A tensor read by a Linear and again, later in the forward, as the residual of
+    ``linear_dropout_add_layernorm`` (a BERT layer's input and its attention output).  Autograd
+    computes the two input gradients separately and adds them: one elementwise pass over [rows, H]
+    per use, 24 per BERT-base step (``CUDAFunctor_add`` in profiles/r4_bert_steady.txt).  With a
+    link, the LayerNorm backward -- which runs first -- parks its residual gradient here and the
+    Linear's input-gradient GEMM accumulates onto it (hipBLASLt beta = 1).  The Linear arms the link
+    with its input; the LayerNorm only parks a gradient when its residual is that same tensor."""
+
+    __slots__ = ("x", "dr")
+
+    def __init__(self) -> None:
+        self.x = None  # type: Optional[torch.Tensor]
+        self.dr = None  # type: Optional[torch.Tensor]
+
+    def take(self) -> Optional[torch.Tensor]:
+        dr, self.dr = self.dr, None
+        return dr
+
+
+def _arm(link: Optional[ResidualGradLink], x: torch.Tensor) -> Optional[ResidualGradLink]:
+    if link is None or not (torch.is_grad_enabled() and x.requires_grad):
+        return None
+    link.x, link.dr = x, None
+    return link
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, acc):
+    def forward(ctx, x, weight, bias, acc, link=None):
         x2 = x.reshape(-1, x.shape[-1])
         y = _addmm(x2, weight, bias)
         ctx.acc = acc
+        ctx.link = link
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         ctx.xshape = x.shape
@@ -229,7 +266,8 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x2, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, weight.shape[0]).contiguous()
-        dx, dw = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
+        dr = ctx.link.take() if ctx.link is not None else None
+        dx, dw = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc, dr)
         db = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             lib = _lib.get_lib()
@@ -238,13 +276,14 @@ class _Linear(torch.autograd.Function):
             ws = torch.empty(int(lib.det_tf_col_ws_elems(rows, C)), dtype=torch.float32, device=dy2.device)
             _lib.check(lib.det_tf_colsum(_stream(dy2), _DT[dy2.dtype], dy2.data_ptr(), rows, C, db.data_ptr(),
                                          ws.data_ptr()), "det_tf_colsum")
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None
 
 
 class _LinearGELU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, approx, acc):
+    def forward(ctx, x, weight, bias, approx, acc, link=None):
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.link = link
         z = _addmm(x2, weight, bias)
         a = torch.empty_like(z)
         lib = _lib.get_lib()
@@ -269,8 +308,9 @@ class _LinearGELU(torch.autograd.Function):
                          device=z.device)
         _lib.check(lib.det_tf_gelu_bwd(_stream(z), _DT[z.dtype], da2.data_ptr(), z.data_ptr(), dz.data_ptr(), rows, C,
                                        _ptr(db), ws.data_ptr(), ctx.approx), "det_tf_gelu_bwd")
-        dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
-        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None
+        dr = ctx.link.take() if ctx.link is not None else None
+        dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc, dr)
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None, None
 
 
 def _ln_forward(h: torch.Tensor, r: Optional[torch.Tensor], gamma, beta, p: float, eps: float):
@@ -305,9 +345,11 @@ def _ln_backward(ctx, dy, h, r, gamma, mean, rstd, need_dh: bool, need_dr: bool,
 
 class _LinearDropAddLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, gamma, beta, p, eps, acc):
+    def forward(ctx, x, weight, bias, residual, gamma, beta, p, eps, acc, link=None):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.acc = acc
+        # park the residual gradient for the Linear that read this same tensor (ResidualGradLink)
+        ctx.link = link if link is not None and link.x is residual else None
         h = _addmm(x2, weight, bias)
         r2 = residual.reshape(h.shape).contiguous()
         y, mean, rstd, ctx.seed, ctx.off = _ln_forward(h, r2, gamma, beta, p, eps)
@@ -325,10 +367,12 @@ class _LinearDropAddLN(torch.autograd.Function):
         dh, dr, dgamma, dbeta, dbias = _ln_backward(
             ctx, dy, h, r2, gamma, mean, rstd, need_dh=True, need_dr=ctx.needs_input_grad[3],
             need_bias=ctx.has_bias and ctx.needs_input_grad[2])
+        if ctx.link is not None and dr is not None:
+            ctx.link.dr, dr = dr, None
         dx, dw = (_mm_backward(dh, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
                   if need_h else (None, None))
         return ((dx.view(ctx.xshape) if dx is not None else None), dw, dbias,
-                (dr.view(ctx.rshape) if dr is not None else None), dgamma, dbeta, None, None, None)
+                (dr.view(ctx.rshape) if dr is not None else None), dgamma, dbeta, None, None, None, None)
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -497,28 +541,31 @@ class _Attention(torch.autograd.Function):
 # public functional API (composite reference on CPU / uncovered layouts)
 # ------------------------------------------------------------------------------------------------
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
-           acc: Optional[SharedWeightGrads] = None) -> torch.Tensor:
+           acc: Optional[SharedWeightGrads] = None, link: Optional[ResidualGradLink] = None) -> torch.Tensor:
+    """``link``: x is also a later ``linear_dropout_add_layernorm``'s residual (ResidualGradLink)."""
     (x, weight, bias), ac = _autocast(x, weight, bias)
     if not _native(x, weight, bias, width=weight.shape[0]):
         return F.linear(x, weight, bias)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _Linear.apply(x, weight, bias, _track(acc, weight))
+        return _Linear.apply(x, weight, bias, _track(acc, weight), _arm(link, x))
 
 
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
-                approximate: str = "none", *, acc: Optional[SharedWeightGrads] = None) -> torch.Tensor:
+                approximate: str = "none", *, acc: Optional[SharedWeightGrads] = None,
+                link: Optional[ResidualGradLink] = None) -> torch.Tensor:
     """``gelu(x W^T + b)``; ``approximate="tanh"`` is HF's ``gelu_new`` (ALBERT, GPT-2)."""
     (x, weight, bias), ac = _autocast(x, weight, bias)
     if not _native(x, weight, bias, width=weight.shape[0]):
         return F.gelu(F.linear(x, weight, bias), approximate=approximate)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _LinearGELU.apply(x, weight, bias, approximate == "tanh", _track(acc, weight))
+        return _LinearGELU.apply(x, weight, bias, approximate == "tanh", _track(acc, weight), _arm(link, x))
 
 
 def linear_dropout_add_layernorm(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
                                  residual: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, p: float = 0.0,
                                  eps: float = 1e-12, training: bool = True, *,
-                                 acc: Optional[SharedWeightGrads] = None) -> torch.Tensor:
+                                 acc: Optional[SharedWeightGrads] = None,
+                                 link: Optional[ResidualGradLink] = None) -> torch.Tensor:
     """``LayerNorm(dropout(x W^T + b) + residual)`` — BERT's SelfOutput / Output block."""
     p = float(p) if training else 0.0
     (x, weight, bias, residual, gamma, beta), ac = _autocast(x, weight, bias, residual, gamma, beta)
@@ -526,7 +573,7 @@ def linear_dropout_add_layernorm(x: torch.Tensor, weight: torch.Tensor, bias: Op
         h = F.dropout(F.linear(x, weight, bias), p, training)
         return F.layer_norm(h + residual, (weight.shape[0],), gamma, beta, eps)
     with torch.autocast("cuda", enabled=False) if ac else _null():
-        return _LinearDropAddLN.apply(x, weight, bias, residual, gamma, beta, p, float(eps), _track(acc, weight))
+        return _LinearDropAddLN.apply(x, weight, bias, residual, gamma, beta, p, float(eps), _track(acc, weight), link)
 
 
 def layer_norm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:

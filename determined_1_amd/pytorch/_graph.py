@@ -47,6 +47,10 @@ WARMUP = 2        # eager batches per key before capturing (lazy init, MIOpen fi
 MAX_GRAPHS = 2    # live graphs (the epoch's full batch + its tail batch)
 THRASH_LIMIT = 8  # captures that replayed fewer than THRASH_MIN times -> graphs off
 THRASH_MIN = 4
+# Captured steps keep the arena GradSink (ops/arena.py): each window's gradients land in the arena
+# with one copy launch per group (tables written by GradSink.finish_capture) instead of one
+# `grad += new` launch per parameter (~180 per BERT-base step, 0.9 ms in the r5s20 graph profile).
+GRAPH_SINK = os.environ.get("DET_GRAPH_SINK", "1") != "0"
 
 
 @contextlib.contextmanager
@@ -177,12 +181,11 @@ class TrainStepGraph:
         self.epoch_sensitive = reads_argument(train_batch, "epoch_idx") if epoch_sensitive is None \
             else epoch_sensitive
         self.fused = [st.fused for st in context._opt_states if st.fused is not None]
-        for f in self.fused:
-            # in a graph the per-parameter accumulate launches cost nothing on the host, and the
-            # sink's host-staged pointer tables are not replay-safe: plain arena accumulation
-            if f.sink is not None:
-                f.sink.detach()
-                f.sink = None
+        if not GRAPH_SINK:
+            for f in self.fused:  # plain arena accumulation: one `grad += new` launch per parameter
+                if f.sink is not None:
+                    f.sink.detach()
+                    f.sink = None
         self.graphs: Dict[Any, _Graph] = {}
         self.seen: Dict[Any, int] = {}
         self.captures = 0
@@ -304,16 +307,23 @@ class TrainStepGraph:
                 for f in self.fused:
                     f.capturing(False)
         except Exception as e:  # capture-unsafe op in user code or a library: stay eager
+            self._finish_sinks(False)
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
             self.failed_captures += 1
             self._disable(f"capture failed: {type(e).__name__}: {e}")
             torch.cuda.synchronize()
             return None
+        self._finish_sinks(True)
         self.captures += 1
         g = _Graph(graph, static_in, spec, out)
         self.graphs[key] = g
         return g
+
+    def _finish_sinks(self, ok: bool) -> None:
+        for f in self.fused:
+            if f.sink is not None:
+                f.sink.finish_capture(ok)
 
     def _disable(self, reason: str) -> None:
         if self.disabled_reason is None:
@@ -399,12 +409,14 @@ class TrainStepGraph:
                     raise TypeError("train_batch metric names differ between batches")
                 out = {k: torch.stack([o[k].detach().float() for o in outs]) for k in names}
         except Exception as e:  # noqa: BLE001 - stay on per-batch replays
+            self._finish_sinks(False)
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
             self.chunk_disabled = f"{type(e).__name__}: {e}"
             logging.warning("hip_graph: multi-batch capture failed, replaying per batch: %s", self.chunk_disabled)
             torch.cuda.synchronize()
             return None
+        self._finish_sinks(True)
         self.captures += 1
         g = _Graph(graph, static_in, spec, out)
         self.chunk_graphs[key] = g
