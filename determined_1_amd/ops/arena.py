@@ -200,8 +200,7 @@ class GradSink:
         self._keep = []  # type: List[torch.Tensor]
         self._landing_taken = set()  # type: set  # (group, index) slots handed out by landing_buffer
         self._tables = {}  # type: Dict[int, Any]
-        self._capture_tables = []  # type: List[Tuple[torch.Tensor, List[int]]]  # filled by finish_capture
-        self._graph_tables = []  # type: List[torch.Tensor]  # read by captured graphs at every replay
+        self.captured_flushes = 0  # landing copies recorded into hipGraphs (foreach copies)
         self._handles = []
         # per parameter, everything the hook compares against (one dict lookup instead of ~10
         # tensor attribute reads per parameter per backward: the hook runs 150-160 times a step)
@@ -282,7 +281,16 @@ class GradSink:
         stolen = self._stolen[gi]
         self._stolen[gi] = []
         if stolen:
-            if a.flat_grad.device.type == "cuda":
+            if a.flat_grad.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+                # under hipGraph capture: a multi-tensor copy whose pointers travel as kernel
+                # arguments.  A device pointer table allocated in the capture gets an address the
+                # graph's private pool already gave a tensor freed earlier in the same step, so a
+                # replay's forward overwrites it before the copy reads it (r5s22: the table written
+                # once after capture faulted the first replay)
+                with torch.no_grad():
+                    torch._foreach_copy_([a.grad_views[i] for i, _ in stolen], [g for _, g in stolen])
+                self.captured_flushes += 1
+            elif a.flat_grad.device.type == "cuda":
                 from determined_1_amd.ops import _lib
                 from determined_1_amd.ops.functional import dtype_code
 
@@ -305,26 +313,8 @@ class GradSink:
         for fn in self.listeners:
             fn(gi)
 
-    def finish_capture(self, ok: bool = True) -> None:
-        """After a hipGraph capture (pytorch/_graph.py): write the pointer tables the captured copies
-        read.  Under capture every pointer is final (the graph's private pool fixes them), so each
-        table is written once here, before the first replay, instead of through a host staging
-        buffer that a replay would re-read after it was reused."""
-        pending, self._capture_tables = self._capture_tables, []
-        if not ok:
-            dead = {id(dev) for dev, _ in pending}
-            self._graph_tables = [t for t in self._graph_tables if id(t) not in dead]
-            return
-        for dev, rows in pending:
-            dev.copy_(torch.tensor(rows, dtype=torch.int64))
-
     def _table(self, gi: int, rows: List[int], device: torch.device) -> torch.Tensor:
         """Upload the pointer table through a double-buffered pinned staging area."""
-        if torch.cuda.is_current_stream_capturing():
-            dev = torch.empty(len(rows), dtype=torch.int64, device=device)  # written by finish_capture
-            self._capture_tables.append((dev, rows))
-            self._graph_tables.append(dev)
-            return dev
         slot = self._tables.get(gi)
         n = len(rows)
         if slot is None or slot["cap"] < n:

@@ -1,0 +1,64 @@
+"""Measured vendor-BLAS solutions for the GEMMs that stay on hipBLASLt / rocBLAS (MI355X, gfx950).
+
+The dense layers of the transformer models (ops/transformer.py: BERT, ALBERT) multiply through
+``torch.addmm`` / ``torch.mm``, which take the solution the library heuristic picks for a shape.
+PyTorch's TunableOp can time every hipBLASLt and rocBLAS solution of a shape and keep the fastest;
+the winners for the shapes the framework's models run are measured once on an MI355X
+(``scripts/tune_gemms.py``) and shipped in ``tuned/gemm_gfx950.csv``.  A GPU trial loads that file
+read-only at start-up: nothing is tuned at run time (a timing sweep inside a train step would stall
+it and cannot run under hipGraph capture), and shapes the file does not list keep the heuristic.
+The file's validator lines pin the torch / HIP / hipBLASLt / rocBLAS versions and the GPU arch it
+was measured with; TunableOp ignores it on any other stack.
+
+Measured (round 5, r5s21, BERT-base SQuAD bs12 O2): eager 1245 -> 1360 ex/s; the weight-gradient
+GEMMs (reduction over the 4608 tokens) move to rocBLAS solutions, the forward ones stay on
+hipBLASLt.  ``DET_TUNED_GEMMS=0`` turns it off; ``DET_TUNED_GEMMS=<path>`` loads another file.
+"""
+import logging
+import os
+import tempfile
+from typing import Dict, Optional
+
+import torch
+
+SHIPPED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "gemm_gfx950.csv")
+_STATE = {"loaded": None}  # type: Dict[str, Optional[bool]]
+
+
+def enable(path: Optional[str] = None) -> bool:
+    """Load the measured solutions (once per process).  True when TunableOp now serves them."""
+    if _STATE["loaded"] is not None:
+        return bool(_STATE["loaded"])
+    env = os.environ.get("DET_TUNED_GEMMS", "1")
+    if env == "0" or not torch.cuda.is_available():
+        _STATE["loaded"] = False
+        return False
+    src = path or (env if env not in ("", "1") else SHIPPED)
+    arch = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+    if not os.path.exists(src) or not arch.startswith("gfx950"):
+        _STATE["loaded"] = False
+        return False
+    from torch.cuda import tunable
+
+    # results TunableOp may write at exit go to a scratch file, never over the shipped one
+    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"det_tunableop_{os.getpid()}.csv"))
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    ok = bool(tunable.read_file(src))
+    if not ok:
+        logging.warning("tuned GEMM file %s was not accepted (other torch/ROCm stack?): library heuristics", src)
+        tunable.enable(False)
+    _STATE["loaded"] = ok
+    return ok
+
+
+def entries(path: str = SHIPPED) -> Dict[str, str]:
+    """``{op,shape: solution}`` of a TunableOp results file (validator lines skipped)."""
+    out = {}
+    with open(path) as f:
+        for line in f:
+            parts = line.strip().split(",")
+            if len(parts) >= 3 and parts[0] != "Validator":
+                out[parts[0] + "," + parts[1]] = parts[2]
+    return out

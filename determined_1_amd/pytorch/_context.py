@@ -106,6 +106,10 @@ class PyTorchTrialContext(trial.TrialContext):
             self.device = torch.device("cuda", 0)
         else:
             self.device = torch.device("cpu")
+        if self.device.type == "cuda":
+            from determined_1_amd.ops import gemm_tuning
+
+            gemm_tuning.enable()  # measured hipBLASLt / rocBLAS solutions of the library GEMMs
 
     def to_device(self, data: Any) -> TorchData:
         return to_device(data, self.device, self._to_device_warned_types)

@@ -341,6 +341,20 @@ def _record_stream(data: Any, stream: Any) -> None:
             _record_stream(v, stream)
 
 
+def shutdown_iterator(it: Any) -> None:
+    """Stop the worker processes behind a (wrapped) torch DataLoader iterator.  A trial's training
+    iterator repeats forever, so torch never reaches the end that shuts its workers down; left to
+    the garbage collector, the shutdown (a join per worker) lands inside whatever runs next."""
+    for _ in range(4):
+        if it is None:
+            return
+        stop = getattr(it, "_shutdown_workers", None)
+        if callable(stop):
+            stop()
+            return
+        it = getattr(it, "_it", None)
+
+
 class DevicePrefetcher:
     """Iterator adaptor: pulls host batches (collation happens in DataLoader workers when
     ``num_workers > 0``) and issues their pinned H2D copies on a dedicated HIP stream ``depth``

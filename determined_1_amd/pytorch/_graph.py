@@ -48,8 +48,8 @@ MAX_GRAPHS = 2    # live graphs (the epoch's full batch + its tail batch)
 THRASH_LIMIT = 8  # captures that replayed fewer than THRASH_MIN times -> graphs off
 THRASH_MIN = 4
 # Captured steps keep the arena GradSink (ops/arena.py): each window's gradients land in the arena
-# with one copy launch per group (tables written by GradSink.finish_capture) instead of one
-# `grad += new` launch per parameter (~180 per BERT-base step, 0.9 ms in the r5s20 graph profile).
+# through one multi-tensor copy per group instead of one `grad += new` launch per parameter (~180 per
+# BERT-base step, 0.9 ms in the r5s20 graph profile).
 GRAPH_SINK = os.environ.get("DET_GRAPH_SINK", "1") != "0"
 
 
@@ -307,23 +307,16 @@ class TrainStepGraph:
                 for f in self.fused:
                     f.capturing(False)
         except Exception as e:  # capture-unsafe op in user code or a library: stay eager
-            self._finish_sinks(False)
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
             self.failed_captures += 1
             self._disable(f"capture failed: {type(e).__name__}: {e}")
             torch.cuda.synchronize()
             return None
-        self._finish_sinks(True)
         self.captures += 1
         g = _Graph(graph, static_in, spec, out)
         self.graphs[key] = g
         return g
-
-    def _finish_sinks(self, ok: bool) -> None:
-        for f in self.fused:
-            if f.sink is not None:
-                f.sink.finish_capture(ok)
 
     def _disable(self, reason: str) -> None:
         if self.disabled_reason is None:
@@ -409,14 +402,12 @@ class TrainStepGraph:
                     raise TypeError("train_batch metric names differ between batches")
                 out = {k: torch.stack([o[k].detach().float() for o in outs]) for k in names}
         except Exception as e:  # noqa: BLE001 - stay on per-batch replays
-            self._finish_sinks(False)
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
             self.chunk_disabled = f"{type(e).__name__}: {e}"
             logging.warning("hip_graph: multi-batch capture failed, replaying per batch: %s", self.chunk_disabled)
             torch.cuda.synchronize()
             return None
-        self._finish_sinks(True)
         self.captures += 1
         g = _Graph(graph, static_in, spec, out)
         self.chunk_graphs[key] = g

@@ -79,9 +79,12 @@ def test_graph_replay_matches_eager(gpu, monkeypatch, hp):
     assert g is not None and g.disabled_reason is None, g and g.stats()
     st = g.stats()
     assert st["captures"] >= 1 and st["replays"] >= 12, st
-    # captured steps land their gradients through the arena GradSink (tables written after capture)
+    # captured steps land their gradients through the arena GradSink (multi-tensor copies)
+    from determined_1_amd.pytorch import _graph
+
     sinks = [s.fused.sink for s in ctrl.context._opt_states if s.fused is not None]
-    assert sinks and all(s is not None and s._graph_tables for s in sinks), sinks
+    if _graph.GRAPH_SINK:
+        assert sinks and all(s is not None and s.captured_flushes > 0 for s in sinks), sinks
     if hp.get("lr_step"):
         assert st["captures"] >= 2  # the epoch boundary (10 batches) changes lr -> new key
     if hp["opt"] == "adam":

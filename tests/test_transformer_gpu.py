@@ -313,3 +313,22 @@ def test_residual_gradient_link_sums_in_the_gemm(gpu, monkeypatch):
     torch.testing.assert_close(outs[True][0], outs[False][0], rtol=1e-5, atol=1e-5)
     for k in outs[False][1]:
         torch.testing.assert_close(outs[True][1][k], outs[False][1][k], rtol=1e-5, atol=1e-5, msg=k)
+
+
+def test_tuned_gemm_solutions_load_and_keep_numerics(gpu):
+    """The measured hipBLASLt / rocBLAS solutions (ops/gemm_tuning.py) load read-only on gfx950, and
+    the tuned weight-gradient shape of BERT-base (reduction over 4608 tokens) stays within bf16
+    accuracy of the fp32 product."""
+    from determined_1_amd.ops import gemm_tuning
+
+    assert gemm_tuning.enable()
+    assert torch.cuda.tunable.is_enabled() and not torch.cuda.tunable.tuning_is_enabled()
+    g = torch.Generator(device=gpu).manual_seed(0)
+    dz = torch.randn(4608, 3072, device=gpu, generator=g).to(torch.bfloat16)
+    x = torch.randn(4608, 768, device=gpu, generator=g).to(torch.bfloat16)
+    w = dz.t() @ x
+    ref = dz.float().t() @ x.float()
+    assert float((w.float() - ref).norm() / ref.norm()) < 1e-2
+    y = torch.addmm(torch.zeros(2304, device=gpu, dtype=torch.bfloat16), x, torch.randn(2304, 768, device=gpu,
+                    generator=g).to(torch.bfloat16).t())
+    assert bool(torch.isfinite(y).all())
