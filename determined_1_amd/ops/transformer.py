@@ -154,13 +154,26 @@ class SharedWeightGrads:
         return out
 
 
-# Dense layers on the hand-written det_conv.hip GEMMs instead of hipBLASLt (A/B switch, see module doc)
-NATIVE_LINEAR = os.environ.get("DET_NATIVE_LINEAR", "0") == "1"
+# Dense layers on the hand-written det_conv.hip GEMMs instead of the vendor BLAS.
+#   "1": every pass;  "0": none;  "auto" (default): the forward and input-gradient GEMMs of small
+#   weights (<= NATIVE_AUTO_MAX_WEIGHT elements), where the tiles beat the (tuned) library: BERT-base's
+#   768x768 attention output at 4608 tokens, forward 14.1 vs 23.9 us, input gradient 13.4 vs 26.5 us;
+#   the 768x2304 / 768x3072 layers and every weight gradient stay on the library, which wins there
+#   (profiles/r5_bert_linear_shapes.json, scripts/bench_linear_shapes.py).
+NATIVE_LINEAR = os.environ.get("DET_NATIVE_LINEAR", "auto")
+NATIVE_AUTO_MAX_WEIGHT = 1 << 20
 LINEAR_COUNTS = {"native_fwd": 0, "native_dgrad": 0, "native_wgrad": 0}
 
 
-def _native_linear(x2: torch.Tensor, weight: torch.Tensor) -> bool:
-    return (NATIVE_LINEAR and x2.is_cuda and x2.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+def _native_linear(x2: torch.Tensor, weight: torch.Tensor, wgrad: bool = False) -> bool:
+    mode = NATIVE_LINEAR
+    if mode is True or mode == "1":
+        on = True
+    elif mode == "auto":
+        on = not wgrad and weight.numel() <= NATIVE_AUTO_MAX_WEIGHT
+    else:
+        on = False
+    return (on and x2.is_cuda and x2.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and x2.dim() == 2 and x2.is_contiguous() and weight.is_contiguous() and weight.shape[0] % 64 == 0
             and weight.shape[1] % 64 == 0 and x2.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
 
@@ -169,7 +182,7 @@ def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> to
     """dW = dz^T x, written straight into the parameter's gradient-arena slot when that is where
     it will land (ops.arena.landing_buffer): no separate landing copy for the largest gradients."""
     buf = landing_buffer(weight) if weight.is_cuda else None
-    if _native_linear(x2, weight) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
+    if _native_linear(x2, weight, wgrad=True) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
         from determined_1_amd.ops.conv import conv1x1_wgrad
 
         out = buf if (buf is not None and buf.dtype in (torch.bfloat16, torch.float32) and buf.is_contiguous()) \
