@@ -954,10 +954,11 @@ bool launch_kinds(const Launch& L, bool has1, int blocks, hipStream_t st) {
 constexpr int kMaxFin = 4;
 struct FinishLaunch {
   Job job[kMaxFin];
-  int64_t first[kMaxFin];
+  // lanes of job j: [lfirst[j], lfirst[j + 1]), its output elements x tpe[j], padded to whole waves so a
+  // wave never straddles two jobs (the group sums shuffle within a wave)
+  int64_t lfirst[kMaxFin + 1];
+  int tpe[kMaxFin];  // lanes per output element of each job (power of two <= 32): they split its slab sum
   int njobs;
-  int tpe;  // threads per output element (power of two <= 32): they split the slab sum
-  int64_t total;
 };
 
 // sum of the slabs of (m, n) taken by lane `sub` of a group of T: 4 independent partial sums
@@ -982,27 +983,32 @@ __device__ __forceinline__ float group_sum(float v, int T) {
 }
 
 __global__ void __launch_bounds__(NT) cnn_finish_kernel(FinishLaunch L) {
-  // T adjacent lanes per output element, each summing every T-th slab (the weight-gradient slabs
-  // run to ~200 splits: one lane per element left that sum a serial chain of load latencies)
-  const int T = L.tpe;
-  const int sub = threadIdx.x & (T - 1);
-  const int64_t groups = static_cast<int64_t>(gridDim.x) * (NT / T);
-  for (int64_t e = (static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x) / T; e < L.total; e += groups) {
+  // T adjacent lanes per output element, each summing every T-th slab, with T sized per job: the
+  // weight-gradient slabs run to ~450 splits (one lane per element would be a serial chain of load
+  // latencies) while an input gradient finished in the same launch has a handful
+  const int64_t total = L.lfirst[L.njobs];
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * NT;
+  for (int64_t gl = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x; gl < total; gl += stride) {
     int ji = 0;
-    while (ji + 1 < L.njobs && e >= L.first[ji + 1]) ++ji;
+    while (ji + 1 < L.njobs && gl >= L.lfirst[ji + 1]) ++ji;
     const Job& J = L.job[ji];
-    const int64_t i = e - L.first[ji];
-    if (J.epi == E_BIAS_RELU_POOL) {  // i = (window, n): the window's 4 rows summed, then pooled
-      const int64_t win = i / J.N, n = i - win * J.N;
-      const float s0 = group_sum(slab_part(J, 4 * win, n, sub, T), T);
-      const float s1 = group_sum(slab_part(J, 4 * win + 1, n, sub, T), T);
-      const float s2 = group_sum(slab_part(J, 4 * win + 2, n, sub, T), T);
-      const float s3 = group_sum(slab_part(J, 4 * win + 3, n, sub, T), T);
-      if (sub == 0) pool_store(J, static_cast<uint32_t>(win), n, s0, s1, s2, s3);
+    const int T = L.tpe[ji];
+    const int64_t rel = gl - L.lfirst[ji];
+    const int sub = static_cast<int>(rel & (T - 1));
+    const int64_t e = rel / T;
+    if (J.epi == E_BIAS_RELU_POOL) {  // e = (window, n): the window's 4 rows summed, then pooled
+      const bool act = e < (J.M / 4) * J.N;
+      const int64_t win = act ? e / J.N : 0, n = act ? e - win * J.N : 0;
+      const float s0 = group_sum(act ? slab_part(J, 4 * win, n, sub, T) : 0.f, T);
+      const float s1 = group_sum(act ? slab_part(J, 4 * win + 1, n, sub, T) : 0.f, T);
+      const float s2 = group_sum(act ? slab_part(J, 4 * win + 2, n, sub, T) : 0.f, T);
+      const float s3 = group_sum(act ? slab_part(J, 4 * win + 3, n, sub, T) : 0.f, T);
+      if (act && sub == 0) pool_store(J, static_cast<uint32_t>(win), n, s0, s1, s2, s3);
     } else {
-      const int64_t m = i / J.N, n = i - m * J.N;
-      const float sum = group_sum(slab_part(J, m, n, sub, T), T);
-      if (sub == 0) epi_store(J, m, n, sum);
+      const bool act = e < J.M * J.N;
+      const int64_t m = act ? e / J.N : 0, n = act ? e - m * J.N : 0;
+      const float sum = group_sum(act ? slab_part(J, m, n, sub, T) : 0.f, T);
+      if (act && sub == 0) epi_store(J, m, n, sum);
     }
   }
 }
@@ -1227,24 +1233,23 @@ int det_cnn_gemm(void* stream, int32_t bf16, const DetCnnJob* j0, const DetCnnJo
 int det_cnn_finish(void* stream, const DetCnnJob* jobs, int32_t njobs) {
   if (njobs < 1 || njobs > kMaxFin) return static_cast<int>(hipErrorInvalidValue);
   FinishLaunch L;
-  int64_t total = 0;
+  int64_t lanes = 0;
   for (int i = 0; i < njobs; ++i) {
     if (fill_job(jobs[i], &L.job[i]) <= 0 || L.job[i].splits < 2) return static_cast<int>(hipErrorInvalidValue);
-    L.first[i] = total;
-    total += (L.job[i].epi == E_BIAS_RELU_POOL ? L.job[i].M / 4 : L.job[i].M) * L.job[i].N;
+    int T = 1;
+    while (T < 32 && T * 8 < L.job[i].splits) T <<= 1;  // ~8 slabs per lane
+    L.tpe[i] = T;
+    L.lfirst[i] = lanes;
+    const int64_t nel = (L.job[i].epi == E_BIAS_RELU_POOL ? L.job[i].M / 4 : L.job[i].M) * L.job[i].N;
+    lanes += (nel * T + 63) / 64 * 64;
   }
   for (int i = njobs; i < kMaxFin; ++i) {
     L.job[i] = L.job[0];
-    L.first[i] = total;
+    L.tpe[i] = 1;
   }
+  for (int i = njobs; i <= kMaxFin; ++i) L.lfirst[i] = lanes;
   L.njobs = njobs;
-  L.total = total;
-  int maxs = 1;
-  for (int i = 0; i < njobs; ++i) maxs = L.job[i].splits > maxs ? L.job[i].splits : maxs;
-  int T = 1;
-  while (T < 32 && T * 8 < maxs) T <<= 1;  // ~8 slabs per lane
-  L.tpe = T;
-  int64_t want = (total * T + NT - 1) / NT;
+  int64_t want = (lanes + NT - 1) / NT;
   const int blocks = static_cast<int>(want > 2048 ? 2048 : want);
   cnn_finish_kernel<<<blocks, NT, 0, static_cast<hipStream_t>(stream)>>>(L);
   return static_cast<int>(hipGetLastError());

@@ -30,6 +30,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -166,8 +168,10 @@ struct LnArgs {
 // ---------------------------------------------------------------------------------------------
 // y = LN(dropout(h) + r): one wave per row, grid-stride over rows.
 // ---------------------------------------------------------------------------------------------
-template <typename T, int K>
+template <typename T, int K, int R = 1>
 __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(LnArgs a) {
+  // R rows per wave per iteration: their loads are all in flight before the first reduction (a row
+  // of BERT-base is 3 loads per lane, too little to cover the memory latency on its own)
   const int lane = threadIdx.x & 63;
   const int H4 = a.H >> 2;
   const T* h = static_cast<const T*>(a.h);
@@ -186,61 +190,74 @@ __global__ void __launch_bounds__(kThreads) ln_fwd_kernel(LnArgs a) {
     }
   }
   const float inv_h = 1.f / static_cast<float>(a.H);
-  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6); row < a.rows;
-       row += static_cast<int64_t>(gridDim.x) * kWaves) {
-    const int64_t base = row * a.H;
-    float v[K][4];
-    float s = 0.f;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kWaves;
+  for (int64_t row0 = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6); row0 < a.rows;
+       row0 += stride * R) {
+    float v[R][K][4];
+    float s[R];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < H4) {
-        V4<T>::load(h + base + 4 * c4, v[i]);
-        if (a.dropout) {
-          float m[4];
-          drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m);
+    for (int q = 0; q < R; ++q) {
+      const int64_t row = row0 + q * stride;
+      const bool ok = row < a.rows;
+      const int64_t base = (ok ? row : 0) * a.H;
+      s[q] = 0.f;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[i][j] *= m[j];
+      for (int i = 0; i < K; ++i) {
+        const int c4 = lane + 64 * i;
+        if (ok && c4 < H4) {
+          V4<T>::load(h + base + 4 * c4, v[q][i]);
+          if (a.dropout) {
+            float m[4];
+            drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[q][i][j] *= m[j];
+          }
+          if (r) {
+            float t[4];
+            V4<T>::load(r + base + 4 * c4, t);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[q][i][j] += t[j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[q][i][j] = 0.f;
         }
-        if (r) {
-          float t[4];
-          V4<T>::load(r + base + 4 * c4, t);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[i][j] += t[j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] = 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s += v[i][j];
-    }
-    const float mean = wave_sum(s) * inv_h;
-    float s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-      if (lane + 64 * i < H4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float d = v[i][j] - mean;
-          s2 += d * d;
-        }
+        for (int j = 0; j < 4; ++j) s[q] += v[q][i][j];
       }
     }
-    const float rstd = rsqrtf(wave_sum(s2) * inv_h + a.eps);
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < H4) {
-        float o[4];
+    for (int q = 0; q < R; ++q) {
+      const int64_t row = row0 + q * stride;
+      const float mean = wave_sum(s[q]) * inv_h;
+      float s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[i][j] + b[i][j];
-        V4<T>::store(y + base + 4 * c4, o);
+      for (int i = 0; i < K; ++i) {
+        if (lane + 64 * i < H4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = v[q][i][j] - mean;
+            s2 += d * d;
+          }
+        }
       }
-    }
-    if (lane == 0) {
-      a.mean[row] = mean;
-      a.rstd[row] = rstd;
+      const float rstd = rsqrtf(wave_sum(s2) * inv_h + a.eps);
+      if (row >= a.rows) continue;
+      const int64_t base = row * a.H;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < H4) {
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (v[q][i][j] - mean) * rstd * g[i][j] + b[i][j];
+          V4<T>::store(y + base + 4 * c4, o);
+        }
+      }
+      if (lane == 0) {
+        a.mean[row] = mean;
+        a.rstd[row] = rstd;
+      }
     }
   }
 }
@@ -261,10 +278,11 @@ struct LnBwdArgs {
   Rng rng;
 };
 
-template <typename T, int K>
+template <typename T, int K, int R = 1>
 __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
   // H <= 2048 (K <= 8): dy, xhat and the dropout factors of the row stay in registers between the
-  // two passes; wider rows use ln_bwd_wide.
+  // two passes; wider rows use ln_bwd_wide.  R rows per wave per iteration, their loads all issued
+  // before the first reduction.
   extern __shared__ float red[];  // [kWaves][H]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int H4 = a.H >> 2;
@@ -285,62 +303,80 @@ __global__ void __launch_bounds__(kThreads) ln_bwd_kernel(LnBwdArgs a) {
     }
   }
   const float inv_h = 1.f / static_cast<float>(a.H);
-  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wave; row < a.rows;
-       row += static_cast<int64_t>(gridDim.x) * kWaves) {
-    const int64_t base = row * a.H;
-    const float mean = a.mean[row], rstd = a.rstd[row];
-    float d[K][4], xh[K][4], m[K][4];
-    float s1 = 0.f, s2 = 0.f;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kWaves;
+  for (int64_t row0 = static_cast<int64_t>(blockIdx.x) * kWaves + wave; row0 < a.rows; row0 += stride * R) {
+    float d[R][K][4], hv[R][K][4], rv[R][K][4];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < H4) {
-        float z[4];  // z = dropout(h) + r
-        V4<T>::load(dy + base + 4 * c4, d[i]);
-        V4<T>::load(h + base + 4 * c4, z);
-        if (a.dropout) {
-          drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m[i]);
+    for (int q = 0; q < R; ++q) {
+      const int64_t row = row0 + q * stride;
+      const bool ok = row < a.rows;
+      const int64_t base = (ok ? row : 0) * a.H;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) z[j] *= m[i][j];
+      for (int i = 0; i < K; ++i) {
+        const int c4 = lane + 64 * i;
+        if (ok && c4 < H4) {
+          V4<T>::load(dy + base + 4 * c4, d[q][i]);
+          V4<T>::load(h + base + 4 * c4, hv[q][i]);
+          if (r) V4<T>::load(r + base + 4 * c4, rv[q][i]);
+          else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rv[q][i][j] = 0.f;
+          }
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) m[i][j] = 1.f;
+          for (int j = 0; j < 4; ++j) d[q][i][j] = hv[q][i][j] = rv[q][i][j] = 0.f;
         }
-        if (r) {
-          float t[4];
-          V4<T>::load(r + base + 4 * c4, t);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) z[j] += t[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          xh[i][j] = (z[j] - mean) * rstd;
-          const float dx = d[i][j] * g[i][j];
-          s1 += dx;
-          s2 += dx * xh[i][j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[i][j] = xh[i][j] = m[i][j] = 0.f;
       }
     }
-    s1 = wave_sum(s1) * inv_h;
-    s2 = wave_sum(s2) * inv_h;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < H4) {
-        float dz[4], dhv[4];
+    for (int q = 0; q < R; ++q) {
+      const int64_t row = row0 + q * stride;
+      if (row >= a.rows) continue;  // uniform across the wave
+      const int64_t base = row * a.H;
+      const float mean = a.mean[row], rstd = a.rstd[row];
+      float xh[K][4], m[K][4];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dz[j] = rstd * (d[i][j] * g[i][j] - s1 - xh[i][j] * s2);
-          dhv[j] = dz[j] * m[i][j];
-          adg[i][j] += d[i][j] * xh[i][j];
-          adb[i][j] += d[i][j];
-          adh[i][j] += dhv[j];
+      for (int i = 0; i < K; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < H4) {
+          if (a.dropout) {
+            drop_factors(static_cast<uint64_t>(row) * H4 + c4, a.rng, m[i]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[i][j] = 1.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float z = hv[q][i][j] * m[i][j] + rv[q][i][j];  // z = dropout(h) + r
+            xh[i][j] = (z - mean) * rstd;
+            const float dx = d[q][i][j] * g[i][j];
+            s1 += dx;
+            s2 += dx * xh[i][j];
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) xh[i][j] = m[i][j] = 0.f;
         }
-        if (dr) V4<T>::store(dr + base + 4 * c4, dz);
-        if (dh) V4<T>::store(dh + base + 4 * c4, dhv);
+      }
+      s1 = wave_sum(s1) * inv_h;
+      s2 = wave_sum(s2) * inv_h;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < H4) {
+          float dz[4], dhv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            dz[j] = rstd * (d[q][i][j] * g[i][j] - s1 - xh[i][j] * s2);
+            dhv[j] = dz[j] * m[i][j];
+            adg[i][j] += d[q][i][j] * xh[i][j];
+            adb[i][j] += d[q][i][j];
+            adh[i][j] += dhv[j];
+          }
+          if (dr) V4<T>::store(dr + base + 4 * c4, dz);
+          if (dh) V4<T>::store(dh + base + 4 * c4, dhv);
+        }
       }
     }
   }
@@ -748,9 +784,34 @@ Rng make_rng(float p, uint64_t seed, uint64_t offset, const uint32_t* obase) {
 
 int ln_k(int H) { return (H / 4 + 63) / 64; }
 
+// rows per wave per iteration of the wave-per-row LayerNorm kernels (DET_LN_ROWS, 1 or 2) and
+// whether H % 8 == 0 rows up to 2048 take them for the forward instead of a workgroup per row
+// (DET_LN_FWD=narrow|wide)
+int ln_rows_per_wave() {
+  static const int r = [] {
+    const char* e = std::getenv("DET_LN_ROWS");
+    return (e != nullptr && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  return r;
+}
+bool ln_fwd_narrow() {
+  static const bool n = [] {
+    const char* e = std::getenv("DET_LN_FWD");
+    return e != nullptr && std::strcmp(e, "narrow") == 0;
+  }();
+  return n;
+}
+
+// workgroups of the LayerNorm backward (each writes one partial row of dgamma / dbeta / dbias):
+// at most DET_LN_BWD_BLOCKS (default 512)
 int64_t ln_bwd_blocks(int64_t rows) {
+  static const int64_t cap = [] {
+    const char* e = std::getenv("DET_LN_BWD_BLOCKS");
+    const int64_t v = e != nullptr ? std::atoll(e) : 0;
+    return v > 0 ? v : int64_t{512};
+  }();
   int64_t b = (rows + kWaves - 1) / kWaves;
-  return b < 512 ? b : 512;
+  return b < cap ? b : cap;
 }
 
 int grid_for(int64_t work, int per_block) {
@@ -776,7 +837,8 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
   if (H % 4 != 0 || H > kMaxH || rows <= 0) return -1;
   LnArgs a{h, r, y, gamma, beta, mean, rstd, rows, H, eps, p > 0.f, make_rng(p, seed, offset, obase)};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (H % 8 == 0) {  // workgroup per row (128 / 256 / 512 threads of 8 columns each)
+  const int R = ln_rows_per_wave();
+  if (H % 8 == 0 && !(ln_fwd_narrow() && H <= kMaxNarrowH)) {  // workgroup per row (128 / 256 / 512 threads of 8 columns each)
     const dim3 wg(static_cast<unsigned>(rows < 65536 ? rows : 65536));
 #define DET_LNFW(T, VV, NT) hipLaunchKernelGGL((ln_fwd_wide<T, VV, NT>), wg, dim3(NT), 0, st, a)
 #define DET_LNFW_T(T)                                   \
@@ -796,7 +858,9 @@ int det_tf_ln_fwd(void* stream, int dtype, const void* h, const void* r, void* y
   if (H > kMaxNarrowH) return -1;
   const int grid = grid_for(rows, kWaves);
   const int K = ln_k(H);
-#define DET_LNF(T, KK) hipLaunchKernelGGL((ln_fwd_kernel<T, KK>), dim3(grid), dim3(kThreads), 0, st, a)
+#define DET_LNF(T, KK)                                                                        \
+  if (R == 2) hipLaunchKernelGGL((ln_fwd_kernel<T, KK, 2>), dim3(grid), dim3(kThreads), 0, st, a); \
+  else hipLaunchKernelGGL((ln_fwd_kernel<T, KK, 1>), dim3(grid), dim3(kThreads), 0, st, a)
 #define DET_LNF_K(T)                                                              \
   switch (K) {                                                                    \
     case 1: DET_LNF(T, 1); break;                                                 \
@@ -846,7 +910,10 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
   }
   const size_t lds = static_cast<size_t>(kWaves) * H * sizeof(float);
   const int K = ln_k(H);
-#define DET_LNB(T, KK) hipLaunchKernelGGL((ln_bwd_kernel<T, KK>), dim3(blocks), dim3(kThreads), lds, st, a)
+  const int R = ln_rows_per_wave();
+#define DET_LNB(T, KK)                                                                                  \
+  if (R == 2) hipLaunchKernelGGL((ln_bwd_kernel<T, KK, 2>), dim3(blocks), dim3(kThreads), lds, st, a);     \
+  else hipLaunchKernelGGL((ln_bwd_kernel<T, KK, 1>), dim3(blocks), dim3(kThreads), lds, st, a)
 #define DET_LNB_K(T)                                                              \
   switch (K) {                                                                    \
     case 1: DET_LNB(T, 1); break;                                                 \

@@ -16,7 +16,6 @@ hipBLASLt.  ``DET_TUNED_GEMMS=0`` turns it off; ``DET_TUNED_GEMMS=<path>`` loads
 """
 import logging
 import os
-import tempfile
 from typing import Dict, Optional
 
 import torch
@@ -40,8 +39,10 @@ def enable(path: Optional[str] = None) -> bool:
         return False
     from torch.cuda import tunable
 
-    # results TunableOp may write at exit go to a scratch file, never over the shipped one
-    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"det_tunableop_{os.getpid()}.csv"))
+    # TunableOp fills its table lazily from its file name at the first tunable GEMM, so the file is
+    # named rather than read here (a read_file before that first call is replaced by the lazy read);
+    # with tuning off nothing is written back to it at exit
+    tunable.set_filename(src, insert_device_ordinal=False)
     tunable.enable(True)
     tunable.tuning_enable(False)
     tunable.record_untuned_enable(False)
