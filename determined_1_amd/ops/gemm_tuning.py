@@ -10,9 +10,12 @@ it and cannot run under hipGraph capture), and shapes the file does not list kee
 The file's validator lines pin the torch / HIP / hipBLASLt / rocBLAS versions and the GPU arch it
 was measured with; TunableOp ignores it on any other stack.
 
-Measured (round 5, r5s21, BERT-base SQuAD bs12 O2): eager 1245 -> 1360 ex/s; the weight-gradient
-GEMMs (reduction over the 4608 tokens) move to rocBLAS solutions, the forward ones stay on
-hipBLASLt.  ``DET_TUNED_GEMMS=0`` turns it off; ``DET_TUNED_GEMMS=<path>`` loads another file.
+Opt-in (``DET_TUNED_GEMMS=1``, or ``=<path>`` for another file).  Measured on BERT-base SQuAD bs12
+O2 in one session (profiles/r5_bert_sink_link_tuning_ab.jsonl, r5s24): with hipGraph replays the
+tuned and heuristic solutions give the same 1,484 ex/s -- at these shapes the heuristic already
+picks solutions as fast as the best measured ones -- while eager steps lose 10-14 % (1,199-1,220 vs
+1,374) to TunableOp's per-call lookup on the host.  So the file is not loaded by default; it stays
+for shapes where a sweep does find faster solutions (``scripts/tune_gemms.py``).
 """
 import logging
 import os
@@ -28,8 +31,8 @@ def enable(path: Optional[str] = None) -> bool:
     """Load the measured solutions (once per process).  True when TunableOp now serves them."""
     if _STATE["loaded"] is not None:
         return bool(_STATE["loaded"])
-    env = os.environ.get("DET_TUNED_GEMMS", "1")
-    if env == "0" or not torch.cuda.is_available():
+    env = os.environ.get("DET_TUNED_GEMMS", "0")
+    if env in ("", "0") or not torch.cuda.is_available():
         _STATE["loaded"] = False
         return False
     src = path or (env if env not in ("", "1") else SHIPPED)

@@ -15,7 +15,11 @@ def test_shipped_file_lists_the_bert_shapes_and_validators():
     assert {"PT_VERSION", "HIPBLASLT_VERSION", "ROCBLAS_VERSION", "GCN_ARCH_NAME"} <= validators
 
 
-def test_enable_is_a_no_op_without_a_gpu(monkeypatch):
+def test_enable_is_opt_in_and_a_no_op_without_a_gpu(monkeypatch):
     monkeypatch.setitem(gemm_tuning._STATE, "loaded", None)
+    monkeypatch.delenv("DET_TUNED_GEMMS", raising=False)
+    assert gemm_tuning.enable() is False
+    monkeypatch.setitem(gemm_tuning._STATE, "loaded", None)
+    monkeypatch.setenv("DET_TUNED_GEMMS", "1")
     monkeypatch.setattr(gemm_tuning.torch.cuda, "is_available", lambda: False)
     assert gemm_tuning.enable() is False
