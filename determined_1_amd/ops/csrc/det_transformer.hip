@@ -37,10 +37,14 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kFinThreads = 1024;
+// colsum_finalize: 8 columns x 32 partial-row lanes per 256-thread block.  The sums are latency-bound
+// (a few MB of partials just written): the LayerNorm backward's 512 partial rows were 32 dependent-ish
+// loads per lane with 64-column blocks of 16 lanes (~12 us of the 21 us LN backward at the BERT shape,
+// r5s25); now 16 per lane in 8 independent chains, over 8x as many blocks.
+constexpr int kFinThreads = 256;
 constexpr int kMaxH = 8192;        // LayerNorm width limit (workgroup-per-row kernels above 2048)
 constexpr int kMaxNarrowH = 2048;  // wave-per-row kernels up to here
-constexpr int kFinCols = 64;
+constexpr int kFinCols = 8;
 constexpr int kFinLanes = kFinThreads / kFinCols;
 
 __device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
@@ -628,14 +632,15 @@ colsum_finalize(const float* __restrict__ ws, int parts, int W, int seg, T* __re
   float s = 0.f;
   if (col < W) {
     int p = ln;
-    for (; p + 3 * kFinLanes < parts; p += 4 * kFinLanes) {
-      const float a = ws[static_cast<int64_t>(p) * W + col];
-      const float b = ws[static_cast<int64_t>(p + kFinLanes) * W + col];
-      const float c = ws[static_cast<int64_t>(p + 2 * kFinLanes) * W + col];
-      const float d = ws[static_cast<int64_t>(p + 3 * kFinLanes) * W + col];
-      s += (a + b) + (c + d);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (; p + 7 * kFinLanes < parts; p += 8 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += ws[static_cast<int64_t>(p + u * kFinLanes) * W + col];
     }
-    for (; p < parts; p += kFinLanes) s += ws[static_cast<int64_t>(p) * W + col];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)  // the remaining < 8 rows of this lane, one per chain
+      if (p + u * kFinLanes < parts) acc[u] += ws[static_cast<int64_t>(p + u * kFinLanes) * W + col];
+    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
   red[ln][cl] = s;
   __syncthreads();
