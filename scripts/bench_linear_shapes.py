@@ -6,8 +6,12 @@ per pass, in TF/s of HIP-event time over back-to-back calls.
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from determined_1_amd.ops import _lib, gemm_tuning
 from determined_1_amd.ops.conv import conv1x1_wgrad, dgrad_1x1
