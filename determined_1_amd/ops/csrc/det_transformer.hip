@@ -37,14 +37,10 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-// colsum_finalize: 8 columns x 32 partial-row lanes per 256-thread block.  The sums are latency-bound
-// (a few MB of partials just written): the LayerNorm backward's 512 partial rows were 32 dependent-ish
-// loads per lane with 64-column blocks of 16 lanes (~12 us of the 21 us LN backward at the BERT shape,
-// r5s25); now 16 per lane in 8 independent chains, over 8x as many blocks.
-constexpr int kFinThreads = 256;
+constexpr int kFinThreads = 1024;
 constexpr int kMaxH = 8192;        // LayerNorm width limit (workgroup-per-row kernels above 2048)
 constexpr int kMaxNarrowH = 2048;  // wave-per-row kernels up to here
-constexpr int kFinCols = 8;
+constexpr int kFinCols = 64;
 constexpr int kFinLanes = kFinThreads / kFinCols;
 
 __device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
@@ -632,15 +628,14 @@ colsum_finalize(const float* __restrict__ ws, int parts, int W, int seg, T* __re
   float s = 0.f;
   if (col < W) {
     int p = ln;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (; p + 7 * kFinLanes < parts; p += 8 * kFinLanes) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc[u] += ws[static_cast<int64_t>(p + u * kFinLanes) * W + col];
+    for (; p + 3 * kFinLanes < parts; p += 4 * kFinLanes) {
+      const float a = ws[static_cast<int64_t>(p) * W + col];
+      const float b = ws[static_cast<int64_t>(p + kFinLanes) * W + col];
+      const float c = ws[static_cast<int64_t>(p + 2 * kFinLanes) * W + col];
+      const float d = ws[static_cast<int64_t>(p + 3 * kFinLanes) * W + col];
+      s += (a + b) + (c + d);
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)  // the remaining < 8 rows of this lane, one per chain
-      if (p + u * kFinLanes < parts) acc[u] += ws[static_cast<int64_t>(p + u * kFinLanes) * W + col];
-    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    for (; p < parts; p += kFinLanes) s += ws[static_cast<int64_t>(p) * W + col];
   }
   red[ln][cl] = s;
   __syncthreads();
@@ -799,6 +794,13 @@ int ln_rows_per_wave() {
   }();
   return r;
 }
+bool ln_bwd_wide_rows() {  // DET_LN_BWD=wide: workgroup-per-row backward for H % 8 == 0 rows up to 2048 too
+  static const bool w = [] {
+    const char* e = std::getenv("DET_LN_BWD");
+    return e != nullptr && std::strcmp(e, "wide") == 0;
+  }();
+  return w;
+}
 bool ln_fwd_narrow() {
   static const bool n = [] {
     const char* e = std::getenv("DET_LN_FWD");
@@ -894,18 +896,21 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
   hipStream_t st = static_cast<hipStream_t>(stream);
   int blocks = static_cast<int>(ln_bwd_blocks(rows));
   LnBwdArgs a{dy, h, r, mean, rstd, gamma, dr, dh, ws, rows, H, p > 0.f, make_rng(p, seed, offset, obase)};
-  if (H > kMaxNarrowH) {
+  if (H > kMaxNarrowH || (ln_bwd_wide_rows() && H % 8 == 0)) {
     if (H % 8 != 0) return -1;
-    if (blocks > 256) blocks = 256;  // <= ln_bwd_blocks(rows): fits det_tf_ln_ws_elems
+    const bool small = H <= 8 * 128;  // 128-thread rows (DET_LN_BWD=wide at BERT widths)
+    if (!small && blocks > 256) blocks = 256;  // <= ln_bwd_blocks(rows): fits det_tf_ln_ws_elems
     const bool v1 = H <= 8 * kWideThreads;
     if (dtype == 1) {
-      if (v1) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      if (small) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1, 128>), dim3(blocks), dim3(128), 0, st, a);
+      else if (v1) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       else hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 2, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads),
                          0, st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
                          static_cast<unsigned short*>(dbeta), static_cast<unsigned short*>(dbias));
     } else {
-      if (v1) hipLaunchKernelGGL((ln_bwd_wide<float, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
+      if (small) hipLaunchKernelGGL((ln_bwd_wide<float, 1, 128>), dim3(blocks), dim3(128), 0, st, a);
+      else if (v1) hipLaunchKernelGGL((ln_bwd_wide<float, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       else hipLaunchKernelGGL((ln_bwd_wide<float, 2, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       hipLaunchKernelGGL(colsum_finalize<float>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st,
                          ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
