@@ -56,7 +56,7 @@ def test_synthetic_coco_instance_load():
     and inside its box.  The default "uniform" load is unchanged (1..max_objects)."""
     from determined_1_amd.models.detection import SyntheticCocoInstances
 
-    ds = SyntheticCocoInstances(300, min_size=200, max_size=260, instance_dist="coco")
+    ds = SyntheticCocoInstances(150, min_size=200, max_size=260, instance_dist="coco")
     counts, small = [], 0
     for i in range(len(ds)):
         img, t = ds[i]
