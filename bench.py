@@ -21,6 +21,14 @@ kernel -> ResNet-50 fwd/bwd (bf16 autocast, channels_last) -> [RCCL bucketed all
 with backward] -> fused arena SGD-momentum HIP kernel.  Weak scaling: fixed per-GPU batch.
 
 Rank 0 prints ONE JSON line; ``value`` = K * global_batch / max-over-ranks(t1 - t0).
+
+HIP runtime setting: kernel arguments are placed in device memory (``HIP_FORCE_DEV_KERNARG=1``, set
+here before anything initialises HIP, inherited by the ranks) -- this step is GPU-bound with ~290
+launches, and each kernel then fetches its arguments from HBM instead of host memory over PCIe:
+12,470-12,478 vs 12,277-12,280 samples/s in three alternating same-box runs each
+(``profiles/r5_bench_resnet50_kernarg_ab.jsonl``).  A host-bound eager step loses with it (BERT
+eager 1,159-1,272 vs 1,410-1,414: the host writes every launch's arguments across PCIe), so it is
+a per-workload choice, not a framework default.
 """
 import argparse
 import json
@@ -33,6 +41,7 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # see the module docstring
 
 BASELINE_VALUE = None  # BASELINE.json "published": {} -- the reference publishes no ResNet-50 number
 

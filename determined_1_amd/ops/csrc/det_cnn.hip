@@ -1058,8 +1058,10 @@ __global__ void __launch_bounds__(NT) cnn_masks_kernel(MaskLaunch L) {
 // ---- cross entropy -----------------------------------------------------------------------------
 // loss = mean_n (logsumexp(z_n) - z_n[y_n]); correct = #(argmax z_n == y_n) (first max, as torch);
 // backward dz = g * (softmax(z) - onehot(y)) / N.
+// dz1 (nullable): the backward for a seed gradient of exactly 1, written by the same pass (the
+// autograd backward then hands it over without a launch when its seed is the shared unit tensor)
 __global__ void __launch_bounds__(NT) cnn_xent_fwd_kernel(const float* z, const int64_t* y, int N, int C,
-                                                          float* loss_out, float* acc_out) {
+                                                          float* loss_out, float* acc_out, float* dz1) {
   __shared__ float sl[NT], sa[NT];
   float l = 0.f, a = 0.f;
   for (int n = threadIdx.x; n < N; n += NT) {
@@ -1076,6 +1078,10 @@ __global__ void __launch_bounds__(NT) cnn_xent_fwd_kernel(const float* z, const 
     const int yy = static_cast<int>(y[n]);
     l += logf(se) + mx - r[yy];
     a += arg == yy ? 1.f : 0.f;
+    if (dz1 != nullptr) {  // exactly cnn_xent_bwd_kernel's arithmetic with g = 1
+      const float gs = 1.f / N, inv = 1.f / se;
+      for (int c = 0; c < C; ++c) dz1[static_cast<int64_t>(n) * C + c] = gs * (expf(r[c] - mx) * inv - (c == yy ? 1.f : 0.f));
+    }
   }
   sl[threadIdx.x] = l;
   sa[threadIdx.x] = a;
@@ -1279,9 +1285,9 @@ int det_cnn_masks(void* stream, float* m0, int64_t n0, float p0, float* m1, int6
 }
 
 int det_cnn_xent_fwd(void* stream, const float* z, const int64_t* y, int32_t N, int32_t C, float* loss,
-                     float* acc) {
+                     float* acc, float* dz1) {
   if (N < 1 || C < 1) return static_cast<int>(hipErrorInvalidValue);
-  cnn_xent_fwd_kernel<<<1, NT, 0, static_cast<hipStream_t>(stream)>>>(z, y, N, C, loss, acc);
+  cnn_xent_fwd_kernel<<<1, NT, 0, static_cast<hipStream_t>(stream)>>>(z, y, N, C, loss, acc, dz1);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -302,28 +302,14 @@ class PyTorchTrialContext(trial.TrialContext):
             loss = self._amp.scaler.scale_loss(loss)
         self._timers.backward_start()
         if gradient is None and not create_graph:
-            gradient = self._unit_gradient(loss)
+            from determined_1_amd.ops import seed_grad
+
+            gradient = seed_grad.unit_for(loss)  # a shared constant instead of a per-backward fill
         loss.backward(gradient=gradient, retain_graph=retain_graph, create_graph=create_graph)  # type: ignore
         self._timers.backward_end()
         for st in self._opt_states:
             if st.fused is not None and st.fused.sink is not None:
                 st.fused.sink.end_backward()
-
-    def _unit_gradient(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
-        """The seed gradient of a scalar GPU loss as a cached constant: autograd's implicit
-        ``ones_like`` is a fill launch per backward (a few microseconds of a ~0.3 ms CIFAR batch).
-        Created only outside a hipGraph capture: a tensor allocated inside one takes an address the
-        graph reuses for earlier temporaries, which a replay would overwrite."""
-        if loss.dim() != 0 or not loss.is_cuda or loss.grad_fn is None:
-            return None  # (a leaf loss would keep the seed as its .grad and accumulate into it)
-        key = (loss.dtype, loss.device)
-        cache = self.__dict__.setdefault("_unit_grads", {})
-        t = cache.get(key)
-        if t is None:
-            if torch.cuda.is_current_stream_capturing():
-                return None
-            t = cache[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
-        return t
 
     def _partial_window_grads(self) -> Optional[List[List[Optional[torch.Tensor]]]]:
         """The accumulated gradients of an unfinished aggregation window (checkpointed so that a

@@ -161,6 +161,28 @@ def test_cross_entropy_matches_torch(gpu):
     assert torch.allclose(z.grad, z2.grad, rtol=1e-5, atol=1e-7)
 
 
+def test_cross_entropy_unit_seed_gradient_from_the_forward_launch(gpu):
+    """With the shared unit seed (ops.seed_grad, what the trial context passes) the backward hands
+    over the gradient the forward launch already wrote: bit-equal to the backward kernel's for a seed
+    of 1 from a private tensor, and any other seed still scales through the backward kernel."""
+    from determined_1_amd.ops import seed_grad
+    from determined_1_amd.ops.cnn import cross_entropy
+
+    torch.manual_seed(4)
+    z0 = torch.randn(32, 10, device=gpu)
+    y = torch.randint(0, 10, (32,), device=gpu)
+    grads = []
+    for seed in ("unit", 1.0, 2.5):
+        z = z0.clone().requires_grad_(True)
+        loss = cross_entropy(z, y)
+        g = seed_grad.unit_for(loss) if seed == "unit" else torch.full((), seed, device=gpu)
+        assert seed_grad.is_unit(g) == (seed == "unit")
+        loss.backward(g)
+        grads.append(z.grad)
+    assert torch.equal(grads[0], grads[1])
+    torch.testing.assert_close(grads[2], 2.5 * grads[1], rtol=1e-6, atol=1e-8)
+
+
 def test_graph_replays_train_the_native_cnn(gpu, monkeypatch):
     """The whole native step (masks, GEMMs, finishes, RMSprop) captured and replayed: finite, learning,
     fresh masks per replay (the device offset counter), grads landing in the arena in place."""
