@@ -7,7 +7,7 @@ O=gpurun_out/r5s27
 mkdir -p $O
 export TMPDIR=/tmp
 for f in wide narrow; do
-  DET_LN_FWD=$f timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /tmp/lnprof_$f -o ln -- python3 -u scripts/bench_ln.py --iters 200 > $O/ln_$f.json 2> $O/ln.err || { tail -20 $O/ln.err; exit 1; }
+  DET_LN_FWD=$f timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/lnprof_$f -o ln -- python3 -u scripts/bench_ln.py --iters 200 > $O/ln_$f.json 2> $O/ln.err || { tail -20 $O/ln.err; exit 1; }
   cat $O/ln_$f.json
   find /tmp/lnprof_$f -name "*kernel_stats.csv" -exec cp {} $O/ln_${f}_kernel_stats.csv \;
   python3 -c "
