@@ -18,7 +18,7 @@ HERE = pathlib.Path(__file__).resolve().parent
 SRC_DIR = HERE / "csrc"
 SOURCES = [SRC_DIR / "det_kernels.hip", SRC_DIR / "det_norm.hip", SRC_DIR / "det_transformer.hip", SRC_DIR / "det_attention.hip",
            SRC_DIR / "det_pool.hip", SRC_DIR / "det_conv.hip", SRC_DIR / "det_igemm.hip", SRC_DIR / "det_detect.hip",
-           SRC_DIR / "det_stream.hip", SRC_DIR / "det_cnn.hip", SRC_DIR / "det_embed.hip"]
+           SRC_DIR / "det_stream.hip", SRC_DIR / "det_cnn.hip", SRC_DIR / "det_embed.hip", SRC_DIR / "det_blaslt.hip"]
 OUT = HERE / "libdetkernels.so"
 ARCH = os.environ.get("DET_OFFLOAD_ARCH", "gfx950")
 
@@ -61,7 +61,7 @@ def build(force: bool = False, verbose: bool = False) -> pathlib.Path:
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, sources))
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs] + ["-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

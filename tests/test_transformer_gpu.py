@@ -337,3 +337,40 @@ def test_tuned_gemm_solutions_load_and_keep_numerics(gpu, monkeypatch):
     y = torch.addmm(torch.zeros(2304, device=gpu, dtype=torch.bfloat16), x, torch.randn(2304, 768, device=gpu,
                     generator=g).to(torch.bfloat16).t())
     assert bool(torch.isfinite(y).all())
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_blaslt_plans_match_torch_gemms(gpu, dt):
+    """The cached-plan hipBLASLt path (ops/csrc/det_blaslt.hip) for the three Linear passes at a
+    BERT shape -- forward with the bias epilogue, input gradient (alone and accumulated onto a
+    residual gradient, beta = 1), weight gradient (alone and accumulated) -- against the fp32
+    products, and against torch's own hipBLASLt calls to bf16 rounding."""
+    M, K, N = 4608, 768, 2304
+    g = torch.Generator(device=gpu).manual_seed(2)
+    x = torch.randn(M, K, device=gpu, generator=g).to(dt)
+    w = (torch.randn(N, K, device=gpu, generator=g) * 0.05).to(dt)
+    b = torch.randn(N, device=gpu, generator=g).to(dt)
+    dz = torch.randn(M, N, device=gpu, generator=g).to(dt)
+    dr = torch.randn(M, K, device=gpu, generator=g).to(dt)
+    assert tfops._bl_ok(x, w)
+    tol = dict(rtol=2e-2, atol=2e-2) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-3)
+
+    def close(a, ref):
+        torch.testing.assert_close(a.float(), ref, **tol)
+
+    y = torch.empty(M, N, device=gpu, dtype=dt)
+    tfops._bl_gemm(1, 0, N, M, K, w, K, x, K, y, N, bias=b)
+    close(y, x.float() @ w.float().t() + b.float())
+    close(y, torch.addmm(b, x, w.t()).float())
+    dx = torch.empty(M, K, device=gpu, dtype=dt)
+    tfops._bl_gemm(0, 0, K, M, N, w, K, dz, N, dx, K)
+    close(dx, dz.float() @ w.float())
+    acc = dr.clone()
+    tfops._bl_gemm(0, 0, K, M, N, w, K, dz, N, acc, K, beta=1.0)
+    close(acc, dr.float() + dz.float() @ w.float())
+    dw = torch.empty(N, K, device=gpu, dtype=dt)
+    tfops._bl_wgrad(dz, x, dw)
+    close(dw, dz.float().t() @ x.float())
+    close(dw, (dz.t() @ x).float())
+    tfops._bl_wgrad(dz, x, dw, beta=1.0)
+    close(dw, 2 * (dz.float().t() @ x.float()))
