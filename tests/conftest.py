@@ -27,16 +27,3 @@ def gpu():
     _lib.get_lib()  # must load: GPU tests never run on an eager fallback
     return torch.device("cuda", 0)
 
-
-@pytest.fixture(autouse=True)
-def _freeze_earlier_objects(request):
-    """CPU runs (``-m "not gpu"``): objects that outlived earlier tests (module caches, models held by
-    fixtures) are moved out of the cyclic collector's view before each test.  In one long pytest
-    process every gen-2 collection otherwise rescans all of them, and tests that allocate many small
-    objects late in the suite ran 2-8x slower than alone (the COCO instance-load test 36 s vs 5 s).
-    Not on GPU runs, where a frozen cycle could keep device memory alive for the rest of the suite."""
-    if (request.config.option.markexpr or "").replace(" ", "") == "notgpu":
-        import gc
-
-        gc.freeze()
-    yield
