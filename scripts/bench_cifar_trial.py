@@ -29,6 +29,7 @@ def main() -> None:
     ap.add_argument("--train-records", type=int, default=50000, help="records per epoch")
     ap.add_argument("--no-dropout", action="store_true", help="dropout 0 (deterministic eager/graph comparison)")
     ap.add_argument("--batch-losses", action="store_true", help="also print every batch's loss")
+    ap.add_argument("--validations", type=int, default=1, help="validation passes at the end (the first captures)")
     args = ap.parse_args()
     t0 = time.time()
     import torch
@@ -65,7 +66,8 @@ def main() -> None:
             yield workload.train_workload(step, num_batches=n, total_batches_processed=done), [], keep(f"train{step}")
             done += n
             step += 1
-        yield workload.validation_workload(step, total_batches_processed=done), [], keep("val")
+        for v in range(args.validations):
+            yield workload.validation_workload(step, total_batches_processed=done), [], keep("val" if v == 0 else f"val{v}")
         yield workload.terminate_workload(step, total_batches_processed=done), [], workload.ignore_response
 
     t1 = time.time()
@@ -86,6 +88,7 @@ def main() -> None:
                       "seed": args.seed,
                       "records_per_s": round(args.batch * 1000.0 / ms_batch, 1),
                       "first_chunk_s": round(trains[0], 3), "validation_10k_s": round(per["val"], 3),
+                      "validation_10k_s_later": [round(per[n], 4) for n in names if n.startswith("val") and n != "val"],
                       "import_s": round(t_import, 2), "controller_build_s": round(t_build, 2),
                       "hip_graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
                       "loss": res[names[-2]]["metrics"]["avg_metrics"].get("loss") if len(names) > 1 else None,
