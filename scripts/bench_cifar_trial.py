@@ -91,7 +91,7 @@ def main() -> None:
                       "validation_10k_s_later": [round(per[n], 4) for n in names if n.startswith("val") and n != "val"],
                       "import_s": round(t_import, 2), "controller_build_s": round(t_build, 2),
                       "hip_graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
-                      "loss": res[names[-2]]["metrics"]["avg_metrics"].get("loss") if len(names) > 1 else None,
+                      "loss": res[[n for n in names if n.startswith("train")][-1]]["metrics"]["avg_metrics"].get("loss"),
                       "loss_per_chunk": [float(res[n]["metrics"]["avg_metrics"].get("loss", float("nan")))
                                          for n in names if n.startswith("train")],
                       "batch_losses": [float(m["loss"]) for n in names if n.startswith("train")
