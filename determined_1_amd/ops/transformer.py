@@ -200,7 +200,9 @@ def _bl_ok(*ts: torch.Tensor) -> bool:
     ready = _BL["ready"]
     if ready is None:
         path = os.path.join(os.path.dirname(torch.__file__), "lib", "libhipblaslt.so")
-        ready = _BL["ready"] = os.path.exists(path) and _lib.get_lib().det_blaslt_init(path.encode()) == 0
+        lib = _lib.get_lib()
+        ready = _BL["ready"] = os.path.exists(path) and lib.det_blaslt_init(path.encode()) == 0
+        _BL["fn"] = lib.det_blaslt_gemm
     if not ready:
         return False
     dev = ts[0].device.index
@@ -214,10 +216,12 @@ def _bl_ok(*ts: torch.Tensor) -> bool:
 def _bl_gemm(ta: int, tb: int, m: int, n: int, k: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
              D: torch.Tensor, ldd: int, bias: Optional[torch.Tensor] = None, beta: float = 0.0) -> None:
     """Column-major D[m, n] = op(A) op(B) [+ bias per row] [+ beta D] (see det_blaslt.hip)."""
-    ws = _BL["ws"][D.device.index]
-    _lib.check(_lib.get_lib().det_blaslt_gemm(_stream(D), ta, tb, m, n, k, A.data_ptr(), lda, B.data_ptr(), ldb,
-                                              D.data_ptr(), ldd, _ptr(bias), float(beta), _BL_DT[D.dtype],
-                                              ws.data_ptr(), _BL_WS_BYTES), "det_blaslt_gemm")
+    dev = D.device.index
+    rc = _BL["fn"](torch._C._cuda_getCurrentRawStream(dev), ta, tb, m, n, k, A.data_ptr(), lda, B.data_ptr(), ldb,
+                   D.data_ptr(), ldd, None if bias is None else bias.data_ptr(), beta, _BL_DT[D.dtype],
+                   _BL["ws"][dev].data_ptr(), _BL_WS_BYTES)
+    if rc != 0:
+        _lib.check(rc, "det_blaslt_gemm")
 
 
 def _bl_wgrad(dz: torch.Tensor, x2: torch.Tensor, out: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
