@@ -49,7 +49,10 @@
 
 namespace {
 
-constexpr int kWaves = 4;
+#ifndef DET_ATTN_WAVES
+#define DET_ATTN_WAVES 4
+#endif
+constexpr int kWaves = DET_ATTN_WAVES;  // 32 query (or key) rows per wave
 constexpr int kThreads = 64 * kWaves;
 constexpr int kQB = 32 * kWaves;  // rows (queries, or keys for dK/dV) per workgroup
 constexpr int kKB = 64;           // streamed tokens per block
