@@ -49,9 +49,7 @@ class Job(ctypes.Structure):
                [(n, c_i32) for n in ("splits", "epi", "out_dt", "bias_dt", "drop_cols", "HW", "C", "PW", "PH", "gC",
                                      "gS", "accumulate")] + \
                [(n, c_void_p) for n in ("out", "bias", "drop", "act", "idx")] + \
-               [(n, c_i64) for n in ("gso", "gsc", "gsr", "gss")] + [("gbias", c_void_p), ("slab", c_void_p)] + \
-               [("dseed", ctypes.c_uint64), ("doff", ctypes.c_uint64), ("dbase", c_void_p), ("dthr", ctypes.c_uint32),
-                ("dscale", ctypes.c_float), ("dmask", c_i32)]
+               [(n, c_i64) for n in ("gso", "gsc", "gsr", "gss")] + [("gbias", c_void_p), ("slab", c_void_p)]
 
 
 SIGNATURES = {
@@ -140,49 +138,19 @@ class _Runner:
             _lib.check(self.lib.det_cnn_finish(self.st, arr, len(chunk)), "det_cnn_finish")
 
 
-class _Philox:
-    """Dropout mask ``s`` of a forward, drawn in the consuming epilogues (det_cnn.hip drop_factor):
-    the factor of element i is exactly cnn_masks_kernel's, so no mask tensor is generated or read."""
-
-    __slots__ = ("s", "seed", "off", "base", "thr", "scale")
-
-    def __init__(self, s: int, p: float, seed: int, off: int, base: int) -> None:
-        import numpy as np
-
-        p32 = np.float32(p)
-        self.s, self.seed, self.off, self.base = s, seed, off, base
-        self.thr = 0xFFFFFFFF if p32 >= 1 else int(float(p32) * 4294967296.0)
-        keep = np.float32(1.0) - p32
-        self.scale = float(np.float32(1.0) / keep) if keep > 0 else 0.0
-
-
-def _drop_kw(m, cols: int) -> dict:
-    if m is None:
-        return {}
-    if isinstance(m, _Philox):
-        return dict(drop_cols=cols, dseed=m.seed, doff=m.off, dbase=m.base, dthr=m.thr, dscale=m.scale,
-                    dmask=m.s + 1)
-    return dict(drop=m.data_ptr(), drop_cols=cols)
-
-
 def _masks(x: torch.Tensor, n: int, ps: Tuple[float, float, float], training: bool):
-    """Dropout of the two Dropout2d layers ([N, 32], [N, 64] factors) and the element dropout on fc1
-    ([N, 512]): one Philox (seed, offset) per forward, drawn in the epilogues that apply it; None
-    where the layer is inactive.  Tests (DEBUG["keep_masks"]) also get the factor tensors, written by
-    cnn_masks_kernel from the same draw."""
+    """Dropout factors (0 or 1/(1-p)) for the two Dropout2d layers ([N, 32], [N, 64]) and the element
+    dropout on fc1 ([N, 512]); None where the layer is inactive."""
     if not training or all(p <= 0 for p in ps):
         return None, None, None
+    lib = _lib.get_lib()
+    sizes = (n * 32, n * 64, n * 512)
+    outs = [torch.empty(sz, dtype=torch.float32, device=x.device) if p > 0 else None for sz, p in zip(sizes, ps)]
     seed, off = _tf.next_rng()
     base = _tf.rng_base(x.device)
-    specs = tuple(_Philox(s, p, seed, off, base) if p > 0 else None for s, p in enumerate(ps))
-    if DEBUG["keep_masks"]:
-        lib = _lib.get_lib()
-        sizes = (n * 32, n * 64, n * 512)
-        outs = [torch.empty(sz, dtype=torch.float32, device=x.device) if p > 0 else None for sz, p in zip(sizes, ps)]
-        _lib.check(lib.det_cnn_masks(_stream(x), _p(outs[0]), sizes[0], float(ps[0]), _p(outs[1]), sizes[1],
-                                     float(ps[1]), _p(outs[2]), sizes[2], float(ps[2]), seed, off, base), "det_cnn_masks")
-        DEBUG["masks"] = tuple(outs)
-    return specs
+    _lib.check(lib.det_cnn_masks(_stream(x), _p(outs[0]), sizes[0], float(ps[0]), _p(outs[1]), sizes[1], float(ps[1]),
+                                 _p(outs[2]), sizes[2], float(ps[2]), seed, off, base), "det_cnn_masks")
+    return tuple(outs)
 
 
 def _forward(x: torch.Tensor, params: Sequence[torch.Tensor], ps, training: bool):
@@ -194,6 +162,8 @@ def _forward(x: torch.Tensor, params: Sequence[torch.Tensor], ps, training: bool
         xh = xh.contiguous()
     R = _Runner(x)
     m2, m4, m5 = _masks(x, n, ps, training)
+    if DEBUG["keep_masks"]:
+        DEBUG["masks"] = (m2, m4, m5)
     kw = dict(dtype=x.dtype, device=x.device)
     a1 = torch.empty(n, 30, 30, 32, **kw)
     a2 = torch.empty(n, 14, 14, 32, **kw)
@@ -210,7 +180,7 @@ def _forward(x: torch.Tensor, params: Sequence[torch.Tensor], ps, training: bool
     # (not split: 784 tiles already fill the chip; split + finish measured 30 vs 19 us)
     R.finish(R.gemm(R.prepare(Job(a=_conv_act(a1, dt, 30, 32, 0, 28, pool=1), b=_wgt(w2, dt, S_WGT_CONV, 32), M=n * 784,
                                   N=32, K=288, epi=E_BIAS_RELU_POOL, out=a2.data_ptr(), out_dt=dt, bias=b2.data_ptr(),
-                                  bias_dt=dt, **_drop_kw(m2, 32), idx=idx2.data_ptr(), PH=14, PW=14),
+                                  bias_dt=dt, drop=_p(m2), drop_cols=32, idx=idx2.data_ptr(), PH=14, PW=14),
                               split=n * 784 < 16384)))
     # conv3 32->64 pad 1 + bias + relu
     R.finish(R.gemm(R.prepare(Job(a=_conv_act(a2, dt, 14, 32, 1, 14), b=_wgt(w3, dt, S_WGT_CONV, 32), M=n * 196, N=64,
@@ -218,11 +188,12 @@ def _forward(x: torch.Tensor, params: Sequence[torch.Tensor], ps, training: bool
     # conv4 64->64 + bias + relu + maxpool + dropout2d
     R.finish(R.gemm(R.prepare(Job(a=_conv_act(a3, dt, 14, 64, 0, 12, pool=1), b=_wgt(w4, dt, S_WGT_CONV, 64), M=n * 144,
                                   N=64, K=576, epi=E_BIAS_RELU_POOL, out=a4.data_ptr(), out_dt=dt, bias=b4.data_ptr(),
-                                  bias_dt=dt, **_drop_kw(m4, 64), idx=idx4.data_ptr(), PH=6, PW=6))))
+                                  bias_dt=dt, drop=_p(m4), drop_cols=64, idx=idx4.data_ptr(), PH=6, PW=6))))
     # fc1 2304->512 (torch's NCHW flatten order) + bias + relu + dropout: split-K, finished by a launch
     fin = R.gemm(R.prepare(Job(a=Operand(p=a4.data_ptr(), dt=dt, src=S_ACT_FLAT, H=6, W=6, C=64),
                                b=_wgt(w5, dt, S_WGT_FC, 2304), M=n, N=512, K=2304, epi=E_BIAS_RELU_DROP,
-                               out=a5.data_ptr(), out_dt=dt, bias=b5.data_ptr(), bias_dt=dt, **_drop_kw(m5, 512))))
+                               out=a5.data_ptr(), out_dt=dt, bias=b5.data_ptr(), bias_dt=dt, drop=_p(m5),
+                               drop_cols=512)))
     R.finish(fin)
     # fc2 512->10 + bias -> fp32 logits (split-K: one block would walk K serially)
     fin = R.gemm(R.prepare(Job(a=Operand(p=a5.data_ptr(), dt=dt, src=S_ACT_ROWS, C=512), b=_wgt(w6, dt, S_WGT_FC, 512),
@@ -296,7 +267,7 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
                        b=Operand(p=a5.data_ptr(), dt=dt, src=S_ACT_ROWS, C=512), M=10, N=513, K=n, **gfc(10, n))),
          R.prepare(Job(a=Operand(p=dl.data_ptr(), dt=0, src=S_GRAD_ROWS, C=10), b=_wgt(w6, dt, S_WGT_FC_T, 0),
                        M=n, N=512, K=10, epi=E_DROP_POS, out=dz5.data_ptr(), out_dt=dt, act=a5.data_ptr(),
-                       **_drop_kw(m5, 512), HW=1)))
+                       drop=_p(m5), drop_cols=512, HW=1)))
     # fc1: weight grad || input grad -> d(a4) * drop2d * (a4 > 0), written unpooled (the argmax of each
     # 2x2 window, zeros elsewhere) as conv4's output gradient g4
     step(R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512, transpose=1),
@@ -304,7 +275,7 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
                        **gfc(8, n))),
          R.prepare(Job(a=Operand(p=dz5.data_ptr(), dt=dt, src=S_GRAD_ROWS, C=512), b=_wgt(w5, dt, S_WGT_FC_T, 0),
                        M=n, N=2304, K=512, epi=E_DROP_POS_FLAT, out=g4.data_ptr(), out_dt=dt,
-                       act=a4.data_ptr(), **_drop_kw(m4, 64), HW=36, C=64, idx=idx4.data_ptr(), PH=6, PW=6)))
+                       act=a4.data_ptr(), drop=_p(m4), drop_cols=64, HW=36, C=64, idx=idx4.data_ptr(), PH=6, PW=6)))
     # conv4: weight grad || input grad -> dy3 = d(a3) * (a3 > 0)
     step(R.prepare(Job(a=Operand(p=g4.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=64, OH=12, OW=12, transpose=1),
                        b=_conv_act(a3, dt, 14, 64, 0, 12), M=64, N=577, K=n * 144, **gconv(6, 64))),
@@ -318,7 +289,7 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
          R.prepare(Job(a=Operand(p=dy3.data_ptr(), dt=dt, src=S_GRAD_CONV_T, H=14, W=14, C=64, R=3, S=3, pad=1,
                                  OH=14, OW=14),
                        b=_wgt(w3, dt, S_WGT_CONV_T, 64), M=n * 196, N=32, K=576, epi=E_DROP_POS,
-                       out=g2.data_ptr(), out_dt=dt, act=a2.data_ptr(), **_drop_kw(m2, 32), HW=196,
+                       out=g2.data_ptr(), out_dt=dt, act=a2.data_ptr(), drop=_p(m2), drop_cols=32, HW=196,
                        idx=idx2.data_ptr(), PH=14, PW=14)))
     # conv2: weight grad || input grad -> dy1 = d(a1) * (a1 > 0)
     step(R.prepare(Job(a=Operand(p=g2.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=28, OW=28, transpose=1),

@@ -350,13 +350,6 @@ struct Job {
   void* gbias;                   // bias gradient (its column is N-1) or null
   int accumulate;                // E_GRAD_*: add into the existing gradient
   float* slab;                   // split-K partials [splits][M][N] (splits > 1)
-  // dropout drawn in the epilogue (drop == null, dmask = s + 1): factor of element (row, col) of mask
-  // s = exactly cnn_masks_kernel's, so no mask tensor is generated, written or read
-  uint64_t dseed, doff;
-  const uint32_t* dbase;
-  uint32_t dthr;
-  float dscale;
-  int dmask;
 };
 
 struct Launch {
@@ -364,32 +357,8 @@ struct Launch {
   int nblocks0;
 };
 
-// ---- dropout factors ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t philox_u0(uint64_t idx, uint32_t k0, uint32_t k1, uint32_t c2, uint32_t c3) {
-  uint32_t c0 = static_cast<uint32_t>(idx), c1 = static_cast<uint32_t>(idx >> 32);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-    c0 = hi1 ^ c1 ^ k0;
-    c1 = lo1;
-    c2 = hi0 ^ c3 ^ k1;
-    c3 = lo0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c0;
-}
-
 __device__ __forceinline__ float drop_factor(const Job& j, int64_t row, int64_t col) {
-  if (j.drop != nullptr) return j.drop[row * j.drop_cols + col];
-  if (j.dmask == 0) return 1.f;
-  const uint32_t base = j.dbase != nullptr ? *j.dbase : 0u;
-  const uint32_t u = philox_u0(static_cast<uint64_t>(row * j.drop_cols + col), static_cast<uint32_t>(j.dseed),
-                               static_cast<uint32_t>(j.dseed >> 32),
-                               static_cast<uint32_t>(j.doff) + static_cast<uint32_t>(j.dmask - 1) * 0x9E3779B9u,
-                               static_cast<uint32_t>(j.doff >> 32) + base);
-  return u >= j.dthr ? j.dscale : 0.f;
+  return j.drop == nullptr ? 1.f : j.drop[row * j.drop_cols + col];
 }
 
 // the gradient of one pooled element routed to its 2x2 window of the (2PH, 2PW) pre-pool grid: g at
@@ -1044,6 +1013,23 @@ __global__ void __launch_bounds__(NT) cnn_finish_kernel(FinishLaunch L) {
   }
 }
 
+// ---- dropout factors ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t philox_u0(uint64_t idx, uint32_t k0, uint32_t k1, uint32_t c2, uint32_t c3) {
+  uint32_t c0 = static_cast<uint32_t>(idx), c1 = static_cast<uint32_t>(idx >> 32);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c0;
+}
+
 struct MaskLaunch {
   float* out[3];
   int64_t n[3];
@@ -1154,11 +1140,6 @@ struct DetCnnJob {
   int64_t gso, gsc, gsr, gss;
   void* gbias;
   float* slab;
-  uint64_t dseed, doff;
-  const uint32_t* dbase;
-  uint32_t dthr;
-  float dscale;
-  int32_t dmask;
 };
 
 static Operand to_operand(const DetCnnOperand& d) {
@@ -1230,12 +1211,6 @@ static int fill_job(const DetCnnJob& d, Job* j) {
   j->gbias = d.gbias;
   j->accumulate = d.accumulate;
   j->slab = d.slab;
-  j->dseed = d.dseed;
-  j->doff = d.doff;
-  j->dbase = d.dbase;
-  j->dthr = d.dthr;
-  j->dscale = d.dscale;
-  j->dmask = d.dmask;
   if (j->splits > 1 && d.slab == nullptr) return -1;
   if (d.epi == E_BIAS_RELU_POOL && (d.M & 3)) return -1;
   return j->tiles_m * j->tiles_n * j->splits;
