@@ -14,7 +14,7 @@ import torch.nn as nn
 
 from determined_1_amd.ops import conv as native_conv
 from determined_1_amd.ops.norm import BatchNormAct2d, linked_conv2d
-from determined_1_amd.ops.pool import MaxPool3x3s2
+from determined_1_amd.ops.pool import MaxPool3x3s2, global_avg_pool
 
 # Fused BN(+add)(+ReLU) HIP kernels (ops/csrc/det_norm.hip) on by default; set
 # ``resnet.FUSED_BN = False`` (or hparam ``fused_bn: false``) for the stock MIOpen path.
@@ -231,7 +231,9 @@ class ResNet(nn.Module):
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             _FWD.depth -= 1
-        x = torch.flatten(self.avgpool(x), 1)
+        # the head's pooling on det_pool.hip (one read of the layer-4 output, one channels_last write
+        # of its gradient) unless a hook could observe the pool module's output
+        x = global_avg_pool(x) if FUSED_BN and _quiet(self.avgpool) else torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 

@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -119,6 +119,9 @@ _SIGNATURES = {
     "det_maxpool3s2_bwd_rows_per_block": ([], c_int),
     "det_maxpool3s2_bwd_partial_rows": ([c_int] * 4, c_i64),
     "det_maxpool3s2_set_fwd_rows": ([c_int], None),
+    # stream, dtype, x|dy, y|dx, N, HW, C (global average pooling, channels_last)
+    "det_gap_fwd": ([c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 3, c_int),
+    "det_gap_bwd": ([c_void_p, c_int, c_void_p, c_void_p] + [c_int] * 3, c_int),
     "det_bn_apply": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_i64, c_int, c_void_p, c_void_p, c_int], c_int),
     # stream, dtype, dy, x, mask_bits, M, C, mask_mode, gamma, save_mean, save_rstd, scale, shift, dx, dres,
     # dgamma, dbeta, ws

@@ -479,6 +479,62 @@ int grid_for(int64_t work) {
   return static_cast<int>(b < 1 ? 1 : b);
 }
 
+// ---- global average pooling (the ResNet head: [N, H, W, C] -> [N, C]) ----
+// torch lowers AdaptiveAvgPool2d((1, 1)) to a mean whose backward is grad.expand(N, C, H, W) / HW
+// (a strided elementwise kernel) followed by a channels_last copy for the consuming BN backward: two
+// non-vectorised passes over the 102-MB ResNet-50 layer-4 activation at batch 512
+// (profiles/r5_resnet50_steady.csv, 'elementwise_kernel_manual_unroll' x2, 0.16 ms/step).
+// forward: a block owns kGapVec 8-channel vectors of one image; its kGapPix pixel lanes each sum every
+// kGapPix-th pixel in fp32 and the lanes combine in a fixed order through LDS (deterministic).
+constexpr int kGapVec = 32, kGapPix = kThreads / kGapVec;
+template <typename T>
+__global__ void __launch_bounds__(kThreads) gap_fwd(const T* __restrict__ x, T* __restrict__ y, int HW, int C,
+                                                    float inv_hw) {
+  __shared__ float part[kGapPix][kGapVec][8];
+  const int vpi = C / 8 / kGapVec;  // blocks per image
+  const int n = blockIdx.x / vpi, cb = blockIdx.x - n * vpi;
+  const int v = threadIdx.x % kGapVec, pl = threadIdx.x / kGapVec;
+  const int c0 = (cb * kGapVec + v) * 8;
+  const T* base = x + static_cast<int64_t>(n) * HW * C + c0;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int p = pl; p < HW; p += kGapPix) {
+    float f[8];
+    Vec8<T>::load(base + static_cast<int64_t>(p) * C, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[pl][v][j] = acc[j];
+  __syncthreads();
+  if (pl != 0) return;
+  for (int q = 1; q < kGapPix; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += part[q][v][j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv_hw;
+  Vec8<T>::store(y + static_cast<int64_t>(n) * C + c0, acc);
+}
+
+// backward: dx[n, p, c] = dy[n, c] / HW, one 16-B vector of one pixel per thread (grid-stride); the
+// dy row is L2-resident, so this is a pure write stream
+template <typename T>
+__global__ void __launch_bounds__(kThreads) gap_bwd(const T* __restrict__ dy, T* __restrict__ dx, int HW, int C,
+                                                    float hw, int64_t nvec) {
+  const int cv = C / 8;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const int64_t np = i / cv;  // n * HW + p
+    const int c = static_cast<int>(i - np * cv) * 8;
+    const int64_t n = np / HW;
+    float f[8];
+    Vec8<T>::load(dy + n * C + c, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] / hw;  // as torch's MeanBackward: grad / HW, one rounding
+    Vec8<T>::store(dx + i * 8, f);
+  }
+}
+
 }  // namespace
 
 int g_fwd_rows = -1;  // -1: DET_POOL_FWD_ROWS decides on first use
@@ -609,6 +665,38 @@ int det_maxpool3s2_bwd(void* stream, int dtype, const void* dy, const void* dy2,
     else
       hipLaunchKernelGGL((maxpool_bwd<float, false, false>), grid, block, 0, st, a, b, idx, o, g, bn);
   }
+  return static_cast<int>(hipGetLastError());
+}
+
+// Global average pooling of channels_last x [N, H, W, C] -> y [N, C]; dtype 0 = fp32, 1 = bf16.
+// C % 256 == 0 (32 vectors of 8 channels per workgroup).
+int det_gap_fwd(void* stream, int dtype, const void* x, void* y, int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % (8 * kGapVec) != 0) return -1;
+  const int64_t nblk = static_cast<int64_t>(N) * (C / 8 / kGapVec);
+  if (nblk >= (static_cast<int64_t>(1) << 31)) return -3;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const float inv = 1.f / static_cast<float>(HW);
+  if (dtype == 1)
+    hipLaunchKernelGGL(gap_fwd<unsigned short>, dim3(static_cast<unsigned>(nblk)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(x), static_cast<unsigned short*>(y), HW, C, inv);
+  else
+    hipLaunchKernelGGL(gap_fwd<float>, dim3(static_cast<unsigned>(nblk)), dim3(kThreads), 0, st,
+                       static_cast<const float*>(x), static_cast<float*>(y), HW, C, inv);
+  return static_cast<int>(hipGetLastError());
+}
+
+// dy [N, C] -> dx [N, H, W, C] (channels_last, fully overwritten) = dy / HW.  C % 8 == 0.
+int det_gap_bwd(void* stream, int dtype, const void* dy, void* dx, int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % 8 != 0) return -1;
+  const int64_t nvec = static_cast<int64_t>(N) * HW * (C / 8);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const float hw = static_cast<float>(HW);
+  if (dtype == 1)
+    hipLaunchKernelGGL(gap_bwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
+                       static_cast<const unsigned short*>(dy), static_cast<unsigned short*>(dx), HW, C, hw, nvec);
+  else
+    hipLaunchKernelGGL(gap_bwd<float>, dim3(grid_for(nvec)), dim3(kThreads), 0, st, static_cast<const float*>(dy),
+                       static_cast<float*>(dx), HW, C, hw, nvec);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -1,4 +1,5 @@
-"""3x3 / stride-2 / pad-1 max pooling for channels_last activations (``det_pool.hip``).
+"""3x3 / stride-2 / pad-1 max pooling and global average pooling for channels_last activations
+(``det_pool.hip``).
 
 GPU path: one-byte argmax per output element and a gather backward (no zero fill, no atomics);
 CPU tensors and layouts the kernel does not cover (C % 8 != 0, not channels_last, fp16) use
@@ -132,3 +133,46 @@ class MaxPool3x3s2(nn.Module):
 
     def forward(self, x: torch.Tensor, bn_exclusive: bool = False) -> torch.Tensor:
         return max_pool_3x3s2(x, bn_exclusive)
+
+
+GAP_COUNTS = {"native": 0}
+
+
+def _gap_ok(x: torch.Tensor) -> bool:
+    return (x.device.type == "cuda" and x.dim() == 4 and x.dtype in _DT and x.shape[1] % 256 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+class _GlobalAvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+        st = torch._C._cuda_getCurrentRawStream(x.device.index)
+        _lib.check(_lib.get_lib().det_gap_fwd(st, _DT[x.dtype], x.data_ptr(), y.data_ptr(), N, H * W, C), "det_gap_fwd")
+        ctx.shape = (N, C, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, C, H, W = ctx.shape
+        dy = dy.contiguous()
+        dx = torch.empty((N, C, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        st = torch._C._cuda_getCurrentRawStream(dy.device.index)
+        _lib.check(_lib.get_lib().det_gap_bwd(st, _DT[dy.dtype], dy.data_ptr(), dx.data_ptr(), N, H * W, C),
+                   "det_gap_bwd")
+        return dx
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)`` (the ResNet head) for channels_last
+    activations with C % 256 == 0 on ``det_pool.hip`` (``det_gap_fwd`` / ``det_gap_bwd``); other
+    inputs take the torch path, which is also the numerics reference of the GPU test."""
+    if getattr(x, "_det_affine_apply", None) is not None:
+        from determined_1_amd.ops.conv import materialize_fwd_apply
+
+        materialize_fwd_apply(x)
+    if _gap_ok(x):
+        GAP_COUNTS["native"] += 1
+        return _GlobalAvgPool.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -165,3 +165,36 @@ def test_stem_chain_defers_bn_apply_into_patch_wgrad(gpu):
     assert torch.equal(yf, yu)  # the pool's BN + ReLU rounds exactly like the materialised apply
     torch.testing.assert_close(wf, wu, atol=2e-2 * float(wu.abs().max()), rtol=2e-2)
     torch.testing.assert_close(gf, gu, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("N,C,H,W", [(8, 2048, 7, 7), (3, 512, 1, 1), (2, 256, 14, 14), (5, 768, 7, 9)])
+def test_global_avg_pool_matches_fp32_torch(gpu, N, C, H, W, dt):
+    """det_gap_fwd / det_gap_bwd against the fp32 torch head pooling (flatten(adaptive_avg_pool2d))."""
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device=gpu).to(dt).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    n0 = pool.GAP_COUNTS["native"]
+    y = pool.global_avg_pool(x)
+    assert pool.GAP_COUNTS["native"] == n0 + 1  # the HIP path ran, not the torch fallback
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.flatten(F.adaptive_avg_pool2d(xr, 1), 1)
+    assert y.shape == yr.shape and y.dtype == dt
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), yr, rtol=tol, atol=tol)
+    g = torch.randn(N, C, device=gpu).to(dt)
+    (dx,) = torch.autograd.grad(y, x, g)
+    (dxr,) = torch.autograd.grad(yr, xr, g.float())
+    assert dx.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(dx.float(), dxr, rtol=tol, atol=tol)
+    # the gradient is g / HW in fp32 rounded once to dt: bit-exact
+    exact = (g.float() / (H * W))[:, :, None, None].expand(N, C, H, W).to(dt)
+    torch.testing.assert_close(dx, exact, rtol=0, atol=0)
+
+
+def test_global_avg_pool_falls_back_off_the_kernel_shapes(gpu):
+    x = torch.randn(2, 64, 5, 5, device=gpu).contiguous(memory_format=torch.channels_last)
+    n0 = pool.GAP_COUNTS["native"]
+    y = pool.global_avg_pool(x)
+    assert pool.GAP_COUNTS["native"] == n0
+    torch.testing.assert_close(y, x.mean((2, 3)))
