@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -176,6 +176,8 @@ _SIGNATURES = {
     "det_igemm_rows_per_block_cfg": ([c_int, c_int], c_int),
     # stream, W (KRSC), in_dtype (0 fp32 / 1 bf16), out [C, R*S*K] bf16, K, C, R, S
     "det_conv_dgrad_weight": ([c_void_p, c_void_p, c_int, c_void_p] + [c_int] * 4, c_int),
+    # stream, n, w ptrs (int64[n]), out ptrs (int64[n]), dims (int32[n][5]: K, C, R, S, bf16)
+    "det_conv_dgrad_weight_multi": ([c_void_p, c_int, c_void_p, c_void_p, c_void_p], c_int),
     # ... + cfg (0 = automatic per shape)
     "det_igemm_conv_cfg": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 2 + [c_int], c_int),
     "det_igemm_conv_bnbwd": ([c_void_p] * 5 + [c_i64] + [c_int] * 10 + [c_void_p] * 6 + [c_int], c_int),

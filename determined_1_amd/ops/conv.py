@@ -6,6 +6,7 @@ multiples of 64 (every 1x1 conv of ResNet-50 qualifies); ``supported()`` says wh
 can take the HIP path.  On CPU tensors the functions compute the same result with torch ops
 (fp32 accumulate), which is what the unit tests compare against.
 """
+import ctypes
 import os
 from typing import NamedTuple, Optional, Tuple
 
@@ -275,12 +276,66 @@ def igemm_conv(x: torch.Tensor, w: torch.Tensor, stride: int = 1, pad: int = 0, 
     return y, parts
 
 
+def _dw_ok(w: torch.Tensor) -> bool:
+    return is_gpu(w) and w.dtype in (torch.float32, torch.bfloat16) and w.is_contiguous(memory_format=torch.channels_last)
+
+
+# Batched flips (det_conv_dgrad_weight_multi): every R x S conv forward that will need its input
+# gradient registers its weight (_DW_PENDING); the first dgrad_weight call of the backward flips all
+# pending weights in one launch into _DW_READY, and each later call takes its own.  Entries are keyed
+# by (data_ptr, shape, dtype) and computed during the backward from the weights as they are then --
+# a weight changes only between backward passes (optimizer), and its next forward drops its old
+# entry -- so no flip is ever older than the forward that uses it.  DW_BATCH = False: one launch each.
+DW_BATCH = os.environ.get("DET_DW_BATCH", "1") != "0"
+_DW_PENDING: dict = {}
+_DW_READY: dict = {}
+DW_COUNTS = {"batched_launches": 0, "served": 0}
+
+
+def _dw_key(w: torch.Tensor):
+    return (w.data_ptr(), tuple(w.shape), w.dtype)
+
+
+def dgrad_weight_register(w: torch.Tensor) -> None:
+    """Called by the forward of an R x S conv whose backward will flip ``w`` (see DW_BATCH)."""
+    if DW_BATCH and _dw_ok(w):
+        key = _dw_key(w)
+        _DW_READY.pop(key, None)
+        _DW_PENDING[key] = w
+
+
+def _dgrad_weight_flush(w: torch.Tensor) -> None:
+    _DW_PENDING[_dw_key(w)] = w
+    items = list(_DW_PENDING.items())
+    _DW_PENDING.clear()
+    ws, outs, dims = [], [], []
+    for key, t in items:
+        k, c, r, s = t.shape
+        out = torch.empty(c, r * s * k, dtype=torch.bfloat16, device=t.device)
+        _DW_READY[key] = out
+        ws.append(t.data_ptr())
+        outs.append(out.data_ptr())
+        dims += [k, c, r, s, 1 if t.dtype == torch.bfloat16 else 0]
+    wa = (ctypes.c_int64 * len(ws))(*ws)
+    oa = (ctypes.c_int64 * len(outs))(*outs)
+    da = (ctypes.c_int * len(dims))(*dims)
+    _lib.check(_lib.get_lib().det_conv_dgrad_weight_multi(_stream(w), len(ws), wa, oa, da), "conv_dgrad_weight_multi")
+    DW_COUNTS["batched_launches"] += 1
+
+
 def dgrad_weight(w: torch.Tensor) -> torch.Tensor:
     """[Cout, Cin, R, S] -> the [Cin, R*S*Cout] KRSC weight whose forward conv (stride 1, pad
     (R-1)/2) of dY is the input gradient: W'[c][r][s][k] = W[k][c][R-1-r][S-1-s].  One HIP
-    transpose launch for channels_last fp32/bf16 weights on the GPU."""
+    transpose launch for channels_last fp32/bf16 weights on the GPU, or one for all the weights
+    registered by their forwards (DW_BATCH)."""
     k, c, r, s = w.shape
-    if is_gpu(w) and w.dtype in (torch.float32, torch.bfloat16) and w.is_contiguous(memory_format=torch.channels_last):
+    if DW_BATCH and _dw_ok(w) and (_DW_PENDING or _DW_READY):
+        key = _dw_key(w)
+        if key not in _DW_READY:
+            _dgrad_weight_flush(w)
+        DW_COUNTS["served"] += 1
+        return _DW_READY.pop(key)
+    if _dw_ok(w):
         out = torch.empty(c, r * s * k, dtype=torch.bfloat16, device=w.device)
         _lib.check(_lib.get_lib().det_conv_dgrad_weight(_stream(w), w.data_ptr(), 1 if w.dtype == torch.bfloat16 else 0,
                                                          out.data_ptr(), int(k), int(c), int(r), int(s)),
@@ -823,6 +878,8 @@ class _ConvRS(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
         ctx.bn_producer = bn_producer
+        if ctx.needs_input_grad[0]:
+            dgrad_weight_register(weight)  # flipped with the step's other R x S weights (DW_BATCH)
         return y
 
     @staticmethod

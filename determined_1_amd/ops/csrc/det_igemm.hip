@@ -1140,6 +1140,48 @@ __global__ void __launch_bounds__(256) dgrad_weight_kernel(const TI* __restrict_
   }
 }
 
+// The same transpose for up to kDwMulti weights in ONE launch (ops/conv.py flips every R x S weight a
+// backward pass needs at its first input gradient): one launch per weight was 16 latency-bound
+// launches of 9-576 workgroups per ResNet-50 step (0.19 ms, profiles/r5_resnet50_steady.csv).
+constexpr int kDwMulti = 32;
+struct DwMultiArgs {
+  int n;
+  int start[kDwMulti + 1];  // first workgroup of each weight (prefix sums)
+  const void* w[kDwMulti];
+  unsigned short* out[kDwMulti];
+  int K[kDwMulti], C[kDwMulti], R[kDwMulti], S[kDwMulti], bf16[kDwMulti];
+};
+
+__global__ void __launch_bounds__(256) dgrad_weight_multi_kernel(DwMultiArgs a) {
+  __shared__ float tile[64][65];
+  int t = 0;
+  while (t + 1 < a.n && static_cast<int>(blockIdx.x) >= a.start[t + 1]) ++t;
+  const int K = a.K[t], C = a.C[t], R = a.R[t], S = a.S[t];
+  const int gx = (C + 63) / 64, gy = (K + 63) / 64;
+  const int local = static_cast<int>(blockIdx.x) - a.start[t];
+  const int tap = local / (gx * gy), rem = local - tap * gx * gy;
+  const int k0 = (rem / gx) * 64, c0 = (rem % gx) * 64;
+  const int r = tap / S, s2 = tap - r * S;
+  const int src_tap = (R - 1 - r) * S + (S - 1 - s2);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const bool bf = a.bf16[t] != 0;
+  for (int i = ty; i < 64; i += 4) {
+    const int k = k0 + i, c = c0 + tx;
+    float v = 0.f;
+    if (k < K && c < C) {
+      const int64_t off = (static_cast<int64_t>(k) * R * S + src_tap) * C + c;
+      v = bf ? bf2f(static_cast<const unsigned short*>(a.w[t])[off]) : static_cast<const float*>(a.w[t])[off];
+    }
+    tile[i][tx] = v;
+  }
+  __syncthreads();
+  unsigned short* out = a.out[t];
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, k = k0 + tx;
+    if (c < C && k < K) out[(static_cast<int64_t>(c) * R * S + tap) * K + k] = f2bf(tile[tx][i]);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Weight gradient on the LDS-DMA ring: P[split][N][RSC] (fp32 slab per pixel split) =
 //   sum_{m in split} dY[m][n] . im2col(X)[m][rsc]            (rsc = (r*S + s)*Cin + c, KRSC order)
@@ -2194,6 +2236,33 @@ int det_stemp_fwd(void* stream, const void* X, const void* W, void* Y, int64_t M
 }
 
 // out[C][R*S*K] bf16 = the flipped, transposed KRSC weight the stride-1 input gradient convolves with.
+// det_conv_dgrad_weight for n weights in one launch per kDwMulti: w[i] (KRSC, fp32 or bf16 per
+// dims[i*5+4] = 1 for bf16) -> out[i] (bf16 [C, R*S*K]); dims[i*5 .. +3] = K, C, R, S.
+int det_conv_dgrad_weight_multi(void* stream, int n, const int64_t* w, const int64_t* out, const int* dims) {
+  if (n <= 0) return -1;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  for (int b = 0; b < n; b += kDwMulti) {
+    DwMultiArgs a{};
+    a.n = n - b < kDwMulti ? n - b : kDwMulti;
+    int64_t total = 0;
+    for (int i = 0; i < a.n; ++i) {
+      const int* d = dims + 5 * (b + i);
+      if (d[0] <= 0 || d[1] <= 0 || d[2] <= 0 || d[3] <= 0) return -1;
+      a.K[i] = d[0]; a.C[i] = d[1]; a.R[i] = d[2]; a.S[i] = d[3]; a.bf16[i] = d[4];
+      a.w[i] = reinterpret_cast<const void*>(w[b + i]);
+      a.out[i] = reinterpret_cast<unsigned short*>(out[b + i]);
+      a.start[i] = static_cast<int>(total);
+      total += static_cast<int64_t>((d[1] + 63) / 64) * ((d[0] + 63) / 64) * d[2] * d[3];
+      if (total >= (static_cast<int64_t>(1) << 31)) return -3;
+    }
+    a.start[a.n] = static_cast<int>(total);
+    hipLaunchKernelGGL(dgrad_weight_multi_kernel, dim3(static_cast<unsigned>(total)), dim3(256), 0, st, a);
+    const int rc = static_cast<int>(hipGetLastError());
+    if (rc != 0) return rc;
+  }
+  return 0;
+}
+
 int det_conv_dgrad_weight(void* stream, const void* W, int in_dtype, void* out, int K, int C, int R, int S) {
   if (K <= 0 || C <= 0 || R <= 0 || S <= 0) return -1;
   const dim3 grid((C + 63) / 64, (K + 63) / 64, R * S);

@@ -146,6 +146,57 @@ def test_dgrad_weight_kernel_matches_torch(gpu):
         assert torch.equal(got, ref)
 
 
+def test_dgrad_weight_multi_matches_single_flips(gpu, monkeypatch):
+    """det_conv_dgrad_weight_multi: every weight registered by a forward flipped in ONE launch at the
+    backward's first dgrad_weight call, bit-equal to the torch flip (40 weights: two 32-entry chunks)."""
+    monkeypatch.setattr(conv, "DW_BATCH", True)
+    conv._DW_PENDING.clear()
+    conv._DW_READY.clear()
+    torch.manual_seed(0)
+    shapes = [(64, 64, 3, 3), (128, 128, 3, 3), (512, 512, 3, 3), (96, 192, 3, 3), (64, 8, 7, 7), (200, 72, 5, 5)]
+    ws = []
+    for i in range(40):
+        k, c, r, s = shapes[i % len(shapes)]
+        dt = torch.bfloat16 if i % 3 else torch.float32
+        ws.append(torch.randn(k, c, r, s, device=gpu).to(dt).contiguous(memory_format=torch.channels_last))
+    for w in ws:
+        conv.dgrad_weight_register(w)
+    b0, s0 = conv.DW_COUNTS["batched_launches"], conv.DW_COUNTS["served"]
+    for w in reversed(ws):  # backward order
+        k, c, r, s = w.shape
+        ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).to(torch.bfloat16)
+        assert torch.equal(conv.dgrad_weight(w), ref)
+    assert conv.DW_COUNTS["batched_launches"] == b0 + 1
+    assert conv.DW_COUNTS["served"] == s0 + len(ws)
+    assert not conv._DW_PENDING and not conv._DW_READY
+
+
+def test_batched_flips_follow_in_place_weight_updates(gpu, monkeypatch):
+    """Three forward/backward steps of two 3x3 convs with the weights changed in place between steps
+    (as the fused optimizer does, without a version bump): every input gradient uses the weights of
+    its own forward."""
+    monkeypatch.setattr(conv, "DW_BATCH", True)
+    torch.manual_seed(1)
+    m1 = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).to(gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    m2 = torch.nn.Conv2d(64, 64, 3, padding=1, bias=False).to(gpu).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for step in range(3):
+        x = torch.randn(2, 64, 14, 14, device=gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x.requires_grad_(True)
+        b0 = conv.DW_COUNTS["batched_launches"]
+        y = conv.conv_rs(conv.conv_rs(x, m1), m2)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        assert conv.DW_COUNTS["batched_launches"] == b0 + 1  # both flips in one launch
+        xr = x.detach().float().requires_grad_(True)
+        yr = F.conv2d(F.conv2d(xr, m1.weight.detach().float(), padding=1).to(torch.bfloat16).float(),
+                      m2.weight.detach().float(), padding=1)
+        yr.backward(dy.float())
+        torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-2 * float(xr.grad.abs().max()))
+        with torch.no_grad():  # in-place update through the raw storage: no version counter change
+            m1.weight.data.copy_(torch.randn_like(m1.weight) * 0.05)
+            m2.weight.data.copy_(torch.randn_like(m2.weight) * 0.05)
+
+
 @pytest.mark.parametrize("wgrad_mode", ["miopen", "auto", "native"])
 @pytest.mark.parametrize("stride", [1, 2])
 def test_conv_rs_autograd_end_to_end(gpu, stride, wgrad_mode, monkeypatch):

@@ -187,9 +187,10 @@ def test_global_avg_pool_matches_fp32_torch(gpu, N, C, H, W, dt):
     (dxr,) = torch.autograd.grad(yr, xr, g.float())
     assert dx.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(dx.float(), dxr, rtol=tol, atol=tol)
-    # the gradient is g / HW in fp32 rounded once to dt: bit-exact
+    # the gradient is g / HW in fp32 rounded once to dt: bit-exact in bf16, within 1 fp32 ulp in fp32
+    # (the device's fp32 division vs torch's)
     exact = (g.float() / (H * W))[:, :, None, None].expand(N, C, H, W).to(dt)
-    torch.testing.assert_close(dx, exact, rtol=0, atol=0)
+    torch.testing.assert_close(dx, exact, rtol=0 if dt == torch.bfloat16 else 2.4e-7, atol=0)
 
 
 def test_global_avg_pool_falls_back_off_the_kernel_shapes(gpu):
