@@ -421,6 +421,23 @@ def test_u8_normalize_pad4(gpu):
     assert float(got[:, 3].abs().max()) == 0.0
 
 
+def test_u8_normalize_pad4_quad_kernel_bit_equal(gpu):
+    """The four-pixel C=3 kernel (npix % 4 == 0) against the per-pixel kernel (npix % 4 != 0) on the same
+    pixels: bit-equal, and within bf16 rounding of the CPU reference."""
+    from determined_1_amd.ops.functional import u8_normalize
+
+    g = torch.Generator().manual_seed(1)
+    u8 = torch.randint(0, 256, (2, 16, 28, 3), generator=g, dtype=torch.uint8)
+    mean, std = (0.485 * 255, 0.456 * 255, 0.406 * 255), (0.229 * 255, 0.224 * 255, 0.225 * 255)
+    quad = u8_normalize(u8.to(gpu), mean, std, out_dtype=torch.bfloat16, pad4=True)   # 896 pixels
+    part = u8[:, :5, :7].contiguous()                                                 # 70 pixels
+    single = u8_normalize(part.to(gpu), mean, std, out_dtype=torch.bfloat16, pad4=True)
+    assert torch.equal(quad[:, :, :5, :7], single)
+    ref = u8_normalize(u8, mean, std, out_dtype=torch.bfloat16, pad4=True)
+    torch.testing.assert_close(quad.cpu().float(), ref.float(), rtol=1e-2, atol=1e-2)
+    assert float(quad[:, 3].abs().max()) == 0.0
+
+
 def test_resnet50_native_stem_matches_miopen(gpu):
     """Three SGD steps of ResNet-50 with the stem on det_conv (4-channel padded input) vs on MIOpen."""
     from determined_1_amd.models import resnet
