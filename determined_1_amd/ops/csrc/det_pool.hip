@@ -518,20 +518,20 @@ __global__ void __launch_bounds__(kThreads) gap_fwd(const T* __restrict__ x, T* 
 
 // backward: dx[n, p, c] = dy[n, c] / HW, one 16-B vector of one pixel per thread (grid-stride); the
 // dy row is L2-resident, so this is a pure write stream
+// (32-bit index math: nvec < 2^31, checked by the host -- a 64-bit division is a long software sequence)
 template <typename T>
 __global__ void __launch_bounds__(kThreads) gap_bwd(const T* __restrict__ dy, T* __restrict__ dx, int HW, int C,
-                                                    float hw, int64_t nvec) {
-  const int cv = C / 8;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < nvec;
-       i += static_cast<int64_t>(gridDim.x) * kThreads) {
-    const int64_t np = i / cv;  // n * HW + p
-    const int c = static_cast<int>(i - np * cv) * 8;
-    const int64_t n = np / HW;
+                                                    float hw, int nvec) {
+  const uint32_t cv = static_cast<uint32_t>(C) / 8;
+  for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < static_cast<uint32_t>(nvec); i += gridDim.x * kThreads) {
+    const uint32_t np = i / cv;  // n * HW + p
+    const uint32_t c = (i - np * cv) * 8;
+    const uint32_t n = np / static_cast<uint32_t>(HW);
     float f[8];
-    Vec8<T>::load(dy + n * C + c, f);
+    Vec8<T>::load(dy + static_cast<int64_t>(n) * C + c, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = f[j] / hw;  // as torch's MeanBackward: grad / HW, one rounding
-    Vec8<T>::store(dx + i * 8, f);
+    Vec8<T>::store(dx + static_cast<int64_t>(i) * 8, f);
   }
 }
 
@@ -689,14 +689,15 @@ int det_gap_fwd(void* stream, int dtype, const void* x, void* y, int N, int HW, 
 int det_gap_bwd(void* stream, int dtype, const void* dy, void* dx, int N, int HW, int C) {
   if (N <= 0 || HW <= 0 || C <= 0 || C % 8 != 0) return -1;
   const int64_t nvec = static_cast<int64_t>(N) * HW * (C / 8);
+  if (nvec >= (static_cast<int64_t>(1) << 31)) return -3;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const float hw = static_cast<float>(HW);
   if (dtype == 1)
     hipLaunchKernelGGL(gap_bwd<unsigned short>, dim3(grid_for(nvec)), dim3(kThreads), 0, st,
-                       static_cast<const unsigned short*>(dy), static_cast<unsigned short*>(dx), HW, C, hw, nvec);
+                       static_cast<const unsigned short*>(dy), static_cast<unsigned short*>(dx), HW, C, hw, static_cast<int>(nvec));
   else
     hipLaunchKernelGGL(gap_bwd<float>, dim3(grid_for(nvec)), dim3(kThreads), 0, st, static_cast<const float*>(dy),
-                       static_cast<float*>(dx), HW, C, hw, nvec);
+                       static_cast<float*>(dx), HW, C, hw, static_cast<int>(nvec));
   return static_cast<int>(hipGetLastError());
 }
 
