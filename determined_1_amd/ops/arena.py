@@ -143,6 +143,20 @@ def landing_buffer(p: torch.Tensor) -> Optional[torch.Tensor]:
     return a.view(a.flat_grad, i)
 
 
+def notify_direct_grads(params: Sequence[torch.Tensor]) -> None:
+    """A backward that accumulated into ``p.grad`` in place (inside a hipGraph capture, the arena
+    views pinned) returns None to autograd, so AccumulateGrad -- and with it every post-accumulate
+    hook -- never runs for ``p``.  Run those hooks here, in the order autograd would have, so the
+    DP gradient bucketer still counts the parameter (its bucket, and the buckets behind it, launch
+    on time instead of at synchronize()) and user hooks see the gradient.  Direct writers:
+    transformer._Embed, cnn._CifarCNN."""
+    for p in params:
+        hooks = getattr(p, "_post_accumulate_grad_hooks", None)
+        if hooks:
+            for h in list(hooks.values()):
+                h(p)
+
+
 def build_arenas(params: Sequence[torch.nn.Parameter], device: torch.device) -> List[Arena]:
     """Group ``params`` (one optimizer param group) by dtype and build one arena per dtype.
 

@@ -74,9 +74,16 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+# largest per-image tensor of the network (conv1's activation / gradient, 30 x 30 x 32): det_cnn.hip's
+# index math is 32-bit, so a batch is native only while N * this < 2^31
+_MAX_ELEMS_PER_IMAGE = 30 * 30 * 32
+
+
 def supported(x: torch.Tensor, params: Sequence[torch.Tensor]) -> bool:
     if not (x.is_cuda and x.dim() == 4 and tuple(x.shape[1:]) == (3, 32, 32) and x.dtype in _DT):
         return False
+    if x.shape[0] * _MAX_ELEMS_PER_IMAGE >= (1 << 31):
+        return False  # det_cnn.hip indexes with 32-bit math: the torch layers take oversized batches
     if any(p.device != x.device or p.dtype != x.dtype for p in params):
         return False
     shapes = [(32, 3, 3, 3), (32,), (32, 32, 3, 3), (32,), (64, 32, 3, 3), (64,), (64, 64, 3, 3), (64,), (512, 2304),
@@ -302,6 +309,9 @@ def _backward(dlogits: torch.Tensor, params: Sequence[torch.Tensor], saved):
     step(R.prepare(Job(a=Operand(p=dy1.data_ptr(), dt=dt, src=S_GRAD_CONV_T, C=32, OH=30, OW=30, transpose=1),
                         b=_conv_act(xh, dt, 32, 3, 0, 30), M=32, N=28, K=n * 900, **gconv(0, 3))))
     R.finish(deferred)
+    from determined_1_amd.ops.arena import notify_direct_grads
+
+    notify_direct_grads([p for p, t in zip(params, targets) if not t[1]])  # written in place: no AccumulateGrad
     return [t[0] if t[1] else None for t in targets]
 
 

@@ -49,8 +49,9 @@ struct Plan {
   bool bias;
 };
 
-// (transa, transb, m, n, k, lda, ldb, ldd, bias, beta != 0, dtype)
-typedef std::tuple<int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int> Key;
+// (device, transa, transb, m, n, k, lda, ldb, ldd, bias, beta != 0, dtype).  The plan is only used
+// with 16-B aligned operands (ops/transformer.py _bl_ok), so alignment needs no key field.
+typedef std::tuple<int, int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int> Key;
 std::map<Key, Plan> g_plans;
 
 template <typename F>
@@ -93,7 +94,9 @@ int det_blaslt_gemm(void* stream, int transa, int transb, int64_t m, int64_t n, 
                     const void* B, int64_t ldb, void* D, int64_t ldd, const void* bias, float beta, int dtype, void* ws,
                     int64_t ws_bytes) {
   if (!g_api.ok) return -10;
-  const Key key{transa, transb, m, n, k, lda, ldb, ldd, bias != nullptr, beta != 0.f, dtype};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -16;
+  const Key key{dev, transa, transb, m, n, k, lda, ldb, ldd, bias != nullptr, beta != 0.f, dtype};
   Plan p;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -136,12 +139,11 @@ int det_blaslt_gemm(void* stream, int transa, int transb, int64_t m, int64_t n, 
   if (static_cast<int64_t>(p.ws) > ws_bytes) return -15;
   const float alpha = 1.f;
   hipblasStatus_t st;
-  if (p.bias) {  // the bias pointer lives in the shared descriptor: set it and launch under the lock
+  {
+    // one handle for the process, used from the forward thread and autograd's backward thread: every
+    // launch runs under the lock (the bias pointer also lives in the shared descriptor)
     std::lock_guard<std::mutex> lk(g_mu);
-    g_api.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
-    st = g_api.matmul(g_api.handle, p.desc, &alpha, A, p.a, B, p.b, &beta, D, p.d, D, p.d, &p.algo, ws, p.ws,
-                      static_cast<hipStream_t>(stream));
-  } else {
+    if (p.bias) g_api.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
     st = g_api.matmul(g_api.handle, p.desc, &alpha, A, p.a, B, p.b, &beta, D, p.d, D, p.d, &p.algo, ws, p.ws,
                       static_cast<hipStream_t>(stream));
   }

@@ -195,8 +195,8 @@ def _bl_ok(*ts: torch.Tensor) -> bool:
     if not BLASLT or not ts[0].is_cuda:
         return False
     dt = ts[0].dtype
-    if dt not in _BL_DT or any(t.dtype != dt or not t.is_contiguous() or t.dim() > 2 for t in ts):
-        return False
+    if dt not in _BL_DT or any(t.dtype != dt or not t.is_contiguous() or t.dim() > 2 or t.data_ptr() % 16 for t in ts):
+        return False  # the cached plans assume 16-B aligned operands
     ready = _BL["ready"]
     if ready is None:
         path = os.path.join(os.path.dirname(torch.__file__), "lib", "libhipblaslt.so")
@@ -205,11 +205,12 @@ def _bl_ok(*ts: torch.Tensor) -> bool:
         _BL["fn"] = lib.det_blaslt_gemm
     if not ready:
         return False
-    dev = ts[0].device.index
-    if dev not in _BL["ws"]:
-        if torch.cuda.is_current_stream_capturing():
-            return False  # the workspace must outlive any graph: allocated by an eager call first
-        _BL["ws"][dev] = torch.empty(_BL_WS_BYTES, dtype=torch.uint8, device=ts[0].device)
+    key = (ts[0].device.index, torch._C._cuda_getCurrentRawStream(ts[0].device.index))
+    if key not in _BL["ws"]:
+        # one workspace per (device, stream), as torch keeps its BLAS workspaces: GEMMs on two
+        # streams (an eager step beside a graph replay, a side stream) never share scratch.  Made
+        # inside a capture it comes from that graph's private pool and stays allocated (held here).
+        _BL["ws"][key] = torch.empty(_BL_WS_BYTES, dtype=torch.uint8, device=ts[0].device)
     return True
 
 
@@ -217,9 +218,10 @@ def _bl_gemm(ta: int, tb: int, m: int, n: int, k: int, A: torch.Tensor, lda: int
              D: torch.Tensor, ldd: int, bias: Optional[torch.Tensor] = None, beta: float = 0.0) -> None:
     """Column-major D[m, n] = op(A) op(B) [+ bias per row] [+ beta D] (see det_blaslt.hip)."""
     dev = D.device.index
-    rc = _BL["fn"](torch._C._cuda_getCurrentRawStream(dev), ta, tb, m, n, k, A.data_ptr(), lda, B.data_ptr(), ldb,
+    stream = torch._C._cuda_getCurrentRawStream(dev)
+    rc = _BL["fn"](stream, ta, tb, m, n, k, A.data_ptr(), lda, B.data_ptr(), ldb,
                    D.data_ptr(), ldd, None if bias is None else bias.data_ptr(), beta, _BL_DT[D.dtype],
-                   _BL["ws"][dev].data_ptr(), _BL_WS_BYTES)
+                   _BL["ws"][(dev, stream)].data_ptr(), _BL_WS_BYTES)
     if rc != 0:
         _lib.check(rc, "det_blaslt_gemm")
 
@@ -279,6 +281,8 @@ def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_
         K = weight.shape[1]
         dx = torch.empty(M, K, dtype=dz.dtype, device=dz.device)
         _bl_gemm(0, 0, K, M, N, weight, K, dz, N, dx, K)
+        if dr is not None:  # a linked residual gradient the beta = 1 branch could not take (layout)
+            dx.add_(dr.reshape(dx.shape))
     else:
         dx = dz @ weight if need_x else None
         if dr is not None:
@@ -714,6 +718,9 @@ class _Embed(torch.autograd.Function):
                                      g.data_ptr(), dww.data_ptr(), dwt.data_ptr(), dwp.data_ptr(), B * S, S, H, wt.shape[0],
                                      ctx.pad, ws.data_ptr(), acc), "det_embed_bwd")
         if direct:
+            from determined_1_amd.ops.arena import notify_direct_grads
+
+            notify_direct_grads((ww, wt, wp))  # autograd's post-accumulate hooks never see these
             return None, None, None, None, None, None
         return None, None, dww, dwt, dwp, None
 

@@ -324,21 +324,33 @@ class PyTorchTrialContext(trial.TrialContext):
         agg = self.dist_config.aggregation_frequency
         if agg <= 1 or self._current_batch_idx is None or (self._current_batch_idx + 1) % agg == 0:
             return None
-        grads = [[p.grad for p in m.parameters()] for m in self.models]
+        params = [list(m.parameters()) for m in self.models]
+        grads = [[p.grad for p in ps] for ps in params]
         if self.dist_config.use and pdist.is_initialized() and self.distributed.get_size() > 1:
             import torch.distributed as tdist
 
-            live = [g for gs in grads for g in gs if g is not None]
-            if live:
-                flat = torch.cat([g.detach().reshape(-1).float() for g in live])
+            # one flat buffer over EVERY parameter on every rank (zeros where this rank has no
+            # .grad) plus a presence flag per parameter, so all ranks issue the same collective of
+            # the same length even when a parameter is unused on some of them
+            flat_ps = [p for ps in params for p in ps]
+            if flat_ps:
+                dev = flat_ps[0].device
+                parts = [(p.grad.detach().reshape(-1).float().to(dev) if p.grad is not None
+                          else torch.zeros(p.numel(), dtype=torch.float32, device=dev)) for p in flat_ps]
+                present = torch.tensor([1.0 if p.grad is not None else 0.0 for p in flat_ps], dtype=torch.float32,
+                                       device=dev)
+                flat = torch.cat(parts + [present])
                 tdist.all_reduce(flat)
+                n = sum(p.numel() for p in flat_ps)
+                present = flat[n:]
                 off = 0
                 summed = []
-                for g in live:
-                    summed.append(flat[off:off + g.numel()].view_as(g).to(g.dtype))
-                    off += g.numel()
+                for i, p in enumerate(flat_ps):
+                    g = flat[off:off + p.numel()].view_as(p)
+                    off += p.numel()
+                    summed.append(g.to(p.grad.dtype if p.grad is not None else p.dtype) if present[i] > 0 else None)
                 it = iter(summed)
-                grads = [[None if g is None else next(it) for g in gs] for gs in grads]
+                grads = [[next(it) for _ in ps] for ps in params]
             if self.distributed.get_rank() != 0:
                 return None
         return [[None if g is None else g.detach().to("cpu", copy=True) for g in gs] for gs in grads]

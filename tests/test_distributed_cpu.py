@@ -166,3 +166,23 @@ def test_bench_rejects_mismatched_world():
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=300, cwd=repo, env=env)
     assert r.returncode == 2 and "--gpus is 2" in r.stderr
+
+
+def test_partial_window_grads_with_missing_grad_on_one_rank(tmp_path):
+    """one rank without a .grad for a parameter still joins the same all-reduce (zeros
+    plus a presence flag), so the mid-window checkpoint neither hangs nor misaligns the sums."""
+    port = _free_port()
+    out = str(tmp_path / "pw.pt")
+    script = os.path.join(HERE, "dist_scripts", "partial_window_worker.py")
+    procs = [subprocess.Popen([sys.executable, script, out],
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                                       MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
+    for p in procs:
+        o, _ = p.communicate(timeout=120)
+        assert p.returncode == 0, o.decode()[-3000:]
+    got = torch.load(out)[0]
+    # parameter i holds (rank + 1 + i) on each rank that has it; rank 1 has none for i = 2
+    for i, g in enumerate(got):
+        want = float(1 + i) + (0.0 if i == 2 else float(2 + i))
+        assert torch.equal(g, torch.full_like(g, want)), (i, g)
