@@ -79,7 +79,9 @@ CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 # off MIOpen (torch.backends.cudnn.enabled = False), or with only Linear layers replay exactly; every
 # MIOpen op captured alone replays exactly.  This was the round-4 "O2 + dropout" NaN of the CIFAR
 # trial (dropout was incidental: the NaN stays with dropout removed and with masks from a fixed bank).
-# The first warm-up step of a graph key runs under this probe; a hit keeps train_batch eager.
+# The first warm-up step of EVERY graph key runs under this probe; a hit keeps that key eager (other
+# keys still capture: their graphs hold no MIOpen kernel, so eager MIOpen work between their replays
+# is harmless).
 # DET_GRAPH_LIBRARY_CONVS=1 captures anyway (for the reproduction scripts).
 LIBRARY_CONV_OPS = ("aten::convolution", "aten::convolution_backward", "aten::_convolution",
                     "aten::miopen_convolution", "aten::cudnn_convolution")
@@ -197,7 +199,10 @@ class TrainStepGraph:
         self.chunk_disabled: Optional[str] = None
         self.chunk_replays = 0
         self.last_chunk_metrics: Optional[List[Any]] = None
-        self.probed = False  # the first warm-up step ran under the library-convolution probe
+        # graph key -> None (its first warm-up step ran clean under the library-convolution probe) or
+        # the reason it stays eager.  Per key, not per controller: another batch shape, an epoch-
+        # sensitive key or a new hyper-parameter signature can route to different kernels.
+        self.probed: Dict[Any, Optional[str]] = {}
 
     # ------------------------------------------------------------------------------------------
     @staticmethod
@@ -241,16 +246,18 @@ class TrainStepGraph:
         g = self.graphs.get(key)
         if g is not None:
             return self._replay(g, leaves)
+        if self.probed.get(key) is not None:  # this key routes to replay-unsafe kernels: eager
+            return self._eager(batch, epoch_idx, batch_idx)
         n = self.seen.get(key, 0) + 1
         self.seen[key] = n
-        if n <= WARMUP:
-            if self.probed:
-                return self._eager(batch, epoch_idx, batch_idx)
-            self.probed = True
+        if key not in self.probed:
             out, reason = library_conv_reason(lambda: self._eager(batch, epoch_idx, batch_idx))
+            self.probed[key] = reason
             if reason is not None:
-                self._disable(reason)
+                logging.warning("hip_graph: train_batch runs eagerly for batch signature %s: %s", key[0], reason)
             return out
+        if n <= WARMUP:
+            return self._eager(batch, epoch_idx, batch_idx)
         g = self._capture(key, leaves, spec, epoch_idx, batch_idx)
         if g is None:
             return self._eager(batch, epoch_idx, batch_idx)
@@ -340,6 +347,8 @@ class TrainStepGraph:
             if all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
                 key = ("chunk", chunk.sizes, self._key(leaves, epoch_idx))
                 g = self.chunk_graphs.get(key)
+                if g is None and not self._batch_key_clean(chunk, epoch_idx):
+                    key = None  # warm up / probe per batch first; a replay-unsafe key stays per batch
                 if g is not None:
                     for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
                         dst.copy_(src, non_blocking=True)
@@ -351,8 +360,9 @@ class TrainStepGraph:
                     self.chunk_replays += 1
                     g.replays += 1
                     return self._clone_out(g.out)
-                n = self.seen.get(key, 0) + 1
-                self.seen[key] = n
+                n = self.seen.get(key, 0) + 1 if key is not None else 0
+                if key is not None:
+                    self.seen[key] = n
                 if n > CHUNK_WARMUP:
                     g = self._capture_chunk(key, leaves, spec, chunk.sizes, epoch_idx, batch_idx)
                     if g is not None:
@@ -369,6 +379,12 @@ class TrainStepGraph:
                                         self.run(b, epoch_idx, batch_idx + i)))
         self.last_chunk_metrics = outs
         return None
+
+    def _batch_key_clean(self, chunk: Any, epoch_idx: int) -> bool:
+        """Whether the per-batch graph key of the chunk's first batch probed clean."""
+        bl, _ = pytree.tree_flatten(chunk.batches[0])
+        k = self._key(bl, epoch_idx)
+        return k in self.probed and self.probed[k] is None
 
     def _capture_chunk(self, key: Any, leaves: List[Any], spec: Any, sizes: Tuple[int, ...], epoch_idx: int,
                        batch_idx: int) -> Optional[_Graph]:
@@ -435,6 +451,7 @@ class EvalStepGraph:
         self.disabled_reason: Optional[str] = None
         self.captures = 0
         self.replays = 0
+        self.probed: Dict[Any, Optional[str]] = {}
 
     def _eager(self, batch: Any) -> Any:
         with self.context._autocast():
@@ -452,15 +469,16 @@ class EvalStepGraph:
         if g is None:
             n = self.seen.get(key, 0) + 1
             self.seen[key] = n
-            if n <= self.WARMUP:
-                if getattr(self, "probed", False):
-                    return self._eager(batch)
-                self.probed = True
+            if self.probed.get(key) is not None:
+                return self._eager(batch)
+            if key not in self.probed:  # every key's first batch under the probe (as TrainStepGraph)
                 out, reason = library_conv_reason(lambda: self._eager(batch))
+                self.probed[key] = reason
                 if reason is not None:
-                    logging.warning("hip_graph: evaluate_batch runs eagerly: %s", reason)
-                    self.disabled_reason = reason
+                    logging.warning("hip_graph: evaluate_batch runs eagerly for batch signature %s: %s", key, reason)
                 return out
+            if n <= self.WARMUP:
+                return self._eager(batch)
             if len(self.graphs) >= MAX_GRAPHS:
                 torch.cuda.synchronize()
                 while len(self.graphs) >= MAX_GRAPHS:
@@ -500,7 +518,9 @@ class EvalStepGraph:
                 all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
             key = ("chunk", chunk.sizes, tuple(_leaf_sig(x) for x in leaves))
             g = self.graphs.get(key)
-            if g is None and self.seen.get(key, 0) >= self.WARMUP:
+            bkey = tuple(_leaf_sig(x) for x in pytree.tree_flatten(chunk.batches[0])[0])
+            clean = bkey in self.probed and self.probed[bkey] is None  # per-batch key probed clean
+            if g is None and self.seen.get(key, 0) >= self.WARMUP and clean:
                 if len(self.graphs) >= CHUNK_MAX_GRAPHS:
                     torch.cuda.synchronize()
                     while len(self.graphs) >= CHUNK_MAX_GRAPHS:

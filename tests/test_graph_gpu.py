@@ -104,3 +104,50 @@ def test_eval_graph_matches_eager(gpu, monkeypatch):
         if graph:
             assert ctrl._eval_graph is not None and ctrl._eval_graph.replays >= 8, ctrl._eval_graph.__dict__
     assert abs(results[0] - results[1]) <= 1e-4 * abs(results[0]) + 1e-5
+
+
+class TwoKeyTrial(ConvTrial):
+    """The epoch's tail batch (6 of 150 records at batch 16) runs its convolutions under bf16 autocast
+    (functional convs on MIOpen); the full batches stay fp32.  Two graph keys, one replay-unsafe."""
+
+    def build_training_data_loader(self):
+        g = torch.Generator().manual_seed(1)
+        x = torch.randn(150, 3, 16, 16, generator=g)
+        y = torch.randint(0, 10, (150,), generator=g)
+        return pytorch.DataLoader(torch.utils.data.TensorDataset(x, y), batch_size=self.context.get_per_slot_batch_size())
+
+    def train_batch(self, batch, epoch_idx, batch_idx):
+        x, y = batch
+        if x.shape[0] == 16:
+            out = self.model(x)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = self.model(x)
+        loss = nn.functional.cross_entropy(out.float(), y)
+        self.context.backward(loss)
+        self.context.step_optimizer(self.opt)
+        return {"loss": loss}
+
+
+def test_graph_probe_runs_per_key(gpu, monkeypatch):
+    """the library-convolution probe covers every graph key, not only the first one.  The
+    tail-batch key routes to bf16 MIOpen convolutions (functional, under autocast) and stays eager;
+    the full-batch key is captured and replayed; the run matches eager."""
+    res = {}
+    for graph in (False, True):
+        monkeypatch.setenv("DET_HIP_GRAPH", "1" if graph else "0")
+        rec = Recorder().train(1, 30, 0)
+        ctrl, resp = run(TwoKeyTrial, {"opt": "sgd", "global_batch_size": 16}, rec, use_gpu=True, records_per_epoch=150)
+        torch.cuda.synchronize()
+        res[graph] = (torch.cat([p.detach().float().reshape(-1) for p in ctrl.context.models[0].parameters()]).cpu(),
+                      [b["loss"] for b in resp[0]["metrics"]["batch_metrics"]], ctrl)
+    g = res[True][2]._graph
+    assert g is not None and g.disabled_reason is None, g and g.stats()
+    reasons = list(g.probed.values())
+    assert len(reasons) >= 2 and reasons.count(None) >= 1, g.probed
+    bad = [r for r in reasons if r is not None]
+    assert bad and all("MIOpen" in r and "bfloat16" in r for r in bad), bad
+    st = g.stats()
+    assert st["captures"] >= 1 and st["replays"] >= 20, st
+    assert all(l == l for l in res[True][1])
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=2e-3, atol=2e-4)
