@@ -249,6 +249,24 @@ class GradSink:
         for a, _ in self.groups:
             a.zero_grad()
 
+    def host_state(self) -> bool:
+        """The window state a hipGraph replay must leave behind (pytorch/_graph.py): True = fresh
+        (gradients None, the next backward steals them), False = continuing (``.grad`` pinned to the
+        arena views, the next backward accumulates in place)."""
+        return self.fresh
+
+    def set_host_state(self, fresh: bool) -> None:
+        """After a replay (which runs no Python): put the host side where the captured step left it."""
+        if fresh:
+            self.start_window()
+            return
+        self.fresh = False
+        for a, idx in self.groups:
+            for i in idx:
+                a.params[i].grad = a.grad_views[i]
+        self._keep = []
+        self._landing_taken = set()
+
     def start_window(self) -> None:
         """Called by zero_grad: grads become None and the next backward steals them."""
         self.fresh = True

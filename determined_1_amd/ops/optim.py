@@ -117,6 +117,7 @@ class FusedOptimizer:
         self.grad_scale_dev = None  # type: Optional[torch.Tensor]
         self.found_inf = None  # type: Optional[torch.Tensor]
         self.sink = None  # type: Optional[Any]  # ops.arena.GradSink, attached by the trial context
+        self.steps_called = 0
         self._orig_step = optimizer.step
         self._orig_zero_grad = optimizer.zero_grad
         self._orig_load_state_dict = optimizer.load_state_dict
@@ -309,6 +310,7 @@ class FusedOptimizer:
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self.steps_called += 1  # host count of step() calls (a hipGraph capture notes whether it stepped)
         for gi, gs in enumerate(self.groups):
             if not gs.initialized:
                 self._bind_state(gi)

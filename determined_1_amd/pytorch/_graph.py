@@ -23,9 +23,20 @@ capture.  What is NOT in the graph and is handled on the host:
 Requirements on user code (documented in the README): ``train_batch`` must not branch on host
 values other than the epoch index and must not synchronise (``.item()``) -- the same contract as
 CUDA graphs.  A ``train_batch`` that reads ``batch_idx`` at all runs eagerly (checked from its
-bytecode by ``reads_argument``, logged once).  Eligibility is checked once: one process (no data-parallel bucketer), aggregation
-frequency 1, no dynamic loss scaler, every optimizer fused with step-invariant kernel arguments.
-Anything else runs eagerly, logged once.
+bytecode by ``reads_argument``, logged once).  Eligibility is checked once: no dynamic loss scaler, every optimizer fused with step-invariant
+kernel arguments.  Anything else runs eagerly, logged once.
+
+Data-parallel and aggregation steps are captured too (round 6).  The gradient bucketer's RCCL
+collectives (all-reduce, or the fp32_accum all-to-all + det_sum_rows + all-gather on its side
+stream) are issued from the capturing stream's backward hooks, so they are recorded into the step's
+graph in bucket order and replay overlapped with the backward exactly as they ran eagerly; every
+rank replays the same collective sequence whether a given rank replays or runs eagerly (a capture
+executes nothing).  With ``aggregation_frequency`` N each position in the window (N - 1 local
+backwards, then the communicating one) is its own graph key; a replay runs no Python, so the host
+state a step leaves behind -- the GradSink window (fresh / accumulating) and the fused optimizer's
+step counters, only for graphs that stepped -- is restored from what the capture recorded, which
+lets replayed and eager positions mix inside one window.  The bucket-cap autotuner measures eager
+windows: steps stay eager until it has decided.
 
 Multi-batch graphs (``optimizations.hip_graph_batches: K``): even one replay per batch leaves the
 CIFAR trial host-bound (data fetch, input copy, replay launch, metric clones: ~0.8 ms/batch against
@@ -163,12 +174,16 @@ def _leaf_sig(x: Any) -> Any:
 
 class _Graph:
     def __init__(self, graph: "torch.cuda.CUDAGraph", static_in: List[torch.Tensor], in_spec: Any,
-                 out: Any) -> None:
+                 out: Any, stepped: Optional[List[int]] = None, sinks_after: Optional[List[bool]] = None) -> None:
         self.graph = graph
         self.static_in = static_in
         self.in_spec = in_spec
         self.out = out
         self.replays = 0
+        # per fused optimizer: step() calls the capture recorded (0 for a non-communicating position
+        # of an aggregation window), and per GradSink: the window state the captured step left
+        self.stepped = stepped
+        self.sinks_after = sinks_after
 
 
 class TrainStepGraph:
@@ -209,10 +224,6 @@ class TrainStepGraph:
     def ineligible_reason(context: Any) -> Optional[str]:
         if context.device.type != "cuda":
             return "not on a GPU"
-        if context.dist_config.use:
-            return "data-parallel trial (gradient bucketer runs on its own stream)"
-        if context.dist_config.aggregation_frequency != 1:
-            return "aggregation_frequency > 1"
         if context._amp is not None and context._amp.scaler is not None:
             return "dynamic loss scaling syncs on overflow"
         if context._timers.enabled:
@@ -226,13 +237,44 @@ class TrainStepGraph:
                 return f"fused {st.fused.kind} changes kernel arguments every step"
         return None
 
-    def _key(self, leaves: List[Any], epoch_idx: int) -> Any:
+    def _agg(self) -> int:
+        return max(1, int(getattr(self.context.dist_config, "aggregation_frequency", 1) or 1))
+
+    def _key(self, leaves: List[Any], epoch_idx: int, batch_idx: int = 0) -> Any:
+        # the position in an aggregation window decides which kernels run (local accumulation or
+        # the communicating backward + optimizer step): one graph per position
+        pos = batch_idx % self._agg() if self._agg() > 1 else None
         return (tuple(_leaf_sig(x) for x in leaves), epoch_idx if self.epoch_sensitive else None,
-                tuple(f.graph_signature() for f in self.fused))
+                tuple(f.graph_signature() for f in self.fused), pos)
+
+    def _max_graphs(self) -> int:
+        return MAX_GRAPHS * self._agg()
+
+    def _tuning(self) -> bool:
+        """A bucket-cap autotuner still measuring eager windows."""
+        for st in getattr(self.context, "_opt_states", []):
+            tuner = getattr(getattr(st, "bucketer", None), "_tuner", None)
+            if tuner is not None and not tuner.done:
+                return True
+        return False
+
+    def _sinks(self) -> List[Any]:
+        return [f.sink for f in self.fused if f.sink is not None]
 
     def _eager(self, batch: Any, epoch_idx: int, batch_idx: int) -> Any:
+        self.context._current_batch_idx = batch_idx  # chunk batches: the window position of each
         with self.context._autocast():
             return self.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
+
+    def _after_replay(self, g: "_Graph", batches: int = 1) -> None:
+        """Host bookkeeping of a replay: optimizer step counters (for the graphs that stepped) and
+        the GradSink window state the captured step(s) left."""
+        for i, f in enumerate(self.fused):
+            for _ in range(g.stepped[i] if g.stepped is not None else batches):
+                f.graph_replayed()
+        if g.sinks_after is not None:
+            for sink, fresh in zip(self._sinks(), g.sinks_after):
+                sink.set_host_state(fresh)
 
     # ------------------------------------------------------------------------------------------
     def run(self, batch: Any, epoch_idx: int, batch_idx: int) -> Any:
@@ -242,7 +284,9 @@ class TrainStepGraph:
         if any(isinstance(x, torch.Tensor) and x.device.type != "cuda" for x in leaves):
             self._disable("train batch has host tensors")
             return self._eager(batch, epoch_idx, batch_idx)
-        key = self._key(leaves, epoch_idx)
+        if self._tuning():
+            return self._eager(batch, epoch_idx, batch_idx)
+        key = self._key(leaves, epoch_idx, batch_idx)
         g = self.graphs.get(key)
         if g is not None:
             return self._replay(g, leaves)
@@ -263,8 +307,9 @@ class TrainStepGraph:
             return self._eager(batch, epoch_idx, batch_idx)
         # the capture recorded but did not execute this batch's work: run it now (host state
         # was advanced during the capture itself)
-        for f in self.fused:
-            f.graph_prepare(advanced=True)
+        for i, f in enumerate(self.fused):
+            if g.stepped is None or g.stepped[i]:
+                f.graph_prepare(advanced=True)
         g.graph.replay()
         self.replays += 1
         g.replays += 1
@@ -273,11 +318,11 @@ class TrainStepGraph:
     def _replay(self, g: _Graph, leaves: List[Any]) -> Any:
         for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
             dst.copy_(src, non_blocking=True)
-        for f in self.fused:
-            f.graph_prepare()
+        for i, f in enumerate(self.fused):
+            if g.stepped is None or g.stepped[i]:
+                f.graph_prepare()
         g.graph.replay()
-        for f in self.fused:
-            f.graph_replayed()
+        self._after_replay(g)
         self.replays += 1
         g.replays += 1
         return self._clone_out(g.out)
@@ -291,15 +336,16 @@ class TrainStepGraph:
         if self.captures - len(self.graphs) >= THRASH_LIMIT and len(stale) == len(self.graphs):
             self._disable("graph key changes every few batches (per-batch hyper-parameter schedule?)")
             return None
-        if len(self.graphs) >= MAX_GRAPHS:
+        if len(self.graphs) >= self._max_graphs():
             torch.cuda.synchronize()  # never destroy a graph exec that may still be running
-            while len(self.graphs) >= MAX_GRAPHS:
+            while len(self.graphs) >= self._max_graphs():
                 del self.graphs[next(iter(self.graphs))]
         static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
         it = iter(static_in)
         static_leaves = [next(it) if isinstance(x, torch.Tensor) else x for x in leaves]
         static_batch = pytree.tree_unflatten(static_leaves, spec)
         host = [f.host_state() for f in self.fused]
+        calls0 = [f.steps_called for f in self.fused]
         graph = torch.cuda.CUDAGraph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
@@ -321,7 +367,8 @@ class TrainStepGraph:
             torch.cuda.synchronize()
             return None
         self.captures += 1
-        g = _Graph(graph, static_in, spec, out)
+        g = _Graph(graph, static_in, spec, out, stepped=[f.steps_called - c for f, c in zip(self.fused, calls0)],
+                   sinks_after=[sk.host_state() for sk in self._sinks()])
         self.graphs[key] = g
         return g
 
@@ -342,10 +389,10 @@ class TrainStepGraph:
         self.last_chunk_metrics = None
         if self.chunk_disabled is None and not all(f.chunk_capturable() for f in self.fused):
             self.chunk_disabled = "the optimizer's per-step hyper-parameters hold one step (replaying per batch)"
-        if capture and self.disabled_reason is None and self.chunk_disabled is None:
+        if capture and self.disabled_reason is None and self.chunk_disabled is None and not self._tuning():
             leaves, spec = pytree.tree_flatten(chunk.stacked)
             if all(not isinstance(x, torch.Tensor) or x.device.type == "cuda" for x in leaves):
-                key = ("chunk", chunk.sizes, self._key(leaves, epoch_idx))
+                key = ("chunk", chunk.sizes, self._key(leaves, epoch_idx, batch_idx))
                 g = self.chunk_graphs.get(key)
                 if g is None and not self._batch_key_clean(chunk, epoch_idx):
                     key = None  # warm up / probe per batch first; a replay-unsafe key stays per batch
@@ -353,9 +400,7 @@ class TrainStepGraph:
                     for dst, src in zip(g.static_in, (x for x in leaves if isinstance(x, torch.Tensor))):
                         dst.copy_(src, non_blocking=True)
                     g.graph.replay()
-                    for f in self.fused:
-                        for _ in chunk.sizes:
-                            f.graph_replayed()
+                    self._after_replay(g, len(chunk.sizes))
                     self.replays += 1
                     self.chunk_replays += 1
                     g.replays += 1
@@ -383,7 +428,7 @@ class TrainStepGraph:
     def _batch_key_clean(self, chunk: Any, epoch_idx: int) -> bool:
         """Whether the per-batch graph key of the chunk's first batch probed clean."""
         bl, _ = pytree.tree_flatten(chunk.batches[0])
-        k = self._key(bl, epoch_idx)
+        k = self._key(bl, epoch_idx, self.context._current_batch_idx or 0)
         return k in self.probed and self.probed[k] is None
 
     def _capture_chunk(self, key: Any, leaves: List[Any], spec: Any, sizes: Tuple[int, ...], epoch_idx: int,
@@ -399,6 +444,7 @@ class TrainStepGraph:
         views = BatchChunk(pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x for x in leaves],
                                                  spec), sizes).batches
         host = [f.host_state() for f in self.fused]
+        calls0 = [f.steps_called for f in self.fused]
         graph = torch.cuda.CUDAGraph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
@@ -425,7 +471,8 @@ class TrainStepGraph:
             torch.cuda.synchronize()
             return None
         self.captures += 1
-        g = _Graph(graph, static_in, spec, out)
+        g = _Graph(graph, static_in, spec, out, stepped=[f.steps_called - c for f, c in zip(self.fused, calls0)],
+                   sinks_after=[sk.host_state() for sk in self._sinks()])
         self.chunk_graphs[key] = g
         return g
 

@@ -53,7 +53,66 @@ def _hip():
     return ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
 
 
-def graph_nodes(graph_handle: int):
+class _Dim3(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_uint), ("y", ctypes.c_uint), ("z", ctypes.c_uint)]
+
+
+class _KParams(ctypes.Structure):  # hipKernelNodeParams
+    _fields_ = [("blockDim", _Dim3), ("extra", ctypes.POINTER(ctypes.c_void_p)), ("func", ctypes.c_void_p),
+                ("gridDim", _Dim3), ("kernelParams", ctypes.POINTER(ctypes.c_void_p)), ("sharedMemBytes", ctypes.c_uint)]
+
+
+def _segments():
+    """torch allocator segments: (start, end, pool id) -- the graph's private pool vs the default one."""
+    out = []
+    for seg in torch.cuda.memory_snapshot():
+        out.append((seg["address"], seg["address"] + seg["total_size"], tuple(seg.get("segment_pool_id", (0, 0)))))
+    return out
+
+
+def _classify(v: int, segs, user_ptrs):
+    for name, (lo, hi) in user_ptrs.items():
+        if lo <= v < hi:
+            return name
+    for lo, hi, pool in segs:
+        if lo <= v < hi:
+            return "graph_pool" if pool != (0, 0) else "default_pool"
+    return "foreign"
+
+
+def kernel_args(hip, node, segs, user_ptrs):
+    """Name of a kernel node and every 8-byte kernel argument word that looks like a device pointer,
+    classified by the memory it points into."""
+    kp = _KParams()
+    if hip.hipGraphKernelNodeGetParams(ctypes.c_void_p(node), ctypes.byref(kp)) != 0:
+        return {"error": "params"}
+    name = None
+    try:
+        hip.hipKernelNameRef.restype = ctypes.c_char_p
+        raw = hip.hipKernelNameRef(ctypes.c_void_p(kp.func))
+        name = raw.decode()[:90] if raw else None
+    except Exception:  # noqa: BLE001
+        pass
+    words = []
+    if kp.extra:
+        # HIP_LAUNCH_PARAM_BUFFER_POINTER (1), ptr, HIP_LAUNCH_PARAM_BUFFER_SIZE (2), &size, END (3)
+        buf, size, i = None, 0, 0
+        while i < 8 and kp.extra[i] not in (None, 3):
+            tag = kp.extra[i]
+            if tag == 1:
+                buf = kp.extra[i + 1]
+            elif tag == 2:
+                size = ctypes.cast(kp.extra[i + 1], ctypes.POINTER(ctypes.c_size_t))[0]
+            i += 2
+        if buf and size:
+            arr = (ctypes.c_uint64 * (size // 8)).from_address(buf)
+            words = list(arr)
+    ptrs = [{"off": 8 * k, "kind": _classify(w, segs, user_ptrs)} for k, w in enumerate(words) if w > (1 << 32)]
+    return {"name": name, "grid": [kp.gridDim.x, kp.gridDim.y, kp.gridDim.z], "kernarg_words": len(words),
+            "pointers": ptrs, "via": "extra" if kp.extra else ("kernelParams" if kp.kernelParams else None)}
+
+
+def graph_nodes(graph_handle: int, user_ptrs=None):
     hip = _hip()
     n = ctypes.c_size_t(0)
     assert hip.hipGraphGetNodes(ctypes.c_void_p(graph_handle), None, ctypes.byref(n)) == 0
@@ -64,6 +123,8 @@ def graph_nodes(graph_handle: int):
         t = ctypes.c_int(-1)
         hip.hipGraphNodeGetType(ctypes.c_void_p(node), ctypes.byref(t))
         rec = {"type": NODE_TYPES.get(t.value, t.value)}
+        if t.value == 0 and user_ptrs is not None:
+            rec.update(kernel_args(hip, node, _segments(), user_ptrs))
         if t.value == 1:
             p = _Memcpy3D()
             if hip.hipGraphMemcpyNodeGetParams(ctypes.c_void_p(node), ctypes.byref(p)) == 0:
@@ -80,6 +141,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--args", default="", help="comma-separated ops whose kernel arguments are classified")
     args = ap.parse_args()
     dev = torch.device("cuda")
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.dtype]
@@ -93,13 +155,22 @@ def main() -> None:
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g):
-            fn(x, dy)
-        nodes = graph_nodes(g.raw_cuda_graph())
+            out = fn(x, dy)
+        user = None
+        if name in args.args.split(","):
+            user = {"x": (x.data_ptr(), x.data_ptr() + x.numel() * x.element_size()),
+                    "dy": (dy.data_ptr(), dy.data_ptr() + dy.numel() * dy.element_size()),
+                    "out": (out.data_ptr(), out.data_ptr() + out.numel() * out.element_size())}
+            for d in (fn.__defaults__ or ()):
+                if isinstance(d, torch.Tensor):
+                    user["w"] = (d.data_ptr(), d.data_ptr() + d.numel() * d.element_size())
+        nodes = graph_nodes(g.raw_cuda_graph(), user)
         counts = {}
         for r in nodes:
             counts[r["type"]] = counts.get(r["type"], 0) + 1
         print(json.dumps({"op": name, "dtype": args.dtype, "nodes": counts,
-                          "memcpy": [r for r in nodes if r["type"] == "memcpy"]}), flush=True)
+                          "memcpy": [r for r in nodes if r["type"] == "memcpy"],
+                          "kernels": [r for r in nodes if r["type"] == "kernel" and "pointers" in r]}), flush=True)
         del g
 
 

@@ -50,9 +50,15 @@ class MLPTrial(pytorch.PyTorchTrial):
         return self.build_training_data_loader()
 
 
+def ctrl_responses(rec: Recorder):
+    return [r["metrics"]["batch_metrics"] for r in rec.responses if isinstance(r, dict) and "batch_metrics" in
+            r.get("metrics", {})]
+
+
 def main() -> None:
     out, amp, agg, compress, reduction = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4] == "1", sys.argv[5]
-    rec = Recorder().train(1, 4, 0).train(2, 4, 4)
+    half = int(os.environ.get("GDP_HALF_STEPS", "4"))  # batches per training workload (2 workloads)
+    rec = Recorder().train(1, half, 0).train(2, half, half)
     gpu = torch.cuda.is_available()
     ctrl, _ = run(MLPTrial, {"global_batch_size": 16, "amp": amp}, rec, trial_seed=5, use_gpu=gpu,
                   optimizations={"aggregation_frequency": agg, "gradient_compression": compress,
@@ -65,7 +71,9 @@ def main() -> None:
 
     info = {"params": params, "dist": dist.is_initialized(),
             "backend": dist.get_backend() if dist.is_initialized() else None,
-            "buckets": [st.bucketer.describe() for st in ctx._opt_states if st.bucketer is not None]}
+            "buckets": [st.bucketer.describe() for st in ctx._opt_states if st.bucketer is not None],
+            "graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
+            "losses": [b["loss"] for r in ctrl_responses(rec) for b in r]}
     torch.save(info, out + ".pt")
     from determined_1_amd.parallel import dist as pdist
 
