@@ -25,23 +25,36 @@ from determined_1_amd.env import EnvContext, RendezvousInfo
 from determined_1_amd.parallel.dist import DistributedConfig, RankInfo
 
 
-def notebook_to_py(ipynb: pathlib.Path) -> pathlib.Path:
-    """Convert a Jupyter notebook's code cells into ``<name>.py`` next to it (reference
-    ``load/_load_implementation.py:147``); magics and shell escapes are commented out."""
-    import json
-
-    nb = json.loads(ipynb.read_text())
-    lines = []
-    for cell in nb.get("cells", []):
+def notebook_source(notebook_path: str) -> str:
+    """The code cells of a Jupyter notebook as one Python script (reference
+    ``load/_load_implementation.py:147``): IPython magics (``%...``) are commented out and shell
+    escapes (``!...``) dropped, so the script runs under plain Python.  The one converter behind
+    both the entrypoint loader (``notebook_to_py``) and the Native-API loader
+    (``convert_notebook_to_python_script``)."""
+    if not notebook_path.endswith(".ipynb"):
+        raise errors.InvalidExperimentException(f"{notebook_path} is not a .ipynb notebook")
+    nb = json.loads(pathlib.Path(notebook_path).read_text())
+    if "cells" not in nb:
+        raise errors.InvalidExperimentException(f"{notebook_path}: not a notebook (no cells)")
+    out = []  # type: List[str]
+    for cell in nb["cells"]:
         if cell.get("cell_type") != "code":
             continue
         src = cell.get("source", [])
         text = "".join(src) if isinstance(src, list) else str(src)
         for ln in text.splitlines():
-            lines.append(("# " + ln) if ln.lstrip().startswith(("%", "!")) else ln)
-        lines.append("")
+            st = ln.lstrip()
+            if st.startswith("!"):
+                continue
+            out.append(("# " + ln) if st.startswith("%") else ln)
+        out.append("")
+    return "\n".join(out)
+
+
+def notebook_to_py(ipynb: pathlib.Path) -> pathlib.Path:
+    """An entrypoint module shipped as ``<name>.ipynb``: write ``<name>.py`` next to it."""
     out = ipynb.with_suffix(".py")
-    out.write_text("\n".join(lines))
+    out.write_text(notebook_source(str(ipynb)))
     return out
 
 
@@ -133,27 +146,11 @@ class RunpyGlobals:
 
 
 def convert_notebook_to_python_script(notebook_path: str) -> str:
-    """``x.ipynb`` -> ``x__det__.py`` with the code cells (shell escapes dropped, magics commented),
-    next to the notebook so relative imports and data paths keep working."""
-    if not notebook_path.endswith(".ipynb"):
-        raise errors.InvalidExperimentException(f"{notebook_path} is not a .ipynb notebook")
-    nb = json.loads(pathlib.Path(notebook_path).read_text())
-    if "cells" not in nb:
-        raise errors.InvalidExperimentException(f"{notebook_path}: not a notebook (no cells)")
-    out = []  # type: List[str]
-    for cell in nb["cells"]:
-        if cell.get("cell_type") != "code":
-            continue
-        src = cell.get("source", [])
-        text = "".join(src) if isinstance(src, list) else str(src)
-        for ln in text.splitlines():
-            st = ln.lstrip()
-            if st.startswith("!"):
-                continue
-            out.append(("# " + ln) if st.startswith("%") else ln)
-        out.append("")
+    """``x.ipynb`` -> ``x__det__.py`` (a Native-API notebook command), next to the notebook so
+    relative imports and data paths keep working."""
+    src = notebook_source(notebook_path)
     dst = notebook_path[: -len(".ipynb")] + "__det__.py"
-    pathlib.Path(dst).write_text("\n".join(out))
+    pathlib.Path(dst).write_text(src)
     return dst
 
 

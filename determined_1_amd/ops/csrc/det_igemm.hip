@@ -575,8 +575,8 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm2_kernel(IgArgs a) {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int swz64(int row, int ch) { return row * 64 + ((ch ^ ((-(row >> 2)) & 3)) << 4); }
 
-template <int BM, int BN, int WM, int WN, int NS, bool STATS, bool BNB = false>
-__global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
+template <int BM, int BN, int WM, int WN, int NS, bool STATS, bool BNB = false, int OCC = 1>
+__global__ void __launch_bounds__(WM * WN * 64, OCC) igemm3_kernel(IgArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   constexpr int BK = 32;
   constexpr int NW = WM * WN, kThreads = NW * 64;
@@ -768,7 +768,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) igemm3_kernel(IgArgs a) {
 #endif
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+// OCC: workgroups per CU the LDS footprint and register budget are sized for.  At OCC 2 one
+// workgroup's epilogue (C tile through LDS, 16-B stores, BN statistics) overlaps the other's K loop;
+// with one workgroup per CU the short-K GEMMs (1x1 expansions, K = 64..512) serialise load ->
+// compute -> store per tile.
+template <int BM, int BN, int WM, int WN, int NS, int OCC = 1>
 int launch3(hipStream_t st, const IgArgs& a_in, bool stats, bool bnb = false) {
   IgArgs a = a_in;
   a.stats_first = stats_first_flag();
@@ -778,15 +782,17 @@ int launch3(hipStream_t st, const IgArgs& a_in, bool stats, bool bnb = false) {
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
   constexpr int ring = NS * (BM + BN) * 64, ctile = BM * (BN + 16) * 2 + 12 * WM * BN;
   constexpr int smem = ring > ctile ? ring : ctile;
-  static_assert(smem <= 163840, "LDS");
+  static_assert(smem * OCC <= 163840, "LDS");
   static_assert(BM * (BN + 16) * 2 >= kThreads * 16 * 4, "BN-backward scratch fits in the C tile");
   if (bnb)
-    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false, true>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem,
-                       st, a);
+    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false, true, OCC>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads),
+                       smem, st, a);
   else if (stats)
-    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, true>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, true, false, OCC>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads),
+                       smem, st, a);
   else
-    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads), smem, st, a);
+    hipLaunchKernelGGL((igemm3_kernel<BM, BN, WM, WN, NS, false, false, OCC>), dim3(static_cast<unsigned>(nwg)), dim3(kThreads),
+                       smem, st, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -855,6 +861,12 @@ static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool st
     case 13: return launch3<512, 128, 4, 2, 4>(st, a, stats, bnb);
     case 14: return launch3<512, 64, 8, 1, 4>(st, a, stats, bnb);   // 64x64 wave tiles at N = 64, 8 waves
     case 15: return launch3<512, 64, 4, 1, 4>(st, a, stats, bnb);   // 128x64 wave tiles at N = 64, 4 waves
+    // two workgroups per CU (one's epilogue under the other's K loop)
+    case 16: return launch3<256, 128, 4, 2, 3, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 3 stages
+    case 17: return launch3<256, 64, 4, 1, 4, 2>(st, a, stats, bnb);   // cfg 11 at 2 per CU
+    case 18: return launch3<256, 64, 4, 1, 3, 2>(st, a, stats, bnb);
+    case 19: return launch3<128, 128, 2, 2, 4, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 4 waves
+    case 20: return launch3<128, 256, 2, 4, 3, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 8 waves
     default: return -7;
   }
 }
@@ -2281,7 +2293,7 @@ int det_igemm_rows_per_block_cfg(int N, int cfg) {
   IgArgs a{};
   a.N = N;
   const int c = cfg > 0 ? cfg : auto_cfg(a);
-  return (c == 4 || c == 6 || c == 7) ? 128 : (c >= 12 ? 512 : 256);
+  return (c == 4 || c == 6 || c == 7 || c == 19 || c == 20) ? 128 : ((c >= 12 && c <= 15) ? 512 : 256);
 }
 int det_igemm_rows_per_block() { return 256; }
 

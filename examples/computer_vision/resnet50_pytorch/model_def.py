@@ -3,9 +3,11 @@
 class.
 
 Per batch: uint8 NHWC images (pinned, DMA'd ahead by the DevicePrefetcher) -> ``u8_normalize``
-HIP kernel -> bf16 channels_last tensor -> ResNet-50 forward/backward (fused BN / native 1x1-conv
-HIP kernels + MIOpen for the rest) -> fused arena SGD-momentum HIP kernel, with gradient buckets
-reduced over RCCL during backward when ``slots_per_trial > 1``.
+HIP kernel -> bf16 channels_last tensor -> ResNet-50 forward/backward entirely on the hand-written
+HIP kernels (stem patch conv, 1x1 GEMMs and 3x3 implicit GEMMs with the BatchNorm statistics /
+apply / backward partials fused into their prologues and epilogues, max/avg pool, head; no MIOpen
+call in the step: profiles/r5_resnet50_steady_final.txt) -> fused arena SGD-momentum HIP kernel,
+with gradient buckets reduced over RCCL during backward when ``slots_per_trial > 1``.
 
 Hyperparameters: ``global_batch_size``, ``lr``, ``momentum``, ``weight_decay``, ``arch``,
 ``amp`` (O0/O1/O2), ``channels_last``, ``num_classes``, ``image_size``, ``fused_bn``,

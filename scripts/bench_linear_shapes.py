@@ -36,6 +36,8 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--igemm", default="", help="comma-separated det_igemm tile cfgs to time as plain GEMMs")
+    ap.add_argument("--wgcfg", default="", help="comma-separated det_igemm_wgrad cfgs (1x1 geometry)")
     args = ap.parse_args()
     tuned = gemm_tuning.enable()
     dev = torch.device("cuda")
@@ -59,8 +61,32 @@ def main():
             "wgrad/blas": lambda: torch.mm(dz.t(), x, out=wg),
             "wgrad/native": lambda: conv1x1_wgrad(dz, x, wg),
         }
+        zero = torch.zeros(64, device=dev, dtype=bf)
+        wt = w.t().contiguous()  # [K, N]: the input gradient's B operand as the NT kernel reads it
+        dx = torch.empty(T, K, device=dev, dtype=bf)
+
+        def ig(cfg, X, W, Y, M, Nn, Kk):
+            # X [M, Kk] as a 1 x M image of Kk channels, W [Nn, Kk]: Y = X W^T
+            return lambda: _lib.check(lib.det_igemm_conv_cfg(st, X.data_ptr(), W.data_ptr(), Y.data_ptr(), zero.data_ptr(),
+                                                             M, Nn, Kk, 1, M, 1, M, 1, 1, 1, 0, None, None, cfg), "ig")
+
+        for c in [int(v) for v in args.igemm.split(",") if v]:
+            cases[f"fwd/igemm{c}"] = ig(c, x, w, y, T, N, K)
+            cases[f"dgrad/igemm{c}"] = ig(c, dz, wt, dx, T, K, N)
+        for c in [int(v) for v in args.wgcfg.split(",") if v]:
+            n_ws = int(lib.det_igemm_wgrad_ws_elems(T, N, K, c))
+            if n_ws <= 0:
+                continue
+            ws = torch.empty(n_ws, device=dev, dtype=torch.float32)
+            cases[f"wgrad/wg{c}"] = (lambda ws=ws, c=c: _lib.check(lib.det_igemm_wgrad(
+                st, dz.data_ptr(), x.data_ptr(), wg.data_ptr(), 1, T, N, K, 1, T, 1, T, 1, 1, 1, 0, ws.data_ptr(),
+                1.0, c), "wg"))
         for cname, fn in cases.items():
-            us = timed(fn, args.iters)
+            try:
+                us = timed(fn, args.iters)
+            except RuntimeError as e:  # a tile that does not fit the shape
+                res["passes"][f"{name}/{cname}"] = {"error": str(e)[:80]}
+                continue
             res["passes"][f"{name}/{cname}"] = {"us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}
     print(json.dumps(res))
 

@@ -87,26 +87,15 @@ def kernel_args(hip, node, segs, user_ptrs):
     if hip.hipGraphKernelNodeGetParams(ctypes.c_void_p(node), ctypes.byref(kp)) != 0:
         return {"error": "params"}
     name = None
-    try:
-        hip.hipKernelNameRef.restype = ctypes.c_char_p
-        raw = hip.hipKernelNameRef(ctypes.c_void_p(kp.func))
-        name = raw.decode()[:90] if raw else None
-    except Exception:  # noqa: BLE001
-        pass
     words = []
-    if kp.extra:
-        # HIP_LAUNCH_PARAM_BUFFER_POINTER (1), ptr, HIP_LAUNCH_PARAM_BUFFER_SIZE (2), &size, END (3)
-        buf, size, i = None, 0, 0
-        while i < 8 and kp.extra[i] not in (None, 3):
-            tag = kp.extra[i]
-            if tag == 1:
-                buf = kp.extra[i + 1]
-            elif tag == 2:
-                size = ctypes.cast(kp.extra[i + 1], ctypes.POINTER(ctypes.c_size_t))[0]
-            i += 2
-        if buf and size:
-            arr = (ctypes.c_uint64 * (size // 8)).from_address(buf)
-            words = list(arr)
+    ex = kp.extra
+    # HIP_LAUNCH_PARAM_BUFFER_POINTER (1), ptr, HIP_LAUNCH_PARAM_BUFFER_SIZE (2), &size, END (3): read only
+    # that exact layout (anything else is left alone)
+    if ex and ex[0] == 1 and ex[2] == 2 and ex[4] in (None, 3, 0):
+        buf = ex[1]
+        size = ctypes.cast(ex[3], ctypes.POINTER(ctypes.c_size_t))[0] if ex[3] else 0
+        if buf and 0 < size <= 4096:
+            words = list((ctypes.c_uint64 * (size // 8)).from_address(buf))
     ptrs = [{"off": 8 * k, "kind": _classify(w, segs, user_ptrs)} for k, w in enumerate(words) if w > (1 << 32)]
     return {"name": name, "grid": [kp.gridDim.x, kp.gridDim.y, kp.gridDim.z], "kernarg_words": len(words),
             "pointers": ptrs, "via": "extra" if kp.extra else ("kernelParams" if kp.kernelParams else None)}

@@ -73,7 +73,9 @@ def main() -> None:
             "backend": dist.get_backend() if dist.is_initialized() else None,
             "buckets": [st.bucketer.describe() for st in ctx._opt_states if st.bucketer is not None],
             "graph": ctrl._graph.stats() if getattr(ctrl, "_graph", None) is not None else None,
-            "losses": [b["loss"] for r in ctrl_responses(rec) for b in r]}
+            "losses": [float(b["loss"]) for r in ctrl_responses(rec) for b in r]}
+    if info["graph"] is not None:
+        info["graph"] = {k: (v if isinstance(v, (int, type(None))) else str(v)) for k, v in info["graph"].items()}
     torch.save(info, out + ".pt")
     from determined_1_amd.parallel import dist as pdist
 
