@@ -871,12 +871,22 @@ static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool st
   }
 }
 
+// block-tile N (output channels) of a tile configuration
+static int cfg_bn(int c) {
+  switch (c) {
+    case 3: case 5: case 6: case 11: case 14: case 15: case 17: case 18: return 64;
+    case 8: case 10: case 20: return 256;
+    default: return 128;
+  }
+}
+
 static int auto_cfg(const IgArgs& a) {
   static const int forced = [] {
     const char* e = std::getenv("DET_IGEMM_CFG");
     return e ? std::atoi(e) : 0;
   }();
-  if (forced > 0) return forced;
+  // a forced configuration (sweeps) applies where its tile fits; other shapes keep the heuristic
+  if (forced > 0 && a.N % cfg_bn(forced) == 0 && (forced < 8 ? a.Cin % 64 == 0 : a.Cin % 32 == 0)) return forced;
   // measured per ResNet-50 shape (profiles/r3_igemm_cfgs.jsonl): 256 x 256 / BK 32 wherever N
   // allows, 256 x 128 / BK 64 at N = 128, 256 x 64 / BK 32 (4 waves) at N = 64
   if (a.N % 256 == 0 && a.Cin % 32 == 0) return 8;

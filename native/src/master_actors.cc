@@ -563,6 +563,9 @@ void TrialActor::Advance(Context& ctx) {
 void TrialActor::RequestResources(Context& ctx) {
   ++alloc_gen_;
   task_id_ = TaskID();
+  // scheduling events (scripts/bench_asha.py splits idle slot time into "no runnable trial" and
+  // "a trial waits for resources or its container": the control plane's share)
+  Log("[sched] event=requested request=" + rid_ + " trial=" + std::to_string(trial_id_) + " task=" + task_id_);
   AllocateRequest req;
   req.task_id = task_id_;
   req.group = std::to_string(exp_id_);
@@ -575,6 +578,7 @@ void TrialActor::RequestResources(Context& ctx) {
 
 void TrialActor::OnAllocated(Context& ctx, const ResourcesAllocated& ra) {
   if (ra.task_id != task_id_ || !containers_.empty()) return;
+  Log("[sched] event=allocated request=" + rid_ + " trial=" + std::to_string(trial_id_) + " task=" + task_id_);
   if (exp_state_ != "ACTIVE" || seq_->UpToDate() || canceled_) {
     m_->Pool(pool_)->Tell(ResourcesReleased{task_id_});
     task_id_.clear();

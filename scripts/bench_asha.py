@@ -102,6 +102,77 @@ def idle_breakdown(cl, trials, slots, t_start, t_end):
             "idle_trial_without_container_frac": round(parked / tot, 3)}
 
 
+def control_plane_breakdown(cl, trials, slots, t_start, t_end):
+    """Idle slot time by cause, from the master's [sched] events (resources requested / allocated per
+    trial task) and each trial container's log records:
+
+      * ``work``: container time from the harness's "controller ready" mark to its last record;
+      * ``container_init``: container time before "controller ready" (process start, imports, storage
+        probe, rendezvous, trial construction) -- control plane;
+      * ``waiting``: slots free while a task that asked for resources has no container yet (the
+        scheduler, the agent's container launch) -- control plane;
+      * ``no_runnable_trial``: the rest -- no trial had work for the slot (ASHA waits on rung results
+        before promoting or creating; inherent to the search).
+    Fractions are of slots x wall."""
+    import re
+    from collections import defaultdict
+
+    pat = re.compile(r"\[sched\] event=(\w+) request=(\S+) trial=(\d+) task=(\S+)")
+    req, alloc = {}, {}
+    rid_of_task = {}
+    for rec in cl.get("/logs", limit=25000):
+        m = pat.search(rec.get("message", ""))
+        if not m:
+            continue
+        ev, rid, _, task = m.groups()
+        ts = _ts(rec.get("time"))
+        rid_of_task[task] = rid
+        (req if ev == "requested" else alloc).setdefault(task, ts)
+    by_rid = {t.get("request_id"): t for t in trials}
+    cont_spans = defaultdict(list)  # trial id -> [(first, ready, last)]
+    for t in trials:
+        spans = defaultdict(list)
+        ready = {}
+        for rec in cl.get(f"/trials/{t['id']}/logs"):
+            ts = _ts(rec.get("timestamp"))
+            if ts is None:
+                continue
+            cid = rec.get("container_id")
+            spans[cid].append(ts)
+            if "controller ready" in rec.get("message", "") and cid not in ready:
+                ready[cid] = ts
+        for cid, v in spans.items():
+            cont_spans[t["id"]].append((min(v), ready.get(cid, min(v)), max(v)))
+    waits = []  # (from request, until the task's container's first record)
+    for task, t0 in req.items():
+        t = by_rid.get(rid_of_task.get(task))
+        if t is None:
+            continue
+        after = sorted(c[0] for c in cont_spans.get(t["id"], []) if c[0] >= t0 - 0.5)
+        waits.append((t0, after[0] if after else t_end))
+    step = 0.02
+    n = int((t_end - t_start) / step) + 1
+    work = init = waiting = 0.0
+    allc = [c for v in cont_spans.values() for c in v]
+    for i in range(n):
+        t = t_start + i * step
+        nw = sum(1 for a, r, b in allc if r <= t < b)
+        ni = sum(1 for a, r, b in allc if a <= t < r)
+        nwait = sum(1 for a, b in waits if a <= t < b)
+        free = max(0, slots - nw - ni)
+        work += min(slots, nw) * step
+        init += min(slots - min(slots, nw), ni) * step
+        waiting += min(free, nwait) * step
+    tot = slots * (t_end - t_start)
+    out = {"work_frac": work / tot, "container_init_frac": init / tot, "waiting_frac": waiting / tot}
+    out["no_runnable_trial_frac"] = max(0.0, 1.0 - sum(out.values()))
+    out["control_plane_idle_frac"] = out["container_init_frac"] + out["waiting_frac"]
+    out = {k: round(v, 4) for k, v in out.items()}
+    out["tasks"] = len(req)
+    out["mean_wait_s"] = round(sum(b - a for a, b in waits) / max(1, len(waits)), 3)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--max-length-batches", type=int, default=0,
@@ -116,6 +187,9 @@ def main() -> None:
     ap.add_argument("--validation-records", type=int, default=0,
                     help="shrink the validation set (scaled-down CPU runs; 0 = CIFAR-10's 10,000)")
     ap.add_argument("--amp", default=None, help="override hyperparameters.amp (O0 = fp32, the reference precision)")
+    ap.add_argument("--modelled-batch-ms", type=float, default=0.0,
+                    help="run scripts/asha_model's trial: each batch waits this long (the MI355X time at batch 32) "
+                         "instead of computing -- the control plane at the real shape on CPU slots")
     ap.add_argument("--graph-batches", type=int, default=0,
                     help="override optimizations.hip_graph_batches (train steps per hipGraph replay)")
     args = ap.parse_args()
@@ -124,6 +198,8 @@ def main() -> None:
     from determined_1_amd.deploy import LocalCluster
 
     ex = REPO / "examples" / "computer_vision" / "cifar10_pytorch"
+    if args.modelled_batch_ms:
+        ex = REPO / "scripts" / "asha_model"
     cfg = yaml.safe_load((ex / "adaptive.yaml").read_text())
     cfg["searcher"]["max_trials"] = args.max_trials
     cfg.setdefault("reproducibility", {})["experiment_seed"] = args.seed
@@ -144,12 +220,15 @@ def main() -> None:
         cfg.pop("records_per_epoch", None)
     env_vars = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
     env_vars.append("DET_TIMELINE=1")
+    if args.modelled_batch_ms:
+        env_vars.append(f"DET_MODEL_BATCH_MS={args.modelled_batch_ms}")
     env_vars.append("PYTHONFAULTHANDLER=1")  # a crashing trial logs its Python stack
     if args.artificial_slots:
         env_vars.append("OMP_NUM_THREADS=1")  # N CPU trial processes share the host's cores
-        # a scheduler dry run: a 10k-record validation pass per rung on one CPU thread per trial
-        # would dominate the wall time it measures
-        cfg["hyperparameters"]["validation_records"] = 512
+        if not args.modelled_batch_ms:
+            # a scheduler dry run: a 10k-record validation pass per rung on one CPU thread per trial
+            # would dominate the wall time it measures (the modelled trial keeps the real 10k)
+            cfg["hyperparameters"]["validation_records"] = 512
     busy = []
     stop = threading.Event()
 
@@ -205,7 +284,18 @@ def main() -> None:
             idle = idle_breakdown(cl, e["trials"], slots, t0, t0 + wall)
         except Exception as ex:  # diagnostics only
             idle = {"error": f"{type(ex).__name__}: {ex}"[:200]}
+        try:
+            cp = control_plane_breakdown(cl, e["trials"], slots, t0, t0 + wall)
+        except Exception as ex:  # diagnostics only
+            cp = {"error": f"{type(ex).__name__}: {ex}"[:200]}
         containers = timeline.pop("_containers", 0)
+        if "work_frac" in cp:
+            # the master's round trip between a container's workloads (sequencer, searcher, socket) is
+            # control plane too: taken out of "work"
+            bw = timeline.get("between workloads", 0.0) * containers / max(1e-9, wall * slots)
+            cp["between_workloads_frac"] = round(bw, 4)
+            cp["work_frac"] = round(cp["work_frac"] - bw, 4)
+            cp["control_plane_idle_frac"] = round(cp["control_plane_idle_frac"] + bw, 4)
         # slot occupancy from the container log spans (idle_breakdown); the per-container timeline
         # totals are kept for the phase split only
         occupancy = (1.0 - idle["idle_frac"]) if "idle_frac" in idle else \
@@ -218,7 +308,8 @@ def main() -> None:
                           "containers": containers, "train_records": records,
                           "gpu_busy_frac": round(sum(busy) / len(busy) / 100.0, 3) if busy else None,
                           "slot_occupancy": round(occupancy, 3), "scheduler_idle_frac": round(1 - occupancy, 3),
-                          "peak_busy_slots": peak_busy, "idle_breakdown": idle,
+                          "peak_busy_slots": peak_busy, "idle_breakdown": idle, "control_plane": cp,
+                          "modelled_batch_ms": args.modelled_batch_ms or None,
                           "zygote": not args.no_zygote, "per_container_s": timeline,
                           "hip_graph": bool((cfg.get("optimizations") or {}).get("hip_graph", False)),
                           "hip_graph_batches": (cfg.get("optimizations") or {}).get("hip_graph_batches", 1),

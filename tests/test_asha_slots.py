@@ -1,7 +1,11 @@
-"""The ASHA benchmark's multi-slot scheduling path on CPU: ``scripts/bench_asha.py`` with 8
-artificial slots runs the 16-trial adaptive_asha CIFAR-10 search (scaled down to 40 batches, fp32)
-through det-master + det-agent, fills all 8 slots at once, and reports slot occupancy / scheduler
-idle time (BASELINE's ASHA shape is 8 GPUs; the real-GPU runs use 1 slot per box)."""
+"""The ASHA benchmark's multi-slot control plane on CPU: ``scripts/bench_asha.py``
+with 8 artificial slots runs the 16-trial adaptive_asha CIFAR-10 search at the BASELINE shape
+(reference examples/computer_vision/cifar10_pytorch/adaptive.yaml: 32 epochs x 50,000 records,
+validation every epoch) through the real det-master + det-agent + harness, with each batch's GPU
+work modelled as the measured MI355X time (0.289 ms at batch 32, scripts/asha_model).  Slot time
+lost to the control plane -- waiting for resources or a container, container start-up, the master's
+round trip between workloads -- must stay under 5 %; the rest of the idle time is ASHA's own (no
+trial has work while rungs complete).  Full-shape record: profiles/r6_asha_8slot_baseline_shape.json."""
 import json
 import os
 import pathlib
@@ -14,10 +18,10 @@ REPO = pathlib.Path(__file__).resolve().parent.parent
 
 
 @pytest.mark.timeout(900)
-def test_bench_asha_eight_artificial_slots(tmp_path):
+def test_bench_asha_eight_slots_control_plane_bound(tmp_path):
     env = dict(os.environ, DET_BENCH_LOGDIR=str(tmp_path), MASTER_ADDR="127.0.0.1")
     p = subprocess.run([sys.executable, str(REPO / "scripts" / "bench_asha.py"), "--artificial-slots", "8",
-                        "--max-length-batches", "16", "--max-trials", "16", "--amp", "O0", "--validation-records", "128", "--timeout", "600"],
+                        "--modelled-batch-ms", "0.289", "--max-trials", "16", "--timeout", "600"],
                        capture_output=True, text=True, timeout=800, env=env, cwd=str(REPO))
     assert p.returncode == 0, p.stderr[-3000:]
     res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
@@ -25,5 +29,8 @@ def test_bench_asha_eight_artificial_slots(tmp_path):
     assert res["trials_completed"] == 16
     assert res["slots"] == 8
     assert res["peak_busy_slots"] == 8, res  # the scheduler ran 8 trials at once
-    assert 0.0 <= res["scheduler_idle_frac"] < 1.0
+    assert res["config"]["max_length"] == {"epochs": 32}
+    cp = res["control_plane"]
+    assert "error" not in cp, cp
+    assert cp["control_plane_idle_frac"] <= 0.05, cp
     (tmp_path / "asha_8slot.json").write_text(json.dumps(res))
