@@ -1239,7 +1239,8 @@ class _Shortcut1x1(torch.autograd.Function):
     def forward(ctx, x, weight, stride, stats, link):
         n, c, h, w_ = x.shape
         cout = weight.shape[0]
-        wk = weight.reshape(cout, c).contiguous()
+        wk = weight.reshape(cout, c)
+        wk = (wk if wk.dtype == torch.bfloat16 else wk.to(torch.bfloat16)).contiguous()  # fp32 weights (conv2d_native)
         if stride == 2:
             cfg = SHORTCUT_S2_CFG.get((c, cout), 8 if cout % 256 == 0 else 0)  # cfg 8: 256-wide N tiles
             y, parts = igemm_conv(x, weight, stride=2, stats=stats, w_krsc=wk, cfg=cfg)
@@ -1276,7 +1277,8 @@ class _Shortcut1x1(torch.autograd.Function):
         dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
         dx = dw = None
         if ctx.needs_input_grad[0] or link is not None:
-            w2 = weight.reshape(cout, c).contiguous()
+            w2 = weight.reshape(cout, c)
+            w2 = (w2 if w2.dtype == torch.bfloat16 else w2.to(torch.bfloat16)).contiguous()
             abn = None
             if pend is not None:  # dY = the deferred BN apply, staged by the dgrad and written into dy2
                 d, bx, coef = pend
@@ -1316,3 +1318,67 @@ def shortcut_conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, link=None, stat
     """Projection-shortcut conv on the native path (``shortcut_native_ok`` must hold)."""
     SHORTCUT_COUNTS["native"] += 1
     return _Shortcut1x1.apply(x, conv_mod.weight, int(conv_mod.stride[0]), stats, link)
+
+
+# ------------------------------------------------------------------------------------------------
+# generic conv2d on the native kernels (detection backbones, FPN)
+# ------------------------------------------------------------------------------------------------
+# The R50-FPN detectors (Faster / Mask R-CNN, RetinaNet, DETR) run the same ResNet-50 convolution
+# shapes as the benchmark, at batch 2 and detection image sizes, without training BatchNorm (frozen,
+# folded into the weight and a bias).  ``conv2d_native`` routes a bias-free conv2d to the kernels
+# the ResNet trial uses -- 1x1 stride 1 (det_conv gemm_nt / det_igemm), 1x1 stride 2 (det_igemm
+# gather), R x S stride 1 / 2 (det_igemm implicit GEMM forward and input gradient, ring / halo-patch
+# weight gradient), the 7x7/2 stem (det_conv GM_STEM / patch kernel) -- with the BatchNorm
+# statistics epilogues off.  Shapes the tiles do not cover (channels not multiples of 64: the RPN
+# / box heads) return None and stay on the library conv.  DET_NATIVE_CONV2D=0 turns it off (A/B).
+NATIVE_CONV2D = os.environ.get("DET_NATIVE_CONV2D", "1") != "0"
+CONV2D_COUNTS = {"native": 0, "fallback": 0}
+
+
+def conv2d_native(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, pad: int = 0) -> Optional[torch.Tensor]:
+    """``F.conv2d(x, weight, None, stride, pad)`` on the native kernels, or None when not covered
+    (CPU, non-channels_last input, fp32 without bf16 autocast, unsupported shape)."""
+    if not (NATIVE_CONV2D and ENABLED and x.device.type == "cuda" and x.dim() == 4 and weight.dim() == 4):
+        return None
+    cout, cin, r, s = weight.shape
+    bf = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                       and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    if not bf or not x.is_contiguous(memory_format=torch.channels_last) or x.data_ptr() % 16 != 0 or \
+            x.shape[1] != cin or x.numel() >= (1 << 31):
+        CONV2D_COUNTS["fallback"] += 1
+        return None
+    kind = None
+    if r == s == 1 and pad == 0 and cin % 64 == 0 and cout % 64 == 0 and stride in (1, 2):
+        kind = "1x1"
+    elif r == s and r in (3, 5) and pad == (r - 1) // 2 and stride in (1, 2) and cin % 64 == 0 and cout % 64 == 0:
+        kind = "rs"
+    elif r == s == 7 and stride == 2 and pad == 3 and cin in (3, 4) and cout == 64:
+        kind = "stem"
+    if kind is None:
+        CONV2D_COUNTS["fallback"] += 1
+        return None
+    CONV2D_COUNTS["native"] += 1
+    xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+    with torch.autocast("cuda", enabled=False):
+        if kind == "1x1":
+            if stride == 1:
+                return _Conv1x1.apply(xb, weight, False, None, None)
+            return _Shortcut1x1.apply(xb, weight, 2, False, None)
+        if kind == "rs":
+            return _ConvRS.apply(xb, weight, int(stride), int(pad), False, None)
+        return _StemConv.apply(pad_channels4(xb) if cin == 3 else xb, weight, False)
+
+
+def conv2d_module(x: torch.Tensor, conv_mod: torch.nn.Conv2d, fallback=None) -> torch.Tensor:
+    """``conv_mod(x)`` with the convolution on the native kernels where ``conv2d_native`` covers it
+    (square kernel, symmetric zero padding, groups 1, dilation 1); the bias is added after.
+    ``fallback`` (default ``conv_mod``) runs the uncovered cases."""
+    st, pd = conv_mod.stride, conv_mod.padding
+    if isinstance(pd, tuple) and st[0] == st[1] and pd[0] == pd[1] and conv_mod.groups == 1 and \
+            conv_mod.dilation == (1, 1) and conv_mod.padding_mode == "zeros":
+        y = conv2d_native(x, conv_mod.weight, int(st[0]), int(pd[0]))
+        if y is not None:
+            if conv_mod.bias is not None:
+                y = y + conv_mod.bias.to(y.dtype).view(1, -1, 1, 1)
+            return y
+    return fallback(x) if fallback is not None else conv_mod(x)

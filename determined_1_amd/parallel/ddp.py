@@ -78,7 +78,7 @@ def auto_bucket_cap(total_bytes: int, threshold_bytes: int) -> int:
 
 
 class _Bucket:
-    __slots__ = ("arena", "lo", "hi", "params", "comp", "recv", "work", "mode")
+    __slots__ = ("arena", "lo", "hi", "params", "comp", "recv", "work", "mode", "f32", "f32_shard")
 
     def __init__(self, arena: Arena, lo: int, hi: int, params: List[int]) -> None:
         self.arena = arena
@@ -89,6 +89,8 @@ class _Bucket:
         self.recv = None  # type: Optional[torch.Tensor]
         self.work = None  # type: Any
         self.mode = "allreduce"
+        self.f32 = None  # type: Optional[torch.Tensor]  # fp32_accum under hipGraph capture (see _launch)
+        self.f32_shard = None  # type: Optional[torch.Tensor]
 
     @property
     def grad(self) -> torch.Tensor:
@@ -333,6 +335,24 @@ class GradientBucketer:
             wire = b.comp
         if b.mode == "allreduce":
             b.work = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        elif wire.is_cuda and torch.cuda.is_current_stream_capturing():
+            # inside a hipGraph capture (pytorch/_graph.py): RCCL's all-to-all does not capture on this
+            # stack (the process faults; all-reduce, reduce-scatter and all-gather do --
+            # scripts/dbg/rccl_capture.py, profiles/r6_rccl_capture.jsonl), so the one-rounding
+            # reduction becomes an fp32 reduce-scatter of the widened bucket, the shard rounded to the
+            # wire dtype once, and the same in-place all-gather
+            n = wire.numel() // self.world_size
+            if b.f32 is None or b.f32.numel() != wire.numel():
+                b.f32 = torch.empty(wire.numel(), dtype=torch.float32, device=wire.device)
+                b.f32_shard = torch.empty(n, dtype=torch.float32, device=wire.device)
+            shard = wire[self.rank * n:(self.rank + 1) * n]
+            b.f32.copy_(wire)
+            w1 = dist.reduce_scatter_tensor(b.f32_shard, b.f32, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            side = self._side_stream(wire.device)
+            with torch.cuda.stream(side):
+                w1.wait()
+                shard.copy_(b.f32_shard)
+                b.work = dist.all_gather_into_tensor(wire, shard, group=self.group, async_op=True)
         else:
             assert b.recv is not None
             n = wire.numel() // self.world_size

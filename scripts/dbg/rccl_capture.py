@@ -9,7 +9,8 @@ import os
 import subprocess
 import sys
 
-CASES = ["all_reduce", "all_reduce_async", "all_to_all_async", "all_gather_async", "side_stream_chain"]
+CASES = ["all_reduce", "all_reduce_async", "all_gather_async", "reduce_scatter_async", "rs_ag_side_chain",
+         "all_to_all_async", "side_stream_chain"]
 
 
 def run_case(case: str) -> dict:
@@ -41,6 +42,18 @@ def run_case(case: str) -> dict:
             elif case == "all_gather_async":
                 dist.all_gather_into_tensor(out, y, async_op=True).wait()
                 y = out
+            elif case == "reduce_scatter_async":
+                dist.reduce_scatter_tensor(out, y, async_op=True).wait()
+                y = out
+            elif case == "rs_ag_side_chain":  # fp32 reduce-scatter, cast on a side stream, all-gather
+                w1 = dist.reduce_scatter_tensor(out, y, async_op=True)
+                with torch.cuda.stream(side):
+                    w1.wait()
+                    z = out + 1
+                    w2 = dist.all_gather_into_tensor(out, z, async_op=True)
+                w2.wait()
+                torch.cuda.current_stream().wait_stream(side)
+                y = out
             elif case == "side_stream_chain":  # the bucketer's fp32_accum shape
                 w1 = dist.all_to_all_single(out, y, async_op=True)
                 with torch.cuda.stream(side):
@@ -55,7 +68,7 @@ def run_case(case: str) -> dict:
         g.replay()
         torch.cuda.synchronize()
         rec["replayed"] = True
-        want = x * 2 + (1 if case == "side_stream_chain" else 0)
+        want = x * 2 + (1 if case in ("side_stream_chain", "rs_ag_side_chain") else 0)
         rec["correct"] = bool(torch.equal(res, want))
     except Exception as e:  # noqa: BLE001
         rec["error"] = f"{type(e).__name__}: {e}"[:300]
@@ -77,7 +90,7 @@ def main() -> None:
             print(line[-1], flush=True)
         else:
             print(json.dumps({"case": case, "rc": r.returncode, "stderr": r.stderr[-600:]}), flush=True)
-        if r.returncode < 0:  # a fault: stop here
+        if r.returncode < 0:  # a fault (a host-side crash of that child): the later cases are not run
             break
 
 
