@@ -420,6 +420,138 @@ bn_stats_combine_par(const double* __restrict__ part, int S, Geom g, FinArgs a) 
   }
 }
 
+// One-launch sliced finalize: bn_stats_reduce, then the block that arrives last for its channel
+// block merges the S slices (bn_stats_combine_par's work) -- one launch per BN instead of two.  The
+// round-3 version of this published the slices with an agent-scope release fence per block, which
+// writes back the XCD's whole L2 (41 vs 16 us per BN, profiles/r3_resnet50_lastblock_finalize_
+// negative_steady.csv).  Here the slice sums go out as write-through (sc1) stores, the storing wave
+// drains them (vmcnt(0)) before its lane 0 adds to the channel block's arrival counter, and the last
+// arriver reads every slice back with sc1 loads behind a workgroup barrier -- the hand-off form the
+// guide measures without fences (MI355X_MICROARCH.md "Valid forms", first table row).  The counter
+// goes back to 0 for the next BatchNorm on the stream.  No spinning: blocks that are not last exit.
+constexpr int kMaxChanBlocks = 64;  // C <= 4096
+__device__ unsigned g_bn_stats_arrivals[kMaxChanBlocks];
+__device__ unsigned g_bn_bwd_arrivals[kMaxChanBlocks];
+
+__device__ __forceinline__ void stats_finish(double t1, double t2, int c, const Geom& g, const FinArgs& a) {
+  const double M = static_cast<double>(g.M);
+  const double meand = t1 / M;
+  double m2 = t2 - M * meand * meand;
+  if (m2 < 0) m2 = 0;
+  const float mean = static_cast<float>(meand);
+  const float var = static_cast<float>(m2 / M);
+  const float rstd = rsqrtf(var + a.eps);
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  const float bt = a.beta ? a.beta[c] : 0.f;
+  const float sc = gm * rstd;
+  a.save_mean[c] = mean;
+  a.save_rstd[c] = rstd;
+  a.scale[c] = sc;
+  a.shift[c] = bt - mean * sc;
+  if (a.running_mean) {
+    float f = a.momentum;
+    if (f < 0.f) f = a.num_batches_tracked ? 1.f / static_cast<float>(*a.num_batches_tracked + 1) : 0.f;
+    const float unbiased = g.M > 1 ? static_cast<float>(m2 / (M - 1.0)) : var;
+    a.running_mean[c] = (1.f - f) * a.running_mean[c] + f * mean;
+    a.running_var[c] = (1.f - f) * a.running_var[c] + f * unbiased;
+  }
+}
+
+// true in every thread of the block that arrives last (wave 0 published this block's slice)
+__device__ __forceinline__ bool last_arrival(unsigned* counter, unsigned total, int* flag) {
+  if (threadIdx.x < 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's write-through slice stores landed
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = old == total - 1 ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+__global__ void __launch_bounds__(kFinThreads)
+bn_stats_reduce_last(const float* __restrict__ pmean, const float* __restrict__ pm2, Geom g, int per_slice,
+                     double* __restrict__ part, FinArgs a) {
+  __shared__ double red1[kFinLanes][kFinCh];
+  __shared__ double red2[kFinLanes][kFinCh];
+  __shared__ int is_last;
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  const int b0 = blockIdx.y * per_slice;
+  const int b1 = min(g.nrb, b0 + per_slice);
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  if (ok) {
+    const int last = g.nrb - 1;
+    const double n_full = static_cast<double>(g.rpb);
+    const double n_last = static_cast<double>(g.M - static_cast<int64_t>(last) * g.rpb);
+    int b = b0 + lane;
+    for (; b + 3 * kFinLanes < b1; b += 4 * kFinLanes) {
+      float mv[4], qv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = static_cast<int64_t>(b + u * kFinLanes) * g.C + c;
+        mv[u] = pmean[o];
+        qv[u] = pm2[o];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double nb = (b + u * kFinLanes) == last ? n_last : n_full;
+        const double m = mv[u];
+        s1[u] += nb * m;
+        s2[u] += static_cast<double>(qv[u]) + nb * m * m;
+      }
+    }
+    for (; b < b1; b += kFinLanes) {
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      const double nb = b == last ? n_last : n_full;
+      const double m = pmean[o];
+      s1[0] += nb * m;
+      s2[0] += static_cast<double>(pm2[o]) + nb * m * m;
+    }
+  }
+  red1[lane][cl] = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+  red2[lane][cl] = (s2[0] + s2[1]) + (s2[2] + s2[3]);
+  __syncthreads();
+  if (lane == 0 && ok) {  // wave 0
+    double t1 = 0, t2 = 0;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) {
+      t1 += red1[q][cl];
+      t2 += red2[q][cl];
+    }
+    const int64_t o = (static_cast<int64_t>(blockIdx.y) * g.C + c) * 2;
+    __hip_atomic_store(part + o, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + o + 1, t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!last_arrival(&g_bn_stats_arrivals[blockIdx.x], gridDim.y, &is_last)) return;
+  // the last block of this channel block: merge the S slices in a fixed order (deterministic)
+  if (a.bump && blockIdx.x == 0 && threadIdx.x == 0) *a.bump += 1;
+  double t1 = 0, t2 = 0;
+  if (ok) {
+    for (int q = lane; q < static_cast<int>(gridDim.y); q += kFinLanes) {
+      const int64_t o = (static_cast<int64_t>(q) * g.C + c) * 2;
+      t1 += __hip_atomic_load(part + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t2 += __hip_atomic_load(part + o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();  // red1/red2 reuse
+  red1[lane][cl] = t1;
+  red2[lane][cl] = t2;
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&g_bn_stats_arrivals[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane != 0 || !ok) return;
+  t1 = 0;
+  t2 = 0;
+#pragma unroll
+  for (int q = 0; q < kFinLanes; ++q) {
+    t1 += red1[q][cl];
+    t2 += red2[q][cl];
+  }
+  stats_finish(t1, t2, c, g, a);
+}
+
 __global__ void __launch_bounds__(256)
 bn_stats_combine(const double* __restrict__ part, int S, Geom g, FinArgs a) {
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -453,6 +585,16 @@ bn_stats_combine(const double* __restrict__ part, int S, Geom g, FinArgs a) {
   }
 }
 
+// DET_BN_LASTBLOCK=0: the two-launch sliced finalizes (reduce, then combine) instead of the one-launch
+// last-arriving-block form (A/B switch, read once)
+inline bool bn_last_block() {
+  static const bool v = [] {
+    const char* e = std::getenv("DET_BN_LASTBLOCK");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return v;
+}
+
 // fp32 elements of scratch the two-stage finalize needs for C channels (fp64 pairs per slice)
 inline int64_t fin_scratch_elems(int C) { return static_cast<int64_t>(kMaxSlices) * C * 4; }
 
@@ -471,6 +613,10 @@ void launch_stats_finalize(hipStream_t st, const float* pmean, const float* pm2,
   const int per = (g.nrb + S - 1) / S;
   S = (g.nrb + per - 1) / per;
   double* part = reinterpret_cast<double*>(scratch);
+  if (bn_last_block() && cb <= kMaxChanBlocks) {
+    hipLaunchKernelGGL(bn_stats_reduce_last, dim3(cb, S), dim3(kFinThreads), 0, st, pmean, pm2, g, per, part, fa);
+    return;
+  }
   hipLaunchKernelGGL(bn_stats_reduce, dim3(cb, S), dim3(kFinThreads), 0, st, pmean, pm2, g, per, part);
   hipLaunchKernelGGL(bn_stats_combine_par, dim3(cb), dim3(kFinThreads), 0, st, part, S, g, fa);
 }
@@ -820,6 +966,84 @@ bn_bwd_combine(const float* __restrict__ part, int S, Geom g, BwdFin a) {
   a.coef[2 * g.C + c] = C0;
 }
 
+__device__ __forceinline__ void bwd_finish(float ts, float tsx, int c, const Geom& g, const BwdFin& a) {
+  const float rstd = a.rstd[c], mu = a.mean[c];
+  const float gm = a.gamma ? a.gamma[c] : 1.f;
+  const float dbeta = ts;
+  const float dgamma = tsx * rstd;
+  if (a.dgamma) a.dgamma[c] = dgamma;
+  if (a.dbeta) a.dbeta[c] = dbeta;
+  const float invM = 1.f / static_cast<float>(g.M);
+  const float A = gm * rstd;
+  const float B = -gm * rstd * rstd * dgamma * invM;
+  const float C0 = -A * dbeta * invM - B * mu;
+  a.coef[c] = A;
+  a.coef[g.C + c] = B;
+  a.coef[2 * g.C + c] = C0;
+}
+
+// bn_bwd_reduce + bn_bwd_combine in one launch (the hand-off of bn_stats_reduce_last)
+__global__ void __launch_bounds__(kFinThreads)
+bn_bwd_reduce_last(const float* __restrict__ psum, const float* __restrict__ psumx, Geom g, int per_slice,
+                   float* __restrict__ part, BwdFin a) {
+  __shared__ float r1[kFinLanes][kFinCh];
+  __shared__ float r2[kFinLanes][kFinCh];
+  __shared__ int is_last;
+  const int cl = threadIdx.x % kFinCh, lane = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  const bool ok = c < g.C;
+  const int b0 = blockIdx.y * per_slice;
+  const int b1 = min(g.nrb, b0 + per_slice);
+  float sa[4] = {0.f, 0.f, 0.f, 0.f}, sb[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    int b = b0 + lane;
+    for (; b + 3 * kFinLanes < b1; b += 4 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t o = static_cast<int64_t>(b + u * kFinLanes) * g.C + c;
+        sa[u] += psum[o];
+        sb[u] += psumx[o];
+      }
+    }
+    for (; b < b1; b += kFinLanes) {
+      const int64_t o = static_cast<int64_t>(b) * g.C + c;
+      sa[0] += psum[o];
+      sb[0] += psumx[o];
+    }
+  }
+  r1[lane][cl] = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+  r2[lane][cl] = (sb[0] + sb[1]) + (sb[2] + sb[3]);
+  __syncthreads();
+  if (lane == 0 && ok) {  // wave 0
+    float ts = 0.f, tsx = 0.f;
+#pragma unroll
+    for (int q = 0; q < kFinLanes; ++q) { ts += r1[q][cl]; tsx += r2[q][cl]; }
+    const int64_t o = (static_cast<int64_t>(blockIdx.y) * g.C + c) * 2;
+    __hip_atomic_store(part + o, ts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + o + 1, tsx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!last_arrival(&g_bn_bwd_arrivals[blockIdx.x], gridDim.y, &is_last)) return;
+  float ts = 0.f, tsx = 0.f;
+  if (ok) {
+    for (int q = lane; q < static_cast<int>(gridDim.y); q += kFinLanes) {
+      const int64_t o = (static_cast<int64_t>(q) * g.C + c) * 2;
+      ts += __hip_atomic_load(part + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tsx += __hip_atomic_load(part + o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  r1[lane][cl] = ts;
+  r2[lane][cl] = tsx;
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&g_bn_bwd_arrivals[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane != 0 || !ok) return;
+  ts = 0.f;
+  tsx = 0.f;
+#pragma unroll
+  for (int q = 0; q < kFinLanes; ++q) { ts += r1[q][cl]; tsx += r2[q][cl]; }
+  bwd_finish(ts, tsx, c, g, a);
+}
+
 // Backward finalize: sliced reduce + parallel combine when the partial list is long and scratch
 // (>= 2 * kMaxSlices * C floats) is given, else the single-launch walk.
 void launch_bwd_finalize(hipStream_t st, const float* psum, const float* psumx, const Geom& g, const BwdFin& bf,
@@ -835,6 +1059,10 @@ void launch_bwd_finalize(hipStream_t st, const float* psum, const float* psumx, 
   }
   const int per = (g.nrb + S - 1) / S;
   S = (g.nrb + per - 1) / per;
+  if (bn_last_block() && cb <= kMaxChanBlocks) {
+    hipLaunchKernelGGL(bn_bwd_reduce_last, dim3(cb, S), dim3(kFinThreads), 0, st, psum, psumx, g, per, scratch, bf);
+    return;
+  }
   hipLaunchKernelGGL(bn_bwd_reduce, dim3(cb, S), dim3(kFinThreads), 0, st, psum, psumx, g, per, scratch);
   hipLaunchKernelGGL(bn_bwd_combine, dim3(cb), dim3(kFinThreads), 0, st, scratch, S, g, bf);
 }

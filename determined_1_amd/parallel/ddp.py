@@ -337,7 +337,8 @@ class GradientBucketer:
             b.work = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         elif wire.is_cuda and torch.cuda.is_current_stream_capturing():
             # inside a hipGraph capture (pytorch/_graph.py): RCCL's all-to-all does not capture on this
-            # stack (the process faults; all-reduce, reduce-scatter and all-gather do --
+            # stack (the process faults; all-reduce, reduce-scatter and all-gather issued from the
+            # capturing stream do --
             # scripts/dbg/rccl_capture.py, profiles/r6_rccl_capture.jsonl), so the one-rounding
             # reduction becomes an fp32 reduce-scatter of the widened bucket, the shard rounded to the
             # wire dtype once, and the same in-place all-gather
@@ -347,12 +348,12 @@ class GradientBucketer:
                 b.f32_shard = torch.empty(n, dtype=torch.float32, device=wire.device)
             shard = wire[self.rank * n:(self.rank + 1) * n]
             b.f32.copy_(wire)
-            w1 = dist.reduce_scatter_tensor(b.f32_shard, b.f32, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            side = self._side_stream(wire.device)
-            with torch.cuda.stream(side):
-                w1.wait()
-                shard.copy_(b.f32_shard)
-                b.work = dist.all_gather_into_tensor(wire, shard, group=self.group, async_op=True)
+            # issued from the capturing stream itself: a collective chained through a side stream
+            # faults the capture (rs_ag_side_chain / side_stream_chain in the probe)
+            dist.reduce_scatter_tensor(b.f32_shard, b.f32, op=dist.ReduceOp.SUM, group=self.group,
+                                       async_op=True).wait()
+            shard.copy_(b.f32_shard)
+            b.work = dist.all_gather_into_tensor(wire, shard, group=self.group, async_op=True)
         else:
             assert b.recv is not None
             n = wire.numel() // self.world_size
@@ -386,7 +387,8 @@ class GradientBucketer:
                 b.work = None
                 if b.comp is not None:
                     scale_cast_(b.comp, b.grad)
-        if self._side is not None:
+        if self._side is not None and not torch.cuda.is_current_stream_capturing():
+            # (a captured window keeps its collectives on the capturing stream: nothing to join)
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         self._comm = False
         if self._tuner is not None:

@@ -55,6 +55,10 @@ import torch
 from torch.utils import _pytree as pytree
 
 WARMUP = 2        # eager batches per key before capturing (lazy init, MIOpen find, allocator)
+# "thread_local": other threads may keep calling the HIP API while a step is being captured -- the
+# RCCL process group's watchdog thread queries its work events continuously, which "global" mode
+# turns into a capture error (hipErrorStreamCaptureUnsupported) and a process abort
+CAPTURE_MODE = "thread_local"
 MAX_GRAPHS = 2    # live graphs (the epoch's full batch + its tail batch)
 THRASH_LIMIT = 8  # captures that replayed fewer than THRASH_MIN times -> graphs off
 THRASH_MIN = 4
@@ -354,7 +358,7 @@ class TrainStepGraph:
             for f in self.fused:
                 f.capturing(True)
             try:
-                with torch.cuda.graph(graph, pool=self.pool), _native_rng_advance():
+                with torch.cuda.graph(graph, pool=self.pool, capture_error_mode=CAPTURE_MODE), _native_rng_advance():
                     out = self._eager(static_batch, epoch_idx, batch_idx)
             finally:
                 for f in self.fused:
@@ -450,7 +454,7 @@ class TrainStepGraph:
             self.pool = torch.cuda.graph_pool_handle()
         try:
             torch.cuda.synchronize()
-            with torch.cuda.graph(graph, pool=self.pool), _native_rng_advance():
+            with torch.cuda.graph(graph, pool=self.pool, capture_error_mode=CAPTURE_MODE), _native_rng_advance():
                 outs = []
                 for i, b in enumerate(views):
                     o = self._eager(b, epoch_idx, batch_idx + i)
@@ -538,7 +542,7 @@ class EvalStepGraph:
                 self.pool = torch.cuda.graph_pool_handle()
             try:
                 torch.cuda.synchronize()
-                with torch.cuda.graph(graph, pool=self.pool):
+                with torch.cuda.graph(graph, pool=self.pool, capture_error_mode=CAPTURE_MODE):
                     out = self._eager(static_batch)
             except Exception as e:
                 logging.warning("hip_graph: evaluate_batch runs eagerly: capture failed: %s: %s", type(e).__name__, e)
@@ -581,7 +585,7 @@ class EvalStepGraph:
                     self.pool = torch.cuda.graph_pool_handle()
                 try:
                     torch.cuda.synchronize()
-                    with torch.cuda.graph(graph, pool=self.pool):
+                    with torch.cuda.graph(graph, pool=self.pool, capture_error_mode=CAPTURE_MODE):
                         outs = [self._eager(b) for b in views]
                         if not all(isinstance(o, dict) and all(isinstance(v, torch.Tensor) and v.dim() == 0
                                                                for v in o.values()) for o in outs):

@@ -137,6 +137,8 @@ def main() -> None:
     ctrl = make_controller(Trial, cfg, stream(), trial_seed=7)
     ctrl.run()
     el = max(pdist.allgather_object(t["t1"] - t["t0"]))
+    from determined_1_amd.ops import conv as _native_conv
+
     if rank == 0:
         print(json.dumps({
             "metric": f"images/sec (whole node) {args.model} PyTorchTrial", "value": round(steps * gbs / el, 2),
@@ -147,6 +149,7 @@ def main() -> None:
             "config": {"model": model_name, "per_gpu_batch": args.batch_per_gpu, "global_batch": gbs, "amp": args.amp,
                        "optimizer": "AdamW, backbone lr 1e-5, clip 0.1" if args.model == "detr" else "SGD momentum",
                        "s_per_iter": round(el / steps, 4),
+                       "native_conv2d": dict(_native_conv.CONV2D_COUNTS), "native_conv2d_on": _native_conv.NATIVE_CONV2D,
                        "parallelism": f"dp{world}"}}), flush=True)
     pdist.shutdown()
 

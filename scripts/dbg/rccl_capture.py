@@ -9,8 +9,10 @@ import os
 import subprocess
 import sys
 
-CASES = ["all_reduce", "all_reduce_async", "all_gather_async", "reduce_scatter_async", "rs_ag_side_chain",
-         "all_to_all_async", "side_stream_chain"]
+# the cases that crash the capturing process on this stack (r6s5 / r6s6) come last: the run stops at
+# the first crash
+CASES = ["all_reduce", "all_reduce_async", "all_gather_async", "reduce_scatter_async", "rs_ag_chain",
+         "rs_ag_side_chain", "all_to_all_async", "side_stream_chain"]
 
 
 def run_case(case: str) -> dict:
@@ -45,6 +47,11 @@ def run_case(case: str) -> dict:
             elif case == "reduce_scatter_async":
                 dist.reduce_scatter_tensor(out, y, async_op=True).wait()
                 y = out
+            elif case == "rs_ag_chain":  # the bucketer's capture path: all on the capturing stream
+                dist.reduce_scatter_tensor(out, y, async_op=True).wait()
+                z = out + 1
+                dist.all_gather_into_tensor(out, z, async_op=True).wait()
+                y = out
             elif case == "rs_ag_side_chain":  # fp32 reduce-scatter, cast on a side stream, all-gather
                 w1 = dist.reduce_scatter_tensor(out, y, async_op=True)
                 with torch.cuda.stream(side):
@@ -68,7 +75,7 @@ def run_case(case: str) -> dict:
         g.replay()
         torch.cuda.synchronize()
         rec["replayed"] = True
-        want = x * 2 + (1 if case in ("side_stream_chain", "rs_ag_side_chain") else 0)
+        want = x * 2 + (1 if case in ("side_stream_chain", "rs_ag_side_chain", "rs_ag_chain") else 0)
         rec["correct"] = bool(torch.equal(res, want))
     except Exception as e:  # noqa: BLE001
         rec["error"] = f"{type(e).__name__}: {e}"[:300]
@@ -90,7 +97,7 @@ def main() -> None:
             print(line[-1], flush=True)
         else:
             print(json.dumps({"case": case, "rc": r.returncode, "stderr": r.stderr[-600:]}), flush=True)
-        if r.returncode < 0:  # a fault (a host-side crash of that child): the later cases are not run
+        if r.returncode < 0:  # a crashed child: nothing more runs on the GPU in this call
             break
 
 
