@@ -66,6 +66,8 @@ def parse() -> argparse.Namespace:
                     help="apply bottleneck bn2 in conv3's GEMM prologue instead of materialising it (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
                     help="MIOpen find mode for the conv algorithms (tuned during the untimed warmup)")
+    ap.add_argument("--params-out", default="", help="(verification) save per-tensor float64 sums / norms of the "
+                                                     "final parameters to this path")
     ap.add_argument("--launch-timeout", type=float, default=float(os.environ.get("DET_BENCH_LAUNCH_TIMEOUT", "0")),
                     help="self-launch mode: kill all ranks after this many seconds (0 = no limit)")
     return ap.parse_args()
@@ -251,6 +253,10 @@ def main() -> None:
     ctrl = make_controller(ResNetImageNetTrial, config, stream(), trial_seed=1234)
     timing["ctrl_built"] = time.perf_counter()
     ctrl.run()
+    if args.params_out and int(os.environ.get("RANK", "0")) == 0:
+        ps = [p.detach().double() for p in ctrl.context.models[0].parameters()]
+        torch.save({"sums": torch.stack([p.sum() for p in ps]).cpu(), "norms": torch.stack([p.norm() for p in ps]).cpu(),
+                    "graph": getattr(getattr(ctrl, "_graph", None), "stats", lambda: None)()}, args.params_out)
     elapsed = timing["t1"] - timing["t0"]
     warmup_s = timing["t0"] - t_start
     import torch.distributed as tdist

@@ -53,7 +53,9 @@ class BertEncoderConfig:
         return cls(hidden_size=int(hp.get("hidden_size", 768)), num_hidden_layers=int(hp.get("num_hidden_layers", 12)),
                    num_attention_heads=int(hp.get("num_attention_heads", 12)),
                    intermediate_size=int(hp.get("intermediate_size", 3072)),
-                   vocab_size=int(hp.get("vocab_size", 30522)))
+                   vocab_size=int(hp.get("vocab_size", 30522)),
+                   hidden_dropout_prob=float(hp.get("hidden_dropout_prob", 0.1)),
+                   attention_probs_dropout_prob=float(hp.get("attention_probs_dropout_prob", 0.1)))
 
 
 class _LN(nn.Module):

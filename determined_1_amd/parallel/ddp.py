@@ -188,6 +188,10 @@ class GradientBucketer:
             for p in a.params:
                 self._handles.append(p.register_post_accumulate_grad_hook(self._hook))
         self._tuner = _FusionAutotuner(self, autotune_log) if autotune else None
+        # the reduction a hipGraph capture records (see _launch): forced on for the gloo CPU tests of
+        # that path; launch_log, when a list, records the bucket order of every launch
+        self.graph_path = False
+        self.launch_log = None  # type: Optional[List[int]]
 
     # ------------------------------------------------------------------------------------------
     def _wire_dtype(self, b: _Bucket) -> torch.dtype:
@@ -320,6 +324,8 @@ class GradientBucketer:
 
     def _launch_in_order(self) -> None:
         while self._next < len(self.buckets) and self._ready[self._next]:
+            if self.launch_log is not None:
+                self.launch_log.append(self._next)
             self._launch(self.buckets[self._next])
             self._next += 1
 
@@ -335,7 +341,7 @@ class GradientBucketer:
             wire = b.comp
         if b.mode == "allreduce":
             b.work = dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        elif wire.is_cuda and torch.cuda.is_current_stream_capturing():
+        elif self.graph_path or (wire.is_cuda and torch.cuda.is_current_stream_capturing()):
             # inside a hipGraph capture (pytorch/_graph.py): RCCL's all-to-all does not capture on this
             # stack (the process faults; all-reduce, reduce-scatter and all-gather issued from the
             # capturing stream do --

@@ -82,7 +82,7 @@ Json Line(const std::string& msg) {
 }  // namespace
 
 TEST(logstore_backend_appends_do_not_wait_and_nothing_is_lost) {
-  auto* be = new FlakyBackend(100);
+  auto* be = new FlakyBackend(400);
   LogStore ls;
   LogShipOptions opt;
   opt.batch_lines = 200;
@@ -120,7 +120,9 @@ TEST(logstore_backend_appends_do_not_wait_and_nothing_is_lost) {
   reading = false;
   reader.join();
   EXPECT_EQ(bad_reads.load(), 0);
-  EXPECT(worst_ms < 50.0);  // never a 100 ms backend call on the appending thread
+  // never a 400 ms backend call on the appending thread (the bound leaves room for a loaded host and
+  // sanitizer builds: the suite runs on parallel workers)
+  EXPECT(worst_ms < 200.0);
   Json st = ls.Stats();
   EXPECT(st.get_int("failed_batches", 0) >= 1);
   EXPECT_EQ(st.get_int("shipped_lines", 0), kLines);

@@ -25,6 +25,8 @@ def main() -> None:
     ap.add_argument("--agg", type=int, default=1, help="optimizations.aggregation_frequency")
     ap.add_argument("--impl", default="native", choices=["native", "hf"], help="fused MI355X encoder or HF BERT")
     ap.add_argument("--hip-graph", action="store_true", help="optimizations.hip_graph: replay train_batch as a hipGraph")
+    ap.add_argument("--no-dropout", action="store_true", help="dropout 0 (graph vs eager parameter comparisons)")
+    ap.add_argument("--params-out", default="", help="save per-tensor float64 sums / norms of the final parameters")
     ap.add_argument("--loss-every", type=int, default=0,
                     help="timed steps in workloads of this many batches, reporting each one's mean loss (long-run "
                          "graph-vs-eager tracking)")
@@ -52,7 +54,8 @@ def main() -> None:
     gbs = args.batch_per_gpu * world
     cfg = {
         "hyperparameters": {"global_batch_size": gbs, "learning_rate": 3e-5, "max_seq_length": 384, "amp": args.amp,
-                            "max_grad_norm": 1.0, "train_records": 100000, "impl": args.impl},
+                            "max_grad_norm": 1.0, "train_records": 100000, "impl": args.impl,
+                            **({"hidden_dropout_prob": 0.0, "attention_probs_dropout_prob": 0.0} if args.no_dropout else {})},
         "resources": {"slots_per_trial": world},
         "optimizations": {"aggregation_frequency": args.agg, "hip_graph": bool(args.hip_graph)},
         "searcher": {"name": "single", "metric": "f1", "max_length": {"batches": args.steps}, "smaller_is_better": False},
@@ -110,6 +113,10 @@ def main() -> None:
     g = getattr(ctrl, "_graph", None)
     graph_stats = {k: getattr(g, k, None) for k in ("captures", "failed_captures", "replays")} if g is not None else None
     el = max(pdist.allgather_object(t["t1"] - t["t0"]))
+    if args.params_out and rank == 0:
+        ps = [p.detach().double() for p in ctrl.context.models[0].parameters()]
+        torch.save({"sums": torch.stack([p.sum() for p in ps]).cpu(), "norms": torch.stack([p.norm() for p in ps]).cpu(),
+                    "head": torch.cat([p.reshape(-1)[:64] for p in ps]).cpu()}, args.params_out)
     from determined_1_amd.ops import transformer as tfops
 
     if rank == 0:

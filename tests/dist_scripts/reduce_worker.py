@@ -33,14 +33,21 @@ def main() -> None:
                          autotune_log=f"{out}.autotune.csv" if autotune else None)
     caps = []
     windows = int(os.environ.get("DET_TEST_WINDOWS", "1"))
+    b.graph_path = os.environ.get("DET_TEST_GRAPH_PATH") == "1"  # the reduction a hipGraph capture records
+    b.launch_log = []
     for _ in range(windows):
         arena.flat_grad.copy_(full.to(dtype))
         b.prepare_backward(True)
+        # buckets complete in reverse arena order here (the sink/hooks would announce them as
+        # backward produces them); the bucketer must still launch them in bucket order
+        for bi in reversed(range(len(b.buckets))):
+            b._group_ready(bi)
         b.synchronize()
         caps.append(b.cap_bytes)
     torch.save({"reduced": arena.flat_grad.clone(), "modes": [x.mode for x in b.buckets],
                 "nbuckets": len(b.buckets), "auto_choice": b.auto_choice, "downgraded": b.downgraded,
-                "caps": caps, "tuned": None if b._tuner is None else b._tuner.result}, f"{out}.{rank}.pt")
+                "caps": caps, "tuned": None if b._tuner is None else b._tuner.result,
+                "launch_log": b.launch_log}, f"{out}.{rank}.pt")
     dist.destroy_process_group()
 
 

@@ -162,3 +162,26 @@ def test_tensor_fusion_autotune_converges_identically(tmp_path):
     exact = _exact_sum(2, res[0]["reduced"].numel(), torch.bfloat16)
     err = (res[0]["reduced"].double() - exact).abs()
     assert bool((err <= exact.abs() * 2.0 ** -8 + 1e-30).all())
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_graph_capture_reduction_path_order_and_numerics(tmp_path, world):
+    """the reduction a hipGraph capture records for fp32_accum buckets (fp32
+    reduce-scatter of the widened bucket, one rounding of the shard, in-place all-gather, all on the
+    capturing stream -- RCCL's all-to-all does not capture) launches the buckets in the same order as
+    the eager path and reduces to the same sums: exactly at 2 ranks, within one bf16 rounding of the
+    eager fp32_accum result at 4 (the fp32 sums of the two paths may round differently)."""
+    eager = _run(str(tmp_path / "e"), world, "fp32_accum")
+    graph = _run(str(tmp_path / "g"), world, "fp32_accum", extra_env={"DET_TEST_GRAPH_PATH": "1"})
+    n = eager[0]["nbuckets"]
+    for r in range(world):
+        assert eager[r]["launch_log"] == graph[r]["launch_log"] == list(range(n))
+        torch.testing.assert_close(graph[r]["reduced"], graph[0]["reduced"], rtol=0, atol=0)  # ranks agree
+    ge, gg = eager[0]["reduced"].double(), graph[0]["reduced"].double()
+    if world == 2:
+        torch.testing.assert_close(gg, ge, rtol=0, atol=0)
+    else:
+        ulp = ge.abs() * 2.0 ** -7 + 1e-30
+        assert bool(((gg - ge).abs() <= ulp).all())
+    exact = _exact_sum(world, gg.numel(), torch.bfloat16)
+    assert float((gg - exact).abs().max()) <= float((exact.abs() * 2.0 ** -8).max()) + 1e-6
