@@ -19,7 +19,7 @@ from typing import Optional
 _HERE = pathlib.Path(__file__).resolve().parent
 LIB_NAME = "libdetkernels.so"
 LIB_PATH = _HERE / LIB_NAME
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _lock = threading.Lock()
 _lib = None  # type: Optional[ctypes.CDLL]
@@ -80,6 +80,8 @@ _SIGNATURES = {
     ),
     "det_unscale_check": ([c_void_p, c_void_p, c_int, c_i64, c_float, c_void_p], c_int),
     "det_mt_copy": ([c_void_p, c_void_p, c_int, c_int, c_int, c_i64, c_float], c_int),
+    # hipGraph_t, mode (0 count, 1 replace memset nodes by fill-kernel nodes) -> memsets found
+    "det_graph_fix_memsets": ([c_void_p, c_int], c_int),
     "det_u8_normalize": (
         [c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_void_p, c_void_p],
         c_int,

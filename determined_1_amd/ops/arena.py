@@ -19,6 +19,7 @@ Here every parameter of an optimizer param group is *re-homed* into one contiguo
 Parameters are laid out in REVERSE registration order: backward produces gradients roughly from
 the last layer to the first, so buckets become ready front-to-back along the arena.
 """
+import os
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -186,6 +187,10 @@ def find_arena(arenas: Sequence[Arena], p: torch.Tensor) -> Optional[Arena]:
     return None
 
 
+# (debugging) DET_SINK_CAPTURE_FOREACH=0: captured landings copy one tensor per launch
+CAPTURE_FOREACH = os.environ.get("DET_SINK_CAPTURE_FOREACH", "1") != "0"
+
+
 class GradSink:
     """Steal-then-batch-copy gradient landing for arena parameters.
 
@@ -313,7 +318,12 @@ class GradSink:
         stolen = self._stolen[gi]
         self._stolen[gi] = []
         if stolen:
-            if a.flat_grad.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            if a.flat_grad.device.type == "cuda" and torch.cuda.is_current_stream_capturing() and not CAPTURE_FOREACH:
+                with torch.no_grad():
+                    for i, g in stolen:
+                        a.grad_views[i].copy_(g)
+                self.captured_flushes += 1
+            elif a.flat_grad.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 # under hipGraph capture: a multi-tensor copy whose pointers travel as kernel
                 # arguments.  A device pointer table allocated in the capture gets an address the
                 # graph's private pool already gave a tensor freed earlier in the same step, so a

@@ -536,7 +536,7 @@ sum_rows_kernel(const TI* __restrict__ in, TO* __restrict__ out, int rows, int64
 // ============================================================================================
 extern "C" {
 
-int det_abi_version() { return 20; }
+int det_abi_version() { return 21; }
 
 int det_sgd_step(void* stream, int g_dtype, int out_dtype, float* p, const void* g, float* buf,
                  void* out_model, int64_t n, float lr, float momentum, float dampening, float wd,

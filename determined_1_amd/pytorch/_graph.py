@@ -66,6 +66,38 @@ THRASH_MIN = 4
 # through one multi-tensor copy per group instead of one `grad += new` launch per parameter (~180 per
 # BERT-base step, 0.9 ms in the r5s20 graph profile).
 GRAPH_SINK = os.environ.get("DET_GRAPH_SINK", "1") != "0"
+# (debugging) keep the captured hipGraph_t so scripts can list its nodes (scripts/dbg/graph_nodes.py)
+KEEP_GRAPH = os.environ.get("DET_GRAPH_KEEP", "0") == "1"
+# HIP runtime defect on this stack: a small hipMemsetAsync captured into a graph writes a stale, garbage
+# pattern from the graph's second launch on (<= 4 KiB reproduced, 1 MiB fine; scripts/dbg/
+# memset_graph_repro.py, profiles/r6_graph_memset_root_cause.txt).  torch's cross-block reductions
+# reset their semaphores that way -- e.g. the bias gradient of a bf16 Linear at batch >= 512, which
+# froze at its captured value in every later ResNet-50 replay.  Every capture therefore keeps its
+# hipGraph_t, has its memset nodes rewritten into fill-kernel nodes (ops/csrc/det_graph.hip), and is
+# instantiated after that.  DET_GRAPH_FIX_MEMSETS=0 leaves the graphs as captured.
+FIX_MEMSETS = os.environ.get("DET_GRAPH_FIX_MEMSETS", "1") != "0"
+MEMSET_FIXES = {"graphs": 0, "memset_nodes": 0}
+
+
+def new_graph() -> "torch.cuda.CUDAGraph":
+    return torch.cuda.CUDAGraph(keep_graph=True) if (KEEP_GRAPH or FIX_MEMSETS) else torch.cuda.CUDAGraph()
+
+
+def finish_capture(graph: "torch.cuda.CUDAGraph") -> int:
+    """After ``torch.cuda.graph(graph)`` exits: rewrite the memset nodes, then instantiate.
+    Returns the number of memset nodes rewritten."""
+    n = 0
+    if FIX_MEMSETS:
+        from determined_1_amd.ops import _lib
+
+        n = int(_lib.get_lib().det_graph_fix_memsets(graph.raw_cuda_graph(), 1))
+        if n < 0:
+            raise RuntimeError(f"hipGraph memset rewrite failed (code {n})")
+        MEMSET_FIXES["graphs"] += 1
+        MEMSET_FIXES["memset_nodes"] += n
+    if FIX_MEMSETS or KEEP_GRAPH:
+        graph.instantiate()
+    return n
 
 
 @contextlib.contextmanager
@@ -86,17 +118,15 @@ CHUNK_WARMUP = 1  # per-batch chunks per multi-batch key before capturing it
 CHUNK_MAX_GRAPHS = 8  # full chunks + the partial sizes steps and epochs end on
 
 
-# Half-precision convolutions on the vendor library (MIOpen) do not replay correctly from a captured
-# graph once other MIOpen work runs between replays: the graph's results diverge from eager and go
-# non-finite within a few replays.  Reproduced without this framework (scripts/dbg/
-# miopen_graph_repro.py --step, round 5): a plain bf16 torch CNN trained K steps per graph with
-# eager steps in between goes NaN on the second replay; the same steps in fp32, with the convolutions
-# off MIOpen (torch.backends.cudnn.enabled = False), or with only Linear layers replay exactly; every
-# MIOpen op captured alone replays exactly.  This was the round-4 "O2 + dropout" NaN of the CIFAR
-# trial (dropout was incidental: the NaN stays with dropout removed and with masks from a fixed bank).
+# Half-precision convolutions on the vendor library (MIOpen) looked replay-unsafe in round 5: a plain
+# bf16 torch CNN trained K steps per graph with eager steps in between went NaN on the second replay
+# (scripts/dbg/miopen_graph_repro.py --step).  Round 6 pinned the mechanism: MIOpen's weight-gradient
+# solvers zero their accumulation buffers with small hipMemsetAsync calls, and a captured small memset
+# replays a stale pattern from the graph's second launch on (FIX_MEMSETS above).  With the memset nodes
+# rewritten, the same repro replays exactly (profiles/r6_graph_memset_root_cause.txt), so the probe
+# below only keeps MIOpen steps eager when the rewrite is turned off (DET_GRAPH_FIX_MEMSETS=0).
 # The first warm-up step of EVERY graph key runs under this probe; a hit keeps that key eager (other
-# keys still capture: their graphs hold no MIOpen kernel, so eager MIOpen work between their replays
-# is harmless).
+# keys still capture).
 # DET_GRAPH_LIBRARY_CONVS=1 captures anyway (for the reproduction scripts).
 LIBRARY_CONV_OPS = ("aten::convolution", "aten::convolution_backward", "aten::_convolution",
                     "aten::miopen_convolution", "aten::cudnn_convolution")
@@ -121,7 +151,7 @@ class _LibraryConvProbe:
             def __torch_dispatch__(self, func, types, args=(), kwargs=None):  # noqa: ANN001
                 if probe.found is None:
                     name = func.name()
-                    if name in LIBRARY_CONV_OPS and torch.backends.cudnn.enabled:
+                    if name in LIBRARY_CONV_OPS and torch.backends.cudnn.enabled and not FIX_MEMSETS:
                         x = args[0] if args else None
                         if isinstance(x, torch.Tensor) and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
                             probe.found = f"half-precision MIOpen convolution ({name} on {x.dtype})"
@@ -350,7 +380,7 @@ class TrainStepGraph:
         static_batch = pytree.tree_unflatten(static_leaves, spec)
         host = [f.host_state() for f in self.fused]
         calls0 = [f.steps_called for f in self.fused]
-        graph = torch.cuda.CUDAGraph()
+        graph = new_graph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         try:
@@ -363,6 +393,7 @@ class TrainStepGraph:
             finally:
                 for f in self.fused:
                     f.capturing(False)
+            finish_capture(graph)
         except Exception as e:  # capture-unsafe op in user code or a library: stay eager
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
@@ -449,7 +480,7 @@ class TrainStepGraph:
                                                  spec), sizes).batches
         host = [f.host_state() for f in self.fused]
         calls0 = [f.steps_called for f in self.fused]
-        graph = torch.cuda.CUDAGraph()
+        graph = new_graph()
         if self.pool is None:
             self.pool = torch.cuda.graph_pool_handle()
         try:
@@ -467,6 +498,7 @@ class TrainStepGraph:
                 if any(list(o.keys()) != names for o in outs):
                     raise TypeError("train_batch metric names differ between batches")
                 out = {k: torch.stack([o[k].detach().float() for o in outs]) for k in names}
+            finish_capture(graph)
         except Exception as e:  # noqa: BLE001 - stay on per-batch replays
             for f, h in zip(self.fused, host):
                 f.set_host_state(h)
@@ -483,7 +515,7 @@ class TrainStepGraph:
     def stats(self) -> Dict[str, Any]:
         return {"captures": self.captures, "replays": self.replays, "failed_captures": self.failed_captures,
                 "disabled": self.disabled_reason, "chunk_replays": self.chunk_replays,
-                "chunk_disabled": self.chunk_disabled}
+                "chunk_disabled": self.chunk_disabled, "memset_nodes_rewritten": MEMSET_FIXES["memset_nodes"]}
 
 
 class EvalStepGraph:
@@ -537,13 +569,14 @@ class EvalStepGraph:
             static_in = [x.detach().clone() for x in leaves if isinstance(x, torch.Tensor)]
             it = iter(static_in)
             static_batch = pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x for x in leaves], spec)
-            graph = torch.cuda.CUDAGraph()
+            graph = new_graph()
             if self.pool is None:
                 self.pool = torch.cuda.graph_pool_handle()
             try:
                 torch.cuda.synchronize()
                 with torch.cuda.graph(graph, pool=self.pool, capture_error_mode=CAPTURE_MODE):
                     out = self._eager(static_batch)
+                finish_capture(graph)
             except Exception as e:
                 logging.warning("hip_graph: evaluate_batch runs eagerly: capture failed: %s: %s", type(e).__name__, e)
                 self.disabled_reason = f"capture failed: {e}"
@@ -580,7 +613,7 @@ class EvalStepGraph:
                 it = iter(static_in)
                 views = BatchChunk(pytree.tree_unflatten([next(it) if isinstance(x, torch.Tensor) else x
                                                           for x in leaves], spec), chunk.sizes).batches
-                graph = torch.cuda.CUDAGraph()
+                graph = new_graph()
                 if self.pool is None:
                     self.pool = torch.cuda.graph_pool_handle()
                 try:
@@ -591,6 +624,7 @@ class EvalStepGraph:
                                                                for v in o.values()) for o in outs):
                             raise TypeError("evaluate_batch metrics are not all scalar tensors")
                         out = {k: torch.stack([o[k].detach().float() for o in outs]) for k in outs[0]}
+                    finish_capture(graph)
                 except Exception as e:  # noqa: BLE001
                     self.chunk_disabled = f"{type(e).__name__}: {e}"
                     logging.warning("hip_graph: multi-batch evaluate capture failed: %s", self.chunk_disabled)

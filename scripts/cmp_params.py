@@ -7,7 +7,7 @@ import torch
 
 
 def main() -> None:
-    a, b = torch.load(sys.argv[1], weights_only=False), torch.load(sys.argv[2], weights_only=False)
+    a, b = torch.load(sys.argv[1], weights_only=True), torch.load(sys.argv[2], weights_only=True)
     tol = float(sys.argv[sys.argv.index("--tol") + 1]) if "--tol" in sys.argv else 1e-3
     out = {}
     for k in ("sums", "norms"):

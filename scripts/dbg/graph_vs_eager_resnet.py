@@ -34,9 +34,14 @@ def run(args: argparse.Namespace) -> None:
     rec = {"params": [], "grads": [], "loss": [], "names": None}
     holder = {}
 
+    # --one-workload W: W one-batch workloads (bench.py's warmup) then the remaining steps as ONE
+    # workload (no host synchronisation between its batches), recording only after each workload
+    plan = [(i, 1) for i in range(args.steps)] if args.one_workload <= 0 else \
+        [(i, 1) for i in range(args.one_workload)] + [(args.one_workload, args.steps - args.one_workload)]
+
     def stream():
-        for i in range(args.steps):
-            yield workload.train_workload(i + 1, num_batches=1, total_batches_processed=i), [], \
+        for wi, (start, nb) in enumerate(plan):
+            yield workload.train_workload(wi + 1, num_batches=nb, total_batches_processed=start), [], \
                 lambda r: rec["loss"].append(r)
             ctrl = holder["ctrl"]
             m = ctrl.context.models[0]
@@ -49,16 +54,75 @@ def run(args: argparse.Namespace) -> None:
                                  (p.grad.detach().double().cpu() if p.numel() <= 4096 else
                                   torch.stack([p.grad.detach().double().sum(), p.grad.detach().double().norm()]).cpu())
                                  for _, p in named])
+            # the arena gradient slots (a fresh window overwrites them; they keep the last step's
+            # gradient) and the arena params of every 1-D [num_classes] tensor (fc.bias)
+            small = []
+            for st in ctrl.context._opt_states:
+                sink = getattr(st.fused, "sink", None) if st.fused is not None else None
+                for a, idx in (sink.groups if sink is not None else []):
+                    for i in idx:
+                        if tuple(a.params[i].shape) == (1000,):
+                            small.append((a.grad_views[i].detach().double().cpu(), a.params[i].detach().double().cpu()))
+            rec.setdefault("fcb", []).append(small)
         yield workload.terminate_workload(args.steps + 1), [], workload.ignore_response
 
+    if args.trace_sink:
+        _trace_sink(rec)
     torch.cuda.set_device(0)
     holder["ctrl"] = make_controller(trial_cls, config, stream(), trial_seed=1234)
     holder["ctrl"].run()
     g = getattr(holder["ctrl"], "_graph", None)
     rec["graph"] = g.stats() if g is not None else None
+    if args.dump_nodes and g is not None:  # needs DET_GRAPH_KEEP=1
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from graph_nodes import graph_nodes
+
+        for key, cg in g.graphs.items():
+            nodes = graph_nodes(cg.graph.raw_cuda_graph())
+            counts = {}
+            for r in nodes:
+                counts[r["type"]] = counts.get(r["type"], 0) + 1
+            print("graph nodes", counts, flush=True)
+            for k, r in enumerate(nodes):
+                if r["type"] not in ("kernel", "empty"):
+                    print("  node", k, r, flush=True)
     rec["loss"] = [repr(x)[:200] for x in rec["loss"]]
     torch.save(rec, args.out)
     print("saved", args.out, rec["graph"], flush=True)
+    for e in rec.get("sink_log", []):
+        print(e)
+
+
+def _trace_sink(rec: dict) -> None:
+    """Log what the GradSink does with the fc-layer gradients (shapes [1000] / [1000, 2048])."""
+    import torch
+
+    from determined_1_amd.ops import arena
+
+    log = rec.setdefault("sink_log", [])
+    hook0, flush0, end0 = arena.GradSink._hook, arena.GradSink._flush, arena.GradSink.end_backward
+
+    def hook(self, p):
+        if tuple(p.shape) in ((1000,), (1000, 2048)):
+            slot = self._slot.get(id(p))
+            g = p.grad
+            log.append(("hook", tuple(p.shape), self.fresh, torch.cuda.is_current_stream_capturing(),
+                        None if g is None else (g.dtype == slot[7], tuple(g.stride()) == tuple(slot[6]),
+                                                g.data_ptr() == slot[4], g is slot[3]),
+                        slot[0], self._pending[slot[0]]))
+        return hook0(self, p)
+
+    def flush(self, gi):
+        shapes = [tuple(g.shape) for _, g in self._stolen[gi]]
+        log.append(("flush", gi, len(shapes), [s for s in shapes if s in ((1000,), (1000, 2048))],
+                    torch.cuda.is_current_stream_capturing()))
+        return flush0(self, gi)
+
+    def end(self):
+        log.append(("end_backward", self.fresh, list(self._pending)))
+        return end0(self)
+
+    arena.GradSink._hook, arena.GradSink._flush, arena.GradSink.end_backward = hook, flush, end
 
 
 def compare(a_path: str, b_path: str) -> None:
@@ -94,6 +158,9 @@ def main() -> None:
     ap.add_argument("--bs", type=int, default=64)
     ap.add_argument("--image", type=int, default=64)
     ap.add_argument("--arch", default="resnet50")
+    ap.add_argument("--one-workload", type=int, default=0)
+    ap.add_argument("--trace-sink", action="store_true")
+    ap.add_argument("--dump-nodes", action="store_true")
     args = ap.parse_args()
     if args.compare:
         compare(*args.compare)

@@ -16,6 +16,22 @@ import torch
 import torch.nn.functional as F
 
 
+def _maybe_fix(args, g) -> None:
+    """--fix-memsets: rewrite the captured memset nodes into fill-kernel nodes (ops/csrc/det_graph.hip;
+    the HIP runtime's small captured memsets replay a stale value, memset_graph_repro.py)."""
+    if not args.fix_memsets:
+        return
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from determined_1_amd.ops import _lib
+
+    n = _lib.get_lib().det_graph_fix_memsets(g.raw_cuda_graph(), 1)
+    print(json.dumps({"memset_nodes_rewritten": n}), flush=True)
+    g.instantiate()
+
+
 def cases(dev, dt, n):
     cl = torch.channels_last
     convs = [("conv1", 3, 32, 32, 0), ("conv2", 32, 32, 30, 0), ("conv3", 32, 64, 14, 1), ("conv4", 64, 64, 14, 0)]
@@ -157,9 +173,10 @@ def step_mode(args, dev, dt):
     with torch.cuda.stream(s):
         steps()
     torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
+    g = torch.cuda.CUDAGraph(keep_graph=args.fix_memsets)
     with torch.cuda.graph(g):
         static = steps()
+    _maybe_fix(args, g)
     for r in range(args.replays):
         start = [p.detach().clone() for p in params]
         bufs = clobber(args, dev)
@@ -201,6 +218,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--step", action="store_true", help="whole training steps instead of single ops")
+    ap.add_argument("--fix-memsets", action="store_true", help="rewrite captured memset nodes (det_graph.hip)")
     ap.add_argument("--clobber", type=int, default=0,
                     help="GiB of NaN-filled memory allocated after empty_cache() before every replay")
     ap.add_argument("--only", default="", help="comma-separated op names (op mode)")
@@ -241,9 +259,10 @@ def main():
             for x, dy in zip(xs, dys):
                 fn(x, dy)
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=args.fix_memsets)
         with torch.cuda.graph(g):
             outs = [fn(x, dy) for x, dy in zip(xs, dys)]
+        _maybe_fix(args, g)
         worst, nonfinite, first_bad, foreign = 0.0, 0, None, 0
         for r in range(args.replays):
             for o in outs:

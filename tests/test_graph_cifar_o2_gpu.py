@@ -6,6 +6,10 @@ other MIOpen work runs between replays (pure-PyTorch reproduction: scripts/dbg/m
 pytorch/_graph.py LIBRARY_CONV_OPS note) -- dropout was incidental.  The trial now runs on the
 native CNN kernels (no MIOpen), its graphs stay on, and the graph controller detects library
 half-precision convolutions in its first warm-up step and keeps such a train_batch eager.
+Round 6 pinned the mechanism underneath: the HIP runtime's captured small memsets (which MIOpen's
+weight-gradient solvers issue) replay a stale pattern; with the graphs' memset nodes rewritten into
+fill kernels (ops/csrc/det_graph.hip) MIOpen steps replay exactly and the probe is only armed when
+that rewrite is off (profiles/r6_graph_memset_root_cause.txt).
 """
 import os
 
@@ -76,10 +80,18 @@ class _HalfConvTrialNet(nn.Module):
         return self.fc(torch.relu(self.conv(x)).mean((2, 3)))
 
 
-def test_half_precision_library_convs_keep_train_batch_eager(gpu):
-    """A train_batch whose bf16 convolutions go to MIOpen is detected in the first warm-up step and
-    runs eagerly (finite, learning); the same model in fp32 captures and replays."""
+def test_half_precision_library_convs_keep_train_batch_eager(gpu, monkeypatch):
+    """With the captured-memset rewrite off, a train_batch whose bf16 convolutions go to MIOpen is
+    detected in the first warm-up step and runs eagerly (finite, learning); the same model in fp32
+    captures and replays.  With the rewrite on (default) nothing is flagged."""
+    from determined_1_amd.pytorch import _graph
     from determined_1_amd.pytorch._graph import library_conv_reason
+
+    net = _HalfConvTrialNet().to(gpu).to(torch.bfloat16)
+    x = torch.randn(4, 3, 16, 16, device=gpu, dtype=torch.bfloat16)
+    out, reason = library_conv_reason(lambda: net(x).float().square().mean())
+    assert reason is None and torch.isfinite(out), reason
+    monkeypatch.setattr(_graph, "FIX_MEMSETS", False)
 
     torch.manual_seed(0)
     for dtype, expect_hit in ((torch.bfloat16, True), (torch.float32, False)):
