@@ -62,6 +62,10 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--no-native-conv1x1", action="store_true", help="1x1 convs on MIOpen instead of det_conv GEMMs (A/B)")
     ap.add_argument("--no-native-stem", action="store_true", help="7x7 stem conv on MIOpen instead of det_conv (A/B)")
     ap.add_argument("--no-native-conv3x3", action="store_true", help="3x3 convs on MIOpen instead of det_igemm (A/B)")
+    ap.add_argument("--no-hip-graph", action="store_true",
+                    help="run every step eagerly (A/B).  By default a 1-GPU run replays the step from a hipGraph "
+                         "(pytorch/_graph.py; bitwise equal to eager, tests/test_graph_memset_gpu.py); multi-GPU "
+                         "runs keep DET_STEP_TIMERS on, which keeps their steps eager")
     ap.add_argument("--bn-prologue", action="store_true",
                     help="apply bottleneck bn2 in conv3's GEMM prologue instead of materialising it (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
@@ -204,7 +208,7 @@ def main() -> None:
             "image_size": args.image_size,
         },
         "resources": {"slots_per_trial": world},
-        "optimizations": {"tensor_fusion_threshold": args.bucket_mb},
+        "optimizations": {"tensor_fusion_threshold": args.bucket_mb, "hip_graph": world == 1 and not args.no_hip_graph},
         "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": args.steps}},
         "scheduling_unit": args.steps,
     }
@@ -306,6 +310,7 @@ def main() -> None:
                 "warmup_batch_done_s": timing.get("warm"),
                 "startup_s": round(timing.get("ctrl_built", 0.0) - t_start, 1),
                 "miopen_find_db": os.environ.get("MIOPEN_USER_DB_PATH"),
+                "hip_graph": getattr(getattr(ctrl, "_graph", None), "stats", lambda: None)(),
             },
         }
         if phases:  # DET_STEP_TIMERS=1: per-batch device phases of the timed window (forward/backward/comm/opt)
