@@ -19,7 +19,7 @@ SRC_DIR = HERE / "csrc"
 SOURCES = [SRC_DIR / "det_kernels.hip", SRC_DIR / "det_norm.hip", SRC_DIR / "det_transformer.hip", SRC_DIR / "det_attention.hip",
            SRC_DIR / "det_pool.hip", SRC_DIR / "det_conv.hip", SRC_DIR / "det_igemm.hip", SRC_DIR / "det_detect.hip",
            SRC_DIR / "det_stream.hip", SRC_DIR / "det_cnn.hip", SRC_DIR / "det_embed.hip", SRC_DIR / "det_blaslt.hip",
-           SRC_DIR / "det_graph.hip"]
+           SRC_DIR / "det_graph.hip", SRC_DIR / "det_gemm8.hip"]
 OUT = HERE / "libdetkernels.so"
 ARCH = os.environ.get("DET_OFFLOAD_ARCH", "gfx950")
 

@@ -768,6 +768,212 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm3_kernel(IgArgs a) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// v8: the eight-phase ping-pong schedule of det_gemm8.hip (see its header) on igemm3's implicit-GEMM
+// gather.  256 x 256 block tile, 8 waves of 128 x 64 (the igemm3 cfg-8 wave decomposition, so the
+// igemm3 epilogues apply unchanged), K tiles of 64 = one tap x 64 channels (Cin % 64 == 0), LDS as
+// two K tiles x four 16 KiB half-tiles (A rows 0-127 / 128-255, B rows 0-127 / 128-255) of two
+// 64-B-row sub-images each.  Per K tile: P1 reads A rows 0-63 + B cols 0-31 and issues A(t+1),
+// P2 reads A rows 64-127 + B cols 32-63, P3 only computes, P4 issues B(t+2) into this tile's buffer
+// and retires tile t+1 (vmcnt 4).  The wave group of the lower 128 rows runs one barrier late.
+// ------------------------------------------------------------------------------------------------
+template <bool STATS, bool BNB>
+__global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NW = 8, kThreads = 512;
+  constexpr int TM = 128, TN = 64, FM = 8, FN = 4;
+  constexpr int HALF = 128 * 64 * 2, BUF = 4 * HALF;
+  constexpr int LDC = BN + 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntn = a.N / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int64_t m0 = static_cast<int64_t>(mt) * BM;
+  const int n0 = nt * BN;
+  const int lrow = lane >> 2;
+  const int gch = (lane & 3) ^ ((-(lrow >> 2)) & 3);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(a.X), 0, static_cast<int>(a.x_bytes), 0x00020000);
+  const int64_t KB = a.kb_stride > 0 ? a.kb_stride : a.K;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned short*>(a.W), 0, static_cast<int>(static_cast<int64_t>(a.N) * KB * 2), 0x00020000);
+  constexpr unsigned kOOB = 0xFFFFFFF0u;
+  // this lane's DMA rows: half h, row h*128 + wid*16 + lrow (4 lanes per 64-B row, chunk gch)
+  int aoff[2];
+  unsigned amask[2], boff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t m = m0 + h * 128 + wid * 16 + lrow;
+    aoff[h] = 0;
+    amask[h] = 0;
+    if (m < a.M) {
+      const int64_t hw = static_cast<int64_t>(a.Ho) * a.Wo;
+      const int64_t n = m / hw;
+      const int rem = static_cast<int>(m - n * hw);
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      const int hi0 = ho * a.stride - a.pad, wi0 = wo * a.stride - a.pad;
+      aoff[h] = static_cast<int>(((n * a.Hi + hi0) * a.Wi + wi0) * a.Cin * 2 + gch * 16);
+      for (int r = 0; r < a.R; ++r)
+        for (int s2 = 0; s2 < a.S; ++s2) {
+          const int hi = hi0 + r, wi = wi0 + s2;
+          if (hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi) amask[h] |= 1u << (r * a.S + s2);
+        }
+    }
+    boff[h] = static_cast<unsigned>(((static_cast<int64_t>(n0) + h * 128 + wid * 16 + lrow) * KB + gch * 8) * 2);
+  }
+  auto stage = [&](int ht, int kt) {
+    unsigned char* dst = smem + (kt & 1) * BUF + ht * HALF + wid * 1024;
+    const int k0 = kt * 64;
+    const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
+    if (ht < 2) {
+      const int r = tap / a.S, s2 = tap - r * a.S;
+      const int toff = ((r * a.Wi + s2) * a.Cin + c0) * 2;
+      const bool ok = (amask[ht] >> tap) & 1u;
+      const unsigned v = ok ? static_cast<unsigned>(aoff[ht] + toff) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)dst, 16, v, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(dst + 8192), 16, ok ? v + 64u : kOOB, 0, 0, 0);
+    } else {
+      const int kb = a.tapmap ? static_cast<int>((a.tapmap >> (4 * tap)) & 15u) * a.Cin + c0 : k0;
+      const unsigned v = boff[ht - 2] + static_cast<unsigned>(kb) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)dst, 16, v, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(dst + 8192), 16, v + 64u, 0, 0, 0);
+    }
+  };
+  // a raw barrier that also keeps every instruction in its phase
+  auto phase_barrier = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    block_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[FM][2], bfm[FN][2];
+  const int fr = lane & 15, fch = lane >> 4;
+  auto read_a = [&](int kt, int i0) {
+    const unsigned char* base = smem + (kt & 1) * BUF + wm * HALF;
+#pragma unroll
+    for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) af[i][kh] = *reinterpret_cast<const bf16x8*>(base + kh * 8192 + swz64(i * 16 + fr, fch));
+  };
+  auto read_b = [&](int kt, int j0) {
+    const unsigned char* base = smem + (kt & 1) * BUF + (2 + (wn >> 1)) * HALF;
+#pragma unroll
+    for (int j = j0; j < j0 + 2; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+        bfm[j][kh] = *reinterpret_cast<const bf16x8*>(base + kh * 8192 + swz64((wn & 1) * 64 + j * 16 + fr, fch));
+  };
+  auto mfma = [&](int i0, int j0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+        for (int j = j0; j < j0 + 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kh], bfm[j][kh], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = a.K / 64;
+  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+  if (nk > 1) { stage(2, 1); stage(3, 1); wait_vmcnt<4>(); } else wait_vmcnt<0>();
+  phase_barrier();
+  if (wm == 1) phase_barrier();  // the late group
+  for (int t = 0; t < nk; ++t) {
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    read_a(t, 0);
+    read_b(t, 0);
+    if (n1) { stage(0, t + 1); stage(1, t + 1); }
+    phase_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mfma(0, 0);
+    phase_barrier();
+    read_a(t, 4);
+    read_b(t, 2);
+    phase_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mfma(0, 2);
+    phase_barrier();
+    phase_barrier();
+    mfma(4, 2);
+    phase_barrier();
+    if (n2) { stage(2, t + 2); stage(3, t + 2); wait_vmcnt<4>(); } else wait_vmcnt<0>();
+    phase_barrier();
+    mfma(4, 0);
+    phase_barrier();
+  }
+  if (wm == 0) phase_barrier();
+  __syncthreads();
+
+  unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
+  const int64_t rows_left = a.M - m0;
+  const int nvalid = rows_left < BM ? static_cast<int>(rows_left) : BM;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * TN + j * 16 + (lane & 15);
+        ct[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  if (STATS && a.stats_first && !BNB)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
+  __syncthreads();
+  if constexpr (BNB) {
+    if (STATS)
+      det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                  static_cast<int64_t>(mt) * a.N + n0);
+    bnb_epilogue<BM, BN, kThreads>(a, smem, ct, LDC, m0, n0, mt, nvalid, tid);
+    return;
+  }
+  constexpr int CPR = BN / 8;
+#pragma unroll
+  for (int q = 0; q < (BM * CPR + kThreads - 1) / kThreads; ++q) {
+    const int idx = tid + q * kThreads;
+    const int row = idx / CPR, cc = idx - row * CPR;
+    if (idx < BM * CPR && row < nvalid)
+      *reinterpret_cast<us8*>(a.Y + out_row(a, m0 + row) * a.N + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * LDC + cc * 8);
+  }
+  if (STATS && !a.stats_first)
+    det_block_bn_stats<FM, FN, WM, TM, TN, BN>(acc, red, wm, wn, lane, tid, nvalid, a.pmean, a.pm2,
+                                                static_cast<int64_t>(mt) * a.N + n0);
+  (void)NW;
+#endif
+}
+
+inline int launch8(hipStream_t st, const IgArgs& a_in, bool stats, bool bnb) {
+  IgArgs a = a_in;
+  a.stats_first = stats_first_flag();
+  if (a.N % 256 != 0 || a.Cin % 64 != 0 || a.K % 64 != 0) return -6;
+  const int64_t nwg = ((a.M + 255) / 256) * (a.N / 256);
+  if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
+  constexpr int ring = 2 * 4 * 128 * 64 * 2, ctile = 256 * (256 + 16) * 2 + 12 * 2 * 256;
+  constexpr int smem = ring > ctile ? ring : ctile;
+  static_assert(smem <= 163840, "LDS");
+  if (bnb)
+    hipLaunchKernelGGL((igemm8_kernel<false, true>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
+  else if (stats)
+    hipLaunchKernelGGL((igemm8_kernel<true, false>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
+  else
+    hipLaunchKernelGGL((igemm8_kernel<false, false>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
+  return static_cast<int>(hipGetLastError());
+}
+
 // OCC: workgroups per CU the LDS footprint and register budget are sized for.  At OCC 2 one
 // workgroup's epilogue (C tile through LDS, 16-B stores, BN statistics) overlaps the other's K loop;
 // with one workgroup per CU the short-K GEMMs (1x1 expansions, K = 64..512) serialise load ->
@@ -867,6 +1073,7 @@ static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool st
     case 18: return launch3<256, 64, 4, 1, 3, 2>(st, a, stats, bnb);
     case 19: return launch3<128, 128, 2, 2, 4, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 4 waves
     case 20: return launch3<128, 256, 2, 4, 3, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 8 waves
+    case 21: return launch8(st, a, stats, bnb);  // eight-phase ping-pong, 256x256, BK 64
     default: return -7;
   }
 }
@@ -875,7 +1082,7 @@ static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool st
 static int cfg_bn(int c) {
   switch (c) {
     case 3: case 5: case 6: case 11: case 14: case 15: case 17: case 18: return 64;
-    case 8: case 10: case 20: return 256;
+    case 8: case 10: case 20: case 21: return 256;
     default: return 128;
   }
 }
@@ -886,9 +1093,19 @@ static int auto_cfg(const IgArgs& a) {
     return e ? std::atoi(e) : 0;
   }();
   // a forced configuration (sweeps) applies where its tile fits; other shapes keep the heuristic
-  if (forced > 0 && a.N % cfg_bn(forced) == 0 && (forced < 8 ? a.Cin % 64 == 0 : a.Cin % 32 == 0)) return forced;
+  if (forced > 0 && a.N % cfg_bn(forced) == 0 && ((forced < 8 || forced == 21) ? a.Cin % 64 == 0 : a.Cin % 32 == 0))
+    return forced;
   // measured per ResNet-50 shape (profiles/r3_igemm_cfgs.jsonl): 256 x 256 / BK 32 wherever N
   // allows, 256 x 128 / BK 64 at N = 128, 256 x 64 / BK 32 (4 waves) at N = 64
+  // R x S convolutions with 256-multiple N on the eight-phase schedule (cfg 21): 7-9 % faster than
+  // cfg 8 on ResNet-50's 256/512-channel 3x3 forward and stride-1 input-gradient passes; the
+  // stride-2 parity-class input gradients (tapmap) and 1x1 gathers (short K) stay on cfg 8
+  // (profiles/r6_igemm8_conv3x3.jsonl).  DET_IGEMM8=0 turns it off (A/B).
+  static const bool use8 = [] {
+    const char* e = std::getenv("DET_IGEMM8");
+    return !(e && e[0] == '0');
+  }();
+  if (use8 && a.N % 256 == 0 && a.Cin % 64 == 0 && a.tapmap == 0 && a.R * a.S > 1) return 21;
   if (a.N % 256 == 0 && a.Cin % 32 == 0) return 8;
   if (a.N % 128 == 0 && a.Cin % 64 == 0) return 2;
   return a.Cin % 32 == 0 ? 11 : 1;
