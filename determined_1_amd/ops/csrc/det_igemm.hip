@@ -777,12 +777,15 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) igemm3_kernel(IgArgs a) {
 // P2 reads A rows 64-127 + B cols 32-63, P3 only computes, P4 issues B(t+2) into this tile's buffer
 // and retires tile t+1 (vmcnt 4).  The wave group of the lower 128 rows runs one barrier late.
 // ------------------------------------------------------------------------------------------------
-template <bool STATS, bool BNB>
+template <int BM, int BN, bool STATS, bool BNB>
 __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NW = 8, kThreads = 512;
+  // 8 waves of 128 x 64: BM x BN = 256 x 256 (2 x 4 waves) or 512 x 128 (4 x 2)
+  constexpr int WM = BM / 128, WN = BN / 64, NW = 8, kThreads = 512;
+  static_assert(WM * WN == NW, "eight waves");
+  constexpr int NA = BM / 128, NB = BN / 128;  // A / B half-tiles per K tile
   constexpr int TM = 128, TN = 64, FM = 8, FN = 4;
-  constexpr int HALF = 128 * 64 * 2, BUF = 4 * HALF;
+  constexpr int HALF = 128 * 64 * 2, BUF = (NA + NB) * HALF;
   constexpr int LDC = BN + 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem + BM * LDC * 2);
@@ -805,10 +808,10 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
       const_cast<unsigned short*>(a.W), 0, static_cast<int>(static_cast<int64_t>(a.N) * KB * 2), 0x00020000);
   constexpr unsigned kOOB = 0xFFFFFFF0u;
   // this lane's DMA rows: half h, row h*128 + wid*16 + lrow (4 lanes per 64-B row, chunk gch)
-  int aoff[2];
-  unsigned amask[2], boff[2];
+  int aoff[NA];
+  unsigned amask[NA], boff[NB];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < NA; ++h) {
     const int64_t m = m0 + h * 128 + wid * 16 + lrow;
     aoff[h] = 0;
     amask[h] = 0;
@@ -825,13 +828,15 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
           if (hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi) amask[h] |= 1u << (r * a.S + s2);
         }
     }
-    boff[h] = static_cast<unsigned>(((static_cast<int64_t>(n0) + h * 128 + wid * 16 + lrow) * KB + gch * 8) * 2);
   }
+#pragma unroll
+  for (int h = 0; h < NB; ++h)
+    boff[h] = static_cast<unsigned>(((static_cast<int64_t>(n0) + h * 128 + wid * 16 + lrow) * KB + gch * 8) * 2);
   auto stage = [&](int ht, int kt) {
     unsigned char* dst = smem + (kt & 1) * BUF + ht * HALF + wid * 1024;
     const int k0 = kt * 64;
     const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
-    if (ht < 2) {
+    if (ht < NA) {
       const int r = tap / a.S, s2 = tap - r * a.S;
       const int toff = ((r * a.Wi + s2) * a.Cin + c0) * 2;
       const bool ok = (amask[ht] >> tap) & 1u;
@@ -840,7 +845,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(dst + 8192), 16, ok ? v + 64u : kOOB, 0, 0, 0);
     } else {
       const int kb = a.tapmap ? static_cast<int>((a.tapmap >> (4 * tap)) & 15u) * a.Cin + c0 : k0;
-      const unsigned v = boff[ht - 2] + static_cast<unsigned>(kb) * 2u;
+      const unsigned v = boff[ht - NA] + static_cast<unsigned>(kb) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)dst, 16, v, 0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void*)(dst + 8192), 16, v + 64u, 0, 0, 0);
     }
@@ -867,7 +872,7 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
       for (int kh = 0; kh < 2; ++kh) af[i][kh] = *reinterpret_cast<const bf16x8*>(base + kh * 8192 + swz64(i * 16 + fr, fch));
   };
   auto read_b = [&](int kt, int j0) {
-    const unsigned char* base = smem + (kt & 1) * BUF + (2 + (wn >> 1)) * HALF;
+    const unsigned char* base = smem + (kt & 1) * BUF + (NA + (wn >> 1)) * HALF;
 #pragma unroll
     for (int j = j0; j < j0 + 2; ++j)
 #pragma unroll
@@ -887,12 +892,22 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
   };
 
   const int nk = a.K / 64;
-  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
-  if (nk > 1) { stage(2, 1); stage(3, 1); wait_vmcnt<4>(); } else wait_vmcnt<0>();
+  // the late wave group: waves 4-7 (each SIMD holds waves s and s + 4)
+  const bool late = wid >= 4;
+#pragma unroll
+  for (int h = 0; h < NA + NB; ++h) stage(h, 0);
+  if (nk > 1) {
+#pragma unroll
+    for (int h = 0; h < NB; ++h) stage(NA + h, 1);
+    wait_vmcnt<2 * NB>();
+  } else {
+    wait_vmcnt<0>();
+  }
   phase_barrier();
-  if (wm == 1) phase_barrier();  // the late group
+  if (late) phase_barrier();
   for (int t = 0; t < nk; ++t) {
     const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    // P1: A rows 0-63 + B cols 0-31 of tile t; A(t+1) (first two half-tiles)
     read_a(t, 0);
     read_b(t, 0);
     if (n1) { stage(0, t + 1); stage(1, t + 1); }
@@ -900,8 +915,10 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);
     mfma(0, 0);
     phase_barrier();
+    // P2: A rows 64-127 + B cols 32-63 (the tile is now in registers); A(t+1) half-tiles 2-3
     read_a(t, 4);
     read_b(t, 2);
+    if (NA > 2 && n1) { stage(2, t + 1); stage(3, t + 1); }
     phase_barrier();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     mfma(0, 2);
@@ -909,12 +926,19 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
     phase_barrier();
     mfma(4, 2);
     phase_barrier();
-    if (n2) { stage(2, t + 2); stage(3, t + 2); wait_vmcnt<4>(); } else wait_vmcnt<0>();
+    // P4: B(t+2) into this tile's buffer (its last reads were in P2), then retire tile t+1
+    if (n2) {
+#pragma unroll
+      for (int h = 0; h < NB; ++h) stage(NA + h, t + 2);
+      wait_vmcnt<2 * NB>();
+    } else {
+      wait_vmcnt<0>();
+    }
     phase_barrier();
     mfma(4, 0);
     phase_barrier();
   }
-  if (wm == 0) phase_barrier();
+  if (!late) phase_barrier();
   __syncthreads();
 
   unsigned short* ct = reinterpret_cast<unsigned short*>(smem);
@@ -956,21 +980,22 @@ __global__ void __launch_bounds__(512, 1) igemm8_kernel(IgArgs a) {
 #endif
 }
 
-inline int launch8(hipStream_t st, const IgArgs& a_in, bool stats, bool bnb) {
+template <int BM, int BN>
+int launch8(hipStream_t st, const IgArgs& a_in, bool stats, bool bnb) {
   IgArgs a = a_in;
   a.stats_first = stats_first_flag();
-  if (a.N % 256 != 0 || a.Cin % 64 != 0 || a.K % 64 != 0) return -6;
-  const int64_t nwg = ((a.M + 255) / 256) * (a.N / 256);
+  if (a.N % BN != 0 || a.Cin % 64 != 0 || a.K % 64 != 0) return -6;
+  const int64_t nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   if (nwg >= (static_cast<int64_t>(1) << 31)) return -4;
-  constexpr int ring = 2 * 4 * 128 * 64 * 2, ctile = 256 * (256 + 16) * 2 + 12 * 2 * 256;
+  constexpr int ring = 2 * (BM + BN) * 64 * 2, ctile = BM * (BN + 16) * 2 + 12 * (BM / 128) * BN;
   constexpr int smem = ring > ctile ? ring : ctile;
   static_assert(smem <= 163840, "LDS");
   if (bnb)
-    hipLaunchKernelGGL((igemm8_kernel<false, true>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
+    hipLaunchKernelGGL((igemm8_kernel<BM, BN, false, true>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
   else if (stats)
-    hipLaunchKernelGGL((igemm8_kernel<true, false>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
+    hipLaunchKernelGGL((igemm8_kernel<BM, BN, true, false>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
   else
-    hipLaunchKernelGGL((igemm8_kernel<false, false>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
+    hipLaunchKernelGGL((igemm8_kernel<BM, BN, false, false>), dim3(static_cast<unsigned>(nwg)), dim3(512), smem, st, a);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1073,7 +1098,8 @@ static int run_cfg(int cfg, hipStream_t st, const IgArgs& a, bool dense, bool st
     case 18: return launch3<256, 64, 4, 1, 3, 2>(st, a, stats, bnb);
     case 19: return launch3<128, 128, 2, 2, 4, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 4 waves
     case 20: return launch3<128, 256, 2, 4, 3, 2>(st, a, stats, bnb);  // 64x64 wave tiles, 8 waves
-    case 21: return launch8(st, a, stats, bnb);  // eight-phase ping-pong, 256x256, BK 64
+    case 21: return launch8<256, 256>(st, a, stats, bnb);  // eight-phase ping-pong, 256x256, BK 64
+    case 22: return launch8<512, 128>(st, a, stats, bnb);  // eight-phase, 512x128 (4 x 2 waves of 128x64)
     default: return -7;
   }
 }
@@ -1093,7 +1119,7 @@ static int auto_cfg(const IgArgs& a) {
     return e ? std::atoi(e) : 0;
   }();
   // a forced configuration (sweeps) applies where its tile fits; other shapes keep the heuristic
-  if (forced > 0 && a.N % cfg_bn(forced) == 0 && ((forced < 8 || forced == 21) ? a.Cin % 64 == 0 : a.Cin % 32 == 0))
+  if (forced > 0 && a.N % cfg_bn(forced) == 0 && ((forced < 8 || forced >= 21) ? a.Cin % 64 == 0 : a.Cin % 32 == 0))
     return forced;
   // measured per ResNet-50 shape (profiles/r3_igemm_cfgs.jsonl): 256 x 256 / BK 32 wherever N
   // allows, 256 x 128 / BK 64 at N = 128, 256 x 64 / BK 32 (4 waves) at N = 64
@@ -1106,6 +1132,8 @@ static int auto_cfg(const IgArgs& a) {
     return !(e && e[0] == '0');
   }();
   if (use8 && a.N % 256 == 0 && a.Cin % 64 == 0 && a.tapmap == 0 && a.R * a.S > 1) return 21;
+  // 128-channel R x S convolutions: the 512 x 128 eight-phase tile, 2-3 % faster forward (r6s30)
+  if (use8 && a.N % 128 == 0 && a.Cin % 64 == 0 && a.tapmap == 0 && a.R * a.S > 1) return 22;
   if (a.N % 256 == 0 && a.Cin % 32 == 0) return 8;
   if (a.N % 128 == 0 && a.Cin % 64 == 0) return 2;
   return a.Cin % 32 == 0 ? 11 : 1;
@@ -2520,7 +2548,7 @@ int det_igemm_rows_per_block_cfg(int N, int cfg) {
   IgArgs a{};
   a.N = N;
   const int c = cfg > 0 ? cfg : auto_cfg(a);
-  return (c == 4 || c == 6 || c == 7 || c == 19 || c == 20) ? 128 : ((c >= 12 && c <= 15) ? 512 : 256);
+  return (c == 4 || c == 6 || c == 7 || c == 19 || c == 20) ? 128 : (((c >= 12 && c <= 15) || c == 22) ? 512 : 256);
 }
 int det_igemm_rows_per_block() { return 256; }
 
@@ -2588,8 +2616,7 @@ static int s2_cfg(int cin, int cfg) {
   return cin % 256 == 0 ? 8 : (cin % 128 == 0 ? 9 : 11);
 }
 int det_igemm_dgrad_s2_rows_per_block(int Cin, int cfg) {
-  const int c = s2_cfg(Cin, cfg);
-  return c >= 12 ? 512 : 256;
+  return det_igemm_rows_per_block_cfg(Cin, s2_cfg(Cin, cfg));
 }
 
 // Input gradient of a 3x3 / stride-2 / pad-1 convolution (Hi = 2 Ho, Wi = 2 Wo) without MIOpen:

@@ -42,7 +42,7 @@ def _run_cfg(xg, wg, st, pad, cfg, stats=False):
         raise
 
 
-@pytest.mark.parametrize("cfg", list(range(1, 16)) + [21])
+@pytest.mark.parametrize("cfg", list(range(1, 16)) + [21, 22])
 @pytest.mark.parametrize("case", CFG_SHAPES)
 def test_every_cfg_exact_on_integer_operands(gpu, case, cfg):
     nb, cin, h, w, cout, r, st, pad = case
@@ -54,7 +54,7 @@ def test_every_cfg_exact_on_integer_operands(gpu, case, cfg):
     torch.testing.assert_close(y.float().cpu(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 8, 11, 13, 21])
+@pytest.mark.parametrize("cfg", [0, 2, 8, 11, 13, 21, 22])
 def test_cfg_stats_partials(gpu, cfg):
     case = (4, 256, 28, 28, 256, 3, 1, 1)  # M = 3136: ragged last block for 256 and 512 rows
     nb, cin, h, w, cout, r, st, pad = case
