@@ -82,8 +82,8 @@ _SIGNATURES = {
     "det_mt_copy": ([c_void_p, c_void_p, c_int, c_int, c_int, c_i64, c_float], c_int),
     # hipGraph_t, mode (0 count, 1 replace memset nodes by fill-kernel nodes) -> memsets found
     "det_graph_fix_memsets": ([c_void_p, c_int], c_int),
-    # stream, A, B, C, bias, bias_dt, M, N, K, lda, ldb, ldc, mode
-    "det_gemm8": ([c_void_p] * 5 + [c_int, c_i64] + [c_int] * 6, c_int),
+    # stream, A, B, C, bias, bias_dt, M, N, K, lda, ldb, ldc, mode, C2, epi
+    "det_gemm8": ([c_void_p] * 5 + [c_int, c_i64] + [c_int] * 6 + [c_void_p, c_int], c_int),
     "det_u8_normalize": (
         [c_void_p, c_void_p, c_void_p, c_int, c_i64, c_int, c_void_p, c_void_p],
         c_int,

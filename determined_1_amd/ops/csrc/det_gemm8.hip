@@ -77,7 +77,17 @@ struct G8Args {
   int64_t M;
   int N, K, lda, ldb, ldc, bias_dt;
   unsigned a_bytes, b_bytes;  // buffer ranges
+  unsigned short* C2;         // epi 1 / 2: gelu(C) [M, ldc] (C keeps the pre-activation for the backward)
+  int epi;                    // 0 none, 1 erf GELU (BERT), 2 tanh GELU (gelu_new)
 };
+
+// the GELU of ops/csrc/det_transformer.hip gelu_f, applied to the bf16-rounded pre-activation (so
+// the fused output equals the separate det_tf_gelu_fwd pass bit for bit)
+__device__ __forceinline__ float gelu_epi(float z, int epi) {
+  if (epi == 1) return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+  const float u = 0.7978845608028654f * (z + 0.044715f * z * z * z);
+  return 0.5f * z * (1.f + tanhf(u));
+}
 
 template <int MODE>
 __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
@@ -238,8 +248,16 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
   for (int q = 0; q < kBM * CPR / kNT; ++q) {
     const int idx = tid + q * kNT;
     const int row = idx / CPR, cc = idx - row * CPR;
-    if (row < nvalid && cc * 8 < cols_left)
-      *reinterpret_cast<us8*>(g.C + (m0 + row) * g.ldc + n0 + cc * 8) = *reinterpret_cast<const us8*>(ct + row * kLDC + cc * 8);
+    if (row < nvalid && cc * 8 < cols_left) {
+      const us8 z = *reinterpret_cast<const us8*>(ct + row * kLDC + cc * 8);
+      *reinterpret_cast<us8*>(g.C + (m0 + row) * g.ldc + n0 + cc * 8) = z;
+      if (g.epi != 0) {
+        us8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_epi(bf2f(z[e]), g.epi));
+        *reinterpret_cast<us8*>(g.C2 + (m0 + row) * g.ldc + n0 + cc * 8) = o;
+      }
+    }
   }
 #endif
 }
@@ -260,15 +278,18 @@ extern "C" {
 // C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]); bf16 operands and output, fp32 accumulation.
 // Requirements (checked): K % 64 == 0, N % 8 == 0, lda/ldb/ldc % 8 == 0, 16-B aligned pointers,
 // operand byte ranges < 2^31.  mode 0 / 1: staging schedule (see the header).
+// epi 1 / 2: C2 [M, ldc] = gelu(C) (erf / tanh form), C keeps the pre-activation.
 int det_gemm8(void* stream, const void* A, const void* B, void* C, const void* bias, int bias_dt, int64_t M, int N,
-              int K, int lda, int ldb, int ldc, int mode) {
+              int K, int lda, int ldb, int ldc, int mode, void* C2, int epi) {
+  if (epi != 0 && (C2 == nullptr || (reinterpret_cast<uintptr_t>(C2) & 15) || epi > 2)) return -5;
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 != 0 || N % 8 != 0 || lda % 8 || ldb % 8 || ldc % 8) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(C)) & 15) return -2;
   const int64_t ab = ((M - 1) * lda + K) * 2, bb = (static_cast<int64_t>(N - 1) * ldb + K) * 2;
   if (ab >= (int64_t(1) << 31) || bb >= (int64_t(1) << 31)) return -3;
   if (((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN) >= (int64_t(1) << 31)) return -4;
   G8Args a{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), static_cast<unsigned short*>(C), bias,
-           M, N, K, lda, ldb, ldc, bias ? bias_dt : 0, static_cast<unsigned>(ab), static_cast<unsigned>(bb)};
+           M, N, K, lda, ldb, ldc, bias ? bias_dt : 0, static_cast<unsigned>(ab), static_cast<unsigned>(bb),
+           static_cast<unsigned short*>(C2), epi};
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int m = mode == 0 ? 0 : 1;
   if (!g_attr_set[m]) {

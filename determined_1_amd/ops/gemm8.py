@@ -23,8 +23,10 @@ def supported(a: torch.Tensor, b: torch.Tensor) -> bool:
 
 
 def gemm8(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-          mode: Optional[int] = None) -> torch.Tensor:
-    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N].  Raises if the shape is not supported."""
+          mode: Optional[int] = None, gelu_out: Optional[torch.Tensor] = None, gelu: int = 0) -> torch.Tensor:
+    """a [M, K] @ b[N, K]^T (+ bias[N]) -> bf16 [M, N].  gelu 1 (erf) / 2 (tanh): also writes
+    gelu(result) into ``gelu_out`` (same shape and strides as the result).  Raises if the shape is not
+    supported."""
     if not supported(a, b):
         raise ValueError(f"gemm8: unsupported operands {tuple(a.shape)} {a.dtype} / {tuple(b.shape)} {b.dtype}")
     m, k = a.shape
@@ -37,8 +39,12 @@ def gemm8(a: torch.Tensor, b: torch.Tensor, bias: Optional[torch.Tensor] = None,
         assert bias.is_contiguous() and bias.numel() == n
         bias_dt = 1 if bias.dtype == torch.float32 else 2
         assert bias.dtype in (torch.float32, torch.bfloat16)
+    if gelu:
+        assert gelu_out is not None and gelu_out.shape == out.shape and gelu_out.stride() == out.stride()
+        assert gelu_out.dtype == torch.bfloat16 and gelu_out.data_ptr() % 16 == 0
     st = torch.cuda.current_stream(a.device).cuda_stream
     _lib.check(get_lib().det_gemm8(st, a.data_ptr(), b.data_ptr(), out.data_ptr(),
                                    bias.data_ptr() if bias is not None else None, bias_dt, m, n, k,
-                                   a.stride(0), b.stride(0), out.stride(0), MODE if mode is None else mode), "gemm8")
+                                   a.stride(0), b.stride(0), out.stride(0), MODE if mode is None else mode,
+                                   gelu_out.data_ptr() if gelu else None, int(gelu)), "gemm8")
     return out

@@ -167,7 +167,31 @@ class SharedWeightGrads:
 #   (profiles/r5_bert_linear_shapes.json, scripts/bench_linear_shapes.py).
 NATIVE_LINEAR = os.environ.get("DET_NATIVE_LINEAR", "auto")
 NATIVE_AUTO_MAX_WEIGHT = 1 << 20
-LINEAR_COUNTS = {"native_fwd": 0, "native_dgrad": 0, "native_wgrad": 0}
+LINEAR_COUNTS = {"native_fwd": 0, "native_dgrad": 0, "native_wgrad": 0, "gemm8_gelu_fwd": 0}
+
+# The FFN-in Linear + GELU forward on the hand-written eight-phase GEMM (ops/csrc/det_gemm8.hip) with
+# the GELU in its epilogue (pre-activation and activation written from one C tile) instead of the
+# vendor GEMM plus a separate GELU pass; for outputs of at least GEMM8_MIN_ELEMS elements (the tile
+# is 256 x 256).  DET_GEMM8_FFN=0 turns it off (A/B).
+GEMM8_FFN = os.environ.get("DET_GEMM8_FFN", "1") != "0"
+GEMM8_MIN_ELEMS = 1 << 22
+
+
+def _gemm8_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], approx: bool):
+    """(z, gelu(z)) from one det_gemm8 launch, or None when the shape / dtypes do not fit."""
+    if not (GEMM8_FFN and x2.is_cuda and x2.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and x2.shape[0] * weight.shape[0] >= GEMM8_MIN_ELEMS
+            and (bias is None or (bias.dtype in (torch.bfloat16, torch.float32) and bias.is_contiguous()))):
+        return None
+    from determined_1_amd.ops import gemm8 as _g8
+
+    if not _g8.supported(x2, weight):
+        return None
+    z = torch.empty(x2.shape[0], weight.shape[0], dtype=torch.bfloat16, device=x2.device)
+    a = torch.empty_like(z)
+    _g8.gemm8(x2, weight, bias=bias, out=z, gelu_out=a, gelu=2 if approx else 1)
+    LINEAR_COUNTS["gemm8_gelu_fwd"] += 1
+    return z, a
 
 
 def _native_linear(x2: torch.Tensor, weight: torch.Tensor, wgrad: bool = False) -> bool:
@@ -377,11 +401,15 @@ class _LinearGELU(torch.autograd.Function):
     def forward(ctx, x, weight, bias, approx, acc, link=None):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.link = link
-        z = _addmm(x2, weight, bias)
-        a = torch.empty_like(z)
-        lib = _lib.get_lib()
-        _lib.check(lib.det_tf_gelu_fwd(_stream(z), _DT[z.dtype], z.data_ptr(), a.data_ptr(), z.numel(), int(approx)),
-                   "det_tf_gelu_fwd")
+        fused = None if _native_linear(x2, weight) else _gemm8_gelu(x2, weight, bias, bool(approx))
+        if fused is not None:
+            z, a = fused
+        else:
+            z = _addmm(x2, weight, bias)
+            a = torch.empty_like(z)
+            lib = _lib.get_lib()
+            _lib.check(lib.det_tf_gelu_fwd(_stream(z), _DT[z.dtype], z.data_ptr(), a.data_ptr(), z.numel(),
+                                           int(approx)), "det_tf_gelu_fwd")
         ctx.approx = int(approx)
         ctx.acc = acc
         ctx.save_for_backward(x2, weight, z)
