@@ -172,8 +172,10 @@ LINEAR_COUNTS = {"native_fwd": 0, "native_dgrad": 0, "native_wgrad": 0, "gemm8_g
 # The FFN-in Linear + GELU forward on the hand-written eight-phase GEMM (ops/csrc/det_gemm8.hip) with
 # the GELU in its epilogue (pre-activation and activation written from one C tile) instead of the
 # vendor GEMM plus a separate GELU pass; for outputs of at least GEMM8_MIN_ELEMS elements (the tile
-# is 256 x 256).  DET_GEMM8_FFN=0 turns it off (A/B).
-GEMM8_FFN = os.environ.get("DET_GEMM8_FFN", "1") != "0"
+# is 256 x 256).  Opt-in (DET_GEMM8_FFN=1): measured 0.4-1.1 % slower than hipBLASLt + the GELU pass
+# in the BERT graph step (1,462-1,465 vs 1,471-1,479 examples/s, profiles/r6_bert_gemm8_ffn_ab.jsonl)
+# -- the 4608 x 3072 x 768 GEMM is 8 % slower on the hand-written tile (r6_gemm8_vs_hipblaslt.jsonl).
+GEMM8_FFN = os.environ.get("DET_GEMM8_FFN", "0") == "1"
 GEMM8_MIN_ELEMS = 1 << 22
 
 

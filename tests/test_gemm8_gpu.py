@@ -100,6 +100,6 @@ def test_linear_gelu_routes_large_ffn_to_gemm8(gpu):
             assert (tf.LINEAR_COUNTS["gemm8_gelu_fwd"] > before) == on
             res[on] = (y.float(), x.grad.float(), w.grad.float(), b.grad.float())
         finally:
-            tf.GEMM8_FFN = True
+            tf.GEMM8_FFN = False
     for u, v in zip(res[False], res[True]):
         torch.testing.assert_close(v, u, rtol=2e-2, atol=2e-2 * float(u.abs().max()))

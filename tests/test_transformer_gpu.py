@@ -232,7 +232,7 @@ def test_native_linear_exact_on_integer_operands(gpu, monkeypatch, rows, K, N):
     xd, wd, bd = _leaf(x, gpu), _leaf(w, gpu), _leaf(b, gpu)
     y = tfops.linear(xd, wd, bd)
     y.backward(dy.to(gpu))
-    assert all(tfops.LINEAR_COUNTS[k] == before[k] + 1 for k in before), tfops.LINEAR_COUNTS
+    assert all(tfops.LINEAR_COUNTS[k] == before[k] + 1 for k in before if k.startswith("native_")), tfops.LINEAR_COUNTS
     assert torch.equal(y.cpu(), (x.float() @ w.float().t() + b.float()).to(torch.bfloat16))
     assert torch.equal(xd.grad.cpu(), (dy.float() @ w.float()).to(torch.bfloat16))
     assert torch.equal(wd.grad.float().cpu(), (dy.float().t() @ x.float()).to(torch.bfloat16).float())
