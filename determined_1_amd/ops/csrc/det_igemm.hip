@@ -1131,9 +1131,19 @@ static int auto_cfg(const IgArgs& a) {
     const char* e = std::getenv("DET_IGEMM8");
     return !(e && e[0] == '0');
   }();
-  if (use8 && a.N % 256 == 0 && a.Cin % 64 == 0 && a.tapmap == 0 && a.R * a.S > 1) return 21;
-  // 128-channel R x S convolutions: the 512 x 128 eight-phase tile, 2-3 % faster forward (r6s30)
-  if (use8 && a.N % 128 == 0 && a.Cin % 64 == 0 && a.tapmap == 0 && a.R * a.S > 1) return 22;
+  // 1x1 convolutions (opt-in DET_IGEMM8_1X1=1): in isolation the stride-2 gathers, K = 64 and
+  // K >= 2048 expansions gain 2-9 % on cfg 21 (profiles/r6_igemm8_conv1x1.jsonl), but in the step
+  // the bench reads 0.15 % lower with them than with the 3x3 convs alone (r6s35, three rounds)
+  static const bool use8_1x1 = [] {
+    const char* e = std::getenv("DET_IGEMM8_1X1");
+    return e && e[0] == '1';
+  }();
+  const bool one = a.R * a.S == 1;
+  const bool one8 = one && use8_1x1 && (a.stride == 2 || a.K == 64 || a.K >= 2048);
+  if (use8 && a.N % 256 == 0 && a.Cin % 64 == 0 && a.tapmap == 0 && (!one || one8)) return 21;
+  // 128-channel convolutions: the 512 x 128 eight-phase tile, 2-4 % faster forward (r6s30, r6s33)
+  if (use8 && a.N % 128 == 0 && a.N % 256 != 0 && a.Cin % 64 == 0 && a.tapmap == 0 && (!one || (use8_1x1 && a.K >= 512)))
+    return 22;
   if (a.N % 256 == 0 && a.Cin % 32 == 0) return 8;
   if (a.N % 128 == 0 && a.Cin % 64 == 0) return 2;
   return a.Cin % 32 == 0 ? 11 : 1;
