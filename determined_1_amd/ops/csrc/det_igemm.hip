@@ -1663,6 +1663,184 @@ __global__ void __launch_bounds__(WM * WN * 64, OCC) wgrad3_kernel(WgArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// wgrad8: the ring weight gradient (wgrad3, above) on the eight-phase ping-pong schedule of
+// det_gemm8.hip: a 256 (Cout) x 256 (R*S*Cin) tile, 8 waves of 128 x 64 in two staggered groups, K
+// tiles of 64 pixels held as four 16 KiB half-tiles (dY channels 0-127 / 128-255, im2col columns
+// 0-127 / 128-255), each half-tile two 32-pixel groups of two [32][64] sub-tiles in wgrad3's
+// transposed-read image.  P1 reads the wave's dY rows 0-63 and im2col columns 0-31 and issues
+// dY(t+1), P2 reads the rest, P3 computes, P4 issues im2col(t+2) and retires tile t+1.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512, 1) wgrad8_kernel(WgArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  constexpr int BM = 256, BN = 256, WN = 4, TM = 128, TN = 64, FM = 8, FN = 4;
+  constexpr int HALF = 16384, BUF = 4 * HALF;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = a.N / BM, ntn = a.RSC / BN, ntiles = ntm * ntn;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntiles, tile = bid - split * ntiles;
+  const int mt = tile / ntn, nt = tile - mt * ntn;
+  const int n0 = mt * BM, k0 = nt * BN;
+  const int64_t mbeg = static_cast<int64_t>(split) * a.rows_per_split;
+  int64_t mend = mbeg + a.rows_per_split;
+  if (mend > a.M) mend = a.M;
+  const int nk = mend > mbeg ? static_cast<int>((mend - mbeg + 63) / 64) : 0;
+
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.dY), 0, a.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(a.X), 0, a.x_bytes, 0x00020000);
+  constexpr unsigned kOOB = 0xFFFFFFF0u;
+
+  // this wave's pieces of every half-tile: sub-tile `sub`, pixel row `row` (of a 32-pixel group), two
+  // groups (pieces wid and wid + 8); the lane's 16-B chunk pre-swizzled for the transposed reads
+  const int q = wid;
+  const int sub = q >> 2, row = (q & 3) * 8 + (lane >> 3);
+  const int ch = (lane & 7) ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2));
+  int yoff[2];
+  int xc[2], xrr[2], xss[2], xn[2], xho[2], xwo[2];  // im2col half h: column state, pixel (group 0)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    yoff[h] = static_cast<int>(((mbeg + row) * a.N + n0 + h * 128 + sub * 64 + ch * 8) * 2);
+    const int k = k0 + h * 128 + sub * 64 + ch * 8;
+    const int tap = k / a.Cin;
+    xc[h] = k - tap * a.Cin;
+    xrr[h] = tap / a.S;
+    xss[h] = tap - xrr[h] * a.S;
+    const int64_t m = mbeg + row;
+    const int hw = a.Ho * a.Wo;
+    xn[h] = static_cast<int>(m / hw);
+    const int rem = static_cast<int>(m - static_cast<int64_t>(xn[h]) * hw);
+    xho[h] = rem / a.Wo;
+    xwo[h] = rem - xho[h] * a.Wo;
+  }
+  const int adv_h = 32 / a.Wo, adv_w = 32 - adv_h * a.Wo;
+  auto adv32 = [&](int& n, int& ho, int& wo) {
+    wo += adv_w;
+    const int carry = wo >= a.Wo;
+    wo -= carry ? a.Wo : 0;
+    ho += adv_h + carry;
+    while (ho >= a.Ho) {
+      ho -= a.Ho;
+      ++n;
+    }
+  };
+  auto xsrc = [&](int h, int n, int ho, int wo, bool valid) -> unsigned {
+    const int hi = ho * a.stride - a.pad + xrr[h], wi = wo * a.stride - a.pad + xss[h];
+    const bool ok = valid && hi >= 0 && hi < a.Hi && wi >= 0 && wi < a.Wi;
+    return ok ? static_cast<unsigned>((((n * a.Hi + hi) * a.Wi + wi) * a.Cin + xc[h]) * 2) : kOOB;
+  };
+  // half-tile ht (0/1 dY channel halves, 2/3 im2col column halves) of K tile kt; the im2col halves
+  // must be issued in increasing kt (their pixel state advances 64 per call)
+  auto stage = [&](int ht, int kt) {
+    unsigned char* dst = smem + (kt & 1) * BUF + ht * HALF + q * 1024;
+    const int64_t px0 = mbeg + static_cast<int64_t>(kt) * 64 + row;
+    if (ht < 2) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const bool valid = px0 + g * 32 < mend;
+        const unsigned v = valid ? static_cast<unsigned>(yoff[ht] + (kt * 64 + g * 32) * a.N * 2) : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(yr, (lds_void*)(dst + g * 8192), 16, v, 0, 0, 0);
+      }
+    } else {
+      const int h = ht - 2;
+      const unsigned v0 = xsrc(h, xn[h], xho[h], xwo[h], px0 < mend);
+      int n1 = xn[h], ho1 = xho[h], wo1 = xwo[h];
+      adv32(n1, ho1, wo1);
+      const unsigned v1 = xsrc(h, n1, ho1, wo1, px0 + 32 < mend);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)dst, 16, v0, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_void*)(dst + 8192), 16, v1, 0, 0, 0);
+      adv32(n1, ho1, wo1);
+      xn[h] = n1;
+      xho[h] = ho1;
+      xwo[h] = wo1;
+    }
+  };
+  auto phase_barrier = []() {
+    __builtin_amdgcn_sched_barrier(0);
+    block_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[FM][2], bfm[FN][2];
+  auto read_a = [&](int kt, int i0) {
+    const unsigned char* base = smem + (kt & 1) * BUF + wm * HALF;
+#pragma unroll
+    for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) af[i][g] = wtr_frag(base + g * 8192 + (i >> 2) * 4096, (i * 16) & 63, lane);
+  };
+  auto read_b = [&](int kt, int j0) {
+    const unsigned char* base = smem + (kt & 1) * BUF + (2 + (wn >> 1)) * HALF + (wn & 1) * 4096;
+#pragma unroll
+    for (int j = j0; j < j0 + 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) bfm[j][g] = wtr_frag(base + g * 8192, j * 16, lane);
+  };
+  auto mfma = [&](int i0, int j0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+        for (int j = j0; j < j0 + 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][g], bfm[j][g], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const bool late = wid >= 4;
+  if (nk > 0) {
+    stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+    if (nk > 1) { stage(2, 1); stage(3, 1); wait_vmcnt<4>(); } else wait_vmcnt<0>();
+  }
+  phase_barrier();
+  if (late) phase_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    read_a(t, 0);
+    read_b(t, 0);
+    if (n1) { stage(0, t + 1); stage(1, t + 1); }
+    phase_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mfma(0, 0);
+    phase_barrier();
+    read_a(t, 4);
+    read_b(t, 2);
+    phase_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mfma(0, 2);
+    phase_barrier();
+    phase_barrier();
+    mfma(4, 2);
+    phase_barrier();
+    if (n2) { stage(2, t + 2); stage(3, t + 2); wait_vmcnt<4>(); } else wait_vmcnt<0>();
+    phase_barrier();
+    mfma(4, 0);
+    phase_barrier();
+  }
+  if (!late) phase_barrier();
+
+  float* out = a.P + static_cast<int64_t>(split) * a.N * a.RSC;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wn * TN + j * 16 + (lane & 15);
+        out[static_cast<int64_t>(n) * a.RSC + k] = acc[i][j][r];
+      }
+#endif
+}
+
+// ------------------------------------------------------------------------------------------------
 // conv3p_wgrad: weight gradient of a 3x3 / stride-1 / pad-1 convolution on the halo patch.
 //   P[split][n][tap * Cin + c] = sum_{m in split} dY[m][n] . Xpad[patch(m) + off(tap)][c]
 // A 512-thread block owns one 64 (Cout) x 9 x 64 (Cin) tile of the weight gradient and a range of
@@ -2065,6 +2243,8 @@ constexpr WgCfg kWgCfgs[] = {
     {128, 64, 4, 1, 2},    // 11: 2 x 2 waves of 64 x 32, 64 pixels per stage
     {64, 192, 4, 1, 2},    // 12: cfg 1 at 64 pixels per stage
     {64, 64, 4, 1, 4},     // 13: cfg 9 at 128 pixels per stage
+    {256, 256, 8, 1, 2},   // 14: wgrad8 -- cfg 3's tile on the eight-phase schedule, 64 pixels per K tile
+                           //     (opt-in via DET_WGRAD_CFG: -2..-6 % at 256 channels, +1-2 % at 512, r6s36)
 };
 constexpr int kWgNumCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
 
@@ -2342,6 +2522,11 @@ int det_igemm_wgrad(void* stream, const void* dY, const void* X, void* out, int 
     case 11: launch_wg<128, 64, 2, 2, 1, 2>(st, a, nwg); break;
     case 12: launch_wg<64, 192, 1, 4, 1, 2>(st, a, nwg); break;
     case 13: launch_wg<64, 64, 2, 2, 1, 4>(st, a, nwg); break;
+    case 14: {
+      constexpr int smem = 2 * 4 * 16384;
+      hipLaunchKernelGGL(wgrad8_kernel, dim3(nwg), dim3(512), smem, st, a);
+      break;
+    }
     default: return -7;
   }
   const int rc = static_cast<int>(hipGetLastError());

@@ -97,10 +97,13 @@ WGRAD_SHAPES = [  # (Nb, Cin, H, W, Cout, R, stride, pad)
     (2, 256, 7, 7, 256, 3, 1, 1),      # Ho*Wo = 49 > 32: image carries inside a step
     (2, 128, 14, 14, 256, 1, 2, 0),    # 1x1 stride-2
     (4, 256, 7, 7, 64, 1, 1, 0),       # 1x1, N = 64
+    (3, 256, 10, 9, 256, 3, 2, 1),     # 256 x 256 tiles (wgrad8): stride 2, ragged K tail
+    (1, 512, 5, 7, 512, 3, 1, 1),      # 256 x 256 tiles, M = 35 < one K tile
+    (2, 256, 9, 9, 512, 1, 1, 0),      # 1x1, N = 512, RSC = 256
 ]
 
 
-@pytest.mark.parametrize("cfg", list(range(1, 14)))
+@pytest.mark.parametrize("cfg", list(range(1, 15)))
 @pytest.mark.parametrize("case", WGRAD_SHAPES)
 def test_ring_wgrad_every_cfg_exact(gpu, case, cfg):
     """det_igemm_wgrad (LDS-DMA ring + transposed reads) per tile configuration on small-integer
