@@ -92,6 +92,11 @@ __device__ __forceinline__ float gelu_epi(float z, int epi) {
 template <int MODE>
 __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  // MODE bits (schedule experiments, scripts/bench_gemm8.py): 1 paired staging (else balanced),
+  // 2 issue the phase's DMAs before its fragment reads, 4 no explicit lgkmcnt(0) before the MFMA
+  // cluster (the compiler's per-operand waits only), 8 no group stagger (both groups in lockstep)
+  constexpr bool kPaired = MODE & 1, kStageFirst = MODE & 2, kNoLgkm = MODE & 4, kNoStagger = MODE & 8;
+  constexpr bool kNoPrio = MODE & 16;  // 16: MFMA clusters at normal priority
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -160,7 +165,7 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
         bfm[j][kh] = *reinterpret_cast<const bf16x8*>(base + kh * 8192 + swz64((wc & 1) * 64 + j * 16 + fr, fch));
   };
   auto mfma = [&](int i0, int j0) {
-    __builtin_amdgcn_s_setprio(1);
+    if (!kNoPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -168,13 +173,15 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
 #pragma unroll
         for (int j = j0; j < j0 + 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kh], bfm[j][kh], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (!kNoPrio) __builtin_amdgcn_s_setprio(0);
   };
-  auto lgkm0 = [&]() { __builtin_amdgcn_s_waitcnt(0xC07F); };
+  auto lgkm0 = [&]() {
+    if (!kNoLgkm) __builtin_amdgcn_s_waitcnt(0xC07F);
+  };
 
   const int nk = g.K / 64;
   // prologue: tile 0 complete plus what the steady state expects in flight at tile 0's entry
-  if (MODE == 1) {
+  if (kPaired) {
     stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
     if (nk > 1) { stage(2, 1); stage(3, 1); wait_vmcnt<4>(); } else wait_vmcnt<0>();
   } else {
@@ -182,14 +189,15 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
     if (nk > 1) { stage(2, 1); wait_vmcnt<2>(); } else wait_vmcnt<0>();
   }
   barrier();
-  if (wr == 1) barrier();  // the late group: one barrier behind from here on
+  if (!kNoStagger && wr == 1) barrier();  // the late group: one barrier behind from here on
 
   for (int t = 0; t < nk; ++t) {
     const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
     // P1
+    if (kStageFirst && kPaired && n1) { stage(0, t + 1); stage(1, t + 1); }
     read_a(t, 0);
     read_b(t, 0);
-    if (MODE == 1) { if (n1) { stage(0, t + 1); stage(1, t + 1); } }
+    if (kPaired) { if (!kStageFirst && n1) { stage(0, t + 1); stage(1, t + 1); } }
     else { if (n1) stage(3, t + 1); }
     barrier();
     lgkm0();
@@ -198,19 +206,19 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
     // P2
     read_a(t, 4);
     read_b(t, 2);
-    if (MODE == 0 && n1) stage(0, t + 1);
+    if (!kPaired && n1) stage(0, t + 1);
     barrier();
     lgkm0();
     mfma(0, 2);
     barrier();
     // P3
-    if (MODE == 0 && n1) stage(1, t + 1);
+    if (!kPaired && n1) stage(1, t + 1);
     barrier();
     mfma(4, 2);
     barrier();
     // P4: restage this tile's buffer with B(t+2); then retire tile t+1 (everything older than the
     // B(t+2) pieces just issued)
-    if (MODE == 1) {
+    if (kPaired) {
       if (n2) { stage(2, t + 2); stage(3, t + 2); wait_vmcnt<4>(); } else wait_vmcnt<0>();
     } else {
       if (n2) { stage(2, t + 2); wait_vmcnt<2>(); } else wait_vmcnt<0>();
@@ -219,7 +227,7 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
     mfma(4, 0);
     barrier();
   }
-  if (wr == 0) barrier();  // the early group catches up: every wave has passed the same barriers
+  if (!kNoStagger && wr == 0) barrier();  // the early group catches up: every wave has passed the same barriers
   __syncthreads();
 
   // epilogue: C tile through LDS (bias added in fp32), 16-B row stores
@@ -264,12 +272,17 @@ __global__ void __launch_bounds__(kNT, 1) gemm8_kernel(G8Args g) {
 
 template <int MODE>
 int launch(hipStream_t st, const G8Args& a) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<MODE>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
+    if (e != hipSuccess) return static_cast<int>(e);
+    attr = true;
+  }
   const int64_t nwg = ((a.M + kBM - 1) / kBM) * ((a.N + kBN - 1) / kBN);
   hipLaunchKernelGGL((gemm8_kernel<MODE>), dim3(static_cast<unsigned>(nwg)), dim3(kNT), kSmem, st, a);
   return static_cast<int>(hipGetLastError());
 }
-
-bool g_attr_set[2] = {false, false};
 
 }  // namespace
 
@@ -291,16 +304,16 @@ int det_gemm8(void* stream, const void* A, const void* B, void* C, const void* b
            M, N, K, lda, ldb, ldc, bias ? bias_dt : 0, static_cast<unsigned>(ab), static_cast<unsigned>(bb),
            static_cast<unsigned short*>(C2), epi};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const int m = mode == 0 ? 0 : 1;
-  if (!g_attr_set[m]) {
-    hipError_t e = m == 0 ? hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<0>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, kSmem)
-                          : hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm8_kernel<1>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, kSmem);
-    if (e != hipSuccess) return static_cast<int>(e);
-    g_attr_set[m] = true;
+  switch (mode) {
+    case 0: return launch<0>(st, a);
+    case 3: return launch<3>(st, a);
+    case 5: return launch<5>(st, a);
+    case 7: return launch<7>(st, a);
+    case 9: return launch<9>(st, a);
+    case 21: return launch<21>(st, a);
+    case 23: return launch<23>(st, a);
+    default: return launch<1>(st, a);
   }
-  return m == 0 ? launch<0>(st, a) : launch<1>(st, a);
 }
 
 }  // extern "C"

@@ -45,6 +45,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=15)
     ap.add_argument("--only", default="")
+    ap.add_argument("--modes", default="0,1", help="det_gemm8 schedule variants (det_gemm8.hip MODE bits)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     for name, (m, n, k) in SHAPES.items():
@@ -56,7 +57,7 @@ def main() -> None:
         flop = 2.0 * m * n * k
         rec = {"shape": name, "M": m, "N": n, "K": k}
         rec["blas_us"] = round(timeit(lambda: torch.mm(a, b.t(), out=out), args.iters), 2)
-        for mode in (0, 1):
+        for mode in [int(x) for x in args.modes.split(",")]:
             rec[f"gemm8_m{mode}_us"] = round(timeit(lambda: gemm8(a, b, out=out, mode=mode), args.iters), 2)
         for key in [k_ for k_ in rec if k_.endswith("_us")]:
             rec[key.replace("_us", "_tfs")] = round(flop / rec[key] / 1e6, 1)
