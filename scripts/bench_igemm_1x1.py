@@ -33,13 +33,16 @@ def timeit(fn, iters=20):
 
 
 dev = torch.device("cuda")
+CFGS = [int(c) for c in os.environ.get("CFGS", "0,8,21,22").split(",")]
+STATS = os.environ.get("STATS", "1") == "1"
 for cin, cout, h, st in SHAPES:
     x = torch.randn(NB, cin, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(cout, cin, 1, 1, device=dev) / cin ** 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     r = {"cin": cin, "cout": cout, "h": h, "stride": st}
-    for cfg in (0, 8, 21, 22):
+    r["stats"] = STATS
+    for cfg in CFGS:
         try:
-            r[f"cfg{cfg}_ms"] = round(timeit(lambda: conv.igemm_conv(x, w, stride=st, pad=0, stats=True, cfg=cfg)), 4)
+            r[f"cfg{cfg}_ms"] = round(timeit(lambda: conv.igemm_conv(x, w, stride=st, pad=0, stats=STATS, cfg=cfg)), 4)
         except RuntimeError as e:
             r[f"cfg{cfg}_ms"] = None
     print(json.dumps(r), flush=True)
