@@ -164,7 +164,7 @@ _SIGNATURES = {
     "det_blaslt_init": ([ctypes.c_char_p], c_int),
     # stream, transa, transb, m, n, k, A, lda, B, ldb, D, ldd, bias, beta, dtype, ws, ws_bytes
     "det_blaslt_gemm": ([c_void_p, c_int, c_int, c_i64, c_i64, c_i64, c_void_p, c_i64, c_void_p, c_i64, c_void_p, c_i64,
-                         c_void_p, ctypes.c_float, c_int, c_void_p, c_i64], c_int),
+                         c_void_p, ctypes.c_float, c_int, c_void_p, c_i64, c_int], c_int),
     # stream, A, B, C, M, N, K, scale, shift, pmean, pm2, Ho, Wo, Hi, Wi
     # ... + res, aout, abits, res_scale, res_shift
     "det_conv_nt": ([c_void_p] * 4 + [c_i64, c_int, c_int] + [c_void_p] * 4 + [c_int] * 4 + [c_void_p] * 5, c_int),

@@ -12,7 +12,9 @@
 // RTLD_NOLOAD and resolved with dlsym), so there is one hipBLASLt and one HIP runtime in the process.
 //
 // BLAS convention (column-major): D[m, n] = alpha * op(A) . op(B) + beta * C (C = D), optional
-// per-row bias added in the epilogue (HIPBLASLT_EPILOGUE_BIAS: one rounding into D).
+// per-row bias added in the epilogue (HIPBLASLT_EPILOGUE_BIAS: one rounding into D), or (bias_mode 2)
+// the bias gradient of B written by the epilogue (HIPBLASLT_EPILOGUE_BGRADB: bias[n] = sum_k op(B)[k, n],
+// a Linear's db from its weight-gradient GEMM instead of a separate column-sum pass).
 
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
@@ -47,10 +49,11 @@ struct Plan {
   hipblasLtMatmulAlgo_t algo;
   size_t ws;
   bool bias;
+  int bias_mode;
 };
 
-// (device, transa, transb, m, n, k, lda, ldb, ldd, bias, beta != 0, dtype).  The plan is only used
-// with 16-B aligned operands (ops/transformer.py _bl_ok), so alignment needs no key field.
+// (device, transa, transb, m, n, k, lda, ldb, ldd, bias mode, beta != 0, dtype).  The plan is only
+// used with 16-B aligned operands (ops/transformer.py _bl_ok), so alignment needs no key field.
 typedef std::tuple<int, int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int, int> Key;
 std::map<Key, Plan> g_plans;
 
@@ -88,15 +91,17 @@ int det_blaslt_init(const char* path) {
 }
 
 // D = op(A) op(B) [+ bias per row of D] [+ beta * D].  transa / transb: 0 = N, 1 = T.  dtype 1 =
-// bf16 operands and output (fp32 accumulate), 0 = fp32.  bias (nullable) has D's dtype.
-// ws: device workspace of ws_bytes.  Returns 0, or a negative code / hipblasStatus_t on failure.
+// bf16 operands and output (fp32 accumulate), 0 = fp32.  bias (nullable) has D's dtype; bias_mode
+// 2 makes it an OUTPUT: the bias gradient of B (length n).  ws: device workspace of ws_bytes.
+// Returns 0, or a negative code / hipblasStatus_t on failure (-14: no algorithm for this epilogue).
 int det_blaslt_gemm(void* stream, int transa, int transb, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
                     const void* B, int64_t ldb, void* D, int64_t ldd, const void* bias, float beta, int dtype, void* ws,
-                    int64_t ws_bytes) {
+                    int64_t ws_bytes, int bias_mode) {
   if (!g_api.ok) return -10;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -16;
-  const Key key{dev, transa, transb, m, n, k, lda, ldb, ldd, bias != nullptr, beta != 0.f, dtype};
+  const int bmode = bias == nullptr ? 0 : (bias_mode == 2 ? 2 : 1);
+  const Key key{dev, transa, transb, m, n, k, lda, ldb, ldd, bmode, beta != 0.f, dtype};
   Plan p;
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -108,8 +113,9 @@ int det_blaslt_gemm(void* stream, int transa, int transb, int64_t m, int64_t n, 
       g_api.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
       g_api.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
       p.bias = bias != nullptr;
+      p.bias_mode = bmode;
       if (p.bias) {
-        const uint32_t epi = HIPBLASLT_EPILOGUE_BIAS;
+        const uint32_t epi = bmode == 2 ? HIPBLASLT_EPILOGUE_BGRADB : HIPBLASLT_EPILOGUE_BIAS;
         const int32_t bt = dt;
         g_api.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
         g_api.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));

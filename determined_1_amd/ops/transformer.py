@@ -147,7 +147,7 @@ class SharedWeightGrads:
     def accumulate(self, weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> Optional[torch.Tensor]:
         st = self._state[id(weight)]
         if st[1] is None:
-            st[1] = _weight_grad(weight, dz, x2)
+            st[1] = _weight_grad(weight, dz, x2)[0]
         elif _bl_ok(dz, x2, st[1]):
             _bl_wgrad(dz, x2, st[1].view(dz.shape[1], x2.shape[1]), beta=1.0)
         else:
@@ -241,28 +241,53 @@ def _bl_ok(*ts: torch.Tensor) -> bool:
 
 
 def _bl_gemm(ta: int, tb: int, m: int, n: int, k: int, A: torch.Tensor, lda: int, B: torch.Tensor, ldb: int,
-             D: torch.Tensor, ldd: int, bias: Optional[torch.Tensor] = None, beta: float = 0.0) -> None:
-    """Column-major D[m, n] = op(A) op(B) [+ bias per row] [+ beta D] (see det_blaslt.hip)."""
+             D: torch.Tensor, ldd: int, bias: Optional[torch.Tensor] = None, beta: float = 0.0,
+             bias_grad: bool = False) -> int:
+    """Column-major D[m, n] = op(A) op(B) [+ bias per row] [+ beta D] (see det_blaslt.hip); with
+    ``bias_grad`` the epilogue instead WRITES bias[n] = sum_k op(B)[k, n] (returns the library code,
+    non-zero when no algorithm supports that epilogue, instead of raising)."""
     dev = D.device.index
     stream = torch._C._cuda_getCurrentRawStream(dev)
     rc = _BL["fn"](stream, ta, tb, m, n, k, A.data_ptr(), lda, B.data_ptr(), ldb,
                    D.data_ptr(), ldd, None if bias is None else bias.data_ptr(), beta, _BL_DT[D.dtype],
-                   _BL["ws"][(dev, stream)].data_ptr(), _BL_WS_BYTES)
-    if rc != 0:
+                   _BL["ws"][(dev, stream)].data_ptr(), _BL_WS_BYTES, 2 if bias_grad else 1)
+    if rc != 0 and not bias_grad:
         _lib.check(rc, "det_blaslt_gemm")
+    return rc
 
 
-def _bl_wgrad(dz: torch.Tensor, x2: torch.Tensor, out: torch.Tensor, beta: float = 0.0) -> torch.Tensor:
-    """out[N, K] (+)= dz[M, N]^T x2[M, K]."""
+# Linear bias gradients from the weight-gradient GEMM's epilogue (hipBLASLt BGRADB) instead of a
+# two-launch column sum; shapes whose plan has no such algorithm fall back (remembered here).
+# Opt-in (DET_BGRAD_EPILOGUE=1): the BERT graph step measured the same either way (1,514-1,527 vs
+# 1,516-1,522 examples/s, profiles/r6_bert_bgrad_epilogue_ab.jsonl) -- the epilogue plan's GEMM costs
+# what the column sum saved.
+BGRAD_EPILOGUE = os.environ.get("DET_BGRAD_EPILOGUE", "0") == "1"
+_BGRAD_UNSUPPORTED = set()  # type: set
+LINEAR_BGRAD_COUNTS = {"epilogue": 0, "colsum": 0}
+
+
+def _bl_wgrad(dz: torch.Tensor, x2: torch.Tensor, out: torch.Tensor, beta: float = 0.0,
+              db: Optional[torch.Tensor] = None) -> bool:
+    """out[N, K] (+)= dz[M, N]^T x2[M, K]; with ``db`` [N] also db = column sums of dz from the
+    same GEMM when the library supports it.  Returns whether db was written."""
     M, N = dz.shape
     K = x2.shape[1]
+    key = (M, N, K, dz.dtype, beta != 0.0)
+    if db is not None and BGRAD_EPILOGUE and key not in _BGRAD_UNSUPPORTED:
+        if _bl_gemm(0, 1, K, N, M, x2, K, dz, N, out, K, bias=db, beta=beta, bias_grad=True) == 0:
+            LINEAR_BGRAD_COUNTS["epilogue"] += 1
+            return True
+        _BGRAD_UNSUPPORTED.add(key)
     _bl_gemm(0, 1, K, N, M, x2, K, dz, N, out, K, beta=beta)
-    return out
+    return False
 
 
-def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor,
+                 db: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, bool]:
     """dW = dz^T x, written straight into the parameter's gradient-arena slot when that is where
-    it will land (ops.arena.landing_buffer): no separate landing copy for the largest gradients."""
+    it will land (ops.arena.landing_buffer): no separate landing copy for the largest gradients.
+    With ``db``: also the bias gradient from the GEMM epilogue where the library path allows it;
+    returns (dW, whether db was written)."""
     buf = landing_buffer(weight) if weight.is_cuda else None
     if _native_linear(x2, weight, wgrad=True) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
         from determined_1_amd.ops.conv import conv1x1_wgrad
@@ -271,19 +296,23 @@ def _weight_grad(weight: torch.Tensor, dz: torch.Tensor, x2: torch.Tensor) -> to
             else torch.empty(weight.shape, dtype=weight.dtype, device=weight.device)
         conv1x1_wgrad(dz, x2, out.view(weight.shape[0], -1))
         LINEAR_COUNTS["native_wgrad"] += 1
-        return out
+        return out, False
     if _bl_ok(dz, x2):
         out = buf if (buf is not None and buf.dtype == dz.dtype and buf.is_contiguous()) else \
             torch.empty(weight.shape, dtype=dz.dtype, device=dz.device)
-        return _bl_wgrad(dz, x2, out.view(dz.shape[1], x2.shape[1])).view(weight.shape)
+        done = _bl_wgrad(dz, x2, out.view(dz.shape[1], x2.shape[1]), db=db)
+        return out.view(weight.shape), done
     if buf is not None and buf.dtype == dz.dtype and buf.is_contiguous():
-        return torch.mm(dz.t(), x2, out=buf)
-    return dz.t() @ x2
+        return torch.mm(dz.t(), x2, out=buf), False
+    return dz.t() @ x2, False
 
 
 def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_x: bool, need_w: bool,
-                 acc: Optional[SharedWeightGrads] = None, dr: Optional[torch.Tensor] = None):
-    """dr: a gradient of x2 from another use (ResidualGradLink), summed into dx by the GEMM."""
+                 acc: Optional[SharedWeightGrads] = None, dr: Optional[torch.Tensor] = None,
+                 db: Optional[torch.Tensor] = None):
+    """dr: a gradient of x2 from another use (ResidualGradLink), summed into dx by the GEMM.  db: a
+    bias-gradient buffer the weight-gradient GEMM may fill from its epilogue; the third result says
+    whether it did."""
     if dr is not None and not need_x:
         raise RuntimeError("a linked residual gradient reached a Linear whose input needs no gradient")
     if need_x and _native_linear(x2, weight) and dz.dtype == torch.bfloat16 and dz.is_contiguous():
@@ -314,9 +343,13 @@ def _mm_backward(dz: torch.Tensor, x2: torch.Tensor, weight: torch.Tensor, need_
         if dr is not None:
             dx = dx + dr.view(dx.shape)
     dw = None
+    db_done = False
     if need_w:
-        dw = acc.accumulate(weight, dz, x2) if acc is not None else _weight_grad(weight, dz, x2)
-    return dx, dw
+        if acc is not None:
+            dw = acc.accumulate(weight, dz, x2)
+        else:
+            dw, db_done = _weight_grad(weight, dz, x2, db)
+    return dx, dw, db_done
 
 
 def _track(acc: Optional[SharedWeightGrads], weight: torch.Tensor) -> Optional[SharedWeightGrads]:
@@ -386,15 +419,17 @@ class _Linear(torch.autograd.Function):
         x2, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, weight.shape[0]).contiguous()
         dr = ctx.link.take() if ctx.link is not None else None
-        dx, dw = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc, dr)
-        db = None
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        db = torch.empty(dy2.shape[1], dtype=dy2.dtype, device=dy2.device) if want_db else None
+        dx, dw, db_done = _mm_backward(dy2, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc, dr,
+                                       db=db)
+        if want_db and not db_done:
             lib = _lib.get_lib()
             rows, C = dy2.shape
-            db = torch.empty(C, dtype=dy2.dtype, device=dy2.device)
             ws = torch.empty(int(lib.det_tf_col_ws_elems(rows, C)), dtype=torch.float32, device=dy2.device)
             _lib.check(lib.det_tf_colsum(_stream(dy2), _DT[dy2.dtype], dy2.data_ptr(), rows, C, db.data_ptr(),
                                          ws.data_ptr()), "det_tf_colsum")
+            LINEAR_BGRAD_COUNTS["colsum"] += 1
         return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None
 
 
@@ -432,7 +467,7 @@ class _LinearGELU(torch.autograd.Function):
         _lib.check(lib.det_tf_gelu_bwd(_stream(z), _DT[z.dtype], da2.data_ptr(), z.data_ptr(), dz.data_ptr(), rows, C,
                                        _ptr(db), ws.data_ptr(), ctx.approx), "det_tf_gelu_bwd")
         dr = ctx.link.take() if ctx.link is not None else None
-        dx, dw = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc, dr)
+        dx, dw, _ = _mm_backward(dz, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc, dr)
         return (dx.view(ctx.xshape) if dx is not None else None), dw, db, None, None, None
 
 
@@ -492,8 +527,8 @@ class _LinearDropAddLN(torch.autograd.Function):
             need_bias=ctx.has_bias and ctx.needs_input_grad[2])
         if ctx.link is not None and dr is not None:
             ctx.link.dr, dr = dr, None
-        dx, dw = (_mm_backward(dh, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
-                  if need_h else (None, None))
+        dx, dw, _ = (_mm_backward(dh, x2, weight, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.acc)
+                     if need_h else (None, None, False))
         return ((dx.view(ctx.xshape) if dx is not None else None), dw, dbias,
                 (dr.view(ctx.rshape) if dr is not None else None), dgamma, dbeta, None, None, None, None)
 

@@ -23,7 +23,7 @@ def test_linked_residual_grad_kept_on_library_branch(monkeypatch):
     dz, x2, w = torch.randn(M, N), torch.randn(M, K), torch.randn(N, K)
     dr = torch.randn(K, M).t()  # [M, K], not contiguous: skips the beta = 1 branch
     assert not dr.is_contiguous()
-    dx, dw = T._mm_backward(dz, x2, w, True, False, None, dr)
+    dx, dw, _ = T._mm_backward(dz, x2, w, True, False, None, dr)
     torch.testing.assert_close(dx, dz @ w + dr)
     assert dw is None
 

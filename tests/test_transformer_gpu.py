@@ -374,3 +374,33 @@ def test_blaslt_plans_match_torch_gemms(gpu, dt):
     close(dw, (dz.t() @ x).float())
     tfops._bl_wgrad(dz, x, dw, beta=1.0)
     close(dw, 2 * (dz.float().t() @ x.float()))
+
+
+@pytest.mark.parametrize("rows,K,N", [(4608, 768, 2304), (333, 128, 192)])
+def test_linear_bias_grad_from_gemm_epilogue(gpu, monkeypatch, rows, K, N):
+    """ops.transformer.linear's bias gradient from the weight-gradient GEMM's epilogue (hipBLASLt
+    BGRADB) equals the column sums of dy (the separate det_tf_colsum pass it replaces); a shape the
+    library cannot do that for falls back to the column sum, counted either way."""
+    monkeypatch.setattr(tfops, "NATIVE_LINEAR", False)
+    g = torch.Generator().manual_seed(rows + N)
+    x = torch.randn(rows, K, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, generator=g).to(torch.bfloat16)
+    dy = torch.randn(rows, N, generator=g).to(torch.bfloat16)
+    res = {}
+    for on in (False, True):
+        monkeypatch.setattr(tfops, "BGRAD_EPILOGUE", on)
+        before = dict(tfops.LINEAR_BGRAD_COUNTS)
+        xd, wd, bd = _leaf(x, gpu), _leaf(w, gpu), _leaf(b, gpu)
+        tfops.linear(xd, wd, bd).backward(dy.to(gpu))
+        used = tfops.LINEAR_BGRAD_COUNTS["epilogue"] - before["epilogue"]
+        assert used + tfops.LINEAR_BGRAD_COUNTS["colsum"] - before["colsum"] == 1
+        if not on:
+            assert used == 0
+        res[on] = (bd.grad.float().cpu(), wd.grad.float().cpu(), xd.grad.float().cpu())
+    ref = dy.float().sum(0)
+    torch.testing.assert_close(res[True][0], ref, rtol=2e-2, atol=0.5)
+    torch.testing.assert_close(res[False][0], ref, rtol=2e-2, atol=0.5)
+    # the epilogue plan may use another algorithm (accumulation order) for the weight gradient
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=2e-2, atol=2e-2 * float(res[False][1].abs().max()))
+    assert torch.equal(res[True][2], res[False][2])
