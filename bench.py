@@ -62,10 +62,14 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--no-native-conv1x1", action="store_true", help="1x1 convs on MIOpen instead of det_conv GEMMs (A/B)")
     ap.add_argument("--no-native-stem", action="store_true", help="7x7 stem conv on MIOpen instead of det_conv (A/B)")
     ap.add_argument("--no-native-conv3x3", action="store_true", help="3x3 convs on MIOpen instead of det_igemm (A/B)")
-    ap.add_argument("--no-hip-graph", action="store_true",
-                    help="run every step eagerly (A/B).  By default a 1-GPU run replays the step from a hipGraph "
-                         "(pytorch/_graph.py; bitwise equal to eager, tests/test_graph_memset_gpu.py); multi-GPU "
-                         "runs keep DET_STEP_TIMERS on, which keeps their steps eager")
+    ap.add_argument("--hip-graph", action="store_true",
+                    help="1-GPU runs: replay the step from a hipGraph (pytorch/_graph.py; bitwise equal to eager, "
+                         "tests/test_graph_memset_gpu.py).  Off by default: the eager step overlaps the conv weight "
+                         "gradients on a side stream (ops/arena.py side_work) and that beats the graph replay, which "
+                         "runs the two branches one after the other on this runtime (12,96-13,18k vs 12,74-12,89k, "
+                         "profiles/r6_wgrad_side_stream_ab.jsonl).  Multi-GPU runs keep DET_STEP_TIMERS on, which "
+                         "keeps their steps eager either way")
+    ap.add_argument("--no-hip-graph", action="store_true", help="(kept for old command lines: the default now)")
     ap.add_argument("--bn-prologue", action="store_true",
                     help="apply bottleneck bn2 in conv3's GEMM prologue instead of materialising it (A/B)")
     ap.add_argument("--cudnn-benchmark", type=int, default=int(os.environ.get("DET_BENCH_CUDNN_BENCHMARK", "1")),
@@ -208,7 +212,7 @@ def main() -> None:
             "image_size": args.image_size,
         },
         "resources": {"slots_per_trial": world},
-        "optimizations": {"tensor_fusion_threshold": args.bucket_mb, "hip_graph": world == 1 and not args.no_hip_graph},
+        "optimizations": {"tensor_fusion_threshold": args.bucket_mb, "hip_graph": world == 1 and args.hip_graph and not args.no_hip_graph},
         "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": args.steps}},
         "scheduling_unit": args.steps,
     }
@@ -257,6 +261,9 @@ def main() -> None:
     ctrl = make_controller(ResNetImageNetTrial, config, stream(), trial_seed=1234)
     timing["ctrl_built"] = time.perf_counter()
     ctrl.run()
+    from determined_1_amd.ops import arena
+
+    side_wgrad = {"on": arena.SIDE_WGRAD, **arena.SIDE_COUNTS}
     if args.params_out and int(os.environ.get("RANK", "0")) == 0:
         ps = [p.detach().double() for p in ctrl.context.models[0].parameters()]
         torch.save({"sums": torch.stack([p.sum() for p in ps]).cpu(), "norms": torch.stack([p.norm() for p in ps]).cpu(),
@@ -311,6 +318,7 @@ def main() -> None:
                 "startup_s": round(timing.get("ctrl_built", 0.0) - t_start, 1),
                 "miopen_find_db": os.environ.get("MIOPEN_USER_DB_PATH"),
                 "hip_graph": getattr(getattr(ctrl, "_graph", None), "stats", lambda: None)(),
+                "wgrad_side_stream": side_wgrad,
             },
         }
         if phases:  # DET_STEP_TIMERS=1: per-batch device phases of the timed window (forward/backward/comm/opt)

@@ -13,6 +13,7 @@ from typing import NamedTuple, Optional, Tuple
 import torch
 
 from determined_1_amd.ops import _lib
+from determined_1_amd.ops.arena import side_work
 from determined_1_amd.ops.functional import is_gpu
 
 Gather = Tuple[int, int, int, int]  # (Ho, Wo, Hi, Wi) of a 1x1 stride-2 conv
@@ -20,6 +21,23 @@ Gather = Tuple[int, int, int, int]  # (Ho, Wo, Hi, Wi) of a 1x1 stride-2 conv
 
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _wgrad_target(weight: torch.Tensor, needed: bool, gpu: bool,
+                  memory_format: torch.memory_format = torch.contiguous_format) -> Tuple[Optional[torch.Tensor], bool]:
+    """(dw, side) for a conv weight gradient: the parameter's arena slot when its GradSink offers
+    one (arena.landing_buffer), else a fresh tensor; ``side`` = the gradient may be computed on the
+    side stream (arena.side_work: only into the arena slot, whose readers all join first)."""
+    if not needed:
+        return None, False
+    from determined_1_amd.ops import arena
+
+    buf = arena.landing_buffer(weight)
+    if buf is not None and buf.is_contiguous(memory_format=memory_format) and \
+            buf.dtype in (torch.bfloat16, torch.float32):
+        return buf, arena.SIDE_WGRAD and gpu and buf.dtype == weight.dtype
+    dt = weight.dtype if weight.dtype in (torch.bfloat16, torch.float32) else torch.float32
+    return torch.empty(weight.shape, dtype=dt, device=weight.device, memory_format=memory_format), False
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -751,6 +769,11 @@ class _Conv1x1(torch.autograd.Function):
         if pend is not None:  # dY = the deferred BN apply, computed in the dgrad's A staging into dy2
             d, bx, coef = pend
             abn = (d.permute(0, 2, 3, 1).reshape(-1, cout), bx, coef, dy2)
+        dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dy2))
+        if side and pend is None:  # independent of the dgrad: fork before it
+            with side_work(True, dy2, x2):
+                conv1x1_wgrad(dy2, x2, dw.view(cout, c))
+            side = None
         if ctx.needs_input_grad[0]:
             w2 = weight.reshape(cout, c).to(torch.bfloat16).contiguous()
             dx2 = _fused_bn_dgrad(prod, dy2, w2, n * h * w_, c, abn) if (prod is not None and is_gpu(dy2)) else None
@@ -763,16 +786,9 @@ class _Conv1x1(torch.autograd.Function):
             if abn is not None:
                 BN_APPLY_COUNTS["in_gemm"] += 1
             dx = dx2.view(n, h, w_, c).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
-            from determined_1_amd.ops.arena import landing_buffer
-
-            buf = landing_buffer(weight)
-            if buf is not None and buf.is_contiguous() and buf.dtype in (torch.bfloat16, torch.float32):
-                dw = buf
-            else:
-                dw = torch.empty(weight.shape, dtype=weight.dtype if weight.dtype in (torch.bfloat16, torch.float32)
-                                 else torch.float32, device=weight.device)
-            conv1x1_wgrad(dy2, x2, dw.view(cout, c))
+        if dw is not None and side is not None:
+            with side_work(side, dy2, x2):
+                conv1x1_wgrad(dy2, x2, dw.view(cout, c))
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         return dx, dw, None, None, None
@@ -889,6 +905,17 @@ class _ConvRS(torch.autograd.Function):
         cout, cin, r, s = weight.shape
         dyc = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
+        # auto: the ring at >= 128 channels (at 128 a tie with MIOpen, 0.224 / 0.253 ms at stride 1 / 2,
+        # profiles/r4_conv3x3_microbench.jsonl, and no library launch), the halo patch for the stride-1
+        # 3x3 at 64 channels
+        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 128) or \
+            (WGRAD_RS_MODE == "auto" and conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc))
+        side = False
+        if native_wgrad:
+            dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dyc), torch.channels_last)
+            if side:  # fork before the input gradient: the two only share dY
+                with side_work(True, dyc, x):
+                    _native_wgrad_rs(dyc, x, dw, stride, pad)
         if ctx.needs_input_grad[0]:
             if stride == 1 and 2 * pad == r - 1 and r == s:
                 wd = dgrad_weight(weight)
@@ -916,38 +943,30 @@ class _ConvRS(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
                 CONV3X3_COUNTS["dgrad_miopen"] += 1
-        # auto: the ring at >= 128 channels (at 128 a tie with MIOpen, 0.224 / 0.253 ms at stride 1 / 2,
-        # profiles/r4_conv3x3_microbench.jsonl, and no library launch), the halo patch for the stride-1
-        # 3x3 at 64 channels
-        native_wgrad = WGRAD_RS_MODE == "native" or (WGRAD_RS_MODE == "auto" and WGRAD_RING and cin >= 128) or \
-            (WGRAD_RS_MODE == "auto" and conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc))
         if ctx.needs_input_grad[1] and not native_wgrad:
             wb = weight.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             gw = torch.ops.aten.convolution_backward(dyc, x, wb, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [False, True, False])[1]
             dw = gw.to(weight.dtype)
             CONV3X3_COUNTS["wgrad_miopen"] += 1
-        elif ctx.needs_input_grad[1]:
-            from determined_1_amd.ops.arena import landing_buffer
-
-            buf = landing_buffer(weight)
-            if buf is not None and buf.is_contiguous(memory_format=torch.channels_last) and \
-                    buf.dtype in (torch.bfloat16, torch.float32):
-                dw = buf
-                out = buf.permute(0, 2, 3, 1).reshape(cout, -1)  # KRSC view of channels_last memory
-            else:
-                dt = weight.dtype if weight.dtype in (torch.bfloat16, torch.float32) else torch.float32
-                dw = torch.empty(weight.shape, dtype=dt, device=weight.device, memory_format=torch.channels_last)
-                out = dw.permute(0, 2, 3, 1).reshape(cout, -1)
-            assert out.data_ptr() == dw.data_ptr() and out.is_contiguous()
-            if not (conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc) and x.data_ptr() % 16 == 0
-                    and conv3p_wgrad(dyc, x, out)):
-                conv_wgrad(dyc, x, out, r, s, stride, pad)
-            CONV3X3_COUNTS["wgrad_native"] += 1
+        elif dw is not None and not side:
+            _native_wgrad_rs(dyc, x, dw, stride, pad)
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         ctx.bn_producer = None
         return dx, dw, None, None, None, None
+
+
+def _native_wgrad_rs(dyc: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, stride: int, pad: int) -> None:
+    """R x S weight gradient into channels_last ``dw``: the 64-channel halo patch kernel where it
+    applies, else the det_igemm wgrad ring / gathered gemm_tn."""
+    cout, cin, r, s = dw.shape
+    out = dw.permute(0, 2, 3, 1).reshape(cout, -1)  # KRSC view of channels_last memory
+    assert out.data_ptr() == dw.data_ptr() and out.is_contiguous()
+    if not (conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc) and x.data_ptr() % 16 == 0
+            and conv3p_wgrad(dyc, x, out)):
+        conv_wgrad(dyc, x, out, r, s, stride, pad)
+    CONV3X3_COUNTS["wgrad_native"] += 1
 
 
 def conv_rs(x: torch.Tensor, conv_mod: torch.nn.Conv2d, stats: bool = True, bn_exclusive: bool = False) -> torch.Tensor:
@@ -1275,7 +1294,12 @@ class _Shortcut1x1(torch.autograd.Function):
             materialize_pending_apply(dy, pend)
             pend = None
         dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
-        dx = dw = None
+        dx = None
+        dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dy2))
+        if side and pend is None:  # independent of the dgrad: fork before it
+            with side_work(True, dy2, x):
+                _shortcut_wgrad(dy2, x, dw, st, g)
+            side = None
         if ctx.needs_input_grad[0] or link is not None:
             w2 = weight.reshape(cout, c)
             w2 = (w2 if w2.dtype == torch.bfloat16 else w2.to(torch.bfloat16)).contiguous()
@@ -1292,26 +1316,26 @@ class _Shortcut1x1(torch.autograd.Function):
                 hand_linked_grad(link, extra)
             else:
                 dx = full_res_grad(extra)
-        if ctx.needs_input_grad[1]:
-            from determined_1_amd.ops.arena import landing_buffer
-
-            buf = landing_buffer(weight)
-            if buf is not None and buf.is_contiguous() and buf.dtype in (torch.bfloat16, torch.float32):
-                dw = buf
-            else:
-                dw = torch.empty(weight.shape, dtype=weight.dtype if weight.dtype in (torch.bfloat16, torch.float32)
-                                 else torch.float32, device=weight.device)
-            if st == 2 and WGRAD_RING and int(_lib.get_lib().det_igemm_wgrad_ws_elems(dy2.shape[0], cout, c, 0)) > 0:
-                # stride 2: the ring's strided im2col beats the gathered gemm_tn on all three ResNet-50
-                # projections (0.209 / 0.185 / 0.243 vs 0.228 / 0.208 / 0.316 ms,
-                # profiles/r3_shortcut_microbench.jsonl); stride 1 stays on gemm_tn (0.188 vs 0.243)
-                dyc = dy2.view(n, ho, wo, cout).permute(0, 3, 1, 2)
-                conv_wgrad(dyc, x, dw.view(cout, c), 1, 1, 2, 0)
-            else:
-                conv1x1_wgrad(dy2, x.permute(0, 2, 3, 1).reshape(-1, c), dw.view(cout, c), gather=g)
+        if dw is not None and side is not None:
+            with side_work(side, dy2, x):
+                _shortcut_wgrad(dy2, x, dw, st, g)
             if dw.dtype != weight.dtype:
                 dw = dw.to(weight.dtype)
         return dx, dw, None, None, None
+
+
+def _shortcut_wgrad(dy2: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, st: int, g: Optional[Gather]) -> None:
+    n, c = x.shape[0], x.shape[1]
+    cout = dw.shape[0]
+    if st == 2 and WGRAD_RING and int(_lib.get_lib().det_igemm_wgrad_ws_elems(dy2.shape[0], cout, c, 0)) > 0:
+        # stride 2: the ring's strided im2col beats the gathered gemm_tn on all three ResNet-50
+        # projections (0.209 / 0.185 / 0.243 vs 0.228 / 0.208 / 0.316 ms,
+        # profiles/r3_shortcut_microbench.jsonl); stride 1 stays on gemm_tn (0.188 vs 0.243)
+        ho, wo = g[0], g[1]
+        dyc = dy2.view(n, ho, wo, cout).permute(0, 3, 1, 2)
+        conv_wgrad(dyc, x, dw.view(cout, c), 1, 1, 2, 0)
+    else:
+        conv1x1_wgrad(dy2, x.permute(0, 2, 3, 1).reshape(-1, c), dw.view(cout, c), gather=g)
 
 
 def shortcut_conv1x1(x: torch.Tensor, conv_mod: torch.nn.Conv2d, link=None, stats: bool = True) -> torch.Tensor:

@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from determined_1_amd import check, constants, errors, trial
 from determined_1_amd.ops import functional as F
-from determined_1_amd.ops.arena import GradSink
+from determined_1_amd.ops.arena import GradSink, join_side_work
 from determined_1_amd.ops.optim import FusedOptimizer, fused_kind
 from determined_1_amd.parallel import dist as pdist
 from determined_1_amd.parallel.ddp import GradientBucketer, broadcast_arenas, broadcast_tensors_coalesced
@@ -306,6 +306,7 @@ class PyTorchTrialContext(trial.TrialContext):
 
             gradient = seed_grad.unit_for(loss)  # a shared constant instead of a per-backward fill
         loss.backward(gradient=gradient, retain_graph=retain_graph, create_graph=create_graph)  # type: ignore
+        join_side_work()
         self._timers.backward_end()
         for st in self._opt_states:
             if st.fused is not None and st.fused.sink is not None:

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-6 session 48: the whole GPU suite with the side-stream weight gradients on by default,
+# smoke(), bench.py (defaults: eager + side stream) twice, and a kernel-trace profile of it.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r6s48
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_suite.log 2>&1
+rc=$?; tail -2 $O/gpu_suite.log; grep -E "FAILED|ERROR" $O/gpu_suite.log | head -30
+grep -q -E "Fatal Python|Segmentation fault" $O/gpu_suite.log && exit 3
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; echo "smoke rc=$?"; tail -1 $O/smoke.log
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py > $O/bench$i.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+  echo "bench: $(cut -c1-150 $O/bench$i.json)"
+done
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 20 --warmup 10 \
+  > $O/prof.log 2>&1 || { echo "prof rc=$?"; tail -20 $O/prof.log; exit 1; }
+find $O/prof -name "*stats*" | head

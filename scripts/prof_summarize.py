@@ -59,9 +59,20 @@ def main() -> None:
         agg[short(n)][1] += 1
         busy += e - s
     wall = rows[hi][1] - rows[lo][1]
+    # time with at least one kernel running: with kernels on two streams (side-stream weight
+    # gradients) the per-kernel sum exceeds the wall and each overlapped kernel runs slower
+    occupied, cur_s, cur_e = 0, None, None
+    for s, e, _ in sorted(win):
+        if cur_e is None or s > cur_e:
+            occupied += 0 if cur_e is None else cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    occupied += 0 if cur_e is None else cur_e - cur_s
     out = sorted(agg.items(), key=lambda kv: -kv[1][0])
     print(f"steady-state window: {n_steps} steps, wall {wall / 1e6 / n_steps:.3f} ms/step, "
-          f"kernel busy {busy / 1e6 / n_steps:.3f} ms/step ({100.0 * busy / max(1, wall):.1f}%)")
+          f"kernel busy {busy / 1e6 / n_steps:.3f} ms/step ({100.0 * busy / max(1, wall):.1f}%), "
+          f"occupied {occupied / 1e6 / n_steps:.3f} ms/step ({100.0 * occupied / max(1, wall):.1f}%)")
     for k, (t, c) in out[:40]:
         print(f"{t / 1e6 / n_steps:8.3f} ms/step {c / n_steps:6.1f}/step {100.0 * t / busy:5.1f}%  {k}")
     if args.sequence:

@@ -1,0 +1,57 @@
+"""Conv weight gradients on a side stream (ops/arena.py side_work, DET_WGRAD_STREAM=1).
+
+The ResNet-50 trial trained with its 1x1 / 3x3 / shortcut weight gradients forked onto a side
+stream must leave the same parameters as the single-stream run -- bitwise, since every kernel is
+the same and only the stream order changes -- eagerly and replayed from a hipGraph (where the
+fork/join become graph edges)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _train(monkeypatch, side: bool, graph: bool, batch: int = 128, steps: int = 6):
+    from determined_1_amd import workload
+    from determined_1_amd.experimental import load_model_def, make_controller
+    from determined_1_amd.ops import arena
+
+    monkeypatch.setattr(arena, "SIDE_WGRAD", side)
+    monkeypatch.setenv("DET_HIP_GRAPH", "1" if graph else "0")
+    trial_cls = load_model_def(os.path.join(REPO, "examples", "computer_vision", "resnet50_pytorch")).ResNetImageNetTrial
+    config = {
+        "entrypoint": "model_def:ResNetImageNetTrial",
+        "hyperparameters": {"global_batch_size": batch, "lr": 0.2, "momentum": 0.9, "weight_decay": 5e-5,
+                            "arch": "resnet50", "amp": "O2", "channels_last": True, "image_size": 224},
+        "resources": {"slots_per_trial": 1},
+        "searcher": {"name": "single", "metric": "validation_loss", "max_length": {"batches": steps}},
+        "scheduling_unit": steps,
+    }
+
+    def stream():
+        yield workload.train_workload(1, num_batches=steps, total_batches_processed=0), [], workload.ignore_response
+        yield workload.terminate_workload(2), [], workload.ignore_response
+
+    forks0 = arena.SIDE_COUNTS["forks"]
+    ctrl = make_controller(trial_cls, config, stream(), trial_seed=1234)
+    ctrl.run()
+    torch.cuda.synchronize()
+    params = [p.detach().float().cpu() for p in ctrl.context.models[0].parameters()]
+    forks = arena.SIDE_COUNTS["forks"] - forks0
+    assert arena._SIDE["pending"] is None and not arena._SIDE["keep"]
+    del ctrl
+    torch.cuda.empty_cache()
+    return params, forks
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_side_stream_wgrad_matches_single_stream(gpu, monkeypatch, graph):
+    ref, forks_off = _train(monkeypatch, False, graph)
+    got, forks_on = _train(monkeypatch, True, graph)
+    assert forks_off == 0
+    assert forks_on >= 50, forks_on  # ~52 native conv weight gradients per ResNet-50 backward
+    for i, (pr, pg) in enumerate(zip(ref, got)):
+        assert torch.equal(pr, pg), (i, float((pr - pg).abs().max()))
