@@ -51,8 +51,11 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DET_BENCH_BS", "512")),
-                    help="per-GPU batch (weak scaling); 512 uses the 288 GB HBM of an MI355X")
+    ap.add_argument("--batch-per-gpu", type=int, default=int(os.environ.get("DET_BENCH_BS", "1024")),
+                    help="per-GPU batch (weak scaling).  1024 is the largest whose layer-1 activations stay under "
+                         "the kernels' 2 GiB buffer-descriptor range; it peaks at 44.6 GB of the 288 GB HBM and gives "
+                         "layer 3/4 (14x14, 7x7) GEMMs enough tiles to fill 256 CUs: 13,53-13,69k vs 13,01-13,09k "
+                         "samples/s at 512 (profiles/r6_bench_resnet50_side_stream_batch_sweep.jsonl)")
     ap.add_argument("--amp", default=os.environ.get("DET_BENCH_AMP", "O2"), choices=["O0", "O1", "O2"])
     ap.add_argument("--arch", default="resnet50")
     ap.add_argument("--image-size", type=int, default=224, help="(smoke tests only; the metric is 224)")
@@ -319,6 +322,7 @@ def main() -> None:
                 "miopen_find_db": os.environ.get("MIOPEN_USER_DB_PATH"),
                 "hip_graph": getattr(getattr(ctrl, "_graph", None), "stats", lambda: None)(),
                 "wgrad_side_stream": side_wgrad,
+                "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
             },
         }
         if phases:  # DET_STEP_TIMERS=1: per-batch device phases of the timed window (forward/backward/comm/opt)
