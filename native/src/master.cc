@@ -478,6 +478,11 @@ void Master::InstallRoutes() {
     Json body = Json::parse(r.body);
     std::string name = body.get_string("username", "");
     if (name.empty()) return Err(400, "username required");
+    if (cfg_.require_auth) {  // with authentication on, only an admin creates users (reference user/service.go postUser)
+      bool caller_admin = false;
+      for (auto& cu : store_->Where("users", "username", Json(UserForRequest(r)))) caller_admin = cu.get_bool("admin", false);
+      if (!caller_admin) return Err(403, "only an admin can create users");
+    }
     if (!store_->Where("users", "username", Json(name)).empty()) return Err(409, "user exists");
     Json u = Json::object();
     u["username"] = name;

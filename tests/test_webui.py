@@ -44,8 +44,42 @@ def test_webui_served_and_its_api_calls_exist(tmp_path):
         for verb in ("archive", "unarchive"):
             assert requests.post(base + f"/api/v1/experiments/{eid}/{verb}", headers=h).status_code == 200
         assert requests.post(base + f"/api/v1/trials/{tid}/kill", headers=h).status_code in (200, 409)
+        # round 6 pages: edit (saveExperiment), fork (forkExperiment), users, templates, slot toggles
+        r = requests.patch(base + f"/api/v1/experiments/{eid}", json={"description": "edited", "labels": ["x", "y"],
+                                                                      "notes": "n"}, headers=h)
+        assert r.status_code == 200, r.text
+        e = requests.get(base + f"/api/v1/experiments/{eid}", headers=h).json()["experiment"]
+        assert e["description"] == "edited" and e["labels"] == ["x", "y"]
+        md = requests.get(base + f"/experiments/{eid}/model_def", headers=h).json()
+        cfg = requests.get(base + f"/api/v1/experiments/{eid}", headers=h).json()["config"]
+        r = requests.post(base + "/api/v1/experiments", json={"config": cfg, "modelDefinition": md["files"],
+                                                              "parentId": eid, "activate": False}, headers=h)
+        assert r.status_code == 200, r.text
+        fork = r.json()["experiment"]
+        assert fork["parentId"] == eid and fork["id"] != eid
+        # user administration needs an admin session; a plain user is refused
+        body = {"user": {"username": "ui-user", "admin": False}, "password": "pw"}
+        assert requests.post(base + "/api/v1/users", json=body, headers=h).status_code == 403
+        atok = requests.post(base + "/api/v1/auth/login", json={"username": "admin", "password": ""}).json()["token"]
+        ha = {"Authorization": f"Bearer {atok}"}
+        r = requests.post(base + "/api/v1/users", json=body, headers=ha)
+        assert r.status_code == 200 and r.json()["user"]["username"] == "ui-user", r.text
+        assert requests.post(base + "/api/v1/users/ui-user/password", json={"password": "pw2"},
+                             headers=h).status_code == 403
+        assert requests.post(base + "/api/v1/users/ui-user/password", json={"password": "pw2"},
+                             headers=ha).status_code == 200
+        assert requests.post(base + "/api/v1/auth/login", json={"username": "ui-user", "password": "pw2"}).status_code == 200
+        r = requests.put(base + "/api/v1/templates/ui-model", json={"template": {"name": "ui-model",
+                                                                              "config": {"resources": {"slots_per_trial": 1}}}},
+                         headers=h)
+        assert r.status_code == 200, r.text
+        agent = requests.get(base + "/api/v1/agents", headers=h).json()["agents"][0]
+        slot = next(iter(agent["slots"].values()))["id"]
+        for verb in ("disable", "enable"):
+            assert requests.post(base + f"/api/v1/agents/{agent['id']}/slots/{slot}/{verb}", headers=h).status_code == 200
         js = WEBUI.read_text()
-        for route in ("#/models", "#/compare/", "checkpointTable", "compareSelected", "registerCheckpoint", "killTrial"):
+        for route in ("#/models", "#/compare/", "checkpointTable", "compareSelected", "registerCheckpoint", "killTrial",
+                      "#/users", "#/templates", "saveExperiment", "forkExperiment", "slotToggle", "downloadLogs"):
             assert route in js
         paths = set(re.findall(r'[`"](/api/v1/[^`"?]*)', js))
         assert len(paths) >= 10, paths
@@ -53,10 +87,12 @@ def test_webui_served_and_its_api_calls_exist(tmp_path):
             concrete = re.sub(r"\$\{[^}]*\}", lambda m: {"${kind}": "commands", "${verb}": "archive",
                                                            "${encodeURIComponent(name)}": "ui-model"}.get(
                 m.group(0), str(tid) if "/trials/" in p and "experiments" not in p else str(eid)), p)
-            if "metrics-stream" in p or "/logs" in p or "auth/login" in p or "/archive" in concrete or p.endswith("/kill"):
+            if "metrics-stream" in p or "/logs" in p or "auth/log" in p or "/archive" in concrete or p.endswith("/kill") \
+                    or "/password" in p or "/api/v1/agents/${" in p:
                 continue  # streams and mutations are covered above and by tests/test_api_v1.py
             r = requests.get(base + concrete, headers=h, timeout=10)
             assert r.status_code == 200, (p, concrete, r.status_code, r.text[:200])
+        assert requests.delete(base + "/api/v1/templates/ui-model", headers=h).status_code == 200
         # without a token the API refuses, so the page falls back to its login form
         assert requests.get(base + "/api/v1/experiments", timeout=10).status_code == 401
 
@@ -139,6 +175,24 @@ const pts = trials.map((t) => ({{trialId: t.id, hparams: t.hparams, metric: t.be
 const pc = parcoords(axes, pts, "validation_error", true), sc = scatterPlots(axes, pts, "validation_error", true);
 if ((pc.match(/<polyline/g) || []).length !== 3) throw new Error("parcoords " + pc);
 if ((sc.match(/<circle/g) || []).length !== 3) throw new Error("scatter " + sc);
+// experiment list filtering / sorting, the best-so-far history, a trial's training / validation series
+const exps = [{{id: 1, description: "resnet", labels: ["cv"], state: "STATE_ACTIVE", username: "a", archived: false}},
+              {{id: 2, description: "bert", labels: ["nlp"], state: "STATE_COMPLETED", username: "b", archived: false}},
+              {{id: 3, description: "old", labels: [], state: "STATE_COMPLETED", username: "a", archived: true}}];
+const f = (o) => filteredExperiments(exps, Object.assign({{q: "", state: "", user: "", label: "", archived: false, sort: "id", desc: true}}, o)).map((e) => e.id).join(",");
+if (f({{}}) !== "2,1" || f({{archived: true}}) !== "3,2,1" || f({{label: "nlp"}}) !== "2" || f({{state: "ACTIVE"}}) !== "1"
+    || f({{user: "a", archived: true, desc: false}}) !== "1,3" || f({{q: "cv"}}) !== "1" || f({{sort: "description", desc: false}}) !== "2,1")
+  throw new Error("filters");
+const hist = historyChart([{{endTime: "2026-01-01T00:00:00Z", searcherMetric: 0.5, trialId: 1}},
+                           {{endTime: "2026-01-01T00:01:00Z", searcherMetric: 0.7, trialId: 2}},
+                           {{endTime: "2026-01-01T00:02:00Z", searcherMetric: 0.3, trialId: 1}}], true);
+const hp = hist.match(/points="([^"]*)"/)[1].trim().split(" ");
+if (hp.length !== 3 || hp[0].split(",")[1] !== hp[1].split(",")[1]) throw new Error("history " + hist);
+const wl = [{{training: {{state: "STATE_COMPLETED", priorBatchesProcessed: 0, numBatches: 2, metrics: {{avg_metrics: {{loss: 0.8}}}}}}}},
+            {{training: {{state: "STATE_COMPLETED", priorBatchesProcessed: 2, numBatches: 2, metrics: {{avg_metrics: {{loss: 0.6}}}}}}}},
+            {{validation: {{state: "STATE_COMPLETED", priorBatchesProcessed: 4, metrics: {{validation_metrics: {{acc: 0.9}}}}}}}}];
+if (JSON.stringify(trialSeries(wl, "loss", true)) !== "[[2,0.8],[4,0.6]]" || JSON.stringify(trialSeries(wl, "acc", false)) !== "[[4,0.9]]")
+  throw new Error("series");
 console.log("ok");
 """
     f = tmp_path / "ui_test.js"
