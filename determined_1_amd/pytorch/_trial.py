@@ -34,6 +34,9 @@ from determined_1_amd.pytorch._data import (BatchChunk, ChunkedBatches, ChunkPre
 from determined_1_amd.pytorch._lr_scheduler import LRScheduler
 from determined_1_amd.pytorch._reducer import Reducer, _reduce_metrics
 
+# (experiment) DET_COMPUTE_STREAM_HIGH_PRIO=1: run training steps on a high-priority stream
+COMPUTE_STREAM_HIGH_PRIO = os.environ.get("DET_COMPUTE_STREAM_HIGH_PRIO", "0") == "1"
+
 try:
     import cloudpickle as _pickle_module  # reference checkpoints are written with cloudpickle
 except ImportError:  # pragma: no cover
@@ -79,6 +82,7 @@ class PyTorchTrialController(trial.LoopTrialController):
         self.training_iterator = self._make_train_iterator()
         self._graph = None  # type: Optional[_graph.TrainStepGraph]
         self._graph_checked = False
+        self._hp_stream = None  # type: Any  # COMPUTE_STREAM_HIGH_PRIO
         self._eval_graph = None  # type: Optional[_graph.EvalStepGraph]
         # arenas / fused optimizers / bucketers, then restore, then rank-0 broadcast
         self.context._finalize()
@@ -280,6 +284,23 @@ class PyTorchTrialController(trial.LoopTrialController):
                 lr_scheduler.step()
 
     def _train_for_step(self, step_id: int, num_batches: int, total_batches_processed: int) -> workload.Response:
+        if not (COMPUTE_STREAM_HIGH_PRIO and self.context.device.type == "cuda"):
+            return self._train_for_step_on_stream(step_id, num_batches, total_batches_processed)
+        # the training step on a high-priority stream: work forked to a side stream (the conv weight
+        # gradients, ops/arena.py side_work) then yields the CUs to the input-gradient chain, which
+        # is the step's critical path
+        dev = self.context.device
+        if self._hp_stream is None:
+            self._hp_stream = torch.cuda.Stream(dev, priority=-1)
+        default = torch.cuda.current_stream(dev)
+        self._hp_stream.wait_stream(default)
+        try:
+            with torch.cuda.stream(self._hp_stream):
+                return self._train_for_step_on_stream(step_id, num_batches, total_batches_processed)
+        finally:
+            default.wait_stream(self._hp_stream)
+
+    def _train_for_step_on_stream(self, step_id: int, num_batches: int, total_batches_processed: int) -> workload.Response:
         check.gt(step_id, 0)
         for model in self.context.models:
             model.train()
