@@ -57,6 +57,8 @@ def parse() -> argparse.Namespace:
                          "layer 3/4 (14x14, 7x7) GEMMs enough tiles to fill 256 CUs: 13,53-13,69k vs 13,01-13,09k "
                          "samples/s at 512 (profiles/r6_bench_resnet50_side_stream_batch_sweep.jsonl)")
     ap.add_argument("--amp", default=os.environ.get("DET_BENCH_AMP", "O2"), choices=["O0", "O1", "O2"])
+    ap.add_argument("--lr", type=float, default=None,
+                    help="SGD learning rate (default: the linear scaling rule, 0.1 x global batch / 256)")
     ap.add_argument("--arch", default="resnet50")
     ap.add_argument("--image-size", type=int, default=224, help="(smoke tests only; the metric is 224)")
     ap.add_argument("--bucket-mb", type=int, default=int(os.environ.get("DET_BENCH_BUCKET_MB", "64")))
@@ -201,7 +203,7 @@ def main() -> None:
         "entrypoint": "model_def:ResNetImageNetTrial",
         "hyperparameters": {
             "global_batch_size": gbs,
-            "lr": 0.1 * gbs / 256,
+            "lr": args.lr if args.lr is not None else 0.1 * gbs / 256,
             "momentum": 0.9,
             "weight_decay": 5e-5,
             "arch": args.arch,
