@@ -2244,7 +2244,8 @@ constexpr WgCfg kWgCfgs[] = {
     {64, 192, 4, 1, 2},    // 12: cfg 1 at 64 pixels per stage
     {64, 64, 4, 1, 4},     // 13: cfg 9 at 128 pixels per stage
     {256, 256, 8, 1, 2},   // 14: wgrad8 -- cfg 3's tile on the eight-phase schedule, 64 pixels per K tile
-                           //     (opt-in via DET_WGRAD_CFG: -2..-6 % at 256 channels, +1-2 % at 512, r6s36)
+                           //     (in isolation -2..-6 % at 256 channels, +1-2 % at 512, r6s36; in the
+                           //     side-stream step at 1,024 images/GPU +0.7 %, r6s62: the default where it fits)
 };
 constexpr int kWgNumCfgs = sizeof(kWgCfgs) / sizeof(kWgCfgs[0]);
 
@@ -2255,6 +2256,11 @@ int wg_auto_cfg(int N, int RSC) {
   }();
   auto fits = [&](int c) { return N % kWgCfgs[c].bm == 0 && RSC % kWgCfgs[c].bn == 0; };
   if (forced > 0 && forced < kWgNumCfgs && fits(forced)) return forced;
+  static const bool use8 = [] {  // DET_WGRAD8=0: cfg 3 (the 4-stage ring) where cfg 14 fits
+    const char* e = std::getenv("DET_WGRAD8");
+    return !(e != nullptr && std::atoi(e) == 0);
+  }();
+  if (use8 && fits(14)) return 14;
   for (int c : {3, 2, 7, 6, 10, 1, 5, 4, 11, 8, 9})
     if (fits(c)) return c;
   return 0;
