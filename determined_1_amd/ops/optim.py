@@ -311,6 +311,9 @@ class FusedOptimizer:
             with torch.enable_grad():
                 loss = closure()
         self.steps_called += 1  # host count of step() calls (a hipGraph capture notes whether it stepped)
+        from determined_1_amd.ops.arena import join_side_work
+
+        join_side_work()  # side-stream weight gradients (a loss.backward() outside context.backward)
         for gi, gs in enumerate(self.groups):
             if not gs.initialized:
                 self._bind_state(gi)

@@ -387,6 +387,7 @@ class PyTorchTrialContext(trial.TrialContext):
                    "to be true.")
         if not self._should_communicate_and_update():
             return
+        join_side_work()  # gradients a side stream still writes (a loss.backward() outside context.backward)
         st = next((s for s in self._opt_states if s.opt is optimizer), None)
         check.is_not_none(st, "step_optimizer() needs an optimizer returned by wrap_optimizer()")
         assert st is not None
