@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _train(monkeypatch, side: bool, graph: bool, batch: int = 128, steps: int = 6):
+def _train(monkeypatch, side: bool, graph: bool, batch: int = 128, steps: int = 6, plain_backward: bool = False):
     from determined_1_amd import workload
     from determined_1_amd.experimental import load_model_def, make_controller
     from determined_1_amd.ops import arena
@@ -37,6 +37,9 @@ def _train(monkeypatch, side: bool, graph: bool, batch: int = 128, steps: int = 
 
     forks0 = arena.SIDE_COUNTS["forks"]
     ctrl = make_controller(trial_cls, config, stream(), trial_seed=1234)
+    if plain_backward:  # user code calling loss.backward() itself: step_optimizer must still join
+        ctx = ctrl.context
+        monkeypatch.setattr(ctx, "backward", lambda loss, **kw: loss.float().backward())
     ctrl.run()
     torch.cuda.synchronize()
     params = [p.detach().float().cpu() for p in ctrl.context.models[0].parameters()]
@@ -53,5 +56,15 @@ def test_side_stream_wgrad_matches_single_stream(gpu, monkeypatch, graph):
     got, forks_on = _train(monkeypatch, True, graph)
     assert forks_off == 0
     assert forks_on >= 50, forks_on  # ~52 native conv weight gradients per ResNet-50 backward
+    for i, (pr, pg) in enumerate(zip(ref, got)):
+        assert torch.equal(pr, pg), (i, float((pr - pg).abs().max()))
+
+
+def test_side_stream_joined_without_context_backward(gpu, monkeypatch):
+    """A train_batch that calls loss.backward() instead of context.backward(): the GradSink flush and
+    step_optimizer join the side stream before the optimizer reads the gradients."""
+    ref, _ = _train(monkeypatch, False, False, plain_backward=True)
+    got, forks = _train(monkeypatch, True, False, plain_backward=True)
+    assert forks >= 50, forks
     for i, (pr, pg) in enumerate(zip(ref, got)):
         assert torch.equal(pr, pg), (i, float((pr - pg).abs().max()))
