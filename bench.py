@@ -17,8 +17,9 @@ is built exactly as a cluster trial process builds it and fed ``RUN_STEP`` workl
   warmup RUN_STEP(W batches) -> barrier + synchronize -> t0 -> RUN_STEP(K batches)
   -> synchronize + barrier -> t1.
 Each batch is: synthetic uint8 ImageNet-shape images DMA'd from pinned memory -> HIP normalize
-kernel -> ResNet-50 fwd/bwd (bf16 autocast, channels_last) -> [RCCL bucketed all-reduce overlapped
-with backward] -> fused arena SGD-momentum HIP kernel.  Weak scaling: fixed per-GPU batch.
+kernel -> ResNet-50 fwd/bwd (bf16 autocast, channels_last; the conv weight gradients on a side HIP
+stream beside the input-gradient chain) -> [RCCL bucketed all-reduce overlapped with backward] ->
+fused arena SGD-momentum HIP kernel.  Weak scaling: fixed per-GPU batch (1,024 by default).
 
 Rank 0 prints ONE JSON line; ``value`` = K * global_batch / max-over-ranks(t1 - t0).
 
