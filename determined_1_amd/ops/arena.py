@@ -154,6 +154,9 @@ def landing_buffer(p: torch.Tensor) -> Optional[torch.Tensor]:
 # edges, and the replay is bitwise equal but no faster: this runtime's graph launch does not run the
 # two branches concurrently.
 SIDE_WGRAD = os.environ.get("DET_WGRAD_STREAM", "1") != "0"
+# only weight gradients whose output gradient has at least this many elements fork (small convs of
+# host-bound steps gain nothing from the overlap and pay the fork / join)
+SIDE_MIN_ELEMS = int(os.environ.get("DET_WGRAD_STREAM_MIN", "0"))
 _SIDE = {"streams": {}, "keep": [], "pending": None}  # type: Dict[str, Any]
 SIDE_COUNTS = {"forks": 0, "joins": 0}
 

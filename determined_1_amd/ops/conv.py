@@ -23,7 +23,7 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def _wgrad_target(weight: torch.Tensor, needed: bool, gpu: bool,
+def _wgrad_target(weight: torch.Tensor, needed: bool, gpu: bool, dy_numel: int,
                   memory_format: torch.memory_format = torch.contiguous_format) -> Tuple[Optional[torch.Tensor], bool]:
     """(dw, side) for a conv weight gradient: the parameter's arena slot when its GradSink offers
     one (arena.landing_buffer), else a fresh tensor; ``side`` = the gradient may be computed on the
@@ -35,7 +35,7 @@ def _wgrad_target(weight: torch.Tensor, needed: bool, gpu: bool,
     buf = arena.landing_buffer(weight)
     if buf is not None and buf.is_contiguous(memory_format=memory_format) and \
             buf.dtype in (torch.bfloat16, torch.float32):
-        return buf, arena.SIDE_WGRAD and gpu and buf.dtype == weight.dtype
+        return buf, arena.SIDE_WGRAD and gpu and buf.dtype == weight.dtype and dy_numel >= arena.SIDE_MIN_ELEMS
     dt = weight.dtype if weight.dtype in (torch.bfloat16, torch.float32) else torch.float32
     return torch.empty(weight.shape, dtype=dt, device=weight.device, memory_format=memory_format), False
 
@@ -769,7 +769,7 @@ class _Conv1x1(torch.autograd.Function):
         if pend is not None:  # dY = the deferred BN apply, computed in the dgrad's A staging into dy2
             d, bx, coef = pend
             abn = (d.permute(0, 2, 3, 1).reshape(-1, cout), bx, coef, dy2)
-        dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dy2))
+        dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dy2), dy2.numel())
         if side and pend is None:  # independent of the dgrad: fork before it
             with side_work(True, dy2, x2):
                 conv1x1_wgrad(dy2, x2, dw.view(cout, c))
@@ -912,7 +912,7 @@ class _ConvRS(torch.autograd.Function):
             (WGRAD_RS_MODE == "auto" and conv3p_wgrad_ok(cin, cout, r, s, stride, pad) and is_gpu(dyc))
         side = False
         if native_wgrad:
-            dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dyc), torch.channels_last)
+            dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dyc), dyc.numel(), torch.channels_last)
             if side:  # fork before the input gradient: the two only share dY
                 with side_work(True, dyc, x):
                     _native_wgrad_rs(dyc, x, dw, stride, pad)
@@ -1295,7 +1295,7 @@ class _Shortcut1x1(torch.autograd.Function):
             pend = None
         dy2 = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, cout)
         dx = None
-        dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dy2))
+        dw, side = _wgrad_target(weight, ctx.needs_input_grad[1], is_gpu(dy2), dy2.numel())
         if side and pend is None:  # independent of the dgrad: fork before it
             with side_work(True, dy2, x):
                 _shortcut_wgrad(dy2, x, dw, st, g)
