@@ -41,7 +41,6 @@ constexpr int kFinThreads = 1024;
 constexpr int kMaxH = 8192;        // LayerNorm width limit (workgroup-per-row kernels above 2048)
 constexpr int kMaxNarrowH = 2048;  // wave-per-row kernels up to here
 constexpr int kFinCols = 64;
-constexpr int kFinLanes = kFinThreads / kFinCols;
 
 __device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(static_cast<uint32_t>(u) << 16); }
 // RNE; adjacent conversions pair into gfx950's v_cvt_pk_bf16_f32
@@ -618,13 +617,16 @@ __global__ void __launch_bounds__(NT) ln_bwd_wide(LnBwdArgs a) {
 }
 
 // Sum `parts` partial rows of width W (fp32) -> up to 3 outputs of width W/3 each (or one of W).
-template <typename T>
+// COLS columns per block (kFinThreads / COLS lanes split each column's rows); DET_FIN_COLS=16|32|64
+// picks it (32 by default: twice the blocks of 64 and half the serial rows per lane)
+template <typename T, int COLS = kFinCols>
 __global__ void __launch_bounds__(kFinThreads)
 colsum_finalize(const float* __restrict__ ws, int parts, int W, int seg, T* __restrict__ o0, T* __restrict__ o1,
                 T* __restrict__ o2) {
-  __shared__ float red[kFinLanes][kFinCols];
-  const int cl = threadIdx.x % kFinCols, ln = threadIdx.x / kFinCols;
-  const int col = blockIdx.x * kFinCols + cl;
+  constexpr int kFinLanes = kFinThreads / COLS;
+  __shared__ float red[kFinLanes][COLS];
+  const int cl = threadIdx.x % COLS, ln = threadIdx.x / COLS;
+  const int col = blockIdx.x * COLS + cl;
   float s = 0.f;
   if (col < W) {
     int p = ln;
@@ -647,6 +649,26 @@ colsum_finalize(const float* __restrict__ ws, int parts, int W, int seg, T* __re
     T* o = which == 0 ? o0 : which == 1 ? o1 : o2;
     if (o) o[c] = from_float<T>(t);
   }
+}
+
+int fin_cols() {
+  static const int c = [] {
+    const char* e = std::getenv("DET_FIN_COLS");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v == 16 || v == 64 ? v : 32;  // 32: LN backward 19.1 vs 20.4 us, BERT graph +0.56 % (r6s73)
+  }();
+  return c;
+}
+template <typename T>
+void launch_colsum_finalize(hipStream_t st, const float* ws, int parts, int W, int seg, T* o0, T* o1, T* o2) {
+  const int cols = fin_cols();
+  if (cols == 16)
+    hipLaunchKernelGGL((colsum_finalize<T, 16>), dim3((W + 15) / 16), dim3(kFinThreads), 0, st, ws, parts, W, seg, o0, o1, o2);
+  else if (cols == 32)
+    hipLaunchKernelGGL((colsum_finalize<T, 32>), dim3((W + 31) / 32), dim3(kFinThreads), 0, st, ws, parts, W, seg, o0, o1, o2);
+  else
+    hipLaunchKernelGGL((colsum_finalize<T, kFinCols>), dim3((W + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
+                       parts, W, seg, o0, o1, o2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -905,15 +927,13 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
       if (small) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1, 128>), dim3(blocks), dim3(128), 0, st, a);
       else if (v1) hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       else hipLaunchKernelGGL((ln_bwd_wide<unsigned short, 2, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
-      hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads),
-                         0, st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
+      launch_colsum_finalize<unsigned short>(st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
                          static_cast<unsigned short*>(dbeta), static_cast<unsigned short*>(dbias));
     } else {
       if (small) hipLaunchKernelGGL((ln_bwd_wide<float, 1, 128>), dim3(blocks), dim3(128), 0, st, a);
       else if (v1) hipLaunchKernelGGL((ln_bwd_wide<float, 1, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
       else hipLaunchKernelGGL((ln_bwd_wide<float, 2, kWideThreads>), dim3(blocks), dim3(kWideThreads), 0, st, a);
-      hipLaunchKernelGGL(colsum_finalize<float>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st,
-                         ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
+      launch_colsum_finalize<float>(st, ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
                          static_cast<float*>(dbias));
     }
     return static_cast<int>(hipGetLastError());
@@ -935,13 +955,11 @@ int det_tf_ln_bwd(void* stream, int dtype, const void* dy, const void* h, const 
   }
   if (dtype == 1) {
     DET_LNB_K(unsigned short)
-    hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads),
-                       0, st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
+    launch_colsum_finalize<unsigned short>(st, ws, blocks, 3 * H, H, static_cast<unsigned short*>(dgamma),
                        static_cast<unsigned short*>(dbeta), static_cast<unsigned short*>(dbias));
   } else {
     DET_LNB_K(float)
-    hipLaunchKernelGGL(colsum_finalize<float>, dim3((3 * H + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st,
-                       ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
+    launch_colsum_finalize<float>(st, ws, blocks, 3 * H, H, static_cast<float*>(dgamma), static_cast<float*>(dbeta),
                        static_cast<float*>(dbias));
   }
   return static_cast<int>(hipGetLastError());
@@ -988,8 +1006,7 @@ int det_tf_gelu_bwd(void* stream, int dtype, const void* da, const void* z, void
                          static_cast<const unsigned short*>(da), static_cast<const unsigned short*>(z),
                          static_cast<unsigned short*>(dz), g, w);
     if (dbias)
-      hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0,
-                         st, ws, g.nrb, C, C, static_cast<unsigned short*>(dbias), nullptr, nullptr);
+      launch_colsum_finalize<unsigned short>(st, ws, g.nrb, C, C, static_cast<unsigned short*>(dbias), static_cast<unsigned short*>(nullptr), static_cast<unsigned short*>(nullptr));
   } else {
     if (approx)
       hipLaunchKernelGGL((col_kernel<float, 2>), grid, dim3(kThreads), 0, st, static_cast<const float*>(da),
@@ -998,8 +1015,8 @@ int det_tf_gelu_bwd(void* stream, int dtype, const void* da, const void* z, void
       hipLaunchKernelGGL((col_kernel<float, 1>), grid, dim3(kThreads), 0, st, static_cast<const float*>(da),
                          static_cast<const float*>(z), static_cast<float*>(dz), g, w);
     if (dbias)
-      hipLaunchKernelGGL(colsum_finalize<float>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
-                         g.nrb, C, C, static_cast<float*>(dbias), nullptr, nullptr);
+      launch_colsum_finalize<float>(st, ws,
+                         g.nrb, C, C, static_cast<float*>(dbias), static_cast<float*>(nullptr), static_cast<float*>(nullptr));
   }
   return static_cast<int>(hipGetLastError());
 }
@@ -1013,12 +1030,11 @@ int det_tf_colsum(void* stream, int dtype, const void* x, int64_t rows, int C, v
   if (dtype == 1) {
     hipLaunchKernelGGL((col_kernel<unsigned short, 0>), grid, dim3(kThreads), 0, st,
                        static_cast<const unsigned short*>(x), nullptr, nullptr, g, ws);
-    hipLaunchKernelGGL(colsum_finalize<unsigned short>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0,
-                       st, ws, g.nrb, C, C, static_cast<unsigned short*>(out), nullptr, nullptr);
+    launch_colsum_finalize<unsigned short>(st, ws, g.nrb, C, C, static_cast<unsigned short*>(out), nullptr, nullptr);
   } else {
     hipLaunchKernelGGL((col_kernel<float, 0>), grid, dim3(kThreads), 0, st, static_cast<const float*>(x), nullptr,
                        nullptr, g, ws);
-    hipLaunchKernelGGL(colsum_finalize<float>, dim3((C + kFinCols - 1) / kFinCols), dim3(kFinThreads), 0, st, ws,
+    launch_colsum_finalize<float>(st, ws,
                        g.nrb, C, C, static_cast<float*>(out), nullptr, nullptr);
   }
   return static_cast<int>(hipGetLastError());
