@@ -150,9 +150,9 @@ def landing_buffer(p: torch.Tensor) -> Optional[torch.Tensor]:
 # GradSink flushes, end_backward and context.backward.  Operands stay referenced until the join, so
 # the caching allocator cannot hand their blocks to the main stream while the side stream still
 # reads them.  Eager ResNet-50 at batch 512: 12,68k -> 12,96-13,18k samples/s
-# (profiles/r6_wgrad_side_stream_ab.jsonl).  Inside a hipGraph capture the fork/join become graph
-# edges, and the replay is bitwise equal but no faster: this runtime's graph launch does not run the
-# two branches concurrently.
+# (profiles/r6_wgrad_side_stream_ab.jsonl).  A captured fork/join replayed bitwise equal but no
+# faster (this runtime's graph launch runs the two branches one after the other), so captures do
+# not fork.
 SIDE_WGRAD = os.environ.get("DET_WGRAD_STREAM", "1") != "0"
 # only weight gradients whose output gradient has at least this many elements fork (small convs of
 # host-bound steps gain nothing from the overlap and pay the fork / join)
@@ -165,7 +165,9 @@ class side_work:
     """``with side_work(on, *operands):`` run the body on the device's side stream when ``on``."""
 
     def __init__(self, on: bool, *keep: torch.Tensor) -> None:
-        self.on = bool(on) and SIDE_WGRAD
+        # not under hipGraph capture: a replay runs the forked branch serialised anyway on this runtime,
+        # so a captured step stays single-stream (simpler graphs, same numbers)
+        self.on = bool(on) and SIDE_WGRAD and not torch.cuda.is_current_stream_capturing()
         self.keep = keep
         self._ctx = None
 

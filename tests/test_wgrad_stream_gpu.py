@@ -2,8 +2,8 @@
 
 The ResNet-50 trial trained with its 1x1 / 3x3 / shortcut weight gradients forked onto a side
 stream must leave the same parameters as the single-stream run -- bitwise, since every kernel is
-the same and only the stream order changes -- eagerly and replayed from a hipGraph (where the
-fork/join become graph edges)."""
+the same and only the stream order changes -- eagerly and with hipGraph replays (whose captures do
+not fork: the warm-up steps before the capture run the side stream)."""
 import os
 
 import pytest
