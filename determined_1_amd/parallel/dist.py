@@ -160,6 +160,11 @@ def init_process_groups(device: torch.device, timeout_s: int = constants.DIST_ST
     kwargs = {}
     if backend == "nccl":
         kwargs["device_id"] = device  # eager RCCL communicator init, bound to this GPU
+        # fresh events per collective instead of torch's event cache: a cached event re-recorded by a
+        # collective inside a hipGraph capture can still be queried by the watchdog thread for the
+        # eager work that last used it ("operation not permitted on an event last recorded in a
+        # capturing stream", seen once in the world-1 DP graph test, profiles/r6_s76_final_rehearsal.txt)
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
     _control_group = dist.new_group(backend="gloo") if backend == "nccl" else dist.group.WORLD
     logging.info("initialized %s data group + gloo control group: rank %d/%d", backend, dist.get_rank(),
